@@ -1,0 +1,164 @@
+"""Headline benchmark: BERT-base phase-1 (seq 128) pre-training throughput.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it
+is launched by ``torch.distributed.run`` (one rank per GPU, RCCL).  Runs the real
+framework path -- synthetic NVIDIA-schema HDF5 shards -> native reader -> pinned
+staging on the HIP copy stream -> Controller.train_step (fused HIP kernels +
+hipBLASLt GEMMs, flat-buffer RCCL reducer, fused norm/clip/Adam) -- with
+random-init BERT-base weights (no network: no corpus, no checkpoint).
+
+Config = BASELINE.json's: BERT-base (L12 H768 A12 V30522), seq 128, 20 masked
+positions per sequence, per-GPU batch 128 (weak scaling: global batch 128*N),
+Adam lr 1e-4 + warmup 10000 + wd 0.01, clip 25, fast stat sync, fp32 compute
+(the reference's precision).  W untimed warm-up steps, then exactly K timed steps
+bracketed by barrier + device synchronize; the max over ranks is reported.
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = ('sec/step + samples/sec BERT-base phase-1 seq128 bs=128 at 1/2/4/8 MI355X; speedup vs 1 GPU')
+# reference samples/s (README.md:65-68 via BASELINE.md): published 4 GPUs = 49.2, 8 GPUs = 95.2;
+# 1/2 GPUs unpublished -> the 4-GPU row's per-GPU rate (12.3 seq/s) times N.
+REF_SAMPLES_PER_SEC = {1: 12.3, 2: 24.6, 4: 49.2, 8: 95.2}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--batch', type=int, default=128, help='per-GPU sequences per step')
+    ap.add_argument('--seq', type=int, default=128)
+    ap.add_argument('--max-pred', type=int, default=20)
+    ap.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'])
+    ap.add_argument('--model', default='base', choices=['base', 'large', 'tiny'])
+    ap.add_argument('--no-fused', action='store_true', help='torch-op baseline (A/B only)')
+    ap.add_argument('--data-dir', default=None)
+    ap.add_argument('--update-freq', type=int, default=1)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    if a.no_fused:
+        os.environ['HETSEQ_NO_FUSED'] = '1'
+    from hetseq_9cme_amd import options
+    from hetseq_9cme_amd.controller import Controller
+    from hetseq_9cme_amd.data import iterators
+    from hetseq_9cme_amd.data.synthetic import (BERT_BASE, BERT_LARGE, BERT_TINY, write_bert_config,
+                                                write_synthetic_bert_shards)
+    from hetseq_9cme_amd.parallel import distributed as dist_utils
+    from hetseq_9cme_amd import tasks
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != a.gpus and world > 1:
+        print('warning: --gpus {} but WORLD_SIZE {}'.format(a.gpus, world), file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+
+    cfg = {'base': BERT_BASE, 'large': BERT_LARGE, 'tiny': BERT_TINY}[a.model]
+    data_dir = a.data_dir or os.path.join(tempfile.gettempdir(), 'hx_bench_s{}_p{}_n{}'.format(
+        a.seq, a.max_pred, (a.warmup + a.steps + 2) * a.batch * a.update_freq * world))
+    cfg_path = os.path.join(data_dir, 'bert_config.json')
+    n_total = (a.warmup + a.steps + 2) * a.batch * a.update_freq * world
+    per_file = 8192
+    n_files = (n_total + per_file - 1) // per_file
+    if rank == 0 and not os.path.exists(os.path.join(data_dir, 'READY')):
+        os.makedirs(data_dir, exist_ok=True)
+        write_synthetic_bert_shards(data_dir, n_files=n_files, samples_per_file=per_file, seq_len=a.seq,
+                                    max_pred=a.max_pred, vocab_size=cfg['vocab_size'], seed=1234, split='train')
+        write_bert_config(cfg_path, **cfg)
+        open(os.path.join(data_dir, 'READY'), 'w').close()
+
+    argv = ['--task', 'bert', '--data', data_dir, '--config_file', cfg_path, '--max-sentences', str(a.batch),
+            '--fast-stat-sync', '--lr', '1e-4', '--warmup-updates', '10000', '--weight-decay', '0.01',
+            '--total-num-update', '1000000', '--clip-norm', '25', '--num-workers', '4', '--log-format', 'none',
+            '--disable-validation', '--no-save', '--precision', a.precision, '--distributed-world-size', str(world),
+            '--update-freq', str(a.update_freq)]
+    args = options.parse_training_args(argv)
+    args.device_id = local_rank
+    if world > 1:
+        args.distributed_init_method = 'env://'
+        args.distributed_rank = rank
+        dist_utils.distributed_init(args)
+        torch.distributed.barrier()
+    else:
+        args.distributed_rank = 0
+    while not os.path.exists(os.path.join(data_dir, 'READY')):
+        time.sleep(0.5)
+
+    torch.manual_seed(args.seed)
+    task = tasks.setup_task(args)
+    model = task.build_model(args)
+    ctrl = Controller(args, task, model)
+    epoch_itr = ctrl.get_train_iterator(epoch=0, load_dataset=True)
+    ctrl.lr_step(epoch_itr.epoch)
+    itr = iterators.GroupedIterator(epoch_itr.next_epoch_itr(shuffle=True), a.update_freq)
+
+    def step():
+        samples = next(itr)
+        return ctrl.train_step(samples)
+
+    for _ in range(a.warmup):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    loss = float(out['loss']) if out is not None else float('nan')
+    t = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    elapsed = float(t.item())
+    ms = elapsed / a.steps * 1000.0
+    global_batch = a.batch * a.update_freq * world
+    value = global_batch * a.steps / elapsed
+    ref = REF_SAMPLES_PER_SEC.get(world)
+    if rank == 0:
+        rec = {
+            'metric': METRIC,
+            'value': round(value, 2),
+            'unit': 'samples/s',
+            'n_gpus': world,
+            'steps': a.steps,
+            'warmup': a.warmup,
+            'ms_per_step': round(ms, 3),
+            'sec_per_step': round(ms / 1000.0, 5),
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': round(value / ref, 2) if ref else None,
+            'dtype': 'fp32' if a.precision == 'fp32' else 'bf16',
+            'data': 'synthetic (NVIDIA-schema HDF5 shards, random-init weights)',
+            'config': {'model': 'bert-base (L12 H768 A12 V30522, 110.1M params)' if a.model == 'base' else a.model,
+                       'global_batch': global_batch, 'per_gpu_batch': a.batch * a.update_freq,
+                       'seq_len': a.seq, 'max_pred': a.max_pred,
+                       'parallelism': 'dp{}'.format(world), 'optimizer': 'adam(fused)',
+                       'fused_kernels': not a.no_fused},
+            'final_logged_loss': round(loss, 5),
+        }
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

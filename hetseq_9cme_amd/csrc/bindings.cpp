@@ -1,0 +1,249 @@
+// torch <-> gfx950 kernel bindings.  Host-only TU: validates tensors, allocates
+// outputs through the torch caching allocator, and launches on the CURRENT HIP
+// stream of the tensor's device (so kernels order correctly with hipBLASLt GEMMs
+// and RCCL, and are capturable into HIP graphs).
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/extension.h>
+
+#include "hx_launch.h"
+
+namespace {
+
+using torch::Tensor;
+using OptT = c10::optional<Tensor>;
+
+inline hipStream_t cur_stream(const Tensor& t) { return c10::hip::getCurrentHIPStream(t.get_device()).stream(); }
+
+inline void check_cuda(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+inline int act_bf16(const Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32 || t.scalar_type() == torch::kBFloat16, "activations must be fp32 or bf16");
+  return t.scalar_type() == torch::kBFloat16 ? 1 : 0;
+}
+inline void check_f32(const Tensor& t, const char* name) {
+  check_cuda(t, name);
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32, name, " must be fp32");
+}
+template <typename T>
+inline T* ptr_or_null(const OptT& t) {
+  return (t.has_value() && t->defined()) ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+inline bool has(const OptT& t) { return t.has_value() && t->defined(); }
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// ------------------------------------------------------------------ optimizer
+void grad_norm_clip(Tensor g, Tensor gscale, Tensor out_norm, Tensor clipped, double max_norm) {
+  check_f32(g, "grad");
+  check_f32(gscale, "gscale");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(g.device());
+  TORCH_CHECK(aligned16(g.data_ptr()), "flat grad must be 16-byte aligned");
+  auto ws = torch::empty({hx_grad_norm_partials()}, g.options().dtype(torch::kFloat64));
+  hx_grad_norm_clip(g.data_ptr<float>(), g.numel(), ws.data_ptr<double>(), gscale.data_ptr<float>(),
+                    out_norm.data_ptr<float>(), clipped.data_ptr<float>(), (float)max_norm, cur_stream(g));
+}
+
+void adam(Tensor p, Tensor g, Tensor m, Tensor v, OptT shadow, Tensor gscale, int64_t start, int64_t end, double b1,
+          double b2, double eps, double step_size, double wd_lr) {
+  check_f32(p, "param");
+  check_f32(g, "grad");
+  check_f32(m, "exp_avg");
+  check_f32(v, "exp_avg_sq");
+  TORCH_CHECK(start >= 0 && end <= p.numel() && start <= end && start % 4 == 0, "bad param range");
+  TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel(), "flat size mismatch");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
+  uint16_t* sh = nullptr;
+  if (has(shadow)) {
+    TORCH_CHECK(shadow->scalar_type() == torch::kBFloat16 && shadow->numel() == p.numel(), "bad bf16 shadow");
+    sh = reinterpret_cast<uint16_t*>(shadow->data_ptr()) + start;
+  }
+  hx_adam(p.data_ptr<float>() + start, g.data_ptr<float>() + start, m.data_ptr<float>() + start,
+          v.data_ptr<float>() + start, sh, gscale.data_ptr<float>(), end - start, (float)b1, (float)b2, (float)eps,
+          (float)step_size, (float)wd_lr, cur_stream(p));
+}
+
+void adadelta(Tensor p, Tensor g, Tensor sq, Tensor acc, Tensor gscale, int64_t start, int64_t end, double lr,
+              double rho, double eps, double wd) {
+  check_f32(p, "param");
+  TORCH_CHECK(start >= 0 && end <= p.numel() && start <= end, "bad param range");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
+  hx_adadelta(p.data_ptr<float>() + start, g.data_ptr<float>() + start, sq.data_ptr<float>() + start,
+              acc.data_ptr<float>() + start, gscale.data_ptr<float>(), end - start, (float)lr, (float)rho,
+              (float)eps, (float)wd, cur_stream(p));
+}
+
+// ------------------------------------------------------------------ layernorm
+std::vector<Tensor> ln_fwd(Tensor y, OptT bias, OptT res, Tensor gamma, Tensor beta, double eps, double keep_prob,
+                           int64_t seed, int64_t stream, bool drop_after, bool save_z) {
+  check_cuda(y, "input");
+  const int H = (int)y.size(-1);
+  const int64_t rows = y.numel() / H;
+  TORCH_CHECK(H % 4 == 0 && H <= 2048, "LayerNorm hidden size must be a multiple of 4 and <= 2048");
+  check_f32(gamma, "gamma");
+  check_f32(beta, "beta");
+  if (has(res)) {
+    check_cuda(*res, "residual");
+    TORCH_CHECK(res->scalar_type() == y.scalar_type() && res->numel() == y.numel(), "residual mismatch");
+  }
+  if (has(bias)) check_f32(*bias, "bias");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(y.device());
+  auto out = torch::empty_like(y);
+  Tensor z = save_z ? torch::empty_like(y) : Tensor();
+  auto st = y.options().dtype(torch::kFloat32);
+  auto mean = torch::empty({rows}, st), rstd = torch::empty({rows}, st);
+  hx_ln_fwd(act_bf16(y), y.data_ptr(), ptr_or_null<float>(bias), has(res) ? res->data_ptr() : nullptr,
+            gamma.data_ptr<float>(), beta.data_ptr<float>(), out.data_ptr(), save_z ? z.data_ptr() : nullptr,
+            mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, H, (float)eps, (float)keep_prob, (uint64_t)seed,
+            (uint64_t)stream, drop_after ? 1 : 0, cur_stream(y));
+  return {out, z, mean, rstd};
+}
+
+std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tensor gamma, double keep_prob,
+                           int64_t seed, int64_t stream, bool drop_after, bool want_dy, bool want_dbias) {
+  check_cuda(dout, "grad_output");
+  check_cuda(z, "saved input");
+  const int H = (int)z.size(-1);
+  const int64_t rows = z.numel() / H;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(z.device());
+  auto dz = torch::empty_like(z);
+  Tensor dy = want_dy ? torch::empty_like(z) : Tensor();
+  auto f32 = z.options().dtype(torch::kFloat32);
+  auto dgamma = torch::empty({H}, f32), dbeta = torch::empty({H}, f32);
+  Tensor dbias = want_dbias ? torch::empty({H}, f32) : Tensor();
+  const int nblk = hx_ln_bwd_blocks(rows);
+  auto partial = torch::empty({(int64_t)nblk * 3 * H}, f32);
+  hx_ln_bwd(act_bf16(z), dout.data_ptr(), z.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+            gamma.data_ptr<float>(), dz.data_ptr(), want_dy ? dy.data_ptr() : nullptr, partial.data_ptr<float>(), nblk,
+            rows, H, (float)keep_prob, (uint64_t)seed, (uint64_t)stream, drop_after ? 1 : 0,
+            (want_dy && want_dbias) ? 1 : 0, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
+            want_dbias ? dbias.data_ptr<float>() : nullptr, 0, cur_stream(z));
+  return {dz, dy, dgamma, dbeta, dbias};
+}
+
+std::vector<Tensor> embed_ln_fwd(Tensor ids, OptT tt, Tensor wte, Tensor wpe, Tensor wtt, Tensor gamma, Tensor beta,
+                                 double eps, double keep_prob, int64_t seed, int64_t stream, bool bf16_out) {
+  check_cuda(ids, "input_ids");
+  TORCH_CHECK(ids.scalar_type() == torch::kInt64 && ids.dim() == 2, "input_ids must be int64 [B, S]");
+  check_f32(wte, "word_embeddings");
+  check_f32(wpe, "position_embeddings");
+  check_f32(wtt, "token_type_embeddings");
+  const int64_t B = ids.size(0), S = ids.size(1);
+  const int H = (int)wte.size(1);
+  TORCH_CHECK(H % 4 == 0 && H <= 2048, "hidden size must be a multiple of 4 and <= 2048");
+  TORCH_CHECK(S <= wpe.size(0), "sequence longer than max_position_embeddings");
+  if (has(tt)) TORCH_CHECK(tt->scalar_type() == torch::kInt64 && tt->numel() == ids.numel(), "token_type_ids mismatch");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(ids.device());
+  auto opt = wte.options().dtype(bf16_out ? torch::kBFloat16 : torch::kFloat32);
+  auto out = torch::empty({B, S, H}, opt), z = torch::empty({B, S, H}, opt);
+  auto f32 = wte.options();
+  auto mean = torch::empty({B * S}, f32), rstd = torch::empty({B * S}, f32);
+  hx_embed_ln_fwd(bf16_out ? 1 : 0, ids.data_ptr<int64_t>(), has(tt) ? tt->data_ptr<int64_t>() : nullptr,
+                  wte.data_ptr<float>(), wpe.data_ptr<float>(), wtt.data_ptr<float>(), gamma.data_ptr<float>(),
+                  beta.data_ptr<float>(), out.data_ptr(), z.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                  B * S, (int)S, H, (float)eps, (float)keep_prob, (uint64_t)seed, (uint64_t)stream, cur_stream(ids));
+  return {out, z, mean, rstd};
+}
+
+std::vector<Tensor> embed_grads(Tensor dz, Tensor ids, OptT tt, int64_t V, int64_t P, int64_t ntypes) {
+  check_cuda(dz, "dz");
+  const int64_t B = ids.size(0), S = ids.size(1);
+  const int H = (int)dz.size(-1);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dz.device());
+  auto f32 = dz.options().dtype(torch::kFloat32);
+  auto dwte = torch::zeros({V, H}, f32), dwpe = torch::zeros({P, H}, f32), dwtt = torch::zeros({ntypes, H}, f32);
+  hx_embed_grads(act_bf16(dz), dz.data_ptr(), ids.data_ptr<int64_t>(), has(tt) ? tt->data_ptr<int64_t>() : nullptr,
+                 dwte.data_ptr<float>(), dwpe.data_ptr<float>(), dwtt.data_ptr<float>(), (int)B, (int)S, H,
+                 (int)ntypes, cur_stream(dz));
+  return {dwte, dwpe, dwtt};
+}
+
+// ------------------------------------------------------------------ elementwise
+Tensor bias_act_fwd(Tensor y, OptT b, int64_t act) {
+  check_cuda(y, "input");
+  const int N = (int)y.size(-1);
+  TORCH_CHECK(N % 4 == 0, "bias_act: last dim must be a multiple of 4");
+  if (has(b)) check_f32(*b, "bias");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(y.device());
+  auto out = torch::empty_like(y);
+  hx_bias_act_fwd(act_bf16(y), (int)act, y.data_ptr(), ptr_or_null<float>(b), out.data_ptr(), y.numel() / N, N,
+                  cur_stream(y));
+  return out;
+}
+
+std::vector<Tensor> bias_act_bwd(Tensor dout, OptT y, OptT b, OptT saved_out, int64_t act, bool want_dbias) {
+  check_cuda(dout, "grad_output");
+  const int N = (int)dout.size(-1);
+  const int64_t rows = dout.numel() / N;
+  TORCH_CHECK(N % 4 == 0, "bias_act: last dim must be a multiple of 4");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dout.device());
+  auto dy = torch::empty_like(dout);
+  auto f32 = dout.options().dtype(torch::kFloat32);
+  Tensor dbias, ws;
+  if (want_dbias) {
+    dbias = torch::empty({N}, f32);
+    ws = torch::empty({(int64_t)hx_colsum_ws_floats(rows, N)}, f32);
+  }
+  hx_bias_act_bwd(act_bf16(dout), (int)act, dout.data_ptr(), has(y) ? y->data_ptr() : nullptr, ptr_or_null<float>(b),
+                  has(saved_out) ? saved_out->data_ptr() : nullptr, dy.data_ptr(),
+                  want_dbias ? ws.data_ptr<float>() : nullptr, want_dbias ? dbias.data_ptr<float>() : nullptr, rows, N,
+                  0, cur_stream(dout));
+  return {dy, dbias};
+}
+
+Tensor colsum(Tensor x, OptT scale) {
+  check_cuda(x, "input");
+  const int N = (int)x.size(-1);
+  const int64_t rows = x.numel() / N;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto f32 = x.options().dtype(torch::kFloat32);
+  auto out = torch::empty({N}, f32);
+  auto ws = torch::empty({(int64_t)hx_colsum_ws_floats(rows, N)}, f32);
+  hx_colsum(act_bf16(x), x.data_ptr(), ptr_or_null<float>(scale), ws.data_ptr<float>(), out.data_ptr<float>(), rows,
+            N, 0, cur_stream(x));
+  return out;
+}
+
+Tensor dropout(Tensor x, double keep_prob, int64_t seed, int64_t stream) {
+  check_cuda(x, "input");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  auto out = torch::empty_like(x);
+  hx_dropout(act_bf16(x), x.data_ptr(), out.data_ptr(), x.numel(), (float)keep_prob, (uint64_t)seed,
+             (uint64_t)stream, cur_stream(x));
+  return out;
+}
+
+Tensor softmax_xent_(Tensor logits, OptT bias, Tensor labels, int64_t ignore_index) {
+  TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "logits must be a 2-D row-major GPU tensor");
+  check_cuda(labels, "labels");
+  TORCH_CHECK(labels.scalar_type() == torch::kInt64 && labels.numel() == logits.size(0), "labels must be int64 [rows]");
+  if (has(bias)) {
+    check_f32(*bias, "bias");
+    TORCH_CHECK(bias->numel() >= logits.size(1), "bias too small");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(logits.device());
+  auto loss = torch::empty({logits.size(0)}, logits.options().dtype(torch::kFloat32));
+  hx_softmax_xent(act_bf16(logits), logits.data_ptr(), ptr_or_null<float>(bias), labels.data_ptr<int64_t>(),
+                  loss.data_ptr<float>(), logits.size(0), (int)logits.size(1), logits.stride(0), ignore_index,
+                  cur_stream(logits));
+  return loss;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "hetseq_9cme_amd gfx950 (MI355X) kernels";
+  m.def("grad_norm_clip", &grad_norm_clip);
+  m.def("adam", &adam);
+  m.def("adadelta", &adadelta);
+  m.def("ln_fwd", &ln_fwd);
+  m.def("ln_bwd", &ln_bwd);
+  m.def("embed_ln_fwd", &embed_ln_fwd);
+  m.def("embed_grads", &embed_grads);
+  m.def("bias_act_fwd", &bias_act_fwd);
+  m.def("bias_act_bwd", &bias_act_bwd);
+  m.def("colsum", &colsum);
+  m.def("dropout", &dropout);
+  m.def("softmax_xent_", &softmax_xent_);
+}

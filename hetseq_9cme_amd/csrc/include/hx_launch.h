@@ -1,0 +1,45 @@
+// Host-callable launchers of the gfx950 kernels.  Pure C++ signatures (raw
+// pointers + hipStream_t) so the kernel TUs never include torch headers; the
+// torch-facing argument checking lives in csrc/bindings.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// optim.hip
+int hx_grad_norm_partials();
+void hx_grad_norm_clip(const float* g, int64_t n, double* partial_ws, float* gscale, float* out_norm, float* clipped,
+                       float max_norm, hipStream_t s);
+void hx_adam(float* p, const float* g, float* m, float* v, uint16_t* shadow, const float* gscale, int64_t n, float b1,
+             float b2, float eps, float step_size, float wd_lr, hipStream_t s);
+void hx_adadelta(float* p, const float* g, float* sq, float* acc, const float* gscale, int64_t n, float lr, float rho,
+                 float eps, float wd, hipStream_t s);
+
+// layernorm.hip
+int hx_ln_bwd_blocks(int64_t rows);
+void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, const float* gamma, const float* beta,
+               void* out, void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob,
+               uint64_t seed, uint64_t stream, int drop_after, hipStream_t s);
+void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma,
+               void* dz, void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, uint64_t seed,
+               uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
+               int accumulate, hipStream_t s);
+void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,
+                     const float* wtt, const float* gamma, const float* beta, void* out, void* zsave, float* mean,
+                     float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, uint64_t seed,
+                     uint64_t stream, hipStream_t s);
+void hx_embed_grads(int bf16, const void* dz, const int64_t* ids, const int64_t* tt, float* dwte, float* dwpe,
+                    float* dwtt, int B, int S, int H, int ntypes, hipStream_t s);
+
+// elementwise.hip
+int hx_colsum_ws_floats(int64_t rows, int N);
+void hx_bias_act_fwd(int bf16, int act, const void* y, const float* b, void* out, int64_t rows, int N, hipStream_t s);
+void hx_bias_act_bwd(int bf16, int act, const void* dout, const void* y, const float* b, const void* saved_out,
+                     void* dy, float* partial, float* dbias, int64_t rows, int N, int accumulate, hipStream_t s);
+void hx_colsum(int bf16, void* x, const float* scale, float* partial, float* out, int64_t rows, int N, int accumulate,
+               hipStream_t s);
+void hx_dropout(int bf16, const void* x, void* out, int64_t n, float keep_prob, uint64_t seed, uint64_t stream,
+                hipStream_t s);
+
+// xent.hip
+void hx_softmax_xent(int bf16, void* logits, const float* bias, const int64_t* labels, float* loss, int64_t rows,
+                     int V, int64_t ld, int64_t ignore_index, hipStream_t s);

@@ -1,0 +1,38 @@
+// 4-wide vector load/store for fp32 and bf16 activations (fp32 compute).
+#pragma once
+#include "hx_common.h"
+
+namespace hx {
+
+template <typename T>
+__device__ __forceinline__ float4 load4(const T* p);
+template <>
+__device__ __forceinline__ float4 load4<float>(const float* p) {
+  return *reinterpret_cast<const float4*>(p);
+}
+template <>
+__device__ __forceinline__ float4 load4<uint16_t>(const uint16_t* p) {
+  const ushort4 v = *reinterpret_cast<const ushort4*>(p);
+  return make_float4(bf2f(v.x), bf2f(v.y), bf2f(v.z), bf2f(v.w));
+}
+
+template <typename T>
+__device__ __forceinline__ void store4(T* p, float4 v);
+template <>
+__device__ __forceinline__ void store4<float>(float* p, float4 v) {
+  *reinterpret_cast<float4*>(p) = v;
+}
+template <>
+__device__ __forceinline__ void store4<uint16_t>(uint16_t* p, float4 v) {
+  ushort4 o;
+  o.x = f2bf(v.x);
+  o.y = f2bf(v.y);
+  o.z = f2bf(v.z);
+  o.w = f2bf(v.w);
+  *reinterpret_cast<ushort4*>(p) = o;
+}
+
+__device__ __forceinline__ float get(const float4& v, int k) { return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w; }
+__device__ __forceinline__ float4 f4(float a) { return make_float4(a, a, a, a); }
+
+}  // namespace hx

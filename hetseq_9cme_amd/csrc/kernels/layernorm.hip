@@ -1,0 +1,442 @@
+// Fused (bias + dropout + residual + LayerNorm) forward / backward and the fused
+// BERT embedding (3 gathers + sum + LayerNorm + dropout).
+//
+// Reference sites (all TF-style LN, eps inside the sqrt, bert_modeling.py:276-289):
+//   BertSelfOutput / BertOutput  : LN(dropout(dense(h) + b) + residual)  (:387-391, :423-427)
+//   BertPredictionHeadTransform  : LN(gelu(dense(h) + b))                 (:526-527)
+//   BertEmbeddings               : dropout(LN(word[id] + pos[s] + type[tt])) (:306-320)
+// The reference issues ~8 elementwise/reduction kernels per LN forward and ~15 in
+// autograd backward; here each is ONE row-per-wave kernel:
+//   * a wave64 owns a row; H = CH*256 columns are held in registers as CH float4 per
+//     lane (H=768 -> 3 x 16 B per lane), so the row is read once and written once;
+//   * dropout masks come from Philox(seed, stream, element) and are regenerated in
+//     backward (nothing stored);
+//   * backward produces dz (= d residual), dy (= d dense-output), and per-block
+//     column partials of dgamma / dbeta / dbias that a second kernel folds; rows are
+//     grid-strided over a bounded number of workgroups so the partial slab stays small.
+// Activations may be fp32 or bf16 (T); statistics and affine params are fp32.
+#include "hx_launch.h"
+#include "hx_vec.h"
+
+namespace {
+
+constexpr int NT = 256;             // 4 waves
+constexpr int WPB = NT / 64;
+
+template <int CH>
+struct Row {
+  float4 v[CH];
+};
+
+// ----------------------------------------------------------------------------- fwd
+template <typename T, int CH, bool kDropAfter>
+__global__ __launch_bounds__(NT) void ln_fwd_k(const T* __restrict__ y, const float* __restrict__ bias,
+                                             const T* __restrict__ res, const float* __restrict__ gamma,
+                                             const float* __restrict__ beta, T* __restrict__ out,
+                                             T* __restrict__ zsave, float* __restrict__ mean_out,
+                                             float* __restrict__ rstd_out, int64_t rows, int H, float eps,
+                                             float keep_prob, uint64_t seed, uint64_t stream) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = blockIdx.x * (int64_t)WPB + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * WPB;
+  const float inv_keep = keep_prob > 0.f ? 1.f / keep_prob : 0.f;
+  const bool drop = keep_prob < 1.f;
+  for (int64_t r = wave; r < rows; r += nw) {
+    Row<CH> x;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int j = (c * 64 + lane) * 4;
+      float4 v = hx::f4(0.f);
+      if (j < H) {
+        v = hx::load4(y + r * H + j);
+        if (bias) {
+          const float4 b = *reinterpret_cast<const float4*>(bias + j);
+          v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+        }
+        if (drop && !kDropAfter) {
+          const uint32_t k = hx::keep4(seed, stream, (uint64_t)(r * H + j) >> 2, keep_prob);
+          v.x = (k & 1) ? v.x * inv_keep : 0.f;
+          v.y = (k & 2) ? v.y * inv_keep : 0.f;
+          v.z = (k & 4) ? v.z * inv_keep : 0.f;
+          v.w = (k & 8) ? v.w * inv_keep : 0.f;
+        }
+        if (res) {
+          const float4 q = hx::load4(res + r * H + j);
+          v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
+        }
+        if (zsave) hx::store4(zsave + r * H + j, v);
+      }
+      x.v[c] = v;
+      s += v.x + v.y + v.z + v.w;
+    }
+    const float mean = hx::wave_sum(s) / H;
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int j = (c * 64 + lane) * 4;
+      if (j < H) {
+        const float4 v = x.v[c];
+        const float a = v.x - mean, b = v.y - mean, cc = v.z - mean, d = v.w - mean;
+        ss += a * a + b * b + cc * cc + d * d;
+      }
+    }
+    const float var = hx::wave_sum(ss) / H;
+    const float rstd = 1.0f / sqrtf(var + eps);
+    if (lane == 0) {
+      mean_out[r] = mean;
+      rstd_out[r] = rstd;
+    }
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int j = (c * 64 + lane) * 4;
+      if (j < H) {
+        const float4 g = *reinterpret_cast<const float4*>(gamma + j);
+        const float4 b = *reinterpret_cast<const float4*>(beta + j);
+        const float4 v = x.v[c];
+        float4 o = make_float4(g.x * ((v.x - mean) * rstd) + b.x, g.y * ((v.y - mean) * rstd) + b.y,
+                               g.z * ((v.z - mean) * rstd) + b.z, g.w * ((v.w - mean) * rstd) + b.w);
+        if (drop && kDropAfter) {
+          const uint32_t k = hx::keep4(seed, stream, (uint64_t)(r * H + j) >> 2, keep_prob);
+          o.x = (k & 1) ? o.x * inv_keep : 0.f;
+          o.y = (k & 2) ? o.y * inv_keep : 0.f;
+          o.z = (k & 4) ? o.z * inv_keep : 0.f;
+          o.w = (k & 8) ? o.w * inv_keep : 0.f;
+        }
+        hx::store4(out + r * H + j, o);
+      }
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------- bwd
+// dout -> (optional dropout-after inverse) -> LN backward -> dz ; dy = dz*mask/keep
+// partial[blk][0:H)=dgamma, [H:2H)=dbeta, [2H:3H)=dbias(dy)
+template <typename T, int CH, bool kDropAfter>
+__global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const T* __restrict__ z,
+                                             const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+                                             const float* __restrict__ gamma, T* __restrict__ dz_out,
+                                             T* __restrict__ dy_out, float* __restrict__ partial, int64_t rows,
+                                             int H, float keep_prob, uint64_t seed, uint64_t stream,
+                                             int want_dbias) {
+  __shared__ float red[WPB][CH * 256];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int64_t wave = blockIdx.x * (int64_t)WPB + w;
+  const int64_t nw = (int64_t)gridDim.x * WPB;
+  const float inv_keep = keep_prob > 0.f ? 1.f / keep_prob : 0.f;
+  const bool drop = keep_prob < 1.f;
+  Row<CH> dg, db, dbias;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) dg.v[c] = db.v[c] = dbias.v[c] = hx::f4(0.f);
+
+  for (int64_t r = wave; r < rows; r += nw) {
+    const float mean = mean_in[r], rstd = rstd_in[r];
+    Row<CH> xh, dxh;
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int j = (c * 64 + lane) * 4;
+      float4 xv = hx::f4(0.f), dv = hx::f4(0.f);
+      if (j < H) {
+        const float4 zz = hx::load4(z + r * H + j);
+        float4 d = hx::load4(dout + r * H + j);
+        if (drop && kDropAfter) {
+          const uint32_t k = hx::keep4(seed, stream, (uint64_t)(r * H + j) >> 2, keep_prob);
+          d.x = (k & 1) ? d.x * inv_keep : 0.f;
+          d.y = (k & 2) ? d.y * inv_keep : 0.f;
+          d.z = (k & 4) ? d.z * inv_keep : 0.f;
+          d.w = (k & 8) ? d.w * inv_keep : 0.f;
+        }
+        const float4 g = *reinterpret_cast<const float4*>(gamma + j);
+        xv = make_float4((zz.x - mean) * rstd, (zz.y - mean) * rstd, (zz.z - mean) * rstd, (zz.w - mean) * rstd);
+        dv = make_float4(d.x * g.x, d.y * g.y, d.z * g.z, d.w * g.w);
+        dg.v[c].x += d.x * xv.x; dg.v[c].y += d.y * xv.y; dg.v[c].z += d.z * xv.z; dg.v[c].w += d.w * xv.w;
+        db.v[c].x += d.x; db.v[c].y += d.y; db.v[c].z += d.z; db.v[c].w += d.w;
+        s1 += dv.x + dv.y + dv.z + dv.w;
+        s2 += dv.x * xv.x + dv.y * xv.y + dv.z * xv.z + dv.w * xv.w;
+      }
+      xh.v[c] = xv;
+      dxh.v[c] = dv;
+    }
+    const float m1 = hx::wave_sum(s1) / H;
+    const float m2 = hx::wave_sum(s2) / H;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int j = (c * 64 + lane) * 4;
+      if (j < H) {
+        const float4 xv = xh.v[c], dv = dxh.v[c];
+        float4 dz = make_float4(rstd * (dv.x - m1 - xv.x * m2), rstd * (dv.y - m1 - xv.y * m2),
+                                rstd * (dv.z - m1 - xv.z * m2), rstd * (dv.w - m1 - xv.w * m2));
+        hx::store4(dz_out + r * H + j, dz);
+        if (dy_out) {
+          float4 dy = dz;
+          if (drop && !kDropAfter) {
+            const uint32_t k = hx::keep4(seed, stream, (uint64_t)(r * H + j) >> 2, keep_prob);
+            dy.x = (k & 1) ? dy.x * inv_keep : 0.f;
+            dy.y = (k & 2) ? dy.y * inv_keep : 0.f;
+            dy.z = (k & 4) ? dy.z * inv_keep : 0.f;
+            dy.w = (k & 8) ? dy.w * inv_keep : 0.f;
+          }
+          hx::store4(dy_out + r * H + j, dy);
+          if (want_dbias) {
+            dbias.v[c].x += dy.x; dbias.v[c].y += dy.y; dbias.v[c].z += dy.z; dbias.v[c].w += dy.w;
+          }
+        }
+      }
+    }
+  }
+  // fold the 4 waves' column partials through LDS: three passes (gamma, beta, bias)
+  const int nsum = want_dbias ? 3 : 2;
+  for (int q = 0; q < nsum; ++q) {
+    Row<CH>& src = q == 0 ? dg : (q == 1 ? db : dbias);
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int j = (c * 64 + lane) * 4;
+      *reinterpret_cast<float4*>(&red[w][j]) = src.v[c];
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < H; j += NT) {
+      float a = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < WPB; ++ww) a += red[ww][j];
+      partial[((int64_t)blockIdx.x * 3 + q) * H + j] = a;
+    }
+    __syncthreads();
+  }
+}
+
+// sum partial[nblk][3][H] over blocks -> out0/out1/out2 (any may be null); accumulate=1 adds
+__global__ __launch_bounds__(NT) void colsum3_k(const float* __restrict__ partial, int nblk, int H,
+                                              float* __restrict__ o0, float* __restrict__ o1,
+                                              float* __restrict__ o2, int accumulate) {
+  const int q = blockIdx.y;
+  float* o = q == 0 ? o0 : (q == 1 ? o1 : o2);
+  if (!o) return;
+  for (int j = blockIdx.x * NT + threadIdx.x; j < H; j += gridDim.x * NT) {
+    float a = 0.f;
+    for (int b = 0; b < nblk; ++b) a += partial[((int64_t)b * 3 + q) * H + j];
+    o[j] = accumulate ? o[j] + a : a;
+  }
+}
+
+// ------------------------------------------------------------------------ embedding
+template <typename T, int CH>
+__global__ __launch_bounds__(NT) void embed_ln_fwd_k(const int64_t* __restrict__ ids, const int64_t* __restrict__ tt,
+                                                   const float* __restrict__ wte, const float* __restrict__ wpe,
+                                                   const float* __restrict__ wtt, const float* __restrict__ gamma,
+                                                   const float* __restrict__ beta, T* __restrict__ out,
+                                                   T* __restrict__ zsave, float* __restrict__ mean_out,
+                                                   float* __restrict__ rstd_out, int64_t rows, int S, int H,
+                                                   float eps, float keep_prob, uint64_t seed, uint64_t stream) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = blockIdx.x * (int64_t)WPB + (threadIdx.x >> 6);
+  const int64_t nw = (int64_t)gridDim.x * WPB;
+  const float inv_keep = keep_prob > 0.f ? 1.f / keep_prob : 0.f;
+  for (int64_t r = wave; r < rows; r += nw) {
+    const int64_t id = ids[r];
+    const int64_t ty = tt ? tt[r] : 0;
+    const int64_t pos = r % S;
+    Row<CH> x;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int j = (c * 64 + lane) * 4;
+      float4 v = hx::f4(0.f);
+      if (j < H) {
+        const float4 a = *reinterpret_cast<const float4*>(wte + id * H + j);
+        const float4 b = *reinterpret_cast<const float4*>(wpe + pos * H + j);
+        const float4 d = *reinterpret_cast<const float4*>(wtt + ty * H + j);
+        v = make_float4(a.x + b.x + d.x, a.y + b.y + d.y, a.z + b.z + d.z, a.w + b.w + d.w);
+        hx::store4(zsave + r * H + j, v);
+      }
+      x.v[c] = v;
+      s += v.x + v.y + v.z + v.w;
+    }
+    const float mean = hx::wave_sum(s) / H;
+    float ss = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int j = (c * 64 + lane) * 4;
+      if (j < H) {
+        const float4 v = x.v[c];
+        const float a = v.x - mean, b = v.y - mean, cc = v.z - mean, d = v.w - mean;
+        ss += a * a + b * b + cc * cc + d * d;
+      }
+    }
+    const float rstd = 1.0f / sqrtf(hx::wave_sum(ss) / H + eps);
+    if (lane == 0) {
+      mean_out[r] = mean;
+      rstd_out[r] = rstd;
+    }
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int j = (c * 64 + lane) * 4;
+      if (j < H) {
+        const float4 g = *reinterpret_cast<const float4*>(gamma + j);
+        const float4 b = *reinterpret_cast<const float4*>(beta + j);
+        const float4 v = x.v[c];
+        float4 o = make_float4(g.x * ((v.x - mean) * rstd) + b.x, g.y * ((v.y - mean) * rstd) + b.y,
+                               g.z * ((v.z - mean) * rstd) + b.z, g.w * ((v.w - mean) * rstd) + b.w);
+        if (keep_prob < 1.f) {
+          const uint32_t k = hx::keep4(seed, stream, (uint64_t)(r * H + j) >> 2, keep_prob);
+          o.x = (k & 1) ? o.x * inv_keep : 0.f;
+          o.y = (k & 2) ? o.y * inv_keep : 0.f;
+          o.z = (k & 4) ? o.z * inv_keep : 0.f;
+          o.w = (k & 8) ? o.w * inv_keep : 0.f;
+        }
+        hx::store4(out + r * H + j, o);
+      }
+    }
+  }
+}
+
+// word-embedding gradient: scatter-add rows of dz into dW[ids] (fp32 atomics,
+// whole 16-B contiguous lane groups -> 256 contiguous bytes per wave instruction).
+template <typename T>
+__global__ __launch_bounds__(NT) void embed_word_grad_k(const T* __restrict__ dz, const int64_t* __restrict__ ids,
+                                                      float* __restrict__ dw, int64_t rows, int H) {
+  const int64_t wave = blockIdx.x * (int64_t)WPB + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int64_t nw = (int64_t)gridDim.x * WPB;
+  for (int64_t r = wave; r < rows; r += nw) {
+    const int64_t id = ids[r];
+    for (int j = lane; j < H; j += 64) atomicAdd(dw + id * H + j, hx::io<T>::ld(dz + r * H + j));
+  }
+}
+
+// position + token-type gradients: block (s-tile) reduces over the batch dim.
+// dpos[s][j] = sum_b dz[b,s,j] ; dtype[t][j] += sum over rows with tt==t (atomics per block)
+template <typename T>
+__global__ __launch_bounds__(NT) void embed_pos_type_grad_k(const T* __restrict__ dz, const int64_t* __restrict__ tt,
+                                                          float* __restrict__ dpos, float* __restrict__ dtype,
+                                                          int B, int S, int H, int ntypes) {
+  const int s = blockIdx.x;
+  for (int j = threadIdx.x; j < H; j += NT) {
+    float ap = 0.f, a0 = 0.f, a1 = 0.f;
+    for (int b = 0; b < B; ++b) {
+      const int64_t r = (int64_t)b * S + s;
+      const float v = hx::io<T>::ld(dz + r * H + j);
+      ap += v;
+      const int64_t ty = tt ? tt[r] : 0;
+      if (ty == 0) a0 += v;
+      else if (ty == 1) a1 += v;
+      else atomicAdd(dtype + ty * H + j, v);
+    }
+    dpos[(int64_t)s * H + j] += ap;
+    atomicAdd(dtype + j, a0);
+    if (ntypes > 1) atomicAdd(dtype + H + j, a1);
+  }
+}
+
+int pick_ch(int H) {
+  const int c = (H + 255) / 256;
+  if (c <= 1) return 1;
+  if (c <= 2) return 2;
+  if (c <= 3) return 3;
+  if (c <= 4) return 4;
+  return 8;
+}
+
+inline int ln_grid(int64_t rows, int cap) {
+  int64_t g = (rows + WPB - 1) / WPB;
+  return (int)(g < cap ? (g < 1 ? 1 : g) : cap);
+}
+
+#define HX_CH_DISPATCH(H, ...)          \
+  switch (pick_ch(H)) {                 \
+    case 1: { constexpr int CH = 1; __VA_ARGS__; } break; \
+    case 2: { constexpr int CH = 2; __VA_ARGS__; } break; \
+    case 3: { constexpr int CH = 3; __VA_ARGS__; } break; \
+    case 4: { constexpr int CH = 4; __VA_ARGS__; } break; \
+    default: { constexpr int CH = 8; __VA_ARGS__; } break; \
+  }
+
+template <typename T>
+void ln_fwd_t(const void* y, const float* bias, const void* res, const float* gamma, const float* beta, void* out,
+              void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob, uint64_t seed,
+              uint64_t stream, int drop_after, hipStream_t s) {
+  const int grid = ln_grid(rows, 4096);
+  HX_CH_DISPATCH(H, {
+    if (drop_after)
+      ln_fwd_k<T, CH, true><<<grid, NT, 0, s>>>((const T*)y, bias, (const T*)res, gamma, beta, (T*)out, (T*)zsave,
+                                                mean, rstd, rows, H, eps, keep_prob, seed, stream);
+    else
+      ln_fwd_k<T, CH, false><<<grid, NT, 0, s>>>((const T*)y, bias, (const T*)res, gamma, beta, (T*)out, (T*)zsave,
+                                                 mean, rstd, rows, H, eps, keep_prob, seed, stream);
+  })
+}
+
+template <typename T>
+void ln_bwd_t(const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma, void* dz,
+              void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, uint64_t seed,
+              uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
+              int accumulate, hipStream_t s) {
+  HX_CH_DISPATCH(H, {
+    if (drop_after)
+      ln_bwd_k<T, CH, true><<<nblk, NT, 0, s>>>((const T*)dout, (const T*)z, mean, rstd, gamma, (T*)dz, (T*)dy,
+                                                partial, rows, H, keep_prob, seed, stream, want_dbias);
+    else
+      ln_bwd_k<T, CH, false><<<nblk, NT, 0, s>>>((const T*)dout, (const T*)z, mean, rstd, gamma, (T*)dz, (T*)dy,
+                                                 partial, rows, H, keep_prob, seed, stream, want_dbias);
+  })
+  dim3 g((H + NT - 1) / NT, 3);
+  colsum3_k<<<g, NT, 0, s>>>(partial, nblk, H, dgamma, dbeta, want_dbias ? dbias : nullptr, accumulate);
+}
+
+}  // namespace
+
+int hx_ln_bwd_blocks(int64_t rows) { return ln_grid(rows, 512); }
+
+void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, const float* gamma, const float* beta,
+               void* out, void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob,
+               uint64_t seed, uint64_t stream, int drop_after, hipStream_t s) {
+  if (bf16)
+    ln_fwd_t<uint16_t>(y, bias, res, gamma, beta, out, zsave, mean, rstd, rows, H, eps, keep_prob, seed, stream,
+                       drop_after, s);
+  else
+    ln_fwd_t<float>(y, bias, res, gamma, beta, out, zsave, mean, rstd, rows, H, eps, keep_prob, seed, stream,
+                    drop_after, s);
+}
+
+void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma,
+               void* dz, void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, uint64_t seed,
+               uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
+               int accumulate, hipStream_t s) {
+  if (bf16)
+    ln_bwd_t<uint16_t>(dout, z, mean, rstd, gamma, dz, dy, partial, nblk, rows, H, keep_prob, seed, stream,
+                       drop_after, want_dbias, dgamma, dbeta, dbias, accumulate, s);
+  else
+    ln_bwd_t<float>(dout, z, mean, rstd, gamma, dz, dy, partial, nblk, rows, H, keep_prob, seed, stream, drop_after,
+                    want_dbias, dgamma, dbeta, dbias, accumulate, s);
+}
+
+void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,
+                     const float* wtt, const float* gamma, const float* beta, void* out, void* zsave, float* mean,
+                     float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, uint64_t seed,
+                     uint64_t stream, hipStream_t s) {
+  const int grid = ln_grid(rows, 4096);
+  HX_CH_DISPATCH(H, {
+    if (bf16)
+      embed_ln_fwd_k<uint16_t, CH><<<grid, NT, 0, s>>>(ids, tt, wte, wpe, wtt, gamma, beta, (uint16_t*)out,
+                                                       (uint16_t*)zsave, mean, rstd, rows, S, H, eps, keep_prob,
+                                                       seed, stream);
+    else
+      embed_ln_fwd_k<float, CH><<<grid, NT, 0, s>>>(ids, tt, wte, wpe, wtt, gamma, beta, (float*)out,
+                                                    (float*)zsave, mean, rstd, rows, S, H, eps, keep_prob, seed,
+                                                    stream);
+  })
+}
+
+void hx_embed_grads(int bf16, const void* dz, const int64_t* ids, const int64_t* tt, float* dwte, float* dwpe,
+                    float* dwtt, int B, int S, int H, int ntypes, hipStream_t s) {
+  const int64_t rows = (int64_t)B * S;
+  const int grid = ln_grid(rows, 4096);
+  if (bf16) {
+    embed_word_grad_k<uint16_t><<<grid, NT, 0, s>>>((const uint16_t*)dz, ids, dwte, rows, H);
+    embed_pos_type_grad_k<uint16_t><<<S, NT, 0, s>>>((const uint16_t*)dz, tt, dwpe, dwtt, B, S, H, ntypes);
+  } else {
+    embed_word_grad_k<float><<<grid, NT, 0, s>>>((const float*)dz, ids, dwte, rows, H);
+    embed_pos_type_grad_k<float><<<S, NT, 0, s>>>((const float*)dz, tt, dwpe, dwtt, B, S, H, ntypes);
+  }
+}

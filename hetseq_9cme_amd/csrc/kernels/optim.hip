@@ -1,0 +1,170 @@
+// Optimizer-side kernels over the FLAT fp32 parameter / gradient / moment buffers.
+//
+// Replaces the reference's per-parameter Python loops (hetseq/optim.py:59-70
+// multiply_grads + clip_grad_norm_, :162-231 Adam, :263-304 Adadelta; ~1,850
+// launches per BERT step) with:
+//   1. grad_norm_partial : one grid-stride L2 reduction over the whole flat grad
+//      buffer (float4 loads, per-block double partial)
+//   2. grad_norm_finalize: one workgroup folds the partials, applies the pending
+//      grad scale (W / sample_size, a DEVICE scalar), computes the clip coefficient
+//      and folds it into the same scalar -- no host synchronisation.
+//   3. adam / adadelta   : one streaming pass per contiguous parameter run reading
+//      p, g, m, v once (16 B per lane per stream) and writing p, m, v (+ optional
+//      bf16 shadow of p for the bf16 compute path).
+// HBM-bound: BERT-base (110.1M params) Adam moves 7 x 440 MB = 3.1 GB -> ~0.5 ms.
+#include "hx_common.h"
+#include "hx_launch.h"
+
+namespace {
+
+constexpr int NT = 256;
+
+__global__ __launch_bounds__(NT) void grad_norm_partial_k(const float* __restrict__ g, int64_t n,
+                                                        double* __restrict__ partial) {
+  __shared__ float scratch[NT / 64];
+  const int64_t n4 = n >> 2;
+  const float4* g4 = reinterpret_cast<const float4*>(g);
+  float acc = 0.f;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT) {
+    const float4 v = g4[i];
+    acc = fmaf(v.x, v.x, acc);
+    acc = fmaf(v.y, v.y, acc);
+    acc = fmaf(v.z, v.z, acc);
+    acc = fmaf(v.w, v.w, acc);
+  }
+  // tail (n not a multiple of 4)
+  for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT)
+    acc = fmaf(g[i], g[i], acc);
+  const float s = hx::block_sum<NT>(acc, scratch);
+  if (threadIdx.x == 0) partial[blockIdx.x] = (double)s;
+}
+
+__global__ __launch_bounds__(NT) void grad_norm_finalize_k(const double* __restrict__ partial, int np,
+                                                         float* __restrict__ gscale, float* __restrict__ out_norm,
+                                                         float* __restrict__ clipped, float max_norm) {
+  __shared__ double sd[NT / 64];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < np; i += NT) acc += partial[i];
+  acc = hx::wave_sum_d(acc);
+  if ((threadIdx.x & 63) == 0) sd[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < NT / 64; ++w) t += sd[w];
+    const float gs = gscale[0];
+    const float norm = (float)sqrt(t) * fabsf(gs);
+    out_norm[0] = norm;
+    if (max_norm > 0.f) {
+      const float coef = fminf(1.0f, max_norm / (norm + 1e-6f));
+      clipped[0] = norm > max_norm ? 1.f : 0.f;
+      gscale[0] = gs * coef;
+    } else {
+      clipped[0] = 0.f;
+    }
+  }
+}
+
+template <bool kShadow>
+__global__ __launch_bounds__(NT) void adam_k(float* __restrict__ p, const float* __restrict__ g,
+                                           float* __restrict__ m, float* __restrict__ v,
+                                           uint16_t* __restrict__ shadow, const float* __restrict__ gscale,
+                                           int64_t n, float b1, float b2, float eps, float step_size,
+                                           float wd_lr) {
+  const float gs = gscale[0];
+  const float ob1 = 1.f - b1, ob2 = 1.f - b2;
+  const int64_t n4 = n >> 2;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT) {
+    float4 pp = reinterpret_cast<float4*>(p)[i];
+    const float4 gg = reinterpret_cast<const float4*>(g)[i];
+    float4 mm = reinterpret_cast<float4*>(m)[i];
+    float4 vv = reinterpret_cast<float4*>(v)[i];
+    float* pa = &pp.x;
+    const float* ga = &gg.x;
+    float* ma = &mm.x;
+    float* va = &vv.x;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float gr = ga[j] * gs;
+      ma[j] = ma[j] * b1 + ob1 * gr;
+      va[j] = va[j] * b2 + ob2 * gr * gr;
+      const float denom = sqrtf(va[j]) + eps;
+      float x = pa[j];
+      x = x - wd_lr * x;
+      x = x - step_size * (ma[j] / denom);
+      pa[j] = x;
+    }
+    reinterpret_cast<float4*>(p)[i] = pp;
+    reinterpret_cast<float4*>(m)[i] = mm;
+    reinterpret_cast<float4*>(v)[i] = vv;
+    if (kShadow) {
+      ushort4 s;
+      s.x = hx::f2bf(pp.x);
+      s.y = hx::f2bf(pp.y);
+      s.z = hx::f2bf(pp.z);
+      s.w = hx::f2bf(pp.w);
+      reinterpret_cast<ushort4*>(shadow)[i] = s;
+    }
+  }
+  for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    const float gr = g[i] * gs;
+    const float mi = m[i] * b1 + ob1 * gr;
+    const float vi = v[i] * b2 + ob2 * gr * gr;
+    m[i] = mi;
+    v[i] = vi;
+    float x = p[i];
+    x = x - wd_lr * x;
+    x = x - step_size * (mi / (sqrtf(vi) + eps));
+    p[i] = x;
+    if (kShadow) shadow[i] = hx::f2bf(x);
+  }
+}
+
+__global__ __launch_bounds__(NT) void adadelta_k(float* __restrict__ p, const float* __restrict__ g,
+                                               float* __restrict__ sq, float* __restrict__ acc,
+                                               const float* __restrict__ gscale, int64_t n, float lr, float rho,
+                                               float eps, float wd) {
+  const float gs = gscale[0];
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
+    float gr = g[i] * gs;
+    const float x = p[i];
+    if (wd != 0.f) gr = gr + wd * x;
+    const float s = sq[i] * rho + (1.f - rho) * gr * gr;
+    const float std_ = sqrtf(s + eps);
+    const float delta = sqrtf(acc[i] + eps) / std_ * gr;
+    p[i] = x - lr * delta;
+    acc[i] = acc[i] * rho + (1.f - rho) * delta * delta;
+    sq[i] = s;
+  }
+}
+
+inline int grid_for(int64_t n_vec, int cap = 4096) {
+  int64_t b = (n_vec + NT - 1) / NT;
+  if (b < 1) b = 1;
+  if (b > cap) b = cap;
+  return (int)b;
+}
+
+}  // namespace
+
+int hx_grad_norm_partials() { return 1024; }
+
+void hx_grad_norm_clip(const float* g, int64_t n, double* partial_ws, float* gscale, float* out_norm,
+                       float* clipped, float max_norm, hipStream_t s) {
+  const int np = hx_grad_norm_partials();
+  grad_norm_partial_k<<<np, NT, 0, s>>>(g, n, partial_ws);
+  grad_norm_finalize_k<<<1, NT, 0, s>>>(partial_ws, np, gscale, out_norm, clipped, max_norm);
+}
+
+void hx_adam(float* p, const float* g, float* m, float* v, uint16_t* shadow, const float* gscale, int64_t n,
+             float b1, float b2, float eps, float step_size, float wd_lr, hipStream_t s) {
+  const int grid = grid_for((n + 3) / 4, 8192);
+  if (shadow)
+    adam_k<true><<<grid, NT, 0, s>>>(p, g, m, v, shadow, gscale, n, b1, b2, eps, step_size, wd_lr);
+  else
+    adam_k<false><<<grid, NT, 0, s>>>(p, g, m, v, shadow, gscale, n, b1, b2, eps, step_size, wd_lr);
+}
+
+void hx_adadelta(float* p, const float* g, float* sq, float* acc, const float* gscale, int64_t n, float lr,
+                 float rho, float eps, float wd, hipStream_t s) {
+  adadelta_k<<<grid_for(n, 8192), NT, 0, s>>>(p, g, sq, acc, gscale, n, lr, rho, eps, wd);
+}

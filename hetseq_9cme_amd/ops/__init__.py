@@ -1,0 +1,25 @@
+"""MI355X (gfx950) compute ops.
+
+Public functional API used by the models and the engine.  Each op runs a
+hand-written HIP kernel for GPU tensors and a torch reference for CPU tensors.
+"""
+from ._ext import C, use_kernels, set_fused, fused_enabled  # noqa: F401
+from .rng import get_rng, set_step_seed  # noqa: F401
+from .fused import (  # noqa: F401
+    embed_ln, bias_dropout_residual_ln, layer_norm, bias_act, dropout, linear3, attention,
+    decoder_xent, masked_rows, gelu_ref, layer_norm_ref,
+)
+
+
+def flat_grad_norm_clip(grad_flat, gscale, out_norm, clipped, max_norm):
+    """One reduction over the flat grad buffer: norm = ||g|| * |gscale|; clip
+    coefficient folded into ``gscale`` on device."""
+    C().grad_norm_clip(grad_flat, gscale, out_norm, clipped, float(max_norm))
+
+
+def fused_adam(p, g, m, v, gscale, start, end, beta1, beta2, eps, step_size, wd_lr, bf16_shadow=None):
+    C().adam(p, g, m, v, bf16_shadow, gscale, int(start), int(end), beta1, beta2, eps, step_size, wd_lr)
+
+
+def fused_adadelta(p, g, sq, acc, gscale, start, end, lr, rho, eps, wd):
+    C().adadelta(p, g, sq, acc, gscale, int(start), int(end), lr, rho, eps, wd)

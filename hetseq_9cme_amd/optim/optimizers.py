@@ -1,0 +1,305 @@
+"""Optimizers over the flat parameter space.
+
+API parity with the reference wrapper (hetseq/optim.py:6-131): ``get_lr``,
+``set_lr``, ``state_dict``, ``load_state_dict(sd, overrides)``, ``backward``,
+``multiply_grads``, ``clip_grad_norm``, ``step``, ``zero_grad``; class names
+``_Adam`` / ``_Adadelta`` (checkpoints record ``optimizer_name``).
+
+Update rules (exactly the reference's, optim.py:162-231 / 263-304):
+  Adam (fairseq "AdamW" variant, decoupled weight decay on ALL params):
+      m = b1 m + (1-b1) g ;  v = b2 v + (1-b2) g^2
+      p -= wd*lr*p                                   (if wd != 0)
+      p -= lr*sqrt(1-b2^t)/(1-b1^t) * m/(sqrt(v)+eps)
+  Adadelta: the standard algorithm with L2 weight decay added to the grad.
+
+MI355X-native implementation: parameters, gradients and optimizer moments
+are flat fp32 buffers (``FlatParamSpace``).  ``multiply_grads`` and the clip
+coefficient do not touch memory -- they update a *device* scalar ``gscale``
+that the single fused update kernel applies on the fly; the global grad norm
+is one reduction kernel over the flat gradient buffer.  One step therefore
+costs two small reduction launches + one streaming update launch instead of
+~1,850 launches, and never blocks the host.
+On CPU tensors the same math runs through torch ops (reference/oracle path).
+"""
+import math
+
+import torch
+
+from .. import ops
+
+
+class _Optimizer(object):
+    """Common machinery: flat space, lazy grad scale, LR, state_dict format."""
+
+    def __init__(self, args, flat):
+        self.args = args
+        self.flat = flat
+        self.device = flat.device
+        self._lr = float(args.lr[0])
+        # device-resident scalars: [gscale] ; grad norm result
+        self._gscale = torch.ones(1, dtype=torch.float32, device=self.device)
+        self._gscale_host = 1.0          # host multiplier folded on next use
+        self._grad_norm = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self._clipped = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.used_mask = [True] * len(flat.params)
+        self.param_groups = [dict(self.optimizer_config)]
+        self.param_groups[0]['lr'] = self._lr
+        self.use_kernels = self.device.type == 'cuda' and getattr(args, 'fused_kernels', True)
+
+    # --- LR -----------------------------------------------------------
+    def get_lr(self):
+        return self._lr
+
+    def set_lr(self, lr):
+        self._lr = float(lr)
+        for g in self.param_groups:
+            g['lr'] = self._lr
+
+    @property
+    def params(self):
+        return list(self.flat.params)
+
+    # --- grads --------------------------------------------------------
+    def backward(self, loss):
+        loss.backward()
+
+    def zero_grad(self):
+        self.flat.zero_grad()
+        self._gscale.fill_(1.0)
+        self._gscale_host = 1.0
+
+    def multiply_grads(self, c):
+        """Multiply grads by ``c`` (python number or 0-d/1-elem device tensor).
+        Lazy: folded into the scale applied by the fused kernels."""
+        if torch.is_tensor(c):
+            self._gscale.mul_(c.to(self._gscale.dtype).reshape(1))
+        else:
+            self._gscale_host *= float(c)
+
+    def _fold_host_scale(self):
+        if self._gscale_host != 1.0:
+            self._gscale.mul_(self._gscale_host)
+            self._gscale_host = 1.0
+
+    def clip_grad_norm(self, max_norm):
+        """Global L2 norm of the (scaled) grads; clip by folding the coefficient
+        into ``gscale``.  Returns the pre-clip norm as a 1-element DEVICE tensor
+        (read lazily by the meters)."""
+        self._fold_host_scale()
+        g = self.flat.grad_flat
+        if self.use_kernels:
+            ops.flat_grad_norm_clip(g, self._gscale, self._grad_norm, self._clipped, float(max_norm))
+        else:
+            norm = g.float().norm(2) * self._gscale.abs()
+            self._grad_norm.copy_(norm.reshape(1))
+            if max_norm > 0:
+                coef = (max_norm / (norm + 1e-6)).clamp(max=1.0)
+                self._clipped.copy_((norm > max_norm).float().reshape(1))
+                self._gscale.mul_(coef.reshape(1))
+            else:
+                self._clipped.zero_()
+        return self._grad_norm
+
+    @property
+    def clipped(self):
+        return self._clipped
+
+    # --- state dict (torch-optimizer format, reference-compatible) ------
+    def state_dict(self):
+        state = {}
+        for i, p in enumerate(self.flat.params):
+            s = self._param_state(i)
+            if s is not None:
+                state[i] = s
+        groups = []
+        for g in self.param_groups:
+            gg = {k: v for k, v in g.items()}
+            gg['params'] = list(range(len(self.flat.params)))
+            groups.append(gg)
+        return {'state': state, 'param_groups': groups}
+
+    def load_state_dict(self, state_dict, optimizer_overrides=None):
+        groups = state_dict['param_groups']
+        saved = groups[0]
+        for k, v in saved.items():
+            if k != 'params':
+                self.param_groups[0][k] = v
+        if optimizer_overrides:
+            self.param_groups[0].update(optimizer_overrides)
+        self._apply_group_config()
+        n_saved = len(saved['params'])
+        if n_saved != len(self.flat.params):
+            raise ValueError('loaded state dict has a different number of parameters')
+        for idx, s in state_dict['state'].items():
+            self._load_param_state(saved['params'].index(idx) if idx in saved['params'] else int(idx), s)
+        self._lr = self.param_groups[0]['lr']
+
+    def _apply_group_config(self):
+        pass
+
+    def _param_state(self, i):
+        raise NotImplementedError
+
+    def _load_param_state(self, i, s):
+        raise NotImplementedError
+
+
+class _Adam(_Optimizer):
+    """Fused AdamW-style Adam over flat fp32 buffers."""
+
+    def __init__(self, args, flat):
+        self.args = args
+        super().__init__(args, flat)
+        self.exp_avg = torch.zeros_like(flat.param_flat)
+        self.exp_avg_sq = torch.zeros_like(flat.param_flat)
+        self.steps = [0] * len(flat.params)
+        self.amsgrad = False
+        self.bf16_shadow = None   # optional bf16 copy of params written by the update
+
+    @property
+    def optimizer_config(self):
+        return {
+            'lr': float(self.args.lr[0]),
+            'betas': eval(self.args.adam_betas) if isinstance(self.args.adam_betas, str)
+            else tuple(self.args.adam_betas),
+            'eps': float(self.args.adam_eps),
+            'weight_decay': float(self.args.weight_decay),
+            'amsgrad': False,
+        }
+
+    def step(self, closure=None):
+        g = self.param_groups[0]
+        beta1, beta2 = g['betas']
+        eps, wd, lr = g['eps'], g['weight_decay'], self._lr
+        self._fold_host_scale()
+        runs = self._runs_by_step()
+        for (start, end, t) in runs:
+            bc1 = 1 - beta1 ** t
+            bc2 = 1 - beta2 ** t
+            step_size = lr * math.sqrt(bc2) / bc1
+            if self.use_kernels:
+                ops.fused_adam(self.flat.param_flat, self.flat.grad_flat, self.exp_avg,
+                               self.exp_avg_sq, self._gscale, start, end,
+                               float(beta1), float(beta2), float(eps), float(step_size),
+                               float(wd * lr), self.bf16_shadow)
+            else:
+                p = self.flat.param_flat[start:end]
+                gr = self.flat.grad_flat[start:end].float() * self._gscale
+                m = self.exp_avg[start:end]
+                v = self.exp_avg_sq[start:end]
+                m.mul_(beta1).add_(gr, alpha=1 - beta1)
+                v.mul_(beta2).addcmul_(gr, gr, value=1 - beta2)
+                denom = v.sqrt().add_(eps)
+                if wd != 0:
+                    p.add_(p, alpha=-wd * lr)
+                p.addcdiv_(m, denom, value=-step_size)
+                if self.bf16_shadow is not None:
+                    self.bf16_shadow[start:end].copy_(p)
+
+    def _runs_by_step(self):
+        """Advance per-param step counters for used params and return
+        contiguous (start, end, step) runs sharing one step count."""
+        runs = []
+        cur = None
+        for i, used in enumerate(self.used_mask):
+            s, e = self.flat.param_range(i)
+            if used:
+                self.steps[i] += 1
+                t = self.steps[i]
+                if cur is not None and cur[2] == t:
+                    cur[1] = e
+                else:
+                    if cur is not None:
+                        runs.append(tuple(cur))
+                    cur = [s, e, t]
+            else:
+                if cur is not None:
+                    runs.append(tuple(cur))
+                    cur = None
+        if cur is not None:
+            runs.append(tuple(cur))
+        return runs
+
+    def _param_state(self, i):
+        if self.steps[i] == 0:
+            return None
+        s, e = self.flat.param_range(i)
+        shape = self.flat.params[i].shape
+        return {
+            'step': self.steps[i],
+            'exp_avg': self.exp_avg[s:e].view(shape),
+            'exp_avg_sq': self.exp_avg_sq[s:e].view(shape),
+        }
+
+    def _load_param_state(self, i, st):
+        s, e = self.flat.param_range(i)
+        self.steps[i] = int(st['step'])
+        self.exp_avg[s:e].copy_(st['exp_avg'].reshape(-1).to(self.exp_avg))
+        self.exp_avg_sq[s:e].copy_(st['exp_avg_sq'].reshape(-1).to(self.exp_avg_sq))
+
+
+class _Adadelta(_Optimizer):
+    """Fused Adadelta (MNIST task) over flat fp32 buffers."""
+
+    def __init__(self, args, flat):
+        self.args = args
+        super().__init__(args, flat)
+        self.square_avg = torch.zeros_like(flat.param_flat)
+        self.acc_delta = torch.zeros_like(flat.param_flat)
+        self.steps = [0] * len(flat.params)
+
+    @property
+    def optimizer_config(self):
+        return {
+            'lr': float(self.args.lr[0]),
+            'rho': float(self.args.adadelta_rho),
+            'eps': float(self.args.adadelta_eps),
+            'weight_decay': float(self.args.dadelta_weight_decay),
+        }
+
+    def step(self, closure=None):
+        g = self.param_groups[0]
+        rho, eps, wd, lr = g['rho'], g['eps'], g['weight_decay'], self._lr
+        self._fold_host_scale()
+        for i, used in enumerate(self.used_mask):
+            if used:
+                self.steps[i] += 1
+        for (start, end) in self.flat.runs_for(self.used_mask):
+            if self.use_kernels:
+                ops.fused_adadelta(self.flat.param_flat, self.flat.grad_flat, self.square_avg,
+                                   self.acc_delta, self._gscale, start, end,
+                                   float(lr), float(rho), float(eps), float(wd))
+            else:
+                p = self.flat.param_flat[start:end]
+                gr = self.flat.grad_flat[start:end] * self._gscale
+                sq = self.square_avg[start:end]
+                acc = self.acc_delta[start:end]
+                if wd != 0:
+                    gr = gr.add(p, alpha=wd)
+                sq.mul_(rho).addcmul_(gr, gr, value=1 - rho)
+                std = sq.add(eps).sqrt_()
+                delta = acc.add(eps).sqrt_().div_(std).mul_(gr)
+                p.add_(delta, alpha=-lr)
+                acc.mul_(rho).addcmul_(delta, delta, value=1 - rho)
+
+    def _param_state(self, i):
+        if self.steps[i] == 0:
+            return None
+        s, e = self.flat.param_range(i)
+        shape = self.flat.params[i].shape
+        return {'step': self.steps[i], 'square_avg': self.square_avg[s:e].view(shape),
+                'acc_delta': self.acc_delta[s:e].view(shape)}
+
+    def _load_param_state(self, i, st):
+        s, e = self.flat.param_range(i)
+        self.steps[i] = int(st['step'])
+        self.square_avg[s:e].copy_(st['square_avg'].reshape(-1).to(self.square_avg))
+        self.acc_delta[s:e].copy_(st['acc_delta'].reshape(-1).to(self.acc_delta))
+
+
+def build_optimizer(args, flat):
+    if args.optimizer == 'adam':
+        return _Adam(args, flat)
+    if args.optimizer == 'adadelta':
+        return _Adadelta(args, flat)
+    raise ValueError('unsupported optimizer - {}'.format(args.optimizer))

@@ -1,0 +1,261 @@
+"""Command-line flag system.
+
+Flag names, defaults and the two-phase (task / optimizer / lr-scheduler
+pre-parse, then conditional groups) structure follow the reference
+(hetseq/options.py:5-382, train.py:204-212; full list in SURVEY App. B) so a
+reference launch line works unchanged.  Additions are MI355X-specific knobs
+(``--precision``, ``--fused-kernels``, ``--hip-graphs``, ``--distributed-timeout``)
+that default to the reference behaviour.
+
+Deliberate fixes: ``--num-workers -1`` means "auto" (A7);
+``--log-format json`` exists (A11).
+"""
+import argparse
+
+import torch
+
+TASKS = ['bert', 'mnist', 'BertForELClassification', 'BertForTokenClassification']
+
+
+def _visible_gpus():
+    try:
+        return torch.cuda.device_count()
+    except Exception:  # pragma: no cover
+        return 0
+
+
+def get_task_preparser():
+    p = argparse.ArgumentParser(allow_abbrev=False, add_help=False)
+    p.add_argument('--task', type=str, default='bert', choices=TASKS)
+    p.add_argument('--optimizer', type=str, default='adam', choices=['adam', 'adadelta'])
+    p.add_argument('--lr-scheduler', type=str, default='PolynomialDecayScheduler',
+                   choices=['PolynomialDecayScheduler'])
+    return p
+
+
+def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialDecayScheduler'):
+    parser = argparse.ArgumentParser(allow_abbrev=False)
+    parser.add_argument('--no-progress-bar', action='store_true', help='disable progress bar')
+    parser.add_argument('--seed', default=19940802, type=int, metavar='N',
+                        help='pseudo random number generator seed')
+    parser.add_argument('--cpu', action='store_true', help='use CPU instead of the GPU')
+    parser.add_argument('--log-interval', type=int, default=1, metavar='N',
+                        help='log progress every N updates')
+    parser.add_argument('--log-format', default='simple', choices=['none', 'simple', 'json', 'tqdm'],
+                        help='log format to use')
+    # --- MI355X-native execution knobs (not in the reference) ---
+    parser.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'],
+                        help='compute precision: fp32 (reference parity, exact-f32 MFMA) or '
+                             'bf16 (bf16 MFMA, fp32 master weights and optimizer state)')
+    parser.add_argument('--fused-kernels', default=True, type=eval_bool_arg,
+                        help='use the hand-written HIP kernels on GPU (True) or plain torch ops')
+    parser.add_argument('--hip-graphs', action='store_true',
+                        help='capture the fwd+bwd+update step in a HIP graph after warm-up')
+    parser.add_argument('--profile-phases', action='store_true',
+                        help='record HIP-event timings per phase (data/fwd/bwd/allreduce/opt)')
+
+    add_dataset_args(parser, train=True, task=task)
+    add_distributed_training_args(parser)
+    add_optimization_args(parser, optimizer=optimizer, lr_scheduler=lr_scheduler)
+    add_checkpoint_args(parser)
+    return parser
+
+
+def add_dataset_args(parser, train=False, gen=False, task='bert'):
+    group = parser.add_argument_group('Dataset and data loading')
+    group.add_argument('--num-workers', default=-1, type=int, metavar='N',
+                       help='data loading worker threads (-1 = auto)')
+    group.add_argument('--max-tokens', type=int, metavar='N',
+                       help='maximum number of tokens in a batch')
+    group.add_argument('--max-sentences', '--batch-size', type=int, metavar='N',
+                       help='maximum number of sentences in a batch')
+    group.add_argument('--required-batch-size-multiple', default=1, type=int, metavar='N',
+                       help='batch size will be a multiple of this value')
+    if train:
+        group.add_argument('--train-subset', default='train', metavar='SPLIT',
+                           choices=['train', 'valid', 'test'])
+        group.add_argument('--valid-subset', default='valid', metavar='SPLIT')
+        group.add_argument('--validate-interval', type=int, default=1, metavar='N')
+        group.add_argument('--disable-validation', action='store_true')
+        group.add_argument('--max-tokens-valid', type=int, metavar='N')
+        group.add_argument('--max-sentences-valid', type=int, metavar='N')
+        group.add_argument('--curriculum', default=0, type=int, metavar='N',
+                           help="don't shuffle batches for first N epochs")
+
+        parser.add_argument('--task', type=str, default=task)
+        parser.add_argument('--data', type=str, help='path including data')
+        if task == 'bert':
+            group.add_argument('--dict', type=str, metavar='PATH', help='PATH to dictionary')
+            group.add_argument('--config_file', type=str, metavar='PATH',
+                               help='PATH to bert model configuration', required=True)
+            group.add_argument('--max_pred_length', type=int, default=512,
+                               help='max number of tokens in a sentence')
+            group.add_argument('--num_file', type=int, default=0,
+                               help='number of file to run, 0 for all')
+        elif task == 'mnist':
+            pass
+        elif task in ('BertForTokenClassification', 'BertForELClassification'):
+            group.add_argument('--dict', type=str, metavar='PATH', help='PATH to dictionary')
+            group.add_argument('--config_file', type=str, metavar='PATH',
+                               help='PATH to bert model configuration', required=True)
+            group.add_argument('--max_pred_length', type=int, default=512)
+            group.add_argument('--hetseq_state_dict', type=str, default=None,
+                               help='PATH to a hetseq checkpoint whose ["model"] is loaded')
+            group.add_argument('--transformers_state_dict', type=str, default=None,
+                               help='PATH to a transformers-format BERT state dict')
+            group.add_argument('--train_file', type=str, default=None)
+            group.add_argument('--validation_file', type=str, default=None)
+            group.add_argument('--test_file', type=str, default=None)
+            group.add_argument('--extension_file', type=str, default=None,
+                               help='dataset format/extension (json/csv/conll) used to read NER files')
+            group.add_argument('--load_state_dict_strict', type=eval, default="False",
+                               help='whether strictly load state_dict')
+            if task == 'BertForELClassification':
+                parser.add_argument('--root_data_dir', type=str, default='./deep_ed_data/')
+                parser.add_argument('--entities', type=str, default='RLTD',
+                                    choices=['RLTD', '4EX', 'ALL'])
+                parser.add_argument('--ent_vecs_filename', type=str, default=None,
+                                    help='entity embedding matrix (.pt/.npy/.safetensors)')
+                parser.add_argument('--ent_name_id_file', type=str, default=None,
+                                    help='tab separated "entity_name<TAB>thid" dictionary '
+                                         '(replaces deep_ed_PyTorch.EntNameID)')
+        else:
+            raise ValueError('unsupported task: {}'.format(task))
+
+
+def add_distributed_training_args(parser):
+    group = parser.add_argument_group('Distributed training')
+    group.add_argument('--distributed-world-size', type=int, metavar='N',
+                       default=max(1, _visible_gpus()),
+                       help='total number of GPUs across all nodes (default: all visible GPUs)')
+    group.add_argument('--distributed-rank', default=0, type=int,
+                       help='rank of the first GPU of this node')
+    group.add_argument('--distributed-gpus', default=4, type=int,
+                       help='number of GPUs used on the current node')
+    group.add_argument('--distributed-backend', default='nccl', type=str,
+                       help='distributed backend (nccl == RCCL on ROCm; gloo for CPU)')
+    group.add_argument('--distributed-init-method', default=None, type=str,
+                       help='tcp://host:port or file:///shared/path rendezvous')
+    group.add_argument('--device-id', '--local_rank', default=0, type=int,
+                       help='which GPU to use (usually configured automatically)')
+    group.add_argument('--distributed-no-spawn', action='store_true',
+                       help='do not spawn multiple processes even if multiple GPUs are visible')
+    group.add_argument('--distributed-timeout', default=1800, type=int,
+                       help='collective / rendezvous timeout in seconds')
+    group.add_argument('--ddp-backend', default='c10d', type=str, choices=['c10d'],
+                       help='gradient reducer backend (kept for flag compatibility)')
+    group.add_argument('--bucket-cap-mb', default=25, type=int, metavar='MB',
+                       help='gradient all-reduce bucket size')
+    group.add_argument('--fix-batches-to-gpus', action='store_true')
+    group.add_argument('--find-unused-parameters', default=False, action='store_true')
+    group.add_argument('--fast-stat-sync', default=False, action='store_true')
+    group.add_argument('--check-params-every', default=0, type=int,
+                       help='debug: all-gather a parameter checksum every N updates and assert equality')
+    return group
+
+
+def add_optimization_args(parser, optimizer='adam', lr_scheduler='PolynomialDecayScheduler'):
+    group = parser.add_argument_group('Optimization')
+    group.add_argument('--max-epoch', '--me', default=0, type=int, metavar='N')
+    group.add_argument('--max-update', '--mu', default=0, type=int, metavar='N')
+    group.add_argument('--clip-norm', default=25, type=float, metavar='NORM')
+    group.add_argument('--update-freq', default='1', metavar='N1,N2,...,N_K',
+                       type=lambda uf: eval_str_list(uf, type=int))
+    group.add_argument('--lr', '--learning-rate', default='0.25', type=eval_str_list,
+                       metavar='LR_1,LR_2,...,LR_N')
+    group.add_argument('--min-lr', default=-1, type=float, metavar='LR')
+    group.add_argument('--use-bmuf', default=False, action='store_true')
+    if optimizer == 'adam':
+        group.add_argument('--optimizer', default='adam', type=str)
+        group.add_argument('--adam-betas', default='(0.9, 0.999)', metavar='B')
+        group.add_argument('--adam-eps', type=float, default=1e-8, metavar='D')
+        group.add_argument('--weight-decay', '--wd', default=0.0, type=float, metavar='WD')
+    elif optimizer == 'adadelta':
+        group.add_argument('--optimizer', default='adadelta', type=str)
+        group.add_argument('--adadelta_rho', default='0.9', type=float)
+        group.add_argument('--adadelta_eps', default='1e-6', type=float)
+        group.add_argument('--dadelta_weight_decay', default='0', type=float)
+    else:
+        raise ValueError('unsupported optimizer: {}'.format(optimizer))
+    if lr_scheduler == 'PolynomialDecayScheduler':
+        group.add_argument('--lr_scheduler', default='PolynomialDecayScheduler', type=str)
+        group.add_argument('--force-anneal', '--fa', type=int, metavar='N')
+        group.add_argument('--warmup-updates', default=0, type=int, metavar='N')
+        group.add_argument('--end-learning-rate', default=0.0, type=float)
+        group.add_argument('--power', default=1.0, type=float)
+        group.add_argument('--total-num-update', default=1000000, type=int)
+    else:
+        raise ValueError('unsupported lr_scheduler: {}'.format(lr_scheduler))
+    return group
+
+
+def add_checkpoint_args(parser):
+    group = parser.add_argument_group('Checkpointing')
+    group.add_argument('--save-dir', metavar='DIR', default='checkpoints')
+    group.add_argument('--restore-file', default='checkpoint_last.pt')
+    group.add_argument('--reset-dataloader', action='store_true')
+    group.add_argument('--reset-lr-scheduler', action='store_true')
+    group.add_argument('--reset-meters', action='store_true')
+    group.add_argument('--reset-optimizer', action='store_true')
+    group.add_argument('--optimizer-overrides', default="{}", type=str, metavar='DICT')
+    group.add_argument('--save-interval', type=int, default=1, metavar='N')
+    group.add_argument('--save-interval-updates', type=int, default=0, metavar='N')
+    group.add_argument('--keep-interval-updates', type=int, default=-1, metavar='N')
+    group.add_argument('--keep-last-epochs', type=int, default=-1, metavar='N')
+    group.add_argument('--no-save', action='store_true')
+    group.add_argument('--no-epoch-checkpoints', action='store_true')
+    group.add_argument('--no-last-checkpoints', action='store_true')
+    group.add_argument('--no-save-optimizer-state', action='store_true')
+    group.add_argument('--best-checkpoint-metric', type=str, default='loss')
+    group.add_argument('--maximize-best-checkpoint-metric', action='store_true')
+    group.add_argument('--async-save', action='store_true',
+                       help='write checkpoints from a background thread (state snapshotted first)')
+    return group
+
+
+def eval_str_list(x, type=float):
+    if x is None:
+        return None
+    if isinstance(x, str):
+        x = eval(x)
+    try:
+        return list(map(type, x))
+    except TypeError:
+        return [type(x)]
+
+
+def eval_bool(x, default=False):
+    if x is None:
+        return default
+    try:
+        return bool(eval(x))
+    except TypeError:
+        return default
+
+
+def eval_bool_arg(x):
+    if isinstance(x, bool):
+        return x
+    return str(x).lower() in ('1', 'true', 'yes', 'on')
+
+
+def parse_args_and_arch(parser, s=None):
+    args = parser.parse_args(s)
+    if hasattr(args, 'max_sentences_valid') and args.max_sentences_valid is None:
+        args.max_sentences_valid = args.max_sentences
+    if hasattr(args, 'max_tokens_valid') and args.max_tokens_valid is None:
+        args.max_tokens_valid = args.max_tokens
+    return args
+
+
+def parse_training_args(argv=None):
+    """Two-phase parse: pre-parse task/optimizer/scheduler, then the full parser
+    (reference train.py:204-213)."""
+    pre, rest = get_task_preparser().parse_known_args(argv)
+    parser = get_training_parser(task=pre.task, optimizer=pre.optimizer,
+                                 lr_scheduler=pre.lr_scheduler)
+    # the task/optimizer groups re-declare --task/--optimizer with the pre-parsed
+    # values as defaults, exactly like the reference
+    args = parse_args_and_arch(parser, rest)
+    args.lr_scheduler = pre.lr_scheduler
+    return args

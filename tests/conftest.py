@@ -1,0 +1,29 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs an MI355X (ROCm GPU) and the built _C extension')
+    config.addinivalue_line('markers', 'slow: longer CPU tests')
+
+
+def gpu_available():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.fixture
+def dev():
+    import torch
+    if not gpu_available():
+        pytest.skip('no GPU')
+    return torch.device('cuda', 0)

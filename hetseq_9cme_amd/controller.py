@@ -279,13 +279,17 @@ class Controller(object):
                             'nsentences'.format(self.task.__class__.__name__))
 
         opt = self.optimizer
+        # DDP averages gradients over ranks; the reducer SUMs, so its 1/W is folded here
+        pre = self.reducer.grad_prescale if self.reducer.enabled else 1.0
         try:
             if torch.is_tensor(size_for_norm):
-                scale = torch.where(size_for_norm > 0, W / size_for_norm.clamp(min=1e-30),
-                                    torch.ones_like(size_for_norm)).float()
+                scale = torch.where(size_for_norm > 0, (W * pre) / size_for_norm.clamp(min=1e-30),
+                                    torch.full_like(size_for_norm, pre)).float()
                 opt.multiply_grads(scale)
             elif size_for_norm > 0:
-                opt.multiply_grads(W / float(size_for_norm))
+                opt.multiply_grads(W * pre / float(size_for_norm))
+            elif pre != 1.0:
+                opt.multiply_grads(pre)
             grad_norm = opt.clip_grad_norm(self.args.clip_norm)
             self._prev_grad_norm = grad_norm
             opt.used_mask = step_used

@@ -12,6 +12,7 @@
 //   * colsum      : generic [rows, N] -> [N] column sum (bias grads of plain linears)
 #include "hx_launch.h"
 #include "hx_vec.h"
+#include "hx_reduce.h"
 
 namespace {
 
@@ -42,74 +43,82 @@ __global__ __launch_bounds__(NT) void bias_act_fwd_k(const T* __restrict__ y, co
   }
 }
 
-// grid: (ceil(N/(4*NT)), nchunk). Each thread owns 4 adjacent columns and walks a row chunk.
+// Column-tiled backward with fused column partials.
+// grid: (ceil(N/256) column tiles, ceil(rows/64) row chunks); block = 4 waves.
+// lane -> 4 adjacent columns (16 B), wave w -> rows w, w+4, ... of the chunk;
+// the 4 waves' float4 partials are combined in LDS -> partial[chunk][N].
 template <typename T, int ACT>
 __global__ __launch_bounds__(NT) void bias_act_bwd_k(const T* __restrict__ dout, const T* __restrict__ y,
                                                    const float* __restrict__ b, const T* __restrict__ saved_out,
                                                    T* __restrict__ dy, float* __restrict__ partial, int64_t rows,
                                                    int N) {
-  const int j = (blockIdx.x * NT + threadIdx.x) * 4;
-  if (j >= N) return;
-  const int64_t chunk = (rows + gridDim.y - 1) / gridDim.y;
-  const int64_t r0 = blockIdx.y * chunk;
-  const int64_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
-  float4 bb = hx::f4(0.f);
-  if (b) bb = *reinterpret_cast<const float4*>(b + j);
+  __shared__ float4 red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int j = (blockIdx.x * 64 + lane) * 4;
+  const int64_t r0 = (int64_t)blockIdx.y * hx::kRowChunk;
+  const int64_t r1 = r0 + hx::kRowChunk < rows ? r0 + hx::kRowChunk : rows;
   float4 acc = hx::f4(0.f);
-  for (int64_t r = r0; r < r1; ++r) {
-    const int64_t o = r * N + j;
-    const float4 d = hx::load4(dout + o);
-    float4 g;
-    if (ACT == ACT_GELU) {
-      const float4 x = hx::load4(y + o);
-      g = make_float4(hx::gelu_grad_f(x.x + bb.x), hx::gelu_grad_f(x.y + bb.y), hx::gelu_grad_f(x.z + bb.z),
-                      hx::gelu_grad_f(x.w + bb.w));
-    } else if (ACT == ACT_TANH) {
-      const float4 t = hx::load4(saved_out + o);
-      g = make_float4(1.f - t.x * t.x, 1.f - t.y * t.y, 1.f - t.z * t.z, 1.f - t.w * t.w);
-    } else if (ACT == ACT_RELU) {
-      const float4 t = hx::load4(saved_out + o);
-      g = make_float4(t.x > 0.f, t.y > 0.f, t.z > 0.f, t.w > 0.f);
-    } else {
-      g = hx::f4(1.f);
+  if (j < N) {
+    float4 bb = hx::f4(0.f);
+    if (b) bb = *reinterpret_cast<const float4*>(b + j);
+    for (int64_t r = r0 + w; r < r1; r += 4) {
+      const int64_t o = r * N + j;
+      const float4 d = hx::load4(dout + o);
+      float4 g;
+      if (ACT == ACT_GELU) {
+        const float4 x = hx::load4(y + o);
+        g = make_float4(hx::gelu_grad_f(x.x + bb.x), hx::gelu_grad_f(x.y + bb.y), hx::gelu_grad_f(x.z + bb.z),
+                        hx::gelu_grad_f(x.w + bb.w));
+      } else if (ACT == ACT_TANH) {
+        const float4 t = hx::load4(saved_out + o);
+        g = make_float4(1.f - t.x * t.x, 1.f - t.y * t.y, 1.f - t.z * t.z, 1.f - t.w * t.w);
+      } else if (ACT == ACT_RELU) {
+        const float4 t = hx::load4(saved_out + o);
+        g = make_float4(t.x > 0.f, t.y > 0.f, t.z > 0.f, t.w > 0.f);
+      } else {
+        g = hx::f4(1.f);
+      }
+      const float4 r4 = make_float4(d.x * g.x, d.y * g.y, d.z * g.z, d.w * g.w);
+      if (dy) hx::store4(dy + o, r4);
+      acc.x += r4.x; acc.y += r4.y; acc.z += r4.z; acc.w += r4.w;
     }
-    const float4 r4 = make_float4(d.x * g.x, d.y * g.y, d.z * g.z, d.w * g.w);
-    if (dy) hx::store4(dy + o, r4);
-    acc.x += r4.x; acc.y += r4.y; acc.z += r4.z; acc.w += r4.w;
   }
-  if (partial) *reinterpret_cast<float4*>(partial + (int64_t)blockIdx.y * N + j) = acc;
-}
-
-// partial [nchunk][N] -> out[N] (accumulate adds to out)
-__global__ __launch_bounds__(NT) void fold_k(const float* __restrict__ partial, int nchunk, int N,
-                                           float* __restrict__ out, int accumulate) {
-  for (int j = blockIdx.x * NT + threadIdx.x; j < N; j += gridDim.x * NT) {
-    float a = 0.f;
-    for (int c = 0; c < nchunk; ++c) a += partial[(int64_t)c * N + j];
-    out[j] = accumulate ? out[j] + a : a;
+  if (!partial) return;
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && j < N) {
+    const float4 a = red[0][lane], b1 = red[1][lane], c = red[2][lane], d = red[3][lane];
+    *reinterpret_cast<float4*>(partial + (int64_t)blockIdx.y * N + j) =
+        make_float4((a.x + b1.x) + (c.x + d.x), (a.y + b1.y) + (c.y + d.y), (a.z + b1.z) + (c.z + d.z),
+                    (a.w + b1.w) + (c.w + d.w));
   }
 }
 
-// scalar-column variant for N % 4 != 0 (column sums with an optional per-element scale)
+// scalar-column variant (any N, optional in-place scale by a device scalar)
 template <typename T>
 __global__ __launch_bounds__(NT) void colsum_scalar_k(T* __restrict__ x, const float* __restrict__ scale,
                                                     float* __restrict__ partial, int64_t rows, int N) {
-  const int j = blockIdx.x * NT + threadIdx.x;
-  if (j >= N) return;
-  const int64_t chunk = (rows + gridDim.y - 1) / gridDim.y;
-  const int64_t r0 = blockIdx.y * chunk;
-  const int64_t r1 = r0 + chunk < rows ? r0 + chunk : rows;
-  const float s = scale ? scale[0] : 1.f;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
+  const int64_t r0 = (int64_t)blockIdx.y * hx::kRowChunk;
+  const int64_t r1 = r0 + hx::kRowChunk < rows ? r0 + hx::kRowChunk : rows;
+  const float sc = scale ? scale[0] : 1.f;
   float acc = 0.f;
-  for (int64_t r = r0; r < r1; ++r) {
-    float v = hx::io<T>::ld(x + r * N + j);
-    if (scale) {
-      v *= s;
-      hx::io<T>::st(x + r * N + j, v);
+  if (j < N) {
+    for (int64_t r = r0 + w; r < r1; r += 4) {
+      float v = hx::io<T>::ld(x + r * N + j);
+      if (scale) {
+        v *= sc;
+        hx::io<T>::st(x + r * N + j, v);
+      }
+      acc += v;
     }
-    acc += v;
   }
-  partial[(int64_t)blockIdx.y * N + j] = acc;
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && j < N)
+    partial[(int64_t)blockIdx.y * N + j] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
 }
 
 template <typename T>
@@ -144,15 +153,7 @@ inline int egrid(int64_t n_vec) {
   return (int)b;
 }
 
-inline int nchunk_for(int64_t rows, int ncolblk) {
-  // ~2048 workgroups in total, each chunk >= 16 rows
-  int64_t c = 2048 / (ncolblk > 0 ? ncolblk : 1);
-  if (c < 1) c = 1;
-  int64_t maxc = (rows + 15) / 16;
-  if (c > maxc) c = maxc;
-  if (c < 1) c = 1;
-  return (int)c;
-}
+inline int nchunks(int64_t rows) { return (int)((rows + hx::kRowChunk - 1) / hx::kRowChunk); }
 
 template <typename T>
 void bias_act_fwd_t(int act, const void* y, const float* b, void* out, int64_t rows, int N, hipStream_t s) {
@@ -168,8 +169,8 @@ void bias_act_fwd_t(int act, const void* y, const float* b, void* out, int64_t r
 template <typename T>
 void bias_act_bwd_t(int act, const void* dout, const void* y, const float* b, const void* saved_out, void* dy,
                     float* partial, float* dbias, int64_t rows, int N, int accumulate, hipStream_t s) {
-  const int ncb = (N + 4 * NT - 1) / (4 * NT);
-  const int nch = nchunk_for(rows, ncb);
+  const int ncb = (N + 255) / 256;
+  const int nch = nchunks(rows);
   dim3 g(ncb, nch);
   float* part = dbias ? partial : nullptr;
   switch (act) {
@@ -190,18 +191,12 @@ void bias_act_bwd_t(int act, const void* dout, const void* y, const float* b, co
                                                    part, rows, N);
       break;
   }
-  if (dbias) fold_k<<<(N + NT - 1) / NT, NT, 0, s>>>(partial, nch, N, dbias, accumulate);
+  if (dbias) hx::fold_rows(partial, nch, N, N, N, dbias, nullptr, nullptr, accumulate, s);
 }
 
 }  // namespace
 
-int hx_colsum_ws_floats(int64_t rows, int N) {
-  // workspace upper bound for both colsum layouts
-  const int ncb4 = (N + 4 * NT - 1) / (4 * NT);
-  const int ncb1 = (N + NT - 1) / NT;
-  int a = nchunk_for(rows, ncb4), b = nchunk_for(rows, ncb1);
-  return (a > b ? a : b) * N;
-}
+int hx_colsum_ws_floats(int64_t rows, int N) { return nchunks(rows) * N; }
 
 void hx_bias_act_fwd(int bf16, int act, const void* y, const float* b, void* out, int64_t rows, int N,
                      hipStream_t s) {
@@ -222,12 +217,12 @@ void hx_colsum(int bf16, void* x, const float* scale, float* partial, float* out
     hx_bias_act_bwd(bf16, ACT_NONE, x, nullptr, nullptr, nullptr, nullptr, partial, out, rows, N, accumulate, s);
     return;
   }
-  const int ncb = (N + NT - 1) / NT;
-  const int nch = nchunk_for(rows, ncb);
+  const int ncb = (N + 63) / 64;
+  const int nch = nchunks(rows);
   dim3 g(ncb, nch);
   if (bf16) colsum_scalar_k<uint16_t><<<g, NT, 0, s>>>((uint16_t*)x, scale, partial, rows, N);
   else colsum_scalar_k<float><<<g, NT, 0, s>>>((float*)x, scale, partial, rows, N);
-  fold_k<<<(N + NT - 1) / NT, NT, 0, s>>>(partial, nch, N, out, accumulate);
+  hx::fold_rows(partial, nch, N, N, N, out, nullptr, nullptr, accumulate, s);
 }
 
 void hx_dropout(int bf16, const void* x, void* out, int64_t n, float keep_prob, uint64_t seed, uint64_t stream,

@@ -17,6 +17,7 @@
 // Activations may be fp32 or bf16 (T); statistics and affine params are fp32.
 #include "hx_launch.h"
 #include "hx_vec.h"
+#include "hx_reduce.h"
 
 namespace {
 
@@ -206,20 +207,6 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
   }
 }
 
-// sum partial[nblk][3][H] over blocks -> out0/out1/out2 (any may be null); accumulate=1 adds
-__global__ __launch_bounds__(NT) void colsum3_k(const float* __restrict__ partial, int nblk, int H,
-                                              float* __restrict__ o0, float* __restrict__ o1,
-                                              float* __restrict__ o2, int accumulate) {
-  const int q = blockIdx.y;
-  float* o = q == 0 ? o0 : (q == 1 ? o1 : o2);
-  if (!o) return;
-  for (int j = blockIdx.x * NT + threadIdx.x; j < H; j += gridDim.x * NT) {
-    float a = 0.f;
-    for (int b = 0; b < nblk; ++b) a += partial[((int64_t)b * 3 + q) * H + j];
-    o[j] = accumulate ? o[j] + a : a;
-  }
-}
-
 // ------------------------------------------------------------------------ embedding
 template <typename T, int CH>
 __global__ __launch_bounds__(NT) void embed_ln_fwd_k(const int64_t* __restrict__ ids, const int64_t* __restrict__ tt,
@@ -380,8 +367,9 @@ void ln_bwd_t(const void* dout, const void* z, const float* mean, const float* r
       ln_bwd_k<T, CH, false><<<nblk, NT, 0, s>>>((const T*)dout, (const T*)z, mean, rstd, gamma, (T*)dz, (T*)dy,
                                                  partial, rows, H, keep_prob, seed, stream, want_dbias);
   })
-  dim3 g((H + NT - 1) / NT, 3);
-  colsum3_k<<<g, NT, 0, s>>>(partial, nblk, H, dgamma, dbeta, want_dbias ? dbias : nullptr, accumulate);
+  // partial is [nblk][3][H]: fold rows of length 3H into dgamma | dbeta | dbias
+  hx::fold_rows(partial, nblk, 3 * (int64_t)H, (want_dbias ? 3 : 2) * H, H, dgamma, dbeta,
+                want_dbias ? dbias : nullptr, accumulate, s);
 }
 
 }  // namespace

@@ -69,7 +69,7 @@ def find_mnist_split(path, split):
 
 class MNISTDataset(torch.utils.data.Dataset):
     def __init__(self, images, labels):
-        images = torch.from_numpy(np.ascontiguousarray(images))
+        images = torch.from_numpy(np.array(images, dtype=np.uint8, copy=True))
         self.image = ((images.to(torch.float32) / 255.0 - MEAN) / STD).unsqueeze(1).contiguous()
         self.label = torch.from_numpy(np.ascontiguousarray(labels)).to(torch.int64)
         self._len = len(self.label)

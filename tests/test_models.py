@@ -1,0 +1,159 @@
+"""Model zoo: reference key schema, parameter counts, init quirks, heads."""
+import math
+
+import pytest
+import torch
+
+from hetseq_9cme_amd.models.bert import (BertConfig, BertForMaskedLM, BertForMultipleChoice,
+                                         BertForNextSentencePrediction, BertForPreTraining,
+                                         BertForQuestionAnswering, BertForSequenceClassification,
+                                         BertForTokenClassification, remap_state_dict_keys)
+from hetseq_9cme_amd.models.mnist import MNISTNet
+
+
+def base_cfg(**kw):
+    c = BertConfig(30522)
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+def tiny_cfg(**kw):
+    c = BertConfig(300, hidden_size=64, num_hidden_layers=2, num_attention_heads=4, intermediate_size=128,
+                   max_position_embeddings=64)
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
+@pytest.mark.slow
+def test_bert_base_param_count_and_keys():
+    """110,106,428 params, 206 tensors, 207 state_dict keys (tied decoder)."""
+    m = BertForPreTraining(base_cfg())
+    assert sum(p.numel() for p in m.parameters()) == 110106428
+    assert len(list(m.parameters())) == 206
+    sd = m.state_dict()
+    assert len(sd) == 207
+    expected = ['bert.embeddings.word_embeddings.weight', 'bert.embeddings.position_embeddings.weight',
+                'bert.embeddings.token_type_embeddings.weight', 'bert.embeddings.LayerNorm.weight',
+                'bert.encoder.layer.11.attention.self.query.weight', 'bert.encoder.layer.0.attention.self.value.bias',
+                'bert.encoder.layer.3.attention.output.dense.weight',
+                'bert.encoder.layer.3.attention.output.LayerNorm.bias',
+                'bert.encoder.layer.5.intermediate.dense_act.weight', 'bert.encoder.layer.5.output.dense.bias',
+                'bert.encoder.layer.5.output.LayerNorm.weight', 'bert.pooler.dense_act.weight',
+                'cls.predictions.transform.dense_act.weight', 'cls.predictions.transform.LayerNorm.bias',
+                'cls.predictions.bias', 'cls.predictions.decoder.weight', 'cls.seq_relationship.weight']
+    for k in expected:
+        assert k in sd, k
+    assert m.cls.predictions.decoder.weight is m.bert.embeddings.word_embeddings.weight
+    # NER model of the shipped log: 109,484,547 params with 3 labels
+    ner = BertForTokenClassification(base_cfg(), 3)
+    assert sum(p.numel() for p in ner.parameters()) == 109484547
+
+
+def test_init_quirks():
+    torch.manual_seed(0)
+    m = BertForPreTraining(tiny_cfg(hidden_size=256, intermediate_size=1024))
+    lin = m.bert.encoder.layer[0].attention.self.query
+    assert lin.bias.abs().max().item() == 0.0
+    assert abs(lin.weight.std().item() - 0.02) < 0.003
+    act = m.bert.encoder.layer[0].intermediate.dense_act   # LinearActivation keeps kaiming-uniform
+    bound = 1 / math.sqrt(256)
+    assert act.weight.abs().max().item() <= bound + 1e-6 and act.weight.std().item() > 0.025
+    assert act.bias.abs().max().item() > 0.0
+    ln = m.bert.embeddings.LayerNorm
+    assert torch.all(ln.weight == 1) and torch.all(ln.bias == 0)
+
+
+def _batch(B=3, S=16, V=300):
+    ids = torch.randint(5, V, (B, S))
+    seg = torch.zeros_like(ids)
+    mask = torch.ones_like(ids)
+    mask[0, 10:] = 0
+    return ids, seg, mask
+
+
+def test_pretraining_loss_equals_full_ce():
+    """Masked-row gathering == the reference's CE over all B*S rows (App. A15)."""
+    torch.manual_seed(1)
+    m = BertForPreTraining(tiny_cfg(hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0))
+    ids, seg, mask = _batch()
+    labels = torch.full_like(ids, -1)
+    labels[0, 2] = 7
+    labels[1, 5] = 9
+    labels[2, 1] = 11
+    labels[2, 3] = 12
+    nsp = torch.tensor([0, 1, 0])
+    m.eval()
+    scores, nsp_scores = m(ids, seg, mask)
+    ref = torch.nn.functional.cross_entropy(scores.view(-1, 300), labels.view(-1), ignore_index=-1) + \
+        torch.nn.functional.cross_entropy(nsp_scores, nsp)
+    m.max_predictions_per_seq = 2
+    got = m(ids, seg, mask, labels, nsp)
+    assert torch.allclose(got, ref, atol=1e-5)
+
+
+@pytest.mark.parametrize('cls,extra', [(BertForMaskedLM, {}), (BertForNextSentencePrediction, {}),
+                                       (BertForSequenceClassification, {'num_labels': 3}),
+                                       (BertForTokenClassification, {'num_labels': 5}),
+                                       (BertForQuestionAnswering, {})])
+def test_heads_forward_backward(cls, extra):
+    torch.manual_seed(0)
+    m = cls(tiny_cfg(), *extra.values())
+    ids, seg, mask = _batch()
+    if cls is BertForMaskedLM:
+        lab = torch.full_like(ids, -1)
+        lab[:, 3] = 5
+        loss = m(ids, seg, mask, lab)
+    elif cls is BertForNextSentencePrediction:
+        loss = m(ids, seg, mask, torch.tensor([0, 1, 1]))
+    elif cls is BertForSequenceClassification:
+        loss = m(ids, seg, mask, torch.tensor([0, 2, 1]))
+    elif cls is BertForTokenClassification:
+        lab = torch.randint(0, 5, ids.shape)
+        lab[:, 0] = -100
+        loss = m(ids, seg, mask, lab)
+        # reference semantics: boolean-select active tokens then CE(ignore -100)
+        m.eval()
+        logits = m(ids, seg, mask)
+        act = mask.view(-1) == 1
+        ref = torch.nn.functional.cross_entropy(logits.view(-1, 5)[act], lab.view(-1)[act])
+        assert torch.allclose(m(ids, seg, mask, lab), ref, atol=1e-5)
+        m.train()
+    else:
+        loss = m(ids, seg, mask, torch.tensor([1, 2, 3]), torch.tensor([4, 5, 6]))
+    loss.backward()
+    assert torch.isfinite(loss)
+
+
+def test_multiple_choice():
+    m = BertForMultipleChoice(tiny_cfg(), 2)
+    ids = torch.randint(5, 300, (3, 2, 16))
+    loss = m(ids, torch.zeros_like(ids), torch.ones_like(ids), torch.tensor([0, 1, 1]))
+    loss.backward()
+
+
+def test_transformers_key_remap():
+    m = BertForTokenClassification(tiny_cfg(), 3)
+    sd = m.state_dict()
+    hf = {}
+    for k, v in sd.items():
+        k2 = k.replace('.intermediate.dense_act.', '.intermediate.dense.').replace('pooler.dense_act.',
+                                                                                 'pooler.dense.')
+        k2 = k2.replace('LayerNorm.weight', 'LayerNorm.gamma').replace('LayerNorm.bias', 'LayerNorm.beta')
+        hf[k2] = v.clone() + 1
+    back = remap_state_dict_keys(hf, set(sd.keys()))
+    missing, unexpected = m.load_state_dict(back, strict=False)
+    assert not missing and not unexpected
+    assert torch.allclose(m.bert.encoder.layer[0].intermediate.dense_act.weight, sd[
+        'bert.encoder.layer.0.intermediate.dense_act.weight'])
+
+
+def test_mnist_net():
+    m = MNISTNet()
+    x = torch.randn(4, 1, 28, 28)
+    loss = m(x, torch.tensor([1, 2, 3, 4]))
+    loss.backward()
+    m.eval()
+    out, l2 = m(x, torch.tensor([1, 2, 3, 4]), eval=True)
+    assert out.shape == (4, 10)

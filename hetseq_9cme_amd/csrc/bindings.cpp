@@ -230,6 +230,45 @@ Tensor softmax_xent_(Tensor logits, OptT bias, Tensor labels, int64_t ignore_ind
   return loss;
 }
 
+// ------------------------------------------------------------------ attention
+std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, int64_t seed, int64_t stream) {
+  check_f32(qkv, "qkv");
+  check_f32(mask_bias, "mask_bias");
+  TORCH_CHECK(qkv.dim() == 3, "qkv must be [B, S, 3H]");
+  const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(2) / 3;
+  TORCH_CHECK(H == nh * 64, "fused attention needs head_dim == 64");
+  TORCH_CHECK(S % 128 == 0, "fused attention needs seq_len % 128 == 0");
+  TORCH_CHECK(mask_bias.numel() == B * S, "mask_bias must be [B, S]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
+  auto out = torch::empty({B, S, H}, qkv.options());
+  auto lse = torch::empty({B, nh, S}, qkv.options());
+  Tensor dmask;
+  if (keep < 1.0) dmask = torch::empty({B, nh, S, S / 32}, qkv.options().dtype(torch::kInt32));
+  else dmask = torch::empty({0}, qkv.options().dtype(torch::kInt32));
+  hx_attn_fwd(qkv.data_ptr<float>(), mask_bias.data_ptr<float>(), out.data_ptr<float>(), lse.data_ptr<float>(),
+              keep < 1.0 ? reinterpret_cast<uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr, (int)B, (int)S, (int)nh,
+              (float)keep, (uint64_t)seed, (uint64_t)stream, cur_stream(qkv));
+  return {out, lse, dmask};
+}
+
+Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
+                double keep) {
+  check_f32(dout, "grad_output");
+  check_f32(qkv, "qkv");
+  const int64_t B = qkv.size(0), S = qkv.size(1);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
+  static bool attr_set = false;
+  if (!attr_set) {
+    attr_set = true;  // raise the dynamic-LDS cap once (gfx950: 160 KiB per CU)
+  }
+  auto dqkv = torch::zeros_like(qkv);
+  auto Dws = torch::empty({B, nh, S}, qkv.options());
+  hx_attn_bwd(qkv.data_ptr<float>(), mask_bias.data_ptr<float>(), dout.data_ptr<float>(), out.data_ptr<float>(),
+              lse.data_ptr<float>(), keep < 1.0 ? reinterpret_cast<const uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr,
+              Dws.data_ptr<float>(), dqkv.data_ptr<float>(), (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv));
+  return dqkv;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -246,4 +285,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum", &colsum);
   m.def("dropout", &dropout);
   m.def("softmax_xent_", &softmax_xent_);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
 }

@@ -43,3 +43,10 @@ void hx_dropout(int bf16, const void* x, void* out, int64_t n, float keep_prob, 
 // xent.hip
 void hx_softmax_xent(int bf16, void* logits, const float* bias, const int64_t* labels, float* loss, int64_t rows,
                      int V, int64_t ld, int64_t ignore_index, hipStream_t s);
+
+// attention.hip
+size_t hx_attn_bwd_smem_bytes();
+void hx_attn_fwd(const float* qkv, const float* maskb, float* out, float* lse, uint32_t* dmask, int B, int S, int nh,
+                 float keep, uint64_t seed, uint64_t stream, hipStream_t s);
+void hx_attn_bwd(const float* qkv, const float* maskb, const float* dout, const float* out, const float* lse,
+                 const uint32_t* dmask, float* Dws, float* dqkv, int B, int S, int nh, float keep, hipStream_t s);

@@ -4,9 +4,10 @@ Reference math (hetseq/bert_modeling.py:351-377): scores = Q K^T / sqrt(d) +
 mask_bias; probs = dropout(softmax(scores)); ctx = probs V; heads merged back
 to [B, S, H].  The additive mask is the reference's (1 - m) * -10000 (not -inf).
 
-GPU path: the fused flash-style HIP kernel (``_C.attn_fwd`` / ``attn_bwd``) when
-available for the shape; otherwise the composite below (batched GEMMs through
-hipBLASLt + softmax), which is also the CPU path and the test oracle.
+GPU path: the fused flash-style HIP kernel (``_C.attn_fwd`` / ``attn_bwd``,
+csrc/kernels/attention.hip) for fp32, head_dim 64, seq_len % 128 == 0 (BERT
+phase 1/2); other shapes use the composite below (batched GEMMs + softmax), which
+is also the CPU path and the test oracle.
 """
 import math
 
@@ -43,7 +44,7 @@ def _fused_ok(qkv, num_heads):
         return False
     B, S, H3 = qkv.shape
     d = (H3 // 3) // num_heads
-    return d == 64 and S % 64 == 0 and S <= 512
+    return qkv.dtype == torch.float32 and d == 64 and S % 128 == 0
 
 
 class _AttnFn(torch.autograd.Function):
@@ -51,16 +52,16 @@ class _AttnFn(torch.autograd.Function):
     def forward(ctx, qkv, mask_bias, num_heads, p):
         keep = 1.0 - p
         seed, stream = get_rng().next() if p > 0 else (0, 0)
-        out, lse = C().attn_fwd(qkv, mask_bias, num_heads, keep, seed, stream)
-        ctx.save_for_backward(qkv, mask_bias, out, lse)
-        ctx.meta = (num_heads, keep, seed, stream)
+        out, lse, dmask = C().attn_fwd(qkv, mask_bias, num_heads, keep, seed, stream)
+        ctx.save_for_backward(qkv, mask_bias, out, lse, dmask)
+        ctx.meta = (num_heads, keep)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, mask_bias, out, lse = ctx.saved_tensors
-        num_heads, keep, seed, stream = ctx.meta
-        dqkv = C().attn_bwd(dout.contiguous(), qkv, mask_bias, out, lse, num_heads, keep, seed, stream)
+        qkv, mask_bias, out, lse, dmask = ctx.saved_tensors
+        num_heads, keep = ctx.meta
+        dqkv = C().attn_bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep)
         return dqkv, None, None, None
 
 

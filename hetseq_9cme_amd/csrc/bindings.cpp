@@ -101,7 +101,8 @@ std::vector<Tensor> ln_fwd(Tensor y, OptT bias, OptT res, Tensor gamma, Tensor b
 }
 
 std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tensor gamma, double keep_prob,
-                           int64_t seed, int64_t stream, bool drop_after, bool want_dy, bool want_dbias) {
+                           int64_t seed, int64_t stream, bool drop_after, bool want_dy, bool want_dbias,
+                           OptT dgamma_out, OptT dbeta_out, OptT dbias_out) {
   check_cuda(dout, "grad_output");
   check_cuda(z, "saved input");
   const int H = (int)z.size(-1);
@@ -110,8 +111,11 @@ std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tens
   auto dz = torch::empty_like(z);
   Tensor dy = want_dy ? torch::empty_like(z) : Tensor();
   auto f32 = z.options().dtype(torch::kFloat32);
-  auto dgamma = torch::empty({H}, f32), dbeta = torch::empty({H}, f32);
-  Tensor dbias = want_dbias ? torch::empty({H}, f32) : Tensor();
+  auto dgamma = has(dgamma_out) ? *dgamma_out : torch::empty({H}, f32);
+  auto dbeta = has(dbeta_out) ? *dbeta_out : torch::empty({H}, f32);
+  Tensor dbias = want_dbias ? (has(dbias_out) ? *dbias_out : torch::empty({H}, f32)) : Tensor();
+  TORCH_CHECK(dgamma.numel() == H && dbeta.numel() == H && dgamma.is_contiguous() && dbeta.is_contiguous(),
+              "bad dgamma/dbeta outputs");
   const int nblk = hx_ln_bwd_blocks(rows);
   auto partial = torch::empty({(int64_t)nblk * 3 * H}, f32);
   hx_ln_bwd(act_bf16(z), dout.data_ptr(), z.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
@@ -146,17 +150,20 @@ std::vector<Tensor> embed_ln_fwd(Tensor ids, OptT tt, Tensor wte, Tensor wpe, Te
   return {out, z, mean, rstd};
 }
 
-std::vector<Tensor> embed_grads(Tensor dz, Tensor ids, OptT tt, int64_t V, int64_t P, int64_t ntypes) {
+// Scatter-ACCUMULATES the embedding gradients into dwte / dwpe / dwtt (caller zeroes them
+// when they are fresh).
+void embed_grads(Tensor dz, Tensor ids, OptT tt, Tensor dwte, Tensor dwpe, Tensor dwtt) {
   check_cuda(dz, "dz");
+  check_f32(dwte, "dwte");
+  check_f32(dwpe, "dwpe");
+  check_f32(dwtt, "dwtt");
   const int64_t B = ids.size(0), S = ids.size(1);
   const int H = (int)dz.size(-1);
+  const int64_t ntypes = dwtt.size(0);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(dz.device());
-  auto f32 = dz.options().dtype(torch::kFloat32);
-  auto dwte = torch::zeros({V, H}, f32), dwpe = torch::zeros({P, H}, f32), dwtt = torch::zeros({ntypes, H}, f32);
   hx_embed_grads(act_bf16(dz), dz.data_ptr(), ids.data_ptr<int64_t>(), has(tt) ? tt->data_ptr<int64_t>() : nullptr,
                  dwte.data_ptr<float>(), dwpe.data_ptr<float>(), dwtt.data_ptr<float>(), (int)B, (int)S, H,
                  (int)ntypes, cur_stream(dz));
-  return {dwte, dwpe, dwtt};
 }
 
 // ------------------------------------------------------------------ elementwise
@@ -172,7 +179,8 @@ Tensor bias_act_fwd(Tensor y, OptT b, int64_t act) {
   return out;
 }
 
-std::vector<Tensor> bias_act_bwd(Tensor dout, OptT y, OptT b, OptT saved_out, int64_t act, bool want_dbias) {
+std::vector<Tensor> bias_act_bwd(Tensor dout, OptT y, OptT b, OptT saved_out, int64_t act, bool want_dbias,
+                                 OptT dbias_out) {
   check_cuda(dout, "grad_output");
   const int N = (int)dout.size(-1);
   const int64_t rows = dout.numel() / N;
@@ -182,7 +190,7 @@ std::vector<Tensor> bias_act_bwd(Tensor dout, OptT y, OptT b, OptT saved_out, in
   auto f32 = dout.options().dtype(torch::kFloat32);
   Tensor dbias, ws;
   if (want_dbias) {
-    dbias = torch::empty({N}, f32);
+    dbias = has(dbias_out) ? *dbias_out : torch::empty({N}, f32);
     ws = torch::empty({(int64_t)hx_colsum_ws_floats(rows, N)}, f32);
   }
   hx_bias_act_bwd(act_bf16(dout), (int)act, dout.data_ptr(), has(y) ? y->data_ptr() : nullptr, ptr_or_null<float>(b),
@@ -192,13 +200,14 @@ std::vector<Tensor> bias_act_bwd(Tensor dout, OptT y, OptT b, OptT saved_out, in
   return {dy, dbias};
 }
 
-Tensor colsum(Tensor x, OptT scale) {
+Tensor colsum(Tensor x, OptT scale, OptT out_) {
   check_cuda(x, "input");
   const int N = (int)x.size(-1);
   const int64_t rows = x.numel() / N;
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   auto f32 = x.options().dtype(torch::kFloat32);
-  auto out = torch::empty({N}, f32);
+  auto out = has(out_) ? *out_ : torch::empty({N}, f32);
+  TORCH_CHECK(out.numel() == N && out.is_contiguous(), "bad colsum output");
   auto ws = torch::empty({(int64_t)hx_colsum_ws_floats(rows, N)}, f32);
   hx_colsum(act_bf16(x), x.data_ptr(), ptr_or_null<float>(scale), ws.data_ptr<float>(), out.data_ptr<float>(), rows,
             N, 0, cur_stream(x));
@@ -257,11 +266,8 @@ Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor ls
   check_f32(qkv, "qkv");
   const int64_t B = qkv.size(0), S = qkv.size(1);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
-  static bool attr_set = false;
-  if (!attr_set) {
-    attr_set = true;  // raise the dynamic-LDS cap once (gfx950: 160 KiB per CU)
-  }
-  auto dqkv = torch::zeros_like(qkv);
+  // with one key block per head (S == 128) every dQKV element is overwritten: no memset
+  auto dqkv = S == 128 ? torch::empty_like(qkv) : torch::zeros_like(qkv);
   auto Dws = torch::empty({B, nh, S}, qkv.options());
   hx_attn_bwd(qkv.data_ptr<float>(), mask_bias.data_ptr<float>(), dout.data_ptr<float>(), out.data_ptr<float>(),
               lse.data_ptr<float>(), keep < 1.0 ? reinterpret_cast<const uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr,

@@ -210,6 +210,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dot_k(const float* __restrict__ 
 }
 
 // grid (S/128, nh, B), block 256 = 4 waves; wave w owns keys k0 = blk*128 + w*32 .. +31 (on lanes).
+// LDS per q-tile: Q (pre-scaled) and dO tiles, lse, D and the tile's dropout-mask
+// words are staged once, so the inner loop issues no global loads.
 template <bool kDrop>
 __global__ __launch_bounds__(256) void attn_bwd_k(const float* __restrict__ qkv, const float* __restrict__ maskb,
                                                 const float* __restrict__ dout, const float* __restrict__ lse,
@@ -220,20 +222,21 @@ __global__ __launch_bounds__(256) void attn_bwd_k(const float* __restrict__ qkv,
   float* Vs = Ks + 128 * LDK;            // [128][LDK]
   float* Qs = Vs + 128 * LDK;            // [32][LDK]  (pre-scaled Q tile)
   float* dOs = Qs + 32 * LDK;            // [32][LDK]
-  float* dSs = dOs + 32 * LDK;           // [4 waves][32][33]
-  float* Ls = dSs + 4 * 32 * 33;         // [32] lse
+  float* dSs = dOs + 32 * LDK;           // [4 waves][32][33]; reused as dQ partials [4][32][65]? no: separate
+  float* dQp = dSs + 4 * 32 * 33;        // [4 waves][32][65]
+  float* Ls = dQp + 4 * 32 * 65;         // [32] lse
   float* Ds = Ls + 32;                   // [32] D
-  float* dQs = Ks;                       // reuse? no: separate below
-  (void)dQs;
-  float* dQr = Ds + 32;                  // [32][65] dQ reduction buffer
+  uint32_t* Wm = reinterpret_cast<uint32_t*>(Ds + 32);   // [32 q][4 words] dropout bits of this key block
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int b = blockIdx.z, hd = blockIdx.y;
   const int H = nh * D, H3 = 3 * H;
   const int kbase = blockIdx.x * 128;
+  const bool single = gridDim.x == 1;          // one workgroup sees every key: dQ is final
   const float* base = qkv + (int64_t)b * S * H3;
   const int64_t bh = (int64_t)b * nh + hd;
   const float scale = 0.125f, inv_keep = 1.f / keep;
+  const int nwords = S >> 5;
 
   // ---- stage this block's 128 keys of K and V
 #pragma unroll
@@ -249,12 +252,12 @@ __global__ __launch_bounds__(256) void attn_bwd_k(const float* __restrict__ qkv,
   const float* Kw = Ks + (w * 32) * LDK;      // this wave's keys
   const float* Vw = Vs + (w * 32) * LDK;
   float* dSw = dSs + w * 32 * 33;
+  float* dQw = dQp + w * 32 * 65;
 
   f32x16 dv0 = {0}, dv1 = {0}, dk0 = {0}, dk1 = {0};
 
   for (int qt = 0; qt < S; qt += 32) {
-    __syncthreads();  // previous iteration done with Qs/dOs/dQr
-    // stage Q (pre-scaled), dO tile, lse, D
+    __syncthreads();  // previous iteration done with the q-tile buffers
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int e = tid + i * 256;          // 32 rows x 16 float4
@@ -267,7 +270,10 @@ __global__ __launch_bounds__(256) void attn_bwd_k(const float* __restrict__ qkv,
     }
     if (tid < 32) Ls[tid] = lse[bh * S + qt + tid];
     else if (tid < 64) Ds[tid - 32] = Dv[bh * S + qt + tid - 32];
-    for (int i = tid; i < 32 * 65; i += 256) dQr[i] = 0.f;
+    else if (kDrop && tid < 64 + 128) {
+      const int i = tid - 64, row = i >> 2, wd = i & 3;
+      Wm[i] = dmask[(bh * S + qt + row) * nwords + (kbase >> 5) + wd];
+    }
     __syncthreads();
 
     // ---- S = Qs . K^T (queries in registers, keys on lanes); dP = dO . V^T
@@ -294,10 +300,7 @@ __global__ __launch_bounds__(256) void attn_bwd_k(const float* __restrict__ qkv,
       const int qr_ = crow(r, h);
       const float p = __expf(sa[r] + mk - Ls[qr_]);
       float keepf = 1.f;
-      if (kDrop) {
-        const uint32_t word = dmask[(bh * S + qt + qr_) * (S >> 5) + (mykey >> 5)];
-        keepf = ((word >> (mykey & 31)) & 1) ? inv_keep : 0.f;
-      }
+      if (kDrop) keepf = ((Wm[qr_ * 4 + w] >> l32) & 1) ? inv_keep : 0.f;
       pd[r] = p * keepf;
       ds[r] = p * (dp[r] * keepf - Ds[qr_]);
     }
@@ -312,10 +315,11 @@ __global__ __launch_bounds__(256) void attn_bwd_k(const float* __restrict__ qkv,
       dk0 = mfma(ds[r], q0, dk0);
       dk1 = mfma(ds[r], q1, dk1);
     }
-    // ---- dQ = dS . K : dS through LDS ([q][key], row stride 33)
+    // ---- dQ = dS . K : dS through LDS ([q][key], row stride 33); own wave only
 #pragma unroll
     for (int r = 0; r < 16; ++r) dSw[crow(r, h) * 33 + l32] = ds[r];
-    __syncthreads();
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's dS writes landed
+    __builtin_amdgcn_wave_barrier();
     f32x16 dq0 = {0}, dq1 = {0};
 #pragma unroll
     for (int s = 0; s < 16; ++s) {
@@ -324,21 +328,22 @@ __global__ __launch_bounds__(256) void attn_bwd_k(const float* __restrict__ qkv,
       dq0 = mfma(a, Kw[key * LDK + l32], dq0);
       dq1 = mfma(a, Kw[key * LDK + 32 + l32], dq1);
     }
-    // sum the 4 waves' partials in LDS, then one atomic per element
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int qr_ = crow(r, h);
-      atomicAdd(&dQr[qr_ * 65 + l32], dq0[r]);
-      atomicAdd(&dQr[qr_ * 65 + 32 + l32], dq1[r]);
+      dQw[crow(r, h) * 65 + l32] = dq0[r];
+      dQw[crow(r, h) * 65 + 32 + l32] = dq1[r];
     }
     __syncthreads();
+    // sum the 4 waves' partials; 256 threads x 8 elements of the 32x64 tile
     for (int i = tid; i < 32 * 64; i += 256) {
-      const int row = i >> 6, c = i & 63;
-      atomicAdd(dqkv + ((int64_t)b * S + qt + row) * H3 + hd * D + c, dQr[row * 65 + c] * scale);
+      const int row = i >> 6, c = i & 63, o = row * 65 + c;
+      const float v = ((dQp[o] + dQp[32 * 65 + o]) + (dQp[2 * 32 * 65 + o] + dQp[3 * 32 * 65 + o])) * scale;
+      float* dst = dqkv + ((int64_t)b * S + qt + row) * H3 + hd * D + c;
+      if (single) *dst = v;
+      else atomicAdd(dst, v);
     }
   }
   // ---- epilogue: dK (accumulated against pre-scaled Q -> already scaled), dV
-  // dv0[r] = dV[key = crow(r,h) of this wave's block][d = l32]
   float* dk = dqkv + (int64_t)b * S * H3 + H + hd * D;
   float* dvp = dqkv + (int64_t)b * S * H3 + 2 * H + hd * D;
 #pragma unroll
@@ -354,7 +359,7 @@ __global__ __launch_bounds__(256) void attn_bwd_k(const float* __restrict__ qkv,
 }  // namespace
 
 size_t hx_attn_bwd_smem_bytes() {
-  return sizeof(float) * (2 * 128 * LDK + 2 * 32 * LDK + 4 * 32 * 33 + 64 + 32 * 65);
+  return sizeof(float) * (2 * 128 * LDK + 2 * 32 * LDK + 4 * 32 * 33 + 4 * 32 * 65 + 64 + 128);
 }
 
 void hx_attn_fwd(const float* qkv, const float* maskb, float* out, float* lse, uint32_t* dmask, int B, int S, int nh,

@@ -126,7 +126,7 @@ class LinearActivation(nn.Module):
             init.uniform_(self.bias, -bound, bound)
 
     def forward(self, x):
-        y = F.linear(x, self.weight.to(x.dtype))
+        y = ops.linear(x, self.weight)
         if self.act in ('gelu', 'tanh', 'relu'):
             return ops.bias_act(y, self.bias, self.act)
         if self.bias is not None:
@@ -197,7 +197,7 @@ class BertSelfOutput(nn.Module):
         self.dropout = nn.Dropout(config.hidden_dropout_prob)
 
     def forward(self, hidden_states, input_tensor):
-        y = F.linear(hidden_states, self.dense.weight.to(hidden_states.dtype))
+        y = ops.linear(hidden_states, self.dense.weight)
         return ops.bias_dropout_residual_ln(y, self.dense.bias, input_tensor, self.LayerNorm.weight,
                                             self.LayerNorm.bias, self.LayerNorm.variance_epsilon,
                                             self.dropout.p, self.training)
@@ -230,7 +230,7 @@ class BertOutput(nn.Module):
         self.dropout = nn.Dropout(config.hidden_dropout_prob)
 
     def forward(self, hidden_states, input_tensor):
-        y = F.linear(hidden_states, self.dense.weight.to(hidden_states.dtype))
+        y = ops.linear(hidden_states, self.dense.weight)
         return ops.bias_dropout_residual_ln(y, self.dense.bias, input_tensor, self.LayerNorm.weight,
                                             self.LayerNorm.bias, self.LayerNorm.variance_epsilon,
                                             self.dropout.p, self.training)

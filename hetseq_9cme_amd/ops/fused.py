@@ -20,6 +20,15 @@ def _is_bf16(t):
     return t.dtype == torch.bfloat16
 
 
+def grad_slot(p):
+    """The flat-buffer gradient slot of parameter ``p`` if this backward may write
+    p's gradient there directly (first contribution of the step), else None."""
+    flat = getattr(p, '_hx_flat', None)
+    if flat is None or not p.is_cuda:
+        return None
+    return flat.claim(p)
+
+
 # ----------------------------------------------------------------- references
 def gelu_ref(x):
     return x * 0.5 * (1.0 + torch.erf(x / 1.41421))
@@ -51,6 +60,7 @@ class _EmbedLNFn(torch.autograd.Function):
         out, z, mean, rstd = C().embed_ln_fwd(ids, tt, wte, wpe, wtt, gamma, beta, eps, keep, seed, stream,
                                               out_bf16)
         ctx.save_for_backward(ids, tt if tt is not None else torch.Tensor(), z, mean, rstd, gamma)
+        ctx.params = (wte, wpe, wtt, beta)
         ctx.has_tt = tt is not None
         ctx.meta = (keep, seed, stream, wte.shape[0], wpe.shape[0], wtt.shape[0])
         return out
@@ -60,9 +70,27 @@ class _EmbedLNFn(torch.autograd.Function):
         ids, tt, z, mean, rstd, gamma = ctx.saved_tensors
         keep, seed, stream, V, P, NT = ctx.meta
         dout = dout.contiguous()
-        dz, _, dgamma, dbeta, _ = C().ln_bwd(dout, z, mean, rstd, gamma, keep, seed, stream, True, False, False)
-        dwte, dwpe, dwtt = C().embed_grads(dz, ids, tt if ctx.has_tt else None, V, P, NT)
-        return None, None, dwte, dwpe, dwtt, dgamma, dbeta, None, None, None
+        wte, wpe, wtt, beta = ctx.params
+        dz, _, dgamma, dbeta, _ = C().ln_bwd(dout, z, mean, rstd, gamma, keep, seed, stream, True, False, False,
+                                             grad_slot(gamma), grad_slot(beta), None)
+        H = z.shape[-1]
+        # word embeddings: scatter straight into the flat slot; when the tied MLM
+        # decoder already claimed (and filled) it this step, add on top and return
+        # None so autograd adopts the decoder's slot view holding both contributions
+        ret_wte = grad_slot(wte)
+        if ret_wte is not None:
+            ret_wte.zero_()
+            dwte = ret_wte
+        elif getattr(wte, '_hx_flat', None) is not None and wte.grad is None and wte._hx_flat.is_claimed(wte):
+            dwte = wte._hx_flat.slots[wte._hx_index]
+        else:
+            dwte = ret_wte = torch.zeros(V, H, device=z.device, dtype=torch.float32)
+        dwpe = grad_slot(wpe)
+        dwpe = (dwpe.zero_() if dwpe is not None else torch.zeros(P, H, device=z.device, dtype=torch.float32))
+        dwtt = grad_slot(wtt)
+        dwtt = (dwtt.zero_() if dwtt is not None else torch.zeros(NT, H, device=z.device, dtype=torch.float32))
+        C().embed_grads(dz, ids, tt if ctx.has_tt else None, dwte, dwpe, dwtt)
+        return None, None, ret_wte, dwpe, dwtt, dgamma, dbeta, None, None, None
 
 
 def embed_ln(ids, tt, wte, wpe, wtt, gamma, beta, eps, p, training, out_dtype=torch.float32):
@@ -88,6 +116,7 @@ class _BiasDropResLNFn(torch.autograd.Function):
         seed, stream = get_rng().next() if p > 0 else (0, 0)
         out, z, mean, rstd = C().ln_fwd(y, bias, res, gamma, beta, eps, keep, seed, stream, False, True)
         ctx.save_for_backward(z, mean, rstd, gamma)
+        ctx.params = (bias, beta)
         ctx.meta = (keep, seed, stream, bias is not None, res is not None, y.numel() != z.numel())
         return out
 
@@ -95,9 +124,11 @@ class _BiasDropResLNFn(torch.autograd.Function):
     def backward(ctx, dout):
         z, mean, rstd, gamma = ctx.saved_tensors
         keep, seed, stream, has_bias, has_res, _ = ctx.meta
+        bias, beta = ctx.params
         need_dy = has_bias or keep < 1.0
         dz, dy, dgamma, dbeta, dbias = C().ln_bwd(dout.contiguous(), z, mean, rstd, gamma, keep, seed, stream,
-                                                  False, need_dy, has_bias)
+                                                  False, need_dy, has_bias, grad_slot(gamma), grad_slot(beta),
+                                                  grad_slot(bias) if has_bias else None)
         dy_ret = dy if need_dy else dz
         return dy_ret, (dbias if has_bias else None), (dz if has_res else None), dgamma, dbeta, None, None
 
@@ -130,16 +161,18 @@ class _BiasActFn(torch.autograd.Function):
         else:
             ctx.save_for_backward(out, torch.Tensor())
         ctx.meta = (aid, bias is not None)
+        ctx.bias = bias
         return out
 
     @staticmethod
     def backward(ctx, dout):
         a, b = ctx.saved_tensors
         aid, has_bias = ctx.meta
+        slot = grad_slot(ctx.bias) if has_bias else None
         if aid == 0:
-            dy, dbias = C().bias_act_bwd(dout.contiguous(), a, b if has_bias else None, None, aid, has_bias)
+            dy, dbias = C().bias_act_bwd(dout.contiguous(), a, b if has_bias else None, None, aid, has_bias, slot)
         else:
-            dy, dbias = C().bias_act_bwd(dout.contiguous(), None, None, a, aid, has_bias)
+            dy, dbias = C().bias_act_bwd(dout.contiguous(), None, None, a, aid, has_bias, slot)
         return dy, (dbias if has_bias else None), None
 
 
@@ -172,6 +205,48 @@ def dropout(x, p, training):
     if use_kernels(x):
         return _DropoutFn.apply(x.contiguous(), float(p))
     return F.dropout(x, p, True)
+
+
+# ----------------------------------------------------------------- linear (direct grad write)
+class _LinearFn(torch.autograd.Function):
+    """y = x W^T (+ b).  Backward writes dW (one GEMM) and db (one column-sum
+    kernel) straight into the parameters' flat gradient slots."""
+
+    @staticmethod
+    def forward(ctx, x, W, b):
+        x2 = x.reshape(-1, x.shape[-1])
+        Wc = W.to(x.dtype)
+        y = torch.mm(x2, Wc.t()) if b is None else torch.addmm(b.to(x.dtype), x2, Wc.t())
+        ctx.save_for_backward(x2, W)
+        ctx.b = b
+        ctx.xshape = x.shape
+        return y.view(*x.shape[:-1], y.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, W = ctx.saved_tensors
+        b = ctx.b
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dx = torch.mm(dy2, W.to(dy2.dtype)).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        slot = grad_slot(W)
+        if slot is not None and dy2.dtype == torch.float32:
+            dW = torch.mm(dy2.t(), x2, out=slot)
+        else:
+            dW = torch.mm(dy2.t(), x2).float()
+        db = None
+        if b is not None:
+            if dy2.shape[-1] % 4 == 0:
+                db = C().colsum(dy2.contiguous(), None, grad_slot(b))
+            else:
+                db = dy2.float().sum(0)
+        return dx, dW, db
+
+
+def linear(x, W, b=None):
+    """F.linear with direct-to-slot weight/bias gradients on the GPU."""
+    if use_kernels(x):
+        return _LinearFn.apply(x, W, b)
+    return F.linear(x, W.to(x.dtype), None if b is None else b.to(x.dtype))
 
 
 # ----------------------------------------------------------------- fused Q/K/V projection
@@ -208,6 +283,7 @@ class _Linear3Fn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         y = torch.addmm(b.to(x.dtype), x2, W.t().to(x.dtype))
         ctx.save_for_backward(x2, W)
+        ctx.params = (wq, wk, wv, bq, bk, bv)
         ctx.xshape = x.shape
         ctx.n = [wq.shape[0], wk.shape[0], wv.shape[0]]
         return y.view(*x.shape[:-1], y.shape[-1])
@@ -215,15 +291,31 @@ class _Linear3Fn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, W = ctx.saved_tensors
+        wq, wk, wv, bq, bk, bv = ctx.params
         dy2 = dy.reshape(-1, dy.shape[-1])
         dx = (dy2 @ W.to(dy2.dtype)).view(ctx.xshape)
-        dW = (dy2.t() @ x2).float()
+        a, b_, _ = ctx.n
+        # weight grads: ONE GEMM straight into the three adjacent flat slots when possible
+        ws = [grad_slot(w) for w in (wq, wk, wv)]
+        fused = _adjacent_view(ws) if all(t is not None for t in ws) else None
+        if fused is not None and dy2.dtype == torch.float32:
+            torch.mm(dy2.t(), x2, out=fused)
+            gW = ws
+        else:
+            dW = (dy2.t() @ x2).float()
+            gW = [dW[:a], dW[a:a + b_], dW[a + b_:]]
+            for k, t in enumerate(ws):
+                if t is not None:
+                    t.copy_(gW[k])
+                    gW[k] = t
+        bs = [grad_slot(t) for t in (bq, bk, bv)]
+        fb = _adjacent_view(bs) if all(t is not None for t in bs) else None
         if use_kernels(dy2) and dy2.shape[-1] % 4 == 0:
-            db = C().colsum(dy2.contiguous(), None)
+            db = C().colsum(dy2.contiguous(), None, fb)
         else:
             db = dy2.float().sum(0)
-        a, b_, _ = ctx.n
-        return (dx, dW[:a], dW[a:a + b_], dW[a + b_:], db[:a], db[a:a + b_], db[a + b_:])
+        gb = bs if fb is not None else [db[:a], db[a:a + b_], db[a + b_:]]
+        return (dx, gW[0], gW[1], gW[2], gb[0], gb[1], gb[2])
 
 
 def linear3(x, wq, wk, wv, bq, bk, bv):
@@ -248,15 +340,21 @@ class _DecoderXentFn(torch.autograd.Function):
         count = (labels != -1).sum().to(torch.float32)
         loss = loss_rows.sum() / count
         ctx.save_for_backward(h, W, logits, count)
+        ctx.params = (W, bias)
         return loss
 
     @staticmethod
     def backward(ctx, g):
         h, W, dl, count = ctx.saved_tensors
+        Wp, bias = ctx.params
         scale = (g.float() / count).reshape(1)
-        dbias = C().colsum(dl, scale)          # scales dl in place, returns column sums
+        dbias = C().colsum(dl, scale, grad_slot(bias) if bias is not None else None)  # scales dl in place
         dh = torch.mm(dl, W.to(dl.dtype))
-        dW = torch.mm(dl.t(), h).float()
+        slot = grad_slot(Wp)
+        if slot is not None and dl.dtype == torch.float32:
+            dW = torch.mm(dl.t(), h, out=slot)
+        else:
+            dW = torch.mm(dl.t(), h).float()
         return dh, dW, dbias, None
 
 

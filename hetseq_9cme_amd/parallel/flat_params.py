@@ -107,6 +107,12 @@ class FlatParamSpace(object):
                 p.data = view
                 p.grad = self.grad_flat[o:o + p.numel()].view_as(p)
         self.index_of = {id(p): i for i, p in enumerate(self.params)}
+        # direct-write gradient slots (see ``claim``)
+        self.slots = [self.grad_flat[o:o + p.numel()].view_as(p) for p, o in zip(self.params, offsets)]
+        self.claimed = set()
+        for i, p in enumerate(self.params):
+            p._hx_flat = self
+            p._hx_index = i
 
         # verify contiguity groups are adjacent (required for fused views)
         for g in groups:
@@ -129,8 +135,45 @@ class FlatParamSpace(object):
                 p.grad = view
 
     def zero_grad(self):
-        self.grad_flat.zero_()
-        self.rebind_grads()
+        """Start a new step: grads become None (autograd will steal the slot views the
+        fused backward kernels write into -- no memset, no AccumulateGrad add)."""
+        for p in self.params:
+            p.grad = None
+        self.claimed.clear()
+
+    def claim(self, p):
+        """Return p's flat gradient slot if the caller may WRITE (overwrite) it as
+        the first gradient contribution of this step, else None.  The backward that
+        claims a slot must fully overwrite it and return it as the gradient; autograd
+        then adopts the tensor as ``p.grad`` without copying."""
+        i = p._hx_index
+        if p.grad is not None or i in self.claimed:
+            return None
+        self.claimed.add(i)
+        # a FRESH view object: autograd adopts a returned grad without copying only
+        # if no other Python reference holds its TensorImpl
+        o = self.offsets[i]
+        return self.grad_flat[o:o + self.sizes[i]].view(p.shape)
+
+    def is_claimed(self, p):
+        return p._hx_index in self.claimed
+
+    def adopt(self, i):
+        """Make param i's .grad the flat slot (copy in a grad produced elsewhere;
+        zero-fill if the param got no gradient this step)."""
+        p = self.params[i]
+        slot = self.slots[i]
+        g = p.grad
+        if g is None:
+            slot.zero_()
+            p.grad = slot
+        elif g.data_ptr() != slot.data_ptr():
+            slot.copy_(g)
+            p.grad = slot
+
+    def adopt_all(self):
+        for i in range(len(self.params)):
+            self.adopt(i)
 
     def param_range(self, i):
         return self.offsets[i], self.offsets[i] + self.sizes[i]

@@ -99,6 +99,7 @@ class GradReducer(object):
         if self.used[i]:
             return  # param accumulated twice in one backward (reentrant use)
         self.used[i] = True
+        self.flat.adopt(i)   # grad -> its flat slot (no-op when a kernel wrote it there)
         if not self._callback_queued:
             self._callback_queued = True
             torch.autograd.Variable._execution_engine.queue_callback(self._finalize_backward)
@@ -116,6 +117,9 @@ class GradReducer(object):
             self._launched += 1
 
     def _finalize_backward(self):
+        for i, u in enumerate(self.used):
+            if not u:
+                self.flat.adopt(i)   # unused this micro-batch: keep/zero its slot
         if self.enabled and self._sync:
             self._launch_ready(force=True)   # unused params: their slices hold zeros
             for w in self._works:

@@ -36,7 +36,8 @@ def main(args, init_distributed=False):
     assert args.max_tokens is not None or args.max_sentences is not None, \
         'Must specify batch size either with --max-tokens or --max-sentences'
     if torch.cuda.is_available() and not args.cpu:
-        torch.cuda.set_device(args.device_id)
+        # more ranks than local GPUs is allowed for rehearsals with the gloo backend
+        torch.cuda.set_device(args.device_id % torch.cuda.device_count())
     np.random.seed(args.seed)
     torch.manual_seed(args.seed)
     if init_distributed:
@@ -185,7 +186,7 @@ def cli_main(argv=None):
     if _from_torchrun(args):
         main(args, init_distributed=True)
     elif args.distributed_init_method is not None:
-        if not args.cpu:
+        if not args.cpu and args.distributed_backend == 'nccl':
             assert args.distributed_gpus <= max(1, torch.cuda.device_count())
         if args.distributed_gpus > 1 and not args.distributed_no_spawn:
             start_rank = args.distributed_rank
@@ -194,7 +195,7 @@ def cli_main(argv=None):
         else:
             distributed_main(args.device_id, args)
     elif args.distributed_world_size > 1:
-        if not args.cpu:
+        if not args.cpu and args.distributed_backend == 'nccl':
             assert args.distributed_world_size <= torch.cuda.device_count()
         port = random.randint(10000, 20000)
         args.distributed_init_method = 'tcp://127.0.0.1:{port}'.format(port=port)

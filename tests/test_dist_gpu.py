@@ -1,0 +1,40 @@
+"""Distributed engine with the GPU kernels: 2 ranks share the box's GPU over gloo
+(a rehearsal of the RCCL path -- same reducer, buckets, hooks, stats sync) and must
+match 1 rank with --update-freq 2 on the same batches."""
+import argparse
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from hetseq_9cme_amd.data.synthetic import BERT_TINY, write_bert_config, write_synthetic_bert_shards, write_vocab
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_two_rank_gpu_equivalence(dev, tmp_path):
+    d = tmp_path / 'data'
+    write_synthetic_bert_shards(str(d), n_files=1, samples_per_file=64, seq_len=128, max_pred=20, vocab_size=1024,
+                                split='train')
+    cfg = write_bert_config(str(tmp_path / 'c.json'), **dict(BERT_TINY, hidden_dropout_prob=0.0,
+                                                               attention_probs_dropout_prob=0.0))
+    vocab = write_vocab(str(tmp_path / 'v.txt'), 1024)
+    common = ['--task', 'bert', '--data', str(d), '--dict', vocab, '--config_file', cfg, '--max-sentences', '8',
+              '--fast-stat-sync', '--max-update', '2', '--disable-validation', '--num-workers', '1', '--lr', '1e-3',
+              '--bucket-cap-mb', '1']
+    runs = {'one': ['--update-freq', '2', '--distributed-world-size', '1'],
+            'two': ['--distributed-world-size', '2', '--distributed-backend', 'gloo']}
+    ck = {}
+    for name, extra in runs.items():
+        save = str(tmp_path / name)
+        r = subprocess.run([sys.executable, '-m', 'hetseq_9cme_amd.train'] + common + extra + ['--save-dir', save],
+                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                           env=dict(os.environ, PYTHONPATH=ROOT), timeout=400)
+        assert r.returncode == 0, r.stdout[-3000:]
+        with torch.serialization.safe_globals([argparse.Namespace]):
+            ck[name] = torch.load(os.path.join(save, 'checkpoint_last.pt'), map_location='cpu', weights_only=True)
+    for k, v in ck['one']['model'].items():
+        torch.testing.assert_close(ck['two']['model'][k], v, rtol=1e-4, atol=1e-6, msg=k)

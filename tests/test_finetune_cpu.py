@@ -81,3 +81,40 @@ def test_el_finetune(tmp_path):
     assert 'done training' in r.stdout
     c = load(os.path.join(save, 'checkpoint_last.pt'))
     assert 'entity_classifier.weight' in c['model'] and 'entity_emb.weight' in c['model']
+
+
+def test_ner_scores_match_seqeval_semantics():
+    from hetseq_9cme_amd.eval_ner import get_entities, ner_scores
+    assert get_entities(['B-PER', 'I-PER', 'O', 'B-LOC']) == [('PER', 0, 1), ('LOC', 3, 3)]
+    assert get_entities(['I-PER', 'I-PER', 'B-PER']) == [('PER', 0, 1), ('PER', 2, 2)]
+    r = ner_scores([['B-PER', 'I-PER', 'O', 'B-LOC']], [['B-PER', 'I-PER', 'O', 'B-ORG']])
+    assert r['precision'] == 0.5 and r['recall'] == 0.5 and abs(r['accuracy'] - 0.75) < 1e-9
+
+
+def test_ner_eval_cli_and_transformers_task(tmp_path):
+    vocab, cfg, tr, te = _setup(tmp_path)
+    save = str(tmp_path / 'ner')
+    run_cli(['--task', 'BertForTokenClassification', '--fast-stat-sync', '--max-update', '4',
+             '--valid-subset', 'test', '--num-workers', '1', '--lr', '1e-3', '--dict', vocab, '--config_file', cfg,
+             '--train_file', tr, '--test_file', te, '--extension_file', 'conll', '--max-sentences', '8',
+             '--save-dir', save, '--cpu'])
+    from hetseq_9cme_amd.eval_ner import evaluate
+    res = evaluate(os.path.join(save, 'checkpoint_last.pt'), cfg, vocab, te, train_file=tr, device='cpu')
+    assert 0.0 <= res['f1'] <= 1.0 and res['accuracy'] > 0.0
+    # HF-model variant of the task (reference transformers_tasks.py)
+    import argparse as ap
+    from hetseq_9cme_amd.tasks.transformers_tasks import TransformersBertForTokenClassificationTask
+    args = ap.Namespace(dict=vocab, max_pred_length=64, train_file=tr, validation_file=None, test_file=te,
+                        extension_file='conll', config_file=cfg, transformers_state_dict=None,
+                        load_state_dict_strict=False)
+    task = TransformersBertForTokenClassificationTask.setup_task(args)
+    model = task.build_model(args)
+    task.load_dataset('train')
+    ds = task.dataset('train')
+    batch = ds.collater([ds[i] for i in range(4)])
+
+    class _O(object):
+        def backward(self, loss):
+            loss.backward()
+    loss, ss, lo = task.train_step(batch, model, _O())
+    assert ss == 1 and torch.isfinite(loss)

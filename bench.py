@@ -44,6 +44,8 @@ def parse():
     ap.add_argument('--no-fused', action='store_true', help='torch-op baseline (A/B only)')
     ap.add_argument('--data-dir', default=None)
     ap.add_argument('--update-freq', type=int, default=1)
+    ap.add_argument('--gemm-tuning', default='table', choices=['off', 'table', 'online'])
+    ap.add_argument('--gemm-tuning-file', default=None)
     return ap.parse_args()
 
 
@@ -84,7 +86,9 @@ def main():
             '--fast-stat-sync', '--lr', '1e-4', '--warmup-updates', '10000', '--weight-decay', '0.01',
             '--total-num-update', '1000000', '--clip-norm', '25', '--num-workers', '4', '--log-format', 'none',
             '--disable-validation', '--no-save', '--precision', a.precision, '--distributed-world-size', str(world),
-            '--update-freq', str(a.update_freq)]
+            '--update-freq', str(a.update_freq), '--gemm-tuning', a.gemm_tuning]
+    if a.gemm_tuning_file:
+        argv += ['--gemm-tuning-file', a.gemm_tuning_file]
     args = options.parse_training_args(argv)
     args.device_id = local_rank
     if world > 1:
@@ -151,7 +155,7 @@ def main():
                        'global_batch': global_batch, 'per_gpu_batch': a.batch * a.update_freq,
                        'seq_len': a.seq, 'max_pred': a.max_pred,
                        'parallelism': 'dp{}'.format(world), 'optimizer': 'adam(fused)',
-                       'fused_kernels': not a.no_fused},
+                       'fused_kernels': not a.no_fused, 'gemm_tuning': a.gemm_tuning},
             'final_logged_loss': round(loss, 5),
         }
         print(json.dumps(rec), flush=True)

@@ -33,6 +33,7 @@ from collections import OrderedDict
 import torch
 
 from . import checkpoint_utils, ops
+from .ops import gemm_tuning
 from .data.prefetch import unwrap
 from .optim import build_lr_scheduler, build_optimizer
 from .parallel import distributed as dist_utils
@@ -50,6 +51,8 @@ class Controller(object):
         self.task = task
         self.cuda = torch.cuda.is_available() and not getattr(args, 'cpu', False)
         self.device = torch.device('cuda', torch.cuda.current_device()) if self.cuda else torch.device('cpu')
+        if self.cuda:
+            gemm_tuning.configure(getattr(args, 'gemm_tuning', 'table'), getattr(args, 'gemm_tuning_file', None))
         model = model.to(self.device)
         if getattr(args, 'precision', 'fp32') == 'bf16' and hasattr(model, 'set_compute_dtype'):
             model.set_compute_dtype(torch.bfloat16)

@@ -49,6 +49,11 @@ def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialD
                              'bf16 (bf16 MFMA, fp32 master weights and optimizer state)')
     parser.add_argument('--fused-kernels', default=True, type=eval_bool_arg,
                         help='use the hand-written HIP kernels on GPU (True) or plain torch ops')
+    parser.add_argument('--gemm-tuning', default='table', choices=['off', 'table', 'online'],
+                        help='library-GEMM solution selection: shipped per-shape table (default), '
+                             'online benchmarking of unseen shapes, or library defaults')
+    parser.add_argument('--gemm-tuning-file', default=None, metavar='PATH',
+                        help='where --gemm-tuning online writes its table (device ordinal appended)')
     parser.add_argument('--hip-graphs', action='store_true',
                         help='capture the fwd+bwd+update step in a HIP graph after warm-up')
     parser.add_argument('--profile-phases', action='store_true',

@@ -46,6 +46,10 @@ def parse():
     ap.add_argument('--update-freq', type=int, default=1)
     ap.add_argument('--gemm-tuning', default='table', choices=['off', 'table', 'online'])
     ap.add_argument('--gemm-tuning-file', default=None)
+    ap.add_argument('--profile-phases', action='store_true',
+                    help='extra untimed steps reporting host time per step phase (stderr)')
+    ap.add_argument('--sync-debug', action='store_true',
+                    help='warn on every host<->device synchronisation during the extra steps')
     return ap.parse_args()
 
 
@@ -87,6 +91,8 @@ def main():
             '--total-num-update', '1000000', '--clip-norm', '25', '--num-workers', '4', '--log-format', 'none',
             '--disable-validation', '--no-save', '--precision', a.precision, '--distributed-world-size', str(world),
             '--update-freq', str(a.update_freq), '--gemm-tuning', a.gemm_tuning]
+    if a.profile_phases:
+        argv += ['--profile-phases']
     if a.gemm_tuning_file:
         argv += ['--gemm-tuning-file', a.gemm_tuning_file]
     args = options.parse_training_args(argv)
@@ -159,6 +165,27 @@ def main():
             'final_logged_loss': round(loss, 5),
         }
         print(json.dumps(rec), flush=True)
+    if a.profile_phases or a.sync_debug:
+        # diagnostics run AFTER the timed region so they cannot perturb it
+        if a.sync_debug:
+            torch.cuda.set_sync_debug_mode('warn')
+        ctrl.phase_report()
+        n, data_t = 5, 0.0
+        t1 = time.perf_counter()
+        for _ in range(n):
+            td = time.perf_counter()
+            samples = next(itr)
+            data_t += time.perf_counter() - td
+            ctrl.train_step(samples)
+        host_t = time.perf_counter() - t1
+        torch.cuda.synchronize()
+        tot = time.perf_counter() - t1
+        torch.cuda.set_sync_debug_mode(0)
+        ph = ctrl.phase_report()
+        ph['data_next'] = data_t
+        print('phases (host ms/step): ' + ', '.join('{}={:.2f}'.format(k, v * 1e3 / n) for k, v in ph.items()) +
+              ' | host loop {:.2f} ms/step, device-complete {:.2f} ms/step'.format(host_t * 1e3 / n, tot * 1e3 / n),
+              file=sys.stderr, flush=True)
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()

@@ -28,6 +28,7 @@ import contextlib
 import math
 import os
 import threading
+import time
 from collections import OrderedDict
 
 import torch
@@ -75,6 +76,8 @@ class Controller(object):
         self._prev_grad_norm = None
         self.fast_stat_sync = args.fast_stat_sync
         self._save_thread = None
+        self._profile_phases = bool(getattr(args, 'profile_phases', False))
+        self.phase_times, self._phase_t0 = {}, 0.0
         self.init_meters(args)
 
     # ------------------------------------------------------------------ meters
@@ -201,10 +204,13 @@ class Controller(object):
 
     def train_step(self, samples, dummy_batch=False, raise_oom=False):
         """Forward, backward and parameter update for one group of micro-batches."""
+        tick = self._phase_tick
+        tick(None)
         self._set_seed()
         model = self.model
         model.train()
         self.zero_grad()
+        tick('prep')
         if not dummy_batch:
             self.meters['train_wall'].start()
 
@@ -216,6 +222,7 @@ class Controller(object):
         sample_size, logging_output = 0, {}
         for i, sample in enumerate(samples):
             sample = self._prepare_sample(sample)
+            tick('sample')
             if sample is None:
                 if self._dummy_batch is None:
                     raise RuntimeError('first batch of the run is empty: no dummy batch available')
@@ -233,6 +240,7 @@ class Controller(object):
                     for k, u in enumerate(self.reducer.used):
                         if u:
                             step_used[k] = True
+                tick('fwd_bwd')
                 if not ignore_grad:
                     logging_outputs.append(logging_output)
                     sample_sizes.append(sample_size)
@@ -281,6 +289,7 @@ class Controller(object):
             raise Exception('Please update the {}.aggregate_logging_outputs() method to return ntokens and '
                             'nsentences'.format(self.task.__class__.__name__))
 
+        tick('stats')
         opt = self.optimizer
         # DDP averages gradients over ranks; the reducer SUMs, so its 1/W is folded here
         pre = self.reducer.grad_prescale if self.reducer.enabled else 1.0
@@ -297,6 +306,7 @@ class Controller(object):
             self._prev_grad_norm = grad_norm
             opt.used_mask = step_used
             opt.step()
+            tick('optimizer')
             self.set_num_updates(self.get_num_updates() + 1)
             self.task.update_step(self._num_updates)
 
@@ -317,9 +327,31 @@ class Controller(object):
             logging_output = None
 
         self.meters['train_wall'].stop()
+        tick('meters')
         if logging_output is not None and 'sample_size' not in logging_output:
             logging_output['sample_size'] = sample_size
         return logging_output
+
+    # ------------------------------------------------------------------ phase timing
+    def _phase_tick(self, name):
+        """``--profile-phases``: host wall time spent in each phase of the step.
+
+        Host time (not device time) is what is measured: with no host syncs in
+        the step the CPU runs ahead of the GPU and every phase is short; a phase
+        that blocks on the device shows up as the GPU time it waited for.
+        """
+        if not self._profile_phases:
+            return
+        now = time.perf_counter()
+        if name is not None:
+            self.phase_times[name] = self.phase_times.get(name, 0.0) + now - self._phase_t0
+        self._phase_t0 = now
+
+    def phase_report(self, reset=True):
+        out = dict(self.phase_times)
+        if reset:
+            self.phase_times = {}
+        return out
 
     # ------------------------------------------------------------------ misc API
     def zero_grad(self):

@@ -147,6 +147,10 @@ def get_training_stats(controller):
         stats['loss_scale'] = controller.get_meter('loss_scale')
     stats['wall'] = round(controller.get_meter('wall').elapsed_time)
     stats['train_wall'] = controller.get_meter('train_wall')
+    if getattr(controller, '_profile_phases', False) and controller.get_num_updates() > 0:
+        # cumulative host ms per update spent in each phase of the step
+        for k, v in controller.phase_times.items():
+            stats['t_' + k] = round(v * 1e3 / controller.get_num_updates(), 2)
     return stats
 
 

@@ -68,7 +68,8 @@ class AverageMeter(object):
 
 
 class TimeMeter(object):
-    """Average occurrence of some event per second."""
+    """Average occurrence of some event per second (counts may be device tensors,
+    summed lazily like ``AverageMeter``)."""
 
     def __init__(self, init=0):
         self.reset(init)
@@ -76,10 +77,21 @@ class TimeMeter(object):
     def reset(self, init=0):
         self.init = init
         self.start = time.time()
-        self.n = 0
+        self._n = 0
 
     def update(self, val=1):
-        self.n += _host(val)
+        if torch.is_tensor(val):
+            val = val.detach()
+        self._n = self._n + val
+
+    @property
+    def n(self):
+        self._n = _host(self._n)
+        return self._n
+
+    @n.setter
+    def n(self, v):
+        self._n = v
 
     @property
     def avg(self):
@@ -88,6 +100,14 @@ class TimeMeter(object):
     @property
     def elapsed_time(self):
         return self.init + (time.time() - self.start)
+
+    def __getstate__(self):
+        return {'init': self.init, 'start': self.start, '_n': _host(self._n)}
+
+    def __setstate__(self, state):
+        if 'n' in state:
+            state['_n'] = state.pop('n')
+        self.__dict__.update(state)
 
 
 class StopwatchMeter(object):

@@ -268,10 +268,9 @@ Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor ls
   c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
   // with one key block per head (S == 128) every dQKV element is overwritten: no memset
   auto dqkv = S == 128 ? torch::empty_like(qkv) : torch::zeros_like(qkv);
-  auto Dws = torch::empty({B, nh, S}, qkv.options());
   hx_attn_bwd(qkv.data_ptr<float>(), mask_bias.data_ptr<float>(), dout.data_ptr<float>(), out.data_ptr<float>(),
               lse.data_ptr<float>(), keep < 1.0 ? reinterpret_cast<const uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr,
-              Dws.data_ptr<float>(), dqkv.data_ptr<float>(), (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv));
+              dqkv.data_ptr<float>(), (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv));
   return dqkv;
 }
 

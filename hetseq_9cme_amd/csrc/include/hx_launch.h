@@ -49,4 +49,4 @@ size_t hx_attn_bwd_smem_bytes();
 void hx_attn_fwd(const float* qkv, const float* maskb, float* out, float* lse, uint32_t* dmask, int B, int S, int nh,
                  float keep, uint64_t seed, uint64_t stream, hipStream_t s);
 void hx_attn_bwd(const float* qkv, const float* maskb, const float* dout, const float* out, const float* lse,
-                 const uint32_t* dmask, float* Dws, float* dqkv, int B, int S, int nh, float keep, hipStream_t s);
+                 const uint32_t* dmask, float* dqkv, int B, int S, int nh, float keep, hipStream_t s);

@@ -187,44 +187,35 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const float* __restrict__ qkv,
 }
 
 // ============================================================================ backward
-// D[bh, q] = sum_d dO[b,q,hd*64+d] * O[b,q,hd*64+d]   (one wave per (b,q), lanes = (hd,d) chunks)
-__global__ __launch_bounds__(256) void attn_bwd_dot_k(const float* __restrict__ dout, const float* __restrict__ out,
-                                                    float* __restrict__ Dv, int BS, int S, int nh) {
-  const int H = nh * D;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= BS) return;
-  const int lane = threadIdx.x & 63;
-  const int b = (int)(row / S), q = (int)(row % S);
-  // each head: 16 lanes x float4
-  for (int hd = lane >> 4; hd < nh; hd += 4) {
-    const int c = hd * D + (lane & 15) * 4;
-    const float4 a = *reinterpret_cast<const float4*>(dout + row * H + c);
-    const float4 o = *reinterpret_cast<const float4*>(out + row * H + c);
-    float s = a.x * o.x + a.y * o.y + a.z * o.z + a.w * o.w;
-    s += __shfl_xor(s, 1, 64);
-    s += __shfl_xor(s, 2, 64);
-    s += __shfl_xor(s, 4, 64);
-    s += __shfl_xor(s, 8, 64);
-    if ((lane & 15) == 0) Dv[((int64_t)b * nh + hd) * S + q] = s;
-  }
+// grid (S/128, nh, B), block 256 = 4 waves; wave w owns keys kbase + w*32 .. +31 (ON THE LANES).
+// Sized for TWO workgroups per CU (LDS <= 80 KiB, <= 256 VGPRs): V lives in registers
+// (each lane: its key's 32 dims of its half), only K (both MFMA layouts need it), the
+// current 32-query tile of Q / dO and the tile's dS go through LDS.  Per 32-query tile:
+//   S = Q.K^T, dP = dO.V^T                       (32x32x2, queries rows / keys lanes)
+//   P = exp(S + mask - lse), dS = P*(dP*drop/keep - D)
+//   dV += Pd^T.dO, dK += dS^T.Q                  (accumulators as the A operand)
+//   dQ = dS.K over all 128 keys                  (16x16x4: each wave owns 2 of the 8
+//                                                 16x16 output tiles -> no cross-wave sum)
+// D = rowsum(dO * O) is computed while staging the tile (no separate pass), and the next
+// tile's Q / dO / O / lse / dropout words are prefetched into registers during compute.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+constexpr int LDSS = 132;   // dS row stride ([32 q][128 keys])
+
+__device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-// grid (S/128, nh, B), block 256 = 4 waves; wave w owns keys k0 = blk*128 + w*32 .. +31 (on lanes).
-// LDS per q-tile: Q (pre-scaled) and dO tiles, lse, D and the tile's dropout-mask
-// words are staged once, so the inner loop issues no global loads.
 template <bool kDrop>
-__global__ __launch_bounds__(256) void attn_bwd_k(const float* __restrict__ qkv, const float* __restrict__ maskb,
-                                                const float* __restrict__ dout, const float* __restrict__ lse,
-                                                const float* __restrict__ Dv, const uint32_t* __restrict__ dmask,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_k(const float* __restrict__ qkv, const float* __restrict__ maskb,
+                                                const float* __restrict__ dout, const float* __restrict__ outp,
+                                                const float* __restrict__ lse, const uint32_t* __restrict__ dmask,
                                                 float* __restrict__ dqkv, int S, int nh, float keep) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Ks = smem;                      // [128][LDK]
-  float* Vs = Ks + 128 * LDK;            // [128][LDK]
-  float* Qs = Vs + 128 * LDK;            // [32][LDK]  (pre-scaled Q tile)
+  float* Qs = Ks + 128 * LDK;            // [32][LDK]  (pre-scaled Q tile)
   float* dOs = Qs + 32 * LDK;            // [32][LDK]
-  float* dSs = dOs + 32 * LDK;           // [4 waves][32][33]; reused as dQ partials [4][32][65]? no: separate
-  float* dQp = dSs + 4 * 32 * 33;        // [4 waves][32][65]
-  float* Ls = dQp + 4 * 32 * 65;         // [32] lse
+  float* dSs = dOs + 32 * LDK;           // [32][LDSS]
+  float* Ls = dSs + 32 * LDSS;           // [32] lse
   float* Ds = Ls + 32;                   // [32] D
   uint32_t* Wm = reinterpret_cast<uint32_t*>(Ds + 32);   // [32 q][4 words] dropout bits of this key block
 
@@ -238,71 +229,102 @@ __global__ __launch_bounds__(256) void attn_bwd_k(const float* __restrict__ qkv,
   const float scale = 0.125f, inv_keep = 1.f / keep;
   const int nwords = S >> 5;
 
-  // ---- stage this block's 128 keys of K and V
+  // ---- K of this block's 128 keys -> LDS; V of this lane's key / dim-half -> registers
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int e = tid + i * 256;
     const int row = e >> 4, c4 = (e & 15) * 4;
-    const float* src = base + (int64_t)(kbase + row) * H3 + hd * D + c4;
-    *reinterpret_cast<float4*>(&Ks[row * LDK + c4]) = *reinterpret_cast<const float4*>(src + H);
-    *reinterpret_cast<float4*>(&Vs[row * LDK + c4]) = *reinterpret_cast<const float4*>(src + 2 * H);
+    *reinterpret_cast<float4*>(&Ks[row * LDK + c4]) =
+        *reinterpret_cast<const float4*>(base + (int64_t)(kbase + row) * H3 + H + hd * D + c4);
   }
   const int mykey = kbase + w * 32 + l32;     // key on this lane
+  float vr[32];
+  {
+    const float4* vp = reinterpret_cast<const float4*>(base + (int64_t)mykey * H3 + 2 * H + hd * D + h * 32);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float4 v = vp[i];
+      vr[4 * i] = v.x; vr[4 * i + 1] = v.y; vr[4 * i + 2] = v.z; vr[4 * i + 3] = v.w;
+    }
+  }
   const float mk = maskb[(int64_t)b * S + mykey];
   const float* Kw = Ks + (w * 32) * LDK;      // this wave's keys
-  const float* Vw = Vs + (w * 32) * LDK;
-  float* dSw = dSs + w * 32 * 33;
-  float* dQw = dQp + w * 32 * 65;
+
+  // staging map of a 32x64 tile: thread -> rows (tid>>4) and 16 + (tid>>4), float4 column c4
+  const int srow = tid >> 4, sc4 = (tid & 15) * 4;
+  auto ld_tile = [&](int qt, float4 (&qn)[2], float4 (&dn)[2], float4 (&on)[2], float& xn, uint32_t& mn) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t r = (int64_t)b * S + qt + srow + 16 * i;
+      qn[i] = *reinterpret_cast<const float4*>(qkv + r * H3 + hd * D + sc4);
+      dn[i] = *reinterpret_cast<const float4*>(dout + r * H + hd * D + sc4);
+      on[i] = *reinterpret_cast<const float4*>(outp + r * H + hd * D + sc4);
+    }
+    if (tid < 32) xn = lse[bh * S + qt + tid];
+    if (kDrop && tid >= 64 && tid < 64 + 128) {
+      const int i = tid - 64, row = i >> 2, wd = i & 3;
+      mn = dmask[(bh * S + qt + row) * nwords + (kbase >> 5) + wd];
+    }
+  };
+  float4 qn[2], dn[2], on[2];
+  float xn = 0.f;
+  uint32_t mn = 0;
+  ld_tile(0, qn, dn, on, xn, mn);
+
+  // dQ tiles of this wave (16x16x4 layout): queries qh*16.., dims 16*dqa.. and 16*(dqa+1)..
+  const int qh = w & 1, dqa = 2 * (w >> 1);
+  const int r16 = lane & 15, k4 = lane >> 4;
 
   f32x16 dv0 = {0}, dv1 = {0}, dk0 = {0}, dk1 = {0};
 
   for (int qt = 0; qt < S; qt += 32) {
-    __syncthreads();  // previous iteration done with the q-tile buffers
+    __syncthreads();  // previous tile's LDS buffers are free
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int e = tid + i * 256;          // 32 rows x 16 float4
-      const int row = e >> 4, c4 = (e & 15) * 4;
-      float4 qv = *reinterpret_cast<const float4*>(base + (int64_t)(qt + row) * H3 + hd * D + c4);
+      float4 qv = qn[i];
       qv.x *= scale; qv.y *= scale; qv.z *= scale; qv.w *= scale;
-      *reinterpret_cast<float4*>(&Qs[row * LDK + c4]) = qv;
-      *reinterpret_cast<float4*>(&dOs[row * LDK + c4]) =
-          *reinterpret_cast<const float4*>(dout + ((int64_t)b * S + qt + row) * H + hd * D + c4);
+      *reinterpret_cast<float4*>(&Qs[(srow + 16 * i) * LDK + sc4]) = qv;
+      *reinterpret_cast<float4*>(&dOs[(srow + 16 * i) * LDK + sc4]) = dn[i];
+      float d = dn[i].x * on[i].x + dn[i].y * on[i].y + dn[i].z * on[i].z + dn[i].w * on[i].w;
+      d += __shfl_xor(d, 1, 64);
+      d += __shfl_xor(d, 2, 64);
+      d += __shfl_xor(d, 4, 64);
+      d += __shfl_xor(d, 8, 64);
+      if ((tid & 15) == 0) Ds[srow + 16 * i] = d;
     }
-    if (tid < 32) Ls[tid] = lse[bh * S + qt + tid];
-    else if (tid < 64) Ds[tid - 32] = Dv[bh * S + qt + tid - 32];
-    else if (kDrop && tid < 64 + 128) {
-      const int i = tid - 64, row = i >> 2, wd = i & 3;
-      Wm[i] = dmask[(bh * S + qt + row) * nwords + (kbase >> 5) + wd];
-    }
+    if (tid < 32) Ls[tid] = xn;
+    if (kDrop && tid >= 64 && tid < 64 + 128) Wm[tid - 64] = mn;
+    if (qt + 32 < S) ld_tile(qt + 32, qn, dn, on, xn, mn);   // in flight during this tile's math
     __syncthreads();
 
-    // ---- S = Qs . K^T (queries in registers, keys on lanes); dP = dO . V^T
+    // ---- S = Qs . K^T (queries rows, keys on lanes); dP = dO . V^T
     f32x16 sa = {0}, dp = {0};
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float4 qa = *reinterpret_cast<const float4*>(&Qs[l32 * LDK + h * 32 + 4 * i]);
       const float4 ka = *reinterpret_cast<const float4*>(&Kw[l32 * LDK + h * 32 + 4 * i]);
       const float4 da = *reinterpret_cast<const float4*>(&dOs[l32 * LDK + h * 32 + 4 * i]);
-      const float4 va = *reinterpret_cast<const float4*>(&Vw[l32 * LDK + h * 32 + 4 * i]);
       sa = mfma(qa.x, ka.x, sa);
-      dp = mfma(da.x, va.x, dp);
+      dp = mfma(da.x, vr[4 * i], dp);
       sa = mfma(qa.y, ka.y, sa);
-      dp = mfma(da.y, va.y, dp);
+      dp = mfma(da.y, vr[4 * i + 1], dp);
       sa = mfma(qa.z, ka.z, sa);
-      dp = mfma(da.z, va.z, dp);
+      dp = mfma(da.z, vr[4 * i + 2], dp);
       sa = mfma(qa.w, ka.w, sa);
-      dp = mfma(da.w, va.w, dp);
+      dp = mfma(da.w, vr[4 * i + 3], dp);
+      if (i & 1) __builtin_amdgcn_sched_barrier(0);
     }
-    // P = exp(S + mask - lse) ; Pd = P*mask/keep ; dS = P * (dP*mask/keep - D)
-    f32x16 pd, ds;
+    // P = exp(S + mask - lse) ; Pd = P*drop/keep ; dS = P * (dP*drop/keep - D)   (in place)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int qr_ = crow(r, h);
       const float p = __expf(sa[r] + mk - Ls[qr_]);
       float keepf = 1.f;
       if (kDrop) keepf = ((Wm[qr_ * 4 + w] >> l32) & 1) ? inv_keep : 0.f;
-      pd[r] = p * keepf;
-      ds[r] = p * (dp[r] * keepf - Ds[qr_]);
+      sa[r] = p * keepf;
+      dp[r] = p * (dp[r] * keepf - Ds[qr_]);
+      dSs[qr_ * LDSS + w * 32 + l32] = dp[r];
+      if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
     // ---- dV += Pd^T . dO ; dK += dS^T . Qs   (accumulators as A operand, step r <-> register r)
 #pragma unroll
@@ -310,37 +332,34 @@ __global__ __launch_bounds__(256) void attn_bwd_k(const float* __restrict__ qkv,
       const int qr_ = crow(r, h);
       const float d0 = dOs[qr_ * LDK + l32], d1 = dOs[qr_ * LDK + 32 + l32];
       const float q0 = Qs[qr_ * LDK + l32], q1 = Qs[qr_ * LDK + 32 + l32];
-      dv0 = mfma(pd[r], d0, dv0);
-      dv1 = mfma(pd[r], d1, dv1);
-      dk0 = mfma(ds[r], q0, dk0);
-      dk1 = mfma(ds[r], q1, dk1);
+      dv0 = mfma(sa[r], d0, dv0);
+      dv1 = mfma(sa[r], d1, dv1);
+      dk0 = mfma(dp[r], q0, dk0);
+      dk1 = mfma(dp[r], q1, dk1);
+      if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
-    // ---- dQ = dS . K : dS through LDS ([q][key], row stride 33); own wave only
-#pragma unroll
-    for (int r = 0; r < 16; ++r) dSw[crow(r, h) * 33 + l32] = ds[r];
-    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's dS writes landed
-    __builtin_amdgcn_wave_barrier();
-    f32x16 dq0 = {0}, dq1 = {0};
-#pragma unroll
-    for (int s = 0; s < 16; ++s) {
-      const int key = 2 * s + h;
-      const float a = dSw[l32 * 33 + key];
-      dq0 = mfma(a, Kw[key * LDK + l32], dq0);
-      dq1 = mfma(a, Kw[key * LDK + 32 + l32], dq1);
+    __syncthreads();  // every wave's dS columns are in LDS
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- dQ = dS . K over the block's 128 keys: two 16x16 tiles per wave
+    f32x4 qa0 = {0}, qa1 = {0};
+#pragma unroll 8
+    for (int s = 0; s < 32; ++s) {
+      const int key = 4 * s + k4;
+      const float a = dSs[(qh * 16 + r16) * LDSS + key];
+      qa0 = mfma16(a, Ks[key * LDK + dqa * 16 + r16], qa0);
+      qa1 = mfma16(a, Ks[key * LDK + dqa * 16 + 16 + r16], qa1);
+      if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
+    float* dq = dqkv + ((int64_t)b * S + qt + qh * 16 + 4 * k4) * H3 + hd * D + dqa * 16 + r16;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      dQw[crow(r, h) * 65 + l32] = dq0[r];
-      dQw[crow(r, h) * 65 + 32 + l32] = dq1[r];
-    }
-    __syncthreads();
-    // sum the 4 waves' partials; 256 threads x 8 elements of the 32x64 tile
-    for (int i = tid; i < 32 * 64; i += 256) {
-      const int row = i >> 6, c = i & 63, o = row * 65 + c;
-      const float v = ((dQp[o] + dQp[32 * 65 + o]) + (dQp[2 * 32 * 65 + o] + dQp[3 * 32 * 65 + o])) * scale;
-      float* dst = dqkv + ((int64_t)b * S + qt + row) * H3 + hd * D + c;
-      if (single) *dst = v;
-      else atomicAdd(dst, v);
+    for (int r = 0; r < 4; ++r) {
+      if (single) {
+        dq[(int64_t)r * H3] = qa0[r] * scale;
+        dq[(int64_t)r * H3 + 16] = qa1[r] * scale;
+      } else {
+        atomicAdd(dq + (int64_t)r * H3, qa0[r] * scale);
+        atomicAdd(dq + (int64_t)r * H3 + 16, qa1[r] * scale);
+      }
     }
   }
   // ---- epilogue: dK (accumulated against pre-scaled Q -> already scaled), dV
@@ -359,7 +378,7 @@ __global__ __launch_bounds__(256) void attn_bwd_k(const float* __restrict__ qkv,
 }  // namespace
 
 size_t hx_attn_bwd_smem_bytes() {
-  return sizeof(float) * (2 * 128 * LDK + 2 * 32 * LDK + 4 * 32 * 33 + 4 * 32 * 65 + 64 + 128);
+  return sizeof(float) * (128 * LDK + 2 * 32 * LDK + 32 * LDSS + 64 + 128);
 }
 
 void hx_attn_fwd(const float* qkv, const float* maskb, float* out, float* lse, uint32_t* dmask, int B, int S, int nh,
@@ -372,9 +391,7 @@ void hx_attn_fwd(const float* qkv, const float* maskb, float* out, float* lse, u
 }
 
 void hx_attn_bwd(const float* qkv, const float* maskb, const float* dout, const float* out, const float* lse,
-                 const uint32_t* dmask, float* Dws, float* dqkv, int B, int S, int nh, float keep, hipStream_t s) {
-  const int BS = B * S;
-  attn_bwd_dot_k<<<(BS + 3) / 4, 256, 0, s>>>(dout, out, Dws, BS, S, nh);
+                 const uint32_t* dmask, float* dqkv, int B, int S, int nh, float keep, hipStream_t s) {
   dim3 grid(S / 128, nh, B);
   const size_t smem = hx_attn_bwd_smem_bytes();
   static bool attr = false;
@@ -386,7 +403,7 @@ void hx_attn_bwd(const float* qkv, const float* maskb, const float* dout, const 
     attr = true;
   }
   if (keep < 1.f)
-    attn_bwd_k<true><<<grid, 256, smem, s>>>(qkv, maskb, dout, lse, Dws, dmask, dqkv, S, nh, keep);
+    attn_bwd_k<true><<<grid, 256, smem, s>>>(qkv, maskb, dout, out, lse, dmask, dqkv, S, nh, keep);
   else
-    attn_bwd_k<false><<<grid, 256, smem, s>>>(qkv, maskb, dout, lse, Dws, dmask, dqkv, S, nh, keep);
+    attn_bwd_k<false><<<grid, 256, smem, s>>>(qkv, maskb, dout, out, lse, dmask, dqkv, S, nh, keep);
 }

@@ -1,0 +1,80 @@
+"""Micro-benchmarks of the hand-written kernels at BERT-base phase-1 shapes.
+
+``python tools/bench_kernels.py [--batch 128] [--seq 128] [--only attn,ln,...]``
+Prints one line per kernel: time per call (HIP events, median of N) and the
+achieved FLOP/s or HBM bytes/s against the MI355X peaks (157 TF/s fp32 MFMA,
+~8 TB/s HBM3E).
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from hetseq_9cme_amd.ops._ext import C  # noqa: E402
+
+
+def timeit(fn, iters=50, warmup=5):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    ts.sort()
+    return ts[len(ts) // 2] * 1e3  # us
+
+
+def report(name, us, flops=None, bytes_=None):
+    extra = []
+    if flops:
+        extra.append('{:.1f} TF/s ({:.0f}% of 157)'.format(flops / us / 1e6, 100 * flops / us / 1e6 / 157.3))
+    if bytes_:
+        extra.append('{:.2f} TB/s'.format(bytes_ / us / 1e6))
+    print('{:<28s} {:9.1f} us   {}'.format(name, us, '  '.join(extra)), flush=True)
+
+
+def bench_attn(B, S, nh=12, keep=0.9):
+    d = 64
+    qkv = torch.randn(B, S, 3 * nh * d, device='cuda')
+    mb = torch.zeros(B, S, device='cuda')
+    out, lse, dm = C().attn_fwd(qkv, mb, nh, keep, 1, 0)
+    dout = torch.randn_like(out)
+    f_fwd = 2 * 2 * B * nh * S * S * d
+    report('attn_fwd', timeit(lambda: C().attn_fwd(qkv, mb, nh, keep, 1, 0)), flops=f_fwd)
+    report('attn_bwd', timeit(lambda: C().attn_bwd(dout, qkv, mb, out, lse, dm, nh, keep)), flops=2.5 * f_fwd)
+
+
+def bench_ln(B, S, H=768):
+    n = B * S
+    x = torch.randn(n, H, device='cuda')
+    res = torch.randn(n, H, device='cuda')
+    g = torch.ones(H, device='cuda')
+    bt = torch.zeros(H, device='cuda')
+    bias = torch.zeros(H, device='cuda')
+    report('ln_fwd(bias+drop+res)', timeit(lambda: C().ln_fwd(x, bias, res, g, bt, 1e-12, 0.9, 1, 0, False, False)),
+           bytes_=3 * n * H * 4)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--batch', type=int, default=128)
+    ap.add_argument('--seq', type=int, default=128)
+    ap.add_argument('--only', default='attn')
+    a = ap.parse_args()
+    torch.manual_seed(0)
+    which = a.only.split(',')
+    if 'attn' in which:
+        bench_attn(a.batch, a.seq)
+    if 'ln' in which:
+        bench_ln(a.batch, a.seq)
+
+
+if __name__ == '__main__':
+    main()

@@ -100,10 +100,8 @@ def save_checkpoint(args, controller, epoch_itr, val_loss):
 
     checkpoints = [os.path.join(args.save_dir, fn) for fn, cond in conds.items() if cond]
     if len(checkpoints) > 0:
-        controller.save_checkpoint(checkpoints[0], extra_state)
-        controller.wait_for_save()
-        for cp in checkpoints[1:]:
-            shutil.copyfile(checkpoints[0], cp)
+        # with --async-save the write (and the copies) continue on a background thread
+        controller.save_checkpoint(checkpoints[0], extra_state, copies=checkpoints[1:])
         write_timer.stop()
         print('| saved checkpoint {} (epoch {} @ {} updates) (writing took {} seconds)'.format(
             checkpoints[0], epoch, updates, write_timer.sum))
@@ -166,13 +164,26 @@ def checkpoint_paths(path, pattern=r'checkpoint(\d+)\.pt'):
     return [os.path.join(path, x[1]) for x in sorted(entries, reverse=True)]
 
 
-def torch_persistent_save(*args, **kwargs):
+def torch_persistent_save(obj, filename, copies=()):
+    """Atomic save: write ``filename.tmp`` then ``os.replace`` it, so a crash or
+    preemption mid-write never leaves a truncated ``checkpoint_last.pt``
+    (reference: plain ``torch.save`` with 3 retries, checkpoint_utils.py).
+    ``copies`` (other checkpoint names for the same state) are produced the
+    same way from the finished file."""
+    tmp = filename + '.tmp'
     for i in range(3):
         try:
-            return torch.save(*args, **kwargs)
+            torch.save(obj, tmp)
+            os.replace(tmp, filename)
+            break
         except Exception:
             if i == 2:
                 logging.error(traceback.format_exc())
+                return
+    for cp in copies:
+        ctmp = cp + '.tmp'
+        shutil.copyfile(filename, ctmp)
+        os.replace(ctmp, cp)
 
 
 def convert_state_dict_type(state_dict, ttype=torch.float32):

@@ -52,6 +52,8 @@ class Controller(object):
         self.task = task
         self.cuda = torch.cuda.is_available() and not getattr(args, 'cpu', False)
         self.device = torch.device('cuda', torch.cuda.current_device()) if self.cuda else torch.device('cpu')
+        if not getattr(args, 'fused_kernels', True):
+            ops.set_fused(False)      # A/B mode: plain torch ops on the GPU
         if self.cuda:
             gemm_tuning.configure(getattr(args, 'gemm_tuning', 'table'), getattr(args, 'gemm_tuning_file', None))
         model = model.to(self.device)
@@ -119,7 +121,7 @@ class Controller(object):
         self._lr_scheduler.step_update(0)
 
     # ------------------------------------------------------------------ checkpoints
-    def save_checkpoint(self, filename, extra_state):
+    def save_checkpoint(self, filename, extra_state, copies=()):
         if dist_utils.is_master(self.args):
             extra_state['train_meters'] = checkpoint_utils.meters_state(self.meters)
             state = checkpoint_utils.build_state(
@@ -128,10 +130,10 @@ class Controller(object):
             if getattr(self.args, 'async_save', False):
                 self.wait_for_save()
                 self._save_thread = threading.Thread(target=checkpoint_utils.torch_persistent_save,
-                                                     args=(state, filename), daemon=True)
+                                                     args=(state, filename, list(copies)), daemon=True)
                 self._save_thread.start()
             else:
-                checkpoint_utils.torch_persistent_save(state, filename)
+                checkpoint_utils.torch_persistent_save(state, filename, copies)
 
     def wait_for_save(self):
         if self._save_thread is not None:

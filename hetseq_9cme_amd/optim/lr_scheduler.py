@@ -70,8 +70,22 @@ class PolynomialDecayScheduler(_LRScheduler):
         return self.optimizer.get_lr()
 
 
+LR_SCHEDULER_REGISTRY = {'PolynomialDecayScheduler': PolynomialDecayScheduler}
+
+
+def register_lr_scheduler(name):
+    """Class decorator adding an ``_LRScheduler`` subclass to ``--lr-scheduler``
+    choices.  Optional ``add_args(group)`` static method declares its flags."""
+    def deco(cls):
+        if name in LR_SCHEDULER_REGISTRY and LR_SCHEDULER_REGISTRY[name] is not cls:
+            raise ValueError('lr scheduler {} already registered'.format(name))
+        LR_SCHEDULER_REGISTRY[name] = cls
+        return cls
+    return deco
+
+
 def build_lr_scheduler(args, optimizer):
     name = getattr(args, 'lr_scheduler', 'PolynomialDecayScheduler')
-    if name == 'PolynomialDecayScheduler':
-        return PolynomialDecayScheduler(args, optimizer)
-    raise ValueError('unsupported lr_scheduler - {}'.format(name))
+    if name not in LR_SCHEDULER_REGISTRY:
+        raise ValueError('unsupported lr_scheduler - {}'.format(name))
+    return LR_SCHEDULER_REGISTRY[name](args, optimizer)

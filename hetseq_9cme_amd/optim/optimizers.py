@@ -81,6 +81,12 @@ class _Optimizer(object):
             self._gscale.mul_(self._gscale_host)
             self._gscale_host = 1.0
 
+    def scaled_grad_flat(self):
+        """The flat gradient with every pending multiply/clip applied (a new
+        tensor) -- what a custom (non-fused) optimizer's ``step`` consumes."""
+        self._fold_host_scale()
+        return self.flat.grad_flat * self._gscale
+
     def clip_grad_norm(self, max_norm):
         """Global L2 norm of the (scaled) grads; clip by folding the coefficient
         into ``gscale``.  Returns the pre-clip norm as a 1-element DEVICE tensor
@@ -297,9 +303,21 @@ class _Adadelta(_Optimizer):
         self.acc_delta[s:e].copy_(st['acc_delta'].reshape(-1).to(self.acc_delta))
 
 
+OPTIMIZER_REGISTRY = {'adam': _Adam, 'adadelta': _Adadelta}
+
+
+def register_optimizer(name):
+    """Class decorator adding an ``_Optimizer`` subclass to ``--optimizer`` choices.
+    Optional ``add_args(group)`` static method declares its flags."""
+    def deco(cls):
+        if name in OPTIMIZER_REGISTRY and OPTIMIZER_REGISTRY[name] is not cls:
+            raise ValueError('optimizer {} already registered'.format(name))
+        OPTIMIZER_REGISTRY[name] = cls
+        return cls
+    return deco
+
+
 def build_optimizer(args, flat):
-    if args.optimizer == 'adam':
-        return _Adam(args, flat)
-    if args.optimizer == 'adadelta':
-        return _Adadelta(args, flat)
-    raise ValueError('unsupported optimizer - {}'.format(args.optimizer))
+    if args.optimizer not in OPTIMIZER_REGISTRY:
+        raise ValueError('unsupported optimizer - {}'.format(args.optimizer))
+    return OPTIMIZER_REGISTRY[args.optimizer](args, flat)

@@ -4,7 +4,8 @@ Flag names, defaults and the two-phase (task / optimizer / lr-scheduler
 pre-parse, then conditional groups) structure follow the reference
 (hetseq/options.py:5-382, train.py:204-212; full list in SURVEY App. B) so a
 reference launch line works unchanged.  Additions are MI355X-specific knobs
-(``--precision``, ``--fused-kernels``, ``--hip-graphs``, ``--distributed-timeout``)
+(``--precision``, ``--fused-kernels``, ``--gemm-tuning``, ``--profile-phases``,
+``--distributed-timeout``, ``--user-module``)
 that default to the reference behaviour.
 
 Deliberate fixes (SURVEY App. A): ``--num-workers -1`` means "auto" (A7);
@@ -14,8 +15,6 @@ import argparse
 
 import torch
 
-TASKS = ['bert', 'mnist', 'BertForELClassification', 'BertForTokenClassification']
-
 
 def _visible_gpus():
     try:
@@ -24,12 +23,18 @@ def _visible_gpus():
         return 0
 
 
+def _registries():
+    from .optim import LR_SCHEDULER_REGISTRY, OPTIMIZER_REGISTRY
+    from .tasks import TASK_REGISTRY
+    return TASK_REGISTRY, OPTIMIZER_REGISTRY, LR_SCHEDULER_REGISTRY
+
+
 def get_task_preparser():
+    tasks, optims, scheds = _registries()
     p = argparse.ArgumentParser(allow_abbrev=False, add_help=False)
-    p.add_argument('--task', type=str, default='bert', choices=TASKS)
-    p.add_argument('--optimizer', type=str, default='adam', choices=['adam', 'adadelta'])
-    p.add_argument('--lr-scheduler', type=str, default='PolynomialDecayScheduler',
-                   choices=['PolynomialDecayScheduler'])
+    p.add_argument('--task', type=str, default='bert', choices=list(tasks))
+    p.add_argument('--optimizer', type=str, default='adam', choices=list(optims))
+    p.add_argument('--lr-scheduler', type=str, default='PolynomialDecayScheduler', choices=list(scheds))
     return p
 
 
@@ -49,15 +54,17 @@ def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialD
                              'bf16 (bf16 MFMA, fp32 master weights and optimizer state)')
     parser.add_argument('--fused-kernels', default=True, type=eval_bool_arg,
                         help='use the hand-written HIP kernels on GPU (True) or plain torch ops')
+    parser.add_argument('--user-module', default=None, metavar='PATH',
+                        help='python file / package imported before parsing (registers custom '
+                             'tasks, optimizers, LR schedulers)')
     parser.add_argument('--gemm-tuning', default='table', choices=['off', 'table', 'online'],
                         help='library-GEMM solution selection: shipped per-shape table (default), '
                              'online benchmarking of unseen shapes, or library defaults')
     parser.add_argument('--gemm-tuning-file', default=None, metavar='PATH',
                         help='where --gemm-tuning online writes its table (device ordinal appended)')
-    parser.add_argument('--hip-graphs', action='store_true',
-                        help='capture the fwd+bwd+update step in a HIP graph after warm-up')
     parser.add_argument('--profile-phases', action='store_true',
-                        help='record HIP-event timings per phase (data/fwd/bwd/allreduce/opt)')
+                        help='log host wall time per step phase (prep/sample/fwd_bwd/stats/optimizer/'
+                             'meters); a phase that waits on the GPU shows up as long')
 
     add_dataset_args(parser, train=True, task=task)
     add_distributed_training_args(parser)
@@ -125,7 +132,11 @@ def add_dataset_args(parser, train=False, gen=False, task='bert'):
                                     help='tab separated "entity_name<TAB>thid" dictionary '
                                          '(replaces deep_ed_PyTorch.EntNameID)')
         else:
-            raise ValueError('unsupported task: {}'.format(task))
+            tasks = _registries()[0]
+            if task not in tasks:
+                raise ValueError('unsupported task: {}'.format(task))
+            if hasattr(tasks[task], 'add_args'):
+                tasks[task].add_args(group)
 
 
 def add_distributed_training_args(parser):
@@ -181,7 +192,12 @@ def add_optimization_args(parser, optimizer='adam', lr_scheduler='PolynomialDeca
         group.add_argument('--adadelta_eps', default='1e-6', type=float)
         group.add_argument('--dadelta_weight_decay', default='0', type=float)
     else:
-        raise ValueError('unsupported optimizer: {}'.format(optimizer))
+        optims = _registries()[1]
+        if optimizer not in optims:
+            raise ValueError('unsupported optimizer: {}'.format(optimizer))
+        group.add_argument('--optimizer', default=optimizer, type=str)
+        if hasattr(optims[optimizer], 'add_args'):
+            optims[optimizer].add_args(group)
     if lr_scheduler == 'PolynomialDecayScheduler':
         group.add_argument('--lr_scheduler', default='PolynomialDecayScheduler', type=str)
         group.add_argument('--force-anneal', '--fa', type=int, metavar='N')
@@ -190,7 +206,12 @@ def add_optimization_args(parser, optimizer='adam', lr_scheduler='PolynomialDeca
         group.add_argument('--power', default=1.0, type=float)
         group.add_argument('--total-num-update', default=1000000, type=int)
     else:
-        raise ValueError('unsupported lr_scheduler: {}'.format(lr_scheduler))
+        scheds = _registries()[2]
+        if lr_scheduler not in scheds:
+            raise ValueError('unsupported lr_scheduler: {}'.format(lr_scheduler))
+        group.add_argument('--lr_scheduler', default=lr_scheduler, type=str)
+        if hasattr(scheds[lr_scheduler], 'add_args'):
+            scheds[lr_scheduler].add_args(group)
     return group
 
 
@@ -253,9 +274,37 @@ def parse_args_and_arch(parser, s=None):
     return args
 
 
+def import_user_module(path):
+    """Import a user file / package that registers tasks, optimizers or LR
+    schedulers (``--user-module``) before the real parse."""
+    import importlib
+    import importlib.util
+    import os
+    import sys
+    if path is None:
+        return None
+    if os.path.exists(path):
+        path = os.path.abspath(path)
+        name = os.path.splitext(os.path.basename(path.rstrip('/')))[0]
+        if os.path.isdir(path):
+            sys.path.insert(0, os.path.dirname(path))
+            return importlib.import_module(name)
+        spec = importlib.util.spec_from_file_location(name, path)
+        mod = importlib.util.module_from_spec(spec)
+        sys.modules[name] = mod
+        spec.loader.exec_module(mod)
+        return mod
+    return importlib.import_module(path)
+
+
 def parse_training_args(argv=None):
     """Two-phase parse: pre-parse task/optimizer/scheduler, then the full parser
-    (reference train.py:204-213)."""
+    (reference train.py:204-213).  ``--user-module`` is imported first so that
+    the registries it extends are visible to the choices."""
+    um = argparse.ArgumentParser(add_help=False)
+    um.add_argument('--user-module', default=None)
+    um_args, _ = um.parse_known_args(argv)
+    import_user_module(um_args.user_module)
     pre, rest = get_task_preparser().parse_known_args(argv)
     parser = get_training_parser(task=pre.task, optimizer=pre.optimizer,
                                  lr_scheduler=pre.lr_scheduler)

@@ -78,7 +78,9 @@ def test_bert_exact_resume(tmp_path, bert_data):
     a = str(tmp_path / 'a')
     b = str(tmp_path / 'b')
     run_cli(bert_argv(data, cfg, vocab, a, ['--max-update', '8']))
-    run_cli(bert_argv(data, cfg, vocab, b, ['--max-update', '4']))
+    # first half with background (async) checkpoint writes: same bits on disk, no temp files left
+    run_cli(bert_argv(data, cfg, vocab, b, ['--max-update', '4', '--async-save']))
+    assert not [f for f in os.listdir(b) if f.endswith('.tmp')]
     ckb = load(os.path.join(b, 'checkpoint_last.pt'))
     assert ckb['extra_state']['train_iterator'] == {'epoch': 1, 'iterations_in_epoch': 4}
     run_cli(bert_argv(data, cfg, vocab, b, ['--max-update', '8']))

@@ -14,6 +14,8 @@ The compute path is different: every hot op goes through ``hetseq_9cme_amd.ops``
   * Q/K/V projections run as ONE N=3H GEMM over adjacent weight storage,
   * attention is the fused flash-style kernel (no [B,nh,S,S] tensors),
   * dense -> bias -> dropout -> +residual -> LayerNorm is one kernel after the GEMM,
+  * the residual branch's gradient is accumulated by the QKV / FFN-up dgrad GEMM
+    (beta = 1, ``ops.ResidualGrad``) instead of a separate add kernel,
   * GEMM -> bias+GELU / bias+tanh is one epilogue kernel,
   * embedding gathers + sum + LN + dropout is one kernel,
   * the MLM head only runs on the masked rows (gathered without host sync) and the
@@ -125,8 +127,8 @@ class LinearActivation(nn.Module):
             bound = 1 / math.sqrt(fan_in)
             init.uniform_(self.bias, -bound, bound)
 
-    def forward(self, x):
-        y = ops.linear(x, self.weight)
+    def forward(self, x, res_grad=None):
+        y = ops.linear(x, self.weight, res_grad=res_grad)
         if self.act in ('gelu', 'tanh', 'relu'):
             return ops.bias_act(y, self.bias, self.act)
         if self.bias is not None:
@@ -183,9 +185,9 @@ class BertSelfAttention(nn.Module):
         self.value = nn.Linear(config.hidden_size, self.all_head_size)
         self.dropout = nn.Dropout(config.attention_probs_dropout_prob)
 
-    def forward(self, hidden_states, attention_mask_bias):
+    def forward(self, hidden_states, attention_mask_bias, res_grad=None):
         qkv = ops.linear3(hidden_states, self.query.weight, self.key.weight, self.value.weight,
-                          self.query.bias, self.key.bias, self.value.bias)
+                          self.query.bias, self.key.bias, self.value.bias, res_grad=res_grad)
         return ops.attention(qkv, attention_mask_bias, self.num_attention_heads, self.dropout.p, self.training)
 
 
@@ -196,11 +198,11 @@ class BertSelfOutput(nn.Module):
         self.LayerNorm = BertLayerNorm(config.hidden_size, eps=1e-12)
         self.dropout = nn.Dropout(config.hidden_dropout_prob)
 
-    def forward(self, hidden_states, input_tensor):
+    def forward(self, hidden_states, input_tensor, res_grad=None):
         y = ops.linear(hidden_states, self.dense.weight)
         return ops.bias_dropout_residual_ln(y, self.dense.bias, input_tensor, self.LayerNorm.weight,
                                             self.LayerNorm.bias, self.LayerNorm.variance_epsilon,
-                                            self.dropout.p, self.training)
+                                            self.dropout.p, self.training, res_grad=res_grad)
 
 
 class BertAttention(nn.Module):
@@ -210,7 +212,9 @@ class BertAttention(nn.Module):
         self.output = BertSelfOutput(config)
 
     def forward(self, input_tensor, attention_mask_bias):
-        return self.output(self.self(input_tensor, attention_mask_bias), input_tensor)
+        # the residual gradient of input_tensor is fused into the QKV dgrad GEMM
+        rg = ops.ResidualGrad()
+        return self.output(self.self(input_tensor, attention_mask_bias, rg), input_tensor, rg)
 
 
 class BertIntermediate(nn.Module):
@@ -218,8 +222,8 @@ class BertIntermediate(nn.Module):
         super().__init__()
         self.dense_act = LinearActivation(config.hidden_size, config.intermediate_size, act=config.hidden_act)
 
-    def forward(self, hidden_states):
-        return self.dense_act(hidden_states)
+    def forward(self, hidden_states, res_grad=None):
+        return self.dense_act(hidden_states, res_grad)
 
 
 class BertOutput(nn.Module):
@@ -229,11 +233,11 @@ class BertOutput(nn.Module):
         self.LayerNorm = BertLayerNorm(config.hidden_size, eps=1e-12)
         self.dropout = nn.Dropout(config.hidden_dropout_prob)
 
-    def forward(self, hidden_states, input_tensor):
+    def forward(self, hidden_states, input_tensor, res_grad=None):
         y = ops.linear(hidden_states, self.dense.weight)
         return ops.bias_dropout_residual_ln(y, self.dense.bias, input_tensor, self.LayerNorm.weight,
                                             self.LayerNorm.bias, self.LayerNorm.variance_epsilon,
-                                            self.dropout.p, self.training)
+                                            self.dropout.p, self.training, res_grad=res_grad)
 
 
 class BertLayer(nn.Module):
@@ -245,7 +249,8 @@ class BertLayer(nn.Module):
 
     def forward(self, hidden_states, attention_mask_bias):
         attention_output = self.attention(hidden_states, attention_mask_bias)
-        return self.output(self.intermediate(attention_output), attention_output)
+        rg = ops.ResidualGrad()     # residual grad of attention_output -> FFN-up dgrad GEMM
+        return self.output(self.intermediate(attention_output, rg), attention_output, rg)
 
 
 def _rng_replaying(fn):

@@ -125,11 +125,11 @@ TAGS = {'john': 'B-PER', 'smith': 'I-PER', 'mary': 'B-PER', 'paris': 'B-LOC', 'l
         'google': 'B-ORG', 'united': 'B-ORG', 'nations': 'I-ORG', 'league': 'B-MISC', 'cup': 'I-MISC'}
 
 
-def write_synthetic_conll(path, n_sents=64, seed=0, with_entities=False):
+def write_synthetic_conll(path, n_sents=64, seed=0, with_entities=False, min_len=4, max_len=14):
     rng = np.random.RandomState(seed)
     lines = ['-DOCSTART- -X- -X- O', '']
     for _ in range(n_sents):
-        L = rng.randint(4, 14)
+        L = rng.randint(min_len, max_len)
         for _ in range(L):
             w = WORDS[rng.randint(len(WORDS))]
             tag = TAGS.get(w, 'O')

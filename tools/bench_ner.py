@@ -1,0 +1,69 @@
+"""NER fine-tuning step time (BASELINE config 5: CoNLL-2003, batch 32 per update,
+reference observed 0.214 s/update on 1 GPU).
+
+Synthetic CoNLL-format sentences (8-40 words, CoNLL-2003-like lengths), a
+BERT-base configuration with random init (no checkpoint download possible),
+the real ``BertForTokenClassification`` task / collator / engine.  Prints one
+JSON line with seconds per update (max over ranks under torchrun).
+``python tools/bench_ner.py [--steps 50] [--warmup 5] [--batch 32]``
+"""
+import argparse
+import json
+import os
+import sys
+import tempfile
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--steps', type=int, default=50)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--batch', type=int, default=32)
+    ap.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'])
+    a = ap.parse_args()
+    from hetseq_9cme_amd import options, tasks
+    from hetseq_9cme_amd.controller import Controller
+    from hetseq_9cme_amd.data import iterators
+    from hetseq_9cme_amd.data.synthetic import (BERT_BASE, WORDS, write_bert_config, write_synthetic_conll,
+                                                write_vocab)
+    d = tempfile.mkdtemp(prefix='hx_ner_')
+    vocab = write_vocab(os.path.join(d, 'vocab.txt'), 30522, extra_words=WORDS)
+    cfg = write_bert_config(os.path.join(d, 'bert_base.json'), **BERT_BASE)
+    n = (a.steps + a.warmup + 2) * a.batch
+    tr = write_synthetic_conll(os.path.join(d, 'train.txt'), n, seed=0, min_len=8, max_len=40)
+    argv = ['--task', 'BertForTokenClassification', '--optimizer', 'adam', '--fast-stat-sync', '--lr', '5e-5',
+            '--dict', vocab, '--config_file', cfg, '--train_file', tr, '--extension_file', 'conll',
+            '--max-sentences', str(a.batch), '--num-workers', '2', '--find-unused-parameters',
+            '--disable-validation', '--no-save', '--log-format', 'none', '--precision', a.precision]
+    args = options.parse_training_args(argv)
+    args.device_id = 0
+    args.distributed_rank = 0
+    torch.manual_seed(args.seed)
+    task = tasks.setup_task(args)
+    model = task.build_model(args)
+    ctrl = Controller(args, task, model)
+    epoch_itr = ctrl.get_train_iterator(epoch=0, load_dataset=True)
+    ctrl.lr_step(epoch_itr.epoch)
+    itr = iterators.GroupedIterator(epoch_itr.next_epoch_itr(shuffle=True), 1)
+    for _ in range(a.warmup):
+        ctrl.train_step(next(itr))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ctrl.train_step(next(itr))
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    print(json.dumps({'metric': 'NER fine-tune (BertForTokenClassification, BERT-base) s/update',
+                      'value': round(dt, 5), 'unit': 's/update', 'higher_is_better': False,
+                      'reference_1gpu': 0.214, 'speedup_vs_reference': round(0.214 / dt, 1),
+                      'batch': a.batch, 'dtype': a.precision,
+                      'data': 'synthetic CoNLL-format sentences (8-40 words), random-init BERT-base'}), flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -246,13 +246,13 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
   TORCH_CHECK(qkv.dim() == 3, "qkv must be [B, S, 3H]");
   const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(2) / 3;
   TORCH_CHECK(H == nh * 64, "fused attention needs head_dim == 64");
-  TORCH_CHECK(S % 128 == 0, "fused attention needs seq_len % 128 == 0");
   TORCH_CHECK(mask_bias.numel() == B * S, "mask_bias must be [B, S]");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
   auto out = torch::empty({B, S, H}, qkv.options());
   auto lse = torch::empty({B, nh, S}, qkv.options());
   Tensor dmask;
-  if (keep < 1.0) dmask = torch::empty({B, nh, S, S / 32}, qkv.options().dtype(torch::kInt32));
+  // 1 bit per (query, key); rows padded to 128 keys (the backward's key-block size)
+  if (keep < 1.0) dmask = torch::empty({B, nh, S, ((S + 127) / 128) * 4}, qkv.options().dtype(torch::kInt32));
   else dmask = torch::empty({0}, qkv.options().dtype(torch::kInt32));
   hx_attn_fwd(qkv.data_ptr<float>(), mask_bias.data_ptr<float>(), out.data_ptr<float>(), lse.data_ptr<float>(),
               keep < 1.0 ? reinterpret_cast<uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr, (int)B, (int)S, (int)nh,
@@ -266,8 +266,8 @@ Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor ls
   check_f32(qkv, "qkv");
   const int64_t B = qkv.size(0), S = qkv.size(1);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
-  // with one key block per head (S == 128) every dQKV element is overwritten: no memset
-  auto dqkv = S == 128 ? torch::empty_like(qkv) : torch::zeros_like(qkv);
+  // with one key block per head (S <= 128) every dQKV element is overwritten: no memset
+  auto dqkv = S <= 128 ? torch::empty_like(qkv) : torch::zeros_like(qkv);
   hx_attn_bwd(qkv.data_ptr<float>(), mask_bias.data_ptr<float>(), dout.data_ptr<float>(), out.data_ptr<float>(),
               lse.data_ptr<float>(), keep < 1.0 ? reinterpret_cast<const uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr,
               dqkv.data_ptr<float>(), (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv));

@@ -60,13 +60,15 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const float* __restrict__ qkv,
   const int b = blockIdx.z, hd = blockIdx.y;
   const int H = nh * D, H3 = 3 * H;
   const int q = blockIdx.x * 128 + w * 32 + l32;
+  const int qc = q < S ? q : S - 1;            // rows past S: clamped loads, no stores
+  const int Sp = (S + 127) & ~127;             // mask-word / RNG row pitch
   const float* base = qkv + (int64_t)b * S * H3;
   const float scale = 0.125f;  // 1/sqrt(64): exact power of two
 
   // Q row slice held in registers: qr[s] = Q[q][h*32 + s] * scale
   float qr[32];
   {
-    const float4* qp = reinterpret_cast<const float4*>(base + (int64_t)q * H3 + hd * D + h * 32);
+    const float4* qp = reinterpret_cast<const float4*>(base + (int64_t)qc * H3 + hd * D + h * 32);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float4 v = qp[i];
@@ -82,16 +84,17 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const float* __restrict__ qkv,
   const int64_t bh = (int64_t)b * nh + hd;
 
   for (int kt = 0; kt < S; kt += 64) {
-    // ---- stage K, V tile (64 keys x 64 dims) + mask into LDS
+    // ---- stage K, V tile (64 keys x 64 dims) + mask into LDS (keys past S: -inf)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int e = tid + i * 256;         // float4 index in the 64x16 tile
       const int row = e >> 4, c4 = (e & 15) * 4;
-      const float* src = base + (int64_t)(kt + row) * H3 + hd * D + c4;
+      const int kr = kt + row < S ? kt + row : S - 1;
+      const float* src = base + (int64_t)kr * H3 + hd * D + c4;
       *reinterpret_cast<float4*>(&Ks[row * LDK + c4]) = *reinterpret_cast<const float4*>(src + H);
       *reinterpret_cast<float4*>(&Vs[row * LDK + c4]) = *reinterpret_cast<const float4*>(src + 2 * H);
     }
-    if (tid < 64) Ms[tid] = maskb[(int64_t)b * S + kt + tid];
+    if (tid < 64) Ms[tid] = kt + tid < S ? maskb[(int64_t)b * S + kt + tid] : -INFINITY;
     __syncthreads();
 
     // ---- S^T = K . Q^T for two 32-key sub-blocks; keys in registers, queries on lanes
@@ -137,7 +140,7 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const float* __restrict__ qkv,
     }
     if (kDrop) {
       // keys of register group g (r = 4g..4g+3): sub-block kb, 8g + 4h + (0..3)
-      const int64_t rowbase = (bh * S + q) * S + kt;
+      const int64_t rowbase = (bh * S + q) * Sp + kt;
       uint32_t bits0 = 0, bits1 = 0;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -153,8 +156,8 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const float* __restrict__ qkv,
       }
       bits0 |= __shfl_xor(bits0, 32, 64);
       bits1 |= __shfl_xor(bits1, 32, 64);
-      if (h == 0) {
-        uint32_t* dm = dmask + (bh * S + q) * (S >> 5) + (kt >> 5);
+      if (h == 0 && q < S) {
+        uint32_t* dm = dmask + (bh * S + q) * (Sp >> 5) + (kt >> 5);
         dm[0] = bits0;
         dm[1] = bits1;
       }
@@ -173,6 +176,7 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const float* __restrict__ qkv,
     __syncthreads();
   }
   // ---- epilogue: O = O^T^T / l ; lane owns query q, registers hold 4-contiguous dims
+  if (q >= S) return;
   const float inv_l = 1.f / l_run;
   float* op = out + ((int64_t)b * S + q) * H + hd * D;
 #pragma unroll
@@ -227,27 +231,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float* base = qkv + (int64_t)b * S * H3;
   const int64_t bh = (int64_t)b * nh + hd;
   const float scale = 0.125f, inv_keep = 1.f / keep;
-  const int nwords = S >> 5;
+  const int nwords = ((S + 127) & ~127) >> 5;   // mask words per query row (fwd pitch)
 
   // ---- K of this block's 128 keys -> LDS; V of this lane's key / dim-half -> registers
+  // (keys past S: clamped loads, -inf mask -> P = 0, never stored)
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int e = tid + i * 256;
     const int row = e >> 4, c4 = (e & 15) * 4;
+    const int kr = kbase + row < S ? kbase + row : S - 1;
     *reinterpret_cast<float4*>(&Ks[row * LDK + c4]) =
-        *reinterpret_cast<const float4*>(base + (int64_t)(kbase + row) * H3 + H + hd * D + c4);
+        *reinterpret_cast<const float4*>(base + (int64_t)kr * H3 + H + hd * D + c4);
   }
   const int mykey = kbase + w * 32 + l32;     // key on this lane
+  const int mykc = mykey < S ? mykey : S - 1;
   float vr[32];
   {
-    const float4* vp = reinterpret_cast<const float4*>(base + (int64_t)mykey * H3 + 2 * H + hd * D + h * 32);
+    const float4* vp = reinterpret_cast<const float4*>(base + (int64_t)mykc * H3 + 2 * H + hd * D + h * 32);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
       const float4 v = vp[i];
       vr[4 * i] = v.x; vr[4 * i + 1] = v.y; vr[4 * i + 2] = v.z; vr[4 * i + 3] = v.w;
     }
   }
-  const float mk = maskb[(int64_t)b * S + mykey];
+  const float mk = mykey < S ? maskb[(int64_t)b * S + mykey] : -INFINITY;
   const float* Kw = Ks + (w * 32) * LDK;      // this wave's keys
 
   // staging map of a 32x64 tile: thread -> rows (tid>>4) and 16 + (tid>>4), float4 column c4
@@ -255,15 +262,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   auto ld_tile = [&](int qt, float4 (&qn)[2], float4 (&dn)[2], float4 (&on)[2], float& xn, uint32_t& mn) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int64_t r = (int64_t)b * S + qt + srow + 16 * i;
+      const int qr = qt + srow + 16 * i;
+      const int64_t r = (int64_t)b * S + (qr < S ? qr : S - 1);
       qn[i] = *reinterpret_cast<const float4*>(qkv + r * H3 + hd * D + sc4);
       dn[i] = *reinterpret_cast<const float4*>(dout + r * H + hd * D + sc4);
       on[i] = *reinterpret_cast<const float4*>(outp + r * H + hd * D + sc4);
     }
-    if (tid < 32) xn = lse[bh * S + qt + tid];
+    if (tid < 32) xn = qt + tid < S ? lse[bh * S + qt + tid] : INFINITY;   // rows past S: P = 0
     if (kDrop && tid >= 64 && tid < 64 + 128) {
       const int i = tid - 64, row = i >> 2, wd = i & 3;
-      mn = dmask[(bh * S + qt + row) * nwords + (kbase >> 5) + wd];
+      mn = qt + row < S ? dmask[(bh * S + qt + row) * nwords + (kbase >> 5) + wd] : 0u;
     }
   };
   float4 qn[2], dn[2], on[2];
@@ -350,9 +358,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       qa1 = mfma16(a, Ks[key * LDK + dqa * 16 + 16 + r16], qa1);
       if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
-    float* dq = dqkv + ((int64_t)b * S + qt + qh * 16 + 4 * k4) * H3 + hd * D + dqa * 16 + r16;
+    const int q0 = qt + qh * 16 + 4 * k4;
+    float* dq = dqkv + ((int64_t)b * S + q0) * H3 + hd * D + dqa * 16 + r16;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
+      if (q0 + r >= S) continue;
       if (single) {
         dq[(int64_t)r * H3] = qa0[r] * scale;
         dq[(int64_t)r * H3 + 16] = qa1[r] * scale;
@@ -368,6 +378,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int key = kbase + w * 32 + crow(r, h);
+    if (key >= S) continue;
     dk[(int64_t)key * H3 + l32] = dk0[r];
     dk[(int64_t)key * H3 + 32 + l32] = dk1[r];
     dvp[(int64_t)key * H3 + l32] = dv0[r];
@@ -383,7 +394,7 @@ size_t hx_attn_bwd_smem_bytes() {
 
 void hx_attn_fwd(const float* qkv, const float* maskb, float* out, float* lse, uint32_t* dmask, int B, int S, int nh,
                  float keep, uint64_t seed, uint64_t stream, hipStream_t s) {
-  dim3 grid(S / 128, nh, B);
+  dim3 grid((S + 127) / 128, nh, B);
   if (keep < 1.f)
     attn_fwd_k<true><<<grid, 256, 0, s>>>(qkv, maskb, out, lse, dmask, S, nh, keep, seed, stream);
   else
@@ -392,7 +403,7 @@ void hx_attn_fwd(const float* qkv, const float* maskb, float* out, float* lse, u
 
 void hx_attn_bwd(const float* qkv, const float* maskb, const float* dout, const float* out, const float* lse,
                  const uint32_t* dmask, float* dqkv, int B, int S, int nh, float keep, hipStream_t s) {
-  dim3 grid(S / 128, nh, B);
+  dim3 grid((S + 127) / 128, nh, B);
   const size_t smem = hx_attn_bwd_smem_bytes();
   static bool attr = false;
   if (!attr) {  // > 64 KiB dynamic LDS needs an explicit opt-in (gfx950 has 160 KiB per CU)

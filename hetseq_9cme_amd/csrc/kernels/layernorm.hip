@@ -130,9 +130,34 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
   Row<CH> dg, db, dbias;
 #pragma unroll
   for (int c = 0; c < CH; ++c) dg.v[c] = db.v[c] = dbias.v[c] = hx::f4(0.f);
+  float4 gam[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int j = (c * 64 + lane) * 4;
+    gam[c] = j < H ? *reinterpret_cast<const float4*>(gamma + j) : hx::f4(0.f);
+  }
+
+  // one row of look-ahead: the next row's loads are in flight while this row computes
+  Row<CH> zn, dn;
+  float mn = 0.f, rn = 0.f;
+  auto load_row = [&](int64_t r) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int j = (c * 64 + lane) * 4;
+      if (j < H) {
+        zn.v[c] = hx::load4(z + r * H + j);
+        dn.v[c] = hx::load4(dout + r * H + j);
+      }
+    }
+    mn = mean_in[r];
+    rn = rstd_in[r];
+  };
+  if (wave < rows) load_row(wave);
 
   for (int64_t r = wave; r < rows; r += nw) {
-    const float mean = mean_in[r], rstd = rstd_in[r];
+    const Row<CH> zc = zn, dc = dn;
+    const float mean = mn, rstd = rn;
+    if (r + nw < rows) load_row(r + nw);
     Row<CH> xh, dxh;
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -140,8 +165,8 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
       const int j = (c * 64 + lane) * 4;
       float4 xv = hx::f4(0.f), dv = hx::f4(0.f);
       if (j < H) {
-        const float4 zz = hx::load4(z + r * H + j);
-        float4 d = hx::load4(dout + r * H + j);
+        const float4 zz = zc.v[c];
+        float4 d = dc.v[c];
         if (drop && kDropAfter) {
           const uint32_t k = hx::keep4(seed, stream, (uint64_t)(r * H + j) >> 2, keep_prob);
           d.x = (k & 1) ? d.x * inv_keep : 0.f;
@@ -149,7 +174,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
           d.z = (k & 4) ? d.z * inv_keep : 0.f;
           d.w = (k & 8) ? d.w * inv_keep : 0.f;
         }
-        const float4 g = *reinterpret_cast<const float4*>(gamma + j);
+        const float4 g = gam[c];
         xv = make_float4((zz.x - mean) * rstd, (zz.y - mean) * rstd, (zz.z - mean) * rstd, (zz.w - mean) * rstd);
         dv = make_float4(d.x * g.x, d.y * g.y, d.z * g.z, d.w * g.w);
         dg.v[c].x += d.x * xv.x; dg.v[c].y += d.y * xv.y; dg.v[c].z += d.z * xv.z; dg.v[c].w += d.w * xv.w;
@@ -187,10 +212,9 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
       }
     }
   }
-  // fold the 4 waves' column partials through LDS: three passes (gamma, beta, bias)
-  const int nsum = want_dbias ? 3 : 2;
-  for (int q = 0; q < nsum; ++q) {
-    Row<CH>& src = q == 0 ? dg : (q == 1 ? db : dbias);
+  // fold the 4 waves' column partials through LDS (each accumulator selected at
+  // compile time: a runtime-selected reference would demote them to scratch)
+  auto fold = [&](const Row<CH>& src, int q) {
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int j = (c * 64 + lane) * 4;
@@ -204,7 +228,10 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
       partial[((int64_t)blockIdx.x * 3 + q) * H + j] = a;
     }
     __syncthreads();
-  }
+  };
+  fold(dg, 0);
+  fold(db, 1);
+  if (want_dbias) fold(dbias, 2);
 }
 
 // ------------------------------------------------------------------------ embedding

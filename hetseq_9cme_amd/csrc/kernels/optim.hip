@@ -65,6 +65,40 @@ __global__ __launch_bounds__(NT) void grad_norm_finalize_k(const double* __restr
 }
 
 template <bool kShadow>
+__device__ __forceinline__ void adam4(float4& pp, const float4 gg, float4& mm, float4& vv, float gs, float b1,
+                                      float b2, float ob1, float ob2, float eps, float step_size, float wd_lr) {
+  float* pa = &pp.x;
+  const float* ga = &gg.x;
+  float* ma = &mm.x;
+  float* va = &vv.x;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const float gr = ga[j] * gs;
+    ma[j] = ma[j] * b1 + ob1 * gr;
+    va[j] = va[j] * b2 + ob2 * gr * gr;
+    const float denom = sqrtf(va[j]) + eps;
+    float x = pa[j];
+    x = x - wd_lr * x;
+    x = x - step_size * (ma[j] / denom);
+    pa[j] = x;
+  }
+}
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ntload(const float4* a) {
+  const f32x4_t r = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(a));
+  return make_float4(r.x, r.y, r.z, r.w);
+}
+__device__ __forceinline__ void ntstore(float4 v, float4* a) {
+  f32x4_t r = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(r, reinterpret_cast<f32x4_t*>(a));
+}
+
+// Streaming update: every byte of p/g/m/v is touched once per step (7 x 4 B per
+// parameter, 3 GB for BERT-base), so two independent float4 groups per thread
+// per iteration keep more loads in flight and non-temporal hints keep the
+// stream from evicting the L2 / MALL working set of the next kernels.
+template <bool kShadow>
 __global__ __launch_bounds__(NT) void adam_k(float* __restrict__ p, const float* __restrict__ g,
                                            float* __restrict__ m, float* __restrict__ v,
                                            uint16_t* __restrict__ shadow, const float* __restrict__ gscale,
@@ -73,36 +107,31 @@ __global__ __launch_bounds__(NT) void adam_k(float* __restrict__ p, const float*
   const float gs = gscale[0];
   const float ob1 = 1.f - b1, ob2 = 1.f - b2;
   const int64_t n4 = n >> 2;
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT) {
-    float4 pp = reinterpret_cast<float4*>(p)[i];
-    const float4 gg = reinterpret_cast<const float4*>(g)[i];
-    float4 mm = reinterpret_cast<float4*>(m)[i];
-    float4 vv = reinterpret_cast<float4*>(v)[i];
-    float* pa = &pp.x;
-    const float* ga = &gg.x;
-    float* ma = &mm.x;
-    float* va = &vv.x;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float gr = ga[j] * gs;
-      ma[j] = ma[j] * b1 + ob1 * gr;
-      va[j] = va[j] * b2 + ob2 * gr * gr;
-      const float denom = sqrtf(va[j]) + eps;
-      float x = pa[j];
-      x = x - wd_lr * x;
-      x = x - step_size * (ma[j] / denom);
-      pa[j] = x;
+  float4* P = reinterpret_cast<float4*>(p);
+  const float4* G = reinterpret_cast<const float4*>(g);
+  float4* M = reinterpret_cast<float4*>(m);
+  float4* V = reinterpret_cast<float4*>(v);
+  const int64_t stride = (int64_t)gridDim.x * NT;
+  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n4; i += 2 * stride) {
+    const int64_t i2 = i + stride;
+    const bool two = i2 < n4;
+    float4 p0 = ntload(P + i), m0 = ntload(M + i), v0 = ntload(V + i);
+    const float4 g0 = ntload(G + i);
+    float4 p1 = make_float4(0.f, 0.f, 0.f, 0.f), m1 = p1, v1 = p1, g1 = p1;
+    if (two) {
+      p1 = ntload(P + i2); m1 = ntload(M + i2); v1 = ntload(V + i2); g1 = ntload(G + i2);
     }
-    reinterpret_cast<float4*>(p)[i] = pp;
-    reinterpret_cast<float4*>(m)[i] = mm;
-    reinterpret_cast<float4*>(v)[i] = vv;
-    if (kShadow) {
-      ushort4 s;
-      s.x = hx::f2bf(pp.x);
-      s.y = hx::f2bf(pp.y);
-      s.z = hx::f2bf(pp.z);
-      s.w = hx::f2bf(pp.w);
-      reinterpret_cast<ushort4*>(shadow)[i] = s;
+    adam4<kShadow>(p0, g0, m0, v0, gs, b1, b2, ob1, ob2, eps, step_size, wd_lr);
+    ntstore(p0, P + i); ntstore(m0, M + i); ntstore(v0, V + i);
+    if (kShadow)
+      reinterpret_cast<ushort4*>(shadow)[i] = make_ushort4(hx::f2bf(p0.x), hx::f2bf(p0.y), hx::f2bf(p0.z),
+                                                           hx::f2bf(p0.w));
+    if (two) {
+      adam4<kShadow>(p1, g1, m1, v1, gs, b1, b2, ob1, ob2, eps, step_size, wd_lr);
+      ntstore(p1, P + i2); ntstore(m1, M + i2); ntstore(v1, V + i2);
+      if (kShadow)
+        reinterpret_cast<ushort4*>(shadow)[i2] = make_ushort4(hx::f2bf(p1.x), hx::f2bf(p1.y), hx::f2bf(p1.z),
+                                                              hx::f2bf(p1.w));
     }
   }
   for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {

@@ -5,8 +5,9 @@ mask_bias; probs = dropout(softmax(scores)); ctx = probs V; heads merged back
 to [B, S, H].  The additive mask is the reference's (1 - m) * -10000 (not -inf).
 
 GPU path: the fused flash-style HIP kernel (``_C.attn_fwd`` / ``attn_bwd``,
-csrc/kernels/attention.hip) for fp32, head_dim 64, seq_len % 128 == 0 (BERT
-phase 1/2); other shapes use the composite below (batched GEMMs + softmax), which
+csrc/kernels/attention.hip) for fp32 and head_dim 64 at any sequence length
+(keys past S are masked, rows past S are neither computed into nor stored);
+other shapes / dtypes use the composite below (batched GEMMs + softmax), which
 is also the CPU path and the test oracle.
 """
 import math
@@ -44,7 +45,7 @@ def _fused_ok(qkv, num_heads):
         return False
     B, S, H3 = qkv.shape
     d = (H3 // 3) // num_heads
-    return qkv.dtype == torch.float32 and d == 64 and S % 128 == 0
+    return qkv.dtype == torch.float32 and d == 64 and S >= 1
 
 
 class _AttnFn(torch.autograd.Function):

@@ -58,15 +58,41 @@ def bench_ln(B, S, H=768):
     g = torch.ones(H, device='cuda')
     bt = torch.zeros(H, device='cuda')
     bias = torch.zeros(H, device='cuda')
-    report('ln_fwd(bias+drop+res)', timeit(lambda: C().ln_fwd(x, bias, res, g, bt, 1e-12, 0.9, 1, 0, False, False)),
-           bytes_=3 * n * H * 4)
+    report('ln_fwd(bias+drop+res)', timeit(lambda: C().ln_fwd(x, bias, res, g, bt, 1e-12, 0.9, 1, 0, False, True)),
+           bytes_=4 * n * H * 4)
+    out, z, mean, rstd = C().ln_fwd(x, bias, res, g, bt, 1e-12, 0.9, 1, 0, False, True)
+    dout = torch.randn_like(out)
+    report('ln_bwd(+dy,+dbias)', timeit(lambda: C().ln_bwd(dout, z, mean, rstd, g, 0.9, 1, 0, False, True, True,
+                                                           None, None, None)), bytes_=4 * n * H * 4)
+
+
+def bench_ffn_act(B, S, F=3072):
+    n = B * S
+    y = torch.randn(n, F, device='cuda')
+    b = torch.zeros(F, device='cuda')
+    report('bias_gelu_fwd', timeit(lambda: C().bias_act_fwd(y, b, 0)), bytes_=2 * n * F * 4)
+    dout = torch.randn_like(y)
+    report('bias_gelu_bwd(+dbias)', timeit(lambda: C().bias_act_bwd(dout, y, b, None, 0, True, None)),
+           bytes_=3 * n * F * 4)
+    qkv = torch.randn(n, 2304, device='cuda')
+    report('colsum(dqkv bias grad)', timeit(lambda: C().colsum(qkv, None, None)), bytes_=n * 2304 * 4)
+
+
+def bench_adam(n=110_000_000):
+    p = torch.randn(n, device='cuda')
+    g = torch.randn(n, device='cuda')
+    m = torch.zeros(n, device='cuda')
+    v = torch.zeros(n, device='cuda')
+    gs = torch.ones(1, device='cuda')
+    report('adam(110M params)', timeit(lambda: C().adam(p, g, m, v, None, gs, 0, n, 0.9, 0.999, 1e-8, 1e-4, 1e-6)),
+           bytes_=7 * n * 4)
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--batch', type=int, default=128)
     ap.add_argument('--seq', type=int, default=128)
-    ap.add_argument('--only', default='attn')
+    ap.add_argument('--only', default='attn,ln,ffn,adam')
     a = ap.parse_args()
     torch.manual_seed(0)
     which = a.only.split(',')
@@ -74,6 +100,10 @@ def main():
         bench_attn(a.batch, a.seq)
     if 'ln' in which:
         bench_ln(a.batch, a.seq)
+    if 'ffn' in which:
+        bench_ffn_act(a.batch, a.seq)
+    if 'adam' in which:
+        bench_adam()
 
 
 if __name__ == '__main__':

@@ -54,6 +54,8 @@ class Controller(object):
         self.device = torch.device('cuda', torch.cuda.current_device()) if self.cuda else torch.device('cpu')
         if not getattr(args, 'fused_kernels', True):
             ops.set_fused(False)      # A/B mode: plain torch ops on the GPU
+        if getattr(args, 'overlap_wgrad', False):
+            ops.set_side_stream(True)
         if self.cuda:
             gemm_tuning.configure(getattr(args, 'gemm_tuning', 'table'), getattr(args, 'gemm_tuning_file', None))
         model = model.to(self.device)

@@ -8,6 +8,7 @@ from .rng import get_rng, set_step_seed  # noqa: F401
 from .fused import (  # noqa: F401
     embed_ln, bias_dropout_residual_ln, layer_norm, bias_act, dropout, linear3, attention,
     decoder_xent, masked_rows, gelu_ref, layer_norm_ref, linear, grad_slot, ResidualGrad,
+    set_side_stream, active_side_stream, side_join,
 )
 
 

@@ -6,6 +6,7 @@ the same math (used by the CPU test-suite and as the numerics oracle for the GPU
 kernel tests).  Semantics follow the reference model (hetseq/bert_modeling.py).
 """
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -18,6 +19,11 @@ ACT_IDS = {'gelu': 0, 'tanh': 1, 'relu': 2, 'none': 3}
 
 def _is_bf16(t):
     return t.dtype == torch.bfloat16
+
+
+def _nullctx():
+    import contextlib
+    return contextlib.nullcontext()
 
 
 def grad_slot(p):
@@ -74,6 +80,55 @@ def _dgrad(dy2, W, xshape, mbox):
     return dx if other is None else dx + other.view(xshape).to(dx.dtype)
 
 
+# ----------------------------------------------------------------- weight-grad side stream
+class _Side(object):
+    # opt-in: measured 71.7 vs 69.5 ms/step on BERT-base fp32 (1x MI355X) -- the
+    # co-scheduled kernels cost the full-GPU GEMM tiles more than the overlap wins
+    enabled = os.environ.get('HETSEQ_SIDE_STREAM', '0') == '1'
+    streams = {}          # device index -> torch.cuda.Stream
+    active = set()        # device indices with side work queued in the current backward
+
+
+def set_side_stream(flag):
+    """Enable / disable overlapping weight-gradient work on a side stream."""
+    _Side.enabled = bool(flag)
+
+
+def side_begin(device):
+    """Side stream for off-critical-path weight-gradient work (dW GEMMs, bias
+    column sums) of the running backward, ordered after everything already
+    queued on the compute stream.  While the compute stream continues with the
+    dgrad chain (attention / LayerNorm / GELU backward: mostly memory-bound),
+    the side stream's GEMMs fill the matrix cores.  Joined back into the compute
+    stream by an end-of-backward callback (``side_join``)."""
+    if not _Side.enabled or device.type != 'cuda':
+        return None
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    st = _Side.streams.get(idx)
+    if st is None:
+        st = _Side.streams[idx] = torch.cuda.Stream(device=idx)
+    st.wait_stream(torch.cuda.current_stream(idx))
+    if not _Side.active:
+        torch.autograd.Variable._execution_engine.queue_callback(side_join)
+    _Side.active.add(idx)
+    return st
+
+
+def active_side_stream(device):
+    """The side stream if this backward queued work on it (reducer ordering)."""
+    if device.type != 'cuda':
+        return None
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    return _Side.streams.get(idx) if idx in _Side.active else None
+
+
+def side_join():
+    """Make the compute stream wait for all queued side-stream work."""
+    for idx in list(_Side.active):
+        torch.cuda.current_stream(idx).wait_stream(_Side.streams[idx])
+    _Side.active.clear()
+
+
 # ----------------------------------------------------------------- references
 def gelu_ref(x):
     return x * 0.5 * (1.0 + torch.erf(x / 1.41421))
@@ -112,6 +167,7 @@ class _EmbedLNFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dout):
+        side_join()   # the tied decoder's dW may still be in flight on the side stream
         ids, tt, z, mean, rstd, gamma = ctx.saved_tensors
         keep, seed, stream, V, P, NT = ctx.meta
         dout = dout.contiguous()
@@ -282,16 +338,22 @@ class _LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox) if ctx.needs_input_grad[0] else None
         slot = grad_slot(W)
-        if slot is not None and dy2.dtype == torch.float32:
-            dW = torch.mm(dy2.t(), x2, out=slot)
-        else:
-            dW = torch.mm(dy2.t(), x2).float()
-        db = None
-        if b is not None:
-            if dy2.shape[-1] % 4 == 0:
-                db = C().colsum(dy2.contiguous(), None, grad_slot(b))
+        direct = slot is not None and dy2.dtype == torch.float32
+        side = side_begin(dy2.device) if direct else None
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            if direct:
+                dW = torch.mm(dy2.t(), x2, out=slot)
             else:
-                db = dy2.float().sum(0)
+                dW = torch.mm(dy2.t(), x2).float()
+            db = None
+            if b is not None:
+                if dy2.shape[-1] % 4 == 0:
+                    db = C().colsum(dy2.contiguous(), None, grad_slot(b))
+                else:
+                    db = dy2.float().sum(0)
+        if side is not None:
+            dy2.record_stream(side)
+            x2.record_stream(side)
         return dx, dW, db, None
 
 
@@ -353,22 +415,28 @@ class _Linear3Fn(torch.autograd.Function):
         # weight grads: ONE GEMM straight into the three adjacent flat slots when possible
         ws = [grad_slot(w) for w in (wq, wk, wv)]
         fused = _adjacent_view(ws) if all(t is not None for t in ws) else None
-        if fused is not None and dy2.dtype == torch.float32:
-            torch.mm(dy2.t(), x2, out=fused)
-            gW = ws
-        else:
-            dW = (dy2.t() @ x2).float()
-            gW = [dW[:a], dW[a:a + b_], dW[a + b_:]]
-            for k, t in enumerate(ws):
-                if t is not None:
-                    t.copy_(gW[k])
-                    gW[k] = t
         bs = [grad_slot(t) for t in (bq, bk, bv)]
         fb = _adjacent_view(bs) if all(t is not None for t in bs) else None
-        if use_kernels(dy2) and dy2.shape[-1] % 4 == 0:
-            db = C().colsum(dy2.contiguous(), None, fb)
-        else:
-            db = dy2.float().sum(0)
+        direct = fused is not None and fb is not None and dy2.dtype == torch.float32
+        side = side_begin(dy2.device) if direct else None
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            if fused is not None and dy2.dtype == torch.float32:
+                torch.mm(dy2.t(), x2, out=fused)
+                gW = ws
+            else:
+                dW = (dy2.t() @ x2).float()
+                gW = [dW[:a], dW[a:a + b_], dW[a + b_:]]
+                for k, t in enumerate(ws):
+                    if t is not None:
+                        t.copy_(gW[k])
+                        gW[k] = t
+            if use_kernels(dy2) and dy2.shape[-1] % 4 == 0:
+                db = C().colsum(dy2.contiguous(), None, fb)
+            else:
+                db = dy2.float().sum(0)
+        if side is not None:
+            dy2.record_stream(side)
+            x2.record_stream(side)
         gb = bs if fb is not None else [db[:a], db[a:a + b_], db[a + b_:]]
         return (dx, gW[0], gW[1], gW[2], gb[0], gb[1], gb[2], None)
 
@@ -407,7 +475,12 @@ class _DecoderXentFn(torch.autograd.Function):
         dh = torch.mm(dl, W.to(dl.dtype))
         slot = grad_slot(Wp)
         if slot is not None and dl.dtype == torch.float32:
-            dW = torch.mm(dl.t(), h, out=slot)
+            side = side_begin(dl.device)
+            with torch.cuda.stream(side) if side is not None else _nullctx():
+                dW = torch.mm(dl.t(), h, out=slot)
+            if side is not None:
+                dl.record_stream(side)
+                h.record_stream(side)
         else:
             dW = torch.mm(dl.t(), h).float()
         return dh, dW, dbias, None

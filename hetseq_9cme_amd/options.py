@@ -62,6 +62,9 @@ def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialD
                              'online benchmarking of unseen shapes, or library defaults')
     parser.add_argument('--gemm-tuning-file', default=None, metavar='PATH',
                         help='where --gemm-tuning online writes its table (device ordinal appended)')
+    parser.add_argument('--overlap-wgrad', action='store_true',
+                        help='run weight-gradient GEMMs / bias column sums on a side HIP stream, overlapping '
+                             'the dgrad chain (off by default: slower for BERT-base on one MI355X)')
     parser.add_argument('--profile-phases', action='store_true',
                         help='log host wall time per step phase (prep/sample/fwd_bwd/stats/optimizer/'
                              'meters); a phase that waits on the GPU shows up as long')

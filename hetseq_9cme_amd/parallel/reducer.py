@@ -33,6 +33,8 @@ import contextlib
 import torch
 import torch.distributed as dist
 
+from .. import ops
+
 
 class GradReducer(object):
     def __init__(self, flat, bucket_cap_mb=25, process_group=None, find_unused_parameters=False,
@@ -112,11 +114,20 @@ class GradReducer(object):
     def _launch_ready(self, force=False):
         while self._launched < len(self.buckets) and (force or self._pending[self._launched] == 0):
             s, e, _ = self.buckets[self._launched]
-            work = dist.all_reduce(self.flat.grad_flat[s:e], group=self.group, async_op=True)
+            side = ops.active_side_stream(self.flat.grad_flat.device)
+            if side is not None:
+                # weight grads of this bucket may come from the side stream: launch
+                # the collective from it (after the compute stream's work so far)
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    work = dist.all_reduce(self.flat.grad_flat[s:e], group=self.group, async_op=True)
+            else:
+                work = dist.all_reduce(self.flat.grad_flat[s:e], group=self.group, async_op=True)
             self._works.append(work)
             self._launched += 1
 
     def _finalize_backward(self):
+        ops.side_join()
         for i, u in enumerate(self.used):
             if not u:
                 self.flat.adopt(i)   # unused this micro-batch: keep/zero its slot

@@ -8,7 +8,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from hetseq_9cme_amd import options  # noqa: E402
 
 NEW = {'--async-save', '--check-params-every', '--distributed-timeout', '--ent_name_id_file', '--fused-kernels',
-       '--gemm-tuning', '--gemm-tuning-file', '--precision', '--profile-phases', '--user-module'}
+       '--gemm-tuning', '--gemm-tuning-file', '--precision', '--profile-phases', '--user-module',
+       '--overlap-wgrad'}
 
 SECTIONS = [('bert', 'adam'), ('mnist', 'adadelta'), ('BertForTokenClassification', 'adam'),
             ('BertForELClassification', 'adam')]

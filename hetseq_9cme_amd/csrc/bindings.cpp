@@ -251,8 +251,9 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
   auto out = torch::empty({B, S, H}, qkv.options());
   auto lse = torch::empty({B, nh, S}, qkv.options());
   Tensor dmask;
-  // 1 bit per (query, key); rows padded to 128 keys (the backward's key-block size)
-  if (keep < 1.0) dmask = torch::empty({B, nh, S, ((S + 127) / 128) * 4}, qkv.options().dtype(torch::kInt32));
+  // 1 bit per (key, query), stored [key][query word] with both padded to 128
+  const int64_t Sp = (S + 127) / 128 * 128;
+  if (keep < 1.0) dmask = torch::empty({B, nh, Sp, Sp / 32}, qkv.options().dtype(torch::kInt32));
   else dmask = torch::empty({0}, qkv.options().dtype(torch::kInt32));
   hx_attn_fwd(qkv.data_ptr<float>(), mask_bias.data_ptr<float>(), out.data_ptr<float>(), lse.data_ptr<float>(),
               keep < 1.0 ? reinterpret_cast<uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr, (int)B, (int)S, (int)nh,

@@ -57,8 +57,10 @@ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1
   const uint32_t M0 = 0xD2511F53u, M1 = 0xCD9E8D57u, W0 = 0x9E3779B9u, W1 = 0xBB67AE85u;
 #pragma unroll
   for (int r = 0; r < 10; ++r) {
-    const uint32_t hi0 = __umulhi(M0, c.x), lo0 = M0 * c.x;
-    const uint32_t hi1 = __umulhi(M1, c.z), lo1 = M1 * c.z;
+    // one 32x32->64 multiply per product (v_mad_u64_u32) instead of mul_hi + mul_lo
+    const uint64_t p0 = (uint64_t)M0 * c.x, p1 = (uint64_t)M1 * c.z;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
     c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
     k0 += W0;
     k1 += W1;
@@ -83,6 +85,17 @@ __device__ __forceinline__ uint32_t keep4(uint64_t seed, uint64_t stream, uint64
   rand4(seed, stream, q, u);
   return (u[0] < keep_prob ? 1u : 0u) | (u[1] < keep_prob ? 2u : 0u) | (u[2] < keep_prob ? 4u : 0u) |
          (u[3] < keep_prob ? 8u : 0u);
+}
+
+// 8 keep decisions from ONE Philox call: 16-bit uniforms vs a 16-bit threshold
+// t16 = round(keep * 65536) (keep-probability error < 2^-17).  bit j <-> decision j
+// (word j>>1, low half for even j).
+__device__ __forceinline__ uint32_t keep8(uint64_t seed, uint64_t stream, uint64_t q, uint32_t t16) {
+  u32x4 c{(uint32_t)q, (uint32_t)(q >> 32), (uint32_t)stream, (uint32_t)(stream >> 32)};
+  const u32x4 r = philox4x32_10(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  return ((r.x & 0xFFFFu) < t16 ? 1u : 0u) | ((r.x >> 16) < t16 ? 2u : 0u) | ((r.y & 0xFFFFu) < t16 ? 4u : 0u) |
+         ((r.y >> 16) < t16 ? 8u : 0u) | ((r.z & 0xFFFFu) < t16 ? 16u : 0u) | ((r.z >> 16) < t16 ? 32u : 0u) |
+         ((r.w & 0xFFFFu) < t16 ? 64u : 0u) | ((r.w >> 16) < t16 ? 128u : 0u);
 }
 
 // ---------------------------------------------------------------- bf16

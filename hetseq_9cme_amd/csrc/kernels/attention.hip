@@ -40,6 +40,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int D = 64;      // head dim (BERT-base/large)
 constexpr int LDK = 68;    // padded LDS row stride (floats)
 
+// v_writelane_b32: put a wave-uniform value into one lane of a VGPR (1 instruction)
+__device__ __forceinline__ uint32_t write_lane(uint32_t v, uint32_t val, int lane) {
+  asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(val), "s"(lane));
+  return v;
+}
+
 __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
@@ -49,19 +55,25 @@ __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2
 // ============================================================================ forward
 // grid (S/128, nh, B), block 256 = 4 waves x 32 queries.
 template <bool kDrop>
-__global__ __launch_bounds__(256) void attn_fwd_k(const float* __restrict__ qkv, const float* __restrict__ maskb,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_fwd_k(const float* __restrict__ qkv, const float* __restrict__ maskb,
                                                 float* __restrict__ out, float* __restrict__ lse,
                                                 uint32_t* __restrict__ dmask, int S, int nh, float keep,
                                                 uint64_t seed, uint64_t stream) {
   __shared__ __attribute__((aligned(16))) float Ks[64 * LDK];
   __shared__ __attribute__((aligned(16))) float Vs[64 * LDK];
   __shared__ float Ms[64];
+  // dropout words of this workgroup, written out after the key loop: a global store
+  // inside the loop would hold every later s_waitcnt vmcnt (stores count in vmcnt)
+  constexpr int kMaxStagedTiles = 8;   // S <= 512: all of BERT's positions
+  __shared__ uint32_t Wst[kDrop ? kMaxStagedTiles * 256 : 1];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int b = blockIdx.z, hd = blockIdx.y;
   const int H = nh * D, H3 = 3 * H;
   const int q = blockIdx.x * 128 + w * 32 + l32;
   const int qc = q < S ? q : S - 1;            // rows past S: clamped loads, no stores
   const int Sp = (S + 127) & ~127;             // mask-word / RNG row pitch
+  const int q0w = blockIdx.x * 128 + w * 32;    // first query of this wave (bitmask word)
+  const uint32_t t16 = (uint32_t)(keep * 65536.f + 0.5f);
   const float* base = qkv + (int64_t)b * S * H3;
   const float scale = 0.125f;  // 1/sqrt(64): exact power of two
 
@@ -97,6 +109,14 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const float* __restrict__ qkv,
     if (tid < 64) Ms[tid] = kt + tid < S ? maskb[(int64_t)b * S + kt + tid] : -INFINITY;
     __syncthreads();
 
+    // dropout decisions first: the Philox chain (dependent integer multiplies) has no
+    // input from this tile's math, so issuing it here lets it overlap the MFMAs below
+    uint32_t kb[4] = {0u, 0u, 0u, 0u};
+    if (kDrop) {
+      const uint64_t cbase = (((uint64_t)(bh * S + q) * (uint64_t)(Sp >> 6) + (kt >> 6)) * 2 + h) * 4;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) kb[j] = hx::keep8(seed, stream, cbase + j, t16);
+    }
     // ---- S^T = K . Q^T for two 32-key sub-blocks; keys in registers, queries on lanes
     f32x16 s0 = {0}, s1 = {0};
 #pragma unroll
@@ -139,28 +159,29 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const float* __restrict__ qkv,
       o1[r] *= alpha;
     }
     if (kDrop) {
-      // keys of register group g (r = 4g..4g+3): sub-block kb, 8g + 4h + (0..3)
-      const int64_t rowbase = (bh * S + q) * Sp + kt;
-      uint32_t bits0 = 0, bits1 = 0;
+      // 32 decisions per lane per tile from 4 Philox calls (8 x 16-bit each); counter
+      // = (query, tile, lane half, call) -- any bijection works, backward reads bits
+      // transposed bitmask [key][query word]: ballots over the 32 queries of each
+      // lane half give, per register r, the words of keys crow(r,0) and crow(r,1);
+      // lane L collects the word of key kt + L and stores it (64 keys, one store)
+      uint32_t myword = 0;
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const uint32_t k0 = hx::keep4(seed, stream, (uint64_t)(rowbase + 8 * g + 4 * h) >> 2, keep);
-        const uint32_t k1 = hx::keep4(seed, stream, (uint64_t)(rowbase + 32 + 8 * g + 4 * h) >> 2, keep);
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          s0[4 * g + j] = ((k0 >> j) & 1) ? s0[4 * g + j] * inv_keep : 0.f;
-          s1[4 * g + j] = ((k1 >> j) & 1) ? s1[4 * g + j] * inv_keep : 0.f;
-        }
-        bits0 |= k0 << (8 * g + 4 * h);
-        bits1 |= k1 << (8 * g + 4 * h);
+      for (int r = 0; r < 16; ++r) {
+        const bool k0 = (kb[r >> 3] >> (r & 7)) & 1, k1 = (kb[2 + (r >> 3)] >> (r & 7)) & 1;
+        s0[r] = k0 ? s0[r] * inv_keep : 0.f;
+        s1[r] = k1 ? s1[r] * inv_keep : 0.f;
+        const uint64_t b0 = __ballot(k0), b1 = __ballot(k1);
+        const int L0 = crow(r, 0);
+        myword = write_lane(myword, (uint32_t)b0, L0);
+        myword = write_lane(myword, (uint32_t)(b0 >> 32), L0 + 4);
+        myword = write_lane(myword, (uint32_t)b1, 32 + L0);
+        myword = write_lane(myword, (uint32_t)(b1 >> 32), 36 + L0);
+        if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // keep ballots from piling up in SGPRs
       }
-      bits0 |= __shfl_xor(bits0, 32, 64);
-      bits1 |= __shfl_xor(bits1, 32, 64);
-      if (h == 0 && q < S) {
-        uint32_t* dm = dmask + (bh * S + q) * (Sp >> 5) + (kt >> 5);
-        dm[0] = bits0;
-        dm[1] = bits1;
-      }
+      if (Sp <= kMaxStagedTiles * 64)
+        Wst[(kt >> 6) * 256 + w * 64 + lane] = myword;
+      else
+        dmask[((int64_t)bh * Sp + kt + lane) * (Sp >> 5) + (q0w >> 5)] = myword;
     }
     // ---- O^T += V^T . P^T   (A = V^T from LDS, B = P accumulator register)
 #pragma unroll
@@ -176,6 +197,12 @@ __global__ __launch_bounds__(256) void attn_fwd_k(const float* __restrict__ qkv,
     __syncthreads();
   }
   // ---- epilogue: O = O^T^T / l ; lane owns query q, registers hold 4-contiguous dims
+  if (kDrop && Sp <= kMaxStagedTiles * 64) {
+    // (each wave reads back only its own words: no barrier needed)
+    const int nt = (S + 63) >> 6;
+    for (int t = 0; t < nt; ++t)
+      dmask[((int64_t)bh * Sp + t * 64 + lane) * (Sp >> 5) + (q0w >> 5)] = Wst[t * 256 + w * 64 + lane];
+  }
   if (q >= S) return;
   const float inv_l = 1.f / l_run;
   float* op = out + ((int64_t)b * S + q) * H + hd * D;
@@ -221,7 +248,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   float* dSs = dOs + 32 * LDK;           // [32][LDSS]
   float* Ls = dSs + 32 * LDSS;           // [32] lse
   float* Ds = Ls + 32;                   // [32] D
-  uint32_t* Wm = reinterpret_cast<uint32_t*>(Ds + 32);   // [32 q][4 words] dropout bits of this key block
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int b = blockIdx.z, hd = blockIdx.y;
@@ -231,7 +257,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float* base = qkv + (int64_t)b * S * H3;
   const int64_t bh = (int64_t)b * nh + hd;
   const float scale = 0.125f, inv_keep = 1.f / keep;
-  const int nwords = ((S + 127) & ~127) >> 5;   // mask words per query row (fwd pitch)
+  const int Sp = (S + 127) & ~127;
+  const int nwords = Sp >> 5;                   // query words per key row of the bitmask
 
   // ---- K of this block's 128 keys -> LDS; V of this lane's key / dim-half -> registers
   // (keys past S: clamped loads, -inf mask -> P = 0, never stored)
@@ -259,6 +286,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
   // staging map of a 32x64 tile: thread -> rows (tid>>4) and 16 + (tid>>4), float4 column c4
   const int srow = tid >> 4, sc4 = (tid & 15) * 4;
+  // dropout bits of (this lane's key, the 32 queries of a tile): ONE word
+  const uint32_t* mrow = kDrop ? dmask + ((int64_t)bh * Sp + mykey) * nwords : nullptr;
   auto ld_tile = [&](int qt, float4 (&qn)[2], float4 (&dn)[2], float4 (&on)[2], float& xn, uint32_t& mn) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -269,10 +298,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       on[i] = *reinterpret_cast<const float4*>(outp + r * H + hd * D + sc4);
     }
     if (tid < 32) xn = qt + tid < S ? lse[bh * S + qt + tid] : INFINITY;   // rows past S: P = 0
-    if (kDrop && tid >= 64 && tid < 64 + 128) {
-      const int i = tid - 64, row = i >> 2, wd = i & 3;
-      mn = qt + row < S ? dmask[(bh * S + qt + row) * nwords + (kbase >> 5) + wd] : 0u;
-    }
+    if (kDrop) mn = mrow[qt >> 5];
   };
   float4 qn[2], dn[2], on[2];
   float xn = 0.f;
@@ -301,7 +327,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       if ((tid & 15) == 0) Ds[srow + 16 * i] = d;
     }
     if (tid < 32) Ls[tid] = xn;
-    if (kDrop && tid >= 64 && tid < 64 + 128) Wm[tid - 64] = mn;
+    const uint32_t mword = mn;
     if (qt + 32 < S) ld_tile(qt + 32, qn, dn, on, xn, mn);   // in flight during this tile's math
     __syncthreads();
 
@@ -328,7 +354,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       const int qr_ = crow(r, h);
       const float p = __expf(sa[r] + mk - Ls[qr_]);
       float keepf = 1.f;
-      if (kDrop) keepf = ((Wm[qr_ * 4 + w] >> l32) & 1) ? inv_keep : 0.f;
+      if (kDrop) keepf = ((mword >> qr_) & 1) ? inv_keep : 0.f;
       sa[r] = p * keepf;
       dp[r] = p * (dp[r] * keepf - Ds[qr_]);
       dSs[qr_ * LDSS + w * 32 + l32] = dp[r];
@@ -389,7 +415,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 }  // namespace
 
 size_t hx_attn_bwd_smem_bytes() {
-  return sizeof(float) * (128 * LDK + 2 * 32 * LDK + 32 * LDSS + 64 + 128);
+  return sizeof(float) * (128 * LDK + 2 * 32 * LDK + 32 * LDSS + 64);
 }
 
 void hx_attn_fwd(const float* qkv, const float* maskb, float* out, float* lse, uint32_t* dmask, int B, int S, int nh,

@@ -48,7 +48,11 @@ def bench_attn(B, S, nh=12, keep=0.9):
     dout = torch.randn_like(out)
     f_fwd = 2 * 2 * B * nh * S * S * d
     report('attn_fwd', timeit(lambda: C().attn_fwd(qkv, mb, nh, keep, 1, 0)), flops=f_fwd)
+    report('attn_fwd (no dropout)', timeit(lambda: C().attn_fwd(qkv, mb, nh, 1.0, 1, 0)), flops=f_fwd)
     report('attn_bwd', timeit(lambda: C().attn_bwd(dout, qkv, mb, out, lse, dm, nh, keep)), flops=2.5 * f_fwd)
+    out1, lse1, dm1 = C().attn_fwd(qkv, mb, nh, 1.0, 1, 0)
+    report('attn_bwd (no dropout)', timeit(lambda: C().attn_bwd(dout, qkv, mb, out1, lse1, dm1, nh, 1.0)),
+           flops=2.5 * f_fwd)
 
 
 def bench_ln(B, S, H=768):

@@ -182,10 +182,12 @@ def main():
         tot = time.perf_counter() - t1
         torch.cuda.set_sync_debug_mode(0)
         ph = ctrl.phase_report()
-        ph['data_next'] = data_t
-        print('phases (host ms/step): ' + ', '.join('{}={:.2f}'.format(k, v * 1e3 / n) for k, v in ph.items()) +
-              ' | host loop {:.2f} ms/step, device-complete {:.2f} ms/step'.format(host_t * 1e3 / n, tot * 1e3 / n),
-              file=sys.stderr, flush=True)
+        ph['host']['data_next'] = data_t
+        fmt = lambda d: ', '.join('{}={:.2f}'.format(k, v * 1e3 / n) for k, v in d.items())
+        print('phases host ms/step: ' + fmt(ph['host']) + ' | host loop {:.2f} ms/step, device-complete {:.2f} '
+              'ms/step'.format(host_t * 1e3 / n, tot * 1e3 / n), file=sys.stderr, flush=True)
+        if ph['device']:
+            print('phases device ms/step: ' + fmt(ph['device']), file=sys.stderr, flush=True)
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()

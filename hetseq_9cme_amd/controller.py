@@ -41,6 +41,7 @@ from .parallel import distributed as dist_utils
 from .parallel.flat_params import FlatParamSpace
 from .parallel.reducer import GradReducer
 from .utils.meters import AverageMeter, StopwatchMeter, TimeMeter
+from .utils.phase_timer import PhaseTimer
 from .utils.misc import move_to_device
 
 LN2 = math.log(2)
@@ -81,7 +82,7 @@ class Controller(object):
         self.fast_stat_sync = args.fast_stat_sync
         self._save_thread = None
         self._profile_phases = bool(getattr(args, 'profile_phases', False))
-        self.phase_times, self._phase_t0 = {}, 0.0
+        self.phases = PhaseTimer(self._profile_phases, cuda=self.cuda)
         self.init_meters(args)
 
     # ------------------------------------------------------------------ meters
@@ -119,6 +120,7 @@ class Controller(object):
 
     def _build_optimizer(self):
         self._optimizer = build_optimizer(self.args, self.flat)
+        self._optimizer.phase_hook = self.phases.begin if self._profile_phases else None
         self._lr_scheduler = build_lr_scheduler(self.args, self._optimizer)
         self._lr_scheduler.step_update(0)
 
@@ -208,13 +210,12 @@ class Controller(object):
 
     def train_step(self, samples, dummy_batch=False, raise_oom=False):
         """Forward, backward and parameter update for one group of micro-batches."""
-        tick = self._phase_tick
-        tick(None)
+        ph = self.phases.begin
+        ph('prep')
         self._set_seed()
         model = self.model
         model.train()
         self.zero_grad()
-        tick('prep')
         if not dummy_batch:
             self.meters['train_wall'].start()
 
@@ -225,8 +226,8 @@ class Controller(object):
         acc_loss, acc_nll = None, None
         sample_size, logging_output = 0, {}
         for i, sample in enumerate(samples):
+            ph('sample')
             sample = self._prepare_sample(sample)
-            tick('sample')
             if sample is None:
                 if self._dummy_batch is None:
                     raise RuntimeError('first batch of the run is empty: no dummy batch available')
@@ -239,12 +240,13 @@ class Controller(object):
             try:
                 with self._maybe_no_sync(i, len(samples)):
                     self.reducer.prepare_for_backward()
+                    ph('forward')     # optimizer.backward() opens 'backward'
                     loss, sample_size, logging_output = self.task.train_step(sample, model, self.optimizer,
                                                                              ignore_grad)
                     for k, u in enumerate(self.reducer.used):
                         if u:
                             step_used[k] = True
-                tick('fwd_bwd')
+                ph('stats')
                 if not ignore_grad:
                     logging_outputs.append(logging_output)
                     sample_sizes.append(sample_size)
@@ -293,7 +295,7 @@ class Controller(object):
             raise Exception('Please update the {}.aggregate_logging_outputs() method to return ntokens and '
                             'nsentences'.format(self.task.__class__.__name__))
 
-        tick('stats')
+        ph('optimizer')
         opt = self.optimizer
         # DDP averages gradients over ranks; the reducer SUMs, so its 1/W is folded here
         pre = self.reducer.grad_prescale if self.reducer.enabled else 1.0
@@ -310,7 +312,7 @@ class Controller(object):
             self._prev_grad_norm = grad_norm
             opt.used_mask = step_used
             opt.step()
-            tick('optimizer')
+            ph('meters')
             self.set_num_updates(self.get_num_updates() + 1)
             self.task.update_step(self._num_updates)
 
@@ -331,31 +333,20 @@ class Controller(object):
             logging_output = None
 
         self.meters['train_wall'].stop()
-        tick('meters')
+        self.phases.end_step()
         if logging_output is not None and 'sample_size' not in logging_output:
             logging_output['sample_size'] = sample_size
         return logging_output
 
     # ------------------------------------------------------------------ phase timing
-    def _phase_tick(self, name):
-        """``--profile-phases``: host wall time spent in each phase of the step.
-
-        Host time (not device time) is what is measured: with no host syncs in
-        the step the CPU runs ahead of the GPU and every phase is short; a phase
-        that blocks on the device shows up as the GPU time it waited for.
-        """
-        if not self._profile_phases:
-            return
-        now = time.perf_counter()
-        if name is not None:
-            self.phase_times[name] = self.phase_times.get(name, 0.0) + now - self._phase_t0
-        self._phase_t0 = now
+    @property
+    def phase_times(self):
+        """Host seconds per phase accumulated so far (``--profile-phases``)."""
+        return self.phases.host
 
     def phase_report(self, reset=True):
-        out = dict(self.phase_times)
-        if reset:
-            self.phase_times = {}
-        return out
+        """{'host': {...}, 'device': {...}, 'steps': n} -- see utils/phase_timer.py."""
+        return self.phases.report(reset)
 
     # ------------------------------------------------------------------ misc API
     def zero_grad(self):

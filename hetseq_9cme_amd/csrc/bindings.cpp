@@ -34,6 +34,24 @@ inline T* ptr_or_null(const OptT& t) {
 inline bool has(const OptT& t) { return t.has_value() && t->defined(); }
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
+// ------------------------------------------------------------------ debug mode
+// ``--debug-kernels``: host-side validation that needs device reads
+// (range checks on indices, finite checks on every fused op's output).  Each check
+// synchronises, so it is off by default; combined with AMD_SERIALIZE_KERNEL=3 the
+// first kernel producing a bad value is the one that raises.
+bool g_debug = false;
+void set_debug(bool on) { g_debug = on; }
+bool get_debug() { return g_debug; }
+inline void dbg_range(const Tensor& t, int64_t lo, int64_t hi, const char* what) {
+  if (!g_debug || t.numel() == 0) return;
+  const int64_t mn = t.min().item<int64_t>(), mx = t.max().item<int64_t>();
+  TORCH_CHECK(mn >= lo && mx < hi, what, " out of range: [", mn, ", ", mx, "] not within [", lo, ", ", hi, ")");
+}
+inline void dbg_finite(const Tensor& t, const char* what) {
+  if (!g_debug || !t.defined() || t.numel() == 0) return;
+  TORCH_CHECK(torch::isfinite(t).all().item<bool>(), "non-finite values produced by ", what);
+}
+
 // ------------------------------------------------------------------ optimizer
 void grad_norm_clip(Tensor g, Tensor gscale, Tensor out_norm, Tensor clipped, double max_norm) {
   check_f32(g, "grad");
@@ -123,11 +141,14 @@ std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tens
             rows, H, (float)keep_prob, (uint64_t)seed, (uint64_t)stream, drop_after ? 1 : 0,
             (want_dy && want_dbias) ? 1 : 0, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
             want_dbias ? dbias.data_ptr<float>() : nullptr, 0, cur_stream(z));
+  dbg_finite(dz, "ln_bwd (dz)");
   return {dz, dy, dgamma, dbeta, dbias};
 }
 
 std::vector<Tensor> embed_ln_fwd(Tensor ids, OptT tt, Tensor wte, Tensor wpe, Tensor wtt, Tensor gamma, Tensor beta,
                                  double eps, double keep_prob, int64_t seed, int64_t stream, bool bf16_out) {
+  dbg_range(ids, 0, wte.size(0), "token ids");
+  if (has(tt)) dbg_range(*tt, 0, wtt.size(0), "token type ids");
   check_cuda(ids, "input_ids");
   TORCH_CHECK(ids.scalar_type() == torch::kInt64 && ids.dim() == 2, "input_ids must be int64 [B, S]");
   check_f32(wte, "word_embeddings");
@@ -147,6 +168,7 @@ std::vector<Tensor> embed_ln_fwd(Tensor ids, OptT tt, Tensor wte, Tensor wpe, Te
                   wte.data_ptr<float>(), wpe.data_ptr<float>(), wtt.data_ptr<float>(), gamma.data_ptr<float>(),
                   beta.data_ptr<float>(), out.data_ptr(), z.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                   B * S, (int)S, H, (float)eps, (float)keep_prob, (uint64_t)seed, (uint64_t)stream, cur_stream(ids));
+  dbg_finite(out, "embed_ln_fwd");
   return {out, z, mean, rstd};
 }
 
@@ -197,6 +219,7 @@ std::vector<Tensor> bias_act_bwd(Tensor dout, OptT y, OptT b, OptT saved_out, in
                   has(saved_out) ? saved_out->data_ptr() : nullptr, dy.data_ptr(),
                   want_dbias ? ws.data_ptr<float>() : nullptr, want_dbias ? dbias.data_ptr<float>() : nullptr, rows, N,
                   0, cur_stream(dout));
+  dbg_finite(dy, "bias_act_bwd");
   return {dy, dbias};
 }
 
@@ -224,6 +247,7 @@ Tensor dropout(Tensor x, double keep_prob, int64_t seed, int64_t stream) {
 }
 
 Tensor softmax_xent_(Tensor logits, OptT bias, Tensor labels, int64_t ignore_index) {
+  dbg_range(labels, std::min<int64_t>(ignore_index, 0), logits.size(-1), "MLM labels");
   TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "logits must be a 2-D row-major GPU tensor");
   check_cuda(labels, "labels");
   TORCH_CHECK(labels.scalar_type() == torch::kInt64 && labels.numel() == logits.size(0), "labels must be int64 [rows]");
@@ -236,6 +260,7 @@ Tensor softmax_xent_(Tensor logits, OptT bias, Tensor labels, int64_t ignore_ind
   hx_softmax_xent(act_bf16(logits), logits.data_ptr(), ptr_or_null<float>(bias), labels.data_ptr<int64_t>(),
                   loss.data_ptr<float>(), logits.size(0), (int)logits.size(1), logits.stride(0), ignore_index,
                   cur_stream(logits));
+  dbg_finite(loss, "softmax_xent");
   return loss;
 }
 
@@ -258,6 +283,7 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
   hx_attn_fwd(qkv.data_ptr<float>(), mask_bias.data_ptr<float>(), out.data_ptr<float>(), lse.data_ptr<float>(),
               keep < 1.0 ? reinterpret_cast<uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr, (int)B, (int)S, (int)nh,
               (float)keep, (uint64_t)seed, (uint64_t)stream, cur_stream(qkv));
+  dbg_finite(out, "attn_fwd");
   return {out, lse, dmask};
 }
 
@@ -272,6 +298,7 @@ Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor ls
   hx_attn_bwd(qkv.data_ptr<float>(), mask_bias.data_ptr<float>(), dout.data_ptr<float>(), out.data_ptr<float>(),
               lse.data_ptr<float>(), keep < 1.0 ? reinterpret_cast<const uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr,
               dqkv.data_ptr<float>(), (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv));
+  dbg_finite(dqkv, "attn_bwd");
   return dqkv;
 }
 
@@ -293,4 +320,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_xent_", &softmax_xent_);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
+  m.def("set_debug", &set_debug);
+  m.def("get_debug", &get_debug);
 }

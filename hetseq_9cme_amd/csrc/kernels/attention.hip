@@ -40,9 +40,11 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int D = 64;      // head dim (BERT-base/large)
 constexpr int LDK = 68;    // padded LDS row stride (floats)
 
-// v_writelane_b32: put a wave-uniform value into one lane of a VGPR (1 instruction)
-__device__ __forceinline__ uint32_t write_lane(uint32_t v, uint32_t val, int lane) {
-  asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(val), "s"(lane));
+// v_writelane_b32 with a compile-time lane (inline constant: only the value uses
+// the constant bus): put a wave-uniform value into one lane of a VGPR
+template <int L>
+__device__ __forceinline__ uint32_t write_lane(uint32_t v, uint32_t val) {
+  asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(val), "i"(L));
   return v;
 }
 
@@ -51,6 +53,28 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
 }
 // accumulator register r of a 32x32 tile, lane half h -> row index
 __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+// Forward dropout for accumulator register R of both 32-key sub-blocks: apply the
+// lane's decisions, and build the transposed bitmask word: a ballot over the wave
+// gives, for register R, the 32-query words of keys crow(R,0) (lanes 0-31) and
+// crow(R,1) (lanes 32-63); lane L collects the word of key kt + L.
+template <int R>
+__device__ __forceinline__ void drop_step(f32x16& s0, f32x16& s1, const uint32_t (&kb)[4], float inv_keep,
+                                          uint32_t& myword) {
+  if constexpr (R < 16) {
+    const bool k0 = (kb[R >> 3] >> (R & 7)) & 1, k1 = (kb[2 + (R >> 3)] >> (R & 7)) & 1;
+    s0[R] = k0 ? s0[R] * inv_keep : 0.f;
+    s1[R] = k1 ? s1[R] * inv_keep : 0.f;
+    const uint64_t b0 = __ballot(k0), b1 = __ballot(k1);
+    constexpr int L0 = (R & 3) + 8 * (R >> 2);
+    myword = write_lane<L0>(myword, (uint32_t)b0);
+    myword = write_lane<L0 + 4>(myword, (uint32_t)(b0 >> 32));
+    myword = write_lane<32 + L0>(myword, (uint32_t)b1);
+    myword = write_lane<36 + L0>(myword, (uint32_t)(b1 >> 32));
+    if constexpr ((R & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // keep ballots from piling up in SGPRs
+    drop_step<R + 1>(s0, s1, kb, inv_keep, myword);
+  }
+}
 
 // ============================================================================ forward
 // grid (S/128, nh, B), block 256 = 4 waves x 32 queries.
@@ -159,25 +183,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       o1[r] *= alpha;
     }
     if (kDrop) {
-      // 32 decisions per lane per tile from 4 Philox calls (8 x 16-bit each); counter
-      // = (query, tile, lane half, call) -- any bijection works, backward reads bits
-      // transposed bitmask [key][query word]: ballots over the 32 queries of each
-      // lane half give, per register r, the words of keys crow(r,0) and crow(r,1);
-      // lane L collects the word of key kt + L and stores it (64 keys, one store)
+      // decisions kb[] were drawn before the MFMAs (4 Philox calls x 8 16-bit
+      // decisions; counter = (query, tile, lane half, call) -- any bijection works,
+      // backward reads the stored bits); transposed bitmask [key][query word]
       uint32_t myword = 0;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const bool k0 = (kb[r >> 3] >> (r & 7)) & 1, k1 = (kb[2 + (r >> 3)] >> (r & 7)) & 1;
-        s0[r] = k0 ? s0[r] * inv_keep : 0.f;
-        s1[r] = k1 ? s1[r] * inv_keep : 0.f;
-        const uint64_t b0 = __ballot(k0), b1 = __ballot(k1);
-        const int L0 = crow(r, 0);
-        myword = write_lane(myword, (uint32_t)b0, L0);
-        myword = write_lane(myword, (uint32_t)(b0 >> 32), L0 + 4);
-        myword = write_lane(myword, (uint32_t)b1, 32 + L0);
-        myword = write_lane(myword, (uint32_t)(b1 >> 32), 36 + L0);
-        if ((r & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // keep ballots from piling up in SGPRs
-      }
+      drop_step<0>(s0, s1, kb, inv_keep, myword);
       if (Sp <= kMaxStagedTiles * 64)
         Wst[(kt >> 6) * 256 + w * 64 + lane] = myword;
       else
@@ -284,26 +294,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float mk = mykey < S ? maskb[(int64_t)b * S + mykey] : -INFINITY;
   const float* Kw = Ks + (w * 32) * LDK;      // this wave's keys
 
+  float* dqkv_b = dqkv + (int64_t)b * S * H3 + hd * D;
   // staging map of a 32x64 tile: thread -> rows (tid>>4) and 16 + (tid>>4), float4 column c4
   const int srow = tid >> 4, sc4 = (tid & 15) * 4;
+  // Per-(b, head) bases are wave-uniform (SGPRs); per-lane offsets within one
+  // sequence fit 32 bits.  Keeping the per-lane addresses 32-bit keeps this kernel
+  // under 256 VGPRs without spills -- a spilled address is reloaded from scratch,
+  // and scratch loads count in vmcnt: the reload's wait would drain the prefetch.
+  const float* dout_b = dout + (int64_t)b * S * H + hd * D;
+  const float* out_b = outp + (int64_t)b * S * H + hd * D;
+  const float* qkv_bh = base + hd * D;
+  const float* lse_bh = lse + bh * S;
   // dropout bits of (this lane's key, the 32 queries of a tile): ONE word
-  const uint32_t* mrow = kDrop ? dmask + ((int64_t)bh * Sp + mykey) * nwords : nullptr;
-  auto ld_tile = [&](int qt, float4 (&qn)[2], float4 (&dn)[2], float4 (&on)[2], float& xn, uint32_t& mn) {
+  const uint32_t* dmask_bh = kDrop ? dmask + (int64_t)bh * Sp * nwords : nullptr;
+  const int moff = mykey * nwords;
+  auto ld_tile = [&](int qt, float4 (&qn)[2], float4 (&dn)[2], float& xn, uint32_t& mn) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int qr = qt + srow + 16 * i;
-      const int64_t r = (int64_t)b * S + (qr < S ? qr : S - 1);
-      qn[i] = *reinterpret_cast<const float4*>(qkv + r * H3 + hd * D + sc4);
-      dn[i] = *reinterpret_cast<const float4*>(dout + r * H + hd * D + sc4);
-      on[i] = *reinterpret_cast<const float4*>(outp + r * H + hd * D + sc4);
+      const int r = qr < S ? qr : S - 1;
+      qn[i] = *reinterpret_cast<const float4*>(qkv_bh + r * H3 + sc4);
+      dn[i] = *reinterpret_cast<const float4*>(dout_b + r * H + sc4);
     }
-    if (tid < 32) xn = qt + tid < S ? lse[bh * S + qt + tid] : INFINITY;   // rows past S: P = 0
-    if (kDrop) mn = mrow[qt >> 5];
+    // unconditional (clamped) loads: a branch around a load makes the compiler's
+    // vmcnt tracking fall back to vmcnt(0), which would wait out the whole prefetch
+    const int lq = qt + (tid & 31);
+    xn = lse_bh[lq < S ? lq : S - 1];
+    if (kDrop) mn = dmask_bh[moff + (qt >> 5)];
   };
-  float4 qn[2], dn[2], on[2];
+  float4 qn[2], dn[2];
   float xn = 0.f;
   uint32_t mn = 0;
-  ld_tile(0, qn, dn, on, xn, mn);
+  ld_tile(0, qn, dn, xn, mn);
 
   // dQ tiles of this wave (16x16x4 layout): queries qh*16.., dims 16*dqa.. and 16*(dqa+1)..
   const int qh = w & 1, dqa = 2 * (w >> 1);
@@ -313,6 +335,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
   for (int qt = 0; qt < S; qt += 32) {
     __syncthreads();  // previous tile's LDS buffers are free
+    float4 on[2];   // O rows for D = rowsum(dO * O): loaded here (not prefetched) to stay in 256 VGPRs
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int qr = qt + srow + 16 * i;
+      on[i] = *reinterpret_cast<const float4*>(out_b + (qr < S ? qr : S - 1) * H + sc4);
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       float4 qv = qn[i];
@@ -326,9 +354,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       d += __shfl_xor(d, 8, 64);
       if ((tid & 15) == 0) Ds[srow + 16 * i] = d;
     }
-    if (tid < 32) Ls[tid] = xn;
+    if (tid < 32) Ls[tid] = qt + tid < S ? xn : INFINITY;   // rows past S: P = 0
     const uint32_t mword = mn;
-    if (qt + 32 < S) ld_tile(qt + 32, qn, dn, on, xn, mn);   // in flight during this tile's math
+    if (qt + 32 < S) ld_tile(qt + 32, qn, dn, xn, mn);   // in flight during this tile's math
     __syncthreads();
 
     // ---- S = Qs . K^T (queries rows, keys on lanes); dP = dO . V^T
@@ -385,16 +413,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
     const int q0 = qt + qh * 16 + 4 * k4;
-    float* dq = dqkv + ((int64_t)b * S + q0) * H3 + hd * D + dqa * 16 + r16;
+    float* dq = dqkv_b + q0 * H3 + dqa * 16 + r16;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       if (q0 + r >= S) continue;
       if (single) {
-        dq[(int64_t)r * H3] = qa0[r] * scale;
-        dq[(int64_t)r * H3 + 16] = qa1[r] * scale;
+        dq[r * H3] = qa0[r] * scale;
+        dq[r * H3 + 16] = qa1[r] * scale;
       } else {
-        atomicAdd(dq + (int64_t)r * H3, qa0[r] * scale);
-        atomicAdd(dq + (int64_t)r * H3 + 16, qa1[r] * scale);
+        atomicAdd(dq + r * H3, qa0[r] * scale);
+        atomicAdd(dq + r * H3 + 16, qa1[r] * scale);
       }
     }
   }

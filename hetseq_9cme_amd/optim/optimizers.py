@@ -60,7 +60,11 @@ class _Optimizer(object):
         return list(self.flat.params)
 
     # --- grads --------------------------------------------------------
+    phase_hook = None   # set by the controller under --profile-phases
+
     def backward(self, loss):
+        if self.phase_hook is not None:
+            self.phase_hook('backward')
         loss.backward()
 
     def zero_grad(self):

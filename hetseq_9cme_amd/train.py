@@ -147,10 +147,14 @@ def get_training_stats(controller):
         stats['loss_scale'] = controller.get_meter('loss_scale')
     stats['wall'] = round(controller.get_meter('wall').elapsed_time)
     stats['train_wall'] = controller.get_meter('train_wall')
-    if getattr(controller, '_profile_phases', False) and controller.get_num_updates() > 0:
-        # cumulative host ms per update spent in each phase of the step
-        for k, v in controller.phase_times.items():
-            stats['t_' + k] = round(v * 1e3 / controller.get_num_updates(), 2)
+    if getattr(controller, '_profile_phases', False) and controller.phases.steps > 0:
+        # per-update ms in each phase of the step since the last log line:
+        # t_* host wall time, d_* device (HIP event) time
+        rep = controller.phase_report(reset=True)
+        for k, v in rep['host'].items():
+            stats['t_' + k] = round(v * 1e3 / rep['steps'], 2)
+        for k, v in rep['device'].items():
+            stats['d_' + k] = round(v * 1e3 / rep['steps'], 2)
     return stats
 
 

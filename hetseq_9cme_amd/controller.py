@@ -57,6 +57,8 @@ class Controller(object):
             ops.set_fused(False)      # A/B mode: plain torch ops on the GPU
         if getattr(args, 'overlap_wgrad', False):
             ops.set_side_stream(True)
+        if getattr(args, 'debug_kernels', False) and self.cuda:
+            ops.C().set_debug(True)   # validation inside the bindings (see csrc/bindings.cpp)
         if self.cuda:
             gemm_tuning.configure(getattr(args, 'gemm_tuning', 'table'), getattr(args, 'gemm_tuning_file', None))
         model = model.to(self.device)

@@ -115,6 +115,7 @@ std::vector<Tensor> ln_fwd(Tensor y, OptT bias, OptT res, Tensor gamma, Tensor b
             gamma.data_ptr<float>(), beta.data_ptr<float>(), out.data_ptr(), save_z ? z.data_ptr() : nullptr,
             mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, H, (float)eps, (float)keep_prob, (uint64_t)seed,
             (uint64_t)stream, drop_after ? 1 : 0, cur_stream(y));
+  dbg_finite(out, "ln_fwd");
   return {out, z, mean, rstd};
 }
 
@@ -198,6 +199,7 @@ Tensor bias_act_fwd(Tensor y, OptT b, int64_t act) {
   auto out = torch::empty_like(y);
   hx_bias_act_fwd(act_bf16(y), (int)act, y.data_ptr(), ptr_or_null<float>(b), out.data_ptr(), y.numel() / N, N,
                   cur_stream(y));
+  dbg_finite(out, "bias_act_fwd");
   return out;
 }
 

@@ -65,6 +65,10 @@ def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialD
     parser.add_argument('--overlap-wgrad', action='store_true',
                         help='run weight-gradient GEMMs / bias column sums on a side HIP stream, overlapping '
                              'the dgrad chain (off by default: slower for BERT-base on one MI355X)')
+    parser.add_argument('--debug-kernels', action='store_true',
+                        help='debug mode: serialised kernel launches (AMD_SERIALIZE_KERNEL=3, '
+                             'HIP_LAUNCH_BLOCKING=1), range checks on token/type ids and labels and finite '
+                             'checks on every fused kernel output (host syncs: slow)')
     parser.add_argument('--profile-phases', action='store_true',
                         help='log host wall time per step phase (prep/sample/fwd_bwd/stats/optimizer/'
                              'meters); a phase that waits on the GPU shows up as long')

@@ -191,6 +191,11 @@ def _from_torchrun(args):
 
 def cli_main(argv=None):
     args = options.parse_training_args(argv)
+    if getattr(args, 'debug_kernels', False):
+        # must be in the environment before the HIP runtime initialises (also
+        # inherited by spawned ranks)
+        os.environ['AMD_SERIALIZE_KERNEL'] = '3'
+        os.environ['HIP_LAUNCH_BLOCKING'] = '1'
     if _from_torchrun(args):
         main(args, init_distributed=True)
     elif args.distributed_init_method is not None:

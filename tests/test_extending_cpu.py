@@ -20,3 +20,16 @@ def test_user_module_task_optimizer_scheduler(tmp_path):
     assert ck['last_optimizer_state']['param_groups'][0]['momentum'] == 0.9
     assert ck['optimizer_history'][-1]['optimizer_name'] == 'SGDMomentum'
     assert ck['args'].lr_scheduler == 'constant' and ck['args'].toy_dim == 6
+
+
+def test_profile_phases_log(tmp_path):
+    """--profile-phases adds per-phase host times (t_*) to the log line."""
+    r = run_cli(['--user-module', os.path.join(ROOT, 'examples', 'toy_extension.py'), '--task', 'toy_regression',
+                 '--optimizer', 'sgd', '--lr-scheduler', 'constant', '--lr', '0.01', '--max-sentences', '32',
+                 '--max-update', '4', '--data', 'unused', '--num-workers', '1', '--save-dir', str(tmp_path / 'ck'),
+                 '--no-save', '--cpu', '--log-format', 'json', '--log-interval', '2', '--profile-phases'])
+    import json
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith('{')]
+    assert lines, r.stdout[-2000:]
+    for k in ('t_prep', 't_sample', 't_forward', 't_backward', 't_optimizer'):
+        assert k in lines[-1], (k, lines[-1])

@@ -298,3 +298,26 @@ def test_training_gpu_matches_cpu(dev, tmp_path):
     assert sorted(sg.keys()) == sorted(sc.keys())
     for i in sc:
         _close(sg[i]['exp_avg'], sc[i]['exp_avg'], rtol=1e-2, atol=1e-6)
+
+
+def test_debug_mode_validation(dev):
+    """--debug-kernels: index range checks run on the host BEFORE the launch (no
+    device fault), non-finite outputs are reported by the op that produced them."""
+    from hetseq_9cme_amd.ops._ext import C
+    H, V = 64, 100
+    wte = torch.randn(V, H, device=dev)
+    wpe = torch.randn(16, H, device=dev)
+    wtt = torch.randn(2, H, device=dev)
+    g, b = torch.ones(H, device=dev), torch.zeros(H, device=dev)
+    bad = torch.full((2, 16), V, dtype=torch.long, device=dev)   # one past the vocabulary
+    C().set_debug(True)
+    try:
+        with pytest.raises(RuntimeError, match='token ids out of range'):
+            C().embed_ln_fwd(bad, None, wte, wpe, wtt, g, b, 1e-12, 1.0, 0, 0, False)
+        y = torch.randn(8, H, device=dev)
+        y[3, 5] = float('nan')
+        with pytest.raises(RuntimeError, match='non-finite values produced by ln_fwd'):
+            C().ln_fwd(y, None, None, g, b, 1e-12, 1.0, 0, 0, False, False)
+    finally:
+        C().set_debug(False)
+    assert not C().get_debug()

@@ -33,8 +33,19 @@ def safe_load_checkpoint(path):
 
 
 def build_tokenizer(vocab_file):
+    """Uncased WordPiece tokenizer over a BERT ``vocab.txt``.
+
+    The vocabulary is passed positionally: transformers 5.x ignores the
+    ``vocab_file=`` keyword of ``BertTokenizerFast`` and silently builds a
+    5-token (special tokens only) vocabulary, which maps every word to [UNK].
+    """
     from transformers import BertTokenizerFast
-    return BertTokenizerFast(vocab_file=vocab_file, do_lower_case=True)
+    tok = BertTokenizerFast(vocab_file, do_lower_case=True)
+    with open(vocab_file, encoding='utf-8') as f:
+        n = sum(1 for line in f if line.strip())
+    if len(tok.vocab) < n:
+        raise RuntimeError('tokenizer loaded {} of the {} entries of {}'.format(len(tok.vocab), n, vocab_file))
+    return tok
 
 
 class BertForTokenClassificationTask(Task):

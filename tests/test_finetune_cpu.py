@@ -24,8 +24,9 @@ def test_conll_reader_and_alignment(tmp_path):
     vocab, cfg, tr, te = _setup(tmp_path)
     sents = read_conll(tr)
     assert len(sents) == 48 and all(len(s['tokens']) == len(s['ner_tags']) for s in sents)
-    from transformers import BertTokenizerFast
-    tok = BertTokenizerFast(vocab_file=vocab, do_lower_case=True)
+    from hetseq_9cme_amd.tasks.token_classification import build_tokenizer
+    tok = build_tokenizer(vocab)
+    assert tok.tokenize('John went to Paris') == ['john', 'went', 'to', 'paris']
     ex = [{'tokens': ['John', 'xyzzyplugh', 'Paris'], 'ner_tags': ['B-PER', 'O', 'B-LOC']}]
     f = tokenize_and_align(ex, tok, {'B-PER': 1, 'O': 0, 'B-LOC': 5})[0]
     # [CLS] john <pieces of unknown word...> paris [SEP]: first pieces labelled, rest -100
@@ -94,13 +95,14 @@ def test_ner_scores_match_seqeval_semantics():
 def test_ner_eval_cli_and_transformers_task(tmp_path):
     vocab, cfg, tr, te = _setup(tmp_path)
     save = str(tmp_path / 'ner')
-    run_cli(['--task', 'BertForTokenClassification', '--fast-stat-sync', '--max-update', '4',
-             '--valid-subset', 'test', '--num-workers', '1', '--lr', '1e-3', '--dict', vocab, '--config_file', cfg,
+    run_cli(['--task', 'BertForTokenClassification', '--fast-stat-sync', '--max-update', '24', '--lr', '2e-3',
+             '--valid-subset', 'test', '--num-workers', '1', '--dict', vocab, '--config_file', cfg,
              '--train_file', tr, '--test_file', te, '--extension_file', 'conll', '--max-sentences', '8',
              '--save-dir', save, '--cpu'])
     from hetseq_9cme_amd.eval_ner import evaluate
     res = evaluate(os.path.join(save, 'checkpoint_last.pt'), cfg, vocab, te, train_file=tr, device='cpu')
-    assert 0.0 <= res['f1'] <= 1.0 and res['accuracy'] > 0.0
+    # tags are a deterministic function of the word: a working pipeline learns them
+    assert res['f1'] > 0.9, res
     # HF-model variant of the task (reference transformers_tasks.py)
     import argparse as ap
     from hetseq_9cme_amd.tasks.transformers_tasks import TransformersBertForTokenClassificationTask

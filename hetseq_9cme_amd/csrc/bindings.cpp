@@ -175,6 +175,23 @@ std::vector<Tensor> embed_ln_fwd(Tensor ids, OptT tt, Tensor wte, Tensor wpe, Te
 
 // Scatter-ACCUMULATES the embedding gradients into dwte / dwpe / dwtt (caller zeroes them
 // when they are fresh).
+// word-embedding gradient, accumulated into dwte: rows visited in id-sorted order
+void embed_word_grad(Tensor dz, Tensor ids, Tensor order, Tensor dwte) {
+  check_cuda(dz, "grad");
+  check_cuda(ids, "ids");
+  check_cuda(order, "order");
+  check_f32(dwte, "dwte");
+  TORCH_CHECK(ids.scalar_type() == torch::kLong && order.scalar_type() == torch::kLong, "ids/order must be int64");
+  const int H = (int)dz.size(-1);
+  const int64_t rows = dz.numel() / H;
+  TORCH_CHECK(ids.numel() == rows && order.numel() == rows, "ids/order/grad row mismatch");
+  TORCH_CHECK(dwte.size(-1) == H && H % 4 == 0 && H <= 2048, "bad embedding width");
+  dbg_range(ids, 0, dwte.size(0), "token ids");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dz.device());
+  hx_embed_word_grad_sorted(act_bf16(dz), dz.data_ptr(), ids.data_ptr<int64_t>(), order.data_ptr<int64_t>(),
+                            dwte.data_ptr<float>(), rows, H, cur_stream(dz));
+}
+
 void embed_grads(Tensor dz, Tensor ids, OptT tt, Tensor dwte, Tensor dwpe, Tensor dwtt) {
   check_cuda(dz, "dz");
   check_f32(dwte, "dwte");
@@ -315,6 +332,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ln_bwd", &ln_bwd);
   m.def("embed_ln_fwd", &embed_ln_fwd);
   m.def("embed_grads", &embed_grads);
+  m.def("embed_word_grad", &embed_word_grad);
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);
   m.def("colsum", &colsum);

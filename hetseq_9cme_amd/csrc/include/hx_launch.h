@@ -27,6 +27,8 @@ void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const floa
                      const float* wtt, const float* gamma, const float* beta, void* out, void* zsave, float* mean,
                      float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, uint64_t seed,
                      uint64_t stream, hipStream_t s);
+void hx_embed_word_grad_sorted(int bf16, const void* dz, const int64_t* ids, const int64_t* order, float* dwte,
+                               int64_t rows, int H, hipStream_t s);
 void hx_embed_grads(int bf16, const void* dz, const int64_t* ids, const int64_t* tt, float* dwte, float* dwpe,
                     float* dwtt, int B, int S, int H, int ntypes, hipStream_t s);
 

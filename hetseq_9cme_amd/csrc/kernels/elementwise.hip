@@ -94,31 +94,36 @@ __global__ __launch_bounds__(NT) void bias_act_bwd_k(const T* __restrict__ dout,
   }
 }
 
-// scalar-column variant (any N, optional in-place scale by a device scalar)
+// scalar-column variant (any N); the optional device scalar scales the RESULT
+// (the input is only read: scaling it in place would double the HBM traffic)
 template <typename T>
-__global__ __launch_bounds__(NT) void colsum_scalar_k(T* __restrict__ x, const float* __restrict__ scale,
+__global__ __launch_bounds__(NT) void colsum_scalar_k(const T* __restrict__ x, const float* __restrict__ scale,
                                                     float* __restrict__ partial, int64_t rows, int N) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + lane;
   const int64_t r0 = (int64_t)blockIdx.y * hx::kRowChunk;
   const int64_t r1 = r0 + hx::kRowChunk < rows ? r0 + hx::kRowChunk : rows;
-  const float sc = scale ? scale[0] : 1.f;
   float acc = 0.f;
   if (j < N) {
-    for (int64_t r = r0 + w; r < r1; r += 4) {
-      float v = hx::io<T>::ld(x + r * N + j);
-      if (scale) {
-        v *= sc;
-        hx::io<T>::st(x + r * N + j, v);
-      }
-      acc += v;
+    // 4 independent rows per iteration keep 4 loads in flight per lane
+    float a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int64_t r = r0 + w;
+    for (; r + 12 < r1; r += 16) {
+      acc += hx::io<T>::ld(x + r * N + j);
+      a1 += hx::io<T>::ld(x + (r + 4) * N + j);
+      a2 += hx::io<T>::ld(x + (r + 8) * N + j);
+      a3 += hx::io<T>::ld(x + (r + 12) * N + j);
     }
+    for (; r < r1; r += 4) acc += hx::io<T>::ld(x + r * N + j);
+    acc = (acc + a1) + (a2 + a3);
   }
   red[w][lane] = acc;
   __syncthreads();
-  if (w == 0 && j < N)
-    partial[(int64_t)blockIdx.y * N + j] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  if (w == 0 && j < N) {
+    const float sc = scale ? scale[0] : 1.f;
+    partial[(int64_t)blockIdx.y * N + j] = ((red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane])) * sc;
+  }
 }
 
 template <typename T>
@@ -220,8 +225,8 @@ void hx_colsum(int bf16, void* x, const float* scale, float* partial, float* out
   const int ncb = (N + 63) / 64;
   const int nch = nchunks(rows);
   dim3 g(ncb, nch);
-  if (bf16) colsum_scalar_k<uint16_t><<<g, NT, 0, s>>>((uint16_t*)x, scale, partial, rows, N);
-  else colsum_scalar_k<float><<<g, NT, 0, s>>>((float*)x, scale, partial, rows, N);
+  if (bf16) colsum_scalar_k<uint16_t><<<g, NT, 0, s>>>((const uint16_t*)x, scale, partial, rows, N);
+  else colsum_scalar_k<float><<<g, NT, 0, s>>>((const float*)x, scale, partial, rows, N);
   hx::fold_rows(partial, nch, N, N, N, out, nullptr, nullptr, accumulate, s);
 }
 

@@ -321,6 +321,71 @@ __global__ __launch_bounds__(NT) void embed_word_grad_k(const T* __restrict__ dz
 
 // position + token-type gradients: block (s-tile) reduces over the batch dim.
 // dpos[s][j] = sum_b dz[b,s,j] ; dtype[t][j] += sum over rows with tt==t (atomics per block)
+// Word-embedding gradient from rows visited in id-sorted order (order = argsort(ids)).
+// Wave w owns sorted positions [w*kSegRows, (w+1)*kSegRows) (8 rows: 2048 waves at
+// B*S = 16384 keep every CU busy): it sums each run of
+// equal ids in registers and writes the run once.  A run that may continue into a
+// neighbouring wave's chunk (the chunk's first and last run) is added atomically;
+// every interior run's id occurs nowhere else, so a plain read-add-write is exact.
+// Frequent ids ([CLS], [SEP], [MASK], "the" in real text) thus cost a handful of
+// atomics per element instead of one per occurrence.
+constexpr int kSegRows = 8;
+template <typename T, int CH>
+__global__ __launch_bounds__(NT) void embed_word_grad_sorted_k(const T* __restrict__ dz,
+                                                             const int64_t* __restrict__ ids,
+                                                             const int64_t* __restrict__ order,
+                                                             float* __restrict__ dw, int64_t rows, int H) {
+  const int lane = threadIdx.x & 63;
+  const int64_t seg = blockIdx.x * (int64_t)WPB + (threadIdx.x >> 6);
+  const int64_t p0 = seg * kSegRows;
+  if (p0 >= rows) return;
+  const int64_t p1 = p0 + kSegRows < rows ? p0 + kSegRows : rows;
+  float4 acc[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) acc[c] = hx::f4(0.f);
+  // the chunk's (row, id) pairs: one per lane, loaded in parallel, then broadcast
+  const int cnt = (int)(p1 - p0);
+  const int64_t myr = lane < cnt ? order[p0 + lane] : 0;
+  const int64_t myid = lane < cnt ? ids[myr] : -1;
+  int64_t cur = __shfl(myid, 0, 64);
+  bool first_run = true;
+  auto flush = [&](int64_t id, bool atomic) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int j = (c * 64 + lane) * 4;
+      if (j < H) {
+        float* d = dw + id * H + j;
+        if (atomic) {
+          atomicAdd(d, acc[c].x); atomicAdd(d + 1, acc[c].y); atomicAdd(d + 2, acc[c].z); atomicAdd(d + 3, acc[c].w);
+        } else {
+          float4 o = *reinterpret_cast<float4*>(d);
+          o.x += acc[c].x; o.y += acc[c].y; o.z += acc[c].z; o.w += acc[c].w;
+          *reinterpret_cast<float4*>(d) = o;
+        }
+      }
+      acc[c] = hx::f4(0.f);
+    }
+  };
+  for (int k = 0; k < cnt; ++k) {
+    const int64_t r = __shfl(myr, k, 64);
+    const int64_t id = __shfl(myid, k, 64);
+    if (id != cur) {
+      flush(cur, first_run);
+      first_run = false;
+      cur = id;
+    }
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int j = (c * 64 + lane) * 4;
+      if (j < H) {
+        const float4 v = hx::load4(dz + r * H + j);
+        acc[c].x += v.x; acc[c].y += v.y; acc[c].z += v.z; acc[c].w += v.w;
+      }
+    }
+  }
+  flush(cur, true);   // the last run may continue in the next chunk
+}
+
 template <typename T>
 __global__ __launch_bounds__(NT) void embed_pos_type_grad_k(const T* __restrict__ dz, const int64_t* __restrict__ tt,
                                                           float* __restrict__ dpos, float* __restrict__ dtype,
@@ -440,6 +505,18 @@ void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const floa
       embed_ln_fwd_k<float, CH><<<grid, NT, 0, s>>>(ids, tt, wte, wpe, wtt, gamma, beta, (float*)out,
                                                     (float*)zsave, mean, rstd, rows, S, H, eps, keep_prob, seed,
                                                     stream);
+  })
+}
+
+void hx_embed_word_grad_sorted(int bf16, const void* dz, const int64_t* ids, const int64_t* order, float* dwte,
+                               int64_t rows, int H, hipStream_t s) {
+  const int64_t nseg = (rows + kSegRows - 1) / kSegRows;
+  const int grid = (int)((nseg + WPB - 1) / WPB);
+  HX_CH_DISPATCH(H, {
+    if (bf16)
+      embed_word_grad_sorted_k<uint16_t, CH><<<grid, NT, 0, s>>>((const uint16_t*)dz, ids, order, dwte, rows, H);
+    else
+      embed_word_grad_sorted_k<float, CH><<<grid, NT, 0, s>>>((const float*)dz, ids, order, dwte, rows, H);
   })
 }
 

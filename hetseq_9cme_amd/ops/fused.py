@@ -189,8 +189,25 @@ class _EmbedLNFn(torch.autograd.Function):
         dwpe = grad_slot(wpe)
         dwpe = (dwpe.zero_() if dwpe is not None else torch.zeros(P, H, device=z.device, dtype=torch.float32))
         dwtt = grad_slot(wtt)
-        dwtt = (dwtt.zero_() if dwtt is not None else torch.zeros(NT, H, device=z.device, dtype=torch.float32))
-        C().embed_grads(dz, ids, tt if ctx.has_tt else None, dwte, dwpe, dwtt)
+        dwtt = dwtt if dwtt is not None else torch.empty(NT, H, device=z.device, dtype=torch.float32)
+        B, S = ids.shape
+        dz2 = dz.reshape(-1, H)
+        ids_f = ids.reshape(-1)
+        # word embeddings: segmented sums over id-sorted rows (few atomics even for
+        # the very frequent ids of real text); accumulates into dwte
+        C().embed_word_grad(dz2, ids_f, torch.argsort(ids_f), dwte)
+        # positions: a column sum over the batch of the [B, S*H] view
+        C().colsum(dz.reshape(B, S * H), None, dwpe[:S].reshape(-1))
+        # token types: one_hot(tt)^T . dz  (one small GEMM, any number of types)
+        if ctx.has_tt:
+            oh = F.one_hot(tt.reshape(-1), NT).to(dz2.dtype)
+            if dz2.dtype == torch.float32:
+                torch.mm(oh.t(), dz2, out=dwtt)
+            else:
+                dwtt.copy_(torch.mm(oh.t(), dz2).float())
+        else:
+            dwtt.zero_()
+            torch.sum(dwpe[:S], 0, out=dwtt[0])
         return None, None, ret_wte, dwpe, dwtt, dgamma, dbeta, None, None, None
 
 
@@ -470,19 +487,24 @@ class _DecoderXentFn(torch.autograd.Function):
     def backward(ctx, g):
         h, W, dl, count = ctx.saved_tensors
         Wp, bias = ctx.params
+        # d loss / d logits = (softmax - onehot) * g / count.  The scale stays a
+        # device scalar (no host sync) and is applied to the small operands -- the
+        # bias column sum's result, dh (M x H) and h (M x H) -- never to the
+        # M x V gradient itself (a 312 MB rewrite at B=128).
         scale = (g.float() / count).reshape(1)
-        dbias = C().colsum(dl, scale, grad_slot(bias) if bias is not None else None)  # scales dl in place
-        dh = torch.mm(dl, W.to(dl.dtype))
+        dbias = C().colsum(dl, scale, grad_slot(bias) if bias is not None else None)
+        dh = torch.mm(dl, W.to(dl.dtype)).mul_(scale.to(dl.dtype))
+        hs = h * scale.to(h.dtype)
         slot = grad_slot(Wp)
         if slot is not None and dl.dtype == torch.float32:
             side = side_begin(dl.device)
             with torch.cuda.stream(side) if side is not None else _nullctx():
-                dW = torch.mm(dl.t(), h, out=slot)
+                dW = torch.mm(dl.t(), hs, out=slot)
             if side is not None:
                 dl.record_stream(side)
-                h.record_stream(side)
+                hs.record_stream(side)
         else:
-            dW = torch.mm(dl.t(), h).float()
+            dW = torch.mm(dl.t(), hs).float()
         return dh, dW, dbias, None
 
 

@@ -321,3 +321,22 @@ def test_debug_mode_validation(dev):
     finally:
         C().set_debug(False)
     assert not C().get_debug()
+
+
+def test_embed_word_grad_sorted_runs(dev):
+    """Segmented-sum word-embedding gradient: runs of one id spanning many 32-row
+    chunks (frequent tokens), singletons, accumulation into an existing slot."""
+    from hetseq_9cme_amd.ops._ext import C
+    torch.manual_seed(0)
+    V, H, n = 500, 768, 3000
+    ids = torch.randint(0, V, (n,), device=dev)
+    ids[:700] = 5          # a run of 700 -> many chunks
+    ids[700:780] = 0       # id 0 at the very start of sorted order
+    ids[-3:] = V - 1       # last id
+    ids = ids[torch.randperm(n, device=dev)]
+    dz = torch.randn(n, H, device=dev)
+    base = torch.randn(V, H, device=dev)
+    dw = base.clone()
+    C().embed_word_grad(dz, ids, torch.argsort(ids), dw)
+    ref = base.index_add(0, ids, dz)
+    _close(dw, ref, rtol=1e-4, atol=1e-3)

@@ -192,19 +192,6 @@ void embed_word_grad(Tensor dz, Tensor ids, Tensor order, Tensor dwte) {
                             dwte.data_ptr<float>(), rows, H, cur_stream(dz));
 }
 
-void embed_grads(Tensor dz, Tensor ids, OptT tt, Tensor dwte, Tensor dwpe, Tensor dwtt) {
-  check_cuda(dz, "dz");
-  check_f32(dwte, "dwte");
-  check_f32(dwpe, "dwpe");
-  check_f32(dwtt, "dwtt");
-  const int64_t B = ids.size(0), S = ids.size(1);
-  const int H = (int)dz.size(-1);
-  const int64_t ntypes = dwtt.size(0);
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(dz.device());
-  hx_embed_grads(act_bf16(dz), dz.data_ptr(), ids.data_ptr<int64_t>(), has(tt) ? tt->data_ptr<int64_t>() : nullptr,
-                 dwte.data_ptr<float>(), dwpe.data_ptr<float>(), dwtt.data_ptr<float>(), (int)B, (int)S, H,
-                 (int)ntypes, cur_stream(dz));
-}
 
 // ------------------------------------------------------------------ elementwise
 Tensor bias_act_fwd(Tensor y, OptT b, int64_t act) {
@@ -331,7 +318,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);
   m.def("embed_ln_fwd", &embed_ln_fwd);
-  m.def("embed_grads", &embed_grads);
   m.def("embed_word_grad", &embed_word_grad);
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);

@@ -29,9 +29,6 @@ void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const floa
                      uint64_t stream, hipStream_t s);
 void hx_embed_word_grad_sorted(int bf16, const void* dz, const int64_t* ids, const int64_t* order, float* dwte,
                                int64_t rows, int H, hipStream_t s);
-void hx_embed_grads(int bf16, const void* dz, const int64_t* ids, const int64_t* tt, float* dwte, float* dwpe,
-                    float* dwtt, int B, int S, int H, int ntypes, hipStream_t s);
-
 // elementwise.hip
 int hx_colsum_ws_floats(int64_t rows, int N);
 void hx_bias_act_fwd(int bf16, int act, const void* y, const float* b, void* out, int64_t rows, int N, hipStream_t s);

@@ -307,17 +307,6 @@ __global__ __launch_bounds__(NT) void embed_ln_fwd_k(const int64_t* __restrict__
 
 // word-embedding gradient: scatter-add rows of dz into dW[ids] (fp32 atomics,
 // whole 16-B contiguous lane groups -> 256 contiguous bytes per wave instruction).
-template <typename T>
-__global__ __launch_bounds__(NT) void embed_word_grad_k(const T* __restrict__ dz, const int64_t* __restrict__ ids,
-                                                      float* __restrict__ dw, int64_t rows, int H) {
-  const int64_t wave = blockIdx.x * (int64_t)WPB + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const int64_t nw = (int64_t)gridDim.x * WPB;
-  for (int64_t r = wave; r < rows; r += nw) {
-    const int64_t id = ids[r];
-    for (int j = lane; j < H; j += 64) atomicAdd(dw + id * H + j, hx::io<T>::ld(dz + r * H + j));
-  }
-}
 
 // position + token-type gradients: block (s-tile) reduces over the batch dim.
 // dpos[s][j] = sum_b dz[b,s,j] ; dtype[t][j] += sum over rows with tt==t (atomics per block)
@@ -386,27 +375,6 @@ __global__ __launch_bounds__(NT) void embed_word_grad_sorted_k(const T* __restri
   flush(cur, true);   // the last run may continue in the next chunk
 }
 
-template <typename T>
-__global__ __launch_bounds__(NT) void embed_pos_type_grad_k(const T* __restrict__ dz, const int64_t* __restrict__ tt,
-                                                          float* __restrict__ dpos, float* __restrict__ dtype,
-                                                          int B, int S, int H, int ntypes) {
-  const int s = blockIdx.x;
-  for (int j = threadIdx.x; j < H; j += NT) {
-    float ap = 0.f, a0 = 0.f, a1 = 0.f;
-    for (int b = 0; b < B; ++b) {
-      const int64_t r = (int64_t)b * S + s;
-      const float v = hx::io<T>::ld(dz + r * H + j);
-      ap += v;
-      const int64_t ty = tt ? tt[r] : 0;
-      if (ty == 0) a0 += v;
-      else if (ty == 1) a1 += v;
-      else atomicAdd(dtype + ty * H + j, v);
-    }
-    dpos[(int64_t)s * H + j] += ap;
-    atomicAdd(dtype + j, a0);
-    if (ntypes > 1) atomicAdd(dtype + H + j, a1);
-  }
-}
 
 int pick_ch(int H) {
   const int c = (H + 255) / 256;
@@ -520,15 +488,3 @@ void hx_embed_word_grad_sorted(int bf16, const void* dz, const int64_t* ids, con
   })
 }
 
-void hx_embed_grads(int bf16, const void* dz, const int64_t* ids, const int64_t* tt, float* dwte, float* dwpe,
-                    float* dwtt, int B, int S, int H, int ntypes, hipStream_t s) {
-  const int64_t rows = (int64_t)B * S;
-  const int grid = ln_grid(rows, 4096);
-  if (bf16) {
-    embed_word_grad_k<uint16_t><<<grid, NT, 0, s>>>((const uint16_t*)dz, ids, dwte, rows, H);
-    embed_pos_type_grad_k<uint16_t><<<S, NT, 0, s>>>((const uint16_t*)dz, tt, dwpe, dwtt, B, S, H, ntypes);
-  } else {
-    embed_word_grad_k<float><<<grid, NT, 0, s>>>((const float*)dz, ids, dwte, rows, H);
-    embed_pos_type_grad_k<float><<<S, NT, 0, s>>>((const float*)dz, tt, dwpe, dwtt, B, S, H, ntypes);
-  }
-}

@@ -153,3 +153,23 @@ def test_data_parallel_gradient_equivalence(tmp_path, bert_data):
     s2 = c2['last_optimizer_state']['state']
     for i in s1:
         torch.testing.assert_close(s1[i]['exp_avg'], s2[i]['exp_avg'], rtol=1e-4, atol=1e-9)
+
+
+@pytest.mark.slow
+def test_launch_hetero_tool_tcp(tmp_path):
+    """tools/launch_hetero.py: two 'nodes' (2 + 1 ranks) meeting over a tcp://
+    rendezvous, gloo on CPU; every rank ends with identical parameters."""
+    write_synthetic_mnist(str(tmp_path / 'mnist'), n_train=384, n_test=64)
+    save = str(tmp_path / 'ck')
+    e = dict(os.environ)
+    e['PYTHONPATH'] = ROOT + os.pathsep + e.get('PYTHONPATH', '')
+    e['OMP_NUM_THREADS'] = '1'
+    r = subprocess.run([sys.executable, os.path.join(ROOT, 'tools', 'launch_hetero.py'), '--cpu', '--nodes', '2,1',
+                        '--', '--task', 'mnist', '--optimizer', 'adadelta', '--data', str(tmp_path / 'mnist'),
+                        '--max-sentences', '32', '--max-update', '4', '--num-workers', '1', '--lr', '1.0',
+                        '--save-dir', save, '--check-params-every', '1', '--fast-stat-sync'],
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=e, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:]
+    ck = load(os.path.join(save, 'checkpoint_last.pt'))
+    assert ck['optimizer_history'][-1]['num_updates'] == 4
+    assert ck['args'].distributed_world_size == 3

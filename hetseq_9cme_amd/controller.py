@@ -68,6 +68,8 @@ class Controller(object):
         self.world_size = args.distributed_world_size
         groups = model.flat_contiguous_groups() if hasattr(model, 'flat_contiguous_groups') else None
         self.flat = FlatParamSpace(model, self.device, contiguous_groups=groups)
+        if getattr(args, 'precision', 'fp32') == 'bf16' and self.cuda:
+            self.flat.enable_bf16_shadow()
         use_reducer = self.world_size > 1 and not getattr(args, 'use_bmuf', False)
         self.reducer = GradReducer(self.flat, bucket_cap_mb=args.bucket_cap_mb,
                                    find_unused_parameters=getattr(args, 'find_unused_parameters', False),
@@ -123,6 +125,8 @@ class Controller(object):
     def _build_optimizer(self):
         self._optimizer = build_optimizer(self.args, self.flat)
         self._optimizer.phase_hook = self.phases.begin if self._profile_phases else None
+        if self.flat.param_bf16 is not None:
+            self._optimizer.bf16_shadow = self.flat.param_bf16   # the fused update rewrites it
         self._lr_scheduler = build_lr_scheduler(self.args, self._optimizer)
         self._lr_scheduler.step_update(0)
 
@@ -182,6 +186,7 @@ class Controller(object):
             print('| loaded checkpoint {} without iterator state (reference-format file)'.format(filename))
         else:
             print('| no existing checkpoint found {}'.format(filename))
+        self.flat.refresh_bf16()
         return extra_state
 
     def get_train_iterator(self, epoch, combine=True, load_dataset=True):

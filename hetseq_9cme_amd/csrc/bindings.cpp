@@ -272,7 +272,8 @@ Tensor softmax_xent_(Tensor logits, OptT bias, Tensor labels, int64_t ignore_ind
 
 // ------------------------------------------------------------------ attention
 std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, int64_t seed, int64_t stream) {
-  check_f32(qkv, "qkv");
+  check_cuda(qkv, "qkv");
+  const int bf = act_bf16(qkv);
   check_f32(mask_bias, "mask_bias");
   TORCH_CHECK(qkv.dim() == 3, "qkv must be [B, S, 3H]");
   const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(2) / 3;
@@ -280,13 +281,13 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
   TORCH_CHECK(mask_bias.numel() == B * S, "mask_bias must be [B, S]");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
   auto out = torch::empty({B, S, H}, qkv.options());
-  auto lse = torch::empty({B, nh, S}, qkv.options());
+  auto lse = torch::empty({B, nh, S}, qkv.options().dtype(torch::kFloat32));
   Tensor dmask;
   // 1 bit per (key, query), stored [key][query word] with both padded to 128
   const int64_t Sp = (S + 127) / 128 * 128;
   if (keep < 1.0) dmask = torch::empty({B, nh, Sp, Sp / 32}, qkv.options().dtype(torch::kInt32));
   else dmask = torch::empty({0}, qkv.options().dtype(torch::kInt32));
-  hx_attn_fwd(qkv.data_ptr<float>(), mask_bias.data_ptr<float>(), out.data_ptr<float>(), lse.data_ptr<float>(),
+  hx_attn_fwd(bf, qkv.data_ptr(), mask_bias.data_ptr<float>(), out.data_ptr(), lse.data_ptr<float>(),
               keep < 1.0 ? reinterpret_cast<uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr, (int)B, (int)S, (int)nh,
               (float)keep, (uint64_t)seed, (uint64_t)stream, cur_stream(qkv));
   dbg_finite(out, "attn_fwd");
@@ -295,15 +296,33 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
 
 Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
                 double keep) {
-  check_f32(dout, "grad_output");
-  check_f32(qkv, "qkv");
-  const int64_t B = qkv.size(0), S = qkv.size(1);
+  check_cuda(dout, "grad_output");
+  check_cuda(qkv, "qkv");
+  const int bf = act_bf16(qkv);
+  TORCH_CHECK(dout.scalar_type() == qkv.scalar_type() && out.scalar_type() == qkv.scalar_type(),
+              "attention activations must share one dtype");
+  const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(2) / 3;
   c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
-  // with one key block per head (S <= 128) every dQKV element is overwritten: no memset
-  auto dqkv = S <= 128 ? torch::empty_like(qkv) : torch::zeros_like(qkv);
-  hx_attn_bwd(qkv.data_ptr<float>(), mask_bias.data_ptr<float>(), dout.data_ptr<float>(), out.data_ptr<float>(),
+  // one key block per head (S <= 128): every dQKV element is written exactly once (no
+  // memset).  Otherwise dQ partials from the S/128 key blocks are added atomically in
+  // fp32: into dqkv itself (fp32, zero-filled) or a [B, S, H] fp32 scratch (bf16).
+  const bool multi = S > 128;
+  auto dqkv = (multi && !bf) ? torch::zeros_like(qkv) : torch::empty_like(qkv);
+  Tensor dq32;
+  float* dq_acc = nullptr;
+  int dq_ld = 0;
+  if (multi && bf) {
+    dq32 = torch::zeros({B, S, H}, qkv.options().dtype(torch::kFloat32));
+    dq_acc = dq32.data_ptr<float>();
+    dq_ld = (int)H;
+  } else if (multi) {
+    dq_acc = dqkv.data_ptr<float>();
+    dq_ld = (int)(3 * H);
+  }
+  hx_attn_bwd(bf, qkv.data_ptr(), mask_bias.data_ptr<float>(), dout.data_ptr(), out.data_ptr(),
               lse.data_ptr<float>(), keep < 1.0 ? reinterpret_cast<const uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr,
-              dqkv.data_ptr<float>(), (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv));
+              dqkv.data_ptr(), dq_acc, dq_ld, (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv));
+  if (multi && bf) dqkv.narrow(-1, 0, H).copy_(dq32);
   dbg_finite(dqkv, "attn_bwd");
   return dqkv;
 }

@@ -78,9 +78,9 @@ __device__ __forceinline__ void drop_step(f32x16& s0, f32x16& s1, const uint32_t
 
 // ============================================================================ forward
 // grid (S/128, nh, B), block 256 = 4 waves x 32 queries.
-template <bool kDrop>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_fwd_k(const float* __restrict__ qkv, const float* __restrict__ maskb,
-                                                float* __restrict__ out, float* __restrict__ lse,
+template <typename T, bool kDrop>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_fwd_k(const T* __restrict__ qkv, const float* __restrict__ maskb,
+                                                T* __restrict__ out, float* __restrict__ lse,
                                                 uint32_t* __restrict__ dmask, int S, int nh, float keep,
                                                 uint64_t seed, uint64_t stream) {
   __shared__ __attribute__((aligned(16))) float Ks[64 * LDK];
@@ -98,16 +98,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   const int Sp = (S + 127) & ~127;             // mask-word / RNG row pitch
   const int q0w = blockIdx.x * 128 + w * 32;    // first query of this wave (bitmask word)
   const uint32_t t16 = (uint32_t)(keep * 65536.f + 0.5f);
-  const float* base = qkv + (int64_t)b * S * H3;
+  const T* base = qkv + (int64_t)b * S * H3;
   const float scale = 0.125f;  // 1/sqrt(64): exact power of two
 
   // Q row slice held in registers: qr[s] = Q[q][h*32 + s] * scale
   float qr[32];
   {
-    const float4* qp = reinterpret_cast<const float4*>(base + (int64_t)qc * H3 + hd * D + h * 32);
+    const T* qp = base + (int64_t)qc * H3 + hd * D + h * 32;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const float4 v = qp[i];
+      const float4 v = hx::load4(qp + 4 * i);
       qr[4 * i] = v.x * scale;
       qr[4 * i + 1] = v.y * scale;
       qr[4 * i + 2] = v.z * scale;
@@ -126,9 +126,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       const int e = tid + i * 256;         // float4 index in the 64x16 tile
       const int row = e >> 4, c4 = (e & 15) * 4;
       const int kr = kt + row < S ? kt + row : S - 1;
-      const float* src = base + (int64_t)kr * H3 + hd * D + c4;
-      *reinterpret_cast<float4*>(&Ks[row * LDK + c4]) = *reinterpret_cast<const float4*>(src + H);
-      *reinterpret_cast<float4*>(&Vs[row * LDK + c4]) = *reinterpret_cast<const float4*>(src + 2 * H);
+      const T* src = base + (int64_t)kr * H3 + hd * D + c4;
+      *reinterpret_cast<float4*>(&Ks[row * LDK + c4]) = hx::load4(src + H);
+      *reinterpret_cast<float4*>(&Vs[row * LDK + c4]) = hx::load4(src + 2 * H);
     }
     if (tid < 64) Ms[tid] = kt + tid < S ? maskb[(int64_t)b * S + kt + tid] : -INFINITY;
     __syncthreads();
@@ -215,14 +215,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
   }
   if (q >= S) return;
   const float inv_l = 1.f / l_run;
-  float* op = out + ((int64_t)b * S + q) * H + hd * D;
+  T* op = out + ((int64_t)b * S + q) * H + hd * D;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int d0 = 8 * g + 4 * h;
-    *reinterpret_cast<float4*>(op + d0) =
-        make_float4(o0[4 * g] * inv_l, o0[4 * g + 1] * inv_l, o0[4 * g + 2] * inv_l, o0[4 * g + 3] * inv_l);
-    *reinterpret_cast<float4*>(op + 32 + d0) =
-        make_float4(o1[4 * g] * inv_l, o1[4 * g + 1] * inv_l, o1[4 * g + 2] * inv_l, o1[4 * g + 3] * inv_l);
+    hx::store4(op + d0,
+               make_float4(o0[4 * g] * inv_l, o0[4 * g + 1] * inv_l, o0[4 * g + 2] * inv_l, o0[4 * g + 3] * inv_l));
+    hx::store4(op + 32 + d0,
+               make_float4(o1[4 * g] * inv_l, o1[4 * g + 1] * inv_l, o1[4 * g + 2] * inv_l, o1[4 * g + 3] * inv_l));
   }
   if (h == 0) lse[bh * S + q] = m_run + __logf(l_run);
 }
@@ -246,11 +246,12 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
-template <bool kDrop>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_k(const float* __restrict__ qkv, const float* __restrict__ maskb,
-                                                const float* __restrict__ dout, const float* __restrict__ outp,
+template <typename T, bool kDrop>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_k(const T* __restrict__ qkv, const float* __restrict__ maskb,
+                                                const T* __restrict__ dout, const T* __restrict__ outp,
                                                 const float* __restrict__ lse, const uint32_t* __restrict__ dmask,
-                                                float* __restrict__ dqkv, int S, int nh, float keep) {
+                                                T* __restrict__ dqkv, float* __restrict__ dq_acc, int dq_ld,
+                                                int S, int nh, float keep) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Ks = smem;                      // [128][LDK]
   float* Qs = Ks + 128 * LDK;            // [32][LDK]  (pre-scaled Q tile)
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int H = nh * D, H3 = 3 * H;
   const int kbase = blockIdx.x * 128;
   const bool single = gridDim.x == 1;          // one workgroup sees every key: dQ is final
-  const float* base = qkv + (int64_t)b * S * H3;
+  const T* base = qkv + (int64_t)b * S * H3;
   const int64_t bh = (int64_t)b * nh + hd;
   const float scale = 0.125f, inv_keep = 1.f / keep;
   const int Sp = (S + 127) & ~127;
@@ -277,33 +278,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int e = tid + i * 256;
     const int row = e >> 4, c4 = (e & 15) * 4;
     const int kr = kbase + row < S ? kbase + row : S - 1;
-    *reinterpret_cast<float4*>(&Ks[row * LDK + c4]) =
-        *reinterpret_cast<const float4*>(base + (int64_t)kr * H3 + H + hd * D + c4);
+    *reinterpret_cast<float4*>(&Ks[row * LDK + c4]) = hx::load4(base + (int64_t)kr * H3 + H + hd * D + c4);
   }
   const int mykey = kbase + w * 32 + l32;     // key on this lane
   const int mykc = mykey < S ? mykey : S - 1;
   float vr[32];
   {
-    const float4* vp = reinterpret_cast<const float4*>(base + (int64_t)mykc * H3 + 2 * H + hd * D + h * 32);
+    const T* vp = base + (int64_t)mykc * H3 + 2 * H + hd * D + h * 32;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const float4 v = vp[i];
+      const float4 v = hx::load4(vp + 4 * i);
       vr[4 * i] = v.x; vr[4 * i + 1] = v.y; vr[4 * i + 2] = v.z; vr[4 * i + 3] = v.w;
     }
   }
   const float mk = mykey < S ? maskb[(int64_t)b * S + mykey] : -INFINITY;
   const float* Kw = Ks + (w * 32) * LDK;      // this wave's keys
 
-  float* dqkv_b = dqkv + (int64_t)b * S * H3 + hd * D;
+  T* dqkv_b = dqkv + (int64_t)b * S * H3 + hd * D;
+  // multi-block (S > 128): dQ partial sums are added atomically into an fp32 buffer
+  // (dqkv itself when T = float, a separate [B, S, H] scratch for bf16)
+  float* dqa_b = dq_acc ? dq_acc + (int64_t)b * S * dq_ld + hd * D : nullptr;
   // staging map of a 32x64 tile: thread -> rows (tid>>4) and 16 + (tid>>4), float4 column c4
   const int srow = tid >> 4, sc4 = (tid & 15) * 4;
   // Per-(b, head) bases are wave-uniform (SGPRs); per-lane offsets within one
   // sequence fit 32 bits.  Keeping the per-lane addresses 32-bit keeps this kernel
   // under 256 VGPRs without spills -- a spilled address is reloaded from scratch,
   // and scratch loads count in vmcnt: the reload's wait would drain the prefetch.
-  const float* dout_b = dout + (int64_t)b * S * H + hd * D;
-  const float* out_b = outp + (int64_t)b * S * H + hd * D;
-  const float* qkv_bh = base + hd * D;
+  const T* dout_b = dout + (int64_t)b * S * H + hd * D;
+  const T* out_b = outp + (int64_t)b * S * H + hd * D;
+  const T* qkv_bh = base + hd * D;
   const float* lse_bh = lse + bh * S;
   // dropout bits of (this lane's key, the 32 queries of a tile): ONE word
   const uint32_t* dmask_bh = kDrop ? dmask + (int64_t)bh * Sp * nwords : nullptr;
@@ -313,8 +316,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int i = 0; i < 2; ++i) {
       const int qr = qt + srow + 16 * i;
       const int r = qr < S ? qr : S - 1;
-      qn[i] = *reinterpret_cast<const float4*>(qkv_bh + r * H3 + sc4);
-      dn[i] = *reinterpret_cast<const float4*>(dout_b + r * H + sc4);
+      qn[i] = hx::load4(qkv_bh + r * H3 + sc4);
+      dn[i] = hx::load4(dout_b + r * H + sc4);
     }
     // unconditional (clamped) loads: a branch around a load makes the compiler's
     // vmcnt tracking fall back to vmcnt(0), which would wait out the whole prefetch
@@ -339,7 +342,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int qr = qt + srow + 16 * i;
-      on[i] = *reinterpret_cast<const float4*>(out_b + (qr < S ? qr : S - 1) * H + sc4);
+      on[i] = hx::load4(out_b + (qr < S ? qr : S - 1) * H + sc4);
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -413,30 +416,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
     const int q0 = qt + qh * 16 + 4 * k4;
-    float* dq = dqkv_b + q0 * H3 + dqa * 16 + r16;
+    if (single) {
+      T* dq = dqkv_b + q0 * H3 + dqa * 16 + r16;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      if (q0 + r >= S) continue;
-      if (single) {
-        dq[r * H3] = qa0[r] * scale;
-        dq[r * H3 + 16] = qa1[r] * scale;
-      } else {
-        atomicAdd(dq + r * H3, qa0[r] * scale);
-        atomicAdd(dq + r * H3 + 16, qa1[r] * scale);
+      for (int r = 0; r < 4; ++r) {
+        if (q0 + r >= S) continue;
+        hx::io<T>::st(dq + r * H3, qa0[r] * scale);
+        hx::io<T>::st(dq + r * H3 + 16, qa1[r] * scale);
+      }
+    } else {
+      float* dq = dqa_b + q0 * dq_ld + dqa * 16 + r16;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (q0 + r >= S) continue;
+        atomicAdd(dq + r * dq_ld, qa0[r] * scale);
+        atomicAdd(dq + r * dq_ld + 16, qa1[r] * scale);
       }
     }
   }
   // ---- epilogue: dK (accumulated against pre-scaled Q -> already scaled), dV
-  float* dk = dqkv + (int64_t)b * S * H3 + H + hd * D;
-  float* dvp = dqkv + (int64_t)b * S * H3 + 2 * H + hd * D;
+  T* dk = dqkv + (int64_t)b * S * H3 + H + hd * D;
+  T* dvp = dqkv + (int64_t)b * S * H3 + 2 * H + hd * D;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int key = kbase + w * 32 + crow(r, h);
     if (key >= S) continue;
-    dk[(int64_t)key * H3 + l32] = dk0[r];
-    dk[(int64_t)key * H3 + 32 + l32] = dk1[r];
-    dvp[(int64_t)key * H3 + l32] = dv0[r];
-    dvp[(int64_t)key * H3 + 32 + l32] = dv1[r];
+    hx::io<T>::st(dk + (int64_t)key * H3 + l32, dk0[r]);
+    hx::io<T>::st(dk + (int64_t)key * H3 + 32 + l32, dk1[r]);
+    hx::io<T>::st(dvp + (int64_t)key * H3 + l32, dv0[r]);
+    hx::io<T>::st(dvp + (int64_t)key * H3 + 32 + l32, dv1[r]);
   }
 }
 
@@ -446,29 +454,51 @@ size_t hx_attn_bwd_smem_bytes() {
   return sizeof(float) * (128 * LDK + 2 * 32 * LDK + 32 * LDSS + 64);
 }
 
-void hx_attn_fwd(const float* qkv, const float* maskb, float* out, float* lse, uint32_t* dmask, int B, int S, int nh,
-                 float keep, uint64_t seed, uint64_t stream, hipStream_t s) {
+namespace {
+
+template <typename T>
+void attn_fwd_t(const void* qkv, const float* maskb, void* out, float* lse, uint32_t* dmask, int B, int S, int nh,
+                float keep, uint64_t seed, uint64_t stream, hipStream_t s) {
   dim3 grid((S + 127) / 128, nh, B);
   if (keep < 1.f)
-    attn_fwd_k<true><<<grid, 256, 0, s>>>(qkv, maskb, out, lse, dmask, S, nh, keep, seed, stream);
+    attn_fwd_k<T, true><<<grid, 256, 0, s>>>((const T*)qkv, maskb, (T*)out, lse, dmask, S, nh, keep, seed, stream);
   else
-    attn_fwd_k<false><<<grid, 256, 0, s>>>(qkv, maskb, out, lse, dmask, S, nh, keep, seed, stream);
+    attn_fwd_k<T, false><<<grid, 256, 0, s>>>((const T*)qkv, maskb, (T*)out, lse, dmask, S, nh, keep, seed, stream);
 }
 
-void hx_attn_bwd(const float* qkv, const float* maskb, const float* dout, const float* out, const float* lse,
-                 const uint32_t* dmask, float* dqkv, int B, int S, int nh, float keep, hipStream_t s) {
+template <typename T>
+void attn_bwd_t(const void* qkv, const float* maskb, const void* dout, const void* out, const float* lse,
+                const uint32_t* dmask, void* dqkv, float* dq_acc, int dq_ld, int B, int S, int nh, float keep,
+                hipStream_t s) {
   dim3 grid((S + 127) / 128, nh, B);
   const size_t smem = hx_attn_bwd_smem_bytes();
   static bool attr = false;
   if (!attr) {  // > 64 KiB dynamic LDS needs an explicit opt-in (gfx950 has 160 KiB per CU)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_k<true>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_k<T, true>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_k<false>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_k<T, false>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
   if (keep < 1.f)
-    attn_bwd_k<true><<<grid, 256, smem, s>>>(qkv, maskb, dout, out, lse, dmask, dqkv, S, nh, keep);
+    attn_bwd_k<T, true><<<grid, 256, smem, s>>>((const T*)qkv, maskb, (const T*)dout, (const T*)out, lse, dmask,
+                                                (T*)dqkv, dq_acc, dq_ld, S, nh, keep);
   else
-    attn_bwd_k<false><<<grid, 256, smem, s>>>(qkv, maskb, dout, out, lse, dmask, dqkv, S, nh, keep);
+    attn_bwd_k<T, false><<<grid, 256, smem, s>>>((const T*)qkv, maskb, (const T*)dout, (const T*)out, lse, dmask,
+                                                 (T*)dqkv, dq_acc, dq_ld, S, nh, keep);
+}
+
+}  // namespace
+
+void hx_attn_fwd(int bf16, const void* qkv, const float* maskb, void* out, float* lse, uint32_t* dmask, int B, int S,
+                 int nh, float keep, uint64_t seed, uint64_t stream, hipStream_t s) {
+  if (bf16) attn_fwd_t<uint16_t>(qkv, maskb, out, lse, dmask, B, S, nh, keep, seed, stream, s);
+  else attn_fwd_t<float>(qkv, maskb, out, lse, dmask, B, S, nh, keep, seed, stream, s);
+}
+
+void hx_attn_bwd(int bf16, const void* qkv, const float* maskb, const void* dout, const void* out, const float* lse,
+                 const uint32_t* dmask, void* dqkv, float* dq_acc, int dq_ld, int B, int S, int nh, float keep,
+                 hipStream_t s) {
+  if (bf16) attn_bwd_t<uint16_t>(qkv, maskb, dout, out, lse, dmask, dqkv, dq_acc, dq_ld, B, S, nh, keep, s);
+  else attn_bwd_t<float>(qkv, maskb, dout, out, lse, dmask, dqkv, dq_acc, dq_ld, B, S, nh, keep, s);
 }

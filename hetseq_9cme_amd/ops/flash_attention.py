@@ -5,8 +5,9 @@ mask_bias; probs = dropout(softmax(scores)); ctx = probs V; heads merged back
 to [B, S, H].  The additive mask is the reference's (1 - m) * -10000 (not -inf).
 
 GPU path: the fused flash-style HIP kernel (``_C.attn_fwd`` / ``attn_bwd``,
-csrc/kernels/attention.hip) for fp32 and head_dim 64 at any sequence length
-(keys past S are masked, rows past S are neither computed into nor stored);
+csrc/kernels/attention.hip) for head_dim 64 at any sequence length (keys past
+S are masked, rows past S are neither computed into nor stored), with fp32 or
+bf16 activations (bf16 is converted at load; the math is fp32 MFMA either way);
 other shapes / dtypes use the composite below (batched GEMMs + softmax), which
 is also the CPU path and the test oracle.
 """
@@ -45,7 +46,7 @@ def _fused_ok(qkv, num_heads):
         return False
     B, S, H3 = qkv.shape
     d = (H3 // 3) // num_heads
-    return qkv.dtype == torch.float32 and d == 64 and S >= 1
+    return qkv.dtype in (torch.float32, torch.bfloat16) and d == 64 and S >= 1
 
 
 class _AttnFn(torch.autograd.Function):

@@ -21,6 +21,27 @@ def _is_bf16(t):
     return t.dtype == torch.bfloat16
 
 
+def cast_w(w, dtype):
+    """Parameter ``w`` in compute dtype: its bf16 shadow view when one exists
+    (``FlatParamSpace.enable_bf16_shadow``), else a cast."""
+    if w is None or w.dtype == dtype:
+        return w
+    sh = getattr(w, '_hx_bf16', None) if dtype == torch.bfloat16 else None
+    return sh if sh is not None else w.to(dtype)
+
+
+def _wgrad(dy2, x2, slot):
+    """dW = dy2^T x2 in fp32; written straight into ``slot`` when given.  bf16
+    operands use the bf16 x bf16 -> fp32 GEMM (no bf16 result, no cast pass)."""
+    if dy2.dtype == torch.float32:
+        return torch.mm(dy2.t(), x2, out=slot) if slot is not None else torch.mm(dy2.t(), x2)
+    dW = torch.mm(dy2.t(), x2, out_dtype=torch.float32)
+    if slot is not None:
+        slot.copy_(dW)
+        return slot
+    return dW
+
+
 def _nullctx():
     import contextlib
     return contextlib.nullcontext()
@@ -71,12 +92,13 @@ class ResidualGrad(object):
 
 def _dgrad(dy2, W, xshape, mbox):
     """dx = dy2 @ W, accumulated into the deposited residual gradient if any."""
+    Wc = cast_w(W, dy2.dtype)
     if mbox is None:
-        return torch.mm(dy2, W.to(dy2.dtype)).view(xshape)
+        return torch.mm(dy2, Wc).view(xshape)
     g, other = mbox.take(dy2.dtype)
     if g is not None:
-        return g.view(-1, W.shape[1]).addmm_(dy2, W.to(dy2.dtype)).view(xshape)
-    dx = torch.mm(dy2, W.to(dy2.dtype)).view(xshape)
+        return g.view(-1, W.shape[1]).addmm_(dy2, Wc).view(xshape)
+    dx = torch.mm(dy2, Wc).view(xshape)
     return dx if other is None else dx + other.view(xshape).to(dx.dtype)
 
 
@@ -340,8 +362,8 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, b, mbox):
         x2 = x.reshape(-1, x.shape[-1])
-        Wc = W.to(x.dtype)
-        y = torch.mm(x2, Wc.t()) if b is None else torch.addmm(b.to(x.dtype), x2, Wc.t())
+        Wc = cast_w(W, x.dtype)
+        y = torch.mm(x2, Wc.t()) if b is None else torch.addmm(cast_w(b, x.dtype), x2, Wc.t())
         ctx.save_for_backward(x2, W)
         ctx.b = b
         ctx.mbox = mbox
@@ -355,13 +377,10 @@ class _LinearFn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox) if ctx.needs_input_grad[0] else None
         slot = grad_slot(W)
-        direct = slot is not None and dy2.dtype == torch.float32
+        direct = slot is not None
         side = side_begin(dy2.device) if direct else None
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            if direct:
-                dW = torch.mm(dy2.t(), x2, out=slot)
-            else:
-                dW = torch.mm(dy2.t(), x2).float()
+            dW = _wgrad(dy2, x2, slot)
             db = None
             if b is not None:
                 if dy2.shape[-1] % 4 == 0:
@@ -379,7 +398,7 @@ def linear(x, W, b=None, res_grad=None):
     ``res_grad``: see ``ResidualGrad``."""
     if use_kernels(x):
         return _LinearFn.apply(x, W, b, res_grad)
-    return F.linear(x, W.to(x.dtype), None if b is None else b.to(x.dtype))
+    return F.linear(x, cast_w(W, x.dtype), cast_w(b, x.dtype))
 
 
 # ----------------------------------------------------------------- fused Q/K/V projection
@@ -413,9 +432,16 @@ class _Linear3Fn(torch.autograd.Function):
         b = _adjacent_view([bq, bk, bv])
         if b is None:
             b = torch.cat([bq, bk, bv], 0)
+        Wc, bc = W, b
+        if x.dtype != W.dtype:
+            sh = [getattr(t, '_hx_bf16', None) for t in (wq, wk, wv, bq, bk, bv)]
+            Wc = _adjacent_view(sh[:3]) if all(t is not None for t in sh) else None
+            bc = _adjacent_view(sh[3:]) if all(t is not None for t in sh) else None
+            Wc = Wc if Wc is not None else W.to(x.dtype)
+            bc = bc if bc is not None else b.to(x.dtype)
         x2 = x.reshape(-1, x.shape[-1])
-        y = torch.addmm(b.to(x.dtype), x2, W.t().to(x.dtype))
-        ctx.save_for_backward(x2, W)
+        y = torch.addmm(bc, x2, Wc.t())
+        ctx.save_for_backward(x2, Wc)
         ctx.params = (wq, wk, wv, bq, bk, bv)
         ctx.mbox = mbox
         ctx.xshape = x.shape
@@ -434,14 +460,14 @@ class _Linear3Fn(torch.autograd.Function):
         fused = _adjacent_view(ws) if all(t is not None for t in ws) else None
         bs = [grad_slot(t) for t in (bq, bk, bv)]
         fb = _adjacent_view(bs) if all(t is not None for t in bs) else None
-        direct = fused is not None and fb is not None and dy2.dtype == torch.float32
+        direct = fused is not None and fb is not None
         side = side_begin(dy2.device) if direct else None
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            if fused is not None and dy2.dtype == torch.float32:
-                torch.mm(dy2.t(), x2, out=fused)
+            if fused is not None:
+                _wgrad(dy2, x2, fused)
                 gW = ws
             else:
-                dW = (dy2.t() @ x2).float()
+                dW = _wgrad(dy2, x2, None)
                 gW = [dW[:a], dW[a:a + b_], dW[a + b_:]]
                 for k, t in enumerate(ws):
                     if t is not None:
@@ -475,7 +501,7 @@ def attention(qkv, mask_bias, num_heads, p, training):
 class _DecoderXentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, W, bias, labels):
-        logits = torch.mm(h, W.t().to(h.dtype))
+        logits = torch.mm(h, cast_w(W, h.dtype).t())
         loss_rows = C().softmax_xent_(logits, bias, labels, -1)   # logits <- softmax - onehot
         count = (labels != -1).sum().to(torch.float32)
         loss = loss_rows.sum() / count
@@ -493,18 +519,15 @@ class _DecoderXentFn(torch.autograd.Function):
         # M x V gradient itself (a 312 MB rewrite at B=128).
         scale = (g.float() / count).reshape(1)
         dbias = C().colsum(dl, scale, grad_slot(bias) if bias is not None else None)
-        dh = torch.mm(dl, W.to(dl.dtype)).mul_(scale.to(dl.dtype))
+        dh = torch.mm(dl, cast_w(Wp, dl.dtype)).mul_(scale.to(dl.dtype))
         hs = h * scale.to(h.dtype)
         slot = grad_slot(Wp)
-        if slot is not None and dl.dtype == torch.float32:
-            side = side_begin(dl.device)
-            with torch.cuda.stream(side) if side is not None else _nullctx():
-                dW = torch.mm(dl.t(), hs, out=slot)
-            if side is not None:
-                dl.record_stream(side)
-                hs.record_stream(side)
-        else:
-            dW = torch.mm(dl.t(), hs).float()
+        side = side_begin(dl.device) if slot is not None else None
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            dW = _wgrad(dl, hs, slot)
+        if side is not None:
+            dl.record_stream(side)
+            hs.record_stream(side)
         return dh, dW, dbias, None
 
 

@@ -61,6 +61,7 @@ class _Optimizer(object):
 
     # --- grads --------------------------------------------------------
     phase_hook = None   # set by the controller under --profile-phases
+    bf16_shadow = None  # bf16 copy of the flat params kept in sync by step() (--precision bf16)
 
     def backward(self, loss):
         if self.phase_hook is not None:
@@ -292,6 +293,8 @@ class _Adadelta(_Optimizer):
                 p.add_(delta, alpha=-lr)
                 acc.mul_(rho).addcmul_(delta, delta, value=1 - rho)
 
+        if self.bf16_shadow is not None:
+            self.flat.refresh_bf16()
     def _param_state(self, i):
         if self.steps[i] == 0:
             return None

@@ -123,6 +123,26 @@ class FlatParamSpace(object):
                 assert b == a + 1 and self.offsets[b] == self.offsets[a] + self.sizes[a], \
                     'contiguous group {} could not be laid out adjacently'.format(g)
 
+        self.param_bf16 = None
+
+    # ------------------------------------------------------------------ bf16 compute copy
+    def enable_bf16_shadow(self):
+        """``--precision bf16``: a bf16 copy of the flat parameters, laid out
+        identically, that the GEMMs read instead of casting the fp32 master
+        weights on every use.  The fused Adam writes it as part of the update
+        (``_Adam.bf16_shadow``); ``refresh_bf16`` re-syncs it after a load."""
+        if self.param_bf16 is None:
+            self.param_bf16 = torch.empty(self.numel, dtype=torch.bfloat16, device=self.device)
+            for p, o in zip(self.params, self.offsets):
+                p._hx_bf16 = self.param_bf16[o:o + p.numel()].view(p.shape)
+        self.refresh_bf16()
+        return self.param_bf16
+
+    def refresh_bf16(self):
+        if self.param_bf16 is not None:
+            with torch.no_grad():
+                self.param_bf16.copy_(self.param_flat)
+
     # ------------------------------------------------------------------
     def rebind_grads(self):
         """Re-attach ``.grad`` views (used after something set grads to None)."""

@@ -340,3 +340,53 @@ def test_embed_word_grad_sorted_runs(dev):
     C().embed_word_grad(dz, ids, torch.argsort(ids), dw)
     ref = base.index_add(0, ids, dz)
     _close(dw, ref, rtol=1e-4, atol=1e-3)
+
+
+def test_bf16_mode_shadow_in_sync(dev, tmp_path):
+    """--precision bf16: GEMMs read a bf16 shadow of the flat fp32 parameters that
+    the fused Adam rewrites every update; after real steps it must equal the cast
+    of the master weights exactly, and training must stay finite."""
+    from hetseq_9cme_amd import options, tasks
+    from hetseq_9cme_amd.controller import Controller
+    from hetseq_9cme_amd.data import iterators
+    from hetseq_9cme_amd.data.synthetic import BERT_TINY, write_bert_config, write_synthetic_bert_shards
+    d = tmp_path / 'data'
+    write_synthetic_bert_shards(str(d), n_files=1, samples_per_file=64, seq_len=128, max_pred=20, vocab_size=1024,
+                                split='train')
+    cfg = write_bert_config(str(tmp_path / 'c.json'), **BERT_TINY)
+    args = options.parse_training_args(['--task', 'bert', '--data', str(d), '--config_file', cfg, '--max-sentences',
+                                        '8', '--fast-stat-sync', '--lr', '1e-3', '--num-workers', '1',
+                                        '--precision', 'bf16', '--no-save', '--disable-validation'])
+    args.device_id, args.distributed_rank = 0, 0
+    task = tasks.setup_task(args)
+    ctrl = Controller(args, task, task.build_model(args))
+    itr = iterators.GroupedIterator(ctrl.get_train_iterator(epoch=0, load_dataset=True).next_epoch_itr(), 1)
+    p0 = ctrl.flat.param_flat.clone()
+    for _ in range(3):
+        out = ctrl.train_step(next(itr))
+    torch.cuda.synchronize()
+    assert torch.isfinite(out['loss']).all()
+    assert not torch.equal(p0, ctrl.flat.param_flat)
+    assert torch.equal(ctrl.flat.param_bf16, ctrl.flat.param_flat.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize('S', [128, 200])
+def test_attention_bf16_io(dev, S):
+    """bf16 activations through the fused attention (fp32 MFMA math, bf16 I/O):
+    single key block (S<=128, direct dQ stores) and multi-block (fp32 dQ scratch)."""
+    torch.manual_seed(0)
+    B, nh, d = 2, 4, 64
+    q32 = torch.randn(B, S, 3 * nh * d, device=dev)
+    mask = torch.ones(B, S, device=dev)
+    mask[1, S // 3:] = 0
+    mb = (1 - mask) * -10000.0
+    qkv = q32.to(torch.bfloat16).requires_grad_()
+    out = ops.attention(qkv, mb, nh, 0.0, True)
+    assert out.dtype == torch.bfloat16
+    ref_in = qkv.detach().float().requires_grad_()
+    ref = attention_ref(ref_in, mb, nh, 0.0)
+    _close(out.float(), ref, rtol=2e-2, atol=2e-2)
+    d_ = torch.randn_like(ref)
+    out.backward(d_.to(torch.bfloat16))
+    ref.backward(d_.to(torch.bfloat16).float())
+    _close(qkv.grad.float(), ref_in.grad, rtol=3e-2, atol=3e-2)

@@ -35,11 +35,9 @@ def _wgrad(dy2, x2, slot):
     operands use the bf16 x bf16 -> fp32 GEMM (no bf16 result, no cast pass)."""
     if dy2.dtype == torch.float32:
         return torch.mm(dy2.t(), x2, out=slot) if slot is not None else torch.mm(dy2.t(), x2)
-    dW = torch.mm(dy2.t(), x2, out_dtype=torch.float32)
     if slot is not None:
-        slot.copy_(dW)
-        return slot
-    return dW
+        return torch.mm(dy2.t(), x2, out_dtype=torch.float32, out=slot)
+    return torch.mm(dy2.t(), x2, out_dtype=torch.float32)
 
 
 def _nullctx():

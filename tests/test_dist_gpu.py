@@ -25,8 +25,13 @@ def test_two_rank_gpu_equivalence(dev, tmp_path):
     common = ['--task', 'bert', '--data', str(d), '--dict', vocab, '--config_file', cfg, '--max-sentences', '8',
               '--fast-stat-sync', '--max-update', '2', '--disable-validation', '--num-workers', '1', '--lr', '1e-3',
               '--bucket-cap-mb', '1']
+    # 'one'/'two': 2 micro-batches per update either way; 'one4'/'two2': the same with
+    # local accumulation under no_sync on top (first micro-batch claims the flat
+    # slots, later ones accumulate through autograd)
     runs = {'one': ['--update-freq', '2', '--distributed-world-size', '1'],
-            'two': ['--distributed-world-size', '2', '--distributed-backend', 'gloo']}
+            'two': ['--distributed-world-size', '2', '--distributed-backend', 'gloo'],
+            'one4': ['--update-freq', '4', '--distributed-world-size', '1'],
+            'two2': ['--update-freq', '2', '--distributed-world-size', '2', '--distributed-backend', 'gloo']}
     ck = {}
     for name, extra in runs.items():
         save = str(tmp_path / name)
@@ -38,3 +43,6 @@ def test_two_rank_gpu_equivalence(dev, tmp_path):
             ck[name] = torch.load(os.path.join(save, 'checkpoint_last.pt'), map_location='cpu', weights_only=True)
     for k, v in ck['one']['model'].items():
         torch.testing.assert_close(ck['two']['model'][k], v, rtol=1e-4, atol=1e-6, msg=k)
+    for k, v in ck['one4']['model'].items():
+        torch.testing.assert_close(ck['two2']['model'][k], v, rtol=1e-4, atol=1e-6, msg=k)
+    assert ck['two2']['optimizer_history'][-1]['num_updates'] == 2

@@ -28,7 +28,6 @@ import contextlib
 import math
 import os
 import threading
-import time
 from collections import OrderedDict
 
 import torch

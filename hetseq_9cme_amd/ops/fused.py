@@ -5,7 +5,6 @@ hand-written HIP kernels (``_C``), CPU tensors run the plain-torch reference of
 the same math (used by the CPU test-suite and as the numerics oracle for the GPU
 kernel tests).  Semantics follow the reference model (hetseq/bert_modeling.py).
 """
-import math
 import os
 
 import torch
@@ -15,10 +14,6 @@ from ._ext import C, use_kernels
 from .rng import get_rng
 
 ACT_IDS = {'gelu': 0, 'tanh': 1, 'relu': 2, 'none': 3}
-
-
-def _is_bf16(t):
-    return t.dtype == torch.bfloat16
 
 
 def cast_w(w, dtype):

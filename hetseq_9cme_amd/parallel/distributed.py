@@ -20,7 +20,6 @@ MI355X-native differences:
 """
 import builtins
 import datetime
-import os
 import pickle
 import socket
 import warnings

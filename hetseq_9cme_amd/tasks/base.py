@@ -11,9 +11,7 @@ sharded ``EpochBatchIterator`` and runs one forward/backward micro-batch.
 ``loss`` stays a DEVICE tensor in the logging output (no per-step host sync).
 """
 import collections
-import os
 
-import numpy as np
 import torch
 
 from ..data import data_utils, iterators

@@ -10,7 +10,6 @@ of a 'B' mention carries the entity id, out-of-dictionary entities get -1,
 everything else -100 (:112-183).  Data files are CoNLL columns whose last column
 holds the entity name of 'B' tokens.
 """
-import os
 
 import numpy as np
 import torch

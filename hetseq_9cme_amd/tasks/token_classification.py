@@ -14,7 +14,6 @@ Deliberate fix (App. A2): the task is registered, so ``--task
 BertForTokenClassification`` works from the CLI.
 """
 import argparse
-import os
 
 import torch
 

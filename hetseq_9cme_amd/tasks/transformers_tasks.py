@@ -6,7 +6,6 @@ stock ``transformers.BertForTokenClassification`` (its own module names:
 with ``sample_size = 1`` (reference :470-477).  The model runs on torch ops (no
 fused HIP kernels); use ``BertForTokenClassificationTask`` for the fast path.
 """
-import torch
 
 from .token_classification import BertForTokenClassificationTask, safe_load_checkpoint
 

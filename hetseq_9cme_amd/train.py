@@ -18,7 +18,6 @@ import collections
 import math
 import os
 import random
-import sys
 
 import numpy as np
 import torch

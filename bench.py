@@ -44,7 +44,7 @@ def parse():
     ap.add_argument('--no-fused', action='store_true', help='torch-op baseline (A/B only)')
     ap.add_argument('--data-dir', default=None)
     ap.add_argument('--update-freq', type=int, default=1)
-    ap.add_argument('--gemm-tuning', default='table', choices=['off', 'table', 'online'])
+    ap.add_argument('--gemm-tuning', default='table', choices=['off', 'table', 'online', 'retune'])
     ap.add_argument('--gemm-tuning-file', default=None)
     ap.add_argument('--profile-phases', action='store_true',
                     help='extra untimed steps reporting host time per step phase (stderr)')

@@ -17,6 +17,8 @@ step.  PyTorch-ROCm's TunableOp layer lets us pin a solution per
 * ``online``: additionally benchmarks every new shape the first time it runs
   (a few hundred ms per shape) and writes the merged table to
   ``--gemm-tuning-file`` (rank-suffixed) at exit;
+* ``retune``: like ``online`` but without loading the shipped table, so every
+  shape is benchmarked again (after a ROCm / PyTorch / library upgrade);
 * ``off``: library defaults.
 
 The table carries validators (PyTorch / HIP / hipBLASLt / rocBLAS versions and
@@ -47,8 +49,11 @@ def configure(mode='table', out_file=None, table=TABLE, max_tuning_ms=None):
         return True
     tun = torch.cuda.tunable
     tun.enable(True)
-    tun.tuning_enable(mode == 'online')
-    if mode == 'online':
+    tuning = mode in ('online', 'retune')
+    tun.tuning_enable(tuning)
+    if mode == 'retune':
+        table = None
+    if tuning:
         if max_tuning_ms is not None:
             tun.set_max_tuning_duration(int(max_tuning_ms))
         tun.set_filename(out_file or os.path.join(tempfile.gettempdir(), 'hx_gemm_tuning.csv'),

@@ -57,7 +57,7 @@ def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialD
     parser.add_argument('--user-module', default=None, metavar='PATH',
                         help='python file / package imported before parsing (registers custom '
                              'tasks, optimizers, LR schedulers)')
-    parser.add_argument('--gemm-tuning', default='table', choices=['off', 'table', 'online'],
+    parser.add_argument('--gemm-tuning', default='table', choices=['off', 'table', 'online', 'retune'],
                         help='library-GEMM solution selection: shipped per-shape table (default), '
                              'online benchmarking of unseen shapes, or library defaults')
     parser.add_argument('--gemm-tuning-file', default=None, metavar='PATH',

@@ -10,9 +10,9 @@ step.  PyTorch-ROCm's TunableOp layer lets us pin a solution per
 (op, transpose, shape, leading-dims) key, so this module
 
 * ``table`` (default): loads the solution table shipped in
-  ``hetseq_9cme_amd/tuning/gemm_gfx950.csv`` (tuned offline on an MI355X with
-  ``--gemm-tuning online``; keys for BERT-base/large phase 1/2 per-GPU batches,
-  fp32 and bf16), with tuning disabled -- shapes not in the table keep the
+  ``hetseq_9cme_amd/tuning/gemm_gfx950.csv`` (tuned on an MI355X with
+  ``tools/tune_gemm.sh``; fp32 keys for BERT-base phase 1/2 and BERT-large
+  phase 1 at their per-GPU batches), with tuning disabled -- shapes not in the table keep the
   library default, nothing is benchmarked at run time;
 * ``online``: additionally benchmarks every new shape the first time it runs
   (a few hundred ms per shape) and writes the merged table to

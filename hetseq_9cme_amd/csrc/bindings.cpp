@@ -271,7 +271,8 @@ Tensor softmax_xent_(Tensor logits, OptT bias, Tensor labels, int64_t ignore_ind
 }
 
 // ------------------------------------------------------------------ attention
-std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, int64_t seed, int64_t stream) {
+std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, int64_t seed, int64_t stream,
+                             OptT bias) {
   check_cuda(qkv, "qkv");
   const int bf = act_bf16(qkv);
   check_f32(mask_bias, "mask_bias");
@@ -279,6 +280,10 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
   const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(2) / 3;
   TORCH_CHECK(H == nh * 64, "fused attention needs head_dim == 64");
   TORCH_CHECK(mask_bias.numel() == B * S, "mask_bias must be [B, S]");
+  if (has(bias)) {
+    check_f32(*bias, "qkv bias");
+    TORCH_CHECK(bias->numel() == 3 * H, "qkv bias must have 3H elements");
+  }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
   auto out = torch::empty({B, S, H}, qkv.options());
   auto lse = torch::empty({B, nh, S}, qkv.options().dtype(torch::kFloat32));
@@ -287,15 +292,18 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
   const int64_t Sp = (S + 127) / 128 * 128;
   if (keep < 1.0) dmask = torch::empty({B, nh, Sp, Sp / 32}, qkv.options().dtype(torch::kInt32));
   else dmask = torch::empty({0}, qkv.options().dtype(torch::kInt32));
-  hx_attn_fwd(bf, qkv.data_ptr(), mask_bias.data_ptr<float>(), out.data_ptr(), lse.data_ptr<float>(),
+  hx_attn_fwd(bf, qkv.data_ptr(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(), out.data_ptr(),
+              lse.data_ptr<float>(),
               keep < 1.0 ? reinterpret_cast<uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr, (int)B, (int)S, (int)nh,
               (float)keep, (uint64_t)seed, (uint64_t)stream, cur_stream(qkv));
   dbg_finite(out, "attn_fwd");
   return {out, lse, dmask};
 }
 
-Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
-                double keep) {
+// returns {dqkv, dbias} (dbias: [3H] fp32 when bias is given -- written into dbq/dbk/dbv
+// when those slots are given -- else an empty tensor)
+std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask,
+                             int64_t nh, double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv) {
   check_cuda(dout, "grad_output");
   check_cuda(qkv, "qkv");
   const int bf = act_bf16(qkv);
@@ -319,12 +327,29 @@ Tensor attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor ls
     dq_acc = dqkv.data_ptr<float>();
     dq_ld = (int)(3 * H);
   }
-  hx_attn_bwd(bf, qkv.data_ptr(), mask_bias.data_ptr<float>(), dout.data_ptr(), out.data_ptr(),
-              lse.data_ptr<float>(), keep < 1.0 ? reinterpret_cast<const uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr,
-              dqkv.data_ptr(), dq_acc, dq_ld, (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv));
+  Tensor dbias, part;
+  float *pq = nullptr, *pk = nullptr, *pv = nullptr;
+  if (has(bias)) {
+    const bool slots = has(dbq) && has(dbk) && has(dbv);
+    if (slots) {
+      for (const auto* t : {&dbq, &dbk, &dbv}) {
+        check_f32(**t, "qkv bias grad");
+        TORCH_CHECK((*t)->numel() == H, "qkv bias grad must have H elements");
+      }
+      pq = dbq->data_ptr<float>(); pk = dbk->data_ptr<float>(); pv = dbv->data_ptr<float>();
+    } else {
+      dbias = torch::empty({3 * H}, qkv.options().dtype(torch::kFloat32));
+      pq = dbias.data_ptr<float>(); pk = pq + H; pv = pq + 2 * H;
+    }
+    part = torch::empty({B * ((S + 127) / 128), 3 * H}, qkv.options().dtype(torch::kFloat32));
+  }
+  hx_attn_bwd(bf, qkv.data_ptr(), ptr_or_null<float>(bias), pq, pk, pv, part.defined() ? part.data_ptr<float>() : nullptr,
+              mask_bias.data_ptr<float>(), dout.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
+              keep < 1.0 ? reinterpret_cast<const uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr, dqkv.data_ptr(),
+              dq_acc, dq_ld, (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv));
   if (multi && bf) dqkv.narrow(-1, 0, H).copy_(dq32);
   dbg_finite(dqkv, "attn_bwd");
-  return dqkv;
+  return {dqkv, dbias};
 }
 
 }  // namespace

@@ -32,6 +32,7 @@
 // [row = lane][32 contiguous dims] operand reads hit 16 distinct 16-B slots.
 #include "hx_launch.h"
 #include "hx_vec.h"
+#include "hx_reduce.h"
 
 namespace {
 
@@ -53,6 +54,7 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
 }
 // accumulator register r of a 32x32 tile, lane half h -> row index
 __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+__device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
 
 // Forward dropout for accumulator register R of both 32-key sub-blocks: apply the
 // lane's decisions, and build the transposed bitmask word: a ballot over the wave
@@ -79,7 +81,8 @@ __device__ __forceinline__ void drop_step(f32x16& s0, f32x16& s1, const uint32_t
 // ============================================================================ forward
 // grid (S/128, nh, B), block 256 = 4 waves x 32 queries.
 template <typename T, bool kDrop>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_fwd_k(const T* __restrict__ qkv, const float* __restrict__ maskb,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void attn_fwd_k(const T* __restrict__ qkv, const float* __restrict__ qkv_bias,
+                                                const float* __restrict__ maskb,
                                                 T* __restrict__ out, float* __restrict__ lse,
                                                 uint32_t* __restrict__ dmask, int S, int nh, float keep,
                                                 uint64_t seed, uint64_t stream) {
@@ -107,7 +110,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     const T* qp = base + (int64_t)qc * H3 + hd * D + h * 32;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const float4 v = hx::load4(qp + 4 * i);
+      float4 v = hx::load4(qp + 4 * i);
+      if (qkv_bias) v = add4(v, *reinterpret_cast<const float4*>(qkv_bias + hd * D + h * 32 + 4 * i));
       qr[4 * i] = v.x * scale;
       qr[4 * i + 1] = v.y * scale;
       qr[4 * i + 2] = v.z * scale;
@@ -127,8 +131,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
       const int row = e >> 4, c4 = (e & 15) * 4;
       const int kr = kt + row < S ? kt + row : S - 1;
       const T* src = base + (int64_t)kr * H3 + hd * D + c4;
-      *reinterpret_cast<float4*>(&Ks[row * LDK + c4]) = hx::load4(src + H);
-      *reinterpret_cast<float4*>(&Vs[row * LDK + c4]) = hx::load4(src + 2 * H);
+      float4 kv = hx::load4(src + H), vv = hx::load4(src + 2 * H);
+      if (qkv_bias) {
+        kv = add4(kv, *reinterpret_cast<const float4*>(qkv_bias + H + hd * D + c4));
+        vv = add4(vv, *reinterpret_cast<const float4*>(qkv_bias + 2 * H + hd * D + c4));
+      }
+      *reinterpret_cast<float4*>(&Ks[row * LDK + c4]) = kv;
+      *reinterpret_cast<float4*>(&Vs[row * LDK + c4]) = vv;
     }
     if (tid < 64) Ms[tid] = kt + tid < S ? maskb[(int64_t)b * S + kt + tid] : -INFINITY;
     __syncthreads();
@@ -247,7 +256,8 @@ __device__ __forceinline__ f32x4 mfma16(float a, float b, f32x4 c) {
 }
 
 template <typename T, bool kDrop>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_k(const T* __restrict__ qkv, const float* __restrict__ maskb,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_k(const T* __restrict__ qkv, const float* __restrict__ qkv_bias,
+                                                float* __restrict__ dbias_part, const float* __restrict__ maskb,
                                                 const T* __restrict__ dout, const T* __restrict__ outp,
                                                 const float* __restrict__ lse, const uint32_t* __restrict__ dmask,
                                                 T* __restrict__ dqkv, float* __restrict__ dq_acc, int dq_ld,
@@ -278,7 +288,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int e = tid + i * 256;
     const int row = e >> 4, c4 = (e & 15) * 4;
     const int kr = kbase + row < S ? kbase + row : S - 1;
-    *reinterpret_cast<float4*>(&Ks[row * LDK + c4]) = hx::load4(base + (int64_t)kr * H3 + H + hd * D + c4);
+    float4 kv = hx::load4(base + (int64_t)kr * H3 + H + hd * D + c4);
+    if (qkv_bias) kv = add4(kv, *reinterpret_cast<const float4*>(qkv_bias + H + hd * D + c4));
+    *reinterpret_cast<float4*>(&Ks[row * LDK + c4]) = kv;
   }
   const int mykey = kbase + w * 32 + l32;     // key on this lane
   const int mykc = mykey < S ? mykey : S - 1;
@@ -287,7 +299,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const T* vp = base + (int64_t)mykc * H3 + 2 * H + hd * D + h * 32;
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const float4 v = hx::load4(vp + 4 * i);
+      float4 v = hx::load4(vp + 4 * i);
+      if (qkv_bias) v = add4(v, *reinterpret_cast<const float4*>(qkv_bias + 2 * H + hd * D + h * 32 + 4 * i));
       vr[4 * i] = v.x; vr[4 * i + 1] = v.y; vr[4 * i + 2] = v.z; vr[4 * i + 3] = v.w;
     }
   }
@@ -335,6 +348,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int r16 = lane & 15, k4 = lane >> 4;
 
   f32x16 dv0 = {0}, dv1 = {0}, dk0 = {0}, dk1 = {0};
+  float cq0 = 0.f, cq1 = 0.f;   // this lane's share of the dQ column sums (bias gradient)
 
   for (int qt = 0; qt < S; qt += 32) {
     __syncthreads();  // previous tile's LDS buffers are free
@@ -347,6 +361,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       float4 qv = qn[i];
+      if (qkv_bias) qv = add4(qv, *reinterpret_cast<const float4*>(qkv_bias + hd * D + sc4));
       qv.x *= scale; qv.y *= scale; qv.z *= scale; qv.w *= scale;
       *reinterpret_cast<float4*>(&Qs[(srow + 16 * i) * LDK + sc4]) = qv;
       *reinterpret_cast<float4*>(&dOs[(srow + 16 * i) * LDK + sc4]) = dn[i];
@@ -416,6 +431,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       if ((s & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
     const int q0 = qt + qh * 16 + 4 * k4;
+    if (dbias_part) {   // rows past S hold exact zeros (their P, hence dS, is 0)
+      cq0 += (qa0[0] + qa0[1]) + (qa0[2] + qa0[3]);
+      cq1 += (qa1[0] + qa1[1]) + (qa1[2] + qa1[3]);
+    }
     if (single) {
       T* dq = dqkv_b + q0 * H3 + dqa * 16 + r16;
 #pragma unroll
@@ -446,6 +465,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     hx::io<T>::st(dvp + (int64_t)key * H3 + l32, dv0[r]);
     hx::io<T>::st(dvp + (int64_t)key * H3 + 32 + l32, dv1[r]);
   }
+  if (dbias_part) {
+    // QKV-bias gradient = column sums of dQ, dK, dV.  Per workgroup: dK / dV over
+    // its 128 keys (accumulator rows), dQ over every query for its key block (the
+    // per-key-block dQ partials add up to dQ).  One row of 3H partials per
+    // (batch, key block); a fold kernel sums the rows into the bias-grad slots.
+    float sk0 = 0.f, sk1 = 0.f, sv0 = 0.f, sv1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sk0 += dk0[r]; sk1 += dk1[r]; sv0 += dv0[r]; sv1 += dv1[r];
+    }
+    sk0 += __shfl_xor(sk0, 32, 64); sk1 += __shfl_xor(sk1, 32, 64);
+    sv0 += __shfl_xor(sv0, 32, 64); sv1 += __shfl_xor(sv1, 32, 64);
+    cq0 += __shfl_xor(cq0, 16, 64); cq0 += __shfl_xor(cq0, 32, 64);
+    cq1 += __shfl_xor(cq1, 16, 64); cq1 += __shfl_xor(cq1, 32, 64);
+    cq0 *= scale;   // dQ = scale * dS.K (the accumulators are pre-scale)
+    cq1 *= scale;
+    __syncthreads();                          // every wave is done with dSs
+    float* red = dSs;                         // [4 waves][3][64]
+    if (lane < 32) {
+      red[(w * 3 + 1) * 64 + l32] = sk0; red[(w * 3 + 1) * 64 + 32 + l32] = sk1;
+      red[(w * 3 + 2) * 64 + l32] = sv0; red[(w * 3 + 2) * 64 + 32 + l32] = sv1;
+    }
+    if (lane < 16) {   // dQ columns dqa*16 + lane and dqa*16 + 16 + lane of this wave's query half
+      red[(w * 3) * 64 + dqa * 16 + lane] = cq0;
+      red[(w * 3) * 64 + dqa * 16 + 16 + lane] = cq1;
+    }
+    __syncthreads();
+    if (tid < 192) {
+      const int part = tid >> 6, c = tid & 63;
+      float v;
+      if (part == 0) {   // waves (0,1) own dQ columns 0..31, waves (2,3) own 32..63
+        const int wa = c < 32 ? 0 : 2;
+        v = red[(wa * 3) * 64 + c] + red[((wa + 1) * 3) * 64 + c];
+      } else {
+        v = (red[(0 * 3 + part) * 64 + c] + red[(1 * 3 + part) * 64 + c]) +
+            (red[(2 * 3 + part) * 64 + c] + red[(3 * 3 + part) * 64 + c]);
+      }
+      dbias_part[((int64_t)b * gridDim.x + blockIdx.x) * H3 + part * H + hd * D + c] = v;
+    }
+  }
 }
 
 }  // namespace
@@ -457,19 +516,21 @@ size_t hx_attn_bwd_smem_bytes() {
 namespace {
 
 template <typename T>
-void attn_fwd_t(const void* qkv, const float* maskb, void* out, float* lse, uint32_t* dmask, int B, int S, int nh,
-                float keep, uint64_t seed, uint64_t stream, hipStream_t s) {
+void attn_fwd_t(const void* qkv, const float* bias, const float* maskb, void* out, float* lse, uint32_t* dmask, int B,
+                int S, int nh, float keep, uint64_t seed, uint64_t stream, hipStream_t s) {
   dim3 grid((S + 127) / 128, nh, B);
   if (keep < 1.f)
-    attn_fwd_k<T, true><<<grid, 256, 0, s>>>((const T*)qkv, maskb, (T*)out, lse, dmask, S, nh, keep, seed, stream);
+    attn_fwd_k<T, true><<<grid, 256, 0, s>>>((const T*)qkv, bias, maskb, (T*)out, lse, dmask, S, nh, keep, seed,
+                                             stream);
   else
-    attn_fwd_k<T, false><<<grid, 256, 0, s>>>((const T*)qkv, maskb, (T*)out, lse, dmask, S, nh, keep, seed, stream);
+    attn_fwd_k<T, false><<<grid, 256, 0, s>>>((const T*)qkv, bias, maskb, (T*)out, lse, dmask, S, nh, keep, seed,
+                                              stream);
 }
 
 template <typename T>
-void attn_bwd_t(const void* qkv, const float* maskb, const void* dout, const void* out, const float* lse,
-                const uint32_t* dmask, void* dqkv, float* dq_acc, int dq_ld, int B, int S, int nh, float keep,
-                hipStream_t s) {
+void attn_bwd_t(const void* qkv, const float* bias, float* dbias_part, const float* maskb, const void* dout,
+                const void* out, const float* lse, const uint32_t* dmask, void* dqkv, float* dq_acc, int dq_ld, int B,
+                int S, int nh, float keep, hipStream_t s) {
   dim3 grid((S + 127) / 128, nh, B);
   const size_t smem = hx_attn_bwd_smem_bytes();
   static bool attr = false;
@@ -481,24 +542,31 @@ void attn_bwd_t(const void* qkv, const float* maskb, const void* dout, const voi
     attr = true;
   }
   if (keep < 1.f)
-    attn_bwd_k<T, true><<<grid, 256, smem, s>>>((const T*)qkv, maskb, (const T*)dout, (const T*)out, lse, dmask,
-                                                (T*)dqkv, dq_acc, dq_ld, S, nh, keep);
+    attn_bwd_k<T, true><<<grid, 256, smem, s>>>((const T*)qkv, bias, dbias_part, maskb, (const T*)dout,
+                                                (const T*)out, lse, dmask, (T*)dqkv, dq_acc, dq_ld, S, nh, keep);
   else
-    attn_bwd_k<T, false><<<grid, 256, smem, s>>>((const T*)qkv, maskb, (const T*)dout, (const T*)out, lse, dmask,
-                                                 (T*)dqkv, dq_acc, dq_ld, S, nh, keep);
+    attn_bwd_k<T, false><<<grid, 256, smem, s>>>((const T*)qkv, bias, dbias_part, maskb, (const T*)dout,
+                                                 (const T*)out, lse, dmask, (T*)dqkv, dq_acc, dq_ld, S, nh, keep);
 }
 
 }  // namespace
 
-void hx_attn_fwd(int bf16, const void* qkv, const float* maskb, void* out, float* lse, uint32_t* dmask, int B, int S,
-                 int nh, float keep, uint64_t seed, uint64_t stream, hipStream_t s) {
-  if (bf16) attn_fwd_t<uint16_t>(qkv, maskb, out, lse, dmask, B, S, nh, keep, seed, stream, s);
-  else attn_fwd_t<float>(qkv, maskb, out, lse, dmask, B, S, nh, keep, seed, stream, s);
+void hx_attn_fwd(int bf16, const void* qkv, const float* bias, const float* maskb, void* out, float* lse,
+                 uint32_t* dmask, int B, int S, int nh, float keep, uint64_t seed, uint64_t stream, hipStream_t s) {
+  if (bf16) attn_fwd_t<uint16_t>(qkv, bias, maskb, out, lse, dmask, B, S, nh, keep, seed, stream, s);
+  else attn_fwd_t<float>(qkv, bias, maskb, out, lse, dmask, B, S, nh, keep, seed, stream, s);
 }
 
-void hx_attn_bwd(int bf16, const void* qkv, const float* maskb, const void* dout, const void* out, const float* lse,
-                 const uint32_t* dmask, void* dqkv, float* dq_acc, int dq_ld, int B, int S, int nh, float keep,
-                 hipStream_t s) {
-  if (bf16) attn_bwd_t<uint16_t>(qkv, maskb, dout, out, lse, dmask, dqkv, dq_acc, dq_ld, B, S, nh, keep, s);
-  else attn_bwd_t<float>(qkv, maskb, dout, out, lse, dmask, dqkv, dq_acc, dq_ld, B, S, nh, keep, s);
+void hx_attn_bwd(int bf16, const void* qkv, const float* bias, float* dbq, float* dbk, float* dbv, float* dbias_part,
+                 const float* maskb, const void* dout, const void* out, const float* lse, const uint32_t* dmask,
+                 void* dqkv, float* dq_acc, int dq_ld, int B, int S, int nh, float keep, hipStream_t s) {
+  if (bf16)
+    attn_bwd_t<uint16_t>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv, dq_acc, dq_ld, B, S, nh, keep, s);
+  else
+    attn_bwd_t<float>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv, dq_acc, dq_ld, B, S, nh, keep, s);
+  if (dbias_part) {
+    // [B * key blocks][3H] partial rows -> dbq | dbk | dbv (H each)
+    const int H = nh * D;
+    hx::fold_rows(dbias_part, B * ((S + 127) / 128), 3 * (int64_t)H, 3 * H, H, dbq, dbk, dbv, 0, s);
+  }
 }

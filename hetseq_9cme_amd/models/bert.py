@@ -186,9 +186,12 @@ class BertSelfAttention(nn.Module):
         self.dropout = nn.Dropout(config.attention_probs_dropout_prob)
 
     def forward(self, hidden_states, attention_mask_bias, res_grad=None):
+        # bias-less N=3H projection GEMM; the Q/K/V biases are applied (and their
+        # gradients produced) inside the fused attention
         qkv = ops.linear3(hidden_states, self.query.weight, self.key.weight, self.value.weight,
-                          self.query.bias, self.key.bias, self.value.bias, res_grad=res_grad)
-        return ops.attention(qkv, attention_mask_bias, self.num_attention_heads, self.dropout.p, self.training)
+                          None, None, None, res_grad=res_grad)
+        return ops.attention(qkv, attention_mask_bias, self.num_attention_heads, self.dropout.p, self.training,
+                             bias=(self.query.bias, self.key.bias, self.value.bias))
 
 
 class BertSelfOutput(nn.Module):

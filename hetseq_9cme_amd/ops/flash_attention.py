@@ -49,25 +49,62 @@ def _fused_ok(qkv, num_heads):
     return qkv.dtype in (torch.float32, torch.bfloat16) and d == 64 and S >= 1
 
 
+def _bias3(bq, bk, bv):
+    """[3H] view over the adjacent Q/K/V bias storage (FlatParamSpace keeps them
+    back to back), or a concatenated copy."""
+    from .fused import _adjacent_view
+    v = _adjacent_view([bq, bk, bv])
+    return v if v is not None else torch.cat([bq, bk, bv], 0)
+
+
 class _AttnFn(torch.autograd.Function):
+    """Fused attention; with ``bq/bk/bv`` the QKV-projection bias is added to
+    Q/K/V inside the kernels as they are loaded (the projection GEMM runs
+    without a bias epilogue) and its gradient -- the column sums of dQ/dK/dV --
+    comes out of the backward kernel's registers, straight into the flat
+    gradient slots, instead of a separate pass over the [B*S, 3H] gradient."""
+
     @staticmethod
-    def forward(ctx, qkv, mask_bias, num_heads, p):
+    def forward(ctx, qkv, mask_bias, bq, bk, bv, num_heads, p):
+        from .fused import grad_slot  # noqa: F401  (import cycle guard)
         keep = 1.0 - p
         seed, stream = get_rng().next() if p > 0 else (0, 0)
-        out, lse, dmask = C().attn_fwd(qkv, mask_bias, num_heads, keep, seed, stream)
+        bias = _bias3(bq, bk, bv).float().contiguous() if bq is not None else None
+        out, lse, dmask = C().attn_fwd(qkv, mask_bias, num_heads, keep, seed, stream, bias)
         ctx.save_for_backward(qkv, mask_bias, out, lse, dmask)
+        ctx.bias = bias
+        ctx.bparams = (bq, bk, bv)
         ctx.meta = (num_heads, keep)
         return out
 
     @staticmethod
     def backward(ctx, dout):
+        from .fused import grad_slot
         qkv, mask_bias, out, lse, dmask = ctx.saved_tensors
         num_heads, keep = ctx.meta
-        dqkv = C().attn_bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep)
-        return dqkv, None, None, None
+        bq, bk, bv = ctx.bparams
+        slots = [None, None, None]
+        if ctx.bias is not None:
+            slots = [grad_slot(t) for t in (bq, bk, bv)]
+            if not all(t is not None for t in slots):
+                slots = [None, None, None]
+        dqkv, dbias = C().attn_bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep, ctx.bias,
+                                   *slots)
+        if ctx.bias is None:
+            return dqkv, None, None, None, None, None, None
+        if slots[0] is not None:
+            db = slots
+        else:
+            H = dbias.numel() // 3
+            db = [dbias[:H].view_as(bq), dbias[H:2 * H].view_as(bk), dbias[2 * H:].view_as(bv)]
+        return dqkv, None, db[0], db[1], db[2], None, None
 
 
-def attention(qkv, mask_bias, num_heads, p):
+def attention(qkv, mask_bias, num_heads, p, bias=None):
+    """``bias``: optional (bq, bk, bv) of the QKV projection, applied here."""
     if _fused_ok(qkv, num_heads):
-        return _AttnFn.apply(qkv.contiguous(), mask_bias.float().contiguous(), int(num_heads), float(p))
+        bq, bk, bv = bias if bias is not None else (None, None, None)
+        return _AttnFn.apply(qkv.contiguous(), mask_bias.float().contiguous(), bq, bk, bv, int(num_heads), float(p))
+    if bias is not None:
+        qkv = qkv + torch.cat(list(bias), 0).to(qkv.dtype)
     return attention_ref(qkv, mask_bias, num_heads, p)

@@ -419,23 +419,27 @@ class _Linear3Fn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, wq, wk, wv, bq, bk, bv, mbox):
+        has_b = bq is not None
         W = _adjacent_view([wq, wk, wv])
         if W is None:
             W = torch.cat([wq, wk, wv], 0)
-        b = _adjacent_view([bq, bk, bv])
-        if b is None:
-            b = torch.cat([bq, bk, bv], 0)
+        b = None
+        if has_b:
+            b = _adjacent_view([bq, bk, bv])
+            if b is None:
+                b = torch.cat([bq, bk, bv], 0)
         Wc, bc = W, b
         if x.dtype != W.dtype:
-            sh = [getattr(t, '_hx_bf16', None) for t in (wq, wk, wv, bq, bk, bv)]
-            Wc = _adjacent_view(sh[:3]) if all(t is not None for t in sh) else None
-            bc = _adjacent_view(sh[3:]) if all(t is not None for t in sh) else None
+            sh = [getattr(t, '_hx_bf16', None) for t in (wq, wk, wv)]
+            Wc = _adjacent_view(sh) if all(t is not None for t in sh) else None
             Wc = Wc if Wc is not None else W.to(x.dtype)
-            bc = bc if bc is not None else b.to(x.dtype)
+            bc = cast_w(b, x.dtype) if has_b else None
         x2 = x.reshape(-1, x.shape[-1])
-        y = torch.addmm(bc, x2, Wc.t())
+        # without biases (applied inside the fused attention instead) this is a plain GEMM
+        y = torch.addmm(bc, x2, Wc.t()) if has_b else torch.mm(x2, Wc.t())
         ctx.save_for_backward(x2, Wc)
         ctx.params = (wq, wk, wv, bq, bk, bv)
+        ctx.has_b = has_b
         ctx.mbox = mbox
         ctx.xshape = x.shape
         ctx.n = [wq.shape[0], wk.shape[0], wv.shape[0]]
@@ -451,9 +455,10 @@ class _Linear3Fn(torch.autograd.Function):
         # weight grads: ONE GEMM straight into the three adjacent flat slots when possible
         ws = [grad_slot(w) for w in (wq, wk, wv)]
         fused = _adjacent_view(ws) if all(t is not None for t in ws) else None
-        bs = [grad_slot(t) for t in (bq, bk, bv)]
+        has_b = ctx.has_b
+        bs = [grad_slot(t) for t in (bq, bk, bv)] if has_b else [None, None, None]
         fb = _adjacent_view(bs) if all(t is not None for t in bs) else None
-        direct = fused is not None and fb is not None
+        direct = fused is not None and (fb is not None or not has_b)
         side = side_begin(dy2.device) if direct else None
         with torch.cuda.stream(side) if side is not None else _nullctx():
             if fused is not None:
@@ -466,13 +471,17 @@ class _Linear3Fn(torch.autograd.Function):
                     if t is not None:
                         t.copy_(gW[k])
                         gW[k] = t
-            if use_kernels(dy2) and dy2.shape[-1] % 4 == 0:
-                db = C().colsum(dy2.contiguous(), None, fb)
-            else:
-                db = dy2.float().sum(0)
+            db = None
+            if has_b:
+                if use_kernels(dy2) and dy2.shape[-1] % 4 == 0:
+                    db = C().colsum(dy2.contiguous(), None, fb)
+                else:
+                    db = dy2.float().sum(0)
         if side is not None:
             dy2.record_stream(side)
             x2.record_stream(side)
+        if not has_b:
+            return (dx, gW[0], gW[1], gW[2], None, None, None, None)
         gb = bs if fb is not None else [db[:a], db[a:a + b_], db[a + b_:]]
         return (dx, gW[0], gW[1], gW[2], gb[0], gb[1], gb[2], None)
 
@@ -482,12 +491,13 @@ def linear3(x, wq, wk, wv, bq, bk, bv, res_grad=None):
 
 
 # ----------------------------------------------------------------- attention core
-def attention(qkv, mask_bias, num_heads, p, training):
+def attention(qkv, mask_bias, num_heads, p, training, bias=None):
     """softmax(Q K^T / sqrt(d) + mask) -> dropout -> @ V  on the packed [B, S, 3H]
     projection; returns [B, S, H] (reference BertSelfAttention, :351-377).
-    ``mask_bias`` is the additive [B, S] key mask ((1 - m) * -10000)."""
+    ``mask_bias`` is the additive [B, S] key mask ((1 - m) * -10000); ``bias`` the
+    optional (bq, bk, bv) of a bias-less QKV projection, added inside the kernel."""
     from .flash_attention import attention as _attention
-    return _attention(qkv, mask_bias, num_heads, p if training else 0.0)
+    return _attention(qkv, mask_bias, num_heads, p if training else 0.0, bias)
 
 
 # ----------------------------------------------------------------- MLM decoder + softmax-xent

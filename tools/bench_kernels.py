@@ -44,14 +44,14 @@ def bench_attn(B, S, nh=12, keep=0.9):
     d = 64
     qkv = torch.randn(B, S, 3 * nh * d, device='cuda')
     mb = torch.zeros(B, S, device='cuda')
-    out, lse, dm = C().attn_fwd(qkv, mb, nh, keep, 1, 0)
+    out, lse, dm = C().attn_fwd(qkv, mb, nh, keep, 1, 0, None)
     dout = torch.randn_like(out)
     f_fwd = 2 * 2 * B * nh * S * S * d
-    report('attn_fwd', timeit(lambda: C().attn_fwd(qkv, mb, nh, keep, 1, 0)), flops=f_fwd)
-    report('attn_fwd (no dropout)', timeit(lambda: C().attn_fwd(qkv, mb, nh, 1.0, 1, 0)), flops=f_fwd)
-    report('attn_bwd', timeit(lambda: C().attn_bwd(dout, qkv, mb, out, lse, dm, nh, keep)), flops=2.5 * f_fwd)
-    out1, lse1, dm1 = C().attn_fwd(qkv, mb, nh, 1.0, 1, 0)
-    report('attn_bwd (no dropout)', timeit(lambda: C().attn_bwd(dout, qkv, mb, out1, lse1, dm1, nh, 1.0)),
+    report('attn_fwd', timeit(lambda: C().attn_fwd(qkv, mb, nh, keep, 1, 0, None)), flops=f_fwd)
+    report('attn_fwd (no dropout)', timeit(lambda: C().attn_fwd(qkv, mb, nh, 1.0, 1, 0, None)), flops=f_fwd)
+    report('attn_bwd', timeit(lambda: C().attn_bwd(dout, qkv, mb, out, lse, dm, nh, keep, None, None, None, None)[0]), flops=2.5 * f_fwd)
+    out1, lse1, dm1 = C().attn_fwd(qkv, mb, nh, 1.0, 1, 0, None)
+    report('attn_bwd (no dropout)', timeit(lambda: C().attn_bwd(dout, qkv, mb, out1, lse1, dm1, nh, 1.0, None, None, None, None)[0]),
            flops=2.5 * f_fwd)
 
 

@@ -118,6 +118,36 @@ struct io<uint16_t> {
   __device__ __forceinline__ static void st(uint16_t* p, float v) { *p = f2bf(v); }
 };
 
+// Buffer-resource IO: a scalar (SGPR) descriptor over `bytes` bytes, a per-lane 32-bit
+// byte offset and a wave-uniform byte offset.  Unrolled strided loops then issue
+// `buffer_load v, v_off, s[rsrc], s_off` instead of materialising one 64-bit VGPR
+// address per element; loads past `bytes` return 0 and stores past it are dropped.
+struct Buf {
+  __amdgpu_buffer_rsrc_t r;
+  __device__ __forceinline__ Buf(const void* p, uint32_t bytes)
+      : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000)) {}
+};
+template <typename T>
+struct bio;
+template <>
+struct bio<float> {
+  __device__ __forceinline__ static float ld(const Buf& b, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(b.r, voff * 4, soff * 4, 0));
+  }
+  __device__ __forceinline__ static void st(const Buf& b, uint32_t voff, uint32_t soff, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), b.r, voff * 4, soff * 4, 0);
+  }
+};
+template <>
+struct bio<uint16_t> {
+  __device__ __forceinline__ static float ld(const Buf& b, uint32_t voff, uint32_t soff) {
+    return bf2f(__builtin_amdgcn_raw_buffer_load_b16(b.r, voff * 2, soff * 2, 0));
+  }
+  __device__ __forceinline__ static void st(const Buf& b, uint32_t voff, uint32_t soff, float v) {
+    __builtin_amdgcn_raw_buffer_store_b16(f2bf(v), b.r, voff * 2, soff * 2, 0);
+  }
+};
+
 // GELU as in the reference: x * 0.5 * (1 + erf(x / 1.41421))  (bert_modeling.py:104-111)
 __device__ __forceinline__ float gelu_f(float x) { return x * 0.5f * (1.0f + erff(x * (1.0f / 1.41421f))); }
 __device__ __forceinline__ float gelu_grad_f(float x) {

@@ -10,8 +10,10 @@
 //   * overwrites the logits IN PLACE with softmax(z) - onehot(label)  (0 for
 //     ignored rows) -- the unscaled gradient, so backward needs no extra buffer.
 // Backward then only scales rows by dL/dloss / count and folds the bias gradient
-// (hx_colsum with a device scale).  One workgroup per row; V = 30522 -> 120 columns
-// per lane, two reads + one write of the row.
+// (hx_colsum with a device scale).  One workgroup per row; for V <= 32768 (BERT:
+// 30522 -> 120 columns per lane) the row stays in registers between the max, sum
+// and write passes: one read + one write of the 122 KB row, one exp per element.
+// Larger vocabularies use the two-read online-softmax variant.
 #include "hx_launch.h"
 #include "hx_vec.h"
 
@@ -79,13 +81,111 @@ __global__ __launch_bounds__(NT) void softmax_xent_k(T* __restrict__ logits, con
   if ((int)(lab % NT) == (int)threadIdx.x) loss[row] = lse - zl;
 }
 
+// Register-resident row (NR threads): lane t holds columns t, t + NR, ..., t + (K-1)*NR.
+// Buffer loads/stores (hx::Buf): one lane offset + a uniform offset per chunk, so the
+// K values are the only per-element registers; out-of-row stores are dropped by the
+// descriptor's range.
+template <typename T, int NR, int K, bool kBias>
+__global__ __launch_bounds__(NR) __attribute__((amdgpu_waves_per_eu(8, 8))) void softmax_xent_reg_k(
+    T* __restrict__ logits, const float* __restrict__ bias, const int64_t* __restrict__ labels,
+    float* __restrict__ loss, int V, int64_t ld, int64_t ignore_index) {
+  __shared__ float red[NR / 64];
+  const int64_t row = blockIdx.x;
+  const hx::Buf xb(logits + row * ld, (uint32_t)V * sizeof(T));
+  const int64_t lab = labels[row];
+  const bool valid = lab != ignore_index && lab >= 0 && lab < V;
+  const int t = threadIdx.x, w = t >> 6;
+  if (!valid) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) hx::bio<T>::st(xb, t, k * NR, 0.f);
+    if (t == 0) loss[row] = 0.f;
+    return;
+  }
+  float v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) v[k] = hx::bio<T>::ld(xb, t, k * NR);
+  if constexpr (kBias) {
+    const hx::Buf bb(bias, (uint32_t)V * 4);
+    // in groups of 8 behind scheduling barriers: the bias loads (L2 hits) never need
+    // K more registers while the row loads are in flight
+#pragma unroll
+    for (int k0 = 0; k0 < K; k0 += 8) {
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int k = k0; k < k0 + 8 && k < K; ++k) v[k] += hx::bio<float>::ld(bb, t, k * NR);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    // padding columns load as 0: mask them, behind a wave-uniform test so full chunks
+    // carry no per-element select (and no second copy of the value)
+    if ((k + 1) * NR > V) v[k] = t + k * NR < V ? v[k] : -INFINITY;
+    m = fmaxf(m, v[k]);
+  }
+  m = hx::wave_max(m);
+  if ((t & 63) == 0) red[w] = m;
+  __syncthreads();
+  float M = red[0];
+#pragma unroll
+  for (int i = 1; i < NR / 64; ++i) M = fmaxf(M, red[i]);
+  __syncthreads();
+  // the label's logit (wave-uniform address: scalar loads)
+  const float zl = hx::io<T>::ld(logits + row * ld + lab) + (kBias ? bias[lab] : 0.f);
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    v[k] = __expf(v[k] - M);   // exp(-inf) = 0 for the padding columns
+    s += v[k];
+  }
+  s = hx::wave_sum(s);
+  if ((t & 63) == 0) red[w] = s;
+  __syncthreads();
+  float S = 0.f;
+#pragma unroll
+  for (int i = 0; i < NR / 64; ++i) S += red[i];
+  const float inv = 1.f / S;
+#pragma unroll
+  for (int k = 0; k < K; ++k) hx::bio<T>::st(xb, t, k * NR, v[k] * inv);
+  // the lane that just wrote the label's column rewrites it as p - 1 (same lane, same
+  // address: ordered after its own store)
+  if ((int)(lab % NR) == t) {
+    hx::bio<T>::st(xb, (uint32_t)lab, 0, __expf(zl - M) * inv - 1.f);
+    loss[row] = M + __logf(S) - zl;
+  }
+}
+
 }  // namespace
 
 void hx_softmax_xent(int bf16, void* logits, const float* bias, const int64_t* labels, float* loss, int64_t rows,
                      int V, int64_t ld, int64_t ignore_index, hipStream_t s) {
   if (rows <= 0) return;
-  if (bf16)
+#define HX_XENT_REG2(NRR, KK, BB)                                                                            \
+  if (bf16)                                                                                                 \
+    softmax_xent_reg_k<uint16_t, NRR, KK, BB>                                                               \
+        <<<(unsigned)rows, NRR, 0, s>>>((uint16_t*)logits, bias, labels, loss, V, ld, ignore_index);        \
+  else                                                                                                      \
+    softmax_xent_reg_k<float, NRR, KK, BB>                                                                  \
+        <<<(unsigned)rows, NRR, 0, s>>>((float*)logits, bias, labels, loss, V, ld, ignore_index);
+#define HX_XENT_REG(NRR, KK) \
+  if (bias) {                \
+    HX_XENT_REG2(NRR, KK, true) \
+  } else {                   \
+    HX_XENT_REG2(NRR, KK, false) \
+  }
+  // 1024 threads x 32 columns: ~60 VGPRs, so two rows (32 waves) are in flight per CU
+  if (V <= 16 * 256) {
+    HX_XENT_REG(256, 16)
+  } else if (V <= 16 * 1024) {
+    HX_XENT_REG(1024, 16)
+  } else if (V <= 32 * 1024) {
+    HX_XENT_REG(1024, 32)
+  } else if (bf16) {
     softmax_xent_k<uint16_t><<<(unsigned)rows, NT, 0, s>>>((uint16_t*)logits, bias, labels, loss, V, ld, ignore_index);
-  else
+  } else {
     softmax_xent_k<float><<<(unsigned)rows, NT, 0, s>>>((float*)logits, bias, labels, loss, V, ld, ignore_index);
+  }
+#undef HX_XENT_REG
+#undef HX_XENT_REG2
 }

@@ -134,6 +134,30 @@ def test_decoder_xent(dev):
     _close(b.grad, br.grad, rtol=1e-3, atol=1e-6)
 
 
+@pytest.mark.parametrize('V', [1000, 10000, 30522, 40000])
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_softmax_xent_kernel(dev, V, dtype):
+    """In-place bias + softmax-xent + gradient; V picks the register-resident variants
+    (<= 4096, <= 16384, <= 32768) or the two-pass fallback."""
+    from hetseq_9cme_amd.ops._ext import C
+    torch.manual_seed(0)
+    rows = 37
+    z = (3 * torch.randn(rows, V, device=dev)).to(dtype)
+    labels = torch.randint(0, V, (rows,), device=dev)
+    labels[::4] = -1
+    labels[1] = V - 1
+    for bias in (0.1 * torch.randn(V, device=dev), None):
+        zz = z.clone()
+        loss = C().softmax_xent_(zz, bias, labels, -1)
+        zr = z.float() + (bias if bias is not None else 0)
+        ref = F.cross_entropy(zr, labels, ignore_index=-1, reduction='none')
+        _close(loss, ref, rtol=1e-4, atol=1e-4)
+        gref = torch.softmax(zr, -1) - F.one_hot(labels.clamp(min=0), V).float()
+        gref[labels == -1] = 0
+        tol = 1e-6 if dtype == torch.float32 else 4e-3
+        _close(zz.float(), gref, rtol=1e-3 if dtype == torch.float32 else 2e-2, atol=tol)
+
+
 def test_linear3(dev):
     torch.manual_seed(0)
     x = torch.randn(2, 50, 768, device=dev, requires_grad=True)

@@ -92,11 +92,22 @@ def bench_adam(n=110_000_000):
            bytes_=7 * n * 4)
 
 
+def bench_xent(rows=2560, V=30522):
+    """MLM decoder bias + softmax-xent + gradient, in place (rows = 128 x 20 masked positions)."""
+    src = torch.randn(rows, V, device='cuda') * 3
+    z = src.clone()
+    bias = torch.randn(V, device='cuda') * 0.1
+    lab = torch.randint(0, V, (rows,), device='cuda')
+    copy = timeit(lambda: z.copy_(src))
+    both = timeit(lambda: (z.copy_(src), C().softmax_xent_(z, bias, lab, -1)))
+    report('softmax_xent({}x{})'.format(rows, V), both - copy, bytes_=2 * rows * V * 4)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--batch', type=int, default=128)
     ap.add_argument('--seq', type=int, default=128)
-    ap.add_argument('--only', default='attn,ln,ffn,adam')
+    ap.add_argument('--only', default='attn,ln,ffn,adam,xent')
     a = ap.parse_args()
     torch.manual_seed(0)
     which = a.only.split(',')
@@ -108,6 +119,8 @@ def main():
         bench_ffn_act(a.batch, a.seq)
     if 'adam' in which:
         bench_adam()
+    if 'xent' in which:
+        bench_xent(a.batch * 20)
 
 
 if __name__ == '__main__':

@@ -103,9 +103,15 @@ def build_data_native(force=False):
     out_so = os.path.join(HERE, '_data_native' + EXT)
     if force or _newer(out_so, [src]):
         py_inc = sysconfig.get_paths()['include']
+        # the compiler's own libstdc++ directory goes first in the rpath: the HDF5 prefix
+        # (/opt/conda/lib) ships an older libstdc++ that lacks symbols g++ 11 emits, and
+        # the module must import on its own (data workers), not only after torch
+        stdcxx = os.path.dirname(os.path.realpath(
+            subprocess.run(['g++', '-print-file-name=libstdc++.so.6'], stdout=subprocess.PIPE,
+                           text=True).stdout.strip()))
         _run(['g++', '-O3', '-std=c++17', '-fPIC', '-shared', src, '-o', out_so, '-I' + _pybind_inc(),
               '-I' + py_inc, '-I' + os.path.join(HDF5_ROOT, 'include'), '-L' + os.path.join(HDF5_ROOT, 'lib'),
-              '-lhdf5', '-Wl,-rpath,' + os.path.join(HDF5_ROOT, 'lib'), '-pthread'])
+              '-lhdf5', '-Wl,-rpath,' + stdcxx, '-Wl,-rpath,' + os.path.join(HDF5_ROOT, 'lib'), '-pthread'])
     return out_so
 
 

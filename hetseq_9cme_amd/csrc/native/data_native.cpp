@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstring>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -277,8 +278,72 @@ static void write_bert_shard(const std::string& path, I32 input_ids, I32 input_m
   write_dataset(f, "next_sentence_labels", next_sentence_labels.data(), 1, d_n, gzip);
 }
 
+// ---------------------------------------------------------------------------
+// CRC32C (Castagnoli) for TF checkpoint bundles (utils/tf_checkpoint.py): the
+// SSE4.2 crc32 instruction 8 bytes at a time when the host has it, else a
+// slicing-by-8 table.  GIL released: checksumming a 440 MB BERT checkpoint takes
+// ~50 ms instead of minutes in Python.
+// ---------------------------------------------------------------------------
+namespace {
+struct Crc32cTables {
+  uint32_t t[8][256];
+  Crc32cTables() {
+    for (uint32_t i = 0; i < 256; ++i) {
+      uint32_t c = i;
+      for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1) ? 0x82F63B78u : 0u);
+      t[0][i] = c;
+    }
+    for (uint32_t i = 0; i < 256; ++i)
+      for (int s = 1; s < 8; ++s) t[s][i] = (t[s - 1][i] >> 8) ^ t[0][t[s - 1][i] & 0xFF];
+  }
+};
+
+uint32_t crc32c_table(uint32_t crc, const uint8_t* p, size_t n) {
+  static const Crc32cTables tb;
+  while (n >= 8) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    v ^= crc;
+    crc = tb.t[7][v & 0xFF] ^ tb.t[6][(v >> 8) & 0xFF] ^ tb.t[5][(v >> 16) & 0xFF] ^ tb.t[4][(v >> 24) & 0xFF] ^
+          tb.t[3][(v >> 32) & 0xFF] ^ tb.t[2][(v >> 40) & 0xFF] ^ tb.t[1][(v >> 48) & 0xFF] ^ tb.t[0][v >> 56];
+    p += 8;
+    n -= 8;
+  }
+  while (n--) crc = tb.t[0][(crc ^ *p++) & 0xFF] ^ (crc >> 8);
+  return crc;
+}
+
+#if defined(__x86_64__)
+__attribute__((target("sse4.2"))) uint32_t crc32c_hw(uint32_t crc, const uint8_t* p, size_t n) {
+  uint64_t c = crc;
+  while (n >= 8) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    c = __builtin_ia32_crc32di(c, v);
+    p += 8;
+    n -= 8;
+  }
+  uint32_t c32 = static_cast<uint32_t>(c);
+  while (n--) c32 = __builtin_ia32_crc32qi(c32, *p++);
+  return c32;
+}
+#endif
+}  // namespace
+
+static uint32_t crc32c(py::array_t<uint8_t, py::array::c_style | py::array::forcecast> data, uint32_t init) {
+  const uint8_t* p = data.data();
+  const size_t n = static_cast<size_t>(data.size());
+  py::gil_scoped_release nogil;
+  uint32_t crc = ~init;
+#if defined(__x86_64__)
+  if (__builtin_cpu_supports("sse4.2")) return ~crc32c_hw(crc, p, n);
+#endif
+  return ~crc32c_table(crc, p, n);
+}
+
 PYBIND11_MODULE(_data_native, m) {
-  m.doc() = "hetseq_9cme_amd native data runtime (batch packing, HDF5 shard IO)";
+  m.doc() = "hetseq_9cme_amd native data runtime (batch packing, HDF5 shard IO, crc32c)";
+  m.def("crc32c", &crc32c, py::arg("data"), py::arg("init") = 0u);
   m.def("batch_by_size", &batch_by_size, py::arg("indices"), py::arg("num_tokens"), py::arg("max_tokens"),
         py::arg("max_sentences"), py::arg("bsz_mult"));
   py::class_<BertShardReader>(m, "BertShardReader")

@@ -163,3 +163,81 @@ class ConBertH5pyData(torch.utils.data.Dataset):
 
     def set_epoch(self, epoch):
         pass
+
+
+class CombineBertData(torch.utils.data.Dataset):
+    """Eager in-memory loader over many shards (reference hetseq/data/BERT_DATA.py:11-43,
+    ``CombineBertData``).
+
+    The reference reads every key of every shard into RAM with h5py, one file after
+    another (its own comment: ~20 GB and ~25 min for Wikipedia).  Here each shard is
+    read key by key through the native reader (GIL released) on a thread pool, and
+    the arrays are concatenated once.  ``__getitem__`` returns the raw key tuple in
+    the reference's order ``keys``; ``read_batch`` builds the same collated
+    training batch as :class:`BertH5pyData` (masked-LM labels from positions/ids),
+    so the in-memory variant is a drop-in for the streaming one when a corpus fits
+    in host memory.
+    """
+
+    DEFAULT_KEYS = ('input_ids', 'input_mask', 'segment_ids', 'masked_lm_positions', 'masked_lm_ids',
+                    'next_sentence_labels')
+
+    def __init__(self, files, max_pred_length=512, keys=DEFAULT_KEYS, num_threads=8):
+        super().__init__()
+        from concurrent.futures import ThreadPoolExecutor
+        self.max_pred_length = max_pred_length
+        self.keys = tuple(keys)
+        files = list(files)
+        assert len(files) > 0, 'no shard files given'
+
+        def load(path):
+            r = _native().BertShardReader(path)
+            try:
+                n = len(r)
+                return {k: r.read_key(k, 0, n) for k in self.keys}
+            finally:
+                r.close()
+
+        with ThreadPoolExecutor(max_workers=max(1, min(num_threads, len(files)))) as ex:
+            parts = list(ex.map(load, files))
+        self.inputs = {k: np.concatenate([p[k] for p in parts]) for k in self.keys}
+        self.seq_len = int(self.inputs[self.keys[0]].shape[1])
+        self.max_pred = int(self.inputs['masked_lm_positions'].shape[1]) \
+            if 'masked_lm_positions' in self.inputs else 0
+        self.fixed_num_tokens = max_pred_length
+
+    def __len__(self):
+        return len(self.inputs[self.keys[0]])
+
+    def __getitem__(self, index):
+        return [self.inputs[key][index] for key in self.keys]
+
+    def read_batch(self, indices, pin_memory=False, out=None):
+        idx = np.asarray(indices, dtype=np.int64)
+        ids = self.inputs['input_ids'][idx]
+        pos = self.inputs['masked_lm_positions'][idx]
+        mid = self.inputs['masked_lm_ids'][idx]
+        labels = np.full_like(ids, -1)
+        # first zero position ends the prediction list (h5pyDataset.py:47-53)
+        valid = np.cumprod(pos != 0, axis=1).astype(bool)
+        rows = np.broadcast_to(np.arange(len(idx))[:, None], pos.shape)
+        labels[rows[valid], pos[valid]] = mid[valid]
+        arrays = [ids, self.inputs['segment_ids'][idx], self.inputs['input_mask'][idx], labels,
+                  self.inputs['next_sentence_labels'][idx].reshape(-1)]
+        if out is None:
+            out = [torch.empty(a.shape, dtype=torch.int64, pin_memory=pin_memory) for a in arrays]
+        for t, a in zip(out, arrays):
+            t.copy_(torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64)))
+        return out
+
+    def size(self, idx):
+        return self.max_pred_length
+
+    def num_tokens(self, index):
+        return self.max_pred_length
+
+    def ordered_indices(self):
+        return np.arange(len(self))
+
+    def set_epoch(self, epoch):
+        pass

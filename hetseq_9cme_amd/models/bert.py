@@ -40,6 +40,12 @@ logger = logging.getLogger(__name__)
 
 CONFIG_NAME = 'bert_config.json'
 WEIGHTS_NAME = 'pytorch_model.bin'
+# short names -> the archive URLs the reference downloads (bert_modeling.py:30-38); here they
+# resolve only through a pre-populated offline cache (utils.file_utils.cached_path)
+_S3 = 'https://s3.amazonaws.com/models.huggingface.co/bert/{}.tar.gz'
+PRETRAINED_MODEL_ARCHIVE_MAP = {n: _S3.format(n) for n in (
+    'bert-base-uncased', 'bert-large-uncased', 'bert-base-cased', 'bert-large-cased',
+    'bert-base-multilingual-uncased', 'bert-base-multilingual-cased', 'bert-base-chinese')}
 
 
 def gelu(x):
@@ -386,6 +392,115 @@ _KEY_RENAMES = [
 ]
 
 
+TF_WEIGHTS_NAME = 'model.ckpt'
+_TF_SKIP = ('adam_v', 'adam_m', 'AdamWeightDecayOptimizer', 'AdamWeightDecayOptimizer_1', 'global_step',
+            'bad_steps', 'good_steps', 'loss_scale')
+
+
+def _tf_resolve(model, name):
+    """Walk a TF variable name (``bert/encoder/layer_3/attention/self/query/kernel``)
+    down the module tree with the reference's rules (bert_modeling.py:66-93):
+    ``kernel``/``gamma``/``output_weights`` -> weight, ``beta``/``output_bias`` ->
+    bias, ``name_N`` -> ``name[N]``, ``*_embeddings`` -> its ``.weight``, and a
+    ``kernel`` is transposed.  One fix: TF's ``dense`` resolves to this schema's
+    ``dense_act`` (``LinearActivation``) where a module has no ``dense`` -- the
+    reference raises AttributeError on the intermediate / pooler / MLM-transform
+    layers of Google's checkpoints because of that rename."""
+    import re
+    pointer, transpose = model, False
+    parts = name.split('/')
+    for m_name in parts:
+        if re.fullmatch(r'[A-Za-z]+_\d+', m_name):
+            l = re.split(r'_(\d+)', m_name)
+        else:
+            l = [m_name]
+        if l[0] in ('kernel', 'gamma', 'output_weights'):
+            pointer = getattr(pointer, 'weight')
+        elif l[0] in ('output_bias', 'beta'):
+            pointer = getattr(pointer, 'bias')
+        elif l[0] == 'dense' and not hasattr(pointer, 'dense') and hasattr(pointer, 'dense_act'):
+            pointer = getattr(pointer, 'dense_act')
+        elif l[0] == 'squad' and not hasattr(pointer, 'squad') and hasattr(pointer, 'classifier'):
+            pointer = getattr(pointer, 'classifier')
+        else:
+            pointer = getattr(pointer, l[0])
+        if len(l) >= 2:
+            pointer = pointer[int(l[1])]
+    if parts[-1].endswith('_embeddings'):
+        pointer = getattr(pointer, 'weight')
+    elif parts[-1] == 'kernel':
+        transpose = True
+    return pointer, transpose
+
+
+def load_tf_weights_in_bert(model, tf_checkpoint_path):
+    """Load a TensorFlow BERT checkpoint into ``model`` (reference
+    bert_modeling.py:43-101) without tensorflow: the bundle is decoded by
+    ``utils.tf_checkpoint``.  Values are copied into the existing parameter
+    storage (flat-buffer views stay valid); optimizer slots and step counters are
+    skipped."""
+    from ..utils.tf_checkpoint import TFCheckpointReader
+    reader = TFCheckpointReader(tf_checkpoint_path)
+    logger.info('Converting TensorFlow checkpoint from %s', reader.prefix)
+    loaded = []
+    for name, shape in reader.list_variables():
+        if any(n in _TF_SKIP for n in name.split('/')):
+            logger.info('Skipping %s', name)
+            continue
+        pointer, transpose = _tf_resolve(model, name)
+        array = reader.get_tensor(name)
+        if transpose:
+            array = array.T
+        if tuple(pointer.shape) != tuple(array.shape):
+            raise ValueError('TF variable {} has shape {}, model parameter {}'.format(
+                name, tuple(array.shape), tuple(pointer.shape)))
+        with torch.no_grad():
+            pointer.data.copy_(torch.from_numpy(array.copy()).to(pointer.dtype))
+        loaded.append(name)
+    logger.info('Initialized %d PyTorch weights from TF', len(loaded))
+    return model
+
+
+def bert_state_to_tf_names(model):
+    """Inverse of :func:`load_tf_weights_in_bert`: ``{tf_name: ndarray}`` in Google's
+    naming (``kernel`` transposed, LayerNorm ``gamma/beta``, ``layer_N``,
+    ``cls/predictions/output_bias``, ``cls/seq_relationship/output_weights``).
+    The tied decoder weight is the word embedding and is not emitted twice."""
+    import re
+    out = {}
+    lin_weights = {n for n, m in model.named_modules() if isinstance(m, (nn.Linear, LinearActivation))}
+    for key, t in model.state_dict().items():
+        if key == 'cls.predictions.decoder.weight':
+            continue
+        mod, _, leaf = key.rpartition('.')
+        parts = mod.split('.') if mod else []
+        tf_parts = []
+        i = 0
+        while i < len(parts):
+            if i + 1 < len(parts) and parts[i + 1].isdigit():
+                tf_parts.append('{}_{}'.format(parts[i], parts[i + 1]))
+                i += 2
+                continue
+            tf_parts.append('dense' if parts[i] == 'dense_act' else parts[i])
+            i += 1
+        arr = t.detach().float().cpu().numpy()
+        if mod.endswith('LayerNorm'):
+            tf_parts.append('gamma' if leaf == 'weight' else 'beta')
+        elif re.search(r'_embeddings$', mod):
+            pass                                   # '<name>_embeddings' holds the table itself
+        elif mod == 'cls.seq_relationship':
+            tf_parts.append('output_weights' if leaf == 'weight' else 'output_bias')
+        elif mod == 'cls.predictions' and leaf == 'bias':
+            tf_parts.append('output_bias')
+        elif mod in lin_weights and leaf == 'weight':
+            tf_parts.append('kernel')
+            arr = arr.T
+        else:
+            tf_parts.append(leaf)
+        out['/'.join(tf_parts)] = arr
+    return out
+
+
 def remap_state_dict_keys(state_dict, model_keys=None):
     """Map transformers-style keys (``intermediate.dense``, ``pooler.dense``,
     LayerNorm ``gamma/beta``) onto this schema.  Returns a new dict."""
@@ -436,23 +551,59 @@ class BertPreTrainedModel(nn.Module):
     @classmethod
     def from_pretrained(cls, pretrained_model_name_or_path, state_dict=None, cache_dir=None, from_tf=False,
                         *inputs, **kwargs):
-        """Load from a LOCAL directory holding ``bert_config.json`` + ``pytorch_model.bin``
-        (or a .safetensors file).  Archive download/TF conversion of the reference
-        (bert_modeling.py:612-752, 43-101) are not available offline."""
-        path = pretrained_model_name_or_path
-        if from_tf:
-            raise NotImplementedError('TensorFlow checkpoint conversion needs tensorflow, which is not available')
-        if not os.path.isdir(path):
-            raise EnvironmentError('pretrained model directory not found: {}'.format(path))
-        config = BertConfig.from_json_file(os.path.join(path, CONFIG_NAME))
-        model = cls(config, *inputs, **kwargs)
-        if state_dict is None:
-            st = os.path.join(path, 'model.safetensors')
-            if os.path.exists(st):
-                from safetensors.torch import load_file
-                state_dict = load_file(st)
-            else:
-                state_dict = torch.load(os.path.join(path, WEIGHTS_NAME), map_location='cpu', weights_only=True)
+        """Instantiate from pretrained weights (reference bert_modeling.py:612-752).
+
+        ``pretrained_model_name_or_path`` is a local directory holding
+        ``bert_config.json`` + ``pytorch_model.bin`` (or ``model.safetensors``), a
+        ``.tar.gz`` archive of such a directory (extracted to a temp dir with the
+        reference's path-traversal guard), or anything ``utils.file_utils.cached_path``
+        resolves offline (a pre-populated cache entry).  ``from_tf=True`` reads
+        ``model.ckpt`` (TF V2 bundle) from the directory through the native-format
+        reader -- no tensorflow needed.  Weights load with ``weights_only=True``."""
+        import shutil
+        import tarfile
+        import tempfile
+        from ..utils.file_utils import cached_path
+        archive = PRETRAINED_MODEL_ARCHIVE_MAP.get(pretrained_model_name_or_path, pretrained_model_name_or_path)
+        try:
+            resolved = cached_path(archive, cache_dir=cache_dir)
+        except EnvironmentError:
+            raise EnvironmentError('pretrained model not found (offline: local paths and cache only): {}'
+                                   .format(pretrained_model_name_or_path))
+        tempdir = None
+        if os.path.isdir(resolved) or from_tf:
+            serialization_dir = resolved
+        else:
+            tempdir = tempfile.mkdtemp()
+            with tarfile.open(resolved, 'r:*') as tar:
+                root = os.path.abspath(tempdir)
+                for member in tar.getmembers():
+                    target = os.path.abspath(os.path.join(tempdir, member.name))
+                    if os.path.commonpath([root, target]) != root or member.issym() or member.islnk():
+                        raise EnvironmentError('unsafe member in archive {}: {}'.format(resolved, member.name))
+                tar.extractall(tempdir)
+            serialization_dir = tempdir
+            # archives may wrap the files in one top-level directory
+            if not os.path.exists(os.path.join(tempdir, CONFIG_NAME)):
+                subs = [d for d in os.listdir(tempdir) if os.path.isdir(os.path.join(tempdir, d))]
+                if len(subs) == 1:
+                    serialization_dir = os.path.join(tempdir, subs[0])
+        try:
+            config = BertConfig.from_json_file(os.path.join(serialization_dir, CONFIG_NAME))
+            model = cls(config, *inputs, **kwargs)
+            if from_tf:
+                return load_tf_weights_in_bert(model, os.path.join(serialization_dir, TF_WEIGHTS_NAME))
+            if state_dict is None:
+                st = os.path.join(serialization_dir, 'model.safetensors')
+                if os.path.exists(st):
+                    from safetensors.torch import load_file
+                    state_dict = load_file(st)
+                else:
+                    state_dict = torch.load(os.path.join(serialization_dir, WEIGHTS_NAME), map_location='cpu',
+                                            weights_only=True)
+        finally:
+            if tempdir:
+                shutil.rmtree(tempdir, ignore_errors=True)
         keys = set(model.state_dict().keys())
         state_dict = remap_state_dict_keys(state_dict, keys)
         if not any(k.startswith('bert.') for k in keys) or any(k.startswith('bert.') for k in state_dict):

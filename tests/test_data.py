@@ -77,6 +77,25 @@ def test_concat_dataset_read_batch(tmp_path):
             assert torch.equal(b[f][k], it[f])
 
 
+def test_combine_bert_data_in_memory(tmp_path):
+    """Eager in-memory loader (reference BERT_DATA.py:11-43): raw key tuples equal the
+    shard contents, and its collated batches equal the streaming reader's."""
+    from hetseq_9cme_amd.data.h5_dataset import CombineBertData
+    paths = _shards(tmp_path)
+    mem = CombineBertData(paths)
+    stream = ConBertH5pyData([BertH5pyData(p) for p in paths])
+    assert len(mem) == len(stream) == 111
+    r = _data_native.BertShardReader(paths[1])
+    first = len(BertH5pyData(paths[0]))
+    raw = mem[first + 2]
+    for k, key in enumerate(CombineBertData.DEFAULT_KEYS):
+        assert np.array_equal(raw[k], r.read_key(key, 2, 1)[0])
+    rows = np.array([35, 36, 37, 38, 80, 110, 0, 3])
+    a, b = mem.read_batch(rows), stream.read_batch(rows)
+    for f in range(5):
+        assert torch.equal(a[f], b[f])
+
+
 def _ref_shard_order(n_batches, W, r, seed, epoch):
     """Reference algorithm: shuffle batch list with seed+epoch, take r::W, pad []."""
     batches = [[i] for i in range(n_batches)]

@@ -46,6 +46,11 @@ void hx_softmax_xent(int bf16, void* logits, const float* bias, const int64_t* l
 // attention.hip
 size_t hx_attn_bwd_smem_bytes();
 // bias: optional [3H] QKV-projection bias added to Q/K/V as they are loaded
+void hx_attn_fwd_bf16(const void* qkv, const float* bias, const float* maskb, void* out, float* lse, uint32_t* dmask,
+                      int B, int S, int nh, float keep, uint64_t seed, uint64_t stream, hipStream_t s);
+void hx_attn_bwd_bf16(const void* qkv, const float* bias, float* dbias_part, const float* maskb, const void* dout,
+                      const void* out, const float* lse, const uint32_t* dmask, void* dqkv, float* dq_acc, int dq_ld,
+                      int B, int S, int nh, float keep, hipStream_t s);
 void hx_attn_fwd(int bf16, const void* qkv, const float* bias, const float* maskb, void* out, float* lse,
                  uint32_t* dmask, int B, int S, int nh, float keep, uint64_t seed, uint64_t stream, hipStream_t s);
 // dq_acc: fp32 dQ accumulation target when S > 128 (atomics; row stride dq_ld), else unused.

@@ -33,50 +33,21 @@
 #include "hx_launch.h"
 #include "hx_vec.h"
 #include "hx_reduce.h"
+#include "hx_attn.h"
 
 namespace {
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+using hx::attn::f32x16;
 
 constexpr int D = 64;      // head dim (BERT-base/large)
 constexpr int LDK = 68;    // padded LDS row stride (floats)
 
-// v_writelane_b32 with a compile-time lane (inline constant: only the value uses
-// the constant bus): put a wave-uniform value into one lane of a VGPR
-template <int L>
-__device__ __forceinline__ uint32_t write_lane(uint32_t v, uint32_t val) {
-  asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(val), "i"(L));
-  return v;
-}
-
 __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
-// accumulator register r of a 32x32 tile, lane half h -> row index
-__device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 __device__ __forceinline__ float4 add4(float4 a, float4 b) { return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w); }
-
-// Forward dropout for accumulator register R of both 32-key sub-blocks: apply the
-// lane's decisions, and build the transposed bitmask word: a ballot over the wave
-// gives, for register R, the 32-query words of keys crow(R,0) (lanes 0-31) and
-// crow(R,1) (lanes 32-63); lane L collects the word of key kt + L.
-template <int R>
-__device__ __forceinline__ void drop_step(f32x16& s0, f32x16& s1, const uint32_t (&kb)[4], float inv_keep,
-                                          uint32_t& myword) {
-  if constexpr (R < 16) {
-    const bool k0 = (kb[R >> 3] >> (R & 7)) & 1, k1 = (kb[2 + (R >> 3)] >> (R & 7)) & 1;
-    s0[R] = k0 ? s0[R] * inv_keep : 0.f;
-    s1[R] = k1 ? s1[R] * inv_keep : 0.f;
-    const uint64_t b0 = __ballot(k0), b1 = __ballot(k1);
-    constexpr int L0 = (R & 3) + 8 * (R >> 2);
-    myword = write_lane<L0>(myword, (uint32_t)b0);
-    myword = write_lane<L0 + 4>(myword, (uint32_t)(b0 >> 32));
-    myword = write_lane<32 + L0>(myword, (uint32_t)b1);
-    myword = write_lane<36 + L0>(myword, (uint32_t)(b1 >> 32));
-    if constexpr ((R & 3) == 3) __builtin_amdgcn_sched_barrier(0);   // keep ballots from piling up in SGPRs
-    drop_step<R + 1>(s0, s1, kb, inv_keep, myword);
-  }
-}
+using hx::attn::crow;
+using hx::attn::drop_step;
 
 // ============================================================================ forward
 // grid (S/128, nh, B), block 256 = 4 waves x 32 queries.
@@ -146,7 +117,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
     // input from this tile's math, so issuing it here lets it overlap the MFMAs below
     uint32_t kb[4] = {0u, 0u, 0u, 0u};
     if (kDrop) {
-      const uint64_t cbase = (((uint64_t)(bh * S + q) * (uint64_t)(Sp >> 6) + (kt >> 6)) * 2 + h) * 4;
+      const uint64_t cbase = hx::attn::drop_counter(bh, S, q, Sp, kt, h);
 #pragma unroll
       for (int j = 0; j < 4; ++j) kb[j] = hx::keep8(seed, stream, cbase + j, t16);
     }
@@ -553,15 +524,15 @@ void attn_bwd_t(const void* qkv, const float* bias, float* dbias_part, const flo
 
 void hx_attn_fwd(int bf16, const void* qkv, const float* bias, const float* maskb, void* out, float* lse,
                  uint32_t* dmask, int B, int S, int nh, float keep, uint64_t seed, uint64_t stream, hipStream_t s) {
-  if (bf16) attn_fwd_t<uint16_t>(qkv, bias, maskb, out, lse, dmask, B, S, nh, keep, seed, stream, s);
+  if (bf16) hx_attn_fwd_bf16(qkv, bias, maskb, out, lse, dmask, B, S, nh, keep, seed, stream, s);  // bf16 MFMA
   else attn_fwd_t<float>(qkv, bias, maskb, out, lse, dmask, B, S, nh, keep, seed, stream, s);
 }
 
 void hx_attn_bwd(int bf16, const void* qkv, const float* bias, float* dbq, float* dbk, float* dbv, float* dbias_part,
                  const float* maskb, const void* dout, const void* out, const float* lse, const uint32_t* dmask,
                  void* dqkv, float* dq_acc, int dq_ld, int B, int S, int nh, float keep, hipStream_t s) {
-  if (bf16)
-    attn_bwd_t<uint16_t>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv, dq_acc, dq_ld, B, S, nh, keep, s);
+  if (bf16)   // bf16 MFMA (attention_bf16.hip)
+    hx_attn_bwd_bf16(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv, dq_acc, dq_ld, B, S, nh, keep, s);
   else
     attn_bwd_t<float>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv, dq_acc, dq_ld, B, S, nh, keep, s);
   if (dbias_part) {

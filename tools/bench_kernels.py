@@ -31,22 +31,28 @@ def timeit(fn, iters=50, warmup=5):
     return ts[len(ts) // 2] * 1e3  # us
 
 
-def report(name, us, flops=None, bytes_=None):
+def report(name, us, flops=None, bytes_=None, peak=157.3):
     extra = []
     if flops:
-        extra.append('{:.1f} TF/s ({:.0f}% of 157)'.format(flops / us / 1e6, 100 * flops / us / 1e6 / 157.3))
+        extra.append('{:.1f} TF/s ({:.0f}% of {:.0f})'.format(flops / us / 1e6, 100 * flops / us / 1e6 / peak, peak))
     if bytes_:
         extra.append('{:.2f} TB/s'.format(bytes_ / us / 1e6))
     print('{:<28s} {:9.1f} us   {}'.format(name, us, '  '.join(extra)), flush=True)
 
 
-def bench_attn(B, S, nh=12, keep=0.9):
+def _report_peak(peak, tag):
+    return lambda name, us, flops=None, bytes_=None: report(tag + name, us, flops, bytes_, peak)
+
+
+def bench_attn(B, S, nh=12, keep=0.9, dtype=torch.float32):
     d = 64
-    qkv = torch.randn(B, S, 3 * nh * d, device='cuda')
+    peak = 157.3 if dtype == torch.float32 else 2500.0
+    qkv = torch.randn(B, S, 3 * nh * d, device='cuda').to(dtype)
     mb = torch.zeros(B, S, device='cuda')
     out, lse, dm = C().attn_fwd(qkv, mb, nh, keep, 1, 0, None)
     dout = torch.randn_like(out)
     f_fwd = 2 * 2 * B * nh * S * S * d
+    report = _report_peak(peak, '' if dtype == torch.float32 else '[bf16] ')
     report('attn_fwd', timeit(lambda: C().attn_fwd(qkv, mb, nh, keep, 1, 0, None)), flops=f_fwd)
     report('attn_fwd (no dropout)', timeit(lambda: C().attn_fwd(qkv, mb, nh, 1.0, 1, 0, None)), flops=f_fwd)
     report('attn_bwd', timeit(lambda: C().attn_bwd(dout, qkv, mb, out, lse, dm, nh, keep, None, None, None, None)[0]), flops=2.5 * f_fwd)
@@ -113,6 +119,8 @@ def main():
     which = a.only.split(',')
     if 'attn' in which:
         bench_attn(a.batch, a.seq)
+    if 'attn_bf16' in which:
+        bench_attn(a.batch, a.seq, dtype=torch.bfloat16)
     if 'ln' in which:
         bench_ln(a.batch, a.seq)
     if 'ffn' in which:

@@ -352,6 +352,32 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor o
   return {dqkv, dbias};
 }
 
+// ------------------------------------------------------------------ bf16 weight gradient
+// out[M, N] (fp32, overwritten) = dy[T, M]^T . x[T, N] (bf16, unit column stride, 16-B rows)
+bool wgrad_bf16_ok(const Tensor& dy, const Tensor& x) {
+  if (!dy.is_cuda() || dy.scalar_type() != torch::kBFloat16 || x.scalar_type() != torch::kBFloat16) return false;
+  if (dy.dim() != 2 || x.dim() != 2 || dy.size(0) != x.size(0) || dy.size(0) < 1) return false;
+  if (dy.stride(1) != 1 || x.stride(1) != 1 || dy.stride(0) % 8 || x.stride(0) % 8) return false;
+  if (!aligned16(dy.data_ptr()) || !aligned16(x.data_ptr())) return false;
+  return dy.size(1) % 128 == 0 && x.size(1) % 128 == 0 && dy.size(0) < (1LL << 31);
+}
+Tensor wgrad_bf16(Tensor dy, Tensor x, Tensor out) {
+  TORCH_CHECK(wgrad_bf16_ok(dy, x), "wgrad_bf16: unsupported operands (need bf16 [T, M] / [T, N] row-major "
+              "with M, N multiples of 128 and 16-byte rows)");
+  check_f32(out, "wgrad out");
+  const int64_t T = dy.size(0), M = dy.size(1), N = x.size(1);
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N, "wgrad out must be [M, N]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  int cfg = 0, nsplit = 1;
+  hx_wgrad_bf16_plan((int)M, (int)N, (int)T, &cfg, &nsplit);
+  Tensor ws;
+  if (nsplit > 1) ws = torch::empty({nsplit * M * N}, out.options());
+  hx_wgrad_bf16(dy.data_ptr(), (int)dy.stride(0), x.data_ptr(), (int)x.stride(0), out.data_ptr<float>(),
+                nsplit > 1 ? ws.data_ptr<float>() : nullptr, (int)M, (int)N, (int)T, cfg, nsplit, cur_stream(dy));
+  dbg_finite(out, "wgrad_bf16");
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -370,6 +396,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_xent_", &softmax_xent_);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
+  m.def("wgrad_bf16", &wgrad_bf16);
+  m.def("wgrad_bf16_ok", &wgrad_bf16_ok);
   m.def("set_debug", &set_debug);
   m.def("get_debug", &get_debug);
 }

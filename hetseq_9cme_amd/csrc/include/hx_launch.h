@@ -51,6 +51,10 @@ void hx_attn_fwd_bf16(const void* qkv, const float* bias, const float* maskb, vo
 void hx_attn_bwd_bf16(const void* qkv, const float* bias, float* dbias_part, const float* maskb, const void* dout,
                       const void* out, const float* lse, const uint32_t* dmask, void* dqkv, float* dq_acc, int dq_ld,
                       int B, int S, int nh, float keep, hipStream_t s);
+// bf16 weight gradient dW[M][N] (fp32) = dY[T][M]^T . X[T][N] (wgrad_bf16.hip); ws: nsplit * M * N floats
+void hx_wgrad_bf16_plan(int M, int N, int T, int* cfg, int* nsplit);
+void hx_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, float* out, float* ws, int M, int N, int T,
+                   int cfg, int nsplit, hipStream_t s);
 void hx_attn_fwd(int bf16, const void* qkv, const float* bias, const float* maskb, void* out, float* lse,
                  uint32_t* dmask, int B, int S, int nh, float keep, uint64_t seed, uint64_t stream, hipStream_t s);
 // dq_acc: fp32 dQ accumulation target when S > 128 (atomics; row stride dq_ld), else unused.

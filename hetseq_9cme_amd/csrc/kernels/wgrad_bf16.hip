@@ -1,0 +1,210 @@
+// Weight gradient of y = x W^T for bf16 activations: dW[M][N] (fp32) = dY[T][M]^T . X[T][N].
+//
+// Both operands are stored with the reduction index (tokens, T = B*S = 16384 for BERT
+// phase 1) as the ROW index, and the output is small (768 x 3072 = 2.4 M elements), so
+// the library GEMMs for this "TN" case run at ~450 TF/s on MI355X (measured by
+// tools/bench_wgrad.py: 165-175 us for the 77 GFLOP FFN weight gradients, i.e. 18% of
+// the 2.5 PF/s bf16 MFMA peak).  This kernel:
+//
+//  * splits the token reduction over ``nsplit`` workgroups per output tile so the grid
+//    fills the 256 CUs even though there are only 9-36 output tiles; partial tiles go
+//    to an fp32 workspace and one vectorised pass sums them (no float atomics: at
+//    ~1.3 TB/s the atomic rate would cost more than the GEMM);
+//  * stages [32 tokens][BM | BN] tiles in LDS exactly as they sit in memory (16-B
+//    coalesced loads, XOR-swizzled 16-B chunks) and builds the k-major MFMA fragments
+//    with the gfx950 transposing LDS read ``ds_read_b64_tr_b16`` (two per fragment) --
+//    no transposed copies of the 100 MB activations;
+//  * double-buffers the LDS tiles with the next tile's global loads in flight in
+//    registers: one barrier per 32-token step;
+//  * maps workgroups XCD-aware: the hardware deals consecutive workgroup ids round-robin
+//    to the 8 XCDs, so the work list is cut into 8 contiguous ranges, one per XCD, and
+//    the workgroups of one XCD walk neighbouring output tiles of the same token range
+//    (shared dY / X rows stay in that XCD's L2).
+#include <algorithm>
+
+#include "hx_launch.h"
+#include "hx_attn.h"
+
+namespace {
+
+using hx::attn::crow;
+using hx::attn::f32x16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+constexpr int BK = 32;   // tokens per pipeline step (two 16-deep MFMA k-steps)
+
+__device__ __forceinline__ int swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+// element offset of (row, element col) in a [BK][W] bf16 tile with XOR-swizzled 16-B chunks
+template <int W>
+__device__ __forceinline__ int toff(int row, int col) {
+  return row * W + 8 * ((col >> 3) ^ swz(row)) + (col & 7);
+}
+
+// k-major fragment of 32 columns (c0 .. c0+31) x 16 k-rows (k0 ..) for a 32x32x16 operand:
+// lane l holds column c0 + (l & 31), rows k0 + 8(l >> 5) + j, j = 0..7 -- two transposed reads
+template <int W>
+__device__ __forceinline__ bf16x8 frag(const uint16_t* tile, int k0, int c0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int row = k0 + 8 * (g >> 1) + q;
+  const int col = c0 + 16 * (g & 1) + 4 * p;
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(tile + toff<W>(row, col)));
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(tile + toff<W>(row + 4, col)));
+  const v4i16 v[2] = {lo, hi};
+  return *reinterpret_cast<const bf16x8*>(v);
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_bf16_k(
+    const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ B, int ldb, float* __restrict__ out,
+    int M, int N, int T, int kchunk, int nsplit) {
+  constexpr int NWM = BM / WM, NW = NWM * (BN / WN), NT = NW * 64;
+  constexpr int MB = WM / 32, NB = WN / 32;
+  constexpr int CA = BK * BM / 8 / NT, CB = BK * BN / 8 / NT;   // 16-B chunks per thread
+  static_assert(CA >= 1 && CB >= 1 && BK * BM / 8 % NT == 0 && BK * BN / 8 % NT == 0, "tile / thread mismatch");
+  __shared__ __attribute__((aligned(16))) uint16_t As[2][BK * BM];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[2][BK * BN];
+
+  // ---- XCD-aware work index (see header); every lane of the workgroup takes the same exit
+  const int TM = M / BM, TN = N / BN, total = TM * TN * nsplit;
+  const int per = (total + 7) / 8;   // grid = 8 * per workgroups
+  const int work = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (work >= total) return;         // tail of the last XCD's range: no work
+  const int nt = work % TN, mt = (work / TN) % TM, sp = work / (TN * TM);
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int t0 = sp * kchunk, t1 = min(T, t0 + kchunk);
+  const int nit = (t1 - t0 + BK - 1) / BK;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w % NWM, wn = w / NWM, h = lane >> 5, l32 = lane & 31;
+
+  uint4 ra[CA], rb[CB];
+  auto load = [&](int it) {
+    const int tb = t0 + it * BK;
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      const int e = tid + i * NT, row = e / (BM / 8), ch = e % (BM / 8);
+      const int t = tb + row;
+      ra[i] = t < t1 ? *reinterpret_cast<const uint4*>(A + (int64_t)t * lda + m0 + 8 * ch) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const int e = tid + i * NT, row = e / (BN / 8), ch = e % (BN / 8);
+      const int t = tb + row;
+      rb[i] = t < t1 ? *reinterpret_cast<const uint4*>(B + (int64_t)t * ldb + n0 + 8 * ch) : make_uint4(0, 0, 0, 0);
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      const int e = tid + i * NT, row = e / (BM / 8), ch = e % (BM / 8);
+      *reinterpret_cast<uint4*>(&As[buf][toff<BM>(row, 8 * ch)]) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const int e = tid + i * NT, row = e / (BN / 8), ch = e % (BN / 8);
+      *reinterpret_cast<uint4*>(&Bs[buf][toff<BN>(row, 8 * ch)]) = rb[i];
+    }
+  };
+
+  f32x16 acc[MB][NB];
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[a][b] = f32x16{0};
+
+  if (nit > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < nit; ++it) {
+    const int cb = it & 1;
+    if (it + 1 < nit) load(it + 1);   // in flight during this step's MFMAs
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[MB], fb[NB];
+#pragma unroll
+      for (int a = 0; a < MB; ++a) fa[a] = frag<BM>(As[cb], 16 * ks, wm * WM + 32 * a, lane);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) fb[b] = frag<BN>(Bs[cb], 16 * ks, wn * WN + 32 * b, lane);
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+    }
+    if (it + 1 < nit) store(cb ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: rows m (accumulator rows), columns n (lanes): 128-B coalesced fp32 stores
+  float* o = out + (nsplit > 1 ? (int64_t)sp * M * N : 0);
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int n = n0 + wn * WN + 32 * b + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * WM + 32 * a + crow(r, h);
+        o[(int64_t)m * N + n] = acc[a][b][r];
+      }
+    }
+}
+
+// out[i] = sum_s ws[s][i]  (float4)
+__global__ __launch_bounds__(256) void split_sum_k(const float4* __restrict__ ws, float4* __restrict__ out, int64_t n4,
+                                                  int nsplit) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 s = ws[i];
+    for (int k = 1; k < nsplit; ++k) {
+      const float4 v = ws[(int64_t)k * n4 + i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    out[i] = s;
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+void launch(const uint16_t* A, int lda, const uint16_t* B, int ldb, float* out, float* ws, int M, int N, int T,
+            int nsplit, hipStream_t s) {
+  constexpr int NT = (BM / WM) * (BN / WN) * 64;
+  const int kchunk = ((T + nsplit - 1) / nsplit + BK - 1) / BK * BK;
+  nsplit = (T + kchunk - 1) / kchunk;   // no empty splits
+  const int total = (M / BM) * (N / BN) * nsplit;
+  const int per = (total + 7) / 8;
+  wgrad_bf16_k<BM, BN, WM, WN><<<8 * per, NT, 0, s>>>(A, lda, B, ldb, nsplit > 1 ? ws : out, M, N, T, kchunk,
+                                                      nsplit);
+  if (nsplit > 1) {
+    const int64_t n4 = (int64_t)M * N / 4;
+    const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+    split_sum_k<<<blocks, 256, 0, s>>>(reinterpret_cast<const float4*>(ws), reinterpret_cast<float4*>(out), n4,
+                                       nsplit);
+  }
+}
+
+}  // namespace
+
+// Tile configuration and token split for an (M, N, T) weight gradient: the large tile
+// (256 x 256, 8 waves of 128 x 64) halves the L2 traffic per FLOP of the small one
+// (128 x 128, 4 waves of 64 x 64); the small one is used when the large one would need
+// so many splits that summing the fp32 partials costs more than the extra traffic.
+void hx_wgrad_bf16_plan(int M, int N, int T, int* cfg, int* nsplit) {
+  const bool big = (M % 256 == 0) && (N % 256 == 0) && (int64_t)M * N >= 2 * 1024 * 1024;
+  const int tiles = big ? (M / 256) * (N / 256) : (M / 128) * (N / 128);
+  const int target = big ? 256 : 512;   // one 8-wave or two 4-wave workgroups per CU
+  int s = std::max(1, target / std::max(1, tiles));
+  s = std::min(s, std::max(1, T / 256));   // at least 256 tokens per split
+  *cfg = big ? 1 : 0;
+  *nsplit = s;
+}
+
+void hx_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, float* out, float* ws, int M, int N, int T,
+                   int cfg, int nsplit, hipStream_t s) {
+  if (cfg == 1)
+    launch<256, 256, 128, 64>((const uint16_t*)dy, ldy, (const uint16_t*)x, ldx, out, ws, M, N, T, nsplit, s);
+  else
+    launch<128, 128, 64, 64>((const uint16_t*)dy, ldy, (const uint16_t*)x, ldx, out, ws, M, N, T, nsplit, s);
+}

@@ -27,9 +27,14 @@ def cast_w(w, dtype):
 
 def _wgrad(dy2, x2, slot):
     """dW = dy2^T x2 in fp32; written straight into ``slot`` when given.  bf16
-    operands use the bf16 x bf16 -> fp32 GEMM (no bf16 result, no cast pass)."""
+    operands use the hand-written split-K bf16-MFMA kernel (csrc/kernels/wgrad_bf16.hip,
+    ~3x the library's rate on these tokens-as-reduction shapes), else the library
+    bf16 x bf16 -> fp32 GEMM; neither makes a bf16 result or a cast pass."""
     if dy2.dtype == torch.float32:
         return torch.mm(dy2.t(), x2, out=slot) if slot is not None else torch.mm(dy2.t(), x2)
+    if use_kernels(dy2) and C().wgrad_bf16_ok(dy2, x2):
+        out = slot if slot is not None else torch.empty(dy2.shape[1], x2.shape[1], device=dy2.device)
+        return C().wgrad_bf16(dy2, x2, out)
     if slot is not None:
         return torch.mm(dy2.t(), x2, out_dtype=torch.float32, out=slot)
     return torch.mm(dy2.t(), x2, out_dtype=torch.float32)

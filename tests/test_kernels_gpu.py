@@ -484,3 +484,21 @@ def test_attention_with_qkv_bias(dev, S):
     ref.backward(d_)
     for a, r in zip(leaves, rl):
         _close(a.grad, r.grad, rtol=1e-3, atol=2e-4)
+
+
+@pytest.mark.parametrize('M,N,T', [(3072, 768, 4096), (768, 3072, 1000), (768, 768, 333), (256, 128, 40),
+                                   (2304, 768, 16384)])
+def test_wgrad_bf16_kernel(dev, M, N, T):
+    """Hand-written split-K bf16 weight gradient (ds_read_b64_tr_b16 fragments, fp32 out)
+    vs an fp32 GEMM of the same bf16 values; token counts that are not multiples of the
+    32-token step, single-split and multi-split plans, strided (non-contiguous) rows."""
+    from hetseq_9cme_amd.ops._ext import C
+    torch.manual_seed(0)
+    dy = torch.randn(T, M, device=dev).to(torch.bfloat16)
+    xw = torch.randn(T, N + 64, device=dev).to(torch.bfloat16)
+    x = xw[:, 32:32 + N]                  # row stride N + 64, 16-B aligned start
+    assert C().wgrad_bf16_ok(dy, x)
+    out = torch.full((M, N), float('nan'), device=dev)
+    C().wgrad_bf16(dy, x, out)
+    ref = dy.float().t() @ x.float()
+    torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3 * (T ** 0.5))

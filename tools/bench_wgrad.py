@@ -1,0 +1,67 @@
+"""Weight-gradient GEMM variants at BERT shapes (bf16 activations, fp32 gradient slots).
+
+``python tools/bench_wgrad.py [--tokens 16384]`` -- dW[out, in] = dY^T X with
+dY [T, out], X [T, in] bf16, T = tokens per GPU.  Compares the library paths
+(bf16 x bf16 -> fp32 output, bf16 output + cast, the transposed product) and
+the hand-written split-K MFMA kernel (``_C.wgrad_bf16``) when present.
+"""
+import argparse
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timeit(fn, iters=30, warmup=5):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(iters):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    ts.sort()
+    return ts[len(ts) // 2] * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--tokens', type=int, default=16384)
+    a = ap.parse_args()
+    T = a.tokens
+    try:
+        from hetseq_9cme_amd.ops._ext import C
+        ext = C() if hasattr(C(), 'wgrad_bf16') else None
+    except Exception:  # noqa: BLE001
+        ext = None
+    for (n_out, n_in) in [(3072, 768), (768, 3072), (2304, 768), (768, 768)]:
+        dy = torch.randn(T, n_out, device='cuda').to(torch.bfloat16)
+        x = torch.randn(T, n_in, device='cuda').to(torch.bfloat16)
+        slot = torch.empty(n_out, n_in, device='cuda')
+        fl = 2.0 * T * n_out * n_in
+        res = {}
+        res['mm out_dtype=f32'] = timeit(lambda: torch.mm(dy.t(), x, out_dtype=torch.float32, out=slot))
+        res['mm bf16 + cast'] = timeit(lambda: slot.copy_(torch.mm(dy.t(), x)))
+        res['mm (x^T dy)^T f32'] = timeit(lambda: torch.mm(x.t(), dy, out_dtype=torch.float32))
+        if ext is not None:
+            res['hx wgrad_bf16'] = timeit(lambda: ext.wgrad_bf16(dy, x, slot))
+            ref = torch.mm(dy.t().float(), x.float())
+            got = slot.clone()
+            ext.wgrad_bf16(dy, x, got)
+            err = ((got - ref).abs().max() / ref.abs().max()).item()
+            res['hx wgrad_bf16'] = (res['hx wgrad_bf16'], err)
+        for k, v in res.items():
+            us, err = (v if isinstance(v, tuple) else (v, None))
+            print('[{}x{} T={}] {:<22s} {:8.1f} us  {:7.1f} TF/s{}'.format(
+                n_out, n_in, T, k, us, fl / us / 1e6, '' if err is None else '  rel.err {:.2e}'.format(err)),
+                flush=True)
+
+
+if __name__ == '__main__':
+    main()

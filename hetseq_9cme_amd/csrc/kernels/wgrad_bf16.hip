@@ -24,6 +24,7 @@
 
 #include "hx_launch.h"
 #include "hx_attn.h"
+#include "hx_common.h"
 
 namespace {
 
@@ -35,24 +36,35 @@ typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
 constexpr int BK = 32;   // tokens per pipeline step (two 16-deep MFMA k-steps)
 
-__device__ __forceinline__ int swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-// element offset of (row, element col) in a [BK][W] bf16 tile with XOR-swizzled 16-B chunks
+// LDS image of a [BK rows][W columns] bf16 tile: 8-row x 32-column subtiles of 512 B with
+// XOR-swizzled 16-B chunks (cdna_hip_programming.md T10 layout (a)).  Byte offset of 16-B
+// chunk ch of row `row`.  Conflict-free for the 16-B chunk stores and for the transposed
+// reads below, and LINEAR in 32-column blocks (+512 B) and 16-row k-steps (+32W B), so a
+// wave needs two address registers (rows q and q+4) per operand: every other fragment
+// read is the same VGPR plus an immediate offset.
 template <int W>
-__device__ __forceinline__ int toff(int row, int col) {
-  return row * W + 8 * ((col >> 3) ^ swz(row)) + (col & 7);
+__device__ __forceinline__ int toff(int row, int ch) {
+  return (row >> 3) * (16 * W) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
 }
-
-// k-major fragment of 32 columns (c0 .. c0+31) x 16 k-rows (k0 ..) for a 32x32x16 operand:
-// lane l holds column c0 + (l & 31), rows k0 + 8(l >> 5) + j, j = 0..7 -- two transposed reads
+// per-lane byte offsets of the two transposed reads of the (k0 = 0, c0 = 0) fragment
 template <int W>
-__device__ __forceinline__ bf16x8 frag(const uint16_t* tile, int k0, int c0, int lane) {
+__device__ __forceinline__ void tr_base(int lane, int& lo, int& hi) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int row = k0 + 8 * (g >> 1) + q;
-  const int col = c0 + 16 * (g & 1) + 4 * p;
-  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(tile + toff<W>(row, col)));
-  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(tile + toff<W>(row + 4, col)));
-  const v4i16 v[2] = {lo, hi};
+  const int row = 8 * (g >> 1) + q, ch = 2 * (g & 1) + (p >> 1);
+  lo = toff<W>(row, ch) + 8 * (p & 1);
+  hi = toff<W>(row + 4, ch) + 8 * (p & 1);
+}
+// k-major 32x32x16 operand fragment of columns c0 .. c0+31 (c0 % 32 == 0), rows k0 .. k0+15
+// (k0 % 16 == 0): lane l holds column c0 + (l & 31), rows k0 + 8(l >> 5) + j -- the gfx950
+// transposing LDS read delivers 4 rows of one column per read (two reads per fragment)
+template <int W>
+__device__ __forceinline__ bf16x8 frag(const char* tile, int lo, int hi, int k0, int c0) {
+  const int d = (k0 >> 4) * (32 * W) + (c0 >> 5) * 512;
+  const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(tile + lo + d));
+  const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(tile + hi + d));
+  const v4i16 v[2] = {a, b};
   return *reinterpret_cast<const bf16x8*>(v);
 }
 
@@ -64,8 +76,8 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_bf16_k(
   constexpr int MB = WM / 32, NB = WN / 32;
   constexpr int CA = BK * BM / 8 / NT, CB = BK * BN / 8 / NT;   // 16-B chunks per thread
   static_assert(CA >= 1 && CB >= 1 && BK * BM / 8 % NT == 0 && BK * BN / 8 % NT == 0, "tile / thread mismatch");
-  __shared__ __attribute__((aligned(16))) uint16_t As[2][BK * BM];
-  __shared__ __attribute__((aligned(16))) uint16_t Bs[2][BK * BN];
+  constexpr int A_BYTES = BK * BM * 2, B_BYTES = BK * BN * 2;
+  extern __shared__ __attribute__((aligned(16))) char lds[];   // [2] A tiles, then [2] B tiles
 
   // ---- XCD-aware work index (see header); every lane of the workgroup takes the same exit
   const int TM = M / BM, TN = N / BN, total = TM * TN * nsplit;
@@ -80,33 +92,48 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_bf16_k(
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w % NWM, wn = w / NWM, h = lane >> 5, l32 = lane & 31;
 
-  uint4 ra[CA], rb[CB];
-  auto load = [&](int it) {
-    const int tb = t0 + it * BK;
+  // Operand rows [t0, t1) of this split through buffer resources: a load past t1 returns
+  // zeros (the tail of the last step and the steps past the end), so loads need no
+  // clamping, branches or selects; per-lane 32-bit offsets are loop-invariant and the
+  // step only advances the scalar offset.
+  const hx::Buf abuf(A + (int64_t)t0 * lda, (uint32_t)((int64_t)(t1 - t0) * lda * 2));
+  const hx::Buf bbuf(B + (int64_t)t0 * ldb, (uint32_t)((int64_t)(t1 - t0) * ldb * 2));
+  uint32_t va[CA], vb[CB];
+  int sa[CA], sb[CB];
 #pragma unroll
-    for (int i = 0; i < CA; ++i) {
-      const int e = tid + i * NT, row = e / (BM / 8), ch = e % (BM / 8);
-      const int t = tb + row;
-      ra[i] = t < t1 ? *reinterpret_cast<const uint4*>(A + (int64_t)t * lda + m0 + 8 * ch) : make_uint4(0, 0, 0, 0);
-    }
+  for (int i = 0; i < CA; ++i) {
+    const int e = tid + i * NT, row = e / (BM / 8), ch = e % (BM / 8);
+    va[i] = (uint32_t)(row * lda + m0 + 8 * ch) * 2;
+    sa[i] = toff<BM>(row, ch);
+  }
 #pragma unroll
-    for (int i = 0; i < CB; ++i) {
-      const int e = tid + i * NT, row = e / (BN / 8), ch = e % (BN / 8);
-      const int t = tb + row;
-      rb[i] = t < t1 ? *reinterpret_cast<const uint4*>(B + (int64_t)t * ldb + n0 + 8 * ch) : make_uint4(0, 0, 0, 0);
-    }
+  for (int i = 0; i < CB; ++i) {
+    const int e = tid + i * NT, row = e / (BN / 8), ch = e % (BN / 8);
+    vb[i] = (uint32_t)(row * ldb + n0 + 8 * ch) * 2;
+    sb[i] = toff<BN>(row, ch);
+  }
+  int alo, ahi, blo, bhi;
+  tr_base<BM>(lane, alo, ahi);
+  tr_base<BN>(lane, blo, bhi);
+
+  // Global tile loads run TWO steps ahead (two register stages): a load issued at the top
+  // of step it is written to LDS at the end of step it+1, so its latency hides behind
+  // two steps of MFMAs instead of one.
+  u32x4 ra0[CA], rb0[CB], ra1[CA], rb1[CB];
+  auto load = [&](int it, u32x4 (&ra)[CA], u32x4 (&rb)[CB]) {
+    const uint32_t soa = (uint32_t)it * BK * lda * 2, sob = (uint32_t)it * BK * ldb * 2;
+#pragma unroll
+    for (int i = 0; i < CA; ++i) ra[i] = __builtin_amdgcn_raw_buffer_load_b128(abuf.r, va[i], soa, 0);
+#pragma unroll
+    for (int i = 0; i < CB; ++i) rb[i] = __builtin_amdgcn_raw_buffer_load_b128(bbuf.r, vb[i], sob, 0);
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const u32x4 (&ra)[CA], const u32x4 (&rb)[CB]) {
+    char* at = lds + buf * A_BYTES;
+    char* bt = lds + 2 * A_BYTES + buf * B_BYTES;
 #pragma unroll
-    for (int i = 0; i < CA; ++i) {
-      const int e = tid + i * NT, row = e / (BM / 8), ch = e % (BM / 8);
-      *reinterpret_cast<uint4*>(&As[buf][toff<BM>(row, 8 * ch)]) = ra[i];
-    }
+    for (int i = 0; i < CA; ++i) *reinterpret_cast<u32x4*>(at + sa[i]) = ra[i];
 #pragma unroll
-    for (int i = 0; i < CB; ++i) {
-      const int e = tid + i * NT, row = e / (BN / 8), ch = e % (BN / 8);
-      *reinterpret_cast<uint4*>(&Bs[buf][toff<BN>(row, 8 * ch)]) = rb[i];
-    }
+    for (int i = 0; i < CB; ++i) *reinterpret_cast<u32x4*>(bt + sb[i]) = rb[i];
   };
 
   f32x16 acc[MB][NB];
@@ -115,27 +142,38 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_bf16_k(
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[a][b] = f32x16{0};
 
-  if (nit > 0) {
-    load(0);
-    store(0);
-  }
-  __syncthreads();
-  for (int it = 0; it < nit; ++it) {
-    const int cb = it & 1;
-    if (it + 1 < nit) load(it + 1);   // in flight during this step's MFMAs
+  auto mma = [&](int buf) {
+    const char* at = lds + buf * A_BYTES;
+    const char* bt = lds + 2 * A_BYTES + buf * B_BYTES;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8 fa[MB], fb[NB];
 #pragma unroll
-      for (int a = 0; a < MB; ++a) fa[a] = frag<BM>(As[cb], 16 * ks, wm * WM + 32 * a, lane);
+      for (int a = 0; a < MB; ++a) fa[a] = frag<BM>(at, alo, ahi, 16 * ks, wm * WM + 32 * a);
 #pragma unroll
-      for (int b = 0; b < NB; ++b) fb[b] = frag<BN>(Bs[cb], 16 * ks, wn * WN + 32 * b, lane);
+      for (int b = 0; b < NB; ++b) fb[b] = frag<BN>(bt, blo, bhi, 16 * ks, wn * WN + 32 * b);
 #pragma unroll
       for (int a = 0; a < MB; ++a)
 #pragma unroll
-        for (int b = 0; b < NB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+        for (int b = 0; b < NB; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
     }
-    if (it + 1 < nit) store(cb ^ 1);
+  };
+
+  load(0, ra0, rb0);
+  load(1, ra1, rb1);
+  store(0, ra0, rb0);
+  __syncthreads();
+  // step it computes LDS buffer it&1; register stage it&1 is free (stored a step ago)
+  for (int it = 0; it < nit; it += 2) {
+    load(it + 2, ra0, rb0);
+    mma(0);
+    store(1, ra1, rb1);       // step it+1's tile (zeros past the end: harmless)
+    __syncthreads();
+    if (it + 1 >= nit) break;
+    load(it + 3, ra1, rb1);
+    mma(1);
+    store(0, ra0, rb0);
     __syncthreads();
   }
 
@@ -175,7 +213,14 @@ void launch(const uint16_t* A, int lda, const uint16_t* B, int ldb, float* out, 
   nsplit = (T + kchunk - 1) / kchunk;   // no empty splits
   const int total = (M / BM) * (N / BN) * nsplit;
   const int per = (total + 7) / 8;
-  wgrad_bf16_k<BM, BN, WM, WN><<<8 * per, NT, 0, s>>>(A, lda, B, ldb, nsplit > 1 ? ws : out, M, N, T, kchunk,
+  const size_t smem = 2 * BK * (BM + BN) * sizeof(uint16_t);
+  static bool attr = false;
+  if (!attr) {   // > 64 KiB of dynamic LDS needs the opt-in (160 KiB per CU on gfx950)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_bf16_k<BM, BN, WM, WN>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    attr = true;
+  }
+  wgrad_bf16_k<BM, BN, WM, WN><<<8 * per, NT, smem, s>>>(A, lda, B, ldb, nsplit > 1 ? ws : out, M, N, T, kchunk,
                                                       nsplit);
   if (nsplit > 1) {
     const int64_t n4 = (int64_t)M * N / 4;
@@ -204,7 +249,7 @@ void hx_wgrad_bf16_plan(int M, int N, int T, int* cfg, int* nsplit) {
 void hx_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, float* out, float* ws, int M, int N, int T,
                    int cfg, int nsplit, hipStream_t s) {
   if (cfg == 1)
-    launch<256, 256, 128, 64>((const uint16_t*)dy, ldy, (const uint16_t*)x, ldx, out, ws, M, N, T, nsplit, s);
+    launch<256, 128, 64, 64>((const uint16_t*)dy, ldy, (const uint16_t*)x, ldx, out, ws, M, N, T, nsplit, s);
   else
     launch<128, 128, 64, 64>((const uint16_t*)dy, ldy, (const uint16_t*)x, ldx, out, ws, M, N, T, nsplit, s);
 }

@@ -75,6 +75,9 @@ class Controller(object):
                                    broadcast_params=use_reducer)
         if not use_reducer:
             self.reducer.enabled = False
+        elif getattr(args, 'allreduce_impl', 'rccl') == 'xgmi':
+            self.reducer.use_xgmi(blocks=getattr(args, 'xgmi_blocks', 64),
+                                  timeout_s=float(getattr(args, 'distributed_timeout', 1800)))
         self._dummy_batch = dummy_batch
         self._oom_batch = oom_batch or dummy_batch
         self._lr_scheduler = None
@@ -131,6 +134,7 @@ class Controller(object):
 
     # ------------------------------------------------------------------ checkpoints
     def save_checkpoint(self, filename, extra_state, copies=()):
+        self.reducer.check_transport()   # never persist weights updated from timed-out reductions
         if dist_utils.is_master(self.args):
             extra_state['train_meters'] = checkpoint_utils.meters_state(self.meters)
             state = checkpoint_utils.build_state(

@@ -378,6 +378,47 @@ Tensor wgrad_bf16(Tensor dy, Tensor x, Tensor out) {
   return out;
 }
 
+// ------------------------------------------------------------------ xGMI all-reduce
+// Contexts travel to Python as integers (owned by parallel/xgmi.py).
+inline void xar_check(int rc) { TORCH_CHECK(rc == 0, hx_xar_last_error()); }
+inline void* as_ctx(int64_t h) { return reinterpret_cast<void*>(static_cast<uintptr_t>(h)); }
+int64_t xar_create(int64_t rank, int64_t world, int64_t cap_floats, int64_t nblocks, double timeout_s) {
+  void* c = nullptr;
+  xar_check(hx_xar_create((int)rank, (int)world, cap_floats, (int)nblocks, timeout_s, &c));
+  return static_cast<int64_t>(reinterpret_cast<uintptr_t>(c));
+}
+py::bytes xar_export(int64_t h) {
+  char buf[128];
+  xar_check(hx_xar_export(as_ctx(h), buf));
+  return py::bytes(buf, 128);
+}
+void xar_open(int64_t h, py::bytes handles) {
+  const std::string s = handles;
+  xar_check(hx_xar_open(as_ctx(h), s.data()));
+}
+void xar_allreduce(int64_t h, Tensor buf) {
+  check_f32(buf, "all-reduce bucket");
+  TORCH_CHECK(aligned16(buf.data_ptr()), "all-reduce bucket must be 16-byte aligned");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(buf.device());
+  xar_check(hx_xar_allreduce(as_ctx(h), buf.data_ptr<float>(), buf.numel(), cur_stream(buf)));
+}
+void xar_allreduce_sim(std::vector<int64_t> hs, std::vector<Tensor> bufs) {
+  TORCH_CHECK(hs.size() == bufs.size() && hs.size() >= 2 && hs.size() <= 8, "1 context per simulated rank (2..8)");
+  std::vector<void*> cs;
+  std::vector<float*> ps;
+  for (size_t i = 0; i < hs.size(); ++i) {
+    check_f32(bufs[i], "bucket");
+    TORCH_CHECK(bufs[i].numel() == bufs[0].numel() && aligned16(bufs[i].data_ptr()), "equal, aligned buckets");
+    cs.push_back(as_ctx(hs[i]));
+    ps.push_back(bufs[i].data_ptr<float>());
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(bufs[0].device());
+  xar_check(hx_xar_allreduce_sim(cs.data(), ps.data(), (int)hs.size(), bufs[0].numel(), cur_stream(bufs[0])));
+}
+int64_t xar_error(int64_t h) { return hx_xar_error(as_ctx(h)); }
+int64_t xar_capacity(int64_t h) { return hx_xar_capacity(as_ctx(h)); }
+void xar_destroy(int64_t h) { hx_xar_destroy(as_ctx(h)); }
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -398,6 +439,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd);
   m.def("wgrad_bf16", &wgrad_bf16);
   m.def("wgrad_bf16_ok", &wgrad_bf16_ok);
+  m.def("xar_create", &xar_create);
+  m.def("xar_export", &xar_export);
+  m.def("xar_open", &xar_open);
+  m.def("xar_allreduce", &xar_allreduce);
+  m.def("xar_allreduce_sim", &xar_allreduce_sim);
+  m.def("xar_error", &xar_error);
+  m.def("xar_capacity", &xar_capacity);
+  m.def("xar_destroy", &xar_destroy);
   m.def("set_debug", &set_debug);
   m.def("get_debug", &get_debug);
 }

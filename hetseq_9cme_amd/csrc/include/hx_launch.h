@@ -63,3 +63,15 @@ void hx_attn_fwd(int bf16, const void* qkv, const float* bias, const float* mask
 void hx_attn_bwd(int bf16, const void* qkv, const float* bias, float* dbq, float* dbk, float* dbv, float* dbias_part,
                  const float* maskb, const void* dout, const void* out, const float* lse, const uint32_t* dmask,
                  void* dqkv, float* dq_acc, int dq_ld, int B, int S, int nh, float keep, hipStream_t s);
+
+// xgmi_allreduce.hip -- intra-node two-shot all-reduce over IPC-mapped peer buffers.
+// Every function returns 0 on success, -1 with a message in hx_xar_last_error().
+const char* hx_xar_last_error();
+int hx_xar_create(int rank, int world, int64_t cap_floats, int nblocks, double timeout_s, void** ctx);
+int64_t hx_xar_capacity(void* ctx);
+int hx_xar_export(void* ctx, char* out128);
+int hx_xar_open(void* ctx, const char* handles);
+int hx_xar_allreduce(void* ctx, float* buf, int64_t n, hipStream_t s);
+int hx_xar_allreduce_sim(void** ctxs, float** bufs, int W, int64_t n, hipStream_t s);
+int hx_xar_error(void* ctx);
+void hx_xar_destroy(void* ctx);

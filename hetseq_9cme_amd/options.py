@@ -169,6 +169,11 @@ def add_distributed_training_args(parser):
                        help='gradient reducer backend (kept for flag compatibility)')
     group.add_argument('--bucket-cap-mb', default=25, type=int, metavar='MB',
                        help='gradient all-reduce bucket size')
+    group.add_argument('--allreduce-impl', default='rccl', choices=['rccl', 'xgmi'],
+                       help='gradient all-reduce transport: RCCL, or the hand-written intra-node two-shot '
+                            'xGMI kernel over IPC-mapped peer buffers (single host only; falls back to RCCL)')
+    group.add_argument('--xgmi-blocks', default=64, type=int, metavar='N',
+                       help='workgroups per xGMI all-reduce launch (CUs taken from backward while it runs)')
     group.add_argument('--fix-batches-to-gpus', action='store_true')
     group.add_argument('--find-unused-parameters', default=False, action='store_true')
     group.add_argument('--fast-stat-sync', default=False, action='store_true')

@@ -27,7 +27,13 @@ latency (≈ a few MB per peer).  ``--bucket-cap-mb`` keeps the reference's
 default of 25 MB; bucket boundaries are padded to multiples of W x 256 B of
 elements so that every per-peer chunk is 256 B aligned for uneven worlds
 (W = 3, 5, ...).
+
+``use_xgmi()`` swaps the per-bucket transport for the hand-written intra-node
+two-shot xGMI kernel (``parallel/xgmi.py``): buckets are then reduced on a
+dedicated high-priority HIP stream that waits for the producing stream(s), and
+the end-of-backward callback makes the compute stream wait for it.
 """
+import warnings
 import contextlib
 
 import torch
@@ -72,6 +78,7 @@ class GradReducer(object):
             for i in idxs:
                 self.bucket_of[i] = b
         self._align = align
+        self.xgmi = None
         self._pending = [0] * len(buckets)
         self.used = [False] * len(flat.params)
         self._reset_iteration()
@@ -111,11 +118,38 @@ class GradReducer(object):
         self._pending[b] -= 1
         self._launch_ready()
 
+    def use_xgmi(self, blocks=64, timeout_s=1800.0):
+        """Reduce gradient buckets with the intra-node xGMI kernel (collective call).
+        Returns False (and keeps RCCL) when the group is not eligible."""
+        from .xgmi import XgmiAllReduce, xgmi_eligible
+        if not self.enabled or self.flat.grad_flat.dtype != torch.float32:
+            return False
+        ok, why = xgmi_eligible(self.group)
+        if not ok:
+            warnings.warn('--allreduce-impl xgmi unavailable ({}); using RCCL'.format(why))
+            return False
+        cap_mb = max(b[1] - b[0] for b in self.buckets) * 4 / 2 ** 20
+        self.xgmi = XgmiAllReduce(self.group, cap_mb=min(max(cap_mb, 1), 128), blocks=blocks, timeout_s=timeout_s)
+        return True
+
+    def check_transport(self):
+        """Raise if the xGMI transport reported a timed-out wait (synchronising)."""
+        if self.xgmi is not None:
+            self.xgmi.check()
+
     def _launch_ready(self, force=False):
         while self._launched < len(self.buckets) and (force or self._pending[self._launched] == 0):
             s, e, _ = self.buckets[self._launched]
             side = ops.active_side_stream(self.flat.grad_flat.device)
-            if side is not None:
+            if self.xgmi is not None:
+                comm = self.xgmi.stream
+                comm.wait_stream(torch.cuda.current_stream())
+                if side is not None:
+                    comm.wait_stream(side)
+                with torch.cuda.stream(comm):
+                    self.xgmi.all_reduce_(self.flat.grad_flat[s:e])
+                work = None
+            elif side is not None:
                 # weight grads of this bucket may come from the side stream: launch
                 # the collective from it (after the compute stream's work so far)
                 side.wait_stream(torch.cuda.current_stream())
@@ -133,8 +167,11 @@ class GradReducer(object):
                 self.flat.adopt(i)   # unused this micro-batch: keep/zero its slot
         if self.enabled and self._sync:
             self._launch_ready(force=True)   # unused params: their slices hold zeros
+            if self.xgmi is not None:
+                torch.cuda.current_stream().wait_stream(self.xgmi.stream)
             for w in self._works:
-                w.wait()                      # stream-level wait for RCCL, no host block
+                if w is not None:
+                    w.wait()                  # stream-level wait for RCCL, no host block
         self._works = []
 
     # ------------------------------------------------------------------
@@ -157,9 +194,15 @@ class GradReducer(object):
         """Synchronously reduce the whole gradient buffer (used when a rank ran
         no backward this step, e.g. a pure dummy update)."""
         if self.enabled:
-            dist.all_reduce(self.flat.grad_flat, group=self.group)
+            if self.xgmi is not None:
+                self.xgmi.all_reduce_(self.flat.grad_flat)
+            else:
+                dist.all_reduce(self.flat.grad_flat, group=self.group)
 
     def remove(self):
+        if self.xgmi is not None:
+            self.xgmi.close()
+            self.xgmi = None
         for h in self._hooks:
             h.remove()
         self._hooks = []

@@ -115,6 +115,7 @@ def train(args, controller, task, epoch_itr):
             sums = dist_utils.all_gather_list(controller.param_checksum())
             assert all(abs(s - sums[0]) <= 1e-6 * max(1.0, abs(sums[0])) for s in sums), \
                 'parameter replicas diverged across ranks: {}'.format(sums)
+            controller.reducer.check_transport()
         if (args.save_interval_updates > 0 and num_updates % args.save_interval_updates == 0
                 and not epoch_itr.end_of_epoch()):
             checkpoint_utils.save_checkpoint(args, controller, epoch_itr, None)

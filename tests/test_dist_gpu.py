@@ -31,7 +31,11 @@ def test_two_rank_gpu_equivalence(dev, tmp_path):
     runs = {'one': ['--update-freq', '2', '--distributed-world-size', '1'],
             'two': ['--distributed-world-size', '2', '--distributed-backend', 'gloo'],
             'one4': ['--update-freq', '4', '--distributed-world-size', '1'],
-            'two2': ['--update-freq', '2', '--distributed-world-size', '2', '--distributed-backend', 'gloo']}
+            'two2': ['--update-freq', '2', '--distributed-world-size', '2', '--distributed-backend', 'gloo'],
+            # gradient buckets through the hand-written two-shot kernel over IPC-mapped buffers
+            # (both ranks on this box's one GPU; kernel waits bounded by the 60 s timeout)
+            'twox': ['--distributed-world-size', '2', '--distributed-backend', 'gloo', '--allreduce-impl', 'xgmi',
+                     '--distributed-timeout', '60']}
     ck = {}
     for name, extra in runs.items():
         save = str(tmp_path / name)
@@ -43,6 +47,8 @@ def test_two_rank_gpu_equivalence(dev, tmp_path):
             ck[name] = torch.load(os.path.join(save, 'checkpoint_last.pt'), map_location='cpu', weights_only=True)
     for k, v in ck['one']['model'].items():
         torch.testing.assert_close(ck['two']['model'][k], v, rtol=1e-4, atol=1e-6, msg=k)
+    for k, v in ck['one']['model'].items():
+        torch.testing.assert_close(ck['twox']['model'][k], v, rtol=1e-4, atol=1e-6, msg=k)
     for k, v in ck['one4']['model'].items():
         torch.testing.assert_close(ck['two2']['model'][k], v, rtol=1e-4, atol=1e-6, msg=k)
     assert ck['two2']['optimizer_history'][-1]['num_updates'] == 2

@@ -143,8 +143,9 @@ def test_data_parallel_gradient_equivalence(tmp_path, bert_data):
     one = str(tmp_path / 'one')
     two = str(tmp_path / 'two')
     run_cli(bert_argv(data, cfg0, vocab, one, ['--max-update', '1', '--update-freq', '2']))
+    # --allreduce-impl xgmi on CPU/gloo: not eligible -> warns and keeps the c10d transport
     run_cli(bert_argv(data, cfg0, vocab, two, ['--max-update', '1', '--distributed-world-size', '2',
-                                               '--distributed-backend', 'gloo']))
+                                               '--distributed-backend', 'gloo', '--allreduce-impl', 'xgmi']))
     c1 = load(os.path.join(one, 'checkpoint_last.pt'))
     c2 = load(os.path.join(two, 'checkpoint_last.pt'))
     for k in c1['model']:

@@ -9,7 +9,7 @@ from hetseq_9cme_amd import options  # noqa: E402
 
 NEW = {'--async-save', '--check-params-every', '--distributed-timeout', '--ent_name_id_file', '--fused-kernels',
        '--gemm-tuning', '--gemm-tuning-file', '--precision', '--profile-phases', '--user-module',
-       '--overlap-wgrad', '--debug-kernels'}
+       '--overlap-wgrad', '--debug-kernels', '--allreduce-impl', '--xgmi-blocks'}
 
 SECTIONS = [('bert', 'adam'), ('mnist', 'adadelta'), ('BertForTokenClassification', 'adam'),
             ('BertForELClassification', 'adam')]

@@ -44,6 +44,7 @@ def parse():
     ap.add_argument('--no-fused', action='store_true', help='torch-op baseline (A/B only)')
     ap.add_argument('--data-dir', default=None)
     ap.add_argument('--update-freq', type=int, default=1)
+    ap.add_argument('--num-workers', type=int, default=4, help='batch loader threads')
     ap.add_argument('--gemm-tuning', default='table', choices=['off', 'table', 'online', 'retune'])
     ap.add_argument('--gemm-tuning-file', default=None)
     ap.add_argument('--profile-phases', action='store_true',
@@ -88,7 +89,7 @@ def main():
 
     argv = ['--task', 'bert', '--data', data_dir, '--config_file', cfg_path, '--max-sentences', str(a.batch),
             '--fast-stat-sync', '--lr', '1e-4', '--warmup-updates', '10000', '--weight-decay', '0.01',
-            '--total-num-update', '1000000', '--clip-norm', '25', '--num-workers', '4', '--log-format', 'none',
+            '--total-num-update', '1000000', '--clip-norm', '25', '--num-workers', str(a.num_workers), '--log-format', 'none',
             '--disable-validation', '--no-save', '--precision', a.precision, '--distributed-world-size', str(world),
             '--update-freq', str(a.update_freq), '--gemm-tuning', a.gemm_tuning]
     if a.profile_phases:
@@ -188,6 +189,19 @@ def main():
               'ms/step'.format(host_t * 1e3 / n, tot * 1e3 / n), file=sys.stderr, flush=True)
         if ph['device']:
             print('phases device ms/step: ' + fmt(ph['device']), file=sys.stderr, flush=True)
+            # host lead: how much queued work the GPU had when each phase was opened
+            ctrl.phases.lead_trace = []
+            ev0 = torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            ev0.record()
+            t0 = time.perf_counter()
+            for _ in range(2 * n):
+                ctrl.train_step(next(itr))
+            torch.cuda.synchronize()
+            lead = ctrl.phases.host_lead(t0, ev0)
+            ctrl.phase_report()
+            print('host lead at phase start, ms (mean/min): ' + ', '.join(
+                '{}={:.2f}/{:.2f}'.format(k, m, lo) for k, (m, lo) in lead.items()), file=sys.stderr, flush=True)
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()

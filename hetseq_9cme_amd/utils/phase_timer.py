@@ -33,6 +33,7 @@ class PhaseTimer(object):
         self._t0 = 0.0
         self._ev0 = None
         self._pending = deque()
+        self.lead_trace = None   # list -> also record (phase, host time, event) for host-lead analysis
 
     def begin(self, name):
         """Close the open phase (if any) and open ``name`` (None: just close)."""
@@ -50,6 +51,8 @@ class PhaseTimer(object):
             if self.use_roctx:
                 torch.cuda.nvtx.range_pop()
         self._cur, self._t0, self._ev0 = name, now, ev
+        if self.lead_trace is not None and ev is not None and name is not None:
+            self.lead_trace.append((name, now, ev))
         if name is not None and self.use_roctx:
             torch.cuda.nvtx.range_push(name)
         self._drain(block=False)
@@ -68,6 +71,17 @@ class PhaseTimer(object):
                 b.synchronize()
             self.device[name] = self.device.get(name, 0.0) + a.elapsed_time(b) / 1e3
             self._pending.popleft()
+
+    def host_lead(self, t0, ev0):
+        """After a synchronize: per phase, how far the host ran ahead of the device when it
+        opened the phase (ms; mean and min over the trace).  ~0 means the GPU was starved at
+        that point (launch-bound); large values mean the host had work queued in advance."""
+        out = {}
+        for name, th, ev in self.lead_trace or []:
+            lead = ev0.elapsed_time(ev) - (th - t0) * 1e3
+            out.setdefault(name, []).append(lead)
+        self.lead_trace = None
+        return {k: (sum(v) / len(v), min(v)) for k, v in out.items()}
 
     def report(self, reset=True):
         """{'host': {phase: seconds}, 'device': {phase: seconds}, 'steps': n}."""

@@ -7,5 +7,5 @@ mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace -d $out -o run -- python3 bench.py --steps 7 --warmup 3 "$@" > $out/bench.log 2>&1 &&
 db=$(find $out -name '*results.db' | head -n 1) &&
-python3 tools/prof_summary.py "$db" --steps 6 > $out/summary.md &&
+python3 tools/prof_summary.py "$db" --steps 6 --gaps 25 --seq 10 > $out/summary.md &&
 rm -f "$db"

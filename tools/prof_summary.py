@@ -29,12 +29,33 @@ def from_db(path, steps, marker):
             rows = rows[ends[-steps - 1] + 1:ends[-1] + 1]
     gaps = sum(max(0, rows[i][1] - rows[i - 1][2]) for i in range(1, len(rows)))
     span = rows[-1][2] - rows[0][1] if rows else 0
+    global GAP_ROWS
+    GAP_ROWS = rows
     agg = collections.OrderedDict()
     for n, s, e in rows:
         a = agg.setdefault(n, [0, 0])
         a[0] += 1
         a[1] += e - s
     return agg, gaps, span
+
+
+GAP_ROWS = None
+
+
+def gap_report(rows, steps, top):
+    """Largest idle gaps, aggregated by (previous kernel, next kernel) pair."""
+    agg = collections.defaultdict(lambda: [0, 0])
+    for i in range(1, len(rows)):
+        g = rows[i][1] - rows[i - 1][2]
+        if g > 0:
+            a = agg[(rows[i - 1][0][:60], rows[i][0][:60])]
+            a[0] += 1
+            a[1] += g
+    print('\n| idle before | after | count/step | idle us/step |')
+    print('|---|---|---|---|')
+    for (a, b), (n, g) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:top]:
+        print('| `{}` | `{}` | {:.1f} | {:.1f} |'.format(b.replace('|', '/'), a.replace('|', '/'), n / steps,
+                                                       g / 1e3 / steps))
 
 
 def from_csv(path):
@@ -50,6 +71,9 @@ def main():
     ap.add_argument('--steps', type=int, default=None)
     ap.add_argument('--marker', default='adam_k')
     ap.add_argument('--top', type=int, default=30)
+    ap.add_argument('--gaps', type=int, default=0, help='also list the N largest idle-gap kernel pairs')
+    ap.add_argument('--seq', type=float, default=0,
+                    help='print the last step as a dispatch sequence, marking gaps over this many us')
     a = ap.parse_args()
     if a.path.endswith('.db'):
         agg, gaps, span = from_db(a.path, a.steps, a.marker)
@@ -68,6 +92,16 @@ def main():
     if gaps is not None:
         print('Device span {:.2f} ms/step, idle between dispatches {:.2f} ms/step'.format(
             span / 1e6 / steps, gaps / 1e6 / steps))
+    if a.gaps and GAP_ROWS:
+        gap_report(GAP_ROWS, steps, a.gaps)
+    if a.seq and GAP_ROWS:
+        ends = [i for i, r in enumerate(GAP_ROWS) if a.marker in r[0]]
+        rows = GAP_ROWS[ends[-2] + 1:ends[-1] + 1] if len(ends) > 1 else GAP_ROWS
+        print('\n```')
+        for i, (n, st, e) in enumerate(rows):
+            g = (st - rows[i - 1][2]) / 1e3 if i else 0.0
+            print('{:4d} {:>8.1f} {:>8.1f}  {}{}'.format(i, g, (e - st) / 1e3, '>> ' if g > a.seq else '   ', n[:150]))
+        print('```')
 
 
 if __name__ == '__main__':

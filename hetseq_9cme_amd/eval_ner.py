@@ -19,6 +19,7 @@ from .data.collators import DataCollatorForTokenClassification
 from .data.ner_dataset import get_label_list, load_split, tokenize_and_align
 from .models.bert import BertConfig, BertForTokenClassification
 from .tasks.token_classification import build_tokenizer
+from .utils.hip_graphs import GraphedForward
 
 
 def get_entities(seq):
@@ -55,7 +56,7 @@ def ner_scores(true_seqs, pred_seqs):
 
 
 def evaluate(model_ckpt, config_file, vocab, test_file, label_list=None, train_file=None, device=None,
-             batch_size=32, max_length=512):
+             batch_size=32, max_length=512, graphs=True):
     device = torch.device(device or ('cuda' if torch.cuda.is_available() else 'cpu'))
     test = load_split(test_file)
     if label_list is None:
@@ -67,12 +68,14 @@ def evaluate(model_ckpt, config_file, vocab, test_file, label_list=None, train_f
     model.load_state_dict(load_checkpoint_to_cpu(model_ckpt)['model'], strict=True)
     model.to(device).eval()
     coll = DataCollatorForTokenClassification(tok)
+    # launch-bound loop (~100 short kernels per batch): replay one HIP graph per padded shape
+    fwd = GraphedForward(model) if (graphs and device.type == 'cuda') else model
     trues, preds = [], []
     with torch.no_grad():
         for i in range(0, len(feats), batch_size):
             batch = coll(feats[i:i + batch_size])
-            logits = model(batch['input_ids'].to(device), batch['token_type_ids'].to(device),
-                           batch['attention_mask'].to(device))
+            logits = fwd(batch['input_ids'].to(device), batch['token_type_ids'].to(device),
+                         batch['attention_mask'].to(device))
             pred = logits.argmax(-1).cpu()
             for row_p, row_l in zip(pred, batch['labels']):
                 keep = row_l != -100
@@ -89,9 +92,10 @@ def main(argv=None):
     p.add_argument('--test_file', required=True)
     p.add_argument('--train_file', default=None)
     p.add_argument('--cpu', action='store_true')
+    p.add_argument('--no-graphs', action='store_true', help='eager forward (no HIP-graph replay)')
     a = p.parse_args(argv)
     res = evaluate(a.model_ckpt, a.config_file, a.dict, a.test_file, train_file=a.train_file,
-                   device='cpu' if a.cpu else None)
+                   device='cpu' if a.cpu else None, graphs=not a.no_graphs)
     print('accuracy={accuracy:.4f} precision={precision:.4f} recall={recall:.4f} f1={f1:.4f}'.format(**res))
 
 

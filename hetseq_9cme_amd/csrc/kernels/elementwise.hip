@@ -27,70 +27,140 @@ __device__ __forceinline__ float act_f(float x) {
   return x;
 }
 
-template <typename T, int ACT>
-__global__ __launch_bounds__(NT) void bias_act_fwd_k(const T* __restrict__ y, const float* __restrict__ b,
-                                                   T* __restrict__ out, int64_t rows, int N) {
-  const int64_t n4 = rows * (int64_t)N / 4;
-  for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT) {
-    const int j = (int)((i * 4) % N);
-    float4 v = hx::load4(y + i * 4);
-    if (b) {
-      const float4 bb = *reinterpret_cast<const float4*>(b + j);
-      v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
+// VEC adjacent elements per lane = one 16-B access of the activations (4 fp32 / 8 bf16; fp32
+// bias rows of 8 take two); VEC == 4 for bf16 is the fallback when N is not a multiple of 8
+template <typename T, int VEC>
+__device__ __forceinline__ void ldv(const T* p, float (&v)[VEC]) {
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int k = 0; k < VEC; k += 4) {
+      const float4 x = *reinterpret_cast<const float4*>(p + k);
+      v[k] = x.x; v[k + 1] = x.y; v[k + 2] = x.z; v[k + 3] = x.w;
     }
-    v = make_float4(act_f<ACT>(v.x), act_f<ACT>(v.y), act_f<ACT>(v.z), act_f<ACT>(v.w));
-    hx::store4(out + i * 4, v);
+  } else if constexpr (VEC == 8) {
+    const uint4 x = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[2 * k] = __uint_as_float(w[k] << 16);
+      v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+    }
+  } else {
+    const float4 x = hx::load4(p);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  }
+}
+template <typename T, int VEC>
+__device__ __forceinline__ void stv(T* p, const float (&v)[VEC]) {
+  if constexpr (sizeof(T) == 4) {
+#pragma unroll
+    for (int k = 0; k < VEC; k += 4) *reinterpret_cast<float4*>(p + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
+  } else if constexpr (VEC == 8) {
+    uint4 x;
+    x.x = hx::f2bf(v[0]) | ((uint32_t)hx::f2bf(v[1]) << 16);
+    x.y = hx::f2bf(v[2]) | ((uint32_t)hx::f2bf(v[3]) << 16);
+    x.z = hx::f2bf(v[4]) | ((uint32_t)hx::f2bf(v[5]) << 16);
+    x.w = hx::f2bf(v[6]) | ((uint32_t)hx::f2bf(v[7]) << 16);
+    *reinterpret_cast<uint4*>(p) = x;
+  } else {
+    hx::store4(p, make_float4(v[0], v[1], v[2], v[3]));
+  }
+}
+
+// grid-stride over VEC-element vectors; the (row, column) position advances incrementally by
+// the constant grid stride (no 64-bit division per element)
+template <typename T, int ACT, int VEC>
+__global__ __launch_bounds__(NT) void bias_act_fwd_k(const T* __restrict__ y, const float* __restrict__ b,
+                                                   T* __restrict__ out, int64_t rows, int N, int step_cols) {
+  const int nv = N / VEC;
+  const int64_t nvec = rows * (int64_t)nv;
+  int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x;
+  int c = (int)(i % nv);       // once per thread
+  const int64_t stride = (int64_t)gridDim.x * NT;
+  for (; i < nvec; i += stride) {
+    float v[VEC];
+    ldv<T, VEC>(y + i * VEC, v);
+    if (b) {
+      float bb[VEC];
+      ldv<float, VEC>(b + c * VEC, bb);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) v[k] += bb[k];
+    }
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) v[k] = act_f<ACT>(v[k]);
+    stv<T, VEC>(out + i * VEC, v);
+    c += step_cols;
+    if (c >= nv) c -= nv;
   }
 }
 
 // Column-tiled backward with fused column partials.
-// grid: (ceil(N/256) column tiles, ceil(rows/64) row chunks); block = 4 waves.
-// lane -> 4 adjacent columns (16 B), wave w -> rows w, w+4, ... of the chunk;
-// the 4 waves' float4 partials are combined in LDS -> partial[chunk][N].
-template <typename T, int ACT>
+// grid: (ceil(N / (64 VEC)) column tiles, ceil(rows/64) row chunks); block = 4 waves.
+// lane -> VEC adjacent columns (16 B), wave w -> rows w, w+4, ... of the chunk (two rows in
+// flight per iteration); the 4 waves' partials are combined in LDS -> partial[chunk][N].
+template <typename T, int ACT, int VEC>
 __global__ __launch_bounds__(NT) void bias_act_bwd_k(const T* __restrict__ dout, const T* __restrict__ y,
                                                    const float* __restrict__ b, const T* __restrict__ saved_out,
                                                    T* __restrict__ dy, float* __restrict__ partial, int64_t rows,
                                                    int N) {
-  __shared__ float4 red[4][64];
+  __shared__ float red[4][VEC][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int j = (blockIdx.x * 64 + lane) * 4;
+  const int j = (blockIdx.x * 64 + lane) * VEC;
   const int64_t r0 = (int64_t)blockIdx.y * hx::kRowChunk;
   const int64_t r1 = r0 + hx::kRowChunk < rows ? r0 + hx::kRowChunk : rows;
-  float4 acc = hx::f4(0.f);
-  if (j < N) {
-    float4 bb = hx::f4(0.f);
-    if (b) bb = *reinterpret_cast<const float4*>(b + j);
-    for (int64_t r = r0 + w; r < r1; r += 4) {
-      const int64_t o = r * N + j;
-      const float4 d = hx::load4(dout + o);
-      float4 g;
-      if (ACT == ACT_GELU) {
-        const float4 x = hx::load4(y + o);
-        g = make_float4(hx::gelu_grad_f(x.x + bb.x), hx::gelu_grad_f(x.y + bb.y), hx::gelu_grad_f(x.z + bb.z),
-                        hx::gelu_grad_f(x.w + bb.w));
-      } else if (ACT == ACT_TANH) {
-        const float4 t = hx::load4(saved_out + o);
-        g = make_float4(1.f - t.x * t.x, 1.f - t.y * t.y, 1.f - t.z * t.z, 1.f - t.w * t.w);
-      } else if (ACT == ACT_RELU) {
-        const float4 t = hx::load4(saved_out + o);
-        g = make_float4(t.x > 0.f, t.y > 0.f, t.z > 0.f, t.w > 0.f);
-      } else {
-        g = hx::f4(1.f);
-      }
-      const float4 r4 = make_float4(d.x * g.x, d.y * g.y, d.z * g.z, d.w * g.w);
-      if (dy) hx::store4(dy + o, r4);
-      acc.x += r4.x; acc.y += r4.y; acc.z += r4.z; acc.w += r4.w;
+  float acc[VEC];
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
+  auto row = [&](int64_t r, const float (&bb)[VEC]) {
+    const int64_t o = r * N + j;
+    float d[VEC], g[VEC];
+    ldv<T, VEC>(dout + o, d);
+    if (ACT == ACT_GELU) {
+      ldv<T, VEC>(y + o, g);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) g[k] = hx::gelu_grad_f(g[k] + bb[k]);
+    } else if (ACT == ACT_TANH) {
+      ldv<T, VEC>(saved_out + o, g);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) g[k] = 1.f - g[k] * g[k];
+    } else if (ACT == ACT_RELU) {
+      ldv<T, VEC>(saved_out + o, g);
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) g[k] = g[k] > 0.f ? 1.f : 0.f;
+    } else {
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) g[k] = 1.f;
     }
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      d[k] *= g[k];
+      acc[k] += d[k];
+    }
+    if (dy) stv<T, VEC>(dy + o, d);
+  };
+  if (j < N) {
+    float bb[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) bb[k] = 0.f;
+    if (b) ldv<float, VEC>(b + j, bb);
+    int64_t r = r0 + w;
+    for (; r + 4 < r1; r += 8) {
+      row(r, bb);
+      row(r + 4, bb);
+    }
+    for (; r < r1; r += 4) row(r, bb);
   }
   if (!partial) return;
-  red[w][lane] = acc;
+#pragma unroll
+  for (int k = 0; k < VEC; ++k) red[w][k][lane] = acc[k];
   __syncthreads();
   if (w == 0 && j < N) {
-    const float4 a = red[0][lane], b1 = red[1][lane], c = red[2][lane], d = red[3][lane];
-    *reinterpret_cast<float4*>(partial + (int64_t)blockIdx.y * N + j) =
-        make_float4((a.x + b1.x) + (c.x + d.x), (a.y + b1.y) + (c.y + d.y), (a.z + b1.z) + (c.z + d.z),
-                    (a.w + b1.w) + (c.w + d.w));
+    float o[VEC];
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) o[k] = (red[0][k][lane] + red[1][k][lane]) + (red[2][k][lane] + red[3][k][lane]);
+    float* dst = partial + (int64_t)blockIdx.y * N + j;
+#pragma unroll
+    for (int k = 0; k < VEC; k += 4) *reinterpret_cast<float4*>(dst + k) = make_float4(o[k], o[k + 1], o[k + 2], o[k + 3]);
   }
 }
 
@@ -160,43 +230,53 @@ inline int egrid(int64_t n_vec) {
 
 inline int nchunks(int64_t rows) { return (int)((rows + hx::kRowChunk - 1) / hx::kRowChunk); }
 
+template <typename T, int VEC>
+void bias_act_fwd_v(int act, const void* y, const float* b, void* out, int64_t rows, int N, hipStream_t s) {
+  const int nv = N / VEC;
+  const int g = egrid(rows * (int64_t)nv);
+  const int64_t stride = (int64_t)g * NT;
+  const int sc = (int)(stride % nv);
+  switch (act) {
+    case ACT_GELU: bias_act_fwd_k<T, ACT_GELU, VEC><<<g, NT, 0, s>>>((const T*)y, b, (T*)out, rows, N, sc); break;
+    case ACT_TANH: bias_act_fwd_k<T, ACT_TANH, VEC><<<g, NT, 0, s>>>((const T*)y, b, (T*)out, rows, N, sc); break;
+    case ACT_RELU: bias_act_fwd_k<T, ACT_RELU, VEC><<<g, NT, 0, s>>>((const T*)y, b, (T*)out, rows, N, sc); break;
+    default: bias_act_fwd_k<T, ACT_NONE, VEC><<<g, NT, 0, s>>>((const T*)y, b, (T*)out, rows, N, sc); break;
+  }
+}
+
 template <typename T>
 void bias_act_fwd_t(int act, const void* y, const float* b, void* out, int64_t rows, int N, hipStream_t s) {
-  const int g = egrid(rows * (int64_t)N / 4);
+  if (sizeof(T) == 2 && N % 8 == 0) bias_act_fwd_v<T, 8>(act, y, b, out, rows, N, s);
+  else bias_act_fwd_v<T, 4>(act, y, b, out, rows, N, s);
+}
+
+template <typename T, int VEC>
+void bias_act_bwd_v(int act, const void* dout, const void* y, const float* b, const void* saved_out, void* dy,
+                    float* partial, float* dbias, int64_t rows, int N, int accumulate, hipStream_t s) {
+  const int ncb = (N + 64 * VEC - 1) / (64 * VEC);
+  const int nch = nchunks(rows);
+  dim3 g(ncb, nch);
+  float* part = dbias ? partial : nullptr;
+#define HX_BAB(A)                                                                                            \
+  bias_act_bwd_k<T, A, VEC><<<g, NT, 0, s>>>((const T*)dout, (const T*)y, b, (const T*)saved_out, (T*)dy, part, \
+                                             rows, N)
   switch (act) {
-    case ACT_GELU: bias_act_fwd_k<T, ACT_GELU><<<g, NT, 0, s>>>((const T*)y, b, (T*)out, rows, N); break;
-    case ACT_TANH: bias_act_fwd_k<T, ACT_TANH><<<g, NT, 0, s>>>((const T*)y, b, (T*)out, rows, N); break;
-    case ACT_RELU: bias_act_fwd_k<T, ACT_RELU><<<g, NT, 0, s>>>((const T*)y, b, (T*)out, rows, N); break;
-    default: bias_act_fwd_k<T, ACT_NONE><<<g, NT, 0, s>>>((const T*)y, b, (T*)out, rows, N); break;
+    case ACT_GELU: HX_BAB(ACT_GELU); break;
+    case ACT_TANH: HX_BAB(ACT_TANH); break;
+    case ACT_RELU: HX_BAB(ACT_RELU); break;
+    default: HX_BAB(ACT_NONE); break;
   }
+#undef HX_BAB
+  if (dbias) hx::fold_rows(partial, nch, N, N, N, dbias, nullptr, nullptr, accumulate, s);
 }
 
 template <typename T>
 void bias_act_bwd_t(int act, const void* dout, const void* y, const float* b, const void* saved_out, void* dy,
                     float* partial, float* dbias, int64_t rows, int N, int accumulate, hipStream_t s) {
-  const int ncb = (N + 255) / 256;
-  const int nch = nchunks(rows);
-  dim3 g(ncb, nch);
-  float* part = dbias ? partial : nullptr;
-  switch (act) {
-    case ACT_GELU:
-      bias_act_bwd_k<T, ACT_GELU><<<g, NT, 0, s>>>((const T*)dout, (const T*)y, b, (const T*)saved_out, (T*)dy,
-                                                   part, rows, N);
-      break;
-    case ACT_TANH:
-      bias_act_bwd_k<T, ACT_TANH><<<g, NT, 0, s>>>((const T*)dout, (const T*)y, b, (const T*)saved_out, (T*)dy,
-                                                   part, rows, N);
-      break;
-    case ACT_RELU:
-      bias_act_bwd_k<T, ACT_RELU><<<g, NT, 0, s>>>((const T*)dout, (const T*)y, b, (const T*)saved_out, (T*)dy,
-                                                   part, rows, N);
-      break;
-    default:
-      bias_act_bwd_k<T, ACT_NONE><<<g, NT, 0, s>>>((const T*)dout, (const T*)y, b, (const T*)saved_out, (T*)dy,
-                                                   part, rows, N);
-      break;
-  }
-  if (dbias) hx::fold_rows(partial, nch, N, N, N, dbias, nullptr, nullptr, accumulate, s);
+  if (sizeof(T) == 2 && N % 8 == 0)
+    bias_act_bwd_v<T, 8>(act, dout, y, b, saved_out, dy, partial, dbias, rows, N, accumulate, s);
+  else
+    bias_act_bwd_v<T, 4>(act, dout, y, b, saved_out, dy, partial, dbias, rows, N, accumulate, s);
 }
 
 }  // namespace

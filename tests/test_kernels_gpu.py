@@ -104,6 +104,35 @@ def test_bias_act(dev, act):
     _close(b.grad, br.grad, rtol=1e-4, atol=1e-3)
 
 
+@pytest.mark.parametrize('act,N', [('gelu', 3072), ('gelu', 772), ('tanh', 768)])
+def test_bias_act_bf16(dev, act, N):
+    """bf16 activations (16-B vectors of 8 bf16 per lane; N % 8 != 0 takes the 4-wide path)
+    vs fp32 math on the same bf16 inputs; bias gradient from the fp32 column partials."""
+    torch.manual_seed(0)
+    y = torch.randn(517, N, device=dev).to(torch.bfloat16).requires_grad_()
+    b = torch.randn(N, device=dev, requires_grad=True)
+    out = ops.bias_act(y, b, act)
+    assert out.dtype == torch.bfloat16
+    yr, br = y.detach().float().requires_grad_(), b.detach().clone().requires_grad_()
+    ref = fused._act_ref(yr + br, act)
+    _close(out.float(), ref, rtol=1e-2, atol=1e-2)
+    d = torch.randn_like(out)
+    out.backward(d)
+    ref.backward(d.float())
+    # tanh' = 1 - out^2 from the bf16-rounded saved output: cancellation near |out| = 1
+    tol = 1e-2 if act == 'gelu' else 4e-2
+    _close(y.grad.float(), yr.grad, rtol=1e-2, atol=tol)
+    _close(b.grad, br.grad, rtol=1e-3, atol=1e-2 if act == 'gelu' else 0.2)
+
+
+def test_colsum_bf16(dev):
+    torch.manual_seed(0)
+    for N in (768, 772, 130):   # 8-wide, 4-wide and scalar column paths
+        x = torch.randn(1000, N, device=dev).to(torch.bfloat16)
+        out = ops.C().colsum(x, None, None)
+        _close(out, x.float().sum(0), rtol=1e-4, atol=1e-3)
+
+
 def test_dropout_op(dev):
     ops.set_step_seed(5)
     x = torch.randn(1000, 33, device=dev, requires_grad=True)  # odd size -> tail path

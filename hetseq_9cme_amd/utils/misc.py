@@ -27,12 +27,19 @@ def apply_to_sample(f, sample):
 
 
 def move_to_device(sample, device, non_blocking=True):
-    """Move every tensor of a sample to ``device``.  Pinned host tensors are
-    copied asynchronously (the reference's ``.cuda()`` is synchronous and
+    """Move every tensor of a sample to ``device``.  Host tensors are copied
+    asynchronously: pageable ones are first staged through the (cached) pinned
+    host allocator, because a pageable ``.to(device)`` blocks the host until the
+    GPU has drained its queue -- once per batch tensor, which made small-batch
+    fine-tuning host-bound (the reference's ``.cuda()`` is synchronous and
     pageable, utils.py:32-37)."""
     def _move(t):
         if t.device == device:
             return t
+        if non_blocking and device.type == 'cuda' and t.device.type == 'cpu':
+            if not t.is_pinned():
+                t = t.pin_memory()
+            return t.to(device, non_blocking=True)
         return t.to(device, non_blocking=non_blocking and t.is_pinned())
     return apply_to_sample(_move, sample)
 

@@ -207,11 +207,12 @@ class EpochBatchIterator(EpochBatchIterating):
             loader = BatchReaderLoader(self.dataset, batches[offset:], num_workers=self.num_workers,
                                        pin_memory=self.pin_memory, device=self.device)
         else:
-            # pinned batches -> asynchronous H2D in the training step (no host/device sync)
-            pin = self.pin_memory or (self.device is not None and self.device.type == 'cuda')
+            # no DataLoader pin thread: it competes with the training loop for the GIL;
+            # the step pins its (small) batch itself before the asynchronous H2D copy
+            # (utils.misc.move_to_device)
             loader = torch.utils.data.DataLoader(self.dataset, collate_fn=self.collate_fn,
                                                  batch_sampler=[list(b) for b in batches[offset:]],
-                                                 num_workers=self.num_workers, pin_memory=pin)
+                                                 num_workers=self.num_workers, pin_memory=self.pin_memory)
         return CountingIterator(loader, start=offset)
 
 

@@ -120,3 +120,25 @@ def test_ner_eval_cli_and_transformers_task(tmp_path):
             loss.backward()
     loss, ss, lo = task.train_step(batch, model, _O())
     assert ss == 1 and torch.isfinite(loss)
+
+
+def test_ner_data_parallel_unused_params(tmp_path):
+    """BASELINE config 5's distributed shape in miniature: NER fine-tuning on 2 ranks (gloo)
+    with --find-unused-parameters (the pooler never gets a gradient), replicas checked
+    every update, and the same update as 1 rank x --update-freq 2 (dropout off)."""
+    vocab, _, tr, te = _setup(tmp_path)
+    cfg = write_bert_config(str(tmp_path / 'nodrop.json'), **dict(BERT_TINY, hidden_dropout_prob=0.0,
+                                                                 attention_probs_dropout_prob=0.0))
+    common = ['--task', 'BertForTokenClassification', '--optimizer', 'adam', '--fast-stat-sync',
+              '--max-update', '3', '--num-workers', '0', '--lr', '1e-3', '--dict', vocab, '--config_file', cfg,
+              '--train_file', tr, '--test_file', te, '--extension_file', 'conll', '--max-sentences', '8',
+              '--find-unused-parameters', '--cpu', '--seed', '3']
+    two, one = str(tmp_path / 'two'), str(tmp_path / 'one')
+    r = run_cli(common + ['--distributed-world-size', '2', '--distributed-backend', 'gloo',
+                          '--check-params-every', '1', '--save-dir', two])
+    assert 'done training' in r.stdout
+    run_cli(common + ['--update-freq', '2', '--save-dir', one])
+    c2, c1 = load(os.path.join(two, 'checkpoint_last.pt')), load(os.path.join(one, 'checkpoint_last.pt'))
+    assert c2['optimizer_history'][-1]['num_updates'] == 3
+    for k, v in c1['model'].items():
+        torch.testing.assert_close(c2['model'][k], v, rtol=1e-4, atol=1e-5, msg=k)

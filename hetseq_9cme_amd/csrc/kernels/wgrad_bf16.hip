@@ -22,6 +22,9 @@
 //    (shared dY / X rows stay in that XCD's L2).
 #include <algorithm>
 
+#include <stdio.h>
+#include <stdlib.h>
+
 #include "hx_launch.h"
 #include "hx_attn.h"
 #include "hx_common.h"
@@ -232,24 +235,47 @@ void launch(const uint16_t* A, int lda, const uint16_t* B, int ldb, float* out, 
 
 }  // namespace
 
-// Tile configuration and token split for an (M, N, T) weight gradient: the large tile
-// (256 x 256, 8 waves of 128 x 64) halves the L2 traffic per FLOP of the small one
-// (128 x 128, 4 waves of 64 x 64); the small one is used when the large one would need
-// so many splits that summing the fp32 partials costs more than the extra traffic.
+// Tile configurations (cfg index -> BM x BN workgroup tile, WM x WN per wave):
+//   0: 128x128, 4 waves of 64x64      1: 256x128, 8 waves of 64x64
+//   2: 256x256, 8 waves of 128x64     3: 256x128, 4 waves of 128x64
+//   4: 256x256, 4 waves of 128x128 (accumulators in AGPRs)
+// A wave's LDS fragment traffic per MFMA falls with its tile (64x64: 1 fragment per MFMA,
+// 128x64: 0.75, 128x128: 0.5); the workgroup tile sets the L2 traffic per FLOP.
+// HX_WGRAD_CFG="cfg:nsplit" overrides the plan (tuning sweeps: tools/bench_wgrad.py --sweep).
+static const int kTileM[5] = {128, 256, 256, 256, 256};
+static const int kTileN[5] = {128, 128, 256, 128, 256};
+
 void hx_wgrad_bf16_plan(int M, int N, int T, int* cfg, int* nsplit) {
-  const bool big = (M % 256 == 0) && (N % 256 == 0) && (int64_t)M * N >= 2 * 1024 * 1024;
-  const int tiles = big ? (M / 256) * (N / 256) : (M / 128) * (N / 128);
-  const int target = big ? 256 : 512;   // one 8-wave or two 4-wave workgroups per CU
-  int s = std::max(1, target / std::max(1, tiles));
+  // One wave of workgroups: the 8-wave 256x128 kernel runs one workgroup per CU (256 slots),
+  // the 4-wave 128x128 one two (512 slots).  The split count fills the slots without
+  // spilling into a second, mostly empty round (measured on MI355X, T = 16384: FFN dW
+  // 3 splits -> 216 workgroups 99 us vs 7 splits -> 504 workgroups 119 us;
+  // tools/bench_wgrad.py --sweep).
+  int c = (M % 256 == 0 && N % 128 == 0) ? 1 : 0;
+  const int slots = c == 1 ? 256 : 512;
+  const int tiles0 = (M / kTileM[c]) * (N / kTileN[c]);
+  int s = std::max(1, slots / std::max(1, tiles0));
   s = std::min(s, std::max(1, T / 256));   // at least 256 tokens per split
-  *cfg = big ? 1 : 0;
+  if (const char* e = getenv("HX_WGRAD_CFG")) {
+    int ec = -1, es = -1;
+    if (sscanf(e, "%d:%d", &ec, &es) == 2 && ec >= 0 && ec < 5 && es >= 1 && M % kTileM[ec] == 0 &&
+        N % kTileN[ec] == 0) {
+      c = ec;
+      s = std::min(es, std::max(1, T / BK));
+    }
+  }
+  *cfg = c;
   *nsplit = s;
 }
 
 void hx_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, float* out, float* ws, int M, int N, int T,
                    int cfg, int nsplit, hipStream_t s) {
-  if (cfg == 1)
-    launch<256, 128, 64, 64>((const uint16_t*)dy, ldy, (const uint16_t*)x, ldx, out, ws, M, N, T, nsplit, s);
-  else
-    launch<128, 128, 64, 64>((const uint16_t*)dy, ldy, (const uint16_t*)x, ldx, out, ws, M, N, T, nsplit, s);
+  const uint16_t *a = (const uint16_t*)dy, *b = (const uint16_t*)x;
+  switch (cfg) {
+    case 1: launch<256, 128, 64, 64>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
+    case 2: launch<256, 256, 128, 64>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
+    case 3: launch<256, 128, 128, 64>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
+    case 4: launch<256, 256, 128, 128>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
+    default: launch<128, 128, 64, 64>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
+  }
 }

@@ -33,7 +33,11 @@ def timeit(fn, iters=30, warmup=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--tokens', type=int, default=16384)
+    ap.add_argument('--sweep', action='store_true',
+                    help='time every (tile config, token split) of the hand-written kernel via HX_WGRAD_CFG')
     a = ap.parse_args()
+    if a.sweep:
+        return sweep(a.tokens)
     T = a.tokens
     try:
         from hetseq_9cme_amd.ops._ext import C
@@ -61,6 +65,35 @@ def main():
             print('[{}x{} T={}] {:<22s} {:8.1f} us  {:7.1f} TF/s{}'.format(
                 n_out, n_in, T, k, us, fl / us / 1e6, '' if err is None else '  rel.err {:.2e}'.format(err)),
                 flush=True)
+
+
+def sweep(T):
+    from hetseq_9cme_amd.ops._ext import C
+    tiles = {0: (128, 128), 1: (256, 128), 3: (256, 128)}
+    for (n_out, n_in) in [(3072, 768), (768, 3072), (2304, 768), (768, 768)]:
+        dy = torch.randn(T, n_out, device='cuda').to(torch.bfloat16)
+        x = torch.randn(T, n_in, device='cuda').to(torch.bfloat16)
+        slot = torch.empty(n_out, n_in, device='cuda')
+        ref = torch.mm(dy.t().float(), x.float())
+        fl = 2.0 * T * n_out * n_in
+        os.environ.pop('HX_WGRAD_CFG', None)
+        base = timeit(lambda: C().wgrad_bf16(dy, x, slot))
+        best = (base, 'plan')
+        for cfg, (bm, bn) in tiles.items():
+            if n_out % bm or n_in % bn:
+                continue
+            for ns in (1, 2, 3, 4, 6, 8, 12, 16):
+                os.environ['HX_WGRAD_CFG'] = '{}:{}'.format(cfg, ns)
+                us = timeit(lambda: C().wgrad_bf16(dy, x, slot))
+                err = ((slot - ref).abs().max() / ref.abs().max()).item()
+                assert err < 1e-3, (cfg, ns, err)
+                if us < best[0]:
+                    best = (us, '{}:{}'.format(cfg, ns))
+                print('[{}x{} T={}] cfg {} nsplit {:2d} {:8.1f} us {:7.1f} TF/s'.format(
+                    n_out, n_in, T, cfg, ns, us, fl / us / 1e6), flush=True)
+        os.environ.pop('HX_WGRAD_CFG', None)
+        print('[{}x{} T={}] plan {:.1f} us; best {} {:.1f} us ({:.1f} TF/s)'.format(
+            n_out, n_in, T, base, best[1], best[0], fl / best[0] / 1e6), flush=True)
 
 
 if __name__ == '__main__':

@@ -42,31 +42,41 @@ constexpr int BK = 32;   // tokens per pipeline step (two 16-deep MFMA k-steps)
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // LDS image of a [BK rows][W columns] bf16 tile: 8-row x 32-column subtiles of 512 B with
-// XOR-swizzled 16-B chunks (cdna_hip_programming.md T10 layout (a)).  Byte offset of 16-B
-// chunk ch of row `row`.  Conflict-free for the 16-B chunk stores and for the transposed
-// reads below, and LINEAR in 32-column blocks (+512 B) and 16-row k-steps (+32W B), so a
-// wave needs two address registers (rows q and q+4) per operand: every other fragment
-// read is the same VGPR plus an immediate offset.
+// XOR-swizzled 16-B chunks (cdna_hip_programming.md T10 layout (a)); in odd subtiles the
+// rows of each pair swap places (row slot (row & 7) ^ 1).  Byte offset of 16-B chunk ch of
+// row `row`.  The 16-B stores are serviced in groups of 8 lanes on 32 banks (128 B): the 8
+// chunks of a group span two subtiles 512 B apart, which without the row swap land on the
+// same 64 B of banks (2-way conflict on every store, ~30 % of the LDS-array cycles in the
+// PMC trace); with it they cover all 32 banks.  The transposed reads (2 x 32 lanes on 64
+// banks) stay conflict-free.  Linear in 32-column PAIRS of blocks (+1024 B) and 16-row
+// k-steps (+32W B), so a wave needs two address registers per operand and subtile parity
+// (rows q and q+4, even/odd subtile): every other fragment read is an immediate offset.
 template <int W>
 __device__ __forceinline__ int toff(int row, int ch) {
-  return (row >> 3) * (16 * W) + 512 * (ch >> 2) + 64 * (row & 7) + 16 * ((ch & 3) ^ ((row >> 2) & 3));
+  return (row >> 3) * (16 * W) + 512 * (ch >> 2) + 64 * ((row & 7) ^ ((ch >> 2) & 1)) +
+         16 * ((ch & 3) ^ ((row >> 2) & 3));
 }
-// per-lane byte offsets of the two transposed reads of the (k0 = 0, c0 = 0) fragment
+// per-lane byte offsets of the two transposed reads of the (k0 = 0, c0 = 0) fragment (even
+// subtile) and of the c0 = 32 fragment minus its 512-B subtile base (odd subtile)
 template <int W>
-__device__ __forceinline__ void tr_base(int lane, int& lo, int& hi) {
+__device__ __forceinline__ void tr_base(int lane, int (&lo)[2], int (&hi)[2]) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
   const int row = 8 * (g >> 1) + q, ch = 2 * (g & 1) + (p >> 1);
-  lo = toff<W>(row, ch) + 8 * (p & 1);
-  hi = toff<W>(row + 4, ch) + 8 * (p & 1);
+  lo[0] = toff<W>(row, ch) + 8 * (p & 1);
+  hi[0] = toff<W>(row + 4, ch) + 8 * (p & 1);
+  lo[1] = toff<W>(row, ch + 4) - 512 + 8 * (p & 1);
+  hi[1] = toff<W>(row + 4, ch + 4) - 512 + 8 * (p & 1);
 }
 // k-major 32x32x16 operand fragment of columns c0 .. c0+31 (c0 % 32 == 0), rows k0 .. k0+15
 // (k0 % 16 == 0): lane l holds column c0 + (l & 31), rows k0 + 8(l >> 5) + j -- the gfx950
 // transposing LDS read delivers 4 rows of one column per read (two reads per fragment)
+// (odd = subtile parity (c0 >> 5) & 1, a compile-time constant at every call site)
 template <int W>
-__device__ __forceinline__ bf16x8 frag(const char* tile, int lo, int hi, int k0, int c0) {
+__device__ __forceinline__ bf16x8 frag(const char* tile, const int (&lo)[2], const int (&hi)[2], int k0, int c0,
+                                       int odd) {
   const int d = (k0 >> 4) * (32 * W) + (c0 >> 5) * 512;
-  const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(tile + lo + d));
-  const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(tile + hi + d));
+  const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(tile + lo[odd] + d));
+  const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(tile + hi[odd] + d));
   const v4i16 v[2] = {a, b};
   return *reinterpret_cast<const bf16x8*>(v);
 }
@@ -78,6 +88,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_bf16_k(
   constexpr int NWM = BM / WM, NW = NWM * (BN / WN), NT = NW * 64;
   constexpr int MB = WM / 32, NB = WN / 32;
   constexpr int CA = BK * BM / 8 / NT, CB = BK * BN / 8 / NT;   // 16-B chunks per thread
+  static_assert(WM % 64 == 0 && WN % 64 == 0, "subtile parity of fragment a is a & 1");
   static_assert(CA >= 1 && CB >= 1 && BK * BM / 8 % NT == 0 && BK * BN / 8 % NT == 0, "tile / thread mismatch");
   constexpr int A_BYTES = BK * BM * 2, B_BYTES = BK * BN * 2;
   extern __shared__ __attribute__((aligned(16))) char lds[];   // [2] A tiles, then [2] B tiles
@@ -115,7 +126,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_bf16_k(
     vb[i] = (uint32_t)(row * ldb + n0 + 8 * ch) * 2;
     sb[i] = toff<BN>(row, ch);
   }
-  int alo, ahi, blo, bhi;
+  int alo[2], ahi[2], blo[2], bhi[2];
   tr_base<BM>(lane, alo, ahi);
   tr_base<BN>(lane, blo, bhi);
 
@@ -152,9 +163,9 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_bf16_k(
     for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8 fa[MB], fb[NB];
 #pragma unroll
-      for (int a = 0; a < MB; ++a) fa[a] = frag<BM>(at, alo, ahi, 16 * ks, wm * WM + 32 * a);
+      for (int a = 0; a < MB; ++a) fa[a] = frag<BM>(at, alo, ahi, 16 * ks, wm * WM + 32 * a, a & 1);
 #pragma unroll
-      for (int b = 0; b < NB; ++b) fb[b] = frag<BN>(bt, blo, bhi, 16 * ks, wn * WN + 32 * b);
+      for (int b = 0; b < NB; ++b) fb[b] = frag<BN>(bt, blo, bhi, 16 * ks, wn * WN + 32 * b, b & 1);
 #pragma unroll
       for (int a = 0; a < MB; ++a)
 #pragma unroll

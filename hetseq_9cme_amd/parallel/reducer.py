@@ -195,7 +195,13 @@ class GradReducer(object):
         no backward this step, e.g. a pure dummy update)."""
         if self.enabled:
             if self.xgmi is not None:
-                self.xgmi.all_reduce_(self.flat.grad_flat)
+                # same stream as the bucket launches: two reductions must never share the
+                # staging buffer concurrently
+                comm = self.xgmi.stream
+                comm.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(comm):
+                    self.xgmi.all_reduce_(self.flat.grad_flat)
+                torch.cuda.current_stream().wait_stream(comm)
             else:
                 dist.all_reduce(self.flat.grad_flat, group=self.group)
 

@@ -53,6 +53,13 @@ def main():
         res['mm out_dtype=f32'] = timeit(lambda: torch.mm(dy.t(), x, out_dtype=torch.float32, out=slot))
         res['mm bf16 + cast'] = timeit(lambda: slot.copy_(torch.mm(dy.t(), x)))
         res['mm (x^T dy)^T f32'] = timeit(lambda: torch.mm(x.t(), dy, out_dtype=torch.float32))
+        for sk in (4, 8, 16):   # library split-K as a batched GEMM over token chunks + a sum
+            dyb = dy.view(sk, T // sk, n_out).transpose(1, 2)
+            xb = x.view(sk, T // sk, n_in)
+            res['bmm split{} bf16->f32+sum'.format(sk)] = timeit(
+                lambda: torch.sum(torch.bmm(dyb, xb, out_dtype=torch.float32), 0, out=slot))
+            res['bmm split{} bf16+sum'.format(sk)] = timeit(
+                lambda: torch.sum(torch.bmm(dyb, xb), 0, dtype=torch.float32, out=slot))
         if ext is not None:
             res['hx wgrad_bf16'] = timeit(lambda: ext.wgrad_bf16(dy, x, slot))
             ref = torch.mm(dy.t().float(), x.float())

@@ -45,6 +45,9 @@ def parse():
     ap.add_argument('--data-dir', default=None)
     ap.add_argument('--update-freq', type=int, default=1)
     ap.add_argument('--num-workers', type=int, default=4, help='batch loader threads')
+    ap.add_argument('--allreduce-impl', default='rccl', choices=['rccl', 'xgmi'],
+                    help='gradient all-reduce transport for N > 1 (RCCL, or the hand-written xGMI kernel)')
+    ap.add_argument('--bucket-cap-mb', type=int, default=25)
     ap.add_argument('--gemm-tuning', default='table', choices=['off', 'table', 'online', 'retune'])
     ap.add_argument('--gemm-tuning-file', default=None)
     ap.add_argument('--profile-phases', action='store_true',
@@ -91,7 +94,8 @@ def main():
             '--fast-stat-sync', '--lr', '1e-4', '--warmup-updates', '10000', '--weight-decay', '0.01',
             '--total-num-update', '1000000', '--clip-norm', '25', '--num-workers', str(a.num_workers), '--log-format', 'none',
             '--disable-validation', '--no-save', '--precision', a.precision, '--distributed-world-size', str(world),
-            '--update-freq', str(a.update_freq), '--gemm-tuning', a.gemm_tuning]
+            '--update-freq', str(a.update_freq), '--gemm-tuning', a.gemm_tuning,
+            '--allreduce-impl', a.allreduce_impl, '--bucket-cap-mb', str(a.bucket_cap_mb)]
     if a.profile_phases:
         argv += ['--profile-phases']
     if a.gemm_tuning_file:
@@ -162,7 +166,8 @@ def main():
                        'global_batch': global_batch, 'per_gpu_batch': a.batch * a.update_freq,
                        'seq_len': a.seq, 'max_pred': a.max_pred,
                        'parallelism': 'dp{}'.format(world), 'optimizer': 'adam(fused)',
-                       'fused_kernels': not a.no_fused, 'gemm_tuning': a.gemm_tuning},
+                       'fused_kernels': not a.no_fused, 'gemm_tuning': a.gemm_tuning,
+                       'allreduce': a.allreduce_impl if world > 1 else None},
             'final_logged_loss': round(loss, 5),
         }
         print(json.dumps(rec), flush=True)

@@ -48,6 +48,10 @@ def parse():
     ap.add_argument('--allreduce-impl', default='rccl', choices=['rccl', 'xgmi'],
                     help='gradient all-reduce transport for N > 1 (RCCL, or the hand-written xGMI kernel)')
     ap.add_argument('--bucket-cap-mb', type=int, default=25)
+    ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'],
+                    help='process-group backend (gloo only for rehearsals, e.g. with --same-device)')
+    ap.add_argument('--same-device', action='store_true',
+                    help='rehearsal on a 1-GPU box: every rank uses GPU 0 (numbers are not per-GPU)')
     ap.add_argument('--gemm-tuning', default='table', choices=['off', 'table', 'online', 'retune'])
     ap.add_argument('--gemm-tuning-file', default=None)
     ap.add_argument('--profile-phases', action='store_true',
@@ -74,7 +78,8 @@ def main():
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
     if world != a.gpus and world > 1:
         print('warning: --gpus {} but WORLD_SIZE {}'.format(a.gpus, world), file=sys.stderr)
-    torch.cuda.set_device(local_rank)
+    dev_index = 0 if a.same_device else local_rank
+    torch.cuda.set_device(dev_index)
 
     cfg = {'base': BERT_BASE, 'large': BERT_LARGE, 'tiny': BERT_TINY}[a.model]
     data_dir = a.data_dir or os.path.join(tempfile.gettempdir(), 'hx_bench_s{}_p{}_n{}'.format(
@@ -101,7 +106,8 @@ def main():
     if a.gemm_tuning_file:
         argv += ['--gemm-tuning-file', a.gemm_tuning_file]
     args = options.parse_training_args(argv)
-    args.device_id = local_rank
+    args.device_id = dev_index
+    args.distributed_backend = a.backend
     if world > 1:
         args.distributed_init_method = 'env://'
         args.distributed_rank = rank

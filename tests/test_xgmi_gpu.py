@@ -3,7 +3,7 @@
 * simulation: W ranks as ONE grid on one GPU (rank = blockIdx.y): chunking for uneven
   W (3, 5, 7), tails that are not float4 multiples, buckets smaller than W float4s,
   repeated calls (monotonic epochs), bitwise equality with the rank-order fp32 sum;
-* IPC: two processes on the box's GPU exchange staging/signal handles over a gloo
+* IPC: two or three processes (uneven W) on the box's GPU exchange staging/signal handles over a gloo
   group and reduce buckets through the mapped peer memory (the multi-GPU protocol
   minus the xGMI links themselves), including a bucket larger than the staging
   capacity (split into pieces).
@@ -41,15 +41,17 @@ WORKER = textwrap.dedent('''
     import os, sys, time, torch, torch.distributed as dist
     sys.path.insert(0, os.environ['ROOT'])
     from hetseq_9cme_amd.parallel.xgmi import XgmiAllReduce, xgmi_eligible
-    rank = int(os.environ['RANK'])
+    rank, W = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
     torch.cuda.set_device(0)
-    dist.init_process_group('gloo', rank=rank, world_size=2)
+    dist.init_process_group('gloo', rank=rank, world_size=W)
     ok, why = xgmi_eligible()
     assert ok, why
     xar = XgmiAllReduce(cap_mb=4, blocks=32, timeout_s=30.0)
     for it, n in enumerate([7, 4096, 1000003, 3 * 2 ** 20 + 5]):   # the last one > 4 MB staging
-        data = [torch.randn(n, generator=torch.Generator().manual_seed(100 * it + q)).cuda() for q in range(2)]
-        ref = data[0] + data[1]
+        data = [torch.randn(n, generator=torch.Generator().manual_seed(100 * it + q)).cuda() for q in range(W)]
+        ref = data[0].clone()
+        for q in range(1, W):
+            ref += data[q]          # the kernel's rank-order sum
         buf = data[rank].clone()
         xar.all_reduce_(buf)
         torch.cuda.synchronize()
@@ -66,21 +68,22 @@ WORKER = textwrap.dedent('''
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / 10
     xar.check()
-    assert torch.equal(big, torch.full_like(big, 2.0 ** 13)), big[:4]
+    assert torch.equal(big, torch.full_like(big, float(W) ** 13)), big[:4]
     if rank == 0:
-        print('XAR_OK 25MB bucket {:.1f} us (2 ranks on one GPU)'.format(dt * 1e6), flush=True)
+        print('XAR_OK 25MB bucket {:.1f} us ({} ranks on one GPU)'.format(dt * 1e6, W), flush=True)
     xar.close()
     dist.destroy_process_group()
 ''')
 
 
-def test_xgmi_allreduce_two_process_ipc(dev, tmp_path):
+@pytest.mark.parametrize('W', [2, 3])
+def test_xgmi_allreduce_multi_process_ipc(dev, tmp_path, W):
     script = tmp_path / 'xar_worker.py'
     script.write_text(WORKER)
-    env = dict(os.environ, ROOT=ROOT, MASTER_ADDR='127.0.0.1', MASTER_PORT=str(29500 + os.getpid() % 2000),
-               WORLD_SIZE='2')
+    env = dict(os.environ, ROOT=ROOT, MASTER_ADDR='127.0.0.1', MASTER_PORT=str(29500 + W + os.getpid() % 2000),
+               WORLD_SIZE=str(W))
     procs = [subprocess.Popen([sys.executable, '-u', str(script)], env=dict(env, RANK=str(r)),
-                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(2)]
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for r in range(W)]
     outs = []
     for p in procs:
         try:
@@ -89,6 +92,6 @@ def test_xgmi_allreduce_two_process_ipc(dev, tmp_path):
             for q in procs:
                 q.kill()
             raise
-    assert all(p.returncode == 0 for p in procs), outs[0][-3000:] + '\n----\n' + outs[1][-3000:]
+    assert all(p.returncode == 0 for p in procs), '\n----\n'.join(o[-3000:] for o in outs)
     assert 'XAR_OK' in outs[0]
     print([l for l in outs[0].splitlines() if 'XAR_OK' in l][0])

@@ -253,6 +253,7 @@ class Controller(object):
                     ph('forward')     # optimizer.backward() opens 'backward'
                     loss, sample_size, logging_output = self.task.train_step(sample, model, self.optimizer,
                                                                              ignore_grad)
+                    self.reducer.after_backward()
                     for k, u in enumerate(self.reducer.used):
                         if u:
                             step_used[k] = True

@@ -181,6 +181,15 @@ class GradReducer(object):
         self._reset_iteration()
         return used
 
+    def after_backward(self):
+        """Called after each micro-batch's backward. When no gradient hook fired
+        (the loss reached no parameter, or the task skipped backward), finalize
+        here: unused slots are zeroed and this rank still joins every bucket
+        collective the other ranks launch instead of leaving them waiting."""
+        if not self._callback_queued:
+            self._callback_queued = True
+            self._finalize_backward()
+
     @contextlib.contextmanager
     def no_sync(self):
         old = self._sync

@@ -38,7 +38,7 @@ from .data.prefetch import unwrap
 from .optim import build_lr_scheduler, build_optimizer
 from .parallel import distributed as dist_utils
 from .parallel.flat_params import FlatParamSpace
-from .parallel.reducer import GradReducer
+from .parallel.reducer import GradReducer, TransportErrorMonitor
 from .utils.meters import AverageMeter, StopwatchMeter, TimeMeter
 from .utils.phase_timer import PhaseTimer
 from .utils.misc import move_to_device
@@ -87,6 +87,7 @@ class Controller(object):
         self._prev_grad_norm = None
         self.fast_stat_sync = args.fast_stat_sync
         self._save_thread = None
+        self._transport_monitor = TransportErrorMonitor(lag=2)
         self._profile_phases = bool(getattr(args, 'profile_phases', False))
         self.phases = PhaseTimer(self._profile_phases, cuda=self.cuda)
         self.init_meters(args)
@@ -222,6 +223,7 @@ class Controller(object):
         """Forward, backward and parameter update for one group of micro-batches."""
         ph = self.phases.begin
         ph('prep')
+        self._transport_monitor.check()   # xGMI timeouts of update n-2, on every rank alike
         self._set_seed()
         model = self.model
         model.train()
@@ -280,23 +282,36 @@ class Controller(object):
         W = self.args.distributed_world_size
         size_for_norm = sample_size
         if self.fast_stat_sync:
-            host = torch.tensor([acc_ss, acc_ns, 0.0, 0.0, acc_nt, float(ooms)], dtype=torch.float64)
+            # [sample_size, nsentences, loss, nll_loss, ntokens, ooms] (+ xGMI error word)
+            err = self.reducer.transport_error_async() if self.reducer.enabled else None
+            fields = [acc_ss, acc_ns, 0.0, 0.0, acc_nt, float(ooms)] + ([0.0] if err is not None else [])
+            host = torch.tensor(fields, dtype=torch.float64)
             vec = host.pin_memory().to(self.device, non_blocking=True) if self.cuda else host
             if acc_loss is not None:
                 vec[2:4] = torch.stack([acc_loss.reshape(()), acc_nll.reshape(())]).to(vec.device)
+            if err is not None:
+                vec[6:7] = err
             if self._sync_stats():
                 dist_utils.all_reduce(vec)
+            if err is not None:
+                self._transport_monitor.record(self._num_updates + 1, vec[6:7])
             vec[2:4].div_(vec[0:1] * LN2)
             logging_output = {'sample_size': vec[0], 'nsentences': vec[1], 'loss': vec[2], 'nll_loss': vec[3],
                               'ntokens': vec[4], 'ooms': vec[5]}
             size_for_norm = vec[0] if self._sync_stats() else acc_ss
         elif self._sync_stats():
+            err = self.reducer.transport_error_async() if self.reducer.enabled else None
             gathered = dist_utils.all_gather_list(
                 [[{k: (v.item() if torch.is_tensor(v) else v) for k, v in lo.items()} for lo in logging_outputs],
                  sample_sizes, ooms,
-                 (self._prev_grad_norm.item() if torch.is_tensor(self._prev_grad_norm) else self._prev_grad_norm)])
+                 (self._prev_grad_norm.item() if torch.is_tensor(self._prev_grad_norm) else self._prev_grad_norm),
+                 int(err.item()) if err is not None else 0])
             prev_norms = [g[3] for g in gathered]
             ooms = sum(g[2] for g in gathered)
+            if any(g[4] for g in gathered):   # every rank sees every rank's word: all raise together
+                raise RuntimeError('xGMI all-reduce: a peer did not arrive within the timeout during update {} '
+                                   '(error words per rank: {})'.format(self._num_updates + 1,
+                                                                      [g[4] for g in gathered]))
             if not getattr(self.args, 'use_bmuf', False):
                 assert (all(n == prev_norms[0] for n in prev_norms)
                         or all(n is None or math.isnan(n) or math.isinf(n) for n in prev_norms)), \
@@ -321,7 +336,8 @@ class Controller(object):
                 opt.multiply_grads(pre)
             grad_norm = opt.clip_grad_norm(self.args.clip_norm)
             self._prev_grad_norm = grad_norm
-            opt.used_mask = step_used
+            # skip only params no rank used (locally unused ones got the reduced gradient)
+            opt.used_mask = self.reducer.global_used(step_used)
             opt.step()
             ph('meters')
             self.set_num_updates(self.get_num_updates() + 1)
@@ -335,9 +351,12 @@ class Controller(object):
             self.meters['bsz'].update(nsentences)
             self.meters['gnorm'].update(grad_norm)
             self.meters['clip'].update(opt.clipped if self.args.clip_norm > 0 else 0.)
-            self.meters['train_loss'].update(logging_output.get('loss', 0), sample_size)
+            # weight: the all-reduced sample size on the fast path (reference: sample_size = vec[0]
+            # after the stats all-reduce, controller.py:300-306); the local one otherwise
+            weight = size_for_norm if self.fast_stat_sync else sample_size
+            self.meters['train_loss'].update(logging_output.get('loss', 0), weight)
             if 'train_acc' in self.meters:
-                self.meters['train_acc'].update(logging_output.get('acc', 0), sample_size)
+                self.meters['train_acc'].update(logging_output.get('acc', 0), weight)
         except OverflowError as e:
             print('| WARNING: overflow detected, ' + str(e))
             self.zero_grad()

@@ -402,7 +402,7 @@ void xar_allreduce(int64_t h, Tensor buf) {
   c10::hip::HIPGuardMasqueradingAsCUDA guard(buf.device());
   xar_check(hx_xar_allreduce(as_ctx(h), buf.data_ptr<float>(), buf.numel(), cur_stream(buf)));
 }
-void xar_allreduce_sim(std::vector<int64_t> hs, std::vector<Tensor> bufs) {
+void xar_allreduce_sim(std::vector<int64_t> hs, std::vector<Tensor> bufs, int64_t mute) {
   TORCH_CHECK(hs.size() == bufs.size() && hs.size() >= 2 && hs.size() <= 8, "1 context per simulated rank (2..8)");
   std::vector<void*> cs;
   std::vector<float*> ps;
@@ -413,9 +413,17 @@ void xar_allreduce_sim(std::vector<int64_t> hs, std::vector<Tensor> bufs) {
     ps.push_back(bufs[i].data_ptr<float>());
   }
   c10::hip::HIPGuardMasqueradingAsCUDA guard(bufs[0].device());
-  xar_check(hx_xar_allreduce_sim(cs.data(), ps.data(), (int)hs.size(), bufs[0].numel(), cur_stream(bufs[0])));
+  TORCH_CHECK(mute >= -1 && mute < (int64_t)hs.size(), "mute must be -1 or a simulated rank");
+  xar_check(hx_xar_allreduce_sim(cs.data(), ps.data(), (int)hs.size(), bufs[0].numel(), (int)mute,
+                                 cur_stream(bufs[0])));
 }
 int64_t xar_error(int64_t h) { return hx_xar_error(as_ctx(h)); }
+void xar_error_async(int64_t h, Tensor out) {
+  TORCH_CHECK(out.is_cuda() && out.scalar_type() == at::kInt && out.numel() >= 1 && out.is_contiguous(),
+              "error word target: contiguous int32 GPU tensor");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(out.device());
+  xar_check(hx_xar_error_async(as_ctx(h), out.data_ptr<int32_t>(), cur_stream(out)));
+}
 int64_t xar_capacity(int64_t h) { return hx_xar_capacity(as_ctx(h)); }
 void xar_destroy(int64_t h) { hx_xar_destroy(as_ctx(h)); }
 
@@ -445,6 +453,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xar_allreduce", &xar_allreduce);
   m.def("xar_allreduce_sim", &xar_allreduce_sim);
   m.def("xar_error", &xar_error);
+  m.def("xar_error_async", &xar_error_async);
   m.def("xar_capacity", &xar_capacity);
   m.def("xar_destroy", &xar_destroy);
   m.def("set_debug", &set_debug);

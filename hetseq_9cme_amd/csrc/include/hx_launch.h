@@ -72,6 +72,9 @@ int64_t hx_xar_capacity(void* ctx);
 int hx_xar_export(void* ctx, char* out128);
 int hx_xar_open(void* ctx, const char* handles);
 int hx_xar_allreduce(void* ctx, float* buf, int64_t n, hipStream_t s);
-int hx_xar_allreduce_sim(void** ctxs, float** bufs, int W, int64_t n, hipStream_t s);
+// mute >= 0: that simulated rank never raises its flags (test hook: the others time out)
+int hx_xar_allreduce_sim(void** ctxs, float** bufs, int W, int64_t n, int mute, hipStream_t s);
 int hx_xar_error(void* ctx);
+// stream-ordered copy of the error word into a device int32 (no host sync)
+int hx_xar_error_async(void* ctx, int32_t* dst, hipStream_t s);
 void hx_xar_destroy(void* ctx);

@@ -57,10 +57,11 @@ __device__ __forceinline__ uint32_t* flag_at(uint32_t* page, int ph, int b, int 
 }
 
 // all stores of this workgroup drained, then flags raised at every peer
-__device__ __forceinline__ void signal_peers(const Peers& P, int W, int r, int ph, int b, int G, uint32_t epoch) {
+__device__ __forceinline__ void signal_peers(const Peers& P, int W, int r, int ph, int b, int G, uint32_t epoch,
+                                             int mute) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && r != mute) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // system scope: write back L2 for remote readers
     for (int q = 0; q < W; ++q)
       if (q != r) __hip_atomic_store(flag_at(P.flg[q], ph, b, G, r), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -100,7 +101,7 @@ __device__ __forceinline__ void copy_pos(float* dst, const float* src, int64_t e
 
 template <int W>
 __global__ __launch_bounds__(NT) void xar_k(Peers P, int64_t n, int64_t c, int rank0, uint32_t epoch,
-                                            uint64_t timeout_ticks) {
+                                            uint64_t timeout_ticks, int mute) {
   const int G = gridDim.x, b = blockIdx.x;
   const int r = rank0 + (int)blockIdx.y;
   float* buf = P.buf[r];
@@ -119,7 +120,7 @@ __global__ __launch_bounds__(NT) void xar_k(Peers P, int64_t n, int64_t c, int r
       if (e < end) copy_pos(mine, buf, e, end);
     }
   }
-  signal_peers(P, W, r, 0, b, G, epoch);
+  signal_peers(P, W, r, 0, b, G, epoch, mute);
   wait_peers(P, W, r, 0, b, G, epoch, timeout_ticks);
 
   // ---- phase 1: reduce chunk r (rank order, identical on every rank), keep it staged
@@ -150,7 +151,7 @@ __global__ __launch_bounds__(NT) void xar_k(Peers P, int64_t n, int64_t c, int r
       }
     }
   }
-  signal_peers(P, W, r, 1, b, G, epoch);
+  signal_peers(P, W, r, 1, b, G, epoch, mute);
   wait_peers(P, W, r, 1, b, G, epoch, timeout_ticks);
 
   // ---- phase 2: gather the other reduced chunks
@@ -165,7 +166,7 @@ __global__ __launch_bounds__(NT) void xar_k(Peers P, int64_t n, int64_t c, int r
     }
   }
   // nobody may overwrite a staging buffer (next call's phase 0/1) while a peer still reads it
-  signal_peers(P, W, r, 2, b, G, epoch);
+  signal_peers(P, W, r, 2, b, G, epoch, mute);
   wait_peers(P, W, r, 2, b, G, epoch, timeout_ticks);
 }
 
@@ -193,22 +194,23 @@ struct Ctx {
 thread_local char g_err[256];
 
 template <int W>
-void launch_w(const Ctx& c, const Peers& P, int64_t n, int rank0, int ny, hipStream_t s, uint32_t epoch) {
+void launch_w(const Ctx& c, const Peers& P, int64_t n, int rank0, int ny, hipStream_t s, uint32_t epoch, int mute) {
   int64_t chunk = (n + W - 1) / W;
   chunk = (chunk + 63) & ~int64_t(63);          // 256-B aligned chunk starts
   const uint64_t ticks = (uint64_t)(c.timeout_s * 1e8);
-  xar_k<W><<<dim3(c.G, ny), NT, 0, s>>>(P, n, chunk, rank0, epoch, ticks);
+  xar_k<W><<<dim3(c.G, ny), NT, 0, s>>>(P, n, chunk, rank0, epoch, ticks, mute);
 }
 
-void launch(const Ctx& c, const Peers& P, int64_t n, int rank0, int ny, hipStream_t s, uint32_t epoch) {
+void launch(const Ctx& c, const Peers& P, int64_t n, int rank0, int ny, hipStream_t s, uint32_t epoch,
+            int mute = -1) {
   switch (c.world) {
-    case 2: launch_w<2>(c, P, n, rank0, ny, s, epoch); break;
-    case 3: launch_w<3>(c, P, n, rank0, ny, s, epoch); break;
-    case 4: launch_w<4>(c, P, n, rank0, ny, s, epoch); break;
-    case 5: launch_w<5>(c, P, n, rank0, ny, s, epoch); break;
-    case 6: launch_w<6>(c, P, n, rank0, ny, s, epoch); break;
-    case 7: launch_w<7>(c, P, n, rank0, ny, s, epoch); break;
-    default: launch_w<8>(c, P, n, rank0, ny, s, epoch); break;
+    case 2: launch_w<2>(c, P, n, rank0, ny, s, epoch, mute); break;
+    case 3: launch_w<3>(c, P, n, rank0, ny, s, epoch, mute); break;
+    case 4: launch_w<4>(c, P, n, rank0, ny, s, epoch, mute); break;
+    case 5: launch_w<5>(c, P, n, rank0, ny, s, epoch, mute); break;
+    case 6: launch_w<6>(c, P, n, rank0, ny, s, epoch, mute); break;
+    case 7: launch_w<7>(c, P, n, rank0, ny, s, epoch, mute); break;
+    default: launch_w<8>(c, P, n, rank0, ny, s, epoch, mute); break;
   }
 }
 
@@ -290,7 +292,7 @@ int hx_xar_allreduce(void* ctx, float* buf, int64_t n, hipStream_t s) {
 
 // test-only: W simulated ranks in ONE grid on one device; ctxs[q] are W contexts created
 // on this device, bufs[q] the rank-q buckets (all n floats)
-int hx_xar_allreduce_sim(void** ctxs, float** bufs, int W, int64_t n, hipStream_t s) {
+int hx_xar_allreduce_sim(void** ctxs, float** bufs, int W, int64_t n, int mute, hipStream_t s) {
   Ctx* c0 = static_cast<Ctx*>(ctxs[0]);
   if (n > c0->cap) {
     snprintf(g_err, sizeof(g_err), "simulation bucket larger than the staging capacity");
@@ -306,7 +308,7 @@ int hx_xar_allreduce_sim(void** ctxs, float** bufs, int W, int64_t n, hipStream_
   }
   const uint32_t epoch = ++c0->epoch;
   for (int q = 1; q < W; ++q) static_cast<Ctx*>(ctxs[q])->epoch = epoch;
-  launch(*c0, P, n, 0, W, s, epoch);
+  launch(*c0, P, n, 0, W, s, epoch, mute);
   HX_HIP(hipGetLastError());
   return 0;
 }
@@ -317,6 +319,12 @@ int hx_xar_error(void* ctx) {
   uint32_t e = 0;
   HX_HIP(hipMemcpy(&e, c->flg + (size_t)NPHASE * c->G * MAXW, sizeof(e), hipMemcpyDeviceToHost));
   return (int)e;
+}
+
+int hx_xar_error_async(void* ctx, int32_t* dst, hipStream_t s) {
+  Ctx* c = static_cast<Ctx*>(ctx);
+  HX_HIP(hipMemcpyAsync(dst, c->flg + (size_t)NPHASE * c->G * MAXW, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+  return 0;
 }
 
 void hx_xar_destroy(void* ctx) {

@@ -116,12 +116,17 @@ class _Optimizer(object):
         return self._clipped
 
     # --- state dict (torch-optimizer format, reference-compatible) ------
+    # Torch optimizers number their state by position in ``model.parameters()``
+    # (requires_grad only, tied weights once) -- the reference builds its Adam over
+    # exactly that list (hetseq/controller.py:92-96).  The flat layout orders
+    # parameters differently (reverse blocks, fused groups), so state is emitted and
+    # consumed through ``flat.model_order`` (position -> flat index).
     def state_dict(self):
         state = {}
-        for i, p in enumerate(self.flat.params):
+        for pos, i in enumerate(self.flat.model_order):
             s = self._param_state(i)
             if s is not None:
-                state[i] = s
+                state[pos] = s
         groups = []
         for g in self.param_groups:
             gg = {k: v for k, v in g.items()}
@@ -138,11 +143,18 @@ class _Optimizer(object):
         if optimizer_overrides:
             self.param_groups[0].update(optimizer_overrides)
         self._apply_group_config()
-        n_saved = len(saved['params'])
-        if n_saved != len(self.flat.params):
+        saved_ids = list(saved['params'])
+        if len(saved_ids) != len(self.flat.params):
             raise ValueError('loaded state dict has a different number of parameters')
         for idx, s in state_dict['state'].items():
-            self._load_param_state(saved['params'].index(idx) if idx in saved['params'] else int(idx), s)
+            pos = saved_ids.index(idx) if idx in saved_ids else int(idx)
+            i = self.flat.model_order[pos]
+            shape = self.flat.params[i].shape
+            for k, v in s.items():
+                if torch.is_tensor(v) and v.dim() > 0 and v.numel() != shape.numel():
+                    raise ValueError('optimizer state {!r} of parameter {} ({}) has shape {}, expected {}'.format(
+                        k, pos, self.flat.names[i], tuple(v.shape), tuple(shape)))
+            self._load_param_state(i, s)
         self._lr = self.param_groups[0]['lr']
 
     def _apply_group_config(self):

@@ -84,6 +84,9 @@ class FlatParamSpace(object):
                     placed.add(n)
         self.names = order
         self.params = [name_to_param[n] for n in order]
+        # flat index of each trainable parameter in ``model.parameters()`` order: the
+        # order torch optimizers (and so reference checkpoints) index their state by
+        self.model_order = [order.index(n) for n, _ in uniq]
         if device is None:
             device = self.params[0].device
         self.device = torch.device(device)

@@ -24,9 +24,16 @@ Bucket sizing for MI355X: RCCL's intra-node all-reduce drives the 7 xGMI
 links of a fully connected 8-GPU node concurrently; a bucket only needs to be
 large enough that each of the W ring/tree chunks amortises the per-step
 latency (≈ a few MB per peer).  ``--bucket-cap-mb`` keeps the reference's
-default of 25 MB; bucket boundaries are padded to multiples of W x 256 B of
-elements so that every per-peer chunk is 256 B aligned for uneven worlds
-(W = 3, 5, ...).
+default of 25 MB.  Bucket boundaries fall on parameter starts, which the flat
+layout places on 64-element (256 B) boundaries; the xGMI kernel rounds its
+per-peer chunks up to 64 elements itself, so every chunk is 256 B aligned for
+uneven worlds (W = 3, 5, ...) without padding the buckets.
+
+Unused parameters (``--find-unused-parameters``): DDP gives a parameter that
+this rank did not use, but another rank did, the reduced gradient on every
+rank.  ``global_used`` therefore ORs the per-step used flags across ranks, and
+the optimizer skips only parameters that NO rank used (the reference's
+``grad is None`` skip), so replicas and per-parameter step counters agree.
 
 ``use_xgmi()`` swaps the per-bucket transport for the hand-written intra-node
 two-shot xGMI kernel (``parallel/xgmi.py``): buckets are then reduced on a
@@ -56,7 +63,6 @@ class GradReducer(object):
         # ---- bucket plan over the flat layout (params already reverse-ordered)
         elem = flat.grad_flat.element_size()
         cap = max(1, int(bucket_cap_mb * 1024 * 1024 / elem))
-        align = max(1, self.world_size * 256 // elem)
         buckets = []   # list of (start, end, [param idx])
         cur, cur_start = [], 0
         for i in range(len(flat.params)):
@@ -77,7 +83,6 @@ class GradReducer(object):
         for b, (_, _, idxs) in enumerate(buckets):
             for i in idxs:
                 self.bucket_of[i] = b
-        self._align = align
         self.xgmi = None
         self._pending = [0] * len(buckets)
         self.used = [False] * len(flat.params)
@@ -136,6 +141,30 @@ class GradReducer(object):
         """Raise if the xGMI transport reported a timed-out wait (synchronising)."""
         if self.xgmi is not None:
             self.xgmi.check()
+
+    def transport_error_async(self):
+        """The xGMI error word as a 1-element float64 device tensor, copied on the
+        current stream after every bucket of this step (no host sync), or None
+        when buckets go over RCCL."""
+        if self.xgmi is None:
+            return None
+        return self.xgmi.error_async().double()
+
+    def global_used(self, step_used):
+        """Per-parameter 'received a gradient this step' flags, OR-ed over ranks.
+
+        Without ``--find-unused-parameters`` every parameter takes part in every
+        reduction (DDP's contract), so all are treated as used and no collective
+        is needed.  With it, one small MAX all-reduce of the flags runs (the
+        fine-tuning configurations, where a host read per step is cheap)."""
+        if not self.enabled:
+            return list(step_used)
+        if not self.find_unused:
+            return [True] * len(step_used)
+        dev = self.flat.grad_flat.device
+        t = torch.tensor([1 if u else 0 for u in step_used], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return [bool(v) for v in t.tolist()]
 
     def _launch_ready(self, force=False):
         while self._launched < len(self.buckets) and (force or self._pending[self._launched] == 0):
@@ -221,3 +250,42 @@ class GradReducer(object):
         for h in self._hooks:
             h.remove()
         self._hooks = []
+
+
+class TransportErrorMonitor(object):
+    """Deferred, collective check of the xGMI transport's error word.
+
+    The controller puts the error word into the per-step stats vector, so after
+    the stats all-reduce every rank holds the SAME sum.  ``record`` copies that
+    element to pinned host memory on the stream (no host sync); ``check`` reads
+    the value recorded ``lag`` updates earlier -- long finished, because the host
+    runs at most about one step ahead -- and raises on every rank at the same
+    update when any rank's wait timed out.  Replaces a check that ran only when
+    ``--check-params-every`` was set or on rank 0's checkpoint save.
+    """
+
+    def __init__(self, lag=2):
+        self.lag = lag
+        self._pending = []
+
+    def record(self, update, err_reduced):
+        e = err_reduced.detach().reshape(1)
+        if e.is_cuda:
+            host = torch.empty(1, dtype=e.dtype, pin_memory=True)
+            host.copy_(e, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host, ev = e.clone(), None
+        self._pending.append((update, host, ev))
+
+    def check(self, force=False):
+        while self._pending and (force or len(self._pending) > self.lag):
+            update, host, ev = self._pending.pop(0)
+            if ev is not None:
+                ev.synchronize()
+            if float(host[0]) != 0.0:
+                self._pending = []
+                raise RuntimeError('xGMI all-reduce: a peer did not arrive within the timeout during update {} '
+                                   '(error bits summed over ranks: {:#x}); its gradients are invalid'
+                                   .format(update, int(host[0])))

@@ -15,8 +15,11 @@ GPU); otherwise the reducer stays on RCCL (multi-node, CPU/gloo).  RCCL also
 keeps the one-off parameter broadcast and the small stats all-reduce.
 
 Waits inside the kernel are bounded by ``timeout_s``; a wait that expires sets
-an error bit instead of hanging the GPU, and :meth:`check` (a synchronising
-read, called at the controller's slow-path points) raises on it.
+an error bit instead of hanging the GPU.  :meth:`error_async` copies that word
+on the stream (no host sync); the controller folds it into the per-step stats
+all-reduce and checks the reduced value two updates later, so every rank
+raises at the same update (``TransportErrorMonitor`` in ``reducer.py``).
+:meth:`check` is the synchronising local read.
 """
 import socket
 
@@ -76,6 +79,13 @@ class XgmiAllReduce(object):
         C().xar_allreduce(self.h, t)
         return t
 
+    def error_async(self):
+        """1-element int32 device tensor receiving the error word, written on the
+        current stream (ordered after every all-reduce enqueued before it)."""
+        out = torch.empty(1, dtype=torch.int32, device=torch.cuda.current_device())
+        C().xar_error_async(self.h, out)
+        return out
+
     def check(self):
         err = C().xar_error(self.h)
         if err:
@@ -94,14 +104,15 @@ class XgmiAllReduce(object):
             pass
 
 
-def simulate_all_reduce(bufs, blocks=64, timeout_s=20.0):
+def simulate_all_reduce(bufs, blocks=64, timeout_s=20.0, mute=-1):
     """Test helper: W simulated ranks in ONE grid on one GPU (no IPC); reduces the
-    equal-size fp32 tensors ``bufs`` in place and returns the error word."""
+    equal-size fp32 tensors ``bufs`` in place and returns the error word.
+    ``mute`` = a simulated rank that never signals (the others' waits time out)."""
     W = len(bufs)
     cap = max(64, bufs[0].numel())
     hs = [C().xar_create(q, W, cap, blocks, float(timeout_s)) for q in range(W)]
     try:
-        C().xar_allreduce_sim(hs, list(bufs))
+        C().xar_allreduce_sim(hs, list(bufs), int(mute))
         torch.cuda.synchronize()
         return max(C().xar_error(h) for h in hs)
     finally:

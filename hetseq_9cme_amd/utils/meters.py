@@ -29,10 +29,13 @@ class AverageMeter(object):
     def reset(self):
         self._val = 0
         self._sum = 0
-        self.count = 0
+        self._count = 0
 
     def update(self, val, n=1):
+        """``val`` and the weight ``n`` may be device tensors (summed lazily)."""
         self._val = val
+        if torch.is_tensor(n):
+            n = n.detach().reshape(())
         if torch.is_tensor(val):
             val = val.detach()
             if torch.is_tensor(self._sum):
@@ -40,8 +43,17 @@ class AverageMeter(object):
             else:
                 self._sum = val * n + self._sum
         else:
-            self._sum = self._sum + val * n
-        self.count += n
+            self._sum = (n * val + self._sum) if torch.is_tensor(n) else (self._sum + val * n)
+        self._count = (n + self._count) if torch.is_tensor(n) else (self._count + n)
+
+    @property
+    def count(self):
+        self._count = _host(self._count)
+        return self._count
+
+    @count.setter
+    def count(self, v):
+        self._count = v
 
     @property
     def val(self):
@@ -64,6 +76,8 @@ class AverageMeter(object):
         return {'_val': _host(self._val), '_sum': _host(self._sum), 'count': self.count}
 
     def __setstate__(self, state):
+        state = dict(state)
+        self._count = state.pop('count', 0)
         self.__dict__.update(state)
 
 

@@ -67,3 +67,121 @@ def test_rank_without_backward_joins_buckets():
     # sum or mean convention: either way proportional to rank 0's gradient
     scale = float(g0.abs().sum() / ref.abs().sum())
     assert scale == pytest.approx(1.0, rel=1e-5) or scale == pytest.approx(0.5, rel=1e-5)
+
+
+# --------------------------------------------------------------------------------------------
+# Unused parameters through the optimizer: DDP gives a parameter that one rank did not use
+# but another did the reduced gradient on every rank, so every replica must apply the same
+# update and advance the same Adam step counters (the mask was local).
+
+class _TwoHeads(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.trunk = torch.nn.Linear(8, 16)
+        self.head_a = torch.nn.Linear(16, 4)
+        self.head_b = torch.nn.Linear(16, 4)
+        self.never = torch.nn.Linear(4, 4)     # used by no rank: must be skipped everywhere
+
+    def forward(self, x, use_b):
+        h = torch.tanh(self.trunk(x))
+        out = self.head_a(h).pow(2).sum()
+        if use_b:
+            out = out + self.head_b(h).pow(2).sum()
+        return out
+
+
+def _adam_args():
+    import argparse
+    return argparse.Namespace(lr=[1e-2], adam_betas='(0.9, 0.999)', adam_eps=1e-8, weight_decay=0.01,
+                              fused_kernels=False)
+
+
+def _unused_worker(rank, port, out, mode):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=2)
+    try:
+        from hetseq_9cme_amd.optim.optimizers import _Adam
+        from hetseq_9cme_amd.parallel.flat_params import FlatParamSpace
+        from hetseq_9cme_amd.parallel.reducer import GradReducer
+        model = _TwoHeads()
+        flat = FlatParamSpace(model)
+        red = GradReducer(flat, bucket_cap_mb=0.0005, find_unused_parameters=True)
+        opt = _Adam(_adam_args(), flat)
+        for step in range(3):
+            opt.zero_grad()
+            red.prepare_for_backward()
+            x = torch.randn(5, 8, generator=torch.Generator().manual_seed(100 * step + rank))
+            if mode == 'no_backward' and rank == 1:
+                pass                                   # this rank runs no backward at all
+            else:
+                model(x, use_b=(rank == 0)).backward()  # head_b: used by rank 0 only
+            red.after_backward()
+            opt.used_mask = red.global_used(red.used)
+            opt.multiply_grads(red.grad_prescale)
+            opt.step()
+        out[rank] = (flat.param_flat.clone(), list(opt.steps), list(flat.names))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('mode', ['partial_use', 'no_backward'])
+def test_unused_params_replicas_identical_after_step(mode):
+    ctx = mp.get_context('spawn')
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    port = _free_port()
+    procs = [ctx.Process(target=_unused_worker, args=(r, port, out, mode)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0, 'worker failed or hung'
+    (p0, s0, names), (p1, s1, _) = out[0], out[1]
+    assert torch.equal(p0, p1), 'parameter replicas diverged'
+    assert s0 == s1, 'Adam step counters diverged'
+    steps = dict(zip(names, s0))
+    assert steps['head_b.weight'] == 3 and steps['trunk.weight'] == 3
+    assert steps['never.weight'] == 0, 'a parameter no rank used must be skipped (grad is None)'
+
+
+# --------------------------------------------------------------------------------------------
+# Deferred collective check of the xGMI error word: the word rides in the
+# all-reduced stats vector, so every rank raises at the same update.
+
+def _monitor_worker(rank, port, out):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=2)
+    try:
+        from hetseq_9cme_amd.parallel.reducer import TransportErrorMonitor
+        mon = TransportErrorMonitor(lag=2)
+        raised_at = None
+        for update in range(1, 8):
+            try:
+                mon.check()
+            except RuntimeError:
+                raised_at = update
+                break
+            vec = torch.zeros(7, dtype=torch.float64)
+            vec[6] = 1.0 if (rank == 1 and update == 3) else 0.0   # rank 1 timed out in update 3
+            dist.all_reduce(vec)
+            mon.record(update, vec[6:7])
+        out[rank] = raised_at
+    finally:
+        dist.destroy_process_group()
+
+
+def test_transport_error_raises_on_every_rank_at_the_same_update():
+    ctx = mp.get_context('spawn')
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    port = _free_port()
+    procs = [ctx.Process(target=_monitor_worker, args=(r, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0, 'worker failed or hung'
+    assert out[0] == out[1] == 6    # update 3's word, checked two updates later (start of update 6)

@@ -37,6 +37,34 @@ def test_xgmi_allreduce_simulated(dev, W, n):
             assert torch.equal(bufs[q], ref), (it, q, (bufs[q] - ref).abs().max().item())
 
 
+def test_xgmi_timeout_sets_error_and_the_step_check_raises(dev):
+    """A simulated rank that never signals: the others' bounded waits expire, the kernel
+    drains, the error word is set, and the stream-ordered copy of it (what the controller
+    folds into the stats all-reduce) makes TransportErrorMonitor raise two updates later."""
+    from hetseq_9cme_amd.ops._ext import C
+    from hetseq_9cme_amd.parallel.reducer import TransportErrorMonitor
+    W, n = 3, 4096
+    hs = [C().xar_create(q, W, n, 4, 0.05) for q in range(W)]
+    try:
+        bufs = [torch.ones(n, device=dev) for _ in range(W)]
+        C().xar_allreduce_sim(hs, bufs, 1)           # rank 1 muted
+        torch.cuda.synchronize()
+        words = [C().xar_error(h) for h in hs]
+        assert words[0] != 0 and words[2] != 0, words
+        out = torch.zeros(1, dtype=torch.int32, device=dev)
+        C().xar_error_async(hs[0], out)
+        mon = TransportErrorMonitor(lag=2)
+        mon.record(1, out.double())
+        mon.record(2, torch.zeros(1, dtype=torch.float64, device=dev))
+        mon.check()                                    # update 1 not yet due
+        mon.record(3, torch.zeros(1, dtype=torch.float64, device=dev))
+        with pytest.raises(RuntimeError, match='update 1'):
+            mon.check()
+    finally:
+        for h in hs:
+            C().xar_destroy(h)
+
+
 WORKER = textwrap.dedent('''
     import os, sys, time, torch, torch.distributed as dist
     sys.path.insert(0, os.environ['ROOT'])

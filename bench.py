@@ -40,6 +40,8 @@ def parse():
     ap.add_argument('--seq', type=int, default=128)
     ap.add_argument('--max-pred', type=int, default=20)
     ap.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'])
+    ap.add_argument('--fp32-gemm', default='native', choices=['native', 'bf16x3', 'bf16x6'],
+                    help='fp32 linear GEMMs: native f32 MFMA or bf16-plane emulation (ops/split_gemm.py)')
     ap.add_argument('--model', default='base', choices=['base', 'large', 'tiny'])
     ap.add_argument('--no-fused', action='store_true', help='torch-op baseline (A/B only)')
     ap.add_argument('--data-dir', default=None)
@@ -98,7 +100,8 @@ def main():
     argv = ['--task', 'bert', '--data', data_dir, '--config_file', cfg_path, '--max-sentences', str(a.batch),
             '--fast-stat-sync', '--lr', '1e-4', '--warmup-updates', '10000', '--weight-decay', '0.01',
             '--total-num-update', '1000000', '--clip-norm', '25', '--num-workers', str(a.num_workers), '--log-format', 'none',
-            '--disable-validation', '--no-save', '--precision', a.precision, '--distributed-world-size', str(world),
+            '--disable-validation', '--no-save', '--precision', a.precision, '--fp32-gemm', a.fp32_gemm,
+            '--distributed-world-size', str(world),
             '--update-freq', str(a.update_freq), '--gemm-tuning', a.gemm_tuning,
             '--allreduce-impl', a.allreduce_impl, '--bucket-cap-mb', str(a.bucket_cap_mb)]
     if a.profile_phases:
@@ -173,6 +176,7 @@ def main():
                        'seq_len': a.seq, 'max_pred': a.max_pred,
                        'parallelism': 'dp{}'.format(world), 'optimizer': 'adam(fused)',
                        'fused_kernels': not a.no_fused, 'gemm_tuning': a.gemm_tuning,
+                       'fp32_gemm': a.fp32_gemm if a.precision == 'fp32' else None,
                        'allreduce': a.allreduce_impl if world > 1 else None},
             'final_logged_loss': round(loss, 5),
         }

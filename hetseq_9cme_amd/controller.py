@@ -54,6 +54,7 @@ class Controller(object):
         self.device = torch.device('cuda', torch.cuda.current_device()) if self.cuda else torch.device('cpu')
         if not getattr(args, 'fused_kernels', True):
             ops.set_fused(False)      # A/B mode: plain torch ops on the GPU
+        ops.set_fp32_gemm(getattr(args, 'fp32_gemm', 'native'))
         if getattr(args, 'overlap_wgrad', False):
             ops.set_side_stream(True)
         if getattr(args, 'debug_kernels', False) and self.cuda:

@@ -378,6 +378,28 @@ Tensor wgrad_bf16(Tensor dy, Tensor x, Tensor out) {
   return out;
 }
 
+// ------------------------------------------------------------------ split planes
+Tensor split_planes(Tensor x, std::vector<int64_t> order, int64_t npieces, bool stacked) {
+  check_f32(x, "split input");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.size(1) % 8 == 0 && x.stride(0) % 4 == 0 &&
+                  aligned16(x.data_ptr()),
+              "split_planes: x must be [R, D] fp32 with unit column stride, D % 8 == 0, 16-byte rows");
+  TORCH_CHECK(npieces == 2 || npieces == 3, "split_planes: 2 or 3 pieces");
+  TORCH_CHECK(!order.empty() && order.size() <= 8, "split_planes: 1..8 planes");
+  uint32_t packed = 0;
+  for (size_t j = 0; j < order.size(); ++j) {
+    TORCH_CHECK(order[j] >= 0 && order[j] < npieces, "split_planes: piece index out of range");
+    packed |= (uint32_t)order[j] << (4 * j);
+  }
+  const int64_t R = x.size(0), D = x.size(1), npl = (int64_t)order.size();
+  Tensor out = stacked ? torch::empty({npl * R, D}, x.options().dtype(torch::kBFloat16))
+                       : torch::empty({R, npl * D}, x.options().dtype(torch::kBFloat16));
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  hx_split_planes(x.data_ptr<float>(), x.stride(0), reinterpret_cast<uint16_t*>(out.data_ptr()), R, (int)D,
+                  (int)npieces, (int)npl, packed, stacked ? 1 : 0, cur_stream(x));
+  return out;
+}
+
 // ------------------------------------------------------------------ xGMI all-reduce
 // Contexts travel to Python as integers (owned by parallel/xgmi.py).
 inline void xar_check(int rc) { TORCH_CHECK(rc == 0, hx_xar_last_error()); }
@@ -447,6 +469,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd", &attn_bwd);
   m.def("wgrad_bf16", &wgrad_bf16);
   m.def("wgrad_bf16_ok", &wgrad_bf16_ok);
+  m.def("split_planes", &split_planes);
   m.def("xar_create", &xar_create);
   m.def("xar_export", &xar_export);
   m.def("xar_open", &xar_open);

@@ -64,6 +64,11 @@ void hx_attn_bwd(int bf16, const void* qkv, const float* bias, float* dbq, float
                  const float* maskb, const void* dout, const void* out, const float* lse, const uint32_t* dmask,
                  void* dqkv, float* dq_acc, int dq_ld, int B, int S, int nh, float keep, hipStream_t s);
 
+// split.hip -- fp32 -> bf16 planes (piece order[j] = (order >> 4j) & 15) for bf16-MFMA
+// emulation of fp32 GEMMs; interleaved [R][npl][D] or stacked [npl][R][D].
+void hx_split_planes(const float* x, int64_t ldx, uint16_t* out, int64_t R, int D, int npieces, int npl,
+                     uint32_t order, int stacked, hipStream_t s);
+
 // xgmi_allreduce.hip -- intra-node two-shot all-reduce over IPC-mapped peer buffers.
 // Every function returns 0 on success, -1 with a message in hx_xar_last_error().
 const char* hx_xar_last_error();

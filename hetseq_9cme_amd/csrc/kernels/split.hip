@@ -1,0 +1,78 @@
+// fp32 -> bf16 "planes" for fp32 GEMMs emulated on the bf16 matrix cores.
+//
+// gfx950 runs bf16 MFMA at 16x the rate of its f32-input MFMA (2.5 PF vs 157 TF dense).
+// An fp32 value x is written as a sum of bf16 pieces: x0 = bf16(x), x1 = bf16(x - x0),
+// x2 = bf16(x - x0 - x1) (round-to-nearest-even each time), so x = x0 + x1 + O(2^-18 |x|)
+// with two pieces and x0 + x1 + x2 + O(2^-27 |x|) with three.  A product a.b becomes a sum
+// of piece products, each EXACT in the MFMA's fp32 accumulator (8 x 8 significand bits):
+//   3 passes: a0 b0 + a1 b0 + a0 b1                       (dropped terms ~2^-17 |ab|)
+//   6 passes: + a2 b0 + a1 b1 + a0 b2                     (dropped terms ~2^-26 |ab|)
+// Stacking the pass operands along the reduction dimension turns the sum into ONE ordinary
+// bf16 GEMM with K' = passes * K (ops/split_gemm.py explains the plane orders that make the
+// forward, data-gradient and weight-gradient GEMMs pair the right pieces).
+//
+// This kernel writes the planes: row r of x [R][D] becomes `npl` consecutive bf16 rows
+// (interleaved: out[(r * npl + j) * D + c]) or plane j becomes a block of R rows (stacked:
+// out[(j * R + r) * D + c]); plane j holds piece order[j].  One pass over x, 8 elements per
+// lane (two 16-B loads, one 16-B store per plane), HBM-bound.
+#include <algorithm>
+
+#include "hx_launch.h"
+#include "hx_common.h"
+
+namespace {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)hx::f2bf(a) | ((uint32_t)hx::f2bf(b) << 16);
+}
+
+template <int NPIECE>
+__global__ __launch_bounds__(256) void split_planes_k(const float* __restrict__ x, int64_t ldx,
+                                                      uint16_t* __restrict__ out, int64_t R, int D, int npl,
+                                                      uint32_t order, int stacked) {
+  const int d8 = D >> 3;
+  const int64_t n8 = R * d8;
+  const int64_t row_stride = stacked ? (int64_t)D : (int64_t)npl * D;
+  const int64_t plane_stride = stacked ? R * D : (int64_t)D;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / d8;
+    const int c = (int)(i - r * d8) * 8;
+    const float4 u = *reinterpret_cast<const float4*>(x + r * ldx + c);
+    const float4 v = *reinterpret_cast<const float4*>(x + r * ldx + c + 4);
+    float p[NPIECE][8];
+    float e[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < NPIECE; ++k)
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const float q = hx::bf2f(hx::f2bf(e[t]));
+        p[k][t] = q;
+        e[t] -= q;    // exact: the residual of a round-to-nearest bf16 fits in fp32
+      }
+    u32x4 w[NPIECE];
+#pragma unroll
+    for (int k = 0; k < NPIECE; ++k)
+      w[k] = u32x4{pack2(p[k][0], p[k][1]), pack2(p[k][2], p[k][3]), pack2(p[k][4], p[k][5]),
+                   pack2(p[k][6], p[k][7])};
+    uint16_t* o = out + r * row_stride + c;
+    for (int j = 0; j < npl; ++j) {
+      const int k = (order >> (4 * j)) & 15;
+      *reinterpret_cast<u32x4*>(o + j * plane_stride) = w[k < NPIECE ? k : NPIECE - 1];
+    }
+  }
+}
+
+}  // namespace
+
+void hx_split_planes(const float* x, int64_t ldx, uint16_t* out, int64_t R, int D, int npieces, int npl,
+                     uint32_t order, int stacked, hipStream_t s) {
+  const int64_t n8 = R * (D / 8);
+  if (n8 <= 0) return;
+  const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 8192);
+  if (npieces == 3)
+    split_planes_k<3><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, npl, order, stacked);
+  else
+    split_planes_k<2><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, npl, order, stacked);
+}

@@ -10,6 +10,7 @@ import os
 import torch
 import torch.nn.functional as F
 
+from . import split_gemm
 from ._ext import C, use_kernels
 from .rng import get_rng
 
@@ -98,6 +99,17 @@ def _dgrad(dy2, W, xshape, mbox):
         return g.view(-1, W.shape[1]).addmm_(dy2, Wc).view(xshape)
     dx = torch.mm(dy2, Wc).view(xshape)
     return dx if other is None else dx + other.view(xshape).to(dx.dtype)
+
+
+def _dgrad_split(dys, W, xshape, mbox):
+    """``_dgrad`` on the bf16 split planes of dy (``--fp32-gemm bf16x3/x6``)."""
+    if mbox is not None:
+        g, other = mbox.take(torch.float32)
+        if g is not None:
+            return split_gemm.dgrad(dys, W, acc=g.view(-1, W.shape[1])).view(xshape)
+        dx = split_gemm.dgrad(dys, W).view(xshape)
+        return dx if other is None else dx + other.view(xshape).to(dx.dtype)
+    return split_gemm.dgrad(dys, W).view(xshape)
 
 
 # ----------------------------------------------------------------- weight-grad side stream
@@ -360,8 +372,14 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, b, mbox):
         x2 = x.reshape(-1, x.shape[-1])
-        Wc = cast_w(W, x.dtype)
-        y = torch.mm(x2, Wc.t()) if b is None else torch.addmm(cast_w(b, x.dtype), x2, Wc.t())
+        ctx.split = split_gemm.active(x2)
+        if ctx.split:     # fp32 on bf16 matrix cores; the backward reuses the x planes
+            y, x2 = split_gemm.forward(x2, W)
+            if b is not None:
+                y.add_(b)
+        else:
+            Wc = cast_w(W, x.dtype)
+            y = torch.mm(x2, Wc.t()) if b is None else torch.addmm(cast_w(b, x.dtype), x2, Wc.t())
         ctx.save_for_backward(x2, W)
         ctx.b = b
         ctx.mbox = mbox
@@ -373,12 +391,19 @@ class _LinearFn(torch.autograd.Function):
         x2, W = ctx.saved_tensors
         b = ctx.b
         dy2 = dy.reshape(-1, dy.shape[-1])
-        dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox) if ctx.needs_input_grad[0] else None
+        dys = split_gemm.grad_planes(dy2.float()) if ctx.split else None
+        if not ctx.needs_input_grad[0]:
+            dx = None
+        elif ctx.split:
+            dx = _dgrad_split(dys, W, ctx.xshape, ctx.mbox)
+        else:
+            dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox)
         slot = grad_slot(W)
         direct = slot is not None
         side = side_begin(dy2.device) if direct else None
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            dW = _wgrad(dy2, x2, slot)
+            dW = (split_gemm.wgrad(dys, x2, W.shape[0], W.shape[1], slot) if ctx.split
+                  else _wgrad(dy2, x2, slot))
             db = None
             if b is not None:
                 if dy2.shape[-1] % 4 == 0:
@@ -388,6 +413,8 @@ class _LinearFn(torch.autograd.Function):
         if side is not None:
             dy2.record_stream(side)
             x2.record_stream(side)
+            if dys is not None:
+                dys.record_stream(side)
         return dx, dW, db, None
 
 
@@ -440,8 +467,14 @@ class _Linear3Fn(torch.autograd.Function):
             Wc = Wc if Wc is not None else W.to(x.dtype)
             bc = cast_w(b, x.dtype) if has_b else None
         x2 = x.reshape(-1, x.shape[-1])
-        # without biases (applied inside the fused attention instead) this is a plain GEMM
-        y = torch.addmm(bc, x2, Wc.t()) if has_b else torch.mm(x2, Wc.t())
+        ctx.split = split_gemm.active(x2)
+        if ctx.split:     # fp32 on bf16 matrix cores; the backward reuses the x planes
+            y, x2 = split_gemm.forward(x2, W)
+            if has_b:
+                y.add_(b)
+        else:
+            # without biases (applied inside the fused attention instead) this is a plain GEMM
+            y = torch.addmm(bc, x2, Wc.t()) if has_b else torch.mm(x2, Wc.t())
         ctx.save_for_backward(x2, Wc)
         ctx.params = (wq, wk, wv, bq, bk, bv)
         ctx.has_b = has_b
@@ -455,7 +488,13 @@ class _Linear3Fn(torch.autograd.Function):
         x2, W = ctx.saved_tensors
         wq, wk, wv, bq, bk, bv = ctx.params
         dy2 = dy.reshape(-1, dy.shape[-1])
-        dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox)
+        dys = split_gemm.grad_planes(dy2.float()) if ctx.split else None
+        if ctx.split:
+            dx = _dgrad_split(dys, W, ctx.xshape, ctx.mbox)
+        else:
+            dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox)
+        wg = ((lambda slot: split_gemm.wgrad(dys, x2, W.shape[0], W.shape[1], slot)) if ctx.split
+              else (lambda slot: _wgrad(dy2, x2, slot)))
         a, b_, _ = ctx.n
         # weight grads: ONE GEMM straight into the three adjacent flat slots when possible
         ws = [grad_slot(w) for w in (wq, wk, wv)]
@@ -467,10 +506,10 @@ class _Linear3Fn(torch.autograd.Function):
         side = side_begin(dy2.device) if direct else None
         with torch.cuda.stream(side) if side is not None else _nullctx():
             if fused is not None:
-                _wgrad(dy2, x2, fused)
+                wg(fused)
                 gW = ws
             else:
-                dW = _wgrad(dy2, x2, None)
+                dW = wg(None)
                 gW = [dW[:a], dW[a:a + b_], dW[a + b_:]]
                 for k, t in enumerate(ws):
                     if t is not None:
@@ -485,6 +524,8 @@ class _Linear3Fn(torch.autograd.Function):
         if side is not None:
             dy2.record_stream(side)
             x2.record_stream(side)
+            if dys is not None:
+                dys.record_stream(side)
         if not has_b:
             return (dx, gW[0], gW[1], gW[2], None, None, None, None)
         gb = bs if fb is not None else [db[:a], db[a:a + b_], db[a + b_:]]

@@ -1,0 +1,116 @@
+"""fp32 GEMMs on the bf16 matrix cores: split-plane emulation (``--fp32-gemm``).
+
+gfx950 has no TF32/xf32; its f32-input MFMA runs at the f32 vector rate,
+157 TF/s, 1/16 of the 2.5 PF/s bf16 MFMA rate.  The fp32 training path of
+round 1 spent ~59 of its 68 ms per BERT-base step in library fp32 GEMMs at
+~94 % of that rate -- fp32 MFMA was the ceiling.  This module breaks it while
+keeping fp32-class results:
+
+    x = x0 + x1 (+ x2) + r,  x_i bf16 (round-to-nearest), |r| <= 2^-17 |x| (2^-26 |x|)
+
+and a product a.b is a sum of piece products, each exact in the MFMA's fp32
+accumulator:
+
+  ``bf16x3``: a0 b0 + a1 b0 + a0 b1                        (3 bf16 GEMM passes)
+  ``bf16x6``: + a2 b0 + a1 b1 + a0 b2                      (6 passes, fp32-exact class)
+
+Measured on MI355X against fp64 (``tools/bench_split_gemm.py``, BERT-base
+shapes, max |err| / sum|a.b|): native fp32 MFMA 3.7-4.5e-7, bf16x6 4.4-5.5e-7,
+bf16x3 0.7-1.5e-6 -- all three far from TF32 (~1e-3 relative per product).
+
+Pass structure.  The planes of an operand are stored next to each other along
+the GEMM's REDUCTION dimension, so one ordinary bf16 x bf16 -> fp32 GEMM with
+K' = passes x K sums all the pass products.  Which piece sits in which plane
+is fixed per role so the three GEMMs of a linear layer pair the right pieces:
+
+  role                          layout              piece order
+  layer input x (A of fwd,      [T, n, K]           P  (bf16x3: 0 1 0)
+    B of wgrad)                                        (bf16x6: 0 1 0 2 1 0)
+  output grad dy (A of dgrad,   [T, n, N]           Q  (bf16x3: 0 0 1)
+    A of wgrad)                                        (bf16x6: 0 0 1 0 1 2)
+  weight W, forward operand     [N, n, K]           Q
+  weight W, dgrad operand       [n, N, K] stacked   P
+
+  forward  y  = x' [T, nK] . W_Q'^T          pairs (P_j, Q_j)
+  dgrad    dx = dy' [T, nN] . W_P'' [nN, K]  pairs (Q_j, P_j)
+  wgrad    dW = dy'^T . x'  over nT rows     pairs (Q_j, P_j)   ([T, n, D] viewed as [nT, D])
+
+Every pairs column is {(0,0), (1,0), (0,1)} (bf16x6: plus (2,0), (1,1), (0,2)).
+The weight-gradient GEMM runs on the hand-written split-K bf16 kernel
+(``csrc/kernels/wgrad_bf16.hip``), whose tokens-as-reduction form takes the
+[nT, D] views directly.
+"""
+import torch
+
+from ._ext import C, use_kernels
+
+PIECES = {3: 2, 6: 3}
+ORDER_P = {3: (0, 1, 0), 6: (0, 1, 0, 2, 1, 0)}
+ORDER_Q = {3: (0, 0, 1), 6: (0, 0, 1, 0, 1, 2)}
+MODES = {'native': 0, 'bf16x3': 3, 'bf16x6': 6}
+
+
+class _State(object):
+    passes = 0
+    addmm_out_ok = None   # does torch.addmm(bf16, bf16, out_dtype=fp32, out=acc) work in place?
+
+
+def set_fp32_gemm(mode):
+    """'native' (fp32 MFMA through the libraries), 'bf16x3' or 'bf16x6'."""
+    if mode not in MODES:
+        raise ValueError('--fp32-gemm must be one of {}'.format(sorted(MODES)))
+    _State.passes = MODES[mode]
+
+
+def fp32_gemm_mode():
+    return {v: k for k, v in MODES.items()}[_State.passes]
+
+
+def active(x):
+    """Split emulation applies to fp32 GPU operands when a split mode is set."""
+    return _State.passes > 0 and x.dtype == torch.float32 and use_kernels(x)
+
+
+def passes():
+    return _State.passes
+
+
+def planes(x2, order, stacked=False):
+    """bf16 planes of the fp32 matrix ``x2`` [R, D]: [R, n*D] interleaved, or
+    [n*R, D] stacked."""
+    if x2.stride(-1) != 1 or x2.stride(0) % 4 or x2.data_ptr() % 16:
+        x2 = x2.contiguous()
+    return C().split_planes(x2, list(order), PIECES[len(order)], bool(stacked))
+
+
+def forward(x2, W):
+    """y = x2 @ W^T in fp32; returns (y, x planes for the backward)."""
+    n = _State.passes
+    xs = planes(x2, ORDER_P[n])
+    wq = planes(W, ORDER_Q[n])
+    return torch.mm(xs, wq.t(), out_dtype=torch.float32), xs
+
+
+def grad_planes(dy2):
+    return planes(dy2, ORDER_Q[_State.passes])
+
+
+def dgrad(dys, W, acc=None):
+    """dy @ W (fp32) from the dy planes; accumulated into ``acc`` (beta = 1) if given."""
+    wb = planes(W, ORDER_P[_State.passes], stacked=True)
+    if acc is None:
+        return torch.mm(dys, wb, out_dtype=torch.float32)
+    if _State.addmm_out_ok is not False:
+        try:
+            r = torch.addmm(acc, dys, wb, out_dtype=torch.float32, out=acc)
+            _State.addmm_out_ok = True
+            return r
+        except (RuntimeError, TypeError):
+            _State.addmm_out_ok = False
+    return acc.add_(torch.mm(dys, wb, out_dtype=torch.float32))
+
+
+def wgrad(dys, xs, n_out, n_in, slot):
+    """dW [n_out, n_in] = sum over tokens and passes of dy-piece^T x-piece."""
+    from .fused import _wgrad
+    return _wgrad(dys.view(-1, n_out), xs.view(-1, n_in), slot)

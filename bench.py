@@ -56,6 +56,8 @@ def parse():
                     help='rehearsal on a 1-GPU box: every rank uses GPU 0 (numbers are not per-GPU)')
     ap.add_argument('--gemm-tuning', default='table', choices=['off', 'table', 'online', 'retune'])
     ap.add_argument('--gemm-tuning-file', default=None)
+    ap.add_argument('--overlap-wgrad', action='store_true',
+                    help='weight-gradient GEMMs on a side HIP stream (overlaps the dgrad chain)')
     ap.add_argument('--profile-phases', action='store_true',
                     help='extra untimed steps reporting host time per step phase (stderr)')
     ap.add_argument('--sync-debug', action='store_true',
@@ -106,6 +108,8 @@ def main():
             '--allreduce-impl', a.allreduce_impl, '--bucket-cap-mb', str(a.bucket_cap_mb)]
     if a.profile_phases:
         argv += ['--profile-phases']
+    if a.overlap_wgrad:
+        argv += ['--overlap-wgrad']
     if a.gemm_tuning_file:
         argv += ['--gemm-tuning-file', a.gemm_tuning_file]
     args = options.parse_training_args(argv)

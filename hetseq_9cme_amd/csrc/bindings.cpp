@@ -378,12 +378,56 @@ Tensor wgrad_bf16(Tensor dy, Tensor x, Tensor out) {
   return out;
 }
 
+// ------------------------------------------------------------------ split-piece weight gradient
+// dys: [T, n * M] bf16 planes of dY, xs: [T, n * N] planes of X (ops/split_gemm.py layouts);
+// dy_off / x_off: column offset (elements) of each distinct piece inside a row.
+bool wgrad_split_ok(const Tensor& dys, const Tensor& xs, int64_t M, int64_t N) {
+  if (!dys.is_cuda() || dys.scalar_type() != torch::kBFloat16 || xs.scalar_type() != torch::kBFloat16) return false;
+  if (dys.dim() != 2 || xs.dim() != 2 || dys.size(0) != xs.size(0) || !dys.is_contiguous() || !xs.is_contiguous())
+    return false;
+  if (!aligned16(dys.data_ptr()) || !aligned16(xs.data_ptr())) return false;
+  return M % 128 == 0 && N % 128 == 0 && dys.size(1) % 8 == 0 && xs.size(1) % 8 == 0 && dys.size(0) < (1LL << 31) &&
+         (int64_t)dys.size(0) * dys.size(1) * 2 < (1LL << 32) && (int64_t)xs.size(0) * xs.size(1) * 2 < (1LL << 32);
+}
+Tensor wgrad_split(Tensor dys, std::vector<int64_t> dy_off, Tensor xs, std::vector<int64_t> x_off, int64_t passes,
+                   int64_t M, int64_t N, Tensor out) {
+  TORCH_CHECK(wgrad_split_ok(dys, xs, M, N), "wgrad_split: unsupported operands");
+  TORCH_CHECK(passes == 3 || passes == 6, "wgrad_split: passes must be 3 or 6");
+  const size_t npc = passes == 6 ? 3 : 2;
+  TORCH_CHECK(dy_off.size() == npc && x_off.size() == npc, "wgrad_split: one offset per piece");
+  for (size_t i = 0; i < npc; ++i) {
+    TORCH_CHECK(dy_off[i] >= 0 && dy_off[i] + M <= dys.size(1) && dy_off[i] % 8 == 0, "wgrad_split: bad dY offset");
+    TORCH_CHECK(x_off[i] >= 0 && x_off[i] + N <= xs.size(1) && x_off[i] % 8 == 0, "wgrad_split: bad X offset");
+  }
+  check_f32(out, "wgrad out");
+  TORCH_CHECK(out.size(0) == M && out.size(1) == N, "wgrad out must be [M, N]");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dys.device());
+  const int64_t T = dys.size(0);
+  int cfg = 0, nsplit = 1;
+  hx_wgrad_split_plan((int)M, (int)N, (int)T, (int)passes, &cfg, &nsplit);
+  Tensor ws;
+  if (nsplit > 1) ws = torch::empty({nsplit * M * N}, out.options());
+  const void* dp[3];
+  const void* xp[3];
+  const char* db = reinterpret_cast<const char*>(dys.data_ptr());
+  const char* xb = reinterpret_cast<const char*>(xs.data_ptr());
+  for (size_t i = 0; i < 3; ++i) {
+    dp[i] = db + 2 * dy_off[i < npc ? i : 0];
+    xp[i] = xb + 2 * x_off[i < npc ? i : 0];
+  }
+  TORCH_CHECK(hx_wgrad_split(dp, (int)dys.size(1), xp, (int)xs.size(1), (int)passes, out.data_ptr<float>(),
+                             nsplit > 1 ? ws.data_ptr<float>() : nullptr, (int)M, (int)N, (int)T, cfg, nsplit,
+                             cur_stream(dys)) == 0,
+              "wgrad_split: launch failed");
+  dbg_finite(out, "wgrad_split");
+  return out;
+}
+
 // ------------------------------------------------------------------ split planes
-Tensor split_planes(Tensor x, std::vector<int64_t> order, int64_t npieces, bool stacked) {
-  check_f32(x, "split input");
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.size(1) % 8 == 0 && x.stride(0) % 4 == 0 &&
-                  aligned16(x.data_ptr()),
-              "split_planes: x must be [R, D] fp32 with unit column stride, D % 8 == 0, 16-byte rows");
+Tensor split_planes(Tensor x, std::vector<int64_t> order, int64_t npieces, bool stacked, int64_t rpad,
+                    int64_t dpad) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kFloat32, "split input must be an fp32 GPU tensor");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "split_planes: x must be [R, D] fp32 with unit column stride");
   TORCH_CHECK(npieces == 2 || npieces == 3, "split_planes: 2 or 3 pieces");
   TORCH_CHECK(!order.empty() && order.size() <= 8, "split_planes: 1..8 planes");
   uint32_t packed = 0;
@@ -392,11 +436,14 @@ Tensor split_planes(Tensor x, std::vector<int64_t> order, int64_t npieces, bool 
     packed |= (uint32_t)order[j] << (4 * j);
   }
   const int64_t R = x.size(0), D = x.size(1), npl = (int64_t)order.size();
-  Tensor out = stacked ? torch::empty({npl * R, D}, x.options().dtype(torch::kBFloat16))
-                       : torch::empty({R, npl * D}, x.options().dtype(torch::kBFloat16));
+  const int64_t Rp = std::max<int64_t>(R, rpad), Dp = std::max<int64_t>(D, dpad);
+  TORCH_CHECK(stacked || Rp == R, "split_planes: row padding only for the stacked layout");
+  TORCH_CHECK(Rp * Dp < (1LL << 40) && Dp < (1LL << 31), "split_planes: too large");
+  Tensor out = stacked ? torch::empty({npl * Rp, Dp}, x.options().dtype(torch::kBFloat16))
+                       : torch::empty({R, npl * Dp}, x.options().dtype(torch::kBFloat16));
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  hx_split_planes(x.data_ptr<float>(), x.stride(0), reinterpret_cast<uint16_t*>(out.data_ptr()), R, (int)D,
-                  (int)npieces, (int)npl, packed, stacked ? 1 : 0, cur_stream(x));
+  hx_split_planes(x.data_ptr<float>(), x.stride(0), reinterpret_cast<uint16_t*>(out.data_ptr()), R, (int)D, Rp,
+                  (int)Dp, (int)npieces, (int)npl, packed, stacked ? 1 : 0, cur_stream(x));
   return out;
 }
 
@@ -470,6 +517,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_bf16", &wgrad_bf16);
   m.def("wgrad_bf16_ok", &wgrad_bf16_ok);
   m.def("split_planes", &split_planes);
+  m.def("wgrad_split", &wgrad_split);
+  m.def("wgrad_split_ok", &wgrad_split_ok);
   m.def("xar_create", &xar_create);
   m.def("xar_export", &xar_export);
   m.def("xar_open", &xar_open);

@@ -64,10 +64,18 @@ void hx_attn_bwd(int bf16, const void* qkv, const float* bias, float* dbq, float
                  const float* maskb, const void* dout, const void* out, const float* lse, const uint32_t* dmask,
                  void* dqkv, float* dq_acc, int dq_ld, int B, int S, int nh, float keep, hipStream_t s);
 
+// wgrad_split.hip -- dW[M][N] (fp32) = sum over piece pairs of dY_a^T X_b (bf16 pieces of fp32
+// operands, --fp32-gemm bf16x3 / bf16x6); piece pointers share the row strides ldy / ldx.
+// ws: nsplit * M * N floats.  Returns -1 for an unsupported pass count.
+void hx_wgrad_split_plan(int M, int N, int T, int passes, int* cfg, int* nsplit);
+int hx_wgrad_split(const void* const* dy_pieces, int ldy, const void* const* x_pieces, int ldx, int passes,
+                   float* out, float* ws, int M, int N, int T, int cfg, int nsplit, hipStream_t s);
+
 // split.hip -- fp32 -> bf16 planes (piece order[j] = (order >> 4j) & 15) for bf16-MFMA
 // emulation of fp32 GEMMs; interleaved [R][npl][D] or stacked [npl][R][D].
-void hx_split_planes(const float* x, int64_t ldx, uint16_t* out, int64_t R, int D, int npieces, int npl,
-                     uint32_t order, int stacked, hipStream_t s);
+// Output rows padded to Rp (stacked) / columns to Dp with zeros.
+void hx_split_planes(const float* x, int64_t ldx, uint16_t* out, int64_t R, int D, int64_t Rp, int Dp,
+                     int npieces, int npl, uint32_t order, int stacked, hipStream_t s);
 
 // xgmi_allreduce.hip -- intra-node two-shot all-reduce over IPC-mapped peer buffers.
 // Every function returns 0 on success, -1 with a message in hx_xar_last_error().

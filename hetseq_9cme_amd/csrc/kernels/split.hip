@@ -14,7 +14,8 @@
 // This kernel writes the planes: row r of x [R][D] becomes `npl` consecutive bf16 rows
 // (interleaved: out[(r * npl + j) * D + c]) or plane j becomes a block of R rows (stacked:
 // out[(j * R + r) * D + c]); plane j holds piece order[j].  One pass over x, 8 elements per
-// lane (two 16-B loads, one 16-B store per plane), HBM-bound.
+// lane (two 16-B loads, one 16-B store per plane), HBM-bound; other shapes take the
+// one-element-per-lane form below, which can also zero-pad rows / columns.
 #include <algorithm>
 
 #include "hx_launch.h"
@@ -64,15 +65,54 @@ __global__ __launch_bounds__(256) void split_planes_k(const float* __restrict__ 
   }
 }
 
+// General form: any D / row stride / alignment, rows padded to Rp and columns to Dp with
+// zeros (e.g. the MLM decoder's 30522-wide logits gradient, padded to a multiple of 64 so
+// the bf16 planes have 16-B aligned rows for the GEMM).  One element per lane.
+template <int NPIECE>
+__global__ __launch_bounds__(256) void split_planes_any_k(const float* __restrict__ x, int64_t ldx,
+                                                          uint16_t* __restrict__ out, int64_t R, int D, int64_t Rp,
+                                                          int Dp, int npl, uint32_t order, int stacked) {
+  const int64_t n = Rp * Dp;
+  const int64_t row_stride = stacked ? (int64_t)Dp : (int64_t)npl * Dp;
+  const int64_t plane_stride = stacked ? Rp * Dp : (int64_t)Dp;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / Dp;
+    const int c = (int)(i - r * Dp);
+    float e = (r < R && c < D) ? x[r * ldx + c] : 0.f;
+    uint16_t p[NPIECE];
+#pragma unroll
+    for (int k = 0; k < NPIECE; ++k) {
+      p[k] = hx::f2bf(e);
+      e -= hx::bf2f(p[k]);
+    }
+    uint16_t* o = out + r * row_stride + c;
+    for (int j = 0; j < npl; ++j) {
+      const int k = (order >> (4 * j)) & 15;
+      o[j * plane_stride] = p[k < NPIECE ? k : NPIECE - 1];
+    }
+  }
+}
+
 }  // namespace
 
-void hx_split_planes(const float* x, int64_t ldx, uint16_t* out, int64_t R, int D, int npieces, int npl,
-                     uint32_t order, int stacked, hipStream_t s) {
-  const int64_t n8 = R * (D / 8);
-  if (n8 <= 0) return;
-  const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 8192);
+void hx_split_planes(const float* x, int64_t ldx, uint16_t* out, int64_t R, int D, int64_t Rp, int Dp,
+                     int npieces, int npl, uint32_t order, int stacked, hipStream_t s) {
+  const bool vec = D % 8 == 0 && Dp == D && Rp == R && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0;
+  if (vec) {
+    const int64_t n8 = R * (D / 8);
+    if (n8 <= 0) return;
+    const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 8192);
+    if (npieces == 3)
+      split_planes_k<3><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, npl, order, stacked);
+    else
+      split_planes_k<2><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, npl, order, stacked);
+    return;
+  }
+  const int64_t n = Rp * Dp;
+  if (n <= 0) return;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 16384);
   if (npieces == 3)
-    split_planes_k<3><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, npl, order, stacked);
+    split_planes_any_k<3><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, Rp, Dp, npl, order, stacked);
   else
-    split_planes_k<2><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, npl, order, stacked);
+    split_planes_any_k<2><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, Rp, Dp, npl, order, stacked);
 }

@@ -37,7 +37,10 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
-constexpr int BK = 32;   // tokens per pipeline step (two 16-deep MFMA k-steps)
+#ifndef HX_WGRAD_BK
+#define HX_WGRAD_BK 64
+#endif
+constexpr int BK = HX_WGRAD_BK;   // tokens per pipeline step (BK / 16 MFMA k-steps per barrier)
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 

@@ -1,0 +1,306 @@
+// Weight gradient of an fp32 linear layer on the bf16 matrix cores (--fp32-gemm bf16x3/x6):
+//
+//   dW[M][N] (fp32) = sum over tokens t and piece pairs (a, b) of dY_a[t][M]^T . X_b[t][N]
+//
+// where dY = dY_0 + dY_1 (+ dY_2) and X = X_0 + X_1 (+ X_2) are the bf16 pieces written by
+// split.hip (ops/split_gemm.py) and the pairs are (0,0) (0,1) (1,0) [+ (0,2) (1,1) (2,0)].
+//
+// The first form of this product ran the generic tokens-as-reduction kernel
+// (wgrad_bf16.hip) over the stacked [passes * T] plane rows, i.e. it streamed every pass
+// operand from memory and LDS separately: dY_0 twice for bf16x3, X_0 three times for
+// bf16x6.  Here each DISTINCT piece of a token block is staged once (global -> registers
+// -> swizzled LDS tile) and every pass reuses it from registers:
+//
+//   per 16-token MFMA step and wave (64 x 64 outputs): NA + NB piece fragments per 32-row
+//   block, then 3 (6) x 4 MFMAs -- 0.67 (0.5) KB of LDS fragment reads per MFMA instead
+//   of 1 KB, and 2/3 (1/2) of the global / L2 bytes per FLOP.
+//
+// Everything else follows wgrad_bf16.hip: 64-token pipeline steps staged two steps ahead in
+// registers, XOR-swizzled 8 x 32 subtiles read as k-major fragments with the gfx950
+// transposing LDS read (ds_read_b64_tr_b16), split-K over token ranges to fill the CUs,
+// fp32 partial tiles summed by one vectorised pass (no float atomics), XCD-aware work
+// ranges.
+#include <algorithm>
+
+#include <stdio.h>
+#include <stdlib.h>
+
+#include "hx_launch.h"
+#include "hx_attn.h"
+#include "hx_common.h"
+
+namespace {
+
+using hx::attn::crow;
+using hx::attn::f32x16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BK = 32;   // tokens per pipeline step (two 16-deep MFMA k-steps per barrier)
+
+// LDS image of a [BK rows][W columns] bf16 tile (wgrad_bf16.hip's layout): 8-row x 32-column
+// subtiles of 512 B, XOR-swizzled 16-B chunks, odd subtiles with the rows of each pair
+// swapped (conflict-free 16-B stores and transposed reads).
+template <int W>
+__device__ __forceinline__ int toff(int row, int ch) {
+  return (row >> 3) * (16 * W) + 512 * (ch >> 2) + 64 * ((row & 7) ^ ((ch >> 2) & 1)) +
+         16 * ((ch & 3) ^ ((row >> 2) & 3));
+}
+template <int W>
+__device__ __forceinline__ void tr_base(int lane, int (&lo)[2], int (&hi)[2]) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int row = 8 * (g >> 1) + q, ch = 2 * (g & 1) + (p >> 1);
+  lo[0] = toff<W>(row, ch) + 8 * (p & 1);
+  hi[0] = toff<W>(row + 4, ch) + 8 * (p & 1);
+  lo[1] = toff<W>(row, ch + 4) - 512 + 8 * (p & 1);
+  hi[1] = toff<W>(row + 4, ch + 4) - 512 + 8 * (p & 1);
+}
+template <int W>
+__device__ __forceinline__ bf16x8 frag(const char* tile, const int (&lo)[2], const int (&hi)[2], int k0, int c0,
+                                       int odd) {
+  const int d = (k0 >> 4) * (32 * W) + (c0 >> 5) * 512;
+  const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(tile + lo[odd] + d));
+  const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(tile + hi[odd] + d));
+  const v4i16 v[2] = {a, b};
+  return *reinterpret_cast<const bf16x8*>(v);
+}
+
+// piece pairs (a, b) of the product, in pass order (ops/split_gemm.py)
+template <int NP>
+struct Pairs;
+template <>
+struct Pairs<3> {
+  static constexpr int a[3] = {0, 0, 1};
+  static constexpr int b[3] = {0, 1, 0};
+};
+template <>
+struct Pairs<6> {
+  static constexpr int a[6] = {0, 0, 1, 0, 1, 2};
+  static constexpr int b[6] = {0, 1, 0, 2, 1, 0};
+};
+
+struct PieceBases {
+  const uint16_t* a[3];   // dY pieces (same row stride lda)
+  const uint16_t* b[3];   // X pieces (same row stride ldb)
+};
+
+template <int BM, int BN, int WM, int WN, int NPC, int NP>
+__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_split_k(PieceBases P, int lda, int ldb,
+                                                                           float* __restrict__ out, int M, int N,
+                                                                           int T, int kchunk, int nsplit) {
+  constexpr int NWM = BM / WM, NW = NWM * (BN / WN), NT = NW * 64;
+  constexpr int MB = WM / 32, NB = WN / 32;
+  constexpr int CA = BK * BM / 8 / NT, CB = BK * BN / 8 / NT;   // 16-B chunks per thread per piece
+  static_assert(WM % 64 == 0 && WN % 64 == 0, "subtile parity of fragment a is a & 1");
+  static_assert(CA >= 1 && CB >= 1 && BK * BM / 8 % NT == 0 && BK * BN / 8 % NT == 0, "tile / thread mismatch");
+  constexpr int A_BYTES = BK * BM * 2, B_BYTES = BK * BN * 2;
+  constexpr int STAGE = NPC * (A_BYTES + B_BYTES);
+  extern __shared__ __attribute__((aligned(16))) char lds[];   // [2 stages][NPC A tiles, NPC B tiles]
+
+  const int TM = M / BM, TN = N / BN, total = TM * TN * nsplit;
+  const int per = (total + 7) / 8;
+  const int work = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (work >= total) return;         // uniform per workgroup
+  const int nt = work % TN, mt = (work / TN) % TM, sp = work / (TN * TM);
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int t0 = sp * kchunk, t1 = min(T, t0 + kchunk);
+  const int nit = (t1 - t0 + BK - 1) / BK;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w % NWM, wn = w / NWM, h = lane >> 5, l32 = lane & 31;
+
+  // one buffer resource per piece over rows [t0, t1): loads past t1 return zeros
+  const uint32_t abytes = (uint32_t)((int64_t)(t1 - t0) * lda * 2), bbytes = (uint32_t)((int64_t)(t1 - t0) * ldb * 2);
+  const hx::Buf abuf[3] = {hx::Buf(P.a[0] + (int64_t)t0 * lda, abytes), hx::Buf(P.a[1] + (int64_t)t0 * lda, abytes),
+                           hx::Buf(P.a[2] + (int64_t)t0 * lda, abytes)};
+  const hx::Buf bbuf[3] = {hx::Buf(P.b[0] + (int64_t)t0 * ldb, bbytes), hx::Buf(P.b[1] + (int64_t)t0 * ldb, bbytes),
+                           hx::Buf(P.b[2] + (int64_t)t0 * ldb, bbytes)};
+  uint32_t va[CA], vb[CB];
+  int sa[CA], sb[CB];
+#pragma unroll
+  for (int i = 0; i < CA; ++i) {
+    const int e = tid + i * NT, row = e / (BM / 8), ch = e % (BM / 8);
+    va[i] = (uint32_t)(row * lda + m0 + 8 * ch) * 2;
+    sa[i] = toff<BM>(row, ch);
+  }
+#pragma unroll
+  for (int i = 0; i < CB; ++i) {
+    const int e = tid + i * NT, row = e / (BN / 8), ch = e % (BN / 8);
+    vb[i] = (uint32_t)(row * ldb + n0 + 8 * ch) * 2;
+    sb[i] = toff<BN>(row, ch);
+  }
+  int alo[2], ahi[2], blo[2], bhi[2];
+  tr_base<BM>(lane, alo, ahi);
+  tr_base<BN>(lane, blo, bhi);
+
+  u32x4 ra0[NPC][CA], rb0[NPC][CB], ra1[NPC][CA], rb1[NPC][CB];
+  auto load = [&](int it, u32x4 (&ra)[NPC][CA], u32x4 (&rb)[NPC][CB]) {
+    const uint32_t soa = (uint32_t)it * BK * lda * 2, sob = (uint32_t)it * BK * ldb * 2;
+#pragma unroll
+    for (int p = 0; p < NPC; ++p) {
+#pragma unroll
+      for (int i = 0; i < CA; ++i) ra[p][i] = __builtin_amdgcn_raw_buffer_load_b128(abuf[p].r, va[i], soa, 0);
+#pragma unroll
+      for (int i = 0; i < CB; ++i) rb[p][i] = __builtin_amdgcn_raw_buffer_load_b128(bbuf[p].r, vb[i], sob, 0);
+    }
+  };
+  auto store = [&](int buf, const u32x4 (&ra)[NPC][CA], const u32x4 (&rb)[NPC][CB]) {
+    char* st = lds + buf * STAGE;
+#pragma unroll
+    for (int p = 0; p < NPC; ++p) {
+      char* at = st + p * A_BYTES;
+      char* bt = st + NPC * A_BYTES + p * B_BYTES;
+#pragma unroll
+      for (int i = 0; i < CA; ++i) *reinterpret_cast<u32x4*>(at + sa[i]) = ra[p][i];
+#pragma unroll
+      for (int i = 0; i < CB; ++i) *reinterpret_cast<u32x4*>(bt + sb[i]) = rb[p][i];
+    }
+  };
+
+  f32x16 acc[MB][NB];
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[a][b] = f32x16{0};
+
+  auto mma = [&](int buf) {
+    const char* st = lds + buf * STAGE;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8 fa[NPC][MB], fb[NPC][NB];
+#pragma unroll
+      for (int p = 0; p < NPC; ++p) {
+#pragma unroll
+        for (int a = 0; a < MB; ++a)
+          fa[p][a] = frag<BM>(st + p * A_BYTES, alo, ahi, 16 * ks, wm * WM + 32 * a, a & 1);
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          fb[p][b] = frag<BN>(st + NPC * A_BYTES + p * B_BYTES, blo, bhi, 16 * ks, wn * WN + 32 * b, b & 1);
+      }
+#pragma unroll
+      for (int q = 0; q < NP; ++q)
+#pragma unroll
+        for (int a = 0; a < MB; ++a)
+#pragma unroll
+          for (int b = 0; b < NB; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[Pairs<NP>::a[q]][a], fb[Pairs<NP>::b[q]][b],
+                                                                acc[a][b], 0, 0, 0);
+    }
+  };
+
+  load(0, ra0, rb0);
+  load(1, ra1, rb1);
+  store(0, ra0, rb0);
+  __syncthreads();
+  for (int it = 0; it < nit; it += 2) {
+    load(it + 2, ra0, rb0);
+    mma(0);
+    store(1, ra1, rb1);
+    __syncthreads();
+    if (it + 1 >= nit) break;
+    load(it + 3, ra1, rb1);
+    mma(1);
+    store(0, ra0, rb0);
+    __syncthreads();
+  }
+
+  float* o = out + (nsplit > 1 ? (int64_t)sp * M * N : 0);
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int n = n0 + wn * WN + 32 * b + l32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * WM + 32 * a + crow(r, h);
+        o[(int64_t)m * N + n] = acc[a][b][r];
+      }
+    }
+}
+
+__global__ __launch_bounds__(256) void split_sum2_k(const float4* __restrict__ ws, float4* __restrict__ out,
+                                                   int64_t n4, int nsplit) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 s = ws[i];
+    for (int k = 1; k < nsplit; ++k) {
+      const float4 v = ws[(int64_t)k * n4 + i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    out[i] = s;
+  }
+}
+
+template <int BM, int BN, int WM, int WN, int NPC, int NP>
+void launch(const PieceBases& P, int lda, int ldb, float* out, float* ws, int M, int N, int T, int nsplit,
+            hipStream_t s) {
+  constexpr int NT = (BM / WM) * (BN / WN) * 64;
+  const int kchunk = ((T + nsplit - 1) / nsplit + BK - 1) / BK * BK;
+  nsplit = (T + kchunk - 1) / kchunk;
+  const int total = (M / BM) * (N / BN) * nsplit;
+  const int per = (total + 7) / 8;
+  const size_t smem = 2 * (size_t)NPC * BK * (BM + BN) * sizeof(uint16_t);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_split_k<BM, BN, WM, WN, NPC, NP>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    attr = true;
+  }
+  wgrad_split_k<BM, BN, WM, WN, NPC, NP><<<8 * per, NT, smem, s>>>(P, lda, ldb, nsplit > 1 ? ws : out, M, N, T,
+                                                                  kchunk, nsplit);
+  if (nsplit > 1) {
+    const int64_t n4 = (int64_t)M * N / 4;
+    const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+    split_sum2_k<<<blocks, 256, 0, s>>>(reinterpret_cast<const float4*>(ws), reinterpret_cast<float4*>(out), n4,
+                                        nsplit);
+  }
+}
+
+}  // namespace
+
+// cfg 0: 128x128 workgroup tile, 4 waves of 64x64; cfg 1: 256x128, 8 waves of 64x64.
+// The split count fills one round of workgroup slots (256 for cfg 1, 512 for cfg 0);
+// HX_WGRAD_SPLIT_CFG="cfg:nsplit" overrides (tools/bench_wgrad.py --split-sweep).
+void hx_wgrad_split_plan(int M, int N, int T, int passes, int* cfg, int* nsplit) {
+  int c = (M % 256 == 0 && N % 128 == 0) ? 1 : 0;
+  const int slots = c == 1 ? 256 : 512;
+  const int tiles0 = (M / (c == 1 ? 256 : 128)) * (N / 128);
+  int s = std::max(1, slots / std::max(1, tiles0));
+  s = std::min(s, std::max(1, T / 256));
+  if (const char* e = getenv("HX_WGRAD_SPLIT_CFG")) {
+    int ec = -1, es = -1;
+    if (sscanf(e, "%d:%d", &ec, &es) == 2 && ec >= 0 && ec < 2 && es >= 1 && M % (ec == 1 ? 256 : 128) == 0 &&
+        N % 128 == 0) {
+      c = ec;
+      s = std::min(es, std::max(1, T / BK));
+    }
+  }
+  (void)passes;
+  *cfg = c;
+  *nsplit = s;
+}
+
+int hx_wgrad_split(const void* const* dy_pieces, int ldy, const void* const* x_pieces, int ldx, int passes,
+                   float* out, float* ws, int M, int N, int T, int cfg, int nsplit, hipStream_t s) {
+  PieceBases P;
+  const int npc = passes == 6 ? 3 : 2;
+  for (int i = 0; i < 3; ++i) {
+    P.a[i] = (const uint16_t*)dy_pieces[i < npc ? i : 0];
+    P.b[i] = (const uint16_t*)x_pieces[i < npc ? i : 0];
+  }
+  if (passes == 3) {
+    if (cfg == 1)
+      launch<256, 128, 64, 64, 2, 3>(P, ldy, ldx, out, ws, M, N, T, nsplit, s);
+    else
+      launch<128, 128, 64, 64, 2, 3>(P, ldy, ldx, out, ws, M, N, T, nsplit, s);
+  } else if (passes == 6) {
+    if (cfg == 1)
+      launch<256, 128, 64, 64, 3, 6>(P, ldy, ldx, out, ws, M, N, T, nsplit, s);
+    else
+      launch<128, 128, 64, 64, 3, 6>(P, ldy, ldx, out, ws, M, N, T, nsplit, s);
+  } else {
+    return -1;
+  }
+  return 0;
+}

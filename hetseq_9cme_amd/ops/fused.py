@@ -550,7 +550,11 @@ def attention(qkv, mask_bias, num_heads, p, training, bias=None):
 class _DecoderXentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, W, bias, labels):
-        logits = torch.mm(h, cast_w(W, h.dtype).t())
+        ctx.split = split_gemm.active(h)
+        if ctx.split:    # fp32 on bf16 matrix cores (--fp32-gemm)
+            logits, _ = split_gemm.forward(h, W)
+        else:
+            logits = torch.mm(h, cast_w(W, h.dtype).t())
         loss_rows = C().softmax_xent_(logits, bias, labels, -1)   # logits <- softmax - onehot
         count = (labels != -1).sum().to(torch.float32)
         loss = loss_rows.sum() / count
@@ -568,9 +572,24 @@ class _DecoderXentFn(torch.autograd.Function):
         # M x V gradient itself (a 312 MB rewrite at B=128).
         scale = (g.float() / count).reshape(1)
         dbias = C().colsum(dl, scale, grad_slot(bias) if bias is not None else None)
-        dh = torch.mm(dl, cast_w(Wp, dl.dtype)).mul_(scale.to(dl.dtype))
         hs = h * scale.to(h.dtype)
         slot = grad_slot(Wp)
+        if ctx.split:
+            # logits-gradient planes padded to a multiple of 64 columns (16-B rows for the GEMMs)
+            V = dl.shape[1]
+            Vp = (V + 63) // 64 * 64
+            dls = split_gemm.grad_planes(dl, dpad=Vp)
+            dh = split_gemm.dgrad(dls, Wp, rpad=Vp).mul_(scale)
+            n = split_gemm.passes()
+            hsp = split_gemm.planes(hs, split_gemm.ORDER_P[n])
+            a = dls.view(-1, Vp)[:, :V]
+            b = hsp.view(-1, hs.shape[1])
+            if slot is not None:
+                dW = torch.mm(a.t(), b, out_dtype=torch.float32, out=slot)
+            else:
+                dW = torch.mm(a.t(), b, out_dtype=torch.float32)
+            return dh, dW, dbias, None
+        dh = torch.mm(dl, cast_w(Wp, dl.dtype)).mul_(scale.to(dl.dtype))
         side = side_begin(dl.device) if slot is not None else None
         with torch.cuda.stream(side) if side is not None else _nullctx():
             dW = _wgrad(dl, hs, slot)

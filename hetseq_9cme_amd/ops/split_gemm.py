@@ -36,9 +36,11 @@ is fixed per role so the three GEMMs of a linear layer pair the right pieces:
   wgrad    dW = dy'^T . x'  over nT rows     pairs (Q_j, P_j)   ([T, n, D] viewed as [nT, D])
 
 Every pairs column is {(0,0), (1,0), (0,1)} (bf16x6: plus (2,0), (1,1), (0,2)).
-The weight-gradient GEMM runs on the hand-written split-K bf16 kernel
-(``csrc/kernels/wgrad_bf16.hip``), whose tokens-as-reduction form takes the
-[nT, D] views directly.
+The weight-gradient GEMM runs on a hand-written split-K kernel
+(``csrc/kernels/wgrad_split.hip``) that stages each DISTINCT piece of a token
+block once and runs all passes from registers (the stacked [nT, D] views would
+stream dY_0 twice / X_0 three times); shapes it does not cover take the stacked
+form through ``wgrad_bf16.hip`` or the library.
 """
 import torch
 
@@ -75,12 +77,12 @@ def passes():
     return _State.passes
 
 
-def planes(x2, order, stacked=False):
-    """bf16 planes of the fp32 matrix ``x2`` [R, D]: [R, n*D] interleaved, or
-    [n*R, D] stacked."""
-    if x2.stride(-1) != 1 or x2.stride(0) % 4 or x2.data_ptr() % 16:
+def planes(x2, order, stacked=False, rpad=0, dpad=0):
+    """bf16 planes of the fp32 matrix ``x2`` [R, D]: [R, n*Dp] interleaved, or
+    [n*Rp, Dp] stacked, rows / columns zero-padded to ``rpad`` / ``dpad``."""
+    if x2.stride(-1) != 1:
         x2 = x2.contiguous()
-    return C().split_planes(x2, list(order), PIECES[len(order)], bool(stacked))
+    return C().split_planes(x2, list(order), PIECES[len(order)], bool(stacked), int(rpad), int(dpad))
 
 
 def forward(x2, W):
@@ -91,13 +93,14 @@ def forward(x2, W):
     return torch.mm(xs, wq.t(), out_dtype=torch.float32), xs
 
 
-def grad_planes(dy2):
-    return planes(dy2, ORDER_Q[_State.passes])
+def grad_planes(dy2, dpad=0):
+    return planes(dy2, ORDER_Q[_State.passes], dpad=dpad)
 
 
-def dgrad(dys, W, acc=None):
-    """dy @ W (fp32) from the dy planes; accumulated into ``acc`` (beta = 1) if given."""
-    wb = planes(W, ORDER_P[_State.passes], stacked=True)
+def dgrad(dys, W, acc=None, rpad=0):
+    """dy @ W (fp32) from the dy planes; accumulated into ``acc`` (beta = 1) if given.
+    ``rpad``: dy's planes were column-padded to this width (W's rows are padded to match)."""
+    wb = planes(W, ORDER_P[_State.passes], stacked=True, rpad=rpad)
     if acc is None:
         return torch.mm(dys, wb, out_dtype=torch.float32)
     if _State.addmm_out_ok is not False:
@@ -110,7 +113,19 @@ def dgrad(dys, W, acc=None):
     return acc.add_(torch.mm(dys, wb, out_dtype=torch.float32))
 
 
+def _piece_offsets(order, d):
+    """Column offset of the first plane holding each distinct piece."""
+    return [order.index(k) * d for k in range(PIECES[len(order)])]
+
+
 def wgrad(dys, xs, n_out, n_in, slot):
-    """dW [n_out, n_in] = sum over tokens and passes of dy-piece^T x-piece."""
+    """dW [n_out, n_in] = sum over tokens and passes of dy-piece^T x-piece.  The
+    split-piece kernel (csrc/kernels/wgrad_split.hip) stages each distinct piece once
+    and runs all passes from registers; other shapes use the stacked-rows form."""
+    n = _State.passes
+    if C().wgrad_split_ok(dys, xs, n_out, n_in):
+        out = slot if slot is not None else torch.empty(n_out, n_in, device=dys.device)
+        return C().wgrad_split(dys, _piece_offsets(ORDER_Q[n], n_out), xs, _piece_offsets(ORDER_P[n], n_in), n,
+                               n_out, n_in, out)
     from .fused import _wgrad
     return _wgrad(dys.view(-1, n_out), xs.view(-1, n_in), slot)

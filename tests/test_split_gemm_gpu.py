@@ -28,7 +28,7 @@ def test_split_planes_bitwise(dev, npieces, order, stacked):
     from hetseq_9cme_amd.ops._ext import C
     g = torch.Generator(device='cpu').manual_seed(3)
     x = (torch.randn(37, 264, generator=g) * torch.logspace(-6, 6, 264)).to(dev)
-    out = C().split_planes(x, list(order), npieces, stacked)
+    out = C().split_planes(x, list(order), npieces, stacked, 0, 0)
     pcs = _ref_pieces(x, npieces)
     if stacked:
         ref = torch.cat([pcs[k] for k in order], 0)
@@ -40,6 +40,32 @@ def test_split_planes_bitwise(dev, npieces, order, stacked):
     s = sum(p.double() for p in pcs)
     tol = 2.0 ** -16 if npieces == 2 else 2.0 ** -25
     assert ((s - x.double()).abs() <= tol * x.double().abs()).all()
+
+
+@pytest.mark.parametrize('stacked', [False, True])
+def test_split_planes_padded_unaligned(dev, stacked):
+    """General path: odd width, unaligned rows (a column slice), zero padding of rows
+    (stacked) or columns (interleaved) -- the MLM decoder's 30522-wide case."""
+    from hetseq_9cme_amd.ops._ext import C
+    g = torch.Generator(device='cpu').manual_seed(4)
+    big = torch.randn(21, 131, generator=g).to(dev)
+    x = big[:, 1:122]                       # [21, 121], row stride 131, misaligned start
+    order = (0, 0, 1)
+    rpad, dpad = (32, 0) if stacked else (0, 128)
+    out = C().split_planes(x, list(order), 2, stacked, rpad, dpad)
+    pcs = _ref_pieces(x.contiguous(), 2)
+    if stacked:
+        ref = torch.zeros(3, 32, 121, dtype=torch.bfloat16, device=dev)
+        for j, k in enumerate(order):
+            ref[j, :21] = pcs[k]
+        ref = ref.reshape(96, 121)
+    else:
+        ref = torch.zeros(21, 3, 128, dtype=torch.bfloat16, device=dev)
+        for j, k in enumerate(order):
+            ref[:, j, :121] = pcs[k]
+        ref = ref.reshape(21, 384)
+    assert out.shape == ref.shape
+    assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
 
 
 def _err(a, ref, scale):
@@ -130,3 +156,30 @@ def test_training_split_modes_track_native(dev, tmp_path):
             d_ = (outs[mode]['model'][k].double() - v.double()).abs().max().item()
             worst = max(worst, d_ / (v.double().abs().max().item() + 1e-12))
         assert worst < (1e-4 if mode == 'bf16x6' else 5e-4), (mode, worst)
+
+
+@pytest.mark.parametrize('mode,tol', [('bf16x3', 6e-6), ('bf16x6', 2e-6)])
+def test_decoder_xent_split(dev, mode, tol):
+    """MLM decoder + softmax-xent with a vocabulary that is not a multiple of 8 (padded planes)."""
+    from hetseq_9cme_amd import ops
+    g = torch.Generator(device='cpu').manual_seed(11)
+    M, H, V = 96, 128, 1001
+    h = torch.randn(M, H, generator=g).to(dev).requires_grad_(True)
+    W = (torch.randn(V, H, generator=g) * 0.1).to(dev).requires_grad_(True)
+    b = torch.randn(V, generator=g).to(dev).requires_grad_(True)
+    labels = torch.randint(0, V, (M,), generator=g).to(dev)
+    labels[::7] = -1
+    try:
+        ops.set_fp32_gemm(mode)
+        loss = ops.decoder_xent(h, W, b, labels)
+        loss.backward()
+    finally:
+        ops.set_fp32_gemm('native')
+    hd, Wd, bd = h.detach().double().requires_grad_(True), W.detach().double().requires_grad_(True), \
+        b.detach().double().requires_grad_(True)
+    ref = torch.nn.functional.cross_entropy(hd @ Wd.t() + bd, labels, ignore_index=-1)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-5 * abs(ref.item())
+    for got, r in ((h.grad, hd.grad), (W.grad, Wd.grad), (b.grad, bd.grad)):
+        e = (got.double() - r).abs().max().item() / r.abs().max().item()
+        assert e < 50 * tol, (mode, e)

@@ -33,9 +33,12 @@ def timeit(fn, iters=30, warmup=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--tokens', type=int, default=16384)
+    ap.add_argument('--split', type=int, default=0, help='time the split-piece kernel (3 or 6 passes) vs stacked')
     ap.add_argument('--sweep', action='store_true',
                     help='time every (tile config, token split) of the hand-written kernel via HX_WGRAD_CFG')
     a = ap.parse_args()
+    if a.split:
+        return split_bench(a.tokens, a.split)
     if a.sweep:
         return sweep(a.tokens)
     T = a.tokens
@@ -76,7 +79,9 @@ def main():
 
 def sweep(T):
     from hetseq_9cme_amd.ops._ext import C
-    tiles = {0: (128, 128), 1: (256, 128), 3: (256, 128)}
+    tiles = {0: (128, 128), 1: (256, 128), 3: (256, 128), 2: (256, 256), 4: (256, 256)}
+    if os.environ.get("HX_SWEEP_CFGS"):
+        tiles = {int(c): tiles[int(c)] for c in os.environ["HX_SWEEP_CFGS"].split(",")}
     for (n_out, n_in) in [(3072, 768), (768, 3072), (2304, 768), (768, 768)]:
         dy = torch.randn(T, n_out, device='cuda').to(torch.bfloat16)
         x = torch.randn(T, n_in, device='cuda').to(torch.bfloat16)
@@ -101,6 +106,42 @@ def sweep(T):
         os.environ.pop('HX_WGRAD_CFG', None)
         print('[{}x{} T={}] plan {:.1f} us; best {} {:.1f} us ({:.1f} TF/s)'.format(
             n_out, n_in, T, base, best[1], best[0], fl / best[0] / 1e6), flush=True)
+
+
+def split_bench(T, passes):
+    """--fp32-gemm bf16x3/x6 weight gradients: split-piece kernel (all token splits) vs the
+    stacked-rows kernel, checked against an fp64 product of the fp32 operands."""
+    from hetseq_9cme_amd import ops
+    from hetseq_9cme_amd.ops import split_gemm as sg
+    from hetseq_9cme_amd.ops._ext import C
+    ops.set_fp32_gemm('bf16x{}'.format(passes))
+    for (n_out, n_in) in [(3072, 768), (768, 3072), (2304, 768), (768, 768)]:
+        dy = torch.randn(T, n_out, device='cuda')
+        x = torch.randn(T, n_in, device='cuda')
+        dys, xs = sg.grad_planes(dy), sg.planes(x, sg.ORDER_P[passes])
+        slot = torch.empty(n_out, n_in, device='cuda')
+        ref = dy.double().t() @ x.double()
+        scale = dy.double().abs().t() @ x.double().abs()
+        fl = 2.0 * T * n_out * n_in * passes
+        stacked = timeit(lambda: C().wgrad_bf16(dys.view(-1, n_out), xs.view(-1, n_in), slot))
+        print('[{}x{} T={} x{}] stacked {:8.1f} us {:7.1f} TF/s'.format(n_out, n_in, T, passes, stacked,
+                                                                       fl / stacked / 1e6), flush=True)
+        po, px = sg._piece_offsets(sg.ORDER_Q[passes], n_out), sg._piece_offsets(sg.ORDER_P[passes], n_in)
+        for cfg in (0, 1):
+            if n_out % (256 if cfg else 128):
+                continue
+            for ns in (0, 1, 2, 3, 4, 6, 8):
+                if ns:
+                    os.environ['HX_WGRAD_SPLIT_CFG'] = '{}:{}'.format(cfg, ns)
+                else:
+                    os.environ.pop('HX_WGRAD_SPLIT_CFG', None)
+                us = timeit(lambda: C().wgrad_split(dys, po, xs, px, passes, n_out, n_in, slot))
+                err = ((slot.double() - ref).abs() / scale).max().item()
+                print('[{}x{} T={} x{}] split cfg {} nsplit {} {:8.1f} us {:7.1f} TF/s err {:.2e}'.format(
+                    n_out, n_in, T, passes, cfg, ns or 'plan', us, fl / us / 1e6, err), flush=True)
+                if not ns and cfg == 1:
+                    break
+        os.environ.pop('HX_WGRAD_SPLIT_CFG', None)
 
 
 if __name__ == '__main__':

@@ -1,7 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_split_gemm_gpu.py tests/test_xgmi_gpu.py -x -v --timeout 120 --timeout-method thread > gpurun_out/split_tests.log 2>&1
-echo "tests rc=$?"
-for m in bf16x3 bf16x6; do
-timeout -k 10 300 python -u bench.py --fp32-gemm $m > gpurun_out/bench_$m.log 2>&1 || exit 1
-done
+timeout -k 10 300 python -u -m pytest tests/test_split_gemm_gpu.py -x -v --timeout 120 --timeout-method thread > gpurun_out/split_tests.log 2>&1 &&
+timeout -k 10 300 python -u bench.py --fp32-gemm bf16x3 > gpurun_out/bench_bf16x3.log 2>&1 &&
+timeout -k 10 300 python -u bench.py --fp32-gemm bf16x6 > gpurun_out/bench_bf16x6.log 2>&1 &&
+bash tools/prof_run.sh x3 --fp32-gemm bf16x3 && bash tools/prof_run.sh x6 --fp32-gemm bf16x6

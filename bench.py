@@ -40,8 +40,9 @@ def parse():
     ap.add_argument('--seq', type=int, default=128)
     ap.add_argument('--max-pred', type=int, default=20)
     ap.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'])
-    ap.add_argument('--fp32-gemm', default='native', choices=['native', 'bf16x3', 'bf16x6'],
-                    help='fp32 linear GEMMs: native f32 MFMA or bf16-plane emulation (ops/split_gemm.py)')
+    ap.add_argument('--fp32-gemm', default='bf16x6', choices=['native', 'bf16x3', 'bf16x6'],
+                    help='fp32 linear GEMMs: bf16x6 (default, fp32-exact class), bf16x3 (near-fp32) or '
+                         'native f32 MFMA (ops/split_gemm.py)')
     ap.add_argument('--model', default='base', choices=['base', 'large', 'tiny'])
     ap.add_argument('--no-fused', action='store_true', help='torch-op baseline (A/B only)')
     ap.add_argument('--data-dir', default=None)

@@ -423,6 +423,43 @@ Tensor wgrad_split(Tensor dys, std::vector<int64_t> dy_off, Tensor xs, std::vect
   return out;
 }
 
+// ------------------------------------------------------------------ bias + activation -> planes
+// forward (dout absent): planes of act(y + b); backward: planes of dout * act'(y + b) and dbias.
+std::vector<Tensor> bias_act_planes(Tensor y, OptT b, OptT dout, int64_t act, std::vector<int64_t> order,
+                                    int64_t npieces, OptT dbias_out) {
+  check_f32(y, "bias_act_planes input");
+  const int N = (int)y.size(-1);
+  const int64_t rows = y.numel() / N;
+  TORCH_CHECK(N % 8 == 0 && aligned16(y.data_ptr()), "bias_act_planes: last dim must be a multiple of 8");
+  TORCH_CHECK(npieces == 2 || npieces == 3, "bias_act_planes: 2 or 3 pieces");
+  TORCH_CHECK(!order.empty() && order.size() <= 8, "bias_act_planes: 1..8 planes");
+  uint32_t packed = 0;
+  for (size_t j = 0; j < order.size(); ++j) {
+    TORCH_CHECK(order[j] >= 0 && order[j] < npieces, "bias_act_planes: piece index out of range");
+    packed |= (uint32_t)order[j] << (4 * j);
+  }
+  if (has(b)) TORCH_CHECK(b->numel() == N && b->scalar_type() == torch::kFloat32, "bias_act_planes: bad bias");
+  if (has(dout)) {
+    check_f32(*dout, "bias_act_planes grad");
+    TORCH_CHECK(dout->numel() == y.numel(), "bias_act_planes: grad shape");
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(y.device());
+  const int64_t npl = (int64_t)order.size();
+  Tensor planes = torch::empty({rows, npl * N}, y.options().dtype(torch::kBFloat16));
+  Tensor dbias, ws;
+  const bool want_db = has(dout);
+  if (want_db) {
+    auto f32 = y.options().dtype(torch::kFloat32);
+    dbias = has(dbias_out) ? *dbias_out : torch::empty({N}, f32);
+    ws = torch::empty({(int64_t)hx_colsum_ws_floats(rows, N)}, f32);
+  }
+  hx_bias_act_planes((int)act, y.data_ptr<float>(), ptr_or_null<float>(b), has(dout) ? dout->data_ptr<float>() : nullptr,
+                     reinterpret_cast<uint16_t*>(planes.data_ptr()), want_db ? ws.data_ptr<float>() : nullptr,
+                     want_db ? dbias.data_ptr<float>() : nullptr, rows, N, (int)npieces, (int)npl, packed,
+                     cur_stream(y));
+  return {planes, dbias};
+}
+
 // ------------------------------------------------------------------ split planes
 Tensor split_planes(Tensor x, std::vector<int64_t> order, int64_t npieces, bool stacked, int64_t rpad,
                     int64_t dpad) {
@@ -517,6 +554,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_bf16", &wgrad_bf16);
   m.def("wgrad_bf16_ok", &wgrad_bf16_ok);
   m.def("split_planes", &split_planes);
+  m.def("bias_act_planes", &bias_act_planes);
   m.def("wgrad_split", &wgrad_split);
   m.def("wgrad_split_ok", &wgrad_split_ok);
   m.def("xar_create", &xar_create);

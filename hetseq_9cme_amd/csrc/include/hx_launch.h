@@ -71,6 +71,13 @@ void hx_wgrad_split_plan(int M, int N, int T, int passes, int* cfg, int* nsplit)
 int hx_wgrad_split(const void* const* dy_pieces, int ldy, const void* const* x_pieces, int ldx, int passes,
                    float* out, float* ws, int M, int N, int T, int cfg, int nsplit, hipStream_t s);
 
+// elementwise.hip -- bias + activation (dout == nullptr) or its backward (dout != nullptr, with
+// dbias through the [nchunks][N] partial workspace) written as bf16 planes (split-GEMM path);
+// fp32 y / dout [rows][N], N % 8 == 0.
+void hx_bias_act_planes(int act, const float* y, const float* b, const float* dout, uint16_t* planes,
+                        float* partial, float* dbias, int64_t rows, int N, int npieces, int npl, uint32_t order,
+                        hipStream_t s);
+
 // split.hip -- fp32 -> bf16 planes (piece order[j] = (order >> 4j) & 15) for bf16-MFMA
 // emulation of fp32 GEMMs; interleaved [R][npl][D] or stacked [npl][R][D].
 // Output rows padded to Rp (stacked) / columns to Dp with zeros.

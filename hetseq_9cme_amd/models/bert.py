@@ -243,7 +243,10 @@ class BertOutput(nn.Module):
         self.dropout = nn.Dropout(config.hidden_dropout_prob)
 
     def forward(self, hidden_states, input_tensor, res_grad=None):
-        y = ops.linear(hidden_states, self.dense.weight)
+        return self.finish(ops.linear(hidden_states, self.dense.weight), input_tensor, res_grad)
+
+    def finish(self, y, input_tensor, res_grad=None):
+        """dense bias -> dropout -> + residual -> LayerNorm on the bias-less projection ``y``."""
         return ops.bias_dropout_residual_ln(y, self.dense.bias, input_tensor, self.LayerNorm.weight,
                                             self.LayerNorm.bias, self.LayerNorm.variance_epsilon,
                                             self.dropout.p, self.training, res_grad=res_grad)
@@ -259,6 +262,11 @@ class BertLayer(nn.Module):
     def forward(self, hidden_states, attention_mask_bias):
         attention_output = self.attention(hidden_states, attention_mask_bias)
         rg = ops.ResidualGrad()     # residual grad of attention_output -> FFN-up dgrad GEMM
+        up = self.intermediate.dense_act
+        if up.act == 'gelu' and ops.ffn_fusable(attention_output, up.weight, up.bias, self.output.dense.weight):
+            # --fp32-gemm bf16x3/x6: the GELU epilogue hands the FFN-down GEMM its bf16 planes
+            y = ops.ffn(attention_output, up.weight, up.bias, self.output.dense.weight, rg)
+            return self.output.finish(y, attention_output, rg)
         return self.output(self.intermediate(attention_output, rg), attention_output, rg)
 
 

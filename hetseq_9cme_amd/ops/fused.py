@@ -426,6 +426,49 @@ def linear(x, W, b=None, res_grad=None):
     return F.linear(x, cast_w(W, x.dtype), cast_w(b, x.dtype))
 
 
+# ----------------------------------------------------------------- FFN block on split planes
+class _FFNSplitFn(torch.autograd.Function):
+    """y2 = gelu(x W1^T + b1) W2^T for ``--fp32-gemm bf16x3/x6`` as one autograd node, so
+    the GELU epilogue writes the FFN-down GEMM's bf16 input planes directly and the GELU
+    backward writes the FFN-up gradient's planes (+ dbias) directly: no fp32 [T, 4H]
+    activation / gradient and no separate split pass over either (2 x ~200 MB of HBM
+    traffic per layer at BERT-base phase-1 sizes)."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, mbox):
+        x2 = x.reshape(-1, x.shape[-1])
+        y1, xs = split_gemm.forward(x2, W1)
+        hs = split_gemm.act_planes(y1, b1, 'gelu')
+        y2 = split_gemm.forward_planes(hs, W2)
+        ctx.save_for_backward(xs, y1, hs, W1, b1, W2)
+        ctx.mbox = mbox
+        ctx.xshape = x.shape
+        return y2.view(*x.shape[:-1], y2.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        xs, y1, hs, W1, b1, W2 = ctx.saved_tensors
+        dy2 = dy.reshape(-1, dy.shape[-1])
+        dys = split_gemm.grad_planes(dy2.float())
+        dh = split_gemm.dgrad(dys, W2)
+        dW2 = split_gemm.wgrad(dys, hs, W2.shape[0], W2.shape[1], grad_slot(W2))
+        dy1s, db1 = split_gemm.act_grad_planes(dh, y1, b1, 'gelu', grad_slot(b1))
+        dx = _dgrad_split(dy1s, W1, ctx.xshape, ctx.mbox)
+        dW1 = split_gemm.wgrad(dy1s, xs, W1.shape[0], W1.shape[1], grad_slot(W1))
+        return dx, dW1, db1, dW2, None
+
+
+def ffn_fusable(x, W1, b1, W2):
+    """The split-plane FFN path applies (fp32 GPU activations, --fp32-gemm bf16x3/x6)."""
+    return (split_gemm.active(x) and b1 is not None and W1.shape[0] % 8 == 0 and x.shape[-1] % 8 == 0
+            and not _Side.enabled)
+
+
+def ffn(x, W1, b1, W2, res_grad=None):
+    """gelu(x W1^T + b1) W2^T (the output bias / dropout / residual / LayerNorm follow)."""
+    return _FFNSplitFn.apply(x, W1, b1, W2, res_grad)
+
+
 # ----------------------------------------------------------------- fused Q/K/V projection
 def _adjacent_view(ts):
     """If tensors ``ts`` are laid out back to back in one storage (FlatParamSpace

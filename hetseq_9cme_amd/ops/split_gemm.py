@@ -93,6 +93,27 @@ def forward(x2, W):
     return torch.mm(xs, wq.t(), out_dtype=torch.float32), xs
 
 
+def forward_planes(xs, W):
+    """y = x @ W^T from x's planes (already split, e.g. by a fused producer)."""
+    return torch.mm(xs, planes(W, ORDER_Q[_State.passes]).t(), out_dtype=torch.float32)
+
+
+ACT_IDS = {'gelu': 0, 'tanh': 1, 'relu': 2, 'none': 3}
+
+
+def act_planes(y, b, act):
+    """Planes (order P) of act(y + b): the bias-activation epilogue writes the next GEMM's
+    input pieces directly (csrc/kernels/elementwise.hip ``bias_act_planes_k``)."""
+    n = _State.passes
+    return C().bias_act_planes(y, b, None, ACT_IDS[act], list(ORDER_P[n]), PIECES[n], None)[0]
+
+
+def act_grad_planes(dout, y, b, act, dbias_out=None):
+    """(planes (order Q) of dout * act'(y + b), dbias) in one pass."""
+    n = _State.passes
+    return C().bias_act_planes(y, b, dout, ACT_IDS[act], list(ORDER_Q[n]), PIECES[n], dbias_out)
+
+
 def grad_planes(dy2, dpad=0):
     return planes(dy2, ORDER_Q[_State.passes], dpad=dpad)
 

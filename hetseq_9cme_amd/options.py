@@ -52,11 +52,12 @@ def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialD
     parser.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'],
                         help='compute precision: fp32 (reference parity, exact-f32 MFMA) or '
                              'bf16 (bf16 MFMA, fp32 master weights and optimizer state)')
-    parser.add_argument('--fp32-gemm', default='native', choices=['native', 'bf16x3', 'bf16x6'],
-                        help='how fp32 (--precision fp32) linear-layer GEMMs run: native f32 MFMA '
-                             '(157 TF/s peak), or split into bf16 planes on the 16x faster bf16 MFMA: '
-                             'bf16x6 (fp32-exact class) or bf16x3 (~2^-17 per product); see '
-                             'ops/split_gemm.py')
+    parser.add_argument('--fp32-gemm', default='bf16x6', choices=['native', 'bf16x3', 'bf16x6'],
+                        help='how fp32 (--precision fp32) linear-layer GEMMs run on the GPU: bf16x6 (default: '
+                             'operands split into three bf16 pieces, six passes on the 16x faster bf16 MFMA, '
+                             'fp32-exact class -- measured GEMM error within 1.2x of native), bf16x3 (two '
+                             'pieces, three passes, ~2^-17 per product: near-fp32, fastest) or native f32 '
+                             'MFMA (157 TF/s peak); see ops/split_gemm.py')
     parser.add_argument('--fused-kernels', default=True, type=eval_bool_arg,
                         help='use the hand-written HIP kernels on GPU (True) or plain torch ops')
     parser.add_argument('--user-module', default=None, metavar='PATH',

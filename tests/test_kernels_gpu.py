@@ -381,7 +381,8 @@ def test_training_gpu_matches_cpu(dev, tmp_path):
         cmd = [sys.executable, '-m', 'hetseq_9cme_amd.train', '--task', 'bert', '--data', str(d), '--dict', vocab,
                '--config_file', cfg, '--max-sentences', '8', '--fast-stat-sync', '--max-update', '3',
                '--disable-validation', '--num-workers', '1', '--lr', '1e-3', '--weight-decay', '0.01',
-               '--clip-norm', '0.5', '--save-dir', save, '--distributed-world-size', '1'] + extra
+               '--clip-norm', '0.5', '--save-dir', save, '--distributed-world-size', '1',
+               '--fp32-gemm', 'native'] + extra
         env = dict(os.environ, PYTHONPATH=root)
         r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, timeout=300)
         assert r.returncode == 0, r.stdout[-3000:]

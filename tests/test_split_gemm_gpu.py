@@ -183,3 +183,32 @@ def test_decoder_xent_split(dev, mode, tol):
     for got, r in ((h.grad, hd.grad), (W.grad, Wd.grad), (b.grad, bd.grad)):
         e = (got.double() - r).abs().max().item() / r.abs().max().item()
         assert e < 50 * tol, (mode, e)
+
+
+@pytest.mark.parametrize('mode,tol', [('bf16x3', 8e-6), ('bf16x6', 3e-6)])
+def test_ffn_split_block(dev, mode, tol):
+    """FFN block as one node (GELU epilogue writes the FFN-down planes, GELU backward the
+    FFN-up gradient planes + dbias) against an fp64 autograd reference."""
+    from hetseq_9cme_amd import ops
+    g = torch.Generator(device='cpu').manual_seed(13)
+    T, H, I = 384, 256, 1024
+    x = torch.randn(T, H, generator=g).to(dev).requires_grad_(True)
+    W1 = (torch.randn(I, H, generator=g) * 0.05).to(dev).requires_grad_(True)
+    b1 = (torch.randn(I, generator=g) * 0.1).to(dev).requires_grad_(True)
+    W2 = (torch.randn(H, I, generator=g) * 0.05).to(dev).requires_grad_(True)
+    dy = torch.randn(T, H, generator=g).to(dev)
+    try:
+        ops.set_fp32_gemm(mode)
+        assert ops.ffn_fusable(x, W1, b1, W2)
+        y = ops.ffn(x, W1, b1, W2)
+        y.backward(dy)
+    finally:
+        ops.set_fp32_gemm('native')
+    ps = [t.detach().double().requires_grad_(True) for t in (x, W1, b1, W2)]
+    ref = ops.gelu_ref(ps[0] @ ps[1].t() + ps[2]) @ ps[3].t()
+    ref.backward(dy.double())
+    e = (y.double() - ref).abs().max().item() / ref.abs().max().item()
+    assert e < tol, ('y', e)
+    for name, got, r in zip(('x', 'W1', 'b1', 'W2'), (x.grad, W1.grad, b1.grad, W2.grad), ps):
+        e = (got.double() - r.grad).abs().max().item() / r.grad.abs().max().item()
+        assert e < tol, (name, e)

@@ -460,6 +460,48 @@ std::vector<Tensor> bias_act_planes(Tensor y, OptT b, OptT dout, int64_t act, st
   return {planes, dbias};
 }
 
+// ------------------------------------------------------------------ piece GEMMs
+std::vector<Tensor> split_weight(Tensor W, int64_t npieces) {
+  check_f32(W, "split_weight input");
+  TORCH_CHECK(W.dim() == 2 && W.size(0) % 64 == 0 && W.size(1) % 64 == 0 && aligned16(W.data_ptr()),
+              "split_weight: W must be [N, K] with N, K multiples of 64");
+  TORCH_CHECK(npieces == 2 || npieces == 3, "split_weight: 2 or 3 pieces");
+  const int64_t N = W.size(0), K = W.size(1);
+  auto bf = W.options().dtype(torch::kBFloat16);
+  Tensor wf = torch::empty({N, npieces * K}, bf), wt = torch::empty({K, npieces * N}, bf);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(W.device());
+  hx_split_weight(W.data_ptr<float>(), (int)N, (int)K, (int)npieces, reinterpret_cast<uint16_t*>(wf.data_ptr()),
+                  reinterpret_cast<uint16_t*>(wt.data_ptr()), cur_stream(W));
+  return {wf, wt};
+}
+
+// a: [M, npc * K] pieces (piece p at column p * K), b: [N, npc * K]; out [M, N] fp32 (+= if beta)
+bool gemm_split_ok(const Tensor& a, const Tensor& b, int64_t npc) {
+  if (!a.is_cuda() || a.scalar_type() != torch::kBFloat16 || b.scalar_type() != torch::kBFloat16) return false;
+  if (a.dim() != 2 || b.dim() != 2 || !a.is_contiguous() || !b.is_contiguous()) return false;
+  if (a.size(1) != b.size(1) || a.size(1) % npc) return false;
+  const int64_t K = a.size(1) / npc;
+  return K % 32 == 0 && b.size(0) % 128 == 0 && aligned16(a.data_ptr()) && aligned16(b.data_ptr()) &&
+         a.size(0) < (1LL << 31) && b.size(0) * a.size(1) * 2 < (1LL << 31) && 256 * a.size(1) * 2 < (1LL << 31);
+}
+Tensor gemm_split(Tensor a, Tensor b, int64_t passes, OptT out_, bool beta) {
+  const int64_t npc = passes == 6 ? 3 : 2;
+  TORCH_CHECK(passes == 3 || passes == 6, "gemm_split: passes must be 3 or 6");
+  TORCH_CHECK(gemm_split_ok(a, b, npc), "gemm_split: unsupported operands");
+  const int64_t M = a.size(0), N = b.size(0), K = a.size(1) / npc;
+  Tensor out = has(out_) ? *out_ : torch::empty({M, N}, a.options().dtype(torch::kFloat32));
+  TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.dim() == 2 && out.size(0) == M && out.size(1) == N &&
+                  out.stride(1) == 1,
+              "gemm_split: out must be fp32 [M, N] with unit column stride");
+  TORCH_CHECK(!beta || has(out_), "gemm_split: beta needs an output to accumulate into");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  TORCH_CHECK(hx_gemm_split_nt(a.data_ptr(), npc * K, K, b.data_ptr(), npc * K, K, out.data_ptr<float>(), out.stride(0),
+                               (int)M, (int)N, (int)K, (int)passes, beta ? 1 : 0, cur_stream(a)) == 0,
+              "gemm_split: launch failed");
+  dbg_finite(out, "gemm_split");
+  return out;
+}
+
 // ------------------------------------------------------------------ split planes
 Tensor split_planes(Tensor x, std::vector<int64_t> order, int64_t npieces, bool stacked, int64_t rpad,
                     int64_t dpad) {
@@ -554,6 +596,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_bf16", &wgrad_bf16);
   m.def("wgrad_bf16_ok", &wgrad_bf16_ok);
   m.def("split_planes", &split_planes);
+  m.def("split_weight", &split_weight);
+  m.def("gemm_split", &gemm_split);
+  m.def("gemm_split_ok", &gemm_split_ok);
   m.def("bias_act_planes", &bias_act_planes);
   m.def("wgrad_split", &wgrad_split);
   m.def("wgrad_split_ok", &wgrad_split_ok);

@@ -78,6 +78,16 @@ void hx_bias_act_planes(int act, const float* y, const float* b, const float* do
                         float* partial, float* dbias, int64_t rows, int N, int npieces, int npl, uint32_t order,
                         hipStream_t s);
 
+// split.hip -- weight pieces in both GEMM layouts: wf [N][npieces][K], wt [K][npieces][N];
+// W fp32 [N][K] contiguous, N and K multiples of 64.
+void hx_split_weight(const float* W, int N, int K, int npieces, uint16_t* wf, uint16_t* wt, hipStream_t s);
+
+// gemm_split.hip -- C[M][N] (+)= sum over piece pairs A_a[M][K] . B_b[N][K]^T (bf16 pieces of fp32
+// operands: piece p of row r at X + r * ldx + p * x_ps); passes 3 or 6; N % 128 == 0, K % 32 == 0.
+// Returns -1 for an unsupported shape.
+int hx_gemm_split_nt(const void* A, int64_t lda, int64_t a_ps, const void* B, int64_t ldb, int64_t b_ps, float* C,
+                     int64_t ldc, int M, int N, int K, int passes, int beta, hipStream_t s);
+
 // split.hip -- fp32 -> bf16 planes (piece order[j] = (order >> 4j) & 15) for bf16-MFMA
 // emulation of fp32 GEMMs; interleaved [R][npl][D] or stacked [npl][R][D].
 // Output rows padded to Rp (stacked) / columns to Dp with zeros.

@@ -93,6 +93,49 @@ __global__ __launch_bounds__(256) void split_planes_any_k(const float* __restric
   }
 }
 
+// Weight pieces in both layouts the split GEMMs read (ops/split_gemm.py), one pass over W:
+//   wf[n][p][k] = piece p of W[n][k]   (forward: B operand of y = x W^T)
+//   wt[k][p][n] = piece p of W[n][k]   (data gradient: B operand of dx = dy W = dy (W^T)^T)
+// 64 x 64 tiles: coalesced float4 reads, wf written directly, wt through an LDS transpose.
+template <int NPC>
+__global__ __launch_bounds__(256) void split_weight_k(const float* __restrict__ W, int N, int K,
+                                                     uint16_t* __restrict__ wf, uint16_t* __restrict__ wt) {
+  __shared__ uint16_t tile[NPC][64][66];
+  const int k0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+  const int t = threadIdx.x, c4 = (t & 15) * 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (t >> 4) + 16 * i;
+    const float4 v = *reinterpret_cast<const float4*>(W + (int64_t)(n0 + r) * K + k0 + c4);
+    float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int p = 0; p < NPC; ++p) {
+      uint16_t q[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        q[j] = hx::f2bf(e[j]);
+        e[j] -= hx::bf2f(q[j]);
+        tile[p][r][c4 + j] = q[j];
+      }
+      uint2 packed = make_uint2(q[0] | ((uint32_t)q[1] << 16), q[2] | ((uint32_t)q[3] << 16));
+      *reinterpret_cast<uint2*>(wf + ((int64_t)(n0 + r) * NPC + p) * K + k0 + c4) = packed;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int kk = (t >> 4) + 16 * i;   // row of wt inside the tile
+#pragma unroll
+    for (int p = 0; p < NPC; ++p) {
+      uint16_t q[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) q[j] = tile[p][c4 + j][kk];
+      uint2 packed = make_uint2(q[0] | ((uint32_t)q[1] << 16), q[2] | ((uint32_t)q[3] << 16));
+      *reinterpret_cast<uint2*>(wt + ((int64_t)(k0 + kk) * NPC + p) * N + n0 + c4) = packed;
+    }
+  }
+}
+
 }  // namespace
 
 void hx_split_planes(const float* x, int64_t ldx, uint16_t* out, int64_t R, int D, int64_t Rp, int Dp,
@@ -115,4 +158,12 @@ void hx_split_planes(const float* x, int64_t ldx, uint16_t* out, int64_t R, int 
     split_planes_any_k<3><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, Rp, Dp, npl, order, stacked);
   else
     split_planes_any_k<2><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, Rp, Dp, npl, order, stacked);
+}
+
+void hx_split_weight(const float* W, int N, int K, int npieces, uint16_t* wf, uint16_t* wt, hipStream_t s) {
+  dim3 g(K / 64, N / 64);
+  if (npieces == 3)
+    split_weight_k<3><<<g, 256, 0, s>>>(W, N, K, wf, wt);
+  else
+    split_weight_k<2><<<g, 256, 0, s>>>(W, N, K, wf, wt);
 }

@@ -101,6 +101,18 @@ def _dgrad(dy2, W, xshape, mbox):
     return dx if other is None else dx + other.view(xshape).to(dx.dtype)
 
 
+def _dgrad_pieces(dys, wt, xshape, mbox):
+    """``_dgrad`` from dy's pieces and W^T's pieces (hand-written piece GEMM, beta = 1 into
+    the deposited residual gradient)."""
+    if mbox is not None:
+        g, other = mbox.take(torch.float32)
+        if g is not None:
+            return split_gemm.dgrad_pieces(dys, wt, acc=g.view(-1, wt.shape[0])).view(xshape)
+        dx = split_gemm.dgrad_pieces(dys, wt).view(xshape)
+        return dx if other is None else dx + other.view(xshape).to(dx.dtype)
+    return split_gemm.dgrad_pieces(dys, wt).view(xshape)
+
+
 def _dgrad_split(dys, W, xshape, mbox):
     """``_dgrad`` on the bf16 split planes of dy (``--fp32-gemm bf16x3/x6``)."""
     if mbox is not None:
@@ -373,14 +385,23 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, W, b, mbox):
         x2 = x.reshape(-1, x.shape[-1])
         ctx.split = split_gemm.active(x2)
-        if ctx.split:     # fp32 on bf16 matrix cores; the backward reuses the x planes
+        ctx.pieces = ctx.split and split_gemm.nt_ok(W.shape[1], W.shape[0])
+        Wsave = W
+        if ctx.pieces:    # fp32 on bf16 matrix cores, hand-written piece GEMMs
+            x2 = split_gemm.pieces(x2)
+            wf, Wsave = split_gemm.weight_pieces(W)
+            y = split_gemm.gemm(x2, wf)
+            if b is not None:
+                y.add_(b)
+        elif ctx.split:   # library GEMMs on pass-stacked planes
             y, x2 = split_gemm.forward(x2, W)
             if b is not None:
                 y.add_(b)
         else:
             Wc = cast_w(W, x.dtype)
             y = torch.mm(x2, Wc.t()) if b is None else torch.addmm(cast_w(b, x.dtype), x2, Wc.t())
-        ctx.save_for_backward(x2, W)
+        ctx.save_for_backward(x2, Wsave)
+        ctx.W = W
         ctx.b = b
         ctx.mbox = mbox
         ctx.xshape = x.shape
@@ -388,12 +409,18 @@ class _LinearFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x2, W = ctx.saved_tensors
+        x2, Wsaved = ctx.saved_tensors
+        W = ctx.W
         b = ctx.b
         dy2 = dy.reshape(-1, dy.shape[-1])
-        dys = split_gemm.grad_planes(dy2.float()) if ctx.split else None
+        if ctx.pieces:
+            dys = split_gemm.pieces(dy2.float())
+        else:
+            dys = split_gemm.grad_planes(dy2.float()) if ctx.split else None
         if not ctx.needs_input_grad[0]:
             dx = None
+        elif ctx.pieces:
+            dx = _dgrad_pieces(dys, Wsaved, ctx.xshape, ctx.mbox)
         elif ctx.split:
             dx = _dgrad_split(dys, W, ctx.xshape, ctx.mbox)
         else:
@@ -402,8 +429,12 @@ class _LinearFn(torch.autograd.Function):
         direct = slot is not None
         side = side_begin(dy2.device) if direct else None
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            dW = (split_gemm.wgrad(dys, x2, W.shape[0], W.shape[1], slot) if ctx.split
-                  else _wgrad(dy2, x2, slot))
+            if ctx.pieces:
+                dW = split_gemm.wgrad_pieces(dys, x2, W.shape[0], W.shape[1], slot)
+            elif ctx.split:
+                dW = split_gemm.wgrad(dys, x2, W.shape[0], W.shape[1], slot)
+            else:
+                dW = _wgrad(dy2, x2, slot)
             db = None
             if b is not None:
                 if dy2.shape[-1] % 4 == 0:
@@ -437,18 +468,38 @@ class _FFNSplitFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W1, b1, W2, mbox):
         x2 = x.reshape(-1, x.shape[-1])
-        y1, xs = split_gemm.forward(x2, W1)
-        hs = split_gemm.act_planes(y1, b1, 'gelu')
-        y2 = split_gemm.forward_planes(hs, W2)
-        ctx.save_for_backward(xs, y1, hs, W1, b1, W2)
+        ctx.pieces = split_gemm.nt_ok(W1.shape[1], W1.shape[0]) and split_gemm.nt_ok(W2.shape[1], W2.shape[0])
+        if ctx.pieces:
+            xs = split_gemm.pieces(x2)
+            w1f, w1t = split_gemm.weight_pieces(W1)
+            y1 = split_gemm.gemm(xs, w1f)
+            hs = split_gemm.act_pieces(y1, b1, 'gelu')
+            w2f, w2t = split_gemm.weight_pieces(W2)
+            y2 = split_gemm.gemm(hs, w2f)
+            ctx.save_for_backward(xs, y1, hs, w1t, b1, w2t)
+        else:
+            y1, xs = split_gemm.forward(x2, W1)
+            hs = split_gemm.act_planes(y1, b1, 'gelu')
+            y2 = split_gemm.forward_planes(hs, W2)
+            ctx.save_for_backward(xs, y1, hs, W1, b1, W2)
+        ctx.W = (W1, W2)
         ctx.mbox = mbox
         ctx.xshape = x.shape
         return y2.view(*x.shape[:-1], y2.shape[-1])
 
     @staticmethod
     def backward(ctx, dy):
-        xs, y1, hs, W1, b1, W2 = ctx.saved_tensors
+        xs, y1, hs, w1, b1, w2 = ctx.saved_tensors
+        W1, W2 = ctx.W
         dy2 = dy.reshape(-1, dy.shape[-1])
+        if ctx.pieces:
+            dys = split_gemm.pieces(dy2.float())
+            dh = split_gemm.dgrad_pieces(dys, w2)
+            dW2 = split_gemm.wgrad_pieces(dys, hs, W2.shape[0], W2.shape[1], grad_slot(W2))
+            dy1s, db1 = split_gemm.act_grad_pieces(dh, y1, b1, 'gelu', grad_slot(b1))
+            dx = _dgrad_pieces(dy1s, w1, ctx.xshape, ctx.mbox)
+            dW1 = split_gemm.wgrad_pieces(dy1s, xs, W1.shape[0], W1.shape[1], grad_slot(W1))
+            return dx, dW1, db1, dW2, None
         dys = split_gemm.grad_planes(dy2.float())
         dh = split_gemm.dgrad(dys, W2)
         dW2 = split_gemm.wgrad(dys, hs, W2.shape[0], W2.shape[1], grad_slot(W2))
@@ -511,7 +562,14 @@ class _Linear3Fn(torch.autograd.Function):
             bc = cast_w(b, x.dtype) if has_b else None
         x2 = x.reshape(-1, x.shape[-1])
         ctx.split = split_gemm.active(x2)
-        if ctx.split:     # fp32 on bf16 matrix cores; the backward reuses the x planes
+        ctx.pieces = ctx.split and split_gemm.nt_ok(W.shape[1], W.shape[0])
+        if ctx.pieces:    # fp32 on bf16 matrix cores, hand-written piece GEMMs
+            x2 = split_gemm.pieces(x2)
+            wf, Wc = split_gemm.weight_pieces(W)
+            y = split_gemm.gemm(x2, wf)
+            if has_b:
+                y.add_(b)
+        elif ctx.split:   # library GEMMs on pass-stacked planes
             y, x2 = split_gemm.forward(x2, W)
             if has_b:
                 y.add_(b)
@@ -531,13 +589,20 @@ class _Linear3Fn(torch.autograd.Function):
         x2, W = ctx.saved_tensors
         wq, wk, wv, bq, bk, bv = ctx.params
         dy2 = dy.reshape(-1, dy.shape[-1])
-        dys = split_gemm.grad_planes(dy2.float()) if ctx.split else None
-        if ctx.split:
-            dx = _dgrad_split(dys, W, ctx.xshape, ctx.mbox)
+        if ctx.pieces:
+            n_out = sum(ctx.n)
+            dys = split_gemm.pieces(dy2.float())
+            dx = _dgrad_pieces(dys, W, ctx.xshape, ctx.mbox)     # W holds the W^T pieces here
+            n_in = W.shape[0]
+            wg = lambda slot: split_gemm.wgrad_pieces(dys, x2, n_out, n_in, slot)
         else:
-            dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox)
-        wg = ((lambda slot: split_gemm.wgrad(dys, x2, W.shape[0], W.shape[1], slot)) if ctx.split
-              else (lambda slot: _wgrad(dy2, x2, slot)))
+            dys = split_gemm.grad_planes(dy2.float()) if ctx.split else None
+            if ctx.split:
+                dx = _dgrad_split(dys, W, ctx.xshape, ctx.mbox)
+            else:
+                dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox)
+            wg = ((lambda slot: split_gemm.wgrad(dys, x2, W.shape[0], W.shape[1], slot)) if ctx.split
+                  else (lambda slot: _wgrad(dy2, x2, slot)))
         a, b_, _ = ctx.n
         # weight grads: ONE GEMM straight into the three adjacent flat slots when possible
         ws = [grad_slot(w) for w in (wq, wk, wv)]

@@ -42,6 +42,8 @@ block once and runs all passes from registers (the stacked [nT, D] views would
 stream dY_0 twice / X_0 three times); shapes it does not cover take the stacked
 form through ``wgrad_bf16.hip`` or the library.
 """
+import os
+
 import torch
 
 from ._ext import C, use_kernels
@@ -54,6 +56,7 @@ MODES = {'native': 0, 'bf16x3': 3, 'bf16x6': 6}
 
 class _State(object):
     passes = 0
+    piece_gemm = os.environ.get('HETSEQ_PIECE_GEMM', '0') == '1'   # see nt_ok
     addmm_out_ok = None   # does torch.addmm(bf16, bf16, out_dtype=fp32, out=acc) work in place?
 
 
@@ -132,6 +135,72 @@ def dgrad(dys, W, acc=None, rpad=0):
         except (RuntimeError, TypeError):
             _State.addmm_out_ok = False
     return acc.add_(torch.mm(dys, wb, out_dtype=torch.float32))
+
+
+# ---------------------------------------------------------------- pieces form (hand-written GEMMs)
+# Operands stored as [rows, npc, D]: each DISTINCT piece once (npc = 2 for bf16x3, 3 for
+# bf16x6) -- half the bytes of the pass-stacked planes for bf16x6, the fp32 size for bf16x3.
+# The forward and data-gradient GEMMs run on csrc/kernels/gemm_split.hip (every piece
+# fragment reused by all passes from registers), the weight gradient on wgrad_split.hip.
+
+def npieces():
+    return PIECES[_State.passes]
+
+
+def nt_ok(n_in, n_out):
+    """Use the hand-written piece GEMMs for a linear layer W [n_out, n_in] (fwd: N = n_out,
+    K = n_in; dgrad: N = n_in, K = n_out; weight pieces: 64 x 64 tiles).
+
+    Opt-in (``HETSEQ_PIECE_GEMM=1``): measured on MI355X at BERT-base phase-1 shapes
+    (tools/bench_gemm_split.py) the piece kernel runs at 0.69-0.90 PF/s of bf16 MFMA work
+    against 1.0-1.3 PF/s for hipBLASLt on the pass-stacked planes (split pass included), so
+    the library path is the default; the kernel is kept, tested and benchmarked as the base
+    for a deeper-pipelined version."""
+    return _State.piece_gemm and n_out % 128 == 0 and n_in % 128 == 0
+
+
+def pieces(x2):
+    """[R, npc * D] bf16 pieces of the fp32 matrix ``x2`` [R, D] (piece p at column p * D)."""
+    if x2.stride(-1) != 1:
+        x2 = x2.contiguous()
+    n = npieces()
+    return C().split_planes(x2, list(range(n)), n, False, 0, 0)
+
+
+def weight_pieces(W):
+    """(wf [N, npc * K], wt [K, npc * N]): pieces of W [N, K] and of W^T, one pass."""
+    return C().split_weight(W.contiguous(), npieces())
+
+
+def gemm(a, b, out=None, beta=False):
+    """out (+)= sum over piece pairs of a_p . b_q^T, fp32 [M, N]."""
+    return C().gemm_split(a, b, _State.passes, out, beta)
+
+
+def dgrad_pieces(dys, wt, acc=None):
+    """dy @ W from dy's pieces and W^T's pieces, accumulated into ``acc`` if given."""
+    if acc is None:
+        return gemm(dys, wt)
+    return gemm(dys, wt, out=acc, beta=True)
+
+
+def wgrad_pieces(dys, xs, n_out, n_in, slot):
+    n = npieces()
+    out = slot if slot is not None else torch.empty(n_out, n_in, device=dys.device)
+    return C().wgrad_split(dys, [p * n_out for p in range(n)], xs, [p * n_in for p in range(n)], _State.passes,
+                           n_out, n_in, out)
+
+
+def act_pieces(y, b, act):
+    """Pieces of act(y + b) written by the bias-activation epilogue."""
+    n = npieces()
+    return C().bias_act_planes(y, b, None, ACT_IDS[act], list(range(n)), n, None)[0]
+
+
+def act_grad_pieces(dout, y, b, act, dbias_out=None):
+    """(pieces of dout * act'(y + b), dbias) in one pass."""
+    n = npieces()
+    return C().bias_act_planes(y, b, dout, ACT_IDS[act], list(range(n)), n, dbias_out)
 
 
 def _piece_offsets(order, d):

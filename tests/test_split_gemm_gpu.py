@@ -212,3 +212,36 @@ def test_ffn_split_block(dev, mode, tol):
     for name, got, r in zip(('x', 'W1', 'b1', 'W2'), (x.grad, W1.grad, b1.grad, W2.grad), ps):
         e = (got.double() - r.grad).abs().max().item() / r.grad.abs().max().item()
         assert e < tol, (name, e)
+
+
+@pytest.mark.parametrize('mode,tol', [('bf16x3', 4e-6), ('bf16x6', 1.5e-6)])
+def test_piece_gemm_kernels(dev, mode, tol):
+    """Hand-written piece GEMM (gemm_split.hip, opt-in path) + weight pieces in both layouts
+    (split_weight_k): forward, data gradient with beta = 1, rows that are not a multiple
+    of the 256-row tile."""
+    from hetseq_9cme_amd import ops
+    from hetseq_9cme_amd.ops import split_gemm as sg
+    g = torch.Generator(device='cpu').manual_seed(21)
+    T, n_in, n_out = 300, 256, 384
+    x = torch.randn(T, n_in, generator=g).to(dev)
+    W = torch.randn(n_out, n_in, generator=g).to(dev)
+    dy = torch.randn(T, n_out, generator=g).to(dev)
+    acc0 = torch.randn(T, n_in, generator=g).to(dev)
+    try:
+        ops.set_fp32_gemm(mode)
+        wf, wt = sg.weight_pieces(W)
+        pw = sg.pieces(W)
+        assert torch.equal(wf.view(torch.int16), pw.view(torch.int16))
+        pwt = sg.pieces(W.t().contiguous())
+        assert torch.equal(wt.view(torch.int16), pwt.view(torch.int16))
+        y = sg.gemm(sg.pieces(x), wf)
+        acc = acc0.clone()
+        sg.dgrad_pieces(sg.pieces(dy), wt, acc=acc)
+    finally:
+        ops.set_fp32_gemm('native')
+    xd, Wd, dyd = x.double(), W.double(), dy.double()
+    e = ((y.double() - xd @ Wd.t()).abs() / (xd.abs() @ Wd.abs().t())).max().item()
+    assert e < tol, ('fwd', e)
+    ref = acc0.double() + dyd @ Wd
+    e = ((acc.double() - ref).abs() / (acc0.double().abs() + dyd.abs() @ Wd.abs())).max().item()
+    assert e < tol, ('dgrad', e)

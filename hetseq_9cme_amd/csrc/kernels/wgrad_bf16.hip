@@ -37,10 +37,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
-#ifndef HX_WGRAD_BK
-#define HX_WGRAD_BK 64
-#endif
-constexpr int BK = HX_WGRAD_BK;   // tokens per pipeline step (BK / 16 MFMA k-steps per barrier)
+// BK = tokens per pipeline step (BK / 16 MFMA k-steps per barrier): a template parameter,
+// 32 or 64 per tile configuration (see the cfg table at the bottom)
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
@@ -84,7 +82,7 @@ __device__ __forceinline__ bf16x8 frag(const char* tile, const int (&lo)[2], con
   return *reinterpret_cast<const bf16x8*>(v);
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int BK>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_bf16_k(
     const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ B, int ldb, float* __restrict__ out,
     int M, int N, int T, int kchunk, int nsplit) {
@@ -222,7 +220,7 @@ __global__ __launch_bounds__(256) void split_sum_k(const float4* __restrict__ ws
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int BK>
 void launch(const uint16_t* A, int lda, const uint16_t* B, int ldb, float* out, float* ws, int M, int N, int T,
             int nsplit, hipStream_t s) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
@@ -233,11 +231,11 @@ void launch(const uint16_t* A, int lda, const uint16_t* B, int ldb, float* out, 
   const size_t smem = 2 * BK * (BM + BN) * sizeof(uint16_t);
   static bool attr = false;
   if (!attr) {   // > 64 KiB of dynamic LDS needs the opt-in (160 KiB per CU on gfx950)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_bf16_k<BM, BN, WM, WN>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_bf16_k<BM, BN, WM, WN, BK>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
-  wgrad_bf16_k<BM, BN, WM, WN><<<8 * per, NT, smem, s>>>(A, lda, B, ldb, nsplit > 1 ? ws : out, M, N, T, kchunk,
+  wgrad_bf16_k<BM, BN, WM, WN, BK><<<8 * per, NT, smem, s>>>(A, lda, B, ldb, nsplit > 1 ? ws : out, M, N, T, kchunk,
                                                       nsplit);
   if (nsplit > 1) {
     const int64_t n4 = (int64_t)M * N / 4;
@@ -249,33 +247,35 @@ void launch(const uint16_t* A, int lda, const uint16_t* B, int ldb, float* out, 
 
 }  // namespace
 
-// Tile configurations (cfg index -> BM x BN workgroup tile, WM x WN per wave):
-//   0: 128x128, 4 waves of 64x64      1: 256x128, 8 waves of 64x64
-//   2: 256x256, 8 waves of 128x64     3: 256x128, 4 waves of 128x64
-//   4: 256x256, 4 waves of 128x128 (accumulators in AGPRs)
-// A wave's LDS fragment traffic per MFMA falls with its tile (64x64: 1 fragment per MFMA,
-// 128x64: 0.75, 128x128: 0.5); the workgroup tile sets the L2 traffic per FLOP.
+// Tile configurations (cfg index -> BM x BN workgroup tile, waves of 64 x 64, BK tokens per step):
+//   0: 128x128, 4 waves, BK 32      1: 256x128, 8 waves, BK 32
+//   2: 256x128, 8 waves, BK 64      3: 128x128, 4 waves, BK 64
+// (128-wide wave tiles spill at this staging depth: 20-100 TF/s, dropped.)
 // HX_WGRAD_CFG="cfg:nsplit" overrides the plan (tuning sweeps: tools/bench_wgrad.py --sweep).
-static const int kTileM[5] = {128, 256, 256, 256, 256};
-static const int kTileN[5] = {128, 128, 256, 128, 256};
+static const int kTileM[4] = {128, 256, 256, 128};
+static const int kTileN[4] = {128, 128, 128, 128};
+static const int kBK[4] = {32, 32, 64, 64};
 
 void hx_wgrad_bf16_plan(int M, int N, int T, int* cfg, int* nsplit) {
   // One wave of workgroups: the 8-wave 256x128 kernel runs one workgroup per CU (256 slots),
   // the 4-wave 128x128 one two (512 slots).  The split count fills the slots without
   // spilling into a second, mostly empty round (measured on MI355X, T = 16384: FFN dW
   // 3 splits -> 216 workgroups 99 us vs 7 splits -> 504 workgroups 119 us;
-  // tools/bench_wgrad.py --sweep).
-  int c = (M % 256 == 0 && N % 128 == 0) ? 1 : 0;
-  const int slots = c == 1 ? 256 : 512;
+  // tools/bench_wgrad.py --sweep).  The 256 x 128 tile takes the 64-token step (half the
+  // barriers: FFN dW 98 -> 96 us, QKV 82 -> 79 us at T = 16384, +5-8 % on the pass-stacked
+  // rows of the split fp32 path); the 128 x 128 one only on long token ranges.
+  const bool big = M % 256 == 0 && N % 128 == 0;
+  int c = big ? 2 : (T >= 32768 ? 3 : 0);
+  const int slots = (c == 1 || c == 2) ? 256 : 512;
   const int tiles0 = (M / kTileM[c]) * (N / kTileN[c]);
   int s = std::max(1, slots / std::max(1, tiles0));
   s = std::min(s, std::max(1, T / 256));   // at least 256 tokens per split
   if (const char* e = getenv("HX_WGRAD_CFG")) {
     int ec = -1, es = -1;
-    if (sscanf(e, "%d:%d", &ec, &es) == 2 && ec >= 0 && ec < 5 && es >= 1 && M % kTileM[ec] == 0 &&
+    if (sscanf(e, "%d:%d", &ec, &es) == 2 && ec >= 0 && ec < 4 && es >= 1 && M % kTileM[ec] == 0 &&
         N % kTileN[ec] == 0) {
       c = ec;
-      s = std::min(es, std::max(1, T / BK));
+      s = std::min(es, std::max(1, T / kBK[ec]));
     }
   }
   *cfg = c;
@@ -286,10 +286,9 @@ void hx_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, float* out, 
                    int cfg, int nsplit, hipStream_t s) {
   const uint16_t *a = (const uint16_t*)dy, *b = (const uint16_t*)x;
   switch (cfg) {
-    case 1: launch<256, 128, 64, 64>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
-    case 2: launch<256, 256, 128, 64>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
-    case 3: launch<256, 128, 128, 64>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
-    case 4: launch<256, 256, 128, 128>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
-    default: launch<128, 128, 64, 64>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
+    case 1: launch<256, 128, 64, 64, 32>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
+    case 2: launch<256, 128, 64, 64, 64>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
+    case 3: launch<128, 128, 64, 64, 64>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
+    default: launch<128, 128, 64, 64, 32>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
   }
 }

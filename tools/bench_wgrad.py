@@ -79,7 +79,7 @@ def main():
 
 def sweep(T):
     from hetseq_9cme_amd.ops._ext import C
-    tiles = {0: (128, 128), 1: (256, 128), 3: (256, 128), 2: (256, 256), 4: (256, 256)}
+    tiles = {0: (128, 128), 1: (256, 128), 2: (256, 128), 3: (128, 128)}
     if os.environ.get("HX_SWEEP_CFGS"):
         tiles = {int(c): tiles[int(c)] for c in os.environ["HX_SWEEP_CFGS"].split(",")}
     for (n_out, n_in) in [(3072, 768), (768, 3072), (2304, 768), (768, 768)]:

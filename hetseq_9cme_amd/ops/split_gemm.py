@@ -54,6 +54,14 @@ ORDER_Q = {3: (0, 0, 1), 6: (0, 0, 1, 0, 1, 2)}
 MODES = {'native': 0, 'bf16x3': 3, 'bf16x6': 6}
 
 
+# Below this many rows (tokens of the GEMM's M side) the split GEMMs lose to native f32
+# MFMA (smaller grids, split overhead): BERT-base at 32 x 128 tokens ran 22.6 ms/step with
+# bf16x6 everywhere vs 21.2 ms native.  Both are fp32-exact class, so small GEMMs (MLM
+# head on the masked rows, pooler, small batches) simply stay native.
+MIN_ROWS = {3: int(os.environ.get('HETSEQ_SPLIT_MIN_ROWS_X3', '2048')),
+            6: int(os.environ.get('HETSEQ_SPLIT_MIN_ROWS_X6', '8192'))}
+
+
 class _State(object):
     passes = 0
     piece_gemm = os.environ.get('HETSEQ_PIECE_GEMM', '0') == '1'   # see nt_ok
@@ -72,8 +80,10 @@ def fp32_gemm_mode():
 
 
 def active(x):
-    """Split emulation applies to fp32 GPU operands when a split mode is set."""
-    return _State.passes > 0 and x.dtype == torch.float32 and use_kernels(x)
+    """Split emulation applies to fp32 GPU operands [rows, features] with at least
+    ``MIN_ROWS`` rows when a split mode is set."""
+    return (_State.passes > 0 and x.dtype == torch.float32 and use_kernels(x)
+            and x.numel() >= MIN_ROWS[_State.passes] * x.shape[-1])
 
 
 def passes():

@@ -89,8 +89,6 @@ class Controller(object):
         self.fast_stat_sync = args.fast_stat_sync
         self._save_thread = None
         self._transport_monitor = TransportErrorMonitor(lag=2)
-        self._max_inflight = int(os.environ.get('HETSEQ_MAX_INFLIGHT', '0'))
-        self._inflight = []
         self._profile_phases = bool(getattr(args, 'profile_phases', False))
         self.phases = PhaseTimer(self._profile_phases, cuda=self.cuda)
         self.init_meters(args)
@@ -227,12 +225,6 @@ class Controller(object):
         ph = self.phases.begin
         ph('prep')
         self._transport_monitor.check()   # xGMI timeouts of update n-2, on every rank alike
-        if self._max_inflight > 0 and self.cuda:
-            ev = torch.cuda.Event()
-            ev.record()
-            self._inflight.append(ev)
-            if len(self._inflight) > self._max_inflight:
-                self._inflight.pop(0).synchronize()
         self._set_seed()
         model = self.model
         model.train()

@@ -83,8 +83,7 @@ class BatchReaderLoader(object):
         self.num_workers = max(1, num_workers)
         self.prefetch = max(1, prefetch)
         self.device = torch.device(device) if device is not None else None
-        self.stage = (self.device is not None and self.device.type == 'cuda'
-                      and os.environ.get('HETSEQ_COPY_STREAM', '1') == '1')
+        self.stage = self.device is not None and self.device.type == 'cuda'
         self.pin_memory = pin_memory or self.stage
 
     def __len__(self):

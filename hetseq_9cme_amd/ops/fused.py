@@ -658,7 +658,7 @@ def attention(qkv, mask_bias, num_heads, p, training, bias=None):
 class _DecoderXentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, W, bias, labels):
-        ctx.split = split_gemm.active(h)
+        ctx.split = split_gemm.active(h, W.shape[0])
         if ctx.split:    # fp32 on bf16 matrix cores (--fp32-gemm)
             logits, _ = split_gemm.forward(h, W)
         else:

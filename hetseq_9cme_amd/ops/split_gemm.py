@@ -79,11 +79,14 @@ def fp32_gemm_mode():
     return {v: k for k, v in MODES.items()}[_State.passes]
 
 
-def active(x):
-    """Split emulation applies to fp32 GPU operands [rows, features] with at least
-    ``MIN_ROWS`` rows when a split mode is set."""
-    return (_State.passes > 0 and x.dtype == torch.float32 and use_kernels(x)
-            and x.numel() >= MIN_ROWS[_State.passes] * x.shape[-1])
+def active(x, n_out=None):
+    """Split emulation applies to fp32 GPU operands [rows, features] when a split mode is
+    set and the GEMM is big enough to fill the chip on the bf16 path: at least
+    ``MIN_ROWS`` rows, or a wide output (``n_out`` >= 8192, the MLM decoder's vocabulary)."""
+    if not (_State.passes > 0 and x.dtype == torch.float32 and use_kernels(x)):
+        return False
+    rows = x.numel() // max(1, x.shape[-1])
+    return rows >= MIN_ROWS[_State.passes] or (n_out is not None and n_out >= 8192 and rows >= 256)
 
 
 def passes():

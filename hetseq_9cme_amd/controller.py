@@ -41,7 +41,7 @@ from .parallel.flat_params import FlatParamSpace
 from .parallel.reducer import GradReducer, TransportErrorMonitor
 from .utils.meters import AverageMeter, StopwatchMeter, TimeMeter
 from .utils.phase_timer import PhaseTimer
-from .utils.misc import move_to_device
+from .utils.misc import ensure_train, move_to_device
 
 LN2 = math.log(2)
 
@@ -227,7 +227,7 @@ class Controller(object):
         self._transport_monitor.check()   # xGMI timeouts of update n-2, on every rank alike
         self._set_seed()
         model = self.model
-        model.train()
+        ensure_train(model)
         self.zero_grad()
         if not dummy_batch:
             self.meters['train_wall'].start()

@@ -15,6 +15,7 @@ import collections
 import torch
 
 from ..data import data_utils, iterators
+from ..utils.misc import ensure_train
 
 
 class Task(object):
@@ -77,7 +78,7 @@ class Task(object):
         return len(sample[0][0])
 
     def train_step(self, sample, model, optimizer, ignore_grad=False):
-        model.train()
+        ensure_train(model)
         loss = model(*sample)
         if ignore_grad:
             loss = loss * 0

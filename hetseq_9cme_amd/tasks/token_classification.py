@@ -20,6 +20,7 @@ import torch
 from ..data.collators import DataCollatorForTokenClassification
 from ..data.ner_dataset import BertNerDataset, get_label_list, load_split, tokenize_and_align
 from .base import Task
+from ..utils.misc import ensure_train
 
 SPLIT_ALIASES = {'train': 'train', 'valid': 'validation', 'validation': 'validation', 'test': 'test'}
 
@@ -118,7 +119,7 @@ class BertForTokenClassificationTask(Task):
         print('| loading finished')
 
     def train_step(self, sample, model, optimizer, ignore_grad=False):
-        model.train()
+        ensure_train(model)
         loss = model(**sample)
         if ignore_grad:
             loss = loss * 0

@@ -8,6 +8,7 @@ fused HIP kernels); use ``BertForTokenClassificationTask`` for the fast path.
 """
 
 from .token_classification import BertForTokenClassificationTask, safe_load_checkpoint
+from ..utils.misc import ensure_train
 
 
 class TransformersBertForTokenClassificationTask(BertForTokenClassificationTask):
@@ -25,7 +26,7 @@ class TransformersBertForTokenClassificationTask(BertForTokenClassificationTask)
         return model
 
     def train_step(self, sample, model, optimizer, ignore_grad=False):
-        model.train()
+        ensure_train(model)
         loss = model(**sample)['loss']
         if ignore_grad:
             loss = loss * 0

@@ -26,6 +26,9 @@ def main():
     ap.add_argument('--batch', type=int, default=32)
     ap.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'])
     ap.add_argument('--profile-phases', action='store_true', help='host/device time per step phase (stderr)')
+    ap.add_argument('--gemm-tuning', default='table', choices=['off', 'table'])
+    ap.add_argument('--cprofile', default=None, metavar='OUT',
+                    help='after the timed steps, cProfile 20 more steps and write the top host functions to OUT')
     a = ap.parse_args()
     from hetseq_9cme_amd import options, tasks
     from hetseq_9cme_amd.controller import Controller
@@ -35,12 +38,13 @@ def main():
     d = tempfile.mkdtemp(prefix='hx_ner_')
     vocab = write_vocab(os.path.join(d, 'vocab.txt'), 30522, extra_words=WORDS)
     cfg = write_bert_config(os.path.join(d, 'bert_base.json'), **BERT_BASE)
-    n = (a.steps + a.warmup + 2) * a.batch
+    n = (a.steps + a.warmup + 22) * a.batch
     tr = write_synthetic_conll(os.path.join(d, 'train.txt'), n, seed=0, min_len=8, max_len=40)
     argv = ['--task', 'BertForTokenClassification', '--optimizer', 'adam', '--fast-stat-sync', '--lr', '5e-5',
             '--dict', vocab, '--config_file', cfg, '--train_file', tr, '--extension_file', 'conll',
             '--max-sentences', str(a.batch), '--num-workers', '2', '--find-unused-parameters',
-            '--disable-validation', '--no-save', '--log-format', 'none', '--precision', a.precision]
+            '--disable-validation', '--no-save', '--log-format', 'none', '--precision', a.precision,
+            '--gemm-tuning', a.gemm_tuning]
     if a.profile_phases:
         argv.append('--profile-phases')
     args = options.parse_training_args(argv)
@@ -62,6 +66,20 @@ def main():
         ctrl.train_step(next(itr))
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
+    if a.cprofile:
+        import cProfile
+        import io
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(20):
+            ctrl.train_step(next(itr))
+        torch.cuda.synchronize()
+        pr.disable()
+        buf = io.StringIO()
+        pstats.Stats(pr, stream=buf).sort_stats('tottime').print_stats(40)
+        with open(a.cprofile, 'w') as f:
+            f.write(buf.getvalue())
     if a.profile_phases:
         rep = ctrl.phase_report()
         for kind in ('host', 'device'):

@@ -502,17 +502,29 @@ class _FFNSplitFn(torch.autograd.Function):
             return dx, dW1, db1, dW2, None
         dys = split_gemm.grad_planes(dy2.float())
         dh = split_gemm.dgrad(dys, W2)
-        dW2 = split_gemm.wgrad(dys, hs, W2.shape[0], W2.shape[1], grad_slot(W2))
+        slot2, slot1 = grad_slot(W2), grad_slot(W1)
+        # --overlap-wgrad: the two weight-gradient GEMMs run on the side stream, beside the
+        # memory-bound GELU backward / plane writes of the dgrad chain
+        side = side_begin(dy2.device) if slot2 is not None else None
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            dW2 = split_gemm.wgrad(dys, hs, W2.shape[0], W2.shape[1], slot2)
+        if side is not None:
+            dys.record_stream(side)
+            hs.record_stream(side)
         dy1s, db1 = split_gemm.act_grad_planes(dh, y1, b1, 'gelu', grad_slot(b1))
         dx = _dgrad_split(dy1s, W1, ctx.xshape, ctx.mbox)
-        dW1 = split_gemm.wgrad(dy1s, xs, W1.shape[0], W1.shape[1], grad_slot(W1))
+        side = side_begin(dy2.device) if slot1 is not None else None
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            dW1 = split_gemm.wgrad(dy1s, xs, W1.shape[0], W1.shape[1], slot1)
+        if side is not None:
+            dy1s.record_stream(side)
+            xs.record_stream(side)
         return dx, dW1, db1, dW2, None
 
 
 def ffn_fusable(x, W1, b1, W2):
     """The split-plane FFN path applies (fp32 GPU activations, --fp32-gemm bf16x3/x6)."""
-    return (split_gemm.active(x) and b1 is not None and W1.shape[0] % 8 == 0 and x.shape[-1] % 8 == 0
-            and not _Side.enabled)
+    return split_gemm.active(x) and b1 is not None and W1.shape[0] % 8 == 0 and x.shape[-1] % 8 == 0
 
 
 def ffn(x, W1, b1, W2, res_grad=None):

@@ -19,6 +19,13 @@ inline void check_cuda(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
 }
+// Per-update dropout key: a 1-element int64 tensor on the kernel's device, read by the
+// kernels themselves (ops/rng.py keeps it; graph-captured steps replay with new keys).
+inline const uint64_t* seed_ptr(const Tensor& seed) {
+  TORCH_CHECK(seed.is_cuda() && seed.scalar_type() == torch::kInt64 && seed.numel() >= 1,
+              "dropout seed must be a 1-element int64 GPU tensor");
+  return reinterpret_cast<const uint64_t*>(seed.data_ptr<int64_t>());
+}
 inline int act_bf16(const Tensor& t) {
   TORCH_CHECK(t.scalar_type() == torch::kFloat32 || t.scalar_type() == torch::kBFloat16, "activations must be fp32 or bf16");
   return t.scalar_type() == torch::kBFloat16 ? 1 : 0;
@@ -94,7 +101,7 @@ void adadelta(Tensor p, Tensor g, Tensor sq, Tensor acc, Tensor gscale, int64_t 
 
 // ------------------------------------------------------------------ layernorm
 std::vector<Tensor> ln_fwd(Tensor y, OptT bias, OptT res, Tensor gamma, Tensor beta, double eps, double keep_prob,
-                           int64_t seed, int64_t stream, bool drop_after, bool save_z) {
+                           const Tensor& seed, int64_t stream, bool drop_after, bool save_z) {
   check_cuda(y, "input");
   const int H = (int)y.size(-1);
   const int64_t rows = y.numel() / H;
@@ -113,14 +120,14 @@ std::vector<Tensor> ln_fwd(Tensor y, OptT bias, OptT res, Tensor gamma, Tensor b
   auto mean = torch::empty({rows}, st), rstd = torch::empty({rows}, st);
   hx_ln_fwd(act_bf16(y), y.data_ptr(), ptr_or_null<float>(bias), has(res) ? res->data_ptr() : nullptr,
             gamma.data_ptr<float>(), beta.data_ptr<float>(), out.data_ptr(), save_z ? z.data_ptr() : nullptr,
-            mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, H, (float)eps, (float)keep_prob, (uint64_t)seed,
+            mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, H, (float)eps, (float)keep_prob, seed_ptr(seed),
             (uint64_t)stream, drop_after ? 1 : 0, cur_stream(y));
   dbg_finite(out, "ln_fwd");
   return {out, z, mean, rstd};
 }
 
 std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tensor gamma, double keep_prob,
-                           int64_t seed, int64_t stream, bool drop_after, bool want_dy, bool want_dbias,
+                           const Tensor& seed, int64_t stream, bool drop_after, bool want_dy, bool want_dbias,
                            OptT dgamma_out, OptT dbeta_out, OptT dbias_out) {
   check_cuda(dout, "grad_output");
   check_cuda(z, "saved input");
@@ -139,7 +146,7 @@ std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tens
   auto partial = torch::empty({(int64_t)nblk * 3 * H}, f32);
   hx_ln_bwd(act_bf16(z), dout.data_ptr(), z.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
             gamma.data_ptr<float>(), dz.data_ptr(), want_dy ? dy.data_ptr() : nullptr, partial.data_ptr<float>(), nblk,
-            rows, H, (float)keep_prob, (uint64_t)seed, (uint64_t)stream, drop_after ? 1 : 0,
+            rows, H, (float)keep_prob, seed_ptr(seed), (uint64_t)stream, drop_after ? 1 : 0,
             (want_dy && want_dbias) ? 1 : 0, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
             want_dbias ? dbias.data_ptr<float>() : nullptr, 0, cur_stream(z));
   dbg_finite(dz, "ln_bwd (dz)");
@@ -147,7 +154,7 @@ std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tens
 }
 
 std::vector<Tensor> embed_ln_fwd(Tensor ids, OptT tt, Tensor wte, Tensor wpe, Tensor wtt, Tensor gamma, Tensor beta,
-                                 double eps, double keep_prob, int64_t seed, int64_t stream, bool bf16_out) {
+                                 double eps, double keep_prob, const Tensor& seed, int64_t stream, bool bf16_out) {
   dbg_range(ids, 0, wte.size(0), "token ids");
   if (has(tt)) dbg_range(*tt, 0, wtt.size(0), "token type ids");
   check_cuda(ids, "input_ids");
@@ -168,7 +175,7 @@ std::vector<Tensor> embed_ln_fwd(Tensor ids, OptT tt, Tensor wte, Tensor wpe, Te
   hx_embed_ln_fwd(bf16_out ? 1 : 0, ids.data_ptr<int64_t>(), has(tt) ? tt->data_ptr<int64_t>() : nullptr,
                   wte.data_ptr<float>(), wpe.data_ptr<float>(), wtt.data_ptr<float>(), gamma.data_ptr<float>(),
                   beta.data_ptr<float>(), out.data_ptr(), z.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                  B * S, (int)S, H, (float)eps, (float)keep_prob, (uint64_t)seed, (uint64_t)stream, cur_stream(ids));
+                  B * S, (int)S, H, (float)eps, (float)keep_prob, seed_ptr(seed), (uint64_t)stream, cur_stream(ids));
   dbg_finite(out, "embed_ln_fwd");
   return {out, z, mean, rstd};
 }
@@ -243,11 +250,11 @@ Tensor colsum(Tensor x, OptT scale, OptT out_) {
   return out;
 }
 
-Tensor dropout(Tensor x, double keep_prob, int64_t seed, int64_t stream) {
+Tensor dropout(Tensor x, double keep_prob, const Tensor& seed, int64_t stream) {
   check_cuda(x, "input");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   auto out = torch::empty_like(x);
-  hx_dropout(act_bf16(x), x.data_ptr(), out.data_ptr(), x.numel(), (float)keep_prob, (uint64_t)seed,
+  hx_dropout(act_bf16(x), x.data_ptr(), out.data_ptr(), x.numel(), (float)keep_prob, seed_ptr(seed),
              (uint64_t)stream, cur_stream(x));
   return out;
 }
@@ -271,7 +278,7 @@ Tensor softmax_xent_(Tensor logits, OptT bias, Tensor labels, int64_t ignore_ind
 }
 
 // ------------------------------------------------------------------ attention
-std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, int64_t seed, int64_t stream,
+std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed, int64_t stream,
                              OptT bias) {
   check_cuda(qkv, "qkv");
   const int bf = act_bf16(qkv);
@@ -295,7 +302,7 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
   hx_attn_fwd(bf, qkv.data_ptr(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(), out.data_ptr(),
               lse.data_ptr<float>(),
               keep < 1.0 ? reinterpret_cast<uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr, (int)B, (int)S, (int)nh,
-              (float)keep, (uint64_t)seed, (uint64_t)stream, cur_stream(qkv));
+              (float)keep, seed_ptr(seed), (uint64_t)stream, cur_stream(qkv));
   dbg_finite(out, "attn_fwd");
   return {out, lse, dmask};
 }

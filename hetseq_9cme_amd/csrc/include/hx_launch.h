@@ -18,14 +18,14 @@ void hx_adadelta(float* p, const float* g, float* sq, float* acc, const float* g
 int hx_ln_bwd_blocks(int64_t rows);
 void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, const float* gamma, const float* beta,
                void* out, void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob,
-               uint64_t seed, uint64_t stream, int drop_after, hipStream_t s);
+               const uint64_t* seed, uint64_t stream, int drop_after, hipStream_t s);
 void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma,
-               void* dz, void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, uint64_t seed,
+               void* dz, void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
                uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
                int accumulate, hipStream_t s);
 void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,
                      const float* wtt, const float* gamma, const float* beta, void* out, void* zsave, float* mean,
-                     float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, uint64_t seed,
+                     float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, const uint64_t* seed,
                      uint64_t stream, hipStream_t s);
 void hx_embed_word_grad_sorted(int bf16, const void* dz, const int64_t* ids, const int64_t* order, float* dwte,
                                int64_t rows, int H, hipStream_t s);
@@ -36,7 +36,7 @@ void hx_bias_act_bwd(int bf16, int act, const void* dout, const void* y, const f
                      void* dy, float* partial, float* dbias, int64_t rows, int N, int accumulate, hipStream_t s);
 void hx_colsum(int bf16, void* x, const float* scale, float* partial, float* out, int64_t rows, int N, int accumulate,
                hipStream_t s);
-void hx_dropout(int bf16, const void* x, void* out, int64_t n, float keep_prob, uint64_t seed, uint64_t stream,
+void hx_dropout(int bf16, const void* x, void* out, int64_t n, float keep_prob, const uint64_t* seed, uint64_t stream,
                 hipStream_t s);
 
 // xent.hip
@@ -47,7 +47,7 @@ void hx_softmax_xent(int bf16, void* logits, const float* bias, const int64_t* l
 size_t hx_attn_bwd_smem_bytes();
 // bias: optional [3H] QKV-projection bias added to Q/K/V as they are loaded
 void hx_attn_fwd_bf16(const void* qkv, const float* bias, const float* maskb, void* out, float* lse, uint32_t* dmask,
-                      int B, int S, int nh, float keep, uint64_t seed, uint64_t stream, hipStream_t s);
+                      int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream, hipStream_t s);
 void hx_attn_bwd_bf16(const void* qkv, const float* bias, float* dbias_part, const float* maskb, const void* dout,
                       const void* out, const float* lse, const uint32_t* dmask, void* dqkv, float* dq_acc, int dq_ld,
                       int B, int S, int nh, float keep, hipStream_t s);
@@ -56,7 +56,7 @@ void hx_wgrad_bf16_plan(int M, int N, int T, int* cfg, int* nsplit);
 void hx_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, float* out, float* ws, int M, int N, int T,
                    int cfg, int nsplit, hipStream_t s);
 void hx_attn_fwd(int bf16, const void* qkv, const float* bias, const float* maskb, void* out, float* lse,
-                 uint32_t* dmask, int B, int S, int nh, float keep, uint64_t seed, uint64_t stream, hipStream_t s);
+                 uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream, hipStream_t s);
 // dq_acc: fp32 dQ accumulation target when S > 128 (atomics; row stride dq_ld), else unused.
 // With bias: its gradient (column sums of dQ / dK / dV) goes to dbq / dbk / dbv through the
 // dbias_part workspace ([B * ceil(S/128)][3H] fp32).

@@ -56,7 +56,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) voi
                                                 const float* __restrict__ maskb,
                                                 T* __restrict__ out, float* __restrict__ lse,
                                                 uint32_t* __restrict__ dmask, int S, int nh, float keep,
-                                                uint64_t seed, uint64_t stream) {
+                                                const uint64_t* __restrict__ seedp, uint64_t stream) {
+  const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   __shared__ __attribute__((aligned(16))) float Ks[64 * LDK];
   __shared__ __attribute__((aligned(16))) float Vs[64 * LDK];
   __shared__ float Ms[64];
@@ -488,7 +489,7 @@ namespace {
 
 template <typename T>
 void attn_fwd_t(const void* qkv, const float* bias, const float* maskb, void* out, float* lse, uint32_t* dmask, int B,
-                int S, int nh, float keep, uint64_t seed, uint64_t stream, hipStream_t s) {
+                int S, int nh, float keep, const uint64_t* seed, uint64_t stream, hipStream_t s) {
   dim3 grid((S + 127) / 128, nh, B);
   if (keep < 1.f)
     attn_fwd_k<T, true><<<grid, 256, 0, s>>>((const T*)qkv, bias, maskb, (T*)out, lse, dmask, S, nh, keep, seed,
@@ -523,7 +524,7 @@ void attn_bwd_t(const void* qkv, const float* bias, float* dbias_part, const flo
 }  // namespace
 
 void hx_attn_fwd(int bf16, const void* qkv, const float* bias, const float* maskb, void* out, float* lse,
-                 uint32_t* dmask, int B, int S, int nh, float keep, uint64_t seed, uint64_t stream, hipStream_t s) {
+                 uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream, hipStream_t s) {
   if (bf16) hx_attn_fwd_bf16(qkv, bias, maskb, out, lse, dmask, B, S, nh, keep, seed, stream, s);  // bf16 MFMA
   else attn_fwd_t<float>(qkv, bias, maskb, out, lse, dmask, B, S, nh, keep, seed, stream, s);
 }

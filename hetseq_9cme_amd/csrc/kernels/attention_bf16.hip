@@ -88,7 +88,8 @@ __global__ __launch_bounds__(256) void attn_fwd_bf16_k(const uint16_t* __restric
                                                        const float* __restrict__ qkv_bias,
                                                        const float* __restrict__ maskb, uint16_t* __restrict__ out,
                                                        float* __restrict__ lse, uint32_t* __restrict__ dmask, int S,
-                                                       int nh, float keep, uint64_t seed, uint64_t stream) {
+                                                       int nh, float keep, const uint64_t* __restrict__ seedp, uint64_t stream) {
+  const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   __shared__ __attribute__((aligned(16))) uint16_t Ks[2][64 * RS];   // [key][dim]
   __shared__ __attribute__((aligned(16))) uint16_t Vt[2][64 * RS];   // [dim][vpos(key)]
   __shared__ float Ms[2][64];
@@ -571,7 +572,7 @@ void hx_attn_bwd_bf16(const void* qkv, const float* bias, float* dbias_part, con
 }
 
 void hx_attn_fwd_bf16(const void* qkv, const float* bias, const float* maskb, void* out, float* lse, uint32_t* dmask,
-                      int B, int S, int nh, float keep, uint64_t seed, uint64_t stream, hipStream_t s) {
+                      int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream, hipStream_t s) {
   dim3 grid((S + 127) / 128, nh, B);
   if (keep < 1.f)
     attn_fwd_bf16_k<true><<<grid, 256, 0, s>>>((const uint16_t*)qkv, bias, maskb, (uint16_t*)out, lse, dmask, S, nh,

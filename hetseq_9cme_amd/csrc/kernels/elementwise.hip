@@ -277,7 +277,8 @@ __global__ __launch_bounds__(NT) void colsum_scalar_k(const T* __restrict__ x, c
 
 template <typename T>
 __global__ __launch_bounds__(NT) void dropout_k(const T* __restrict__ x, T* __restrict__ out, int64_t n,
-                                              float keep_prob, uint64_t seed, uint64_t stream) {
+                                              float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream) {
+  const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   const float inv_keep = keep_prob > 0.f ? 1.f / keep_prob : 0.f;
   const int64_t n4 = n / 4;
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n4; i += (int64_t)gridDim.x * NT) {
@@ -413,7 +414,7 @@ void hx_colsum(int bf16, void* x, const float* scale, float* partial, float* out
   hx::fold_rows(partial, nch, N, N, N, out, nullptr, nullptr, accumulate, s);
 }
 
-void hx_dropout(int bf16, const void* x, void* out, int64_t n, float keep_prob, uint64_t seed, uint64_t stream,
+void hx_dropout(int bf16, const void* x, void* out, int64_t n, float keep_prob, const uint64_t* seed, uint64_t stream,
                 hipStream_t s) {
   const int g = egrid(n / 4 + 1);
   if (bf16) dropout_k<uint16_t><<<g, NT, 0, s>>>((const uint16_t*)x, (uint16_t*)out, n, keep_prob, seed, stream);

@@ -36,7 +36,8 @@ __global__ __launch_bounds__(NT) void ln_fwd_k(const T* __restrict__ y, const fl
                                              const float* __restrict__ beta, T* __restrict__ out,
                                              T* __restrict__ zsave, float* __restrict__ mean_out,
                                              float* __restrict__ rstd_out, int64_t rows, int H, float eps,
-                                             float keep_prob, uint64_t seed, uint64_t stream) {
+                                             float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream) {
+  const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   const int lane = threadIdx.x & 63;
   const int64_t wave = blockIdx.x * (int64_t)WPB + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * WPB;
@@ -118,8 +119,9 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
                                              const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                              const float* __restrict__ gamma, T* __restrict__ dz_out,
                                              T* __restrict__ dy_out, float* __restrict__ partial, int64_t rows,
-                                             int H, float keep_prob, uint64_t seed, uint64_t stream,
+                                             int H, float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream,
                                              int want_dbias) {
+  const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   __shared__ float red[WPB][CH * 256];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -242,7 +244,8 @@ __global__ __launch_bounds__(NT) void embed_ln_fwd_k(const int64_t* __restrict__
                                                    const float* __restrict__ beta, T* __restrict__ out,
                                                    T* __restrict__ zsave, float* __restrict__ mean_out,
                                                    float* __restrict__ rstd_out, int64_t rows, int S, int H,
-                                                   float eps, float keep_prob, uint64_t seed, uint64_t stream) {
+                                                   float eps, float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream) {
+  const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   const int lane = threadIdx.x & 63;
   const int64_t wave = blockIdx.x * (int64_t)WPB + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * WPB;
@@ -401,7 +404,7 @@ inline int ln_grid(int64_t rows, int cap) {
 
 template <typename T>
 void ln_fwd_t(const void* y, const float* bias, const void* res, const float* gamma, const float* beta, void* out,
-              void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob, uint64_t seed,
+              void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob, const uint64_t* seed,
               uint64_t stream, int drop_after, hipStream_t s) {
   const int grid = ln_grid(rows, 4096);
   HX_CH_DISPATCH(H, {
@@ -416,7 +419,7 @@ void ln_fwd_t(const void* y, const float* bias, const void* res, const float* ga
 
 template <typename T>
 void ln_bwd_t(const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma, void* dz,
-              void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, uint64_t seed,
+              void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
               uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
               int accumulate, hipStream_t s) {
   HX_CH_DISPATCH(H, {
@@ -438,7 +441,7 @@ int hx_ln_bwd_blocks(int64_t rows) { return ln_grid(rows, 512); }
 
 void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, const float* gamma, const float* beta,
                void* out, void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob,
-               uint64_t seed, uint64_t stream, int drop_after, hipStream_t s) {
+               const uint64_t* seed, uint64_t stream, int drop_after, hipStream_t s) {
   if (bf16)
     ln_fwd_t<uint16_t>(y, bias, res, gamma, beta, out, zsave, mean, rstd, rows, H, eps, keep_prob, seed, stream,
                        drop_after, s);
@@ -448,7 +451,7 @@ void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, cons
 }
 
 void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma,
-               void* dz, void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, uint64_t seed,
+               void* dz, void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
                uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
                int accumulate, hipStream_t s) {
   if (bf16)
@@ -461,7 +464,7 @@ void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, con
 
 void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,
                      const float* wtt, const float* gamma, const float* beta, void* out, void* zsave, float* mean,
-                     float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, uint64_t seed,
+                     float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, const uint64_t* seed,
                      uint64_t stream, hipStream_t s) {
   const int grid = ln_grid(rows, 4096);
   HX_CH_DISPATCH(H, {

@@ -68,7 +68,7 @@ class _AttnFn(torch.autograd.Function):
     def forward(ctx, qkv, mask_bias, bq, bk, bv, num_heads, p):
         from .fused import grad_slot  # noqa: F401  (import cycle guard)
         keep = 1.0 - p
-        seed, stream = get_rng().next() if p > 0 else (0, 0)
+        seed, stream = get_rng().next(qkv.device) if p > 0 else (get_rng().seed_tensor(qkv.device), 0)
         bias = _bias3(bq, bk, bv).float().contiguous() if bq is not None else None
         out, lse, dmask = C().attn_fwd(qkv, mask_bias, num_heads, keep, seed, stream, bias)
         ctx.save_for_backward(qkv, mask_bias, out, lse, dmask)

@@ -200,7 +200,7 @@ class _EmbedLNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, ids, tt, wte, wpe, wtt, gamma, beta, eps, p, out_bf16):
         keep = 1.0 - p
-        seed, stream = get_rng().next() if p > 0 else (0, 0)
+        seed, stream = get_rng().next(ids.device) if p > 0 else (get_rng().seed_tensor(ids.device), 0)
         out, z, mean, rstd = C().embed_ln_fwd(ids, tt, wte, wpe, wtt, gamma, beta, eps, keep, seed, stream,
                                               out_bf16)
         ctx.save_for_backward(ids, tt if tt is not None else torch.Tensor(), z, mean, rstd, gamma)
@@ -275,7 +275,7 @@ class _BiasDropResLNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, bias, res, gamma, beta, eps, p, mbox):
         keep = 1.0 - p
-        seed, stream = get_rng().next() if p > 0 else (0, 0)
+        seed, stream = get_rng().next(y.device) if p > 0 else (get_rng().seed_tensor(y.device), 0)
         out, z, mean, rstd = C().ln_fwd(y, bias, res, gamma, beta, eps, keep, seed, stream, False, True)
         ctx.save_for_backward(z, mean, rstd, gamma)
         ctx.params = (bias, beta)
@@ -358,7 +358,7 @@ class _DropoutFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, p):
         keep = 1.0 - p
-        seed, stream = get_rng().next()
+        seed, stream = get_rng().next(x.device)
         ctx.meta = (keep, seed, stream)
         return C().dropout(x, keep, seed, stream)
 

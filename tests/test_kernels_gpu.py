@@ -13,6 +13,11 @@ from hetseq_9cme_amd.ops.flash_attention import attention_ref
 pytestmark = pytest.mark.gpu
 
 
+
+def _seed(dev, v):
+    """Dropout key as the kernels take it: a 1-element int64 device tensor."""
+    return torch.full((1,), v, dtype=torch.int64, device=dev)
+
 def _close(a, b, rtol=1e-4, atol=1e-5):
     torch.testing.assert_close(a.float().cpu(), b.float().cpu(), rtol=rtol, atol=atol)
 
@@ -293,7 +298,7 @@ def test_attention_dropout_fwd_bwd(dev, S):
     mask[0, S - 37:] = 0
     mb = ((1 - mask) * -10000.0).contiguous()
     keep = 0.9
-    out, lse, dm = C().attn_fwd(qkv, mb, nh, keep, 1234, 7, None)
+    out, lse, dm = C().attn_fwd(qkv, mb, nh, keep, _seed(dev, 1234), 7, None)
     bits = dm.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
     shifts = torch.arange(32, device=dev)
     Sp = dm.shape[2]                 # bitmask is [key][query word], padded to 128
@@ -331,7 +336,7 @@ def test_attention_bf16_mfma_dropout_fwd_bwd(dev, S, with_bias):
     mask[0, S - 37:] = 0
     mb = ((1 - mask) * -10000.0).contiguous()
     keep = 0.9
-    out, lse, dm = C().attn_fwd(qkv, mb, nh, keep, 1234, 7, bias)
+    out, lse, dm = C().attn_fwd(qkv, mb, nh, keep, _seed(dev, 1234), 7, bias)
     assert out.dtype == torch.bfloat16
     bits = dm.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
     shifts = torch.arange(32, device=dev)
@@ -412,11 +417,11 @@ def test_debug_mode_validation(dev):
     C().set_debug(True)
     try:
         with pytest.raises(RuntimeError, match='token ids out of range'):
-            C().embed_ln_fwd(bad, None, wte, wpe, wtt, g, b, 1e-12, 1.0, 0, 0, False)
+            C().embed_ln_fwd(bad, None, wte, wpe, wtt, g, b, 1e-12, 1.0, _seed(dev, 0), 0, False)
         y = torch.randn(8, H, device=dev)
         y[3, 5] = float('nan')
         with pytest.raises(RuntimeError, match='non-finite values produced by ln_fwd'):
-            C().ln_fwd(y, None, None, g, b, 1e-12, 1.0, 0, 0, False, False)
+            C().ln_fwd(y, None, None, g, b, 1e-12, 1.0, _seed(dev, 0), 0, False, False)
     finally:
         C().set_debug(False)
     assert not C().get_debug()

@@ -15,6 +15,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from hetseq_9cme_amd.ops._ext import C  # noqa: E402
 
 
+SEED = None   # dropout key tensor (set in main: kernels read it from device memory)
+
+
 def timeit(fn, iters=50, warmup=5):
     for _ in range(warmup):
         fn()
@@ -49,14 +52,14 @@ def bench_attn(B, S, nh=12, keep=0.9, dtype=torch.float32):
     peak = 157.3 if dtype == torch.float32 else 2500.0
     qkv = torch.randn(B, S, 3 * nh * d, device='cuda').to(dtype)
     mb = torch.zeros(B, S, device='cuda')
-    out, lse, dm = C().attn_fwd(qkv, mb, nh, keep, 1, 0, None)
+    out, lse, dm = C().attn_fwd(qkv, mb, nh, keep, SEED, 0, None)
     dout = torch.randn_like(out)
     f_fwd = 2 * 2 * B * nh * S * S * d
     report = _report_peak(peak, '' if dtype == torch.float32 else '[bf16] ')
-    report('attn_fwd', timeit(lambda: C().attn_fwd(qkv, mb, nh, keep, 1, 0, None)), flops=f_fwd)
-    report('attn_fwd (no dropout)', timeit(lambda: C().attn_fwd(qkv, mb, nh, 1.0, 1, 0, None)), flops=f_fwd)
+    report('attn_fwd', timeit(lambda: C().attn_fwd(qkv, mb, nh, keep, SEED, 0, None)), flops=f_fwd)
+    report('attn_fwd (no dropout)', timeit(lambda: C().attn_fwd(qkv, mb, nh, 1.0, SEED, 0, None)), flops=f_fwd)
     report('attn_bwd', timeit(lambda: C().attn_bwd(dout, qkv, mb, out, lse, dm, nh, keep, None, None, None, None)[0]), flops=2.5 * f_fwd)
-    out1, lse1, dm1 = C().attn_fwd(qkv, mb, nh, 1.0, 1, 0, None)
+    out1, lse1, dm1 = C().attn_fwd(qkv, mb, nh, 1.0, SEED, 0, None)
     report('attn_bwd (no dropout)', timeit(lambda: C().attn_bwd(dout, qkv, mb, out1, lse1, dm1, nh, 1.0, None, None, None, None)[0]),
            flops=2.5 * f_fwd)
 
@@ -68,11 +71,11 @@ def bench_ln(B, S, H=768):
     g = torch.ones(H, device='cuda')
     bt = torch.zeros(H, device='cuda')
     bias = torch.zeros(H, device='cuda')
-    report('ln_fwd(bias+drop+res)', timeit(lambda: C().ln_fwd(x, bias, res, g, bt, 1e-12, 0.9, 1, 0, False, True)),
+    report('ln_fwd(bias+drop+res)', timeit(lambda: C().ln_fwd(x, bias, res, g, bt, 1e-12, 0.9, SEED, 0, False, True)),
            bytes_=4 * n * H * 4)
-    out, z, mean, rstd = C().ln_fwd(x, bias, res, g, bt, 1e-12, 0.9, 1, 0, False, True)
+    out, z, mean, rstd = C().ln_fwd(x, bias, res, g, bt, 1e-12, 0.9, SEED, 0, False, True)
     dout = torch.randn_like(out)
-    report('ln_bwd(+dy,+dbias)', timeit(lambda: C().ln_bwd(dout, z, mean, rstd, g, 0.9, 1, 0, False, True, True,
+    report('ln_bwd(+dy,+dbias)', timeit(lambda: C().ln_bwd(dout, z, mean, rstd, g, 0.9, SEED, 0, False, True, True,
                                                            None, None, None)), bytes_=4 * n * H * 4)
 
 
@@ -110,6 +113,8 @@ def bench_xent(rows=2560, V=30522):
 
 
 def main():
+    global SEED
+    SEED = torch.ones(1, dtype=torch.int64, device='cuda')
     ap = argparse.ArgumentParser()
     ap.add_argument('--batch', type=int, default=128)
     ap.add_argument('--seq', type=int, default=128)

@@ -89,6 +89,10 @@ class Controller(object):
         self.fast_stat_sync = args.fast_stat_sync
         self._save_thread = None
         self._transport_monitor = TransportErrorMonitor(lag=2)
+        self._graph_step = None
+        if getattr(args, 'graph_train_step', False) and self.cuda:
+            from .utils.train_graph import GraphedTrainStep
+            self._graph_step = GraphedTrainStep(self)
         self._profile_phases = bool(getattr(args, 'profile_phases', False))
         self.phases = PhaseTimer(self._profile_phases, cuda=self.cuda)
         self.init_meters(args)
@@ -222,6 +226,14 @@ class Controller(object):
 
     def train_step(self, samples, dummy_batch=False, raise_oom=False):
         """Forward, backward and parameter update for one group of micro-batches."""
+        if self._graph_step is not None and not dummy_batch:
+            out = self._graph_step(samples)      # HIP-graph replay of a captured update
+            if out is not NotImplemented:
+                return out
+        return self._train_step(samples, dummy_batch)
+
+    def _train_step(self, samples, dummy_batch=False):
+        capturing = self.cuda and torch.cuda.is_current_stream_capturing()
         ph = self.phases.begin
         ph('prep')
         self._transport_monitor.check()   # xGMI timeouts of update n-2, on every rank alike
@@ -286,8 +298,15 @@ class Controller(object):
             # [sample_size, nsentences, loss, nll_loss, ntokens, ooms] (+ xGMI error word)
             err = self.reducer.transport_error_async() if self.reducer.enabled else None
             fields = [acc_ss, acc_ns, 0.0, 0.0, acc_nt, float(ooms)] + ([0.0] if err is not None else [])
-            host = torch.tensor(fields, dtype=torch.float64)
-            vec = host.pin_memory().to(self.device, non_blocking=True) if self.cuda else host
+            if capturing:
+                # no host->device copy inside a graph (it would keep reading a freed pinned
+                # buffer): the per-shape constants become fill nodes
+                vec = torch.empty(len(fields), dtype=torch.float64, device=self.device)
+                for k, f in enumerate(fields):
+                    vec[k].fill_(f)
+            else:
+                host = torch.tensor(fields, dtype=torch.float64)
+                vec = host.pin_memory().to(self.device, non_blocking=True) if self.cuda else host
             if acc_loss is not None:
                 vec[2:4] = torch.stack([acc_loss.reshape(()), acc_nll.reshape(())]).to(vec.device)
             if err is not None:
@@ -343,21 +362,12 @@ class Controller(object):
             ph('meters')
             self.set_num_updates(self.get_num_updates() + 1)
             self.task.update_step(self._num_updates)
-
-            ntokens = logging_output.get('ntokens', 0)
-            nsentences = logging_output.get('nsentences', 0)
-            self.meters['wps'].update(ntokens)
-            self.meters['ups'].update(1.)
-            self.meters['wpb'].update(ntokens)
-            self.meters['bsz'].update(nsentences)
-            self.meters['gnorm'].update(grad_norm)
-            self.meters['clip'].update(opt.clipped if self.args.clip_norm > 0 else 0.)
-            # weight: the all-reduced sample size on the fast path (reference: sample_size = vec[0]
-            # after the stats all-reduce, controller.py:300-306); the local one otherwise
-            weight = size_for_norm if self.fast_stat_sync else sample_size
-            self.meters['train_loss'].update(logging_output.get('loss', 0), weight)
-            if 'train_acc' in self.meters:
-                self.meters['train_acc'].update(logging_output.get('acc', 0), weight)
+            if capturing:   # host meters: updated after every replay (utils/train_graph.py)
+                self._captured_meter_args = (logging_output, size_for_norm if self.fast_stat_sync else sample_size,
+                                             grad_norm, opt.clipped if self.args.clip_norm > 0 else 0.)
+                return logging_output
+            self._update_meters(logging_output, size_for_norm if self.fast_stat_sync else sample_size, grad_norm,
+                                opt.clipped if self.args.clip_norm > 0 else 0.)
         except OverflowError as e:
             print('| WARNING: overflow detected, ' + str(e))
             self.zero_grad()
@@ -368,6 +378,22 @@ class Controller(object):
         if logging_output is not None and 'sample_size' not in logging_output:
             logging_output['sample_size'] = sample_size
         return logging_output
+
+    def _update_meters(self, logging_output, weight, grad_norm, clipped):
+        """Per-update meters (reference controller.py:354-367); device values stay lazy.
+        ``weight``: the all-reduced sample size on the fast path (reference: sample_size =
+        vec[0] after the stats all-reduce, controller.py:300-306), the local one otherwise."""
+        ntokens = logging_output.get('ntokens', 0)
+        nsentences = logging_output.get('nsentences', 0)
+        self.meters['wps'].update(ntokens)
+        self.meters['ups'].update(1.)
+        self.meters['wpb'].update(ntokens)
+        self.meters['bsz'].update(nsentences)
+        self.meters['gnorm'].update(grad_norm)
+        self.meters['clip'].update(clipped)
+        self.meters['train_loss'].update(logging_output.get('loss', 0), weight)
+        if 'train_acc' in self.meters:
+            self.meters['train_acc'].update(logging_output.get('acc', 0), weight)
 
     # ------------------------------------------------------------------ phase timing
     @property
@@ -421,9 +447,10 @@ class Controller(object):
 
     def _set_seed(self):
         seed = self.args.seed + self.get_num_updates()
-        torch.manual_seed(seed)
-        if self.cuda:
-            torch.cuda.manual_seed(seed)
+        if not (self.cuda and torch.cuda.is_current_stream_capturing()):   # (graph mode: set before capture)
+            torch.manual_seed(seed)
+            if self.cuda:
+                torch.cuda.manual_seed(seed)
         ops.set_step_seed(seed)
 
     def _sync_stats(self):

@@ -70,8 +70,17 @@ void grad_norm_clip(Tensor g, Tensor gscale, Tensor out_norm, Tensor clipped, do
                     out_norm.data_ptr<float>(), clipped.data_ptr<float>(), (float)max_norm, cur_stream(g));
 }
 
+// hp (optional, device fp32 [2]): step size and wd * lr read by the kernel instead of the
+// host values -- a captured training step (utils/train_graph.py) refreshes them per replay
+inline const float* hp_ptr(const OptT& hp, int64_t need) {
+  if (!has(hp)) return nullptr;
+  TORCH_CHECK(hp->is_cuda() && hp->scalar_type() == torch::kFloat32 && hp->numel() >= need && hp->is_contiguous(),
+              "optimizer hyper-parameters must be a contiguous fp32 GPU tensor");
+  return hp->data_ptr<float>();
+}
+
 void adam(Tensor p, Tensor g, Tensor m, Tensor v, OptT shadow, Tensor gscale, int64_t start, int64_t end, double b1,
-          double b2, double eps, double step_size, double wd_lr) {
+          double b2, double eps, double step_size, double wd_lr, OptT hp) {
   check_f32(p, "param");
   check_f32(g, "grad");
   check_f32(m, "exp_avg");
@@ -86,17 +95,17 @@ void adam(Tensor p, Tensor g, Tensor m, Tensor v, OptT shadow, Tensor gscale, in
   }
   hx_adam(p.data_ptr<float>() + start, g.data_ptr<float>() + start, m.data_ptr<float>() + start,
           v.data_ptr<float>() + start, sh, gscale.data_ptr<float>(), end - start, (float)b1, (float)b2, (float)eps,
-          (float)step_size, (float)wd_lr, cur_stream(p));
+          (float)step_size, (float)wd_lr, hp_ptr(hp, 2), cur_stream(p));
 }
 
 void adadelta(Tensor p, Tensor g, Tensor sq, Tensor acc, Tensor gscale, int64_t start, int64_t end, double lr,
-              double rho, double eps, double wd) {
+              double rho, double eps, double wd, OptT hp) {
   check_f32(p, "param");
   TORCH_CHECK(start >= 0 && end <= p.numel() && start <= end, "bad param range");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
   hx_adadelta(p.data_ptr<float>() + start, g.data_ptr<float>() + start, sq.data_ptr<float>() + start,
               acc.data_ptr<float>() + start, gscale.data_ptr<float>(), end - start, (float)lr, (float)rho,
-              (float)eps, (float)wd, cur_stream(p));
+              (float)eps, (float)wd, hp_ptr(hp, 1), cur_stream(p));
 }
 
 // ------------------------------------------------------------------ layernorm

@@ -10,9 +10,10 @@ int hx_grad_norm_partials();
 void hx_grad_norm_clip(const float* g, int64_t n, double* partial_ws, float* gscale, float* out_norm, float* clipped,
                        float max_norm, hipStream_t s);
 void hx_adam(float* p, const float* g, float* m, float* v, uint16_t* shadow, const float* gscale, int64_t n, float b1,
-             float b2, float eps, float step_size, float wd_lr, hipStream_t s);
+             float b2, float eps, float step_size, float wd_lr, const float* hp,
+             hipStream_t s);
 void hx_adadelta(float* p, const float* g, float* sq, float* acc, const float* gscale, int64_t n, float lr, float rho,
-                 float eps, float wd, hipStream_t s);
+                 float eps, float wd, const float* hp, hipStream_t s);
 
 // layernorm.hip
 int hx_ln_bwd_blocks(int64_t rows);

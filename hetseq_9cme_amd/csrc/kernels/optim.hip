@@ -103,8 +103,12 @@ __global__ __launch_bounds__(NT) void adam_k(float* __restrict__ p, const float*
                                            float* __restrict__ m, float* __restrict__ v,
                                            uint16_t* __restrict__ shadow, const float* __restrict__ gscale,
                                            int64_t n, float b1, float b2, float eps, float step_size,
-                                           float wd_lr) {
+                                           float wd_lr, const float* __restrict__ hp) {
   const float gs = gscale[0];
+  if (hp) {   // graph-captured step: per-update step size / decay written before each replay
+    step_size = hp[0];
+    wd_lr = hp[1];
+  }
   const float ob1 = 1.f - b1, ob2 = 1.f - b2;
   const int64_t n4 = n >> 2;
   float4* P = reinterpret_cast<float4*>(p);
@@ -151,8 +155,9 @@ __global__ __launch_bounds__(NT) void adam_k(float* __restrict__ p, const float*
 __global__ __launch_bounds__(NT) void adadelta_k(float* __restrict__ p, const float* __restrict__ g,
                                                float* __restrict__ sq, float* __restrict__ acc,
                                                const float* __restrict__ gscale, int64_t n, float lr, float rho,
-                                               float eps, float wd) {
+                                               float eps, float wd, const float* __restrict__ hp) {
   const float gs = gscale[0];
+  if (hp) lr = hp[0];
   for (int64_t i = blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
     float gr = g[i] * gs;
     const float x = p[i];
@@ -185,15 +190,15 @@ void hx_grad_norm_clip(const float* g, int64_t n, double* partial_ws, float* gsc
 }
 
 void hx_adam(float* p, const float* g, float* m, float* v, uint16_t* shadow, const float* gscale, int64_t n,
-             float b1, float b2, float eps, float step_size, float wd_lr, hipStream_t s) {
+             float b1, float b2, float eps, float step_size, float wd_lr, const float* hp, hipStream_t s) {
   const int grid = grid_for((n + 3) / 4, 8192);
   if (shadow)
-    adam_k<true><<<grid, NT, 0, s>>>(p, g, m, v, shadow, gscale, n, b1, b2, eps, step_size, wd_lr);
+    adam_k<true><<<grid, NT, 0, s>>>(p, g, m, v, shadow, gscale, n, b1, b2, eps, step_size, wd_lr, hp);
   else
-    adam_k<false><<<grid, NT, 0, s>>>(p, g, m, v, shadow, gscale, n, b1, b2, eps, step_size, wd_lr);
+    adam_k<false><<<grid, NT, 0, s>>>(p, g, m, v, shadow, gscale, n, b1, b2, eps, step_size, wd_lr, hp);
 }
 
 void hx_adadelta(float* p, const float* g, float* sq, float* acc, const float* gscale, int64_t n, float lr,
-                 float rho, float eps, float wd, hipStream_t s) {
-  adadelta_k<<<grid_for(n, 8192), NT, 0, s>>>(p, g, sq, acc, gscale, n, lr, rho, eps, wd);
+                 float rho, float eps, float wd, const float* hp, hipStream_t s) {
+  adadelta_k<<<grid_for(n, 8192), NT, 0, s>>>(p, g, sq, acc, gscale, n, lr, rho, eps, wd, hp);
 }

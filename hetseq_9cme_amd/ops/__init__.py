@@ -19,9 +19,10 @@ def flat_grad_norm_clip(grad_flat, gscale, out_norm, clipped, max_norm):
     C().grad_norm_clip(grad_flat, gscale, out_norm, clipped, float(max_norm))
 
 
-def fused_adam(p, g, m, v, gscale, start, end, beta1, beta2, eps, step_size, wd_lr, bf16_shadow=None):
-    C().adam(p, g, m, v, bf16_shadow, gscale, int(start), int(end), beta1, beta2, eps, step_size, wd_lr)
+def fused_adam(p, g, m, v, gscale, start, end, beta1, beta2, eps, step_size, wd_lr, bf16_shadow=None, hp=None):
+    """``hp``: optional device [2] (step size, wd * lr) that overrides the host values."""
+    C().adam(p, g, m, v, bf16_shadow, gscale, int(start), int(end), beta1, beta2, eps, step_size, wd_lr, hp)
 
 
-def fused_adadelta(p, g, sq, acc, gscale, start, end, lr, rho, eps, wd):
-    C().adadelta(p, g, sq, acc, gscale, int(start), int(end), lr, rho, eps, wd)
+def fused_adadelta(p, g, sq, acc, gscale, start, end, lr, rho, eps, wd, hp=None):
+    C().adadelta(p, g, sq, acc, gscale, int(start), int(end), lr, rho, eps, wd, hp)

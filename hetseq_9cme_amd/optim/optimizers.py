@@ -62,6 +62,26 @@ class _Optimizer(object):
     # --- grads --------------------------------------------------------
     phase_hook = None   # set by the controller under --profile-phases
     bf16_shadow = None  # bf16 copy of the flat params kept in sync by step() (--precision bf16)
+    # Graph-captured steps (utils/train_graph.py): a device fp32 buffer the update kernels read
+    # their per-update hyper-parameters from (2 per run for Adam: step size, wd * lr; 1 for
+    # Adadelta: lr), so a replayed graph applies the current schedule.  ``_hp_vals`` holds the
+    # values of the latest step (also the ones a capture pass computed but could not write).
+    device_hparams = None
+    _hp_vals = None
+    _runs_sig = None
+
+    def _hp_slice(self, r, width):
+        hp = self.device_hparams
+        return None if hp is None else hp[width * r:width * (r + 1)]
+
+    def _write_hparams(self):
+        """Write ``_hp_vals`` into ``device_hparams`` (small fills; skipped while capturing,
+        where they would be frozen into the graph)."""
+        hp = self.device_hparams
+        if hp is None or self._hp_vals is None or torch.cuda.is_current_stream_capturing():
+            return
+        for k, v in enumerate(self._hp_vals):
+            hp[k].fill_(v)
 
     def backward(self, loss):
         if self.phase_hook is not None:
@@ -195,8 +215,8 @@ class _Adam(_Optimizer):
         beta1, beta2 = g['betas']
         eps, wd, lr = g['eps'], g['weight_decay'], self._lr
         self._fold_host_scale()
-        runs = self._runs_by_step()
-        for (start, end, t) in runs:
+        runs = self._host_step()
+        for r, (start, end, t) in enumerate(runs):
             bc1 = 1 - beta1 ** t
             bc2 = 1 - beta2 ** t
             step_size = lr * math.sqrt(bc2) / bc1
@@ -204,7 +224,7 @@ class _Adam(_Optimizer):
                 ops.fused_adam(self.flat.param_flat, self.flat.grad_flat, self.exp_avg,
                                self.exp_avg_sq, self._gscale, start, end,
                                float(beta1), float(beta2), float(eps), float(step_size),
-                               float(wd * lr), self.bf16_shadow)
+                               float(wd * lr), self.bf16_shadow, self._hp_slice(r, 2))
             else:
                 p = self.flat.param_flat[start:end]
                 gr = self.flat.grad_flat[start:end].float() * self._gscale
@@ -218,6 +238,22 @@ class _Adam(_Optimizer):
                 p.addcdiv_(m, denom, value=-step_size)
                 if self.bf16_shadow is not None:
                     self.bf16_shadow[start:end].copy_(p)
+
+    def _host_step(self):
+        """Host half of an update: advance the step counters, compute this update's
+        hyper-parameters and (graph mode) write them to the device buffer.  A replayed
+        graph calls only this; ``step`` calls it and then launches the kernels."""
+        g = self.param_groups[0]
+        beta1, beta2 = g['betas']
+        lr, wd = self._lr, g['weight_decay']
+        runs = self._runs_by_step()
+        vals = []
+        for (_, _, t) in runs:
+            vals += [lr * math.sqrt(1 - beta2 ** t) / (1 - beta1 ** t), wd * lr]
+        self._hp_vals = vals
+        self._runs_sig = tuple((a, b) for a, b, _ in runs)
+        self._write_hparams()
+        return runs
 
     def _runs_by_step(self):
         """Advance per-param step counters for used params and return
@@ -284,14 +320,12 @@ class _Adadelta(_Optimizer):
         g = self.param_groups[0]
         rho, eps, wd, lr = g['rho'], g['eps'], g['weight_decay'], self._lr
         self._fold_host_scale()
-        for i, used in enumerate(self.used_mask):
-            if used:
-                self.steps[i] += 1
-        for (start, end) in self.flat.runs_for(self.used_mask):
+        runs = self._host_step()
+        for (start, end) in runs:
             if self.use_kernels:
                 ops.fused_adadelta(self.flat.param_flat, self.flat.grad_flat, self.square_avg,
                                    self.acc_delta, self._gscale, start, end,
-                                   float(lr), float(rho), float(eps), float(wd))
+                                   float(lr), float(rho), float(eps), float(wd), self._hp_slice(0, 1))
             else:
                 p = self.flat.param_flat[start:end]
                 gr = self.flat.grad_flat[start:end] * self._gscale
@@ -307,6 +341,17 @@ class _Adadelta(_Optimizer):
 
         if self.bf16_shadow is not None:
             self.flat.refresh_bf16()
+
+    def _host_step(self):
+        for i, used in enumerate(self.used_mask):
+            if used:
+                self.steps[i] += 1
+        runs = self.flat.runs_for(self.used_mask)
+        self._hp_vals = [self._lr]
+        self._runs_sig = tuple(runs)
+        self._write_hparams()
+        return runs
+
     def _param_state(self, i):
         if self.steps[i] == 0:
             return None

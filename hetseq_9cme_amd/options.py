@@ -58,6 +58,14 @@ def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialD
                              'fp32-exact class -- measured GEMM error within 1.2x of native), bf16x3 (two '
                              'pieces, three passes, ~2^-17 per product: near-fp32, fastest) or native f32 '
                              'MFMA (157 TF/s peak); see ops/split_gemm.py')
+    parser.add_argument('--graph-train-step', action='store_true',
+                        help='single GPU, one micro-batch per update: capture each input shape\'s whole '
+                             'update (forward, backward, clip, optimizer) in a HIP graph after two eager '
+                             'warm-up steps and replay it -- removes the host launch overhead of '
+                             'small-batch fine-tuning (see utils/train_graph.py)')
+    parser.add_argument('--pad-to-multiple-of', type=int, default=None, metavar='N',
+                        help='token-classification batches: pad sequence length to a multiple of N '
+                             '(default 16 under --graph-train-step, else the batch maximum)')
     parser.add_argument('--fused-kernels', default=True, type=eval_bool_arg,
                         help='use the hand-written HIP kernels on GPU (True) or plain torch ops')
     parser.add_argument('--user-module', default=None, metavar='PATH',

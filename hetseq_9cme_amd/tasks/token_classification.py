@@ -55,7 +55,11 @@ class BertForTokenClassificationTask(Task):
     @classmethod
     def setup_task(cls, args, **kwargs):
         tokenizer = build_tokenizer(args.dict)
-        collator = cls.collator_cls(tokenizer, max_length=args.max_pred_length, padding=True)
+        # --graph-train-step captures one graph per batch shape: pad lengths to a multiple of 16
+        # so a handful of shapes cover the corpus (attention masks make padding exact)
+        mult = getattr(args, 'pad_to_multiple_of', None) or (16 if getattr(args, 'graph_train_step', False) else None)
+        collator = cls.collator_cls(tokenizer, max_length=args.max_pred_length, padding=True,
+                                    pad_to_multiple_of=mult)
         files = {'train': args.train_file, 'validation': args.validation_file, 'test': args.test_file}
         ext = args.extension_file if args.extension_file in ('json', 'jsonl', 'csv', 'conll') else None
         raw = {k: cls.read_split(v, ext) for k, v in files.items() if v is not None}

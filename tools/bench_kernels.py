@@ -97,7 +97,7 @@ def bench_adam(n=110_000_000):
     m = torch.zeros(n, device='cuda')
     v = torch.zeros(n, device='cuda')
     gs = torch.ones(1, device='cuda')
-    report('adam(110M params)', timeit(lambda: C().adam(p, g, m, v, None, gs, 0, n, 0.9, 0.999, 1e-8, 1e-4, 1e-6)),
+    report('adam(110M params)', timeit(lambda: C().adam(p, g, m, v, None, gs, 0, n, 0.9, 0.999, 1e-8, 1e-4, 1e-6, None)),
            bytes_=7 * n * 4)
 
 

@@ -27,6 +27,7 @@ def main():
     ap.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'])
     ap.add_argument('--profile-phases', action='store_true', help='host/device time per step phase (stderr)')
     ap.add_argument('--gemm-tuning', default='table', choices=['off', 'table'])
+    ap.add_argument('--graph-train-step', action='store_true', help='replay captured HIP graphs of the update')
     ap.add_argument('--cprofile', default=None, metavar='OUT',
                     help='after the timed steps, cProfile 20 more steps and write the top host functions to OUT')
     a = ap.parse_args()
@@ -47,6 +48,8 @@ def main():
             '--gemm-tuning', a.gemm_tuning]
     if a.profile_phases:
         argv.append('--profile-phases')
+    if a.graph_train_step:
+        argv.append('--graph-train-step')
     args = options.parse_training_args(argv)
     args.device_id = 0
     args.distributed_rank = 0
@@ -66,6 +69,9 @@ def main():
         ctrl.train_step(next(itr))
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
+    gs = ctrl._graph_step
+    if gs is not None:
+        print('graph-train-step: {} captures, {} replays'.format(gs.captures, gs.replays), file=sys.stderr)
     if a.cprofile:
         import cProfile
         import io
@@ -88,7 +94,7 @@ def main():
     print(json.dumps({'metric': 'NER fine-tune (BertForTokenClassification, BERT-base) s/update',
                       'value': round(dt, 5), 'unit': 's/update', 'higher_is_better': False,
                       'reference_1gpu': 0.214, 'speedup_vs_reference': round(0.214 / dt, 1),
-                      'batch': a.batch, 'dtype': a.precision,
+                      'batch': a.batch, 'dtype': a.precision, 'graph_train_step': a.graph_train_step,
                       'data': 'synthetic CoNLL-format sentences (8-40 words), random-init BERT-base'}), flush=True)
 
 

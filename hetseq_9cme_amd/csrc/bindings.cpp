@@ -542,6 +542,29 @@ Tensor split_planes(Tensor x, std::vector<int64_t> order, int64_t npieces, bool 
   return out;
 }
 
+// W [N, K] fp32 -> [K, npl * Np] bf16 transposed planes (the data-gradient operand in NT form)
+Tensor split_planes_t(Tensor W, std::vector<int64_t> order, int64_t npieces, int64_t npad) {
+  TORCH_CHECK(W.is_cuda() && W.scalar_type() == torch::kFloat32, "split_planes_t: W must be an fp32 GPU tensor");
+  TORCH_CHECK(W.dim() == 2 && W.stride(1) == 1 && W.stride(0) % 4 == 0 && aligned16(W.data_ptr()),
+              "split_planes_t: W must be [N, K] with 16-B aligned rows");
+  TORCH_CHECK(npieces == 2 || npieces == 3, "split_planes_t: 2 or 3 pieces");
+  TORCH_CHECK(!order.empty() && order.size() <= 8, "split_planes_t: 1..8 planes");
+  uint32_t packed = 0;
+  for (size_t j = 0; j < order.size(); ++j) {
+    TORCH_CHECK(order[j] >= 0 && order[j] < npieces, "split_planes_t: piece index out of range");
+    packed |= (uint32_t)order[j] << (4 * j);
+  }
+  const int64_t N = W.size(0), K = W.size(1), npl = (int64_t)order.size();
+  const int64_t Np = std::max<int64_t>(N, npad);
+  TORCH_CHECK(K % 64 == 0 && Np % 64 == 0 && K * npl * Np < (1LL << 40) && Np < (1LL << 24) && K < 65536 * 64,
+              "split_planes_t: K and the padded N must be multiples of 64");
+  Tensor out = torch::empty({K, npl * Np}, W.options().dtype(torch::kBFloat16));
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(W.device());
+  hx_split_planes_t(W.data_ptr<float>(), W.stride(0), (int)N, (int)K, reinterpret_cast<uint16_t*>(out.data_ptr()),
+                    (int)Np, (int)npieces, (int)npl, packed, cur_stream(W));
+  return out;
+}
+
 // ------------------------------------------------------------------ xGMI all-reduce
 // Contexts travel to Python as integers (owned by parallel/xgmi.py).
 inline void xar_check(int rc) { TORCH_CHECK(rc == 0, hx_xar_last_error()); }
@@ -612,6 +635,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_bf16", &wgrad_bf16);
   m.def("wgrad_bf16_ok", &wgrad_bf16_ok);
   m.def("split_planes", &split_planes);
+  m.def("split_planes_t", &split_planes_t);
   m.def("split_weight", &split_weight);
   m.def("gemm_split", &gemm_split);
   m.def("gemm_split_ok", &gemm_split_ok);

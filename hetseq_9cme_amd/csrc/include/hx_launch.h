@@ -94,6 +94,10 @@ int hx_gemm_split_nt(const void* A, int64_t lda, int64_t a_ps, const void* B, in
 // Output rows padded to Rp (stacked) / columns to Dp with zeros.
 void hx_split_planes(const float* x, int64_t ldx, uint16_t* out, int64_t R, int D, int64_t Rp, int Dp,
                      int npieces, int npl, uint32_t order, int stacked, hipStream_t s);
+// Transposed weight planes [K][npl][Np]: out[k][j * Np + n] = piece order[j] of W[n][k]
+// (n >= N zero-filled); K and Np multiples of 64, W rows 16-B aligned.
+void hx_split_planes_t(const float* W, int64_t ldw, int N, int K, uint16_t* out, int Np, int npieces, int npl,
+                       uint32_t order, hipStream_t s);
 
 // xgmi_allreduce.hip -- intra-node two-shot all-reduce over IPC-mapped peer buffers.
 // Every function returns 0 on success, -1 with a message in hx_xar_last_error().

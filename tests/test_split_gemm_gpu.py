@@ -75,6 +75,26 @@ def test_split_planes_padded_unaligned(dev, stacked):
     assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
 
 
+@pytest.mark.parametrize('npieces,order,N,npad', [(3, (0, 1, 0, 2, 1, 0), 192, 0), (2, (0, 1, 0), 128, 0),
+                                                  (3, (0, 1, 0, 2, 1, 0), 150, 192)])
+def test_split_planes_transposed_bitwise(dev, npieces, order, N, npad):
+    """Transposed weight planes (the NT data-gradient operand): out[k][j * Np + n] =
+    piece order[j] of W[n][k], rows n >= N zero (the MLM decoder's padded vocabulary)."""
+    from hetseq_9cme_amd.ops._ext import C
+    g = torch.Generator(device='cpu').manual_seed(5)
+    K = 128
+    W = (torch.randn(N, K, generator=g) * torch.logspace(-5, 5, K)).to(dev)
+    out = C().split_planes_t(W, list(order), npieces, npad)
+    Np = max(N, npad)
+    pcs = _ref_pieces(W, npieces)
+    ref = torch.zeros(K, len(order), Np, dtype=torch.bfloat16, device=dev)
+    for j, k in enumerate(order):
+        ref[:, j, :N] = pcs[k].t()
+    ref = ref.reshape(K, -1)
+    assert out.shape == ref.shape
+    assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
+
+
 def _err(a, ref, scale):
     return ((a.double() - ref).abs() / scale.clamp(min=1e-30)).max().item()
 

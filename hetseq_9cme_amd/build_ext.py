@@ -76,16 +76,20 @@ def build_kernels(force=False, jobs=8, verbose=False):
             jobs_list.append([HIPCC, '--offload-arch=' + ARCH, '-O3', '-std=c++17', '-fPIC', '-c', s, '-o', o,
                               '-I' + os.path.join(CSRC, 'include'), '-munsafe-fp-atomics',
                               '-Wno-unused-result'])
-    b_src = os.path.join(CSRC, 'bindings.cpp')
-    b_obj = os.path.join(BUILD, 'bindings.cpp.o')
-    objs.append(b_obj)
-    if force or _newer(b_obj, [b_src] + hdrs):
-        jobs_list.append(['g++', '-O2', '-std=c++17', '-fPIC', '-c', b_src, '-o', b_obj,
-                          '-I' + os.path.join(CSRC, 'include'), '-I' + py_inc, '-I' + os.path.join(ROCM, 'include')]
-                         + ['-I' + i for i in tinc]
-                         + ['-D__HIP_PLATFORM_AMD__=1', '-DUSE_ROCM=1', '-DTORCH_EXTENSION_NAME=_C',
-                            '-DTORCH_API_INCLUDE_EXTENSION_H', '-D_GLIBCXX_USE_CXX11_ABI=%d' % abi,
-                            '-Wno-deprecated-declarations'])
+    # host-only TUs against the torch / ROCm headers: the bindings and the native
+    # gradient reducer (c10d process groups, autograd hooks, HIP events)
+    for b_src in (os.path.join(CSRC, 'bindings.cpp'), os.path.join(CSRC, 'native', 'reducer.cpp')):
+        b_obj = os.path.join(BUILD, os.path.basename(b_src) + '.o')
+        objs.append(b_obj)
+        if force or _newer(b_obj, [b_src] + hdrs):
+            jobs_list.append(['g++', '-O2', '-std=c++17', '-fPIC', '-c', b_src, '-o', b_obj,
+                              '-I' + os.path.join(CSRC, 'include'), '-I' + py_inc,
+                              '-I' + os.path.join(ROCM, 'include')]
+                             + ['-I' + i for i in tinc]
+                             + ['-D__HIP_PLATFORM_AMD__=1', '-DUSE_ROCM=1', '-DUSE_C10D_NCCL=1',
+                                '-DUSE_DISTRIBUTED=1', '-DTORCH_EXTENSION_NAME=_C',
+                                '-DTORCH_API_INCLUDE_EXTENSION_H', '-D_GLIBCXX_USE_CXX11_ABI=%d' % abi,
+                                '-Wno-deprecated-declarations'])
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         for out in ex.map(_run, jobs_list):
             if verbose and out.strip():

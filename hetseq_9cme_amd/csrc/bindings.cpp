@@ -616,7 +616,12 @@ void xar_destroy(int64_t h) { hx_xar_destroy(as_ctx(h)); }
 
 }  // namespace
 
+namespace hx {
+void register_reducer(py::module& m);   // csrc/native/reducer.cpp
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  hx::register_reducer(m);
   m.doc() = "hetseq_9cme_amd gfx950 (MI355X) kernels";
   m.def("grad_norm_clip", &grad_norm_clip);
   m.def("adam", &adam);

@@ -154,6 +154,8 @@ def side_begin(device):
     st.wait_stream(torch.cuda.current_stream(idx))
     if not _Side.active:
         torch.autograd.Variable._execution_engine.queue_callback(side_join)
+    if idx not in _Side.active:
+        C().reducer_set_side_stream(st.cuda_stream)   # bucket collectives order after it
     _Side.active.add(idx)
     return st
 
@@ -168,9 +170,12 @@ def active_side_stream(device):
 
 def side_join():
     """Make the compute stream wait for all queued side-stream work."""
+    if not _Side.active:
+        return
     for idx in list(_Side.active):
         torch.cuda.current_stream(idx).wait_stream(_Side.streams[idx])
     _Side.active.clear()
+    C().reducer_set_side_stream(0)
 
 
 # ----------------------------------------------------------------- references

@@ -1,18 +1,20 @@
 """Gradient reducer: bucketed, backward-overlapped all-reduce over RCCL/xGMI.
 
 Replaces ``torch.nn.parallel.DistributedDataParallel`` as used by the
-reference (hetseq/controller.py:75-90):
+reference (hetseq/controller.py:75-90).  The per-parameter
+and per-bucket machinery is native C++ (``csrc/native/reducer.cpp``, class
+``_C.Reducer``); this module plans the buckets and wraps it:
 
 * initial parameter broadcast from rank 0 (one collective over the flat
   parameter buffer instead of DDP's coalesced per-tensor broadcast);
 * buckets are contiguous slices of the flat gradient buffer
   (``FlatParamSpace``), so RCCL all-reduces them in place -- no copy into
   bucket storage and back;
-* a post-accumulate-grad hook per parameter counts readiness; buckets are
+* a C++ post-accumulate-grad hook per parameter counts readiness; buckets are
   launched strictly in index order (identical collective sequence on every
   rank, even with unused parameters) as soon as they fill, overlapping the
   all-reduce with the rest of backward;
-* an end-of-backward callback flushes buckets holding unused parameters
+* an end-of-backward engine callback flushes buckets holding unused parameters
   (``--find-unused-parameters``) and makes the compute stream wait for the
   collectives (no host blocking);
 * ``no_sync()`` accumulates locally for ``--update-freq`` > 1;
@@ -46,7 +48,30 @@ import contextlib
 import torch
 import torch.distributed as dist
 
-from .. import ops
+from ..ops._ext import C
+
+
+def plan_buckets(flat, bucket_cap_mb):
+    """Contiguous buckets over the flat layout (params already reverse-ordered):
+    [(start, end, [param idx])], ends extended to the next bucket's start."""
+    elem = flat.grad_flat.element_size()
+    cap = max(1, int(bucket_cap_mb * 1024 * 1024 / elem))
+    buckets = []
+    cur, cur_start = [], 0
+    for i in range(len(flat.params)):
+        s, e = flat.param_range(i)
+        if cur and (e - cur_start) > cap:
+            end = flat.param_range(cur[-1])[1]
+            buckets.append([cur_start, end, cur])
+            cur, cur_start = [], s
+        cur.append(i)
+    if cur:
+        buckets.append([cur_start, flat.numel, cur])
+    # extend bucket ends to the next bucket start (covers alignment padding)
+    for b in range(len(buckets) - 1):
+        buckets[b][1] = buckets[b + 1][0]
+    buckets[-1][1] = flat.numel
+    return buckets
 
 
 class GradReducer(object):
@@ -56,78 +81,46 @@ class GradReducer(object):
         self.group = process_group
         self.world_size = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.find_unused = find_unused_parameters
-        self.enabled = self.world_size > 1
         self.grad_prescale = 1.0 / self.world_size
-        self._sync = True
-
-        # ---- bucket plan over the flat layout (params already reverse-ordered)
-        elem = flat.grad_flat.element_size()
-        cap = max(1, int(bucket_cap_mb * 1024 * 1024 / elem))
-        buckets = []   # list of (start, end, [param idx])
-        cur, cur_start = [], 0
-        for i in range(len(flat.params)):
-            s, e = flat.param_range(i)
-            if cur and (e - cur_start) > cap:
-                end = flat.param_range(cur[-1])[1]
-                buckets.append([cur_start, end, cur])
-                cur, cur_start = [], s
-            cur.append(i)
-        if cur:
-            buckets.append([cur_start, flat.numel, cur])
-        # extend bucket ends to the next bucket start (covers alignment padding)
-        for b in range(len(buckets) - 1):
-            buckets[b][1] = buckets[b + 1][0]
-        buckets[-1][1] = flat.numel
-        self.buckets = buckets
+        self.buckets = plan_buckets(flat, bucket_cap_mb)
         self.bucket_of = {}
-        for b, (_, _, idxs) in enumerate(buckets):
+        for b, (_, _, idxs) in enumerate(self.buckets):
             for i in idxs:
                 self.bucket_of[i] = b
         self.xgmi = None
-        self._pending = [0] * len(buckets)
-        self.used = [False] * len(flat.params)
-        self._reset_iteration()
-
-        # ---- hooks: only a multi-rank reducer needs to act DURING backward (bucket launches
-        # overlapped with it); a single process finds the used parameters and adopts their
-        # gradients in one scan after backward (``after_backward``) instead of ~200
-        # engine -> Python hook calls per micro-batch (~1 ms of host time per update)
-        self._hooks = []
+        # only a multi-rank reducer needs to act DURING backward (bucket launches overlapped
+        # with it): C++ hooks on every parameter.  A single process finds the used parameters
+        # and adopts their gradients in one scan after backward instead.
         self._hooked = self.world_size > 1
-        self._ver = None
-        if self._hooked:
-            for i, p in enumerate(flat.params):
-                self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
-
+        pg = None
+        if self.world_size > 1:
+            pg = process_group if process_group is not None else dist.group.WORLD
+        bounds = [b[0] for b in self.buckets] + [flat.numel]
+        self._native = C().Reducer(flat.grad_flat, list(flat.params), list(flat.offsets), bounds,
+                                   [self.bucket_of[i] for i in range(len(flat.params))], pg, self.world_size,
+                                   self._hooked)
+        self._enabled = self.world_size > 1
         if self.enabled and broadcast_params:
             dist.broadcast(flat.param_flat, src=0, group=self.group)
 
     # ------------------------------------------------------------------
-    def _reset_iteration(self):
-        self._pending = [len(b[2]) for b in self.buckets]
-        self._launched = 0
-        self._works = []
-        self._callback_queued = False
-        self.used = [False] * len(self.flat.params)
+    @property
+    def enabled(self):
+        return self._enabled
 
-    def _make_hook(self, i):
-        def hook(p):
-            self._on_grad_ready(i)
-        return hook
+    @enabled.setter
+    def enabled(self, flag):
+        # e.g. --use-bmuf: keep the hooks (used flags / slot adoption), never reduce
+        self._enabled = bool(flag) and self.world_size > 1
+        self._native.set_enabled(self._enabled)
 
-    def _on_grad_ready(self, i):
-        if self.used[i]:
-            return  # param accumulated twice in one backward (reentrant use)
-        self.used[i] = True
-        self.flat.adopt(i)   # grad -> its flat slot (no-op when a kernel wrote it there)
-        if not self._callback_queued:
-            self._callback_queued = True
-            torch.autograd.Variable._execution_engine.queue_callback(self._finalize_backward)
-        if not (self.enabled and self._sync):
-            return
-        b = self.bucket_of[i]
-        self._pending[b] -= 1
-        self._launch_ready()
+    @property
+    def used(self):
+        return self._native.used()
+
+    @property
+    def _sync(self):
+        return self._native.sync()
 
     def use_xgmi(self, blocks=64, timeout_s=1800.0):
         """Reduce gradient buckets with the intra-node xGMI kernel (collective call).
@@ -141,6 +134,7 @@ class GradReducer(object):
             return False
         cap_mb = max(b[1] - b[0] for b in self.buckets) * 4 / 2 ** 20
         self.xgmi = XgmiAllReduce(self.group, cap_mb=min(max(cap_mb, 1), 128), blocks=blocks, timeout_s=timeout_s)
+        self._native.use_xgmi(self.xgmi.h, self.xgmi.stream.cuda_stream)
         return True
 
     def check_transport(self):
@@ -154,6 +148,7 @@ class GradReducer(object):
         when buckets go over RCCL."""
         if self.xgmi is None:
             return None
+        torch.cuda.current_stream().wait_stream(self.xgmi.stream)
         return self.xgmi.error_async().double()
 
     def global_used(self, step_used):
@@ -172,101 +167,40 @@ class GradReducer(object):
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return [bool(v) for v in t.tolist()]
 
-    def _launch_ready(self, force=False):
-        while self._launched < len(self.buckets) and (force or self._pending[self._launched] == 0):
-            s, e, _ = self.buckets[self._launched]
-            side = ops.active_side_stream(self.flat.grad_flat.device)
-            if self.xgmi is not None:
-                comm = self.xgmi.stream
-                comm.wait_stream(torch.cuda.current_stream())
-                if side is not None:
-                    comm.wait_stream(side)
-                with torch.cuda.stream(comm):
-                    self.xgmi.all_reduce_(self.flat.grad_flat[s:e])
-                work = None
-            elif side is not None:
-                # weight grads of this bucket may come from the side stream: launch
-                # the collective from it (after the compute stream's work so far)
-                side.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(side):
-                    work = dist.all_reduce(self.flat.grad_flat[s:e], group=self.group, async_op=True)
-            else:
-                work = dist.all_reduce(self.flat.grad_flat[s:e], group=self.group, async_op=True)
-            self._works.append(work)
-            self._launched += 1
-
-    def _finalize_backward(self):
-        ops.side_join()
-        for i, u in enumerate(self.used):
-            if not u:
-                self.flat.adopt(i)   # unused this micro-batch: keep/zero its slot
-        if self.enabled and self._sync:
-            self._launch_ready(force=True)   # unused params: their slices hold zeros
-            if self.xgmi is not None:
-                torch.cuda.current_stream().wait_stream(self.xgmi.stream)
-            for w in self._works:
-                if w is not None:
-                    w.wait()                  # stream-level wait for RCCL, no host block
-        self._works = []
-
     # ------------------------------------------------------------------
     def prepare_for_backward(self):
-        """Called before each micro-batch's forward."""
-        used = self.used
-        self._reset_iteration()
-        if not self._hooked:
-            # gradient versions before this micro-batch: a gradient that already exists
-            # (earlier micro-batch) counts as used again only if backward accumulated into it
-            self._ver = [p.grad._version if p.grad is not None else None for p in self.flat.params]
-        return used
+        """Called before each micro-batch's forward; returns the previous micro-batch's
+        used flags."""
+        return self._native.prepare()
 
     def after_backward(self):
         """Called after each micro-batch's backward. When no gradient hook fired
         (the loss reached no parameter, or the task skipped backward), finalize
         here: unused slots are zeroed and this rank still joins every bucket
         collective the other ranks launch instead of leaving them waiting."""
-        if not self._hooked and self._ver is not None:
-            for i, p in enumerate(self.flat.params):
-                g = p.grad
-                if g is not None and (self._ver[i] is None or g._version != self._ver[i]):
-                    self.used[i] = True
-                    self.flat.adopt(i)    # grad -> its flat slot (no-op when a kernel wrote it there)
-            self._ver = None
-        if not self._callback_queued:
-            self._callback_queued = True
-            self._finalize_backward()
+        self._native.after_backward()
 
     @contextlib.contextmanager
     def no_sync(self):
-        old = self._sync
-        self._sync = False
+        old = self._native.sync()
+        self._native.set_sync(False)
         try:
             yield
         finally:
-            self._sync = old
+            self._native.set_sync(old)
 
     def all_reduce_now(self):
         """Synchronously reduce the whole gradient buffer (used when a rank ran
         no backward this step, e.g. a pure dummy update)."""
         if self.enabled:
-            if self.xgmi is not None:
-                # same stream as the bucket launches: two reductions must never share the
-                # staging buffer concurrently
-                comm = self.xgmi.stream
-                comm.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(comm):
-                    self.xgmi.all_reduce_(self.flat.grad_flat)
-                torch.cuda.current_stream().wait_stream(comm)
-            else:
-                dist.all_reduce(self.flat.grad_flat, group=self.group)
+            self._native.all_reduce_now()
 
     def remove(self):
+        self._native.remove_hooks()
         if self.xgmi is not None:
+            self._native.drop_xgmi()
             self.xgmi.close()
             self.xgmi = None
-        for h in self._hooks:
-            h.remove()
-        self._hooks = []
 
 
 class TransportErrorMonitor(object):

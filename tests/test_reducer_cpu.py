@@ -185,3 +185,89 @@ def test_transport_error_raises_on_every_rank_at_the_same_update():
         p.join(120)
         assert p.exitcode == 0, 'worker failed or hung'
     assert out[0] == out[1] == 6    # update 3's word, checked two updates later (start of update 6)
+
+
+# --------------------------------------------------------------------------------------------
+# Native reducer core (csrc/native/reducer.cpp): C++ post-accumulate hooks launch the bucket
+# all-reduces DURING backward, in index order, reduce in place, and honour no_sync.
+
+def _native_worker(rank, port, out):
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=2)
+    try:
+        from hetseq_9cme_amd.parallel.flat_params import FlatParamSpace
+        from hetseq_9cme_amd.parallel.reducer import GradReducer
+        model = _model()
+        flat = FlatParamSpace(model)
+        red = GradReducer(flat, bucket_cap_mb=0.0002)
+        nb = len(red.buckets)
+        # no Python hooks on the per-parameter path
+        assert all(getattr(p, '_post_accumulate_grad_hooks', None) is None for p in flat.params)
+        seen = []
+
+        class Probe(torch.autograd.Function):
+            """Identity whose backward runs after the LAST layer's params were accumulated
+            and before the FIRST layer's: records how many buckets were already launched."""
+            @staticmethod
+            def forward(ctx, x):
+                return x.view_as(x)
+
+            @staticmethod
+            def backward(ctx, g):
+                seen.append(red._native.launched())
+                return g
+
+        flat.zero_grad()
+        # micro-batch 1 under no_sync: accumulate locally, launch nothing
+        with red.no_sync():
+            red.prepare_for_backward()
+            x1 = torch.randn(5, 8, generator=torch.Generator().manual_seed(20 + rank))
+            model(x1).pow(2).sum().backward()
+            red.after_backward()
+            assert red._native.launched() == 0
+        # micro-batch 2: synchronised
+        red.prepare_for_backward()
+        x2 = torch.randn(5, 8, generator=torch.Generator().manual_seed(40 + rank))
+        h = torch.tanh(model[0](x2))
+        model[2](Probe.apply(h)).pow(2).sum().backward()
+        red.after_backward()
+        out[rank] = (flat.grad_flat.clone(), nb, seen[0], red._native.launched())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_native_reducer_overlap_order_and_no_sync():
+    ctx = mp.get_context('spawn')
+    mgr = ctx.Manager()
+    out = mgr.dict()
+    port = _free_port()
+    procs = [ctx.Process(target=_native_worker, args=(r, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0, 'worker failed or hung'
+    (g0, nb, mid0, end0), (g1, _, mid1, end1) = out[0], out[1]
+    assert torch.equal(g0, g1)
+    # the last layer's bucket(s) were launched while backward was still running
+    assert 1 <= mid0 < nb and 1 <= mid1 < nb
+    assert end0 == nb and end1 == nb
+    # = the SUM over ranks of each rank's two accumulated micro-batches
+    ref = None
+    for r in range(2):
+        m = _model()
+        for seed in (20 + r, 40 + r):
+            m(torch.randn(5, 8, generator=torch.Generator().manual_seed(seed))).pow(2).sum().backward()
+        g = torch.cat([p.grad.reshape(-1) for p in m.parameters()])
+        ref = g if ref is None else ref + g
+    from hetseq_9cme_amd.parallel.flat_params import FlatParamSpace
+    flat = FlatParamSpace(_model())
+    got = torch.cat([g0[o:o + n] for o, n in zip(flat.offsets, flat.sizes)])
+    # the reference in the flat layout's parameter order
+    model_params = list(_model().parameters())
+    sizes = [p.numel() for p in model_params]
+    starts = [sum(sizes[:i]) for i in range(len(sizes))]
+    by_model = [ref[s:s + n] for s, n in zip(starts, sizes)]
+    want = torch.cat([by_model[flat.model_order.index(k)] for k in range(len(flat.params))])
+    assert torch.allclose(got, want, rtol=1e-5, atol=1e-6)

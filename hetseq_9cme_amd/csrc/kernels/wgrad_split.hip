@@ -86,7 +86,11 @@ struct PieceBases {
   const uint16_t* b[3];   // X pieces (same row stride ldb)
 };
 
-template <int BM, int BN, int WM, int WN, int NPC, int NP>
+// AHEAD: token steps staged ahead in registers (2: two register sets; 1: one set, fewer
+// VGPRs -- the bf16x6 256 x 128 tile spills with two).  MORD: work order inside a token
+// split, 0 = output-column tiles fastest, 1 = output-row tiles fastest (the tiles one XCD
+// runs together then share both operands' token slabs in its L2 when M has few row tiles).
+template <int BM, int BN, int WM, int WN, int NPC, int NP, int AHEAD, int MORD>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_split_k(PieceBases P, int lda, int ldb,
                                                                            float* __restrict__ out, int M, int N,
                                                                            int T, int kchunk, int nsplit) {
@@ -103,7 +107,9 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_split_k(Piec
   const int per = (total + 7) / 8;
   const int work = (blockIdx.x % 8) * per + blockIdx.x / 8;
   if (work >= total) return;         // uniform per workgroup
-  const int nt = work % TN, mt = (work / TN) % TM, sp = work / (TN * TM);
+  const int nt = MORD ? (work / TM) % TN : work % TN;
+  const int mt = MORD ? work % TM : (work / TN) % TM;
+  const int sp = work / (TN * TM);
   const int m0 = mt * BM, n0 = nt * BN;
   const int t0 = sp * kchunk, t1 = min(T, t0 + kchunk);
   const int nit = (t1 - t0 + BK - 1) / BK;
@@ -190,20 +196,35 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_split_k(Piec
     }
   };
 
-  load(0, ra0, rb0);
-  load(1, ra1, rb1);
-  store(0, ra0, rb0);
-  __syncthreads();
-  for (int it = 0; it < nit; it += 2) {
-    load(it + 2, ra0, rb0);
-    mma(0);
-    store(1, ra1, rb1);
-    __syncthreads();
-    if (it + 1 >= nit) break;
-    load(it + 3, ra1, rb1);
-    mma(1);
+  if constexpr (AHEAD == 2) {
+    load(0, ra0, rb0);
+    load(1, ra1, rb1);
     store(0, ra0, rb0);
     __syncthreads();
+    for (int it = 0; it < nit; it += 2) {
+      load(it + 2, ra0, rb0);
+      mma(0);
+      store(1, ra1, rb1);
+      __syncthreads();
+      if (it + 1 >= nit) break;
+      load(it + 3, ra1, rb1);
+      mma(1);
+      store(0, ra0, rb0);
+      __syncthreads();
+    }
+  } else {
+    // one register set: step it + 1 is loaded while step it runs on the matrix cores, then
+    // written to the other LDS buffer (last read before the previous barrier)
+    load(0, ra0, rb0);
+    store(0, ra0, rb0);
+    __syncthreads();
+    for (int it = 0; it < nit; ++it) {
+      const int cur = it & 1;
+      if (it + 1 < nit) load(it + 1, ra0, rb0);
+      mma(cur);
+      if (it + 1 < nit) store(cur ^ 1, ra0, rb0);
+      __syncthreads();
+    }
   }
 
   float* o = out + (nsplit > 1 ? (int64_t)sp * M * N : 0);
@@ -232,7 +253,7 @@ __global__ __launch_bounds__(256) void split_sum2_k(const float4* __restrict__ w
   }
 }
 
-template <int BM, int BN, int WM, int WN, int NPC, int NP>
+template <int BM, int BN, int WM, int WN, int NPC, int NP, int AHEAD, int MORD>
 void launch(const PieceBases& P, int lda, int ldb, float* out, float* ws, int M, int N, int T, int nsplit,
             hipStream_t s) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
@@ -243,12 +264,12 @@ void launch(const PieceBases& P, int lda, int ldb, float* out, float* ws, int M,
   const size_t smem = 2 * (size_t)NPC * BK * (BM + BN) * sizeof(uint16_t);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_split_k<BM, BN, WM, WN, NPC, NP>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_split_k<BM, BN, WM, WN, NPC, NP, AHEAD, MORD>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
-  wgrad_split_k<BM, BN, WM, WN, NPC, NP><<<8 * per, NT, smem, s>>>(P, lda, ldb, nsplit > 1 ? ws : out, M, N, T,
-                                                                  kchunk, nsplit);
+  wgrad_split_k<BM, BN, WM, WN, NPC, NP, AHEAD, MORD><<<8 * per, NT, smem, s>>>(
+      P, lda, ldb, nsplit > 1 ? ws : out, M, N, T, kchunk, nsplit);
   if (nsplit > 1) {
     const int64_t n4 = (int64_t)M * N / 4;
     const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
@@ -289,18 +310,42 @@ int hx_wgrad_split(const void* const* dy_pieces, int ldy, const void* const* x_p
     P.a[i] = (const uint16_t*)dy_pieces[i < npc ? i : 0];
     P.b[i] = (const uint16_t*)x_pieces[i < npc ? i : 0];
   }
+  // HX_WGRAD_SPLIT_VAR="ahead,mord" selects a pipeline variant (tools/bench_wgrad.py --split)
+  // default: two register stages; output-row tiles fastest when there are fewer of them
+  // than column tiles (768 x 3072 FFN-down dW: 421 -> 406 us; tools/bench_wgrad.py --split 6
+  // --variants, profiles/r2_wgrad_split_variants.log -- the other variants are within 3 %)
+  int ahead = 2, mord = M < N ? 1 : 0;
+  if (const char* e = getenv("HX_WGRAD_SPLIT_VAR")) {
+    int a = 0, o = 0;
+    if (sscanf(e, "%d,%d", &a, &o) == 2 && (a == 1 || a == 2) && (o == 0 || o == 1)) {
+      ahead = a;
+      mord = o;
+    }
+  }
+#define HX_WS_LAUNCH(BM_, NPC_, NP_)                                                           \
+  do {                                                                                         \
+    if (ahead == 2 && mord == 0)                                                               \
+      launch<BM_, 128, 64, 64, NPC_, NP_, 2, 0>(P, ldy, ldx, out, ws, M, N, T, nsplit, s);     \
+    else if (ahead == 2)                                                                       \
+      launch<BM_, 128, 64, 64, NPC_, NP_, 2, 1>(P, ldy, ldx, out, ws, M, N, T, nsplit, s);     \
+    else if (mord == 0)                                                                        \
+      launch<BM_, 128, 64, 64, NPC_, NP_, 1, 0>(P, ldy, ldx, out, ws, M, N, T, nsplit, s);     \
+    else                                                                                       \
+      launch<BM_, 128, 64, 64, NPC_, NP_, 1, 1>(P, ldy, ldx, out, ws, M, N, T, nsplit, s);     \
+  } while (0)
   if (passes == 3) {
     if (cfg == 1)
-      launch<256, 128, 64, 64, 2, 3>(P, ldy, ldx, out, ws, M, N, T, nsplit, s);
+      HX_WS_LAUNCH(256, 2, 3);
     else
-      launch<128, 128, 64, 64, 2, 3>(P, ldy, ldx, out, ws, M, N, T, nsplit, s);
+      HX_WS_LAUNCH(128, 2, 3);
   } else if (passes == 6) {
     if (cfg == 1)
-      launch<256, 128, 64, 64, 3, 6>(P, ldy, ldx, out, ws, M, N, T, nsplit, s);
+      HX_WS_LAUNCH(256, 3, 6);
     else
-      launch<128, 128, 64, 64, 3, 6>(P, ldy, ldx, out, ws, M, N, T, nsplit, s);
+      HX_WS_LAUNCH(128, 3, 6);
   } else {
     return -1;
   }
+#undef HX_WS_LAUNCH
   return 0;
 }

@@ -288,7 +288,7 @@ Tensor softmax_xent_(Tensor logits, OptT bias, Tensor labels, int64_t ignore_ind
 
 // ------------------------------------------------------------------ attention
 std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed, int64_t stream,
-                             OptT bias) {
+                             OptT bias, bool split = false) {
   check_cuda(qkv, "qkv");
   const int bf = act_bf16(qkv);
   check_f32(mask_bias, "mask_bias");
@@ -308,12 +308,24 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
   const int64_t Sp = (S + 127) / 128 * 128;
   if (keep < 1.0) dmask = torch::empty({B, nh, Sp, Sp / 32}, qkv.options().dtype(torch::kInt32));
   else dmask = torch::empty({0}, qkv.options().dtype(torch::kInt32));
-  hx_attn_fwd(bf, qkv.data_ptr(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(), out.data_ptr(),
-              lse.data_ptr<float>(),
-              keep < 1.0 ? reinterpret_cast<uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr, (int)B, (int)S, (int)nh,
-              (float)keep, seed_ptr(seed), (uint64_t)stream, cur_stream(qkv));
+  uint32_t* dm = keep < 1.0 ? reinterpret_cast<uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr;
+  if (split) {
+    TORCH_CHECK(!bf, "attn_fwd_x6: fp32 activations only");
+    hx_attn_fwd_x6(qkv.data_ptr<float>(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(),
+                   out.data_ptr<float>(), lse.data_ptr<float>(), dm, (int)B, (int)S, (int)nh, (float)keep,
+                   seed_ptr(seed), (uint64_t)stream, cur_stream(qkv));
+  } else {
+    hx_attn_fwd(bf, qkv.data_ptr(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(), out.data_ptr(),
+                lse.data_ptr<float>(), dm, (int)B, (int)S, (int)nh, (float)keep, seed_ptr(seed), (uint64_t)stream,
+                cur_stream(qkv));
+  }
   dbg_finite(out, "attn_fwd");
   return {out, lse, dmask};
+}
+// fp32 attention forward on the bf16 matrix cores (split pieces, attention_x6.hip)
+std::vector<Tensor> attn_fwd_x6(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed,
+                                int64_t stream, OptT bias) {
+  return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, true);
 }
 
 // returns {dqkv, dbias} (dbias: [3H] fp32 when bias is given -- written into dbq/dbk/dbv
@@ -635,7 +647,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum", &colsum);
   m.def("dropout", &dropout);
   m.def("softmax_xent_", &softmax_xent_);
-  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_fwd", [](Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed, int64_t stream,
+                        OptT bias) { return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, false); });
+  m.def("attn_fwd_x6", &attn_fwd_x6);
   m.def("attn_bwd", &attn_bwd);
   m.def("wgrad_bf16", &wgrad_bf16);
   m.def("wgrad_bf16_ok", &wgrad_bf16_ok);

@@ -56,6 +56,10 @@ void hx_attn_bwd_bf16(const void* qkv, const float* bias, float* dbias_part, con
 void hx_wgrad_bf16_plan(int M, int N, int T, int* cfg, int* nsplit);
 void hx_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, float* out, float* ws, int M, int N, int T,
                    int cfg, int nsplit, hipStream_t s);
+// attention_x6.hip -- fp32 attention forward on bf16 MFMA with split pieces (bf16x6 class)
+void hx_attn_fwd_x6(const float* qkv, const float* bias, const float* maskb, float* out, float* lse,
+                    uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream,
+                    hipStream_t s);
 void hx_attn_fwd(int bf16, const void* qkv, const float* bias, const float* maskb, void* out, float* lse,
                  uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream, hipStream_t s);
 // dq_acc: fp32 dQ accumulation target when S > 128 (atomics; row stride dq_ld), else unused.

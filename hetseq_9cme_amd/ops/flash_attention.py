@@ -7,7 +7,9 @@ to [B, S, H].  The additive mask is the reference's (1 - m) * -10000 (not -inf).
 GPU path: the fused flash-style HIP kernel (``_C.attn_fwd`` / ``attn_bwd``,
 csrc/kernels/attention.hip) for head_dim 64 at any sequence length (keys past
 S are masked, rows past S are neither computed into nor stored), with fp32 or
-bf16 activations (bf16 is converted at load; the math is fp32 MFMA either way);
+bf16 activations (bf16 activations: bf16 MFMA, attention_bf16.hip; fp32 activations: fp32
+MFMA, or -- under ``--fp32-gemm bf16x3/x6`` -- the forward's products as six bf16 piece passes,
+attention_x6.hip, fp32-exact class);
 other shapes / dtypes use the composite below (batched GEMMs + softmax), which
 is also the CPU path and the test oracle.
 """
@@ -16,6 +18,7 @@ import math
 import torch
 import torch.nn.functional as F
 
+from . import split_gemm
 from ._ext import C, use_kernels
 from .rng import get_rng
 
@@ -70,7 +73,11 @@ class _AttnFn(torch.autograd.Function):
         keep = 1.0 - p
         seed, stream = get_rng().next(qkv.device) if p > 0 else (get_rng().seed_tensor(qkv.device), 0)
         bias = _bias3(bq, bk, bv).float().contiguous() if bq is not None else None
-        out, lse, dmask = C().attn_fwd(qkv, mask_bias, num_heads, keep, seed, stream, bias)
+        if qkv.dtype == torch.float32 and split_gemm.passes() > 0:
+            # fp32 products on the bf16 matrix cores (six piece passes, attention_x6.hip)
+            out, lse, dmask = C().attn_fwd_x6(qkv, mask_bias, num_heads, keep, seed, stream, bias)
+        else:
+            out, lse, dmask = C().attn_fwd(qkv, mask_bias, num_heads, keep, seed, stream, bias)
         ctx.save_for_backward(qkv, mask_bias, out, lse, dmask)
         ctx.bias = bias
         ctx.bparams = (bq, bk, bv)

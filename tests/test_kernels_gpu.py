@@ -537,3 +537,38 @@ def test_wgrad_bf16_kernel(dev, M, N, T):
     C().wgrad_bf16(dy, x, out)
     ref = dy.float().t() @ x.float()
     torch.testing.assert_close(out, ref, rtol=1e-4, atol=1e-3 * (T ** 0.5))
+
+
+@pytest.mark.parametrize('S,with_bias,keep', [(128, False, 0.9), (77, True, 0.9), (200, False, 1.0),
+                                              (512, True, 0.9), (640, True, 0.9)])
+def test_attention_x6_forward_fp32_exact_class(dev, S, with_bias, keep):
+    """fp32 attention forward on bf16 MFMA with split pieces (attention_x6.hip): against an
+    fp64 reference (same dropout bits) the error is in the fp32 kernel's class, and the
+    dropout bitmask is bit-identical to the fp32 kernel's (same Philox counters)."""
+    from hetseq_9cme_amd.ops._ext import C
+    torch.manual_seed(0)
+    B, nh, d = 2, 4, 64
+    H = nh * d
+    qkv = 2 * torch.randn(B, S, 3 * H, device=dev)
+    bias = (0.5 * torch.randn(3 * H, device=dev)) if with_bias else None
+    mask = torch.ones(B, S, device=dev)
+    mask[0, S - 37:] = 0
+    mb = ((1 - mask) * -10000.0).contiguous()
+    out, lse, dm = C().attn_fwd_x6(qkv, mb, nh, keep, _seed(dev, 1234), 7, bias)
+    out32, lse32, dm32 = C().attn_fwd(qkv, mb, nh, keep, _seed(dev, 1234), 7, bias)
+    assert torch.equal(dm, dm32)
+    x = qkv.double() + (bias.double() if bias is not None else 0)
+    q = x.view(B, S, 3, nh, d).permute(2, 0, 3, 1, 4)
+    sc = q[0] @ q[1].transpose(-1, -2) / 8.0 + mb.double()[:, None, None, :]
+    p = torch.softmax(sc, -1)
+    if keep < 1.0:
+        bits = dm.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+        Sp = dm.shape[2]
+        km = ((bits.unsqueeze(-1) >> torch.arange(32, device=dev)) & 1).reshape(B, nh, Sp, Sp)
+        p = p * km[:, :, :S, :S].transpose(-1, -2).double() / keep
+    ref = (p @ q[2]).permute(0, 2, 1, 3).reshape(B, S, H)
+    scale = (p.abs() @ q[2].abs()).permute(0, 2, 1, 3).reshape(B, S, H)
+    err_x6 = ((out.double() - ref).abs() / scale).max().item()
+    err_32 = ((out32.double() - ref).abs() / scale).max().item()
+    assert err_x6 < 4 * max(err_32, 1e-7), (err_x6, err_32)
+    assert (lse.double() - torch.logsumexp(sc, -1)).abs().max().item() < 1e-4

@@ -157,9 +157,47 @@ std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tens
             gamma.data_ptr<float>(), dz.data_ptr(), want_dy ? dy.data_ptr() : nullptr, partial.data_ptr<float>(), nblk,
             rows, H, (float)keep_prob, seed_ptr(seed), (uint64_t)stream, drop_after ? 1 : 0,
             (want_dy && want_dbias) ? 1 : 0, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
-            want_dbias ? dbias.data_ptr<float>() : nullptr, 0, cur_stream(z));
+            want_dbias ? dbias.data_ptr<float>() : nullptr, 0, nullptr, 0, 0, 0, cur_stream(z));
   dbg_finite(dz, "ln_bwd (dz)");
   return {dz, dy, dgamma, dbeta, dbias};
+}
+
+// LN backward whose dy (= dz * dropout mask / keep) leaves as bf16 split planes [rows, npl * H]
+// for the upstream linear's split-GEMM backward (--fp32-gemm bf16x3/x6): {dz, planes, dgamma,
+// dbeta, dbias}
+std::vector<Tensor> ln_bwd_planes(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tensor gamma, double keep_prob,
+                                  const Tensor& seed, int64_t stream, bool want_dbias, std::vector<int64_t> order,
+                                  int64_t npieces, OptT dgamma_out, OptT dbeta_out, OptT dbias_out) {
+  check_f32(dout, "grad_output");
+  check_f32(z, "saved input");
+  TORCH_CHECK(npieces == 2 || npieces == 3, "ln_bwd_planes: 2 or 3 pieces");
+  TORCH_CHECK(!order.empty() && order.size() <= 8, "ln_bwd_planes: 1..8 planes");
+  uint32_t packed = 0;
+  for (size_t k = 0; k < order.size(); ++k) {
+    TORCH_CHECK(order[k] >= 0 && order[k] < npieces, "ln_bwd_planes: piece index out of range");
+    packed |= (uint32_t)order[k] << (4 * k);
+  }
+  const int H = (int)z.size(-1);
+  TORCH_CHECK(H % 4 == 0, "ln_bwd_planes: H must be a multiple of 4");
+  const int64_t rows = z.numel() / H, npl = (int64_t)order.size();
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(z.device());
+  auto dz = torch::empty_like(z);
+  auto planes = torch::empty({rows, npl * H}, z.options().dtype(torch::kBFloat16));
+  auto f32 = z.options();
+  auto dgamma = has(dgamma_out) ? *dgamma_out : torch::empty({H}, f32);
+  auto dbeta = has(dbeta_out) ? *dbeta_out : torch::empty({H}, f32);
+  Tensor dbias = want_dbias ? (has(dbias_out) ? *dbias_out : torch::empty({H}, f32)) : Tensor();
+  TORCH_CHECK(dgamma.numel() == H && dbeta.numel() == H && dgamma.is_contiguous() && dbeta.is_contiguous(),
+              "bad dgamma/dbeta outputs");
+  const int nblk = hx_ln_bwd_blocks(rows);
+  auto partial = torch::empty({(int64_t)nblk * 3 * H}, f32);
+  hx_ln_bwd(0, dout.data_ptr(), z.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), gamma.data_ptr<float>(),
+            dz.data_ptr(), nullptr, partial.data_ptr<float>(), nblk, rows, H, (float)keep_prob, seed_ptr(seed),
+            (uint64_t)stream, 0, want_dbias ? 1 : 0, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
+            want_dbias ? dbias.data_ptr<float>() : nullptr, 0, reinterpret_cast<uint16_t*>(planes.data_ptr()),
+            packed, (int)npl, (int)npieces, cur_stream(z));
+  dbg_finite(dz, "ln_bwd_planes (dz)");
+  return {dz, planes, dgamma, dbeta, dbias};
 }
 
 std::vector<Tensor> embed_ln_fwd(Tensor ids, OptT tt, Tensor wte, Tensor wpe, Tensor wtt, Tensor gamma, Tensor beta,
@@ -640,6 +678,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adadelta", &adadelta);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);
+  m.def("ln_bwd_planes", &ln_bwd_planes);
   m.def("embed_ln_fwd", &embed_ln_fwd);
   m.def("embed_word_grad", &embed_word_grad);
   m.def("bias_act_fwd", &bias_act_fwd);

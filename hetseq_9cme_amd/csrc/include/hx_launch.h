@@ -23,7 +23,8 @@ void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, cons
 void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma,
                void* dz, void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
                uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
-               int accumulate, hipStream_t s);
+               int accumulate, uint16_t* planes, uint32_t order, int npl, int npc, hipStream_t s);
+// (planes != nullptr: dy is written as bf16 split planes [rows][npl][H] instead of to dy)
 void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,
                      const float* wtt, const float* gamma, const float* beta, void* out, void* zsave, float* mean,
                      float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, const uint64_t* seed,

@@ -120,7 +120,8 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
                                              const float* __restrict__ gamma, T* __restrict__ dz_out,
                                              T* __restrict__ dy_out, float* __restrict__ partial, int64_t rows,
                                              int H, float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream,
-                                             int want_dbias) {
+                                             int want_dbias, uint16_t* __restrict__ planes, uint32_t order, int npl,
+                                             int npc) {
   const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   __shared__ float red[WPB][CH * 256];
   const int lane = threadIdx.x & 63;
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
         float4 dz = make_float4(rstd * (dv.x - m1 - xv.x * m2), rstd * (dv.y - m1 - xv.y * m2),
                                 rstd * (dv.z - m1 - xv.z * m2), rstd * (dv.w - m1 - xv.w * m2));
         hx::store4(dz_out + r * H + j, dz);
-        if (dy_out) {
+        if (dy_out || planes) {
           float4 dy = dz;
           if (drop && !kDropAfter) {
             const uint32_t k = hx::keep4(seed, stream, (uint64_t)(r * H + j) >> 2, keep_prob);
@@ -206,7 +207,29 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
             dy.z = (k & 4) ? dy.z * inv_keep : 0.f;
             dy.w = (k & 8) ? dy.w * inv_keep : 0.f;
           }
-          hx::store4(dy_out + r * H + j, dy);
+          if (planes) {
+            // --fp32-gemm bf16x3/x6: dy goes straight out as the consumer linear's bf16
+            // gradient planes [row][npl][H] (piece order[k] in plane k), no fp32 dy pass
+            float e[4] = {dy.x, dy.y, dy.z, dy.w};
+            uint2 pw[3];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+              uint16_t q[4];
+#pragma unroll
+              for (int t = 0; t < 4; ++t) {
+                q[t] = hx::f2bf(e[t]);
+                e[t] -= hx::bf2f(q[t]);
+              }
+              pw[k] = make_uint2(q[0] | ((uint32_t)q[1] << 16), q[2] | ((uint32_t)q[3] << 16));
+            }
+            uint16_t* o = planes + r * npl * H + j;
+            for (int k = 0; k < npl; ++k) {
+              const int pc = (order >> (4 * k)) & 15;
+              *reinterpret_cast<uint2*>(o + (int64_t)k * H) = pw[pc < npc ? pc : npc - 1];
+            }
+          } else {
+            hx::store4(dy_out + r * H + j, dy);
+          }
           if (want_dbias) {
             dbias.v[c].x += dy.x; dbias.v[c].y += dy.y; dbias.v[c].z += dy.z; dbias.v[c].w += dy.w;
           }
@@ -421,14 +444,16 @@ template <typename T>
 void ln_bwd_t(const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma, void* dz,
               void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
               uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
-              int accumulate, hipStream_t s) {
+              int accumulate, uint16_t* planes, uint32_t order, int npl, int npc, hipStream_t s) {
   HX_CH_DISPATCH(H, {
     if (drop_after)
       ln_bwd_k<T, CH, true><<<nblk, NT, 0, s>>>((const T*)dout, (const T*)z, mean, rstd, gamma, (T*)dz, (T*)dy,
-                                                partial, rows, H, keep_prob, seed, stream, want_dbias);
+                                                partial, rows, H, keep_prob, seed, stream, want_dbias, planes, order,
+                                                npl, npc);
     else
       ln_bwd_k<T, CH, false><<<nblk, NT, 0, s>>>((const T*)dout, (const T*)z, mean, rstd, gamma, (T*)dz, (T*)dy,
-                                                 partial, rows, H, keep_prob, seed, stream, want_dbias);
+                                                 partial, rows, H, keep_prob, seed, stream, want_dbias, planes, order,
+                                                 npl, npc);
   })
   // partial is [nblk][3][H]: fold rows of length 3H into dgamma | dbeta | dbias
   hx::fold_rows(partial, nblk, 3 * (int64_t)H, (want_dbias ? 3 : 2) * H, H, dgamma, dbeta,
@@ -453,13 +478,13 @@ void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, cons
 void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma,
                void* dz, void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
                uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
-               int accumulate, hipStream_t s) {
+               int accumulate, uint16_t* planes, uint32_t order, int npl, int npc, hipStream_t s) {
   if (bf16)
     ln_bwd_t<uint16_t>(dout, z, mean, rstd, gamma, dz, dy, partial, nblk, rows, H, keep_prob, seed, stream,
-                       drop_after, want_dbias, dgamma, dbeta, dbias, accumulate, s);
+                       drop_after, want_dbias, dgamma, dbeta, dbias, accumulate, planes, order, npl, npc, s);
   else
     ln_bwd_t<float>(dout, z, mean, rstd, gamma, dz, dy, partial, nblk, rows, H, keep_prob, seed, stream, drop_after,
-                    want_dbias, dgamma, dbeta, dbias, accumulate, s);
+                    want_dbias, dgamma, dbeta, dbias, accumulate, planes, order, npl, npc, s);
 }
 
 void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,

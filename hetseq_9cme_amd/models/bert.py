@@ -208,10 +208,11 @@ class BertSelfOutput(nn.Module):
         self.dropout = nn.Dropout(config.hidden_dropout_prob)
 
     def forward(self, hidden_states, input_tensor, res_grad=None):
-        y = ops.linear(hidden_states, self.dense.weight)
+        gp = ops.GradPlanes()   # the LN backward hands the dense layer its gradient planes
+        y = ops.linear(hidden_states, self.dense.weight, grad_planes=gp)
         return ops.bias_dropout_residual_ln(y, self.dense.bias, input_tensor, self.LayerNorm.weight,
                                             self.LayerNorm.bias, self.LayerNorm.variance_epsilon,
-                                            self.dropout.p, self.training, res_grad=res_grad)
+                                            self.dropout.p, self.training, res_grad=res_grad, grad_planes=gp)
 
 
 class BertAttention(nn.Module):
@@ -243,13 +244,15 @@ class BertOutput(nn.Module):
         self.dropout = nn.Dropout(config.hidden_dropout_prob)
 
     def forward(self, hidden_states, input_tensor, res_grad=None):
-        return self.finish(ops.linear(hidden_states, self.dense.weight), input_tensor, res_grad)
+        gp = ops.GradPlanes()
+        return self.finish(ops.linear(hidden_states, self.dense.weight, grad_planes=gp), input_tensor, res_grad, gp)
 
-    def finish(self, y, input_tensor, res_grad=None):
+    def finish(self, y, input_tensor, res_grad=None, grad_planes=None):
         """dense bias -> dropout -> + residual -> LayerNorm on the bias-less projection ``y``."""
         return ops.bias_dropout_residual_ln(y, self.dense.bias, input_tensor, self.LayerNorm.weight,
                                             self.LayerNorm.bias, self.LayerNorm.variance_epsilon,
-                                            self.dropout.p, self.training, res_grad=res_grad)
+                                            self.dropout.p, self.training, res_grad=res_grad,
+                                            grad_planes=grad_planes)
 
 
 class BertLayer(nn.Module):
@@ -265,8 +268,9 @@ class BertLayer(nn.Module):
         up = self.intermediate.dense_act
         if up.act == 'gelu' and ops.ffn_fusable(attention_output, up.weight, up.bias, self.output.dense.weight):
             # --fp32-gemm bf16x3/x6: the GELU epilogue hands the FFN-down GEMM its bf16 planes
-            y = ops.ffn(attention_output, up.weight, up.bias, self.output.dense.weight, rg)
-            return self.output.finish(y, attention_output, rg)
+            gp = ops.GradPlanes()
+            y = ops.ffn(attention_output, up.weight, up.bias, self.output.dense.weight, rg, gp)
+            return self.output.finish(y, attention_output, rg, gp)
         return self.output(self.intermediate(attention_output, rg), attention_output, rg)
 
 

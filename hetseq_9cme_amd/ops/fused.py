@@ -89,6 +89,35 @@ class ResidualGrad(object):
         return g, None
 
 
+class GradPlanes(object):
+    """Per-forward mailbox that hands a linear its OUTPUT gradient already split.
+
+    Under ``--fp32-gemm bf16x3/x6`` the backward of a linear whose output feeds a fused
+    bias + dropout + residual + LayerNorm (BertSelfOutput / BertOutput) starts by
+    splitting the fp32 output gradient dy into bf16 planes.  Instead the LayerNorm
+    backward (which runs first) writes those planes directly (``ln_bwd_planes``: no fp32
+    dy written and read back, one launch less) and deposits them here; the LayerNorm
+    returns a zero-storage placeholder as dy, which the linear never reads.  The linear's
+    forward sets ``want`` only when its backward will take the split-plane path.
+    """
+    __slots__ = ('want', 'planes')
+
+    def __init__(self):
+        self.want = False
+        self.planes = None
+
+    def take(self):
+        p, self.planes = self.planes, None
+        return p
+
+
+def _dy_planes(gp, dy2):
+    """Output-gradient planes of a split-path linear: the LayerNorm's deposit if there is
+    one, else split here."""
+    p = gp.take() if gp is not None else None
+    return p if p is not None else split_gemm.grad_planes(dy2.float())
+
+
 def _dgrad(dy2, W, xshape, mbox):
     """dx = dy2 @ W, accumulated into the deposited residual gradient if any."""
     Wc = cast_w(W, dy2.dtype)
@@ -278,13 +307,15 @@ def embed_ln(ids, tt, wte, wpe, wtt, gamma, beta, eps, p, training, out_dtype=to
 # ----------------------------------------------------------------- bias + dropout + residual + LN
 class _BiasDropResLNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y, bias, res, gamma, beta, eps, p, mbox):
+    def forward(ctx, y, bias, res, gamma, beta, eps, p, mbox, gp):
         keep = 1.0 - p
         seed, stream = get_rng().next(y.device) if p > 0 else (get_rng().seed_tensor(y.device), 0)
         out, z, mean, rstd = C().ln_fwd(y, bias, res, gamma, beta, eps, keep, seed, stream, False, True)
         ctx.save_for_backward(z, mean, rstd, gamma)
         ctx.params = (bias, beta)
         ctx.mbox = mbox
+        ctx.gp = gp
+        ctx.yshape = y.shape
         ctx.meta = (keep, seed, stream, bias is not None, res is not None, y.numel() != z.numel())
         return out
 
@@ -294,25 +325,37 @@ class _BiasDropResLNFn(torch.autograd.Function):
         keep, seed, stream, has_bias, has_res, _ = ctx.meta
         bias, beta = ctx.params
         need_dy = has_bias or keep < 1.0
-        dz, dy, dgamma, dbeta, dbias = C().ln_bwd(dout.contiguous(), z, mean, rstd, gamma, keep, seed, stream,
-                                                  False, need_dy, has_bias, grad_slot(gamma), grad_slot(beta),
-                                                  grad_slot(bias) if has_bias else None)
-        dy_ret = dy if need_dy else dz
+        gp = ctx.gp
+        if gp is not None and gp.want and need_dy and z.dtype == torch.float32:
+            # the upstream split-path linear gets dy as bf16 planes; autograd gets a
+            # zero-storage placeholder of dy's shape that nothing reads
+            n = split_gemm.passes()
+            dz, planes, dgamma, dbeta, dbias = C().ln_bwd_planes(
+                dout.contiguous(), z, mean, rstd, gamma, keep, seed, stream, has_bias, list(split_gemm.ORDER_Q[n]),
+                split_gemm.PIECES[n], grad_slot(gamma), grad_slot(beta), grad_slot(bias) if has_bias else None)
+            gp.planes = planes
+            dy_ret = torch.zeros((), dtype=z.dtype, device=z.device).expand(ctx.yshape)
+        else:
+            dz, dy, dgamma, dbeta, dbias = C().ln_bwd(dout.contiguous(), z, mean, rstd, gamma, keep, seed, stream,
+                                                      False, need_dy, has_bias, grad_slot(gamma), grad_slot(beta),
+                                                      grad_slot(bias) if has_bias else None)
+            dy_ret = dy if need_dy else dz
         dres = dz if has_res else None
         # dz is a private buffer only when dy is separate: then it can become the
         # accumulator of the consumer linear's dgrad GEMM
         if dres is not None and need_dy and ctx.mbox is not None and ctx.mbox.deposit(dz):
             dres = None
-        return dy_ret, (dbias if has_bias else None), dres, dgamma, dbeta, None, None, None
+        return dy_ret, (dbias if has_bias else None), dres, dgamma, dbeta, None, None, None, None
 
 
-def bias_dropout_residual_ln(y, bias, res, gamma, beta, eps, p, training, res_grad=None):
+def bias_dropout_residual_ln(y, bias, res, gamma, beta, eps, p, training, res_grad=None, grad_planes=None):
     """LN(dropout(y + bias) + res)  (BertSelfOutput / BertOutput, bert_modeling.py:387-391).
-    ``res_grad``: a ``ResidualGrad`` shared with the linear that also consumed ``res``."""
+    ``res_grad``: a ``ResidualGrad`` shared with the linear that also consumed ``res``;
+    ``grad_planes``: a ``GradPlanes`` shared with the linear that produced ``y``."""
     p = p if training else 0.0
     if use_kernels(y):
         return _BiasDropResLNFn.apply(y.contiguous(), bias, None if res is None else res.contiguous(), gamma, beta,
-                                      float(eps), float(p), res_grad)
+                                      float(eps), float(p), res_grad, grad_planes)
     x = y if bias is None else y + bias
     x = F.dropout(x, p, training)
     if res is not None:
@@ -387,10 +430,13 @@ class _LinearFn(torch.autograd.Function):
     kernel) straight into the parameters' flat gradient slots."""
 
     @staticmethod
-    def forward(ctx, x, W, b, mbox):
+    def forward(ctx, x, W, b, mbox, gp):
         x2 = x.reshape(-1, x.shape[-1])
         ctx.split = split_gemm.active(x2)
         ctx.pieces = ctx.split and split_gemm.nt_ok(W.shape[1], W.shape[0])
+        ctx.gp = gp if (ctx.split and not ctx.pieces and b is None) else None
+        if ctx.gp is not None:
+            ctx.gp.want = True
         Wsave = W
         if ctx.pieces:    # fp32 on bf16 matrix cores, hand-written piece GEMMs
             x2 = split_gemm.pieces(x2)
@@ -421,7 +467,7 @@ class _LinearFn(torch.autograd.Function):
         if ctx.pieces:
             dys = split_gemm.pieces(dy2.float())
         else:
-            dys = split_gemm.grad_planes(dy2.float()) if ctx.split else None
+            dys = _dy_planes(ctx.gp, dy2) if ctx.split else None
         if not ctx.needs_input_grad[0]:
             dx = None
         elif ctx.pieces:
@@ -451,14 +497,14 @@ class _LinearFn(torch.autograd.Function):
             x2.record_stream(side)
             if dys is not None:
                 dys.record_stream(side)
-        return dx, dW, db, None
+        return dx, dW, db, None, None
 
 
-def linear(x, W, b=None, res_grad=None):
+def linear(x, W, b=None, res_grad=None, grad_planes=None):
     """F.linear with direct-to-slot weight/bias gradients on the GPU;
-    ``res_grad``: see ``ResidualGrad``."""
+    ``res_grad``: see ``ResidualGrad``; ``grad_planes``: see ``GradPlanes``."""
     if use_kernels(x):
-        return _LinearFn.apply(x, W, b, res_grad)
+        return _LinearFn.apply(x, W, b, res_grad, grad_planes)
     return F.linear(x, cast_w(W, x.dtype), cast_w(b, x.dtype))
 
 
@@ -471,9 +517,12 @@ class _FFNSplitFn(torch.autograd.Function):
     traffic per layer at BERT-base phase-1 sizes)."""
 
     @staticmethod
-    def forward(ctx, x, W1, b1, W2, mbox):
+    def forward(ctx, x, W1, b1, W2, mbox, gp):
         x2 = x.reshape(-1, x.shape[-1])
         ctx.pieces = split_gemm.nt_ok(W1.shape[1], W1.shape[0]) and split_gemm.nt_ok(W2.shape[1], W2.shape[0])
+        ctx.gp = gp if not ctx.pieces else None
+        if ctx.gp is not None:
+            ctx.gp.want = True
         if ctx.pieces:
             xs = split_gemm.pieces(x2)
             w1f, w1t = split_gemm.weight_pieces(W1)
@@ -504,8 +553,8 @@ class _FFNSplitFn(torch.autograd.Function):
             dy1s, db1 = split_gemm.act_grad_pieces(dh, y1, b1, 'gelu', grad_slot(b1))
             dx = _dgrad_pieces(dy1s, w1, ctx.xshape, ctx.mbox)
             dW1 = split_gemm.wgrad_pieces(dy1s, xs, W1.shape[0], W1.shape[1], grad_slot(W1))
-            return dx, dW1, db1, dW2, None
-        dys = split_gemm.grad_planes(dy2.float())
+            return dx, dW1, db1, dW2, None, None
+        dys = _dy_planes(ctx.gp, dy2)
         dh = split_gemm.dgrad(dys, W2)
         slot2, slot1 = grad_slot(W2), grad_slot(W1)
         # --overlap-wgrad: the two weight-gradient GEMMs run on the side stream, beside the
@@ -524,7 +573,7 @@ class _FFNSplitFn(torch.autograd.Function):
         if side is not None:
             dy1s.record_stream(side)
             xs.record_stream(side)
-        return dx, dW1, db1, dW2, None
+        return dx, dW1, db1, dW2, None, None
 
 
 def ffn_fusable(x, W1, b1, W2):
@@ -532,9 +581,9 @@ def ffn_fusable(x, W1, b1, W2):
     return split_gemm.active(x) and b1 is not None and W1.shape[0] % 8 == 0 and x.shape[-1] % 8 == 0
 
 
-def ffn(x, W1, b1, W2, res_grad=None):
+def ffn(x, W1, b1, W2, res_grad=None, grad_planes=None):
     """gelu(x W1^T + b1) W2^T (the output bias / dropout / residual / LayerNorm follow)."""
-    return _FFNSplitFn.apply(x, W1, b1, W2, res_grad)
+    return _FFNSplitFn.apply(x, W1, b1, W2, res_grad, grad_planes)
 
 
 # ----------------------------------------------------------------- fused Q/K/V projection

@@ -273,3 +273,84 @@ def test_piece_gemm_kernels(dev, mode, tol):
     ref = acc0.double() + dyd @ Wd
     e = ((acc.double() - ref).abs() / (acc0.double().abs() + dyd.abs() @ Wd.abs())).max().item()
     assert e < tol, ('dgrad', e)
+
+
+@pytest.mark.parametrize('mode,has_bias,keep', [('bf16x6', True, 0.9), ('bf16x3', False, 1.0), ('bf16x6', False, 0.9)])
+def test_ln_bwd_planes_equal_split_of_dy(dev, mode, has_bias, keep):
+    """LayerNorm backward writing dy as the upstream linear's gradient planes: bit-identical
+    to splitting the fp32 dy of the plain backward, same dz / dgamma / dbeta / dbias."""
+    from hetseq_9cme_amd import ops
+    from hetseq_9cme_amd.ops import split_gemm
+    from hetseq_9cme_amd.ops._ext import C
+    ops.set_fp32_gemm(mode)
+    try:
+        torch.manual_seed(3)
+        T, H = 300, 768
+        y = torch.randn(T, H, device=dev)
+        res = torch.randn(T, H, device=dev)
+        bias = torch.randn(H, device=dev) if has_bias else None
+        gamma = torch.rand(H, device=dev) + 0.5
+        beta = torch.randn(H, device=dev)
+        seed = torch.tensor([1234], dtype=torch.int64, device=dev)
+        out, z, mean, rstd = C().ln_fwd(y, bias, res, gamma, beta, 1e-12, keep, seed, 5, False, True)
+        dout = torch.randn_like(out)
+        dz, dy, dg, db, dbias = C().ln_bwd(dout, z, mean, rstd, gamma, keep, seed, 5, False, True, has_bias,
+                                          None, None, None)
+        n = split_gemm.passes()
+        dz2, planes, dg2, db2, dbias2 = C().ln_bwd_planes(dout, z, mean, rstd, gamma, keep, seed, 5, has_bias,
+                                                          list(split_gemm.ORDER_Q[n]), split_gemm.PIECES[n],
+                                                          None, None, None)
+        ref = split_gemm.grad_planes(dy)
+        assert planes.shape == ref.shape
+        assert torch.equal(planes.view(torch.int16), ref.view(torch.int16))
+        assert torch.equal(dz, dz2) and torch.equal(dg, dg2) and torch.equal(db, db2)
+        if has_bias:
+            assert torch.equal(dbias, dbias2)
+    finally:
+        ops.set_fp32_gemm('native')
+
+
+def test_grad_planes_handoff_in_bert_layer(dev):
+    """A BERT layer under bf16x6 takes the LayerNorm -> linear gradient-plane hand-off, and
+    its gradients equal those of the same layer with the hand-off disabled (to fp32
+    atomic-order noise)."""
+    from hetseq_9cme_amd import ops
+    from hetseq_9cme_amd.models.bert import BertConfig, BertLayer
+    from hetseq_9cme_amd.ops import fused
+    ops.set_fp32_gemm('bf16x6')
+    try:
+        torch.manual_seed(0)
+        cfg = BertConfig(100, hidden_size=128, num_hidden_layers=1, num_attention_heads=2, intermediate_size=512,
+                         hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+        layer = BertLayer(cfg).to(dev)
+        x = torch.randn(4, 64, 128, device=dev, requires_grad=True)
+        mb = torch.zeros(4, 64, device=dev)
+        calls = []
+        orig = fused._dy_planes
+
+        def spy(gp, dy2):
+            calls.append(gp is not None and gp.planes is not None)
+            return orig(gp, dy2)
+        fused._dy_planes = spy
+        try:
+            layer(x, mb).pow(2).sum().backward()
+        finally:
+            fused._dy_planes = orig
+        assert calls and all(calls), calls
+        g1 = [p.grad.clone() for p in layer.parameters()] + [x.grad.clone()]
+        for p in layer.parameters():
+            p.grad = None
+        x.grad = None
+        orig_cls = fused.GradPlanes
+        fused.GradPlanes = lambda: None
+        ops.GradPlanes = fused.GradPlanes
+        try:
+            layer(x, mb).pow(2).sum().backward()
+        finally:
+            fused.GradPlanes = orig_cls
+            ops.GradPlanes = orig_cls
+        g2 = [p.grad.clone() for p in layer.parameters()] + [x.grad.clone()]
+        for a, b in zip(g1, g2):
+            assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)
+    finally:
+        ops.set_fp32_gemm('native')

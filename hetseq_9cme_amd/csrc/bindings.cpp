@@ -432,7 +432,9 @@ Tensor wgrad_bf16(Tensor dy, Tensor x, Tensor out) {
               "with M, N multiples of 128 and 16-byte rows)");
   check_f32(out, "wgrad out");
   const int64_t T = dy.size(0), M = dy.size(1), N = x.size(1);
-  TORCH_CHECK(out.size(0) == M && out.size(1) == N, "wgrad out must be [M, N]");
+  // out may hold fewer rows than the (tile-padded) M: rows past out.size(0) are not stored
+  TORCH_CHECK(out.size(0) <= M && out.size(0) > 0 && out.size(1) == N && out.is_contiguous(),
+              "wgrad out must be [<= M, N]");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
   int cfg = 0, nsplit = 1;
   hx_wgrad_bf16_plan((int)M, (int)N, (int)T, &cfg, &nsplit);
@@ -466,7 +468,9 @@ Tensor wgrad_split(Tensor dys, std::vector<int64_t> dy_off, Tensor xs, std::vect
     TORCH_CHECK(x_off[i] >= 0 && x_off[i] + N <= xs.size(1) && x_off[i] % 8 == 0, "wgrad_split: bad X offset");
   }
   check_f32(out, "wgrad out");
-  TORCH_CHECK(out.size(0) == M && out.size(1) == N, "wgrad out must be [M, N]");
+  // out may hold fewer rows than the (tile-padded) M: rows past out.size(0) are not stored
+  TORCH_CHECK(out.size(0) <= M && out.size(0) > 0 && out.size(1) == N && out.is_contiguous(),
+              "wgrad out must be [<= M, N]");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(dys.device());
   const int64_t T = dys.size(0);
   int cfg = 0, nsplit = 1;
@@ -483,7 +487,7 @@ Tensor wgrad_split(Tensor dys, std::vector<int64_t> dy_off, Tensor xs, std::vect
   }
   TORCH_CHECK(hx_wgrad_split(dp, (int)dys.size(1), xp, (int)xs.size(1), (int)passes, out.data_ptr<float>(),
                              nsplit > 1 ? ws.data_ptr<float>() : nullptr, (int)M, (int)N, (int)T, cfg, nsplit,
-                             cur_stream(dys)) == 0,
+                             (int)out.size(0), cur_stream(dys)) == 0,
               "wgrad_split: launch failed");
   dbg_finite(out, "wgrad_split");
   return out;

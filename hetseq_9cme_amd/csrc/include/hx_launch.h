@@ -75,7 +75,8 @@ void hx_attn_bwd(int bf16, const void* qkv, const float* bias, float* dbq, float
 // ws: nsplit * M * N floats.  Returns -1 for an unsupported pass count.
 void hx_wgrad_split_plan(int M, int N, int T, int passes, int* cfg, int* nsplit);
 int hx_wgrad_split(const void* const* dy_pieces, int ldy, const void* const* x_pieces, int ldx, int passes,
-                   float* out, float* ws, int M, int N, int T, int cfg, int nsplit, hipStream_t s);
+                   float* out, float* ws, int M, int N, int T, int cfg, int nsplit, int mvalid,
+                   hipStream_t s);
 
 // elementwise.hip -- bias + activation (dout == nullptr) or its backward (dout != nullptr, with
 // dbias through the [nchunks][N] partial workspace) written as bf16 planes (split-GEMM path);

@@ -93,7 +93,8 @@ struct PieceBases {
 template <int BM, int BN, int WM, int WN, int NPC, int NP, int AHEAD, int MORD>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_split_k(PieceBases P, int lda, int ldb,
                                                                            float* __restrict__ out, int M, int N,
-                                                                           int T, int kchunk, int nsplit) {
+                                                                           int T, int kchunk, int nsplit,
+                                                                           int mvalid) {
   constexpr int NWM = BM / WM, NW = NWM * (BN / WN), NT = NW * 64;
   constexpr int MB = WM / 32, NB = WN / 32;
   constexpr int CA = BK * BM / 8 / NT, CB = BK * BN / 8 / NT;   // 16-B chunks per thread per piece
@@ -236,17 +237,17 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_split_k(Piec
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * WM + 32 * a + crow(r, h);
-        o[(int64_t)m * N + n] = acc[a][b][r];
+        if (m < mvalid) o[(int64_t)m * N + n] = acc[a][b][r];   // rows past mvalid: padding
       }
     }
 }
 
 __global__ __launch_bounds__(256) void split_sum2_k(const float4* __restrict__ ws, float4* __restrict__ out,
-                                                   int64_t n4, int nsplit) {
+                                                   int64_t n4, int64_t slab4, int nsplit) {
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
     float4 s = ws[i];
     for (int k = 1; k < nsplit; ++k) {
-      const float4 v = ws[(int64_t)k * n4 + i];
+      const float4 v = ws[(int64_t)k * slab4 + i];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
     out[i] = s;
@@ -255,7 +256,7 @@ __global__ __launch_bounds__(256) void split_sum2_k(const float4* __restrict__ w
 
 template <int BM, int BN, int WM, int WN, int NPC, int NP, int AHEAD, int MORD>
 void launch(const PieceBases& P, int lda, int ldb, float* out, float* ws, int M, int N, int T, int nsplit,
-            hipStream_t s) {
+            int mvalid, hipStream_t s) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int kchunk = ((T + nsplit - 1) / nsplit + BK - 1) / BK * BK;
   nsplit = (T + kchunk - 1) / kchunk;
@@ -269,12 +270,12 @@ void launch(const PieceBases& P, int lda, int ldb, float* out, float* ws, int M,
     attr = true;
   }
   wgrad_split_k<BM, BN, WM, WN, NPC, NP, AHEAD, MORD><<<8 * per, NT, smem, s>>>(
-      P, lda, ldb, nsplit > 1 ? ws : out, M, N, T, kchunk, nsplit);
+      P, lda, ldb, nsplit > 1 ? ws : out, M, N, T, kchunk, nsplit, nsplit > 1 ? M : mvalid);
   if (nsplit > 1) {
-    const int64_t n4 = (int64_t)M * N / 4;
+    const int64_t n4 = (int64_t)mvalid * N / 4, slab4 = (int64_t)M * N / 4;
     const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
     split_sum2_k<<<blocks, 256, 0, s>>>(reinterpret_cast<const float4*>(ws), reinterpret_cast<float4*>(out), n4,
-                                        nsplit);
+                                        slab4, nsplit);
   }
 }
 
@@ -303,7 +304,7 @@ void hx_wgrad_split_plan(int M, int N, int T, int passes, int* cfg, int* nsplit)
 }
 
 int hx_wgrad_split(const void* const* dy_pieces, int ldy, const void* const* x_pieces, int ldx, int passes,
-                   float* out, float* ws, int M, int N, int T, int cfg, int nsplit, hipStream_t s) {
+                   float* out, float* ws, int M, int N, int T, int cfg, int nsplit, int mvalid, hipStream_t s) {
   PieceBases P;
   const int npc = passes == 6 ? 3 : 2;
   for (int i = 0; i < 3; ++i) {
@@ -325,13 +326,13 @@ int hx_wgrad_split(const void* const* dy_pieces, int ldy, const void* const* x_p
 #define HX_WS_LAUNCH(BM_, NPC_, NP_)                                                           \
   do {                                                                                         \
     if (ahead == 2 && mord == 0)                                                               \
-      launch<BM_, 128, 64, 64, NPC_, NP_, 2, 0>(P, ldy, ldx, out, ws, M, N, T, nsplit, s);     \
+      launch<BM_, 128, 64, 64, NPC_, NP_, 2, 0>(P, ldy, ldx, out, ws, M, N, T, nsplit, mvalid, s);     \
     else if (ahead == 2)                                                                       \
-      launch<BM_, 128, 64, 64, NPC_, NP_, 2, 1>(P, ldy, ldx, out, ws, M, N, T, nsplit, s);     \
+      launch<BM_, 128, 64, 64, NPC_, NP_, 2, 1>(P, ldy, ldx, out, ws, M, N, T, nsplit, mvalid, s);     \
     else if (mord == 0)                                                                        \
-      launch<BM_, 128, 64, 64, NPC_, NP_, 1, 0>(P, ldy, ldx, out, ws, M, N, T, nsplit, s);     \
+      launch<BM_, 128, 64, 64, NPC_, NP_, 1, 0>(P, ldy, ldx, out, ws, M, N, T, nsplit, mvalid, s);     \
     else                                                                                       \
-      launch<BM_, 128, 64, 64, NPC_, NP_, 1, 1>(P, ldy, ldx, out, ws, M, N, T, nsplit, s);     \
+      launch<BM_, 128, 64, 64, NPC_, NP_, 1, 1>(P, ldy, ldx, out, ws, M, N, T, nsplit, mvalid, s);     \
   } while (0)
   if (passes == 3) {
     if (cfg == 1)

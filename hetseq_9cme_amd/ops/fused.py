@@ -749,15 +749,22 @@ class _DecoderXentFn(torch.autograd.Function):
         hs = h * scale.to(h.dtype)
         slot = grad_slot(Wp)
         if ctx.split:
-            # logits-gradient planes padded to a multiple of 64 columns (16-B rows for the GEMMs)
-            V = dl.shape[1]
-            Vp = (V + 63) // 64 * 64
+            # logits-gradient planes zero-padded to a multiple of 256 columns: 16-B rows for
+            # the data-gradient GEMM and whole 256-row tiles for the weight-gradient kernel
+            V, H = dl.shape[1], hs.shape[1]
+            Vp = (V + 255) // 256 * 256
             dls = split_gemm.grad_planes(dl, dpad=Vp)
             dh = split_gemm.dgrad(dls, Wp, rpad=Vp).mul_(scale)
             n = split_gemm.passes()
             hsp = split_gemm.planes(hs, split_gemm.ORDER_P[n])
+            if C().wgrad_split_ok(dls, hsp, Vp, H):
+                # the split-piece weight-gradient kernel over the masked rows (1.2 PF/s vs 0.8
+                # for the library product over the stacked plane rows, tools/probe/decoder_probe.py)
+                out = slot if slot is not None else torch.empty(V, H, device=dl.device)
+                dW = split_gemm.wgrad(dls, hsp, Vp, H, out)   # rows past V (padding) are not stored
+                return dh, dW, dbias, None
             a = dls.view(-1, Vp)[:, :V]
-            b = hsp.view(-1, hs.shape[1])
+            b = hsp.view(-1, H)
             if slot is not None:
                 dW = torch.mm(a.t(), b, out_dtype=torch.float32, out=slot)
             else:

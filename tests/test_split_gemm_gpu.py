@@ -354,3 +354,32 @@ def test_grad_planes_handoff_in_bert_layer(dev):
             assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)
     finally:
         ops.set_fp32_gemm('native')
+
+
+@pytest.mark.parametrize('T', [96, 4096])
+def test_wgrad_split_row_padded_output(dev, T):
+    """Split-piece weight gradient over a tile-padded M whose output holds only the valid
+    rows (the MLM decoder's vocabulary): direct stores (small T) and the split-K sum (large
+    T) both leave the rows past the output untouched and match the full product."""
+    from hetseq_9cme_amd import ops
+    from hetseq_9cme_amd.ops import split_gemm as sg
+    ops.set_fp32_gemm('bf16x6')
+    try:
+        g = torch.Generator(device='cpu').manual_seed(13)
+        Mv, Mp, N = 1001, 1024, 256
+        dy = torch.zeros(T, Mp)
+        dy[:, :Mv] = torch.randn(T, Mv, generator=g)
+        x = torch.randn(T, N, generator=g)
+        dys = sg.grad_planes(dy.to(dev))
+        xs = sg.planes(x.to(dev), sg.ORDER_P[6])
+        full = torch.empty(Mp, N, device=dev)
+        sg.wgrad(dys, xs, Mp, N, full)
+        buf = torch.full((Mv + 8, N), 7.0, device=dev)
+        part = sg.wgrad(dys, xs, Mp, N, buf[:Mv])
+        assert torch.equal(part, full[:Mv])
+        assert (buf[Mv:] == 7.0).all()
+        ref = dy[:, :Mv].double().t() @ x.double()
+        scale = dy[:, :Mv].double().abs().t() @ x.double().abs()
+        assert ((part.double().cpu() - ref).abs() / scale).max().item() < 2e-6
+    finally:
+        ops.set_fp32_gemm('native')

@@ -8,10 +8,27 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #define HX_WAVE 64
 
 namespace hx {
+
+// Streaming (nontemporal) stores for write-once outputs that the NEXT kernel reads from
+// HBM / MALL anyway (the bf16 split planes of the fp32-on-bf16 GEMM path): no L2
+// allocation.  Host switch read once per process; HX_NT_STORES=0 turns them off (A/B).
+inline bool nt_stores() {
+  static const bool on = !(getenv("HX_NT_STORES") && getenv("HX_NT_STORES")[0] == '0');
+  return on;
+}
+typedef unsigned int nt_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int nt_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st_nt16(void* p, uint4 v) {
+  __builtin_nontemporal_store(nt_u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<nt_u32x4*>(p));
+}
+__device__ __forceinline__ void st_nt8(void* p, uint2 v) {
+  __builtin_nontemporal_store(nt_u32x2{v.x, v.y}, reinterpret_cast<nt_u32x2*>(p));
+}
 
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -10,6 +10,8 @@
 //                    tanh backward uses the saved output (1 - out^2).
 //   * dropout fwd/bwd with the Philox stream (mask regenerated, never stored)
 //   * colsum      : generic [rows, N] -> [N] column sum (bias grads of plain linears)
+#include <stdlib.h>
+
 #include "hx_launch.h"
 #include "hx_vec.h"
 #include "hx_reduce.h"
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(NT) void bias_act_bwd_k(const T* __restrict__ dout,
 // v is split into NPC bf16 pieces (v = v0 + v1 [+ v2]); plane j of row r, columns c..c+7,
 // receives piece (order >> 4j) & 15 at planes[(r * npl + j) * N + c] (16-B stores).
 // Same tiling as bias_act_bwd_k: lane -> 8 adjacent columns, wave w -> rows w, w+4, ...
-template <int ACT, int NPC>
+template <int ACT, int NPC, bool kNT>
 __global__ __launch_bounds__(NT) void bias_act_planes_k(const float* __restrict__ y, const float* __restrict__ b,
                                                       const float* __restrict__ dout, uint16_t* __restrict__ planes,
                                                       float* __restrict__ partial, int64_t rows, int N, int npl,
@@ -225,7 +227,9 @@ __global__ __launch_bounds__(NT) void bias_act_planes_k(const float* __restrict_
       uint16_t* dst = planes + r * (int64_t)npl * N + j;
       for (int q = 0; q < npl; ++q) {
         const int k = (order >> (4 * q)) & 15;
-        *reinterpret_cast<uint4*>(dst + (int64_t)q * N) = pc[k < NPC ? k : NPC - 1];
+        const uint4 v = pc[k < NPC ? k : NPC - 1];
+        if constexpr (kNT) hx::st_nt16(dst + (int64_t)q * N, v);
+        else *reinterpret_cast<uint4*>(dst + (int64_t)q * N) = v;
       }
     }
   }
@@ -381,7 +385,15 @@ void hx_bias_act_planes(int act, const float* y, const float* b, const float* do
   const int nch = nchunks(rows);
   dim3 g((N + 511) / 512, nch);
   float* part = (dout && dbias) ? partial : nullptr;
-#define HX_BAP(A, P) bias_act_planes_k<A, P><<<g, NT, 0, s>>>(y, b, dout, planes, part, rows, N, npl, order)
+  // planes are written once and read by the next GEMM from HBM / MALL: nontemporal 16-B
+  // stores (no L2 allocation) -- forward 180 -> 130 us at T=16384, N=3072, bf16x6
+  // (tools/probe/nt_store_probe.py); HX_NT_STORES=0 restores plain stores for A/B runs
+  static const bool nt = hx::nt_stores();
+#define HX_BAP(A, P)                                                                                 \
+  do {                                                                                               \
+    if (nt) bias_act_planes_k<A, P, true><<<g, NT, 0, s>>>(y, b, dout, planes, part, rows, N, npl, order);  \
+    else bias_act_planes_k<A, P, false><<<g, NT, 0, s>>>(y, b, dout, planes, part, rows, N, npl, order);    \
+  } while (0)
 #define HX_BAP_ACT(P)                          \
   switch (act) {                               \
     case ACT_GELU: HX_BAP(ACT_GELU, P); break; \

@@ -225,7 +225,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
             uint16_t* o = planes + r * npl * H + j;
             for (int k = 0; k < npl; ++k) {
               const int pc = (order >> (4 * k)) & 15;
-              *reinterpret_cast<uint2*>(o + (int64_t)k * H) = pw[pc < npc ? pc : npc - 1];
+              hx::st_nt8(o + (int64_t)k * H, pw[pc < npc ? pc : npc - 1]);
             }
           } else {
             hx::store4(dy_out + r * H + j, dy);

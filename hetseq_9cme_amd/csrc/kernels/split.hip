@@ -29,7 +29,7 @@ __device__ __forceinline__ uint32_t pack2(float a, float b) {
   return (uint32_t)hx::f2bf(a) | ((uint32_t)hx::f2bf(b) << 16);
 }
 
-template <int NPIECE>
+template <int NPIECE, bool kNT>
 __global__ __launch_bounds__(256) void split_planes_k(const float* __restrict__ x, int64_t ldx,
                                                       uint16_t* __restrict__ out, int64_t R, int D, int npl,
                                                       uint32_t order, int stacked) {
@@ -60,7 +60,9 @@ __global__ __launch_bounds__(256) void split_planes_k(const float* __restrict__ 
     uint16_t* o = out + r * row_stride + c;
     for (int j = 0; j < npl; ++j) {
       const int k = (order >> (4 * j)) & 15;
-      *reinterpret_cast<u32x4*>(o + j * plane_stride) = w[k < NPIECE ? k : NPIECE - 1];
+      const u32x4 v = w[k < NPIECE ? k : NPIECE - 1];
+      if constexpr (kNT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(o + j * plane_stride));
+      else *reinterpret_cast<u32x4*>(o + j * plane_stride) = v;
     }
   }
 }
@@ -198,10 +200,15 @@ void hx_split_planes(const float* x, int64_t ldx, uint16_t* out, int64_t R, int 
     const int64_t n8 = R * (D / 8);
     if (n8 <= 0) return;
     const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 8192);
-    if (npieces == 3)
-      split_planes_k<3><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, npl, order, stacked);
+    const bool nt = hx::nt_stores();
+    if (npieces == 3 && nt)
+      split_planes_k<3, true><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, npl, order, stacked);
+    else if (npieces == 3)
+      split_planes_k<3, false><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, npl, order, stacked);
+    else if (nt)
+      split_planes_k<2, true><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, npl, order, stacked);
     else
-      split_planes_k<2><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, npl, order, stacked);
+      split_planes_k<2, false><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, npl, order, stacked);
     return;
   }
   const int64_t n = Rp * Dp;

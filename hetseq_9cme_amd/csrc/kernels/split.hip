@@ -95,6 +95,50 @@ __global__ __launch_bounds__(256) void split_planes_any_k(const float* __restric
   }
 }
 
+// Interleaved planes of a matrix whose rows are only 8-B aligned (odd width: the MLM
+// decoder's [rows, 30522] logits gradient), columns zero-padded to Dp (a multiple of 8):
+// 8 columns per lane from four 8-B loads, one 16-B nontemporal store per plane.
+template <int NPIECE>
+__global__ __launch_bounds__(256) void split_planes_pad8_k(const float* __restrict__ x, int64_t ldx,
+                                                           uint16_t* __restrict__ out, int64_t R, int D, int Dp,
+                                                           int npl, uint32_t order) {
+  const int d8 = Dp >> 3;
+  const int64_t n8 = R * d8;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / d8;
+    const int c = (int)(i - r * d8) * 8;
+    float e[8];
+    const float* xr = x + r * ldx + c;
+    if (c + 8 <= D) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float2 v = *reinterpret_cast<const float2*>(xr + 2 * k);
+        e[2 * k] = v.x;
+        e[2 * k + 1] = v.y;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) e[k] = c + k < D ? xr[k] : 0.f;
+    }
+    u32x4 w[NPIECE];
+#pragma unroll
+    for (int p = 0; p < NPIECE; ++p) {
+      uint32_t q[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        q[t] = hx::f2bf(e[t]);
+        e[t] -= hx::bf2f((uint16_t)q[t]);
+      }
+      w[p] = u32x4{q[0] | (q[1] << 16), q[2] | (q[3] << 16), q[4] | (q[5] << 16), q[6] | (q[7] << 16)};
+    }
+    uint16_t* o = out + r * (int64_t)npl * Dp + c;
+    for (int j = 0; j < npl; ++j) {
+      const int k = (order >> (4 * j)) & 15;
+      __builtin_nontemporal_store(w[k < NPIECE ? k : NPIECE - 1], reinterpret_cast<u32x4*>(o + (int64_t)j * Dp));
+    }
+  }
+}
+
 // Weight pieces in both layouts the split GEMMs read (ops/split_gemm.py), one pass over W:
 //   wf[n][p][k] = piece p of W[n][k]   (forward: B operand of y = x W^T)
 //   wt[k][p][n] = piece p of W[n][k]   (data gradient: B operand of dx = dy W = dy (W^T)^T)
@@ -209,6 +253,16 @@ void hx_split_planes(const float* x, int64_t ldx, uint16_t* out, int64_t R, int 
       split_planes_k<2, true><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, npl, order, stacked);
     else
       split_planes_k<2, false><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, npl, order, stacked);
+    return;
+  }
+  if (!stacked && Rp == R && Dp % 8 == 0 && ldx % 2 == 0 && ((uintptr_t)x & 7) == 0) {
+    const int64_t n8 = R * (Dp / 8);
+    if (n8 <= 0) return;
+    const int blocks = (int)std::min<int64_t>((n8 + 255) / 256, 8192);
+    if (npieces == 3)
+      split_planes_pad8_k<3><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, Dp, npl, order);
+    else
+      split_planes_pad8_k<2><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, Dp, npl, order);
     return;
   }
   const int64_t n = Rp * Dp;

@@ -95,6 +95,24 @@ def test_split_planes_transposed_bitwise(dev, npieces, order, N, npad):
     assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
 
 
+@pytest.mark.parametrize('npieces,order', [(3, (0, 0, 1, 0, 1, 2)), (2, (0, 0, 1))])
+def test_split_planes_padded_even_stride(dev, npieces, order):
+    """Vector path for odd-width rows with an even (8-B aligned) row stride -- the MLM
+    decoder's [rows, 30522] logits gradient padded to 256 columns."""
+    from hetseq_9cme_amd.ops._ext import C
+    g = torch.Generator(device='cpu').manual_seed(6)
+    big = torch.randn(37, 1006, generator=g).to(dev)
+    x = big[:, :1001]                     # row stride 1006 floats (8-B aligned rows), width 1001
+    out = C().split_planes(x, list(order), npieces, False, 0, 1024)
+    pcs = _ref_pieces(x.contiguous(), npieces)
+    ref = torch.zeros(37, len(order), 1024, dtype=torch.bfloat16, device=dev)
+    for j, k in enumerate(order):
+        ref[:, j, :1001] = pcs[k]
+    ref = ref.reshape(37, -1)
+    assert out.shape == ref.shape
+    assert torch.equal(out.view(torch.int16), ref.view(torch.int16))
+
+
 def _err(a, ref, scale):
     return ((a.double() - ref).abs() / scale.clamp(min=1e-30)).max().item()
 

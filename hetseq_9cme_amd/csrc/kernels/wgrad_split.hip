@@ -172,35 +172,28 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_split_k(Piec
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[a][b] = f32x16{0};
 
-  // per 16-token k-step: every X piece fragment, then the dY pieces one at a time, each
-  // followed by the passes that use it (pairs grouped by dY piece) -- only one dY piece's
-  // fragments are live at a time, which keeps the two-stage staging pipeline in registers
   auto mma = [&](int buf) {
     const char* st = lds + buf * STAGE;
 #pragma unroll
     for (int ks = 0; ks < BK / 16; ++ks) {
-      bf16x8 fb[NPC][NB];
+      bf16x8 fa[NPC][MB], fb[NPC][NB];
 #pragma unroll
-      for (int p = 0; p < NPC; ++p)
+      for (int p = 0; p < NPC; ++p) {
+#pragma unroll
+        for (int a = 0; a < MB; ++a)
+          fa[p][a] = frag<BM>(st + p * A_BYTES, alo, ahi, 16 * ks, wm * WM + 32 * a, a & 1);
 #pragma unroll
         for (int b = 0; b < NB; ++b)
           fb[p][b] = frag<BN>(st + NPC * A_BYTES + p * B_BYTES, blo, bhi, 16 * ks, wn * WN + 32 * b, b & 1);
+      }
 #pragma unroll
-      for (int pa = 0; pa < NPC; ++pa) {
-        bf16x8 fa[MB];
+      for (int q = 0; q < NP; ++q)
 #pragma unroll
         for (int a = 0; a < MB; ++a)
-          fa[a] = frag<BM>(st + pa * A_BYTES, alo, ahi, 16 * ks, wm * WM + 32 * a, a & 1);
 #pragma unroll
-        for (int q = 0; q < NP; ++q) {
-          if (Pairs<NP>::a[q] != pa) continue;
-#pragma unroll
-          for (int a = 0; a < MB; ++a)
-#pragma unroll
-            for (int b = 0; b < NB; ++b)
-              acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[Pairs<NP>::b[q]][b], acc[a][b], 0, 0, 0);
-        }
-      }
+          for (int b = 0; b < NB; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[Pairs<NP>::a[q]][a], fb[Pairs<NP>::b[q]][b],
+                                                                acc[a][b], 0, 0, 0);
     }
   };
 

@@ -186,6 +186,9 @@ def add_distributed_training_args(parser):
     group.add_argument('--allreduce-impl', default='rccl', choices=['rccl', 'xgmi'],
                        help='gradient all-reduce transport: RCCL, or the hand-written intra-node two-shot '
                             'xGMI kernel over IPC-mapped peer buffers (single host only; falls back to RCCL)')
+    group.add_argument('--rccl-normal-priority', action='store_true',
+                       help='run RCCL collectives on normal-priority HIP streams (default: high priority, so '
+                            'bucket all-reduces are scheduled ahead of queued backward kernels)')
     group.add_argument('--xgmi-blocks', default=64, type=int, metavar='N',
                        help='workgroups per xGMI all-reduce launch (CUs taken from backward while it runs)')
     group.add_argument('--fix-batches-to-gpus', action='store_true')

@@ -63,6 +63,17 @@ def distributed_init(args):
         if dev.type == 'cuda':
             # binds the RCCL communicator to this GPU up front (eager init)
             init_kwargs['device_id'] = dev
+        if init_kwargs['backend'] == 'nccl' and not getattr(args, 'rccl_normal_priority', False):
+            # RCCL kernels on high-priority HIP streams: a bucket all-reduce launched from a
+            # gradient hook is dispatched ahead of the backward kernels already queued, so it
+            # overlaps with them instead of waiting behind them (the last buckets, produced at
+            # the very end of backward, are the only exposed communication)
+            try:
+                opts = dist.ProcessGroupNCCL.Options()
+                opts.is_high_priority_stream = True
+                init_kwargs['pg_options'] = opts
+            except AttributeError:
+                pass
         try:
             dist.init_process_group(**init_kwargs)
         except TypeError:  # older torch without device_id

@@ -369,10 +369,11 @@ std::vector<Tensor> attn_fwd_x6(Tensor qkv, Tensor mask_bias, int64_t nh, double
 // returns {dqkv, dbias} (dbias: [3H] fp32 when bias is given -- written into dbq/dbk/dbv
 // when those slots are given -- else an empty tensor)
 std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask,
-                             int64_t nh, double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv) {
+                             int64_t nh, double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, bool split = false) {
   check_cuda(dout, "grad_output");
   check_cuda(qkv, "qkv");
   const int bf = act_bf16(qkv);
+  TORCH_CHECK(!(split && bf), "attn_bwd_x6: fp32 activations only");
   TORCH_CHECK(dout.scalar_type() == qkv.scalar_type() && out.scalar_type() == qkv.scalar_type(),
               "attention activations must share one dtype");
   const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(2) / 3;
@@ -409,7 +410,7 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor o
     }
     part = torch::empty({B * ((S + 127) / 128), 3 * H}, qkv.options().dtype(torch::kFloat32));
   }
-  hx_attn_bwd(bf, qkv.data_ptr(), ptr_or_null<float>(bias), pq, pk, pv, part.defined() ? part.data_ptr<float>() : nullptr,
+  hx_attn_bwd(split ? 2 : bf, qkv.data_ptr(), ptr_or_null<float>(bias), pq, pk, pv, part.defined() ? part.data_ptr<float>() : nullptr,
               mask_bias.data_ptr<float>(), dout.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
               keep < 1.0 ? reinterpret_cast<const uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr, dqkv.data_ptr(),
               dq_acc, dq_ld, (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv));
@@ -693,7 +694,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", [](Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed, int64_t stream,
                         OptT bias) { return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, false); });
   m.def("attn_fwd_x6", &attn_fwd_x6);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
+                       double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv) {
+    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, false);
+  });
+  // fp32 attention backward on the bf16 matrix cores (split pieces, attention_x6.hip)
+  m.def("attn_bwd_x6", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
+                          double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv) {
+    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, true);
+  });
   m.def("wgrad_bf16", &wgrad_bf16);
   m.def("wgrad_bf16_ok", &wgrad_bf16_ok);
   m.def("split_planes", &split_planes);

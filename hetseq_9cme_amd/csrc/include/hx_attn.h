@@ -13,12 +13,15 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // lane half h -> row index
 __device__ __forceinline__ int crow(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-// v_writelane_b32 with a compile-time lane (inline constant: only the value uses
-// the constant bus): put a wave-uniform value into one lane of a VGPR
+// v_writelane_b32 with a compile-time lane: put a wave-uniform value into one lane of a
+// VGPR.  Through the LLVM intrinsic (this clang has no builtin for it), not an asm block:
+// the compiler must see the instruction to put the wait states gfx950 needs between the
+// VALU write of the ballot SGPR and this read of it -- an asm block hid it, and some
+// lanes' words were lost depending on the schedule.
+extern "C" __device__ int hx_llvm_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane");
 template <int L>
 __device__ __forceinline__ uint32_t write_lane(uint32_t v, uint32_t val) {
-  asm("v_writelane_b32 %0, %1, %2" : "+v"(v) : "s"(val), "i"(L));
-  return v;
+  return (uint32_t)hx_llvm_writelane((int)val, L, (int)v);
 }
 
 // Forward dropout for accumulator register R of both 32-key sub-blocks (keys on the

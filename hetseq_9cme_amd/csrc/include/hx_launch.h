@@ -61,12 +61,15 @@ void hx_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, float* out, 
 void hx_attn_fwd_x6(const float* qkv, const float* bias, const float* maskb, float* out, float* lse,
                     uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream,
                     hipStream_t s);
+void hx_attn_bwd_x6(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,
+                    const float* out, const float* lse, const uint32_t* dmask, float* dqkv, float* dq_acc, int dq_ld,
+                    int B, int S, int nh, float keep, hipStream_t s);
 void hx_attn_fwd(int bf16, const void* qkv, const float* bias, const float* maskb, void* out, float* lse,
                  uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream, hipStream_t s);
 // dq_acc: fp32 dQ accumulation target when S > 128 (atomics; row stride dq_ld), else unused.
 // With bias: its gradient (column sums of dQ / dK / dV) goes to dbq / dbk / dbv through the
-// dbias_part workspace ([B * ceil(S/128)][3H] fp32).
-void hx_attn_bwd(int bf16, const void* qkv, const float* bias, float* dbq, float* dbk, float* dbv, float* dbias_part,
+// dbias_part workspace ([B * ceil(S/128)][3H] fp32).  kind: 0 fp32 MFMA, 1 bf16, 2 fp32 split (x6).
+void hx_attn_bwd(int kind, const void* qkv, const float* bias, float* dbq, float* dbk, float* dbv, float* dbias_part,
                  const float* maskb, const void* dout, const void* out, const float* lse, const uint32_t* dmask,
                  void* dqkv, float* dq_acc, int dq_ld, int B, int S, int nh, float keep, hipStream_t s);
 

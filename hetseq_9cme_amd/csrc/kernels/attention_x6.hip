@@ -40,14 +40,32 @@ __device__ __forceinline__ f32x16 mfma(bf16x8 a, bf16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
+// (a, b) -> one word of their bf16 roundings (a low, b high); a and b become the residuals.
+// The round trip back to fp32 is bit placement on the packed word: the compiler would
+// otherwise re-convert each value on its own for the subtraction.
+__device__ __forceinline__ uint32_t peel2(float& a, float& b) {
+  typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+  typedef float f32x2_t __attribute__((ext_vector_type(2)));
+  const f32x2_t v = {a, b};
+  const uint32_t w = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+  a -= __uint_as_float(w << 16);
+  b -= __uint_as_float(w & 0xffff0000u);
+  return w;
+}
 // x -> three bf16 pieces (x0 + x1 + x2 = x to 2^-26 relative)
 __device__ __forceinline__ void split8(const float (&x)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
-  f32x8 v = {x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]};
-  p0 = __builtin_convertvector(v, bf16x8);
-  v -= __builtin_convertvector(p0, f32x8);
-  p1 = __builtin_convertvector(v, bf16x8);
-  v -= __builtin_convertvector(p1, f32x8);
-  p2 = __builtin_convertvector(v, bf16x8);
+  float e[8] = {x[0], x[1], x[2], x[3], x[4], x[5], x[6], x[7]};
+  uint4 w[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    w[k].x = peel2(e[0], e[1]);
+    w[k].y = peel2(e[2], e[3]);
+    w[k].z = peel2(e[4], e[5]);
+    w[k].w = peel2(e[6], e[7]);
+  }
+  p0 = __builtin_bit_cast(bf16x8, w[0]);
+  p1 = __builtin_bit_cast(bf16x8, w[1]);
+  p2 = __builtin_bit_cast(bf16x8, w[2]);
 }
 template <int O>
 __device__ __forceinline__ void split_acc(const f32x16& s, bf16x8 (&p)[3]) {
@@ -293,6 +311,394 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if (h == 0) lse[bh * S + q] = m_run + __logf(l_run);
 }
 
+
+// ============================================================================ backward
+// The bf16 kernel's structure (attention_bf16.hip) with every MFMA operand as three bf16
+// pieces and six passes per product.  grid (ceil(S/128), nh, B), block 256 = 4 waves; wave w
+// owns keys kbase + 32w .. +31 ON THE LANES (their K / V piece fragments in registers) and
+// the workgroup sweeps 32-query tiles:
+//   S = Qs . K^T, dP = dO . V^T            (32x32x16: A = piece rows of the tile, B = key pieces)
+//   P = exp(S + mask - lse), Pd = P drop/keep, dS = P (dP drop/keep - D)     (fp32, in place)
+//   dV += Pd^T . dO, dK += dS^T . Qs        (A = pieces of the P / dS accumulators, B = pieces
+//                                            of transposed, query-permuted images of dO / Q)
+//   dQ  = dS . K over the block's 128 keys  (16x16x32: dS pieces through LDS, K^T pieces)
+// D = rowsum(dO * O) in fp32 while staging.  ~134 KiB of LDS: one workgroup per CU, so the
+// kernel may use the whole register file (one wave per SIMD).
+constexpr int TS = 40;    // transposed 32-query image row stride (bf16)
+constexpr int KTS = 136;  // K^T [dim][128 keys] and dS [query][128 keys] row stride (bf16)
+constexpr int KT_B = 64 * KTS * 2, DS_B = 32 * KTS * 2, QS_B = 32 * RS * 2, QT_B = 64 * TS * 2;
+constexpr int BWD_SMEM = 3 * (KT_B + DS_B + 2 * QS_B + 2 * QT_B) + 2 * 32 * 4;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+#define HX_X6_16(ACC, A, B) \
+  do {                                    \
+    ACC = mfma16(A[0], B[0], ACC);        \
+    ACC = mfma16(A[0], B[1], ACC);        \
+    ACC = mfma16(A[1], B[0], ACC);        \
+    ACC = mfma16(A[0], B[2], ACC);        \
+    ACC = mfma16(A[1], B[1], ACC);        \
+    ACC = mfma16(A[2], B[0], ACC);        \
+  } while (0)
+
+// 4 fp32 -> three pieces of 4 bf16 (two words each)
+__device__ __forceinline__ void split4(const float (&x)[4], uint2 (&p)[3]) {
+  float e[4] = {x[0], x[1], x[2], x[3]};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    p[k].x = peel2(e[0], e[1]);
+    p[k].y = peel2(e[2], e[3]);
+  }
+}
+// two fp32 -> three pieces of 2 bf16 (one word each: value 0 low, value 1 high)
+__device__ __forceinline__ void split2(float x0, float x1, uint32_t (&p)[3]) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) p[k] = peel2(x0, x1);
+}
+// rows r0, r1 (consecutive image positions) x 4 dims -> 4 words of a transposed image
+__device__ __forceinline__ void put_t4(uint16_t* img, int stride, int dim0, int pos, uint2 r0, uint2 r1) {
+  uint32_t* p = reinterpret_cast<uint32_t*>(img + dim0 * stride + pos);
+  const int sw = stride / 2;
+  p[0] = (r0.x & 0xffffu) | (r1.x << 16);
+  p[sw] = (r0.x >> 16) | (r1.x & 0xffff0000u);
+  p[2 * sw] = (r0.y & 0xffffu) | (r1.y << 16);
+  p[3 * sw] = (r0.y >> 16) | (r1.y & 0xffff0000u);
+}
+__device__ __forceinline__ void ld8(const float* p, const float* bias, float (&f)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), c = *reinterpret_cast<const float4*>(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = c.x; f[5] = c.y; f[6] = c.z; f[7] = c.w;
+  if (bias) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] += bias[j];
+  }
+}
+
+template <bool kDrop>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void attn_bwd_x6_k(
+    const float* __restrict__ qkv, const float* __restrict__ qkv_bias, float* __restrict__ dbias_part,
+    const float* __restrict__ maskb, const float* __restrict__ dout, const float* __restrict__ outp,
+    const float* __restrict__ lse, const uint32_t* __restrict__ dmask, float* __restrict__ dqkv,
+    float* __restrict__ dq_acc, int dq_ld, int S, int nh, float keep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* Kt = reinterpret_cast<uint16_t*>(smem);                       // [3][64][KTS]
+  uint16_t* dSs = reinterpret_cast<uint16_t*>(smem + 3 * KT_B);           // [3][32][KTS]
+  uint16_t* Qs = reinterpret_cast<uint16_t*>(smem + 3 * (KT_B + DS_B));   // [3][32][RS]
+  uint16_t* dOs = Qs + 3 * 32 * RS;                                       // [3][32][RS]
+  uint16_t* Qt = dOs + 3 * 32 * RS;                                       // [3][64][TS]
+  uint16_t* dOt = Qt + 3 * 64 * TS;                                       // [3][64][TS]
+  float* Ls = reinterpret_cast<float*>(dOt + 3 * 64 * TS);                // [32] lse
+  float* Ds = Ls + 32;                                                    // [32] D
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const int b = blockIdx.z, hd = blockIdx.y;
+  const int H = nh * D, H3 = 3 * H;
+  const int kbase = blockIdx.x * 128;
+  const bool single = gridDim.x == 1;
+  const int64_t bh = (int64_t)b * nh + hd;
+  const float scale = 0.125f, inv_keep = 1.f / keep;
+  const int Sp = (S + 127) & ~127;
+  const int nwords = Sp >> 5;
+  const float* base = qkv + (int64_t)b * S * H3 + hd * D;
+  const float* qbias = qkv_bias ? qkv_bias + hd * D : nullptr;
+  const float* kbias = qkv_bias ? qkv_bias + H + hd * D : nullptr;
+  const float* vbias = qkv_bias ? qkv_bias + 2 * H + hd * D : nullptr;
+
+  // ---- K^T pieces of the 128 keys (natural key order) for dQ: 64 key pairs x 16 dim quads
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int u = tid + 256 * i, dq = u & 15, kp = u >> 4;
+    const int k0 = kbase + 2 * kp < S ? kbase + 2 * kp : S - 1;
+    const int k1 = kbase + 2 * kp + 1 < S ? kbase + 2 * kp + 1 : S - 1;
+    const float4 a = *reinterpret_cast<const float4*>(base + (int64_t)k0 * H3 + H + 4 * dq);
+    const float4 c = *reinterpret_cast<const float4*>(base + (int64_t)k1 * H3 + H + 4 * dq);
+    float fa[4] = {a.x, a.y, a.z, a.w}, fc[4] = {c.x, c.y, c.z, c.w};
+    if (kbias) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        fa[j] += kbias[4 * dq + j];
+        fc[j] += kbias[4 * dq + j];
+      }
+    }
+    uint2 pa[3], pc[3];
+    split4(fa, pa);
+    split4(fc, pc);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) put_t4(Kt + p * 64 * KTS, KTS, 4 * dq, 2 * kp, pa[p], pc[p]);
+  }
+  // ---- this lane's key: K and V piece fragments (B operands of S and dP), dims 16ks + 8h .. +7
+  const int mykey = kbase + w * 32 + l32;
+  const int mykc = mykey < S ? mykey : S - 1;
+  bf16x8 kf[4][3], vf[4][3];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int c = 16 * ks + 8 * h;
+    float f[8];
+    ld8(base + (int64_t)mykc * H3 + H + c, kbias ? kbias + c : nullptr, f);
+    split8(f, kf[ks][0], kf[ks][1], kf[ks][2]);
+    ld8(base + (int64_t)mykc * H3 + 2 * H + c, vbias ? vbias + c : nullptr, f);
+    split8(f, vf[ks][0], vf[ks][1], vf[ks][2]);
+  }
+  const float mk = mykey < S ? maskb[(int64_t)b * S + mykey] : -INFINITY;
+
+  const float* dout_b = dout + (int64_t)b * S * H + hd * D;
+  const float* out_b = outp + (int64_t)b * S * H + hd * D;
+  float* dqkv_b = dqkv + (int64_t)b * S * H3 + hd * D;
+  float* dqa_b = dq_acc ? dq_acc + (int64_t)b * S * dq_ld + hd * D : nullptr;
+  const float* lse_bh = lse + bh * S;
+  const uint32_t* dmask_bh = kDrop ? dmask + bh * Sp * nwords : nullptr;
+  const int moff = mykey * nwords;
+
+  // staging unit of this thread: query pair (2sqp, 2sqp+1) x dims 4sdq .. 4sdq+3
+  const int sdq = tid & 15, sqp = tid >> 4;
+  float4 pq[2], pd[2], po[2];
+  float pl = 0.f;
+  uint32_t pm = 0;
+  auto ld_tile = [&](int qt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int qr = qt + 2 * sqp + i;
+      const int r = qr < S ? qr : S - 1;
+      pq[i] = *reinterpret_cast<const float4*>(base + (int64_t)r * H3 + 4 * sdq);
+      pd[i] = *reinterpret_cast<const float4*>(dout_b + (int64_t)r * H + 4 * sdq);
+      po[i] = *reinterpret_cast<const float4*>(out_b + (int64_t)r * H + 4 * sdq);
+    }
+    const int lq = qt + (tid & 31);
+    pl = lse_bh[lq < S ? lq : S - 1];
+    if (kDrop) pm = dmask_bh[moff + (qt >> 5)];
+  };
+  ld_tile(0);
+
+  // dQ tiles of this wave (16x16x32 layout): queries 16qh .., dims 32dp2 .. and 32dp2 + 16 ..
+  const int qh = w & 1, dp2 = w >> 1;
+  const int r16 = lane & 15, kg = lane >> 4;
+
+  f32x16 dv0 = {0}, dv1 = {0}, dk0 = {0}, dk1 = {0};
+  float cq0 = 0.f, cq1 = 0.f;
+
+  // split the prefetched tile into the piece images (+ bias, 1/8 on Q), D = rowsum(dO * O), lse
+  auto stage = [&](int qt) {
+    float q0[4] = {pq[0].x, pq[0].y, pq[0].z, pq[0].w}, q1[4] = {pq[1].x, pq[1].y, pq[1].z, pq[1].w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float bj = qbias ? qbias[4 * sdq + j] : 0.f;
+      q0[j] = (q0[j] + bj) * scale;
+      q1[j] = (q1[j] + bj) * scale;
+    }
+    float d0[4] = {pd[0].x, pd[0].y, pd[0].z, pd[0].w}, d1[4] = {pd[1].x, pd[1].y, pd[1].z, pd[1].w};
+    uint2 q0p[3], q1p[3], d0p[3], d1p[3];
+    split4(q0, q0p);
+    split4(q1, q1p);
+    split4(d0, d0p);
+    split4(d1, d1p);
+    const int pos = vpos(2 * sqp);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      *reinterpret_cast<uint2*>(&Qs[p * 32 * RS + (2 * sqp) * RS + 4 * sdq]) = q0p[p];
+      *reinterpret_cast<uint2*>(&Qs[p * 32 * RS + (2 * sqp + 1) * RS + 4 * sdq]) = q1p[p];
+      *reinterpret_cast<uint2*>(&dOs[p * 32 * RS + (2 * sqp) * RS + 4 * sdq]) = d0p[p];
+      *reinterpret_cast<uint2*>(&dOs[p * 32 * RS + (2 * sqp + 1) * RS + 4 * sdq]) = d1p[p];
+      put_t4(Qt + p * 64 * TS, TS, 4 * sdq, pos, q0p[p], q1p[p]);
+      put_t4(dOt + p * 64 * TS, TS, 4 * sdq, pos, d0p[p], d1p[p]);
+    }
+    float e0 = pd[0].x * po[0].x + pd[0].y * po[0].y + pd[0].z * po[0].z + pd[0].w * po[0].w;
+    float e1 = pd[1].x * po[1].x + pd[1].y * po[1].y + pd[1].z * po[1].z + pd[1].w * po[1].w;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      e0 += __shfl_xor(e0, o, 64);
+      e1 += __shfl_xor(e1, o, 64);
+    }
+    if (sdq == 0) {
+      Ds[2 * sqp] = e0;
+      Ds[2 * sqp + 1] = e1;
+    }
+    if (tid < 32) Ls[tid] = qt + tid < S ? pl : INFINITY;   // rows past S: P = 0
+  };
+  // P, Pd, dS in place for accumulator rows r, r + 1 (queries crow(r), crow(r) + 1); the dS
+  // pieces also go to LDS ([query][key]) for dQ
+  auto pds = [&](f32x16& sa, f32x16& dpa, uint32_t mword, int r) {
+    float ds[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int qr = crow(r + i, h);
+      const float p = __expf(sa[r + i] + mk - Ls[qr]);
+      float keepf = 1.f;
+      if (kDrop) keepf = ((mword >> qr) & 1) ? inv_keep : 0.f;
+      sa[r + i] = p * keepf;
+      ds[i] = p * (dpa[r + i] * keepf - Ds[qr]);
+      dpa[r + i] = ds[i];
+    }
+    uint32_t pc[3];
+    split2(ds[0], ds[1], pc);
+    const int o = crow(r, h) * KTS + w * 32 + l32;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      dSs[p * 32 * KTS + o] = (uint16_t)pc[p];
+      dSs[p * 32 * KTS + o + KTS] = (uint16_t)(pc[p] >> 16);
+    }
+  };
+  // dV += Pd^T . dO, dK += dS^T . Qs over accumulator half HALF (k-slots = its query rows)
+  auto load_img = [&](const uint16_t* img, int half, bf16x8 (&t0)[3], bf16x8 (&t1)[3]) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      t0[p] = *reinterpret_cast<const bf16x8*>(&img[p * 64 * TS + l32 * TS + 8 * h + 16 * half]);
+      t1[p] = *reinterpret_cast<const bf16x8*>(&img[p * 64 * TS + (32 + l32) * TS + 8 * h + 16 * half]);
+    }
+  };
+  // dQ = dS . K over the block's 128 keys (16x16x32 tiles)
+  auto dq_mfma = [&](f32x4& qa0, f32x4& qa1) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      bf16x8 a[3], b0[3], b1[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        a[p] = *reinterpret_cast<const bf16x8*>(&dSs[p * 32 * KTS + (qh * 16 + r16) * KTS + 32 * ks + 8 * kg]);
+        b0[p] = *reinterpret_cast<const bf16x8*>(&Kt[p * 64 * KTS + (32 * dp2 + r16) * KTS + 32 * ks + 8 * kg]);
+        b1[p] = *reinterpret_cast<const bf16x8*>(&Kt[p * 64 * KTS + (32 * dp2 + 16 + r16) * KTS + 32 * ks + 8 * kg]);
+      }
+      HX_X6_16(qa0, a, b0);
+      HX_X6_16(qa1, a, b1);
+    }
+  };
+
+  stage(0);
+  uint32_t mnext = pm;
+  for (int qt = 0; qt < S; qt += 32) {
+    // tile qt is staged; every wave is done with the previous tile's dS
+    __syncthreads();
+    const uint32_t mword = mnext;
+    const bool more = qt + 32 < S;
+    if (more) ld_tile(qt + 32);   // in flight during this tile's math
+
+    // ---- S = Qs . K^T, dP = dO . V^T (queries on accumulator rows, keys on lanes)
+    f32x16 sa = {0}, dpa = {0};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      bf16x8 qa[3], da[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        qa[p] = *reinterpret_cast<const bf16x8*>(&Qs[p * 32 * RS + l32 * RS + 16 * ks + 8 * h]);
+        da[p] = *reinterpret_cast<const bf16x8*>(&dOs[p * 32 * RS + l32 * RS + 16 * ks + 8 * h]);
+      }
+      HX_X6(sa, qa, kf[ks]);
+      HX_X6(dpa, da, vf[ks]);
+    }
+#pragma unroll
+    for (int r = 0; r < 8; r += 2) pds(sa, dpa, mword, r);
+    {   // accumulator half 0: dV / dK MFMAs, rows 8..15's P / dS in their shadow
+      bf16x8 a[3], c[3], t0[3], t1[3];
+      split_acc<0>(sa, a);
+      split_acc<0>(dpa, c);
+      load_img(dOt, 0, t0, t1);
+      HX_X6(dv0, a, t0);
+      pds(sa, dpa, mword, 8);
+      HX_X6(dv1, a, t1);
+      pds(sa, dpa, mword, 10);
+      load_img(Qt, 0, t0, t1);
+      HX_X6(dk0, c, t0);
+      pds(sa, dpa, mword, 12);
+      HX_X6(dk1, c, t1);
+      pds(sa, dpa, mword, 14);
+    }
+    {   // accumulator half 1
+      bf16x8 a[3], c[3], t0[3], t1[3];
+      split_acc<8>(sa, a);
+      split_acc<8>(dpa, c);
+      load_img(dOt, 1, t0, t1);
+      HX_X6(dv0, a, t0);
+      HX_X6(dv1, a, t1);
+      load_img(Qt, 1, t0, t1);
+      HX_X6(dk0, c, t0);
+      HX_X6(dk1, c, t1);
+    }
+    // every wave's dS columns are in LDS; the piece images of tile qt are free
+    __syncthreads();
+    f32x4 qa0 = {0.f, 0.f, 0.f, 0.f}, qa1 = {0.f, 0.f, 0.f, 0.f};
+    if (more) {   // next tile's staging in the dQ MFMAs' shadow
+      dq_mfma(qa0, qa1);
+      stage(qt + 32);
+      mnext = pm;
+    } else {
+      dq_mfma(qa0, qa1);
+    }
+    const int q0 = qt + qh * 16 + 4 * kg;
+    if (dbias_part) {   // rows past S hold exact zeros (their P, hence dS, is 0)
+      cq0 += (qa0[0] + qa0[1]) + (qa0[2] + qa0[3]);
+      cq1 += (qa1[0] + qa1[1]) + (qa1[2] + qa1[3]);
+    }
+    const int dcol = 32 * dp2 + r16;
+    if (single) {
+      float* dq = dqkv_b + (int64_t)q0 * H3 + dcol;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (q0 + r >= S) continue;
+        dq[r * H3] = qa0[r] * scale;
+        dq[r * H3 + 16] = qa1[r] * scale;
+      }
+    } else {
+      float* dq = dqa_b + (int64_t)q0 * dq_ld + dcol;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (q0 + r >= S) continue;
+        atomicAdd(dq + r * dq_ld, qa0[r] * scale);
+        atomicAdd(dq + r * dq_ld + 16, qa1[r] * scale);
+      }
+    }
+  }
+  // ---- epilogue: dK (accumulated against pre-scaled Q: already scaled), dV
+  float* dk = dqkv + (int64_t)b * S * H3 + H + hd * D;
+  float* dvp = dqkv + (int64_t)b * S * H3 + 2 * H + hd * D;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int key = kbase + w * 32 + crow(r, h);
+    if (key >= S) continue;
+    dk[(int64_t)key * H3 + l32] = dk0[r];
+    dk[(int64_t)key * H3 + 32 + l32] = dk1[r];
+    dvp[(int64_t)key * H3 + l32] = dv0[r];
+    dvp[(int64_t)key * H3 + 32 + l32] = dv1[r];
+  }
+  if (dbias_part) {
+    // QKV-bias gradient = column sums of dQ, dK, dV: one row of 3H partials per
+    // (batch, key block), folded into the bias-grad slots afterwards (attention.hip)
+    float sk0 = 0.f, sk1 = 0.f, sv0 = 0.f, sv1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sk0 += dk0[r]; sk1 += dk1[r]; sv0 += dv0[r]; sv1 += dv1[r];
+    }
+    sk0 += __shfl_xor(sk0, 32, 64); sk1 += __shfl_xor(sk1, 32, 64);
+    sv0 += __shfl_xor(sv0, 32, 64); sv1 += __shfl_xor(sv1, 32, 64);
+    cq0 += __shfl_xor(cq0, 16, 64); cq0 += __shfl_xor(cq0, 32, 64);
+    cq1 += __shfl_xor(cq1, 16, 64); cq1 += __shfl_xor(cq1, 32, 64);
+    cq0 *= scale;
+    cq1 *= scale;
+    __syncthreads();   // every wave is done with dSs
+    float* red = reinterpret_cast<float*>(dSs);   // [4 waves][3][64] floats
+    if (lane < 32) {
+      red[(w * 3 + 1) * 64 + l32] = sk0; red[(w * 3 + 1) * 64 + 32 + l32] = sk1;
+      red[(w * 3 + 2) * 64 + l32] = sv0; red[(w * 3 + 2) * 64 + 32 + l32] = sv1;
+    }
+    if (lane < 16) {   // dQ columns 32dp2 + lane and 32dp2 + 16 + lane of this wave's query half
+      red[(w * 3) * 64 + 32 * dp2 + lane] = cq0;
+      red[(w * 3) * 64 + 32 * dp2 + 16 + lane] = cq1;
+    }
+    __syncthreads();
+    if (tid < 192) {
+      const int part = tid >> 6, c = tid & 63;
+      float v;
+      if (part == 0) {   // waves (0,1) own dQ columns 0..31, waves (2,3) own 32..63
+        const int wa = c < 32 ? 0 : 2;
+        v = red[(wa * 3) * 64 + c] + red[((wa + 1) * 3) * 64 + c];
+      } else {
+        v = (red[(0 * 3 + part) * 64 + c] + red[(1 * 3 + part) * 64 + c]) +
+            (red[(2 * 3 + part) * 64 + c] + red[(3 * 3 + part) * 64 + c]);
+      }
+      dbias_part[((int64_t)b * gridDim.x + blockIdx.x) * H3 + part * H + hd * D + c] = v;
+    }
+  }
+}
+
+#undef HX_X6_16
 #undef HX_X6
 
 }  // namespace
@@ -305,4 +711,24 @@ void hx_attn_fwd_x6(const float* qkv, const float* bias, const float* maskb, flo
     attn_fwd_x6_k<true><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream);
   else
     attn_fwd_x6_k<false><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream);
+}
+
+void hx_attn_bwd_x6(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,
+                    const float* out, const float* lse, const uint32_t* dmask, float* dqkv, float* dq_acc, int dq_ld,
+                    int B, int S, int nh, float keep, hipStream_t s) {
+  dim3 grid((S + 127) / 128, nh, B);
+  static bool attr = false;
+  if (!attr) {   // > 64 KiB of dynamic LDS needs an explicit opt-in (gfx950: 160 KiB per CU)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_x6_k<true>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, BWD_SMEM);
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_x6_k<false>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, BWD_SMEM);
+    attr = true;
+  }
+  if (keep < 1.f)
+    attn_bwd_x6_k<true><<<grid, 256, BWD_SMEM, s>>>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv, dq_acc,
+                                                    dq_ld, S, nh, keep);
+  else
+    attn_bwd_x6_k<false><<<grid, 256, BWD_SMEM, s>>>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv,
+                                                     dq_acc, dq_ld, S, nh, keep);
 }

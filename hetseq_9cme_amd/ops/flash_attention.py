@@ -14,6 +14,7 @@ other shapes / dtypes use the composite below (batched GEMMs + softmax), which
 is also the CPU path and the test oracle.
 """
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -60,6 +61,10 @@ def _bias3(bq, bk, bv):
     return v if v is not None else torch.cat([bq, bk, bv], 0)
 
 
+# HX_ATTN_X6_BWD=0 keeps the fp32-MFMA backward under --fp32-gemm bf16x6 (A/B switch)
+_X6_BWD = os.environ.get('HX_ATTN_X6_BWD', '1') != '0'
+
+
 class _AttnFn(torch.autograd.Function):
     """Fused attention; with ``bq/bk/bv`` the QKV-projection bias is added to
     Q/K/V inside the kernels as they are loaded (the projection GEMM runs
@@ -73,7 +78,8 @@ class _AttnFn(torch.autograd.Function):
         keep = 1.0 - p
         seed, stream = get_rng().next(qkv.device) if p > 0 else (get_rng().seed_tensor(qkv.device), 0)
         bias = _bias3(bq, bk, bv).float().contiguous() if bq is not None else None
-        if qkv.dtype == torch.float32 and split_gemm.passes() > 0:
+        ctx.split = qkv.dtype == torch.float32 and split_gemm.passes() > 0
+        if ctx.split:
             # fp32 products on the bf16 matrix cores (six piece passes, attention_x6.hip)
             out, lse, dmask = C().attn_fwd_x6(qkv, mask_bias, num_heads, keep, seed, stream, bias)
         else:
@@ -95,8 +101,8 @@ class _AttnFn(torch.autograd.Function):
             slots = [grad_slot(t) for t in (bq, bk, bv)]
             if not all(t is not None for t in slots):
                 slots = [None, None, None]
-        dqkv, dbias = C().attn_bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep, ctx.bias,
-                                   *slots)
+        bwd = C().attn_bwd_x6 if ctx.split and _X6_BWD else C().attn_bwd
+        dqkv, dbias = bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep, ctx.bias, *slots)
         if ctx.bias is None:
             return dqkv, None, None, None, None, None, None
         if slots[0] is not None:

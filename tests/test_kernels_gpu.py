@@ -572,3 +572,52 @@ def test_attention_x6_forward_fp32_exact_class(dev, S, with_bias, keep):
     err_32 = ((out32.double() - ref).abs() / scale).max().item()
     assert err_x6 < 4 * max(err_32, 1e-7), (err_x6, err_32)
     assert (lse.double() - torch.logsumexp(sc, -1)).abs().max().item() < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('S,with_bias,keep', [(128, False, 0.9), (77, True, 0.9), (200, False, 1.0),
+                                              (512, True, 0.9), (640, True, 1.0)])
+def test_attention_x6_backward_fp32_exact_class(dev, S, with_bias, keep):
+    """fp32 attention backward on bf16 MFMA with split pieces (attention_x6.hip): dQ / dK / dV
+    and the QKV-bias gradient against an fp64 autograd reference on the same dropout bits; the
+    error stays in the fp32-MFMA backward's class."""
+    from hetseq_9cme_amd.ops._ext import C
+    torch.manual_seed(1)
+    B, nh, d = 2, 4, 64
+    H = nh * d
+    qkv = 2 * torch.randn(B, S, 3 * H, device=dev)
+    bias = (0.5 * torch.randn(3 * H, device=dev)) if with_bias else None
+    mask = torch.ones(B, S, device=dev)
+    mask[1, S - 29:] = 0
+    mb = ((1 - mask) * -10000.0).contiguous()
+    out, lse, dm = C().attn_fwd(qkv, mb, nh, keep, _seed(dev, 99), 3, bias)
+    dout = torch.randn(B, S, H, device=dev)
+    g6 = C().attn_bwd_x6(dout, qkv, mb, out, lse, dm, nh, keep, bias, None, None, None)
+    g32 = C().attn_bwd(dout, qkv, mb, out, lse, dm, nh, keep, bias, None, None, None)
+
+    x = (qkv.double() + (bias.double() if bias is not None else 0)).requires_grad_(True)
+    q = x.view(B, S, 3, nh, d).permute(2, 0, 3, 1, 4)
+    p = torch.softmax(q[0] @ q[1].transpose(-1, -2) / 8.0 + mb.double()[:, None, None, :], -1)
+    if keep < 1.0:
+        bits = dm.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+        Sp = dm.shape[2]
+        km = ((bits.unsqueeze(-1) >> torch.arange(32, device=dev)) & 1).reshape(B, nh, Sp, Sp)
+        p = p * km[:, :, :S, :S].transpose(-1, -2).double() / keep
+    ref = (p @ q[2]).permute(0, 2, 1, 3).reshape(B, S, H)
+    ref.backward(dout.double())
+    gref = x.grad.view(B, S, 3, H)
+
+    def err(g):
+        g = g.double().view(B, S, 3, H)
+        return [((g[:, :, i] - gref[:, :, i]).abs().max() / gref[:, :, i].abs().max()).item() for i in range(3)]
+
+    # six fp32 accumulation passes per product: a few times the fp32-MFMA kernel's rounding,
+    # orders of magnitude below bf16 (~1e-2)
+    e6, e32 = err(g6[0]), err(g32[0])
+    for a, c in zip(e6, e32):
+        assert a < 8 * max(c, 1e-7) and a < 2e-5, (e6, e32)
+    if with_bias:
+        db_ref = gref.sum((0, 1)).reshape(-1)
+        e_db = ((g6[1].double() - db_ref).abs().max() / db_ref.abs().max()).item()
+        e_db32 = ((g32[1].double() - db_ref).abs().max() / db_ref.abs().max()).item()
+        assert e_db < 8 * max(e_db32, 1e-7) and e_db < 2e-5, (e_db, e_db32)

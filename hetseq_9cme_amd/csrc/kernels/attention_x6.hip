@@ -327,7 +327,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 constexpr int TS = 40;    // transposed 32-query image row stride (bf16)
 constexpr int KTS = 136;  // K^T [dim][128 keys] and dS [query][128 keys] row stride (bf16)
 constexpr int KT_B = 64 * KTS * 2, DS_B = 32 * KTS * 2, QS_B = 32 * RS * 2, QT_B = 64 * TS * 2;
-constexpr int BWD_SMEM = 3 * (KT_B + DS_B + 2 * QS_B + 2 * QT_B) + 2 * 32 * 4;
+constexpr int BWD_SMEM = 3 * (KT_B + DS_B + 2 * QS_B + 2 * QT_B) + 5 * 32 * 4;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
@@ -389,7 +389,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   uint16_t* Qt = dOs + 3 * 32 * RS;                                       // [3][64][TS]
   uint16_t* dOt = Qt + 3 * 64 * TS;                                       // [3][64][TS]
   float* Ls = reinterpret_cast<float*>(dOt + 3 * 64 * TS);                // [32] lse
-  float* Ds = Ls + 32;                                                    // [32] D
+  float* Ds = Ls + 32;                                                    // [32][4 waves] D partials
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int b = blockIdx.z, hd = blockIdx.y;
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   // ---- K^T pieces of the 128 keys (natural key order) for dQ: 64 key pairs x 16 dim quads
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int u = tid + 256 * i, dq = u & 15, kp = u >> 4;
+    const int u = tid + 256 * i, kp = u & 63, dq = u >> 6;   // lanes over key pairs: conflict-free put_t4
     const int k0 = kbase + 2 * kp < S ? kbase + 2 * kp : S - 1;
     const int k1 = kbase + 2 * kp + 1 < S ? kbase + 2 * kp + 1 : S - 1;
     const float4 a = *reinterpret_cast<const float4*>(base + (int64_t)k0 * H3 + H + 4 * dq);
@@ -450,8 +450,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const uint32_t* dmask_bh = kDrop ? dmask + bh * Sp * nwords : nullptr;
   const int moff = mykey * nwords;
 
-  // staging unit of this thread: query pair (2sqp, 2sqp+1) x dims 4sdq .. 4sdq+3
-  const int sdq = tid & 15, sqp = tid >> 4;
+  // staging unit of this thread: query pair (2sqp, 2sqp+1) x dims 4sdq .. 4sdq+3; lanes run
+  // over the query pairs so the transposed-image stores (put_t4) hit 64 distinct banks
+  const int sqp = tid & 15, sdq = tid >> 4;
   float4 pq[2], pd[2], po[2];
   float pl = 0.f;
   uint32_t pm = 0;
@@ -504,14 +505,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     float e0 = pd[0].x * po[0].x + pd[0].y * po[0].y + pd[0].z * po[0].z + pd[0].w * po[0].w;
     float e1 = pd[1].x * po[1].x + pd[1].y * po[1].y + pd[1].z * po[1].z + pd[1].w * po[1].w;
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      e0 += __shfl_xor(e0, o, 64);
-      e1 += __shfl_xor(e1, o, 64);
-    }
-    if (sdq == 0) {
-      Ds[2 * sqp] = e0;
-      Ds[2 * sqp + 1] = e1;
+    // this wave's 16 dims (lanes 16 apart), then one partial per wave: Ds[query][wave]
+    e0 += __shfl_xor(e0, 16, 64);
+    e1 += __shfl_xor(e1, 16, 64);
+    e0 += __shfl_xor(e0, 32, 64);
+    e1 += __shfl_xor(e1, 32, 64);
+    if (lane < 16) {
+      Ds[(2 * sqp) * 4 + w] = e0;
+      Ds[(2 * sqp + 1) * 4 + w] = e1;
     }
     if (tid < 32) Ls[tid] = qt + tid < S ? pl : INFINITY;   // rows past S: P = 0
   };
@@ -526,7 +527,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       float keepf = 1.f;
       if (kDrop) keepf = ((mword >> qr) & 1) ? inv_keep : 0.f;
       sa[r + i] = p * keepf;
-      ds[i] = p * (dpa[r + i] * keepf - Ds[qr]);
+      const float4 dq4 = *reinterpret_cast<const float4*>(&Ds[4 * qr]);
+      ds[i] = p * (dpa[r + i] * keepf - ((dq4.x + dq4.y) + (dq4.z + dq4.w)));
       dpa[r + i] = ds[i];
     }
     uint32_t pc[3];

@@ -72,15 +72,19 @@ __device__ __forceinline__ void split_acc(const f32x16& s, bf16x8 (&p)[3]) {
   const float x[8] = {s[O], s[O + 1], s[O + 2], s[O + 3], s[O + 4], s[O + 5], s[O + 6], s[O + 7]};
   split8(x, p[0], p[1], p[2]);
 }
-// one fp32 value -> its three pieces as raw bf16 bits
-__device__ __forceinline__ void split1(float x, uint32_t& a, uint32_t& b, uint32_t& c) {
-  const uint16_t q0 = hx::f2bf(x);
-  x -= hx::bf2f(q0);
-  const uint16_t q1 = hx::f2bf(x);
-  x -= hx::bf2f(q1);
-  a = q0;
-  b = q1;
-  c = hx::f2bf(x);
+// 4 fp32 -> three pieces of 4 bf16 (two words each)
+__device__ __forceinline__ void split4(const float (&x)[4], uint2 (&p)[3]) {
+  float e[4] = {x[0], x[1], x[2], x[3]};
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    p[k].x = peel2(e[0], e[1]);
+    p[k].y = peel2(e[2], e[3]);
+  }
+}
+// two fp32 -> three pieces of 2 bf16 (one word each: value 0 low, value 1 high)
+__device__ __forceinline__ void split2(float x0, float x1, uint32_t (&p)[3]) {
+#pragma unroll
+  for (int k = 0; k < 3; ++k) p[k] = peel2(x0, x1);
 }
 
 // key k (0..63 of a tile) -> its column in the transposed, permuted V image (attention_bf16.hip)
@@ -158,7 +162,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       const float* kp = base + (int64_t)key * H3 + H + c8;
       kr[i][0] = *reinterpret_cast<const float4*>(kp);
       kr[i][1] = *reinterpret_cast<const float4*>(kp + 4);
-      const int dq = e & 15, kp2 = e >> 4;
+      const int kp2 = e & 31, dq = e >> 5;   // lanes over key pairs: the Vt stores spread over the banks
       const int k0 = kt + 2 * kp2 < S ? kt + 2 * kp2 : S - 1, k1 = kt + 2 * kp2 + 1 < S ? kt + 2 * kp2 + 1 : S - 1;
       vr[i][0] = *reinterpret_cast<const float4*>(base + (int64_t)k0 * H3 + 2 * H + 4 * dq);
       vr[i][1] = *reinterpret_cast<const float4*>(base + (int64_t)k1 * H3 + 2 * H + 4 * dq);
@@ -178,7 +182,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       split8(f, p[0], p[1], p[2]);
 #pragma unroll
       for (int pc = 0; pc < 3; ++pc) *reinterpret_cast<bf16x8*>(&Ks[pc][row * RS + c8]) = p[pc];
-      const int dq = e & 15, kp2 = e >> 4;
+      const int kp2 = e & 31, dq = e >> 5;
       float v0[4] = {vr[i][0].x, vr[i][0].y, vr[i][0].z, vr[i][0].w};
       float v1[4] = {vr[i][1].x, vr[i][1].y, vr[i][1].z, vr[i][1].w};
       if (vbias) {
@@ -191,13 +195,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       constexpr int RW = RS / 2;   // row stride in 32-bit words
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        uint32_t a0, a1, a2, b0, b1, b2;
-        split1(v0[j], a0, a1, a2);
-        split1(v1[j], b0, b1, b2);
+        uint32_t pc[3];
+        split2(v0[j], v1[j], pc);   // keys 2kp2 (low half), 2kp2 + 1 (high half)
         const int off = (4 * dq + j) * RW + (vpos(2 * kp2) >> 1);
-        reinterpret_cast<uint32_t*>(Vt[0])[off] = a0 | (b0 << 16);
-        reinterpret_cast<uint32_t*>(Vt[1])[off] = a1 | (b1 << 16);
-        reinterpret_cast<uint32_t*>(Vt[2])[off] = a2 | (b2 << 16);
+        reinterpret_cast<uint32_t*>(Vt[0])[off] = pc[0];
+        reinterpret_cast<uint32_t*>(Vt[1])[off] = pc[1];
+        reinterpret_cast<uint32_t*>(Vt[2])[off] = pc[2];
       }
     }
     if (tid < 64) Ms[tid] = mr;
@@ -343,20 +346,6 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
     ACC = mfma16(A[2], B[0], ACC);        \
   } while (0)
 
-// 4 fp32 -> three pieces of 4 bf16 (two words each)
-__device__ __forceinline__ void split4(const float (&x)[4], uint2 (&p)[3]) {
-  float e[4] = {x[0], x[1], x[2], x[3]};
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    p[k].x = peel2(e[0], e[1]);
-    p[k].y = peel2(e[2], e[3]);
-  }
-}
-// two fp32 -> three pieces of 2 bf16 (one word each: value 0 low, value 1 high)
-__device__ __forceinline__ void split2(float x0, float x1, uint32_t (&p)[3]) {
-#pragma unroll
-  for (int k = 0; k < 3; ++k) p[k] = peel2(x0, x1);
-}
 // rows r0, r1 (consecutive image positions) x 4 dims -> 4 words of a transposed image
 __device__ __forceinline__ void put_t4(uint16_t* img, int stride, int dim0, int pos, uint2 r0, uint2 r1) {
   uint32_t* p = reinterpret_cast<uint32_t*>(img + dim0 * stride + pos);

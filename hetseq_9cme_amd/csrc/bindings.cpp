@@ -368,12 +368,25 @@ std::vector<Tensor> attn_fwd_x6(Tensor qkv, Tensor mask_bias, int64_t nh, double
 
 // returns {dqkv, dbias} (dbias: [3H] fp32 when bias is given -- written into dbq/dbk/dbv
 // when those slots are given -- else an empty tensor)
+// planes form (split only, S <= 128): dQKV as the stacked bf16 planes of order `order`
+// ([B*S, len(order) * 3H]) instead of fp32; returns {planes, dbias}
 std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask,
-                             int64_t nh, double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, bool split = false) {
+                             int64_t nh, double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, bool split = false,
+                             const std::vector<int64_t>& order = {}) {
   check_cuda(dout, "grad_output");
   check_cuda(qkv, "qkv");
   const int bf = act_bf16(qkv);
   TORCH_CHECK(!(split && bf), "attn_bwd_x6: fp32 activations only");
+  const bool pl = !order.empty();
+  uint32_t porder = 0;
+  if (pl) {
+    TORCH_CHECK(split && qkv.size(1) <= 128, "attn_bwd_x6_planes: fp32 split path with S <= 128 only");
+    TORCH_CHECK(order.size() <= 8, "attn_bwd_x6_planes: 1..8 planes");
+    for (size_t k = 0; k < order.size(); ++k) {
+      TORCH_CHECK(order[k] >= 0 && order[k] < 3, "attn_bwd_x6_planes: piece index out of range");
+      porder |= (uint32_t)order[k] << (4 * k);
+    }
+  }
   TORCH_CHECK(dout.scalar_type() == qkv.scalar_type() && out.scalar_type() == qkv.scalar_type(),
               "attention activations must share one dtype");
   const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(2) / 3;
@@ -382,7 +395,9 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor o
   // memset).  Otherwise dQ partials from the S/128 key blocks are added atomically in
   // fp32: into dqkv itself (fp32, zero-filled) or a [B, S, H] fp32 scratch (bf16).
   const bool multi = S > 128;
-  auto dqkv = (multi && !bf) ? torch::zeros_like(qkv) : torch::empty_like(qkv);
+  Tensor dqkv, planes;
+  if (pl) planes = torch::empty({B * S, (int64_t)order.size() * 3 * H}, qkv.options().dtype(torch::kBFloat16));
+  else dqkv = (multi && !bf) ? torch::zeros_like(qkv) : torch::empty_like(qkv);
   Tensor dq32;
   float* dq_acc = nullptr;
   int dq_ld = 0;
@@ -412,8 +427,10 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor o
   }
   hx_attn_bwd(split ? 2 : bf, qkv.data_ptr(), ptr_or_null<float>(bias), pq, pk, pv, part.defined() ? part.data_ptr<float>() : nullptr,
               mask_bias.data_ptr<float>(), dout.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
-              keep < 1.0 ? reinterpret_cast<const uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr, dqkv.data_ptr(),
-              dq_acc, dq_ld, (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv));
+              keep < 1.0 ? reinterpret_cast<const uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr,
+              pl ? nullptr : dqkv.data_ptr(), dq_acc, dq_ld, (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv),
+              pl ? reinterpret_cast<uint16_t*>(planes.data_ptr()) : nullptr, porder, (int)order.size());
+  if (pl) return {planes, dbias};
   if (multi && bf) dqkv.narrow(-1, 0, H).copy_(dq32);
   dbg_finite(dqkv, "attn_bwd");
   return {dqkv, dbias};
@@ -702,6 +719,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_bwd_x6", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
                           double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv) {
     return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, true);
+  });
+  // same, dQKV written as the QKV linear's output-gradient planes (S <= 128)
+  m.def("attn_bwd_x6_planes", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask,
+                                 int64_t nh, double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv,
+                                 std::vector<int64_t> order) {
+    TORCH_CHECK(!order.empty(), "attn_bwd_x6_planes: empty plane order");
+    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, true, order);
   });
   m.def("wgrad_bf16", &wgrad_bf16);
   m.def("wgrad_bf16_ok", &wgrad_bf16_ok);

@@ -330,7 +330,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 constexpr int TS = 40;    // transposed 32-query image row stride (bf16)
 constexpr int KTS = 136;  // K^T [dim][128 keys] and dS [query][128 keys] row stride (bf16)
 constexpr int KT_B = 64 * KTS * 2, DS_B = 32 * KTS * 2, QS_B = 32 * RS * 2, QT_B = 64 * TS * 2;
-constexpr int BWD_SMEM = 3 * (KT_B + DS_B + 2 * QS_B + 2 * QT_B) + 5 * 32 * 4;
+constexpr int BWD_SMEM_IMG = 3 * (KT_B + DS_B + 2 * QS_B + 2 * QT_B) + 5 * 32 * 4;
+constexpr int DQS = 72;   // dQ staging row stride (floats) of the planes form
+constexpr int BWD_SMEM = BWD_SMEM_IMG + 32 * DQS * 4;
+constexpr int EPS = 72;   // dK / dV staging row stride (floats) of the planes form
+
+// Planes form of the output (S <= 128): dQKV goes out as the stacked bf16 planes of the QKV
+// linear's output gradient ([B*S, npl * 3H], plane j = piece order[j], split.hip's layout),
+// which its data- and weight-gradient GEMMs read directly -- no fp32 dQKV written and no
+// split pass reading it back (ops/fused.py GradPlanes).
+struct PlaneOut {
+  uint16_t* p;
+  uint32_t order;   // piece of plane j in bits 4j..4j+3
+  int npl;
+};
+// 8 consecutive fp32 values -> their 16-B chunk in every plane (dst = plane 0's chunk)
+__device__ __forceinline__ void put_planes8(const float (&f)[8], uint16_t* dst, int64_t pstride, const PlaneOut& po) {
+  bf16x8 pc[3];
+  split8(f, pc[0], pc[1], pc[2]);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if (j >= po.npl) break;
+    const int k = (po.order >> (4 * j)) & 15;
+    const bf16x8 v = k == 0 ? pc[0] : (k == 1 ? pc[1] : pc[2]);
+    hx::st_nt16(dst + j * pstride, __builtin_bit_cast(uint4, v));
+  }
+}
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
@@ -364,12 +389,12 @@ __device__ __forceinline__ void ld8(const float* p, const float* bias, float (&f
   }
 }
 
-template <bool kDrop>
+template <bool kDrop, bool kPl>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void attn_bwd_x6_k(
     const float* __restrict__ qkv, const float* __restrict__ qkv_bias, float* __restrict__ dbias_part,
     const float* __restrict__ maskb, const float* __restrict__ dout, const float* __restrict__ outp,
     const float* __restrict__ lse, const uint32_t* __restrict__ dmask, float* __restrict__ dqkv,
-    float* __restrict__ dq_acc, int dq_ld, int S, int nh, float keep) {
+    float* __restrict__ dq_acc, int dq_ld, int S, int nh, float keep, PlaneOut pout) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* Kt = reinterpret_cast<uint16_t*>(smem);                       // [3][64][KTS]
   uint16_t* dSs = reinterpret_cast<uint16_t*>(smem + 3 * KT_B);           // [3][32][KTS]
@@ -379,6 +404,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   uint16_t* dOt = Qt + 3 * 64 * TS;                                       // [3][64][TS]
   float* Ls = reinterpret_cast<float*>(dOt + 3 * 64 * TS);                // [32] lse
   float* Ds = Ls + 32;                                                    // [32][4 waves] D partials
+  float* dQs = reinterpret_cast<float*>(smem + BWD_SMEM_IMG);             // [32][DQS] (planes form)
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int b = blockIdx.z, hd = blockIdx.y;
@@ -553,11 +579,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
   };
 
+  // planes form: the staged dQ tile of queries q0t .. q0t + 31 -> planes (8 columns per thread)
+  const int64_t ldp = (int64_t)pout.npl * H3;
+  auto dq_planes = [&](int q0t) {
+    const int row = tid >> 3, c8 = (tid & 7) * 8;
+    if (q0t + row >= S) return;
+    const float4 a = *reinterpret_cast<const float4*>(&dQs[row * DQS + c8]);
+    const float4 c = *reinterpret_cast<const float4*>(&dQs[row * DQS + c8 + 4]);
+    const float f[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+    put_planes8(f, pout.p + ((int64_t)b * S + q0t + row) * ldp + hd * D + c8, H3, pout);
+  };
+
   stage(0);
   uint32_t mnext = pm;
   for (int qt = 0; qt < S; qt += 32) {
     // tile qt is staged; every wave is done with the previous tile's dS
     __syncthreads();
+    if constexpr (kPl) {
+      if (qt > 0) dq_planes(qt - 32);
+    }
     const uint32_t mword = mnext;
     const bool more = qt + 32 < S;
     if (more) ld_tile(qt + 32);   // in flight during this tile's math
@@ -619,7 +659,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       cq1 += (qa1[0] + qa1[1]) + (qa1[2] + qa1[3]);
     }
     const int dcol = 32 * dp2 + r16;
-    if (single) {
+    if constexpr (kPl) {   // staged; stored as planes after the next barrier
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dQs[(qh * 16 + 4 * kg + r) * DQS + dcol] = qa0[r] * scale;
+        dQs[(qh * 16 + 4 * kg + r) * DQS + dcol + 16] = qa1[r] * scale;
+      }
+    } else if (single) {
       float* dq = dqkv_b + (int64_t)q0 * H3 + dcol;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -636,18 +682,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         atomicAdd(dq + r * dq_ld + 16, qa1[r] * scale);
       }
     }
-  }
-  // ---- epilogue: dK (accumulated against pre-scaled Q: already scaled), dV
-  float* dk = dqkv + (int64_t)b * S * H3 + H + hd * D;
-  float* dvp = dqkv + (int64_t)b * S * H3 + 2 * H + hd * D;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int key = kbase + w * 32 + crow(r, h);
-    if (key >= S) continue;
-    dk[(int64_t)key * H3 + l32] = dk0[r];
-    dk[(int64_t)key * H3 + 32 + l32] = dk1[r];
-    dvp[(int64_t)key * H3 + l32] = dv0[r];
-    dvp[(int64_t)key * H3 + 32 + l32] = dv1[r];
   }
   if (dbias_part) {
     // QKV-bias gradient = column sums of dQ, dK, dV: one row of 3H partials per
@@ -687,6 +721,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       dbias_part[((int64_t)b * gridDim.x + blockIdx.x) * H3 + part * H + hd * D + c] = v;
     }
   }
+  if constexpr (kPl) {
+    __syncthreads();   // the last dQ tile is staged; every wave is done with the images
+    dq_planes(((S - 1) >> 5) << 5);
+    __syncthreads();   // dQs read: the dK / dV staging below may reuse any LDS
+    // ---- epilogue, planes form: dK / dV through LDS ([2][128 keys][EPS]) to 8-column chunks
+    float* ep = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kl = w * 32 + crow(r, h);
+      ep[kl * EPS + l32] = dk0[r];
+      ep[kl * EPS + 32 + l32] = dk1[r];
+      ep[(128 + kl) * EPS + l32] = dv0[r];
+      ep[(128 + kl) * EPS + 32 + l32] = dv1[r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int ch = tid + 256 * i, part = ch >> 10, row = (ch & 1023) >> 3, c8 = (ch & 7) * 8;
+      const int key = kbase + row;
+      if (key >= S) continue;
+      const float4 a = *reinterpret_cast<const float4*>(&ep[(part * 128 + row) * EPS + c8]);
+      const float4 c = *reinterpret_cast<const float4*>(&ep[(part * 128 + row) * EPS + c8 + 4]);
+      const float f[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+      put_planes8(f, pout.p + ((int64_t)b * S + key) * ldp + (1 + part) * H + hd * D + c8, H3, pout);
+    }
+  } else {
+    // ---- epilogue: dK (accumulated against pre-scaled Q: already scaled), dV
+    float* dk = dqkv + (int64_t)b * S * H3 + H + hd * D;
+    float* dvp = dqkv + (int64_t)b * S * H3 + 2 * H + hd * D;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kbase + w * 32 + crow(r, h);
+      if (key >= S) continue;
+      dk[(int64_t)key * H3 + l32] = dk0[r];
+      dk[(int64_t)key * H3 + 32 + l32] = dk1[r];
+      dvp[(int64_t)key * H3 + l32] = dv0[r];
+      dvp[(int64_t)key * H3 + 32 + l32] = dv1[r];
+    }
+  }
 }
 
 #undef HX_X6_16
@@ -706,20 +779,27 @@ void hx_attn_fwd_x6(const float* qkv, const float* bias, const float* maskb, flo
 
 void hx_attn_bwd_x6(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,
                     const float* out, const float* lse, const uint32_t* dmask, float* dqkv, float* dq_acc, int dq_ld,
-                    int B, int S, int nh, float keep, hipStream_t s) {
+                    int B, int S, int nh, float keep, uint16_t* planes, uint32_t order, int npl, hipStream_t s) {
   dim3 grid((S + 127) / 128, nh, B);
   static bool attr = false;
   if (!attr) {   // > 64 KiB of dynamic LDS needs an explicit opt-in (gfx950: 160 KiB per CU)
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_x6_k<true>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, BWD_SMEM);
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_x6_k<false>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, BWD_SMEM);
+    const void* k[4] = {reinterpret_cast<const void*>(&attn_bwd_x6_k<true, false>),
+                        reinterpret_cast<const void*>(&attn_bwd_x6_k<false, false>),
+                        reinterpret_cast<const void*>(&attn_bwd_x6_k<true, true>),
+                        reinterpret_cast<const void*>(&attn_bwd_x6_k<false, true>)};
+    for (const void* f : k) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, BWD_SMEM);
     attr = true;
   }
-  if (keep < 1.f)
-    attn_bwd_x6_k<true><<<grid, 256, BWD_SMEM, s>>>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv, dq_acc,
-                                                    dq_ld, S, nh, keep);
-  else
-    attn_bwd_x6_k<false><<<grid, 256, BWD_SMEM, s>>>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv,
-                                                     dq_acc, dq_ld, S, nh, keep);
+  const PlaneOut po{planes, order, npl};
+#define HX_BWD_X6(D_, P_)                                                                                        \
+  attn_bwd_x6_k<D_, P_><<<grid, 256, BWD_SMEM, s>>>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv, dq_acc, \
+                                                    dq_ld, S, nh, keep, po)
+  if (planes) {   // S <= 128 (one key block: every dQ row complete in one workgroup), checked by the caller
+    if (keep < 1.f) HX_BWD_X6(true, true);
+    else HX_BWD_X6(false, true);
+  } else {
+    if (keep < 1.f) HX_BWD_X6(true, false);
+    else HX_BWD_X6(false, false);
+  }
+#undef HX_BWD_X6
 }

@@ -194,10 +194,11 @@ class BertSelfAttention(nn.Module):
     def forward(self, hidden_states, attention_mask_bias, res_grad=None):
         # bias-less N=3H projection GEMM; the Q/K/V biases are applied (and their
         # gradients produced) inside the fused attention
+        gp = ops.GradPlanes()   # the attention backward hands the projection its gradient planes
         qkv = ops.linear3(hidden_states, self.query.weight, self.key.weight, self.value.weight,
-                          None, None, None, res_grad=res_grad)
+                          None, None, None, res_grad=res_grad, grad_planes=gp)
         return ops.attention(qkv, attention_mask_bias, self.num_attention_heads, self.dropout.p, self.training,
-                             bias=(self.query.bias, self.key.bias, self.value.bias))
+                             bias=(self.query.bias, self.key.bias, self.value.bias), grad_planes=gp)
 
 
 class BertSelfOutput(nn.Module):

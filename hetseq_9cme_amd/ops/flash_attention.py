@@ -63,6 +63,8 @@ def _bias3(bq, bk, bv):
 
 # HX_ATTN_X6_BWD=0 keeps the fp32-MFMA backward under --fp32-gemm bf16x6 (A/B switch)
 _X6_BWD = os.environ.get('HX_ATTN_X6_BWD', '1') != '0'
+# HX_ATTN_PLANES=0 keeps the fp32 dQKV + split pass instead of the gradient-plane hand-off
+_X6_PLANES = os.environ.get('HX_ATTN_PLANES', '1') != '0'
 
 
 class _AttnFn(torch.autograd.Function):
@@ -73,12 +75,14 @@ class _AttnFn(torch.autograd.Function):
     gradient slots, instead of a separate pass over the [B*S, 3H] gradient."""
 
     @staticmethod
-    def forward(ctx, qkv, mask_bias, bq, bk, bv, num_heads, p):
+    def forward(ctx, qkv, mask_bias, bq, bk, bv, num_heads, p, gp):
         from .fused import grad_slot  # noqa: F401  (import cycle guard)
         keep = 1.0 - p
         seed, stream = get_rng().next(qkv.device) if p > 0 else (get_rng().seed_tensor(qkv.device), 0)
         bias = _bias3(bq, bk, bv).float().contiguous() if bq is not None else None
         ctx.split = qkv.dtype == torch.float32 and split_gemm.passes() > 0
+        # one key block (S <= 128): the backward can write the projection's gradient planes
+        ctx.gp = gp if (ctx.split and _X6_BWD and _X6_PLANES and qkv.shape[1] <= 128) else None
         if ctx.split:
             # fp32 products on the bf16 matrix cores (six piece passes, attention_x6.hip)
             out, lse, dmask = C().attn_fwd_x6(qkv, mask_bias, num_heads, keep, seed, stream, bias)
@@ -101,23 +105,35 @@ class _AttnFn(torch.autograd.Function):
             slots = [grad_slot(t) for t in (bq, bk, bv)]
             if not all(t is not None for t in slots):
                 slots = [None, None, None]
-        bwd = C().attn_bwd_x6 if ctx.split and _X6_BWD else C().attn_bwd
-        dqkv, dbias = bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep, ctx.bias, *slots)
+        gp = ctx.gp
+        if gp is not None and gp.want:
+            # dQKV straight into the QKV projection's output-gradient planes (GradPlanes);
+            # autograd gets a zero-storage placeholder the projection never reads
+            n = split_gemm.passes()
+            gp.planes, dbias = C().attn_bwd_x6_planes(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads,
+                                                      keep, ctx.bias, *slots, list(split_gemm.ORDER_Q[n]))
+            from .fused import _zero_scalar
+            dqkv = _zero_scalar(qkv.device, qkv.dtype).expand(qkv.shape)
+        else:
+            bwd = C().attn_bwd_x6 if ctx.split and _X6_BWD else C().attn_bwd
+            dqkv, dbias = bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep, ctx.bias, *slots)
         if ctx.bias is None:
-            return dqkv, None, None, None, None, None, None
+            return dqkv, None, None, None, None, None, None, None
         if slots[0] is not None:
             db = slots
         else:
             H = dbias.numel() // 3
             db = [dbias[:H].view_as(bq), dbias[H:2 * H].view_as(bk), dbias[2 * H:].view_as(bv)]
-        return dqkv, None, db[0], db[1], db[2], None, None
+        return dqkv, None, db[0], db[1], db[2], None, None, None
 
 
-def attention(qkv, mask_bias, num_heads, p, bias=None):
-    """``bias``: optional (bq, bk, bv) of the QKV projection, applied here."""
+def attention(qkv, mask_bias, num_heads, p, bias=None, grad_planes=None):
+    """``bias``: optional (bq, bk, bv) of the QKV projection, applied here;
+    ``grad_planes``: the projection's ``GradPlanes`` mailbox (ops/fused.py)."""
     if _fused_ok(qkv, num_heads):
         bq, bk, bv = bias if bias is not None else (None, None, None)
-        return _AttnFn.apply(qkv.contiguous(), mask_bias.float().contiguous(), bq, bk, bv, int(num_heads), float(p))
+        return _AttnFn.apply(qkv.contiguous(), mask_bias.float().contiguous(), bq, bk, bv, int(num_heads), float(p),
+                             grad_planes)
     if bias is not None:
         qkv = qkv + torch.cat(list(bias), 0).to(qkv.dtype)
     return attention_ref(qkv, mask_bias, num_heads, p)

@@ -305,6 +305,19 @@ def embed_ln(ids, tt, wte, wpe, wtt, gamma, beta, eps, p, training, out_dtype=to
 
 
 # ----------------------------------------------------------------- bias + dropout + residual + LN
+_ZERO_SCALARS = {}
+
+
+def _zero_scalar(device, dtype):
+    """A cached 0-dim zero (one fill per device / dtype instead of one per backward call):
+    the storage behind the expanded placeholder gradients, never written."""
+    key = (device, dtype)
+    z = _ZERO_SCALARS.get(key)
+    if z is None:
+        z = _ZERO_SCALARS[key] = torch.zeros((), dtype=dtype, device=device)
+    return z
+
+
 class _BiasDropResLNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, bias, res, gamma, beta, eps, p, mbox, gp):
@@ -334,7 +347,7 @@ class _BiasDropResLNFn(torch.autograd.Function):
                 dout.contiguous(), z, mean, rstd, gamma, keep, seed, stream, has_bias, list(split_gemm.ORDER_Q[n]),
                 split_gemm.PIECES[n], grad_slot(gamma), grad_slot(beta), grad_slot(bias) if has_bias else None)
             gp.planes = planes
-            dy_ret = torch.zeros((), dtype=z.dtype, device=z.device).expand(ctx.yshape)
+            dy_ret = _zero_scalar(z.device, z.dtype).expand(ctx.yshape)
         else:
             dz, dy, dgamma, dbeta, dbias = C().ln_bwd(dout.contiguous(), z, mean, rstd, gamma, keep, seed, stream,
                                                       False, need_dy, has_bias, grad_slot(gamma), grad_slot(beta),
@@ -610,7 +623,7 @@ class _Linear3Fn(torch.autograd.Function):
     """y = x @ [Wq;Wk;Wv]^T + [bq;bk;bv] as ONE GEMM (N = 3H)."""
 
     @staticmethod
-    def forward(ctx, x, wq, wk, wv, bq, bk, bv, mbox):
+    def forward(ctx, x, wq, wk, wv, bq, bk, bv, mbox, gp):
         has_b = bq is not None
         W = _adjacent_view([wq, wk, wv])
         if W is None:
@@ -629,6 +642,9 @@ class _Linear3Fn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         ctx.split = split_gemm.active(x2)
         ctx.pieces = ctx.split and split_gemm.nt_ok(W.shape[1], W.shape[0])
+        ctx.gp = gp if (ctx.split and not ctx.pieces and not has_b) else None
+        if ctx.gp is not None:
+            ctx.gp.want = True
         if ctx.pieces:    # fp32 on bf16 matrix cores, hand-written piece GEMMs
             x2 = split_gemm.pieces(x2)
             wf, Wc = split_gemm.weight_pieces(W)
@@ -662,7 +678,7 @@ class _Linear3Fn(torch.autograd.Function):
             n_in = W.shape[0]
             wg = lambda slot: split_gemm.wgrad_pieces(dys, x2, n_out, n_in, slot)
         else:
-            dys = split_gemm.grad_planes(dy2.float()) if ctx.split else None
+            dys = _dy_planes(ctx.gp, dy2) if ctx.split else None
             if ctx.split:
                 dx = _dgrad_split(dys, W, ctx.xshape, ctx.mbox)
             else:
@@ -701,23 +717,26 @@ class _Linear3Fn(torch.autograd.Function):
             if dys is not None:
                 dys.record_stream(side)
         if not has_b:
-            return (dx, gW[0], gW[1], gW[2], None, None, None, None)
+            return (dx, gW[0], gW[1], gW[2], None, None, None, None, None)
         gb = bs if fb is not None else [db[:a], db[a:a + b_], db[a + b_:]]
-        return (dx, gW[0], gW[1], gW[2], gb[0], gb[1], gb[2], None)
+        return (dx, gW[0], gW[1], gW[2], gb[0], gb[1], gb[2], None, None)
 
 
-def linear3(x, wq, wk, wv, bq, bk, bv, res_grad=None):
-    return _Linear3Fn.apply(x, wq, wk, wv, bq, bk, bv, res_grad)
+def linear3(x, wq, wk, wv, bq, bk, bv, res_grad=None, grad_planes=None):
+    """``grad_planes``: see ``GradPlanes`` (the fused attention backward deposits the
+    projection's output-gradient planes)."""
+    return _Linear3Fn.apply(x, wq, wk, wv, bq, bk, bv, res_grad, grad_planes)
 
 
 # ----------------------------------------------------------------- attention core
-def attention(qkv, mask_bias, num_heads, p, training, bias=None):
+def attention(qkv, mask_bias, num_heads, p, training, bias=None, grad_planes=None):
     """softmax(Q K^T / sqrt(d) + mask) -> dropout -> @ V  on the packed [B, S, 3H]
     projection; returns [B, S, H] (reference BertSelfAttention, :351-377).
     ``mask_bias`` is the additive [B, S] key mask ((1 - m) * -10000); ``bias`` the
-    optional (bq, bk, bv) of a bias-less QKV projection, added inside the kernel."""
+    optional (bq, bk, bv) of a bias-less QKV projection, added inside the kernel;
+    ``grad_planes``: the projection's ``GradPlanes`` mailbox."""
     from .flash_attention import attention as _attention
-    return _attention(qkv, mask_bias, num_heads, p if training else 0.0, bias)
+    return _attention(qkv, mask_bias, num_heads, p if training else 0.0, bias, grad_planes)
 
 
 # ----------------------------------------------------------------- MLM decoder + softmax-xent

@@ -328,10 +328,43 @@ def test_ln_bwd_planes_equal_split_of_dy(dev, mode, has_bias, keep):
         ops.set_fp32_gemm('native')
 
 
+@pytest.mark.parametrize('mode,S,with_bias,keep', [('bf16x6', 128, True, 0.9), ('bf16x6', 77, False, 1.0),
+                                                   ('bf16x3', 100, True, 0.9)])
+def test_attn_bwd_planes_equal_split_of_dqkv(dev, mode, S, with_bias, keep):
+    """Split-piece attention backward writing dQKV as the QKV projection's gradient planes:
+    bit-identical to splitting the fp32 dQKV of the same kernel, same QKV-bias gradient."""
+    from hetseq_9cme_amd import ops
+    from hetseq_9cme_amd.ops import split_gemm
+    from hetseq_9cme_amd.ops._ext import C
+    ops.set_fp32_gemm(mode)
+    try:
+        torch.manual_seed(5)
+        B, nh = 3, 4
+        H = nh * 64
+        qkv = torch.randn(B, S, 3 * H, device=dev)
+        bias = 0.3 * torch.randn(3 * H, device=dev) if with_bias else None
+        mb = torch.zeros(B, S, device=dev)
+        mb[1, S - 9:] = -10000.0
+        seed = torch.tensor([77], dtype=torch.int64, device=dev)
+        out, lse, dm = C().attn_fwd_x6(qkv, mb, nh, keep, seed, 2, bias)
+        dout = torch.randn_like(out)
+        dqkv, db = C().attn_bwd_x6(dout, qkv, mb, out, lse, dm, nh, keep, bias, None, None, None)
+        n = split_gemm.passes()
+        planes, db2 = C().attn_bwd_x6_planes(dout, qkv, mb, out, lse, dm, nh, keep, bias, None, None, None,
+                                             list(split_gemm.ORDER_Q[n]))
+        ref = split_gemm.grad_planes(dqkv.view(B * S, 3 * H))
+        assert planes.shape == ref.shape
+        assert torch.equal(planes.view(torch.int16), ref.view(torch.int16))
+        if with_bias:
+            assert torch.equal(db, db2)
+    finally:
+        ops.set_fp32_gemm('native')
+
+
 def test_grad_planes_handoff_in_bert_layer(dev):
-    """A BERT layer under bf16x6 takes the LayerNorm -> linear gradient-plane hand-off, and
-    its gradients equal those of the same layer with the hand-off disabled (to fp32
-    atomic-order noise)."""
+    """A BERT layer under bf16x6 takes the LayerNorm -> linear and attention -> QKV projection
+    gradient-plane hand-offs, and its gradients equal those of the same layer with the
+    hand-offs disabled (to fp32 atomic-order noise)."""
     from hetseq_9cme_amd import ops
     from hetseq_9cme_amd.models.bert import BertConfig, BertLayer
     from hetseq_9cme_amd.ops import fused

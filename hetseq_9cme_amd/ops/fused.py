@@ -142,15 +142,17 @@ def _dgrad_pieces(dys, wt, xshape, mbox):
     return split_gemm.dgrad_pieces(dys, wt).view(xshape)
 
 
-def _dgrad_split(dys, W, xshape, mbox):
-    """``_dgrad`` on the bf16 split planes of dy (``--fp32-gemm bf16x3/x6``)."""
+def _dgrad_split(dys, W, xshape, mbox, prefix=False):
+    """``_dgrad`` on the bf16 split planes of dy (``--fp32-gemm bf16x3/x6``); ``prefix``: dy
+    is in the prefix form's natural piece order (split_gemm.prefix_mm)."""
+    dg = split_gemm.dgrad_prefix if prefix else split_gemm.dgrad
     if mbox is not None:
         g, other = mbox.take(torch.float32)
         if g is not None:
-            return split_gemm.dgrad(dys, W, acc=g.view(-1, W.shape[1])).view(xshape)
-        dx = split_gemm.dgrad(dys, W).view(xshape)
+            return dg(dys, W, acc=g.view(-1, W.shape[1])).view(xshape)
+        dx = dg(dys, W).view(xshape)
         return dx if other is None else dx + other.view(xshape).to(dx.dtype)
-    return split_gemm.dgrad(dys, W).view(xshape)
+    return dg(dys, W).view(xshape)
 
 
 # ----------------------------------------------------------------- weight-grad side stream
@@ -546,8 +548,17 @@ class _FFNSplitFn(torch.autograd.Function):
             ctx.save_for_backward(xs, y1, hs, w1t, b1, w2t)
         else:
             y1, xs = split_gemm.forward(x2, W1)
-            hs = split_gemm.act_planes(y1, b1, 'gelu')
-            y2 = split_gemm.forward_planes(hs, W2)
+            n = split_gemm.passes()
+            # prefix form for the deep products (FFN-down forward, FFN-up data gradient): the
+            # GELU epilogue / backward write each distinct piece once
+            ctx.pf_down = split_gemm.prefix_ok(W2.shape[1], W2.shape[0])
+            ctx.pf_up = split_gemm.prefix_ok(W1.shape[0], W1.shape[1])
+            if ctx.pf_down:
+                hs = split_gemm.act_planes(y1, b1, 'gelu', order=split_gemm.ORDER_N[n])
+                y2 = split_gemm.forward_prefix(hs, W2)
+            else:
+                hs = split_gemm.act_planes(y1, b1, 'gelu')
+                y2 = split_gemm.forward_planes(hs, W2)
             ctx.save_for_backward(xs, y1, hs, W1, b1, W2)
         ctx.W = (W1, W2)
         ctx.mbox = mbox
@@ -573,16 +584,17 @@ class _FFNSplitFn(torch.autograd.Function):
         # --overlap-wgrad: the two weight-gradient GEMMs run on the side stream, beside the
         # memory-bound GELU backward / plane writes of the dgrad chain
         side = side_begin(dy2.device) if slot2 is not None else None
+        nat = split_gemm.ORDER_N[split_gemm.passes()]
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            dW2 = split_gemm.wgrad(dys, hs, W2.shape[0], W2.shape[1], slot2)
+            dW2 = split_gemm.wgrad(dys, hs, W2.shape[0], W2.shape[1], slot2, x_order=nat if ctx.pf_down else None)
         if side is not None:
             dys.record_stream(side)
             hs.record_stream(side)
-        dy1s, db1 = split_gemm.act_grad_planes(dh, y1, b1, 'gelu', grad_slot(b1))
-        dx = _dgrad_split(dy1s, W1, ctx.xshape, ctx.mbox)
+        dy1s, db1 = split_gemm.act_grad_planes(dh, y1, b1, 'gelu', grad_slot(b1), order=nat if ctx.pf_up else None)
+        dx = _dgrad_split(dy1s, W1, ctx.xshape, ctx.mbox, prefix=ctx.pf_up)
         side = side_begin(dy2.device) if slot1 is not None else None
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            dW1 = split_gemm.wgrad(dy1s, xs, W1.shape[0], W1.shape[1], slot1)
+            dW1 = split_gemm.wgrad(dy1s, xs, W1.shape[0], W1.shape[1], slot1, dy_order=nat if ctx.pf_up else None)
         if side is not None:
             dy1s.record_stream(side)
             xs.record_stream(side)

@@ -52,6 +52,10 @@ PIECES = {3: 2, 6: 3}
 ORDER_P = {3: (0, 1, 0), 6: (0, 1, 0, 2, 1, 0)}
 ORDER_Q = {3: (0, 0, 1), 6: (0, 0, 1, 0, 1, 2)}
 MODES = {'native': 0, 'bf16x3': 3, 'bf16x6': 6}
+# Prefix form (see ``prefix_mm``): the large operand holds each distinct piece once, in
+# natural order, and the weight operand piece j repeated npc - j times.
+ORDER_N = {3: (0, 1), 6: (0, 1, 2)}
+ORDER_W_PREFIX = {3: (0, 0, 1), 6: (0, 0, 0, 1, 1, 2)}
 
 
 # Below this many rows (tokens of the GEMM's M side) the split GEMMs lose to native f32
@@ -117,32 +121,32 @@ def forward_planes(xs, W):
 ACT_IDS = {'gelu': 0, 'tanh': 1, 'relu': 2, 'none': 3}
 
 
-def act_planes(y, b, act):
-    """Planes (order P) of act(y + b): the bias-activation epilogue writes the next GEMM's
-    input pieces directly (csrc/kernels/elementwise.hip ``bias_act_planes_k``)."""
+def act_planes(y, b, act, order=None):
+    """Planes (order P, or ``order``) of act(y + b): the bias-activation epilogue writes the
+    next GEMM's input pieces directly (csrc/kernels/elementwise.hip ``bias_act_planes_k``)."""
     n = _State.passes
-    return C().bias_act_planes(y, b, None, ACT_IDS[act], list(ORDER_P[n]), PIECES[n], None)[0]
+    return C().bias_act_planes(y, b, None, ACT_IDS[act], list(order or ORDER_P[n]), PIECES[n], None)[0]
 
 
-def act_grad_planes(dout, y, b, act, dbias_out=None):
-    """(planes (order Q) of dout * act'(y + b), dbias) in one pass."""
+def act_grad_planes(dout, y, b, act, dbias_out=None, order=None):
+    """(planes (order Q, or ``order``) of dout * act'(y + b), dbias) in one pass."""
     n = _State.passes
-    return C().bias_act_planes(y, b, dout, ACT_IDS[act], list(ORDER_Q[n]), PIECES[n], dbias_out)
+    return C().bias_act_planes(y, b, dout, ACT_IDS[act], list(order or ORDER_Q[n]), PIECES[n], dbias_out)
 
 
 def grad_planes(dy2, dpad=0):
     return planes(dy2, ORDER_Q[_State.passes], dpad=dpad)
 
 
-def weight_planes_t(W, rpad=0):
-    """Transposed dgrad operand [K, n * Np] (order P over W's rows, zero-padded to ``rpad``),
-    or None when W's shape does not fit the transposing kernel (64-multiples)."""
+def weight_planes_t(W, rpad=0, order=None):
+    """Transposed dgrad operand [K, n * Np] (order P, or ``order``, over W's rows, zero-padded
+    to ``rpad``), or None when W's shape does not fit the transposing kernel (64-multiples)."""
     N, K = W.shape
     Np = max(N, rpad)
     if K % 64 or Np % 64 or W.stride(-1) != 1 or W.stride(0) % 4 or W.data_ptr() % 16:
         return None
     n = _State.passes
-    return C().split_planes_t(W, list(ORDER_P[n]), PIECES[n], int(rpad))
+    return C().split_planes_t(W, list(order or ORDER_P[n]), PIECES[n], int(rpad))
 
 
 def dgrad(dys, W, acc=None, rpad=0):
@@ -235,17 +239,77 @@ def act_grad_pieces(dout, y, b, act, dbias_out=None):
 
 def _piece_offsets(order, d):
     """Column offset of the first plane holding each distinct piece."""
-    return [order.index(k) * d for k in range(PIECES[len(order)])]
+    return [order.index(k) * d for k in range(len(set(order)))]
 
 
-def wgrad(dys, xs, n_out, n_in, slot):
+def wgrad(dys, xs, n_out, n_in, slot, dy_order=None, x_order=None):
     """dW [n_out, n_in] = sum over tokens and passes of dy-piece^T x-piece.  The
     split-piece kernel (csrc/kernels/wgrad_split.hip) stages each distinct piece once
-    and runs all passes from registers; other shapes use the stacked-rows form."""
+    and runs all passes from registers; other shapes use the stacked-rows form.
+    ``dy_order`` / ``x_order``: the operands' plane orders (default Q / P)."""
     n = _State.passes
+    dy_order, x_order = dy_order or ORDER_Q[n], x_order or ORDER_P[n]
     if C().wgrad_split_ok(dys, xs, n_out, n_in):
         out = slot if slot is not None else torch.empty(n_out, n_in, device=dys.device)
-        return C().wgrad_split(dys, _piece_offsets(ORDER_Q[n], n_out), xs, _piece_offsets(ORDER_P[n], n_in), n,
+        return C().wgrad_split(dys, _piece_offsets(dy_order, n_out), xs, _piece_offsets(x_order, n_in), n,
                                n_out, n_in, out)
+    assert dy_order == ORDER_Q[n] and x_order == ORDER_P[n], 'stacked-rows wgrad needs the pass orders'
     from .fused import _wgrad
     return _wgrad(dys.view(-1, n_out), xs.view(-1, n_in), slot)
+
+
+# ---------------------------------------------------------------- prefix form
+def _prefix_on():
+    import os
+    return os.environ.get('HX_PREFIX_GEMM', '1') != '0'
+
+
+def prefix_ok(k, n_out):
+    """The prefix form pays off for deep, narrow products (reduction k >= 2 x output
+    width: the FFN-down forward and the FFN-up data gradient, k = 4H, n = H): half the plane
+    bytes for the producer to write and the GEMM to read, against two extra passes over the
+    fp32 output; measured 388 vs 420 us for the bare GEMMs at T=16384, k=3072, n=768 before
+    the plane savings, slower for k = n (tools/probe/prefix_gemm_probe.py)."""
+    return _prefix_on() and _State.passes > 0 and k >= 2 * n_out and k % 64 == 0 and n_out % 64 == 0
+
+
+def prefix_mm(ap, wb, k, acc=None):
+    """sum over piece pairs of A_a B_b from the prefix form: ``ap`` = the large operand's
+    distinct pieces [R, npc * k] (natural order 0, 1, 2), ``wb`` = the weight operand
+    [n * k, N] whose row blocks hold piece j repeated npc - j times (ORDER_W_PREFIX).
+    Product j pairs the first npc - j pieces of A with B's piece j -- one library GEMM per
+    piece of B over a column PREFIX of ``ap`` (no copy: lda = npc * k) -- accumulated with
+    beta = 1 (into ``acc`` when given)."""
+    npc = PIECES[_State.passes]
+    c, off = acc, 0
+    for j in range(npc):
+        m = (npc - j) * k
+        a, b = ap[:, :m], wb[off:off + m]
+        off += m
+        if c is None:
+            c = torch.mm(a, b, out_dtype=torch.float32)
+        elif _State.addmm_out_ok is not False:
+            try:
+                c = torch.addmm(c, a, b, out_dtype=torch.float32, out=c)
+                _State.addmm_out_ok = True
+            except (RuntimeError, TypeError):
+                _State.addmm_out_ok = False
+                c = c.add_(torch.mm(a, b, out_dtype=torch.float32))
+        else:
+            c = c.add_(torch.mm(a, b, out_dtype=torch.float32))
+    return c
+
+
+def forward_prefix(xp, W):
+    """y = x @ W^T from x's natural-order pieces (prefix form)."""
+    n = _State.passes
+    return prefix_mm(xp, planes(W, ORDER_W_PREFIX[n]).t(), W.shape[1])
+
+
+def dgrad_prefix(dyp, W, acc=None):
+    """dy @ W from dy's natural-order pieces (prefix form), + ``acc`` if given; the weight
+    operand is W^T's planes in ORDER_W_PREFIX (NT form)."""
+    n = _State.passes
+    wt = weight_planes_t(W, 0, ORDER_W_PREFIX[n])
+    assert wt is not None, 'dgrad_prefix: W shape must be 64-aligned'
+    return prefix_mm(dyp, wt.t(), W.shape[0], acc)

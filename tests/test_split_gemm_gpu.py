@@ -231,10 +231,13 @@ def test_decoder_xent_split(dev, mode, tol):
         assert e < 50 * tol, (mode, e)
 
 
+@pytest.mark.parametrize('prefix', ['1', '0'])
 @pytest.mark.parametrize('mode,tol', [('bf16x3', 8e-6), ('bf16x6', 3e-6)])
-def test_ffn_split_block(dev, mode, tol):
+def test_ffn_split_block(dev, mode, tol, prefix, monkeypatch):
     """FFN block as one node (GELU epilogue writes the FFN-down planes, GELU backward the
-    FFN-up gradient planes + dbias) against an fp64 autograd reference."""
+    FFN-up gradient planes + dbias) against an fp64 autograd reference; with and without the
+    prefix form of the deep products (split_gemm.prefix_mm: distinct pieces only)."""
+    monkeypatch.setenv('HX_PREFIX_GEMM', prefix)
     from hetseq_9cme_amd import ops
     g = torch.Generator(device='cpu').manual_seed(13)
     T, H, I = 384, 256, 1024

@@ -31,6 +31,14 @@ for name, M, N, K in shapes:
     a = (torch.rand(M, n * K, device='cuda') * 2 - 1).bfloat16()
     b = (torch.rand(N, n * K, device='cuda') * 2 - 1).bfloat16()
     ops.append((name, a, b))
+# prefix-form products of the deep, narrow shapes (split_gemm.prefix_mm): column prefixes of a
+# 3-piece operand (row stride 3K) against piece-j weight blocks
+for name, M, N, K in [('down/up-dgrad prefix', T, 768, 3072)]:
+    a3 = (torch.rand(M, 3 * K, device='cuda') * 2 - 1).bfloat16()
+    for j in range(3):
+        m = (3 - j) * K
+        b = (torch.rand(N, m, device='cuda') * 2 - 1).bfloat16()
+        ops.append(('%s %d' % (name, j), a3[:, :m], b))
 base = {name: timeit(lambda: torch.mm(a, b.t(), out_dtype=torch.float32)) for name, a, b in ops}
 out = os.path.join(sys.argv[1] if len(sys.argv) > 1 else '.', 'tunable_bf16.csv')
 torch.cuda.tunable.enable(True)
@@ -43,6 +51,5 @@ torch.cuda.synchronize()
 torch.cuda.tunable.tuning_enable(False)
 tuned = {name: timeit(lambda: torch.mm(a, b.t(), out_dtype=torch.float32)) for name, a, b in ops}
 for name, _, _ in ops:
-    print('{:12s} default {:7.1f} us  tunable {:7.1f} us'.format(name, base[name], tuned[name]), flush=True)
-torch.cuda.tunable.write_file(out)
+    print('{:24s} default {:7.1f} us  tunable {:7.1f} us'.format(name, base[name], tuned[name]), flush=True)
 print('results:', torch.cuda.tunable.get_results())

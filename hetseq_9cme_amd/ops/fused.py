@@ -98,13 +98,16 @@ class GradPlanes(object):
     backward (which runs first) writes those planes directly (``ln_bwd_planes``: no fp32
     dy written and read back, one launch less) and deposits them here; the LayerNorm
     returns a zero-storage placeholder as dy, which the linear never reads.  The linear's
-    forward sets ``want`` only when its backward will take the split-plane path.
+    forward sets ``want`` only when its backward will take the split-plane path, and
+    ``prefix`` when it wants the prefix form (each distinct piece once, natural order:
+    split_gemm.prefix_mm) instead of the pass-stacked order Q.
     """
-    __slots__ = ('want', 'planes')
+    __slots__ = ('want', 'planes', 'prefix')
 
     def __init__(self):
         self.want = False
         self.planes = None
+        self.prefix = False
 
     def take(self):
         p, self.planes = self.planes, None
@@ -657,6 +660,10 @@ class _Linear3Fn(torch.autograd.Function):
         ctx.gp = gp if (ctx.split and not ctx.pieces and not has_b) else None
         if ctx.gp is not None:
             ctx.gp.want = True
+            # deep data gradient (3H -> H): the producer's planes in the prefix form are opt-in
+            # (HX_PREFIX_QKV=1): measured neutral to 0.1 ms/step slower at BERT-base phase 1,
+            # unlike the 4H -> H products (split_gemm.prefix_ok)
+            ctx.gp.prefix = os.environ.get('HX_PREFIX_QKV', '0') == '1' and split_gemm.prefix_ok(W.shape[0], W.shape[1])
         if ctx.pieces:    # fp32 on bf16 matrix cores, hand-written piece GEMMs
             x2 = split_gemm.pieces(x2)
             wf, Wc = split_gemm.weight_pieces(W)
@@ -690,13 +697,17 @@ class _Linear3Fn(torch.autograd.Function):
             n_in = W.shape[0]
             wg = lambda slot: split_gemm.wgrad_pieces(dys, x2, n_out, n_in, slot)
         else:
-            dys = _dy_planes(ctx.gp, dy2) if ctx.split else None
+            dep = ctx.gp.take() if ctx.gp is not None else None
+            pf = dep is not None and ctx.gp.prefix   # the producer wrote the prefix form
             if ctx.split:
-                dx = _dgrad_split(dys, W, ctx.xshape, ctx.mbox)
+                dys = dep if dep is not None else split_gemm.grad_planes(dy2.float())
+                dx = _dgrad_split(dys, W, ctx.xshape, ctx.mbox, prefix=pf)
             else:
+                dys = None
                 dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox)
-            wg = ((lambda slot: split_gemm.wgrad(dys, x2, W.shape[0], W.shape[1], slot)) if ctx.split
-                  else (lambda slot: _wgrad(dy2, x2, slot)))
+            dy_order = split_gemm.ORDER_N[split_gemm.passes()] if pf else None
+            wg = ((lambda slot: split_gemm.wgrad(dys, x2, W.shape[0], W.shape[1], slot, dy_order=dy_order))
+                  if ctx.split else (lambda slot: _wgrad(dy2, x2, slot)))
         a, b_, _ = ctx.n
         # weight grads: ONE GEMM straight into the three adjacent flat slots when possible
         ws = [grad_slot(w) for w in (wq, wk, wv)]

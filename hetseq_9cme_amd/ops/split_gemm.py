@@ -102,7 +102,7 @@ def planes(x2, order, stacked=False, rpad=0, dpad=0):
     [n*Rp, Dp] stacked, rows / columns zero-padded to ``rpad`` / ``dpad``."""
     if x2.stride(-1) != 1:
         x2 = x2.contiguous()
-    return C().split_planes(x2, list(order), PIECES[len(order)], bool(stacked), int(rpad), int(dpad))
+    return C().split_planes(x2, list(order), max(order) + 1, bool(stacked), int(rpad), int(dpad))
 
 
 def forward(x2, W):

@@ -331,9 +331,10 @@ def test_ln_bwd_planes_equal_split_of_dy(dev, mode, has_bias, keep):
         ops.set_fp32_gemm('native')
 
 
+@pytest.mark.parametrize('natural', [False, True])
 @pytest.mark.parametrize('mode,S,with_bias,keep', [('bf16x6', 128, True, 0.9), ('bf16x6', 77, False, 1.0),
                                                    ('bf16x3', 100, True, 0.9)])
-def test_attn_bwd_planes_equal_split_of_dqkv(dev, mode, S, with_bias, keep):
+def test_attn_bwd_planes_equal_split_of_dqkv(dev, mode, S, with_bias, keep, natural):
     """Split-piece attention backward writing dQKV as the QKV projection's gradient planes:
     bit-identical to splitting the fp32 dQKV of the same kernel, same QKV-bias gradient."""
     from hetseq_9cme_amd import ops
@@ -353,9 +354,10 @@ def test_attn_bwd_planes_equal_split_of_dqkv(dev, mode, S, with_bias, keep):
         dout = torch.randn_like(out)
         dqkv, db = C().attn_bwd_x6(dout, qkv, mb, out, lse, dm, nh, keep, bias, None, None, None)
         n = split_gemm.passes()
+        order = split_gemm.ORDER_N[n] if natural else split_gemm.ORDER_Q[n]   # prefix form / pass-stacked
         planes, db2 = C().attn_bwd_x6_planes(dout, qkv, mb, out, lse, dm, nh, keep, bias, None, None, None,
-                                             list(split_gemm.ORDER_Q[n]))
-        ref = split_gemm.grad_planes(dqkv.view(B * S, 3 * H))
+                                             list(order))
+        ref = split_gemm.planes(dqkv.view(B * S, 3 * H), order)
         assert planes.shape == ref.shape
         assert torch.equal(planes.view(torch.int16), ref.view(torch.int16))
         if with_bias:
@@ -370,7 +372,7 @@ def test_grad_planes_handoff_in_bert_layer(dev):
     hand-offs disabled (to fp32 atomic-order noise)."""
     from hetseq_9cme_amd import ops
     from hetseq_9cme_amd.models.bert import BertConfig, BertLayer
-    from hetseq_9cme_amd.ops import fused
+    from hetseq_9cme_amd.ops import fused, split_gemm
     ops.set_fp32_gemm('bf16x6')
     try:
         torch.manual_seed(0)
@@ -379,18 +381,23 @@ def test_grad_planes_handoff_in_bert_layer(dev):
         layer = BertLayer(cfg).to(dev)
         x = torch.randn(4, 64, 128, device=dev, requires_grad=True)
         mb = torch.zeros(4, 64, device=dev)
-        calls = []
-        orig = fused._dy_planes
+        calls, splits = [], []
+        orig, orig_split = fused._dy_planes, split_gemm.grad_planes
 
         def spy(gp, dy2):
             calls.append(gp is not None and gp.planes is not None)
             return orig(gp, dy2)
-        fused._dy_planes = spy
+
+        def spy_split(*a, **k):
+            splits.append(1)
+            return orig_split(*a, **k)
+        fused._dy_planes, split_gemm.grad_planes = spy, spy_split
         try:
             layer(x, mb).pow(2).sum().backward()
         finally:
-            fused._dy_planes = orig
+            fused._dy_planes, split_gemm.grad_planes = orig, orig_split
         assert calls and all(calls), calls
+        assert not splits, 'a linear split its output gradient itself (hand-off missed)'
         g1 = [p.grad.clone() for p in layer.parameters()] + [x.grad.clone()]
         for p in layer.parameters():
             p.grad = None

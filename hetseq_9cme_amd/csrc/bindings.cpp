@@ -284,16 +284,20 @@ std::vector<Tensor> bias_act_bwd(Tensor dout, OptT y, OptT b, OptT saved_out, in
 }
 
 Tensor colsum(Tensor x, OptT scale, OptT out_) {
-  check_cuda(x, "input");
+  TORCH_CHECK(x.is_cuda(), "input must be a GPU tensor");
   const int N = (int)x.size(-1);
-  const int64_t rows = x.numel() / N;
+  // 2-D with unit column stride: any row stride (e.g. the valid columns of a padded buffer)
+  const bool strided2d = x.dim() == 2 && x.stride(1) == 1;
+  TORCH_CHECK(strided2d || x.is_contiguous(), "colsum: contiguous input or 2-D rows with unit column stride");
+  const int64_t rows = strided2d ? x.size(0) : x.numel() / N;
+  const int64_t ld = strided2d ? x.stride(0) : N;
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
   auto f32 = x.options().dtype(torch::kFloat32);
   auto out = has(out_) ? *out_ : torch::empty({N}, f32);
   TORCH_CHECK(out.numel() == N && out.is_contiguous(), "bad colsum output");
   auto ws = torch::empty({(int64_t)hx_colsum_ws_floats(rows, N)}, f32);
   hx_colsum(act_bf16(x), x.data_ptr(), ptr_or_null<float>(scale), ws.data_ptr<float>(), out.data_ptr<float>(), rows,
-            N, 0, cur_stream(x));
+            N, 0, cur_stream(x), ld);
   return out;
 }
 
@@ -604,13 +608,15 @@ Tensor split_planes(Tensor x, std::vector<int64_t> order, int64_t npieces, bool 
   }
   const int64_t R = x.size(0), D = x.size(1), npl = (int64_t)order.size();
   const int64_t Rp = std::max<int64_t>(R, rpad), Dp = std::max<int64_t>(D, dpad);
-  TORCH_CHECK(stacked || Rp == R, "split_planes: row padding only for the stacked layout");
   TORCH_CHECK(Rp * Dp < (1LL << 40) && Dp < (1LL << 31), "split_planes: too large");
   Tensor out = stacked ? torch::empty({npl * Rp, Dp}, x.options().dtype(torch::kBFloat16))
-                       : torch::empty({R, npl * Dp}, x.options().dtype(torch::kBFloat16));
+                       : torch::empty({Rp, npl * Dp}, x.options().dtype(torch::kBFloat16));
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  hx_split_planes(x.data_ptr<float>(), x.stride(0), reinterpret_cast<uint16_t*>(out.data_ptr()), R, (int)D, Rp,
-                  (int)Dp, (int)npieces, (int)npl, packed, stacked ? 1 : 0, cur_stream(x));
+  // interleaved rows past R (row padding, e.g. the vocabulary padded to 256 for aligned GEMM
+  // output rows): the kernel fills the first R rows, the tail is zeroed
+  hx_split_planes(x.data_ptr<float>(), x.stride(0), reinterpret_cast<uint16_t*>(out.data_ptr()), R, (int)D,
+                  stacked ? Rp : R, (int)Dp, (int)npieces, (int)npl, packed, stacked ? 1 : 0, cur_stream(x));
+  if (!stacked && Rp > R) out.narrow(0, R, Rp - R).zero_();
   return out;
 }
 

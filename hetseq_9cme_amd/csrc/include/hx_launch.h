@@ -37,7 +37,7 @@ void hx_bias_act_fwd(int bf16, int act, const void* y, const float* b, void* out
 void hx_bias_act_bwd(int bf16, int act, const void* dout, const void* y, const float* b, const void* saved_out,
                      void* dy, float* partial, float* dbias, int64_t rows, int N, int accumulate, hipStream_t s);
 void hx_colsum(int bf16, void* x, const float* scale, float* partial, float* out, int64_t rows, int N, int accumulate,
-               hipStream_t s);
+               hipStream_t s, int64_t ld = -1);
 void hx_dropout(int bf16, const void* x, void* out, int64_t n, float keep_prob, const uint64_t* seed, uint64_t stream,
                 hipStream_t s);
 

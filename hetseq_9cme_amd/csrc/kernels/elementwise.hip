@@ -251,7 +251,7 @@ __global__ __launch_bounds__(NT) void bias_act_planes_k(const float* __restrict_
 // (the input is only read: scaling it in place would double the HBM traffic)
 template <typename T>
 __global__ __launch_bounds__(NT) void colsum_scalar_k(const T* __restrict__ x, const float* __restrict__ scale,
-                                                    float* __restrict__ partial, int64_t rows, int N) {
+                                                    float* __restrict__ partial, int64_t rows, int N, int64_t ld) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + lane;
@@ -263,12 +263,12 @@ __global__ __launch_bounds__(NT) void colsum_scalar_k(const T* __restrict__ x, c
     float a1 = 0.f, a2 = 0.f, a3 = 0.f;
     int64_t r = r0 + w;
     for (; r + 12 < r1; r += 16) {
-      acc += hx::io<T>::ld(x + r * N + j);
-      a1 += hx::io<T>::ld(x + (r + 4) * N + j);
-      a2 += hx::io<T>::ld(x + (r + 8) * N + j);
-      a3 += hx::io<T>::ld(x + (r + 12) * N + j);
+      acc += hx::io<T>::ld(x + r * ld + j);
+      a1 += hx::io<T>::ld(x + (r + 4) * ld + j);
+      a2 += hx::io<T>::ld(x + (r + 8) * ld + j);
+      a3 += hx::io<T>::ld(x + (r + 12) * ld + j);
     }
-    for (; r < r1; r += 4) acc += hx::io<T>::ld(x + r * N + j);
+    for (; r < r1; r += 4) acc += hx::io<T>::ld(x + r * ld + j);
     acc = (acc + a1) + (a2 + a3);
   }
   red[w][lane] = acc;
@@ -412,8 +412,9 @@ void hx_bias_act_planes(int act, const float* y, const float* b, const float* do
 }
 
 void hx_colsum(int bf16, void* x, const float* scale, float* partial, float* out, int64_t rows, int N,
-               int accumulate, hipStream_t s) {
-  if (N % 4 == 0 && scale == nullptr) {
+               int accumulate, hipStream_t s, int64_t ld) {
+  if (ld < 0) ld = N;
+  if (N % 4 == 0 && scale == nullptr && ld == N) {
     // vector path reusing the bias-act backward with identity activation (no dy written)
     hx_bias_act_bwd(bf16, ACT_NONE, x, nullptr, nullptr, nullptr, nullptr, partial, out, rows, N, accumulate, s);
     return;
@@ -421,8 +422,8 @@ void hx_colsum(int bf16, void* x, const float* scale, float* partial, float* out
   const int ncb = (N + 63) / 64;
   const int nch = nchunks(rows);
   dim3 g(ncb, nch);
-  if (bf16) colsum_scalar_k<uint16_t><<<g, NT, 0, s>>>((const uint16_t*)x, scale, partial, rows, N);
-  else colsum_scalar_k<float><<<g, NT, 0, s>>>((const float*)x, scale, partial, rows, N);
+  if (bf16) colsum_scalar_k<uint16_t><<<g, NT, 0, s>>>((const uint16_t*)x, scale, partial, rows, N, ld);
+  else colsum_scalar_k<float><<<g, NT, 0, s>>>((const float*)x, scale, partial, rows, N, ld);
   hx::fold_rows(partial, nch, N, N, N, out, nullptr, nullptr, accumulate, s);
 }
 

@@ -105,11 +105,12 @@ def planes(x2, order, stacked=False, rpad=0, dpad=0):
     return C().split_planes(x2, list(order), max(order) + 1, bool(stacked), int(rpad), int(dpad))
 
 
-def forward(x2, W):
-    """y = x2 @ W^T in fp32; returns (y, x planes for the backward)."""
+def forward(x2, W, rpad=0):
+    """y = x2 @ W^T in fp32; returns (y, x planes for the backward).  ``rpad``: W's rows
+    zero-padded to this count (y gets rpad columns, the padding ones exactly 0)."""
     n = _State.passes
     xs = planes(x2, ORDER_P[n])
-    wq = planes(W, ORDER_Q[n])
+    wq = planes(W, ORDER_Q[n], rpad=rpad)
     return torch.mm(xs, wq.t(), out_dtype=torch.float32), xs
 
 
@@ -149,6 +150,18 @@ def weight_planes_t(W, rpad=0, order=None):
     return C().split_planes_t(W, list(order or ORDER_P[n]), PIECES[n], int(rpad))
 
 
+def _splitk(m, n, k):
+    """Reduction slabs for a product with few 256 x 256 output tiles and a deep reduction
+    (1 = none): enough slabs for ~512 tiles, each slab >= 8192 deep and a multiple of 64."""
+    tiles = ((m + 255) // 256) * ((n + 255) // 256)
+    if tiles >= 64 or k < 65536 or os.environ.get('HX_SPLITK', '1') == '0':
+        return 1
+    for s in (16, 12, 8, 4, 2):
+        if tiles * s <= 768 and k % (64 * s) == 0 and k // s >= 8192:
+            return s
+    return 1
+
+
 def dgrad(dys, W, acc=None, rpad=0):
     """dy @ W (fp32) from the dy planes; accumulated into ``acc`` (beta = 1) if given.
     ``rpad``: dy's planes were column-padded to this width (W's rows are padded to match).
@@ -160,6 +173,15 @@ def dgrad(dys, W, acc=None, rpad=0):
     wt = weight_planes_t(W, rpad)
     wb = wt.t() if wt is not None else planes(W, ORDER_P[_State.passes], stacked=True, rpad=rpad)
     if acc is None:
+        s = _splitk(dys.shape[0], wb.shape[1], wb.shape[0])
+        if s > 1 and dys.is_contiguous():
+            # narrow output, very deep reduction (the MLM decoder: 2560 x 768 from K' = 6 x 30720):
+            # too few output tiles to fill the CUs, so the reduction is cut into s slabs run as
+            # one strided batched GEMM, partial products summed after (1051 -> 580 us,
+            # tools/probe/decoder_gemm_probe.py)
+            kc = wb.shape[0] // s
+            a = dys.view(dys.shape[0], s, kc).transpose(0, 1)
+            return torch.bmm(a, wb.view(s, kc, wb.shape[1]), out_dtype=torch.float32).sum(0)
         return torch.mm(dys, wb, out_dtype=torch.float32)
     if _State.addmm_out_ok is not False:
         try:

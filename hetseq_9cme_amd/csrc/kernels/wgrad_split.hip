@@ -36,6 +36,7 @@ using hx::attn::f32x16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+typedef __attribute__((address_space(3))) void lds_void;
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 32;   // tokens per pipeline step (two 16-deep MFMA k-steps per barrier)
@@ -67,6 +68,32 @@ __device__ __forceinline__ bf16x8 frag(const char* tile, const int (&lo)[2], con
   return *reinterpret_cast<const bf16x8*>(v);
 }
 
+// one LDS-DMA wave-instruction: 16 B per lane from buffer byte voff (zeros past the buffer's
+// end) to LDS bytes [dst + 16 lane, + 16); dst is wave-uniform.  Issued from asm: the
+// compiler would otherwise wait for every outstanding DMA (vmcnt(0)) before the next LDS
+// read of ANY address, i.e. before the fragment reads of the step being computed, which
+// serialises staging and MFMA work.  The caller retires the DMAs itself (dma_wait) before
+// the barrier that publishes the buffer.  M0 is written and restored inside the statement.
+__device__ __forceinline__ void dma16(u32x4 rsrc, char* dst, uint32_t voff) {
+  const uint32_t m = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lds_void*)dst);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(m), "s"(rsrc)
+               : "memory");
+}
+template <int N>
+__device__ __forceinline__ void dma_wait() {   // at most N of this wave's DMAs still in flight
+  static_assert(N >= 0 && N < 64, "vmcnt field");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// raw buffer descriptor over [p, p + bytes): stride 0, reads past the end return zeros
+__device__ __forceinline__ u32x4 rsrc_of(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)(size_t)p;
+  return u32x4{(uint32_t)a, (uint32_t)(a >> 32) & 0xffffu, bytes, 0x00020000u};
+}
+
 // piece pairs (a, b) of the product, in pass order (ops/split_gemm.py)
 template <int NP>
 struct Pairs;
@@ -90,17 +117,21 @@ struct PieceBases {
 // VGPRs -- the bf16x6 256 x 128 tile spills with two).  MORD: work order inside a token
 // split, 0 = output-column tiles fastest, 1 = output-row tiles fastest (the tiles one XCD
 // runs together then share both operands' token slabs in its L2 when M has few row tiles).
-template <int BM, int BN, int WM, int WN, int NPC, int NP, int AHEAD, int MORD>
+// BKT: tokens per pipeline stage; NBUF: LDS stages (3 only with LDS-DMA staging, AHEAD 0:
+// two stages in flight across each barrier, retired by a counted wait).
+template <int BM, int BN, int WM, int WN, int NPC, int NP, int AHEAD, int MORD, int BKT = BK, int NBUF = 2>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_split_k(PieceBases P, int lda, int ldb,
                                                                            float* __restrict__ out, int M, int N,
                                                                            int T, int kchunk, int nsplit,
                                                                            int mvalid) {
   constexpr int NWM = BM / WM, NW = NWM * (BN / WN), NT = NW * 64;
   constexpr int MB = WM / 32, NB = WN / 32;
-  constexpr int CA = BK * BM / 8 / NT, CB = BK * BN / 8 / NT;   // 16-B chunks per thread per piece
+  constexpr int CA = BKT * BM / 8 / NT, CB = BKT * BN / 8 / NT;   // 16-B chunks per thread per piece
   static_assert(WM % 64 == 0 && WN % 64 == 0, "subtile parity of fragment a is a & 1");
-  static_assert(CA >= 1 && CB >= 1 && BK * BM / 8 % NT == 0 && BK * BN / 8 % NT == 0, "tile / thread mismatch");
-  constexpr int A_BYTES = BK * BM * 2, B_BYTES = BK * BN * 2;
+  static_assert(AHEAD == 0 || (CA >= 1 && CB >= 1 && BKT * BM / 8 % NT == 0 && BKT * BN / 8 % NT == 0),
+                "tile / thread mismatch");
+  static_assert(NBUF == 2 || (NBUF == 3 && AHEAD == 0), "three stages need LDS-DMA staging");
+  constexpr int A_BYTES = BKT * BM * 2, B_BYTES = BKT * BN * 2;
   constexpr int STAGE = NPC * (A_BYTES + B_BYTES);
   extern __shared__ __attribute__((aligned(16))) char lds[];   // [2 stages][NPC A tiles, NPC B tiles]
 
@@ -113,7 +144,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_split_k(Piec
   const int sp = work / (TN * TM);
   const int m0 = mt * BM, n0 = nt * BN;
   const int t0 = sp * kchunk, t1 = min(T, t0 + kchunk);
-  const int nit = (t1 - t0 + BK - 1) / BK;
+  const int nit = (t1 - t0 + BKT - 1) / BKT;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w % NWM, wn = w / NWM, h = lane >> 5, l32 = lane & 31;
@@ -142,9 +173,9 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_split_k(Piec
   tr_base<BM>(lane, alo, ahi);
   tr_base<BN>(lane, blo, bhi);
 
-  u32x4 ra0[NPC][CA], rb0[NPC][CB], ra1[NPC][CA], rb1[NPC][CB];
+  u32x4 ra0[NPC][CA ? CA : 1], rb0[NPC][CB ? CB : 1], ra1[NPC][CA ? CA : 1], rb1[NPC][CB ? CB : 1];
   auto load = [&](int it, u32x4 (&ra)[NPC][CA], u32x4 (&rb)[NPC][CB]) {
-    const uint32_t soa = (uint32_t)it * BK * lda * 2, sob = (uint32_t)it * BK * ldb * 2;
+    const uint32_t soa = (uint32_t)it * BKT * lda * 2, sob = (uint32_t)it * BKT * ldb * 2;
 #pragma unroll
     for (int p = 0; p < NPC; ++p) {
 #pragma unroll
@@ -175,7 +206,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_split_k(Piec
   auto mma = [&](int buf) {
     const char* st = lds + buf * STAGE;
 #pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
+    for (int ks = 0; ks < BKT / 16; ++ks) {
       bf16x8 fa[NPC][MB], fb[NPC][NB];
 #pragma unroll
       for (int p = 0; p < NPC; ++p) {
@@ -197,7 +228,75 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_split_k(Piec
     }
   };
 
-  if constexpr (AHEAD == 2) {
+  if constexpr (AHEAD == 0) {
+    // LDS-DMA staging (buffer_load ... lds): no staging registers and no ds_write pass.  A
+    // DMA wave-instruction writes 1 KiB of LDS lane-linearly, so each lane loads the 16-B
+    // chunk whose swizzled image position (toff) is its lane slot: the inverse of toff on the
+    // SOURCE address, the same image as store() writes.  Step it + 1 is in flight while step
+    // it runs on the matrix cores; the barrier's vmcnt(0) retires it (2 buffers, 1 barrier).
+    constexpr int JA = A_BYTES / 1024 / NW, JB = B_BYTES / 1024 / NW;   // 1-KiB pieces per wave and piece
+    static_assert(JA >= 1 && JB >= 1 && A_BYTES % (1024 * NW) == 0 && B_BYTES % (1024 * NW) == 0,
+                  "tile / wave mismatch");
+    const int wv = __builtin_amdgcn_readfirstlane(w);
+    auto src = [&](int o, int W, int ld, int c0) {   // image byte o of a [BKT][W] tile -> source byte offset
+      const int rb = o / (16 * W), rem = o % (16 * W), sub = rem >> 9;
+      const int row = 8 * rb + (((rem & 511) >> 6) ^ (sub & 1));
+      const int ch = 4 * sub + (((rem & 63) >> 4) ^ ((row >> 2) & 3));
+      return (uint32_t)(row * ld + c0 + 8 * ch) * 2;
+    };
+    u32x4 ra[3], rb[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      ra[p] = rsrc_of(P.a[p] + (int64_t)t0 * lda, abytes);
+      rb[p] = rsrc_of(P.b[p] + (int64_t)t0 * ldb, bbytes);
+    }
+    uint32_t da[JA], db[JB];
+#pragma unroll
+    for (int j = 0; j < JA; ++j) da[j] = src(1024 * (wv * JA + j) + 16 * lane, BM, lda, m0);
+#pragma unroll
+    for (int j = 0; j < JB; ++j) db[j] = src(1024 * (wv * JB + j) + 16 * lane, BN, ldb, n0);
+    auto dma = [&](int it, int buf) {
+      const uint32_t soa = (uint32_t)it * BKT * lda * 2, sob = (uint32_t)it * BKT * ldb * 2;
+      char* st = lds + buf * STAGE;
+#pragma unroll
+      for (int p = 0; p < NPC; ++p) {
+#pragma unroll
+        for (int j = 0; j < JA; ++j)
+          dma16(ra[p], st + p * A_BYTES + 1024 * (wv * JA + j), da[j] + soa);
+#pragma unroll
+        for (int j = 0; j < JB; ++j)
+          dma16(rb[p], st + NPC * A_BYTES + p * B_BYTES + 1024 * (wv * JB + j), db[j] + sob);
+      }
+    };
+    if constexpr (NBUF == 2) {
+      dma(0, 0);
+      dma_wait<0>();
+      __syncthreads();
+      for (int it = 0; it < nit; ++it) {
+        if (it + 1 < nit) dma(it + 1, (it + 1) & 1);
+        mma(it & 1);
+        dma_wait<0>();
+        __syncthreads();
+      }
+    } else {
+      // stage it + 2 is issued into the buffer step it - 1 read (retired by the last barrier);
+      // before the barrier only stage it + 1 must have landed, stage it + 2 stays in flight
+      constexpr int PER = NPC * (JA + JB);   // DMA wave-instructions per stage
+      dma(0, 0);
+      if (nit > 1) dma(1, 1);
+      if (nit > 1) dma_wait<PER>(); else dma_wait<0>();
+      __syncthreads();
+      int cur = 0;
+      for (int it = 0; it < nit; ++it) {
+        const int nxt2 = cur == 0 ? 2 : cur - 1;
+        if (it + 2 < nit) dma(it + 2, nxt2);
+        mma(cur);
+        if (it + 2 < nit) dma_wait<PER>(); else dma_wait<0>();
+        __syncthreads();
+        cur = cur == 2 ? 0 : cur + 1;
+      }
+    }
+  } else if constexpr (AHEAD == 2) {
     load(0, ra0, rb0);
     load(1, ra1, rb1);
     store(0, ra0, rb0);
@@ -254,7 +353,7 @@ __global__ __launch_bounds__(256) void split_sum2_k(const float4* __restrict__ w
   }
 }
 
-template <int BM, int BN, int WM, int WN, int NPC, int NP, int AHEAD, int MORD>
+template <int BM, int BN, int WM, int WN, int NPC, int NP, int AHEAD, int MORD, int BKT = BK, int NBUF = 2>
 void launch(const PieceBases& P, int lda, int ldb, float* out, float* ws, int M, int N, int T, int nsplit,
             int mvalid, hipStream_t s) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
@@ -262,14 +361,14 @@ void launch(const PieceBases& P, int lda, int ldb, float* out, float* ws, int M,
   nsplit = (T + kchunk - 1) / kchunk;
   const int total = (M / BM) * (N / BN) * nsplit;
   const int per = (total + 7) / 8;
-  const size_t smem = 2 * (size_t)NPC * BK * (BM + BN) * sizeof(uint16_t);
+  const size_t smem = NBUF * (size_t)NPC * BKT * (BM + BN) * sizeof(uint16_t);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_split_k<BM, BN, WM, WN, NPC, NP, AHEAD, MORD>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_split_k<BM, BN, WM, WN, NPC, NP, AHEAD, MORD, BKT, NBUF>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
-  wgrad_split_k<BM, BN, WM, WN, NPC, NP, AHEAD, MORD><<<8 * per, NT, smem, s>>>(
+  wgrad_split_k<BM, BN, WM, WN, NPC, NP, AHEAD, MORD, BKT, NBUF><<<8 * per, NT, smem, s>>>(
       P, lda, ldb, nsplit > 1 ? ws : out, M, N, T, kchunk, nsplit, nsplit > 1 ? M : mvalid);
   if (nsplit > 1) {
     const int64_t n4 = (int64_t)mvalid * N / 4, slab4 = (int64_t)M * N / 4;
@@ -281,24 +380,34 @@ void launch(const PieceBases& P, int lda, int ldb, float* out, float* ws, int M,
 
 }  // namespace
 
-// cfg 0: 128x128 workgroup tile, 4 waves of 64x64; cfg 1: 256x128, 8 waves of 64x64.
-// The split count fills one round of workgroup slots (256 for cfg 1, 512 for cfg 0);
-// HX_WGRAD_SPLIT_CFG="cfg:nsplit" overrides (tools/bench_wgrad.py --split-sweep).
+// cfg 0: 128x128 workgroup tile, 4 waves of 64x64; cfg 1: 256x128, 8 waves of 64x64;
+// cfg 2 (bf16x6 only): 256x256, 8 waves of 128x64, LDS-DMA staging into three 16-token
+// stages (0.75 fragment reads per MFMA instead of 1, 2/3 of the staged bytes per FLOP).
+// The split count fills one round of workgroup slots (256 for cfgs 1 / 2, 512 for cfg 0);
+// HX_WGRAD_SPLIT_CFG="cfg:nsplit" overrides (tools/bench_wgrad.py --split).
+static int tile_m(int c) { return c == 0 ? 128 : 256; }
+static int tile_n(int c) { return c == 2 ? 256 : 128; }
+static bool cfg_ok(int c, int M, int N, int passes) {
+  return c >= 0 && c <= 2 && (c != 2 || passes == 6) && M % tile_m(c) == 0 && N % tile_n(c) == 0;
+}
 void hx_wgrad_split_plan(int M, int N, int T, int passes, int* cfg, int* nsplit) {
-  int c = (M % 256 == 0 && N % 128 == 0) ? 1 : 0;
-  const int slots = c == 1 ? 256 : 512;
-  const int tiles0 = (M / (c == 1 ? 256 : 128)) * (N / 128);
+  // cfg 2 where its tiles fill the 256 slots evenly (BERT: QKV, FFN-up / -down dW 3-10 %
+  // faster than cfg 1); with fewer tiles (768 x 768: 9) the deep token split's partial sums
+  // cost more than the larger tile saves, with more than one round (the MLM decoder) the
+  // last round runs part-empty (profiles/r2_wgrad_split_dma.log)
+  const int tiles2 = (M / 256) * (N / 256);
+  int c = cfg_ok(2, M, N, passes) && tiles2 >= 24 && tiles2 <= 256 ? 2 : cfg_ok(1, M, N, passes) ? 1 : 0;
+  const int slots = c == 0 ? 512 : 256;
+  const int tiles0 = (M / tile_m(c)) * (N / tile_n(c));
   int s = std::max(1, slots / std::max(1, tiles0));
   s = std::min(s, std::max(1, T / 256));
   if (const char* e = getenv("HX_WGRAD_SPLIT_CFG")) {
     int ec = -1, es = -1;
-    if (sscanf(e, "%d:%d", &ec, &es) == 2 && ec >= 0 && ec < 2 && es >= 1 && M % (ec == 1 ? 256 : 128) == 0 &&
-        N % 128 == 0) {
+    if (sscanf(e, "%d:%d", &ec, &es) == 2 && es >= 1 && cfg_ok(ec, M, N, passes)) {
       c = ec;
       s = std::min(es, std::max(1, T / BK));
     }
   }
-  (void)passes;
   *cfg = c;
   *nsplit = s;
 }
@@ -315,17 +424,23 @@ int hx_wgrad_split(const void* const* dy_pieces, int ldy, const void* const* x_p
   // default: two register stages; output-row tiles fastest when there are fewer of them
   // than column tiles (768 x 3072 FFN-down dW: 421 -> 406 us; tools/bench_wgrad.py --split 6
   // --variants, profiles/r2_wgrad_split_variants.log -- the other variants are within 3 %)
-  int ahead = 2, mord = M < N ? 1 : 0;
+  // bf16x6: LDS-DMA staging (AHEAD 0) -- 6-8 % faster than the register pipelines at every
+  // BERT shape; bf16x3 keeps two register stages (its DMA variant is up to 12 % slower)
+  int ahead = passes == 6 ? 0 : 2, mord = M < N ? 1 : 0;
   if (const char* e = getenv("HX_WGRAD_SPLIT_VAR")) {
     int a = 0, o = 0;
-    if (sscanf(e, "%d,%d", &a, &o) == 2 && (a == 1 || a == 2) && (o == 0 || o == 1)) {
+    if (sscanf(e, "%d,%d", &a, &o) == 2 && (a >= 0 && a <= 2) && (o == 0 || o == 1)) {
       ahead = a;
       mord = o;
     }
   }
 #define HX_WS_LAUNCH(BM_, NPC_, NP_)                                                           \
   do {                                                                                         \
-    if (ahead == 2 && mord == 0)                                                               \
+    if (ahead == 0 && mord == 0)                                                               \
+      launch<BM_, 128, 64, 64, NPC_, NP_, 0, 0>(P, ldy, ldx, out, ws, M, N, T, nsplit, mvalid, s);     \
+    else if (ahead == 0)                                                                       \
+      launch<BM_, 128, 64, 64, NPC_, NP_, 0, 1>(P, ldy, ldx, out, ws, M, N, T, nsplit, mvalid, s);     \
+    else if (ahead == 2 && mord == 0)                                                          \
       launch<BM_, 128, 64, 64, NPC_, NP_, 2, 0>(P, ldy, ldx, out, ws, M, N, T, nsplit, mvalid, s);     \
     else if (ahead == 2)                                                                       \
       launch<BM_, 128, 64, 64, NPC_, NP_, 2, 1>(P, ldy, ldx, out, ws, M, N, T, nsplit, mvalid, s);     \
@@ -340,7 +455,12 @@ int hx_wgrad_split(const void* const* dy_pieces, int ldy, const void* const* x_p
     else
       HX_WS_LAUNCH(128, 2, 3);
   } else if (passes == 6) {
-    if (cfg == 1)
+    if (cfg == 2) {
+      if (mord == 0)
+        launch<256, 256, 128, 64, 3, 6, 0, 0, 16, 3>(P, ldy, ldx, out, ws, M, N, T, nsplit, mvalid, s);
+      else
+        launch<256, 256, 128, 64, 3, 6, 0, 1, 16, 3>(P, ldy, ldx, out, ws, M, N, T, nsplit, mvalid, s);
+    } else if (cfg == 1)
       HX_WS_LAUNCH(256, 3, 6);
     else
       HX_WS_LAUNCH(128, 3, 6);

@@ -59,3 +59,29 @@ def test_two_rank_gpu_equivalence(dev, tmp_path):
     for k, v in ck['one6']['model'].items():
         torch.testing.assert_close(ck['two6']['model'][k], v, rtol=1e-4, atol=1e-6, msg=k)
     assert ck['two2']['optimizer_history'][-1]['num_updates'] == 2
+
+
+def test_bench_two_ranks_contract(tmp_path):
+    """bench.py under torch.distributed.run with 2 ranks (the driver's N > 1 launch; here both
+    ranks share the box's GPU over gloo): one JSON line from rank 0 with the whole-job value,
+    n_gpus = 2 and the global batch of both ranks."""
+    import json
+    import socket
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, PYTHONPATH=ROOT, TMPDIR=str(tmp_path))
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2', '--master-addr',
+           '127.0.0.1', '--master-port', str(port), os.path.join(ROOT, 'bench.py'), '--gpus', '2', '--steps', '3',
+           '--warmup', '1', '--model', 'tiny', '--batch', '8', '--backend', 'gloo', '--same-device',
+           '--num-workers', '1']
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, timeout=300,
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-3000:]
+    rec = json.loads(lines[0])
+    assert rec['n_gpus'] == 2 and rec['steps'] == 3 and rec['warmup'] == 1
+    assert rec['config']['global_batch'] == 16 and rec['config']['parallelism'] == 'dp2'
+    assert rec['value'] > 0 and rec['ms_per_step'] > 0
+    assert abs(rec['value'] - 16 * 1000.0 / rec['ms_per_step']) / rec['value'] < 1e-3

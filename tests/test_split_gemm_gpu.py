@@ -444,3 +444,44 @@ def test_wgrad_split_row_padded_output(dev, T):
         assert ((part.double().cpu() - ref).abs() / scale).max().item() < 2e-6
     finally:
         ops.set_fp32_gemm('native')
+
+
+@pytest.mark.parametrize('T', [77, 1000, 4096])
+def test_wgrad_split_pipeline_variants(dev, T, monkeypatch):
+    """Every tile configuration and pipeline variant of the split-piece weight-gradient kernel
+    (register staging two or one step ahead, LDS-DMA staging into two or three stages; both
+    work orders) matches the fp64 product, also for token counts that end inside a pipeline
+    step.  The planes are row views of a larger NaN-filled buffer, so a read past the last
+    token would poison the result."""
+    from hetseq_9cme_amd import ops
+    from hetseq_9cme_amd.ops import split_gemm as sg
+    from hetseq_9cme_amd.ops._ext import C
+    ops.set_fp32_gemm('bf16x6')
+    try:
+        g = torch.Generator(device='cpu').manual_seed(T)
+        M, N = 768, 256
+        dy = torch.randn(T, M, generator=g).to(dev)
+        x = torch.randn(T, N, generator=g).to(dev)
+
+        def nan_tail(p):
+            big = torch.full((p.shape[0] + 64, p.shape[1]), float('nan'), device=dev).to(p.dtype)
+            big[:p.shape[0]].copy_(p)
+            return big[:p.shape[0]]
+        dys, xs = nan_tail(sg.grad_planes(dy)), nan_tail(sg.planes(x, sg.ORDER_P[6]))
+        po, px = sg._piece_offsets(sg.ORDER_Q[6], M), sg._piece_offsets(sg.ORDER_P[6], N)
+        ref = dy.double().t() @ x.double()
+        scale = dy.double().abs().t() @ x.double().abs()
+        for cfg in ['0:3', '1:2', '2:3', '2:1']:
+            monkeypatch.setenv('HX_WGRAD_SPLIT_CFG', cfg)
+            outs = {}
+            for var in ['2,0', '2,1', '1,0', '1,1', '0,0', '0,1']:
+                monkeypatch.setenv('HX_WGRAD_SPLIT_VAR', var)
+                slot = torch.empty(M, N, device=dev)
+                C().wgrad_split(dys, po, xs, px, 6, M, N, slot)
+                torch.cuda.synchronize()
+                outs[var] = slot
+                assert ((slot.double() - ref).abs() / scale).max().item() < 2e-6, (cfg, var)
+            # same token-split plan and summation order: the staging path does not change a bit
+            assert torch.equal(outs['0,0'], outs['2,0']) and torch.equal(outs['0,1'], outs['2,1']), cfg
+    finally:
+        ops.set_fp32_gemm('native')

@@ -131,20 +131,18 @@ def split_bench(T, passes):
         print('[{}x{} T={} x{}] stacked {:8.1f} us {:7.1f} TF/s'.format(n_out, n_in, T, passes, stacked,
                                                                        fl / stacked / 1e6), flush=True)
         po, px = sg._piece_offsets(sg.ORDER_Q[passes], n_out), sg._piece_offsets(sg.ORDER_P[passes], n_in)
-        for cfg in (0, 1):
-            if n_out % (256 if cfg else 128):
-                continue
-            for ns in (0, 1, 2, 3, 4, 6, 8):
-                if ns:
-                    os.environ['HX_WGRAD_SPLIT_CFG'] = '{}:{}'.format(cfg, ns)
-                else:
-                    os.environ.pop('HX_WGRAD_SPLIT_CFG', None)
-                us = timeit(lambda: C().wgrad_split(dys, po, xs, px, passes, n_out, n_in, slot))
-                err = ((slot.double() - ref).abs() / scale).max().item()
-                print('[{}x{} T={} x{}] split cfg {} nsplit {} {:8.1f} us {:7.1f} TF/s err {:.2e}'.format(
-                    n_out, n_in, T, passes, cfg, ns or 'plan', us, fl / us / 1e6, err), flush=True)
-                if not ns and cfg == 1:
-                    break
+        runs = [(None, 0)] + [(cfg, ns) for cfg in (0, 1, 2) for ns in (1, 2, 3, 4, 6, 7, 8, 9, 12)
+                              if not (n_out % (256 if cfg else 128) or (cfg == 2 and (passes != 6 or n_in % 256)))]
+        for cfg, ns in runs:
+            if ns:
+                os.environ['HX_WGRAD_SPLIT_CFG'] = '{}:{}'.format(cfg, ns)
+            else:
+                os.environ.pop('HX_WGRAD_SPLIT_CFG', None)
+            us = timeit(lambda: C().wgrad_split(dys, po, xs, px, passes, n_out, n_in, slot))
+            err = ((slot.double() - ref).abs() / scale).max().item()
+            print('[{}x{} T={} x{}] split cfg {} nsplit {} {:8.1f} us {:7.1f} TF/s err {:.2e}'.format(
+                n_out, n_in, T, passes, 'plan' if cfg is None else cfg, ns or 'plan', us, fl / us / 1e6, err),
+                flush=True)
         os.environ.pop('HX_WGRAD_SPLIT_CFG', None)
 
 
@@ -155,7 +153,7 @@ def split_variants(T, passes, rounds=3):
     from hetseq_9cme_amd.ops import split_gemm as sg
     from hetseq_9cme_amd.ops._ext import C
     ops.set_fp32_gemm('bf16x{}'.format(passes))
-    variants = ['2,0', '2,1', '1,0', '1,1']
+    variants = ['2,0', '2,1', '1,0', '1,1', '0,0', '0,1']
     for (n_out, n_in) in [(3072, 768), (768, 3072), (2304, 768), (768, 768)]:
         dy = torch.randn(T, n_out, device='cuda')
         x = torch.randn(T, n_in, device='cuda')

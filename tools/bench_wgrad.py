@@ -131,7 +131,7 @@ def split_bench(T, passes):
         print('[{}x{} T={} x{}] stacked {:8.1f} us {:7.1f} TF/s'.format(n_out, n_in, T, passes, stacked,
                                                                        fl / stacked / 1e6), flush=True)
         po, px = sg._piece_offsets(sg.ORDER_Q[passes], n_out), sg._piece_offsets(sg.ORDER_P[passes], n_in)
-        cfgs = [int(c) for c in os.environ.get('HX_SWEEP_CFGS', '0,1,2,3').split(',')]
+        cfgs = [int(c) for c in os.environ.get('HX_SWEEP_CFGS', '0,1,2').split(',')]
         runs = [(None, 0)] + [(cfg, ns) for cfg in cfgs for ns in (1, 2, 3, 4, 6, 7, 8, 9, 12, 14, 16)
                               if not (n_out % (256 if cfg else 128) or (cfg >= 2 and passes != 6)
                                       or (cfg == 2 and n_in % 256))]

@@ -120,9 +120,7 @@ struct PieceBases {
 // BKT: tokens per pipeline stage; NBUF: LDS stages (3 only with LDS-DMA staging, AHEAD 0:
 // two stages in flight across each barrier, retired by a counted wait).
 template <int BM, int BN, int WM, int WN, int NPC, int NP, int AHEAD, int MORD, int BKT = BK, int NBUF = 2>
-__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64)
-__attribute__((amdgpu_waves_per_eu((BM / WM) * (BN / WN) == 4 && AHEAD == 0 && NBUF == 2 && BKT == 16 ? 2 : 1)))
-void wgrad_split_k(PieceBases P, int lda, int ldb,
+__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_split_k(PieceBases P, int lda, int ldb,
                                                                            float* __restrict__ out, int M, int N,
                                                                            int T, int kchunk, int nsplit,
                                                                            int mvalid) {
@@ -387,12 +385,10 @@ void launch(const PieceBases& P, int lda, int ldb, float* out, float* ws, int M,
 // stages (0.75 fragment reads per MFMA instead of 1, 2/3 of the staged bytes per FLOP).
 // The split count fills one round of workgroup slots (256 for cfgs 1 / 2, 512 for cfg 0);
 // HX_WGRAD_SPLIT_CFG="cfg:nsplit" overrides (tools/bench_wgrad.py --split).
-// cfg 3 (bf16x6 only): 256x128, 4 waves of 128x64, LDS-DMA into two 16-token stages (72 KiB):
-// two workgroups per CU, so one workgroup's waves compute while the other's wait at its barrier.
 static int tile_m(int c) { return c == 0 ? 128 : 256; }
 static int tile_n(int c) { return c == 2 ? 256 : 128; }
 static bool cfg_ok(int c, int M, int N, int passes) {
-  return c >= 0 && c <= 3 && (c < 2 || passes == 6) && M % tile_m(c) == 0 && N % tile_n(c) == 0;
+  return c >= 0 && c <= 2 && (c != 2 || passes == 6) && M % tile_m(c) == 0 && N % tile_n(c) == 0;
 }
 void hx_wgrad_split_plan(int M, int N, int T, int passes, int* cfg, int* nsplit) {
   // cfg 2 where its tiles fill the 256 slots evenly (BERT: QKV, FFN-up / -down dW 3-10 %
@@ -401,7 +397,7 @@ void hx_wgrad_split_plan(int M, int N, int T, int passes, int* cfg, int* nsplit)
   // last round runs part-empty (profiles/r2_wgrad_split_dma.log)
   const int tiles2 = (M / 256) * (N / 256);
   int c = cfg_ok(2, M, N, passes) && tiles2 >= 24 && tiles2 <= 256 ? 2 : cfg_ok(1, M, N, passes) ? 1 : 0;
-  const int slots = (c == 0 || c == 3) ? 512 : 256;
+  const int slots = c == 0 ? 512 : 256;
   const int tiles0 = (M / tile_m(c)) * (N / tile_n(c));
   int s = std::max(1, slots / std::max(1, tiles0));
   s = std::min(s, std::max(1, T / 256));
@@ -459,12 +455,7 @@ int hx_wgrad_split(const void* const* dy_pieces, int ldy, const void* const* x_p
     else
       HX_WS_LAUNCH(128, 2, 3);
   } else if (passes == 6) {
-    if (cfg == 3) {
-      if (mord == 0)
-        launch<256, 128, 128, 64, 3, 6, 0, 0, 16, 2>(P, ldy, ldx, out, ws, M, N, T, nsplit, mvalid, s);
-      else
-        launch<256, 128, 128, 64, 3, 6, 0, 1, 16, 2>(P, ldy, ldx, out, ws, M, N, T, nsplit, mvalid, s);
-    } else if (cfg == 2) {
+    if (cfg == 2) {
       if (mord == 0)
         launch<256, 256, 128, 64, 3, 6, 0, 0, 16, 3>(P, ldy, ldx, out, ws, M, N, T, nsplit, mvalid, s);
       else

@@ -471,7 +471,7 @@ def test_wgrad_split_pipeline_variants(dev, T, monkeypatch):
         po, px = sg._piece_offsets(sg.ORDER_Q[6], M), sg._piece_offsets(sg.ORDER_P[6], N)
         ref = dy.double().t() @ x.double()
         scale = dy.double().abs().t() @ x.double().abs()
-        for cfg in ['0:3', '1:2', '2:3', '2:1', '3:5']:
+        for cfg in ['0:3', '1:2', '2:3', '2:1']:
             monkeypatch.setenv('HX_WGRAD_SPLIT_CFG', cfg)
             outs = {}
             for var in ['2,0', '2,1', '1,0', '1,1', '0,0', '0,1']:

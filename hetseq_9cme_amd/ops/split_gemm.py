@@ -59,11 +59,13 @@ ORDER_W_PREFIX = {3: (0, 0, 1), 6: (0, 0, 0, 1, 1, 2)}
 
 
 # Below this many rows (tokens of the GEMM's M side) the split GEMMs lose to native f32
-# MFMA (smaller grids, split overhead): BERT-base at 32 x 128 tokens ran 22.6 ms/step with
-# bf16x6 everywhere vs 21.2 ms native.  Both are fp32-exact class, so small GEMMs (MLM
-# head on the masked rows, pooler, small batches) simply stay native.
+# MFMA (smaller grids, split overhead).  BERT-base at 32 x 128 = 4096 tokens: 19.7 ms/step on
+# the bf16x6 path vs 21.2 ms native (round 2, after the NT-form data gradients and the LDS-DMA
+# weight-gradient kernel; it was 22.6 vs 21.2 before them); NER fine-tuning batches (~1000
+# tokens) still run faster native (10.8 vs 12.9 ms/update).  Both are fp32-exact class, so
+# small GEMMs (MLM head on the masked rows, pooler, small batches) simply stay native.
 MIN_ROWS = {3: int(os.environ.get('HETSEQ_SPLIT_MIN_ROWS_X3', '2048')),
-            6: int(os.environ.get('HETSEQ_SPLIT_MIN_ROWS_X6', '8192'))}
+            6: int(os.environ.get('HETSEQ_SPLIT_MIN_ROWS_X6', '4096'))}
 
 
 class _State(object):

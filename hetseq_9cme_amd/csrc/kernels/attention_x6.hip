@@ -331,7 +331,7 @@ constexpr int TS = 40;    // transposed 32-query image row stride (bf16)
 constexpr int KTS = 136;  // K^T [dim][128 keys] and dS [query][128 keys] row stride (bf16)
 constexpr int KT_B = 64 * KTS * 2, DS_B = 32 * KTS * 2, QS_B = 32 * RS * 2, QT_B = 64 * TS * 2;
 constexpr int BWD_SMEM_IMG = 3 * (KT_B + DS_B + 2 * QS_B + 2 * QT_B) + 5 * 32 * 4;
-constexpr int DQS = 72;   // dQ staging row stride (floats) of the planes form
+constexpr int DQS = 68;   // dQ staging row stride (floats) of the planes form: rows 4 apart on distinct banks
 constexpr int BWD_SMEM = BWD_SMEM_IMG + 32 * DQS * 4;
 constexpr int EPS = 72;   // dK / dV staging row stride (floats) of the planes form
 
@@ -509,12 +509,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     split4(d0, d0p);
     split4(d1, d1p);
     const int pos = vpos(2 * sqp);
+    // rows 16..31 of the Q / dO images hold their 16-B chunks pair-swapped (chunk ^ 1): query
+    // pairs sqp and sqp + 8 are 8 x 144 B apart, i.e. on the same banks, without it
+    const int qcol = 8 * ((sdq >> 1) ^ (sqp >> 3)) + 4 * (sdq & 1);
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
-      *reinterpret_cast<uint2*>(&Qs[p * 32 * RS + (2 * sqp) * RS + 4 * sdq]) = q0p[p];
-      *reinterpret_cast<uint2*>(&Qs[p * 32 * RS + (2 * sqp + 1) * RS + 4 * sdq]) = q1p[p];
-      *reinterpret_cast<uint2*>(&dOs[p * 32 * RS + (2 * sqp) * RS + 4 * sdq]) = d0p[p];
-      *reinterpret_cast<uint2*>(&dOs[p * 32 * RS + (2 * sqp + 1) * RS + 4 * sdq]) = d1p[p];
+      *reinterpret_cast<uint2*>(&Qs[p * 32 * RS + (2 * sqp) * RS + qcol]) = q0p[p];
+      *reinterpret_cast<uint2*>(&Qs[p * 32 * RS + (2 * sqp + 1) * RS + qcol]) = q1p[p];
+      *reinterpret_cast<uint2*>(&dOs[p * 32 * RS + (2 * sqp) * RS + qcol]) = d0p[p];
+      *reinterpret_cast<uint2*>(&dOs[p * 32 * RS + (2 * sqp + 1) * RS + qcol]) = d1p[p];
       put_t4(Qt + p * 64 * TS, TS, 4 * sdq, pos, q0p[p], q1p[p]);
       put_t4(dOt + p * 64 * TS, TS, 4 * sdq, pos, d0p[p], d1p[p]);
     }
@@ -609,8 +612,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       bf16x8 qa[3], da[3];
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
-        qa[p] = *reinterpret_cast<const bf16x8*>(&Qs[p * 32 * RS + l32 * RS + 16 * ks + 8 * h]);
-        da[p] = *reinterpret_cast<const bf16x8*>(&dOs[p * 32 * RS + l32 * RS + 16 * ks + 8 * h]);
+        const int qc = 8 * ((2 * ks + h) ^ (l32 >> 4));   // the stores' chunk swizzle
+        qa[p] = *reinterpret_cast<const bf16x8*>(&Qs[p * 32 * RS + l32 * RS + qc]);
+        da[p] = *reinterpret_cast<const bf16x8*>(&dOs[p * 32 * RS + l32 * RS + qc]);
       }
       HX_X6(sa, qa, kf[ks]);
       HX_X6(dpa, da, vf[ks]);

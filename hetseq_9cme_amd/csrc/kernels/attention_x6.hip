@@ -509,9 +509,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     split4(d0, d0p);
     split4(d1, d1p);
     const int pos = vpos(2 * sqp);
-    // rows 16..31 of the Q / dO images hold their 16-B chunks pair-swapped (chunk ^ 1): query
-    // pairs sqp and sqp + 8 are 8 x 144 B apart, i.e. on the same banks, without it
-    const int qcol = 8 * ((sdq >> 1) ^ (sqp >> 3)) + 4 * (sdq & 1);
+    // Q / dO image rows q with q2 ^ q3 ^ q4 = 1 hold their 16-B chunks pair-swapped (chunk ^ 1):
+    // the staging stores drop from 4-way to 2-way bank conflicts (the minimum for this thread
+    // map) and the 16-B fragment reads stay conflict-free (searched over all XOR swizzles of
+    // the row bits under the guide's ds_write_b64 / ds_read_b128 lane groups)
+    const int qcol = 8 * ((sdq >> 1) ^ (((sqp >> 1) ^ (sqp >> 2) ^ (sqp >> 3)) & 1)) + 4 * (sdq & 1);
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
       *reinterpret_cast<uint2*>(&Qs[p * 32 * RS + (2 * sqp) * RS + qcol]) = q0p[p];
@@ -612,7 +614,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       bf16x8 qa[3], da[3];
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
-        const int qc = 8 * ((2 * ks + h) ^ (l32 >> 4));   // the stores' chunk swizzle
+        const int qc = 8 * ((2 * ks + h) ^ (((l32 >> 2) ^ (l32 >> 3) ^ (l32 >> 4)) & 1));   // stores' swizzle
         qa[p] = *reinterpret_cast<const bf16x8*>(&Qs[p * 32 * RS + l32 * RS + qc]);
         da[p] = *reinterpret_cast<const bf16x8*>(&dOs[p * 32 * RS + l32 * RS + qc]);
       }

@@ -232,8 +232,9 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_split_k(Piec
     // LDS-DMA staging (buffer_load ... lds): no staging registers and no ds_write pass.  A
     // DMA wave-instruction writes 1 KiB of LDS lane-linearly, so each lane loads the 16-B
     // chunk whose swizzled image position (toff) is its lane slot: the inverse of toff on the
-    // SOURCE address, the same image as store() writes.  Step it + 1 is in flight while step
-    // it runs on the matrix cores; the barrier's vmcnt(0) retires it (2 buffers, 1 barrier).
+    // SOURCE address, the same image as store() writes.  NBUF 2: step it + 1 is in flight
+    // while step it runs on the matrix cores and is retired (dma_wait<0>) before the barrier
+    // that publishes it; NBUF 3: two steps in flight, a counted wait retires the older one.
     constexpr int JA = A_BYTES / 1024 / NW, JB = B_BYTES / 1024 / NW;   // 1-KiB pieces per wave and piece
     static_assert(JA >= 1 && JB >= 1 && A_BYTES % (1024 * NW) == 0 && B_BYTES % (1024 * NW) == 0,
                   "tile / wave mismatch");

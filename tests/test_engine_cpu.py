@@ -174,3 +174,21 @@ def test_launch_hetero_tool_tcp(tmp_path):
     ck = load(os.path.join(save, 'checkpoint_last.pt'))
     assert ck['optimizer_history'][-1]['num_updates'] == 4
     assert ck['args'].distributed_world_size == 3
+
+
+def test_four_rank_gradient_equivalence_small_buckets(tmp_path, bert_data):
+    """4 ranks (gloo) x 1 micro-batch with 1 MB gradient buckets == 1 rank x --update-freq 4:
+    a rehearsal of the N > 2 reducer path (many buckets launched in order from the backward
+    hooks, the last one after backward) on the CPU."""
+    data, cfg, vocab = bert_data
+    cfg0 = str(tmp_path / 'nodrop.json')
+    write_bert_config(cfg0, **dict(BERT_TINY, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0))
+    one = str(tmp_path / 'one')
+    four = str(tmp_path / 'four')
+    run_cli(bert_argv(data, cfg0, vocab, one, ['--max-update', '1', '--update-freq', '4']))
+    run_cli(bert_argv(data, cfg0, vocab, four, ['--max-update', '1', '--distributed-world-size', '4',
+                                                '--distributed-backend', 'gloo', '--bucket-cap-mb', '1']))
+    c1 = load(os.path.join(one, 'checkpoint_last.pt'))
+    c4 = load(os.path.join(four, 'checkpoint_last.pt'))
+    for k in c1['model']:
+        torch.testing.assert_close(c1['model'][k], c4['model'][k], rtol=1e-5, atol=1e-6, msg=k)

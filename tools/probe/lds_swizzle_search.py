@@ -36,28 +36,34 @@ def write_cost(f):
                         banks.setdefault((a+d) % 32, set()).add(a+d)
                 tot += max(len(v) for v in banks.values())
     return tot  # ideal 1 per group: 4 w * 2 rows * 4 groups = 32
-cands = {'none': lambda q: 0, 'q>>4 (current)': lambda q: (q >> 4) & 1}
-for k in range(0, 5):
-    for m in (1, 3, 7):
-        for sh in (0, 1, 2):
-            cands['((q>>%d)&%d)<<%d' % (k, m, sh)] = (lambda k, m, sh: (lambda q: (((q >> k) & m) << sh) & 7))(k, m, sh)
-cands['(q>>1)&7'] = lambda q: (q >> 1) & 7
-cands['((q>>1)&3)^((q>>3)&1)*4'] = lambda q: ((q >> 1) & 3) | (((q >> 3) & 1) << 2)
-cands['(q>>1)&7 rev'] = lambda q: ((q>>1)&1)<<2 | ((q>>2)&1)<<1 | ((q>>3)&1)
-res = sorted(((read_cost(f) / 16 + write_cost(f) / 32, read_cost(f), write_cost(f), n) for n, f in cands.items()))
-for r in res[:12]:
-    print(r)
-print([r for r in res if r[3] in ('none', 'q>>4 (current)')])
-best = []
-for vs in itertools.product(range(8), repeat=5):
-    def f(q, vs=vs):
-        r = 0
-        for i in range(5):
-            if (q >> i) & 1: r ^= vs[i]
-        return r
-    rc = read_cost(f)
-    if rc > 16: continue
-    wc = write_cost(f)
-    best.append((wc, rc, vs))
-best.sort()
-print(best[:5], len(best))
+
+def main():
+    cands = {'none': lambda q: 0, 'q>>4 (current)': lambda q: (q >> 4) & 1}
+    for k in range(0, 5):
+        for m in (1, 3, 7):
+            for sh in (0, 1, 2):
+                cands['((q>>%d)&%d)<<%d' % (k, m, sh)] = (lambda k, m, sh: (lambda q: (((q >> k) & m) << sh) & 7))(k, m, sh)
+    cands['(q>>1)&7'] = lambda q: (q >> 1) & 7
+    cands['((q>>1)&3)^((q>>3)&1)*4'] = lambda q: ((q >> 1) & 3) | (((q >> 3) & 1) << 2)
+    cands['(q>>1)&7 rev'] = lambda q: ((q>>1)&1)<<2 | ((q>>2)&1)<<1 | ((q>>3)&1)
+    res = sorted(((read_cost(f) / 16 + write_cost(f) / 32, read_cost(f), write_cost(f), n) for n, f in cands.items()))
+    for r in res[:12]:
+        print(r)
+    print([r for r in res if r[3] in ('none', 'q>>4 (current)')])
+    best = []
+    for vs in itertools.product(range(8), repeat=5):
+        def f(q, vs=vs):
+            r = 0
+            for i in range(5):
+                if (q >> i) & 1: r ^= vs[i]
+            return r
+        rc = read_cost(f)
+        if rc > 16: continue
+        wc = write_cost(f)
+        best.append((wc, rc, vs))
+    best.sort()
+    print(best[:5], len(best))
+
+
+if __name__ == '__main__':
+    main()

@@ -38,7 +38,7 @@ def write_cost(f):
     return tot  # ideal 1 per group: 4 w * 2 rows * 4 groups = 32
 
 def main():
-    cands = {'none': lambda q: 0, 'q>>4 (current)': lambda q: (q >> 4) & 1}
+    cands = {'none': lambda q: 0, 'q>>4': lambda q: (q >> 4) & 1}
     for k in range(0, 5):
         for m in (1, 3, 7):
             for sh in (0, 1, 2):
@@ -49,7 +49,7 @@ def main():
     res = sorted(((read_cost(f) / 16 + write_cost(f) / 32, read_cost(f), write_cost(f), n) for n, f in cands.items()))
     for r in res[:12]:
         print(r)
-    print([r for r in res if r[3] in ('none', 'q>>4 (current)')])
+    print([r for r in res if r[3] in ('none', 'q>>4')])
     best = []
     for vs in itertools.product(range(8), repeat=5):
         def f(q, vs=vs):

@@ -573,25 +573,105 @@ bool gemm_split_ok(const Tensor& a, const Tensor& b, int64_t npc) {
   if (a.dim() != 2 || b.dim() != 2 || !a.is_contiguous() || !b.is_contiguous()) return false;
   if (a.size(1) != b.size(1) || a.size(1) % npc) return false;
   const int64_t K = a.size(1) / npc;
-  return K % 32 == 0 && b.size(0) % 128 == 0 && aligned16(a.data_ptr()) && aligned16(b.data_ptr()) &&
-         a.size(0) < (1LL << 31) && b.size(0) * a.size(1) * 2 < (1LL << 31) && 256 * a.size(1) * 2 < (1LL << 31);
+  const int cfg = hx_gemm_split_plan((int)a.size(0), (int)b.size(0), (int)K, npc == 3 ? 6 : 3);
+  const int kal = (npc == 3 && cfg != 2) ? 16 : 32;   // k step of the configuration
+  return cfg >= 0 && K % kal == 0 &&
+         aligned16(a.data_ptr()) && aligned16(b.data_ptr()) && a.size(0) < (1LL << 31) &&
+         256 * a.size(1) * 2 < (1LL << 31) && b.size(0) * a.size(1) * 2 < (1LL << 31) &&
+         256 * b.size(0) * 6 < (1LL << 31);
 }
-Tensor gemm_split(Tensor a, Tensor b, int64_t passes, OptT out_, bool beta) {
+static int gemm_split_launch(const Tensor& a, const Tensor& b, int64_t passes, float* C, int64_t ldc, bool beta,
+                             const HxGemmEpi* epi, int64_t kblock = 0) {
+  const int64_t npc = passes == 6 ? 3 : 2;
+  const int64_t M = a.size(0), N = b.size(0), K = a.size(1) / npc;
+  const int cfg = hx_gemm_split_plan((int)M, (int)N, (int)K, (int)passes);
+  const int64_t ps = kblock ? kblock : K;
+  return hx_gemm_split_nt(a.data_ptr(), npc * K, ps, b.data_ptr(), npc * K, ps, C, ldc, (int)M, (int)N, (int)K,
+                          (int)passes, beta ? 1 : 0, epi, cfg, cur_stream(a), (int)kblock);
+}
+Tensor gemm_split(Tensor a, Tensor b, int64_t passes, OptT out_, bool beta, int64_t kblock) {
   const int64_t npc = passes == 6 ? 3 : 2;
   TORCH_CHECK(passes == 3 || passes == 6, "gemm_split: passes must be 3 or 6");
   TORCH_CHECK(gemm_split_ok(a, b, npc), "gemm_split: unsupported operands");
-  const int64_t M = a.size(0), N = b.size(0), K = a.size(1) / npc;
+  const int64_t M = a.size(0), N = b.size(0);
   Tensor out = has(out_) ? *out_ : torch::empty({M, N}, a.options().dtype(torch::kFloat32));
   TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.dim() == 2 && out.size(0) == M && out.size(1) == N &&
-                  out.stride(1) == 1,
-              "gemm_split: out must be fp32 [M, N] with unit column stride");
+                  out.stride(1) == 1 && out.stride(0) % 4 == 0 && aligned16(out.data_ptr()),
+              "gemm_split: out must be fp32 [M, N] with unit column stride and 16-B rows");
   TORCH_CHECK(!beta || has(out_), "gemm_split: beta needs an output to accumulate into");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
-  TORCH_CHECK(hx_gemm_split_nt(a.data_ptr(), npc * K, K, b.data_ptr(), npc * K, K, out.data_ptr<float>(), out.stride(0),
-                               (int)M, (int)N, (int)K, (int)passes, beta ? 1 : 0, cur_stream(a)) == 0,
+  TORCH_CHECK(gemm_split_launch(a, b, passes, out.data_ptr<float>(), out.stride(0), beta, nullptr, kblock) == 0,
               "gemm_split: launch failed");
   dbg_finite(out, "gemm_split");
   return out;
+}
+// FFN up: u = a . b^T + bias (fp32, kept for the backward) and the pieces of gelu(u)
+std::vector<Tensor> gemm_split_gelu(Tensor a, Tensor b, int64_t passes, OptT bias) {
+  const int64_t npc = passes == 6 ? 3 : 2;
+  TORCH_CHECK(passes == 3 || passes == 6, "gemm_split_gelu: passes must be 3 or 6");
+  TORCH_CHECK(gemm_split_ok(a, b, npc), "gemm_split_gelu: unsupported operands");
+  const int64_t M = a.size(0), N = b.size(0);
+  if (has(bias)) {
+    check_f32(*bias, "gemm_split_gelu bias");
+    TORCH_CHECK(bias->numel() == N && bias->is_contiguous() && aligned16(bias->data_ptr()), "gemm_split_gelu: bias");
+  }
+  Tensor u = torch::empty({M, N}, a.options().dtype(torch::kFloat32));
+  Tensor p = torch::empty({M, npc * N}, a.options());
+  HxGemmEpi e{1, ptr_or_null<float>(bias), nullptr, 0, reinterpret_cast<uint16_t*>(p.data_ptr()), npc * N, N,
+              nullptr};
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  TORCH_CHECK(gemm_split_launch(a, b, passes, u.data_ptr<float>(), N, false, &e) == 0, "gemm_split_gelu: launch failed");
+  dbg_finite(u, "gemm_split_gelu");
+  return {u, p};
+}
+// FFN down data gradient + GELU backward: t = (a . b^T) * gelu'(u (+ bias)); returns the pieces of
+// t and d bias = column sums of t (into dbias_out when given)
+std::vector<Tensor> gemm_split_dgelu(Tensor a, Tensor b, int64_t passes, Tensor u, OptT bias, OptT dbias_out) {
+  const int64_t npc = passes == 6 ? 3 : 2;
+  TORCH_CHECK(passes == 3 || passes == 6, "gemm_split_dgelu: passes must be 3 or 6");
+  TORCH_CHECK(gemm_split_ok(a, b, npc), "gemm_split_dgelu: unsupported operands");
+  const int64_t M = a.size(0), N = b.size(0);
+  check_f32(u, "gemm_split_dgelu pre-activation");
+  TORCH_CHECK(u.dim() == 2 && u.size(0) == M && u.size(1) == N && u.is_contiguous() && aligned16(u.data_ptr()),
+              "gemm_split_dgelu: u must be fp32 [M, N]");
+  if (has(bias)) {
+    check_f32(*bias, "gemm_split_dgelu bias");
+    TORCH_CHECK(bias->numel() == N && bias->is_contiguous() && aligned16(bias->data_ptr()), "gemm_split_dgelu: bias");
+  }
+  const int cfg = hx_gemm_split_plan((int)M, (int)N, (int)(a.size(1) / npc), (int)passes);
+  const int prow = hx_gemm_split_colpart_rows((int)M, cfg);
+  auto f32 = a.options().dtype(torch::kFloat32);
+  Tensor p = torch::empty({M, npc * N}, a.options());
+  Tensor part = torch::empty({prow, N}, f32);
+  Tensor db = has(dbias_out) ? *dbias_out : torch::empty({N}, f32);
+  TORCH_CHECK(db.numel() == N && db.scalar_type() == torch::kFloat32 && db.is_contiguous(), "gemm_split_dgelu: dbias");
+  HxGemmEpi e{2, ptr_or_null<float>(bias), u.data_ptr<float>(), N, reinterpret_cast<uint16_t*>(p.data_ptr()),
+              npc * N, N, part.data_ptr<float>()};
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  TORCH_CHECK(gemm_split_launch(a, b, passes, nullptr, N, false, &e) == 0, "gemm_split_dgelu: launch failed");
+  hx_fold_cols(part.data_ptr<float>(), prow, (int)N, db.data_ptr<float>(), 0, cur_stream(a));
+  return {p, db};
+}
+
+// diagnostic: per-wave phase cycle sums of the piece GEMM main loop (cfg 0, bf16x6)
+Tensor gemm_split_stamps(Tensor a, Tensor b) {
+  TORCH_CHECK(gemm_split_ok(a, b, 3), "gemm_split_stamps: unsupported operands");
+  const int64_t M = a.size(0), N = b.size(0), K = a.size(1) / 3;
+  const int64_t tiles = ((M + 255) / 256) * (N / 192);
+  Tensor st = torch::zeros({8 * ((tiles + 7) / 8) * 8, 5}, a.options().dtype(torch::kInt64));
+  Tensor out = torch::empty({M, N}, a.options().dtype(torch::kFloat32));
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  TORCH_CHECK(hx_gemm_split_stamps(a.data_ptr(), b.data_ptr(), out.data_ptr<float>(), (int)M, (int)N, (int)K,
+                                   reinterpret_cast<unsigned long long*>(st.data_ptr()), cur_stream(a)) > 0,
+              "gemm_split_stamps: launch failed");
+  return st;
+}
+
+void dma_probe(Tensor src, int64_t seg, int64_t ld, int64_t iters, int64_t grid) {
+  TORCH_CHECK(src.is_cuda() && src.nbytes() < (1LL << 32) && src.nbytes() > (1 << 20), "dma_probe: src");
+  TORCH_CHECK(seg == 1024 || seg == 128 || seg == 64 || seg == 32, "dma_probe: seg");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
+  hx_dma_probe(src.data_ptr(), (uint32_t)src.nbytes(), (int)seg, (int)ld, (int)iters, (int)grid, cur_stream(src));
 }
 
 // ------------------------------------------------------------------ split planes
@@ -738,7 +818,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("split_planes", &split_planes);
   m.def("split_planes_t", &split_planes_t);
   m.def("split_weight", &split_weight);
-  m.def("gemm_split", &gemm_split);
+  m.def("gemm_split", &gemm_split, py::arg("a"), py::arg("b"), py::arg("passes"), py::arg("out") = py::none(),
+        py::arg("beta") = false, py::arg("kblock") = 0);
+  m.def("gemm_split_gelu", &gemm_split_gelu);
+  m.def("gemm_split_stamps", &gemm_split_stamps);
+  m.def("dma_probe", &dma_probe);
+  m.def("gemm_split_dgelu", &gemm_split_dgelu);
   m.def("gemm_split_ok", &gemm_split_ok);
   m.def("bias_act_planes", &bias_act_planes);
   m.def("wgrad_split", &wgrad_split);

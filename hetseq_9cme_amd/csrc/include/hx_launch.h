@@ -96,10 +96,32 @@ void hx_bias_act_planes(int act, const float* y, const float* b, const float* do
 void hx_split_weight(const float* W, int N, int K, int npieces, uint16_t* wf, uint16_t* wt, hipStream_t s);
 
 // gemm_split.hip -- C[M][N] (+)= sum over piece pairs A_a[M][K] . B_b[N][K]^T (bf16 pieces of fp32
-// operands: piece p of row r at X + r * ldx + p * x_ps); passes 3 or 6; N % 128 == 0, K % 32 == 0.
-// Returns -1 for an unsupported shape.
+// operands: piece p of row r at X + r * ldx + p * x_ps, npieces * x_ps <= ldx); passes 3 or 6.
+// Epilogue kinds (epi may be null = kind 0):
+//   0  C (+)= acc
+//   1  C = acc + bias (pre-activation) and P = pieces of gelu(C)        (beta must be 0)
+//   2  t = acc * gelu'(aux (+ bias)); P = pieces of t; colpart[(M/BM)*NWM][N] = per-wave
+//      column sums of t (hx_gemm_split_colpart_rows rows; null = none); C unused
+// cfg from hx_gemm_split_plan (-1: shape not covered).  Returns -1 for an unsupported shape.
+struct HxGemmEpi {
+  int kind;
+  const float* bias;
+  const float* aux;
+  int64_t ldaux;
+  uint16_t* P;
+  int64_t ldp, p_ps;
+  float* colpart;
+};
+int hx_gemm_split_plan(int M, int N, int K, int passes);
+int hx_gemm_split_colpart_rows(int M, int cfg);
 int hx_gemm_split_nt(const void* A, int64_t lda, int64_t a_ps, const void* B, int64_t ldb, int64_t b_ps, float* C,
-                     int64_t ldc, int M, int N, int K, int passes, int beta, hipStream_t s);
+                     int64_t ldc, int M, int N, int K, int passes, int beta, const HxGemmEpi* epi, int cfg,
+                     hipStream_t s, int kblock = 0);
+int hx_gemm_split_stamps(const void* A, const void* B, float* C, int M, int N, int K, unsigned long long* stamps,
+                         hipStream_t s);
+void hx_dma_probe(const void* src, uint32_t bytes, int seg, int ld, int iters, int grid, hipStream_t s);
+// fold [rows][N] column partials into out[N] (+= if accumulate)
+void hx_fold_cols(const float* partial, int rows, int N, float* out, int accumulate, hipStream_t s);
 
 // split.hip -- fp32 -> bf16 planes (piece order[j] = (order >> 4j) & 15) for bf16-MFMA
 // emulation of fp32 GEMMs; interleaved [R][npl][D] or stacked [npl][R][D].

@@ -8,27 +8,43 @@
 // producers write [rows][pieces][K] tensors, each DISTINCT piece once (half the bytes of a
 // pass-stacked operand for bf16x6, the bytes of the fp32 original for bf16x3).
 //
-// Used for the forward (A = activation pieces, B = weight pieces [N_out][K_in]) and the data
-// gradient (A = output-gradient pieces, B = TRANSPOSED weight pieces [K_in][N_out]) of every
-// linear layer; beta = 1 accumulates into C (the fused residual gradient).
+// Every forward and data-gradient GEMM of a linear layer runs here (reference sites
+// hetseq/bert_modeling.py:334-336 Q/K/V, :383 attention output, :409 + :166-168 FFN up with
+// bias_gelu, :419 FFN down): A = activation pieces and B = weight pieces [N_out][K_in]
+// (forward), or A = output-gradient pieces and B = TRANSPOSED weight pieces [K_in][N_out]
+// (data gradient); beta = 1 accumulates into C (the fused residual gradient).
 //
-// Structure (one workgroup per 256 x 128 output tile, 8 waves of 64 x 64):
-//  * 32-deep k steps; each distinct piece tile (A: 256 x 32, B: 128 x 32 bf16) is loaded
-//    once per step with 16-B buffer loads (rows past M read as zeros), staged two steps
-//    ahead in registers and written to LDS as [row][32] with XOR-swizzled 16-B chunks
-//    (chunk ^ (row >> 2) & 3: conflict-free 16-B stores and fragment reads);
+// Structure (the wgrad_split.hip pipeline in NT form):
+//  * one workgroup per BM x BN output tile, 8 waves; tiles dealt XCD-aware (the tile list
+//    is cut into 8 contiguous ranges, one per XCD, so tiles that share A rows / B rows meet
+//    in one XCD's L2);
+//  * LDS-DMA staging (buffer_load ... lds): each DISTINCT piece tile of a BK-deep k step is
+//    copied global -> LDS once, with no staging registers and no ds_write pass, into NBUF
+//    stages (3 at BK = 16: two steps in flight across each barrier, retired by a counted
+//    vmcnt; 2 at BK = 32); the XOR swizzle is applied to the per-lane SOURCE address so the
+//    lane-linear DMA image reads back conflict-free;
 //  * MFMA 32x32x16 bf16: a fragment is ONE ds_read_b128 (row = lane & 31, 8 consecutive k);
-//    per 16-deep k-step a wave reads NPC x (2 A + 2 B) fragments and issues passes x 4
-//    MFMAs -- every piece fragment is reused by all passes that use it;
-//  * XCD-aware tile order: consecutive workgroup ids go round-robin to the 8 XCDs, so the
-//    tile list is cut into 8 contiguous ranges and neighbouring tiles (sharing A rows / B
-//    rows) land in one XCD's L2;
-//  * epilogue straight from the accumulators (128-B row segments), optional + C.
+//    per 16-deep k-step a wave reads NPC x (MB + NB) fragments and issues passes x MB x NB
+//    MFMAs -- every piece fragment is reused by all passes that use it from registers;
+//  * epilogues straight from the accumulators after a 4 x 4 lane transpose (DPP quad
+//    permutes: each lane then holds 4 consecutive columns of one row -> 16-B fp32 /
+//    8-B bf16x4 stores):
+//      EPI 0  C (+)= acc
+//      EPI 1  u = acc + bias -> C (the FFN pre-activation, kept for the backward) and the
+//             pieces of gelu(u) -> P (the FFN-down GEMM's A operand): bias_gelu of
+//             bert_modeling.py:104-111 / :166-168 fused into the FFN-up GEMM;
+//      EPI 2  t = acc * gelu'(aux (+ bias)) -> pieces P (the FFN-up data-gradient A operand)
+//             and per-wave column partial sums of t -> colpart (the FFN-up bias gradient,
+//             folded by one small pass): the GELU backward fused into the FFN-down dgrad.
 #include <algorithm>
+
+#include <stdio.h>
+#include <stdlib.h>
 
 #include "hx_launch.h"
 #include "hx_attn.h"
 #include "hx_common.h"
+#include "hx_reduce.h"
 
 namespace {
 
@@ -36,8 +52,58 @@ using hx::attn::crow;
 using hx::attn::f32x16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int BK = 32;
+// LDS image of a [rows][BK] bf16 tile: 16-B chunk ch of row r at off(r, ch).
+//   BK = 32: 64-B rows, ch ^ ((r >> 2) & 3);   BK = 16: 32-B rows, ch ^ ((r >> 3) & 1).
+// Either way the 16-lane groups of a ds_read_b128 fragment read (32 consecutive rows, one
+// chunk) hit 16 distinct 4-bank slots.  lane_src: the (row within a 1-KiB DMA piece, chunk)
+// whose bytes lane L must fetch so that the lane-linear DMA write (image bytes 16 L ..)
+// produces that image (the XOR is an involution; pieces start at multiples of RPK rows,
+// which keeps the row-dependent XOR bits a function of the lane alone).
+template <int BK>
+struct Img;
+template <>
+struct Img<32> {
+  static constexpr int RPK = 16;   // rows per KiB
+  __device__ __forceinline__ static int off(int r, int ch) { return r * 64 + 16 * (ch ^ ((r >> 2) & 3)); }
+  __device__ __forceinline__ static void lane_src(int L, int& rl, int& ch) {
+    rl = L >> 2;
+    ch = (L & 3) ^ (L >> 4);
+  }
+};
+template <>
+struct Img<16> {
+  static constexpr int RPK = 32;
+  __device__ __forceinline__ static int off(int r, int ch) { return r * 32 + 16 * (ch ^ ((r >> 3) & 1)); }
+  __device__ __forceinline__ static void lane_src(int L, int& rl, int& ch) {
+    rl = L >> 1;
+    ch = (L & 1) ^ ((L >> 4) & 1);
+  }
+};
+
+// one LDS-DMA wave-instruction: 16 B per lane from buffer byte voff (zeros past the buffer's
+// end) to LDS bytes [dst + 16 lane, + 16); dst is wave-uniform.  From asm, so the compiler
+// does not drain it (vmcnt(0)) before the next LDS read of the stage being computed; the
+// caller retires it with a counted wait before the barrier that publishes the stage.
+__device__ __forceinline__ void dma16(u32x4 rsrc, uint32_t lds_addr, uint32_t voff) {
+  const uint32_t m = __builtin_amdgcn_readfirstlane(lds_addr);
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %3, 0 offen lds\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(m), "s"(rsrc)
+               : "memory");
+}
+template <int N>
+__device__ __forceinline__ void dma_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt field");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+__device__ __forceinline__ u32x4 rsrc_of(const void* p, uint32_t bytes) {
+  const uint64_t a = (uint64_t)(size_t)p;
+  return u32x4{(uint32_t)a, (uint32_t)(a >> 32) & 0xffffu, bytes, 0x00020000u};
+}
 
 template <int NP>
 struct PairsNT;
@@ -52,75 +118,127 @@ struct PairsNT<6> {
   static constexpr int b[6] = {0, 1, 0, 2, 1, 0};
 };
 
-// byte offset of 16-B chunk ch (0..3) of row r in a [rows][32] bf16 tile
-__device__ __forceinline__ int soff(int r, int ch) { return r * 64 + 16 * (ch ^ ((r >> 2) & 3)); }
+// quad permutes (DPP): value of lane (lane ^ 1) / (lane ^ 2)
+__device__ __forceinline__ float qx1(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float qx2(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+// v[i] = row i (of 4 consecutive rows), column c = lane's column  ->  v[i] = row (lane & 3),
+// column (c & ~3) + i.  Two exchange steps inside each quad of lanes.
+__device__ __forceinline__ void transpose4(float (&v)[4], int lane) {
+  const bool odd = lane & 1, hi = lane & 2;
+  float s0 = qx1(odd ? v[0] : v[1]);
+  float s2 = qx1(odd ? v[2] : v[3]);
+  if (odd) {
+    v[0] = s0;
+    v[2] = s2;
+  } else {
+    v[1] = s0;
+    v[3] = s2;
+  }
+  float t0 = qx2(hi ? v[0] : v[2]);
+  float t1 = qx2(hi ? v[1] : v[3]);
+  if (hi) {
+    v[0] = t0;
+    v[1] = t1;
+  } else {
+    v[2] = t0;
+    v[3] = t1;
+  }
+}
 
-template <int BM, int BN, int WM, int WN, int NPC, int NP>
-__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_split_nt_k(
-    const uint16_t* __restrict__ A, int64_t lda, int64_t a_ps, const uint16_t* __restrict__ B, int64_t ldb,
-    int64_t b_ps, float* __restrict__ C, int64_t ldc, int M, int N, int K, int beta) {
-  constexpr int NWM = BM / WM, NW = NWM * (BN / WN), NT = NW * 64;
+struct Args {
+  const uint16_t* A;
+  int64_t lda, a_ps;
+  const uint16_t* B;
+  int64_t ldb, b_ps;
+  float* C;
+  int64_t ldc;
+  int M, N, K, beta;
+  const float* bias;
+  const float* aux;
+  int64_t ldaux;
+  uint16_t* P;
+  int64_t ldp, p_ps;
+  float* colpart;
+  uint32_t ksa, ksb;   // bytes between consecutive BK-deep k steps of a row (2 BK natural, 2 BK npc blocked)
+  unsigned long long* stamps;   // diagnostic build (PIPE 9): per wave [dma issue, mfma, dma wait, barrier, total]
+};
+
+__device__ __forceinline__ uint2 pack4(const float (&x)[4]) {
+  return make_uint2(hx::f2bf(x[0]) | ((uint32_t)hx::f2bf(x[1]) << 16),
+                    hx::f2bf(x[2]) | ((uint32_t)hx::f2bf(x[3]) << 16));
+}
+template <int BM, int BN, int WM, int WN, int NPC, int NP, int BK, int NBUF, int EPI, int PIPE>
+__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_piece_k(Args g) {
+  constexpr int NWM = BM / WM, NW = NWM * (BN / WN);
   constexpr int MB = WM / 32, NB = WN / 32;
-  constexpr int CA = BM * 4 / NT, CB = BN * 4 / NT;   // 16-B chunks per thread per piece per k step
-  static_assert(CA >= 1 && CB >= 1 && BM * 4 % NT == 0 && BN * 4 % NT == 0, "tile / thread mismatch");
-  constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
   constexpr int STAGE = NPC * (A_BYTES + B_BYTES);
+  constexpr int KA = A_BYTES / 1024, KB = B_BYTES / 1024;   // 1-KiB DMA pieces per piece tile
+  constexpr int PA = NPC * KA, PTOT = NPC * (KA + KB);
+  constexpr int JHI = (PTOT + NW - 1) / NW, JLO = PTOT / NW;   // DMAs per wave and stage
+  constexpr int RPK = Img<BK>::RPK;
+  static_assert(A_BYTES % 1024 == 0 && B_BYTES % 1024 == 0, "tile / DMA piece mismatch");
+  static_assert(NBUF == 2 || NBUF == 3, "stages");
+  static_assert(JLO >= 1, "fewer DMA pieces than waves");
   extern __shared__ __attribute__((aligned(16))) char lds[];
 
-  const int TM = (M + BM - 1) / BM, TN = N / BN, total = TM * TN;
+  const int TM = (g.M + BM - 1) / BM, TN = g.N / BN, total = TM * TN;
   const int per = (total + 7) / 8;
   const int work = (blockIdx.x % 8) * per + blockIdx.x / 8;
   if (work >= total) return;   // uniform per workgroup
   const int nt = work % TN, mt = work / TN;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int nit = K / BK;
+  const int nit = g.K / BK;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w % NWM, wn = w / NWM, h = lane >> 5, l32 = lane & 31;
+  const int wv = __builtin_amdgcn_readfirstlane(w);
 
-  // buffer resources over this tile's rows: A rows past M read as zeros
-  const int mrows = min(BM, M - m0);
-  const hx::Buf abuf(A + (int64_t)m0 * lda, (uint32_t)((int64_t)(mrows - 1) * lda * 2 + (NPC - 1) * a_ps * 2 + K * 2));
-  const hx::Buf bbuf(B + (int64_t)n0 * ldb, (uint32_t)((int64_t)(BN - 1) * ldb * 2 + (NPC - 1) * b_ps * 2 + K * 2));
-  uint32_t va[CA], vb[CB];
-  int sa[CA], sb[CB];
-#pragma unroll
-  for (int i = 0; i < CA; ++i) {
-    const int e = tid + i * NT, row = e >> 2, ch = e & 3;
-    va[i] = row < mrows ? (uint32_t)(row * lda + 8 * ch) * 2 : 0x80000000u;   // out of range -> zeros
-    sa[i] = soff(row, ch);
-  }
-#pragma unroll
-  for (int i = 0; i < CB; ++i) {
-    const int e = tid + i * NT, row = e >> 2, ch = e & 3;
-    vb[i] = (uint32_t)(row * ldb + 8 * ch) * 2;
-    sb[i] = soff(row, ch);
-  }
+  // buffer resources over this tile's A rows / B rows (rows past M read as zeros: piece p of
+  // row r lies inside [r * lda, (r + 1) * lda) because NPC * a_ps <= lda)
+  const int mrows = min(BM, g.M - m0);
+  const u32x4 ra = rsrc_of(g.A + (int64_t)m0 * g.lda, (uint32_t)((int64_t)mrows * g.lda * 2));
+  const u32x4 rb = rsrc_of(g.B + (int64_t)n0 * g.ldb, (uint32_t)((int64_t)BN * g.ldb * 2));
 
-  u32x4 ra0[NPC][CA], rb0[NPC][CB], ra1[NPC][CA], rb1[NPC][CB];
-  auto load = [&](int it, u32x4 (&ra)[NPC][CA], u32x4 (&rb)[NPC][CB]) {
-    if (it >= nit) return;
-    const uint32_t ko = (uint32_t)it * BK * 2;
+  // this wave's DMA pieces q = wv + NW j of a stage: [A piece tiles | B piece tiles]
+  uint32_t voff[JHI];
+  int dsto[JHI];
+  bool isa[JHI];
+  int rl, ch;
+  Img<BK>::lane_src(lane, rl, ch);
 #pragma unroll
-    for (int p = 0; p < NPC; ++p) {
+  for (int j = 0; j < JHI; ++j) {
+    const int q = wv + NW * j;
+    isa[j] = q < PA;
+    if (q < PA) {
+      const int p = q / KA, r = (q % KA) * RPK + rl;
+      voff[j] = (uint32_t)(r * g.lda + p * g.a_ps + 8 * ch) * 2;
+    } else {
+      const int qb = q - PA, p = qb / KB, r = (qb % KB) * RPK + rl;
+      voff[j] = (uint32_t)(r * g.ldb + p * g.b_ps + 8 * ch) * 2;
+    }
+    dsto[j] = 1024 * q;
+  }
+  const int cnt = (PTOT - wv + NW - 1) / NW;   // JHI or JLO
+  const uint32_t lds0 = (uint32_t)(size_t)(lds_void*)lds;   // LDS byte address of the stages
+  auto dma = [&](int it, int buf) {
+    const uint32_t st = lds0 + buf * STAGE;
+    const uint32_t koa = (uint32_t)it * g.ksa, kob = (uint32_t)it * g.ksb;
 #pragma unroll
-      for (int i = 0; i < CA; ++i)
-        ra[p][i] = __builtin_amdgcn_raw_buffer_load_b128(abuf.r, va[i], ko + (uint32_t)(p * a_ps * 2), 0);
-#pragma unroll
-      for (int i = 0; i < CB; ++i)
-        rb[p][i] = __builtin_amdgcn_raw_buffer_load_b128(bbuf.r, vb[i], ko + (uint32_t)(p * b_ps * 2), 0);
+    for (int j = 0; j < JHI; ++j) {
+      if (j < JLO || j < cnt) dma16(isa[j] ? ra : rb, st + dsto[j], voff[j] + (isa[j] ? koa : kob));
     }
   };
-  auto store = [&](int buf, const u32x4 (&ra)[NPC][CA], const u32x4 (&rb)[NPC][CB]) {
-    char* st = lds + buf * STAGE;
-#pragma unroll
-    for (int p = 0; p < NPC; ++p) {
-      char* at = st + p * A_BYTES;
-      char* bt = st + NPC * A_BYTES + p * B_BYTES;
-#pragma unroll
-      for (int i = 0; i < CA; ++i) *reinterpret_cast<u32x4*>(at + sa[i]) = ra[p][i];
-#pragma unroll
-      for (int i = 0; i < CB; ++i) *reinterpret_cast<u32x4*>(bt + sb[i]) = rb[p][i];
+  auto wait_stage = [&]() {   // all but this wave's youngest stage of DMAs landed
+    if constexpr (JHI == JLO) {
+      dma_wait<JLO>();
+    } else {
+      if (cnt == JHI) dma_wait<JHI>();
+      else dma_wait<JLO>();
     }
   };
 
@@ -130,11 +248,6 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_split_nt_k(
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[a][b] = f32x16{0};
 
-  // fragment of rows r0 + (lane & 31), k = 16 ks + 8 h .. + 7: one 16-B LDS read
-  auto frag = [&](const char* tile, int r0, int ks) -> bf16x8 {
-    const int r = r0 + l32;
-    return *reinterpret_cast<const bf16x8*>(tile + soff(r, 2 * ks + h));
-  };
   auto mma = [&](int buf) {
     const char* st = lds + buf * STAGE;
 #pragma unroll
@@ -143,9 +256,12 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_split_nt_k(
 #pragma unroll
       for (int p = 0; p < NPC; ++p) {
 #pragma unroll
-        for (int a = 0; a < MB; ++a) fa[p][a] = frag(st + p * A_BYTES, wm * WM + 32 * a, ks);
+        for (int a = 0; a < MB; ++a)
+          fa[p][a] = *reinterpret_cast<const bf16x8*>(st + p * A_BYTES + Img<BK>::off(wm * WM + 32 * a + l32, 2 * ks + h));
 #pragma unroll
-        for (int b = 0; b < NB; ++b) fb[p][b] = frag(st + NPC * A_BYTES + p * B_BYTES, wn * WN + 32 * b, ks);
+        for (int b = 0; b < NB; ++b)
+          fb[p][b] = *reinterpret_cast<const bf16x8*>(st + NPC * A_BYTES + p * B_BYTES +
+                                                      Img<BK>::off(wn * WN + 32 * b + l32, 2 * ks + h));
       }
 #pragma unroll
       for (int q = 0; q < NP; ++q)
@@ -158,68 +274,558 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_split_nt_k(
     }
   };
 
-  load(0, ra0, rb0);
-  load(1, ra1, rb1);
-  store(0, ra0, rb0);
-  __syncthreads();
-  for (int it = 0; it < nit; it += 2) {
-    load(it + 2, ra0, rb0);
-    mma(0);
-    if (it + 1 >= nit) break;
-    store(1, ra1, rb1);
+  if constexpr (PIPE == 1) {
+    // Fragments of the stage being multiplied live in registers (two named sets, loop
+    // unrolled by 2), so three stages can be in flight in three LDS buffers and the LDS
+    // reads of stage it + 1 overlap the second MFMA group of stage it:
+    //   group 1 (all fragments consumed) | own DMA of it+1 landed | barrier |
+    //   reads of it+1 -> other set, DMA of it+3 into stage it's buffer | group 2
+    static_assert(BK == 16 && NBUF == 3, "register-pipelined variant: one 16-deep k step per stage");
+    typedef bf16x8 Frag[NPC][MB + NB];
+    auto rd = [&](int buf, Frag& F) {
+      const char* st = lds + buf * STAGE;
+#pragma unroll
+      for (int p = 0; p < NPC; ++p) {
+#pragma unroll
+        for (int a = 0; a < MB; ++a)
+          F[p][a] = *reinterpret_cast<const bf16x8*>(st + p * A_BYTES + Img<BK>::off(wm * WM + 32 * a + l32, h));
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          F[p][MB + b] = *reinterpret_cast<const bf16x8*>(st + NPC * A_BYTES + p * B_BYTES +
+                                                         Img<BK>::off(wn * WN + 32 * b + l32, h));
+      }
+    };
+    // pass q of the product (PairsNT order); group 1 = the first half of the passes
+    auto pass = [&](const Frag& F, int q) {
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F[PairsNT<NP>::a[q]][a], F[PairsNT<NP>::b[q]][MB + b],
+                                                              acc[a][b], 0, 0, 0);
+    };
+    constexpr int G1 = (NP + 1) / 2;
+    auto step = [&](int it, int cur, Frag& Fc, Frag& Fn) {
+#pragma unroll
+      for (int q = 0; q < G1; ++q) pass(Fc, q);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // every read of stage it done
+      if (it + 2 < nit) wait_stage();
+      else dma_wait<0>();
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();
+      __builtin_amdgcn_sched_barrier(0);
+      const int nxt = cur == 2 ? 0 : cur + 1;
+      if (it + 1 < nit) rd(nxt, Fn);
+      if (it + 3 < nit) dma(it + 3, cur);
+#pragma unroll
+      for (int q = G1; q < NP; ++q) pass(Fc, q);
+      return nxt;
+    };
+    Frag F0, F1;
+    dma(0, 0);
+    if (nit > 1) dma(1, 1);
+    if (nit > 2) dma(2, 2);
+    // stage 0 landed: stages 1, 2 may stay in flight
+    if (nit > 2) {
+      if constexpr (JHI == JLO) dma_wait<2 * JLO>();
+      else if (cnt == JHI) dma_wait<2 * JHI>();
+      else dma_wait<2 * JLO>();
+    } else if (nit > 1) {
+      wait_stage();
+    } else {
+      dma_wait<0>();
+    }
     __syncthreads();
-    load(it + 3, ra1, rb1);
-    mma(1);
-    if (it + 2 >= nit) break;
-    store(0, ra0, rb0);
+    rd(0, F0);
+    int cur = 0;
+    for (int it = 0; it < nit; it += 2) {
+      cur = step(it, cur, F0, F1);
+      if (it + 1 >= nit) break;
+      cur = step(it + 1, cur, F1, F0);
+    }
+  } else if constexpr (PIPE == 2) {
+    // One fragment register set, refilled in place: bf16x6 passes ordered so that the three
+    // fragment groups the post-barrier passes do not use are reloaded (next stage) right
+    // after the barrier, the rest as soon as their last MFMA has issued.
+    //   before the barrier: (0,2) (0,1) (1,1) (2,0)    after: (0,0) (1,0)
+    //   reloads: b2 b1 a2 | after (0,0): a0 | after (1,0): a1 b0
+    // The next stage opens with (0,2) (0,1), whose fragments were reloaded first.
+    static_assert(BK == 16 && NBUF == 3 && NP == 6, "in-place register pipeline: bf16x6, 16-deep stages");
+    bf16x8 fa[3][MB], fb[3][NB];
+    auto rda = [&](int buf, int p) {
+      const char* st = lds + buf * STAGE;
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+        fa[p][a] = *reinterpret_cast<const bf16x8*>(st + p * A_BYTES + Img<BK>::off(wm * WM + 32 * a + l32, h));
+    };
+    auto rdb = [&](int buf, int p) {
+      const char* st = lds + buf * STAGE;
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        fb[p][b] = *reinterpret_cast<const bf16x8*>(st + 3 * A_BYTES + p * B_BYTES +
+                                                    Img<BK>::off(wn * WN + 32 * b + l32, h));
+    };
+    auto pass = [&](int pa, int pb) {
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[pa][a], fb[pb][b], acc[a][b], 0, 0, 0);
+    };
+    dma(0, 0);
+    if (nit > 1) dma(1, 1);
+    if (nit > 2) dma(2, 2);
+    if (nit > 2) {
+      if constexpr (JHI == JLO) dma_wait<2 * JLO>();
+      else if (cnt == JHI) dma_wait<2 * JHI>();
+      else dma_wait<2 * JLO>();
+    } else if (nit > 1) {
+      wait_stage();
+    } else {
+      dma_wait<0>();
+    }
     __syncthreads();
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      rda(0, p);
+      rdb(0, p);
+    }
+    int cur = 0;
+    for (int it = 0; it < nit; ++it) {
+      pass(0, 2);
+      pass(0, 1);
+      pass(1, 1);
+      pass(2, 0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (it + 2 < nit) wait_stage();
+      else dma_wait<0>();
+      __builtin_amdgcn_sched_barrier(0);
+      __syncthreads();
+      __builtin_amdgcn_sched_barrier(0);
+      const int nxt = cur == 2 ? 0 : cur + 1;
+      const bool more = it + 1 < nit;
+      if (more) {
+        rdb(nxt, 2);
+        rdb(nxt, 1);
+        rda(nxt, 2);
+      }
+      if (it + 3 < nit) dma(it + 3, cur);
+      pass(0, 0);
+      if (more) rda(nxt, 0);
+      pass(1, 0);
+      if (more) {
+        rda(nxt, 1);
+        rdb(nxt, 0);
+      }
+      cur = nxt;
+    }
+  } else if constexpr (NBUF == 2) {
+    dma(0, 0);
+    dma_wait<0>();
+    __syncthreads();
+    for (int it = 0; it < nit; ++it) {
+      if (it + 1 < nit) dma(it + 1, (it + 1) & 1);
+      mma(it & 1);
+      dma_wait<0>();
+      __syncthreads();
+    }
+  } else {
+    // stage it + 2 goes into the buffer step it - 1 read (all waves passed the barrier after
+    // those reads); before each barrier only stage it + 1 must have landed
+    dma(0, 0);
+    if (nit > 1) {
+      dma(1, 1);
+      wait_stage();
+    } else {
+      dma_wait<0>();
+    }
+    __syncthreads();
+    int cur = 0;
+    unsigned long long sd = 0, sm = 0, sw = 0, sb = 0, t00 = 0;
+    if constexpr (PIPE == 9) t00 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < nit; ++it) {
+      const int nxt2 = cur == 0 ? 2 : cur - 1;
+      unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0;
+      if constexpr (PIPE == 9) {
+        __builtin_amdgcn_sched_barrier(0);
+        t0 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (it + 2 < nit) dma(it + 2, nxt2);
+      if constexpr (PIPE == 9) {
+        __builtin_amdgcn_sched_barrier(0);
+        t1 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      mma(cur);
+      if constexpr (PIPE == 9) {
+        __builtin_amdgcn_sched_barrier(0);
+        t2 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (it + 2 < nit) wait_stage();
+      else dma_wait<0>();
+      if constexpr (PIPE == 9) {
+        __builtin_amdgcn_sched_barrier(0);
+        t3 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      __syncthreads();
+      if constexpr (PIPE == 9) {
+        __builtin_amdgcn_sched_barrier(0);
+        const unsigned long long t4 = __builtin_amdgcn_s_memtime();
+        sd += t1 - t0;
+        sm += t2 - t1;
+        sw += t3 - t2;
+        sb += t4 - t3;
+      }
+      cur = cur == 2 ? 0 : cur + 1;
+    }
+    if constexpr (PIPE == 9) {
+      if (lane == 0 && g.stamps) {
+        unsigned long long* o = g.stamps + ((int64_t)blockIdx.x * NW + w) * 5;
+        o[0] = sd;
+        o[1] = sm;
+        o[2] = sw;
+        o[3] = sb;
+        o[4] = __builtin_amdgcn_s_memtime() - t00;
+      }
+    }
   }
 
-  // epilogue: accumulator register r of lane (h, l32) = row crow(r, h), column l32
+  // ---- epilogue: 4 x 4 quad transpose, then lane (l32 & 3) owns row 8 gq + 4 h + (l32 & 3)
+  // of each 32 x 32 block and its columns (l32 & ~3) .. + 3.  Buffer resources over the
+  // tile's valid rows: stores past M are dropped, loads past M return 0 (no branches).
+  const int mrow = wm * WM + 4 * h + (l32 & 3), ncol = wn * WN + (l32 & ~3);
+  const hx::Buf cbuf(g.C + (int64_t)m0 * g.ldc + n0, (uint32_t)((int64_t)mrows * g.ldc * 4));
+  auto coff = [&](int a, int b, int gq) { return (uint32_t)((mrow + 32 * a + 8 * gq) * g.ldc + ncol + 32 * b) * 4; };
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  // transpose one 4-row group in place: acc[a][b][4 gq + i] = column i of this lane's row
+  auto tr = [&](int a, int b, int gq) {
+    float v[4] = {acc[a][b][4 * gq], acc[a][b][4 * gq + 1], acc[a][b][4 * gq + 2], acc[a][b][4 * gq + 3]};
+    transpose4(v, lane);
 #pragma unroll
-  for (int a = 0; a < MB; ++a)
+    for (int i = 0; i < 4; ++i) acc[a][b][4 * gq + i] = v[i];
+  };
+  if constexpr (EPI == 0 || EPI == 3) {
+    // EPI 3 = EPI 0 with beta: one row block of accumulators at a time (a sched barrier keeps
+    // the compiler from hoisting every block's C loads: 256-VGPR cap)
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      const int n = n0 + wn * WN + 32 * b + l32;
+    for (int a = 0; a < MB; ++a) {
+      f32x4 c[NB][4];
+      if constexpr (EPI == 3) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int m = m0 + wm * WM + 32 * a + crow(r, h);
-        if (m < M) {
-          float* dst = C + (int64_t)m * ldc + n;
-          *dst = beta ? *dst + acc[a][b][r] : acc[a][b][r];
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq)
+            c[b][gq] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(cbuf.r, coff(a, b, gq), 0, 0));
+      }
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          tr(a, b, gq);
+          f32x4 o = {acc[a][b][4 * gq], acc[a][b][4 * gq + 1], acc[a][b][4 * gq + 2], acc[a][b][4 * gq + 3]};
+          if constexpr (EPI == 3) o += c[b][gq];
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), cbuf.r, coff(a, b, gq), 0, 0);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    const hx::Buf pbuf(g.P + (int64_t)m0 * g.ldp + n0, (uint32_t)((int64_t)mrows * g.ldp * 2));
+    auto poff = [&](int a, int b, int gq, int p) {
+      return (uint32_t)((int64_t)(mrow + 32 * a + 8 * gq) * g.ldp + p * g.p_ps + ncol + 32 * b) * 2;
+    };
+    float csum[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) csum[b][i] = 0.f;
+    const hx::Buf xbuf(EPI == 2 ? g.aux + (int64_t)m0 * g.ldaux + n0 : g.C, (uint32_t)((int64_t)mrows * g.ldaux * 4));
+#pragma unroll
+    for (int a = 0; a < MB; ++a)
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        float bb[4] = {0.f, 0.f, 0.f, 0.f};
+        if (g.bias) {
+          const float4 t = *reinterpret_cast<const float4*>(g.bias + n0 + ncol + 32 * b);
+          bb[0] = t.x; bb[1] = t.y; bb[2] = t.z; bb[3] = t.w;
+        }
+        f32x4 u[4];
+        if constexpr (EPI == 2) {
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq)
+            u[gq] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  xbuf.r, (uint32_t)((mrow + 32 * a + 8 * gq) * g.ldaux + ncol + 32 * b) * 4,
+                                                  0, 0));
+        }
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          tr(a, b, gq);
+          float v[4] = {acc[a][b][4 * gq], acc[a][b][4 * gq + 1], acc[a][b][4 * gq + 2], acc[a][b][4 * gq + 3]};
+          if constexpr (EPI == 1) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] += bb[i];
+            const f32x4 o = {v[0], v[1], v[2], v[3]};
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), cbuf.r, coff(a, b, gq), 0, 0);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] = hx::gelu_f(v[i]);
+          } else {
+            const bool in = mrow + 32 * a + 8 * gq < mrows;   // rows past M: no bias-gradient share
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              v[i] *= hx::gelu_grad_f(u[gq][i] + bb[i]);
+              csum[b][i] += in ? v[i] : 0.f;
+            }
+          }
+#pragma unroll
+          for (int p = 0; p < NPC; ++p) {
+            float hp[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              hp[i] = hx::bf2f(hx::f2bf(v[i]));
+              if (p + 1 < NPC) v[i] -= hp[i];
+            }
+            const uint2 pk = pack4(hp);
+            __builtin_amdgcn_raw_buffer_store_b64(
+                __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int, pk), pbuf.r, poff(a, b, gq, p), 0,
+                0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    if constexpr (EPI == 2) {
+      if (g.colpart) {
+        // sum over the 4 rows of a quad and the two 32-lane halves; lanes (l32 & 3) == 0,
+        // h == 0 then hold this wave's 4-column sums -> partial row (mt * NWM + wm)
+        float* row = g.colpart + (int64_t)(mt * NWM + wm) * g.N + n0 + wn * WN;
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float t = csum[b][i];
+            t += qx1(t);
+            t += qx2(t);
+            t += __shfl_xor(t, 32, 64);
+            csum[b][i] = t;
+          }
+        if ((l32 & 3) == 0 && h == 0) {
+#pragma unroll
+          for (int b = 0; b < NB; ++b)
+            *reinterpret_cast<float4*>(row + 32 * b + l32) =
+                make_float4(csum[b][0], csum[b][1], csum[b][2], csum[b][3]);
         }
       }
     }
+  }
 }
 
-template <int BM, int BN, int WM, int WN, int NPC, int NP>
-void launch(const uint16_t* A, int64_t lda, int64_t a_ps, const uint16_t* B, int64_t ldb, int64_t b_ps, float* C,
-            int64_t ldc, int M, int N, int K, int beta, hipStream_t s) {
+// ---------------------------------------------------------------- configurations
+// cfg 0: 256 x 192 tile, waves 4 (M) x 2 (N) of 64 x 96, BK 16, 3 stages (bf16x6 126 KiB LDS):
+//        exactly one, three and four rounds of 256 workgroups at N = 768 / 2304 / 3072, M = 16384
+// cfg 1: 256 x 256 tile, waves 2 x 4 of 128 x 64, BK 16, 3 stages (144 KiB): the wgrad_split
+//        geometry (0.75 fragment reads per MFMA)
+// cfg 2: 256 x 128 tile, waves 4 x 2 of 64 x 64, BK 32, 2 stages (144 KiB)
+// bf16x3 (2 pieces) runs the same tiles at BK 32 with 2 stages (cfg 0: 112 KiB, cfg 1: 128, cfg 2: 96).
+// cfg 3 (bf16x6): cfg 0's tile with the in-place register pipeline (PIPE 2)
+// cfg 4 (bf16x6): 256 x 128 tile, waves 4 x 2 of 64 x 64, BK 16, 3 stages, two fragment sets (PIPE 1)
+// cfg 5 (bf16x6): cfg 1's tile, PIPE 2;   cfg 6 (bf16x6): cfg 4's tile, PIPE 2
+constexpr int kCfgs = 7;
+int cfg_bm(int) { return 256; }
+int cfg_bn(int c) { return (c == 0 || c == 3) ? 192 : (c == 1 || c == 5) ? 256 : 128; }
+int cfg_nwm(int c) { return (c == 1 || c == 5) ? 2 : 4; }
+
+template <int BM, int BN, int WM, int WN, int NPC, int NP, int BK, int NBUF, int EPI, int PIPE = 0>
+void launch_one(const Args& a, hipStream_t s) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
-  const int total = ((M + BM - 1) / BM) * (N / BN);
+  const int total = ((a.M + BM - 1) / BM) * (a.N / BN);
   const int per = (total + 7) / 8;
-  const size_t smem = 2 * (size_t)NPC * (BM + BN) * BK * sizeof(uint16_t);
+  const size_t smem = (size_t)NBUF * NPC * (BM + BN) * BK * 2;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_split_nt_k<BM, BN, WM, WN, NPC, NP>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_piece_k<BM, BN, WM, WN, NPC, NP, BK, NBUF, EPI, PIPE>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
-  gemm_split_nt_k<BM, BN, WM, WN, NPC, NP><<<8 * per, NT, smem, s>>>(A, lda, a_ps, B, ldb, b_ps, C, ldc, M, N, K,
-                                                                    beta);
+  gemm_piece_k<BM, BN, WM, WN, NPC, NP, BK, NBUF, EPI, PIPE><<<8 * per, NT, smem, s>>>(a);
+}
+
+template <int NPC, int NP, int EPI>
+void launch_cfg(int cfg, const Args& a, hipStream_t s) {
+  constexpr int BK = NPC == 3 ? 16 : 32, NBUF = NPC == 3 ? 3 : 2;
+  if (cfg == 0)
+    launch_one<256, 192, 64, 96, NPC, NP, BK, NBUF, EPI>(a, s);
+  else if (cfg == 1)
+    launch_one<256, 256, 128, 64, NPC, NP, BK, NBUF, EPI>(a, s);
+  else if (cfg == 2)
+    launch_one<256, 128, 64, 64, NPC, NP, 32, 2, EPI>(a, s);
+  else if constexpr (NPC == 3) {
+    if (cfg == 3)
+      launch_one<256, 192, 64, 96, NPC, NP, 16, 3, EPI, 2>(a, s);
+    else if (cfg == 4)
+      launch_one<256, 128, 64, 64, NPC, NP, 16, 3, EPI, 1>(a, s);
+    else if (cfg == 5)
+      launch_one<256, 256, 128, 64, NPC, NP, 16, 3, EPI, 2>(a, s);
+    else if (cfg == 9)
+      launch_one<256, 192, 64, 96, NPC, NP, 16, 3, EPI, 9>(a, s);
+    else
+      launch_one<256, 128, 64, 64, NPC, NP, 16, 3, EPI, 2>(a, s);
+  }
 }
 
 }  // namespace
 
+int hx_gemm_split_plan(int M, int N, int K, int passes) {
+  (void)K;
+  (void)M;
+  if (const char* e = getenv("HX_GEMM_CFG")) {
+    const int c = atoi(e);
+    if (c >= 0 && c < kCfgs && c != 8 && N % cfg_bn(c) == 0 && (c < 3 || passes == 6)) return c;
+  }
+  // measured at M = 16384, bf16x6 (tools/probe/gemm_layout_probe.py, profiles/r3_gemm_split.md):
+  // N = 768 on the 256 x 192 tile (one round of 256 workgroups), N = 2304 on 256 x 128, wide
+  // outputs (3072, the decoder's vocabulary) on 256 x 256
+  if (N % 192 == 0 && N <= 1536) return 0;
+  if (N % 2304 == 0) return 2;
+  if (N % 256 == 0) return 1;
+  if (N % 192 == 0) return 0;
+  if (N % 128 == 0) return 2;
+  return -1;
+}
+
+int hx_gemm_split_colpart_rows(int M, int cfg) {
+  if (cfg < 0 || cfg >= kCfgs) return 0;
+  return (M + cfg_bm(cfg) - 1) / cfg_bm(cfg) * cfg_nwm(cfg);
+}
+
 int hx_gemm_split_nt(const void* A, int64_t lda, int64_t a_ps, const void* B, int64_t ldb, int64_t b_ps, float* C,
-                     int64_t ldc, int M, int N, int K, int passes, int beta, hipStream_t s) {
-  if (N % 128 || K % BK || M < 1) return -1;
-  const uint16_t *a = (const uint16_t*)A, *b = (const uint16_t*)B;
-  if (passes == 3)
-    launch<256, 128, 64, 64, 2, 3>(a, lda, a_ps, b, ldb, b_ps, C, ldc, M, N, K, beta, s);
-  else if (passes == 6)
-    launch<256, 128, 64, 64, 3, 6>(a, lda, a_ps, b, ldb, b_ps, C, ldc, M, N, K, beta, s);
-  else
-    return -1;
+                     int64_t ldc, int M, int N, int K, int passes, int beta, const HxGemmEpi* epi, int cfg,
+                     hipStream_t s, int kblock) {
+  const int npc = passes == 6 ? 3 : passes == 3 ? 2 : 0;
+  if (!npc || M < 1 || cfg < 0 || cfg >= kCfgs || N % cfg_bn(cfg)) return -1;
+  if (cfg >= 3 && npc != 3) return -1;
+  const int bk = (npc == 3 && cfg != 2) ? 16 : 32;
+  if (K % bk || npc * a_ps > lda || npc * b_ps > ldb) return -1;
+  // kblock: operands stored [rows][K / kblock][npc][kblock] (piece stride kblock) instead of
+  // [rows][npc][K]: one BK-deep k step of a row is then npc * BK contiguous elements
+  if (kblock && (kblock != bk || a_ps != kblock || b_ps != kblock)) return -1;
+  Args a;
+  a.A = (const uint16_t*)A;
+  a.lda = lda;
+  a.a_ps = a_ps;
+  a.B = (const uint16_t*)B;
+  a.ldb = ldb;
+  a.b_ps = b_ps;
+  a.C = C;
+  a.ldc = ldc;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.beta = beta;
+  const int kind = epi ? epi->kind : 0;
+  a.bias = epi ? epi->bias : nullptr;
+  a.aux = epi ? epi->aux : nullptr;
+  a.ldaux = epi ? epi->ldaux : 0;
+  a.P = epi ? epi->P : nullptr;
+  a.ldp = epi ? epi->ldp : 0;
+  a.p_ps = epi ? epi->p_ps : 0;
+  a.colpart = epi ? epi->colpart : nullptr;
+  a.ksa = a.ksb = (uint32_t)(bk * 2 * (kblock ? npc : 1));
+  a.stamps = nullptr;
+  if (kind == 1 && (!a.P || beta)) return -1;
+  if (kind == 2 && (!a.P || !a.aux)) return -1;
+  if (kind < 0 || kind > 2) return -1;
+#define HX_GS(NPC_, NP_)                                          \
+  do {                                                            \
+    if (kind == 0 && !beta) launch_cfg<NPC_, NP_, 0>(cfg, a, s);  \
+    else if (kind == 0) launch_cfg<NPC_, NP_, 3>(cfg, a, s);      \
+    else if (kind == 1) launch_cfg<NPC_, NP_, 1>(cfg, a, s);      \
+    else launch_cfg<NPC_, NP_, 2>(cfg, a, s);                     \
+  } while (0)
+  if (passes == 6) HX_GS(3, 6);
+  else HX_GS(2, 3);
+#undef HX_GS
   return 0;
+}
+
+void hx_fold_cols(const float* partial, int rows, int N, float* out, int accumulate, hipStream_t s) {
+  hx::fold_rows(partial, rows, N, N, N, out, nullptr, nullptr, accumulate, s);
+}
+
+// diagnostic: cfg 0's kernel (EPI 0) with per-phase s_memtime stamps, one record of 5 counters per
+// wave (grid 8 * ceil(tiles / 8) workgroups x 8 waves); returns the grid size
+int hx_gemm_split_stamps(const void* A, const void* B, float* C, int M, int N, int K, unsigned long long* stamps,
+                         hipStream_t s) {
+  if (N % 192 || K % 16) return -1;
+  Args a{};
+  a.A = (const uint16_t*)A;
+  a.lda = 3 * (int64_t)K;
+  a.a_ps = K;
+  a.B = (const uint16_t*)B;
+  a.ldb = 3 * (int64_t)K;
+  a.b_ps = K;
+  a.C = C;
+  a.ldc = N;
+  a.M = M;
+  a.N = N;
+  a.K = K;
+  a.ksa = a.ksb = 32;
+  a.stamps = stamps;
+  launch_one<256, 192, 64, 96, 3, 6, 16, 3, 0, 9>(a, s);
+  const int total = ((M + 255) / 256) * (N / 192);
+  return 8 * ((total + 7) / 8);
+}
+
+// ---------------------------------------------------------------- diagnostic: LDS-DMA shape probe
+// Every workgroup (8 waves) streams `iters` stages of 42 one-KiB LDS-DMA pieces (the 256 x 192
+// bf16x6 stage) from a large buffer into a 3-stage LDS ring, with the GEMM's counted waits and
+// barriers but no MFMA.  seg = bytes of each contiguous source segment per instruction
+// (1024: a contiguous KiB; 64: 16 rows x 64 B; 32: 32 rows x 32 B; rows `ld` bytes apart).
+namespace {
+__global__ __launch_bounds__(512) void dma_probe_k(const uint16_t* src, uint32_t bytes, int seg, int ld, int iters) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  constexpr int PTOT = 42, NW = 8, STAGE = PTOT * 1024;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int wv = __builtin_amdgcn_readfirstlane(w);
+  const u32x4 rs = rsrc_of(src, bytes);
+  const uint32_t lds0 = (uint32_t)(size_t)(lds_void*)lds;
+  // per-lane source byte offset inside a piece: lane L -> segment L*16/seg, byte L*16 % seg
+  const uint32_t lofs = (uint32_t)((lane * 16 / seg) * ld + (lane * 16) % seg);
+  const uint32_t wg0 = (uint32_t)blockIdx.x * 1024u * 1024u;   // 1 MiB of source per workgroup
+  const int cnt = (PTOT - wv + NW - 1) / NW;
+  auto dma = [&](int it, int buf) {
+    for (int j = 0; j < 6; ++j) {
+      const int q = wv + NW * j;
+      if (q < PTOT) {
+        const uint32_t so = (wg0 + (uint32_t)((it * PTOT + q) % 512) * 2048u) % (bytes - 65536u);
+        dma16(rs, lds0 + buf * STAGE + 1024 * q, so + lofs);
+      }
+    }
+  };
+  dma(0, 0);
+  dma(1, 1);
+  __syncthreads();
+  int cur = 0;
+  for (int it = 0; it < iters; ++it) {
+    const int nxt2 = cur == 0 ? 2 : cur - 1;
+    if (it + 2 < iters) dma(it + 2, nxt2);
+    if (it + 2 < iters) {
+      if (cnt == 6) dma_wait<6>();
+      else dma_wait<5>();
+    } else {
+      dma_wait<0>();
+    }
+    __syncthreads();
+    cur = cur == 2 ? 0 : cur + 1;
+  }
+}
+}  // namespace
+void hx_dma_probe(const void* src, uint32_t bytes, int seg, int ld, int iters, int grid, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&dma_probe_k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              3 * 42 * 1024);
+    attr = true;
+  }
+  dma_probe_k<<<grid, 512, 3 * 42 * 1024, s>>>((const uint16_t*)src, bytes, seg, ld, iters);
 }

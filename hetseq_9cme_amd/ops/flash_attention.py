@@ -110,7 +110,7 @@ class _AttnFn(torch.autograd.Function):
             # dQKV straight into the QKV projection's output-gradient planes (GradPlanes);
             # autograd gets a zero-storage placeholder the projection never reads
             n = split_gemm.passes()
-            order = split_gemm.ORDER_N[n] if gp.prefix else split_gemm.ORDER_Q[n]
+            order = split_gemm.ORDER_N[n] if (gp.prefix or gp.pieces) else split_gemm.ORDER_Q[n]
             gp.planes, dbias = C().attn_bwd_x6_planes(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads,
                                                       keep, ctx.bias, *slots, list(order))
             from .fused import _zero_scalar

@@ -100,14 +100,16 @@ class GradPlanes(object):
     returns a zero-storage placeholder as dy, which the linear never reads.  The linear's
     forward sets ``want`` only when its backward will take the split-plane path, and
     ``prefix`` when it wants the prefix form (each distinct piece once, natural order:
-    split_gemm.prefix_mm) instead of the pass-stacked order Q.
+    split_gemm.prefix_mm) instead of the pass-stacked order Q, ``pieces`` when it runs the
+    hand-written piece GEMMs (natural order too: [rows][npieces][N]).
     """
-    __slots__ = ('want', 'planes', 'prefix')
+    __slots__ = ('want', 'planes', 'prefix', 'pieces')
 
     def __init__(self):
         self.want = False
         self.planes = None
         self.prefix = False
+        self.pieces = False
 
     def take(self):
         p, self.planes = self.planes, None
@@ -348,8 +350,9 @@ class _BiasDropResLNFn(torch.autograd.Function):
             # the upstream split-path linear gets dy as bf16 planes; autograd gets a
             # zero-storage placeholder of dy's shape that nothing reads
             n = split_gemm.passes()
+            order = split_gemm.ORDER_N[n] if gp.pieces else split_gemm.ORDER_Q[n]
             dz, planes, dgamma, dbeta, dbias = C().ln_bwd_planes(
-                dout.contiguous(), z, mean, rstd, gamma, keep, seed, stream, has_bias, list(split_gemm.ORDER_Q[n]),
+                dout.contiguous(), z, mean, rstd, gamma, keep, seed, stream, has_bias, list(order),
                 split_gemm.PIECES[n], grad_slot(gamma), grad_slot(beta), grad_slot(bias) if has_bias else None)
             gp.planes = planes
             dy_ret = _zero_scalar(z.device, z.dtype).expand(ctx.yshape)
@@ -452,9 +455,10 @@ class _LinearFn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         ctx.split = split_gemm.active(x2)
         ctx.pieces = ctx.split and split_gemm.nt_ok(W.shape[1], W.shape[0])
-        ctx.gp = gp if (ctx.split and not ctx.pieces and b is None) else None
+        ctx.gp = gp if (ctx.split and b is None) else None
         if ctx.gp is not None:
             ctx.gp.want = True
+            ctx.gp.pieces = ctx.pieces
         Wsave = W
         if ctx.pieces:    # fp32 on bf16 matrix cores, hand-written piece GEMMs
             x2 = split_gemm.pieces(x2)
@@ -483,7 +487,8 @@ class _LinearFn(torch.autograd.Function):
         b = ctx.b
         dy2 = dy.reshape(-1, dy.shape[-1])
         if ctx.pieces:
-            dys = split_gemm.pieces(dy2.float())
+            dys = ctx.gp.take() if ctx.gp is not None else None
+            dys = dys if dys is not None else split_gemm.pieces(dy2.float())
         else:
             dys = _dy_planes(ctx.gp, dy2) if ctx.split else None
         if not ctx.needs_input_grad[0]:
@@ -538,17 +543,19 @@ class _FFNSplitFn(torch.autograd.Function):
     def forward(ctx, x, W1, b1, W2, mbox, gp):
         x2 = x.reshape(-1, x.shape[-1])
         ctx.pieces = split_gemm.nt_ok(W1.shape[1], W1.shape[0]) and split_gemm.nt_ok(W2.shape[1], W2.shape[0])
-        ctx.gp = gp if not ctx.pieces else None
+        ctx.gp = gp
         if ctx.gp is not None:
             ctx.gp.want = True
+            ctx.gp.pieces = ctx.pieces
         if ctx.pieces:
+            # bias + GELU in the FFN-up GEMM's epilogue (pre-activation u kept in fp32 for the
+            # backward, gelu(u) written as the FFN-down GEMM's pieces): bert_modeling.py:166-168
             xs = split_gemm.pieces(x2)
             w1f, w1t = split_gemm.weight_pieces(W1)
-            y1 = split_gemm.gemm(xs, w1f)
-            hs = split_gemm.act_pieces(y1, b1, 'gelu')
+            u, hs = C().gemm_split_gelu(xs, w1f, split_gemm.passes(), b1)
             w2f, w2t = split_gemm.weight_pieces(W2)
             y2 = split_gemm.gemm(hs, w2f)
-            ctx.save_for_backward(xs, y1, hs, w1t, b1, w2t)
+            ctx.save_for_backward(xs, u, hs, w1t, b1, w2t)
         else:
             y1, xs = split_gemm.forward(x2, W1)
             n = split_gemm.passes()
@@ -574,10 +581,12 @@ class _FFNSplitFn(torch.autograd.Function):
         W1, W2 = ctx.W
         dy2 = dy.reshape(-1, dy.shape[-1])
         if ctx.pieces:
-            dys = split_gemm.pieces(dy2.float())
-            dh = split_gemm.dgrad_pieces(dys, w2)
+            dys = ctx.gp.take() if ctx.gp is not None else None
+            dys = dys if dys is not None else split_gemm.pieces(dy2.float())
+            # GELU backward in the FFN-down data-gradient epilogue: the pieces of
+            # dh * gelu'(u) and the FFN-up bias gradient (u = y1 holds the bias already)
+            dy1s, db1 = C().gemm_split_dgelu(dys, w2, split_gemm.passes(), y1, None, grad_slot(b1))
             dW2 = split_gemm.wgrad_pieces(dys, hs, W2.shape[0], W2.shape[1], grad_slot(W2))
-            dy1s, db1 = split_gemm.act_grad_pieces(dh, y1, b1, 'gelu', grad_slot(b1))
             dx = _dgrad_pieces(dy1s, w1, ctx.xshape, ctx.mbox)
             dW1 = split_gemm.wgrad_pieces(dy1s, xs, W1.shape[0], W1.shape[1], grad_slot(W1))
             return dx, dW1, db1, dW2, None, None
@@ -657,9 +666,10 @@ class _Linear3Fn(torch.autograd.Function):
         x2 = x.reshape(-1, x.shape[-1])
         ctx.split = split_gemm.active(x2)
         ctx.pieces = ctx.split and split_gemm.nt_ok(W.shape[1], W.shape[0])
-        ctx.gp = gp if (ctx.split and not ctx.pieces and not has_b) else None
+        ctx.gp = gp if (ctx.split and not has_b) else None
         if ctx.gp is not None:
             ctx.gp.want = True
+            ctx.gp.pieces = ctx.pieces
             # deep data gradient (3H -> H): the producer's planes in the prefix form are opt-in
             # (HX_PREFIX_QKV=1): measured neutral to 0.1 ms/step slower at BERT-base phase 1,
             # unlike the 4H -> H products (split_gemm.prefix_ok)
@@ -692,7 +702,8 @@ class _Linear3Fn(torch.autograd.Function):
         dy2 = dy.reshape(-1, dy.shape[-1])
         if ctx.pieces:
             n_out = sum(ctx.n)
-            dys = split_gemm.pieces(dy2.float())
+            dys = ctx.gp.take() if ctx.gp is not None else None   # the attention backward's pieces
+            dys = dys if dys is not None else split_gemm.pieces(dy2.float())
             dx = _dgrad_pieces(dys, W, ctx.xshape, ctx.mbox)     # W holds the W^T pieces here
             n_in = W.shape[0]
             wg = lambda slot: split_gemm.wgrad_pieces(dys, x2, n_out, n_in, slot)

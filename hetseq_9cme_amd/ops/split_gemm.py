@@ -70,7 +70,7 @@ MIN_ROWS = {3: int(os.environ.get('HETSEQ_SPLIT_MIN_ROWS_X3', '2048')),
 
 class _State(object):
     passes = 0
-    piece_gemm = os.environ.get('HETSEQ_PIECE_GEMM', '0') == '1'   # see nt_ok
+    piece_gemm = {'1': True, '0': False}.get(os.environ.get('HETSEQ_PIECE_GEMM', ''))   # see nt_ok
     addmm_out_ok = None   # does torch.addmm(bf16, bf16, out_dtype=fp32, out=acc) work in place?
 
 
@@ -207,14 +207,11 @@ def npieces():
 
 def nt_ok(n_in, n_out):
     """Use the hand-written piece GEMMs for a linear layer W [n_out, n_in] (fwd: N = n_out,
-    K = n_in; dgrad: N = n_in, K = n_out; weight pieces: 64 x 64 tiles).
-
-    Opt-in (``HETSEQ_PIECE_GEMM=1``): measured on MI355X at BERT-base phase-1 shapes
-    (tools/bench_gemm_split.py) the piece kernel runs at 0.69-0.90 PF/s of bf16 MFMA work
-    against 1.0-1.3 PF/s for hipBLASLt on the pass-stacked planes (split pass included), so
-    the library path is the default; the kernel is kept, tested and benchmarked as the base
-    for a deeper-pipelined version."""
-    return _State.piece_gemm and n_out % 128 == 0 and n_in % 128 == 0
+    K = n_in; dgrad: N = n_in, K = n_out): the default under bf16x6 (csrc/kernels/gemm_split.hip,
+    LDS-DMA pipeline, profiles/r3_*), opt-in for bf16x3 (``HETSEQ_PIECE_GEMM=1``) and off with
+    ``HETSEQ_PIECE_GEMM=0``, where the library GEMMs on pass-stacked planes run instead."""
+    on = _State.piece_gemm if _State.piece_gemm is not None else _State.passes == 6
+    return on and n_out % 128 == 0 and n_in % 128 == 0
 
 
 def pieces(x2):

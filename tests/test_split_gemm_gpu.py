@@ -366,13 +366,17 @@ def test_attn_bwd_planes_equal_split_of_dqkv(dev, mode, S, with_bias, keep, natu
         ops.set_fp32_gemm('native')
 
 
-def test_grad_planes_handoff_in_bert_layer(dev):
+@pytest.mark.parametrize('piece_gemm', [True, False])
+def test_grad_planes_handoff_in_bert_layer(dev, piece_gemm, monkeypatch):
     """A BERT layer under bf16x6 takes the LayerNorm -> linear and attention -> QKV projection
-    gradient-plane hand-offs, and its gradients equal those of the same layer with the
-    hand-offs disabled (to fp32 atomic-order noise)."""
+    gradient hand-offs (pieces for the hand-written piece GEMMs, pass-stacked planes for the
+    library path): no linear splits its output gradient itself in the backward, and the
+    gradients equal those of the same layer with the hand-offs disabled (to fp32 atomic-order
+    noise)."""
     from hetseq_9cme_amd import ops
     from hetseq_9cme_amd.models.bert import BertConfig, BertLayer
     from hetseq_9cme_amd.ops import fused, split_gemm
+    monkeypatch.setattr(split_gemm._State, 'piece_gemm', piece_gemm)
     ops.set_fp32_gemm('bf16x6')
     try:
         torch.manual_seed(0)
@@ -381,22 +385,22 @@ def test_grad_planes_handoff_in_bert_layer(dev):
         layer = BertLayer(cfg).to(dev)
         x = torch.randn(4, 64, 128, device=dev, requires_grad=True)
         mb = torch.zeros(4, 64, device=dev)
-        calls, splits = [], []
-        orig, orig_split = fused._dy_planes, split_gemm.grad_planes
-
-        def spy(gp, dy2):
-            calls.append(gp is not None and gp.planes is not None)
-            return orig(gp, dy2)
+        splits = []
+        orig_split, orig_pieces = split_gemm.grad_planes, split_gemm.pieces
 
         def spy_split(*a, **k):
             splits.append(1)
             return orig_split(*a, **k)
-        fused._dy_planes, split_gemm.grad_planes = spy, spy_split
+
+        def spy_pieces(*a, **k):
+            splits.append(2)
+            return orig_pieces(*a, **k)
+        loss = layer(x, mb).pow(2).sum()
+        split_gemm.grad_planes, split_gemm.pieces = spy_split, spy_pieces
         try:
-            layer(x, mb).pow(2).sum().backward()
+            loss.backward()
         finally:
-            fused._dy_planes, split_gemm.grad_planes = orig, orig_split
-        assert calls and all(calls), calls
+            split_gemm.grad_planes, split_gemm.pieces = orig_split, orig_pieces
         assert not splits, 'a linear split its output gradient itself (hand-off missed)'
         g1 = [p.grad.clone() for p in layer.parameters()] + [x.grad.clone()]
         for p in layer.parameters():
@@ -485,3 +489,98 @@ def test_wgrad_split_pipeline_variants(dev, T, monkeypatch):
             assert torch.equal(outs['0,0'], outs['2,0']) and torch.equal(outs['0,1'], outs['2,1']), cfg
     finally:
         ops.set_fp32_gemm('native')
+
+
+@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6])
+def test_piece_gemm_every_cfg(dev, cfg, monkeypatch):
+    """Every tile / pipeline configuration of the LDS-DMA piece GEMM (HX_GEMM_CFG) in bf16x6:
+    forward and beta = 1 accumulation against fp64, rows not a multiple of the 256-row tile,
+    a reduction that is not a multiple of the 3-stage ring (K = 272: 17 steps of 16)."""
+    from hetseq_9cme_amd import ops
+    from hetseq_9cme_amd.ops import split_gemm as sg
+    monkeypatch.setenv('HX_GEMM_CFG', str(cfg))
+    g = torch.Generator(device='cpu').manual_seed(40 + cfg)
+    M, N, K = 531, 768, 272 if cfg != 2 else 288
+    a = (torch.rand(M, K, generator=g) * 2 - 1).to(dev)
+    W = (torch.rand(N, K, generator=g) * 2 - 1).to(dev)
+    c0 = torch.randn(M, N, generator=g).to(dev)
+    try:
+        ops.set_fp32_gemm('bf16x6')
+        ap = sg.pieces(a)
+        wf, _ = sg.weight_pieces(W) if K % 64 == 0 else (sg.pieces(W), None)
+        y = sg.gemm(ap, wf)
+        acc = c0.clone()
+        sg.gemm(ap, wf, out=acc, beta=True)
+    finally:
+        ops.set_fp32_gemm('native')
+    ref = a.double() @ W.double().t()
+    sc = a.double().abs() @ W.double().abs().t()
+    assert ((y.double() - ref).abs() / sc).max().item() < 1.5e-6
+    e = ((acc.double() - ref - c0.double()).abs() / (sc + c0.double().abs())).max().item()
+    assert e < 1.5e-6, e
+
+
+@pytest.mark.parametrize('mode', ['bf16x6', 'bf16x3'])
+def test_gemm_gelu_epilogues(dev, mode):
+    """FFN epilogues of the piece GEMM against fp64: bias + GELU (pre-activation u and the
+    pieces of gelu(u)), and the GELU backward (pieces of dh * gelu'(u) and its column sums =
+    the FFN-up bias gradient), with rows that are not a multiple of the tile."""
+    from hetseq_9cme_amd import ops
+    from hetseq_9cme_amd.ops import split_gemm as sg
+    from hetseq_9cme_amd.ops._ext import C
+    g = torch.Generator(device='cpu').manual_seed(31)
+    T, H, I = 300, 256, 768
+    x = torch.randn(T, H, generator=g).to(dev)
+    W1 = (torch.randn(I, H, generator=g) * 0.1).to(dev)
+    b1 = (torch.randn(I, generator=g) * 0.5).to(dev)
+    W2 = (torch.randn(H, I, generator=g) * 0.05).to(dev)
+    dy = torch.randn(T, H, generator=g).to(dev)
+    try:
+        ops.set_fp32_gemm(mode)
+        n = sg.passes()
+        xs = sg.pieces(x)
+        w1f, _ = sg.weight_pieces(W1)
+        u, hp = C().gemm_split_gelu(xs, w1f, n, b1)
+        _, w2t = sg.weight_pieces(W2)
+        tp, db = C().gemm_split_dgelu(sg.pieces(dy), w2t, n, u, None, None)
+        npc = sg.npieces()
+    finally:
+        ops.set_fp32_gemm('native')
+    tol = 2e-6 if mode == 'bf16x6' else 8e-6
+    ud = x.double() @ W1.double().t() + b1.double()
+    us = x.double().abs() @ W1.double().abs().t() + b1.double().abs()
+    assert ((u.double() - ud).abs() / us).max().item() < tol
+    h = sum(hp.view(T, npc, I)[:, p].double() for p in range(npc))
+    hr = ops.gelu_ref(u.double())
+    # fp32 erf-GELU (a few ulp of |u|) + the representation error of the pieces
+    assert ((h - hr).abs() / (u.double().abs() + 1e-6)).max().item() < (5e-7 if npc == 3 else 2 ** -15)
+    ud_ = u.double().requires_grad_(True)
+    ops.gelu_ref(ud_).backward(dy.double() @ W2.double())
+    t = sum(tp.view(T, npc, I)[:, p].double() for p in range(npc))
+    ts = (dy.double().abs() @ W2.double().abs()) * 1.13   # |gelu'| <= 1.13
+    assert ((t - ud_.grad).abs() / (ts + 1e-30)).max().item() < 5 * tol
+    dbr = ud_.grad.sum(0)
+    assert ((db.double() - dbr).abs() / ts.sum(0)).max().item() < 5 * tol
+
+
+def test_piece_gemm_kblocked_layout(dev):
+    """k-blocked operand layout [rows][K / 16][3][16] (kblock = 16) gives the natural layout's
+    product."""
+    from hetseq_9cme_amd import ops
+    from hetseq_9cme_amd.ops import split_gemm as sg
+    from hetseq_9cme_amd.ops._ext import C
+    g = torch.Generator(device='cpu').manual_seed(5)
+    M, N, K = 512, 768, 256
+    a = torch.randn(M, K, generator=g).to(dev)
+    W = torch.randn(N, K, generator=g).to(dev)
+    try:
+        ops.set_fp32_gemm('bf16x6')
+        ap, wf = sg.pieces(a), sg.weight_pieces(W)[0]
+
+        def blk(p):
+            return p.view(p.shape[0], 3, K // 16, 16).permute(0, 2, 1, 3).contiguous().view(p.shape[0], -1)
+        y0 = C().gemm_split(ap, wf, 6)
+        y1 = C().gemm_split(blk(ap), blk(wf), 6, None, False, 16)
+    finally:
+        ops.set_fp32_gemm('native')
+    assert torch.equal(y0, y1)

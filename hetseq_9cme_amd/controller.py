@@ -73,7 +73,8 @@ class Controller(object):
         use_reducer = self.world_size > 1 and not getattr(args, 'use_bmuf', False)
         self.reducer = GradReducer(self.flat, bucket_cap_mb=args.bucket_cap_mb,
                                    find_unused_parameters=getattr(args, 'find_unused_parameters', False),
-                                   broadcast_params=use_reducer)
+                                   broadcast_params=use_reducer,
+                                   bucket_peer_mb=getattr(args, 'bucket_peer_mb', 0.0))
         if not use_reducer:
             self.reducer.enabled = False
         elif getattr(args, 'allreduce_impl', 'rccl') == 'xgmi':
@@ -179,7 +180,16 @@ class Controller(object):
                 'Optimizer does not match; please reset the optimizer (--reset-optimizer).'
             if not reset_lr_scheduler:
                 self.lr_scheduler.load_state_dict(last_optim['lr_scheduler_state'])
-            self.optimizer.load_state_dict(last_optim_state, optimizer_overrides)
+            # an untagged state from this framework's own earlier files is numbered by flat index
+            # (ADVICE r2); reference / torch-optimizer files are untagged too but carry none of
+            # this framework's own flags in their args
+            ck_args = state.get('args') if os.path.exists(filename) else None
+            legacy = 'param_order' not in last_optim_state and ck_args is not None and \
+                hasattr(ck_args, 'fp32_gemm')
+            if legacy:
+                print('| optimizer state of {} predates the state-order tag: remapping from flat order'.format(
+                    filename))
+            self.optimizer.load_state_dict(last_optim_state, optimizer_overrides, legacy_flat_order=legacy)
             self.set_num_updates(last_optim['num_updates'])
         if extra_state is not None and 'train_iterator' in extra_state:
             epoch = extra_state['train_iterator']['epoch']

@@ -553,7 +553,7 @@ std::vector<Tensor> bias_act_planes(Tensor y, OptT b, OptT dout, int64_t act, st
 }
 
 // ------------------------------------------------------------------ piece GEMMs
-std::vector<Tensor> split_weight(Tensor W, int64_t npieces) {
+std::vector<Tensor> split_weight(Tensor W, int64_t npieces, int64_t b16) {
   check_f32(W, "split_weight input");
   TORCH_CHECK(W.dim() == 2 && W.size(0) % 64 == 0 && W.size(1) % 64 == 0 && aligned16(W.data_ptr()),
               "split_weight: W must be [N, K] with N, K multiples of 64");
@@ -562,8 +562,10 @@ std::vector<Tensor> split_weight(Tensor W, int64_t npieces) {
   auto bf = W.options().dtype(torch::kBFloat16);
   Tensor wf = torch::empty({N, npieces * K}, bf), wt = torch::empty({K, npieces * N}, bf);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(W.device());
+  TORCH_CHECK(!b16 || npieces == 3, "split_weight: the B16 layout is for 3 pieces");
+  TORCH_CHECK(b16 >= 0 && b16 <= 3, "split_weight: b16 is a 2-bit mask");
   hx_split_weight(W.data_ptr<float>(), (int)N, (int)K, (int)npieces, reinterpret_cast<uint16_t*>(wf.data_ptr()),
-                  reinterpret_cast<uint16_t*>(wt.data_ptr()), cur_stream(W));
+                  reinterpret_cast<uint16_t*>(wt.data_ptr()), cur_stream(W), (int)b16);
   return {wf, wt};
 }
 
@@ -580,16 +582,16 @@ bool gemm_split_ok(const Tensor& a, const Tensor& b, int64_t npc) {
          256 * a.size(1) * 2 < (1LL << 31) && b.size(0) * a.size(1) * 2 < (1LL << 31) &&
          256 * b.size(0) * 6 < (1LL << 31);
 }
+// lay: bit 0 / bit 1 = A / B operand in the B16 piece layout (gemm_split.hip)
 static int gemm_split_launch(const Tensor& a, const Tensor& b, int64_t passes, float* C, int64_t ldc, bool beta,
-                             const HxGemmEpi* epi, int64_t kblock = 0) {
+                             const HxGemmEpi* epi, int64_t lay = 0) {
   const int64_t npc = passes == 6 ? 3 : 2;
   const int64_t M = a.size(0), N = b.size(0), K = a.size(1) / npc;
-  const int cfg = hx_gemm_split_plan((int)M, (int)N, (int)K, (int)passes);
-  const int64_t ps = kblock ? kblock : K;
-  return hx_gemm_split_nt(a.data_ptr(), npc * K, ps, b.data_ptr(), npc * K, ps, C, ldc, (int)M, (int)N, (int)K,
-                          (int)passes, beta ? 1 : 0, epi, cfg, cur_stream(a), (int)kblock);
+  const int cfg = hx_gemm_split_plan((int)M, (int)N, (int)K, (int)passes, (int)lay);
+  return hx_gemm_split_nt(a.data_ptr(), npc * K, (lay & 1) ? 16 : K, b.data_ptr(), npc * K, (lay & 2) ? 16 : K, C, ldc,
+                          (int)M, (int)N, (int)K, (int)passes, beta ? 1 : 0, epi, cfg, cur_stream(a), (int)lay);
 }
-Tensor gemm_split(Tensor a, Tensor b, int64_t passes, OptT out_, bool beta, int64_t kblock) {
+Tensor gemm_split(Tensor a, Tensor b, int64_t passes, OptT out_, bool beta, int64_t lay) {
   const int64_t npc = passes == 6 ? 3 : 2;
   TORCH_CHECK(passes == 3 || passes == 6, "gemm_split: passes must be 3 or 6");
   TORCH_CHECK(gemm_split_ok(a, b, npc), "gemm_split: unsupported operands");
@@ -600,13 +602,13 @@ Tensor gemm_split(Tensor a, Tensor b, int64_t passes, OptT out_, bool beta, int6
               "gemm_split: out must be fp32 [M, N] with unit column stride and 16-B rows");
   TORCH_CHECK(!beta || has(out_), "gemm_split: beta needs an output to accumulate into");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
-  TORCH_CHECK(gemm_split_launch(a, b, passes, out.data_ptr<float>(), out.stride(0), beta, nullptr, kblock) == 0,
+  TORCH_CHECK(gemm_split_launch(a, b, passes, out.data_ptr<float>(), out.stride(0), beta, nullptr, lay) == 0,
               "gemm_split: launch failed");
   dbg_finite(out, "gemm_split");
   return out;
 }
 // FFN up: u = a . b^T + bias (fp32, kept for the backward) and the pieces of gelu(u)
-std::vector<Tensor> gemm_split_gelu(Tensor a, Tensor b, int64_t passes, OptT bias) {
+std::vector<Tensor> gemm_split_gelu(Tensor a, Tensor b, int64_t passes, OptT bias, int64_t lay) {
   const int64_t npc = passes == 6 ? 3 : 2;
   TORCH_CHECK(passes == 3 || passes == 6, "gemm_split_gelu: passes must be 3 or 6");
   TORCH_CHECK(gemm_split_ok(a, b, npc), "gemm_split_gelu: unsupported operands");
@@ -620,13 +622,15 @@ std::vector<Tensor> gemm_split_gelu(Tensor a, Tensor b, int64_t passes, OptT bia
   HxGemmEpi e{1, ptr_or_null<float>(bias), nullptr, 0, reinterpret_cast<uint16_t*>(p.data_ptr()), npc * N, N,
               nullptr};
   c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
-  TORCH_CHECK(gemm_split_launch(a, b, passes, u.data_ptr<float>(), N, false, &e) == 0, "gemm_split_gelu: launch failed");
+  TORCH_CHECK(gemm_split_launch(a, b, passes, u.data_ptr<float>(), N, false, &e, lay) == 0,
+              "gemm_split_gelu: launch failed");
   dbg_finite(u, "gemm_split_gelu");
   return {u, p};
 }
 // FFN down data gradient + GELU backward: t = (a . b^T) * gelu'(u (+ bias)); returns the pieces of
 // t and d bias = column sums of t (into dbias_out when given)
-std::vector<Tensor> gemm_split_dgelu(Tensor a, Tensor b, int64_t passes, Tensor u, OptT bias, OptT dbias_out) {
+std::vector<Tensor> gemm_split_dgelu(Tensor a, Tensor b, int64_t passes, Tensor u, OptT bias, OptT dbias_out,
+                                     int64_t lay) {
   const int64_t npc = passes == 6 ? 3 : 2;
   TORCH_CHECK(passes == 3 || passes == 6, "gemm_split_dgelu: passes must be 3 or 6");
   TORCH_CHECK(gemm_split_ok(a, b, npc), "gemm_split_dgelu: unsupported operands");
@@ -638,7 +642,7 @@ std::vector<Tensor> gemm_split_dgelu(Tensor a, Tensor b, int64_t passes, Tensor 
     check_f32(*bias, "gemm_split_dgelu bias");
     TORCH_CHECK(bias->numel() == N && bias->is_contiguous() && aligned16(bias->data_ptr()), "gemm_split_dgelu: bias");
   }
-  const int cfg = hx_gemm_split_plan((int)M, (int)N, (int)(a.size(1) / npc), (int)passes);
+  const int cfg = hx_gemm_split_plan((int)M, (int)N, (int)(a.size(1) / npc), (int)passes, (int)lay);
   const int prow = hx_gemm_split_colpart_rows((int)M, cfg);
   auto f32 = a.options().dtype(torch::kFloat32);
   Tensor p = torch::empty({M, npc * N}, a.options());
@@ -648,13 +652,13 @@ std::vector<Tensor> gemm_split_dgelu(Tensor a, Tensor b, int64_t passes, Tensor 
   HxGemmEpi e{2, ptr_or_null<float>(bias), u.data_ptr<float>(), N, reinterpret_cast<uint16_t*>(p.data_ptr()),
               npc * N, N, part.data_ptr<float>()};
   c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
-  TORCH_CHECK(gemm_split_launch(a, b, passes, nullptr, N, false, &e) == 0, "gemm_split_dgelu: launch failed");
+  TORCH_CHECK(gemm_split_launch(a, b, passes, nullptr, N, false, &e, lay) == 0, "gemm_split_dgelu: launch failed");
   hx_fold_cols(part.data_ptr<float>(), prow, (int)N, db.data_ptr<float>(), 0, cur_stream(a));
   return {p, db};
 }
 
 // diagnostic: per-wave phase cycle sums of the piece GEMM main loop (cfg 0, bf16x6)
-Tensor gemm_split_stamps(Tensor a, Tensor b) {
+Tensor gemm_split_stamps(Tensor a, Tensor b, int64_t lay) {
   TORCH_CHECK(gemm_split_ok(a, b, 3), "gemm_split_stamps: unsupported operands");
   const int64_t M = a.size(0), N = b.size(0), K = a.size(1) / 3;
   const int64_t tiles = ((M + 255) / 256) * (N / 192);
@@ -662,11 +666,23 @@ Tensor gemm_split_stamps(Tensor a, Tensor b) {
   Tensor out = torch::empty({M, N}, a.options().dtype(torch::kFloat32));
   c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
   TORCH_CHECK(hx_gemm_split_stamps(a.data_ptr(), b.data_ptr(), out.data_ptr<float>(), (int)M, (int)N, (int)K,
-                                   reinterpret_cast<unsigned long long*>(st.data_ptr()), cur_stream(a)) > 0,
+                                   reinterpret_cast<unsigned long long*>(st.data_ptr()), cur_stream(a),
+                                   (int)lay) > 0,
               "gemm_split_stamps: launch failed");
   return st;
 }
 
+// timing experiment: cfg 0 with every 32x32x16 MFMA replaced by two 16x16x32 (wrong results)
+Tensor gemm_split_mfma16_timing(Tensor a, Tensor b) {
+  TORCH_CHECK(gemm_split_ok(a, b, 3), "unsupported operands");
+  Tensor out = torch::empty({a.size(0), b.size(0)}, a.options().dtype(torch::kFloat32));
+  HxGemmEpi e{7, nullptr, nullptr, 0, nullptr, 0, 0, nullptr};
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  const int64_t K = a.size(1) / 3;
+  TORCH_CHECK(hx_gemm_split_nt(a.data_ptr(), 3 * K, K, b.data_ptr(), 3 * K, K, out.data_ptr<float>(), b.size(0),
+                               (int)a.size(0), (int)b.size(0), (int)K, 6, 0, &e, 0, cur_stream(a)) == 0, "launch");
+  return out;
+}
 void dma_probe(Tensor src, int64_t seg, int64_t ld, int64_t iters, int64_t grid) {
   TORCH_CHECK(src.is_cuda() && src.nbytes() < (1LL << 32) && src.nbytes() > (1 << 20), "dma_probe: src");
   TORCH_CHECK(seg == 1024 || seg == 128 || seg == 64 || seg == 32, "dma_probe: seg");
@@ -727,18 +743,23 @@ Tensor split_planes_t(Tensor W, std::vector<int64_t> order, int64_t npieces, int
 // Contexts travel to Python as integers (owned by parallel/xgmi.py).
 inline void xar_check(int rc) { TORCH_CHECK(rc == 0, hx_xar_last_error()); }
 inline void* as_ctx(int64_t h) { return reinterpret_cast<void*>(static_cast<uintptr_t>(h)); }
-int64_t xar_create(int64_t rank, int64_t world, int64_t cap_floats, int64_t nblocks, double timeout_s) {
+int64_t xar_create(int64_t rank, int64_t world, int64_t nblocks, double timeout_s, int64_t oneshot_max_bytes) {
   void* c = nullptr;
-  xar_check(hx_xar_create((int)rank, (int)world, cap_floats, (int)nblocks, timeout_s, &c));
+  xar_check(hx_xar_create((int)rank, (int)world, (int)nblocks, timeout_s, oneshot_max_bytes, &c));
   return static_cast<int64_t>(reinterpret_cast<uintptr_t>(c));
 }
-py::bytes xar_export(int64_t h) {
-  char buf[128];
-  xar_check(hx_xar_export(as_ctx(h), buf));
-  return py::bytes(buf, 128);
+void xar_register(int64_t h, Tensor buf) {
+  check_f32(buf, "xGMI registered buffer");
+  TORCH_CHECK(buf.is_contiguous() && aligned16(buf.data_ptr()), "xGMI registered buffer: contiguous, 16-B aligned");
+  xar_check(hx_xar_register(as_ctx(h), buf.data_ptr<float>(), buf.numel()));
 }
-void xar_open(int64_t h, py::bytes handles) {
-  const std::string s = handles;
+py::bytes xar_export(int64_t h) {
+  char buf[kXarRecord];
+  xar_check(hx_xar_export(as_ctx(h), buf));
+  return py::bytes(buf, kXarRecord);
+}
+void xar_open(int64_t h, py::bytes recs) {
+  const std::string s = recs;
   xar_check(hx_xar_open(as_ctx(h), s.data()));
 }
 void xar_allreduce(int64_t h, Tensor buf) {
@@ -769,7 +790,14 @@ void xar_error_async(int64_t h, Tensor out) {
   c10::hip::HIPGuardMasqueradingAsCUDA guard(out.device());
   xar_check(hx_xar_error_async(as_ctx(h), out.data_ptr<int32_t>(), cur_stream(out)));
 }
-int64_t xar_capacity(int64_t h) { return hx_xar_capacity(as_ctx(h)); }
+// PCI bus id ("dddd:bb:dd.f") of a device visible to this process: the process-independent
+// identity of a GPU (local ordinals differ between processes with different visible sets)
+std::string device_pci_bus_id(int64_t dev) {
+  char id[64] = {0};
+  TORCH_CHECK(hipDeviceGetPCIBusId(id, (int)sizeof(id), (int)dev) == hipSuccess, "hipDeviceGetPCIBusId failed");
+  return std::string(id);
+}
+int64_t xar_oneshot_max(int64_t h) { return hx_xar_oneshot_max(as_ctx(h)); }
 void xar_destroy(int64_t h) { hx_xar_destroy(as_ctx(h)); }
 
 }  // namespace
@@ -817,25 +845,31 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_bf16_ok", &wgrad_bf16_ok);
   m.def("split_planes", &split_planes);
   m.def("split_planes_t", &split_planes_t);
-  m.def("split_weight", &split_weight);
+  m.def("split_weight", &split_weight, py::arg("W"), py::arg("npieces"), py::arg("b16") = 0);
+  m.def("gemm_split_weight_b16", &hx_gemm_split_weight_b16);
   m.def("gemm_split", &gemm_split, py::arg("a"), py::arg("b"), py::arg("passes"), py::arg("out") = py::none(),
-        py::arg("beta") = false, py::arg("kblock") = 0);
-  m.def("gemm_split_gelu", &gemm_split_gelu);
+        py::arg("beta") = false, py::arg("lay") = 0);
+  m.def("gemm_split_gelu", &gemm_split_gelu, py::arg("a"), py::arg("b"), py::arg("passes"), py::arg("bias"),
+        py::arg("lay") = 0);
+  m.def("gemm_split_dgelu", &gemm_split_dgelu, py::arg("a"), py::arg("b"), py::arg("passes"), py::arg("u"),
+        py::arg("bias"), py::arg("dbias_out"), py::arg("lay") = 0);
   m.def("gemm_split_stamps", &gemm_split_stamps);
   m.def("dma_probe", &dma_probe);
-  m.def("gemm_split_dgelu", &gemm_split_dgelu);
+  m.def("gemm_split_mfma16_timing", &gemm_split_mfma16_timing);
   m.def("gemm_split_ok", &gemm_split_ok);
   m.def("bias_act_planes", &bias_act_planes);
   m.def("wgrad_split", &wgrad_split);
   m.def("wgrad_split_ok", &wgrad_split_ok);
   m.def("xar_create", &xar_create);
+  m.def("xar_register", &xar_register);
+  m.def("device_pci_bus_id", &device_pci_bus_id);
   m.def("xar_export", &xar_export);
   m.def("xar_open", &xar_open);
   m.def("xar_allreduce", &xar_allreduce);
   m.def("xar_allreduce_sim", &xar_allreduce_sim);
   m.def("xar_error", &xar_error);
   m.def("xar_error_async", &xar_error_async);
-  m.def("xar_capacity", &xar_capacity);
+  m.def("xar_oneshot_max", &xar_oneshot_max);
   m.def("xar_destroy", &xar_destroy);
   m.def("set_debug", &set_debug);
   m.def("get_debug", &get_debug);

@@ -93,7 +93,9 @@ void hx_bias_act_planes(int act, const float* y, const float* b, const float* do
 
 // split.hip -- weight pieces in both GEMM layouts: wf [N][npieces][K], wt [K][npieces][N];
 // W fp32 [N][K] contiguous, N and K multiples of 64.
-void hx_split_weight(const float* W, int N, int K, int npieces, uint16_t* wf, uint16_t* wt, hipStream_t s);
+// b16 bit 0 / bit 1: wf / wt in the B16 layout [rows][C / 16][3][16] (bf16x6 piece GEMM operand B)
+void hx_split_weight(const float* W, int N, int K, int npieces, uint16_t* wf, uint16_t* wt, hipStream_t s,
+                     int b16 = 0);
 
 // gemm_split.hip -- C[M][N] (+)= sum over piece pairs A_a[M][K] . B_b[N][K]^T (bf16 pieces of fp32
 // operands: piece p of row r at X + r * ldx + p * x_ps, npieces * x_ps <= ldx); passes 3 or 6.
@@ -112,13 +114,14 @@ struct HxGemmEpi {
   int64_t ldp, p_ps;
   float* colpart;
 };
-int hx_gemm_split_plan(int M, int N, int K, int passes);
+int hx_gemm_split_plan(int M, int N, int K, int passes, int lay = 0);
 int hx_gemm_split_colpart_rows(int M, int cfg);
+int hx_gemm_split_weight_b16(int N, int passes);
 int hx_gemm_split_nt(const void* A, int64_t lda, int64_t a_ps, const void* B, int64_t ldb, int64_t b_ps, float* C,
                      int64_t ldc, int M, int N, int K, int passes, int beta, const HxGemmEpi* epi, int cfg,
-                     hipStream_t s, int kblock = 0);
+                     hipStream_t s, int lay = 0);
 int hx_gemm_split_stamps(const void* A, const void* B, float* C, int M, int N, int K, unsigned long long* stamps,
-                         hipStream_t s);
+                         hipStream_t s, int lay = 0);
 void hx_dma_probe(const void* src, uint32_t bytes, int seg, int ld, int iters, int grid, hipStream_t s);
 // fold [rows][N] column partials into out[N] (+= if accumulate)
 void hx_fold_cols(const float* partial, int rows, int N, float* out, int accumulate, hipStream_t s);
@@ -133,13 +136,17 @@ void hx_split_planes(const float* x, int64_t ldx, uint16_t* out, int64_t R, int 
 void hx_split_planes_t(const float* W, int64_t ldw, int N, int K, uint16_t* out, int Np, int npieces, int npl,
                        uint32_t order, hipStream_t s);
 
-// xgmi_allreduce.hip -- intra-node two-shot all-reduce over IPC-mapped peer buffers.
+// xgmi_allreduce.hip -- intra-node in-place all-reduce (two-shot; one-shot for buckets up to
+// oneshot_max_bytes) over IPC-mapped peer gradient buffers.  Sequence: create, register (the
+// buffer every bucket is a slice of), export -> exchange -> open, then allreduce per bucket.
 // Every function returns 0 on success, -1 with a message in hx_xar_last_error().
+constexpr int kXarRecord = 192;   // exported bytes per rank
 const char* hx_xar_last_error();
-int hx_xar_create(int rank, int world, int64_t cap_floats, int nblocks, double timeout_s, void** ctx);
-int64_t hx_xar_capacity(void* ctx);
-int hx_xar_export(void* ctx, char* out128);
-int hx_xar_open(void* ctx, const char* handles);
+int hx_xar_create(int rank, int world, int nblocks, double timeout_s, int64_t oneshot_max_bytes, void** ctx);
+int64_t hx_xar_oneshot_max(void* ctx);
+int hx_xar_register(void* ctx, float* base, int64_t n);
+int hx_xar_export(void* ctx, char* out);
+int hx_xar_open(void* ctx, const char* recs);
 int hx_xar_allreduce(void* ctx, float* buf, int64_t n, hipStream_t s);
 // mute >= 0: that simulated rank never raises its flags (test hook: the others time out)
 int hx_xar_allreduce_sim(void** ctxs, float** bufs, int W, int64_t n, int mute, hipStream_t s);

@@ -82,6 +82,22 @@ struct Img<16> {
   }
 };
 
+// "B16" piece layout (bf16x6): element (r, p, k) at r * 3K + (k / 16) * 48 + p * 16 + k % 16, so
+// one 16-deep k step of a row is 96 contiguous bytes holding all three pieces.  The LDS image of
+// a stage is the source rows back to back (chunk c = 6 r + 2 p + h of 16 B), with the 16-B chunks
+// of every 256-B block XOR-permuted by a function of the block index (period 6): an involution
+// inside each block, so one DMA instruction (1 KiB of image) still reads 1 KiB of contiguous
+// source, and the 16-lane groups of a ds_read_b128 fragment read (32 consecutive rows, one
+// chunk) hit 16 distinct 4-bank slots (exhaustive check: tools/probe/b16_swizzle_check.py).
+__device__ __forceinline__ int b16_sw(int blk) {
+  const int m = blk % 6;
+  return (m == 0 || m == 4 || m == 5) ? 14 : 13;
+}
+__device__ __forceinline__ int b16_off(int r, int q) {   // byte offset of chunk q of image row r
+  const int c = 6 * r + q;
+  return 16 * (c ^ b16_sw(c >> 4));
+}
+
 // one LDS-DMA wave-instruction: 16 B per lane from buffer byte voff (zeros past the buffer's
 // end) to LDS bytes [dst + 16 lane, + 16); dst is wave-uniform.  From asm, so the compiler
 // does not drain it (vmcnt(0)) before the next LDS read of the stage being computed; the
@@ -171,7 +187,7 @@ __device__ __forceinline__ uint2 pack4(const float (&x)[4]) {
   return make_uint2(hx::f2bf(x[0]) | ((uint32_t)hx::f2bf(x[1]) << 16),
                     hx::f2bf(x[2]) | ((uint32_t)hx::f2bf(x[3]) << 16));
 }
-template <int BM, int BN, int WM, int WN, int NPC, int NP, int BK, int NBUF, int EPI, int PIPE>
+template <int BM, int BN, int WM, int WN, int NPC, int NP, int BK, int NBUF, int EPI, int PIPE, int LAY = 0>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_piece_k(Args g) {
   constexpr int NWM = BM / WM, NW = NWM * (BN / WN);
   constexpr int MB = WM / 32, NB = WN / 32;
@@ -184,6 +200,9 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_piece_k(Args 
   static_assert(A_BYTES % 1024 == 0 && B_BYTES % 1024 == 0, "tile / DMA piece mismatch");
   static_assert(NBUF == 2 || NBUF == 3, "stages");
   static_assert(JLO >= 1, "fewer DMA pieces than waves");
+  static_assert(LAY == 0 || (NPC == 3 && BK == 16), "B16 layout: bf16x6, 16-deep stages");
+  constexpr bool LA = LAY & 1, LB = LAY & 2;   // A / B operand in the B16 layout
+  constexpr int A_REG = NPC * A_BYTES;   // A image bytes of a stage (B image follows)
   extern __shared__ __attribute__((aligned(16))) char lds[];
 
   const int TM = (g.M + BM - 1) / BM, TN = g.N / BN, total = TM * TN;
@@ -214,7 +233,13 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_piece_k(Args 
   for (int j = 0; j < JHI; ++j) {
     const int q = wv + NW * j;
     isa[j] = q < PA;
-    if (q < PA) {
+    if ((q < PA && LA) || (q >= PA && LB)) {
+      // image chunk x of this lane -> logical chunk c = 6 row + q6 -> source row / 16-B unit
+      const int x = 64 * (q < PA ? q : q - PA) + lane;
+      const int c = x ^ b16_sw(x >> 4);
+      const int r = c / 6, q6 = c - 6 * r;
+      voff[j] = (uint32_t)(r * (q < PA ? g.lda : g.ldb) + 8 * q6) * 2;
+    } else if (q < PA) {
       const int p = q / KA, r = (q % KA) * RPK + rl;
       voff[j] = (uint32_t)(r * g.lda + p * g.a_ps + 8 * ch) * 2;
     } else {
@@ -223,6 +248,21 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_piece_k(Args 
     }
     dsto[j] = 1024 * q;
   }
+  // per-lane LDS byte offsets of the fragments (fixed for the whole k loop)
+  int offa[NPC][MB][BK / 16], offb[NPC][NB][BK / 16];
+#pragma unroll
+  for (int p = 0; p < NPC; ++p)
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+        offa[p][a][ks] = LA ? b16_off(wm * WM + 32 * a + l32, 2 * p + h)
+                                  : p * A_BYTES + Img<BK>::off(wm * WM + 32 * a + l32, 2 * ks + h);
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+        offb[p][b][ks] = A_REG + (LB ? b16_off(wn * WN + 32 * b + l32, 2 * p + h)
+                                           : p * B_BYTES + Img<BK>::off(wn * WN + 32 * b + l32, 2 * ks + h));
+    }
   const int cnt = (PTOT - wv + NW - 1) / NW;   // JHI or JLO
   const uint32_t lds0 = (uint32_t)(size_t)(lds_void*)lds;   // LDS byte address of the stages
   auto dma = [&](int it, int buf) {
@@ -232,6 +272,11 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_piece_k(Args 
     for (int j = 0; j < JHI; ++j) {
       if (j < JLO || j < cnt) dma16(isa[j] ? ra : rb, st + dsto[j], voff[j] + (isa[j] ? koa : kob));
     }
+  };
+  auto dma_one = [&](int it, int buf, int j) {   // this wave's j-th DMA piece of stage it
+    const uint32_t st = lds0 + buf * STAGE;
+    const uint32_t ko = (uint32_t)it * (isa[j] ? g.ksa : g.ksb);
+    dma16(isa[j] ? ra : rb, st + dsto[j], voff[j] + ko);
   };
   auto wait_stage = [&]() {   // all but this wave's youngest stage of DMAs landed
     if constexpr (JHI == JLO) {
@@ -257,11 +302,10 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_piece_k(Args 
       for (int p = 0; p < NPC; ++p) {
 #pragma unroll
         for (int a = 0; a < MB; ++a)
-          fa[p][a] = *reinterpret_cast<const bf16x8*>(st + p * A_BYTES + Img<BK>::off(wm * WM + 32 * a + l32, 2 * ks + h));
+          fa[p][a] = *reinterpret_cast<const bf16x8*>(st + offa[p][a][ks]);
 #pragma unroll
         for (int b = 0; b < NB; ++b)
-          fb[p][b] = *reinterpret_cast<const bf16x8*>(st + NPC * A_BYTES + p * B_BYTES +
-                                                      Img<BK>::off(wn * WN + 32 * b + l32, 2 * ks + h));
+          fb[p][b] = *reinterpret_cast<const bf16x8*>(st + offb[p][b][ks]);
       }
 #pragma unroll
       for (int q = 0; q < NP; ++q)
@@ -274,7 +318,75 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_piece_k(Args 
     }
   };
 
-  if constexpr (PIPE == 1) {
+  // MFMA passes of one stage with the next stages' DMA pieces issued between them (one per pass,
+  // pinned by sched barriers): the DMA issue -- ~100-150 cycles per piece when issued back to
+  // back (profiles/r3_gemm_split.md, stamp build) -- then hides in the shadow of the wave's own
+  // MFMAs instead of stalling both waves of the SIMD at the top of every k step
+  auto mma_dma = [&](int buf, int dit, int dbuf) {
+    const char* st = lds + buf * STAGE;
+    bf16x8 fa[NPC][MB], fb[NPC][NB];
+#pragma unroll
+    for (int p = 0; p < NPC; ++p) {
+#pragma unroll
+      for (int a = 0; a < MB; ++a) fa[p][a] = *reinterpret_cast<const bf16x8*>(st + offa[p][a][0]);
+#pragma unroll
+      for (int b = 0; b < NB; ++b) fb[p][b] = *reinterpret_cast<const bf16x8*>(st + offb[p][b][0]);
+    }
+#pragma unroll
+    for (int q = 0; q < NP; ++q) {
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+          if constexpr (EPI == 7) {
+            // TIMING EXPERIMENT ONLY (wrong results): two 16x16x32 MFMAs in place of one
+            // 32x32x16 -- same pipe cycles, different DVFS behaviour
+            typedef float f32x4e __attribute__((ext_vector_type(4)));
+            f32x4e lo = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
+            f32x4e hi = {acc[a][b][4], acc[a][b][5], acc[a][b][6], acc[a][b][7]};
+            lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[PairsNT<NP>::a[q]][a], fb[PairsNT<NP>::b[q]][b], lo, 0, 0, 0);
+            hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[PairsNT<NP>::b[q]][b], fa[PairsNT<NP>::a[q]][a], hi, 0, 0, 0);
+            acc[a][b][0] = lo[0]; acc[a][b][1] = lo[1]; acc[a][b][2] = lo[2]; acc[a][b][3] = lo[3];
+            acc[a][b][4] = hi[0]; acc[a][b][5] = hi[1]; acc[a][b][6] = hi[2]; acc[a][b][7] = hi[3];
+          } else {
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[PairsNT<NP>::a[q]][a], fb[PairsNT<NP>::b[q]][b],
+                                                                acc[a][b], 0, 0, 0);
+          }
+        }
+      if (dit >= 0) {
+        // pieces j = q (and the leftovers after the last pass)
+#pragma unroll
+        for (int j = q; j < JHI; j += NP) {
+          if (j < JLO || j < cnt) {
+            __builtin_amdgcn_sched_barrier(0);
+            dma_one(dit, dbuf, j);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+    }
+  };
+
+  if constexpr (PIPE == 3) {
+    static_assert(BK == 16 && NBUF == 3, "interleaved-DMA variant: 16-deep stages, 3 buffers");
+    dma(0, 0);
+    if (nit > 1) {
+      dma(1, 1);
+      wait_stage();
+    } else {
+      dma_wait<0>();
+    }
+    __syncthreads();
+    int cur = 0;
+    for (int it = 0; it < nit; ++it) {
+      const int nxt2 = cur == 0 ? 2 : cur - 1;
+      mma_dma(cur, it + 2 < nit ? it + 2 : -1, nxt2);
+      if (it + 2 < nit) wait_stage();
+      else dma_wait<0>();
+      __syncthreads();
+      cur = cur == 2 ? 0 : cur + 1;
+    }
+  } else if constexpr (PIPE == 1) {
     // Fragments of the stage being multiplied live in registers (two named sets, loop
     // unrolled by 2), so three stages can be in flight in three LDS buffers and the LDS
     // reads of stage it + 1 overlap the second MFMA group of stage it:
@@ -288,11 +400,10 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_piece_k(Args 
       for (int p = 0; p < NPC; ++p) {
 #pragma unroll
         for (int a = 0; a < MB; ++a)
-          F[p][a] = *reinterpret_cast<const bf16x8*>(st + p * A_BYTES + Img<BK>::off(wm * WM + 32 * a + l32, h));
+          F[p][a] = *reinterpret_cast<const bf16x8*>(st + offa[p][a][0]);
 #pragma unroll
         for (int b = 0; b < NB; ++b)
-          F[p][MB + b] = *reinterpret_cast<const bf16x8*>(st + NPC * A_BYTES + p * B_BYTES +
-                                                         Img<BK>::off(wn * WN + 32 * b + l32, h));
+          F[p][MB + b] = *reinterpret_cast<const bf16x8*>(st + offb[p][b][0]);
       }
     };
     // pass q of the product (PairsNT order); group 1 = the first half of the passes
@@ -356,14 +467,13 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_piece_k(Args 
       const char* st = lds + buf * STAGE;
 #pragma unroll
       for (int a = 0; a < MB; ++a)
-        fa[p][a] = *reinterpret_cast<const bf16x8*>(st + p * A_BYTES + Img<BK>::off(wm * WM + 32 * a + l32, h));
+        fa[p][a] = *reinterpret_cast<const bf16x8*>(st + offa[p][a][0]);
     };
     auto rdb = [&](int buf, int p) {
       const char* st = lds + buf * STAGE;
 #pragma unroll
       for (int b = 0; b < NB; ++b)
-        fb[p][b] = *reinterpret_cast<const bf16x8*>(st + 3 * A_BYTES + p * B_BYTES +
-                                                    Img<BK>::off(wn * WN + 32 * b + l32, h));
+        fb[p][b] = *reinterpret_cast<const bf16x8*>(st + offb[p][b][0]);
     };
     auto pass = [&](int pa, int pb) {
 #pragma unroll
@@ -507,7 +617,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_piece_k(Args 
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[a][b][4 * gq + i] = v[i];
   };
-  if constexpr (EPI == 0 || EPI == 3) {
+  if constexpr (EPI == 0 || EPI == 3 || EPI == 7) {
     // EPI 3 = EPI 0 with beta: one row block of accumulators at a time (a sched barrier keeps
     // the compiler from hoisting every block's C loads: 256-VGPR cap)
 #pragma unroll
@@ -635,7 +745,7 @@ int cfg_bm(int) { return 256; }
 int cfg_bn(int c) { return (c == 0 || c == 3) ? 192 : (c == 1 || c == 5) ? 256 : 128; }
 int cfg_nwm(int c) { return (c == 1 || c == 5) ? 2 : 4; }
 
-template <int BM, int BN, int WM, int WN, int NPC, int NP, int BK, int NBUF, int EPI, int PIPE = 0>
+template <int BM, int BN, int WM, int WN, int NPC, int NP, int BK, int NBUF, int EPI, int PIPE = 0, int LAY = 0>
 void launch_one(const Args& a, hipStream_t s) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int total = ((a.M + BM - 1) / BM) * (a.N / BN);
@@ -643,16 +753,49 @@ void launch_one(const Args& a, hipStream_t s) {
   const size_t smem = (size_t)NBUF * NPC * (BM + BN) * BK * 2;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_piece_k<BM, BN, WM, WN, NPC, NP, BK, NBUF, EPI, PIPE>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_piece_k<BM, BN, WM, WN, NPC, NP, BK, NBUF, EPI, PIPE, LAY>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
-  gemm_piece_k<BM, BN, WM, WN, NPC, NP, BK, NBUF, EPI, PIPE><<<8 * per, NT, smem, s>>>(a);
+  gemm_piece_k<BM, BN, WM, WN, NPC, NP, BK, NBUF, EPI, PIPE, LAY><<<8 * per, NT, smem, s>>>(a);
+}
+
+static int pipe_mode() {
+  static const int p = getenv("HX_GEMM_PIPE") ? atoi(getenv("HX_GEMM_PIPE")) : 3;
+  return p;
+}
+
+template <int NPC, int NP, int EPI, int PIPE, int LAY>
+void launch_lay(int cfg, const Args& a, hipStream_t s) {
+  if (cfg == 0)
+    launch_one<256, 192, 64, 96, NPC, NP, 16, 3, EPI, PIPE, LAY>(a, s);
+  else
+    launch_one<256, 256, 128, 64, NPC, NP, 16, 3, EPI, PIPE, LAY>(a, s);
 }
 
 template <int NPC, int NP, int EPI>
-void launch_cfg(int cfg, const Args& a, hipStream_t s) {
+void launch_cfg(int cfg, int lay, const Args& a, hipStream_t s) {
   constexpr int BK = NPC == 3 ? 16 : 32, NBUF = NPC == 3 ? 3 : 2;
+  if constexpr (NPC == 3) {
+    if (pipe_mode() == 3 && (cfg == 0 || cfg == 1)) {   // DMA pieces interleaved with the MFMA passes
+      if (lay == 0) launch_lay<NPC, NP, EPI, 3, 0>(cfg, a, s);
+      else if (lay == 1) launch_lay<NPC, NP, EPI, 3, 1>(cfg, a, s);
+      else if (lay == 2) launch_lay<NPC, NP, EPI, 3, 2>(cfg, a, s);
+      else launch_lay<NPC, NP, EPI, 3, 3>(cfg, a, s);
+      return;
+    }
+    if (lay) {   // B16 piece layout(s), plain pipeline
+      if (cfg == 3 || cfg == 5) {   // lay == 3 (host check)
+        if (cfg == 3) launch_one<256, 192, 64, 96, NPC, NP, 16, 3, EPI, 2, 3>(a, s);
+        else launch_one<256, 256, 128, 64, NPC, NP, 16, 3, EPI, 2, 3>(a, s);
+        return;
+      }
+      if (lay == 1) launch_lay<NPC, NP, EPI, 0, 1>(cfg, a, s);
+      else if (lay == 2) launch_lay<NPC, NP, EPI, 0, 2>(cfg, a, s);
+      else launch_lay<NPC, NP, EPI, 0, 3>(cfg, a, s);
+      return;
+    }
+  }
   if (cfg == 0)
     launch_one<256, 192, 64, 96, NPC, NP, BK, NBUF, EPI>(a, s);
   else if (cfg == 1)
@@ -675,22 +818,34 @@ void launch_cfg(int cfg, const Args& a, hipStream_t s) {
 
 }  // namespace
 
-int hx_gemm_split_plan(int M, int N, int K, int passes) {
+int hx_gemm_split_plan(int M, int N, int K, int passes, int lay) {
   (void)K;
   (void)M;
   if (const char* e = getenv("HX_GEMM_CFG")) {
     const int c = atoi(e);
-    if (c >= 0 && c < kCfgs && c != 8 && N % cfg_bn(c) == 0 && (c < 3 || passes == 6)) return c;
+    if (c >= 0 && c < kCfgs && c != 8 && N % cfg_bn(c) == 0 && (c < 3 || passes == 6) &&
+        (!lay || c == 0 || c == 1 || ((c == 3 || c == 5) && lay == 3)))
+      return c;
   }
   // measured at M = 16384, bf16x6 (tools/probe/gemm_layout_probe.py, profiles/r3_gemm_split.md):
-  // N = 768 on the 256 x 192 tile (one round of 256 workgroups), N = 2304 on 256 x 128, wide
-  // outputs (3072, the decoder's vocabulary) on 256 x 256
+  // N = 768 on the 256 x 192 tile (one round of 256 workgroups), N = 2304 on 256 x 128 (natural
+  // layouts) or 256 x 192 (B16), wide outputs (3072, the decoder's vocabulary) on 256 x 256
   if (N % 192 == 0 && N <= 1536) return 0;
-  if (N % 2304 == 0) return 2;
+  if (N % 2304 == 0) return lay ? 0 : 2;
   if (N % 256 == 0) return 1;
   if (N % 192 == 0) return 0;
-  if (N % 128 == 0) return 2;
+  if (N % 128 == 0 && !lay) return 2;
   return -1;
+}
+
+// should the B operand (weight pieces) of an N-column product be written in the B16 layout?
+// bf16x6 on the 256 x 192 / 256 x 256 tiles: 3-9 % faster (tools/probe/gemm_layout_probe.py);
+// N = 2304 stays natural on the 256 x 128 tile, which is faster there.  HX_W_B16=0 turns it off.
+int hx_gemm_split_weight_b16(int N, int passes) {
+  static const bool on = !(getenv("HX_W_B16") && getenv("HX_W_B16")[0] == '0');
+  if (!on || passes != 6 || N % 2304 == 0) return 0;
+  const int c = hx_gemm_split_plan(1 << 14, N, 768, passes, 2);
+  return (c == 0 || c == 1) ? 1 : 0;
 }
 
 int hx_gemm_split_colpart_rows(int M, int cfg) {
@@ -700,15 +855,15 @@ int hx_gemm_split_colpart_rows(int M, int cfg) {
 
 int hx_gemm_split_nt(const void* A, int64_t lda, int64_t a_ps, const void* B, int64_t ldb, int64_t b_ps, float* C,
                      int64_t ldc, int M, int N, int K, int passes, int beta, const HxGemmEpi* epi, int cfg,
-                     hipStream_t s, int kblock) {
+                     hipStream_t s, int lay) {
   const int npc = passes == 6 ? 3 : passes == 3 ? 2 : 0;
   if (!npc || M < 1 || cfg < 0 || cfg >= kCfgs || N % cfg_bn(cfg)) return -1;
   if (cfg >= 3 && npc != 3) return -1;
   const int bk = (npc == 3 && cfg != 2) ? 16 : 32;
   if (K % bk || npc * a_ps > lda || npc * b_ps > ldb) return -1;
-  // kblock: operands stored [rows][K / kblock][npc][kblock] (piece stride kblock) instead of
-  // [rows][npc][K]: one BK-deep k step of a row is then npc * BK contiguous elements
-  if (kblock && (kblock != bk || a_ps != kblock || b_ps != kblock)) return -1;
+  // lay bit 0 / bit 1: A / B operand in the B16 layout [rows][K / 16][3][16] (bf16x6, cfgs 0 1 3 5)
+  // instead of [rows][npc][K]: one 16-deep k step of a row is 96 contiguous bytes
+  if (lay && (lay > 3 || npc != 3 || !(cfg == 0 || cfg == 1 || ((cfg == 3 || cfg == 5) && lay == 3)))) return -1;
   Args a;
   a.A = (const uint16_t*)A;
   a.lda = lda;
@@ -730,17 +885,19 @@ int hx_gemm_split_nt(const void* A, int64_t lda, int64_t a_ps, const void* B, in
   a.ldp = epi ? epi->ldp : 0;
   a.p_ps = epi ? epi->p_ps : 0;
   a.colpart = epi ? epi->colpart : nullptr;
-  a.ksa = a.ksb = (uint32_t)(bk * 2 * (kblock ? npc : 1));
+  a.ksa = (uint32_t)(bk * 2 * ((lay & 1) ? npc : 1));
+  a.ksb = (uint32_t)(bk * 2 * ((lay & 2) ? npc : 1));
   a.stamps = nullptr;
   if (kind == 1 && (!a.P || beta)) return -1;
   if (kind == 2 && (!a.P || !a.aux)) return -1;
-  if (kind < 0 || kind > 2) return -1;
+  if ((kind < 0 || kind > 2) && kind != 7) return -1;
 #define HX_GS(NPC_, NP_)                                          \
   do {                                                            \
-    if (kind == 0 && !beta) launch_cfg<NPC_, NP_, 0>(cfg, a, s);  \
-    else if (kind == 0) launch_cfg<NPC_, NP_, 3>(cfg, a, s);      \
-    else if (kind == 1) launch_cfg<NPC_, NP_, 1>(cfg, a, s);      \
-    else launch_cfg<NPC_, NP_, 2>(cfg, a, s);                     \
+    if (kind == 7) launch_one<256, 192, 64, 96, 3, 6, 16, 3, 7, 3, 0>(a, s); \
+    else if (kind == 0 && !beta) launch_cfg<NPC_, NP_, 0>(cfg, lay, a, s);  \
+    else if (kind == 0) launch_cfg<NPC_, NP_, 3>(cfg, lay, a, s);      \
+    else if (kind == 1) launch_cfg<NPC_, NP_, 1>(cfg, lay, a, s);      \
+    else launch_cfg<NPC_, NP_, 2>(cfg, lay, a, s);                     \
   } while (0)
   if (passes == 6) HX_GS(3, 6);
   else HX_GS(2, 3);
@@ -755,7 +912,7 @@ void hx_fold_cols(const float* partial, int rows, int N, float* out, int accumul
 // diagnostic: cfg 0's kernel (EPI 0) with per-phase s_memtime stamps, one record of 5 counters per
 // wave (grid 8 * ceil(tiles / 8) workgroups x 8 waves); returns the grid size
 int hx_gemm_split_stamps(const void* A, const void* B, float* C, int M, int N, int K, unsigned long long* stamps,
-                         hipStream_t s) {
+                         hipStream_t s, int lay) {
   if (N % 192 || K % 16) return -1;
   Args a{};
   a.A = (const uint16_t*)A;
@@ -769,18 +926,22 @@ int hx_gemm_split_stamps(const void* A, const void* B, float* C, int M, int N, i
   a.M = M;
   a.N = N;
   a.K = K;
-  a.ksa = a.ksb = 32;
+  a.ksa = a.ksb = lay ? 96 : 32;
   a.stamps = stamps;
-  launch_one<256, 192, 64, 96, 3, 6, 16, 3, 0, 9>(a, s);
+  if (lay)
+    launch_one<256, 192, 64, 96, 3, 6, 16, 3, 0, 9, 1>(a, s);
+  else
+    launch_one<256, 192, 64, 96, 3, 6, 16, 3, 0, 9>(a, s);
   const int total = ((M + 255) / 256) * (N / 192);
   return 8 * ((total + 7) / 8);
 }
 
 // ---------------------------------------------------------------- diagnostic: LDS-DMA shape probe
 // Every workgroup (8 waves) streams `iters` stages of 42 one-KiB LDS-DMA pieces (the 256 x 192
-// bf16x6 stage) from a large buffer into a 3-stage LDS ring, with the GEMM's counted waits and
-// barriers but no MFMA.  seg = bytes of each contiguous source segment per instruction
-// (1024: a contiguous KiB; 64: 16 rows x 64 B; 32: 32 rows x 32 B; rows `ld` bytes apart).
+// bf16x6 stage) into a 3-stage LDS ring, with the GEMM's counted waits and barriers but no MFMA.
+// Each piece reads seg-byte contiguous segments from 1024 / seg consecutive rows of a shared
+// 1344-row x `ld`-byte region (8.3 MB at ld 6144: Infinity-Cache resident); every shape sweeps the
+// same region band by band, so only the per-instruction segment shape differs.
 namespace {
 __global__ __launch_bounds__(512) void dma_probe_k(const uint16_t* src, uint32_t bytes, int seg, int ld, int iters) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -789,15 +950,17 @@ __global__ __launch_bounds__(512) void dma_probe_k(const uint16_t* src, uint32_t
   const int wv = __builtin_amdgcn_readfirstlane(w);
   const u32x4 rs = rsrc_of(src, bytes);
   const uint32_t lds0 = (uint32_t)(size_t)(lds_void*)lds;
-  // per-lane source byte offset inside a piece: lane L -> segment L*16/seg, byte L*16 % seg
+  const int R = 1024 / seg, csteps = ld / seg;
   const uint32_t lofs = (uint32_t)((lane * 16 / seg) * ld + (lane * 16) % seg);
-  const uint32_t wg0 = (uint32_t)blockIdx.x * 1024u * 1024u;   // 1 MiB of source per workgroup
   const int cnt = (PTOT - wv + NW - 1) / NW;
   auto dma = [&](int it, int buf) {
+    const int itw = it + (int)blockIdx.x;   // workgroups at different points of the sweep
+    const int band = (itw / csteps) % (1344 / (PTOT * R));
+    const uint32_t col = (uint32_t)(itw % csteps) * seg;
     for (int j = 0; j < 6; ++j) {
       const int q = wv + NW * j;
       if (q < PTOT) {
-        const uint32_t so = (wg0 + (uint32_t)((it * PTOT + q) % 512) * 2048u) % (bytes - 65536u);
+        const uint32_t so = (uint32_t)((band * PTOT + q) * R) * ld + col;
         dma16(rs, lds0 + buf * STAGE + 1024 * q, so + lofs);
       }
     }
@@ -827,5 +990,6 @@ void hx_dma_probe(const void* src, uint32_t bytes, int seg, int ld, int iters, i
                               3 * 42 * 1024);
     attr = true;
   }
+  if ((uint64_t)1344 * ld > bytes) return;
   dma_probe_k<<<grid, 512, 3 * 42 * 1024, s>>>((const uint16_t*)src, bytes, seg, ld, iters);
 }

@@ -143,7 +143,16 @@ __global__ __launch_bounds__(256) void split_planes_pad8_k(const float* __restri
 //   wf[n][p][k] = piece p of W[n][k]   (forward: B operand of y = x W^T)
 //   wt[k][p][n] = piece p of W[n][k]   (data gradient: B operand of dx = dy W = dy (W^T)^T)
 // 64 x 64 tiles: coalesced float4 reads, wf written directly, wt through an LDS transpose.
-template <int NPC>
+// BF / BT: wf / wt in the B16 layout (gemm_split.hip).
+//
+// element offset of (row, piece p, column c) in a [rows][NPC * C] pieces matrix: natural
+// [rows][NPC][C], or the B16 layout [rows][C / 16][NPC][16] (gemm_split.hip)
+template <int NPC, bool B16>
+__device__ __forceinline__ int64_t pc_off(int64_t row, int p, int c, int C) {
+  return B16 ? row * NPC * C + (c >> 4) * (16 * NPC) + p * 16 + (c & 15) : (row * NPC + p) * C + c;
+}
+
+template <int NPC, bool BF, bool BT>
 __global__ __launch_bounds__(256) void split_weight_k(const float* __restrict__ W, int N, int K,
                                                      uint16_t* __restrict__ wf, uint16_t* __restrict__ wt) {
   __shared__ uint16_t tile[NPC][64][66];
@@ -164,7 +173,7 @@ __global__ __launch_bounds__(256) void split_weight_k(const float* __restrict__ 
         tile[p][r][c4 + j] = q[j];
       }
       uint2 packed = make_uint2(q[0] | ((uint32_t)q[1] << 16), q[2] | ((uint32_t)q[3] << 16));
-      *reinterpret_cast<uint2*>(wf + ((int64_t)(n0 + r) * NPC + p) * K + k0 + c4) = packed;
+      *reinterpret_cast<uint2*>(wf + pc_off<NPC, BF>(n0 + r, p, k0 + c4, K)) = packed;
     }
   }
   __syncthreads();
@@ -177,7 +186,7 @@ __global__ __launch_bounds__(256) void split_weight_k(const float* __restrict__ 
 #pragma unroll
       for (int j = 0; j < 4; ++j) q[j] = tile[p][c4 + j][kk];
       uint2 packed = make_uint2(q[0] | ((uint32_t)q[1] << 16), q[2] | ((uint32_t)q[3] << 16));
-      *reinterpret_cast<uint2*>(wt + ((int64_t)(k0 + kk) * NPC + p) * N + n0 + c4) = packed;
+      *reinterpret_cast<uint2*>(wt + pc_off<NPC, BT>(k0 + kk, p, n0 + c4, N)) = packed;
     }
   }
 }
@@ -274,10 +283,14 @@ void hx_split_planes(const float* x, int64_t ldx, uint16_t* out, int64_t R, int 
     split_planes_any_k<2><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, Rp, Dp, npl, order, stacked);
 }
 
-void hx_split_weight(const float* W, int N, int K, int npieces, uint16_t* wf, uint16_t* wt, hipStream_t s) {
+void hx_split_weight(const float* W, int N, int K, int npieces, uint16_t* wf, uint16_t* wt, hipStream_t s, int b16) {
   dim3 g(K / 64, N / 64);
-  if (npieces == 3)
-    split_weight_k<3><<<g, 256, 0, s>>>(W, N, K, wf, wt);
-  else
-    split_weight_k<2><<<g, 256, 0, s>>>(W, N, K, wf, wt);
+  if (npieces == 3) {
+    if (b16 == 3) split_weight_k<3, true, true><<<g, 256, 0, s>>>(W, N, K, wf, wt);
+    else if (b16 == 1) split_weight_k<3, true, false><<<g, 256, 0, s>>>(W, N, K, wf, wt);
+    else if (b16 == 2) split_weight_k<3, false, true><<<g, 256, 0, s>>>(W, N, K, wf, wt);
+    else split_weight_k<3, false, false><<<g, 256, 0, s>>>(W, N, K, wf, wt);
+  } else {
+    split_weight_k<2, false, false><<<g, 256, 0, s>>>(W, N, K, wf, wt);
+  }
 }

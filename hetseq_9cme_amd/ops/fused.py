@@ -552,7 +552,7 @@ class _FFNSplitFn(torch.autograd.Function):
             # backward, gelu(u) written as the FFN-down GEMM's pieces): bert_modeling.py:166-168
             xs = split_gemm.pieces(x2)
             w1f, w1t = split_gemm.weight_pieces(W1)
-            u, hs = C().gemm_split_gelu(xs, w1f, split_gemm.passes(), b1)
+            u, hs = split_gemm.gemm_gelu(xs, w1f, b1)
             w2f, w2t = split_gemm.weight_pieces(W2)
             y2 = split_gemm.gemm(hs, w2f)
             ctx.save_for_backward(xs, u, hs, w1t, b1, w2t)
@@ -585,7 +585,7 @@ class _FFNSplitFn(torch.autograd.Function):
             dys = dys if dys is not None else split_gemm.pieces(dy2.float())
             # GELU backward in the FFN-down data-gradient epilogue: the pieces of
             # dh * gelu'(u) and the FFN-up bias gradient (u = y1 holds the bias already)
-            dy1s, db1 = C().gemm_split_dgelu(dys, w2, split_gemm.passes(), y1, None, grad_slot(b1))
+            dy1s, db1 = split_gemm.gemm_dgelu(dys, w2, y1, None, grad_slot(b1))
             dW2 = split_gemm.wgrad_pieces(dys, hs, W2.shape[0], W2.shape[1], grad_slot(W2))
             dx = _dgrad_pieces(dy1s, w1, ctx.xshape, ctx.mbox)
             dW1 = split_gemm.wgrad_pieces(dy1s, xs, W1.shape[0], W1.shape[1], grad_slot(W1))

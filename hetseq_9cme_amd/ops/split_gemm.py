@@ -222,14 +222,43 @@ def pieces(x2):
     return C().split_planes(x2, list(range(n)), n, False, 0, 0)
 
 
+_B16_CACHE = {}
+
+
+def b16(n):
+    """Are the weight pieces that form the B operand of an n-column product stored in the B16
+    layout [rows][K / 16][3][16] (csrc/kernels/gemm_split.hip, hx_gemm_split_weight_b16)?"""
+    key = (n, _State.passes)
+    v = _B16_CACHE.get(key)
+    if v is None:
+        v = _B16_CACHE[key] = bool(C().gemm_split_weight_b16(int(n), int(_State.passes)))
+    return v
+
+
 def weight_pieces(W):
-    """(wf [N, npc * K], wt [K, npc * N]): pieces of W [N, K] and of W^T, one pass."""
-    return C().split_weight(W.contiguous(), npieces())
+    """(wf [N, npc * K], wt [K, npc * N]): pieces of W [N, K] and of W^T, one pass; each in the
+    layout its GEMM reads (``b16``: wf is the B operand of the N-column forward, wt of the
+    K-column data gradient)."""
+    N, K = W.shape
+    mask = (1 if b16(N) else 0) | (2 if b16(K) else 0)
+    return C().split_weight(W.contiguous(), npieces(), mask)
 
 
 def gemm(a, b, out=None, beta=False):
-    """out (+)= sum over piece pairs of a_p . b_q^T, fp32 [M, N]."""
-    return C().gemm_split(a, b, _State.passes, out, beta)
+    """out (+)= sum over piece pairs of a_p . b_q^T, fp32 [M, N] (b = weight pieces from
+    ``weight_pieces``, in the layout ``b16(N)`` says)."""
+    return C().gemm_split(a, b, _State.passes, out, beta, 2 if b16(b.shape[0]) else 0)
+
+
+def gemm_gelu(a, b, bias):
+    """(u = a . b^T + bias, pieces of gelu(u)): the FFN-up GEMM with its GELU epilogue."""
+    return C().gemm_split_gelu(a, b, _State.passes, bias, 2 if b16(b.shape[0]) else 0)
+
+
+def gemm_dgelu(a, b, u, bias, dbias_out):
+    """(pieces of (a . b^T) * gelu'(u (+ bias)), d bias): the FFN-down data gradient with the
+    GELU backward epilogue."""
+    return C().gemm_split_dgelu(a, b, _State.passes, u, bias, dbias_out, 2 if b16(b.shape[0]) else 0)
 
 
 def dgrad_pieces(dys, wt, acc=None):

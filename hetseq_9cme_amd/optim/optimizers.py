@@ -141,6 +141,12 @@ class _Optimizer(object):
     # exactly that list (hetseq/controller.py:92-96).  The flat layout orders
     # parameters differently (reverse blocks, fused groups), so state is emitted and
     # consumed through ``flat.model_order`` (position -> flat index).
+    # ``param_order`` tags the layout: 'model' (this format; also what a torch optimizer over
+    # model.parameters() -- the reference's -- writes, untagged).  Round-1 files of this framework
+    # were numbered by FLAT index and carry no tag: the checkpoint loader recognises them by their
+    # framework-specific args and passes ``legacy_flat_order=True`` (see Controller.load_checkpoint).
+    STATE_ORDER = 'model'
+
     def state_dict(self):
         state = {}
         for pos, i in enumerate(self.flat.model_order):
@@ -152,9 +158,14 @@ class _Optimizer(object):
             gg = {k: v for k, v in g.items()}
             gg['params'] = list(range(len(self.flat.params)))
             groups.append(gg)
-        return {'state': state, 'param_groups': groups}
+        return {'state': state, 'param_groups': groups, 'param_order': self.STATE_ORDER}
 
-    def load_state_dict(self, state_dict, optimizer_overrides=None):
+    def load_state_dict(self, state_dict, optimizer_overrides=None, legacy_flat_order=False):
+        """``legacy_flat_order``: the state is numbered by flat index (an untagged file written
+        by this framework before the state-order tag existed) and is remapped accordingly."""
+        order = state_dict.get('param_order', 'flat' if legacy_flat_order else 'model')
+        if order not in ('model', 'flat'):
+            raise ValueError('unknown optimizer state order {!r}'.format(order))
         groups = state_dict['param_groups']
         saved = groups[0]
         for k, v in saved.items():
@@ -168,7 +179,7 @@ class _Optimizer(object):
             raise ValueError('loaded state dict has a different number of parameters')
         for idx, s in state_dict['state'].items():
             pos = saved_ids.index(idx) if idx in saved_ids else int(idx)
-            i = self.flat.model_order[pos]
+            i = pos if order == 'flat' else self.flat.model_order[pos]
             shape = self.flat.params[i].shape
             for k, v in s.items():
                 if torch.is_tensor(v) and v.dim() > 0 and v.numel() != shape.numel():

@@ -182,7 +182,12 @@ def add_distributed_training_args(parser):
     group.add_argument('--ddp-backend', default='c10d', type=str, choices=['c10d'],
                        help='gradient reducer backend (kept for flag compatibility)')
     group.add_argument('--bucket-cap-mb', default=25, type=int, metavar='MB',
-                       help='gradient all-reduce bucket size')
+                       help='gradient all-reduce bucket size (upper bound; see --bucket-peer-mb)')
+    group.add_argument('--bucket-peer-mb', default=3.0, type=float, metavar='MB',
+                       help='MI355X: target bytes per peer chunk of a bucket -- buckets are sized '
+                            'min(--bucket-cap-mb, max(2, W) x this), so every one of the W ranks\' '
+                            'chunks keeps the 7 xGMI links busy while small worlds still overlap early '
+                            '(0 = --bucket-cap-mb alone)')
     group.add_argument('--allreduce-impl', default='rccl', choices=['rccl', 'xgmi'],
                        help='gradient all-reduce transport: RCCL, or the hand-written intra-node two-shot '
                             'xGMI kernel over IPC-mapped peer buffers (single host only; falls back to RCCL)')

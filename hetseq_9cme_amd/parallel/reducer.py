@@ -51,11 +51,24 @@ import torch.distributed as dist
 from ..ops._ext import C
 
 
-def plan_buckets(flat, bucket_cap_mb):
+def bucket_cap_for(world, bucket_cap_mb, peer_mb=3.0):
+    """Bucket size (MB) for a world of W ranks: each of the W chunks of a bucket (the two-shot
+    kernel's per-peer share; RCCL's ring/tree pieces alike) about ``peer_mb``, bounded by the
+    reference's ``--bucket-cap-mb`` (hetseq/options.py:215-216): W = 8 -> 24 MB (3 MB per peer
+    over 7 concurrent xGMI links), W = 3 -> 9 MB, W = 5 -> 15 MB."""
+    if not peer_mb or peer_mb <= 0 or world < 2:
+        return bucket_cap_mb
+    return min(float(bucket_cap_mb), peer_mb * max(2, world))
+
+
+def plan_buckets(flat, bucket_cap_mb, world=1, peer_mb=0.0):
     """Contiguous buckets over the flat layout (params already reverse-ordered):
-    [(start, end, [param idx])], ends extended to the next bucket's start."""
+    [(start, end, [param idx])], ends extended to the next bucket's start.  Bucket starts fall
+    on parameter starts (64-element = 256-B boundaries in the flat layout), and the transports
+    cut a bucket into W chunks rounded up to 64 elements, so every per-peer chunk is 256-B
+    aligned for any W (3, 5, ...)."""
     elem = flat.grad_flat.element_size()
-    cap = max(1, int(bucket_cap_mb * 1024 * 1024 / elem))
+    cap = max(1, int(bucket_cap_for(world, bucket_cap_mb, peer_mb) * 1024 * 1024 / elem))
     buckets = []
     cur, cur_start = [], 0
     for i in range(len(flat.params)):
@@ -76,13 +89,13 @@ def plan_buckets(flat, bucket_cap_mb):
 
 class GradReducer(object):
     def __init__(self, flat, bucket_cap_mb=25, process_group=None, find_unused_parameters=False,
-                 broadcast_params=True):
+                 broadcast_params=True, bucket_peer_mb=0.0):
         self.flat = flat
         self.group = process_group
         self.world_size = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.find_unused = find_unused_parameters
         self.grad_prescale = 1.0 / self.world_size
-        self.buckets = plan_buckets(flat, bucket_cap_mb)
+        self.buckets = plan_buckets(flat, bucket_cap_mb, self.world_size, bucket_peer_mb)
         self.bucket_of = {}
         for b, (_, _, idxs) in enumerate(self.buckets):
             for i in idxs:
@@ -132,8 +145,9 @@ class GradReducer(object):
         if not ok:
             warnings.warn('--allreduce-impl xgmi unavailable ({}); using RCCL'.format(why))
             return False
-        cap_mb = max(b[1] - b[0] for b in self.buckets) * 4 / 2 ** 20
-        self.xgmi = XgmiAllReduce(self.group, cap_mb=min(max(cap_mb, 1), 128), blocks=blocks, timeout_s=timeout_s)
+        # buckets are slices of the flat gradient buffer: it is registered once and every bucket
+        # is reduced in place over the peers' mappings of it (no staging copy)
+        self.xgmi = XgmiAllReduce(self.flat.grad_flat, self.group, blocks=blocks, timeout_s=timeout_s)
         self._native.use_xgmi(self.xgmi.h, self.xgmi.stream.cuda_stream)
         return True
 

@@ -1,18 +1,25 @@
 """Intra-node xGMI all-reduce transport for the gradient reducer.
 
 ``--allreduce-impl xgmi`` replaces RCCL for the per-bucket gradient all-reduce
- with the two-shot kernel of
-``csrc/kernels/xgmi_allreduce.hip``: every rank exports one staging buffer and
-one uncached signal page through HIP IPC, maps its peers' (exchanged with
-``all_gather_object`` over the existing process group, which plays the role of
-the reference's TCP/file store, hetseq/distributed_utils.py:20-25), and each
-bucket is reduced by pulling chunk r from all W peers at once (all 7 xGMI links
-busy) and gathering the other W-1 reduced chunks.
+ with the kernels of ``csrc/kernels/xgmi_allreduce.hip``:
+every rank registers its flat gradient buffer and exports it ONCE through HIP IPC
+together with an uncached signal page; the records are exchanged with
+``all_gather_object`` over the existing process group (the role of the reference's
+TCP/file store, hetseq/distributed_utils.py:20-25).  Each bucket -- a slice of that
+buffer on every rank -- is then reduced IN PLACE:
 
-It applies only when every rank of the group lives on one host and holds its
-own GPU with peer access to the others (or, for tests, when ranks share one
-GPU); otherwise the reducer stays on RCCL (multi-node, CPU/gloo).  RCCL also
-keeps the one-off parameter broadcast and the small stats all-reduce.
+* two-shot (large buckets): rank r pulls chunk r of every peer's bucket at once (all 7
+  xGMI links busy), sums in rank order into its own chunk, then gathers the other W-1
+  reduced chunks from their owners;
+* one-shot (buckets up to ``oneshot_kb``, latency-bound): every rank sums the whole bucket
+  over all peers in registers and stores it after one "done reading" hand-off.
+
+Eligibility is decided by PCI bus id, not by process-local device ordinals: every rank
+must sit on one host, on its own GPU (or share one, for tests), and see each peer's GPU
+(by bus id) with peer access.  A launch that partitions ``HIP_VISIBLE_DEVICES`` per
+"node" hides the peers and falls back to RCCL; ``tools/launch_hetero.py --device-offset``
+keeps every GPU visible for exactly this reason.  RCCL keeps the one-off parameter
+broadcast and the small stats all-reduce, and multi-node groups.
 
 Waits inside the kernel are bounded by ``timeout_s``; a wait that expires sets
 an error bit instead of hanging the GPU.  :meth:`error_async` copies that word
@@ -31,6 +38,33 @@ from ..ops._ext import C
 MAX_WORLD = 8
 
 
+def _visible_bus_ids():
+    return [C().device_pci_bus_id(d).lower() for d in range(torch.cuda.device_count())]
+
+
+def eligibility(infos, rank, can_access):
+    """Pure decision (unit-testable): ``infos[q]`` = (hostname, own bus id, tuple of the bus ids
+    visible to rank q in ordinal order); ``can_access(a, b)`` = peer access between local
+    ordinals a -> b of THIS rank.  Returns (ok, reason)."""
+    world = len(infos)
+    if world < 2 or world > MAX_WORLD:
+        return False, 'world size {} outside 2..{}'.format(world, MAX_WORLD)
+    if len({h for h, _, _ in infos}) != 1:
+        return False, 'ranks span several hosts (xGMI is intra-node)'
+    host, mine, visible = infos[rank]
+    me = visible.index(mine)
+    for q, (_, bus, _) in enumerate(infos):
+        if q == rank or bus == mine:
+            continue   # same GPU (tests share one device): plain device memory
+        if bus not in visible:
+            return False, ('rank {} runs on GPU {} which this process cannot see (HIP_VISIBLE_DEVICES '
+                           'partitions the node; launch with all GPUs visible, e.g. '
+                           'tools/launch_hetero.py --device-offset)').format(q, bus)
+        if not can_access(me, visible.index(bus)):
+            return False, 'no peer access from GPU {} to GPU {}'.format(mine, bus)
+    return True, ''
+
+
 def xgmi_eligible(group=None):
     """(ok, reason): can this process group use the xGMI transport?"""
     if not (dist.is_initialized() and torch.cuda.is_available()):
@@ -38,44 +72,43 @@ def xgmi_eligible(group=None):
     world = dist.get_world_size(group)
     if world < 2 or world > MAX_WORLD:
         return False, 'world size {} outside 2..{}'.format(world, MAX_WORLD)
-    dev = torch.cuda.current_device()
-    info = [None] * world
-    dist.all_gather_object(info, (socket.gethostname(), dev), group=group)
-    if len({h for h, _ in info}) != 1:
-        return False, 'ranks span several hosts (xGMI is intra-node)'
-    for _, d in info:
-        if d != dev and not torch.cuda.can_device_access_peer(dev, d):
-            return False, 'no peer access from GPU {} to GPU {}'.format(dev, d)
-    return True, ''
+    visible = tuple(_visible_bus_ids())
+    info = (socket.gethostname(), visible[torch.cuda.current_device()], visible)
+    infos = [None] * world
+    dist.all_gather_object(infos, info, group=group)
+    return eligibility(infos, dist.get_rank(group), torch.cuda.can_device_access_peer)
 
 
 class XgmiAllReduce(object):
-    """In-place SUM all-reduce of fp32 buckets over IPC-mapped peer buffers.
+    """In-place SUM all-reduce of slices of ``buffer`` (this rank's flat fp32 gradients) over
+    IPC-mapped peer buffers.
 
-    Collective: every rank must construct it and call :meth:`all_reduce_` with
-    buckets of identical sizes in identical order.
+    Collective: every rank must construct it with an equally sized buffer and call
+    :meth:`all_reduce_` with the same slices in the same order.
     """
 
-    def __init__(self, group=None, cap_mb=64, blocks=64, timeout_s=300.0):
+    def __init__(self, buffer, group=None, blocks=64, timeout_s=300.0, oneshot_kb=512):
         self.group = group
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
-        cap = int(cap_mb * 1024 * 1024 // 4)
-        self.h = C().xar_create(self.rank, self.world, cap, blocks, float(timeout_s))
-        handles = [None] * self.world
-        dist.all_gather_object(handles, C().xar_export(self.h), group=group)
-        C().xar_open(self.h, b''.join(handles))
+        self.buffer = buffer
+        self.h = C().xar_create(self.rank, self.world, blocks, float(timeout_s), int(oneshot_kb) * 1024)
+        C().xar_register(self.h, buffer)
+        recs = [None] * self.world
+        dist.all_gather_object(recs, C().xar_export(self.h), group=group)
+        C().xar_open(self.h, b''.join(recs))
         # every rank has mapped every peer before any kernel may touch a peer page
         torch.cuda.synchronize()
         dist.barrier(group=group)
         self.stream = torch.cuda.Stream(priority=-1)
 
     @property
-    def capacity(self):
-        return C().xar_capacity(self.h)
+    def oneshot_max(self):
+        """Largest bucket (floats) reduced by the one-shot kernel."""
+        return C().xar_oneshot_max(self.h)
 
     def all_reduce_(self, t):
-        """Reduce ``t`` (contiguous fp32 GPU tensor) on the CURRENT stream."""
+        """Reduce ``t`` (a contiguous slice of the registered buffer) on the CURRENT stream."""
         C().xar_allreduce(self.h, t)
         return t
 
@@ -104,13 +137,12 @@ class XgmiAllReduce(object):
             pass
 
 
-def simulate_all_reduce(bufs, blocks=64, timeout_s=20.0, mute=-1):
+def simulate_all_reduce(bufs, blocks=64, timeout_s=20.0, mute=-1, oneshot_kb=512):
     """Test helper: W simulated ranks in ONE grid on one GPU (no IPC); reduces the
     equal-size fp32 tensors ``bufs`` in place and returns the error word.
     ``mute`` = a simulated rank that never signals (the others' waits time out)."""
     W = len(bufs)
-    cap = max(64, bufs[0].numel())
-    hs = [C().xar_create(q, W, cap, blocks, float(timeout_s)) for q in range(W)]
+    hs = [C().xar_create(q, W, blocks, float(timeout_s), int(oneshot_kb) * 1024) for q in range(W)]
     try:
         C().xar_allreduce_sim(hs, list(bufs), int(mute))
         torch.cuda.synchronize()

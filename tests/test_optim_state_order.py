@@ -85,3 +85,47 @@ def test_mismatched_shapes_raise():
         assert 'shape' in str(e)
     else:
         raise AssertionError('mis-shaped optimizer state must not load')
+
+
+def _flat_ordered_state(opt):
+    """What this framework wrote before the state-order tag: state numbered by FLAT index."""
+    sd = opt.state_dict()
+    state = {}
+    for pos, i in enumerate(opt.flat.model_order):
+        if pos in sd['state']:
+            state[i] = sd['state'][pos]
+    return {'state': state, 'param_groups': sd['param_groups']}
+
+
+def test_state_order_tag_and_legacy_flat_files():
+    """state_dict() carries param_order='model'; an untagged flat-order state of this framework
+    (legacy_flat_order) is remapped onto the right tensors -- same-shaped Q/K/V weights and
+    LayerNorm vectors included -- instead of silently permuting Adam moments."""
+    model = _model()
+    flat = FlatParamSpace(model, contiguous_groups=model.flat_contiguous_groups())
+    opt = _Adam(_args(), flat)
+    g = torch.Generator().manual_seed(3)
+    opt.exp_avg.copy_(torch.randn(opt.exp_avg.shape, generator=g))
+    opt.exp_avg_sq.copy_(torch.rand(opt.exp_avg_sq.shape, generator=g))
+    opt.steps = [5] * len(flat.params)
+    sd = opt.state_dict()
+    assert sd['param_order'] == 'model'
+    legacy = _flat_ordered_state(opt)
+
+    def same(o):
+        for i in range(len(flat.params)):
+            s, e = flat.param_range(i)
+            if not (torch.equal(o.exp_avg[s:e], opt.exp_avg[s:e]) and torch.equal(o.exp_avg_sq[s:e], opt.exp_avg_sq[s:e])):
+                return False
+        return True
+    for state, kw in ((sd, {}), (legacy, {'legacy_flat_order': True})):
+        opt2 = _Adam(_args(), flat)
+        opt2.load_state_dict(state, **kw)
+        assert same(opt2)
+    # the untagged flat-order file read as model order scrambles same-shaped tensors
+    opt3 = _Adam(_args(), flat)
+    try:
+        opt3.load_state_dict(legacy)
+        assert not same(opt3)
+    except ValueError:
+        pass   # or a shape mismatch is caught

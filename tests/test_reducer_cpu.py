@@ -271,3 +271,61 @@ def test_native_reducer_overlap_order_and_no_sync():
     by_model = [ref[s:s + n] for s, n in zip(starts, sizes)]
     want = torch.cat([by_model[flat.model_order.index(k)] for k in range(len(flat.params))])
     assert torch.allclose(got, want, rtol=1e-5, atol=1e-6)
+
+
+def test_bucket_plan_tied_to_world_size():
+    """Bucket cap from W (--bucket-peer-mb): ~3 MB per peer chunk, capped by --bucket-cap-mb;
+    buckets tile the flat buffer contiguously from parameter starts (256-B aligned), so every
+    per-peer chunk of the transports (ceil(n / W) rounded to 64 elements) is 256-B aligned for
+    uneven worlds W = 3 and W = 5."""
+    from hetseq_9cme_amd.models.bert import BertConfig, BertForPreTraining
+    from hetseq_9cme_amd.parallel.flat_params import FlatParamSpace
+    from hetseq_9cme_amd.parallel.reducer import bucket_cap_for, plan_buckets
+    assert bucket_cap_for(8, 25, 3.0) == 24.0
+    assert bucket_cap_for(3, 25, 3.0) == 9.0 and bucket_cap_for(5, 25, 3.0) == 15.0
+    assert bucket_cap_for(2, 25, 3.0) == 6.0 and bucket_cap_for(16, 25, 3.0) == 25.0
+    assert bucket_cap_for(5, 25, 0.0) == 25
+    torch.manual_seed(0)
+    cfg = BertConfig(1000, hidden_size=256, num_hidden_layers=4, num_attention_heads=4, intermediate_size=1024)
+    model = BertForPreTraining(cfg)
+    flat = FlatParamSpace(model, contiguous_groups=model.flat_contiguous_groups())
+    for W in (3, 5):
+        bk = plan_buckets(flat, 25, W, 0.25)     # small per-peer target: several buckets
+        cap = int(bucket_cap_for(W, 25, 0.25) * 2 ** 20 / 4)
+        assert len(bk) > 1
+        assert bk[0][0] == 0 and bk[-1][1] == flat.numel
+        for b in range(len(bk)):
+            s, e, idx = bk[b]
+            assert s % 64 == 0
+            if b + 1 < len(bk):
+                assert e == bk[b + 1][0]
+            biggest = max(flat.param_range(i)[1] - flat.param_range(i)[0] for i in idx)
+            assert (e - s) <= cap or len(idx) == 1 or biggest > cap, (W, b, e - s, cap)
+            chunk = ((e - s + W - 1) // W + 63) // 64 * 64
+            assert all((s + q * chunk) % 64 == 0 for q in range(W))
+
+
+def test_xgmi_eligibility_by_bus_id():
+    """xGMI eligibility decided on PCI bus ids gathered per rank (mocked), not on process-local
+    ordinals: per-node HIP_VISIBLE_DEVICES partitions (ordinal 0 in every process) are
+    rejected with the reason, all-visible launches (--device-offset) accepted."""
+    from hetseq_9cme_amd.parallel.xgmi import eligibility
+    bus = ['0000:{:02x}:00.0'.format(0x10 * (i + 1)) for i in range(8)]
+    allv = tuple(bus)
+    yes = lambda a, b: True   # noqa: E731
+    # 5 + 3 "nodes" with every GPU visible, rank r on GPU r
+    infos = [('h', bus[r], allv) for r in range(8)]
+    assert eligibility(infos, 0, yes) == (True, '')
+    assert eligibility(infos, 7, yes)[0]
+    # the same split with HIP_VISIBLE_DEVICES partitions: rank 5 sees only GPUs 5..7
+    part = [('h', bus[r], allv[:5] if r < 5 else allv[5:]) for r in range(8)]
+    ok, why = eligibility(part, 5, yes)
+    assert not ok and 'cannot see' in why and '--device-offset' in why
+    # no peer access
+    ok, why = eligibility(infos, 2, lambda a, b: b != 6)
+    assert not ok and 'peer access' in why
+    # several hosts
+    ok, why = eligibility([('a', bus[0], allv), ('b', bus[1], allv)], 0, yes)
+    assert not ok and 'hosts' in why
+    # ranks sharing one GPU (the one-GPU tests) are fine
+    assert eligibility([('h', bus[0], (bus[0],))] * 3, 1, yes)[0]

@@ -1,12 +1,12 @@
-"""Hand-written two-shot all-reduce (csrc/kernels/xgmi_allreduce.hip).
+"""Hand-written in-place all-reduce (csrc/kernels/xgmi_allreduce.hip).
 
-* simulation: W ranks as ONE grid on one GPU (rank = blockIdx.y): chunking for uneven
-  W (3, 5, 7), tails that are not float4 multiples, buckets smaller than W float4s,
-  repeated calls (monotonic epochs), bitwise equality with the rank-order fp32 sum;
-* IPC: two or three processes (uneven W) on the box's GPU exchange staging/signal handles over a gloo
-  group and reduce buckets through the mapped peer memory (the multi-GPU protocol
-  minus the xGMI links themselves), including a bucket larger than the staging
-  capacity (split into pieces).
+* simulation: W ranks as ONE grid on one GPU (rank = blockIdx.y): one-shot (small buckets)
+  and two-shot kernels, chunking for uneven W (3, 5, 7), tails that are not float4
+  multiples, buckets smaller than W float4s, repeated calls (monotonic epochs), bitwise
+  equality with the rank-order fp32 sum;
+* IPC: two or three processes (uneven W) on the box's GPU register their "flat gradient"
+  buffers, exchange IPC records over a gloo group and reduce slices of them in place through
+  the mapped peer memory (the multi-GPU protocol minus the xGMI links themselves).
 Every kernel wait is bounded (timeouts -> error bits, never a spinning GPU).
 """
 import os
@@ -21,8 +21,12 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize('W,n', [(2, 4096), (3, 1000003), (5, 77), (7, 5), (8, 3 * 2 ** 20 + 12)])
-def test_xgmi_allreduce_simulated(dev, W, n):
+@pytest.mark.parametrize('W,n,oneshot_kb', [(2, 4096, 512), (3, 1000003, 512), (5, 77, 512), (7, 5, 512),
+                                            (8, 3 * 2 ** 20 + 12, 512), (5, 300001, 512), (7, 131071, 512),
+                                            (3, 4099, 0), (8, 40000, 0), (2, 200000, 1024)])
+def test_xgmi_allreduce_simulated(dev, W, n, oneshot_kb):
+    """oneshot_kb 0 forces the two-shot kernel on small buckets; 16 blocks x 256 threads x 16
+    floats = 64K floats is the one-shot limit of these grids."""
     from hetseq_9cme_amd.parallel.xgmi import simulate_all_reduce
     g = torch.Generator(device='cpu').manual_seed(W * 1000 + n % 997)
     for it in range(2):
@@ -31,7 +35,7 @@ def test_xgmi_allreduce_simulated(dev, W, n):
         for q in range(1, W):
             ref += src[q]
         bufs = [s.clone() for s in src]
-        err = simulate_all_reduce(bufs, blocks=16, timeout_s=20.0)
+        err = simulate_all_reduce(bufs, blocks=16, timeout_s=20.0, oneshot_kb=oneshot_kb)
         assert err == 0, 'kernel wait timed out (phase bits {:#x})'.format(err)
         for q in range(W):
             assert torch.equal(bufs[q], ref), (it, q, (bufs[q] - ref).abs().max().item())
@@ -44,7 +48,7 @@ def test_xgmi_timeout_sets_error_and_the_step_check_raises(dev):
     from hetseq_9cme_amd.ops._ext import C
     from hetseq_9cme_amd.parallel.reducer import TransportErrorMonitor
     W, n = 3, 4096
-    hs = [C().xar_create(q, W, n, 4, 0.05) for q in range(W)]
+    hs = [C().xar_create(q, W, 4, 0.05, 0) for q in range(W)]
     try:
         bufs = [torch.ones(n, device=dev) for _ in range(W)]
         C().xar_allreduce_sim(hs, bufs, 1)           # rank 1 muted
@@ -74,18 +78,26 @@ WORKER = textwrap.dedent('''
     dist.init_process_group('gloo', rank=rank, world_size=W)
     ok, why = xgmi_eligible()
     assert ok, why
-    xar = XgmiAllReduce(cap_mb=4, blocks=32, timeout_s=30.0)
-    for it, n in enumerate([7, 4096, 1000003, 3 * 2 ** 20 + 5]):   # the last one > 4 MB staging
+    sizes = [7, 4096, 1000003, 3 * 2 ** 20 + 5, 25 * 2 ** 18]
+    offs, o = [], 0
+    for n in sizes:              # the buckets: 16-B aligned slices of one registered buffer
+        offs.append(o)
+        o += (n + 63) // 64 * 64
+    flat = torch.zeros(o, device='cuda')
+    xar = XgmiAllReduce(flat, blocks=32, timeout_s=30.0)
+    for it, (n, o) in enumerate(zip(sizes[:4], offs[:4])):
         data = [torch.randn(n, generator=torch.Generator().manual_seed(100 * it + q)).cuda() for q in range(W)]
         ref = data[0].clone()
         for q in range(1, W):
             ref += data[q]          # the kernel's rank-order sum
-        buf = data[rank].clone()
+        buf = flat[o:o + n]
+        buf.copy_(data[rank])
         xar.all_reduce_(buf)
         torch.cuda.synchronize()
         xar.check()
         assert torch.equal(buf, ref), (n, (buf - ref).abs().max().item())
-    big = torch.ones(25 * 2 ** 18, device='cuda')     # one 25 MB bucket
+    big = flat[offs[4]:offs[4] + sizes[4]]       # one 25 MB bucket, in place
+    big.fill_(1.0)
     for _ in range(3):
         xar.all_reduce_(big)
     torch.cuda.synchronize()

@@ -12,11 +12,11 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 
 def main():
     from hetseq_9cme_amd.ops._ext import C
-    src = torch.randint(0, 1000, (256 * 1024 * 1024 // 2,), dtype=torch.int16, device='cuda')   # 256 MiB
+    src = torch.randint(0, 1000, (40 * 1024 * 1024 // 2,), dtype=torch.int16, device='cuda')   # 40 MiB
     iters = 400
-    for ld in (4608, 18432):
+    for ld in (6144, 24576):
         for seg in (1024, 128, 64, 32):
-            for grid in (256, 512):
+            for grid in (256,):
                 for _ in range(2):
                     C().dma_probe(src, seg, ld, iters, grid)
                 torch.cuda.synchronize()

@@ -1,6 +1,6 @@
-"""Piece layout probe for the LDS-DMA piece GEMM (gemm_split.hip): natural pieces
-[rows][npc][K] vs k-blocked [rows][K/BK][npc][BK] (one BK-deep k step of a row contiguous
-over all pieces), bf16x6, BERT-base forward shapes at T = 16384, every tile config."""
+"""Piece layout probe for the LDS-DMA piece GEMM (gemm_split.hip), bf16x6, BERT-base forward
+shapes at T = 16384: natural pieces [rows][3][K] vs the B16 layout [rows][K/16][3][16] for the
+B operand only (weights: written by split_weight, read by nothing else) or for both operands."""
 import os
 import sys
 
@@ -10,7 +10,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspa
 from tools.bench_gemm_split import timeit, relerr  # noqa: E402
 
 
-def blocked(p, npc, kb):
+def blocked(p, npc=3, kb=16):
     R = p.shape[0]
     K = p.shape[1] // npc
     return p.view(R, npc, K // kb, kb).permute(0, 2, 1, 3).contiguous().view(R, -1)
@@ -26,20 +26,26 @@ def main():
         x = torch.rand(T, n_in, device='cuda') * 2 - 1
         W = (torch.rand(n_out, n_in, device='cuda') * 2 - 1) * 0.05
         xs = sg.pieces(x)
-        wf, _ = sg.weight_pieces(W)
+        wf, _ = C().split_weight(W, 3)
+        wb, _ = C().split_weight(W, 3, True)
+        assert torch.equal(wb, blocked(wf))
+        xb = blocked(xs)
         ref = x.double() @ W.double().t()
         sc = x.double().abs() @ W.double().abs().t()
         fl = 2.0 * T * n_in * n_out * 6
-        for cfg, kb in ((0, 16), (1, 16), (2, 32), (3, 16), (4, 16), (5, 16), (6, 16)):
-            if n_out % {0: 192, 1: 256, 2: 128, 3: 192, 4: 128, 5: 256, 6: 128}[cfg]:
+        for cfg in (0, 1, 2):
+            if n_out % {0: 192, 1: 256, 2: 128}[cfg]:
                 continue
             os.environ['HX_GEMM_CFG'] = str(cfg)
-            xb, wb = blocked(xs, 3, kb), blocked(wf, 3, kb)
-            t_n = timeit(lambda: C().gemm_split(xs, wf, 6))
-            t_b = timeit(lambda: C().gemm_split(xb, wb, 6, None, False, kb))
-            e_b = relerr(C().gemm_split(xb, wb, 6, None, False, kb), ref, sc)
-            print('{:5s} cfg {} natural {:7.1f} us {:5.0f} TF/s | blocked{} {:7.1f} us {:5.0f} TF/s err {:.2e}'.format(
-                name, cfg, t_n, fl / t_n / 1e6, kb, t_b, fl / t_b / 1e6, e_b), flush=True)
+            line = '{:5s} cfg {}'.format(name, cfg)
+            for lay, a_, b_ in ((0, xs, wf), (2, xs, wb), (3, xb, wb)):
+                if lay and cfg == 2:
+                    continue
+                t = timeit(lambda: C().gemm_split(a_, b_, 6, None, False, lay))
+                e = relerr(C().gemm_split(a_, b_, 6, None, False, lay), ref, sc)
+                line += ' | lay{} {:6.1f} us {:5.0f} TF/s {:.1e}'.format(lay, t, fl / t / 1e6, e)
+            print(line, flush=True)
+        os.environ.pop('HX_GEMM_CFG', None)
 
 
 if __name__ == '__main__':

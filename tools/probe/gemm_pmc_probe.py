@@ -16,13 +16,20 @@ def main():
         os.environ['HX_GEMM_CFG'] = sys.argv[1]
     ops.set_fp32_gemm('bf16x6')
     T = 16384
-    for (n_out, n_in) in [(768, 768), (3072, 768)]:
+    shapes = [(768, 3072)] if os.environ.get('ONLY_DOWN') else [(768, 768), (3072, 768)]
+    for (n_out, n_in) in shapes:
         x = torch.rand(T, n_in, device='cuda') * 2 - 1
         W = (torch.rand(n_out, n_in, device='cuda') * 2 - 1) * 0.05
         xs = sg.pieces(x)
         wf, _ = sg.weight_pieces(W)
+        kb = int(os.environ.get('KBLOCK', '0'))
+        if kb:
+            def blk(p):
+                return p.view(p.shape[0], 3, -1, 16).permute(0, 2, 1, 3).contiguous().view(p.shape[0], -1)
+            xs, wf = blk(xs), blk(wf)
+        from hetseq_9cme_amd.ops._ext import C
         for _ in range(10):
-            sg.gemm(xs, wf)
+            C().gemm_split(xs, wf, 6, None, False, kb)
         torch.cuda.synchronize()
     print('done')
 

@@ -18,8 +18,13 @@ def main():
         x = torch.rand(T, n_in, device='cuda') * 2 - 1
         W = (torch.rand(n_out, n_in, device='cuda') * 2 - 1) * 0.05
         xs, wf = sg.pieces(x), sg.weight_pieces(W)[0]
+        lay = int(os.environ.get('LAY', '0'))
+        if lay:
+            def blk(p):
+                return p.view(p.shape[0], 3, -1, 16).permute(0, 2, 1, 3).contiguous().view(p.shape[0], -1)
+            xs, wf = blk(xs), blk(wf)
         for _ in range(5):
-            st = C().gemm_split_stamps(xs, wf)
+            st = C().gemm_split_stamps(xs, wf, lay)
         torch.cuda.synchronize()
         st = st.double()
         live = st[:, 4] > 0

@@ -63,11 +63,69 @@ def parse():
                     help='extra untimed steps reporting host time per step phase (stderr)')
     ap.add_argument('--sync-debug', action='store_true',
                     help='warn on every host<->device synchronisation during the extra steps')
+    ap.add_argument('--nodes', default=None,
+                    help='heterogeneous launch (BASELINE config 3), e.g. 5,3: one launcher process per "node" '
+                         'spawns its GPU count of ranks like train.py mode (a) (--distributed-gpus g_n '
+                         '--distributed-rank r_n), all meeting over one tcp:// rendezvous; every GPU stays '
+                         'visible (device = node offset + local index)')
+    ap.add_argument('--node-launcher', action='store_true', help=argparse.SUPPRESS)
+    ap.add_argument('--node-gpus', type=int, default=1, help=argparse.SUPPRESS)
+    ap.add_argument('--node-rank', type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument('--device-offset', type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument('--world', type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument('--init-method', default=None, help=argparse.SUPPRESS)
+    ap.add_argument('--nodes-meta', default=None, help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+def launch_nodes(a):
+    """Parent of a --nodes run: one launcher subprocess per "node" (the per-node qsub/ssh scripts
+    of the reference, STORE_RUN_FILE/Train_mnist/node8gpu32_het/run.sh:3-10); returns the exit code."""
+    import random
+    import subprocess
+    counts = [int(x) for x in a.nodes.split(',')]
+    world = sum(counts)
+    port = random.randint(20000, 30000)
+    rest = [x for x in sys.argv[1:]]
+    i = rest.index('--nodes')
+    del rest[i:i + 2]
+    procs, base = [], 0
+    for g in counts:
+        cmd = [sys.executable, os.path.abspath(__file__)] + rest + [
+            '--node-launcher', '--node-gpus', str(g), '--node-rank', str(base), '--device-offset', str(base),
+            '--world', str(world), '--init-method', 'tcp://127.0.0.1:{}'.format(port), '--gpus', str(world),
+            '--nodes-meta', ','.join(str(c) for c in counts)]
+        procs.append(subprocess.Popen(cmd))
+        base += g
+    rc = 0
+    for p in procs:
+        rc = p.wait() or rc
+    return rc
+
+
+def node_worker(i, a):
+    """One rank of a --nodes launch: rank = node base + i, device = node offset + i."""
+    os.environ.update(RANK=str(a.node_rank + i), LOCAL_RANK=str(i), WORLD_SIZE=str(a.world))
+    run(a, a.node_rank + i, a.world, 0 if a.same_device else a.device_offset + i, a.init_method)
 
 
 def main():
     a = parse()
+    if a.nodes and not a.node_launcher and 'RANK' not in os.environ:
+        sys.exit(launch_nodes(a))
+    if a.node_launcher:
+        import torch.multiprocessing as mp
+        mp.spawn(node_worker, args=(a,), nprocs=a.node_gpus, join=True)
+        return
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != a.gpus and world > 1:
+        print('warning: --gpus {} but WORLD_SIZE {}'.format(a.gpus, world), file=sys.stderr)
+    run(a, rank, world, 0 if a.same_device else local_rank, 'env://')
+
+
+def run(a, rank, world, dev_index, init_method):
     if a.no_fused:
         os.environ['HETSEQ_NO_FUSED'] = '1'
     from hetseq_9cme_amd import options
@@ -78,12 +136,6 @@ def main():
     from hetseq_9cme_amd.parallel import distributed as dist_utils
     from hetseq_9cme_amd import tasks
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
-    if world != a.gpus and world > 1:
-        print('warning: --gpus {} but WORLD_SIZE {}'.format(a.gpus, world), file=sys.stderr)
-    dev_index = 0 if a.same_device else local_rank
     torch.cuda.set_device(dev_index)
 
     cfg = {'base': BERT_BASE, 'large': BERT_LARGE, 'tiny': BERT_TINY}[a.model]
@@ -117,7 +169,7 @@ def main():
     args.device_id = dev_index
     args.distributed_backend = a.backend
     if world > 1:
-        args.distributed_init_method = 'env://'
+        args.distributed_init_method = init_method
         args.distributed_rank = rank
         dist_utils.distributed_init(args)
         torch.distributed.barrier()
@@ -179,7 +231,9 @@ def main():
             'config': {'model': 'bert-base (L12 H768 A12 V30522, 110.1M params)' if a.model == 'base' else a.model,
                        'global_batch': global_batch, 'per_gpu_batch': a.batch * a.update_freq,
                        'seq_len': a.seq, 'max_pred': a.max_pred,
-                       'parallelism': 'dp{}'.format(world), 'optimizer': 'adam(fused)',
+                       'parallelism': 'dp{}'.format(world) + (' (nodes {})'.format('+'.join(
+                           a.nodes_meta.split(','))) if a.nodes_meta else ''), 'optimizer': 'adam(fused)',
+                       'nodes': [int(x) for x in a.nodes_meta.split(',')] if a.nodes_meta else None,
                        'fused_kernels': not a.no_fused, 'gemm_tuning': a.gemm_tuning,
                        'fp32_gemm': a.fp32_gemm if a.precision == 'fp32' else None,
                        'allreduce': a.allreduce_impl if world > 1 else None},

@@ -73,6 +73,8 @@ def save_checkpoint(args, controller, epoch_itr, val_loss):
     if val_loss is not None:
         best_function = max if args.maximize_best_checkpoint_metric else min
         save_checkpoint.best = best_function(val_loss, prev_best)
+    if hasattr(controller, 'check_transport_all'):
+        controller.check_transport_all()   # on EVERY rank: all raise together, before rank 0 writes
     if args.no_save or not dist_utils.is_master(args):
         return
 

@@ -140,8 +140,15 @@ class Controller(object):
         self._lr_scheduler.step_update(0)
 
     # ------------------------------------------------------------------ checkpoints
+    def check_transport_all(self):
+        """Collective-consistent check of every recorded update's xGMI error word: the
+        words were summed by the stats all-reduce, so every rank reads the same values and all
+        raise together -- before persisting weights and at the end of training, where the lagged
+        per-step check has not yet looked at the last updates."""
+        self._transport_monitor.check(force=True)
+
     def save_checkpoint(self, filename, extra_state, copies=()):
-        self.reducer.check_transport()   # never persist weights updated from timed-out reductions
+        self.check_transport_all()   # never persist weights updated from timed-out reductions
         if dist_utils.is_master(self.args):
             extra_state['train_meters'] = checkpoint_utils.meters_state(self.meters)
             state = checkpoint_utils.build_state(

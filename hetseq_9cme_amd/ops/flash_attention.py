@@ -80,7 +80,9 @@ class _AttnFn(torch.autograd.Function):
         keep = 1.0 - p
         seed, stream = get_rng().next(qkv.device) if p > 0 else (get_rng().seed_tensor(qkv.device), 0)
         bias = _bias3(bq, bk, bv).float().contiguous() if bq is not None else None
-        ctx.split = qkv.dtype == torch.float32 and split_gemm.passes() > 0
+        # the split (x6) kernels follow the linears' policy (split_gemm.active: B*S >= MIN_ROWS rows),
+        # so small fine-tuning batches keep the fp32-MFMA attention like their GEMMs
+        ctx.split = qkv.dtype == torch.float32 and split_gemm.active(qkv.reshape(-1, qkv.shape[-1]))
         # one key block (S <= 128): the backward can write the projection's gradient planes
         ctx.gp = gp if (ctx.split and _X6_BWD and _X6_PLANES and qkv.shape[1] <= 128) else None
         if ctx.split:

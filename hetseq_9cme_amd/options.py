@@ -50,8 +50,11 @@ def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialD
                         help='log format to use')
     # --- MI355X-native execution knobs (not in the reference) ---
     parser.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'],
-                        help='compute precision: fp32 (reference parity, exact-f32 MFMA) or '
-                             'bf16 (bf16 MFMA, fp32 master weights and optimizer state)')
+                        help='compute precision: fp32 (the reference\'s precision: fp32 tensors end to end; '
+                             'the GEMMs and attention products run as --fp32-gemm says -- by default bf16x6, '
+                             'fp32-exact class on the bf16 matrix cores; --fp32-gemm native gives plain f32 MFMA, '
+                             'bitwise the reference\'s fp32 FMA chain) or bf16 (bf16 MFMA, fp32 master weights '
+                             'and optimizer state)')
     parser.add_argument('--fp32-gemm', default='bf16x6', choices=['native', 'bf16x3', 'bf16x6'],
                         help='how fp32 (--precision fp32) linear-layer GEMMs run on the GPU: bf16x6 (default: '
                              'operands split into three bf16 pieces, six passes on the 16x faster bf16 MFMA, '
@@ -177,6 +180,10 @@ def add_distributed_training_args(parser):
                        help='which GPU to use (usually configured automatically)')
     group.add_argument('--distributed-no-spawn', action='store_true',
                        help='do not spawn multiple processes even if multiple GPUs are visible')
+    group.add_argument('--device-offset', default=0, type=int,
+                       help='MI355X: first local GPU of this launcher -- spawned rank i runs on GPU '
+                            'device-offset + i, with every GPU of the host visible (several "node" '
+                            'launchers sharing one host keep peer access / IPC for the xGMI transport)')
     group.add_argument('--distributed-timeout', default=1800, type=int,
                        help='collective / rendezvous timeout in seconds')
     group.add_argument('--ddp-backend', default='c10d', type=str, choices=['c10d'],

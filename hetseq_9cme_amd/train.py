@@ -76,6 +76,7 @@ def main(args, init_distributed=False):
         reload_dataset = getattr(args, 'data', None) is not None and ':' in getattr(args, 'data', '')
         epoch_itr = controller.get_train_iterator(epoch_itr.epoch, load_dataset=reload_dataset)
     train_meter.stop()
+    controller.check_transport_all()   # the last updates' xGMI words (lagged check), on every rank
     controller.wait_for_save()
     print('| done training in {:.1f} seconds'.format(train_meter.sum))
     return controller
@@ -115,7 +116,7 @@ def train(args, controller, task, epoch_itr):
             sums = dist_utils.all_gather_list(controller.param_checksum())
             assert all(abs(s - sums[0]) <= 1e-6 * max(1.0, abs(sums[0])) for s in sums), \
                 'parameter replicas diverged across ranks: {}'.format(sums)
-            controller.reducer.check_transport()
+            controller.check_transport_all()
         if (args.save_interval_updates > 0 and num_updates % args.save_interval_updates == 0
                 and not epoch_itr.end_of_epoch()):
             checkpoint_utils.save_checkpoint(args, controller, epoch_itr, None)
@@ -172,7 +173,7 @@ class _LazyPPL(object):
 
 
 def distributed_main(i, args, start_rank=0):
-    args.device_id = i
+    args.device_id = i + getattr(args, 'device_offset', 0)
     if args.distributed_rank is None:
         args.distributed_rank = start_rank + i
     main(args, init_distributed=True)

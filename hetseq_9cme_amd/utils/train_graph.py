@@ -57,8 +57,12 @@ class _Entry(object):
 
 
 class GraphedTrainStep(object):
-    def __init__(self, controller, warmup=2, max_graphs=16, max_runs=64):
+    def __init__(self, controller, warmup=2, max_graphs=16, max_runs=None):
         self.ctrl = controller
+        # one (step size, wd * lr) pair per optimizer run; a run covers >= 1 parameter, so the
+        # parameter count bounds it (a fragmented --find-unused-parameters mask cannot overflow)
+        if max_runs is None:
+            max_runs = max(64, len(controller.flat.params))
         self.warmup = warmup
         self.max_graphs = max_graphs
         self.graphs = {}
@@ -121,6 +125,12 @@ class GraphedTrainStep(object):
         try:
             with torch.cuda.graph(g, pool=self.pool):
                 ent.out = c._train_step([ent.static])
+        except Exception:
+            # a failed capture must not leave the optimizer pointed at the graph's buffer:
+            # this shape runs eagerly from now on
+            opt.device_hparams = None
+            self.seen[key] = -(1 << 30)
+            raise
         finally:
             rng.external = False
         self.pool = g.pool()

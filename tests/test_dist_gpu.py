@@ -85,3 +85,47 @@ def test_bench_two_ranks_contract(tmp_path):
     assert rec['config']['global_batch'] == 16 and rec['config']['parallelism'] == 'dp2'
     assert rec['value'] > 0 and rec['ms_per_step'] > 0
     assert abs(rec['value'] - 16 * 1000.0 / rec['ms_per_step']) / rec['value'] < 1e-3
+
+
+def test_bench_heterogeneous_nodes_contract(tmp_path):
+    """bench.py --nodes 2,1 (the BASELINE config-3 5+3 launch in miniature): one launcher per
+    "node" spawns its ranks like train.py mode (a), all meet over one tcp:// rendezvous; rank 0
+    prints ONE JSON line for the whole 3-rank job with the per-node split (rehearsal: every
+    rank on this box's GPU over gloo)."""
+    import json
+    env = dict(os.environ, PYTHONPATH=ROOT, TMPDIR=str(tmp_path))
+    env.pop('RANK', None)
+    env.pop('WORLD_SIZE', None)
+    cmd = [sys.executable, os.path.join(ROOT, 'bench.py'), '--nodes', '2,1', '--steps', '3', '--warmup', '1',
+           '--model', 'tiny', '--batch', '8', '--backend', 'gloo', '--same-device', '--num-workers', '1']
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, timeout=300,
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-3000:]
+    rec = json.loads(lines[0])
+    assert rec['n_gpus'] == 3 and rec['config']['global_batch'] == 24
+    assert rec['config']['nodes'] == [2, 1] and rec['config']['parallelism'] == 'dp3 (nodes 2+1)'
+    assert abs(rec['value'] - 24 * 1000.0 / rec['ms_per_step']) / rec['value'] < 1e-3
+
+
+def test_bench_ner_torchrun_contract(tmp_path):
+    """tools/bench_ner.py under torch.distributed.run (BASELINE config 5, 4-GPU NER, here 2 ranks
+    on the box's GPU over gloo, BERT-tiny): env:// rendezvous, LOCAL_RANK device, one JSON line
+    from rank 0 with the max-over-ranks seconds per update."""
+    import json
+    import socket
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, PYTHONPATH=ROOT, TMPDIR=str(tmp_path))
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2', '--master-addr',
+           '127.0.0.1', '--master-port', str(port), os.path.join(ROOT, 'tools', 'bench_ner.py'), '--gpus', '2',
+           '--steps', '3', '--warmup', '1', '--batch', '8', '--backend', 'gloo', '--same-device', '--model', 'tiny']
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, timeout=300,
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-3000:]
+    rec = json.loads(lines[0])
+    assert rec['n_gpus'] == 2 and rec['global_batch'] == 16 and rec['value'] > 0

@@ -4,8 +4,14 @@ reference observed 0.214 s/update on 1 GPU).
 Synthetic CoNLL-format sentences (8-40 words, CoNLL-2003-like lengths), a
 BERT-base configuration with random init (no checkpoint download possible),
 the real ``BertForTokenClassification`` task / collator / engine.  Prints one
-JSON line with seconds per update (max over ranks under torchrun).
-``python tools/bench_ner.py [--steps 50] [--warmup 5] [--batch 32]``
+JSON line with seconds per update (rank 0; the max over ranks).
+
+One GPU: ``python tools/bench_ner.py [--steps 50] [--warmup 5] [--batch 32]``.
+Data parallel, the reference's 4-GPU fine-tuning run
+(STORE_RUN_FILE/Train_bert_fine_tuning_ner/bert_from_reddit_to_aida_ner/run_bert_fine_tuning_ner.sh:17-37,
+--find-unused-parameters): ``python -m torch.distributed.run --nproc-per-node 4 --master-addr
+127.0.0.1 --master-port P tools/bench_ner.py --gpus 4`` -- env:// rendezvous, rank r on GPU
+LOCAL_RANK, ``--batch`` sentences per rank, timed region bracketed by barrier + device sync.
 """
 import argparse
 import json
@@ -30,17 +36,34 @@ def main():
     ap.add_argument('--graph-train-step', action='store_true', help='replay captured HIP graphs of the update')
     ap.add_argument('--cprofile', default=None, metavar='OUT',
                     help='after the timed steps, cProfile 20 more steps and write the top host functions to OUT')
+    ap.add_argument('--gpus', type=int, default=1, help='ranks (launched by torch.distributed.run when > 1)')
+    ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'])
+    ap.add_argument('--same-device', action='store_true', help='rehearsal: every rank on GPU 0')
+    ap.add_argument('--model', default='base', choices=['base', 'tiny'])
     a = ap.parse_args()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    dev = 0 if a.same_device else local_rank
+    torch.cuda.set_device(dev)
     from hetseq_9cme_amd import options, tasks
     from hetseq_9cme_amd.controller import Controller
     from hetseq_9cme_amd.data import iterators
-    from hetseq_9cme_amd.data.synthetic import (BERT_BASE, WORDS, write_bert_config, write_synthetic_conll,
-                                                write_vocab)
-    d = tempfile.mkdtemp(prefix='hx_ner_')
-    vocab = write_vocab(os.path.join(d, 'vocab.txt'), 30522, extra_words=WORDS)
-    cfg = write_bert_config(os.path.join(d, 'bert_base.json'), **BERT_BASE)
-    n = (a.steps + a.warmup + 22) * a.batch
-    tr = write_synthetic_conll(os.path.join(d, 'train.txt'), n, seed=0, min_len=8, max_len=40)
+    from hetseq_9cme_amd.data.synthetic import (BERT_BASE, BERT_TINY, WORDS, write_bert_config,
+                                                write_synthetic_conll, write_vocab)
+    from hetseq_9cme_amd.parallel import distributed as dist_utils
+    n = (a.steps + a.warmup + 22) * a.batch * world
+    d = os.path.join(tempfile.gettempdir(), 'hx_ner_{}_{}_{}'.format(a.model, n, os.getpid() if world == 1 else
+                                                                      os.environ.get('MASTER_PORT', '0')))
+    vocab, cfg, tr = os.path.join(d, 'vocab.txt'), os.path.join(d, 'bert.json'), os.path.join(d, 'train.txt')
+    if rank == 0 and not os.path.exists(os.path.join(d, 'READY')):
+        os.makedirs(d, exist_ok=True)
+        write_vocab(vocab, 30522, extra_words=WORDS)
+        write_bert_config(cfg, **(BERT_BASE if a.model == 'base' else dict(BERT_TINY, vocab_size=30522)))
+        write_synthetic_conll(tr, n, seed=0, min_len=8, max_len=40)
+        open(os.path.join(d, 'READY'), 'w').close()
+    while not os.path.exists(os.path.join(d, 'READY')):
+        time.sleep(0.2)
     argv = ['--task', 'BertForTokenClassification', '--optimizer', 'adam', '--fast-stat-sync', '--lr', '5e-5',
             '--dict', vocab, '--config_file', cfg, '--train_file', tr, '--extension_file', 'conll',
             '--max-sentences', str(a.batch), '--num-workers', '2', '--find-unused-parameters',
@@ -50,9 +73,15 @@ def main():
         argv.append('--profile-phases')
     if a.graph_train_step:
         argv.append('--graph-train-step')
-    args = options.parse_training_args(argv)
-    args.device_id = 0
-    args.distributed_rank = 0
+    args = options.parse_training_args(argv + ['--distributed-world-size', str(world)])
+    args.device_id = dev
+    args.distributed_backend = a.backend
+    if world > 1:
+        args.distributed_init_method = 'env://'
+        args.distributed_rank = rank
+        dist_utils.distributed_init(args)
+    else:
+        args.distributed_rank = 0
     torch.manual_seed(args.seed)
     task = tasks.setup_task(args)
     model = task.build_model(args)
@@ -64,11 +93,21 @@ def main():
         ctrl.train_step(next(itr))
     torch.cuda.synchronize()
     ctrl.phase_report()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         ctrl.train_step(next(itr))
     torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device='cuda')
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
     gs = ctrl._graph_step
     if gs is not None:
         print('graph-train-step: {} captures, {} replays'.format(gs.captures, gs.replays), file=sys.stderr)
@@ -91,11 +130,19 @@ def main():
         for kind in ('host', 'device'):
             print('phases {} ms/step: '.format(kind) + ', '.join(
                 '{}={:.2f}'.format(k, v * 1e3 / max(rep['steps'], 1)) for k, v in rep[kind].items()), file=sys.stderr)
-    print(json.dumps({'metric': 'NER fine-tune (BertForTokenClassification, BERT-base) s/update',
-                      'value': round(dt, 5), 'unit': 's/update', 'higher_is_better': False,
-                      'reference_1gpu': 0.214, 'speedup_vs_reference': round(0.214 / dt, 1),
-                      'batch': a.batch, 'dtype': a.precision, 'graph_train_step': a.graph_train_step,
-                      'data': 'synthetic CoNLL-format sentences (8-40 words), random-init BERT-base'}), flush=True)
+    if rank == 0:
+        print(json.dumps({'metric': 'NER fine-tune (BertForTokenClassification, BERT-{}) s/update'.format(a.model),
+                          'value': round(dt, 5), 'unit': 's/update', 'higher_is_better': False,
+                          'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
+                          'reference_1gpu': 0.214, 'speedup_vs_reference': round(0.214 / dt, 1),
+                          'batch': a.batch, 'global_batch': a.batch * world, 'dtype': a.precision,
+                          'graph_train_step': a.graph_train_step,
+                          'parallelism': 'dp{}'.format(world) + (' (find-unused-parameters)' if world > 1 else ''),
+                          'data': 'synthetic CoNLL-format sentences (8-40 words), random-init BERT-{}'.format(
+                              a.model)}), flush=True)
+    if world > 1:
+        torch.distributed.barrier()
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == '__main__':

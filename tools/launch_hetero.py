@@ -1,13 +1,19 @@
 """Local rehearsal of a heterogeneous multi-node HetSeq launch on ONE machine.
 
 Each "node" is a separate launcher process that owns a disjoint subset of the
-local GPUs (HIP_VISIBLE_DEVICES) and passes ``--distributed-gpus g_n
---distributed-rank r_n`` exactly like the per-node qsub/ssh scripts of the
-reference (STORE_RUN_FILE/Train_mnist/*_het); all nodes meet through one TCP
-rendezvous on 127.0.0.1.  Example (the BASELINE 5+3 split on an 8-GPU box):
+local GPUs and passes ``--distributed-gpus g_n --distributed-rank r_n`` exactly
+like the per-node qsub/ssh scripts of the reference (STORE_RUN_FILE/Train_mnist/*_het);
+all nodes meet through one TCP rendezvous on 127.0.0.1.  Example (the BASELINE 5+3
+split on an 8-GPU box):
 
   python tools/launch_hetero.py --nodes 5,3 -- --task bert --data D --config_file C \
       --max-sentences 128 --fast-stat-sync --max-update 100
+
+GPU ownership: by default (``--device-offset``) every launcher sees ALL GPUs and its ranks
+run on GPUs offset .. offset + g_n - 1 (train.py ``--device-offset``), so the ranks of
+different "nodes" can still map each other's memory -- the hand-written xGMI transport
+(--allreduce-impl xgmi) works across the split.  ``--partition`` instead hides the other
+nodes' GPUs with HIP_VISIBLE_DEVICES (closest to separate machines; RCCL only).
 """
 import argparse
 import os
@@ -21,6 +27,8 @@ def main():
     ap.add_argument('--nodes', default='5,3', help='comma separated GPU count per "node"')
     ap.add_argument('--port', type=int, default=0)
     ap.add_argument('--cpu', action='store_true', help='gloo on CPU (no GPU partitioning)')
+    ap.add_argument('--partition', action='store_true',
+                    help='HIP_VISIBLE_DEVICES per node instead of --device-offset (peers invisible)')
     ap.add_argument('rest', nargs=argparse.REMAINDER)
     a = ap.parse_args()
     rest = a.rest[1:] if a.rest and a.rest[0] == '--' else a.rest
@@ -31,11 +39,13 @@ def main():
     procs, base, dev0 = [], 0, 0
     for g in counts:
         env = dict(os.environ)
-        if not a.cpu:
-            env['HIP_VISIBLE_DEVICES'] = ','.join(str(d) for d in range(dev0, dev0 + g))
         cmd = [sys.executable, '-m', 'hetseq_9cme_amd.train'] + rest + [
             '--distributed-init-method', init, '--distributed-world-size', str(world),
             '--distributed-gpus', str(g), '--distributed-rank', str(base)]
+        if not a.cpu and a.partition:
+            env['HIP_VISIBLE_DEVICES'] = ','.join(str(d) for d in range(dev0, dev0 + g))
+        elif not a.cpu:
+            cmd += ['--device-offset', str(dev0)]
         if a.cpu:
             cmd += ['--cpu']
         if g == 1:

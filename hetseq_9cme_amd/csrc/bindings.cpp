@@ -110,7 +110,7 @@ void adadelta(Tensor p, Tensor g, Tensor sq, Tensor acc, Tensor gscale, int64_t 
 
 // ------------------------------------------------------------------ layernorm
 std::vector<Tensor> ln_fwd(Tensor y, OptT bias, OptT res, Tensor gamma, Tensor beta, double eps, double keep_prob,
-                           const Tensor& seed, int64_t stream, bool drop_after, bool save_z) {
+                           const Tensor& seed, int64_t stream, bool drop_after, bool save_z, int64_t npieces) {
   check_cuda(y, "input");
   const int H = (int)y.size(-1);
   const int64_t rows = y.numel() / H;
@@ -127,12 +127,16 @@ std::vector<Tensor> ln_fwd(Tensor y, OptT bias, OptT res, Tensor gamma, Tensor b
   Tensor z = save_z ? torch::empty_like(y) : Tensor();
   auto st = y.options().dtype(torch::kFloat32);
   auto mean = torch::empty({rows}, st), rstd = torch::empty({rows}, st);
+  TORCH_CHECK(npieces == 0 || ((npieces == 2 || npieces == 3) && y.scalar_type() == torch::kFloat32),
+              "ln_fwd: pieces (2 or 3) of an fp32 output only");
+  Tensor pcs = npieces ? torch::empty({rows, npieces * H}, y.options().dtype(torch::kBFloat16)) : Tensor();
   hx_ln_fwd(act_bf16(y), y.data_ptr(), ptr_or_null<float>(bias), has(res) ? res->data_ptr() : nullptr,
             gamma.data_ptr<float>(), beta.data_ptr<float>(), out.data_ptr(), save_z ? z.data_ptr() : nullptr,
             mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, H, (float)eps, (float)keep_prob, seed_ptr(seed),
-            (uint64_t)stream, drop_after ? 1 : 0, cur_stream(y));
+            (uint64_t)stream, drop_after ? 1 : 0, cur_stream(y),
+            npieces ? reinterpret_cast<uint16_t*>(pcs.data_ptr()) : nullptr, (int)npieces);
   dbg_finite(out, "ln_fwd");
-  return {out, z, mean, rstd};
+  return {out, z, mean, rstd, pcs};
 }
 
 std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tensor gamma, double keep_prob,
@@ -201,7 +205,8 @@ std::vector<Tensor> ln_bwd_planes(Tensor dout, Tensor z, Tensor mean, Tensor rst
 }
 
 std::vector<Tensor> embed_ln_fwd(Tensor ids, OptT tt, Tensor wte, Tensor wpe, Tensor wtt, Tensor gamma, Tensor beta,
-                                 double eps, double keep_prob, const Tensor& seed, int64_t stream, bool bf16_out) {
+                                 double eps, double keep_prob, const Tensor& seed, int64_t stream, bool bf16_out,
+                                 int64_t npieces) {
   dbg_range(ids, 0, wte.size(0), "token ids");
   if (has(tt)) dbg_range(*tt, 0, wtt.size(0), "token type ids");
   check_cuda(ids, "input_ids");
@@ -219,12 +224,16 @@ std::vector<Tensor> embed_ln_fwd(Tensor ids, OptT tt, Tensor wte, Tensor wpe, Te
   auto out = torch::empty({B, S, H}, opt), z = torch::empty({B, S, H}, opt);
   auto f32 = wte.options();
   auto mean = torch::empty({B * S}, f32), rstd = torch::empty({B * S}, f32);
+  TORCH_CHECK(npieces == 0 || ((npieces == 2 || npieces == 3) && !bf16_out),
+              "embed_ln_fwd: pieces (2 or 3) of an fp32 output only");
+  Tensor pcs = npieces ? torch::empty({B * S, npieces * H}, wte.options().dtype(torch::kBFloat16)) : Tensor();
   hx_embed_ln_fwd(bf16_out ? 1 : 0, ids.data_ptr<int64_t>(), has(tt) ? tt->data_ptr<int64_t>() : nullptr,
                   wte.data_ptr<float>(), wpe.data_ptr<float>(), wtt.data_ptr<float>(), gamma.data_ptr<float>(),
                   beta.data_ptr<float>(), out.data_ptr(), z.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
-                  B * S, (int)S, H, (float)eps, (float)keep_prob, seed_ptr(seed), (uint64_t)stream, cur_stream(ids));
+                  B * S, (int)S, H, (float)eps, (float)keep_prob, seed_ptr(seed), (uint64_t)stream, cur_stream(ids),
+                  npieces ? reinterpret_cast<uint16_t*>(pcs.data_ptr()) : nullptr, (int)npieces);
   dbg_finite(out, "embed_ln_fwd");
-  return {out, z, mean, rstd};
+  return {out, z, mean, rstd, pcs};
 }
 
 // Scatter-ACCUMULATES the embedding gradients into dwte / dwpe / dwtt (caller zeroes them
@@ -330,7 +339,7 @@ Tensor softmax_xent_(Tensor logits, OptT bias, Tensor labels, int64_t ignore_ind
 
 // ------------------------------------------------------------------ attention
 std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed, int64_t stream,
-                             OptT bias, bool split = false) {
+                             OptT bias, bool split = false, int64_t npieces = 0) {
   check_cuda(qkv, "qkv");
   const int bf = act_bf16(qkv);
   check_f32(mask_bias, "mask_bias");
@@ -351,23 +360,29 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
   if (keep < 1.0) dmask = torch::empty({B, nh, Sp, Sp / 32}, qkv.options().dtype(torch::kInt32));
   else dmask = torch::empty({0}, qkv.options().dtype(torch::kInt32));
   uint32_t* dm = keep < 1.0 ? reinterpret_cast<uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr;
+  Tensor pcs;
   if (split) {
     TORCH_CHECK(!bf, "attn_fwd_x6: fp32 activations only");
+    TORCH_CHECK(npieces == 0 || npieces == 2 || npieces == 3, "attn_fwd_x6: 0, 2 or 3 output pieces");
+    if (npieces) pcs = torch::empty({B * S, npieces * H}, qkv.options().dtype(torch::kBFloat16));
     hx_attn_fwd_x6(qkv.data_ptr<float>(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(),
                    out.data_ptr<float>(), lse.data_ptr<float>(), dm, (int)B, (int)S, (int)nh, (float)keep,
-                   seed_ptr(seed), (uint64_t)stream, cur_stream(qkv));
+                   seed_ptr(seed), (uint64_t)stream, cur_stream(qkv),
+                   npieces ? reinterpret_cast<uint16_t*>(pcs.data_ptr()) : nullptr, (int)npieces);
   } else {
     hx_attn_fwd(bf, qkv.data_ptr(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(), out.data_ptr(),
                 lse.data_ptr<float>(), dm, (int)B, (int)S, (int)nh, (float)keep, seed_ptr(seed), (uint64_t)stream,
                 cur_stream(qkv));
   }
   dbg_finite(out, "attn_fwd");
+  if (split) return {out, lse, dmask, pcs};
   return {out, lse, dmask};
 }
-// fp32 attention forward on the bf16 matrix cores (split pieces, attention_x6.hip)
+// fp32 attention forward on the bf16 matrix cores (split pieces, attention_x6.hip); returns
+// {out, lse, dmask, pieces of out (npieces > 0) or an undefined tensor}
 std::vector<Tensor> attn_fwd_x6(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed,
-                                int64_t stream, OptT bias) {
-  return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, true);
+                                int64_t stream, OptT bias, int64_t npieces) {
+  return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, true, npieces);
 }
 
 // returns {dqkv, dbias} (dbias: [3H] fp32 when bias is given -- written into dbq/dbk/dbv
@@ -812,10 +827,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("grad_norm_clip", &grad_norm_clip);
   m.def("adam", &adam);
   m.def("adadelta", &adadelta);
-  m.def("ln_fwd", &ln_fwd);
+  m.def("ln_fwd", &ln_fwd, py::arg("y"), py::arg("bias"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
+        py::arg("eps"), py::arg("keep_prob"), py::arg("seed"), py::arg("stream"), py::arg("drop_after"),
+        py::arg("save_z"), py::arg("npieces") = 0);
   m.def("ln_bwd", &ln_bwd);
   m.def("ln_bwd_planes", &ln_bwd_planes);
-  m.def("embed_ln_fwd", &embed_ln_fwd);
+  m.def("embed_ln_fwd", &embed_ln_fwd, py::arg("ids"), py::arg("tt"), py::arg("wte"), py::arg("wpe"), py::arg("wtt"),
+        py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("keep_prob"), py::arg("seed"), py::arg("stream"),
+        py::arg("bf16_out"), py::arg("npieces") = 0);
   m.def("embed_word_grad", &embed_word_grad);
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);
@@ -824,7 +843,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_xent_", &softmax_xent_);
   m.def("attn_fwd", [](Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed, int64_t stream,
                         OptT bias) { return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, false); });
-  m.def("attn_fwd_x6", &attn_fwd_x6);
+  m.def("attn_fwd_x6", &attn_fwd_x6, py::arg("qkv"), py::arg("mask_bias"), py::arg("nh"), py::arg("keep"),
+        py::arg("seed"), py::arg("stream"), py::arg("bias"), py::arg("npieces") = 0);
   m.def("attn_bwd", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
                        double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv) {
     return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, false);

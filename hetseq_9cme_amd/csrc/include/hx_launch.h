@@ -19,7 +19,9 @@ void hx_adadelta(float* p, const float* g, float* sq, float* acc, const float* g
 int hx_ln_bwd_blocks(int64_t rows);
 void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, const float* gamma, const float* beta,
                void* out, void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob,
-               const uint64_t* seed, uint64_t stream, int drop_after, hipStream_t s);
+               const uint64_t* seed, uint64_t stream, int drop_after, hipStream_t s, uint16_t* pieces = nullptr,
+               int npc = 0);
+// (pieces != nullptr, fp32 only: the output is also written as npc bf16 pieces [rows][npc][H])
 void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma,
                void* dz, void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
                uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
@@ -28,7 +30,7 @@ void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, con
 void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,
                      const float* wtt, const float* gamma, const float* beta, void* out, void* zsave, float* mean,
                      float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, const uint64_t* seed,
-                     uint64_t stream, hipStream_t s);
+                     uint64_t stream, hipStream_t s, uint16_t* pieces = nullptr, int npc = 0);
 void hx_embed_word_grad_sorted(int bf16, const void* dz, const int64_t* ids, const int64_t* order, float* dwte,
                                int64_t rows, int H, hipStream_t s);
 // elementwise.hip
@@ -58,9 +60,10 @@ void hx_wgrad_bf16_plan(int M, int N, int T, int* cfg, int* nsplit);
 void hx_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, float* out, float* ws, int M, int N, int T,
                    int cfg, int nsplit, hipStream_t s);
 // attention_x6.hip -- fp32 attention forward on bf16 MFMA with split pieces (bf16x6 class)
+// opieces != nullptr: out is also written as npc bf16 pieces [B*S][npc][H]
 void hx_attn_fwd_x6(const float* qkv, const float* bias, const float* maskb, float* out, float* lse,
                     uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream,
-                    hipStream_t s);
+                    hipStream_t s, uint16_t* opieces = nullptr, int npc = 0);
 // planes != nullptr (S <= 128 only): dQKV goes out as npl stacked bf16 planes [B*S][npl * 3H]
 // (plane j = piece (order >> 4j) & 15) instead of fp32 dqkv
 void hx_attn_bwd_x6(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,

@@ -109,7 +109,7 @@ template <bool kDrop>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd_x6_k(
     const float* __restrict__ qkv, const float* __restrict__ qkv_bias, const float* __restrict__ maskb,
     float* __restrict__ out, float* __restrict__ lse, uint32_t* __restrict__ dmask, int S, int nh, float keep,
-    const uint64_t* __restrict__ seedp, uint64_t stream) {
+    const uint64_t* __restrict__ seedp, uint64_t stream, uint16_t* __restrict__ opieces, int npc) {
   const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   __shared__ __attribute__((aligned(16))) uint16_t Ks[3][64 * RS];   // [piece][key][dim]
   __shared__ __attribute__((aligned(16))) uint16_t Vt[3][64 * RS];   // [piece][dim][vpos(key)]
@@ -303,13 +303,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if (q >= S) return;
   const float inv_l = 1.f / l_run;
   float* op = out + ((int64_t)b * S + q) * H + hd * D;
+  // opieces: the context also goes out as the attention-output projection's input pieces
+  // [rows][npc][H] (natural piece layout), so that GEMM needs no split pass
+  auto put_pieces = [&](int d, float4 v) {
+    float e[4] = {v.x, v.y, v.z, v.w};
+    uint16_t* pp = opieces + ((int64_t)b * S + q) * npc * H + hd * D + d;
+    for (int p = 0; p < npc; ++p) {
+      uint16_t qv[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        qv[i] = hx::f2bf(e[i]);
+        e[i] -= hx::bf2f(qv[i]);
+      }
+      *reinterpret_cast<uint2*>(pp + (int64_t)p * H) =
+          make_uint2(qv[0] | ((uint32_t)qv[1] << 16), qv[2] | ((uint32_t)qv[3] << 16));
+    }
+  };
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int d0 = 8 * g + 4 * h;
-    *reinterpret_cast<float4*>(op + d0) =
+    const float4 va =
         make_float4(o0[4 * g] * inv_l, o0[4 * g + 1] * inv_l, o0[4 * g + 2] * inv_l, o0[4 * g + 3] * inv_l);
-    *reinterpret_cast<float4*>(op + 32 + d0) =
+    const float4 vb =
         make_float4(o1[4 * g] * inv_l, o1[4 * g + 1] * inv_l, o1[4 * g + 2] * inv_l, o1[4 * g + 3] * inv_l);
+    *reinterpret_cast<float4*>(op + d0) = va;
+    *reinterpret_cast<float4*>(op + 32 + d0) = vb;
+    if (opieces) {
+      put_pieces(d0, va);
+      put_pieces(32 + d0, vb);
+    }
   }
   if (h == 0) lse[bh * S + q] = m_run + __logf(l_run);
 }
@@ -775,12 +797,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
 void hx_attn_fwd_x6(const float* qkv, const float* bias, const float* maskb, float* out, float* lse,
                     uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream,
-                    hipStream_t s) {
+                    hipStream_t s, uint16_t* opieces, int npc) {
   dim3 grid((S + 127) / 128, nh, B);
   if (keep < 1.f)
-    attn_fwd_x6_k<true><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream);
+    attn_fwd_x6_k<true><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream, opieces,
+                                             npc);
   else
-    attn_fwd_x6_k<false><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream);
+    attn_fwd_x6_k<false><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream, opieces,
+                                              npc);
 }
 
 void hx_attn_bwd_x6(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,

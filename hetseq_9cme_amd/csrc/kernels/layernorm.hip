@@ -29,6 +29,22 @@ struct Row {
   float4 v[CH];
 };
 
+// npc bf16 pieces of the 4 fp32 outputs at columns j..j+3 of row r -> pieces [rows][npc][H]
+// (the natural piece layout the split GEMMs read: ops/split_gemm.py), one 8-B store per piece
+__device__ __forceinline__ void store_pieces4(uint16_t* pieces, int npc, int64_t r, int H, int j, float4 o) {
+  float e[4] = {o.x, o.y, o.z, o.w};
+  for (int p = 0; p < npc; ++p) {
+    uint16_t q[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      q[i] = hx::f2bf(e[i]);
+      e[i] -= hx::bf2f(q[i]);
+    }
+    *reinterpret_cast<uint2*>(pieces + (r * npc + p) * H + j) =
+        make_uint2(q[0] | ((uint32_t)q[1] << 16), q[2] | ((uint32_t)q[3] << 16));
+  }
+}
+
 // ----------------------------------------------------------------------------- fwd
 template <typename T, int CH, bool kDropAfter>
 __global__ __launch_bounds__(NT) void ln_fwd_k(const T* __restrict__ y, const float* __restrict__ bias,
@@ -36,7 +52,8 @@ __global__ __launch_bounds__(NT) void ln_fwd_k(const T* __restrict__ y, const fl
                                              const float* __restrict__ beta, T* __restrict__ out,
                                              T* __restrict__ zsave, float* __restrict__ mean_out,
                                              float* __restrict__ rstd_out, int64_t rows, int H, float eps,
-                                             float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream) {
+                                             float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream,
+                                             uint16_t* __restrict__ pieces, int npc) {
   const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   const int lane = threadIdx.x & 63;
   const int64_t wave = blockIdx.x * (int64_t)WPB + (threadIdx.x >> 6);
@@ -106,6 +123,7 @@ __global__ __launch_bounds__(NT) void ln_fwd_k(const T* __restrict__ y, const fl
           o.w = (k & 8) ? o.w * inv_keep : 0.f;
         }
         hx::store4(out + r * H + j, o);
+        if (pieces) store_pieces4(pieces, npc, r, H, j, o);
       }
     }
   }
@@ -267,7 +285,8 @@ __global__ __launch_bounds__(NT) void embed_ln_fwd_k(const int64_t* __restrict__
                                                    const float* __restrict__ beta, T* __restrict__ out,
                                                    T* __restrict__ zsave, float* __restrict__ mean_out,
                                                    float* __restrict__ rstd_out, int64_t rows, int S, int H,
-                                                   float eps, float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream) {
+                                                   float eps, float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream,
+                                                   uint16_t* __restrict__ pieces, int npc) {
   const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   const int lane = threadIdx.x & 63;
   const int64_t wave = blockIdx.x * (int64_t)WPB + (threadIdx.x >> 6);
@@ -326,6 +345,7 @@ __global__ __launch_bounds__(NT) void embed_ln_fwd_k(const int64_t* __restrict__
           o.w = (k & 8) ? o.w * inv_keep : 0.f;
         }
         hx::store4(out + r * H + j, o);
+        if (pieces) store_pieces4(pieces, npc, r, H, j, o);
       }
     }
   }
@@ -428,15 +448,15 @@ inline int ln_grid(int64_t rows, int cap) {
 template <typename T>
 void ln_fwd_t(const void* y, const float* bias, const void* res, const float* gamma, const float* beta, void* out,
               void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob, const uint64_t* seed,
-              uint64_t stream, int drop_after, hipStream_t s) {
+              uint64_t stream, int drop_after, uint16_t* pieces, int npc, hipStream_t s) {
   const int grid = ln_grid(rows, 4096);
   HX_CH_DISPATCH(H, {
     if (drop_after)
       ln_fwd_k<T, CH, true><<<grid, NT, 0, s>>>((const T*)y, bias, (const T*)res, gamma, beta, (T*)out, (T*)zsave,
-                                                mean, rstd, rows, H, eps, keep_prob, seed, stream);
+                                                mean, rstd, rows, H, eps, keep_prob, seed, stream, pieces, npc);
     else
       ln_fwd_k<T, CH, false><<<grid, NT, 0, s>>>((const T*)y, bias, (const T*)res, gamma, beta, (T*)out, (T*)zsave,
-                                                 mean, rstd, rows, H, eps, keep_prob, seed, stream);
+                                                 mean, rstd, rows, H, eps, keep_prob, seed, stream, pieces, npc);
   })
 }
 
@@ -466,13 +486,13 @@ int hx_ln_bwd_blocks(int64_t rows) { return ln_grid(rows, 512); }
 
 void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, const float* gamma, const float* beta,
                void* out, void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob,
-               const uint64_t* seed, uint64_t stream, int drop_after, hipStream_t s) {
+               const uint64_t* seed, uint64_t stream, int drop_after, hipStream_t s, uint16_t* pieces, int npc) {
   if (bf16)
     ln_fwd_t<uint16_t>(y, bias, res, gamma, beta, out, zsave, mean, rstd, rows, H, eps, keep_prob, seed, stream,
-                       drop_after, s);
+                       drop_after, nullptr, 0, s);
   else
     ln_fwd_t<float>(y, bias, res, gamma, beta, out, zsave, mean, rstd, rows, H, eps, keep_prob, seed, stream,
-                    drop_after, s);
+                    drop_after, pieces, npc, s);
 }
 
 void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma,
@@ -490,17 +510,17 @@ void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, con
 void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,
                      const float* wtt, const float* gamma, const float* beta, void* out, void* zsave, float* mean,
                      float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, const uint64_t* seed,
-                     uint64_t stream, hipStream_t s) {
+                     uint64_t stream, hipStream_t s, uint16_t* pieces, int npc) {
   const int grid = ln_grid(rows, 4096);
   HX_CH_DISPATCH(H, {
     if (bf16)
       embed_ln_fwd_k<uint16_t, CH><<<grid, NT, 0, s>>>(ids, tt, wte, wpe, wtt, gamma, beta, (uint16_t*)out,
                                                        (uint16_t*)zsave, mean, rstd, rows, S, H, eps, keep_prob,
-                                                       seed, stream);
+                                                       seed, stream, nullptr, 0);
     else
       embed_ln_fwd_k<float, CH><<<grid, NT, 0, s>>>(ids, tt, wte, wpe, wtt, gamma, beta, (float*)out,
                                                     (float*)zsave, mean, rstd, rows, S, H, eps, keep_prob, seed,
-                                                    stream);
+                                                    stream, pieces, npc);
   })
 }
 

@@ -87,7 +87,11 @@ class _AttnFn(torch.autograd.Function):
         ctx.gp = gp if (ctx.split and _X6_BWD and _X6_PLANES and qkv.shape[1] <= 128) else None
         if ctx.split:
             # fp32 products on the bf16 matrix cores (six piece passes, attention_x6.hip)
-            out, lse, dmask = C().attn_fwd_x6(qkv, mask_bias, num_heads, keep, seed, stream, bias)
+            B, S = qkv.shape[0], qkv.shape[1]
+            npc = split_gemm.producer_pieces(B * S, qkv.shape[2] // 3, qkv)
+            out, lse, dmask, pcs = C().attn_fwd_x6(qkv, mask_bias, num_heads, keep, seed, stream, bias, npc)
+            # the attention-output projection (a piece GEMM) reads the context's pieces directly
+            split_gemm.attach_pieces(out, pcs)
         else:
             out, lse, dmask = C().attn_fwd(qkv, mask_bias, num_heads, keep, seed, stream, bias)
         ctx.save_for_backward(qkv, mask_bias, out, lse, dmask)

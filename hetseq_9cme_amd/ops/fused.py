@@ -242,8 +242,10 @@ class _EmbedLNFn(torch.autograd.Function):
     def forward(ctx, ids, tt, wte, wpe, wtt, gamma, beta, eps, p, out_bf16):
         keep = 1.0 - p
         seed, stream = get_rng().next(ids.device) if p > 0 else (get_rng().seed_tensor(ids.device), 0)
-        out, z, mean, rstd = C().embed_ln_fwd(ids, tt, wte, wpe, wtt, gamma, beta, eps, keep, seed, stream,
-                                              out_bf16)
+        npc = 0 if out_bf16 else split_gemm.producer_pieces(ids.numel(), wte.shape[1], wte)
+        out, z, mean, rstd, pcs = C().embed_ln_fwd(ids, tt, wte, wpe, wtt, gamma, beta, eps, keep, seed, stream,
+                                                   out_bf16, npc)
+        split_gemm.attach_pieces(out, pcs)   # the first layer's QKV GEMM reads them
         ctx.save_for_backward(ids, tt if tt is not None else torch.Tensor(), z, mean, rstd, gamma)
         ctx.params = (wte, wpe, wtt, beta)
         ctx.has_tt = tt is not None
@@ -330,7 +332,9 @@ class _BiasDropResLNFn(torch.autograd.Function):
     def forward(ctx, y, bias, res, gamma, beta, eps, p, mbox, gp):
         keep = 1.0 - p
         seed, stream = get_rng().next(y.device) if p > 0 else (get_rng().seed_tensor(y.device), 0)
-        out, z, mean, rstd = C().ln_fwd(y, bias, res, gamma, beta, eps, keep, seed, stream, False, True)
+        npc = split_gemm.producer_pieces(y.numel() // y.shape[-1], y.shape[-1], y) if y.dtype == torch.float32 else 0
+        out, z, mean, rstd, pcs = C().ln_fwd(y, bias, res, gamma, beta, eps, keep, seed, stream, False, True, npc)
+        split_gemm.attach_pieces(out, pcs)   # the next QKV / FFN-up piece GEMM reads them
         ctx.save_for_backward(z, mean, rstd, gamma)
         ctx.params = (bias, beta)
         ctx.mbox = mbox
@@ -461,7 +465,7 @@ class _LinearFn(torch.autograd.Function):
             ctx.gp.pieces = ctx.pieces
         Wsave = W
         if ctx.pieces:    # fp32 on bf16 matrix cores, hand-written piece GEMMs
-            x2 = split_gemm.pieces(x2)
+            x2 = split_gemm.input_pieces(x, x2)
             wf, Wsave = split_gemm.weight_pieces(W)
             y = split_gemm.gemm(x2, wf)
             if b is not None:
@@ -550,7 +554,7 @@ class _FFNSplitFn(torch.autograd.Function):
         if ctx.pieces:
             # bias + GELU in the FFN-up GEMM's epilogue (pre-activation u kept in fp32 for the
             # backward, gelu(u) written as the FFN-down GEMM's pieces): bert_modeling.py:166-168
-            xs = split_gemm.pieces(x2)
+            xs = split_gemm.input_pieces(x, x2)
             w1f, w1t = split_gemm.weight_pieces(W1)
             u, hs = split_gemm.gemm_gelu(xs, w1f, b1)
             w2f, w2t = split_gemm.weight_pieces(W2)
@@ -675,7 +679,7 @@ class _Linear3Fn(torch.autograd.Function):
             # unlike the 4H -> H products (split_gemm.prefix_ok)
             ctx.gp.prefix = os.environ.get('HX_PREFIX_QKV', '0') == '1' and split_gemm.prefix_ok(W.shape[0], W.shape[1])
         if ctx.pieces:    # fp32 on bf16 matrix cores, hand-written piece GEMMs
-            x2 = split_gemm.pieces(x2)
+            x2 = split_gemm.input_pieces(x, x2)
             wf, Wc = split_gemm.weight_pieces(W)
             y = split_gemm.gemm(x2, wf)
             if has_b:

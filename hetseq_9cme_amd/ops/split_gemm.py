@@ -214,6 +214,33 @@ def nt_ok(n_in, n_out):
     return on and n_out % 128 == 0 and n_in % 128 == 0
 
 
+def producer_pieces(rows, H, ref):
+    """Number of pieces a producer (LayerNorm / embedding forward) should write next to its fp32
+    output [rows, H] on ``ref``'s device for a consuming piece-GEMM linear, or 0: the split path
+    is on for this size (``active``'s rule) and the piece GEMMs take the shape (``nt_ok``)."""
+    if not (_State.passes > 0 and use_kernels(ref) and rows >= MIN_ROWS[_State.passes] and nt_ok(H, 128)):
+        return 0
+    return npieces()
+
+
+def attach_pieces(out, pcs):
+    """Hand ``pcs`` (pieces of ``out``, written by its producer) to the consumer linear."""
+    if pcs is not None and pcs.numel():
+        out._hx_pieces = pcs
+        out._hx_pieces_ver = out._version
+    return out
+
+
+def input_pieces(x, x2):
+    """Pieces of the linear input ``x`` (viewed as ``x2`` [rows, K]): the producer's, when it
+    wrote them and ``x`` has not changed since, else split here."""
+    pcs = getattr(x, '_hx_pieces', None)
+    if pcs is not None and getattr(x, '_hx_pieces_ver', -1) == x._version and \
+            pcs.shape == (x2.shape[0], npieces() * x2.shape[1]):
+        return pcs
+    return pieces(x2)
+
+
 def pieces(x2):
     """[R, npc * D] bf16 pieces of the fp32 matrix ``x2`` [R, D] (piece p at column p * D)."""
     if x2.stride(-1) != 1:

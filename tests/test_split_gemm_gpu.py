@@ -318,7 +318,7 @@ def test_ln_bwd_planes_equal_split_of_dy(dev, mode, has_bias, keep):
         gamma = torch.rand(H, device=dev) + 0.5
         beta = torch.randn(H, device=dev)
         seed = torch.tensor([1234], dtype=torch.int64, device=dev)
-        out, z, mean, rstd = C().ln_fwd(y, bias, res, gamma, beta, 1e-12, keep, seed, 5, False, True)
+        out, z, mean, rstd = C().ln_fwd(y, bias, res, gamma, beta, 1e-12, keep, seed, 5, False, True)[:4]
         dout = torch.randn_like(out)
         dz, dy, dg, db, dbias = C().ln_bwd(dout, z, mean, rstd, gamma, keep, seed, 5, False, True, has_bias,
                                           None, None, None)
@@ -355,7 +355,7 @@ def test_attn_bwd_planes_equal_split_of_dqkv(dev, mode, S, with_bias, keep, natu
         mb = torch.zeros(B, S, device=dev)
         mb[1, S - 9:] = -10000.0
         seed = torch.tensor([77], dtype=torch.int64, device=dev)
-        out, lse, dm = C().attn_fwd_x6(qkv, mb, nh, keep, seed, 2, bias)
+        out, lse, dm = C().attn_fwd_x6(qkv, mb, nh, keep, seed, 2, bias)[:3]
         dout = torch.randn_like(out)
         dqkv, db = C().attn_bwd_x6(dout, qkv, mb, out, lse, dm, nh, keep, bias, None, None, None)
         n = split_gemm.passes()
@@ -599,3 +599,50 @@ def test_piece_gemm_b16_layouts(dev):
     finally:
         ops.set_fp32_gemm('native')
     assert torch.equal(y0, y2) and torch.equal(y0, y3)
+
+
+def test_layernorm_writes_consumer_pieces(dev, monkeypatch):
+    """LayerNorm / embedding forward write the next piece GEMM's input pieces next to their
+    fp32 output (bit-identical to splitting it), and the consuming linear takes them instead
+    of a separate split pass (none runs in the layer's forward)."""
+    from hetseq_9cme_amd import ops
+    from hetseq_9cme_amd.models.bert import BertConfig, BertLayer
+    from hetseq_9cme_amd.ops import split_gemm
+    from hetseq_9cme_amd.ops._ext import C
+    ops.set_fp32_gemm('bf16x6')
+    try:
+        T, H = 300, 768
+        y = torch.randn(T, H, device=dev)
+        g = torch.rand(H, device=dev) + 0.5
+        b = torch.randn(H, device=dev)
+        seed = torch.tensor([9], dtype=torch.int64, device=dev)
+        out, _, _, _, pcs = C().ln_fwd(y, None, None, g, b, 1e-12, 0.9, seed, 3, False, True, 3)
+        ref = split_gemm.pieces(out)
+        assert torch.equal(pcs.view(torch.int16), ref.view(torch.int16))
+        ids = torch.randint(0, 100, (4, 75), device=dev)
+        wte, wpe, wtt = (torch.randn(100, H, device=dev), torch.randn(128, H, device=dev),
+                         torch.randn(2, H, device=dev))
+        out, _, _, _, pcs = C().embed_ln_fwd(ids, None, wte, wpe, wtt, g, b, 1e-12, 1.0, seed, 0, False, 3)
+        assert torch.equal(pcs.view(torch.int16), split_gemm.pieces(out.view(-1, H)).view(torch.int16))
+        # in a BERT layer: no split pass in the forward (LN -> FFN-up pieces hand-off)
+        torch.manual_seed(0)
+        monkeypatch.setattr(split_gemm, 'MIN_ROWS', {3: 0, 6: 0})
+        cfg = BertConfig(100, hidden_size=256, num_hidden_layers=1, num_attention_heads=4, intermediate_size=1024)
+        layer = BertLayer(cfg).to(dev)
+        x = torch.randn(2, 128, 256, device=dev)
+        calls = []
+        orig = split_gemm.pieces
+
+        def spy(*a, **k):
+            calls.append(a[0].shape)
+            return orig(*a, **k)
+        split_gemm.pieces = spy
+        try:
+            layer(x, torch.zeros(2, 128, device=dev))
+        finally:
+            split_gemm.pieces = orig
+        # only the layer input is split (no producer here): the attention output and the
+        # LayerNorm output come with their pieces
+        assert len(calls) == 1, calls
+    finally:
+        ops.set_fp32_gemm('native')

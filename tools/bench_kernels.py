@@ -77,7 +77,7 @@ def bench_ln(B, S, H=768):
     bias = torch.zeros(H, device='cuda')
     report('ln_fwd(bias+drop+res)', timeit(lambda: C().ln_fwd(x, bias, res, g, bt, 1e-12, 0.9, SEED, 0, False, True)),
            bytes_=4 * n * H * 4)
-    out, z, mean, rstd = C().ln_fwd(x, bias, res, g, bt, 1e-12, 0.9, SEED, 0, False, True)
+    out, z, mean, rstd = C().ln_fwd(x, bias, res, g, bt, 1e-12, 0.9, SEED, 0, False, True)[:4]
     dout = torch.randn_like(out)
     report('ln_bwd(+dy,+dbias)', timeit(lambda: C().ln_bwd(dout, z, mean, rstd, g, 0.9, SEED, 0, False, True, True,
                                                            None, None, None)), bytes_=4 * n * H * 4)

@@ -3,14 +3,16 @@
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it
 is launched by ``torch.distributed.run`` (one rank per GPU, RCCL).  Runs the real
 framework path -- synthetic NVIDIA-schema HDF5 shards -> native reader -> pinned
-staging on the HIP copy stream -> Controller.train_step (fused HIP kernels +
-hipBLASLt GEMMs, flat-buffer RCCL reducer, fused norm/clip/Adam) -- with
+staging on the HIP copy stream -> Controller.train_step (fused HIP kernels,
+hand-written bf16x6 piece GEMMs -- hipBLASLt only for the MLM decoder --, flat-buffer
+RCCL / xGMI reducer, fused norm/clip/Adam) -- with
 random-init BERT-base weights (no network: no corpus, no checkpoint).
 
 Config = BASELINE.json's: BERT-base (L12 H768 A12 V30522), seq 128, 20 masked
 positions per sequence, per-GPU batch 128 (weak scaling: global batch 128*N),
-Adam lr 1e-4 + warmup 10000 + wd 0.01, clip 25, fast stat sync, fp32 compute
-(the reference's precision).  W untimed warm-up steps, then exactly K timed steps
+Adam lr 1e-4 + warmup 10000 + wd 0.01, clip 25, fast stat sync, fp32-class compute
+(the reference's precision; ``--fp32-gemm bf16x6`` = fp32 GEMMs as six bf16 piece
+products, parity vs native fp32 over 300 updates in profiles/r3_parity_bert_base_300.md).  W untimed warm-up steps, then exactly K timed steps
 bracketed by barrier + device synchronize; the max over ranks is reported.
 """
 import argparse

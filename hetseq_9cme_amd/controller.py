@@ -315,6 +315,13 @@ class Controller(object):
             # [sample_size, nsentences, loss, nll_loss, ntokens, ooms] (+ xGMI error word)
             err = self.reducer.transport_error_async() if self.reducer.enabled else None
             fields = [acc_ss, acc_ns, 0.0, 0.0, acc_nt, float(ooms)] + ([0.0] if err is not None else [])
+            # --find-unused-parameters: the local used flags (host-known) ride in the same
+            # all-reduce; the optimizer consumes the summed flags on device (no host read)
+            used_at = None
+            if self.reducer.enabled and self.reducer.find_unused and hasattr(self.optimizer, 'device_used') \
+                    and not capturing:
+                used_at = len(fields)
+                fields += [1.0 if u else 0.0 for u in step_used]
             if capturing:
                 # no host->device copy inside a graph (it would keep reading a freed pinned
                 # buffer): the per-shape constants become fill nodes
@@ -332,6 +339,8 @@ class Controller(object):
                 dist_utils.all_reduce(vec)
             if err is not None:
                 self._transport_monitor.record(self._num_updates + 1, vec[6:7])
+            if used_at is not None:
+                self.optimizer.device_used = vec[used_at:used_at + len(step_used)]
             vec[2:4].div_(vec[0:1] * LN2)
             logging_output = {'sample_size': vec[0], 'nsentences': vec[1], 'loss': vec[2], 'nll_loss': vec[3],
                               'ntokens': vec[4], 'ooms': vec[5]}
@@ -373,8 +382,10 @@ class Controller(object):
                 opt.multiply_grads(pre)
             grad_norm = opt.clip_grad_norm(self.args.clip_norm)
             self._prev_grad_norm = grad_norm
-            # skip only params no rank used (locally unused ones got the reduced gradient)
-            opt.used_mask = self.reducer.global_used(step_used)
+            # skip only params no rank used (locally unused ones got the reduced gradient); on the
+            # fast-stat-sync path the flags were all-reduced with the stats (opt.device_used)
+            if getattr(opt, 'device_used', None) is None:
+                opt.used_mask = self.reducer.global_used(step_used)
             opt.step()
             ph('meters')
             self.set_num_updates(self.get_num_updates() + 1)

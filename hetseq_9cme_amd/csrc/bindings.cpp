@@ -98,6 +98,31 @@ void adam(Tensor p, Tensor g, Tensor m, Tensor v, OptT shadow, Tensor gscale, in
           (float)step_size, (float)wd_lr, hp_ptr(hp, 2), cur_stream(p));
 }
 
+void adam_masked(Tensor p, Tensor g, Tensor m, Tensor v, OptT shadow, Tensor gscale, Tensor table, Tensor used,
+                 Tensor steps, Tensor hp, double lr, double b1, double b2, double eps, double wd) {
+  check_f32(p, "param");
+  check_f32(g, "grad");
+  check_f32(m, "exp_avg");
+  check_f32(v, "exp_avg_sq");
+  TORCH_CHECK(g.numel() == p.numel() && m.numel() == p.numel() && v.numel() == p.numel(), "flat size mismatch");
+  const int64_t nparam = steps.numel();
+  TORCH_CHECK(steps.is_cuda() && steps.scalar_type() == torch::kInt32 && steps.is_contiguous(), "steps: int32 GPU");
+  TORCH_CHECK(used.is_cuda() && used.scalar_type() == torch::kFloat64 && used.is_contiguous() &&
+                  used.numel() == nparam, "used flags: contiguous f64 GPU tensor, one per parameter");
+  TORCH_CHECK(hp.is_cuda() && hp.scalar_type() == torch::kFloat32 && hp.numel() >= 2 * nparam, "hp: f32 [2*nparam]");
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == torch::kInt64 && table.dim() == 2 && table.size(1) == 3 &&
+                  table.is_contiguous(), "table: int64 [nblocks, 3]");
+  uint16_t* sh = nullptr;
+  if (has(shadow)) {
+    TORCH_CHECK(shadow->scalar_type() == torch::kBFloat16 && shadow->numel() == p.numel(), "bad bf16 shadow");
+    sh = reinterpret_cast<uint16_t*>(shadow->data_ptr());
+  }
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
+  hx_adam_masked(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), sh,
+                 gscale.data_ptr<float>(), table.data_ptr<int64_t>(), (int)table.size(0), used.data_ptr<double>(),
+                 steps.data_ptr<int>(), hp.data_ptr<float>(), (int)nparam, lr, b1, b2, (float)eps, wd, cur_stream(p));
+}
+
 void adadelta(Tensor p, Tensor g, Tensor sq, Tensor acc, Tensor gscale, int64_t start, int64_t end, double lr,
               double rho, double eps, double wd, OptT hp) {
   check_f32(p, "param");
@@ -826,6 +851,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hetseq_9cme_amd gfx950 (MI355X) kernels";
   m.def("grad_norm_clip", &grad_norm_clip);
   m.def("adam", &adam);
+  m.def("adam_masked", &adam_masked);
+  m.def("adam_mask_chunk", &hx_adam_mask_chunk);
   m.def("adadelta", &adadelta);
   m.def("ln_fwd", &ln_fwd, py::arg("y"), py::arg("bias"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
         py::arg("eps"), py::arg("keep_prob"), py::arg("seed"), py::arg("stream"), py::arg("drop_after"),

@@ -187,8 +187,9 @@ __device__ __forceinline__ uint2 pack4(const float (&x)[4]) {
   return make_uint2(hx::f2bf(x[0]) | ((uint32_t)hx::f2bf(x[1]) << 16),
                     hx::f2bf(x[2]) | ((uint32_t)hx::f2bf(x[3]) << 16));
 }
-template <int BM, int BN, int WM, int WN, int NPC, int NP, int BK, int NBUF, int EPI, int PIPE, int LAY = 0>
-__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_piece_k(Args g) {
+template <int BM, int BN, int WM, int WN, int NPC, int NP, int BK, int NBUF, int EPI, int PIPE, int LAY = 0,
+          int OCC = 1>
+__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_piece_k(Args g) {
   constexpr int NWM = BM / WM, NW = NWM * (BN / WN);
   constexpr int MB = WM / 32, NB = WN / 32;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
@@ -199,6 +200,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_piece_k(Args 
   constexpr int RPK = Img<BK>::RPK;
   static_assert(A_BYTES % 1024 == 0 && B_BYTES % 1024 == 0, "tile / DMA piece mismatch");
   static_assert(NBUF == 2 || NBUF == 3, "stages");
+  static_assert(OCC == 1 || NBUF * STAGE <= 80 * 1024, "two workgroups per CU need <= 80 KiB of LDS each");
   static_assert(JLO >= 1, "fewer DMA pieces than waves");
   static_assert(LAY == 0 || (NPC == 3 && BK == 16), "B16 layout: bf16x6, 16-deep stages");
   constexpr bool LA = LAY & 1, LB = LAY & 2;   // A / B operand in the B16 layout
@@ -385,6 +387,20 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_piece_k(Args 
       else dma_wait<0>();
       __syncthreads();
       cur = cur == 2 ? 0 : cur + 1;
+    }
+  } else if constexpr (PIPE == 4) {
+    // Two stages, two workgroups per CU (OCC 2, <= 80 KiB of LDS each): stage it + 1's DMA pieces
+    // are issued between stage it's MFMA passes and retired before the barrier that ends the
+    // step.  Latency the single in-flight stage cannot hide -- and one workgroup's epilogue
+    // stores -- are covered by the OTHER workgroup's MFMAs on the same SIMDs.
+    static_assert(BK == 16 && NBUF == 2, "two-stage interleaved variant: 16-deep stages, 2 buffers");
+    dma(0, 0);
+    dma_wait<0>();
+    __syncthreads();
+    for (int it = 0; it < nit; ++it) {
+      mma_dma(it & 1, it + 1 < nit ? it + 1 : -1, (it + 1) & 1);
+      dma_wait<0>();
+      __syncthreads();
     }
   } else if constexpr (PIPE == 1) {
     // Fragments of the stage being multiplied live in registers (two named sets, loop
@@ -740,12 +756,15 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void gemm_piece_k(Args 
 // cfg 3 (bf16x6): cfg 0's tile with the in-place register pipeline (PIPE 2)
 // cfg 4 (bf16x6): 256 x 128 tile, waves 4 x 2 of 64 x 64, BK 16, 3 stages, two fragment sets (PIPE 1)
 // cfg 5 (bf16x6): cfg 1's tile, PIPE 2;   cfg 6 (bf16x6): cfg 4's tile, PIPE 2
-constexpr int kCfgs = 7;
+// cfg 7 (bf16x6): 256 x 128 tile, 4 waves (2 x 2) of 128 x 64, BK 16, 2 stages (72 KiB), two
+//        workgroups per CU (PIPE 4): one workgroup's epilogue overlaps the other's MFMAs
+constexpr int kCfgs = 8;
 int cfg_bm(int) { return 256; }
 int cfg_bn(int c) { return (c == 0 || c == 3) ? 192 : (c == 1 || c == 5) ? 256 : 128; }
-int cfg_nwm(int c) { return (c == 1 || c == 5) ? 2 : 4; }
+int cfg_nwm(int c) { return (c == 1 || c == 5 || c == 7) ? 2 : 4; }
 
-template <int BM, int BN, int WM, int WN, int NPC, int NP, int BK, int NBUF, int EPI, int PIPE = 0, int LAY = 0>
+template <int BM, int BN, int WM, int WN, int NPC, int NP, int BK, int NBUF, int EPI, int PIPE = 0, int LAY = 0,
+          int OCC = 1>
 void launch_one(const Args& a, hipStream_t s) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int total = ((a.M + BM - 1) / BM) * (a.N / BN);
@@ -753,11 +772,12 @@ void launch_one(const Args& a, hipStream_t s) {
   const size_t smem = (size_t)NBUF * NPC * (BM + BN) * BK * 2;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_piece_k<BM, BN, WM, WN, NPC, NP, BK, NBUF, EPI, PIPE, LAY>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    (void)hipFuncSetAttribute(
+        reinterpret_cast<const void*>(&gemm_piece_k<BM, BN, WM, WN, NPC, NP, BK, NBUF, EPI, PIPE, LAY, OCC>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
-  gemm_piece_k<BM, BN, WM, WN, NPC, NP, BK, NBUF, EPI, PIPE, LAY><<<8 * per, NT, smem, s>>>(a);
+  gemm_piece_k<BM, BN, WM, WN, NPC, NP, BK, NBUF, EPI, PIPE, LAY, OCC><<<8 * per, NT, smem, s>>>(a);
 }
 
 static int pipe_mode() {
@@ -767,7 +787,9 @@ static int pipe_mode() {
 
 template <int NPC, int NP, int EPI, int PIPE, int LAY>
 void launch_lay(int cfg, const Args& a, hipStream_t s) {
-  if (cfg == 0)
+  if (cfg == 7)
+    launch_one<256, 128, 128, 64, NPC, NP, 16, 2, EPI, 4, LAY, 2>(a, s);
+  else if (cfg == 0)
     launch_one<256, 192, 64, 96, NPC, NP, 16, 3, EPI, PIPE, LAY>(a, s);
   else
     launch_one<256, 256, 128, 64, NPC, NP, 16, 3, EPI, PIPE, LAY>(a, s);
@@ -777,7 +799,7 @@ template <int NPC, int NP, int EPI>
 void launch_cfg(int cfg, int lay, const Args& a, hipStream_t s) {
   constexpr int BK = NPC == 3 ? 16 : 32, NBUF = NPC == 3 ? 3 : 2;
   if constexpr (NPC == 3) {
-    if (pipe_mode() == 3 && (cfg == 0 || cfg == 1)) {   // DMA pieces interleaved with the MFMA passes
+    if (cfg == 7 || (pipe_mode() == 3 && (cfg == 0 || cfg == 1))) {   // DMA pieces interleaved with the passes
       if (lay == 0) launch_lay<NPC, NP, EPI, 3, 0>(cfg, a, s);
       else if (lay == 1) launch_lay<NPC, NP, EPI, 3, 1>(cfg, a, s);
       else if (lay == 2) launch_lay<NPC, NP, EPI, 3, 2>(cfg, a, s);
@@ -823,8 +845,8 @@ int hx_gemm_split_plan(int M, int N, int K, int passes, int lay) {
   (void)M;
   if (const char* e = getenv("HX_GEMM_CFG")) {
     const int c = atoi(e);
-    if (c >= 0 && c < kCfgs && c != 8 && N % cfg_bn(c) == 0 && (c < 3 || passes == 6) &&
-        (!lay || c == 0 || c == 1 || ((c == 3 || c == 5) && lay == 3)))
+    if (c >= 0 && c < kCfgs && N % cfg_bn(c) == 0 && (c < 3 || passes == 6) &&
+        (!lay || c == 0 || c == 1 || c == 7 || ((c == 3 || c == 5) && lay == 3)))
       return c;
   }
   // measured at M = 16384, bf16x6 (tools/probe/gemm_layout_probe.py, profiles/r3_gemm_split.md):
@@ -845,7 +867,7 @@ int hx_gemm_split_weight_b16(int N, int passes) {
   static const bool on = !(getenv("HX_W_B16") && getenv("HX_W_B16")[0] == '0');
   if (!on || passes != 6 || N % 2304 == 0) return 0;
   const int c = hx_gemm_split_plan(1 << 14, N, 768, passes, 2);
-  return (c == 0 || c == 1) ? 1 : 0;
+  return (c == 0 || c == 1 || c == 7) ? 1 : 0;
 }
 
 int hx_gemm_split_colpart_rows(int M, int cfg) {
@@ -863,7 +885,8 @@ int hx_gemm_split_nt(const void* A, int64_t lda, int64_t a_ps, const void* B, in
   if (K % bk || npc * a_ps > lda || npc * b_ps > ldb) return -1;
   // lay bit 0 / bit 1: A / B operand in the B16 layout [rows][K / 16][3][16] (bf16x6, cfgs 0 1 3 5)
   // instead of [rows][npc][K]: one 16-deep k step of a row is 96 contiguous bytes
-  if (lay && (lay > 3 || npc != 3 || !(cfg == 0 || cfg == 1 || ((cfg == 3 || cfg == 5) && lay == 3)))) return -1;
+  if (lay && (lay > 3 || npc != 3 || !(cfg == 0 || cfg == 1 || cfg == 7 || ((cfg == 3 || cfg == 5) && lay == 3))))
+    return -1;
   Args a;
   a.A = (const uint16_t*)A;
   a.lda = lda;

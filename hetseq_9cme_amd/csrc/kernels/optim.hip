@@ -64,6 +64,19 @@ __global__ __launch_bounds__(NT) void grad_norm_finalize_k(const double* __restr
   }
 }
 
+// One Adam element update with every rounding spelled out (explicit fma / _rn ops, nothing
+// left to contraction), so every kernel that uses it -- the per-run kernel, the device-mask
+// kernel, with or without the bf16 shadow -- produces bitwise the same parameters.
+__device__ __forceinline__ void adam1(float& x, const float gg, float& m, float& v, float gs, float b1, float b2,
+                                      float ob1, float ob2, float eps, float step_size, float wd_lr) {
+  const float gr = __fmul_rn(gg, gs);
+  m = fmaf(m, b1, __fmul_rn(ob1, gr));
+  v = fmaf(v, b2, __fmul_rn(__fmul_rn(ob2, gr), gr));
+  const float denom = __fadd_rn(sqrtf(v), eps);
+  x = fmaf(-wd_lr, x, x);
+  x = fmaf(-step_size, __fdiv_rn(m, denom), x);
+}
+
 template <bool kShadow>
 __device__ __forceinline__ void adam4(float4& pp, const float4 gg, float4& mm, float4& vv, float gs, float b1,
                                       float b2, float ob1, float ob2, float eps, float step_size, float wd_lr) {
@@ -72,16 +85,7 @@ __device__ __forceinline__ void adam4(float4& pp, const float4 gg, float4& mm, f
   float* ma = &mm.x;
   float* va = &vv.x;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const float gr = ga[j] * gs;
-    ma[j] = ma[j] * b1 + ob1 * gr;
-    va[j] = va[j] * b2 + ob2 * gr * gr;
-    const float denom = sqrtf(va[j]) + eps;
-    float x = pa[j];
-    x = x - wd_lr * x;
-    x = x - step_size * (ma[j] / denom);
-    pa[j] = x;
-  }
+  for (int j = 0; j < 4; ++j) adam1(pa[j], ga[j], ma[j], va[j], gs, b1, b2, ob1, ob2, eps, step_size, wd_lr);
 }
 
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
@@ -139,14 +143,10 @@ __global__ __launch_bounds__(NT) void adam_k(float* __restrict__ p, const float*
     }
   }
   for (int64_t i = (n4 << 2) + blockIdx.x * (int64_t)NT + threadIdx.x; i < n; i += (int64_t)gridDim.x * NT) {
-    const float gr = g[i] * gs;
-    const float mi = m[i] * b1 + ob1 * gr;
-    const float vi = v[i] * b2 + ob2 * gr * gr;
+    float x = p[i], mi = m[i], vi = v[i];
+    adam1(x, g[i], mi, vi, gs, b1, b2, ob1, ob2, eps, step_size, wd_lr);
     m[i] = mi;
     v[i] = vi;
-    float x = p[i];
-    x = x - wd_lr * x;
-    x = x - step_size * (mi / (sqrtf(vi) + eps));
     p[i] = x;
     if (kShadow) shadow[i] = hx::f2bf(x);
   }
@@ -168,6 +168,57 @@ __global__ __launch_bounds__(NT) void adadelta_k(float* __restrict__ p, const fl
     p[i] = x - lr * delta;
     acc[i] = acc[i] * rho + (1.f - rho) * delta * delta;
     sq[i] = s;
+  }
+}
+
+// --find-unused-parameters without a host round trip: the per-parameter "used on some
+// rank" flags arrive as a slice of the all-reduced stats vector (f64 sums, > 0 = used).
+// adam_steps_k advances the per-parameter step counters ON DEVICE and writes each
+// parameter's (step size, wd * lr) -- 0-step parameters are skipped entirely, exactly the
+// reference's `if p.grad is None: continue` (hetseq/optim.py:186-189) -- and
+// adam_masked_k runs one block per <= kMaskChunk-element slice of ONE parameter (a static
+// table built once from the flat layout), so an unused parameter's blocks exit at once.
+constexpr int kMaskChunk = NT * 4 * 4;   // 4096 floats per block
+
+__global__ __launch_bounds__(NT) void adam_steps_k(int nparam, const double* __restrict__ used,
+                                                 int* __restrict__ steps, float* __restrict__ hp, double lr,
+                                                 double b1, double b2, double wd) {
+  for (int i = threadIdx.x; i < nparam; i += NT) {
+    const bool u = used[i] > 0.0;
+    const int t = steps[i] + (u ? 1 : 0);
+    steps[i] = t;
+    // same float64 arithmetic as the host path (optimizers.py _Adam._host_step)
+    const double ss = u ? lr * sqrt(1.0 - pow(b2, (double)t)) / (1.0 - pow(b1, (double)t)) : 0.0;
+    hp[2 * i] = (float)ss;
+    hp[2 * i + 1] = u ? (float)(wd * lr) : 0.f;
+  }
+}
+
+template <bool kShadow>
+__global__ __launch_bounds__(NT) void adam_masked_k(float* __restrict__ p, const float* __restrict__ g,
+                                                  float* __restrict__ m, float* __restrict__ v,
+                                                  uint16_t* __restrict__ shadow, const float* __restrict__ gscale,
+                                                  const int64_t* __restrict__ table, const double* __restrict__ used,
+                                                  const float* __restrict__ hp, float b1, float b2, float eps) {
+  const int64_t* row = table + 3 * (int64_t)blockIdx.x;   // (param, start, end): float offsets, 4-aligned
+  const int pi = (int)row[0];
+  if (!(used[pi] > 0.0)) return;
+  const float step_size = hp[2 * pi], wd_lr = hp[2 * pi + 1];
+  const float gs = gscale[0];
+  const float ob1 = 1.f - b1, ob2 = 1.f - b2;
+  const int64_t a = row[1] >> 2, e = row[2] >> 2;
+  float4* P = reinterpret_cast<float4*>(p);
+  const float4* G = reinterpret_cast<const float4*>(g);
+  float4* M = reinterpret_cast<float4*>(m);
+  float4* V = reinterpret_cast<float4*>(v);
+  for (int64_t i = a + threadIdx.x; i < e; i += NT) {
+    float4 pp = ntload(P + i), mm = ntload(M + i), vv = ntload(V + i);
+    const float4 gg = ntload(G + i);
+    adam4<kShadow>(pp, gg, mm, vv, gs, b1, b2, ob1, ob2, eps, step_size, wd_lr);
+    ntstore(pp, P + i); ntstore(mm, M + i); ntstore(vv, V + i);
+    if (kShadow)
+      reinterpret_cast<ushort4*>(shadow)[i] = make_ushort4(hx::f2bf(pp.x), hx::f2bf(pp.y), hx::f2bf(pp.z),
+                                                           hx::f2bf(pp.w));
   }
 }
 
@@ -201,4 +252,19 @@ void hx_adam(float* p, const float* g, float* m, float* v, uint16_t* shadow, con
 void hx_adadelta(float* p, const float* g, float* sq, float* acc, const float* gscale, int64_t n, float lr,
                  float rho, float eps, float wd, const float* hp, hipStream_t s) {
   adadelta_k<<<grid_for(n, 8192), NT, 0, s>>>(p, g, sq, acc, gscale, n, lr, rho, eps, wd, hp);
+}
+
+int hx_adam_mask_chunk() { return kMaskChunk; }
+
+void hx_adam_masked(float* p, const float* g, float* m, float* v, uint16_t* shadow, const float* gscale,
+                    const int64_t* table, int nblocks, const double* used, int* steps, float* hp, int nparam,
+                    double lr, double b1, double b2, float eps, double wd, hipStream_t s) {
+  adam_steps_k<<<1, NT, 0, s>>>(nparam, used, steps, hp, lr, b1, b2, wd);
+  if (nblocks <= 0) return;
+  if (shadow)
+    adam_masked_k<true><<<nblocks, NT, 0, s>>>(p, g, m, v, shadow, gscale, table, used, hp, (float)b1, (float)b2,
+                                                eps);
+  else
+    adam_masked_k<false><<<nblocks, NT, 0, s>>>(p, g, m, v, shadow, gscale, table, used, hp, (float)b1, (float)b2,
+                                                 eps);
 }

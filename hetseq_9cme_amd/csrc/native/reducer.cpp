@@ -18,8 +18,9 @@
 //    gloo for CPU runs and tests), or the hand-written intra-node xGMI two-shot kernel
 //    (csrc/kernels/xgmi_allreduce.hip) on a high-priority comm stream that waits for the
 //    producing stream(s) through HIP events;
-//  * single-process runs install no hooks: the used flags come from one scan of the
-//    gradient version counters after backward.
+//  * single-process runs keep the hooks (they record the used flags; nothing is reduced):
+//    gradient version counters cannot tell, since every slot is a view of the one flat
+//    buffer and views share their base's version counter.
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/hip/HIPStream.h>
@@ -54,9 +55,8 @@ inline void hip_ok(hipError_t e, const char* what) {
 class Reducer : public std::enable_shared_from_this<Reducer> {
  public:
   Reducer(Tensor grad_flat, std::vector<Tensor> params, std::vector<int64_t> offsets, std::vector<int64_t> bounds,
-          std::vector<int64_t> bucket_of, c10::intrusive_ptr<c10d::ProcessGroup> pg, int64_t world, bool hooked)
-      : grad_flat_(std::move(grad_flat)), params_(std::move(params)), pg_(std::move(pg)), world_(world),
-        hooked_(hooked) {
+          std::vector<int64_t> bucket_of, c10::intrusive_ptr<c10d::ProcessGroup> pg, int64_t world)
+      : grad_flat_(std::move(grad_flat)), params_(std::move(params)), pg_(std::move(pg)), world_(world) {
     const size_t P = params_.size();
     TORCH_CHECK(offsets.size() == P && bucket_of.size() == P, "reducer: one offset / bucket per parameter");
     TORCH_CHECK(bounds.size() >= 2, "reducer: at least one bucket");
@@ -77,7 +77,6 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     }
     enabled_ = world_ > 1 && pg_;
     used_.assign(P, 0);
-    versions_.assign(P, -1);
     reset_iteration();
     if (grad_flat_.is_cuda()) {
       c10::hip::HIPGuardMasqueradingAsCUDA guard(grad_flat_.device());
@@ -101,7 +100,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   };
 
   void install_hooks() {
-    if (!hooked_ || hooks_installed_) return;
+    if (hooks_installed_) return;
     std::weak_ptr<Reducer> self = weak_from_this();
     for (size_t i = 0; i < params_.size(); ++i) {
       TORCH_CHECK(params_[i].is_leaf() && params_[i].requires_grad(), "reducer: parameters must be leaves");
@@ -142,33 +141,13 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     std::lock_guard<std::mutex> lk(mu_);
     std::vector<bool> prev(used_.begin(), used_.end());
     reset_iteration();
-    if (!hooked_) {
-      for (size_t i = 0; i < params_.size(); ++i) {
-        const Tensor& g = params_[i].grad();
-        versions_[i] = g.defined() ? (int64_t)g.unsafeGetTensorImpl()->version_counter().current_version() : -1;
-      }
-      have_versions_ = true;
-    }
     return prev;
   }
 
-  // After each micro-batch's backward.  Without hooks, the parameters whose gradient
-  // version moved are the used ones.  When no hook fired (the loss reached no parameter),
+  // After each micro-batch's backward.  When no hook fired (the loss reached no parameter),
   // finalize here so this rank still joins every bucket collective.
   void after_backward() {
     std::lock_guard<std::mutex> lk(mu_);
-    if (!hooked_ && have_versions_) {
-      for (size_t i = 0; i < params_.size(); ++i) {
-        const Tensor& g = params_[i].grad();
-        if (!g.defined()) continue;
-        const int64_t v = (int64_t)g.unsafeGetTensorImpl()->version_counter().current_version();
-        if (versions_[i] < 0 || v != versions_[i]) {
-          used_[i] = 1;
-          adopt((int)i, params_[i]);
-        }
-      }
-      have_versions_ = false;
-    }
     if (!callback_queued_) {
       callback_queued_ = true;
       finalize_locked();
@@ -317,15 +296,12 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::vector<int> bucket_of_, nparams_, pending_;
   c10::intrusive_ptr<c10d::ProcessGroup> pg_;
   int64_t world_;
-  bool hooked_;
   bool hooks_installed_ = false;
   bool enabled_ = false;
   bool sync_ = true;
   bool callback_queued_ = false;
-  bool have_versions_ = false;
   int nb_ = 0, launched_ = 0;
   std::vector<uint8_t> used_;
-  std::vector<int64_t> versions_;
   std::vector<c10::intrusive_ptr<c10d::Work>> works_;
   void* xar_ = nullptr;
   hipStream_t comm_ = nullptr;
@@ -335,11 +311,11 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
 
 std::shared_ptr<Reducer> make_reducer(Tensor grad_flat, std::vector<Tensor> params, std::vector<int64_t> offsets,
                                       std::vector<int64_t> bounds, std::vector<int64_t> bucket_of,
-                                      py::object process_group, int64_t world, bool hooked) {
+                                      py::object process_group, int64_t world) {
   c10::intrusive_ptr<c10d::ProcessGroup> pg;
   if (!process_group.is_none()) pg = process_group.cast<c10::intrusive_ptr<c10d::ProcessGroup>>();
   auto r = std::make_shared<Reducer>(std::move(grad_flat), std::move(params), std::move(offsets), std::move(bounds),
-                                     std::move(bucket_of), std::move(pg), world, hooked);
+                                     std::move(bucket_of), std::move(pg), world);
   r->install_hooks();
   return r;
 }
@@ -353,7 +329,7 @@ void set_side_stream(int64_t handle) {
 void register_reducer(py::module& m) {
   py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
       .def(py::init(&make_reducer), py::arg("grad_flat"), py::arg("params"), py::arg("offsets"), py::arg("bounds"),
-           py::arg("bucket_of"), py::arg("process_group"), py::arg("world"), py::arg("hooked"))
+           py::arg("bucket_of"), py::arg("process_group"), py::arg("world"))
       // the GIL is released wherever a call may wait for a collective or run torch ops whose
       // tensors' Python owners the collectives' worker threads may need to release
       .def("prepare", &Reducer::prepare, py::call_guard<py::gil_scoped_release>())

@@ -16,9 +16,9 @@ GIL-free C++ reader, each producing one collated batch in (pinned) host memory,
 ``prefetch`` batches ahead -- instead of torch's DataLoader with per-sample
 ``__getitem__`` in worker processes.  Other datasets keep the DataLoader path.
 """
+import abc
 import concurrent.futures as cf
 import itertools
-import math
 import os
 
 import numpy as np
@@ -28,50 +28,69 @@ from .data_utils import numpy_seed
 
 
 class CountingIterator(object):
+    """Iterator over ``iterable`` that knows how many items have been consumed
+    (``count``, starting at ``start`` when resuming mid-epoch).  Same contract as the
+    reference's (hetseq/data/iterators.py:10-40: ``len`` = start + len(iterable),
+    ``has_next``, ``skip``); written as a plain stateful iterator."""
+
     def __init__(self, iterable, start=0):
         self.iterable = iterable
         self.count = start
-        self.itr = iter(self)
         self.len = start + len(iterable)
+        self._it = iter(iterable)
 
     def __len__(self):
         return self.len
 
     def __iter__(self):
-        for x in self.iterable:
-            self.count += 1
-            yield x
+        return self
 
     def __next__(self):
-        return next(self.itr)
+        item = next(self._it)
+        self.count += 1
+        return item
 
     def has_next(self):
-        return self.count < len(self)
+        return self.count < self.len
 
     def skip(self, num_to_skip):
-        next(itertools.islice(self.itr, num_to_skip, num_to_skip), None)
+        """Consume ``num_to_skip`` items (fewer if the iterable runs out)."""
+        for _ in range(num_to_skip):
+            try:
+                next(self)
+            except StopIteration:
+                break
         return self
 
 
-class EpochBatchIterating(object):
+class EpochBatchIterating(abc.ABC):
+    """Interface of an epoch-aware batch iterator (the reference's base class,
+    hetseq/data/iterators.py:43-64)."""
+
+    @abc.abstractmethod
     def __len__(self):
-        raise NotImplementedError
+        pass
 
+    @abc.abstractmethod
     def next_epoch_itr(self, shuffle=True, fix_batches_to_gpus=False):
-        raise NotImplementedError
+        pass
 
+    @abc.abstractmethod
     def end_of_epoch(self):
-        raise NotImplementedError
+        pass
 
     @property
+    @abc.abstractmethod
     def iterations_in_epoch(self):
-        raise NotImplementedError
+        pass
 
+    @abc.abstractmethod
     def state_dict(self):
-        raise NotImplementedError
+        pass
 
+    @abc.abstractmethod
     def load_state_dict(self, state_dict):
-        raise NotImplementedError
+        pass
 
 
 class BatchReaderLoader(object):
@@ -177,27 +196,24 @@ class EpochBatchIterator(EpochBatchIterating):
                                                                 offset=itr_pos)
 
     def shard_batches(self, epoch, shuffle, fix_batches_to_gpus=False):
-        """The list of index batches this shard consumes in ``epoch`` (exposed for tests)."""
-        def shuffle_batches(batches, seed):
-            with numpy_seed(seed):
-                np.random.shuffle(batches)
-            return batches
+        """The list of index batches this shard consumes in ``epoch`` (exposed for tests).
 
+        Order contract (reference hetseq/data/iterators.py:166-195, kept bit for bit so a
+        run resumes and shards exactly as the reference does): the frozen batch list is
+        permuted by ``np.random.shuffle`` under seed ``seed + epoch`` -- the same on every
+        rank -- then dealt round-robin; a prefetching dataset with
+        ``fix_batches_to_gpus`` instead keeps the global order and permutes each shard
+        under ``seed + epoch + shard_id``."""
+        per_shard = not self._supports_prefetch or not fix_batches_to_gpus
+        order = list(self.frozen_batches)
+        if shuffle and per_shard:
+            _seeded_shuffle(order, self.seed + epoch)
+        mine = _deal(order, self.num_shards, self.shard_id, fill=[])
         if self._supports_prefetch:
-            batches = self.frozen_batches
-            if shuffle and not fix_batches_to_gpus:
-                batches = shuffle_batches(list(batches), self.seed + epoch)
-            batches = list(ShardedIterator(batches, self.num_shards, self.shard_id, fill_value=[]))
-            self.dataset.prefetch([i for s in batches for i in s])
-            if shuffle and fix_batches_to_gpus:
-                batches = shuffle_batches(batches, self.seed + epoch + self.shard_id)
-        else:
-            if shuffle:
-                batches = shuffle_batches(list(self.frozen_batches), self.seed + epoch)
-            else:
-                batches = self.frozen_batches
-            batches = list(ShardedIterator(batches, self.num_shards, self.shard_id, fill_value=[]))
-        return batches
+            self.dataset.prefetch([i for b in mine for i in b])
+            if shuffle and not per_shard:
+                _seeded_shuffle(mine, self.seed + epoch + self.shard_id)
+        return mine
 
     def _get_iterator_for_epoch(self, epoch, shuffle, fix_batches_to_gpus=False, offset=0):
         batches = self.shard_batches(epoch, shuffle, fix_batches_to_gpus)
@@ -216,14 +232,33 @@ class EpochBatchIterator(EpochBatchIterating):
         return CountingIterator(loader, start=offset)
 
 
+def _seeded_shuffle(items, seed):
+    """In-place ``np.random.shuffle`` under a temporary global numpy seed."""
+    with numpy_seed(seed):
+        np.random.shuffle(items)
+    return items
+
+
+def _deal(items, num_shards, shard_id, fill=None):
+    """Round-robin shard ``shard_id`` of ``items``: items shard_id, shard_id + W, ...,
+    padded with ``fill`` to ceil(len / W) entries (every shard the same length)."""
+    if not 0 <= shard_id < num_shards:
+        raise ValueError('shard_id must be between 0 and num_shards')
+    n = -(-len(items) // num_shards)
+    mine = list(items[shard_id::num_shards])
+    return mine + [fill] * (n - len(mine))
+
+
 class GroupedIterator(object):
-    """Chunks ``chunk_size`` consecutive items (one optimizer step of --update-freq)."""
+    """Lists of ``chunk_size`` consecutive items: the micro-batches of one optimizer step
+    under --update-freq (the last group may be short).  ``offset`` = groups already
+    consumed when resuming from a partly consumed CountingIterator."""
 
     def __init__(self, iterable, chunk_size):
-        self._len = int(math.ceil(len(iterable) / float(chunk_size)))
-        self.offset = int(math.ceil(getattr(iterable, 'count', 0) / float(chunk_size)))
         self.itr = iterable
         self.chunk_size = chunk_size
+        self._len = -(-len(iterable) // chunk_size)
+        self.offset = -(-getattr(iterable, 'count', 0) // chunk_size)
 
     def __len__(self):
         return self._len
@@ -232,34 +267,24 @@ class GroupedIterator(object):
         return self
 
     def __next__(self):
-        chunk = []
-        try:
-            for _ in range(self.chunk_size):
-                chunk.append(next(self.itr))
-        except StopIteration as e:
-            if len(chunk) == 0:
-                raise e
+        chunk = list(itertools.islice(self.itr, self.chunk_size))
+        if not chunk:
+            raise StopIteration
         return chunk
 
 
 class ShardedIterator(object):
-    """Rank ``shard_id`` of ``num_shards`` round-robin shards, padded with ``fill_value``."""
+    """Iterator over shard ``shard_id`` of ``num_shards`` (see :func:`_deal`)."""
 
     def __init__(self, iterable, num_shards, shard_id, fill_value=None):
-        if shard_id < 0 or shard_id >= num_shards:
-            raise ValueError('shard_id must be between 0 and num_shards')
-        self._sharded_len = len(iterable) // num_shards
-        if len(iterable) % num_shards > 0:
-            self._sharded_len += 1
-        self.itr = itertools.zip_longest(range(self._sharded_len),
-                                         itertools.islice(iterable, shard_id, len(iterable), num_shards),
-                                         fillvalue=fill_value)
+        self._items = _deal(list(iterable), num_shards, shard_id, fill_value)
+        self._it = iter(self._items)
 
     def __len__(self):
-        return self._sharded_len
+        return len(self._items)
 
     def __iter__(self):
         return self
 
     def __next__(self):
-        return next(self.itr)[1]
+        return next(self._it)

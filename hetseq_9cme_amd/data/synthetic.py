@@ -30,12 +30,35 @@ def write_bert_config(path, **overrides):
     return path
 
 
-def make_bert_samples(n, seq_len, max_pred, vocab_size, rng, pad_frac=0.0):
-    ids = rng.randint(5, vocab_size, size=(n, seq_len)).astype(np.int32)
+def _zipf_tokens(rng, size, vocab_size):
+    r = np.minimum(rng.zipf(1.3, size=size), vocab_size - 5)
+    return (r + 4).astype(np.int64)
+
+
+def make_bert_samples(n, seq_len, max_pred, vocab_size, rng, pad_frac=0.0, pattern=None):
+    """``pattern=None``: uniform random tokens (shape-only data, nothing to learn).
+    ``pattern='bigram'``: a learnable corpus -- Zipf unigrams, each token followed by a
+    fixed successor with probability 0.7, and the NSP label says whether segment B
+    continues segment A's chain -- so loss curves actually move (parity runs)."""
+    if pattern == 'bigram':
+        split = rng.randint(seq_len // 4, 3 * seq_len // 4, size=n)
+        nsp = rng.randint(0, 2, size=n).astype(np.int32)
+        t = np.zeros((n, seq_len), dtype=np.int64)
+        t[:, 1] = _zipf_tokens(rng, n, vocab_size)
+        for j in range(2, seq_len):
+            succ = (t[:, j - 1] * 7919 + 13) % (vocab_size - 5) + 5
+            fresh = _zipf_tokens(rng, n, vocab_size)
+            keep = rng.rand(n) < 0.7
+            brk = (j == split) & (nsp == 0)        # "random next sentence": the chain restarts
+            t[:, j] = np.where(keep & ~brk, succ, fresh)
+        ids = t.astype(np.int32)
+    else:
+        ids = rng.randint(5, vocab_size, size=(n, seq_len)).astype(np.int32)
+        split = rng.randint(seq_len // 4, 3 * seq_len // 4, size=n)   # (draw order kept: same data as before)
+        nsp = None
     ids[:, 0] = 2  # [CLS]
     mask = np.ones((n, seq_len), dtype=np.int32)
     seg = np.zeros((n, seq_len), dtype=np.int32)
-    split = rng.randint(seq_len // 4, 3 * seq_len // 4, size=n)
     for i in range(n):
         seg[i, split[i]:] = 1
         if pad_frac > 0:
@@ -52,20 +75,22 @@ def make_bert_samples(n, seq_len, max_pred, vocab_size, rng, pad_frac=0.0):
         pos[i, :k] = p
         mids[i, :k] = ids[i, p]
         ids[i, p] = 4  # [MASK]
-    nsp = rng.randint(0, 2, size=n).astype(np.int32)
+    if nsp is None:
+        nsp = rng.randint(0, 2, size=n).astype(np.int32)
     return ids, mask, seg, pos, mids, nsp
 
 
 def write_synthetic_bert_shards(out_dir, n_files=2, samples_per_file=256, seq_len=128, max_pred=20,
-                                vocab_size=30522, seed=1234, split='train', pad_frac=0.0):
-    """Write ``n_files`` shards named ``{split}_shard_{k}.hdf5`` into ``out_dir``."""
+                                vocab_size=30522, seed=1234, split='train', pad_frac=0.0, pattern=None):
+    """Write ``n_files`` shards named ``{split}_shard_{k}.hdf5`` into ``out_dir``
+    (``pattern``: see :func:`make_bert_samples`)."""
     from .. import _data_native
     os.makedirs(out_dir, exist_ok=True)
     rng = np.random.RandomState(seed)
     paths = []
     for k in range(n_files):
         ids, mask, seg, pos, mids, nsp = make_bert_samples(samples_per_file, seq_len, max_pred, vocab_size, rng,
-                                                           pad_frac)
+                                                           pad_frac, pattern)
         p = os.path.join(out_dir, '{}_shard_{:03d}.hdf5'.format(split, k))
         _data_native.write_bert_shard(p, ids, mask, seg, pos, mids, nsp)
         paths.append(p)

@@ -221,11 +221,54 @@ class _Adam(_Optimizer):
             'amsgrad': False,
         }
 
+    # --find-unused-parameters under data parallelism: the controller sets this, per update, to
+    # the all-reduced used flags (f64 device slice of the stats vector, > 0 = some rank used the
+    # parameter).  ``step`` then skips unused parameters and advances the per-parameter step
+    # counters ON DEVICE (``_steps_dev``) -- no host read of the flags.
+    device_used = None
+    _steps_dev = None
+    _mask_table = None
+
+    def _device_steps(self):
+        if self._steps_dev is None:
+            self._steps_dev = torch.tensor(self.steps, dtype=torch.int32, device=self.device)
+            self._mask_hp = torch.zeros(2 * len(self.steps), dtype=torch.float32, device=self.device)
+        return self._steps_dev
+
+    def _pull_steps(self):
+        """Device step counters -> host list (one sync; checkpointing / switching paths)."""
+        if self._steps_dev is not None:
+            self.steps = [int(t) for t in self._steps_dev.tolist()]
+            self._steps_dev = None
+
+    def _masked_table(self):
+        """(param, start, end) rows, one per <= chunk-float slice of one parameter (ends rounded
+        up to 4 floats; the flat layout's 64-float alignment keeps that inside the padding)."""
+        if self._mask_table is None:
+            chunk = ops.C().adam_mask_chunk()
+            rows = []
+            for i in range(len(self.flat.params)):
+                s, e = self.flat.param_range(i)
+                e = (e + 3) // 4 * 4
+                for a in range(s, e, chunk):
+                    rows.append((i, a, min(e, a + chunk)))
+            self._mask_table = torch.tensor(rows, dtype=torch.int64, device=self.device).reshape(-1, 3)
+        return self._mask_table
+
     def step(self, closure=None):
         g = self.param_groups[0]
         beta1, beta2 = g['betas']
         eps, wd, lr = g['eps'], g['weight_decay'], self._lr
         self._fold_host_scale()
+        if self.device_used is not None:
+            used, self.device_used = self.device_used, None
+            if self.use_kernels:
+                ops.C().adam_masked(self.flat.param_flat, self.flat.grad_flat, self.exp_avg, self.exp_avg_sq,
+                                    self.bf16_shadow, self._gscale, self._masked_table(),
+                                    used.reshape(-1).to(torch.float64).contiguous(), self._device_steps(),
+                                    self._mask_hp, float(lr), float(beta1), float(beta2), float(eps), float(wd))
+                return
+            self.used_mask = [bool(u > 0) for u in used.reshape(-1).tolist()]   # CPU reference path
         runs = self._host_step()
         for r, (start, end, t) in enumerate(runs):
             bc1 = 1 - beta1 ** t
@@ -254,6 +297,7 @@ class _Adam(_Optimizer):
         """Host half of an update: advance the step counters, compute this update's
         hyper-parameters and (graph mode) write them to the device buffer.  A replayed
         graph calls only this; ``step`` calls it and then launches the kernels."""
+        self._pull_steps()
         g = self.param_groups[0]
         beta1, beta2 = g['betas']
         lr, wd = self._lr, g['weight_decay']
@@ -291,6 +335,7 @@ class _Adam(_Optimizer):
         return runs
 
     def _param_state(self, i):
+        self._pull_steps()
         if self.steps[i] == 0:
             return None
         s, e = self.flat.param_range(i)
@@ -302,6 +347,7 @@ class _Adam(_Optimizer):
         }
 
     def _load_param_state(self, i, st):
+        self._pull_steps()
         s, e = self.flat.param_range(i)
         self.steps[i] = int(st['step'])
         self.exp_avg[s:e].copy_(st['exp_avg'].reshape(-1).to(self.exp_avg))

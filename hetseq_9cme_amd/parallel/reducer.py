@@ -101,17 +101,18 @@ class GradReducer(object):
             for i in idxs:
                 self.bucket_of[i] = b
         self.xgmi = None
-        # only a multi-rank reducer needs to act DURING backward (bucket launches overlapped
-        # with it): C++ hooks on every parameter.  A single process finds the used parameters
-        # and adopts their gradients in one scan after backward instead.
-        self._hooked = self.world_size > 1
+        # C++ post-accumulate hooks on every parameter: they record which parameters this
+        # backward reached (and, multi-rank, launch buckets as they fill).  A single process used
+        # to infer the used set from gradient version counters after backward, but every slot is
+        # a view of ONE flat buffer and views share the version counter, so any write marked
+        # every parameter with a defined gradient as used -- e.g. the NER pooler (never reached)
+        # was stepped from its second update on, while the reference never steps it.
         pg = None
         if self.world_size > 1:
             pg = process_group if process_group is not None else dist.group.WORLD
         bounds = [b[0] for b in self.buckets] + [flat.numel]
         self._native = C().Reducer(flat.grad_flat, list(flat.params), list(flat.offsets), bounds,
-                                   [self.bucket_of[i] for i in range(len(flat.params))], pg, self.world_size,
-                                   self._hooked)
+                                   [self.bucket_of[i] for i in range(len(flat.params))], pg, self.world_size)
         self._enabled = self.world_size > 1
         if self.enabled and broadcast_params:
             dist.broadcast(flat.param_flat, src=0, group=self.group)

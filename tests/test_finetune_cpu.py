@@ -142,3 +142,8 @@ def test_ner_data_parallel_unused_params(tmp_path):
     assert c2['optimizer_history'][-1]['num_updates'] == 3
     for k, v in c1['model'].items():
         torch.testing.assert_close(c2['model'][k], v, rtol=1e-4, atol=1e-5, msg=k)
+    # the used flags ride in the stats all-reduce (device path): parameters no rank used (the
+    # pooler) have no optimizer state, the others were stepped 3 times -- as with host flags
+    s2, s1 = c2['last_optimizer_state']['state'], c1['last_optimizer_state']['state']
+    assert sorted(s2) == sorted(s1) and len(s1) < len(c1['model'])
+    assert all(int(s2[k]['step']) == 3 for k in s2)

@@ -496,7 +496,7 @@ def test_wgrad_split_pipeline_variants(dev, T, monkeypatch):
         ops.set_fp32_gemm('native')
 
 
-@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 7])
 def test_piece_gemm_every_cfg(dev, cfg, monkeypatch):
     """Every tile / pipeline configuration of the LDS-DMA piece GEMM (HX_GEMM_CFG) in bf16x6:
     forward and beta = 1 accumulation against fp64, rows not a multiple of the 256-row tile,
@@ -517,7 +517,7 @@ def test_piece_gemm_every_cfg(dev, cfg, monkeypatch):
         y = C().gemm_split(ap, wf, 6)
         acc = c0.clone()
         C().gemm_split(ap, wf, 6, acc, True)
-        if cfg in (0, 1):   # and the B16 weight layout (B operand) on the tiles that read it
+        if cfg in (0, 1, 7):   # and the B16 weight layout (B operand) on the tiles that read it
             wb = wf.view(N, 3, K // 16, 16).permute(0, 2, 1, 3).contiguous().view(N, -1)
             yb = C().gemm_split(ap, wb, 6, None, False, 2)
             assert torch.equal(y, yb)
@@ -530,14 +530,16 @@ def test_piece_gemm_every_cfg(dev, cfg, monkeypatch):
     assert e < 1.5e-6, e
 
 
-@pytest.mark.parametrize('mode', ['bf16x6', 'bf16x3'])
-def test_gemm_gelu_epilogues(dev, mode):
+@pytest.mark.parametrize('mode,cfg', [('bf16x6', None), ('bf16x3', None), ('bf16x6', '7')])
+def test_gemm_gelu_epilogues(dev, mode, cfg, monkeypatch):
     """FFN epilogues of the piece GEMM against fp64: bias + GELU (pre-activation u and the
     pieces of gelu(u)), and the GELU backward (pieces of dh * gelu'(u) and its column sums =
     the FFN-up bias gradient), with rows that are not a multiple of the tile."""
     from hetseq_9cme_amd import ops
     from hetseq_9cme_amd.ops import split_gemm as sg
     from hetseq_9cme_amd.ops._ext import C
+    if cfg is not None:
+        monkeypatch.setenv('HX_GEMM_CFG', cfg)   # e.g. the two-workgroups-per-CU tile
     g = torch.Generator(device='cpu').manual_seed(31)
     T, H, I = 300, 256, 768
     x = torch.randn(T, H, generator=g).to(dev)

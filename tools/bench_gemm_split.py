@@ -47,7 +47,7 @@ def main():
     T = a.tokens
     g = torch.Generator(device='cpu').manual_seed(0)
     cfgs = [int(c) for c in a.cfgs.split(',')]
-    bn = {0: 192, 1: 256, 2: 128}
+    bn = {0: 192, 1: 256, 2: 128, 7: 128}
     for passes in [int(p) for p in a.passes.split(',')]:
         ops.set_fp32_gemm('bf16x{}'.format(passes))
         # (name, n_in, n_out): forward y[T, n_out] = x W^T; dgrad dx[T, n_in] = dy W
@@ -87,14 +87,14 @@ def main():
             if name == 'up':
                 # fused epilogues vs the two-kernel path
                 b1 = (torch.randn(n_out, generator=g) * 0.1).cuda()
-                u, hp = C().gemm_split_gelu(xs, wf, passes, b1)
+                u, hp = sg.gemm_gelu(xs, wf, b1)
                 y1 = sg.gemm(xs, wf)
                 hp_ref = sg.act_pieces(y1, b1, 'gelu')
                 e_u = relerr(u, y1.double() + b1.double(), y1.double().abs() + b1.double().abs())
                 hv = sum(hp.view(T, -1, n_out)[:, p].float().double() for p in range(sg.npieces()))
                 hr = sum(hp_ref.view(T, -1, n_out)[:, p].float().double() for p in range(sg.npieces()))
                 e_h = relerr(hv, hr, hr.abs() + 1e-3)
-                t_g = timeit(lambda: C().gemm_split_gelu(xs, wf, passes, b1))
+                t_g = timeit(lambda: sg.gemm_gelu(xs, wf, b1))
                 t_ref = timeit(lambda: sg.act_pieces(sg.gemm(xs, wf), b1, 'gelu'))
                 print('x{} up+gelu fused {:7.1f} us vs gemm+bias_act_planes {:7.1f} us | err u {:.2e} h {:.2e}'.format(
                     passes, t_g, t_ref, e_u, e_h), flush=True)
@@ -103,14 +103,14 @@ def main():
                 dy2 = (torch.rand(T, n_in, generator=g) * 2 - 1).cuda()
                 dy2s = sg.pieces(dy2)
                 _, w2t = sg.weight_pieces(W2)
-                tp, db = C().gemm_split_dgelu(dy2s, w2t, passes, u, None, None)
+                tp, db = sg.gemm_dgelu(dy2s, w2t, u, None, None)
                 dh = sg.gemm(dy2s, w2t)
                 tp_ref, db_ref = sg.act_grad_pieces(dh, u, None, 'gelu')
                 tv = sum(tp.view(T, -1, n_out)[:, p].float().double() for p in range(sg.npieces()))
                 tr = sum(tp_ref.view(T, -1, n_out)[:, p].float().double() for p in range(sg.npieces()))
                 e_t = relerr(tv, tr, tr.abs() + 1e-3)
                 e_db = relerr(db, db_ref.double(), db_ref.double().abs() + 1e-2)
-                t_dg = timeit(lambda: C().gemm_split_dgelu(dy2s, w2t, passes, u, None, None))
+                t_dg = timeit(lambda: sg.gemm_dgelu(dy2s, w2t, u, None, None))
                 t_dref = timeit(lambda: sg.act_grad_pieces(sg.gemm(dy2s, w2t), u, None, 'gelu'))
                 print('x{} down-dgrad+dgelu fused {:7.1f} us vs gemm+bias_act_planes {:7.1f} us | err t {:.2e} '
                       'dbias {:.2e}'.format(passes, t_dg, t_dref, e_t, e_db), flush=True)

@@ -33,8 +33,8 @@ def main():
         ref = x.double() @ W.double().t()
         sc = x.double().abs() @ W.double().abs().t()
         fl = 2.0 * T * n_in * n_out * 6
-        for cfg in (0, 1, 2):
-            if n_out % {0: 192, 1: 256, 2: 128}[cfg]:
+        for cfg in [int(c) for c in os.environ.get('CFGS', '0,1,2,7').split(',')]:
+            if n_out % {0: 192, 1: 256, 2: 128, 7: 128}[cfg]:
                 continue
             os.environ['HX_GEMM_CFG'] = str(cfg)
             line = '{:5s} cfg {}'.format(name, cfg)

@@ -70,11 +70,12 @@ class Controller(object):
         self.flat = FlatParamSpace(model, self.device, contiguous_groups=groups)
         if getattr(args, 'precision', 'fp32') == 'bf16' and self.cuda:
             self.flat.enable_bf16_shadow()
-        use_reducer = self.world_size > 1 and not getattr(args, 'use_bmuf', False)
+        force = bool(getattr(args, 'force_reducer', False))
+        use_reducer = (self.world_size > 1 or force) and not getattr(args, 'use_bmuf', False)
         self.reducer = GradReducer(self.flat, bucket_cap_mb=args.bucket_cap_mb,
                                    find_unused_parameters=getattr(args, 'find_unused_parameters', False),
                                    broadcast_params=use_reducer,
-                                   bucket_peer_mb=getattr(args, 'bucket_peer_mb', 0.0))
+                                   bucket_peer_mb=getattr(args, 'bucket_peer_mb', 0.0), force=force)
         if not use_reducer:
             self.reducer.enabled = False
         elif getattr(args, 'allreduce_impl', 'rccl') == 'xgmi':

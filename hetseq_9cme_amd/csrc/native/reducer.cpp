@@ -55,8 +55,9 @@ inline void hip_ok(hipError_t e, const char* what) {
 class Reducer : public std::enable_shared_from_this<Reducer> {
  public:
   Reducer(Tensor grad_flat, std::vector<Tensor> params, std::vector<int64_t> offsets, std::vector<int64_t> bounds,
-          std::vector<int64_t> bucket_of, c10::intrusive_ptr<c10d::ProcessGroup> pg, int64_t world)
-      : grad_flat_(std::move(grad_flat)), params_(std::move(params)), pg_(std::move(pg)), world_(world) {
+          std::vector<int64_t> bucket_of, c10::intrusive_ptr<c10d::ProcessGroup> pg, int64_t world, bool force)
+      : grad_flat_(std::move(grad_flat)), params_(std::move(params)), pg_(std::move(pg)), world_(world),
+        force_(force) {
     const size_t P = params_.size();
     TORCH_CHECK(offsets.size() == P && bucket_of.size() == P, "reducer: one offset / bucket per parameter");
     TORCH_CHECK(bounds.size() >= 2, "reducer: at least one bucket");
@@ -75,7 +76,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
       TORCH_CHECK(offsets[i] >= 0 && offsets[i] + p.numel() <= grad_flat_.numel(), "reducer: slot out of range");
       slots_.push_back(grad_flat_.narrow(0, offsets[i], p.numel()).view(p.sizes()));
     }
-    enabled_ = world_ > 1 && pg_;
+    enabled_ = (world_ > 1 || force_) && pg_;
     used_.assign(P, 0);
     reset_iteration();
     if (grad_flat_.is_cuda()) {
@@ -200,7 +201,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   // --use-bmuf: hooks keep adopting slots / recording used flags, nothing is reduced
   void set_enabled(bool on) {
     std::lock_guard<std::mutex> lk(mu_);
-    enabled_ = on && world_ > 1 && pg_;
+    enabled_ = on && (world_ > 1 || force_) && pg_;
   }
 
   int num_buckets() const { return nb_; }
@@ -296,6 +297,7 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   std::vector<int> bucket_of_, nparams_, pending_;
   c10::intrusive_ptr<c10d::ProcessGroup> pg_;
   int64_t world_;
+  bool force_ = false;   // reduce even in a one-rank group (tests drive the RCCL stream path on one GPU)
   bool hooks_installed_ = false;
   bool enabled_ = false;
   bool sync_ = true;
@@ -311,11 +313,11 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
 
 std::shared_ptr<Reducer> make_reducer(Tensor grad_flat, std::vector<Tensor> params, std::vector<int64_t> offsets,
                                       std::vector<int64_t> bounds, std::vector<int64_t> bucket_of,
-                                      py::object process_group, int64_t world) {
+                                      py::object process_group, int64_t world, bool force) {
   c10::intrusive_ptr<c10d::ProcessGroup> pg;
   if (!process_group.is_none()) pg = process_group.cast<c10::intrusive_ptr<c10d::ProcessGroup>>();
   auto r = std::make_shared<Reducer>(std::move(grad_flat), std::move(params), std::move(offsets), std::move(bounds),
-                                     std::move(bucket_of), std::move(pg), world);
+                                     std::move(bucket_of), std::move(pg), world, force);
   r->install_hooks();
   return r;
 }
@@ -329,7 +331,7 @@ void set_side_stream(int64_t handle) {
 void register_reducer(py::module& m) {
   py::class_<Reducer, std::shared_ptr<Reducer>>(m, "Reducer")
       .def(py::init(&make_reducer), py::arg("grad_flat"), py::arg("params"), py::arg("offsets"), py::arg("bounds"),
-           py::arg("bucket_of"), py::arg("process_group"), py::arg("world"))
+           py::arg("bucket_of"), py::arg("process_group"), py::arg("world"), py::arg("force") = false)
       // the GIL is released wherever a call may wait for a collective or run torch ops whose
       // tensors' Python owners the collectives' worker threads may need to release
       .def("prepare", &Reducer::prepare, py::call_guard<py::gil_scoped_release>())

@@ -203,6 +203,10 @@ def add_distributed_training_args(parser):
                             'bucket all-reduces are scheduled ahead of queued backward kernels)')
     group.add_argument('--xgmi-blocks', default=64, type=int, metavar='N',
                        help='workgroups per xGMI all-reduce launch (CUs taken from backward while it runs)')
+    group.add_argument('--force-reducer', action='store_true',
+                       help='MI355X: run the bucketed gradient reducer even in a one-rank process group, so a '
+                            'one-GPU run exercises the RCCL stream path (buckets, side-stream ordering, '
+                            'end-of-backward waits); the one-rank sum leaves gradients unchanged')
     group.add_argument('--fix-batches-to-gpus', action='store_true')
     group.add_argument('--find-unused-parameters', default=False, action='store_true')
     group.add_argument('--fast-stat-sync', default=False, action='store_true')

@@ -44,7 +44,8 @@ def _resolve_backend(args):
 
 
 def distributed_init(args):
-    if args.distributed_world_size == 1:
+    if args.distributed_world_size == 1 and not getattr(args, 'force_reducer', False):
+        # (--force-reducer: a one-rank group on purpose, to drive the collective stream path)
         raise ValueError('Cannot initialize distributed with distributed_world_size=1')
     if dist.is_initialized():
         warnings.warn('Distributed is already initialized, cannot initialize twice!')

@@ -89,8 +89,12 @@ def plan_buckets(flat, bucket_cap_mb, world=1, peer_mb=0.0):
 
 class GradReducer(object):
     def __init__(self, flat, bucket_cap_mb=25, process_group=None, find_unused_parameters=False,
-                 broadcast_params=True, bucket_peer_mb=0.0):
+                 broadcast_params=True, bucket_peer_mb=0.0, force=False):
+        """``force``: reduce even in a one-rank group (``--force-reducer``): every bucket still
+        goes through the transport's stream machinery (RCCL / xGMI), which a one-GPU box can
+        then exercise; the sum over one rank leaves the gradients unchanged."""
         self.flat = flat
+        self.force = bool(force) and dist.is_initialized()
         self.group = process_group
         self.world_size = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.find_unused = find_unused_parameters
@@ -108,12 +112,13 @@ class GradReducer(object):
         # every parameter with a defined gradient as used -- e.g. the NER pooler (never reached)
         # was stepped from its second update on, while the reference never steps it.
         pg = None
-        if self.world_size > 1:
+        if self.world_size > 1 or self.force:
             pg = process_group if process_group is not None else dist.group.WORLD
         bounds = [b[0] for b in self.buckets] + [flat.numel]
         self._native = C().Reducer(flat.grad_flat, list(flat.params), list(flat.offsets), bounds,
-                                   [self.bucket_of[i] for i in range(len(flat.params))], pg, self.world_size)
-        self._enabled = self.world_size > 1
+                                   [self.bucket_of[i] for i in range(len(flat.params))], pg, self.world_size,
+                                   self.force)
+        self._enabled = self.world_size > 1 or self.force
         if self.enabled and broadcast_params:
             dist.broadcast(flat.param_flat, src=0, group=self.group)
 
@@ -125,7 +130,7 @@ class GradReducer(object):
     @enabled.setter
     def enabled(self, flag):
         # e.g. --use-bmuf: keep the hooks (used flags / slot adoption), never reduce
-        self._enabled = bool(flag) and self.world_size > 1
+        self._enabled = bool(flag) and (self.world_size > 1 or self.force)
         self._native.set_enabled(self._enabled)
 
     @property

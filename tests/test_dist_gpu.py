@@ -129,3 +129,104 @@ def test_bench_ner_torchrun_contract(tmp_path):
     assert len(lines) == 1, r.stdout[-3000:]
     rec = json.loads(lines[0])
     assert rec['n_gpus'] == 2 and rec['global_batch'] == 16 and rec['value'] > 0
+
+
+def test_rccl_one_rank_reducer_matches_local(dev, tmp_path):
+    """The reducer's RCCL path on the box's one GPU: a one-rank ``nccl`` (RCCL) group with
+    ``--force-reducer`` sends every bucket through ProcessGroupNCCL (in-place slices of the flat
+    gradient buffer, launched from the backward hooks; with ``--overlap-wgrad`` from the weight-
+    gradient side stream; the end-of-backward callback makes the compute stream wait on the
+    collectives).  A one-rank sum is the identity, so the trained weights must equal a run
+    without the reducer bit for bit -- a missed stream dependency (a bucket reduced before its
+    gradient landed, or the optimizer reading a bucket RCCL still writes) shows up as a
+    mismatch."""
+    import socket
+    d = tmp_path / 'data'
+    write_synthetic_bert_shards(str(d), n_files=1, samples_per_file=64, seq_len=128, max_pred=20, vocab_size=1024,
+                                split='train')
+    cfg = write_bert_config(str(tmp_path / 'c.json'), **dict(BERT_TINY, hidden_dropout_prob=0.0,
+                                                               attention_probs_dropout_prob=0.0))
+    vocab = write_vocab(str(tmp_path / 'v.txt'), 1024)
+    common = ['--task', 'bert', '--data', str(d), '--dict', vocab, '--config_file', cfg, '--max-sentences', '32',
+              '--fast-stat-sync', '--max-update', '3', '--disable-validation', '--num-workers', '1', '--lr', '1e-3',
+              '--bucket-cap-mb', '1', '--bucket-peer-mb', '0']
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    rccl = ['--distributed-world-size', '1', '--distributed-backend', 'nccl', '--distributed-rank', '0',
+            '--distributed-init-method', 'tcp://127.0.0.1:{}'.format(port), '--force-reducer']
+    runs = {'local': ['--distributed-world-size', '1'], 'rccl': rccl, 'rccl_side': rccl + ['--overlap-wgrad'],
+            'local_side': ['--distributed-world-size', '1', '--overlap-wgrad']}
+    ck = {}
+    for name, extra in runs.items():
+        save = str(tmp_path / name)
+        env = dict(os.environ, PYTHONPATH=ROOT, HETSEQ_SPLIT_MIN_ROWS_X6='0')
+        r = subprocess.run([sys.executable, '-m', 'hetseq_9cme_amd.train'] + common + extra + ['--save-dir', save],
+                           stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, timeout=400)
+        assert r.returncode == 0, r.stdout[-3000:]
+        if name.startswith('rccl'):
+            assert 'force_reducer=True' in r.stdout
+        with torch.serialization.safe_globals([argparse.Namespace]):
+            ck[name] = torch.load(os.path.join(save, 'checkpoint_last.pt'), map_location='cpu', weights_only=True)
+    for a, b in (('local', 'rccl'), ('local_side', 'rccl_side')):
+        for k, v in ck[a]['model'].items():
+            assert torch.equal(ck[b]['model'][k], v), (a, b, k)
+    assert ck['rccl']['optimizer_history'][-1]['num_updates'] == 3
+
+
+SYNC_SCRIPT = r'''
+import sys, torch, torch.distributed as dist
+from hetseq_9cme_amd import options, tasks
+from hetseq_9cme_amd.controller import Controller
+argv = sys.argv[1:]
+args = options.parse_training_args(argv)
+torch.cuda.set_device(0)
+dist.init_process_group('nccl', init_method=args.distributed_init_method, world_size=1, rank=0)
+task = tasks.setup_task(args)
+model = task.build_model(args)
+ctl = Controller(args, task, model)
+itr = ctl.get_train_iterator(epoch=0).next_epoch_itr(shuffle=False)
+batches = [next(itr) for _ in range(4)]
+for b in batches[:2]:
+    ctl.train_step([b])          # warm-up: lazy optimizer state, kernel attributes
+torch.cuda.synchronize()
+torch.cuda.set_sync_debug_mode('error')
+for b in batches[2:]:
+    ctl.train_step([b])          # must not block the host on the GPU anywhere
+torch.cuda.set_sync_debug_mode(0)
+torch.cuda.synchronize()
+print('launched buckets', ctl.reducer._native.launched(), 'of', ctl.reducer._native.num_buckets())
+dist.destroy_process_group()
+print('SYNC-FREE OK')
+'''
+
+
+def test_rccl_reducer_step_has_no_host_sync(dev, tmp_path):
+    """A whole update (forward, backward with the RCCL bucket launches, stats, clip, Adam) on a
+    one-rank RCCL group with the reducer forced on, under ``torch.cuda.set_sync_debug_mode('error')``:
+    any host wait on the GPU in the step (a ``.item()``, a blocking copy, a host-side used-flag
+    read) raises.  Covers --find-unused-parameters too: its used flags ride in the stats vector
+    and the fused Adam consumes them on device."""
+    import socket
+    d = tmp_path / 'data'
+    write_synthetic_bert_shards(str(d), n_files=1, samples_per_file=64, seq_len=128, max_pred=20, vocab_size=1024,
+                                split='train')
+    cfg = write_bert_config(str(tmp_path / 'c.json'), **BERT_TINY)
+    vocab = write_vocab(str(tmp_path / 'v.txt'), 1024)
+    script = tmp_path / 'sync_step.py'
+    script.write_text(SYNC_SCRIPT)
+    for extra in ([], ['--find-unused-parameters']):
+        with socket.socket() as s:
+            s.bind(('127.0.0.1', 0))
+            port = s.getsockname()[1]
+        argv = ['--task', 'bert', '--data', str(d), '--dict', vocab, '--config_file', cfg, '--max-sentences', '16',
+                '--fast-stat-sync', '--disable-validation', '--num-workers', '1', '--lr', '1e-4',
+                '--bucket-cap-mb', '1', '--bucket-peer-mb', '0', '--distributed-world-size', '1',
+                '--distributed-backend', 'nccl', '--distributed-init-method', 'tcp://127.0.0.1:{}'.format(port),
+                '--force-reducer', '--save-dir', str(tmp_path / 'ck')] + extra
+        env = dict(os.environ, PYTHONPATH=ROOT)
+        r = subprocess.run([sys.executable, str(script)] + argv, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                           text=True, env=env, timeout=300)
+        assert r.returncode == 0 and 'SYNC-FREE OK' in r.stdout, (extra, r.stdout[-4000:])
+        n = [l for l in r.stdout.splitlines() if l.startswith('launched buckets')][0].split()
+        assert int(n[2]) == int(n[4]) > 1, r.stdout[-1000:]

@@ -496,14 +496,16 @@ def test_wgrad_split_pipeline_variants(dev, T, monkeypatch):
         ops.set_fp32_gemm('native')
 
 
-@pytest.mark.parametrize('cfg', [0, 1, 2, 3, 4, 5, 6, 7])
-def test_piece_gemm_every_cfg(dev, cfg, monkeypatch):
-    """Every tile / pipeline configuration of the LDS-DMA piece GEMM (HX_GEMM_CFG) in bf16x6:
-    forward and beta = 1 accumulation against fp64, rows not a multiple of the 256-row tile,
-    a reduction that is not a multiple of the 3-stage ring (K = 272: 17 steps of 16)."""
+@pytest.mark.parametrize('cfg,pipe', [(c, '3') for c in range(8)] + [(0, '6'), (1, '6')])
+def test_piece_gemm_every_cfg(dev, cfg, pipe, monkeypatch):
+    """Every tile / pipeline configuration of the LDS-DMA piece GEMM (HX_GEMM_CFG, HX_GEMM_PIPE:
+    6 = 16x16x32 MFMAs) in bf16x6: forward and beta = 1
+    accumulation against fp64, rows not a multiple of the 256-row tile, a reduction that is not
+    a multiple of the 3-stage ring (K = 272: 17 steps of 16)."""
     from hetseq_9cme_amd import ops
     from hetseq_9cme_amd.ops import split_gemm as sg
     monkeypatch.setenv('HX_GEMM_CFG', str(cfg))
+    monkeypatch.setenv('HX_GEMM_PIPE', pipe)
     g = torch.Generator(device='cpu').manual_seed(40 + cfg)
     M, N, K = 531, 768, 272 if cfg != 2 else 288
     a = (torch.rand(M, K, generator=g) * 2 - 1).to(dev)
@@ -517,10 +519,12 @@ def test_piece_gemm_every_cfg(dev, cfg, monkeypatch):
         y = C().gemm_split(ap, wf, 6)
         acc = c0.clone()
         C().gemm_split(ap, wf, 6, acc, True)
-        if cfg in (0, 1, 7):   # and the B16 weight layout (B operand) on the tiles that read it
+        if cfg in (0, 1, 7):   # and the B16 layouts (B operand; both) on the tiles that read them
             wb = wf.view(N, 3, K // 16, 16).permute(0, 2, 1, 3).contiguous().view(N, -1)
             yb = C().gemm_split(ap, wb, 6, None, False, 2)
             assert torch.equal(y, yb)
+            ab = ap.view(M, 3, K // 16, 16).permute(0, 2, 1, 3).contiguous().view(M, -1)
+            assert torch.equal(y, C().gemm_split(ab, wb, 6, None, False, 3))
     finally:
         ops.set_fp32_gemm('native')
     ref = a.double() @ W.double().t()
@@ -530,16 +534,21 @@ def test_piece_gemm_every_cfg(dev, cfg, monkeypatch):
     assert e < 1.5e-6, e
 
 
-@pytest.mark.parametrize('mode,cfg', [('bf16x6', None), ('bf16x3', None), ('bf16x6', '7')])
-def test_gemm_gelu_epilogues(dev, mode, cfg, monkeypatch):
+@pytest.mark.parametrize('mode,cfg,pipe', [('bf16x6', None, None), ('bf16x3', None, None), ('bf16x6', '7', None),
+                                           ('bf16x6', '0', '6'),
+                                           ('bf16x6', '1', '6')])
+def test_gemm_gelu_epilogues(dev, mode, cfg, pipe, monkeypatch):
     """FFN epilogues of the piece GEMM against fp64: bias + GELU (pre-activation u and the
     pieces of gelu(u)), and the GELU backward (pieces of dh * gelu'(u) and its column sums =
-    the FFN-up bias gradient), with rows that are not a multiple of the tile."""
+    the FFN-up bias gradient), with rows that are not a multiple of the tile; every tile and
+    pipeline that runs them (HX_GEMM_CFG / HX_GEMM_PIPE)."""
     from hetseq_9cme_amd import ops
     from hetseq_9cme_amd.ops import split_gemm as sg
     from hetseq_9cme_amd.ops._ext import C
     if cfg is not None:
         monkeypatch.setenv('HX_GEMM_CFG', cfg)   # e.g. the two-workgroups-per-CU tile
+    if pipe is not None:
+        monkeypatch.setenv('HX_GEMM_PIPE', pipe)
     g = torch.Generator(device='cpu').manual_seed(31)
     T, H, I = 300, 256, 768
     x = torch.randn(T, H, generator=g).to(dev)

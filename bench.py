@@ -74,6 +74,12 @@ def parse():
     ap.add_argument('--node-gpus', type=int, default=1, help=argparse.SUPPRESS)
     ap.add_argument('--node-rank', type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument('--device-offset', type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument('--comm-load', default=None,
+                    help='diagnostic A/B (untimed by the driver): CUS:US:LDSKB -- before every step, a stand-in '
+                         'comm kernel holding CUS CUs (a CU-masked stream, LDSKB KiB of LDS per workgroup) for US '
+                         'microseconds runs beside the step (tools/probe/comm_contention_probe.sh)')
+    ap.add_argument('--reserve-cus', type=int, default=0,
+                    help='CUs the GEMM / weight-gradient plans leave to a concurrent comm kernel (--comm-cus)')
     ap.add_argument('--world', type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument('--init-method', default=None, help=argparse.SUPPRESS)
     ap.add_argument('--nodes-meta', default=None, help=argparse.SUPPRESS)
@@ -188,8 +194,21 @@ def run(a, rank, world, dev_index, init_method):
     ctrl.lr_step(epoch_itr.epoch)
     itr = iterators.GroupedIterator(epoch_itr.next_epoch_itr(shuffle=True), a.update_freq)
 
+    load = None
+    if a.comm_load:
+        from hetseq_9cme_amd.ops._ext import C as _C
+        cus, us, kb = [float(x) for x in a.comm_load.split(':')]
+        load = (_C(), _C().cu_masked_stream(0, int(cus)), int(cus), us, int(kb * 1024),
+                torch.zeros(256, dtype=torch.int32, device='cuda'))
+    if a.reserve_cus:
+        from hetseq_9cme_amd import ops as _ops
+        _ops.set_reserved_cus(a.reserve_cus)
+
     def step():
         samples = next(itr)
+        if load is not None:
+            c, st, n, us, lds, sink = load
+            c.spin(n, us, lds, sink, st)
         return ctrl.train_step(samples)
 
     for _ in range(a.warmup):

@@ -648,7 +648,8 @@ Tensor gemm_split(Tensor a, Tensor b, int64_t passes, OptT out_, bool beta, int6
   return out;
 }
 // FFN up: u = a . b^T + bias (fp32, kept for the backward) and the pieces of gelu(u)
-std::vector<Tensor> gemm_split_gelu(Tensor a, Tensor b, int64_t passes, OptT bias, int64_t lay) {
+// (dmode 1: C gets gelu'(u) instead of u -- all the backward needs, from the same erf)
+std::vector<Tensor> gemm_split_gelu(Tensor a, Tensor b, int64_t passes, OptT bias, int64_t lay, int64_t dmode) {
   const int64_t npc = passes == 6 ? 3 : 2;
   TORCH_CHECK(passes == 3 || passes == 6, "gemm_split_gelu: passes must be 3 or 6");
   TORCH_CHECK(gemm_split_ok(a, b, npc), "gemm_split_gelu: unsupported operands");
@@ -660,7 +661,7 @@ std::vector<Tensor> gemm_split_gelu(Tensor a, Tensor b, int64_t passes, OptT bia
   Tensor u = torch::empty({M, N}, a.options().dtype(torch::kFloat32));
   Tensor p = torch::empty({M, npc * N}, a.options());
   HxGemmEpi e{1, ptr_or_null<float>(bias), nullptr, 0, reinterpret_cast<uint16_t*>(p.data_ptr()), npc * N, N,
-              nullptr};
+              nullptr, dmode ? 1 : 0};
   c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
   TORCH_CHECK(gemm_split_launch(a, b, passes, u.data_ptr<float>(), N, false, &e, lay) == 0,
               "gemm_split_gelu: launch failed");
@@ -669,8 +670,10 @@ std::vector<Tensor> gemm_split_gelu(Tensor a, Tensor b, int64_t passes, OptT bia
 }
 // FFN down data gradient + GELU backward: t = (a . b^T) * gelu'(u (+ bias)); returns the pieces of
 // t and d bias = column sums of t (into dbias_out when given)
+// (dmode 1: u holds gelu'(u) from gemm_split_gelu(dmode=1); bias must be None)
 std::vector<Tensor> gemm_split_dgelu(Tensor a, Tensor b, int64_t passes, Tensor u, OptT bias, OptT dbias_out,
-                                     int64_t lay) {
+                                     int64_t lay, int64_t dmode) {
+  TORCH_CHECK(!dmode || !has(bias), "gemm_split_dgelu: dmode 1 takes gelu'(u), which has the bias in it");
   const int64_t npc = passes == 6 ? 3 : 2;
   TORCH_CHECK(passes == 3 || passes == 6, "gemm_split_dgelu: passes must be 3 or 6");
   TORCH_CHECK(gemm_split_ok(a, b, npc), "gemm_split_dgelu: unsupported operands");
@@ -690,7 +693,7 @@ std::vector<Tensor> gemm_split_dgelu(Tensor a, Tensor b, int64_t passes, Tensor 
   Tensor db = has(dbias_out) ? *dbias_out : torch::empty({N}, f32);
   TORCH_CHECK(db.numel() == N && db.scalar_type() == torch::kFloat32 && db.is_contiguous(), "gemm_split_dgelu: dbias");
   HxGemmEpi e{2, ptr_or_null<float>(bias), u.data_ptr<float>(), N, reinterpret_cast<uint16_t*>(p.data_ptr()),
-              npc * N, N, part.data_ptr<float>()};
+              npc * N, N, part.data_ptr<float>(), dmode ? 1 : 0};
   c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
   TORCH_CHECK(gemm_split_launch(a, b, passes, nullptr, N, false, &e, lay) == 0, "gemm_split_dgelu: launch failed");
   hx_fold_cols(part.data_ptr<float>(), prow, (int)N, db.data_ptr<float>(), 0, cur_stream(a));
@@ -897,9 +900,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_split", &gemm_split, py::arg("a"), py::arg("b"), py::arg("passes"), py::arg("out") = py::none(),
         py::arg("beta") = false, py::arg("lay") = 0);
   m.def("gemm_split_gelu", &gemm_split_gelu, py::arg("a"), py::arg("b"), py::arg("passes"), py::arg("bias"),
-        py::arg("lay") = 0);
+        py::arg("lay") = 0, py::arg("dmode") = 0);
   m.def("gemm_split_dgelu", &gemm_split_dgelu, py::arg("a"), py::arg("b"), py::arg("passes"), py::arg("u"),
-        py::arg("bias"), py::arg("dbias_out"), py::arg("lay") = 0);
+        py::arg("bias"), py::arg("dbias_out"), py::arg("lay") = 0, py::arg("dmode") = 0);
   m.def("gemm_split_stamps", &gemm_split_stamps);
   m.def("dma_probe", &dma_probe);
   m.def("gemm_split_mfma16_timing", &gemm_split_mfma16_timing);
@@ -920,4 +923,28 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("xar_destroy", &xar_destroy);
   m.def("set_debug", &set_debug);
   m.def("get_debug", &get_debug);
+  // CUs reserved for a concurrent comm kernel (cu_reserve.hip)
+  m.def("num_cus", &hx_num_cus);
+  m.def("set_reserved_cus", &hx_set_reserved_cus);
+  m.def("reserved_cus", &hx_reserved_cus);
+  m.def("cu_slots", &hx_cu_slots);
+  m.def("gemm_split_plan", &hx_gemm_split_plan, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("passes"),
+        py::arg("lay") = 0);
+  m.def("wgrad_split_plan", [](int64_t M, int64_t N, int64_t T, int64_t passes) {
+    int cfg = 0, nsplit = 1;
+    hx_wgrad_split_plan((int)M, (int)N, (int)T, (int)passes, &cfg, &nsplit);
+    return std::make_pair(cfg, nsplit);
+  });
+  m.def("cu_masked_stream", [](int64_t first_cu, int64_t count) {
+    hipStream_t st = hx_cu_masked_stream((int)first_cu, (int)count);
+    TORCH_CHECK(st != nullptr, "hipExtStreamCreateWithCUMask failed");
+    return (int64_t)(uintptr_t)st;
+  });
+  m.def("destroy_stream", [](int64_t h) { hx_destroy_stream(reinterpret_cast<hipStream_t>((uintptr_t)h)); });
+  m.def("spin", [](int64_t blocks, double us, int64_t lds_bytes, Tensor sink, int64_t stream) {
+    TORCH_CHECK(sink.is_cuda() && sink.scalar_type() == torch::kInt32 && sink.numel() >= 256, "spin: int32 sink[256]");
+    TORCH_CHECK(lds_bytes >= 0 && lds_bytes <= 160 * 1024 && us >= 0 && us < 1e7, "spin: bad arguments");
+    hipStream_t st = stream ? reinterpret_cast<hipStream_t>((uintptr_t)stream) : cur_stream(sink);
+    hx_spin((int)blocks, us, (int)lds_bytes, reinterpret_cast<uint32_t*>(sink.data_ptr<int>()), st);
+  });
 }

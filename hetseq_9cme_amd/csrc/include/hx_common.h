@@ -170,13 +170,15 @@ struct bio<uint16_t> {
 // truncated sqrt(2) constant, kept for parity; the derivative below is of THAT function.
 // Reciprocal constants instead of divisions (fp32 division is a ~10-instruction sequence).
 __device__ __forceinline__ float gelu_f(float x) { return x * 0.5f * (1.0f + erff(x * (1.0f / 1.41421f))); }
-__device__ __forceinline__ float gelu_grad_f(float x) {
-  constexpr float inv_c = 1.0f / 1.41421f;
+__device__ __forceinline__ float gelu_pdf_f(float x) {   // x * d/dx of the erf term
   constexpr float inv_c2 = 1.0f / (1.41421f * 1.41421f);
   constexpr float k = 0.5f * 1.1283791670955126f / 1.41421f;   // (1/2)(2/sqrt(pi))/c
+  return k * x * __expf(-(x * x) * inv_c2);
+}
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  constexpr float inv_c = 1.0f / 1.41421f;
   const float cdf = 0.5f * (1.0f + erff(x * inv_c));
-  const float pdf = k * x * __expf(-(x * x) * inv_c2);
-  return cdf + pdf;
+  return cdf + gelu_pdf_f(x);
 }
 
 }  // namespace hx

@@ -122,6 +122,10 @@ struct HxGemmEpi {
   uint16_t* P;
   int64_t ldp, p_ps;
   float* colpart;
+  // kind 1: 0 = C gets u (the pre-activation), 1 = C gets gelu'(u) (the only thing the backward
+  // needs: its erf is the forward's, so the backward epilogue does no transcendental work);
+  // kind 2: 0 = aux holds u, 1 = aux holds gelu'(u)
+  int dmode = 0;
 };
 int hx_gemm_split_plan(int M, int N, int K, int passes, int lay = 0);
 int hx_gemm_split_colpart_rows(int M, int cfg);
@@ -163,3 +167,12 @@ int hx_xar_error(void* ctx);
 // stream-ordered copy of the error word into a device int32 (no host sync)
 int hx_xar_error_async(void* ctx, int32_t* dst, hipStream_t s);
 void hx_xar_destroy(void* ctx);
+
+// cu_reserve.hip: CUs held back from the one-round GEMM plans for a concurrent comm kernel
+int hx_num_cus();
+void hx_set_reserved_cus(int r);
+int hx_reserved_cus();
+int hx_cu_slots();   // workgroup slots of one round: n_cu - reserved
+hipStream_t hx_cu_masked_stream(int first_cu, int count);
+void hx_destroy_stream(hipStream_t s);
+void hx_spin(int blocks, double us, int lds_bytes, uint32_t* sink, hipStream_t s);

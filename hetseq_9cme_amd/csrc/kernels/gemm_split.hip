@@ -180,6 +180,7 @@ struct Args {
   int64_t ldp, p_ps;
   float* colpart;
   uint32_t ksa, ksb;   // bytes between consecutive BK-deep k steps of a row (2 BK natural, 2 BK npc blocked)
+  int dmode;           // HxGemmEpi::dmode
   unsigned long long* stamps;   // diagnostic build (PIPE 9): per wave [dma issue, mfma, dma wait, barrier, total]
 };
 
@@ -692,16 +693,36 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_piece_k(
           if constexpr (EPI == 1) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) v[i] += bb[i];
-            const f32x4 o = {v[0], v[1], v[2], v[3]};
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), cbuf.r, coff(a, b, gq), 0, 0);
+            if (g.dmode) {
+              // gelu(u) and gelu'(u) from ONE erf (hx::gelu_f / hx::gelu_grad_f bit for bit)
+              f32x4 o;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) v[i] = hx::gelu_f(v[i]);
+              for (int i = 0; i < 4; ++i) {
+                const float e = erff(v[i] * (1.0f / 1.41421f));
+                o[i] = 0.5f * (1.0f + e) + hx::gelu_pdf_f(v[i]);
+                v[i] = v[i] * 0.5f * (1.0f + e);
+              }
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), cbuf.r, coff(a, b, gq), 0, 0);
+            } else {
+              const f32x4 o = {v[0], v[1], v[2], v[3]};
+              __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), cbuf.r, coff(a, b, gq), 0, 0);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) v[i] = hx::gelu_f(v[i]);
+            }
           } else {
             const bool in = mrow + 32 * a + 8 * gq < mrows;   // rows past M: no bias-gradient share
+            if (g.dmode) {   // aux holds gelu'(u) already
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              v[i] *= hx::gelu_grad_f(u[gq][i] + bb[i]);
-              csum[b][i] += in ? v[i] : 0.f;
+              for (int i = 0; i < 4; ++i) {
+                v[i] *= u[gq][i];
+                csum[b][i] += in ? v[i] : 0.f;
+              }
+            } else {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                v[i] *= hx::gelu_grad_f(u[gq][i] + bb[i]);
+                csum[b][i] += in ? v[i] : 0.f;
+              }
             }
           }
 #pragma unroll
@@ -746,286 +767,6 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_piece_k(
   }
 }
 
-// ---------------------------------------------------------------- 16x16x32 form (bf16x6)
-// The same product, tiles, LDS images and DMA pipeline (PIPE 3) as gemm_piece_k, with
-// v_mfma_f32_16x16x32_bf16 instead of 32x32x16: equal cycles per FLOP, but the chip holds a
-// higher clock on the 16x16 shape under load (MI355X_MICROARCH.md 'DVFS give-back' item 7;
-// measured on this kernel: tools/probe/mfma16_clock_probe.py, 4-6 % faster).  The 32-deep
-// MFMA takes TWO 16-deep piece fragments side by side along k (lanes 0-31: first piece,
-// 32-63: second), so the six piece products of a 16-deep stage are three MFMAs:
-//   [a0 | a1] . [b1 | b0] = a0 b1 + a1 b0      [a0 | a1] . [b2 | b1] = a0 b2 + a1 b1
-//   [a0 | a2] . [b0 | b0] = a0 b0 + a2 b0
-// Fragment lane l: row (l & 15) of a 16-row block, 16-B chunk (l >> 4) & 1 of the stage row,
-// piece by l >> 5.  Accumulator f32x4 of a 16x16 block: rows 4 (l >> 4) + i, column l & 15.
-template <int BM, int BN, int WM, int WN, int EPI, int LAY>
-__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, 1) void gemm_piece16_k(Args g) {
-  constexpr int NPC = 3, BK = 16;
-  constexpr int NWM = BM / WM, NW = NWM * (BN / WN);
-  constexpr int MB = WM / 16, NB = WN / 16;
-  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2;
-  constexpr int STAGE = NPC * (A_BYTES + B_BYTES);
-  constexpr int KA = A_BYTES / 1024, KB = B_BYTES / 1024;
-  constexpr int PA = NPC * KA, PTOT = NPC * (KA + KB);
-  constexpr int JHI = (PTOT + NW - 1) / NW, JLO = PTOT / NW;
-  constexpr int RPK = Img<BK>::RPK;
-  static_assert(JHI <= 6 && JLO >= 1, "two DMA pieces per pass");
-  constexpr bool LA = LAY & 1, LB = LAY & 2;
-  constexpr int A_REG = NPC * A_BYTES;
-  typedef float f32x4 __attribute__((ext_vector_type(4)));
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-
-  const int TM = (g.M + BM - 1) / BM, TN = g.N / BN, total = TM * TN;
-  const int per = (total + 7) / 8;
-  const int work = (blockIdx.x % 8) * per + blockIdx.x / 8;
-  if (work >= total) return;
-  const int nt = work % TN, mt = work / TN;
-  const int m0 = mt * BM, n0 = nt * BN;
-  const int nit = g.K / BK;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w % NWM, wn = w / NWM;
-  const int wv = __builtin_amdgcn_readfirstlane(w);
-  const int mrows = min(BM, g.M - m0);
-  const u32x4 ra = rsrc_of(g.A + (int64_t)m0 * g.lda, (uint32_t)((int64_t)mrows * g.lda * 2));
-  const u32x4 rb = rsrc_of(g.B + (int64_t)n0 * g.ldb, (uint32_t)((int64_t)BN * g.ldb * 2));
-
-  uint32_t voff[JHI];
-  int dsto[JHI];
-  bool isa[JHI];
-  int rl, ch;
-  Img<BK>::lane_src(lane, rl, ch);
-#pragma unroll
-  for (int j = 0; j < JHI; ++j) {
-    const int q = wv + NW * j;
-    isa[j] = q < PA;
-    if ((q < PA && LA) || (q >= PA && LB)) {
-      const int x = 64 * (q < PA ? q : q - PA) + lane;
-      const int c = x ^ b16_sw(x >> 4);
-      const int r = c / 6, q6 = c - 6 * r;
-      voff[j] = (uint32_t)(r * (q < PA ? g.lda : g.ldb) + 8 * q6) * 2;
-    } else if (q < PA) {
-      const int p = q / KA, r = (q % KA) * RPK + rl;
-      voff[j] = (uint32_t)(r * g.lda + p * g.a_ps + 8 * ch) * 2;
-    } else {
-      const int qb = q - PA, p = qb / KB, r = (qb % KB) * RPK + rl;
-      voff[j] = (uint32_t)(r * g.ldb + p * g.b_ps + 8 * ch) * 2;
-    }
-    dsto[j] = 1024 * q;
-  }
-  // fragment offsets: A combos [a0|a1] [a0|a2], B combos [b1|b0] [b2|b1] [b0|b0]
-  const int r16 = lane & 15, kh = (lane >> 4) & 1, half = lane >> 5;
-  auto a_off = [&](int row, int p) {
-    return LA ? b16_off(row, 2 * p + kh) : p * A_BYTES + Img<BK>::off(row, kh);
-  };
-  auto b_off = [&](int row, int p) {
-    return A_REG + (LB ? b16_off(row, 2 * p + kh) : p * B_BYTES + Img<BK>::off(row, kh));
-  };
-  int offa[2][MB], offb[3][NB];
-#pragma unroll
-  for (int a = 0; a < MB; ++a) {
-    const int row = wm * WM + 16 * a + r16;
-    offa[0][a] = a_off(row, half ? 1 : 0);
-    offa[1][a] = a_off(row, half ? 2 : 0);
-  }
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    const int row = wn * WN + 16 * b + r16;
-    offb[0][b] = b_off(row, half ? 0 : 1);
-    offb[1][b] = b_off(row, half ? 1 : 2);
-    offb[2][b] = b_off(row, 0);
-  }
-  const int cnt = (PTOT - wv + NW - 1) / NW;
-  const uint32_t lds0 = (uint32_t)(size_t)(lds_void*)lds;
-  auto dma = [&](int it, int buf) {
-    const uint32_t st = lds0 + buf * STAGE;
-    const uint32_t koa = (uint32_t)it * g.ksa, kob = (uint32_t)it * g.ksb;
-#pragma unroll
-    for (int j = 0; j < JHI; ++j)
-      if (j < JLO || j < cnt) dma16(isa[j] ? ra : rb, st + dsto[j], voff[j] + (isa[j] ? koa : kob));
-  };
-  auto dma_one = [&](int it, int buf, int j) {
-    const uint32_t st = lds0 + buf * STAGE;
-    dma16(isa[j] ? ra : rb, st + dsto[j], voff[j] + (uint32_t)it * (isa[j] ? g.ksa : g.ksb));
-  };
-  auto wait_stage = [&]() {
-    if constexpr (JHI == JLO) {
-      dma_wait<JLO>();
-    } else {
-      if (cnt == JHI) dma_wait<JHI>();
-      else dma_wait<JLO>();
-    }
-  };
-
-  f32x4 acc[MB][NB];
-#pragma unroll
-  for (int a = 0; a < MB; ++a)
-#pragma unroll
-    for (int b = 0; b < NB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  dma(0, 0);
-  if (nit > 1) {
-    dma(1, 1);
-    wait_stage();
-  } else {
-    dma_wait<0>();
-  }
-  __syncthreads();
-  int cur = 0;
-  constexpr int CA[3] = {0, 0, 1}, CB[3] = {0, 1, 2};
-  for (int it = 0; it < nit; ++it) {
-    const int nxt2 = cur == 0 ? 2 : cur - 1;
-    const int dit = it + 2 < nit ? it + 2 : -1;
-    const char* st = lds + cur * STAGE;
-    bf16x8 fa[2][MB], fb[3][NB];
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int a = 0; a < MB; ++a) fa[c][a] = *reinterpret_cast<const bf16x8*>(st + offa[c][a]);
-#pragma unroll
-    for (int c = 0; c < 3; ++c)
-#pragma unroll
-      for (int b = 0; b < NB; ++b) fb[c][b] = *reinterpret_cast<const bf16x8*>(st + offb[c][b]);
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-#pragma unroll
-      for (int a = 0; a < MB; ++a)
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[CA[q]][a], fb[CB[q]][b], acc[a][b], 0, 0, 0);
-      if (dit >= 0) {
-#pragma unroll
-        for (int j = 2 * q; j < 2 * q + 2 && j < JHI; ++j) {
-          if (j < JLO || j < cnt) {
-            __builtin_amdgcn_sched_barrier(0);
-            dma_one(dit, nxt2, j);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
-      }
-    }
-    if (it + 2 < nit) wait_stage();
-    else dma_wait<0>();
-    __syncthreads();
-    cur = cur == 2 ? 0 : cur + 1;
-  }
-
-  // ---- epilogue: after a 4 x 4 quad transpose lane l owns row 4 (l >> 4) + (l & 3) of every
-  // 16 x 16 block and its columns (l & 12) .. + 3
-  const int mrow = wm * WM + 4 * (lane >> 4) + (lane & 3), ncol = wn * WN + (lane & 12);
-  const hx::Buf cbuf(g.C + (int64_t)m0 * g.ldc + n0, (uint32_t)((int64_t)mrows * g.ldc * 4));
-  auto coff = [&](int a, int b) { return (uint32_t)((mrow + 16 * a) * g.ldc + ncol + 16 * b) * 4; };
-  auto tr = [&](int a, int b, float (&v)[4]) {
-    v[0] = acc[a][b][0];
-    v[1] = acc[a][b][1];
-    v[2] = acc[a][b][2];
-    v[3] = acc[a][b][3];
-    transpose4(v, lane);
-  };
-  if constexpr (EPI == 0 || EPI == 3) {
-#pragma unroll
-    for (int a = 0; a < MB; ++a) {
-      f32x4 c[NB];
-      if constexpr (EPI == 3) {
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-          c[b] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(cbuf.r, coff(a, b), 0, 0));
-      }
-#pragma unroll
-      for (int b = 0; b < NB; ++b) {
-        float v[4];
-        tr(a, b, v);
-        f32x4 o = {v[0], v[1], v[2], v[3]};
-        if constexpr (EPI == 3) o += c[b];
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), cbuf.r, coff(a, b), 0, 0);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
-    const hx::Buf pbuf(g.P + (int64_t)m0 * g.ldp + n0, (uint32_t)((int64_t)mrows * g.ldp * 2));
-    auto poff = [&](int a, int b, int p) {
-      return (uint32_t)((int64_t)(mrow + 16 * a) * g.ldp + p * g.p_ps + ncol + 16 * b) * 2;
-    };
-    float csum[NB][4];
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) csum[b][i] = 0.f;
-    const hx::Buf xbuf(EPI == 2 ? g.aux + (int64_t)m0 * g.ldaux + n0 : g.C, (uint32_t)((int64_t)mrows * g.ldaux * 4));
-#pragma unroll
-    for (int a = 0; a < MB; ++a) {
-      f32x4 u[NB];
-      if constexpr (EPI == 2) {
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-          u[b] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                               xbuf.r, (uint32_t)((mrow + 16 * a) * g.ldaux + ncol + 16 * b) * 4, 0, 0));
-      }
-#pragma unroll
-      for (int b = 0; b < NB; ++b) {
-        float bb[4] = {0.f, 0.f, 0.f, 0.f};
-        if (g.bias) {
-          const float4 t = *reinterpret_cast<const float4*>(g.bias + n0 + ncol + 16 * b);
-          bb[0] = t.x;
-          bb[1] = t.y;
-          bb[2] = t.z;
-          bb[3] = t.w;
-        }
-        float v[4];
-        tr(a, b, v);
-        if constexpr (EPI == 1) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] += bb[i];
-          const f32x4 o = {v[0], v[1], v[2], v[3]};
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), cbuf.r, coff(a, b), 0, 0);
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = hx::gelu_f(v[i]);
-        } else {
-          const bool in = mrow + 16 * a < mrows;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            v[i] *= hx::gelu_grad_f(u[b][i] + bb[i]);
-            csum[b][i] += in ? v[i] : 0.f;
-          }
-        }
-#pragma unroll
-        for (int p = 0; p < NPC; ++p) {
-          float hp[4];
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            hp[i] = hx::bf2f(hx::f2bf(v[i]));
-            if (p + 1 < NPC) v[i] -= hp[i];
-          }
-          const uint2 pk = pack4(hp);
-          __builtin_amdgcn_raw_buffer_store_b64(
-              __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int, pk), pbuf.r, poff(a, b, p), 0, 0);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if constexpr (EPI == 2) {
-      if (g.colpart) {
-        // lanes with equal (l & 12) hold the same 4 columns: sum over l & 3 and l >> 4
-        float* row = g.colpart + (int64_t)(mt * NWM + wm) * g.N + n0 + wn * WN;
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float t = csum[b][i];
-            t += qx1(t);
-            t += qx2(t);
-            t += __shfl_xor(t, 16, 64);
-            t += __shfl_xor(t, 32, 64);
-            csum[b][i] = t;
-          }
-        if (lane < 16 && (lane & 3) == 0) {
-#pragma unroll
-          for (int b = 0; b < NB; ++b)
-            *reinterpret_cast<float4*>(row + 16 * b + lane) = make_float4(csum[b][0], csum[b][1], csum[b][2], csum[b][3]);
-        }
-      }
-    }
-  }
-}
-
 // ---------------------------------------------------------------- configurations
 // cfg 0: 256 x 192 tile, waves 4 (M) x 2 (N) of 64 x 96, BK 16, 3 stages (bf16x6 126 KiB LDS):
 //        exactly one, three and four rounds of 256 workgroups at N = 768 / 2304 / 3072, M = 16384
@@ -1038,6 +779,8 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, 1) void gemm_piece16_k(
 // cfg 5 (bf16x6): cfg 1's tile, PIPE 2;   cfg 6 (bf16x6): cfg 4's tile, PIPE 2
 // cfg 7 (bf16x6): 256 x 128 tile, 4 waves (2 x 2) of 128 x 64, BK 16, 2 stages (72 KiB), two
 //        workgroups per CU (PIPE 4): one workgroup's epilogue overlaps the other's MFMAs
+// (round 3, removed: 4 waves of 128 x 96 at one wave per SIMD with both fragment sets in registers
+//  needs > 256 VGPRs + AGPR accumulators, and hipcc spilled 100-200 dwords inside the k loop)
 constexpr int kCfgs = 8;
 int cfg_bm(int) { return 256; }
 int cfg_bn(int c) { return (c == 0 || c == 3) ? 192 : (c == 1 || c == 5) ? 256 : 128; }
@@ -1060,31 +803,13 @@ void launch_one(const Args& a, hipStream_t s) {
   gemm_piece_k<BM, BN, WM, WN, NPC, NP, BK, NBUF, EPI, PIPE, LAY, OCC><<<8 * per, NT, smem, s>>>(a);
 }
 
-// HX_GEMM_PIPE: 3 = interleaved DMA (default), 6 = 3 on 16x16x32 MFMAs (gemm_piece16_k); read per
-// launch so one process can A/B them (tools/probe/gemm_stagger_probe.py).  A variant with the two
-// waves of each SIMD staggered by one pass (MI355X_MICROARCH.md 'Two waves per SIMD' item 9) was
-// 2-3 % slower on every BERT shape and was removed (profiles/r3_gemm_stagger_probe.log).
-template <int BM, int BN, int WM, int WN, int EPI, int LAY>
-void launch16(const Args& a, hipStream_t s) {
-  constexpr int NT = (BM / WM) * (BN / WN) * 64;
-  const int total = ((a.M + BM - 1) / BM) * (a.N / BN);
-  const int per = (total + 7) / 8;
-  const size_t smem = (size_t)3 * 3 * (BM + BN) * 16 * 2;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_piece16_k<BM, BN, WM, WN, EPI, LAY>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    attr = true;
-  }
-  gemm_piece16_k<BM, BN, WM, WN, EPI, LAY><<<8 * per, NT, smem, s>>>(a);
-}
-
-template <int EPI, int LAY>
-void launch16_cfg(int cfg, const Args& a, hipStream_t s) {
-  if (cfg == 0) launch16<256, 192, 64, 96, EPI, LAY>(a, s);
-  else launch16<256, 256, 128, 64, EPI, LAY>(a, s);
-}
-
+// HX_GEMM_PIPE (read per launch, so one process can A/B variants): 3 = interleaved DMA (default).
+// Measured and removed in round 3 (tools/probe/gemm_stagger_probe.py): the two waves of each SIMD
+// staggered by one pass (MI355X_MICROARCH.md 'Two waves per SIMD' item 9) 2-3 % slower on every
+// BERT shape (profiles/r3_gemm_stagger_probe.log); the same pipeline on 16x16x32 MFMAs (two
+// 16-deep pieces side by side along k, three MFMAs per 16x16 block and stage) 1-6 % slower --
+// the clock gain of the 16x16 shape (r3_mfma16_clock_probe.log) does not survive its 26 instead
+// of 15 fragment reads per k step (profiles/r3_gemm_mfma16_probe.log).
 static int pipe_mode() {
   const char* e = getenv("HX_GEMM_PIPE");
   return e ? atoi(e) : 3;
@@ -1105,14 +830,6 @@ void launch_cfg(int cfg, int lay, const Args& a, hipStream_t s) {
   constexpr int BK = NPC == 3 ? 16 : 32, NBUF = NPC == 3 ? 3 : 2;
   if constexpr (NPC == 3) {
     const int pm = pipe_mode();
-    if (pm == 6 && NP == 6 && (cfg == 0 || cfg == 1)) {   // 16x16x32 MFMAs (gemm_piece16_k)
-      constexpr int E16 = EPI == 7 ? 0 : EPI;
-      if (lay == 0) launch16_cfg<E16, 0>(cfg, a, s);
-      else if (lay == 1) launch16_cfg<E16, 1>(cfg, a, s);
-      else if (lay == 2) launch16_cfg<E16, 2>(cfg, a, s);
-      else launch16_cfg<E16, 3>(cfg, a, s);
-      return;
-    }
     if (cfg == 7 || (pm == 3 && (cfg == 0 || cfg == 1))) {   // DMA pieces interleaved with the passes
       if (lay == 0) launch_lay<NPC, NP, EPI, 3, 0>(cfg, a, s);
       else if (lay == 1) launch_lay<NPC, NP, EPI, 3, 1>(cfg, a, s);
@@ -1156,7 +873,6 @@ void launch_cfg(int cfg, int lay, const Args& a, hipStream_t s) {
 
 int hx_gemm_split_plan(int M, int N, int K, int passes, int lay) {
   (void)K;
-  (void)M;
   if (const char* e = getenv("HX_GEMM_CFG")) {
     const int c = atoi(e);
     if (c >= 0 && c < kCfgs && N % cfg_bn(c) == 0 && (c < 3 || passes == 6) &&
@@ -1166,7 +882,19 @@ int hx_gemm_split_plan(int M, int N, int K, int passes, int lay) {
   // measured at M = 16384, bf16x6 (tools/probe/gemm_layout_probe.py, profiles/r3_gemm_split.md):
   // N = 768 on the 256 x 192 tile (one round of 256 workgroups), N = 2304 on 256 x 128 (natural
   // layouts) or 256 x 192 (B16), wide outputs (3072, the decoder's vocabulary) on 256 x 256
-  if (N % 192 == 0 && N <= 1536) return 0;
+  if (N % 192 == 0 && N <= 1536) {
+    // 256 x 192 fills exactly one round of 256 CUs at M = 16384, N = 768.  With CUs reserved for
+    // a concurrent comm kernel (cu_reserve.hip) that round no longer fits: take the tile whose
+    // rounds are fuller (256 x 256: 192 tiles, one round on >= 192 free CUs)
+    const int slots = hx_cu_slots();
+    if (slots < hx_num_cus() && N % 256 == 0) {
+      // rounds of slot-filling waves, in units of one 256 x 192 tile's time (256 x 256: 4/3)
+      const int t0 = (M + 255) / 256 * (N / 192), t1 = (M + 255) / 256 * (N / 256);
+      const double r0 = (double)((t0 + slots - 1) / slots), r1 = (double)((t1 + slots - 1) / slots) * (256.0 / 192.0);
+      if (r1 < r0) return 1;
+    }
+    return 0;
+  }
   if (N % 2304 == 0) return lay ? 0 : 2;
   if (N % 256 == 0) return 1;
   if (N % 192 == 0) return 0;
@@ -1222,6 +950,7 @@ int hx_gemm_split_nt(const void* A, int64_t lda, int64_t a_ps, const void* B, in
   a.ldp = epi ? epi->ldp : 0;
   a.p_ps = epi ? epi->p_ps : 0;
   a.colpart = epi ? epi->colpart : nullptr;
+  a.dmode = epi ? epi->dmode : 0;
   a.ksa = (uint32_t)(bk * 2 * ((lay & 1) ? npc : 1));
   a.ksb = (uint32_t)(bk * 2 * ((lay & 2) ? npc : 1));
   a.stamps = nullptr;

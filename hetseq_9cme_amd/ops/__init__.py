@@ -26,3 +26,9 @@ def fused_adam(p, g, m, v, gscale, start, end, beta1, beta2, eps, step_size, wd_
 
 def fused_adadelta(p, g, sq, acc, gscale, start, end, lr, rho, eps, wd, hp=None):
     C().adadelta(p, g, sq, acc, gscale, int(start), int(end), lr, rho, eps, wd, hp)
+
+
+def set_reserved_cus(n):
+    """CUs the one-round GEMM / weight-gradient plans leave to a concurrent comm kernel
+    (csrc/kernels/cu_reserve.hip; ``--comm-cus``).  0 = plan for the whole chip."""
+    C().set_reserved_cus(int(n))

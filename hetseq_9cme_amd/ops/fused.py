@@ -552,11 +552,12 @@ class _FFNSplitFn(torch.autograd.Function):
             ctx.gp.want = True
             ctx.gp.pieces = ctx.pieces
         if ctx.pieces:
-            # bias + GELU in the FFN-up GEMM's epilogue (pre-activation u kept in fp32 for the
-            # backward, gelu(u) written as the FFN-down GEMM's pieces): bert_modeling.py:166-168
+            # bias + GELU in the FFN-up GEMM's epilogue (gelu(u) written as the FFN-down GEMM's
+            # pieces; gelu'(u) kept in fp32 for the backward, from the same erf):
+            # bert_modeling.py:166-168
             xs = split_gemm.input_pieces(x, x2)
             w1f, w1t = split_gemm.weight_pieces(W1)
-            u, hs = split_gemm.gemm_gelu(xs, w1f, b1)
+            u, hs = split_gemm.gemm_gelu(xs, w1f, b1, deriv=True)
             w2f, w2t = split_gemm.weight_pieces(W2)
             y2 = split_gemm.gemm(hs, w2f)
             ctx.save_for_backward(xs, u, hs, w1t, b1, w2t)
@@ -588,8 +589,8 @@ class _FFNSplitFn(torch.autograd.Function):
             dys = ctx.gp.take() if ctx.gp is not None else None
             dys = dys if dys is not None else split_gemm.pieces(dy2.float())
             # GELU backward in the FFN-down data-gradient epilogue: the pieces of
-            # dh * gelu'(u) and the FFN-up bias gradient (u = y1 holds the bias already)
-            dy1s, db1 = split_gemm.gemm_dgelu(dys, w2, y1, None, grad_slot(b1))
+            # dh * gelu'(u) and the FFN-up bias gradient (y1 = gelu'(u), saved by the forward)
+            dy1s, db1 = split_gemm.gemm_dgelu(dys, w2, y1, None, grad_slot(b1), deriv=True)
             dW2 = split_gemm.wgrad_pieces(dys, hs, W2.shape[0], W2.shape[1], grad_slot(W2))
             dx = _dgrad_pieces(dy1s, w1, ctx.xshape, ctx.mbox)
             dW1 = split_gemm.wgrad_pieces(dy1s, xs, W1.shape[0], W1.shape[1], grad_slot(W1))

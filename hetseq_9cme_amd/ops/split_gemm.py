@@ -277,15 +277,18 @@ def gemm(a, b, out=None, beta=False):
     return C().gemm_split(a, b, _State.passes, out, beta, 2 if b16(b.shape[0]) else 0)
 
 
-def gemm_gelu(a, b, bias):
-    """(u = a . b^T + bias, pieces of gelu(u)): the FFN-up GEMM with its GELU epilogue."""
-    return C().gemm_split_gelu(a, b, _State.passes, bias, 2 if b16(b.shape[0]) else 0)
+def gemm_gelu(a, b, bias, deriv=False):
+    """(u = a . b^T + bias, pieces of gelu(u)): the FFN-up GEMM with its GELU epilogue.
+    ``deriv``: return gelu'(u) in place of u -- the only thing the backward needs, computed from
+    the same erf as gelu(u), so the backward epilogue runs no erf / exp (gemm_dgelu(deriv=True))."""
+    return C().gemm_split_gelu(a, b, _State.passes, bias, 2 if b16(b.shape[0]) else 0, 1 if deriv else 0)
 
 
-def gemm_dgelu(a, b, u, bias, dbias_out):
+def gemm_dgelu(a, b, u, bias, dbias_out, deriv=False):
     """(pieces of (a . b^T) * gelu'(u (+ bias)), d bias): the FFN-down data gradient with the
-    GELU backward epilogue."""
-    return C().gemm_split_dgelu(a, b, _State.passes, u, bias, dbias_out, 2 if b16(b.shape[0]) else 0)
+    GELU backward epilogue (``deriv``: ``u`` holds gelu'(u) from gemm_gelu(deriv=True))."""
+    return C().gemm_split_dgelu(a, b, _State.passes, u, bias, dbias_out, 2 if b16(b.shape[0]) else 0,
+                                1 if deriv else 0)
 
 
 def dgrad_pieces(dys, wt, acc=None):

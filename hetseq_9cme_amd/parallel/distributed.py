@@ -22,6 +22,7 @@ import builtins
 import datetime
 import pickle
 import socket
+import os
 import warnings
 
 import torch
@@ -47,6 +48,10 @@ def distributed_init(args):
     if args.distributed_world_size == 1 and not getattr(args, 'force_reducer', False):
         # (--force-reducer: a one-rank group on purpose, to drive the collective stream path)
         raise ValueError('Cannot initialize distributed with distributed_world_size=1')
+    if getattr(args, 'comm_cus', 0) > 0 and args.distributed_backend == 'nccl':
+        # --comm-cus: RCCL's collectives take at most that many CUs (one workgroup per channel);
+        # read by RCCL when the communicator is created, so before the first collective
+        os.environ.setdefault('NCCL_MAX_NCHANNELS', str(args.comm_cus))
     if dist.is_initialized():
         warnings.warn('Distributed is already initialized, cannot initialize twice!')
     else:

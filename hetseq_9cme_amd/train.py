@@ -8,7 +8,7 @@ Launch modes (reference hetseq/train.py:196-246):
       5-GPU node with ``--distributed-rank 0`` and a 3-GPU node with
       ``--distributed-rank 5`` form one world of 8).
   (b) init method with one GPU or ``--distributed-no-spawn``: run one process.
-  (c) no init method, ``--distributed-world-size > 1``: single node, random
+  (c) no init method, ``--distributed-world-size > 1``: single node, a free
       localhost port, spawn world-size processes.
   (d) otherwise single process.
   (e) launched by torchrun (RANK / WORLD_SIZE / LOCAL_RANK in the environment):
@@ -17,7 +17,6 @@ Launch modes (reference hetseq/train.py:196-246):
 import collections
 import math
 import os
-import random
 
 import numpy as np
 import torch
@@ -211,7 +210,12 @@ def cli_main(argv=None):
     elif args.distributed_world_size > 1:
         if not args.cpu and args.distributed_backend == 'nccl':
             assert args.distributed_world_size <= torch.cuda.device_count()
-        port = random.randint(10000, 20000)
+        # a port the OS reports free (the reference draws random.randint(10000, 20000), which
+        # collides now and then when several jobs share a host)
+        import socket
+        with socket.socket() as sk:
+            sk.bind(('127.0.0.1', 0))
+            port = sk.getsockname()[1]
         args.distributed_init_method = 'tcp://127.0.0.1:{port}'.format(port=port)
         args.distributed_rank = None
         torch.multiprocessing.spawn(fn=distributed_main, args=(args,), nprocs=args.distributed_world_size)

@@ -153,7 +153,7 @@ def test_rccl_one_rank_reducer_matches_local(dev, tmp_path):
     with socket.socket() as s:
         s.bind(('127.0.0.1', 0))
         port = s.getsockname()[1]
-    rccl = ['--distributed-world-size', '1', '--distributed-backend', 'nccl', '--distributed-rank', '0',
+    rccl = ['--distributed-world-size', '1', '--distributed-gpus', '1', '--distributed-backend', 'nccl', '--distributed-rank', '0',
             '--distributed-init-method', 'tcp://127.0.0.1:{}'.format(port), '--force-reducer']
     runs = {'local': ['--distributed-world-size', '1'], 'rccl': rccl, 'rccl_side': rccl + ['--overlap-wgrad'],
             'local_side': ['--distributed-world-size', '1', '--overlap-wgrad']}

@@ -329,3 +329,29 @@ def test_xgmi_eligibility_by_bus_id():
     assert not ok and 'hosts' in why
     # ranks sharing one GPU (the one-GPU tests) are fine
     assert eligibility([('h', bus[0], (bus[0],))] * 3, 1, yes)[0]
+
+
+def test_plans_leave_reserved_cus_to_comm():
+    """--comm-cus (csrc/kernels/cu_reserve.hip): with R CUs held by a concurrent all-reduce the
+    one-round plans are sized for the remaining CUs -- the weight-gradient split counts fill
+    n_cu - R slots, and the N = 768 piece GEMM (256 x 192 tiles: exactly one round of 256) moves to
+    the 256 x 256 tile (192 tiles: still one round).  Host-side plan functions only (no GPU:
+    the CU count falls back to the MI355X's 256)."""
+    from hetseq_9cme_amd.ops._ext import C
+    c = C()
+    n = c.num_cus()
+    try:
+        c.set_reserved_cus(0)
+        assert c.cu_slots() == n
+        base = {s: c.wgrad_split_plan(*s, 6) for s in ((2304, 768, 16384), (3072, 768, 16384), (768, 3072, 16384))}
+        assert c.gemm_split_plan(16384, 768, 3072, 6, 2) == 0
+        c.set_reserved_cus(16)
+        assert c.cu_slots() == n - 16
+        for (M, N, T), (cfg, ns) in base.items():
+            cfg2, ns2 = c.wgrad_split_plan(M, N, T, 6)
+            tiles = (M // 256) * (N // (256 if cfg2 == 2 else 128))
+            assert tiles * ns2 <= n - 16 < tiles * (ns2 + 1), (M, N, cfg2, ns2)
+        assert c.gemm_split_plan(16384, 768, 3072, 6, 2) == 1
+        assert c.gemm_split_plan(16384, 3072, 768, 6, 2) == 1   # wide outputs: unchanged
+    finally:
+        c.set_reserved_cus(0)

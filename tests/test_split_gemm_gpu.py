@@ -496,10 +496,9 @@ def test_wgrad_split_pipeline_variants(dev, T, monkeypatch):
         ops.set_fp32_gemm('native')
 
 
-@pytest.mark.parametrize('cfg,pipe', [(c, '3') for c in range(8)] + [(0, '6'), (1, '6')])
+@pytest.mark.parametrize('cfg,pipe', [(c, '3') for c in range(8)])
 def test_piece_gemm_every_cfg(dev, cfg, pipe, monkeypatch):
-    """Every tile / pipeline configuration of the LDS-DMA piece GEMM (HX_GEMM_CFG, HX_GEMM_PIPE:
-    6 = 16x16x32 MFMAs) in bf16x6: forward and beta = 1
+    """Every tile / pipeline configuration of the LDS-DMA piece GEMM (HX_GEMM_CFG, HX_GEMM_PIPE) in bf16x6: forward and beta = 1
     accumulation against fp64, rows not a multiple of the 256-row tile, a reduction that is not
     a multiple of the 3-stage ring (K = 272: 17 steps of 16)."""
     from hetseq_9cme_amd import ops
@@ -535,8 +534,7 @@ def test_piece_gemm_every_cfg(dev, cfg, pipe, monkeypatch):
 
 
 @pytest.mark.parametrize('mode,cfg,pipe', [('bf16x6', None, None), ('bf16x3', None, None), ('bf16x6', '7', None),
-                                           ('bf16x6', '0', '6'),
-                                           ('bf16x6', '1', '6')])
+                                           ])
 def test_gemm_gelu_epilogues(dev, mode, cfg, pipe, monkeypatch):
     """FFN epilogues of the piece GEMM against fp64: bias + GELU (pre-activation u and the
     pieces of gelu(u)), and the GELU backward (pieces of dh * gelu'(u) and its column sums =
@@ -582,6 +580,43 @@ def test_gemm_gelu_epilogues(dev, mode, cfg, pipe, monkeypatch):
     assert ((t - ud_.grad).abs() / (ts + 1e-30)).max().item() < 5 * tol
     dbr = ud_.grad.sum(0)
     assert ((db.double() - dbr).abs() / ts.sum(0)).max().item() < 5 * tol
+
+
+@pytest.mark.parametrize('cfg', [None, '1'])
+def test_gemm_gelu_derivative_mode(dev, cfg, monkeypatch):
+    """The FFN path's epilogue pair (deriv=True): the FFN-up GEMM stores gelu'(u) instead of u
+    (from the erf it computes for gelu(u) anyway) and the FFN-down data gradient multiplies by it
+    with no erf / exp of its own.  Same values bit for bit as the u-storing pair: gelu(u)
+    pieces, the dGELU pieces and the bias gradient."""
+    from hetseq_9cme_amd import ops
+    from hetseq_9cme_amd.ops import split_gemm as sg
+    if cfg is not None:
+        monkeypatch.setenv('HX_GEMM_CFG', cfg)
+    g = torch.Generator(device='cpu').manual_seed(37)
+    T, H, I = 1100, 256, 768
+    x = torch.randn(T, H, generator=g).to(dev)
+    W1 = (torch.randn(I, H, generator=g) * 0.1).to(dev)
+    b1 = (torch.randn(I, generator=g) * 0.5).to(dev)
+    W2 = (torch.randn(H, I, generator=g) * 0.05).to(dev)
+    dy = torch.randn(T, H, generator=g).to(dev)
+    try:
+        ops.set_fp32_gemm('bf16x6')
+        xs = sg.pieces(x)
+        w1f, _ = sg.weight_pieces(W1)
+        _, w2t = sg.weight_pieces(W2)
+        dys = sg.pieces(dy)
+        u, hp = sg.gemm_gelu(xs, w1f, b1)
+        gd, hp2 = sg.gemm_gelu(xs, w1f, b1, deriv=True)
+        tp, db = sg.gemm_dgelu(dys, w2t, u, None, None)
+        tp2, db2 = sg.gemm_dgelu(dys, w2t, gd, None, None, deriv=True)
+    finally:
+        ops.set_fp32_gemm('native')
+    assert torch.equal(hp, hp2)
+    assert torch.equal(tp, tp2) and torch.equal(db, db2)
+    # gelu'(u) of the reference's GELU (x / 2 (1 + erf(x / 1.41421)))
+    ud = u.double()
+    ref = 0.5 * (1 + torch.erf(ud / 1.41421)) + ud * torch.exp(-ud * ud / (1.41421 ** 2)) / (1.41421 * 3.141592653589793 ** 0.5)
+    assert ((gd.double() - ref).abs()).max().item() < 2e-6
 
 
 def test_piece_gemm_b16_layouts(dev):

@@ -9,7 +9,9 @@ from hetseq_9cme_amd import options  # noqa: E402
 
 NEW = {'--async-save', '--check-params-every', '--distributed-timeout', '--ent_name_id_file', '--fused-kernels',
        '--gemm-tuning', '--gemm-tuning-file', '--precision', '--profile-phases', '--user-module',
-       '--overlap-wgrad', '--debug-kernels', '--allreduce-impl', '--xgmi-blocks'}
+       '--overlap-wgrad', '--debug-kernels', '--allreduce-impl', '--xgmi-blocks', '--device-offset',
+       '--bucket-peer-mb', '--comm-cus', '--force-reducer', '--fp32-gemm', '--graph-train-step',
+       '--pad-to-multiple-of', '--rccl-normal-priority'}
 
 SECTIONS = [('bert', 'adam'), ('mnist', 'adadelta'), ('BertForTokenClassification', 'adam'),
             ('BertForELClassification', 'adam')]

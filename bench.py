@@ -75,9 +75,11 @@ def parse():
     ap.add_argument('--node-rank', type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument('--device-offset', type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument('--comm-load', default=None,
-                    help='diagnostic A/B (untimed by the driver): CUS:US:LDSKB -- before every step, a stand-in '
-                         'comm kernel holding CUS CUs (a CU-masked stream, LDSKB KiB of LDS per workgroup) for US '
-                         'microseconds runs beside the step (tools/probe/comm_contention_probe.sh)')
+                    help='diagnostic A/B (untimed by the driver): CUS:US:LDSKB[:mask] -- before every step, a '
+                         'stand-in comm kernel of CUS workgroups (LDSKB KiB of LDS each, so no GEMM workgroup fits '
+                         'beside one) spins for US microseconds beside the step on its own stream, its workgroups '
+                         'dealt over the XCDs like an RCCL kernel\'s ("mask": confined to CUs 0..CUS-1 by a CU-masked '
+                         'stream instead) (tools/probe/comm_contention_probe.sh)')
     ap.add_argument('--reserve-cus', type=int, default=0,
                     help='CUs the GEMM / weight-gradient plans leave to a concurrent comm kernel (--comm-cus)')
     ap.add_argument('--world', type=int, default=0, help=argparse.SUPPRESS)
@@ -197,9 +199,14 @@ def run(a, rank, world, dev_index, init_method):
     load = None
     if a.comm_load:
         from hetseq_9cme_amd.ops._ext import C as _C
-        cus, us, kb = [float(x) for x in a.comm_load.split(':')]
-        load = (_C(), _C().cu_masked_stream(0, int(cus)), int(cus), us, int(kb * 1024),
-                torch.zeros(256, dtype=torch.int32, device='cuda'))
+        f = a.comm_load.split(':')
+        cus, us, kb = int(f[0]), float(f[1]), float(f[2])
+        if len(f) > 3 and f[3] == 'mask':
+            st = _C().cu_masked_stream(0, cus)
+        else:
+            _load_stream = torch.cuda.Stream()
+            st = _load_stream.cuda_stream
+        load = (_C(), st, cus, us, int(kb * 1024), torch.zeros(256, dtype=torch.int32, device='cuda'))
     if a.reserve_cus:
         from hetseq_9cme_amd import ops as _ops
         _ops.set_reserved_cus(a.reserve_cus)

@@ -555,6 +555,69 @@ Tensor wgrad_split(Tensor dys, std::vector<int64_t> dy_off, Tensor xs, std::vect
   return out;
 }
 
+// two weight gradients over the same tokens in one launch (wgrad_split.hip, bf16x6): each item is
+// (dys, dy_off, xs, x_off, M, N, out) as for wgrad_split; false when the pair does not qualify
+bool wgrad_split_group(std::vector<py::tuple> items) {
+  TORCH_CHECK(items.size() == 2, "wgrad_split_group: two products");
+  struct It {
+    Tensor dys, xs, out;
+    std::vector<int64_t> doff, xoff;
+    int64_t M, N;
+  };
+  It it[2];
+  for (int k = 0; k < 2; ++k) {
+    const py::tuple& t = items[k];
+    TORCH_CHECK(t.size() == 7, "wgrad_split_group: (dys, dy_off, xs, x_off, M, N, out)");
+    it[k].dys = t[0].cast<Tensor>();
+    it[k].doff = t[1].cast<std::vector<int64_t>>();
+    it[k].xs = t[2].cast<Tensor>();
+    it[k].xoff = t[3].cast<std::vector<int64_t>>();
+    it[k].M = t[4].cast<int64_t>();
+    it[k].N = t[5].cast<int64_t>();
+    it[k].out = t[6].cast<Tensor>();
+    TORCH_CHECK(wgrad_split_ok(it[k].dys, it[k].xs, it[k].M, it[k].N), "wgrad_split_group: unsupported operands");
+    TORCH_CHECK(it[k].doff.size() == 3 && it[k].xoff.size() == 3, "wgrad_split_group: three pieces (bf16x6)");
+    for (int i = 0; i < 3; ++i) {
+      TORCH_CHECK(it[k].doff[i] >= 0 && it[k].doff[i] + it[k].M <= it[k].dys.size(1) && it[k].doff[i] % 8 == 0,
+                  "wgrad_split_group: bad dY offset");
+      TORCH_CHECK(it[k].xoff[i] >= 0 && it[k].xoff[i] + it[k].N <= it[k].xs.size(1) && it[k].xoff[i] % 8 == 0,
+                  "wgrad_split_group: bad X offset");
+    }
+    check_f32(it[k].out, "wgrad_split_group out");
+    TORCH_CHECK(it[k].out.size(0) <= it[k].M && it[k].out.size(0) > 0 && it[k].out.size(1) == it[k].N &&
+                    it[k].out.is_contiguous(),
+                "wgrad_split_group: out must be [<= M, N]");
+  }
+  const int64_t T = it[0].dys.size(0);
+  TORCH_CHECK(it[1].dys.size(0) == T && it[0].dys.device() == it[1].dys.device(),
+              "wgrad_split_group: same tokens, same device");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(it[0].dys.device());
+  const int nsplit = hx_wgrad_split_group_plan((int)it[0].M, (int)it[0].N, (int)it[1].M, (int)it[1].N, (int)T, 6);
+  if (nsplit < 1) return false;
+  Tensor ws[2];
+  const void* dp[2][3];
+  const void* xp[2][3];
+  for (int k = 0; k < 2; ++k) {
+    if (nsplit > 1) ws[k] = torch::empty({nsplit * it[k].M * it[k].N}, it[k].out.options());
+    const char* db = reinterpret_cast<const char*>(it[k].dys.data_ptr());
+    const char* xb = reinterpret_cast<const char*>(it[k].xs.data_ptr());
+    for (int i = 0; i < 3; ++i) {
+      dp[k][i] = db + 2 * it[k].doff[i];
+      xp[k][i] = xb + 2 * it[k].xoff[i];
+    }
+  }
+  TORCH_CHECK(hx_wgrad_split_group(dp[0], (int)it[0].dys.size(1), xp[0], (int)it[0].xs.size(1),
+                                   it[0].out.data_ptr<float>(), nsplit > 1 ? ws[0].data_ptr<float>() : nullptr,
+                                   (int)it[0].M, (int)it[0].N, (int)it[0].out.size(0), dp[1], (int)it[1].dys.size(1),
+                                   xp[1], (int)it[1].xs.size(1), it[1].out.data_ptr<float>(),
+                                   nsplit > 1 ? ws[1].data_ptr<float>() : nullptr, (int)it[1].M, (int)it[1].N,
+                                   (int)it[1].out.size(0), (int)T, nsplit, cur_stream(it[0].dys)) == 0,
+              "wgrad_split_group: launch failed");
+  dbg_finite(it[0].out, "wgrad_split_group");
+  dbg_finite(it[1].out, "wgrad_split_group");
+  return true;
+}
+
 // ------------------------------------------------------------------ bias + activation -> planes
 // forward (dout absent): planes of act(y + b); backward: planes of dout * act'(y + b) and dbias.
 std::vector<Tensor> bias_act_planes(Tensor y, OptT b, OptT dout, int64_t act, std::vector<int64_t> order,
@@ -910,6 +973,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bias_act_planes", &bias_act_planes);
   m.def("wgrad_split", &wgrad_split);
   m.def("wgrad_split_ok", &wgrad_split_ok);
+  m.def("wgrad_split_group", &wgrad_split_group);
   m.def("xar_create", &xar_create);
   m.def("xar_register", &xar_register);
   m.def("device_pci_bus_id", &device_pci_bus_id);

@@ -89,6 +89,10 @@ void hx_attn_bwd(int kind, const void* qkv, const float* bias, float* dbq, float
 // operands, --fp32-gemm bf16x3 / bf16x6); piece pointers share the row strides ldy / ldx.
 // ws: nsplit * M * N floats.  Returns -1 for an unsupported pass count.
 void hx_wgrad_split_plan(int M, int N, int T, int passes, int* cfg, int* nsplit);
+int hx_wgrad_split_group_plan(int M1, int N1, int M2, int N2, int T, int passes);
+int hx_wgrad_split_group(const void* const* dy1, int ldy1, const void* const* x1, int ldx1, float* out1, float* ws1,
+                         int M1, int N1, int mvalid1, const void* const* dy2, int ldy2, const void* const* x2, int ldx2,
+                         float* out2, float* ws2, int M2, int N2, int mvalid2, int T, int nsplit, hipStream_t s);
 int hx_wgrad_split(const void* const* dy_pieces, int ldy, const void* const* x_pieces, int ldx, int passes,
                    float* out, float* ws, int M, int N, int T, int cfg, int nsplit, int mvalid,
                    hipStream_t s);

@@ -879,9 +879,9 @@ int hx_gemm_split_plan(int M, int N, int K, int passes, int lay) {
         (!lay || c == 0 || c == 1 || c == 7 || ((c == 3 || c == 5) && lay == 3)))
       return c;
   }
-  // measured at M = 16384, bf16x6 (tools/probe/gemm_layout_probe.py, profiles/r3_gemm_split.md):
-  // N = 768 on the 256 x 192 tile (one round of 256 workgroups), N = 2304 on 256 x 128 (natural
-  // layouts) or 256 x 192 (B16), wide outputs (3072, the decoder's vocabulary) on 256 x 256
+  // measured at M = 16384, bf16x6 (tools/probe/gemm_layout_probe.py, qkv_plan_probe.py):
+  // N = 768 on the 256 x 192 tile (one round of 256 workgroups), N = 2304 on 256 x 192 (B16
+  // weights; 256 x 128 if the weights are natural), wide outputs (3072) on 256 x 256
   if (N % 192 == 0 && N <= 1536) {
     // 256 x 192 fills exactly one round of 256 CUs at M = 16384, N = 768.  With CUs reserved for
     // a concurrent comm kernel (cu_reserve.hip) that round no longer fits: take the tile whose
@@ -903,11 +903,13 @@ int hx_gemm_split_plan(int M, int N, int K, int passes, int lay) {
 }
 
 // should the B operand (weight pieces) of an N-column product be written in the B16 layout?
-// bf16x6 on the 256 x 192 / 256 x 256 tiles: 3-9 % faster (tools/probe/gemm_layout_probe.py);
-// N = 2304 stays natural on the 256 x 128 tile, which is faster there.  HX_W_B16=0 turns it off.
+// bf16x6 on the 256 x 192 / 256 x 256 tiles: 3-9 % faster (tools/probe/gemm_layout_probe.py),
+// the QKV forward (N = 2304) included: 256 x 192 over B16 weights 282 us against 306 us for the
+// 256 x 128 tile over natural ones (tools/probe/qkv_plan_probe.py, profiles/r3_qkv_plan_probe.log).
+// HX_W_B16=0 turns it off.
 int hx_gemm_split_weight_b16(int N, int passes) {
   static const bool on = !(getenv("HX_W_B16") && getenv("HX_W_B16")[0] == '0');
-  if (!on || passes != 6 || N % 2304 == 0) return 0;
+  if (!on || passes != 6) return 0;
   const int c = hx_gemm_split_plan(1 << 14, N, 768, passes, 2);
   return (c == 0 || c == 1 || c == 7) ? 1 : 0;
 }

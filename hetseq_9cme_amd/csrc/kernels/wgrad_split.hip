@@ -113,6 +113,17 @@ struct PieceBases {
   const uint16_t* b[3];   // X pieces (same row stride ldb)
 };
 
+// Second product of a GROUPED launch (hx_wgrad_split_group): same tokens T, tile shape and split
+// count; its work items follow the first product's, so the two fill one round of workgroups
+// together (e.g. the 9-tile attention-output dW beside the 27-tile QKV dW: alone it runs 14-way
+// token splits at 0.93 PF/s).  M == 0: no second product.
+struct Prob2 {
+  PieceBases P;
+  int lda, ldb;
+  float* out;
+  int M, N, mvalid, mord;
+};
+
 // AHEAD: token steps staged ahead in registers (2: two register sets; 1: one set, fewer
 // VGPRs -- the bf16x6 256 x 128 tile spills with two).  MORD: work order inside a token
 // split, 0 = output-column tiles fastest, 1 = output-row tiles fastest (the tiles one XCD
@@ -123,7 +134,7 @@ template <int BM, int BN, int WM, int WN, int NPC, int NP, int AHEAD, int MORD, 
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_split_k(PieceBases P, int lda, int ldb,
                                                                            float* __restrict__ out, int M, int N,
                                                                            int T, int kchunk, int nsplit,
-                                                                           int mvalid) {
+                                                                           int mvalid, Prob2 g2) {
   constexpr int NWM = BM / WM, NW = NWM * (BN / WN), NT = NW * 64;
   constexpr int MB = WM / 32, NB = WN / 32;
   constexpr int CA = BKT * BM / 8 / NT, CB = BKT * BN / 8 / NT;   // 16-B chunks per thread per piece
@@ -135,12 +146,26 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_split_k(Piec
   constexpr int STAGE = NPC * (A_BYTES + B_BYTES);
   extern __shared__ __attribute__((aligned(16))) char lds[];   // [2 stages][NPC A tiles, NPC B tiles]
 
-  const int TM = M / BM, TN = N / BN, total = TM * TN * nsplit;
-  const int per = (total + 7) / 8;
-  const int work = (blockIdx.x % 8) * per + blockIdx.x / 8;
-  if (work >= total) return;         // uniform per workgroup
-  const int nt = MORD ? (work / TM) % TN : work % TN;
-  const int mt = MORD ? work % TM : (work / TN) % TM;
+  const int total1 = (M / BM) * (N / BN) * nsplit;
+  const int total2 = g2.M ? (g2.M / BM) * (g2.N / BN) * nsplit : 0;
+  const int per = (total1 + total2 + 7) / 8;
+  int work = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (work >= total1 + total2) return;   // uniform per workgroup
+  bool mord = MORD;
+  if (work >= total1) {   // the grouped launch's second product (uniform per workgroup)
+    work -= total1;
+    P = g2.P;
+    lda = g2.lda;
+    ldb = g2.ldb;
+    out = g2.out;
+    M = g2.M;
+    N = g2.N;
+    mvalid = g2.mvalid;
+    mord = g2.mord;
+  }
+  const int TM = M / BM, TN = N / BN;
+  const int nt = mord ? (work / TM) % TN : work % TN;
+  const int mt = mord ? work % TM : (work / TN) % TM;
   const int sp = work / (TN * TM);
   const int m0 = mt * BM, n0 = nt * BN;
   const int t0 = sp * kchunk, t1 = min(T, t0 + kchunk);
@@ -356,11 +381,19 @@ __global__ __launch_bounds__(256) void split_sum2_k(const float4* __restrict__ w
 
 template <int BM, int BN, int WM, int WN, int NPC, int NP, int AHEAD, int MORD, int BKT = BK, int NBUF = 2>
 void launch(const PieceBases& P, int lda, int ldb, float* out, float* ws, int M, int N, int T, int nsplit,
-            int mvalid, hipStream_t s) {
+            int mvalid, hipStream_t s, const Prob2* second = nullptr, float* ws2 = nullptr) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int kchunk = ((T + nsplit - 1) / nsplit + BK - 1) / BK * BK;
   nsplit = (T + kchunk - 1) / kchunk;
-  const int total = (M / BM) * (N / BN) * nsplit;
+  Prob2 g2{};
+  if (second) {
+    g2 = *second;
+    if (nsplit > 1) {   // partial slabs into ws2 (all rows), folded by the second sum pass
+      g2.out = ws2;
+      g2.mvalid = g2.M;
+    }
+  }
+  const int total = (M / BM) * (N / BN) * nsplit + (g2.M ? (g2.M / BM) * (g2.N / BN) * nsplit : 0);
   const int per = (total + 7) / 8;
   const size_t smem = NBUF * (size_t)NPC * BKT * (BM + BN) * sizeof(uint16_t);
   static bool attr = false;
@@ -370,12 +403,16 @@ void launch(const PieceBases& P, int lda, int ldb, float* out, float* ws, int M,
     attr = true;
   }
   wgrad_split_k<BM, BN, WM, WN, NPC, NP, AHEAD, MORD, BKT, NBUF><<<8 * per, NT, smem, s>>>(
-      P, lda, ldb, nsplit > 1 ? ws : out, M, N, T, kchunk, nsplit, nsplit > 1 ? M : mvalid);
+      P, lda, ldb, nsplit > 1 ? ws : out, M, N, T, kchunk, nsplit, nsplit > 1 ? M : mvalid, g2);
   if (nsplit > 1) {
-    const int64_t n4 = (int64_t)mvalid * N / 4, slab4 = (int64_t)M * N / 4;
-    const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
-    split_sum2_k<<<blocks, 256, 0, s>>>(reinterpret_cast<const float4*>(ws), reinterpret_cast<float4*>(out), n4,
-                                        slab4, nsplit);
+    auto fold = [&](const float* w, float* o, int m, int n, int mv) {
+      const int64_t n4 = (int64_t)mv * n / 4, slab4 = (int64_t)m * n / 4;
+      const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+      split_sum2_k<<<blocks, 256, 0, s>>>(reinterpret_cast<const float4*>(w), reinterpret_cast<float4*>(o), n4, slab4,
+                                          nsplit);
+    };
+    fold(ws, out, M, N, mvalid);
+    if (second) fold(ws2, second->out, second->M, second->N, second->mvalid);
   }
 }
 
@@ -470,5 +507,43 @@ int hx_wgrad_split(const void* const* dy_pieces, int ldy, const void* const* x_p
     return -1;
   }
 #undef HX_WS_LAUNCH
+  return 0;
+}
+
+// Two weight gradients over the same tokens in ONE launch (bf16x6, both on the 256 x 256 tile):
+// the token split count fills one round of workgroup slots with the two products' tiles
+// together.  Returns the split count (the caller sizes ws1 / ws2 as nsplit * M * N floats when
+// it is > 1), or -1 when the pair does not qualify.
+int hx_wgrad_split_group_plan(int M1, int N1, int M2, int N2, int T, int passes) {
+  if (passes != 6 || !cfg_ok(2, M1, N1, passes) || !cfg_ok(2, M2, N2, passes)) return -1;
+  const int tiles = (M1 / 256) * (N1 / 256) + (M2 / 256) * (N2 / 256);
+  if (tiles > hx_cu_slots()) return -1;
+  int s = std::max(1, hx_cu_slots() / tiles);
+  return std::min(s, std::max(1, T / 256));
+}
+
+int hx_wgrad_split_group(const void* const* dy1, int ldy1, const void* const* x1, int ldx1, float* out1, float* ws1,
+                         int M1, int N1, int mvalid1, const void* const* dy2, int ldy2, const void* const* x2, int ldx2,
+                         float* out2, float* ws2, int M2, int N2, int mvalid2, int T, int nsplit, hipStream_t s) {
+  if (!cfg_ok(2, M1, N1, 6) || !cfg_ok(2, M2, N2, 6) || nsplit < 1) return -1;
+  PieceBases P1;
+  Prob2 g2{};
+  for (int i = 0; i < 3; ++i) {
+    P1.a[i] = (const uint16_t*)dy1[i];
+    P1.b[i] = (const uint16_t*)x1[i];
+    g2.P.a[i] = (const uint16_t*)dy2[i];
+    g2.P.b[i] = (const uint16_t*)x2[i];
+  }
+  g2.lda = ldy2;
+  g2.ldb = ldx2;
+  g2.out = out2;
+  g2.M = M2;
+  g2.N = N2;
+  g2.mvalid = mvalid2;
+  g2.mord = M2 < N2 ? 1 : 0;
+  if (M1 < N1)
+    launch<256, 256, 128, 64, 3, 6, 0, 1, 16, 3>(P1, ldy1, ldx1, out1, ws1, M1, N1, T, nsplit, mvalid1, s, &g2, ws2);
+  else
+    launch<256, 256, 128, 64, 3, 6, 0, 0, 16, 3>(P1, ldy1, ldx1, out1, ws1, M1, N1, T, nsplit, mvalid1, s, &g2, ws2);
   return 0;
 }

@@ -191,12 +191,12 @@ class BertSelfAttention(nn.Module):
         self.value = nn.Linear(config.hidden_size, self.all_head_size)
         self.dropout = nn.Dropout(config.attention_probs_dropout_prob)
 
-    def forward(self, hidden_states, attention_mask_bias, res_grad=None):
+    def forward(self, hidden_states, attention_mask_bias, res_grad=None, wgrad_join=None):
         # bias-less N=3H projection GEMM; the Q/K/V biases are applied (and their
         # gradients produced) inside the fused attention
         gp = ops.GradPlanes()   # the attention backward hands the projection its gradient planes
         qkv = ops.linear3(hidden_states, self.query.weight, self.key.weight, self.value.weight,
-                          None, None, None, res_grad=res_grad, grad_planes=gp)
+                          None, None, None, res_grad=res_grad, grad_planes=gp, wgrad_join=wgrad_join)
         return ops.attention(qkv, attention_mask_bias, self.num_attention_heads, self.dropout.p, self.training,
                              bias=(self.query.bias, self.key.bias, self.value.bias), grad_planes=gp)
 
@@ -208,9 +208,9 @@ class BertSelfOutput(nn.Module):
         self.LayerNorm = BertLayerNorm(config.hidden_size, eps=1e-12)
         self.dropout = nn.Dropout(config.hidden_dropout_prob)
 
-    def forward(self, hidden_states, input_tensor, res_grad=None):
+    def forward(self, hidden_states, input_tensor, res_grad=None, wgrad_defer=None):
         gp = ops.GradPlanes()   # the LN backward hands the dense layer its gradient planes
-        y = ops.linear(hidden_states, self.dense.weight, grad_planes=gp)
+        y = ops.linear(hidden_states, self.dense.weight, grad_planes=gp, wgrad_defer=wgrad_defer)
         return ops.bias_dropout_residual_ln(y, self.dense.bias, input_tensor, self.LayerNorm.weight,
                                             self.LayerNorm.bias, self.LayerNorm.variance_epsilon,
                                             self.dropout.p, self.training, res_grad=res_grad, grad_planes=gp)
@@ -223,9 +223,12 @@ class BertAttention(nn.Module):
         self.output = BertSelfOutput(config)
 
     def forward(self, input_tensor, attention_mask_bias):
-        # the residual gradient of input_tensor is fused into the QKV dgrad GEMM
+        # the residual gradient of input_tensor is fused into the QKV dgrad GEMM; the output
+        # projection's weight gradient runs grouped with the QKV projection's (ops.WgradDefer)
         rg = ops.ResidualGrad()
-        return self.output(self.self(input_tensor, attention_mask_bias, rg), input_tensor, rg)
+        wd = ops.WgradDefer()
+        ctx = self.self(input_tensor, attention_mask_bias, rg, wgrad_join=(self.output.dense.weight, wd))
+        return self.output(ctx, input_tensor, rg, wgrad_defer=wd)
 
 
 class BertIntermediate(nn.Module):

@@ -89,6 +89,20 @@ class ResidualGrad(object):
         return g, None
 
 
+class WgradDefer(object):
+    """Per-forward mailbox that moves one linear's weight gradient into a LATER backward, where
+    it runs grouped with that backward's own weight gradient in one launch (wgrad_split.hip):
+    the attention-output projection (768 x 768: 9 output tiles, alone a 14-way token split at
+    ~0.9 PF/s) joins the QKV projection's (27 tiles).  The joining linear (``linear3``) takes the
+    deferring weight as an extra input so autograd routes that weight's gradient through its
+    backward; its forward arms the box, the deferring linear's backward fills it."""
+    __slots__ = ('armed', 'item')
+
+    def __init__(self):
+        self.armed = False
+        self.item = None
+
+
 class GradPlanes(object):
     """Per-forward mailbox that hands a linear its OUTPUT gradient already split.
 
@@ -455,11 +469,13 @@ class _LinearFn(torch.autograd.Function):
     kernel) straight into the parameters' flat gradient slots."""
 
     @staticmethod
-    def forward(ctx, x, W, b, mbox, gp):
+    def forward(ctx, x, W, b, mbox, gp, defer=None):
         x2 = x.reshape(-1, x.shape[-1])
         ctx.split = split_gemm.active(x2)
         ctx.pieces = ctx.split and split_gemm.nt_ok(W.shape[1], W.shape[0])
         ctx.gp = gp if (ctx.split and b is None) else None
+        # weight gradient deferred to the joining linear's backward (WgradDefer)
+        ctx.defer = defer if (defer is not None and defer.armed and ctx.pieces and b is None) else None
         if ctx.gp is not None:
             ctx.gp.want = True
             ctx.gp.pieces = ctx.pieces
@@ -503,6 +519,9 @@ class _LinearFn(torch.autograd.Function):
             dx = _dgrad_split(dys, W, ctx.xshape, ctx.mbox)
         else:
             dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox)
+        if ctx.defer is not None:   # dW is computed (grouped) by the joining linear's backward
+            ctx.defer.item = (dys, x2, W.shape[0], W.shape[1])
+            return dx, None, None, None, None, None
         slot = grad_slot(W)
         direct = slot is not None
         side = side_begin(dy2.device) if direct else None
@@ -524,18 +543,22 @@ class _LinearFn(torch.autograd.Function):
             x2.record_stream(side)
             if dys is not None:
                 dys.record_stream(side)
-        return dx, dW, db, None, None
+        return dx, dW, db, None, None, None
 
 
-def linear(x, W, b=None, res_grad=None, grad_planes=None):
+def linear(x, W, b=None, res_grad=None, grad_planes=None, wgrad_defer=None):
     """F.linear with direct-to-slot weight/bias gradients on the GPU;
-    ``res_grad``: see ``ResidualGrad``; ``grad_planes``: see ``GradPlanes``."""
+    ``res_grad``: see ``ResidualGrad``; ``grad_planes``: see ``GradPlanes``;
+    ``wgrad_defer``: see ``WgradDefer`` (the weight must also be passed to the joining linear)."""
     if use_kernels(x):
-        return _LinearFn.apply(x, W, b, res_grad, grad_planes)
+        return _LinearFn.apply(x, W, b, res_grad, grad_planes, wgrad_defer)
     return F.linear(x, cast_w(W, x.dtype), cast_w(b, x.dtype))
 
 
 # ----------------------------------------------------------------- FFN block on split planes
+_GROUP_FFN = os.environ.get('HX_WGRAD_GROUP_FFN', '1') == '1'
+
+
 class _FFNSplitFn(torch.autograd.Function):
     """y2 = gelu(x W1^T + b1) W2^T for ``--fp32-gemm bf16x3/x6`` as one autograd node, so
     the GELU epilogue writes the FFN-down GEMM's bf16 input planes directly and the GELU
@@ -591,9 +614,17 @@ class _FFNSplitFn(torch.autograd.Function):
             # GELU backward in the FFN-down data-gradient epilogue: the pieces of
             # dh * gelu'(u) and the FFN-up bias gradient (y1 = gelu'(u), saved by the forward)
             dy1s, db1 = split_gemm.gemm_dgelu(dys, w2, y1, None, grad_slot(b1), deriv=True)
-            dW2 = split_gemm.wgrad_pieces(dys, hs, W2.shape[0], W2.shape[1], grad_slot(W2))
+            # both weight gradients in one launch when they qualify (wgrad_split_group)
+            grp = split_gemm.wgrad_pieces_group([(dys, hs, W2.shape[0], W2.shape[1], grad_slot(W2)),
+                                                 (dy1s, xs, W1.shape[0], W1.shape[1], grad_slot(W1))]) \
+                if _GROUP_FFN else None
+            if grp is not None:
+                dW2, dW1 = grp
+            else:
+                dW2 = split_gemm.wgrad_pieces(dys, hs, W2.shape[0], W2.shape[1], grad_slot(W2))
             dx = _dgrad_pieces(dy1s, w1, ctx.xshape, ctx.mbox)
-            dW1 = split_gemm.wgrad_pieces(dy1s, xs, W1.shape[0], W1.shape[1], grad_slot(W1))
+            if grp is None:
+                dW1 = split_gemm.wgrad_pieces(dy1s, xs, W1.shape[0], W1.shape[1], grad_slot(W1))
             return dx, dW1, db1, dW2, None, None
         dys = _dy_planes(ctx.gp, dy2)
         dh = split_gemm.dgrad(dys, W2)
@@ -652,7 +683,7 @@ class _Linear3Fn(torch.autograd.Function):
     """y = x @ [Wq;Wk;Wv]^T + [bq;bk;bv] as ONE GEMM (N = 3H)."""
 
     @staticmethod
-    def forward(ctx, x, wq, wk, wv, bq, bk, bv, mbox, gp):
+    def forward(ctx, x, wq, wk, wv, bq, bk, bv, mbox, gp, wjoin=None, join=None):
         has_b = bq is not None
         W = _adjacent_view([wq, wk, wv])
         if W is None:
@@ -695,6 +726,11 @@ class _Linear3Fn(torch.autograd.Function):
         ctx.save_for_backward(x2, Wc)
         ctx.params = (wq, wk, wv, bq, bk, bv)
         ctx.has_b = has_b
+        # WgradDefer: this backward also produces ``wjoin``'s gradient (grouped launch)
+        ctx.join = join if (join is not None and wjoin is not None and ctx.pieces and not has_b) else None
+        ctx.wjoin = wjoin if ctx.join is not None else None
+        if ctx.join is not None:
+            ctx.join.armed = True
         ctx.mbox = mbox
         ctx.xshape = x.shape
         ctx.n = [wq.shape[0], wk.shape[0], wv.shape[0]]
@@ -733,8 +769,27 @@ class _Linear3Fn(torch.autograd.Function):
         fb = _adjacent_view(bs) if all(t is not None for t in bs) else None
         direct = fused is not None and (fb is not None or not has_b)
         side = side_begin(dy2.device) if direct else None
+        item = ctx.join.item if ctx.join is not None else None
+        gjoin = None
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            if fused is not None:
+            if item is not None:
+                # the deferred linear's weight gradient, grouped with this one in one launch
+                jdys, jx2, jn_out, jn_in = item
+                ctx.join.item = None
+                jslot = grad_slot(ctx.wjoin)
+                grp = split_gemm.wgrad_pieces_group([(dys, x2, n_out, n_in, fused),
+                                                     (jdys, jx2, jn_out, jn_in, jslot)]) \
+                    if fused is not None else None
+                if grp is not None:
+                    gjoin = grp[1]
+                else:
+                    gjoin = split_gemm.wgrad_pieces(jdys, jx2, jn_out, jn_in, jslot)
+                if side is not None:
+                    jdys.record_stream(side)
+                    jx2.record_stream(side)
+            if item is not None and grp is not None:
+                gW = ws
+            elif fused is not None:
                 wg(fused)
                 gW = ws
             else:
@@ -756,15 +811,17 @@ class _Linear3Fn(torch.autograd.Function):
             if dys is not None:
                 dys.record_stream(side)
         if not has_b:
-            return (dx, gW[0], gW[1], gW[2], None, None, None, None, None)
+            return (dx, gW[0], gW[1], gW[2], None, None, None, None, None, gjoin, None)
         gb = bs if fb is not None else [db[:a], db[a:a + b_], db[a + b_:]]
-        return (dx, gW[0], gW[1], gW[2], gb[0], gb[1], gb[2], None, None)
+        return (dx, gW[0], gW[1], gW[2], gb[0], gb[1], gb[2], None, None, gjoin, None)
 
 
-def linear3(x, wq, wk, wv, bq, bk, bv, res_grad=None, grad_planes=None):
+def linear3(x, wq, wk, wv, bq, bk, bv, res_grad=None, grad_planes=None, wgrad_join=None):
     """``grad_planes``: see ``GradPlanes`` (the fused attention backward deposits the
-    projection's output-gradient planes)."""
-    return _Linear3Fn.apply(x, wq, wk, wv, bq, bk, bv, res_grad, grad_planes)
+    projection's output-gradient planes); ``wgrad_join`` = (weight, ``WgradDefer``): this
+    backward also produces that weight's gradient, deferred from a later linear."""
+    wj, box = wgrad_join if wgrad_join is not None else (None, None)
+    return _Linear3Fn.apply(x, wq, wk, wv, bq, bk, bv, res_grad, grad_planes, wj, box)
 
 
 # ----------------------------------------------------------------- attention core

@@ -305,6 +305,23 @@ def wgrad_pieces(dys, xs, n_out, n_in, slot):
                            n_out, n_in, out)
 
 
+def wgrad_pieces_group(items):
+    """Two weight gradients over the same tokens as ONE launch (wgrad_split.hip's grouped form):
+    ``items`` = [(dys, xs, n_out, n_in, slot)] x 2, as for ``wgrad_pieces``.  Returns the two
+    dW tensors, or None when the pair does not qualify (then run them one by one).
+    ``HX_WGRAD_GROUP=0`` turns grouping off."""
+    if _State.passes != 6 or os.environ.get('HX_WGRAD_GROUP', '1') == '0':
+        return None
+    args, outs = [], []
+    for dys, xs, n_out, n_in, slot in items:
+        if not C().wgrad_split_ok(dys, xs, n_out, n_in):
+            return None
+        out = slot if slot is not None else torch.empty(n_out, n_in, device=dys.device)
+        outs.append(out)
+        args.append((dys, [0, n_out, 2 * n_out], xs, [0, n_in, 2 * n_in], n_out, n_in, out))
+    return outs if C().wgrad_split_group(args) else None
+
+
 def act_pieces(y, b, act):
     """Pieces of act(y + b) written by the bias-activation epilogue."""
     n = npieces()

@@ -137,9 +137,9 @@ def test_rccl_one_rank_reducer_matches_local(dev, tmp_path):
     gradient buffer, launched from the backward hooks; with ``--overlap-wgrad`` from the weight-
     gradient side stream; the end-of-backward callback makes the compute stream wait on the
     collectives).  A one-rank sum is the identity, so the trained weights must equal a run
-    without the reducer bit for bit -- a missed stream dependency (a bucket reduced before its
-    gradient landed, or the optimizer reading a bucket RCCL still writes) shows up as a
-    mismatch."""
+    without the reducer (to the run-to-run noise of the embedding gradient's atomics) -- a
+    missed stream dependency (a bucket reduced before its gradient landed, or the optimizer
+    reading a bucket RCCL still writes) shows up as a mismatch."""
     import socket
     d = tmp_path / 'data'
     write_synthetic_bert_shards(str(d), n_files=1, samples_per_file=64, seq_len=128, max_pred=20, vocab_size=1024,
@@ -168,9 +168,14 @@ def test_rccl_one_rank_reducer_matches_local(dev, tmp_path):
             assert 'force_reducer=True' in r.stdout
         with torch.serialization.safe_globals([argparse.Namespace]):
             ck[name] = torch.load(os.path.join(save, 'checkpoint_last.pt'), map_location='cpu', weights_only=True)
+    # (not bit for bit: the word-embedding gradient adds its frequent-id rows with fp32 atomics,
+    # so two runs differ in the last bits from the first update on -- the tolerance of
+    # test_determinism_gpu.py; a bucket reduced before its gradient landed, or overwritten by a
+    # late collective, moves an Adam update by ~lr, orders of magnitude more)
     for a, b in (('local', 'rccl'), ('local_side', 'rccl_side')):
         for k, v in ck[a]['model'].items():
-            assert torch.equal(ck[b]['model'][k], v), (a, b, k)
+            torch.testing.assert_close(ck[b]['model'][k], v, rtol=1e-5, atol=1e-7, msg=lambda m: '{} {} {}: {}'.format(
+                a, b, k, m))
     assert ck['rccl']['optimizer_history'][-1]['num_updates'] == 3
 
 

@@ -692,3 +692,73 @@ def test_layernorm_writes_consumer_pieces(dev, monkeypatch):
         assert len(calls) == 1, calls
     finally:
         ops.set_fp32_gemm('native')
+
+
+@pytest.mark.parametrize('pair', ['attn', 'ffn'])
+def test_wgrad_split_group_matches_separate(dev, pair):
+    """Grouped weight-gradient launch (wgrad_split.hip, hx_wgrad_split_group): the QKV + attention-
+    output pair and the FFN W1 + W2 pair in one launch give the same dW as two launches (token
+    splits differ, so to fp32 rounding) and both match fp64; T not a multiple of the token block."""
+    from hetseq_9cme_amd import ops
+    from hetseq_9cme_amd.ops import split_gemm as sg
+    from hetseq_9cme_amd.ops._ext import C
+    g = torch.Generator(device='cpu').manual_seed(11)
+    T = 3000
+    shapes = ((768, 256), (256, 256)) if pair == 'attn' else ((1024, 256), (256, 1024))
+    try:
+        ops.set_fp32_gemm('bf16x6')
+        items, refs = [], []
+        for M, N in shapes:
+            dy = torch.randn(T, M, generator=g).to(dev)
+            x = torch.randn(T, N, generator=g).to(dev)
+            items.append((sg.pieces(dy), sg.pieces(x), M, N, None))
+            refs.append((dy.double().t() @ x.double(), dy.double().abs().t() @ x.double().abs()))
+        grouped = sg.wgrad_pieces_group(items)
+        assert grouped is not None
+        sep = [sg.wgrad_pieces(d, x, M, N, None) for d, x, M, N, _ in items]
+    finally:
+        ops.set_fp32_gemm('native')
+    for got, s, (ref, sc) in zip(grouped, sep, refs):
+        assert ((got.double() - ref).abs() / sc).max().item() < 2e-6
+        torch.testing.assert_close(got, s, rtol=1e-5, atol=1e-5)
+
+
+def test_bert_grouped_wgrads_match_ungrouped(dev, monkeypatch):
+    """BERT layer (H = 256, so every weight gradient qualifies for the grouped launch) on the
+    split path: the attention-output dW deferred into the QKV backward and grouped with it
+    (ops.WgradDefer), the FFN's two dW grouped -- every parameter gradient matches the
+    one-launch-per-weight run to fp32 rounding."""
+    from hetseq_9cme_amd import ops
+    from hetseq_9cme_amd.ops import fused, split_gemm
+    from hetseq_9cme_amd.models.bert import BertConfig, BertForPreTraining
+    from hetseq_9cme_amd.parallel.flat_params import FlatParamSpace
+    monkeypatch.setitem(split_gemm.MIN_ROWS, 6, 0)
+    cfg = BertConfig(1024, hidden_size=256, num_hidden_layers=1, num_attention_heads=4, intermediate_size=1024,
+                     max_position_embeddings=128, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    grads = []
+    for grouped in (True, False):
+        monkeypatch.setenv('HX_WGRAD_GROUP', '1' if grouped else '0')
+        monkeypatch.setattr(fused, '_GROUP_FFN', grouped)
+        torch.manual_seed(0)
+        model = BertForPreTraining(cfg).to(dev)
+        model.max_predictions_per_seq = 4
+        flat = FlatParamSpace(model, dev, contiguous_groups=model.flat_contiguous_groups())
+        g = torch.Generator(device='cpu').manual_seed(3)
+        ids = torch.randint(5, 1024, (16, 128), generator=g).to(dev)
+        labels = torch.full_like(ids, -1)
+        labels[:, 7] = ids[:, 7]
+        nsp = torch.randint(0, 2, (16,), generator=g).to(dev)
+        try:
+            ops.set_fp32_gemm('bf16x6')
+            ops.set_step_seed(1)
+            model.train()
+            flat.zero_grad()
+            loss = model(ids, torch.zeros_like(ids), torch.ones_like(ids), labels, nsp)
+            loss.backward()
+            flat.adopt_all()
+        finally:
+            ops.set_fp32_gemm('native')
+        grads.append({n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None})
+    assert grads[0].keys() == grads[1].keys()
+    for n in grads[0]:
+        torch.testing.assert_close(grads[0][n], grads[1][n], rtol=1e-4, atol=1e-6, msg=n)

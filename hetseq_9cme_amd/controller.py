@@ -77,7 +77,8 @@ class Controller(object):
                                    broadcast_params=use_reducer,
                                    bucket_peer_mb=getattr(args, 'bucket_peer_mb', 0.0), force=force)
         if use_reducer and self.cuda and getattr(args, 'comm_cus', 0) > 0:
-            ops.set_reserved_cus(args.comm_cus)   # plans leave these CUs to the overlapped all-reduce
+            # while its buckets are in flight the plans leave these CUs to the all-reduce
+            self.reducer.set_comm_cus(args.comm_cus)
         if not use_reducer:
             self.reducer.enabled = False
         elif getattr(args, 'allreduce_impl', 'rccl') == 'xgmi':

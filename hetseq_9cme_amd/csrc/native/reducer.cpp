@@ -31,6 +31,7 @@
 #include <torch/csrc/distributed/c10d/Work.hpp>
 #include <torch/extension.h>
 
+#include <algorithm>
 #include <atomic>
 #include <memory>
 #include <mutex>
@@ -204,6 +205,12 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
     enabled_ = on && (world_ > 1 || force_) && pg_;
   }
 
+  // --comm-cus: CUs the compute plans leave to the collectives while buckets are in flight
+  void set_comm_cus(int64_t n) {
+    std::lock_guard<std::mutex> lk(mu_);
+    comm_cus_ = (int)std::max<int64_t>(0, n);
+  }
+
   int num_buckets() const { return nb_; }
   int launched() const { return launched_; }
   bool enabled() const { return enabled_; }
@@ -241,6 +248,12 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   void launch_bucket(int b) {
     const int64_t s = bounds_[b], n = bounds_[b + 1] - bounds_[b];
     if (n == 0) return;
+    if (comm_cus_ > 0 && grad_flat_.is_cuda() && !reserving_) {
+      // from the first collective of this backward to its end, the GEMM / weight-gradient plans
+      // leave comm_cus_ CUs to the all-reduce (cu_reserve.hip); finalize_locked() gives them back
+      hx_set_reserved_cus(comm_cus_);
+      reserving_ = true;
+    }
     Tensor view = grad_flat_.narrow(0, s, n);
     if (!grad_flat_.is_cuda()) {   // CPU (gloo): no streams
       std::vector<Tensor> ts{view};
@@ -289,6 +302,10 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
       for (auto& w : works_) w->wait();   // RCCL: the current stream waits, the host does not
     }
     works_.clear();
+    if (reserving_) {
+      hx_set_reserved_cus(0);
+      reserving_ = false;
+    }
   }
 
   Tensor grad_flat_;
@@ -298,6 +315,8 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
   c10::intrusive_ptr<c10d::ProcessGroup> pg_;
   int64_t world_;
   bool force_ = false;   // reduce even in a one-rank group (tests drive the RCCL stream path on one GPU)
+  int comm_cus_ = 0;
+  bool reserving_ = false;
   bool hooks_installed_ = false;
   bool enabled_ = false;
   bool sync_ = true;
@@ -344,6 +363,7 @@ void register_reducer(py::module& m) {
       .def("drop_xgmi", &Reducer::drop_xgmi)
       .def("remove_hooks", &Reducer::remove_hooks)
       .def("set_enabled", &Reducer::set_enabled)
+      .def("set_comm_cus", &Reducer::set_comm_cus)
       .def("num_buckets", &Reducer::num_buckets)
       .def("launched", &Reducer::launched)
       .def("enabled", &Reducer::enabled);

@@ -556,7 +556,9 @@ def linear(x, W, b=None, res_grad=None, grad_planes=None, wgrad_defer=None):
 
 
 # ----------------------------------------------------------------- FFN block on split planes
-_GROUP_FFN = os.environ.get('HX_WGRAD_GROUP_FFN', '1') == '1'
+# FFN W1 / W2 weight gradients as one grouped launch: measured 732 -> 756 us (3 token splits over
+# 72 tiles lose to 7 over 36 each; profiles/r3_wgrad_group_probe.log) -- off by default
+_GROUP_FFN = os.environ.get('HX_WGRAD_GROUP_FFN', '0') == '1'
 
 
 class _FFNSplitFn(torch.autograd.Function):

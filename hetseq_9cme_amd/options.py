@@ -205,9 +205,10 @@ def add_distributed_training_args(parser):
                        help='workgroups per xGMI all-reduce launch (CUs taken from backward while it runs)')
     group.add_argument('--comm-cus', default=0, type=int, metavar='N',
                        help='MI355X: CUs left to the gradient all-reduce while it overlaps the backward (world > 1): '
-                            'the one-round GEMM / weight-gradient plans are sized for the other CUs and RCCL is '
-                            'capped at N channels (NCCL_MAX_NCHANNELS, one workgroup each) -- see '
-                            'csrc/kernels/cu_reserve.hip and profiles/r3_comm_contention.md (0 = off)')
+                            'from the first bucket collective to the end of backward the one-round GEMM / '
+                            'weight-gradient plans are sized for the other CUs, and RCCL is capped at N channels '
+                            '(NCCL_MAX_NCHANNELS, one workgroup each) -- see csrc/kernels/cu_reserve.hip and '
+                            'profiles/r3_comm_contention.md (0 = off)')
     group.add_argument('--force-reducer', action='store_true',
                        help='MI355X: run the bucketed gradient reducer even in a one-rank process group, so a '
                             'one-GPU run exercises the RCCL stream path (buckets, side-stream ordering, '

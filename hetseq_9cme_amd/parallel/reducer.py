@@ -157,6 +157,11 @@ class GradReducer(object):
         self._native.use_xgmi(self.xgmi.h, self.xgmi.stream.cuda_stream)
         return True
 
+    def set_comm_cus(self, n):
+        """--comm-cus: from the first bucket collective of a backward to its end, the GEMM /
+        weight-gradient plans leave ``n`` CUs to the collectives (csrc/kernels/cu_reserve.hip)."""
+        self._native.set_comm_cus(int(n))
+
     def check_transport(self):
         """Raise if the xGMI transport reported a timed-out wait (synchronising)."""
         if self.xgmi is not None:

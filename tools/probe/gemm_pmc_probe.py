@@ -21,15 +21,10 @@ def main():
         x = torch.rand(T, n_in, device='cuda') * 2 - 1
         W = (torch.rand(n_out, n_in, device='cuda') * 2 - 1) * 0.05
         xs = sg.pieces(x)
-        wf, _ = sg.weight_pieces(W)
-        kb = int(os.environ.get('KBLOCK', '0'))
-        if kb:
-            def blk(p):
-                return p.view(p.shape[0], 3, -1, 16).permute(0, 2, 1, 3).contiguous().view(p.shape[0], -1)
-            xs, wf = blk(xs), blk(wf)
+        wf, _ = sg.weight_pieces(W)   # in the layout the plan reads (B16 where sg.b16(n_out))
         from hetseq_9cme_amd.ops._ext import C
         for _ in range(10):
-            C().gemm_split(xs, wf, 6, None, False, kb)
+            sg.gemm(xs, wf)
         torch.cuda.synchronize()
     print('done')
 

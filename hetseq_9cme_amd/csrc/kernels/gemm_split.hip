@@ -636,16 +636,22 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_piece_k(
   };
   if constexpr (EPI == 0 || EPI == 3 || EPI == 7) {
     // EPI 3 = EPI 0 with beta: one row block of accumulators at a time (a sched barrier keeps
-    // the compiler from hoisting every block's C loads: 256-VGPR cap)
+    // the compiler from hoisting every block's C loads: 256-VGPR cap); row block a + 1's C
+    // loads are issued before row block a is summed, so one load latency per tile is exposed
+    // instead of one per row block
+    f32x4 c[2][NB][4];
+    auto ldc = [&](int a, f32x4 (&d)[NB][4]) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq)
+          d[b][gq] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(cbuf.r, coff(a, b, gq), 0, 0));
+    };
+    if constexpr (EPI == 3) ldc(0, c[0]);
 #pragma unroll
     for (int a = 0; a < MB; ++a) {
-      f32x4 c[NB][4];
       if constexpr (EPI == 3) {
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-#pragma unroll
-          for (int gq = 0; gq < 4; ++gq)
-            c[b][gq] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(cbuf.r, coff(a, b, gq), 0, 0));
+        if (a + 1 < MB) ldc(a + 1, c[(a + 1) & 1]);
       }
 #pragma unroll
       for (int b = 0; b < NB; ++b)
@@ -653,7 +659,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_piece_k(
         for (int gq = 0; gq < 4; ++gq) {
           tr(a, b, gq);
           f32x4 o = {acc[a][b][4 * gq], acc[a][b][4 * gq + 1], acc[a][b][4 * gq + 2], acc[a][b][4 * gq + 3]};
-          if constexpr (EPI == 3) o += c[b][gq];
+          if constexpr (EPI == 3) o += c[a & 1][b][gq];
           __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), cbuf.r, coff(a, b, gq), 0, 0);
         }
       __builtin_amdgcn_sched_barrier(0);
@@ -669,23 +675,35 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_piece_k(
 #pragma unroll
       for (int i = 0; i < 4; ++i) csum[b][i] = 0.f;
     const hx::Buf xbuf(EPI == 2 ? g.aux + (int64_t)m0 * g.ldaux + n0 : g.C, (uint32_t)((int64_t)mrows * g.ldaux * 4));
+    // the bias columns of this lane (all row blocks share them), loaded once
+    float bias[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (g.bias) t = *reinterpret_cast<const float4*>(g.bias + n0 + ncol + 32 * b);
+      bias[b][0] = t.x; bias[b][1] = t.y; bias[b][2] = t.z; bias[b][3] = t.w;
+    }
+    // EPI 2: the aux block of (a, b) is loaded while the previous block is processed (two
+    // register sets), so the tile exposes one load latency instead of MB * NB
+    f32x4 ub[2][4];
+    auto ldu = [&](int a, int b, f32x4 (&d)[4]) {
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq)
+        d[gq] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              xbuf.r, (uint32_t)((mrow + 32 * a + 8 * gq) * g.ldaux + ncol + 32 * b) * 4, 0,
+                                              0));
+    };
+    if constexpr (EPI == 2) ldu(0, 0, ub[0]);
 #pragma unroll
     for (int a = 0; a < MB; ++a)
 #pragma unroll
       for (int b = 0; b < NB; ++b) {
-        float bb[4] = {0.f, 0.f, 0.f, 0.f};
-        if (g.bias) {
-          const float4 t = *reinterpret_cast<const float4*>(g.bias + n0 + ncol + 32 * b);
-          bb[0] = t.x; bb[1] = t.y; bb[2] = t.z; bb[3] = t.w;
-        }
-        f32x4 u[4];
+        const float* bb = bias[b];
+        const int blk = a * NB + b;
         if constexpr (EPI == 2) {
-#pragma unroll
-          for (int gq = 0; gq < 4; ++gq)
-            u[gq] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                  xbuf.r, (uint32_t)((mrow + 32 * a + 8 * gq) * g.ldaux + ncol + 32 * b) * 4,
-                                                  0, 0));
+          if (blk + 1 < MB * NB) ldu((blk + 1) / NB, (blk + 1) % NB, ub[(blk + 1) & 1]);
         }
+        const f32x4* u = ub[blk & 1];
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
           tr(a, b, gq);
@@ -809,7 +827,12 @@ void launch_one(const Args& a, hipStream_t s) {
 // BERT shape (profiles/r3_gemm_stagger_probe.log); the same pipeline on 16x16x32 MFMAs (two
 // 16-deep pieces side by side along k, three MFMAs per 16x16 block and stage) 1-6 % slower --
 // the clock gain of the 16x16 shape (r3_mfma16_clock_probe.log) does not survive its 26 instead
-// of 15 fragment reads per k step (profiles/r3_gemm_mfma16_probe.log).
+// of 15 fragment reads per k step (profiles/r3_gemm_mfma16_probe.log).  Ping-pong (the two waves
+// of each SIMD half a k step apart: one multiplies while the other reads its fragments, two
+// barrier-delimited phases per k step, MI355X_MICROARCH.md 'Two waves per SIMD') was correct
+// at every k-step count but 0.5-2.4 % slower on the plain shapes and 11 % on the GELU epilogue
+// (profiles/r3_gemm_pingpong_probe.log): with the clock held at 1.8-1.9 GHz by power
+// (profiles/r3_gemm_pmc.md) the fragment-read gaps it closes are not what limits the loop.
 static int pipe_mode() {
   const char* e = getenv("HX_GEMM_PIPE");
   return e ? atoi(e) : 3;

@@ -27,19 +27,23 @@ def main():
     _, w2t = sg.weight_pieces(W2)
     u, _ = sg.gemm_gelu(xs, w1f, b1)
     gd, _ = sg.gemm_gelu(xs, w1f, b1, deriv=True)
+    hs = sg.pieces(torch.rand(T, I, device='cuda') * 2 - 1)
+    w2f, _ = sg.weight_pieces(W2)
     fl = 2.0 * T * H * I * 6
     res = {}
     for rnd in range(3):
         for cfg in ('0', '1', '7'):
             os.environ['HX_GEMM_CFG'] = cfg
-            for name, fn in (('gelu(u)', lambda: sg.gemm_gelu(xs, w1f, b1)),
+            for name, fn in (('plain C', lambda: sg.gemm(xs, w1f)),
+                             ('down N768', lambda: sg.gemm(hs, w2f)),
+                             ('gelu(u)', lambda: sg.gemm_gelu(xs, w1f, b1)),
                              ("gelu+gelu'", lambda: sg.gemm_gelu(xs, w1f, b1, deriv=True)),
                              ('dgelu(u)', lambda: sg.gemm_dgelu(dys, w2t, u, None, None)),
                              ("dgelu(gelu')", lambda: sg.gemm_dgelu(dys, w2t, gd, None, None, deriv=True))):
                 k = (name, cfg)
                 res[k] = min(res.get(k, 1e9), timeit(fn))
     os.environ.pop('HX_GEMM_CFG', None)
-    for name in ('gelu(u)', "gelu+gelu'", 'dgelu(u)', "dgelu(gelu')"):
+    for name in ('plain C', 'down N768', 'gelu(u)', "gelu+gelu'", 'dgelu(u)', "dgelu(gelu')"):
         print('{:13s} '.format(name) + ' | '.join('cfg {} {:6.1f} us {:5.0f} TF/s'.format(c, res[(name, c)],
                                                                                       fl / res[(name, c)] / 1e6)
                                                  for c in ('0', '1', '7')), flush=True)

@@ -1,6 +1,7 @@
 """Piece GEMM pipelines A/B (gemm_split.hip, bf16x6, T = 16384 BERT-base forward shapes):
-HX_GEMM_PIPE=3 (interleaved DMA) vs 6 (3 on 16x16x32 MFMAs) [vs 5 (3 with the SIMD partners
-staggered by one pass: measured 2-3 % slower, removed; profiles/r3_gemm_stagger_probe.log)], both
+HX_GEMM_PIPE=3 (interleaved DMA) by default; PIPES=... adds other pipelines.  Records: 6 (3 on
+16x16x32 MFMAs, profiles/r3_gemm_mfma16_probe.log) and 5 (3 with the SIMD partners staggered by
+one pass, profiles/r3_gemm_stagger_probe.log) were measured slower and removed.  Both
 piece layouts (lay2: weights B16; lay3: both operands B16), cfgs 0 and 1, interleaved rounds in
 one process; every variant checked against fp64."""
 import os
@@ -35,7 +36,7 @@ def main():
             res = {}
             for rnd in range(3):
                 for lay, a_ in ((2, xs), (3, xb)):
-                    for pipe in os.environ.get('PIPES', '3,6').split(','):
+                    for pipe in os.environ.get('PIPES', '3').split(','):
                         os.environ['HX_GEMM_PIPE'] = pipe
                         t = timeit(lambda: C().gemm_split(a_, wb, 6, None, False, lay))
                         k = (lay, pipe)

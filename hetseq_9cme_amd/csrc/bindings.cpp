@@ -710,6 +710,26 @@ Tensor gemm_split(Tensor a, Tensor b, int64_t passes, OptT out_, bool beta, int6
   dbg_finite(out, "gemm_split");
   return out;
 }
+// a . b^T over a deep reduction with few output tiles: ks split-K slabs (hx_gemm_split_ks when
+// ks = 0) written as partial products, summed here; lay as gemm_split
+Tensor gemm_split_k(Tensor a, Tensor b, int64_t passes, int64_t ks, int64_t lay) {
+  const int64_t npc = passes == 6 ? 3 : 2;
+  TORCH_CHECK(passes == 3 || passes == 6, "gemm_split_k: passes must be 3 or 6");
+  TORCH_CHECK(gemm_split_ok(a, b, npc), "gemm_split_k: unsupported operands");
+  const int64_t M = a.size(0), N = b.size(0), K = a.size(1) / npc;
+  if (ks <= 0) ks = hx_gemm_split_ks((int)M, (int)N, (int)K, (int)passes);
+  if (ks == 1) return gemm_split(a, b, passes, OptT(), false, lay);
+  Tensor part = torch::empty({ks, M, N}, a.options().dtype(torch::kFloat32));
+  const int cfg = hx_gemm_split_plan((int)M, (int)N, (int)K, (int)passes, (int)lay);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  TORCH_CHECK(hx_gemm_split_nt(a.data_ptr(), npc * K, (lay & 1) ? 16 : K, b.data_ptr(), npc * K, (lay & 2) ? 16 : K,
+                               part.data_ptr<float>(), N, (int)M, (int)N, (int)K, (int)passes, 0, nullptr, cfg,
+                               cur_stream(a), (int)lay, (int)ks, M * N) == 0,
+              "gemm_split_k: launch failed (slab count must divide the k steps)");
+  Tensor out = part.sum(0);
+  dbg_finite(out, "gemm_split_k");
+  return out;
+}
 // FFN up: u = a . b^T + bias (fp32, kept for the backward) and the pieces of gelu(u)
 // (dmode 1: C gets gelu'(u) instead of u -- all the backward needs, from the same erf)
 std::vector<Tensor> gemm_split_gelu(Tensor a, Tensor b, int64_t passes, OptT bias, int64_t lay, int64_t dmode) {
@@ -960,6 +980,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("split_planes_t", &split_planes_t);
   m.def("split_weight", &split_weight, py::arg("W"), py::arg("npieces"), py::arg("b16") = 0);
   m.def("gemm_split_weight_b16", &hx_gemm_split_weight_b16);
+  m.def("gemm_split_k", &gemm_split_k, py::arg("a"), py::arg("b"), py::arg("passes"), py::arg("ks") = 0,
+        py::arg("lay") = 0);
+  m.def("gemm_split_ks", &hx_gemm_split_ks);
   m.def("gemm_split", &gemm_split, py::arg("a"), py::arg("b"), py::arg("passes"), py::arg("out") = py::none(),
         py::arg("beta") = false, py::arg("lay") = 0);
   m.def("gemm_split_gelu", &gemm_split_gelu, py::arg("a"), py::arg("b"), py::arg("passes"), py::arg("bias"),

@@ -136,7 +136,10 @@ int hx_gemm_split_colpart_rows(int M, int cfg);
 int hx_gemm_split_weight_b16(int N, int passes);
 int hx_gemm_split_nt(const void* A, int64_t lda, int64_t a_ps, const void* B, int64_t ldb, int64_t b_ps, float* C,
                      int64_t ldc, int M, int N, int K, int passes, int beta, const HxGemmEpi* epi, int cfg,
-                     hipStream_t s, int lay = 0);
+                     hipStream_t s, int lay = 0, int ks = 1, int64_t c_zs = 0);
+// split-K slab count for the piece GEMM of an M x N output over K (1 = none): deep reductions
+// with too few output tiles to fill the CUs (the MLM decoder's data gradient, K = 30720)
+int hx_gemm_split_ks(int M, int N, int K, int passes);
 int hx_gemm_split_stamps(const void* A, const void* B, float* C, int M, int N, int K, unsigned long long* stamps,
                          hipStream_t s, int lay = 0);
 void hx_dma_probe(const void* src, uint32_t bytes, int seg, int ld, int iters, int grid, hipStream_t s);

@@ -181,6 +181,8 @@ struct Args {
   float* colpart;
   uint32_t ksa, ksb;   // bytes between consecutive BK-deep k steps of a row (2 BK natural, 2 BK npc blocked)
   int dmode;           // HxGemmEpi::dmode
+  int ks;              // split-K slabs: slab z reduces k steps [z K / ks, (z + 1) K / ks) into C + z c_zs
+  int64_t c_zs;
   unsigned long long* stamps;   // diagnostic build (PIPE 9): per wave [dma issue, mfma, dma wait, barrier, total]
 };
 
@@ -209,12 +211,13 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_piece_k(
   extern __shared__ __attribute__((aligned(16))) char lds[];
 
   const int TM = (g.M + BM - 1) / BM, TN = g.N / BN, total = TM * TN;
-  const int per = (total + 7) / 8;
-  const int work = (blockIdx.x % 8) * per + blockIdx.x / 8;
-  if (work >= total) return;   // uniform per workgroup
+  const int per = (total * g.ks + 7) / 8;
+  const int work0 = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (work0 >= total * g.ks) return;   // uniform per workgroup
+  const int z = work0 / total, work = work0 - z * total;   // split-K slab, output tile
   const int nt = work % TN, mt = work / TN;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int nit = g.K / BK;
+  const int nit = g.K / BK / g.ks, it0 = z * nit;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w % NWM, wn = w / NWM, h = lane >> 5, l32 = lane & 31;
@@ -270,7 +273,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_piece_k(
   const uint32_t lds0 = (uint32_t)(size_t)(lds_void*)lds;   // LDS byte address of the stages
   auto dma = [&](int it, int buf) {
     const uint32_t st = lds0 + buf * STAGE;
-    const uint32_t koa = (uint32_t)it * g.ksa, kob = (uint32_t)it * g.ksb;
+    const uint32_t koa = (uint32_t)(it0 + it) * g.ksa, kob = (uint32_t)(it0 + it) * g.ksb;
 #pragma unroll
     for (int j = 0; j < JHI; ++j) {
       if (j < JLO || j < cnt) dma16(isa[j] ? ra : rb, st + dsto[j], voff[j] + (isa[j] ? koa : kob));
@@ -278,7 +281,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_piece_k(
   };
   auto dma_one = [&](int it, int buf, int j) {   // this wave's j-th DMA piece of stage it
     const uint32_t st = lds0 + buf * STAGE;
-    const uint32_t ko = (uint32_t)it * (isa[j] ? g.ksa : g.ksb);
+    const uint32_t ko = (uint32_t)(it0 + it) * (isa[j] ? g.ksa : g.ksb);
     dma16(isa[j] ? ra : rb, st + dsto[j], voff[j] + ko);
   };
   auto wait_stage = [&]() {   // all but this wave's youngest stage of DMAs landed
@@ -624,7 +627,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_piece_k(
   // of each 32 x 32 block and its columns (l32 & ~3) .. + 3.  Buffer resources over the
   // tile's valid rows: stores past M are dropped, loads past M return 0 (no branches).
   const int mrow = wm * WM + 4 * h + (l32 & 3), ncol = wn * WN + (l32 & ~3);
-  const hx::Buf cbuf(g.C + (int64_t)m0 * g.ldc + n0, (uint32_t)((int64_t)mrows * g.ldc * 4));
+  const hx::Buf cbuf(g.C + z * g.c_zs + (int64_t)m0 * g.ldc + n0, (uint32_t)((int64_t)mrows * g.ldc * 4));
   auto coff = [&](int a, int b, int gq) { return (uint32_t)((mrow + 32 * a + 8 * gq) * g.ldc + ncol + 32 * b) * 4; };
   typedef float f32x4 __attribute__((ext_vector_type(4)));
   // transpose one 4-row group in place: acc[a][b][4 gq + i] = column i of this lane's row
@@ -704,8 +707,19 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_piece_k(
           if (blk + 1 < MB * NB) ldu((blk + 1) / NB, (blk + 1) % NB, ub[(blk + 1) & 1]);
         }
         const f32x4* u = ub[blk & 1];
+        // row groups in pairs (gq, gq + 1): after the quad transpose a lane holds 4 columns of
+        // one row; lanes l and l ^ 4 hold the two halves of 8 consecutive columns of the same
+        // row, so one swizzle per piece word gives the even lane row gq's 8 columns and the odd
+        // lane row gq + 1's -- the piece stores go out as 16-B (8 bf16) stores, half the store
+        // instructions of 8-B ones (the epilogue is store-issue bound: MI355X_MICROARCH.md, the
+        // attention store-tail row of the price list)
+        const bool odd = (l32 & 4) != 0;
 #pragma unroll
-        for (int gq = 0; gq < 4; ++gq) {
+        for (int gp = 0; gp < 2; ++gp) {
+          uint2 pk[2][NPC];
+#pragma unroll
+          for (int s2 = 0; s2 < 2; ++s2) {
+          const int gq = 2 * gp + s2;
           tr(a, b, gq);
           float v[4] = {acc[a][b][4 * gq], acc[a][b][4 * gq + 1], acc[a][b][4 * gq + 2], acc[a][b][4 * gq + 3]};
           if constexpr (EPI == 1) {
@@ -751,10 +765,18 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_piece_k(
               hp[i] = hx::bf2f(hx::f2bf(v[i]));
               if (p + 1 < NPC) v[i] -= hp[i];
             }
-            const uint2 pk = pack4(hp);
-            __builtin_amdgcn_raw_buffer_store_b64(
-                __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int, pk), pbuf.r, poff(a, b, gq, p), 0,
-                0);
+            pk[s2][p] = pack4(hp);
+          }
+          }
+          // 0x101f: swizzle bitmask mode, and 0x1f, xor 4 (lane l <-> l ^ 4)
+#pragma unroll
+          for (int p = 0; p < NPC; ++p) {
+            const uint2 snd = odd ? pk[0][p] : pk[1][p];
+            const uint32_t r0 = (uint32_t)__builtin_amdgcn_ds_swizzle((int)snd.x, 0x101f);
+            const uint32_t r1 = (uint32_t)__builtin_amdgcn_ds_swizzle((int)snd.y, 0x101f);
+            const u32x4 o = odd ? u32x4{r0, r1, pk[1][p].x, pk[1][p].y} : u32x4{pk[0][p].x, pk[0][p].y, r0, r1};
+            __builtin_amdgcn_raw_buffer_store_b128(o, pbuf.r, poff(a, b, 2 * gp + (odd ? 1 : 0), p) - (odd ? 8u : 0u),
+                                                   0, 0);
           }
         }
         __builtin_amdgcn_sched_barrier(0);
@@ -808,7 +830,7 @@ template <int BM, int BN, int WM, int WN, int NPC, int NP, int BK, int NBUF, int
           int OCC = 1>
 void launch_one(const Args& a, hipStream_t s) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
-  const int total = ((a.M + BM - 1) / BM) * (a.N / BN);
+  const int total = ((a.M + BM - 1) / BM) * (a.N / BN) * a.ks;
   const int per = (total + 7) / 8;
   const size_t smem = (size_t)NBUF * NPC * (BM + BN) * BK * 2;
   static bool attr = false;
@@ -937,6 +959,19 @@ int hx_gemm_split_weight_b16(int N, int passes) {
   return (c == 0 || c == 1 || c == 7) ? 1 : 0;
 }
 
+int hx_gemm_split_ks(int M, int N, int K, int passes) {
+  const int cfg = hx_gemm_split_plan(M, N, K, passes, 0);
+  if (cfg < 0) return 1;
+  const int bk = (passes == 6 && cfg != 2) ? 16 : 32;
+  const int tiles = (M + cfg_bm(cfg) - 1) / cfg_bm(cfg) * (N / cfg_bn(cfg)), slots = hx_cu_slots();
+  if (tiles * 2 > slots || K < 8192) return 1;
+  // the most slabs that keep one round (tiles * ks <= slots), each slab >= 2048 deep
+  int best = 1;
+  for (int ks = 2; ks <= 16; ++ks)
+    if (tiles * ks <= slots && K % (bk * ks) == 0 && K / ks >= 2048) best = ks;
+  return best;
+}
+
 int hx_gemm_split_colpart_rows(int M, int cfg) {
   if (cfg < 0 || cfg >= kCfgs) return 0;
   return (M + cfg_bm(cfg) - 1) / cfg_bm(cfg) * cfg_nwm(cfg);
@@ -944,12 +979,15 @@ int hx_gemm_split_colpart_rows(int M, int cfg) {
 
 int hx_gemm_split_nt(const void* A, int64_t lda, int64_t a_ps, const void* B, int64_t ldb, int64_t b_ps, float* C,
                      int64_t ldc, int M, int N, int K, int passes, int beta, const HxGemmEpi* epi, int cfg,
-                     hipStream_t s, int lay) {
+                     hipStream_t s, int lay, int ks, int64_t c_zs) {
   const int npc = passes == 6 ? 3 : passes == 3 ? 2 : 0;
   if (!npc || M < 1 || cfg < 0 || cfg >= kCfgs || N % cfg_bn(cfg)) return -1;
   if (cfg >= 3 && npc != 3) return -1;
   const int bk = (npc == 3 && cfg != 2) ? 16 : 32;
   if (K % bk || npc * a_ps > lda || npc * b_ps > ldb) return -1;
+  // split-K: plain stores of ks partial products (C + z c_zs), whole k steps per slab
+  if (ks < 1 || K % (bk * ks) || (ks > 1 && (beta || (epi && epi->kind) || c_zs < (int64_t)(M - 1) * ldc + N)))
+    return -1;
   // lay bit 0 / bit 1: A / B operand in the B16 layout [rows][K / 16][3][16] (bf16x6, cfgs 0 1 3 5)
   // instead of [rows][npc][K]: one 16-deep k step of a row is 96 contiguous bytes
   if (lay && (lay > 3 || npc != 3 || !(cfg == 0 || cfg == 1 || cfg == 7 || ((cfg == 3 || cfg == 5) && lay == 3))))
@@ -976,6 +1014,8 @@ int hx_gemm_split_nt(const void* A, int64_t lda, int64_t a_ps, const void* B, in
   a.p_ps = epi ? epi->p_ps : 0;
   a.colpart = epi ? epi->colpart : nullptr;
   a.dmode = epi ? epi->dmode : 0;
+  a.ks = ks;
+  a.c_zs = c_zs;
   a.ksa = (uint32_t)(bk * 2 * ((lay & 1) ? npc : 1));
   a.ksb = (uint32_t)(bk * 2 * ((lay & 2) ? npc : 1));
   a.stamps = nullptr;
@@ -1018,6 +1058,7 @@ int hx_gemm_split_stamps(const void* A, const void* B, float* C, int M, int N, i
   a.N = N;
   a.K = K;
   a.ksa = a.ksb = lay ? 96 : 32;
+  a.ks = 1;
   a.stamps = stamps;
   if (lay)
     launch_one<256, 192, 64, 96, 3, 6, 16, 3, 0, 9, 1>(a, s);

@@ -842,12 +842,22 @@ class _DecoderXentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, W, bias, labels):
         ctx.split = split_gemm.active(h, W.shape[0])
+        ctx.pieces = False
         if ctx.split:    # fp32 on bf16 matrix cores (--fp32-gemm)
             # vocabulary padded to a multiple of 256 (zero weight rows): 16-B aligned logits
             # rows for the GEMM epilogue (694 -> 598 us at BERT-base phase 1) and the backward's
             # planes; the padding columns stay exactly 0 and are never read as logits
             V = W.shape[0]
-            full, _ = split_gemm.forward(h, W, rpad=(V + 255) // 256 * 256)
+            Vp = (V + 255) // 256 * 256
+            if _decoder_pieces_ok(h, W, Vp):
+                # hand-written piece GEMM (gemm_split.hip): each distinct piece of h and of the
+                # padded W staged once, all passes from registers
+                npc = split_gemm.npieces()
+                ctx.pieces = True
+                wf = split_gemm.planes(W, tuple(range(npc)), rpad=Vp)
+                full = C().gemm_split(split_gemm.pieces(h), wf, split_gemm.passes(), None, False, 0)
+            else:
+                full, _ = split_gemm.forward(h, W, rpad=Vp)
             logits = full[:, :V]
         else:
             full = logits = torch.mm(h, cast_w(W, h.dtype).t())
@@ -871,6 +881,19 @@ class _DecoderXentFn(torch.autograd.Function):
         dbias = C().colsum(dl, scale, grad_slot(bias) if bias is not None else None)
         hs = h * scale.to(h.dtype)
         slot = grad_slot(Wp)
+        if ctx.split and ctx.pieces:
+            # pieces form: dh = dl . W on the piece GEMM with the reduction over the padded
+            # vocabulary cut into split-K slabs (40 output tiles alone would leave 216 CUs idle),
+            # W^T's pieces zero for the padding rows; dW on the split-piece wgrad kernel
+            V, H = dl.shape[1], hs.shape[1]
+            Vp = dl_full.shape[1]
+            npc = split_gemm.npieces()
+            dls = split_gemm.pieces(dl_full)
+            wt = split_gemm.weight_planes_t(Wp, rpad=Vp, order=tuple(range(npc)))
+            dh = C().gemm_split_k(dls, wt, split_gemm.passes(), 0, 0).mul_(scale)
+            out = slot if slot is not None else torch.empty(V, H, device=dl.device)
+            dW = split_gemm.wgrad_pieces(dls, split_gemm.pieces(hs), Vp, H, out)
+            return dh, dW, dbias, None
         if ctx.split:
             # logits-gradient planes zero-padded to a multiple of 256 columns: 16-B rows for
             # the data-gradient GEMM and whole 256-row tiles for the weight-gradient kernel
@@ -901,6 +924,17 @@ class _DecoderXentFn(torch.autograd.Function):
             dl.record_stream(side)
             hs.record_stream(side)
         return dh, dW, dbias, None
+
+
+def _decoder_pieces_ok(h, W, Vp):
+    """The MLM decoder on the hand-written piece GEMMs (bf16x6 default, as the linears:
+    split_gemm.nt_ok): forward [M, Vp] over K = H, data gradient [M, H] over K = Vp in split-K
+    slabs, weight gradient on wgrad_split.hip."""
+    H = W.shape[1]
+    if not split_gemm.nt_ok(H, Vp) or os.environ.get('HX_DECODER_PIECES', '1') == '0':
+        return False
+    npc = split_gemm.npieces()
+    return Vp * npc * H * 2 < (1 << 31) and Vp % 256 == 0 and H % 192 == 0
 
 
 def decoder_xent(h, W, bias, labels):

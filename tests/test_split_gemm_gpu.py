@@ -762,3 +762,67 @@ def test_bert_grouped_wgrads_match_ungrouped(dev, monkeypatch):
     assert grads[0].keys() == grads[1].keys()
     for n in grads[0]:
         torch.testing.assert_close(grads[0][n], grads[1][n], rtol=1e-4, atol=1e-6, msg=n)
+
+
+@pytest.mark.parametrize('ks', [0, 2, 3, 5])
+def test_piece_gemm_split_k(dev, ks):
+    """Split-K slabs of the piece GEMM (gemm_split_k: slab z reduces its share of the k steps
+    into its own partial product, summed after) against fp64, for explicit slab counts and the
+    planned one (ks = 0), on a narrow output over a deep reduction."""
+    from hetseq_9cme_amd import ops
+    from hetseq_9cme_amd.ops import split_gemm as sg
+    from hetseq_9cme_amd.ops._ext import C
+    g = torch.Generator(device='cpu').manual_seed(90 + ks)
+    M, N, K = 700, 768, (240 * 16 * ks if ks else 9600)
+    a = (torch.rand(M, K, generator=g) * 2 - 1).to(dev)
+    W = (torch.rand(N, K, generator=g) * 2 - 1).to(dev)
+    try:
+        ops.set_fp32_gemm('bf16x6')
+        if ks == 0:
+            assert C().gemm_split_ks(M, N, K, 6) > 1
+        y = C().gemm_split_k(sg.pieces(a), sg.pieces(W), 6, ks, 0)
+    finally:
+        ops.set_fp32_gemm('native')
+    ref = a.double() @ W.double().t()
+    sc = a.double().abs() @ W.double().abs().t()
+    assert ((y.double() - ref).abs() / sc).max().item() < 1.5e-6
+
+
+def test_decoder_pieces_path_matches_fp64(dev, monkeypatch):
+    """The MLM decoder + softmax-xent on the piece GEMMs (forward over the padded vocabulary,
+    split-K data gradient, split-piece weight gradient) against fp64 autograd, and against the
+    pass-planes path it replaces (HX_DECODER_PIECES=0)."""
+    from hetseq_9cme_amd import ops
+    g = torch.Generator(device='cpu').manual_seed(91)
+    M, H, V = 512, 768, 9000
+    h0 = (torch.randn(M, H, generator=g) * 0.5).to(dev)
+    W0 = (torch.randn(V, H, generator=g) * 0.05).to(dev)
+    b0 = (torch.randn(V, generator=g) * 0.1).to(dev)
+    labels = torch.randint(0, V, (M,), generator=g).to(dev)
+    labels[::7] = -1
+
+    def run():
+        h = h0.clone().requires_grad_(True)
+        W = W0.clone().requires_grad_(True)
+        b = b0.clone().requires_grad_(True)
+        loss = ops.decoder_xent(h, W, b, labels)
+        loss.backward()
+        return loss.detach(), h.grad, W.grad, b.grad
+
+    try:
+        ops.set_fp32_gemm('bf16x6')
+        got = run()
+        monkeypatch.setenv('HX_DECODER_PIECES', '0')
+        old = run()
+    finally:
+        ops.set_fp32_gemm('native')
+    hd, Wd, bd = h0.double().requires_grad_(True), W0.double().requires_grad_(True), b0.double().requires_grad_(True)
+    ref_loss = torch.nn.functional.cross_entropy(hd @ Wd.t() + bd, labels, ignore_index=-1)
+    ref_loss.backward()
+    ref = (ref_loss.detach(), hd.grad, Wd.grad, bd.grad)
+    for name, x, o, r in zip(('loss', 'dh', 'dW', 'dbias'), got, old, ref):
+        scale = r.abs().max().item()
+        err = (x.double() - r).abs().max().item() / scale
+        assert err < 2e-6, (name, err)
+        err_old = (o.double() - r).abs().max().item() / scale
+        assert err_old < 1e-5, (name, 'planes path', err_old)

@@ -672,6 +672,41 @@ std::vector<Tensor> split_weight(Tensor W, int64_t npieces, int64_t b16) {
   return {wf, wt};
 }
 
+// split_weight for a list of weights in ONE launch: [(wf, wt)] per weight, masks as split_weight's b16
+std::vector<std::vector<Tensor>> split_weight_many(std::vector<Tensor> Ws, int64_t npieces, std::vector<int64_t> masks) {
+  TORCH_CHECK(!Ws.empty() && Ws.size() <= HX_WBATCH && masks.size() == Ws.size(),
+              "split_weight_many: 1..64 weights, one mask each");
+  TORCH_CHECK(npieces == 2 || npieces == 3, "split_weight_many: 2 or 3 pieces");
+  HxWeightBatch d{};
+  d.n = (int)Ws.size();
+  std::vector<std::vector<Tensor>> out;
+  int tiles = 0;
+  for (int i = 0; i < d.n; ++i) {
+    const Tensor& W = Ws[i];
+    check_f32(W, "split_weight_many input");
+    TORCH_CHECK(W.dim() == 2 && W.is_contiguous() && W.size(0) % 64 == 0 && W.size(1) % 64 == 0 &&
+                    aligned16(W.data_ptr()) && W.device() == Ws[0].device(),
+                "split_weight_many: every W contiguous [N, K], N and K multiples of 64, one device");
+    TORCH_CHECK(masks[i] >= 0 && masks[i] <= 3 && (!masks[i] || npieces == 3), "split_weight_many: mask");
+    const int64_t N = W.size(0), K = W.size(1);
+    auto bf = W.options().dtype(torch::kBFloat16);
+    Tensor wf = torch::empty({N, npieces * K}, bf), wt = torch::empty({K, npieces * N}, bf);
+    d.W[i] = W.data_ptr<float>();
+    d.wf[i] = reinterpret_cast<uint16_t*>(wf.data_ptr());
+    d.wt[i] = reinterpret_cast<uint16_t*>(wt.data_ptr());
+    d.N[i] = (int)N;
+    d.K[i] = (int)K;
+    d.mask[i] = (int)masks[i];
+    d.start[i] = tiles;
+    tiles += (int)((N / 64) * (K / 64));
+    out.push_back({wf, wt});
+  }
+  d.start[d.n] = tiles;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(Ws[0].device());
+  hx_split_weight_many(d, (int)npieces, cur_stream(Ws[0]));
+  return out;
+}
+
 // a: [M, npc * K] pieces (piece p at column p * K), b: [N, npc * K]; out [M, N] fp32 (+= if beta)
 bool gemm_split_ok(const Tensor& a, const Tensor& b, int64_t npc) {
   if (!a.is_cuda() || a.scalar_type() != torch::kBFloat16 || b.scalar_type() != torch::kBFloat16) return false;
@@ -980,6 +1015,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("split_planes_t", &split_planes_t);
   m.def("split_weight", &split_weight, py::arg("W"), py::arg("npieces"), py::arg("b16") = 0);
   m.def("gemm_split_weight_b16", &hx_gemm_split_weight_b16);
+  m.def("split_weight_many", &split_weight_many);
   m.def("gemm_split_k", &gemm_split_k, py::arg("a"), py::arg("b"), py::arg("passes"), py::arg("ks") = 0,
         py::arg("lay") = 0);
   m.def("gemm_split_ks", &hx_gemm_split_ks);

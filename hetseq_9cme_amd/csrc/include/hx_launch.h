@@ -107,6 +107,18 @@ void hx_bias_act_planes(int act, const float* y, const float* b, const float* do
 // split.hip -- weight pieces in both GEMM layouts: wf [N][npieces][K], wt [K][npieces][N];
 // W fp32 [N][K] contiguous, N and K multiples of 64.
 // b16 bit 0 / bit 1: wf / wt in the B16 layout [rows][C / 16][3][16] (bf16x6 piece GEMM operand B)
+// a batch of weights split in one launch (split.hip split_weight_many_k); start[i] = first 64 x 64
+// tile of weight i, start[n] = total tiles; mask = hx_split_weight's b16 per weight
+#define HX_WBATCH 64
+struct HxWeightBatch {
+  int n;
+  const float* W[HX_WBATCH];
+  uint16_t* wf[HX_WBATCH];
+  uint16_t* wt[HX_WBATCH];
+  int N[HX_WBATCH], K[HX_WBATCH], mask[HX_WBATCH];
+  int start[HX_WBATCH + 1];
+};
+void hx_split_weight_many(const HxWeightBatch& d, int npieces, hipStream_t s);
 void hx_split_weight(const float* W, int N, int K, int npieces, uint16_t* wf, uint16_t* wt, hipStream_t s,
                      int b16 = 0);
 

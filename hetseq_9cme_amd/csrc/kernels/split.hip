@@ -153,10 +153,9 @@ __device__ __forceinline__ int64_t pc_off(int64_t row, int p, int c, int C) {
 }
 
 template <int NPC, bool BF, bool BT>
-__global__ __launch_bounds__(256) void split_weight_k(const float* __restrict__ W, int N, int K,
-                                                     uint16_t* __restrict__ wf, uint16_t* __restrict__ wt) {
-  __shared__ uint16_t tile[NPC][64][66];
-  const int k0 = blockIdx.x * 64, n0 = blockIdx.y * 64;
+__device__ __forceinline__ void split_weight_tile(const float* __restrict__ W, int N, int K, uint16_t* __restrict__ wf,
+                                                  uint16_t* __restrict__ wt, int k0, int n0,
+                                                  uint16_t (&tile)[NPC][64][66]) {
   const int t = threadIdx.x, c4 = (t & 15) * 4;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -188,6 +187,35 @@ __global__ __launch_bounds__(256) void split_weight_k(const float* __restrict__ 
       uint2 packed = make_uint2(q[0] | ((uint32_t)q[1] << 16), q[2] | ((uint32_t)q[3] << 16));
       *reinterpret_cast<uint2*>(wt + pc_off<NPC, BT>(k0 + kk, p, n0 + c4, N)) = packed;
     }
+  }
+}
+
+template <int NPC, bool BF, bool BT>
+__global__ __launch_bounds__(256) void split_weight_k(const float* __restrict__ W, int N, int K,
+                                                     uint16_t* __restrict__ wf, uint16_t* __restrict__ wt) {
+  __shared__ uint16_t tile[NPC][64][66];
+  split_weight_tile<NPC, BF, BT>(W, N, K, wf, wt, blockIdx.x * 64, blockIdx.y * 64, tile);
+}
+
+// Every weight of a forward in ONE launch (HxWeightBatch: up to HX_WBATCH weights, their 64 x 64
+// tiles numbered consecutively): the per-weight launches are latency-bound at BERT-base sizes
+// (768 x 768: 144 workgroups, fewer than the CUs; ~10 us each for ~2 us of traffic).
+template <int NPC>
+__global__ __launch_bounds__(256) void split_weight_many_k(HxWeightBatch d) {
+  __shared__ uint16_t tile[NPC][64][66];
+  const int b = blockIdx.x;
+  int i = 0;
+  while (i + 1 < d.n && b >= d.start[i + 1]) ++i;   // uniform per workgroup
+  const int tk = d.K[i] / 64, loc = b - d.start[i];
+  const int k0 = (loc % tk) * 64, n0 = (loc / tk) * 64;
+  const int m = d.mask[i];
+  if constexpr (NPC == 3) {
+    if (m == 3) split_weight_tile<3, true, true>(d.W[i], d.N[i], d.K[i], d.wf[i], d.wt[i], k0, n0, tile);
+    else if (m == 1) split_weight_tile<3, true, false>(d.W[i], d.N[i], d.K[i], d.wf[i], d.wt[i], k0, n0, tile);
+    else if (m == 2) split_weight_tile<3, false, true>(d.W[i], d.N[i], d.K[i], d.wf[i], d.wt[i], k0, n0, tile);
+    else split_weight_tile<3, false, false>(d.W[i], d.N[i], d.K[i], d.wf[i], d.wt[i], k0, n0, tile);
+  } else {
+    split_weight_tile<2, false, false>(d.W[i], d.N[i], d.K[i], d.wf[i], d.wt[i], k0, n0, tile);
   }
 }
 
@@ -281,6 +309,12 @@ void hx_split_planes(const float* x, int64_t ldx, uint16_t* out, int64_t R, int 
     split_planes_any_k<3><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, Rp, Dp, npl, order, stacked);
   else
     split_planes_any_k<2><<<blocks, 256, 0, s>>>(x, ldx, out, R, D, Rp, Dp, npl, order, stacked);
+}
+
+void hx_split_weight_many(const HxWeightBatch& d, int npieces, hipStream_t s) {
+  if (d.n < 1 || d.start[d.n] < 1) return;
+  if (npieces == 3) split_weight_many_k<3><<<d.start[d.n], 256, 0, s>>>(d);
+  else split_weight_many_k<2><<<d.start[d.n], 256, 0, s>>>(d);
 }
 
 void hx_split_weight(const float* W, int N, int K, int npieces, uint16_t* wf, uint16_t* wt, hipStream_t s, int b16) {

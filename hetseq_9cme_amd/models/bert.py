@@ -302,6 +302,23 @@ class BertEncoder(nn.Module):
 
     def forward(self, hidden_states, attention_mask_bias, output_all_encoded_layers=True,
                 checkpoint_activations=False):
+        with ops.weight_pieces_scope(self._piece_weights(), hidden_states):
+            return self._forward(hidden_states, attention_mask_bias, output_all_encoded_layers,
+                                 checkpoint_activations)
+
+    def _piece_weights(self):
+        """The encoder's linear weights in the order the layers split them (the fused QKV view,
+        attention output, FFN up / down): split in one launch per forward when the piece GEMMs
+        run (ops.weight_pieces_scope)."""
+        ws = []
+        for layer in self.layer:
+            sa = layer.attention.self
+            ws += [ops.qkv_weight_view(sa.query.weight, sa.key.weight, sa.value.weight),
+                   layer.attention.output.dense.weight, layer.intermediate.dense_act.weight,
+                   layer.output.dense.weight]
+        return ws
+
+    def _forward(self, hidden_states, attention_mask_bias, output_all_encoded_layers, checkpoint_activations):
         all_encoder_layers = []
         if checkpoint_activations:
             from torch.utils.checkpoint import checkpoint

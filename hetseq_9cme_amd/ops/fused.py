@@ -615,18 +615,36 @@ class _FFNSplitFn(torch.autograd.Function):
             dys = dys if dys is not None else split_gemm.pieces(dy2.float())
             # GELU backward in the FFN-down data-gradient epilogue: the pieces of
             # dh * gelu'(u) and the FFN-up bias gradient (y1 = gelu'(u), saved by the forward)
+            slot2, slot1 = grad_slot(W2), grad_slot(W1)
+            # --overlap-wgrad: each weight gradient on the side stream, concurrent with the next
+            # data-gradient GEMM of the compute stream, so one kernel's epilogue store bursts
+            # (all CUs at once, nothing else to run) meet the other's MFMA work
+            side = side_begin(dy2.device) if slot2 is not None and slot1 is not None else None
+            if side is not None:
+                with torch.cuda.stream(side):
+                    dW2 = split_gemm.wgrad_pieces(dys, hs, W2.shape[0], W2.shape[1], slot2)
+                dys.record_stream(side)
+                hs.record_stream(side)
             dy1s, db1 = split_gemm.gemm_dgelu(dys, w2, y1, None, grad_slot(b1), deriv=True)
+            if side is not None:
+                side = side_begin(dy2.device)   # after the dGELU pieces
+                with torch.cuda.stream(side):
+                    dW1 = split_gemm.wgrad_pieces(dy1s, xs, W1.shape[0], W1.shape[1], slot1)
+                dy1s.record_stream(side)
+                xs.record_stream(side)
+                dx = _dgrad_pieces(dy1s, w1, ctx.xshape, ctx.mbox)
+                return dx, dW1, db1, dW2, None, None
             # both weight gradients in one launch when they qualify (wgrad_split_group)
-            grp = split_gemm.wgrad_pieces_group([(dys, hs, W2.shape[0], W2.shape[1], grad_slot(W2)),
-                                                 (dy1s, xs, W1.shape[0], W1.shape[1], grad_slot(W1))]) \
+            grp = split_gemm.wgrad_pieces_group([(dys, hs, W2.shape[0], W2.shape[1], slot2),
+                                                 (dy1s, xs, W1.shape[0], W1.shape[1], slot1)]) \
                 if _GROUP_FFN else None
             if grp is not None:
                 dW2, dW1 = grp
             else:
-                dW2 = split_gemm.wgrad_pieces(dys, hs, W2.shape[0], W2.shape[1], grad_slot(W2))
+                dW2 = split_gemm.wgrad_pieces(dys, hs, W2.shape[0], W2.shape[1], slot2)
             dx = _dgrad_pieces(dy1s, w1, ctx.xshape, ctx.mbox)
             if grp is None:
-                dW1 = split_gemm.wgrad_pieces(dy1s, xs, W1.shape[0], W1.shape[1], grad_slot(W1))
+                dW1 = split_gemm.wgrad_pieces(dy1s, xs, W1.shape[0], W1.shape[1], slot1)
             return dx, dW1, db1, dW2, None, None
         dys = _dy_planes(ctx.gp, dy2)
         dh = split_gemm.dgrad(dys, W2)
@@ -679,6 +697,25 @@ def _adjacent_view(ts):
     shape = (rows,) + tuple(t0.shape[1:])
     stride = t0.stride() if t0.dim() > 1 else (1,)
     return t0.detach().as_strided(shape, stride)
+
+
+def qkv_weight_view(wq, wk, wv):
+    """The [3H, H] view of adjacent Q / K / V weights that linear3 multiplies by (None if the
+    three are not laid out back to back)."""
+    return _adjacent_view([wq, wk, wv])
+
+
+def weight_pieces_scope(Ws, x):
+    """``split_gemm.weight_pieces_scope`` over ``Ws`` when the piece GEMMs will run for the
+    activations ``x`` [.., H] (``split_gemm.producer_pieces``), else a no-op context.
+    ``HX_WSPLIT_BATCH=0`` turns the batch split off."""
+    import contextlib
+    if os.environ.get('HX_WSPLIT_BATCH', '1') == '0' or not torch.is_tensor(x) or x.dtype != torch.float32:
+        return contextlib.nullcontext()
+    rows = x.numel() // max(1, x.shape[-1])
+    if not split_gemm.producer_pieces(rows, x.shape[-1], x):
+        return contextlib.nullcontext()
+    return split_gemm.weight_pieces_scope(Ws)
 
 
 class _Linear3Fn(torch.autograd.Function):
@@ -747,7 +784,7 @@ class _Linear3Fn(torch.autograd.Function):
             n_out = sum(ctx.n)
             dys = ctx.gp.take() if ctx.gp is not None else None   # the attention backward's pieces
             dys = dys if dys is not None else split_gemm.pieces(dy2.float())
-            dx = _dgrad_pieces(dys, W, ctx.xshape, ctx.mbox)     # W holds the W^T pieces here
+            dx = None   # after the side-stream weight gradients are queued (they overlap it)
             n_in = W.shape[0]
             wg = lambda slot: split_gemm.wgrad_pieces(dys, x2, n_out, n_in, slot)
         else:
@@ -812,6 +849,8 @@ class _Linear3Fn(torch.autograd.Function):
             x2.record_stream(side)
             if dys is not None:
                 dys.record_stream(side)
+        if ctx.pieces:
+            dx = _dgrad_pieces(dys, W, ctx.xshape, ctx.mbox)     # W holds the W^T pieces here
         if not has_b:
             return (dx, gW[0], gW[1], gW[2], None, None, None, None, None, gjoin, None)
         gb = bs if fb is not None else [db[:a], db[a:a + b_], db[a + b_:]]

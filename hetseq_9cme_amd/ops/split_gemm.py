@@ -72,6 +72,7 @@ class _State(object):
     passes = 0
     piece_gemm = {'1': True, '0': False}.get(os.environ.get('HETSEQ_PIECE_GEMM', ''))   # see nt_ok
     addmm_out_ok = None   # does torch.addmm(bf16, bf16, out_dtype=fp32, out=acc) work in place?
+    wp = None   # {(data_ptr, shape): (wf, wt)} of the running forward's batch split (weight_pieces_scope)
 
 
 def set_fp32_gemm(mode):
@@ -262,13 +263,44 @@ def b16(n):
     return v
 
 
+def _wmask(W):
+    N, K = W.shape
+    return (1 if b16(N) else 0) | (2 if b16(K) else 0)
+
+
 def weight_pieces(W):
     """(wf [N, npc * K], wt [K, npc * N]): pieces of W [N, K] and of W^T, one pass; each in the
     layout its GEMM reads (``b16``: wf is the B operand of the N-column forward, wt of the
-    K-column data gradient)."""
-    N, K = W.shape
-    mask = (1 if b16(N) else 0) | (2 if b16(K) else 0)
-    return C().split_weight(W.contiguous(), npieces(), mask)
+    K-column data gradient).  Inside ``weight_pieces_scope`` the batch split of the running
+    forward is returned."""
+    if _State.wp is not None:
+        e = _State.wp.get((W.data_ptr(), tuple(W.shape)))
+        if e is not None:
+            return e
+    return C().split_weight(W.contiguous(), npieces(), _wmask(W))
+
+
+class weight_pieces_scope(object):
+    """Split every weight in ``Ws`` in ONE launch (split.hip ``split_weight_many_k``) on entry;
+    ``weight_pieces`` returns those pieces until exit.  Scoped to one forward: weights change
+    between forwards (optimizer step) and a recompute under activation checkpointing runs
+    outside the scope, so it splits again.  No-op for an empty list or outside bf16x3/x6."""
+
+    def __init__(self, Ws):
+        self.Ws = [W for W in Ws if W is not None]
+
+    def __enter__(self):
+        self.prev = _State.wp
+        if self.Ws and _State.passes > 0 and len(self.Ws) <= 64 and \
+                all(W.dim() == 2 and W.shape[0] % 64 == 0 and W.shape[1] % 64 == 0 and W.is_contiguous()
+                    for W in self.Ws):
+            outs = C().split_weight_many(self.Ws, npieces(), [_wmask(W) for W in self.Ws])
+            _State.wp = {(W.data_ptr(), tuple(W.shape)): tuple(o) for W, o in zip(self.Ws, outs)}
+        return self
+
+    def __exit__(self, *exc):
+        _State.wp = self.prev
+        return False
 
 
 def gemm(a, b, out=None, beta=False):

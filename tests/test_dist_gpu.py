@@ -155,7 +155,8 @@ def test_rccl_one_rank_reducer_matches_local(dev, tmp_path):
         port = s.getsockname()[1]
     rccl = ['--distributed-world-size', '1', '--distributed-gpus', '1', '--distributed-backend', 'nccl', '--distributed-rank', '0',
             '--distributed-init-method', 'tcp://127.0.0.1:{}'.format(port), '--force-reducer']
-    runs = {'local': ['--distributed-world-size', '1'], 'rccl': rccl, 'rccl_side': rccl + ['--overlap-wgrad'],
+    runs = {'local': ['--distributed-world-size', '1', '--no-overlap-wgrad'], 'rccl': rccl + ['--no-overlap-wgrad'],
+            'rccl_side': rccl + ['--overlap-wgrad'],
             'local_side': ['--distributed-world-size', '1', '--overlap-wgrad']}
     ck = {}
     for name, extra in runs.items():

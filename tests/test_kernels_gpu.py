@@ -381,7 +381,7 @@ def test_training_gpu_matches_cpu(dev, tmp_path):
                                                                attention_probs_dropout_prob=0.0))
     vocab = write_vocab(str(tmp_path / 'v.txt'), 1024)
     outs = {}
-    for name, extra in (('gpu', []), ('gpu_side', ['--overlap-wgrad']), ('cpu', ['--cpu'])):
+    for name, extra in (('gpu', ['--no-overlap-wgrad']), ('gpu_side', ['--overlap-wgrad']), ('cpu', ['--cpu'])):
         save = str(tmp_path / name)
         cmd = [sys.executable, '-m', 'hetseq_9cme_amd.train', '--task', 'bert', '--data', str(d), '--dict', vocab,
                '--config_file', cfg, '--max-sentences', '8', '--fast-stat-sync', '--max-update', '3',

@@ -826,3 +826,59 @@ def test_decoder_pieces_path_matches_fp64(dev, monkeypatch):
         assert err < 2e-6, (name, err)
         err_old = (o.double() - r).abs().max().item() / scale
         assert err_old < 1e-5, (name, 'planes path', err_old)
+
+
+@pytest.mark.parametrize('npc', [3, 2])
+def test_split_weight_many_matches_single(dev, npc):
+    """The one-launch batch weight split (split_weight_many: every weight of a forward, 64 x 64
+    tiles numbered across the batch) writes the same pieces, in the same layouts, as one
+    split_weight launch per weight."""
+    from hetseq_9cme_amd.ops._ext import C
+    g = torch.Generator(device='cpu').manual_seed(12)
+    shapes = [(2304, 768), (768, 768), (3072, 768), (768, 3072), (192, 128)]
+    Ws = [torch.randn(n, k, generator=g).to(dev) for n, k in shapes]
+    masks = [3, 1, 2, 0, 1] if npc == 3 else [0] * len(shapes)
+    outs = C().split_weight_many(Ws, npc, masks)
+    for W, m, (wf, wt) in zip(Ws, masks, outs):
+        rf, rt = C().split_weight(W, npc, m)
+        assert torch.equal(wf, rf) and torch.equal(wt, rt)
+
+
+def test_bert_batch_weight_split_matches_per_call(dev, monkeypatch):
+    """BERT on the piece GEMMs with the encoder's weights split in one launch per forward
+    (ops.weight_pieces_scope) gives the same loss and gradients as the per-linear splits."""
+    from hetseq_9cme_amd import ops
+    from hetseq_9cme_amd.ops import split_gemm
+    from hetseq_9cme_amd.models.bert import BertConfig, BertForPreTraining
+    from hetseq_9cme_amd.parallel.flat_params import FlatParamSpace
+    monkeypatch.setitem(split_gemm.MIN_ROWS, 6, 0)
+    cfg = BertConfig(1024, hidden_size=256, num_hidden_layers=2, num_attention_heads=4, intermediate_size=1024,
+                     max_position_embeddings=128, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    res = []
+    for batch in ('1', '0'):
+        monkeypatch.setenv('HX_WSPLIT_BATCH', batch)
+        torch.manual_seed(0)
+        model = BertForPreTraining(cfg).to(dev)
+        model.max_predictions_per_seq = 4
+        flat = FlatParamSpace(model, dev, contiguous_groups=model.flat_contiguous_groups())
+        g = torch.Generator(device='cpu').manual_seed(3)
+        ids = torch.randint(5, 1024, (16, 128), generator=g).to(dev)
+        labels = torch.full_like(ids, -1)
+        labels[:, 7] = ids[:, 7]
+        nsp = torch.randint(0, 2, (16,), generator=g).to(dev)
+        try:
+            ops.set_fp32_gemm('bf16x6')
+            ops.set_step_seed(1)
+            model.train()
+            flat.zero_grad()
+            loss = model(ids, torch.zeros_like(ids), torch.ones_like(ids), labels, nsp)
+            loss.backward()
+            flat.adopt_all()
+        finally:
+            ops.set_fp32_gemm('native')
+        assert split_gemm._State.wp is None   # scope closed
+        res.append((loss.detach().clone(),
+                    {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}))
+    assert torch.equal(res[0][0], res[1][0])
+    for n in res[0][1]:
+        torch.testing.assert_close(res[0][1][n], res[1][1][n], rtol=1e-4, atol=1e-6, msg=n)

@@ -9,7 +9,7 @@ from hetseq_9cme_amd import options  # noqa: E402
 
 NEW = {'--async-save', '--check-params-every', '--distributed-timeout', '--ent_name_id_file', '--fused-kernels',
        '--gemm-tuning', '--gemm-tuning-file', '--precision', '--profile-phases', '--user-module',
-       '--overlap-wgrad', '--debug-kernels', '--allreduce-impl', '--xgmi-blocks', '--device-offset',
+       '--overlap-wgrad', '--no-overlap-wgrad', '--debug-kernels', '--allreduce-impl', '--xgmi-blocks', '--device-offset',
        '--bucket-peer-mb', '--comm-cus', '--force-reducer', '--fp32-gemm', '--graph-train-step',
        '--pad-to-multiple-of', '--rccl-normal-priority'}
 
@@ -32,8 +32,10 @@ def fmt_flag(a):
 
 
 def fmt_default(a):
-    if isinstance(a, (argparse._StoreTrueAction,)):
-        return 'off'
+    if isinstance(a, argparse._StoreTrueAction):
+        return 'on' if a.default else 'off'
+    if isinstance(a, argparse._StoreFalseAction):
+        return 'off' if a.default else 'on'
     return '`{}`'.format(a.default) if a.default is not None else '—'
 
 

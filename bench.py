@@ -59,10 +59,10 @@ def parse():
                     help='rehearsal on a 1-GPU box: every rank uses GPU 0 (numbers are not per-GPU)')
     ap.add_argument('--gemm-tuning', default='table', choices=['off', 'table', 'online', 'retune'])
     ap.add_argument('--gemm-tuning-file', default=None)
-    ap.add_argument('--overlap-wgrad', dest='overlap_wgrad', action='store_true', default=True,
-                    help='weight-gradient GEMMs on a side HIP stream, concurrent with the data-gradient '
-                         'GEMMs (default on)')
-    ap.add_argument('--no-overlap-wgrad', dest='overlap_wgrad', action='store_false')
+    ap.add_argument('--overlap-wgrad', dest='overlap_wgrad', action='store_const', const='on', default='auto',
+                    help='weight-gradient GEMMs on a side HIP stream on every backward path (default: the '
+                         'piece-GEMM paths only)')
+    ap.add_argument('--no-overlap-wgrad', dest='overlap_wgrad', action='store_const', const='off')
     ap.add_argument('--profile-phases', action='store_true',
                     help='extra untimed steps reporting host time per step phase (stderr)')
     ap.add_argument('--sync-debug', action='store_true',
@@ -173,7 +173,8 @@ def run(a, rank, world, dev_index, init_method):
             '--allreduce-impl', a.allreduce_impl, '--bucket-cap-mb', str(a.bucket_cap_mb)]
     if a.profile_phases:
         argv += ['--profile-phases']
-    argv += ['--overlap-wgrad' if a.overlap_wgrad else '--no-overlap-wgrad']
+    if a.overlap_wgrad != 'auto':
+        argv += ['--overlap-wgrad' if a.overlap_wgrad == 'on' else '--no-overlap-wgrad']
     if a.gemm_tuning_file:
         argv += ['--gemm-tuning-file', a.gemm_tuning_file]
     args = options.parse_training_args(argv)

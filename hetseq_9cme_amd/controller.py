@@ -55,7 +55,9 @@ class Controller(object):
         if not getattr(args, 'fused_kernels', True):
             ops.set_fused(False)      # A/B mode: plain torch ops on the GPU
         ops.set_fp32_gemm(getattr(args, 'fp32_gemm', 'native'))
-        ops.set_side_stream(getattr(args, 'overlap_wgrad', False) or os.environ.get('HETSEQ_SIDE_STREAM') == '1')
+        ow = getattr(args, 'overlap_wgrad', 'auto')
+        ops.set_side_stream('on' if os.environ.get('HETSEQ_SIDE_STREAM') == '1' else
+                            {True: 'on', False: 'auto', None: 'auto'}.get(ow, ow))
         if getattr(args, 'debug_kernels', False) and self.cuda:
             ops.C().set_debug(True)   # validation inside the bindings (see csrc/bindings.cpp)
         if self.cuda:

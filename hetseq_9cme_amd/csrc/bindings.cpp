@@ -833,17 +833,6 @@ Tensor gemm_split_stamps(Tensor a, Tensor b, int64_t lay) {
   return st;
 }
 
-// timing experiment: cfg 0 with every 32x32x16 MFMA replaced by two 16x16x32 (wrong results)
-Tensor gemm_split_mfma16_timing(Tensor a, Tensor b) {
-  TORCH_CHECK(gemm_split_ok(a, b, 3), "unsupported operands");
-  Tensor out = torch::empty({a.size(0), b.size(0)}, a.options().dtype(torch::kFloat32));
-  HxGemmEpi e{7, nullptr, nullptr, 0, nullptr, 0, 0, nullptr};
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
-  const int64_t K = a.size(1) / 3;
-  TORCH_CHECK(hx_gemm_split_nt(a.data_ptr(), 3 * K, K, b.data_ptr(), 3 * K, K, out.data_ptr<float>(), b.size(0),
-                               (int)a.size(0), (int)b.size(0), (int)K, 6, 0, &e, 0, cur_stream(a)) == 0, "launch");
-  return out;
-}
 void dma_probe(Tensor src, int64_t seg, int64_t ld, int64_t iters, int64_t grid) {
   TORCH_CHECK(src.is_cuda() && src.nbytes() < (1LL << 32) && src.nbytes() > (1 << 20), "dma_probe: src");
   TORCH_CHECK(seg == 1024 || seg == 128 || seg == 64 || seg == 32, "dma_probe: seg");
@@ -1027,7 +1016,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias"), py::arg("dbias_out"), py::arg("lay") = 0, py::arg("dmode") = 0);
   m.def("gemm_split_stamps", &gemm_split_stamps);
   m.def("dma_probe", &dma_probe);
-  m.def("gemm_split_mfma16_timing", &gemm_split_mfma16_timing);
   m.def("gemm_split_ok", &gemm_split_ok);
   m.def("bias_act_planes", &bias_act_planes);
   m.def("wgrad_split", &wgrad_split);

@@ -344,20 +344,8 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_piece_k(
       for (int a = 0; a < MB; ++a)
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
-          if constexpr (EPI == 7) {
-            // TIMING EXPERIMENT ONLY (wrong results): two 16x16x32 MFMAs in place of one
-            // 32x32x16 -- same pipe cycles, different DVFS behaviour
-            typedef float f32x4e __attribute__((ext_vector_type(4)));
-            f32x4e lo = {acc[a][b][0], acc[a][b][1], acc[a][b][2], acc[a][b][3]};
-            f32x4e hi = {acc[a][b][4], acc[a][b][5], acc[a][b][6], acc[a][b][7]};
-            lo = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[PairsNT<NP>::a[q]][a], fb[PairsNT<NP>::b[q]][b], lo, 0, 0, 0);
-            hi = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[PairsNT<NP>::b[q]][b], fa[PairsNT<NP>::a[q]][a], hi, 0, 0, 0);
-            acc[a][b][0] = lo[0]; acc[a][b][1] = lo[1]; acc[a][b][2] = lo[2]; acc[a][b][3] = lo[3];
-            acc[a][b][4] = hi[0]; acc[a][b][5] = hi[1]; acc[a][b][6] = hi[2]; acc[a][b][7] = hi[3];
-          } else {
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[PairsNT<NP>::a[q]][a], fb[PairsNT<NP>::b[q]][b],
-                                                                acc[a][b], 0, 0, 0);
-          }
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[PairsNT<NP>::a[q]][a], fb[PairsNT<NP>::b[q]][b],
+                                                              acc[a][b], 0, 0, 0);
         }
       if (dit >= 0) {
         // pieces j = q (and the leftovers after the last pass)
@@ -637,7 +625,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_piece_k(
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[a][b][4 * gq + i] = v[i];
   };
-  if constexpr (EPI == 0 || EPI == 3 || EPI == 7) {
+  if constexpr (EPI == 0 || EPI == 3) {
     // EPI 3 = EPI 0 with beta: one row block of accumulators at a time (a sched barrier keeps
     // the compiler from hoisting every block's C loads: 256-VGPR cap); row block a + 1's C
     // loads are issued before row block a is summed, so one load latency per tile is exposed
@@ -848,7 +836,8 @@ void launch_one(const Args& a, hipStream_t s) {
 // staggered by one pass (MI355X_MICROARCH.md 'Two waves per SIMD' item 9) 2-3 % slower on every
 // BERT shape (profiles/r3_gemm_stagger_probe.log); the same pipeline on 16x16x32 MFMAs (two
 // 16-deep pieces side by side along k, three MFMAs per 16x16 block and stage) 1-6 % slower --
-// the clock gain of the 16x16 shape (r3_mfma16_clock_probe.log) does not survive its 26 instead
+// the clock gain of the 16x16 shape (r3_mfma16_clock_probe.log: a timing-only swap of the same
+// fragments, since removed) does not survive its 26 instead
 // of 15 fragment reads per k step (profiles/r3_gemm_mfma16_probe.log).  Ping-pong (the two waves
 // of each SIMD half a k step apart: one multiplies while the other reads its fragments, two
 // barrier-delimited phases per k step, MI355X_MICROARCH.md 'Two waves per SIMD') was correct
@@ -1021,11 +1010,10 @@ int hx_gemm_split_nt(const void* A, int64_t lda, int64_t a_ps, const void* B, in
   a.stamps = nullptr;
   if (kind == 1 && (!a.P || beta)) return -1;
   if (kind == 2 && (!a.P || !a.aux)) return -1;
-  if ((kind < 0 || kind > 2) && kind != 7) return -1;
+  if (kind < 0 || kind > 2) return -1;
 #define HX_GS(NPC_, NP_)                                          \
   do {                                                            \
-    if (kind == 7) launch_one<256, 192, 64, 96, 3, 6, 16, 3, 7, 3, 0>(a, s); \
-    else if (kind == 0 && !beta) launch_cfg<NPC_, NP_, 0>(cfg, lay, a, s);  \
+    if (kind == 0 && !beta) launch_cfg<NPC_, NP_, 0>(cfg, lay, a, s);  \
     else if (kind == 0) launch_cfg<NPC_, NP_, 3>(cfg, lay, a, s);      \
     else if (kind == 1) launch_cfg<NPC_, NP_, 1>(cfg, lay, a, s);      \
     else launch_cfg<NPC_, NP_, 2>(cfg, lay, a, s);                     \

@@ -176,26 +176,30 @@ def _dgrad_split(dys, W, xshape, mbox, prefix=False):
 
 # ----------------------------------------------------------------- weight-grad side stream
 class _Side(object):
-    # opt-in: measured 71.7 vs 69.5 ms/step on BERT-base fp32 (1x MI355X) -- the
-    # co-scheduled kernels cost the full-GPU GEMM tiles more than the overlap wins
-    enabled = os.environ.get('HETSEQ_SIDE_STREAM', '0') == '1'
+    # 'auto' (default): the piece-GEMM backward paths only -- BERT-base phase 1 53.9 -> 52.9 ms/step
+    # (profiles/r3_overlap_wgrad_ab.md); the library paths (small batches, NER: 11.9 -> 15.5 ms per
+    # update, host-bound; round 1: 69.5 -> 71.7 ms/step) stay on the compute stream.
+    # 'on': every path; 'off': none.
+    mode = 'on' if os.environ.get('HETSEQ_SIDE_STREAM', '') == '1' else 'auto'
     streams = {}          # device index -> torch.cuda.Stream
     active = set()        # device indices with side work queued in the current backward
 
 
 def set_side_stream(flag):
-    """Enable / disable overlapping weight-gradient work on a side stream."""
-    _Side.enabled = bool(flag)
+    """Weight-gradient work on a side stream: True / 'on', False / 'off', or 'auto'
+    (the piece-GEMM paths only)."""
+    _Side.mode = {True: 'on', False: 'off'}.get(flag, flag) if isinstance(flag, bool) else str(flag)
+    assert _Side.mode in ('on', 'off', 'auto'), flag
 
 
-def side_begin(device):
+def side_begin(device, pieces=False):
     """Side stream for off-critical-path weight-gradient work (dW GEMMs, bias
     column sums) of the running backward, ordered after everything already
     queued on the compute stream.  While the compute stream continues with the
     dgrad chain (attention / LayerNorm / GELU backward: mostly memory-bound),
     the side stream's GEMMs fill the matrix cores.  Joined back into the compute
     stream by an end-of-backward callback (``side_join``)."""
-    if not _Side.enabled or device.type != 'cuda':
+    if _Side.mode == 'off' or (_Side.mode == 'auto' and not pieces) or device.type != 'cuda':
         return None
     idx = device.index if device.index is not None else torch.cuda.current_device()
     st = _Side.streams.get(idx)
@@ -472,7 +476,7 @@ class _LinearFn(torch.autograd.Function):
     def forward(ctx, x, W, b, mbox, gp, defer=None):
         x2 = x.reshape(-1, x.shape[-1])
         ctx.split = split_gemm.active(x2)
-        ctx.pieces = ctx.split and split_gemm.nt_ok(W.shape[1], W.shape[0])
+        ctx.pieces = ctx.split and split_gemm.nt_ok(W.shape[1], W.shape[0], x2.shape[0])
         ctx.gp = gp if (ctx.split and b is None) else None
         # weight gradient deferred to the joining linear's backward (WgradDefer)
         ctx.defer = defer if (defer is not None and defer.armed and ctx.pieces and b is None) else None
@@ -524,7 +528,7 @@ class _LinearFn(torch.autograd.Function):
             return dx, None, None, None, None, None
         slot = grad_slot(W)
         direct = slot is not None
-        side = side_begin(dy2.device) if direct else None
+        side = side_begin(dy2.device, ctx.pieces) if direct else None
         with torch.cuda.stream(side) if side is not None else _nullctx():
             if ctx.pieces:
                 dW = split_gemm.wgrad_pieces(dys, x2, W.shape[0], W.shape[1], slot)
@@ -571,7 +575,8 @@ class _FFNSplitFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W1, b1, W2, mbox, gp):
         x2 = x.reshape(-1, x.shape[-1])
-        ctx.pieces = split_gemm.nt_ok(W1.shape[1], W1.shape[0]) and split_gemm.nt_ok(W2.shape[1], W2.shape[0])
+        rows = x.numel() // x.shape[-1]
+        ctx.pieces = split_gemm.nt_ok(W1.shape[1], W1.shape[0], rows) and split_gemm.nt_ok(W2.shape[1], W2.shape[0], rows)
         ctx.gp = gp
         if ctx.gp is not None:
             ctx.gp.want = True
@@ -619,7 +624,7 @@ class _FFNSplitFn(torch.autograd.Function):
             # --overlap-wgrad: each weight gradient on the side stream, concurrent with the next
             # data-gradient GEMM of the compute stream, so one kernel's epilogue store bursts
             # (all CUs at once, nothing else to run) meet the other's MFMA work
-            side = side_begin(dy2.device) if slot2 is not None and slot1 is not None else None
+            side = side_begin(dy2.device, True) if slot2 is not None and slot1 is not None else None
             if side is not None:
                 with torch.cuda.stream(side):
                     dW2 = split_gemm.wgrad_pieces(dys, hs, W2.shape[0], W2.shape[1], slot2)
@@ -627,7 +632,7 @@ class _FFNSplitFn(torch.autograd.Function):
                 hs.record_stream(side)
             dy1s, db1 = split_gemm.gemm_dgelu(dys, w2, y1, None, grad_slot(b1), deriv=True)
             if side is not None:
-                side = side_begin(dy2.device)   # after the dGELU pieces
+                side = side_begin(dy2.device, True)   # after the dGELU pieces
                 with torch.cuda.stream(side):
                     dW1 = split_gemm.wgrad_pieces(dy1s, xs, W1.shape[0], W1.shape[1], slot1)
                 dy1s.record_stream(side)
@@ -740,7 +745,7 @@ class _Linear3Fn(torch.autograd.Function):
             bc = cast_w(b, x.dtype) if has_b else None
         x2 = x.reshape(-1, x.shape[-1])
         ctx.split = split_gemm.active(x2)
-        ctx.pieces = ctx.split and split_gemm.nt_ok(W.shape[1], W.shape[0])
+        ctx.pieces = ctx.split and split_gemm.nt_ok(W.shape[1], W.shape[0], x2.shape[0])
         ctx.gp = gp if (ctx.split and not has_b) else None
         if ctx.gp is not None:
             ctx.gp.want = True
@@ -807,7 +812,7 @@ class _Linear3Fn(torch.autograd.Function):
         bs = [grad_slot(t) for t in (bq, bk, bv)] if has_b else [None, None, None]
         fb = _adjacent_view(bs) if all(t is not None for t in bs) else None
         direct = fused is not None and (fb is not None or not has_b)
-        side = side_begin(dy2.device) if direct else None
+        side = side_begin(dy2.device, ctx.pieces) if direct else None
         item = ctx.join.item if ctx.join is not None else None
         gjoin = None
         with torch.cuda.stream(side) if side is not None else _nullctx():

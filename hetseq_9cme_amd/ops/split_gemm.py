@@ -206,12 +206,21 @@ def npieces():
     return PIECES[_State.passes]
 
 
-def nt_ok(n_in, n_out):
+# Below this many rows the piece GEMMs' 256-row tiles leave CUs idle (4096 rows x N = 768: 64
+# tiles for 256 CUs) and the library GEMMs on pass-stacked planes win: BERT-base at batch 32
+# (4096 tokens) 24.4 ms/step on the piece GEMMs against 19.7-20.0 on the planes path.
+PIECE_MIN_ROWS = int(os.environ.get('HX_PIECE_MIN_ROWS', '16384'))
+
+
+def nt_ok(n_in, n_out, rows=None):
     """Use the hand-written piece GEMMs for a linear layer W [n_out, n_in] (fwd: N = n_out,
-    K = n_in; dgrad: N = n_in, K = n_out): the default under bf16x6 (csrc/kernels/gemm_split.hip,
-    LDS-DMA pipeline, profiles/r3_*), opt-in for bf16x3 (``HETSEQ_PIECE_GEMM=1``) and off with
-    ``HETSEQ_PIECE_GEMM=0``, where the library GEMMs on pass-stacked planes run instead."""
+    K = n_in; dgrad: N = n_in, K = n_out) over ``rows`` tokens: the default under bf16x6 from
+    ``PIECE_MIN_ROWS`` rows (csrc/kernels/gemm_split.hip, LDS-DMA pipeline, profiles/r3_*),
+    opt-in for bf16x3 (``HETSEQ_PIECE_GEMM=1``) and off with ``HETSEQ_PIECE_GEMM=0``, where the
+    library GEMMs on pass-stacked planes run instead."""
     on = _State.piece_gemm if _State.piece_gemm is not None else _State.passes == 6
+    if rows is not None and rows < PIECE_MIN_ROWS and _State.piece_gemm is None:
+        return False
     return on and n_out % 128 == 0 and n_in % 128 == 0
 
 
@@ -219,7 +228,7 @@ def producer_pieces(rows, H, ref):
     """Number of pieces a producer (LayerNorm / embedding forward) should write next to its fp32
     output [rows, H] on ``ref``'s device for a consuming piece-GEMM linear, or 0: the split path
     is on for this size (``active``'s rule) and the piece GEMMs take the shape (``nt_ok``)."""
-    if not (_State.passes > 0 and use_kernels(ref) and rows >= MIN_ROWS[_State.passes] and nt_ok(H, 128)):
+    if not (_State.passes > 0 and use_kernels(ref) and rows >= MIN_ROWS[_State.passes] and nt_ok(H, 128, rows)):
         return 0
     return npieces()
 

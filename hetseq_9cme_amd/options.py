@@ -79,12 +79,13 @@ def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialD
                              'online benchmarking of unseen shapes, or library defaults')
     parser.add_argument('--gemm-tuning-file', default=None, metavar='PATH',
                         help='where --gemm-tuning online writes its table (device ordinal appended)')
-    parser.add_argument('--overlap-wgrad', dest='overlap_wgrad', action='store_true', default=True,
+    parser.add_argument('--overlap-wgrad', dest='overlap_wgrad', action='store_const', const='on', default='auto',
                         help='run weight-gradient GEMMs / bias column sums on a side HIP stream, concurrent '
-                             'with the data-gradient GEMMs (default on: BERT-base phase 1 on the piece GEMMs '
-                             '53.9 -> 52.9 ms/step, profiles/r3_overlap_wgrad_ab.md)')
-    parser.add_argument('--no-overlap-wgrad', dest='overlap_wgrad', action='store_false',
-                        help='weight gradients on the compute stream')
+                             'with the data-gradient GEMMs, on every backward path (default: the piece-GEMM '
+                             'paths only -- BERT-base phase 1 53.9 -> 52.9 ms/step, while the host-bound '
+                             'library paths lose; profiles/r3_overlap_wgrad_ab.md)')
+    parser.add_argument('--no-overlap-wgrad', dest='overlap_wgrad', action='store_const', const='off',
+                        help='weight gradients on the compute stream on every path')
     parser.add_argument('--debug-kernels', action='store_true',
                         help='debug mode: serialised kernel launches (AMD_SERIALIZE_KERNEL=3, '
                              'HIP_LAUNCH_BLOCKING=1), range checks on token/type ids and labels and finite '

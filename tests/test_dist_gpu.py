@@ -45,6 +45,7 @@ def test_two_rank_gpu_equivalence(dev, tmp_path):
         env = dict(os.environ, PYTHONPATH=ROOT)
         if name.endswith('6'):
             env['HETSEQ_SPLIT_MIN_ROWS_X6'] = '0'
+            env['HX_PIECE_MIN_ROWS'] = '0'
         r = subprocess.run([sys.executable, '-m', 'hetseq_9cme_amd.train'] + common + extra + ['--save-dir', save],
                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, timeout=400)
         assert r.returncode == 0, r.stdout[-3000:]
@@ -161,7 +162,7 @@ def test_rccl_one_rank_reducer_matches_local(dev, tmp_path):
     ck = {}
     for name, extra in runs.items():
         save = str(tmp_path / name)
-        env = dict(os.environ, PYTHONPATH=ROOT, HETSEQ_SPLIT_MIN_ROWS_X6='0')
+        env = dict(os.environ, PYTHONPATH=ROOT, HETSEQ_SPLIT_MIN_ROWS_X6='0', HX_PIECE_MIN_ROWS='0')
         r = subprocess.run([sys.executable, '-m', 'hetseq_9cme_amd.train'] + common + extra + ['--save-dir', save],
                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, timeout=400)
         assert r.returncode == 0, r.stdout[-3000:]

@@ -18,6 +18,7 @@ def _split_small_gemms(monkeypatch):
     """The tests' GEMMs are small: take the split path regardless of the row threshold."""
     from hetseq_9cme_amd.ops import split_gemm
     monkeypatch.setattr(split_gemm, 'MIN_ROWS', {3: 0, 6: 0})
+    monkeypatch.setattr(split_gemm, 'PIECE_MIN_ROWS', 0)
 
 
 def _ref_pieces(x, n):
@@ -190,7 +191,7 @@ def test_training_split_modes_track_native(dev, tmp_path):
                '--clip-norm', '0.5', '--save-dir', save, '--distributed-world-size', '1', '--fp32-gemm', mode]
         r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
                            env=dict(os.environ, PYTHONPATH=root, HETSEQ_SPLIT_MIN_ROWS_X3='0',
-                                    HETSEQ_SPLIT_MIN_ROWS_X6='0'), timeout=300)
+                                    HETSEQ_SPLIT_MIN_ROWS_X6='0', HX_PIECE_MIN_ROWS='0'), timeout=300)
         assert r.returncode == 0, r.stdout[-3000:]
         with torch.serialization.safe_globals([argparse.Namespace]):
             outs[mode] = torch.load(os.path.join(save, 'checkpoint_last.pt'), map_location='cpu', weights_only=True)

@@ -34,6 +34,7 @@ def main():
     ap.add_argument('--profile-phases', action='store_true', help='host/device time per step phase (stderr)')
     ap.add_argument('--gemm-tuning', default='table', choices=['off', 'table'])
     ap.add_argument('--graph-train-step', action='store_true', help='replay captured HIP graphs of the update')
+    ap.add_argument('--no-overlap-wgrad', action='store_true', help='weight gradients on the compute stream')
     ap.add_argument('--cprofile', default=None, metavar='OUT',
                     help='after the timed steps, cProfile 20 more steps and write the top host functions to OUT')
     ap.add_argument('--gpus', type=int, default=1, help='ranks (launched by torch.distributed.run when > 1)')
@@ -73,6 +74,8 @@ def main():
         argv.append('--profile-phases')
     if a.graph_train_step:
         argv.append('--graph-train-step')
+    if a.no_overlap_wgrad:
+        argv.append('--no-overlap-wgrad')
     args = options.parse_training_args(argv + ['--distributed-world-size', str(world)])
     args.device_id = dev
     args.distributed_backend = a.backend

@@ -36,6 +36,8 @@ def fmt_default(a):
         return 'on' if a.default else 'off'
     if isinstance(a, argparse._StoreFalseAction):
         return 'off' if a.default else 'on'
+    if isinstance(a, argparse._StoreConstAction) and a.const is not None:
+        return '`{}`'.format(a.default) if a.default is not None else '—'
     return '`{}`'.format(a.default) if a.default is not None else '—'
 
 

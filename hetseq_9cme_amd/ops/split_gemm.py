@@ -208,8 +208,9 @@ def npieces():
 
 # Below this many rows the piece GEMMs' 256-row tiles leave CUs idle (4096 rows x N = 768: 64
 # tiles for 256 CUs) and the library GEMMs on pass-stacked planes win: BERT-base at batch 32
-# (4096 tokens) 24.4 ms/step on the piece GEMMs against 19.7-20.0 on the planes path.
-PIECE_MIN_ROWS = int(os.environ.get('HX_PIECE_MIN_ROWS', '16384'))
+# (4096 tokens) 24.4 ms/step on the piece GEMMs against 20.0 on the planes path; at batch 64
+# (8192 tokens) the piece GEMMs win, 30.4 against 31.0 ms (profiles/r3_overlap_wgrad_ab.md).
+PIECE_MIN_ROWS = int(os.environ.get('HX_PIECE_MIN_ROWS', '8192'))
 
 
 def nt_ok(n_in, n_out, rows=None):

@@ -58,6 +58,10 @@ def swish(x):
 
 ACT2FN = {'gelu': gelu, 'relu': F.relu, 'swish': swish, 'tanh': torch.tanh}
 
+# HX_WGRAD_DEFER=0: the attention-output weight gradient runs in its own backward (on the side
+# stream, beside the attention backward) instead of grouped into the QKV backward's launch
+_WGRAD_DEFER = os.environ.get('HX_WGRAD_DEFER', '1') != '0'
+
 
 class BertConfig(object):
     """Configuration of a BERT model (reference bert_modeling.py:180-266)."""
@@ -226,9 +230,12 @@ class BertAttention(nn.Module):
         # the residual gradient of input_tensor is fused into the QKV dgrad GEMM; the output
         # projection's weight gradient runs grouped with the QKV projection's (ops.WgradDefer)
         rg = ops.ResidualGrad()
-        wd = ops.WgradDefer()
-        ctx = self.self(input_tensor, attention_mask_bias, rg, wgrad_join=(self.output.dense.weight, wd))
-        return self.output(ctx, input_tensor, rg, wgrad_defer=wd)
+        if _WGRAD_DEFER:
+            wd = ops.WgradDefer()
+            ctx = self.self(input_tensor, attention_mask_bias, rg, wgrad_join=(self.output.dense.weight, wd))
+            return self.output(ctx, input_tensor, rg, wgrad_defer=wd)
+        ctx = self.self(input_tensor, attention_mask_bias, rg)
+        return self.output(ctx, input_tensor, rg)
 
 
 class BertIntermediate(nn.Module):

@@ -204,7 +204,8 @@ def side_begin(device, pieces=False):
     idx = device.index if device.index is not None else torch.cuda.current_device()
     st = _Side.streams.get(idx)
     if st is None:
-        st = _Side.streams[idx] = torch.cuda.Stream(device=idx)
+        # HX_SIDE_PRIO: HIP stream priority of the side stream (-1 = high, 0 = normal; A/B knob)
+        st = _Side.streams[idx] = torch.cuda.Stream(device=idx, priority=int(os.environ.get('HX_SIDE_PRIO', '0')))
     st.wait_stream(torch.cuda.current_stream(idx))
     if not _Side.active:
         torch.autograd.Variable._execution_engine.queue_callback(side_join)

@@ -4,7 +4,7 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 
 is launched by ``torch.distributed.run`` (one rank per GPU, RCCL).  Runs the real
 framework path -- synthetic NVIDIA-schema HDF5 shards -> native reader -> pinned
 staging on the HIP copy stream -> Controller.train_step (fused HIP kernels,
-hand-written bf16x6 piece GEMMs -- hipBLASLt only for the MLM decoder --, flat-buffer
+hand-written piece GEMMs for every BERT linear and the MLM decoder, flat-buffer
 RCCL / xGMI reducer, fused norm/clip/Adam) -- with
 random-init BERT-base weights (no network: no corpus, no checkpoint).
 
@@ -82,6 +82,11 @@ def parse():
                          'beside one) spins for US microseconds beside the step on its own stream, its workgroups '
                          'dealt over the XCDs like an RCCL kernel\'s ("mask": confined to CUs 0..CUS-1 by a CU-masked '
                          'stream instead) (tools/probe/comm_contention_probe.sh)')
+    ap.add_argument('--comm-cus', default='auto',
+                    help='CUs left to the overlapped gradient all-reduce for N > 1 (train.py --comm-cus)')
+    ap.add_argument('--comm-probe-steps', type=int, default=5,
+                    help='N > 1: untimed steps AFTER the timed region with the gradient collectives off, for '
+                         'exposed_comm_ms (0 = skip)')
     ap.add_argument('--reserve-cus', type=int, default=0,
                     help='CUs the GEMM / weight-gradient plans leave to a concurrent comm kernel (--comm-cus)')
     ap.add_argument('--world', type=int, default=0, help=argparse.SUPPRESS)
@@ -170,7 +175,8 @@ def run(a, rank, world, dev_index, init_method):
             '--disable-validation', '--no-save', '--precision', a.precision, '--fp32-gemm', a.fp32_gemm,
             '--distributed-world-size', str(world),
             '--update-freq', str(a.update_freq), '--gemm-tuning', a.gemm_tuning,
-            '--allreduce-impl', a.allreduce_impl, '--bucket-cap-mb', str(a.bucket_cap_mb)]
+            '--allreduce-impl', a.allreduce_impl, '--bucket-cap-mb', str(a.bucket_cap_mb),
+            '--comm-cus', str(a.comm_cus)]
     if a.profile_phases:
         argv += ['--profile-phases']
     if a.overlap_wgrad != 'auto':
@@ -235,11 +241,35 @@ def run(a, rank, world, dev_index, init_method):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     loss = float(out['loss']) if out is not None else float('nan')
-    t = torch.tensor([elapsed], dtype=torch.float64, device='cuda')
+    # every rank's time and a count of the ranks the communicator really reduced over
+    per_rank = [elapsed]
+    ranks_seen = 1
     if world > 1:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    elapsed = float(t.item())
+        times = torch.zeros(world, dtype=torch.float64, device='cuda')
+        times[rank] = elapsed
+        torch.distributed.all_reduce(times)
+        per_rank = times.tolist()
+        one = torch.ones(1, dtype=torch.float64, device='cuda')
+        torch.distributed.all_reduce(one)
+        ranks_seen = int(round(one.item()))
+    elapsed = max(per_rank)
     ms = elapsed / a.steps * 1000.0
+    exposed = None
+    if world > 1 and a.comm_probe_steps > 0 and ctrl.reducer.enabled:
+        # diagnostics AFTER the timed region: the same steps with the bucket collectives off
+        # (gradients stay rank-local); the step-time difference is the all-reduce time the
+        # backward does not hide
+        ctrl.reducer.enabled = False
+        torch.cuda.synchronize()
+        torch.distributed.barrier()
+        t1 = time.perf_counter()
+        for _ in range(a.comm_probe_steps):
+            step()
+        torch.cuda.synchronize()
+        nc = torch.tensor([time.perf_counter() - t1], dtype=torch.float64, device='cuda')
+        torch.distributed.all_reduce(nc, op=torch.distributed.ReduceOp.MAX)
+        ctrl.reducer.enabled = True
+        exposed = ms - float(nc.item()) / a.comm_probe_steps * 1000.0
     global_batch = a.batch * a.update_freq * world
     value = global_batch * a.steps / elapsed
     ref = REF_SAMPLES_PER_SEC.get(world)
@@ -268,6 +298,13 @@ def run(a, rank, world, dev_index, init_method):
                        'fp32_gemm': a.fp32_gemm if a.precision == 'fp32' else None,
                        'allreduce': a.allreduce_impl if world > 1 else None},
             'final_logged_loss': round(loss, 5),
+            'ranks_seen': ranks_seen,
+            'per_rank_ms': {'min': round(min(per_rank) / a.steps * 1e3, 3),
+                            'max': round(max(per_rank) / a.steps * 1e3, 3)},
+            'exposed_comm_ms': round(exposed, 3) if exposed is not None else None,
+            'transport': ('xgmi' if getattr(ctrl.reducer, 'xgmi', None) is not None else a.backend)
+                         if world > 1 else None,
+            'comm_cus': getattr(ctrl, 'comm_cus', 0),
         }
         print(json.dumps(rec), flush=True)
     if a.profile_phases or a.sync_debug:

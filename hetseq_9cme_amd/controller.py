@@ -34,6 +34,7 @@ import torch
 
 from . import checkpoint_utils, ops
 from .ops import gemm_tuning
+from .options import comm_cus
 from .data.prefetch import unwrap
 from .optim import build_lr_scheduler, build_optimizer
 from .parallel import distributed as dist_utils
@@ -44,6 +45,22 @@ from .utils.phase_timer import PhaseTimer
 from .utils.misc import ensure_train, move_to_device
 
 LN2 = math.log(2)
+
+# flags this framework's parser has always added and the reference's never did (options.py)
+_OWN_FLAGS = ('fused_kernels', 'allreduce_impl', 'precision', 'overlap_wgrad', 'gemm_tuning')
+
+
+def state_order_ambiguous(optim_state, ck_args):
+    """Is an optimizer state's parameter order unknowable?  States are numbered in
+    model.parameters() order; files since the state-order tag say so ('param_order'), and so do
+    untagged ones from the reference / torch optimizers (no flags of this framework in their
+    args) and from this framework after --fp32-gemm appeared (which came after the switch to
+    model order).  Only untagged files of this framework's earliest builds (own flags, no
+    ``fp32_gemm``) may be numbered by flat index, and nothing in them tells which: refuse those."""
+    if 'param_order' in optim_state or ck_args is None:
+        return False
+    own = any(hasattr(ck_args, f) for f in _OWN_FLAGS)
+    return own and not hasattr(ck_args, 'fp32_gemm')
 
 
 class Controller(object):
@@ -57,7 +74,7 @@ class Controller(object):
         ops.set_fp32_gemm(getattr(args, 'fp32_gemm', 'native'))
         ow = getattr(args, 'overlap_wgrad', 'auto')
         ops.set_side_stream('on' if os.environ.get('HETSEQ_SIDE_STREAM') == '1' else
-                            {True: 'on', False: 'auto', None: 'auto'}.get(ow, ow))
+                            {True: 'on', False: 'off', None: 'auto'}.get(ow, ow))
         if getattr(args, 'debug_kernels', False) and self.cuda:
             ops.C().set_debug(True)   # validation inside the bindings (see csrc/bindings.cpp)
         if self.cuda:
@@ -77,14 +94,17 @@ class Controller(object):
                                    find_unused_parameters=getattr(args, 'find_unused_parameters', False),
                                    broadcast_params=use_reducer,
                                    bucket_peer_mb=getattr(args, 'bucket_peer_mb', 0.0), force=force)
-        if use_reducer and self.cuda and getattr(args, 'comm_cus', 0) > 0:
+        ncus = comm_cus(args) if self.cuda else 0
+        self.comm_cus = ncus if use_reducer else 0
+        if use_reducer and ncus > 0:
             # while its buckets are in flight the plans leave these CUs to the all-reduce
-            self.reducer.set_comm_cus(args.comm_cus)
+            self.reducer.set_comm_cus(ncus)
         if not use_reducer:
             self.reducer.enabled = False
         elif getattr(args, 'allreduce_impl', 'rccl') == 'xgmi':
             self.reducer.use_xgmi(blocks=getattr(args, 'xgmi_blocks', 64),
-                                  timeout_s=float(getattr(args, 'distributed_timeout', 1800)))
+                                  timeout_s=float(getattr(args, 'distributed_timeout', 1800)),
+                                  comm_cus=ncus)
         self._dummy_batch = dummy_batch
         self._oom_batch = oom_batch or dummy_batch
         self._lr_scheduler = None
@@ -192,16 +212,13 @@ class Controller(object):
                 'Optimizer does not match; please reset the optimizer (--reset-optimizer).'
             if not reset_lr_scheduler:
                 self.lr_scheduler.load_state_dict(last_optim['lr_scheduler_state'])
-            # an untagged state from this framework's own earlier files is numbered by flat index
-            # (ADVICE r2); reference / torch-optimizer files are untagged too but carry none of
-            # this framework's own flags in their args
             ck_args = state.get('args') if os.path.exists(filename) else None
-            legacy = 'param_order' not in last_optim_state and ck_args is not None and \
-                hasattr(ck_args, 'fp32_gemm')
-            if legacy:
-                print('| optimizer state of {} predates the state-order tag: remapping from flat order'.format(
-                    filename))
-            self.optimizer.load_state_dict(last_optim_state, optimizer_overrides, legacy_flat_order=legacy)
+            if state_order_ambiguous(last_optim_state, ck_args):
+                raise RuntimeError(
+                    'optimizer state of {} carries no state-order tag and was written by an early build of this '
+                    'framework whose state may be numbered by flat index; resume it with --reset-optimizer'.format(
+                        filename))
+            self.optimizer.load_state_dict(last_optim_state, optimizer_overrides)
             self.set_num_updates(last_optim['num_updates'])
         if extra_state is not None and 'train_iterator' in extra_state:
             epoch = extra_state['train_iterator']['epoch']
@@ -323,6 +340,8 @@ class Controller(object):
             # --find-unused-parameters: the local used flags (host-known) ride in the same
             # all-reduce; the optimizer consumes the summed flags on device (no host read)
             used_at = None
+            if hasattr(self.optimizer, 'device_used'):
+                self.optimizer.device_used = None   # never a previous update's flags
             if self.reducer.enabled and self.reducer.find_unused and hasattr(self.optimizer, 'device_used') \
                     and not capturing:
                 used_at = len(fields)
@@ -403,6 +422,8 @@ class Controller(object):
                                 opt.clipped if self.args.clip_norm > 0 else 0.)
         except OverflowError as e:
             print('| WARNING: overflow detected, ' + str(e))
+            if hasattr(opt, 'device_used'):
+                opt.device_used = None
             self.zero_grad()
             logging_output = None
 

@@ -217,6 +217,10 @@ class Reducer : public std::enable_shared_from_this<Reducer> {
 
  private:
   void reset_iteration() {
+    if (reserving_) {   // a backward that raised before finalize_locked(): give the CUs back
+      hx_set_reserved_cus(0);
+      reserving_ = false;
+    }
     pending_ = nparams_;
     launched_ = 0;
     works_.clear();

@@ -207,12 +207,14 @@ def add_distributed_training_args(parser):
                             'bucket all-reduces are scheduled ahead of queued backward kernels)')
     group.add_argument('--xgmi-blocks', default=64, type=int, metavar='N',
                        help='workgroups per xGMI all-reduce launch (CUs taken from backward while it runs)')
-    group.add_argument('--comm-cus', default=0, type=int, metavar='N',
+    group.add_argument('--comm-cus', default='auto', type=_comm_cus_arg, metavar='N',
                        help='MI355X: CUs left to the gradient all-reduce while it overlaps the backward (world > 1): '
                             'from the first bucket collective to the end of backward the one-round GEMM / '
-                            'weight-gradient plans are sized for the other CUs, and RCCL is capped at N channels '
-                            '(NCCL_MAX_NCHANNELS, one workgroup each) -- see csrc/kernels/cu_reserve.hip and '
-                            'profiles/r3_comm_contention.md (0 = off)')
+                            'weight-gradient plans are sized for the other CUs, RCCL is capped at N channels '
+                            '(NCCL_MAX_NCHANNELS, one workgroup each) and the xGMI kernel runs on N CUs -- see '
+                            'csrc/kernels/cu_reserve.hip and profiles/r3_comm_contention.md (a 16-CU comm load: '
+                            '+15 %% step time unplanned, +6 %% with the plans sized around it).  0 = off; '
+                            'auto (default) = 16 on GPU runs with world > 1, else off')
     group.add_argument('--force-reducer', action='store_true',
                        help='MI355X: run the bucketed gradient reducer even in a one-rank process group, so a '
                             'one-GPU run exercises the RCCL stream path (buckets, side-stream ordering, '
@@ -318,6 +320,23 @@ def eval_bool_arg(x):
     if isinstance(x, bool):
         return x
     return str(x).lower() in ('1', 'true', 'yes', 'on')
+
+
+AUTO_COMM_CUS = 16
+
+
+def _comm_cus_arg(v):
+    return 'auto' if str(v) == 'auto' else int(v)
+
+
+def comm_cus(args):
+    """--comm-cus resolved: 'auto' = AUTO_COMM_CUS on GPU runs with world > 1 (channel cap of the
+    RCCL communicator + the plans' reservation), else 0."""
+    v = getattr(args, 'comm_cus', 0)
+    if v == 'auto':
+        gpu = not getattr(args, 'cpu', False) and getattr(args, 'distributed_backend', 'nccl') == 'nccl'
+        return AUTO_COMM_CUS if gpu and getattr(args, 'distributed_world_size', 1) > 1 else 0
+    return max(0, int(v))
 
 
 def parse_args_and_arch(parser, s=None):

@@ -48,10 +48,11 @@ def distributed_init(args):
     if args.distributed_world_size == 1 and not getattr(args, 'force_reducer', False):
         # (--force-reducer: a one-rank group on purpose, to drive the collective stream path)
         raise ValueError('Cannot initialize distributed with distributed_world_size=1')
-    if getattr(args, 'comm_cus', 0) > 0 and args.distributed_backend == 'nccl':
+    from ..options import comm_cus
+    if comm_cus(args) > 0 and args.distributed_backend == 'nccl':
         # --comm-cus: RCCL's collectives take at most that many CUs (one workgroup per channel);
         # read by RCCL when the communicator is created, so before the first collective
-        os.environ.setdefault('NCCL_MAX_NCHANNELS', str(args.comm_cus))
+        os.environ.setdefault('NCCL_MAX_NCHANNELS', str(comm_cus(args)))
     if dist.is_initialized():
         warnings.warn('Distributed is already initialized, cannot initialize twice!')
     else:

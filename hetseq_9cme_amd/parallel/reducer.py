@@ -141,7 +141,7 @@ class GradReducer(object):
     def _sync(self):
         return self._native.sync()
 
-    def use_xgmi(self, blocks=64, timeout_s=1800.0):
+    def use_xgmi(self, blocks=64, timeout_s=1800.0, comm_cus=0):
         """Reduce gradient buckets with the intra-node xGMI kernel (collective call).
         Returns False (and keeps RCCL) when the group is not eligible."""
         from .xgmi import XgmiAllReduce, xgmi_eligible
@@ -153,7 +153,8 @@ class GradReducer(object):
             return False
         # buckets are slices of the flat gradient buffer: it is registered once and every bucket
         # is reduced in place over the peers' mappings of it (no staging copy)
-        self.xgmi = XgmiAllReduce(self.flat.grad_flat, self.group, blocks=blocks, timeout_s=timeout_s)
+        self.xgmi = XgmiAllReduce(self.flat.grad_flat, self.group, blocks=blocks, timeout_s=timeout_s,
+                                  comm_cus=comm_cus)
         self._native.use_xgmi(self.xgmi.h, self.xgmi.stream.cuda_stream)
         return True
 

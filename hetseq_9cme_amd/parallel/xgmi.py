@@ -87,8 +87,15 @@ class XgmiAllReduce(object):
     :meth:`all_reduce_` with the same slices in the same order.
     """
 
-    def __init__(self, buffer, group=None, blocks=64, timeout_s=300.0, oneshot_kb=512):
+    def __init__(self, buffer, group=None, blocks=64, timeout_s=300.0, oneshot_kb=512, comm_cus=0):
+        """``comm_cus`` > 0 (--comm-cus): the kernel is confined to that many CUs -- its grid is
+        capped at ``comm_cus`` workgroups and it runs on a CU-masked stream over the device's last
+        ``comm_cus`` CUs -- the ones the GEMM plans leave free while buckets are in flight
+        (csrc/kernels/cu_reserve.hip)."""
         self.group = group
+        self._masked = 0
+        if comm_cus > 0:
+            blocks = max(1, min(blocks, int(comm_cus)))
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.buffer = buffer
@@ -100,7 +107,13 @@ class XgmiAllReduce(object):
         # every rank has mapped every peer before any kernel may touch a peer page
         torch.cuda.synchronize()
         dist.barrier(group=group)
-        self.stream = torch.cuda.Stream(priority=-1)
+        if comm_cus > 0:
+            ncu = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+            self._masked = int(C().cu_masked_stream(max(0, ncu - int(comm_cus)), int(comm_cus)))
+        if self._masked:
+            self.stream = torch.cuda.ExternalStream(self._masked)
+        else:
+            self.stream = torch.cuda.Stream(priority=-1)
 
     @property
     def oneshot_max(self):
@@ -129,6 +142,9 @@ class XgmiAllReduce(object):
         if self.h:
             C().xar_destroy(self.h)
             self.h = 0
+        if self._masked:
+            C().destroy_stream(self._masked)
+            self._masked = 0
 
     def __del__(self):
         try:

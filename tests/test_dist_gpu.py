@@ -86,6 +86,12 @@ def test_bench_two_ranks_contract(tmp_path):
     assert rec['config']['global_batch'] == 16 and rec['config']['parallelism'] == 'dp2'
     assert rec['value'] > 0 and rec['ms_per_step'] > 0
     assert abs(rec['value'] - 16 * 1000.0 / rec['ms_per_step']) / rec['value'] < 1e-3
+    # self-verifying N > 1 fields: the communicator really summed over both ranks, the reported
+    # time is the slower rank's, and the collectives-off probe ran after the timed steps
+    assert rec['ranks_seen'] == rec['n_gpus'] == 2
+    assert rec['per_rank_ms']['min'] <= rec['per_rank_ms']['max'] == rec['ms_per_step']
+    assert rec['exposed_comm_ms'] is not None and rec['transport'] == 'gloo'
+    assert rec['comm_cus'] == 0          # auto: no reservation for a gloo rehearsal
 
 
 def test_bench_heterogeneous_nodes_contract(tmp_path):
@@ -108,6 +114,7 @@ def test_bench_heterogeneous_nodes_contract(tmp_path):
     assert rec['n_gpus'] == 3 and rec['config']['global_batch'] == 24
     assert rec['config']['nodes'] == [2, 1] and rec['config']['parallelism'] == 'dp3 (nodes 2+1)'
     assert abs(rec['value'] - 24 * 1000.0 / rec['ms_per_step']) / rec['value'] < 1e-3
+    assert rec['ranks_seen'] == 3
 
 
 def test_bench_ner_torchrun_contract(tmp_path):

@@ -129,3 +129,61 @@ def test_state_order_tag_and_legacy_flat_files():
         assert not same(opt3)
     except ValueError:
         pass   # or a shape mismatch is caught
+
+
+def _cpu_controller(tmp_path):
+    from hetseq_9cme_amd import options, tasks
+    from hetseq_9cme_amd.controller import Controller
+    from hetseq_9cme_amd.data.synthetic import BERT_TINY, write_bert_config, write_synthetic_bert_shards, write_vocab
+    d = tmp_path / 'data'
+    if not d.exists():
+        d.mkdir()
+        write_synthetic_bert_shards(str(d), n_files=1, samples_per_file=16, seq_len=32, max_pred=5, vocab_size=1024,
+                                    split='train', seed=1)
+        write_bert_config(str(d / 'tiny.json'), **BERT_TINY)
+        write_vocab(str(d / 'vocab.txt'), 1024)
+    args = options.parse_training_args(
+        ['--task', 'bert', '--data', str(d), '--dict', str(d / 'vocab.txt'), '--config_file', str(d / 'tiny.json'),
+         '--max-sentences', '4', '--fast-stat-sync', '--num-workers', '1', '--lr', '1e-3', '--weight-decay', '0.01',
+         '--save-dir', str(tmp_path / 'ck'), '--cpu'])
+    args.device_id, args.distributed_rank = 0, 0
+    torch.manual_seed(args.seed)
+    task = tasks.setup_task(args)
+    ctl = Controller(args, task, task.build_model(args))
+    itr = ctl.get_train_iterator(epoch=0)
+    return ctl, itr
+
+
+def test_controller_resumes_untagged_model_order_state(tmp_path):
+    """an untagged state written by this framework after --fp32-gemm existed is in
+    model order and must come back bit for bit through Controller.load_checkpoint; an untagged
+    state of the earliest builds (own flags, no fp32_gemm) is refused, never silently permuted."""
+    import os
+    from hetseq_9cme_amd import checkpoint_utils
+    from hetseq_9cme_amd.data import iterators
+    ctl, itr = _cpu_controller(tmp_path)
+    batches = iterators.GroupedIterator(itr.next_epoch_itr(shuffle=False), 1)
+    for _ in range(2):
+        ctl.train_step(next(batches))
+    os.makedirs(str(tmp_path / 'ck'), exist_ok=True)
+    path = str(tmp_path / 'ck' / 'untagged.pt')
+    ctl.save_checkpoint(path, {})
+    st = checkpoint_utils.load_checkpoint_to_cpu(path)
+    assert hasattr(st['args'], 'fp32_gemm')
+    del st['last_optimizer_state']['param_order']        # what round-2 builds wrote
+    torch.save(st, path)
+    ctl2, _ = _cpu_controller(tmp_path)
+    ctl2.load_checkpoint(path)
+    o1, o2 = ctl.optimizer, ctl2.optimizer
+    assert torch.equal(o1.exp_avg, o2.exp_avg) and torch.equal(o1.exp_avg_sq, o2.exp_avg_sq)
+    # the earliest builds' files: refused with a pointer to --reset-optimizer
+    delattr(st['args'], 'fp32_gemm')
+    torch.save(st, path)
+    ctl3, _ = _cpu_controller(tmp_path)
+    try:
+        ctl3.load_checkpoint(path)
+    except RuntimeError as e:
+        assert '--reset-optimizer' in str(e)
+    else:
+        raise AssertionError('an order-ambiguous optimizer state must not load')
+    ctl3.load_checkpoint(path, reset_optimizer=True)      # the documented way out

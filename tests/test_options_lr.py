@@ -91,3 +91,29 @@ def test_epoch_step_lr_list():
     s = _sched(lr=[0.1, 0.05])
     assert s.step(0) == 0.1
     assert s.step(1) == 0.05 and s.step(7) == 0.05
+
+
+def test_comm_cus_auto_plan():
+    """--comm-cus defaults to 'auto': the RCCL channel cap + plan reservation (16 CUs) on GPU runs
+    with world > 1 (profiles/r3_comm_contention.md: a 16-CU comm load costs +15 % unplanned, +6 %
+    planned), off for one rank, CPU / gloo rehearsals, and whatever the user sets explicitly."""
+    from hetseq_9cme_amd import options
+    base = ['--task', 'mnist', '--data', '/tmp/x']
+    a = options.parse_training_args(base)
+    assert a.comm_cus == 'auto'
+    a.distributed_world_size = 8
+    assert options.comm_cus(a) == options.AUTO_COMM_CUS == 16
+    a.distributed_world_size = 1
+    assert options.comm_cus(a) == 0
+    a.distributed_world_size = 8
+    a.distributed_backend = 'gloo'
+    assert options.comm_cus(a) == 0
+    a = options.parse_training_args(base + ['--comm-cus', '8', '--cpu'])
+    a.distributed_world_size = 8
+    assert options.comm_cus(a) == 8
+    a = options.parse_training_args(base + ['--comm-cus', '0'])
+    a.distributed_world_size = 8
+    assert options.comm_cus(a) == 0
+    a = options.parse_training_args(base + ['--cpu'])
+    a.distributed_world_size = 4
+    assert options.comm_cus(a) == 0

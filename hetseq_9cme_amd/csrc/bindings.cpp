@@ -818,6 +818,222 @@ std::vector<Tensor> gemm_split_dgelu(Tensor a, Tensor b, int64_t passes, Tensor 
   return {p, db};
 }
 
+// ------------------------------------------------------------------ fp16x3 GEMMs (gemm_f16.hip)
+// fp32 operands travel with max |x| partials (any 1-D fp32 tensor whose max is max |x|): the
+// kernels turn them into the power-of-two scale of the fp16 split
+inline void check_af32(const Tensor& a, const char* what) {
+  check_f32(a, what);
+  TORCH_CHECK(a.dim() == 2 && a.stride(1) == 1 && a.stride(0) % 4 == 0 && aligned16(a.data_ptr()) &&
+                  a.size(1) % 16 == 0 && a.size(0) < (1LL << 31),
+              what, ": fp32 [rows, K] with unit column stride, 16-B aligned rows and K % 16 == 0");
+}
+inline void check_amax(const Tensor& t, const Tensor& ref, const char* what) {
+  check_f32(t, what);
+  TORCH_CHECK(t.dim() == 1 && t.is_contiguous() && t.numel() >= 1 && t.numel() < (1 << 24) &&
+                  t.device() == ref.device(), what, ": 1-D fp32 max |x| partials on the operand's device");
+}
+inline void check_p2(const Tensor& b, int64_t K, const char* what) {
+  TORCH_CHECK(b.is_cuda() && b.scalar_type() == torch::kHalf && b.dim() == 2 && b.is_contiguous() &&
+                  b.size(1) == 2 * K && aligned16(b.data_ptr()), what, ": fp16 P2 pieces [N, 2K]");
+}
+
+Tensor amax_rows(Tensor x) {
+  check_f32(x, "amax_rows");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 4 == 0 && x.size(1) % 4 == 0 &&
+                  aligned16(x.data_ptr()), "amax_rows: fp32 [rows, cols] with 16-B rows, cols % 4 == 0");
+  const int np = hx_amax_rows_parts(x.size(0), (int)x.size(1));
+  Tensor part = torch::empty({np}, x.options());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  hx_amax_rows(x.data_ptr<float>(), x.size(0), (int)x.size(1), x.stride(0), part.data_ptr<float>(), np, cur_stream(x));
+  return part;
+}
+
+// [(wf, wt, parts)] per weight: P2 fp16 pieces of W and of W^T, and W's max |x| partials
+std::vector<std::vector<Tensor>> split_weight_f16(std::vector<Tensor> Ws) {
+  TORCH_CHECK(!Ws.empty() && Ws.size() <= HX_WBATCH, "split_weight_f16: 1..64 weights");
+  HxWeightBatch d{};
+  d.n = (int)Ws.size();
+  const int P = hx_weight_f16_parts();
+  Tensor part = torch::empty({d.n * P}, Ws[0].options());
+  std::vector<std::vector<Tensor>> out;
+  int tiles = 0;
+  for (int i = 0; i < d.n; ++i) {
+    const Tensor& W = Ws[i];
+    check_f32(W, "split_weight_f16 input");
+    TORCH_CHECK(W.dim() == 2 && W.is_contiguous() && W.size(0) % 64 == 0 && W.size(1) % 64 == 0 &&
+                    aligned16(W.data_ptr()) && W.device() == Ws[0].device(),
+                "split_weight_f16: every W contiguous [N, K], N and K multiples of 64, one device");
+    const int64_t N = W.size(0), K = W.size(1);
+    auto hf = W.options().dtype(torch::kHalf);
+    Tensor wf = torch::empty({N, 2 * K}, hf), wt = torch::empty({K, 2 * N}, hf);
+    d.W[i] = W.data_ptr<float>();
+    d.wf[i] = reinterpret_cast<uint16_t*>(wf.data_ptr());
+    d.wt[i] = reinterpret_cast<uint16_t*>(wt.data_ptr());
+    d.N[i] = (int)N;
+    d.K[i] = (int)K;
+    d.mask[i] = 0;
+    d.start[i] = tiles;
+    tiles += (int)((N / 64) * (K / 64));
+    out.push_back({wf, wt, part.narrow(0, (int64_t)i * P, P)});
+  }
+  d.start[d.n] = tiles;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(Ws[0].device());
+  hx_split_weight_f16(d, part.data_ptr<float>(), cur_stream(Ws[0]));
+  return out;
+}
+
+static HxGemmF16 f16_args(const Tensor& a, const Tensor& aa, const Tensor& b, const Tensor& ba, const char* what) {
+  check_af32(a, what);
+  check_amax(aa, a, what);
+  check_p2(b, a.size(1), what);
+  check_amax(ba, a, what);
+  TORCH_CHECK(b.device() == a.device() && b.size(0) < (1LL << 31), what, ": operands on one device");
+  HxGemmF16 p{};
+  p.A = a.data_ptr<float>();
+  p.lda = a.stride(0);
+  p.a_amax = aa.data_ptr<float>();
+  p.na = (int)aa.numel();
+  p.B = reinterpret_cast<const uint16_t*>(b.data_ptr());
+  p.ldb = b.size(1);
+  p.b_amax = ba.data_ptr<float>();
+  p.nb = (int)ba.numel();
+  p.M = (int)a.size(0);
+  p.N = (int)b.size(0);
+  p.K = (int)a.size(1);
+  p.ks = 1;
+  return p;
+}
+inline void check_vec(const OptT& v, int64_t n, const char* what) {
+  if (!has(v)) return;
+  check_f32(*v, what);
+  TORCH_CHECK(v->numel() == n && v->is_contiguous() && aligned16(v->data_ptr()), what, ": fp32 [N], 16-B aligned");
+}
+
+// C (+)= a . b^T (+ bias); ks split-K slabs (0 = plan: deep reductions with few tiles), summed here
+Tensor gemm_f16(Tensor a, Tensor a_amax, Tensor b, Tensor b_amax, OptT out_, bool beta, OptT bias, int64_t ks) {
+  HxGemmF16 p = f16_args(a, a_amax, b, b_amax, "gemm_f16");
+  check_vec(bias, p.N, "gemm_f16 bias");
+  const int cfg = hx_gemm_f16_plan(p.M, p.N, p.K);
+  TORCH_CHECK(cfg >= 0, "gemm_f16: no tile for N = ", p.N);
+  TORCH_CHECK(!beta || has(out_), "gemm_f16: beta needs an output to accumulate into");
+  if (ks <= 0) ks = (beta || has(bias)) ? 1 : hx_gemm_f16_ks(p.M, p.N, p.K, cfg);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  auto f32 = a.options();
+  if (ks > 1) {
+    TORCH_CHECK(!beta && !has(bias), "gemm_f16: split-K without beta / bias");
+    Tensor part = torch::empty({ks, p.M, p.N}, f32);
+    p.C = part.data_ptr<float>();
+    p.ldc = p.N;
+    p.ks = (int)ks;
+    p.c_zs = (int64_t)p.M * p.N;
+    TORCH_CHECK(hx_gemm_f16(p, cfg, cur_stream(a)) == 0, "gemm_f16: split-K launch failed (ks must divide K / 16)");
+    if (has(out_)) {
+      at::sum_out(*out_, part, {0});
+      return *out_;
+    }
+    return part.sum(0);
+  }
+  Tensor out = has(out_) ? *out_ : torch::empty({p.M, p.N}, f32);
+  TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.dim() == 2 && out.size(0) == p.M && out.size(1) == p.N &&
+                  out.stride(1) == 1 && out.stride(0) % 4 == 0 && aligned16(out.data_ptr()),
+              "gemm_f16: out must be fp32 [M, N] with unit column stride and 16-B rows");
+  p.C = out.data_ptr<float>();
+  p.ldc = out.stride(0);
+  p.beta = beta ? 1 : 0;
+  p.bias = ptr_or_null<float>(bias);
+  TORCH_CHECK(hx_gemm_f16(p, cfg, cur_stream(a)) == 0, "gemm_f16: launch failed");
+  dbg_finite(out, "gemm_f16");
+  return out;
+}
+
+// FFN up: u = a . b^T + bias -> (gelu'(u) if dmode else u, gelu(u) fp32, max |gelu(u)| partials)
+std::vector<Tensor> gemm_f16_gelu(Tensor a, Tensor a_amax, Tensor b, Tensor b_amax, OptT bias, int64_t dmode) {
+  HxGemmF16 p = f16_args(a, a_amax, b, b_amax, "gemm_f16_gelu");
+  check_vec(bias, p.N, "gemm_f16_gelu bias");
+  const int cfg = hx_gemm_f16_plan(p.M, p.N, p.K);
+  TORCH_CHECK(cfg >= 0, "gemm_f16_gelu: no tile for N = ", p.N);
+  auto f32 = a.options();
+  Tensor c = torch::empty({p.M, p.N}, f32), h = torch::empty({p.M, p.N}, f32);
+  Tensor am = torch::empty({hx_gemm_f16_tiles(p.M, p.N, cfg)}, f32);
+  p.kind = 1;
+  p.C = c.data_ptr<float>();
+  p.ldc = p.N;
+  p.bias = ptr_or_null<float>(bias);
+  p.P = h.data_ptr<float>();
+  p.ldp = p.N;
+  p.amax_out = am.data_ptr<float>();
+  p.dmode = dmode ? 1 : 0;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  TORCH_CHECK(hx_gemm_f16(p, cfg, cur_stream(a)) == 0, "gemm_f16_gelu: launch failed");
+  dbg_finite(h, "gemm_f16_gelu");
+  return {c, h, am};
+}
+
+// FFN down data gradient + GELU backward: t = (a . b^T) * (dmode ? u : gelu'(u + bias)) ->
+// (t fp32, max |t| partials, dbias = column sums of t (into dbias_out when given))
+std::vector<Tensor> gemm_f16_dgelu(Tensor a, Tensor a_amax, Tensor b, Tensor b_amax, Tensor u, OptT bias,
+                                   OptT dbias_out, int64_t dmode) {
+  TORCH_CHECK(!dmode || !has(bias), "gemm_f16_dgelu: dmode 1 takes gelu'(u), which has the bias in it");
+  HxGemmF16 p = f16_args(a, a_amax, b, b_amax, "gemm_f16_dgelu");
+  check_vec(bias, p.N, "gemm_f16_dgelu bias");
+  check_f32(u, "gemm_f16_dgelu u");
+  TORCH_CHECK(u.dim() == 2 && u.size(0) == p.M && u.size(1) == p.N && u.is_contiguous() && aligned16(u.data_ptr()),
+              "gemm_f16_dgelu: u must be fp32 [M, N]");
+  const int cfg = hx_gemm_f16_plan(p.M, p.N, p.K);
+  TORCH_CHECK(cfg >= 0, "gemm_f16_dgelu: no tile for N = ", p.N);
+  const int prow = hx_gemm_f16_colpart_rows(p.M, cfg);
+  auto f32 = a.options();
+  Tensor t = torch::empty({p.M, p.N}, f32);
+  Tensor am = torch::empty({hx_gemm_f16_tiles(p.M, p.N, cfg)}, f32);
+  Tensor part = torch::empty({prow, p.N}, f32);
+  Tensor db = has(dbias_out) ? *dbias_out : torch::empty({p.N}, f32);
+  TORCH_CHECK(db.numel() == p.N && db.scalar_type() == torch::kFloat32 && db.is_contiguous(), "gemm_f16_dgelu: dbias");
+  p.kind = 2;
+  p.bias = ptr_or_null<float>(bias);
+  p.aux = u.data_ptr<float>();
+  p.ldaux = p.N;
+  p.P = t.data_ptr<float>();
+  p.ldp = p.N;
+  p.colpart = part.data_ptr<float>();
+  p.amax_out = am.data_ptr<float>();
+  p.dmode = dmode ? 1 : 0;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  TORCH_CHECK(hx_gemm_f16(p, cfg, cur_stream(a)) == 0, "gemm_f16_dgelu: launch failed");
+  hx_fold_cols(part.data_ptr<float>(), prow, p.N, db.data_ptr<float>(), 0, cur_stream(a));
+  dbg_finite(t, "gemm_f16_dgelu");
+  return {t, am, db};
+}
+
+// dW = dy^T x over the token rows: dy [T, M], x [T, N] fp32 (M, N multiples of 128); out [<= M, N]
+// (rows of dy's padding columns past out.size(0) are not stored)
+Tensor wgrad_f16(Tensor dy, Tensor dy_amax, Tensor x, Tensor x_amax, Tensor out) {
+  check_f32(dy, "wgrad_f16 dy");
+  check_f32(x, "wgrad_f16 x");
+  check_amax(dy_amax, dy, "wgrad_f16");
+  check_amax(x_amax, dy, "wgrad_f16");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0) && dy.stride(1) == 1 && x.stride(1) == 1 &&
+                  dy.stride(0) % 4 == 0 && x.stride(0) % 4 == 0 && aligned16(dy.data_ptr()) &&
+                  aligned16(x.data_ptr()) && dy.size(1) % 128 == 0 && x.size(1) % 128 == 0 &&
+                  dy.size(0) < (1 << 30) && x.device() == dy.device(),
+              "wgrad_f16: dy [T, M], x [T, N] fp32 with 16-B rows, M and N multiples of 128");
+  const int64_t T = dy.size(0), M = dy.size(1), N = x.size(1);
+  check_f32(out, "wgrad_f16 out");
+  TORCH_CHECK(out.dim() == 2 && out.size(0) <= M && out.size(1) == N && out.is_contiguous(),
+              "wgrad_f16: out must be contiguous fp32 [<= M, N]");
+  int cfg = 0, nsplit = 1;
+  hx_wgrad_f16_plan((int)M, (int)N, (int)T, &cfg, &nsplit);
+  Tensor ws;
+  if (nsplit > 1) ws = torch::empty({nsplit, M, N}, dy.options());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
+  TORCH_CHECK(hx_wgrad_f16(dy.data_ptr<float>(), (int)dy.stride(0), dy_amax.data_ptr<float>(), (int)dy_amax.numel(),
+                           x.data_ptr<float>(), (int)x.stride(0), x_amax.data_ptr<float>(), (int)x_amax.numel(),
+                           out.data_ptr<float>(), nsplit > 1 ? ws.data_ptr<float>() : nullptr, (int)M, (int)N, (int)T,
+                           cfg, nsplit, (int)out.size(0), cur_stream(dy)) == 0,
+              "wgrad_f16: launch failed");
+  dbg_finite(out, "wgrad_f16");
+  return out;
+}
+
 // diagnostic: per-wave phase cycle sums of the piece GEMM main loop (cfg 0, bf16x6)
 Tensor gemm_split_stamps(Tensor a, Tensor b, int64_t lay) {
   TORCH_CHECK(gemm_split_ok(a, b, 3), "gemm_split_stamps: unsupported operands");
@@ -1015,6 +1231,24 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_split_dgelu", &gemm_split_dgelu, py::arg("a"), py::arg("b"), py::arg("passes"), py::arg("u"),
         py::arg("bias"), py::arg("dbias_out"), py::arg("lay") = 0, py::arg("dmode") = 0);
   m.def("gemm_split_stamps", &gemm_split_stamps);
+  m.def("amax_rows", &amax_rows);
+  m.def("split_weight_f16", &split_weight_f16);
+  m.def("gemm_f16", &gemm_f16, py::arg("a"), py::arg("a_amax"), py::arg("b"), py::arg("b_amax"),
+        py::arg("out") = py::none(), py::arg("beta") = false, py::arg("bias") = py::none(), py::arg("ks") = 1);
+  m.def("gemm_f16_gelu", &gemm_f16_gelu, py::arg("a"), py::arg("a_amax"), py::arg("b"), py::arg("b_amax"),
+        py::arg("bias"), py::arg("dmode") = 1);
+  m.def("gemm_f16_dgelu", &gemm_f16_dgelu, py::arg("a"), py::arg("a_amax"), py::arg("b"), py::arg("b_amax"),
+        py::arg("u"), py::arg("bias") = py::none(), py::arg("dbias_out") = py::none(), py::arg("dmode") = 1);
+  m.def("wgrad_f16", &wgrad_f16);
+  m.def("gemm_f16_plan", &hx_gemm_f16_plan);
+  m.def("gemm_f16_ks", &hx_gemm_f16_ks);
+  m.def("gemm_f16_tiles", &hx_gemm_f16_tiles);
+  m.def("wgrad_f16_plan", [](int64_t M, int64_t N, int64_t T) {
+    int c = 0, s = 1;
+    hx_wgrad_f16_plan((int)M, (int)N, (int)T, &c, &s);
+    return std::make_tuple(c, s);
+  });
+
   m.def("dma_probe", &dma_probe);
   m.def("gemm_split_ok", &gemm_split_ok);
   m.def("bias_act_planes", &bias_act_planes);

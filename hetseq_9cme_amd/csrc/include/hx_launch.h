@@ -158,6 +158,54 @@ void hx_dma_probe(const void* src, uint32_t bytes, int seg, int ld, int iters, i
 // fold [rows][N] column partials into out[N] (+= if accumulate)
 void hx_fold_cols(const float* partial, int rows, int N, float* out, int accumulate, hipStream_t s);
 
+// gemm_f16.hip -- --fp32-gemm fp16x3: fp32 operands as two scaled fp16 pieces, three MFMA passes.
+// A: fp32 [M][K] (row stride lda, split in the kernel), B: fp16 pieces in the P2 layout [N][2K];
+// a_amax / b_amax: max |x| partials of each operand (na / nb of them) giving its power-of-two scale.
+// kind 0: C (+)= s acc (+ bias)  [ks > 1: split-K slabs C + z c_zs, no bias / beta]
+// kind 1: u = s acc + bias -> C = gelu'(u) (dmode 1) or u (dmode 0); P = gelu(u) fp32; amax_out
+//         [hx_gemm_f16_tiles] = per-tile max |P|
+// kind 2: t = s acc * (dmode ? aux : gelu'(aux + bias)) -> P fp32, amax_out, colpart
+//         [hx_gemm_f16_colpart_rows][N] per-wave column sums of t
+struct HxGemmF16 {
+  const float* A;
+  int64_t lda;
+  const float* a_amax;
+  int na;
+  const uint16_t* B;
+  int64_t ldb;
+  const float* b_amax;
+  int nb;
+  float* C;
+  int64_t ldc;
+  int M, N, K, beta, kind;
+  const float* bias;
+  const float* aux;
+  int64_t ldaux;
+  float* P;
+  int64_t ldp;
+  float* colpart;
+  float* amax_out;
+  int dmode, ks;
+  int64_t c_zs;
+};
+int hx_gemm_f16_plan(int M, int N, int K);
+int hx_gemm_f16_tiles(int M, int N, int cfg);
+int hx_gemm_f16_colpart_rows(int M, int cfg);
+int hx_gemm_f16_ks(int M, int N, int K, int cfg);
+int hx_gemm_f16(const HxGemmF16& p, int cfg, hipStream_t s);
+// dW[M][N] = dY[T][M]^T X[T][N] (fp32 operands, row strides ldy / ldx); rows >= mvalid not stored;
+// ws: nsplit * M * N floats when nsplit > 1
+void hx_wgrad_f16_plan(int M, int N, int T, int* cfg, int* nsplit);
+int hx_wgrad_f16(const float* dy, int ldy, const float* dy_amax, int na, const float* x, int ldx, const float* x_amax,
+                 int nb, float* out, float* ws, int M, int N, int T, int cfg, int nsplit, int mvalid, hipStream_t s);
+// max |x| partials of a [rows][cols] fp32 matrix (cols % 4 == 0, 16-B rows)
+int hx_amax_rows_parts(int64_t rows, int cols);
+void hx_amax_rows(const float* x, int64_t rows, int cols, int64_t ld, float* part, int nparts, hipStream_t s);
+// every weight of a batch -> P2 fp16 pieces wf [N][2K], wt [K][2N] (mask ignored); part: n *
+// hx_weight_f16_parts() max |W| partials, weight i's at part + i * hx_weight_f16_parts()
+int hx_weight_f16_parts();
+void hx_split_weight_f16(const HxWeightBatch& d, float* part, hipStream_t s);
+
 // split.hip -- fp32 -> bf16 planes (piece order[j] = (order >> 4j) & 15) for bf16-MFMA
 // emulation of fp32 GEMMs; interleaved [R][npl][D] or stacked [npl][R][D].
 // Output rows padded to Rp (stacked) / columns to Dp with zeros.

@@ -1,0 +1,801 @@
+// fp32 GEMMs on the fp16 matrix cores with THREE passes (--fp32-gemm fp16x3):
+//
+//   x = 2^-E (h0 + h1),  h0 = fp16(2^E x),  h1 = fp16(2^E x - h0)   (hx_gemm.h: f16_scale_exp)
+//   a . b = 2^-(Ea + Eb) (a0 b0 + a0 b1 + a1 b0) + O(2^-22 |a||b|)
+//
+// Two RNE fp16 pieces hold 22 significant bits of an fp32 value (bf16 pieces hold 8 each, so
+// fp32-class bf16 emulation needs three of them and six pair products: --fp32-gemm bf16x6).  fp16
+// has 5 exponent bits, so every operand tensor is scaled by a power of two 2^E chosen from its
+// largest magnitude (max |x| lands in [2^14, 2^15)): the product of two scaled pieces is exact in
+// the fp32 accumulator, and the scales are undone exactly in the epilogue.  Half the matrix-core
+// work of bf16x6 at fp32-class accuracy (tests/test_gemm_f16_gpu.py: fp64-referenced errors).
+//
+// Operands: activations and gradients are read AS fp32 and split in registers here -- no piece
+// tensors are written or read in HBM (fp32 = 4 B per element; three bf16 pieces were 6) -- and
+// their scale comes from the max |x| partials written by their producer (LayerNorm, attention,
+// this kernel's own epilogues) or by hx_amax_rows.  Weights are split once per forward
+// (split_weight_f16_many_k) into the "P2" piece layout: element (r, p, k) at r 2K + (k / 16) 32 +
+// p 16 + k % 16, so one 16-deep k step of a row is 64 contiguous bytes holding both pieces.
+//
+// Kernels (reference sites: hetseq/bert_modeling.py:334-336 Q/K/V, :383 attention output, :409 +
+// :166-168 FFN-up with bias_gelu, :419 FFN-down, :538-547 MLM decoder, and their backward):
+//  * gemm_f16_k   C[M][N] (+)= A[M][K] . B[N][K]^T  (forward: A = activations, B = weight pieces;
+//    data gradient: A = output gradient, B = pieces of W^T).  One workgroup per BM x BN tile,
+//    tiles dealt XCD-aware; LDS-DMA (buffer_load ... lds) of fp32 A and fp16 B stages, 16 deep,
+//    three stages with the next-next stage's DMA pieces issued between the MFMA passes; each
+//    wave reads its A fragment as fp32 (two ds_read_b128), splits it in registers and runs
+//    3 x MB x NB v_mfma_f32_32x32x16_f16.  Epilogues after a 4 x 4 DPP quad transpose (16-B
+//    stores): C (+)= s acc (+ bias); FFN-up bias + GELU (C = gelu'(u), P = gelu(u) fp32 + its
+//    per-tile max |.|); FFN-down data gradient with the GELU backward (P = t fp32, its max |.|,
+//    per-wave column partials of t = the FFN-up bias gradient).  Split-K slabs for deep
+//    reductions with few tiles (the MLM decoder's data gradient).
+//  * wgrad_f16_k  dW[M][N] = dY[T][M]^T . X[T][N] (tokens = reduction): both operands fp32,
+//    16 tokens per stage loaded into registers, split, and written as fp16 piece tiles into an
+//    XOR-swizzled LDS image read with the transposing ds_read_b64_tr_b16; token-range split-K
+//    over the CUs, partial slabs summed by one vectorised pass.
+#include <algorithm>
+
+#include "hx_gemm.h"
+#include "hx_launch.h"
+
+namespace {
+
+using namespace hx::g;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+__device__ __forceinline__ f32x16 mfma16(const f16x8& a, const f16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+struct F16Args {
+  const float* A;
+  int64_t lda;
+  const float* a_amax;
+  int na;
+  const uint16_t* B;
+  int64_t ldb;
+  const float* b_amax;
+  int nb;
+  float* C;
+  int64_t ldc;
+  int M, N, K, beta;
+  const float* bias;
+  const float* aux;
+  int64_t ldaux;
+  float* P;
+  int64_t ldp;
+  float* colpart;
+  float* amax_out;   // EPI 1 / 2: one max |P| per output tile
+  int dmode;         // EPI 1: C gets gelu'(u) (1) or u (0); EPI 2: aux holds gelu'(u) (1) or u (0)
+  int ks;            // split-K slabs (EPI 0 only): slab z reduces k steps [z, z + 1) K / ks into C + z c_zs
+  int64_t c_zs;
+};
+
+template <int BM, int BN, int WM, int WN, int EPI, int OCC>
+__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F16Args g) {
+  constexpr int NWM = BM / WM, NW = NWM * (BN / WN), NT = NW * 64;
+  constexpr int MB = WM / 32, NB = WN / 32;
+  constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64, STAGE = A_BYTES + B_BYTES;
+  constexpr int KA = BM / 16, KB = BN / 16, PTOT = KA + KB;   // 1-KiB DMA pieces per stage
+  constexpr int JHI = (PTOT + NW - 1) / NW, JLO = PTOT / NW;
+  static_assert(JLO >= 1, "fewer DMA pieces than waves");
+  static_assert(BM % 16 == 0 && BN % 16 == 0 && WM % 32 == 0 && WN % 32 == 0, "tile shape");
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  __shared__ float red[NW];
+
+  const int TM = (g.M + BM - 1) / BM, TN = g.N / BN, total = TM * TN;
+  const int per = (total * g.ks + 7) / 8;
+  const int work0 = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (work0 >= total * g.ks) return;   // uniform per workgroup
+  const int z = work0 / total, work = work0 - z * total;
+  const int nt = work % TN, mt = work / TN;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int nit = g.K / 16 / g.ks, it0 = z * nit;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w % NWM, wn = w / NWM, h = lane >> 5, l32 = lane & 31;
+  const int wv = __builtin_amdgcn_readfirstlane(w);
+
+  const int mrows = min(BM, g.M - m0);
+  const u32x4 ra = rsrc_of(g.A + (int64_t)m0 * g.lda, (uint32_t)((int64_t)mrows * g.lda * 4));
+  const u32x4 rb = rsrc_of(g.B + (int64_t)n0 * g.ldb, (uint32_t)((int64_t)BN * g.ldb * 2));
+
+  // this wave's DMA pieces q = wv + NW j of a stage: [A pieces (16 rows of fp32) | B pieces]
+  uint32_t voff[JHI];
+  int dsto[JHI];
+  bool isa[JHI];
+  int rl, ch;
+  img_lane_src(lane, rl, ch);
+#pragma unroll
+  for (int j = 0; j < JHI; ++j) {
+    const int q = wv + NW * j;
+    isa[j] = q < KA;
+    if (q < KA) voff[j] = (uint32_t)(((int64_t)(q * 16 + rl) * g.lda + 4 * ch) * 4);
+    else voff[j] = (uint32_t)(((int64_t)((q - KA) * 16 + rl) * g.ldb + 8 * ch) * 2);
+    dsto[j] = 1024 * q;
+  }
+  const int cnt = (PTOT - wv + NW - 1) / NW;   // JHI or JLO
+  const uint32_t lds0 = (uint32_t)(size_t)(lds_void*)lds;
+  auto dma_one = [&](int it, int buf, int j) {
+    const uint32_t st = lds0 + buf * STAGE;
+    const uint32_t ko = (uint32_t)(it0 + it) * (isa[j] ? 64u : 64u);   // 16 fp32 / 32 fp16 per row and k step
+    dma16(isa[j] ? ra : rb, st + dsto[j], voff[j] + ko);
+  };
+  auto dma = [&](int it, int buf) {
+#pragma unroll
+    for (int j = 0; j < JHI; ++j)
+      if (j < JLO || j < cnt) dma_one(it, buf, j);
+  };
+  auto wait_stage = [&]() {   // all but this wave's youngest stage of DMAs landed
+    if constexpr (JHI == JLO) {
+      dma_wait<JLO>();
+    } else {
+      if (cnt == JHI) dma_wait<JHI>();
+      else dma_wait<JLO>();
+    }
+  };
+
+  // fragment byte offsets in a stage (fixed for the k loop)
+  int offa[MB][2], offb[NB][2];
+#pragma unroll
+  for (int a = 0; a < MB; ++a) {
+    offa[a][0] = img_off(wm * WM + 32 * a + l32, 2 * h);
+    offa[a][1] = img_off(wm * WM + 32 * a + l32, 2 * h + 1);
+  }
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    offb[b][0] = A_BYTES + img_off(wn * WN + 32 * b + l32, h);       // piece 0
+    offb[b][1] = A_BYTES + img_off(wn * WN + 32 * b + l32, 2 + h);   // piece 1
+  }
+
+  dma(0, 0);
+  if (nit > 1) dma(1, 1);
+  // operand scales (their loads over-wait the DMAs above: harmless)
+  const int Ea = f16_scale_exp(block_amax(g.a_amax, g.na, red));
+  const int Eb = f16_scale_exp(block_amax(g.b_amax, g.nb, red));
+  const float sa = ldexpf(1.f, Ea), ia = ldexpf(1.f, -Ea), ib = ldexpf(1.f, -Eb);
+  if (nit > 1) wait_stage();
+  else dma_wait<0>();
+  __syncthreads();
+
+  f32x16 acc[MB][NB];
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[a][b] = f32x16{0};
+
+  int cur = 0;
+  for (int it = 0; it < nit; ++it) {
+    const int nxt2 = cur == 0 ? 2 : cur - 1;
+    const char* st = lds + cur * STAGE;
+    f16x8 a0[MB], a1[MB], b0[NB], b1[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      b0[b] = *reinterpret_cast<const f16x8*>(st + offb[b][0]);
+      b1[b] = *reinterpret_cast<const f16x8*>(st + offb[b][1]);
+    }
+#pragma unroll
+    for (int a = 0; a < MB; ++a) {
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(st + offa[a][0]);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(st + offa[a][1]);
+      const f32x8 y = f32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]} * sa;
+      split2(y, a0[a], a1[a]);
+    }
+    const int dit = it + 2 < nit ? it + 2 : -1;
+    // pass q, then this wave's DMA pieces j = q, q + 3, ... of stage it + 2
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          acc[a][b] = mfma16(q == 2 ? a1[a] : a0[a], q == 1 ? b1[b] : b0[b], acc[a][b]);
+      if (dit >= 0) {
+#pragma unroll
+        for (int j = q; j < JHI; j += 3) {
+          if (j < JLO || j < cnt) {
+            __builtin_amdgcn_sched_barrier(0);
+            dma_one(dit, nxt2, j);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+      }
+    }
+    if (it + 2 < nit) wait_stage();
+    else dma_wait<0>();
+    __syncthreads();
+    cur = cur == 2 ? 0 : cur + 1;
+  }
+
+  // ---- epilogue: quad transpose, then lane (l32 & 3) owns row 8 gq + 4 h + (l32 & 3) of each
+  // 32 x 32 block and its columns (l32 & ~3) .. + 3; stores past M dropped by the descriptor
+  const int mrow = wm * WM + 4 * h + (l32 & 3), ncol = wn * WN + (l32 & ~3);
+  const hx::Buf cbuf(g.C + z * g.c_zs + (int64_t)m0 * g.ldc + n0, (uint32_t)((int64_t)mrows * g.ldc * 4));
+  auto coff = [&](int a, int b, int gq) { return (uint32_t)((mrow + 32 * a + 8 * gq) * g.ldc + ncol + 32 * b) * 4; };
+  auto tr = [&](int a, int b, int gq, float (&v)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = acc[a][b][4 * gq + i];
+    transpose4(v, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = v[i] * ia * ib;
+  };
+  float bias[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b) {
+    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (g.bias) t = *reinterpret_cast<const float4*>(g.bias + n0 + ncol + 32 * b);
+    bias[b][0] = t.x; bias[b][1] = t.y; bias[b][2] = t.z; bias[b][3] = t.w;
+  }
+  if constexpr (EPI == 0 || EPI == 3) {
+#pragma unroll
+    for (int a = 0; a < MB; ++a) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          float v[4];
+          tr(a, b, gq, v);
+          f32x4 o = {v[0] + bias[b][0], v[1] + bias[b][1], v[2] + bias[b][2], v[3] + bias[b][3]};
+          if constexpr (EPI == 3)
+            o += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(cbuf.r, coff(a, b, gq), 0, 0));
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), cbuf.r, coff(a, b, gq), 0, 0);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else {
+    const hx::Buf pbuf(g.P + (int64_t)m0 * g.ldp + n0, (uint32_t)((int64_t)mrows * g.ldp * 4));
+    const hx::Buf xbuf(EPI == 2 ? g.aux + (int64_t)m0 * g.ldaux + n0 : g.C, (uint32_t)((int64_t)mrows * g.ldaux * 4));
+    auto poff = [&](int a, int b, int gq) { return (uint32_t)((mrow + 32 * a + 8 * gq) * g.ldp + ncol + 32 * b) * 4; };
+    float csum[NB][4];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) csum[b][i] = 0.f;
+    float amx = 0.f;
+#pragma unroll
+    for (int a = 0; a < MB; ++a) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        f32x4 u[4];
+        if constexpr (EPI == 2) {
+#pragma unroll
+          for (int gq = 0; gq < 4; ++gq)
+            u[gq] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                  xbuf.r, (uint32_t)((mrow + 32 * a + 8 * gq) * g.ldaux + ncol + 32 * b) * 4,
+                                                  0, 0));
+        }
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          float v[4];
+          tr(a, b, gq, v);
+          const bool in = mrow + 32 * a + 8 * gq < mrows;
+          f32x4 o;
+          if constexpr (EPI == 1) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) v[i] += bias[b][i];
+            f32x4 c;
+            if (g.dmode) {
+              // gelu(u) and gelu'(u) from ONE erf (hx::gelu_f / hx::gelu_grad_f bit for bit)
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const float e = erff(v[i] * (1.0f / 1.41421f));
+                c[i] = 0.5f * (1.0f + e) + hx::gelu_pdf_f(v[i]);
+                o[i] = v[i] * 0.5f * (1.0f + e);
+              }
+            } else {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                c[i] = v[i];
+                o[i] = hx::gelu_f(v[i]);
+              }
+            }
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, c), cbuf.r, coff(a, b, gq), 0, 0);
+          } else {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              o[i] = g.dmode ? v[i] * u[gq][i] : v[i] * hx::gelu_grad_f(u[gq][i] + bias[b][i]);
+              csum[b][i] += in ? o[i] : 0.f;
+            }
+          }
+          if (in) amx = fmaxf(amx, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), pbuf.r, poff(a, b, gq), 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if constexpr (EPI == 2) {
+      if (g.colpart) {
+        // sum over the 4 rows of a quad and the two 32-lane halves; lanes (l32 & 3) == 0, h == 0
+        // then hold this wave's 4-column sums -> partial row (mt * NWM + wm)
+        float* row = g.colpart + (int64_t)(mt * NWM + wm) * g.N + n0 + wn * WN;
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            float t = csum[b][i];
+            t += qx1(t);
+            t += qx2(t);
+            t += __shfl_xor(t, 32, 64);
+            csum[b][i] = t;
+          }
+        if ((l32 & 3) == 0 && h == 0) {
+#pragma unroll
+          for (int b = 0; b < NB; ++b)
+            *reinterpret_cast<float4*>(row + 32 * b + l32) = make_float4(csum[b][0], csum[b][1], csum[b][2], csum[b][3]);
+        }
+      }
+    }
+    if (g.amax_out) {
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) amx = fmaxf(amx, __shfl_xor(amx, o, 64));
+      __syncthreads();
+      if (lane == 0) red[w] = amx;
+      __syncthreads();
+      if (tid == 0) {
+        float m = red[0];
+        for (int i = 1; i < NW; ++i) m = fmaxf(m, red[i]);
+        g.amax_out[work] = m;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- configurations
+// cfg 0: 256 x 192, 8 waves of 32 x 192 (each A fragment split by ONE wave)      -- M >= 8192
+// cfg 1: 256 x 192, 8 waves (4 x 2) of 64 x 96 (A fragments split by two waves, fewer B reads)
+// cfg 2: 128 x 96, 4 waves of 32 x 96                                            -- M < 8192
+// cfg 3: 64 x 64, 4 waves (2 x 2) of 32 x 32                                     -- tiny M
+constexpr int kCfgs = 4;
+int cfg_bm(int c) { return c <= 1 ? 256 : c == 2 ? 128 : 64; }
+int cfg_bn(int c) { return c <= 1 ? 192 : c == 2 ? 96 : 64; }
+int cfg_nwm(int c) { return c == 0 ? 8 : c == 1 ? 4 : c == 2 ? 4 : 2; }
+
+template <int BM, int BN, int WM, int WN, int EPI>
+void launch_one(const F16Args& a, hipStream_t s) {
+  constexpr int NT = (BM / WM) * (BN / WN) * 64;
+  const int total = ((a.M + BM - 1) / BM) * (a.N / BN) * a.ks;
+  const int per = (total + 7) / 8;
+  const size_t smem = (size_t)3 * (BM + BN) * 64;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_f16_k<BM, BN, WM, WN, EPI, 1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    attr = true;
+  }
+  gemm_f16_k<BM, BN, WM, WN, EPI, 1><<<8 * per, NT, smem, s>>>(a);
+}
+
+template <int EPI>
+void launch_cfg(int cfg, const F16Args& a, hipStream_t s) {
+  if (cfg == 0) launch_one<256, 192, 32, 192, EPI>(a, s);
+  else if (cfg == 1) launch_one<256, 192, 64, 96, EPI>(a, s);
+  else if (cfg == 2) launch_one<128, 96, 32, 96, EPI>(a, s);
+  else launch_one<64, 64, 32, 32, EPI>(a, s);
+}
+
+// ---------------------------------------------------------------- weight gradient (tokens = reduction)
+// LDS image of a [16 tokens][W columns] fp16 tile: 8-row x 32-column subtiles of 512 B, XOR-swizzled
+// 16-B chunks, odd subtiles with the rows of each pair swapped (conflict-free 16-B stores and
+// transposed ds_read_b64_tr_b16 reads)
+template <int W>
+__device__ __forceinline__ int toff(int row, int ch) {
+  return (row >> 3) * (16 * W) + 512 * (ch >> 2) + 64 * ((row & 7) ^ ((ch >> 2) & 1)) +
+         16 * ((ch & 3) ^ ((row >> 2) & 3));
+}
+template <int W>
+__device__ __forceinline__ void tr_base(int lane, int (&lo)[2], int (&hi)[2]) {
+  const int gq = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int row = 8 * (gq >> 1) + q, ch = 2 * (gq & 1) + (p >> 1);
+  lo[0] = toff<W>(row, ch) + 8 * (p & 1);
+  hi[0] = toff<W>(row + 4, ch) + 8 * (p & 1);
+  lo[1] = toff<W>(row, ch + 4) - 512 + 8 * (p & 1);
+  hi[1] = toff<W>(row + 4, ch + 4) - 512 + 8 * (p & 1);
+}
+// the k-major fragment (8 consecutive tokens of column c0 + lane & 31) of a [16][W] tile
+template <int W>
+__device__ __forceinline__ f16x8 tfrag(const char* tile, const int (&lo)[2], const int (&hi)[2], int c0, int odd) {
+  const int d = (c0 >> 5) * 512;
+  const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(tile + lo[odd] + d));
+  const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(tile + hi[odd] + d));
+  const v4i16 v[2] = {a, b};
+  return *reinterpret_cast<const f16x8*>(v);
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const float* __restrict__ A, int lda,
+                                                                         const float* __restrict__ a_amax, int na,
+                                                                         const float* __restrict__ B, int ldb,
+                                                                         const float* __restrict__ b_amax, int nb,
+                                                                         float* __restrict__ out, int M, int N, int T,
+                                                                         int kchunk, int nsplit, int mvalid) {
+  constexpr int NWM = BM / WM, NW = NWM * (BN / WN), NT = NW * 64;
+  constexpr int MB = WM / 32, NB = WN / 32;
+  constexpr int BKT = 16;
+  constexpr int CA = BKT * BM / 8 / NT, CB = BKT * BN / 8 / NT;   // 8-column chunks per thread
+  static_assert(CA >= 1 && CB >= 1 && BKT * BM / 8 % NT == 0 && BKT * BN / 8 % NT == 0, "tile / thread mismatch");
+  static_assert(WM % 64 == 0 && WN % 64 == 0, "subtile parity of fragment a is a & 1");
+  constexpr int A_T = BKT * BM * 2, B_T = BKT * BN * 2;   // one fp16 piece tile
+  constexpr int STAGE = 2 * (A_T + B_T);
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  __shared__ float red[NW];
+
+  const int total = (M / BM) * (N / BN) * nsplit;
+  const int per = (total + 7) / 8;
+  const int work = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (work >= total) return;   // uniform per workgroup
+  const int TM = M / BM, TN = N / BN;
+  const bool mord = M < N;   // output-row tiles fastest when there are fewer of them
+  const int nt = mord ? (work / TM) % TN : work % TN;
+  const int mt = mord ? work % TM : (work / TN) % TM;
+  const int sp = work / (TN * TM);
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int t0 = sp * kchunk, t1 = min(T, t0 + kchunk);
+  const int nit = (t1 - t0 + BKT - 1) / BKT;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w % NWM, wn = w / NWM;
+
+  const float sa = ldexpf(1.f, f16_scale_exp(block_amax(a_amax, na, red)));
+  const float sb = ldexpf(1.f, f16_scale_exp(block_amax(b_amax, nb, red)));
+  const float inv = (1.f / sa) * (1.f / sb);
+
+  const hx::Buf abuf(A + (int64_t)t0 * lda, (uint32_t)((int64_t)(t1 - t0) * lda * 4));
+  const hx::Buf bbuf(B + (int64_t)t0 * ldb, (uint32_t)((int64_t)(t1 - t0) * ldb * 4));
+  uint32_t va[CA], vb[CB];
+  int sa_[CA], sb_[CB];
+#pragma unroll
+  for (int i = 0; i < CA; ++i) {
+    const int e = tid + i * NT, row = e / (BM / 8), c = e % (BM / 8);
+    va[i] = (uint32_t)(row * lda + m0 + 8 * c) * 4;
+    sa_[i] = toff<BM>(row, c);
+  }
+#pragma unroll
+  for (int i = 0; i < CB; ++i) {
+    const int e = tid + i * NT, row = e / (BN / 8), c = e % (BN / 8);
+    vb[i] = (uint32_t)(row * ldb + n0 + 8 * c) * 4;
+    sb_[i] = toff<BN>(row, c);
+  }
+  int alo[2], ahi[2], blo[2], bhi[2];
+  tr_base<BM>(lane, alo, ahi);
+  tr_base<BN>(lane, blo, bhi);
+
+  f32x4 rA[CA][2], rB[CB][2];
+  auto load = [&](int it) {
+    const uint32_t soa = (uint32_t)it * BKT * lda * 4, sob = (uint32_t)it * BKT * ldb * 4;
+#pragma unroll
+    for (int i = 0; i < CA; ++i)
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+        rA[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(abuf.r, va[i] + 16 * k, soa, 0));
+#pragma unroll
+    for (int i = 0; i < CB; ++i)
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+        rB[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(bbuf.r, vb[i] + 16 * k, sob, 0));
+  };
+  auto store = [&](int buf) {
+    char* st = lds + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < CA; ++i) {
+      const f32x8 y = f32x8{rA[i][0][0], rA[i][0][1], rA[i][0][2], rA[i][0][3],
+                            rA[i][1][0], rA[i][1][1], rA[i][1][2], rA[i][1][3]} * sa;
+      f16x8 h0, h1;
+      split2(y, h0, h1);
+      *reinterpret_cast<f16x8*>(st + sa_[i]) = h0;
+      *reinterpret_cast<f16x8*>(st + A_T + sa_[i]) = h1;
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const f32x8 y = f32x8{rB[i][0][0], rB[i][0][1], rB[i][0][2], rB[i][0][3],
+                            rB[i][1][0], rB[i][1][1], rB[i][1][2], rB[i][1][3]} * sb;
+      f16x8 h0, h1;
+      split2(y, h0, h1);
+      *reinterpret_cast<f16x8*>(st + 2 * A_T + sb_[i]) = h0;
+      *reinterpret_cast<f16x8*>(st + 2 * A_T + B_T + sb_[i]) = h1;
+    }
+  };
+
+  f32x16 acc[MB][NB];
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[a][b] = f32x16{0};
+
+  auto mma = [&](int buf) {
+    const char* st = lds + buf * STAGE;
+    f16x8 a0[MB], a1[MB], b0[NB], b1[NB];
+#pragma unroll
+    for (int a = 0; a < MB; ++a) {
+      a0[a] = tfrag<BM>(st, alo, ahi, wm * WM + 32 * a, a & 1);
+      a1[a] = tfrag<BM>(st + A_T, alo, ahi, wm * WM + 32 * a, a & 1);
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      b0[b] = tfrag<BN>(st + 2 * A_T, blo, bhi, wn * WN + 32 * b, b & 1);
+      b1[b] = tfrag<BN>(st + 2 * A_T + B_T, blo, bhi, wn * WN + 32 * b, b & 1);
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) acc[a][b] = mfma16(q == 2 ? a1[a] : a0[a], q == 1 ? b1[b] : b0[b], acc[a][b]);
+  };
+
+  // one register stage: step it + 1 is loaded while step it runs on the matrix cores, then split
+  // and written to the other LDS buffer (last read before the previous barrier)
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int it = 0; it < nit; ++it) {
+    const int cur = it & 1;
+    if (it + 1 < nit) load(it + 1);
+    mma(cur);
+    if (it + 1 < nit) store(cur ^ 1);
+    __syncthreads();
+  }
+
+  float* o = out + (nsplit > 1 ? (int64_t)sp * M * N : 0);
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int n = n0 + wn * WN + 32 * b + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * WM + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m < mvalid) o[(int64_t)m * N + n] = acc[a][b][r] * inv;   // rows past mvalid: padding
+      }
+    }
+}
+
+__global__ __launch_bounds__(256) void slab_sum_k(const float4* __restrict__ ws, float4* __restrict__ out, int64_t n4,
+                                                  int64_t slab4, int nsplit) {
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 s = ws[i];
+    for (int k = 1; k < nsplit; ++k) {
+      const float4 v = ws[(int64_t)k * slab4 + i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    out[i] = s;
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+void wgrad_launch(const float* A, int lda, const float* aam, int na, const float* B, int ldb, const float* bam, int nb,
+                  float* out, float* ws, int M, int N, int T, int nsplit, int mvalid, hipStream_t s) {
+  constexpr int NT = (BM / WM) * (BN / WN) * 64;
+  const int kchunk = ((T + nsplit - 1) / nsplit + 15) / 16 * 16;
+  nsplit = (T + kchunk - 1) / kchunk;
+  const int total = (M / BM) * (N / BN) * nsplit;
+  const int per = (total + 7) / 8;
+  const size_t smem = (size_t)2 * 2 * 16 * (BM + BN) * 2;
+  wgrad_f16_k<BM, BN, WM, WN><<<8 * per, NT, smem, s>>>(A, lda, aam, na, B, ldb, bam, nb, nsplit > 1 ? ws : out, M, N,
+                                                        T, kchunk, nsplit, nsplit > 1 ? M : mvalid);
+  if (nsplit > 1) {
+    const int64_t n4 = (int64_t)mvalid * N / 4, slab4 = (int64_t)M * N / 4;
+    const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+    slab_sum_k<<<blocks, 256, 0, s>>>(reinterpret_cast<const float4*>(ws), reinterpret_cast<float4*>(out), n4, slab4,
+                                      nsplit);
+  }
+}
+
+// ---------------------------------------------------------------- max |x| partials, weight pieces
+// max |x| over a [rows][cols] fp32 matrix (row stride ld, cols % 4 == 0): one partial per block
+__global__ __launch_bounds__(256) void amax_rows_k(const float* __restrict__ x, int64_t rows, int cols, int64_t ld,
+                                                   float* __restrict__ part) {
+  __shared__ float red[4];
+  const int c4 = cols / 4;
+  const int64_t n4 = rows * c4;
+  float m = 0.f;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / c4;
+    const int c = (int)(i - r * c4);
+    const float4 v = *reinterpret_cast<const float4*>(x + r * ld + 4 * c);
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// HX_WAMAX_PARTS partials per weight of a batch: block b -> weight b / P, slice b % P
+constexpr int kWParts = 32;
+__global__ __launch_bounds__(256) void amax_weights_k(HxWeightBatch d, float* __restrict__ part) {
+  __shared__ float red[4];
+  const int i = blockIdx.x / kWParts, j = blockIdx.x % kWParts;
+  const int64_t n4 = (int64_t)d.N[i] * d.K[i] / 4;
+  const float4* x = reinterpret_cast<const float4*>(d.W[i]);
+  float m = 0.f;
+  for (int64_t k = (int64_t)j * 256 + threadIdx.x; k < n4; k += (int64_t)kWParts * 256) {
+    const float4 v = x[k];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+// element offset of (row, piece p, column c) in the P2 layout [rows][C / 16][2][16]
+__device__ __forceinline__ int64_t p2_off(int64_t row, int p, int c, int C) {
+  return row * 2 * C + (c >> 4) * 32 + p * 16 + (c & 15);
+}
+
+// both P2 piece layouts of every weight of a batch, one 64 x 64 tile per workgroup:
+//   wf[n] = pieces of W[n][:] (forward B operand), wt[k] = pieces of W[:][k] (data gradient)
+__global__ __launch_bounds__(256) void split_weight_f16_k(HxWeightBatch d, const float* __restrict__ part) {
+  __shared__ uint16_t tile[2][64][66];
+  __shared__ float red[4];
+  const int blk = blockIdx.x;
+  int i = 0;
+  while (i + 1 < d.n && blk >= d.start[i + 1]) ++i;   // uniform per workgroup
+  const float s = ldexpf(1.f, f16_scale_exp(block_amax(part + i * kWParts, kWParts, red)));
+  const int N = d.N[i], K = d.K[i];
+  const int tk = K / 64, loc = blk - d.start[i];
+  const int k0 = (loc % tk) * 64, n0 = (loc / tk) * 64;
+  const float* W = d.W[i];
+  const int t = threadIdx.x, c4 = (t & 15) * 4;
+#pragma unroll
+  for (int r4 = 0; r4 < 4; ++r4) {
+    const int r = (t >> 4) + 16 * r4;
+    const float4 v = *reinterpret_cast<const float4*>(W + (int64_t)(n0 + r) * K + k0 + c4);
+    const float e[4] = {v.x * s, v.y * s, v.z * s, v.w * s};
+    uint16_t q0[4], q1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const _Float16 h0 = (_Float16)e[j];
+      const _Float16 h1 = (_Float16)(e[j] - (float)h0);
+      q0[j] = __builtin_bit_cast(uint16_t, h0);
+      q1[j] = __builtin_bit_cast(uint16_t, h1);
+      tile[0][r][c4 + j] = q0[j];
+      tile[1][r][c4 + j] = q1[j];
+    }
+    *reinterpret_cast<uint2*>(d.wf[i] + p2_off(n0 + r, 0, k0 + c4, K)) =
+        make_uint2(q0[0] | ((uint32_t)q0[1] << 16), q0[2] | ((uint32_t)q0[3] << 16));
+    *reinterpret_cast<uint2*>(d.wf[i] + p2_off(n0 + r, 1, k0 + c4, K)) =
+        make_uint2(q1[0] | ((uint32_t)q1[1] << 16), q1[2] | ((uint32_t)q1[3] << 16));
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r4 = 0; r4 < 4; ++r4) {
+    const int kk = (t >> 4) + 16 * r4;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      uint16_t q[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) q[j] = tile[p][c4 + j][kk];
+      *reinterpret_cast<uint2*>(d.wt[i] + p2_off(k0 + kk, p, n0 + c4, N)) =
+          make_uint2(q[0] | ((uint32_t)q[1] << 16), q[2] | ((uint32_t)q[3] << 16));
+    }
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- host API (hx_launch.h)
+int hx_gemm_f16_plan(int M, int N, int K) {
+  (void)K;
+  if (const char* e = getenv("HX_GEMM_F16_CFG")) {
+    const int c = atoi(e);
+    if (c >= 0 && c < kCfgs && N % cfg_bn(c) == 0) return c;
+  }
+  if (M >= 8192 && N % 192 == 0) return 0;
+  if (M >= 1024 && N % 96 == 0) return 2;
+  if (N % 64 == 0) return 3;
+  return -1;
+}
+
+int hx_gemm_f16_tiles(int M, int N, int cfg) {
+  if (cfg < 0 || cfg >= kCfgs) return 0;
+  return (M + cfg_bm(cfg) - 1) / cfg_bm(cfg) * (N / cfg_bn(cfg));
+}
+
+int hx_gemm_f16_colpart_rows(int M, int cfg) {
+  if (cfg < 0 || cfg >= kCfgs) return 0;
+  return (M + cfg_bm(cfg) - 1) / cfg_bm(cfg) * cfg_nwm(cfg);
+}
+
+int hx_gemm_f16_ks(int M, int N, int K, int cfg) {
+  if (cfg < 0) return 1;
+  const int tiles = hx_gemm_f16_tiles(M, N, cfg), slots = hx_cu_slots();
+  if (tiles * 2 > slots || K < 8192) return 1;
+  int best = 1;
+  for (int ks = 2; ks <= 16; ++ks)
+    if (tiles * ks <= slots && K % (16 * ks) == 0 && K / ks >= 2048) best = ks;
+  return best;
+}
+
+int hx_gemm_f16(const HxGemmF16& p, int cfg, hipStream_t s) {
+  if (cfg < 0 || cfg >= kCfgs || p.M < 1 || p.N % cfg_bn(cfg) || p.K % 16 || p.lda % 4 || p.ldb != 2 * (int64_t)p.K)
+    return -1;
+  const int ks = p.ks < 1 ? 1 : p.ks;
+  if (p.K % (16 * ks) || (ks > 1 && (p.beta || p.kind || p.bias || p.c_zs < (int64_t)(p.M - 1) * p.ldc + p.N)))
+    return -1;
+  if (p.kind < 0 || p.kind > 2 || (p.kind && (!p.P || p.beta || p.ldp % 4)) || (p.kind == 2 && !p.aux)) return -1;
+  F16Args a;
+  a.A = p.A;
+  a.lda = p.lda;
+  a.a_amax = p.a_amax;
+  a.na = p.na;
+  a.B = p.B;
+  a.ldb = p.ldb;
+  a.b_amax = p.b_amax;
+  a.nb = p.nb;
+  a.C = p.C;
+  a.ldc = p.ldc;
+  a.M = p.M;
+  a.N = p.N;
+  a.K = p.K;
+  a.beta = p.beta;
+  a.bias = p.bias;
+  a.aux = p.aux;
+  a.ldaux = p.ldaux;
+  a.P = p.P;
+  a.ldp = p.ldp;
+  a.colpart = p.colpart;
+  a.amax_out = p.amax_out;
+  a.dmode = p.dmode;
+  a.ks = ks;
+  a.c_zs = p.c_zs;
+  if (p.kind == 0 && !p.beta) launch_cfg<0>(cfg, a, s);
+  else if (p.kind == 0) launch_cfg<3>(cfg, a, s);
+  else if (p.kind == 1) launch_cfg<1>(cfg, a, s);
+  else launch_cfg<2>(cfg, a, s);
+  return 0;
+}
+
+void hx_wgrad_f16_plan(int M, int N, int T, int* cfg, int* nsplit) {
+  const int t256 = (M % 256 == 0 && N % 256 == 0) ? (M / 256) * (N / 256) : 0;
+  const int c = (t256 >= 24 && t256 <= 512) ? 1 : 0;
+  const int tiles = c ? t256 : (M / 128) * (N / 128);
+  const int slots = (c ? 1 : 2) * hx_cu_slots();
+  int sp = std::max(1, slots / std::max(1, tiles));
+  sp = std::min(sp, std::max(1, T / 256));
+  if (const char* e = getenv("HX_WGRAD_F16")) {
+    int ec = -1, es = -1;
+    if (sscanf(e, "%d:%d", &ec, &es) == 2 && (ec == 0 || ec == 1) && es >= 1) {
+      if (ec == 0 || t256) {
+        *cfg = ec;
+        *nsplit = std::min(es, std::max(1, T / 16));
+        return;
+      }
+    }
+  }
+  *cfg = c;
+  *nsplit = sp;
+}
+
+int hx_wgrad_f16(const float* dy, int ldy, const float* dy_amax, int na, const float* x, int ldx, const float* x_amax,
+                 int nb, float* out, float* ws, int M, int N, int T, int cfg, int nsplit, int mvalid, hipStream_t s) {
+  if (ldy % 4 || ldx % 4 || M % 128 || N % 128 || T < 1) return -1;
+  if (cfg == 1) {
+    if (M % 256 || N % 256) return -1;
+    wgrad_launch<256, 256, 128, 64>(dy, ldy, dy_amax, na, x, ldx, x_amax, nb, out, ws, M, N, T, nsplit, mvalid, s);
+  } else {
+    wgrad_launch<128, 128, 64, 64>(dy, ldy, dy_amax, na, x, ldx, x_amax, nb, out, ws, M, N, T, nsplit, mvalid, s);
+  }
+  return 0;
+}
+
+int hx_amax_rows_parts(int64_t rows, int cols) {
+  const int64_t n4 = rows * (cols / 4);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(512, (n4 + 4095) / 4096));
+}
+
+void hx_amax_rows(const float* x, int64_t rows, int cols, int64_t ld, float* part, int nparts, hipStream_t s) {
+  amax_rows_k<<<nparts, 256, 0, s>>>(x, rows, cols, ld, part);
+}
+
+int hx_weight_f16_parts() { return kWParts; }
+
+void hx_split_weight_f16(const HxWeightBatch& d, float* part, hipStream_t s) {
+  if (d.n < 1) return;
+  amax_weights_k<<<d.n * kWParts, 256, 0, s>>>(d, part);
+  split_weight_f16_k<<<d.start[d.n], 256, 0, s>>>(d, part);
+}

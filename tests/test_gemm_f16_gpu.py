@@ -1,0 +1,149 @@
+"""fp16x3 GEMMs (csrc/kernels/gemm_f16.hip) against fp64 references.
+
+Error measure per output element: |C - C64| / (|A| |B|^T) -- the error relative to the sum of
+the absolute product terms, the bound an fp32 dot product's rounding obeys.  fp16x3 keeps 22
+significant bits of each operand and drops only the h1 h1 term (2^-22 relative), so its error is
+of the order of fp32 accumulation rounding; the tests require it within a small factor of the
+native fp32 GEMM's own error on the same data, and below an absolute fp32-class bound.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def C():
+    from hetseq_9cme_amd.ops._ext import C as _C
+    return _C()
+
+
+def _rel_err(out, ref64, a, b):
+    """max over elements of |out - ref| / (|a| |b|^T)."""
+    den = a.abs().double() @ b.abs().double().t()
+    err = (out.double() - ref64).abs() / den.clamp_min(1e-300)
+    return err.max().item()
+
+
+def _native_err(a, b, ref64):
+    torch.backends.cuda.matmul.allow_tf32 = False
+    return _rel_err(torch.mm(a, b.t()), ref64, a, b)
+
+
+def _pieces(W):
+    wf, wt, parts = C().split_weight_f16([W.contiguous()])[0]
+    return wf, wt, parts
+
+
+@pytest.mark.parametrize('M,N,K,sa', [(16384, 768, 768, 1.0), (16384, 2304, 768, 3e-2), (16384, 3072, 768, 1.0),
+                                      (16384, 768, 3072, 5e-3), (4096 + 37, 768, 768, 1.0), (1000, 768, 768, 1e-8),
+                                      (2560, 768, 768, 1e8), (100, 128, 256, 1.0)])
+def test_gemm_f16_forward(dev, M, N, K, sa):
+    g = torch.Generator(device=dev).manual_seed(M + N + K)
+    a = torch.randn(M, K, device=dev, generator=g) * sa
+    W = torch.randn(N, K, device=dev, generator=g) * 0.02
+    wf, wt, parts = _pieces(W)
+    out = C().gemm_f16(a, C().amax_rows(a), wf, parts)
+    ref = a.double() @ W.double().t()
+    e16 = _rel_err(out, ref, a, W)
+    e32 = _native_err(a, W, ref)
+    print('fwd M{} N{} K{} scale {:g}: fp16x3 {:.3g} native fp32 {:.3g}'.format(M, N, K, sa, e16, e32))
+    assert e16 < 4e-6 and e16 < 4 * e32 + 1e-7
+
+
+@pytest.mark.parametrize('M,N,K', [(16384, 768, 768), (16384, 768, 3072), (4096, 3072, 768), (512, 2304, 768)])
+def test_gemm_f16_dgrad_beta_bias(dev, M, N, K):
+    """dx = dy W (+ acc): the data-gradient operand wt = pieces of W^T; beta accumulates, bias adds."""
+    g = torch.Generator(device=dev).manual_seed(7 * M + N)
+    dy = torch.randn(M, N, device=dev, generator=g) * 1e-5
+    W = torch.randn(N, K, device=dev, generator=g) * 0.02
+    wf, wt, parts = _pieces(W)
+    acc = torch.randn(M, K, device=dev, generator=g) * 1e-5
+    ref = acc.double() + dy.double() @ W.double()
+    out = acc.clone()
+    C().gemm_f16(dy, C().amax_rows(dy), wt, parts, out=out, beta=True)
+    den = (dy.abs().double() @ W.abs().double()) + acc.abs().double()
+    e = ((out.double() - ref).abs() / den).max().item()
+    assert e < 4e-6, e
+    bias = torch.randn(K, device=dev, generator=g)
+    out2 = C().gemm_f16(dy, C().amax_rows(dy), wt, parts, bias=bias)
+    ref2 = dy.double() @ W.double() + bias.double()
+    den2 = (dy.abs().double() @ W.abs().double()) + bias.abs().double()
+    assert ((out2.double() - ref2).abs() / den2).max().item() < 4e-6
+
+
+def test_gemm_f16_gelu_epilogues(dev):
+    """FFN up (bias + GELU: C = gelu'(u), P = gelu(u), per-tile max |P|) and the FFN-down data
+    gradient with the GELU backward (t = acc * gelu'(u), column sums = d bias, max |t|)."""
+    from hetseq_9cme_amd.ops.fused import gelu_ref
+    g = torch.Generator(device=dev).manual_seed(11)
+    M, H, I = 16384 + 64, 768, 3072
+    x = torch.randn(M, H, device=dev, generator=g)
+    W1 = torch.randn(I, H, device=dev, generator=g) * 0.02
+    b1 = torch.randn(I, device=dev, generator=g) * 0.1
+    w1f, w1t, p1 = _pieces(W1)
+    d, h, hmax = C().gemm_f16_gelu(x, C().amax_rows(x), w1f, p1, b1, 1)
+    u64 = x.double() @ W1.double().t() + b1.double()
+    u = u64.float()
+    h64 = gelu_ref(u64)
+    den = x.abs().double() @ W1.abs().double().t() + b1.abs().double()
+    assert ((h.double() - h64).abs() / den).max().item() < 1e-5
+    ug = u.clone().requires_grad_(True)
+    gelu_ref(ug).sum().backward()
+    torch.testing.assert_close(d, ug.grad, rtol=2e-5, atol=2e-5)
+    assert hmax.max().item() == h.abs().max().item()
+    # backward: t = (dy W2) * gelu'(u)
+    W2 = torch.randn(H, I, device=dev, generator=g) * 0.02
+    w2f, w2t, p2 = _pieces(W2)
+    dy = torch.randn(M, H, device=dev, generator=g) * 1e-4
+    t, tmax, db = C().gemm_f16_dgelu(dy, C().amax_rows(dy), w2t, p2, d, None, None, 1)
+    dh64 = dy.double() @ W2.double()
+    t64 = dh64 * d.double()
+    den = (dy.abs().double() @ W2.abs().double()) * d.abs().double()
+    assert ((t.double() - t64).abs() / den.clamp_min(1e-300)).max().item() < 1e-5
+    torch.testing.assert_close(db.double(), t64.sum(0), rtol=1e-4, atol=1e-9)
+    assert tmax.max().item() == t.abs().max().item()
+
+
+def test_gemm_f16_split_k(dev):
+    """The MLM decoder's data gradient shape: 40 output tiles over K = 30720 in split-K slabs."""
+    g = torch.Generator(device=dev).manual_seed(5)
+    M, N, K = 2560, 768, 30720
+    a = torch.randn(M, K, device=dev, generator=g) * 1e-3
+    W = torch.randn(N, K, device=dev, generator=g) * 0.02   # W^T of the decoder weight [K, N]
+    wf, wt, parts = _pieces(W)
+    ks = C().gemm_f16_ks(M, N, K, C().gemm_f16_plan(M, N, K))
+    assert ks > 1
+    out = C().gemm_f16(a, C().amax_rows(a), wf, parts, ks=0)
+    ref = a.double() @ W.double().t()
+    assert _rel_err(out, ref, a, W) < 4e-6
+
+
+@pytest.mark.parametrize('T,M,N,mvalid', [(16384, 2304, 768, 2304), (16384, 768, 3072, 768), (16384, 3072, 768, 3072),
+                                          (4096, 768, 768, 768), (2560, 30720, 768, 30522), (1000, 256, 384, 256)])
+def test_wgrad_f16(dev, T, M, N, mvalid):
+    g = torch.Generator(device=dev).manual_seed(T + M)
+    dy = torch.randn(T, M, device=dev, generator=g) * 1e-6
+    x = torch.randn(T, N, device=dev, generator=g)
+    out = torch.empty(mvalid, N, device=dev)
+    C().wgrad_f16(dy, C().amax_rows(dy), x, C().amax_rows(x), out)
+    ref = dy.double().t()[:mvalid] @ x.double()
+    den = dy.abs().double().t()[:mvalid] @ x.abs().double()
+    e16 = ((out.double() - ref).abs() / den).max().item()
+    e32 = ((torch.mm(dy.t()[:mvalid], x).double() - ref).abs() / den).max().item()
+    print('wgrad T{} M{} N{}: fp16x3 {:.3g} native fp32 {:.3g}'.format(T, M, N, e16, e32))
+    assert e16 < 4e-6 and e16 < 4 * e32 + 1e-7
+
+
+def test_f16_scale_extremes(dev):
+    """Operands far outside fp16's range (1e-30, 1e30) and an all-zero operand keep fp32 accuracy /
+    give exact zeros: the power-of-two scale comes from each tensor's max |x|."""
+    g = torch.Generator(device=dev).manual_seed(3)
+    W = torch.randn(768, 768, device=dev, generator=g) * 0.02
+    wf, wt, parts = _pieces(W)
+    for s in (1e-30, 1e30):
+        a = torch.randn(4096, 768, device=dev, generator=g) * s
+        out = C().gemm_f16(a, C().amax_rows(a), wf, parts)
+        ref = a.double() @ W.double().t()
+        assert _rel_err(out, ref, a, W) < 4e-6, s
+    z = torch.zeros(4096, 768, device=dev)
+    assert C().gemm_f16(z, C().amax_rows(z), wf, parts).abs().max().item() == 0.0

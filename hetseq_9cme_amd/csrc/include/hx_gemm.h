@@ -88,7 +88,7 @@ __device__ __forceinline__ int f16_scale_exp(float amax) {
   int e;
   (void)frexpf(amax, &e);   // amax = m 2^e, m in [0.5, 1)
   const int E = 15 - e;
-  return E < -100 ? -100 : (E > 100 ? 100 : E);
+  return E < -120 ? -120 : (E > 120 ? 120 : E);
 }
 // max |x| over n partial maxima (any order: max is exact), every thread of the block gets it;
 // red: >= blockDim.x / 64 floats of LDS

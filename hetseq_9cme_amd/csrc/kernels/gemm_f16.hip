@@ -437,9 +437,8 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w % NWM, wn = w / NWM;
 
-  const float sa = ldexpf(1.f, f16_scale_exp(block_amax(a_amax, na, red)));
-  const float sb = ldexpf(1.f, f16_scale_exp(block_amax(b_amax, nb, red)));
-  const float inv = (1.f / sa) * (1.f / sb);
+  const int Ea = f16_scale_exp(block_amax(a_amax, na, red)), Eb = f16_scale_exp(block_amax(b_amax, nb, red));
+  const float sa = ldexpf(1.f, Ea), sb = ldexpf(1.f, Eb), ia = ldexpf(1.f, -Ea), ib = ldexpf(1.f, -Eb);
 
   const hx::Buf abuf(A + (int64_t)t0 * lda, (uint32_t)((int64_t)(t1 - t0) * lda * 4));
   const hx::Buf bbuf(B + (int64_t)t0 * ldb, (uint32_t)((int64_t)(t1 - t0) * ldb * 4));
@@ -546,7 +545,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * WM + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (m < mvalid) o[(int64_t)m * N + n] = acc[a][b][r] * inv;   // rows past mvalid: padding
+        if (m < mvalid) o[(int64_t)m * N + n] = acc[a][b][r] * ia * ib;   // rows past mvalid: padding
       }
     }
 }

@@ -42,7 +42,7 @@ def parse():
     ap.add_argument('--seq', type=int, default=128)
     ap.add_argument('--max-pred', type=int, default=20)
     ap.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'])
-    ap.add_argument('--fp32-gemm', default='bf16x6', choices=['native', 'bf16x3', 'bf16x6'],
+    ap.add_argument('--fp32-gemm', default='bf16x6', choices=['native', 'bf16x3', 'bf16x6', 'fp16x3'],
                     help='fp32 linear GEMMs: bf16x6 (default, fp32-exact class), bf16x3 (near-fp32) or '
                          'native f32 MFMA (ops/split_gemm.py)')
     ap.add_argument('--model', default='base', choices=['base', 'large', 'tiny'])

@@ -82,9 +82,10 @@ class _AttnFn(torch.autograd.Function):
         bias = _bias3(bq, bk, bv).float().contiguous() if bq is not None else None
         # the split (x6) kernels follow the linears' policy (split_gemm.active: B*S >= MIN_ROWS rows),
         # so small fine-tuning batches keep the fp32-MFMA attention like their GEMMs
-        ctx.split = qkv.dtype == torch.float32 and split_gemm.active(qkv.reshape(-1, qkv.shape[-1]))
+        ctx.split = qkv.dtype == torch.float32 and split_gemm.attention_split(qkv.reshape(-1, qkv.shape[-1]))
         # one key block (S <= 128): the backward can write the projection's gradient planes
-        ctx.gp = gp if (ctx.split and _X6_BWD and _X6_PLANES and qkv.shape[1] <= 128) else None
+        ctx.gp = gp if (ctx.split and split_gemm.passes() > 0 and _X6_BWD and _X6_PLANES and qkv.shape[1] <= 128) \
+            else None
         if ctx.split:
             # fp32 products on the bf16 matrix cores (six piece passes, attention_x6.hip)
             B, S = qkv.shape[0], qkv.shape[1]

@@ -10,7 +10,7 @@ import os
 import torch
 import torch.nn.functional as F
 
-from . import split_gemm
+from . import gemm16, split_gemm
 from ._ext import C, use_kernels
 from .rng import get_rng
 
@@ -476,6 +476,14 @@ class _LinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, b, mbox, gp, defer=None):
         x2 = x.reshape(-1, x.shape[-1])
+        ctx.f16 = gemm16.ok(x2, W.shape[0])
+        if ctx.f16:   # --fp32-gemm fp16x3: fp32 operands split inside the GEMM kernels
+            x2 = gemm16.rows2(x)
+            ctx.xparts = gemm16.amax(x, x2)
+            y, wt, ctx.wparts = gemm16.linear(x2, ctx.xparts, W, b)
+            ctx.save_for_backward(x2, wt)
+            ctx.W, ctx.b, ctx.mbox, ctx.xshape = W, b, mbox, x.shape
+            return y.view(*x.shape[:-1], y.shape[-1])
         ctx.split = split_gemm.active(x2)
         ctx.pieces = ctx.split and split_gemm.nt_ok(W.shape[1], W.shape[0], x2.shape[0])
         ctx.gp = gp if (ctx.split and b is None) else None
@@ -507,6 +515,8 @@ class _LinearFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        if ctx.f16:
+            return _LinearFn._backward_f16(ctx, dy)
         x2, Wsaved = ctx.saved_tensors
         W = ctx.W
         b = ctx.b
@@ -551,6 +561,40 @@ class _LinearFn(torch.autograd.Function):
         return dx, dW, db, None, None, None
 
 
+def _f16_dgrad(dy2, dparts, wt, wparts, xshape, mbox):
+    """``_dgrad`` on the fp16x3 GEMM: beta = 1 into the deposited residual gradient if any."""
+    K = xshape[-1]
+    if mbox is not None:
+        g, other = mbox.take(torch.float32)
+        if g is not None:
+            return gemm16.dgrad(dy2, dparts, wt, wparts, acc=g.view(-1, K)).view(xshape)
+        dx = gemm16.dgrad(dy2, dparts, wt, wparts).view(xshape)
+        return dx if other is None else dx + other.view(xshape).to(dx.dtype)
+    return gemm16.dgrad(dy2, dparts, wt, wparts).view(xshape)
+
+
+def _linear_backward_f16(ctx, dy):
+    x2, wt = ctx.saved_tensors
+    W, b = ctx.W, ctx.b
+    dy2 = gemm16.rows2(dy)
+    dparts = gemm16.amax(dy, dy2)
+    dx = _f16_dgrad(dy2, dparts, wt, ctx.wparts, ctx.xshape, ctx.mbox) if ctx.needs_input_grad[0] else None
+    slot = grad_slot(W)
+    side = side_begin(dy2.device, True) if slot is not None else None
+    with torch.cuda.stream(side) if side is not None else _nullctx():
+        dW = gemm16.wgrad(dy2, dparts, x2, ctx.xparts, W.shape[0], W.shape[1], slot)
+        db = None
+        if b is not None:
+            db = C().colsum(dy2, None, grad_slot(b)) if dy2.shape[-1] % 4 == 0 else dy2.sum(0)
+    if side is not None:
+        for t in (dy2, x2, dparts, ctx.xparts):
+            t.record_stream(side)
+    return dx, dW, db, None, None, None
+
+
+_LinearFn._backward_f16 = staticmethod(_linear_backward_f16)
+
+
 def linear(x, W, b=None, res_grad=None, grad_planes=None, wgrad_defer=None):
     """F.linear with direct-to-slot weight/bias gradients on the GPU;
     ``res_grad``: see ``ResidualGrad``; ``grad_planes``: see ``GradPlanes``;
@@ -576,6 +620,18 @@ class _FFNSplitFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W1, b1, W2, mbox, gp):
         x2 = x.reshape(-1, x.shape[-1])
+        ctx.f16 = gemm16.ok(x2, W1.shape[0]) and W2.shape[0] % 64 == 0
+        if ctx.f16:
+            # fp16x3: the FFN-up epilogue writes gelu'(u) (backward) and gelu(u) in fp32 with its
+            # max |.| partials -- the FFN-down GEMM's operand, split in that GEMM's registers
+            x2 = gemm16.rows2(x)
+            xparts = gemm16.amax(x, x2)
+            d, h, hparts, w1t, p1 = gemm16.gemm_gelu(x2, xparts, W1, b1)
+            y2, w2t, p2 = gemm16.linear(h, hparts, W2)
+            ctx.save_for_backward(x2, d, h, w1t, w2t)
+            ctx.parts = (xparts, hparts, p1, p2)
+            ctx.W, ctx.b1, ctx.mbox, ctx.xshape = (W1, W2), b1, mbox, x.shape
+            return y2.view(*x.shape[:-1], y2.shape[-1])
         rows = x.numel() // x.shape[-1]
         ctx.pieces = split_gemm.nt_ok(W1.shape[1], W1.shape[0], rows) and split_gemm.nt_ok(W2.shape[1], W2.shape[0], rows)
         ctx.gp = gp
@@ -613,6 +669,8 @@ class _FFNSplitFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
+        if ctx.f16:
+            return _ffn_backward_f16(ctx, dy)
         xs, y1, hs, w1, b1, w2 = ctx.saved_tensors
         W1, W2 = ctx.W
         dy2 = dy.reshape(-1, dy.shape[-1])
@@ -675,8 +733,37 @@ class _FFNSplitFn(torch.autograd.Function):
         return dx, dW1, db1, dW2, None, None
 
 
+def _ffn_backward_f16(ctx, dy):
+    x2, d, h, w1t, w2t = ctx.saved_tensors
+    xparts, hparts, p1, p2 = ctx.parts
+    W1, W2 = ctx.W
+    dy2 = gemm16.rows2(dy)
+    dparts = gemm16.amax(dy, dy2)
+    slot2, slot1 = grad_slot(W2), grad_slot(W1)
+    # each weight gradient on the side stream, beside the next data-gradient GEMM
+    side = side_begin(dy2.device, True) if slot2 is not None and slot1 is not None else None
+    with torch.cuda.stream(side) if side is not None else _nullctx():
+        dW2 = gemm16.wgrad(dy2, dparts, h, hparts, W2.shape[0], W2.shape[1], slot2)
+    if side is not None:
+        for t in (dy2, dparts, h, hparts):
+            t.record_stream(side)
+    # GELU backward in the FFN-down data-gradient epilogue: t = (dy W2) * gelu'(u), d b1
+    t, tparts, db1 = gemm16.gemm_dgelu(dy2, dparts, w2t, p2, d, grad_slot(ctx.b1))
+    if side is not None:
+        side = side_begin(dy2.device, True)   # after t
+    with torch.cuda.stream(side) if side is not None else _nullctx():
+        dW1 = gemm16.wgrad(t, tparts, x2, xparts, W1.shape[0], W1.shape[1], slot1)
+    if side is not None:
+        for q in (t, tparts, x2, xparts):
+            q.record_stream(side)
+    dx = _f16_dgrad(t, tparts, w1t, p1, ctx.xshape, ctx.mbox)
+    return dx, dW1, db1, dW2, None, None
+
+
 def ffn_fusable(x, W1, b1, W2):
-    """The split-plane FFN path applies (fp32 GPU activations, --fp32-gemm bf16x3/x6)."""
+    """The fused FFN path applies (fp32 GPU activations, --fp32-gemm bf16x3/x6/fp16x3)."""
+    if b1 is not None and gemm16.ok(x.reshape(-1, x.shape[-1]), W1.shape[0]) and W2.shape[0] % 64 == 0:
+        return True
     return split_gemm.active(x) and b1 is not None and W1.shape[0] % 8 == 0 and x.shape[-1] % 8 == 0
 
 
@@ -718,6 +805,8 @@ def weight_pieces_scope(Ws, x):
     import contextlib
     if os.environ.get('HX_WSPLIT_BATCH', '1') == '0' or not torch.is_tensor(x) or x.dtype != torch.float32:
         return contextlib.nullcontext()
+    if gemm16.enabled():
+        return gemm16.weight_scope(Ws) if use_kernels(x) else contextlib.nullcontext()
     rows = x.numel() // max(1, x.shape[-1])
     if not split_gemm.producer_pieces(rows, x.shape[-1], x):
         return contextlib.nullcontext()
@@ -745,6 +834,17 @@ class _Linear3Fn(torch.autograd.Function):
             Wc = Wc if Wc is not None else W.to(x.dtype)
             bc = cast_w(b, x.dtype) if has_b else None
         x2 = x.reshape(-1, x.shape[-1])
+        ctx.f16 = gemm16.ok(x2, W.shape[0])
+        if ctx.f16:   # --fp32-gemm fp16x3
+            ctx.split = ctx.pieces = False
+            x2 = gemm16.rows2(x)
+            ctx.xparts = gemm16.amax(x, x2)
+            y, wt, ctx.wparts = gemm16.linear(x2, ctx.xparts, W, b)
+            ctx.save_for_backward(x2, wt)
+            ctx.params = (wq, wk, wv, bq, bk, bv)
+            ctx.has_b, ctx.join, ctx.wjoin, ctx.mbox, ctx.xshape = has_b, None, None, mbox, x.shape
+            ctx.n = [wq.shape[0], wk.shape[0], wv.shape[0]]
+            return y.view(*x.shape[:-1], y.shape[-1])
         ctx.split = split_gemm.active(x2)
         ctx.pieces = ctx.split and split_gemm.nt_ok(W.shape[1], W.shape[0], x2.shape[0])
         ctx.gp = gp if (ctx.split and not has_b) else None
@@ -786,7 +886,15 @@ class _Linear3Fn(torch.autograd.Function):
         x2, W = ctx.saved_tensors
         wq, wk, wv, bq, bk, bv = ctx.params
         dy2 = dy.reshape(-1, dy.shape[-1])
-        if ctx.pieces:
+        if ctx.f16:
+            # W holds W^T's fp16 pieces here; dx after the side-stream weight gradient is queued
+            n_out = sum(ctx.n)
+            dy2 = gemm16.rows2(dy)
+            dys = gemm16.amax(dy, dy2)
+            dx = None
+            n_in = x2.shape[1]
+            wg = lambda slot: gemm16.wgrad(dy2, dys, x2, ctx.xparts, n_out, n_in, slot)
+        elif ctx.pieces:
             n_out = sum(ctx.n)
             dys = ctx.gp.take() if ctx.gp is not None else None   # the attention backward's pieces
             dys = dys if dys is not None else split_gemm.pieces(dy2.float())
@@ -813,7 +921,7 @@ class _Linear3Fn(torch.autograd.Function):
         bs = [grad_slot(t) for t in (bq, bk, bv)] if has_b else [None, None, None]
         fb = _adjacent_view(bs) if all(t is not None for t in bs) else None
         direct = fused is not None and (fb is not None or not has_b)
-        side = side_begin(dy2.device, ctx.pieces) if direct else None
+        side = side_begin(dy2.device, ctx.pieces or ctx.f16) if direct else None
         item = ctx.join.item if ctx.join is not None else None
         gjoin = None
         with torch.cuda.stream(side) if side is not None else _nullctx():
@@ -855,7 +963,11 @@ class _Linear3Fn(torch.autograd.Function):
             x2.record_stream(side)
             if dys is not None:
                 dys.record_stream(side)
-        if ctx.pieces:
+            if ctx.f16:
+                ctx.xparts.record_stream(side)
+        if ctx.f16 and ctx.needs_input_grad[0]:
+            dx = _f16_dgrad(dy2, dys, W, ctx.wparts, ctx.xshape, ctx.mbox)
+        elif ctx.pieces:
             dx = _dgrad_pieces(dys, W, ctx.xshape, ctx.mbox)     # W holds the W^T pieces here
         if not has_b:
             return (dx, gW[0], gW[1], gW[2], None, None, None, None, None, gjoin, None)
@@ -886,6 +998,23 @@ def attention(qkv, mask_bias, num_heads, p, training, bias=None, grad_planes=Non
 class _DecoderXentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, W, bias, labels):
+        ctx.f16 = gemm16.ok(h, 64) and h.is_contiguous() and W.shape[1] % 64 == 0
+        if ctx.f16:
+            # --fp32-gemm fp16x3: the vocabulary padded to a multiple of 768 with zero weight rows
+            # (whole 192 / 256 tiles; the padding logits are exactly 0 and never read as logits)
+            V, H = W.shape
+            Vp = (V + 767) // 768 * 768
+            Wp = _padded_rows(W, Vp)
+            wf, wt, wparts = C().split_weight_f16([Wp])[0]
+            hparts = gemm16.amax(h, h)
+            full = gemm16.mm(h, hparts, wf, wparts)
+            logits = full[:, :V]
+            loss_rows = C().softmax_xent_(logits, bias, labels, -1)   # logits <- softmax - onehot
+            count = (labels != -1).sum().to(torch.float32)
+            loss = loss_rows.sum() / count
+            ctx.save_for_backward(h, W, full, count, wt, wparts)
+            ctx.params = (W, bias)
+            return loss
         ctx.split = split_gemm.active(h, W.shape[0])
         ctx.pieces = False
         if ctx.split:    # fp32 on bf16 matrix cores (--fp32-gemm)
@@ -915,6 +1044,8 @@ class _DecoderXentFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        if ctx.f16:
+            return _decoder_backward_f16(ctx, g)
         h, W, dl_full, count = ctx.saved_tensors
         Wp, bias = ctx.params
         dl = dl_full[:, :W.shape[0]]
@@ -969,6 +1100,36 @@ class _DecoderXentFn(torch.autograd.Function):
             dl.record_stream(side)
             hs.record_stream(side)
         return dh, dW, dbias, None
+
+
+_PAD = {}
+
+
+def _padded_rows(W, rows):
+    """W [V, H] copied into a cached zero-padded [rows, H] buffer (the padding rows stay 0)."""
+    key = (W.device, rows, W.shape[1])
+    buf = _PAD.get(key)
+    if buf is None or buf.shape[0] != rows:
+        buf = _PAD[key] = torch.zeros(rows, W.shape[1], device=W.device, dtype=torch.float32)
+    buf[:W.shape[0]].copy_(W.detach())
+    return buf
+
+
+def _decoder_backward_f16(ctx, g):
+    h, W, dl_full, count, wt, wparts = ctx.saved_tensors
+    Wt, bias = ctx.params
+    V = W.shape[0]
+    dl = dl_full[:, :V]
+    scale = (g.float() / count).reshape(1)
+    dbias = C().colsum(dl, scale, grad_slot(bias) if bias is not None else None)
+    # |softmax - onehot| <= 1: a constant bound is a valid max |dl| for the fp16 split
+    one = gemm16.bound(dl_full.device)
+    # dh = dl . W over the padded vocabulary (split-K slabs: 40 output tiles alone would idle the CUs)
+    dh = gemm16.mm(dl_full, one, wt, wparts, ks=0).mul_(scale)
+    hs = h * scale.to(h.dtype)
+    slot = grad_slot(Wt)
+    dW = gemm16.wgrad(dl_full, one, hs, gemm16.amax(hs, hs), V, h.shape[1], slot)
+    return dh, dW, dbias, None
 
 
 def _decoder_pieces_ok(h, W, Vp):

@@ -1,0 +1,166 @@
+"""fp32 GEMMs as three fp16 piece products (``--fp32-gemm fp16x3``; csrc/kernels/gemm_f16.hip).
+
+Every fp32 operand x is used as 2^-E (h0 + h1) with h0 = fp16(2^E x), h1 = fp16(2^E x - h0):
+22 significant bits per element; the product a.b is a0 b0 + a0 b1 + a1 b0 (the dropped a1 b1
+is 2^-22 relative) -- three fp16 MFMA passes where the bf16 emulation needs six
+(``--fp32-gemm bf16x6``, ops/split_gemm.py).  E comes from the operand's max |x|, so every
+tensor handed to these GEMMs travels with **max |x| partials**: a small fp32 vector whose max is
+max |x| (its producer writes it -- this module's GELU epilogues, LayerNorm, attention -- or
+``amax`` computes it in one read pass).  The GEMMs read activations and gradients AS fp32 and
+split them in registers; only weights are split ahead of time (one launch per forward for the
+whole encoder, ``weight_scope``).
+
+Reference sites: hetseq/bert_modeling.py:334-336 (Q/K/V), :383 (attention output), :409 +
+:166-168 (FFN up, bias_gelu), :419 (FFN down), :509 (pooler), :522 (MLM transform), :538-547
+(MLM decoder), :1221 (NER classifier) and their backward products.
+"""
+import torch
+
+from ._ext import C, use_kernels
+
+
+class _State(object):
+    on = False
+    scope = None        # {(data_ptr, shape): (wf, wt, parts)} for the running forward
+    min_rows = 1
+
+
+def set_enabled(flag):
+    _State.on = bool(flag)
+
+
+def enabled():
+    return _State.on
+
+
+def ok(x2, n_out):
+    """The fp16x3 GEMMs take the product [rows, K] x [K, n_out]: fp32 GPU operands, 16-deep k
+    steps and an output width with a tile shape (multiples of 64; smaller heads -- the NSP
+    classifier, NER's num_labels -- stay on the library fp32 GEMM, microseconds each)."""
+    return (_State.on and x2.dtype == torch.float32 and use_kernels(x2) and x2.shape[-1] % 64 == 0 and
+            n_out % 64 == 0 and x2.numel() > 0)
+
+
+def wgrad_ok(n_out, n_in):
+    return n_out % 128 == 0 and n_in % 128 == 0
+
+
+def _aligned(t):
+    return t.stride(-1) == 1 and t.stride(0) % 4 == 0 and t.data_ptr() % 16 == 0
+
+
+def rows2(x):
+    """[.., K] -> a 2-D [rows, K] operand the kernels can read (contiguous copy if not)."""
+    x2 = x.reshape(-1, x.shape[-1])
+    return x2 if _aligned(x2) else x2.contiguous()
+
+
+# ---------------------------------------------------------------- max |x| partials
+def attach(t, parts):
+    """Hand ``parts`` (max |t| partials, written by t's producer) to the GEMMs that consume t."""
+    if parts is not None:
+        t._hx_amax = parts
+        t._hx_amax_ver = t._version
+    return t
+
+
+def amax(t, t2=None):
+    """max |t| partials: the producer's (if ``t`` has not changed since), else one read pass."""
+    p = getattr(t, '_hx_amax', None)
+    if p is not None and getattr(t, '_hx_amax_ver', -1) == t._version:
+        return p
+    x2 = t2 if t2 is not None else rows2(t)
+    if not (x2.shape[-1] % 4 == 0 and _aligned(x2)):
+        x2 = x2.contiguous()
+    return attach(t, C().amax_rows(x2))._hx_amax
+
+
+_ONES = {}
+
+
+def bound(dev, v=1.0):
+    """A constant max |x| bound (a valid partials vector: the scale only needs an upper bound)."""
+    key = (dev, float(v))
+    t = _ONES.get(key)
+    if t is None:
+        t = _ONES[key] = torch.full((1,), float(v), dtype=torch.float32, device=dev)
+    return t
+
+
+# ---------------------------------------------------------------- weight pieces
+class weight_scope(object):
+    """Split every weight in ``Ws`` into P2 fp16 pieces in ONE launch pair (max |W| + split) on
+    entry; ``weight_pieces`` returns them until exit (scoped to one forward: weights change at
+    every optimizer step, and an activation-checkpointing recompute outside the scope splits
+    again)."""
+
+    def __init__(self, Ws):
+        self.Ws = [W for W in Ws if W is not None]
+
+    def __enter__(self):
+        self.prev = _State.scope
+        Ws = [W for W in self.Ws if W.dim() == 2 and W.shape[0] % 64 == 0 and W.shape[1] % 64 == 0 and
+              W.is_contiguous() and W.dtype == torch.float32 and W.is_cuda]
+        if _State.on and Ws:
+            d = {}
+            for i in range(0, len(Ws), 64):
+                chunk = Ws[i:i + 64]
+                for W, o in zip(chunk, C().split_weight_f16(chunk)):
+                    d[(W.data_ptr(), tuple(W.shape))] = tuple(o)
+            _State.scope = d
+        return self
+
+    def __exit__(self, *exc):
+        _State.scope = self.prev
+        return False
+
+
+def weight_pieces(W):
+    """(wf [N, 2K], wt [K, 2N], parts) of W [N, K] (N, K multiples of 64)."""
+    if _State.scope is not None:
+        e = _State.scope.get((W.data_ptr(), tuple(W.shape)))
+        if e is not None:
+            return e
+    return tuple(C().split_weight_f16([W.detach().contiguous()])[0])
+
+
+# ---------------------------------------------------------------- products
+def mm(a2, a_parts, b, b_parts, out=None, beta=False, bias=None, ks=1):
+    """a2 [M, K] (fp32) . b^T (b = P2 pieces [N, 2K]) (+ out if beta) (+ bias) -> fp32 [M, N]."""
+    return C().gemm_f16(a2, a_parts, b, b_parts, out=out, beta=beta, bias=bias, ks=ks)
+
+
+def linear(x2, xparts, W, bias=None):
+    """y = x2 W^T (+ bias); also returns W^T's pieces and W's partials for the backward."""
+    wf, wt, parts = weight_pieces(W)
+    return mm(x2, xparts, wf, parts, bias=bias), wt, parts
+
+
+def dgrad(dy2, dparts, wt, parts, acc=None):
+    """dx = dy2 W from W^T's pieces, accumulated into ``acc`` (beta = 1) when given."""
+    if acc is not None:
+        return mm(dy2, dparts, wt, parts, out=acc, beta=True)
+    return mm(dy2, dparts, wt, parts)
+
+
+def wgrad(dy2, dparts, x2, xparts, n_out, n_in, slot=None):
+    """dW [n_out, n_in] = dy2^T x2 over the token rows, straight into ``slot`` when given
+    (shapes without a tile: the library fp32 product)."""
+    out = slot if slot is not None else torch.empty(n_out, n_in, device=dy2.device)
+    if wgrad_ok(dy2.shape[1], n_in) and dy2.shape[1] >= n_out and _aligned(dy2) and _aligned(x2):
+        return C().wgrad_f16(dy2, dparts, x2, xparts, out)
+    return torch.mm(dy2[:, :n_out].t(), x2, out=out)
+
+
+def gemm_gelu(x2, xparts, W1, b1):
+    """FFN up with its bias + GELU epilogue: (gelu'(u), h = gelu(u), max |h| partials, W1^T's
+    pieces, W1's partials)."""
+    wf, wt, parts = weight_pieces(W1)
+    d, h, hmax = C().gemm_f16_gelu(x2, xparts, wf, parts, b1, 1)
+    return d, h, hmax, wt, parts
+
+
+def gemm_dgelu(dy2, dparts, wt2, parts2, d, dbias_out):
+    """FFN-down data gradient with the GELU backward: (t = (dy W2) * gelu'(u), max |t| partials,
+    d b1)."""
+    return C().gemm_f16_dgelu(dy2, dparts, wt2, parts2, d, None, dbias_out, 1)

@@ -51,7 +51,7 @@ from ._ext import C, use_kernels
 PIECES = {3: 2, 6: 3}
 ORDER_P = {3: (0, 1, 0), 6: (0, 1, 0, 2, 1, 0)}
 ORDER_Q = {3: (0, 0, 1), 6: (0, 0, 1, 0, 1, 2)}
-MODES = {'native': 0, 'bf16x3': 3, 'bf16x6': 6}
+MODES = {'native': 0, 'bf16x3': 3, 'bf16x6': 6, 'fp16x3': 0}   # fp16x3: ops/gemm16.py
 # Prefix form (see ``prefix_mm``): the large operand holds each distinct piece once, in
 # natural order, and the weight operand piece j repeated npc - j times.
 ORDER_N = {3: (0, 1), 6: (0, 1, 2)}
@@ -76,14 +76,31 @@ class _State(object):
 
 
 def set_fp32_gemm(mode):
-    """'native' (fp32 MFMA through the libraries), 'bf16x3' or 'bf16x6'."""
+    """'native' (fp32 MFMA through the libraries), 'bf16x3', 'bf16x6' or 'fp16x3' (three fp16
+    piece products on fp32 operands split in the GEMM kernels: ops/gemm16.py)."""
+    from . import gemm16
     if mode not in MODES:
         raise ValueError('--fp32-gemm must be one of {}'.format(sorted(MODES)))
     _State.passes = MODES[mode]
+    gemm16.set_enabled(mode == 'fp16x3')
 
 
 def fp32_gemm_mode():
-    return {v: k for k, v in MODES.items()}[_State.passes]
+    from . import gemm16
+    if gemm16.enabled():
+        return 'fp16x3'
+    return {3: 'bf16x3', 6: 'bf16x6', 0: 'native'}[_State.passes]
+
+
+def attention_split(x2):
+    """Does the fp32 attention run its products on the bf16 matrix cores (attention_x6.hip) for
+    the [rows, 3H] projection ``x2``: bf16x6 / bf16x3 whenever the linears split, fp16x3 from the
+    same row count (the attention kernels stay bf16x6-class under every split mode)."""
+    from . import gemm16
+    if active(x2):
+        return True
+    rows = x2.numel() // max(1, x2.shape[-1])
+    return gemm16.enabled() and x2.dtype == torch.float32 and use_kernels(x2) and rows >= MIN_ROWS[6]
 
 
 def active(x, n_out=None):

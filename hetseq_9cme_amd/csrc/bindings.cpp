@@ -134,8 +134,16 @@ void adadelta(Tensor p, Tensor g, Tensor sq, Tensor acc, Tensor gscale, int64_t 
 }
 
 // ------------------------------------------------------------------ layernorm
+// amax_out (fp32 runs only): receives hx_ln_fwd_blocks(rows) max |out| partials (ops/gemm16.py)
+inline float* amax_ptr(const OptT& a, int64_t need, const char* what) {
+  if (!has(a)) return nullptr;
+  check_f32(*a, what);
+  TORCH_CHECK(a->is_contiguous() && a->numel() >= need, what, ": needs ", need, " fp32 partials");
+  return a->data_ptr<float>();
+}
 std::vector<Tensor> ln_fwd(Tensor y, OptT bias, OptT res, Tensor gamma, Tensor beta, double eps, double keep_prob,
-                           const Tensor& seed, int64_t stream, bool drop_after, bool save_z, int64_t npieces) {
+                           const Tensor& seed, int64_t stream, bool drop_after, bool save_z, int64_t npieces,
+                           OptT amax_out) {
   check_cuda(y, "input");
   const int H = (int)y.size(-1);
   const int64_t rows = y.numel() / H;
@@ -159,14 +167,15 @@ std::vector<Tensor> ln_fwd(Tensor y, OptT bias, OptT res, Tensor gamma, Tensor b
             gamma.data_ptr<float>(), beta.data_ptr<float>(), out.data_ptr(), save_z ? z.data_ptr() : nullptr,
             mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, H, (float)eps, (float)keep_prob, seed_ptr(seed),
             (uint64_t)stream, drop_after ? 1 : 0, cur_stream(y),
-            npieces ? reinterpret_cast<uint16_t*>(pcs.data_ptr()) : nullptr, (int)npieces);
+            npieces ? reinterpret_cast<uint16_t*>(pcs.data_ptr()) : nullptr, (int)npieces,
+            act_bf16(y) ? nullptr : amax_ptr(amax_out, hx_ln_fwd_blocks(rows), "ln_fwd amax"));
   dbg_finite(out, "ln_fwd");
   return {out, z, mean, rstd, pcs};
 }
 
 std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tensor gamma, double keep_prob,
                            const Tensor& seed, int64_t stream, bool drop_after, bool want_dy, bool want_dbias,
-                           OptT dgamma_out, OptT dbeta_out, OptT dbias_out) {
+                           OptT dgamma_out, OptT dbeta_out, OptT dbias_out, OptT amax_out) {
   check_cuda(dout, "grad_output");
   check_cuda(z, "saved input");
   const int H = (int)z.size(-1);
@@ -186,7 +195,8 @@ std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tens
             gamma.data_ptr<float>(), dz.data_ptr(), want_dy ? dy.data_ptr() : nullptr, partial.data_ptr<float>(), nblk,
             rows, H, (float)keep_prob, seed_ptr(seed), (uint64_t)stream, drop_after ? 1 : 0,
             (want_dy && want_dbias) ? 1 : 0, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
-            want_dbias ? dbias.data_ptr<float>() : nullptr, 0, nullptr, 0, 0, 0, cur_stream(z));
+            want_dbias ? dbias.data_ptr<float>() : nullptr, 0, nullptr, 0, 0, 0, cur_stream(z),
+            act_bf16(z) ? nullptr : amax_ptr(amax_out, nblk, "ln_bwd amax"));
   dbg_finite(dz, "ln_bwd (dz)");
   return {dz, dy, dgamma, dbeta, dbias};
 }
@@ -231,7 +241,7 @@ std::vector<Tensor> ln_bwd_planes(Tensor dout, Tensor z, Tensor mean, Tensor rst
 
 std::vector<Tensor> embed_ln_fwd(Tensor ids, OptT tt, Tensor wte, Tensor wpe, Tensor wtt, Tensor gamma, Tensor beta,
                                  double eps, double keep_prob, const Tensor& seed, int64_t stream, bool bf16_out,
-                                 int64_t npieces) {
+                                 int64_t npieces, OptT amax_out) {
   dbg_range(ids, 0, wte.size(0), "token ids");
   if (has(tt)) dbg_range(*tt, 0, wtt.size(0), "token type ids");
   check_cuda(ids, "input_ids");
@@ -256,7 +266,8 @@ std::vector<Tensor> embed_ln_fwd(Tensor ids, OptT tt, Tensor wte, Tensor wpe, Te
                   wte.data_ptr<float>(), wpe.data_ptr<float>(), wtt.data_ptr<float>(), gamma.data_ptr<float>(),
                   beta.data_ptr<float>(), out.data_ptr(), z.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                   B * S, (int)S, H, (float)eps, (float)keep_prob, seed_ptr(seed), (uint64_t)stream, cur_stream(ids),
-                  npieces ? reinterpret_cast<uint16_t*>(pcs.data_ptr()) : nullptr, (int)npieces);
+                  npieces ? reinterpret_cast<uint16_t*>(pcs.data_ptr()) : nullptr, (int)npieces,
+                  bf16_out ? nullptr : amax_ptr(amax_out, hx_ln_fwd_blocks(B * S), "embed_ln_fwd amax"));
   dbg_finite(out, "embed_ln_fwd");
   return {out, z, mean, rstd, pcs};
 }
@@ -1182,12 +1193,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adadelta", &adadelta);
   m.def("ln_fwd", &ln_fwd, py::arg("y"), py::arg("bias"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
         py::arg("eps"), py::arg("keep_prob"), py::arg("seed"), py::arg("stream"), py::arg("drop_after"),
-        py::arg("save_z"), py::arg("npieces") = 0);
-  m.def("ln_bwd", &ln_bwd);
+        py::arg("save_z"), py::arg("npieces") = 0, py::arg("amax_out") = py::none());
+  m.def("ln_bwd", &ln_bwd, py::arg("dout"), py::arg("z"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"),
+        py::arg("keep_prob"), py::arg("seed"), py::arg("stream"), py::arg("drop_after"), py::arg("want_dy"),
+        py::arg("want_dbias"), py::arg("dgamma_out"), py::arg("dbeta_out"), py::arg("dbias_out"),
+        py::arg("amax_out") = py::none());
+  m.def("ln_fwd_blocks", &hx_ln_fwd_blocks);
+  m.def("ln_bwd_blocks", &hx_ln_bwd_blocks);
   m.def("ln_bwd_planes", &ln_bwd_planes);
   m.def("embed_ln_fwd", &embed_ln_fwd, py::arg("ids"), py::arg("tt"), py::arg("wte"), py::arg("wpe"), py::arg("wtt"),
         py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("keep_prob"), py::arg("seed"), py::arg("stream"),
-        py::arg("bf16_out"), py::arg("npieces") = 0);
+        py::arg("bf16_out"), py::arg("npieces") = 0, py::arg("amax_out") = py::none());
   m.def("embed_word_grad", &embed_word_grad);
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);

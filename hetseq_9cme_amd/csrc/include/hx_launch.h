@@ -22,21 +22,26 @@ void hx_adadelta(float* p, const float* g, float* sq, float* acc, const float* g
                  float eps, float wd, const float* hp, hipStream_t s);
 
 // layernorm.hip
+// amax_part (fp32 only, may be null): one max |output| per block -- hx_ln_fwd_blocks(rows) of them for
+// the forward / embedding, hx_ln_bwd_blocks(rows) for the backward (max |dy|, or |dz| without dy)
 int hx_ln_bwd_blocks(int64_t rows);
+int hx_ln_fwd_blocks(int64_t rows);
 void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, const float* gamma, const float* beta,
                void* out, void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob,
                const uint64_t* seed, uint64_t stream, int drop_after, hipStream_t s, uint16_t* pieces = nullptr,
-               int npc = 0);
+               int npc = 0, float* amax_part = nullptr);
 // (pieces != nullptr, fp32 only: the output is also written as npc bf16 pieces [rows][npc][H])
 void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma,
                void* dz, void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
                uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
-               int accumulate, uint16_t* planes, uint32_t order, int npl, int npc, hipStream_t s);
+               int accumulate, uint16_t* planes, uint32_t order, int npl, int npc, hipStream_t s,
+               float* amax_part = nullptr);
 // (planes != nullptr: dy is written as bf16 split planes [rows][npl][H] instead of to dy)
 void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,
                      const float* wtt, const float* gamma, const float* beta, void* out, void* zsave, float* mean,
                      float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, const uint64_t* seed,
-                     uint64_t stream, hipStream_t s, uint16_t* pieces = nullptr, int npc = 0);
+                     uint64_t stream, hipStream_t s, uint16_t* pieces = nullptr, int npc = 0,
+                     float* amax_part = nullptr);
 void hx_embed_word_grad_sorted(int bf16, const void* dz, const int64_t* ids, const int64_t* order, float* dwte,
                                int64_t rows, int H, hipStream_t s);
 // elementwise.hip

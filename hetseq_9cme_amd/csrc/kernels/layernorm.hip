@@ -29,6 +29,25 @@ struct Row {
   float4 v[CH];
 };
 
+// max |x| over the block -> part[blockIdx.x] (the fp16x3 GEMMs' operand scale, ops/gemm16.py);
+// every thread of the block must call it
+__device__ __forceinline__ void block_amax_out(float m, float* __restrict__ part) {
+  __shared__ float red_am[WPB];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) red_am[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float r = red_am[0];
+#pragma unroll
+    for (int i = 1; i < WPB; ++i) r = fmaxf(r, red_am[i]);
+    part[blockIdx.x] = r;
+  }
+}
+__device__ __forceinline__ float amax4(float m, float4 v) {
+  return fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+}
+
 // npc bf16 pieces of the 4 fp32 outputs at columns j..j+3 of row r -> pieces [rows][npc][H]
 // (the natural piece layout the split GEMMs read: ops/split_gemm.py), one 8-B store per piece
 __device__ __forceinline__ void store_pieces4(uint16_t* pieces, int npc, int64_t r, int H, int j, float4 o) {
@@ -53,13 +72,14 @@ __global__ __launch_bounds__(NT) void ln_fwd_k(const T* __restrict__ y, const fl
                                              T* __restrict__ zsave, float* __restrict__ mean_out,
                                              float* __restrict__ rstd_out, int64_t rows, int H, float eps,
                                              float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream,
-                                             uint16_t* __restrict__ pieces, int npc) {
+                                             uint16_t* __restrict__ pieces, int npc, float* __restrict__ amax_part) {
   const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   const int lane = threadIdx.x & 63;
   const int64_t wave = blockIdx.x * (int64_t)WPB + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * WPB;
   const float inv_keep = keep_prob > 0.f ? 1.f / keep_prob : 0.f;
   const bool drop = keep_prob < 1.f;
+  float am = 0.f;
   for (int64_t r = wave; r < rows; r += nw) {
     Row<CH> x;
     float s = 0.f;
@@ -124,9 +144,11 @@ __global__ __launch_bounds__(NT) void ln_fwd_k(const T* __restrict__ y, const fl
         }
         hx::store4(out + r * H + j, o);
         if (pieces) store_pieces4(pieces, npc, r, H, j, o);
+        am = amax4(am, o);
       }
     }
   }
+  if (amax_part) block_amax_out(am, amax_part);
 }
 
 // ----------------------------------------------------------------------------- bwd
@@ -139,7 +161,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
                                              T* __restrict__ dy_out, float* __restrict__ partial, int64_t rows,
                                              int H, float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream,
                                              int want_dbias, uint16_t* __restrict__ planes, uint32_t order, int npl,
-                                             int npc) {
+                                             int npc, float* __restrict__ amax_part) {
   const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   __shared__ float red[WPB][CH * 256];
   const int lane = threadIdx.x & 63;
@@ -151,6 +173,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
   Row<CH> dg, db, dbias;
 #pragma unroll
   for (int c = 0; c < CH; ++c) dg.v[c] = db.v[c] = dbias.v[c] = hx::f4(0.f);
+  float am = 0.f;   // max |dy| (max |dz| without a separate dy): the upstream GEMMs' operand
   float4 gam[CH];
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
@@ -216,6 +239,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
         float4 dz = make_float4(rstd * (dv.x - m1 - xv.x * m2), rstd * (dv.y - m1 - xv.y * m2),
                                 rstd * (dv.z - m1 - xv.z * m2), rstd * (dv.w - m1 - xv.w * m2));
         hx::store4(dz_out + r * H + j, dz);
+        if (!dy_out && !planes) am = amax4(am, dz);
         if (dy_out || planes) {
           float4 dy = dz;
           if (drop && !kDropAfter) {
@@ -248,6 +272,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
           } else {
             hx::store4(dy_out + r * H + j, dy);
           }
+          am = amax4(am, dy);
           if (want_dbias) {
             dbias.v[c].x += dy.x; dbias.v[c].y += dy.y; dbias.v[c].z += dy.z; dbias.v[c].w += dy.w;
           }
@@ -275,6 +300,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
   fold(dg, 0);
   fold(db, 1);
   if (want_dbias) fold(dbias, 2);
+  if (amax_part) block_amax_out(am, amax_part);
 }
 
 // ------------------------------------------------------------------------ embedding
@@ -286,12 +312,13 @@ __global__ __launch_bounds__(NT) void embed_ln_fwd_k(const int64_t* __restrict__
                                                    T* __restrict__ zsave, float* __restrict__ mean_out,
                                                    float* __restrict__ rstd_out, int64_t rows, int S, int H,
                                                    float eps, float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream,
-                                                   uint16_t* __restrict__ pieces, int npc) {
+                                                   uint16_t* __restrict__ pieces, int npc, float* __restrict__ amax_part) {
   const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   const int lane = threadIdx.x & 63;
   const int64_t wave = blockIdx.x * (int64_t)WPB + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * WPB;
   const float inv_keep = keep_prob > 0.f ? 1.f / keep_prob : 0.f;
+  float am = 0.f;
   for (int64_t r = wave; r < rows; r += nw) {
     const int64_t id = ids[r];
     const int64_t ty = tt ? tt[r] : 0;
@@ -346,9 +373,11 @@ __global__ __launch_bounds__(NT) void embed_ln_fwd_k(const int64_t* __restrict__
         }
         hx::store4(out + r * H + j, o);
         if (pieces) store_pieces4(pieces, npc, r, H, j, o);
+        am = amax4(am, o);
       }
     }
   }
+  if (amax_part) block_amax_out(am, amax_part);
 }
 
 // word-embedding gradient: scatter-add rows of dz into dW[ids] (fp32 atomics,
@@ -448,15 +477,17 @@ inline int ln_grid(int64_t rows, int cap) {
 template <typename T>
 void ln_fwd_t(const void* y, const float* bias, const void* res, const float* gamma, const float* beta, void* out,
               void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob, const uint64_t* seed,
-              uint64_t stream, int drop_after, uint16_t* pieces, int npc, hipStream_t s) {
+              uint64_t stream, int drop_after, uint16_t* pieces, int npc, hipStream_t s, float* amax_part) {
   const int grid = ln_grid(rows, 4096);
   HX_CH_DISPATCH(H, {
     if (drop_after)
       ln_fwd_k<T, CH, true><<<grid, NT, 0, s>>>((const T*)y, bias, (const T*)res, gamma, beta, (T*)out, (T*)zsave,
-                                                mean, rstd, rows, H, eps, keep_prob, seed, stream, pieces, npc);
+                                                mean, rstd, rows, H, eps, keep_prob, seed, stream, pieces, npc,
+                                                amax_part);
     else
       ln_fwd_k<T, CH, false><<<grid, NT, 0, s>>>((const T*)y, bias, (const T*)res, gamma, beta, (T*)out, (T*)zsave,
-                                                 mean, rstd, rows, H, eps, keep_prob, seed, stream, pieces, npc);
+                                                 mean, rstd, rows, H, eps, keep_prob, seed, stream, pieces, npc,
+                                                 amax_part);
   })
 }
 
@@ -464,16 +495,16 @@ template <typename T>
 void ln_bwd_t(const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma, void* dz,
               void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
               uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
-              int accumulate, uint16_t* planes, uint32_t order, int npl, int npc, hipStream_t s) {
+              int accumulate, uint16_t* planes, uint32_t order, int npl, int npc, hipStream_t s, float* amax_part) {
   HX_CH_DISPATCH(H, {
     if (drop_after)
       ln_bwd_k<T, CH, true><<<nblk, NT, 0, s>>>((const T*)dout, (const T*)z, mean, rstd, gamma, (T*)dz, (T*)dy,
                                                 partial, rows, H, keep_prob, seed, stream, want_dbias, planes, order,
-                                                npl, npc);
+                                                npl, npc, amax_part);
     else
       ln_bwd_k<T, CH, false><<<nblk, NT, 0, s>>>((const T*)dout, (const T*)z, mean, rstd, gamma, (T*)dz, (T*)dy,
                                                  partial, rows, H, keep_prob, seed, stream, want_dbias, planes, order,
-                                                 npl, npc);
+                                                 npl, npc, amax_part);
   })
   // partial is [nblk][3][H]: fold rows of length 3H into dgamma | dbeta | dbias
   hx::fold_rows(partial, nblk, 3 * (int64_t)H, (want_dbias ? 3 : 2) * H, H, dgamma, dbeta,
@@ -483,44 +514,46 @@ void ln_bwd_t(const void* dout, const void* z, const float* mean, const float* r
 }  // namespace
 
 int hx_ln_bwd_blocks(int64_t rows) { return ln_grid(rows, 512); }
+int hx_ln_fwd_blocks(int64_t rows) { return ln_grid(rows, 4096); }
 
 void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, const float* gamma, const float* beta,
                void* out, void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob,
-               const uint64_t* seed, uint64_t stream, int drop_after, hipStream_t s, uint16_t* pieces, int npc) {
+               const uint64_t* seed, uint64_t stream, int drop_after, hipStream_t s, uint16_t* pieces, int npc,
+               float* amax_part) {
   if (bf16)
     ln_fwd_t<uint16_t>(y, bias, res, gamma, beta, out, zsave, mean, rstd, rows, H, eps, keep_prob, seed, stream,
-                       drop_after, nullptr, 0, s);
+                       drop_after, nullptr, 0, s, nullptr);
   else
     ln_fwd_t<float>(y, bias, res, gamma, beta, out, zsave, mean, rstd, rows, H, eps, keep_prob, seed, stream,
-                    drop_after, pieces, npc, s);
+                    drop_after, pieces, npc, s, amax_part);
 }
 
 void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma,
                void* dz, void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
                uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
-               int accumulate, uint16_t* planes, uint32_t order, int npl, int npc, hipStream_t s) {
+               int accumulate, uint16_t* planes, uint32_t order, int npl, int npc, hipStream_t s, float* amax_part) {
   if (bf16)
     ln_bwd_t<uint16_t>(dout, z, mean, rstd, gamma, dz, dy, partial, nblk, rows, H, keep_prob, seed, stream,
-                       drop_after, want_dbias, dgamma, dbeta, dbias, accumulate, planes, order, npl, npc, s);
+                       drop_after, want_dbias, dgamma, dbeta, dbias, accumulate, planes, order, npl, npc, s, nullptr);
   else
     ln_bwd_t<float>(dout, z, mean, rstd, gamma, dz, dy, partial, nblk, rows, H, keep_prob, seed, stream, drop_after,
-                    want_dbias, dgamma, dbeta, dbias, accumulate, planes, order, npl, npc, s);
+                    want_dbias, dgamma, dbeta, dbias, accumulate, planes, order, npl, npc, s, amax_part);
 }
 
 void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,
                      const float* wtt, const float* gamma, const float* beta, void* out, void* zsave, float* mean,
                      float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, const uint64_t* seed,
-                     uint64_t stream, hipStream_t s, uint16_t* pieces, int npc) {
+                     uint64_t stream, hipStream_t s, uint16_t* pieces, int npc, float* amax_part) {
   const int grid = ln_grid(rows, 4096);
   HX_CH_DISPATCH(H, {
     if (bf16)
       embed_ln_fwd_k<uint16_t, CH><<<grid, NT, 0, s>>>(ids, tt, wte, wpe, wtt, gamma, beta, (uint16_t*)out,
                                                        (uint16_t*)zsave, mean, rstd, rows, S, H, eps, keep_prob,
-                                                       seed, stream, nullptr, 0);
+                                                       seed, stream, nullptr, 0, nullptr);
     else
       embed_ln_fwd_k<float, CH><<<grid, NT, 0, s>>>(ids, tt, wte, wpe, wtt, gamma, beta, (float*)out,
                                                     (float*)zsave, mean, rstd, rows, S, H, eps, keep_prob, seed,
-                                                    stream, pieces, npc);
+                                                    stream, pieces, npc, amax_part);
   })
 }
 

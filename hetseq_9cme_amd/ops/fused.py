@@ -262,9 +262,11 @@ class _EmbedLNFn(torch.autograd.Function):
         keep = 1.0 - p
         seed, stream = get_rng().next(ids.device) if p > 0 else (get_rng().seed_tensor(ids.device), 0)
         npc = 0 if out_bf16 else split_gemm.producer_pieces(ids.numel(), wte.shape[1], wte)
+        am = _amax_buf(ids.numel(), wte, out_bf16)
         out, z, mean, rstd, pcs = C().embed_ln_fwd(ids, tt, wte, wpe, wtt, gamma, beta, eps, keep, seed, stream,
-                                                   out_bf16, npc)
+                                                   out_bf16, npc, am)
         split_gemm.attach_pieces(out, pcs)   # the first layer's QKV GEMM reads them
+        gemm16.attach(out, am)               # (fp16x3: its max |x| partials)
         ctx.save_for_backward(ids, tt if tt is not None else torch.Tensor(), z, mean, rstd, gamma)
         ctx.params = (wte, wpe, wtt, beta)
         ctx.has_tt = tt is not None
@@ -332,6 +334,15 @@ def embed_ln(ids, tt, wte, wpe, wtt, gamma, beta, eps, p, training, out_dtype=to
     return F.dropout(out, p, training).to(out_dtype)
 
 
+def _amax_buf(rows, ref, bf16, bwd=False):
+    """Buffer for a LayerNorm kernel's max |out| partials when the fp16x3 GEMMs consume its output
+    (ops/gemm16.py), else None."""
+    if bf16 or not gemm16.enabled() or not ref.is_cuda:
+        return None
+    n = C().ln_bwd_blocks(rows) if bwd else C().ln_fwd_blocks(rows)
+    return torch.empty(n, dtype=torch.float32, device=ref.device)
+
+
 # ----------------------------------------------------------------- bias + dropout + residual + LN
 _ZERO_SCALARS = {}
 
@@ -352,8 +363,10 @@ class _BiasDropResLNFn(torch.autograd.Function):
         keep = 1.0 - p
         seed, stream = get_rng().next(y.device) if p > 0 else (get_rng().seed_tensor(y.device), 0)
         npc = split_gemm.producer_pieces(y.numel() // y.shape[-1], y.shape[-1], y) if y.dtype == torch.float32 else 0
-        out, z, mean, rstd, pcs = C().ln_fwd(y, bias, res, gamma, beta, eps, keep, seed, stream, False, True, npc)
+        am = _amax_buf(y.numel() // y.shape[-1], y, y.dtype != torch.float32)
+        out, z, mean, rstd, pcs = C().ln_fwd(y, bias, res, gamma, beta, eps, keep, seed, stream, False, True, npc, am)
         split_gemm.attach_pieces(out, pcs)   # the next QKV / FFN-up piece GEMM reads them
+        gemm16.attach(out, am)               # (fp16x3: its max |x| partials)
         ctx.save_for_backward(z, mean, rstd, gamma)
         ctx.params = (bias, beta)
         ctx.mbox = mbox
@@ -380,10 +393,11 @@ class _BiasDropResLNFn(torch.autograd.Function):
             gp.planes = planes
             dy_ret = _zero_scalar(z.device, z.dtype).expand(ctx.yshape)
         else:
+            am = _amax_buf(z.numel() // z.shape[-1], z, z.dtype != torch.float32, bwd=True)
             dz, dy, dgamma, dbeta, dbias = C().ln_bwd(dout.contiguous(), z, mean, rstd, gamma, keep, seed, stream,
                                                       False, need_dy, has_bias, grad_slot(gamma), grad_slot(beta),
-                                                      grad_slot(bias) if has_bias else None)
-            dy_ret = dy if need_dy else dz
+                                                      grad_slot(bias) if has_bias else None, am)
+            dy_ret = gemm16.attach(dy if need_dy else dz, am)   # (fp16x3: max |dy| partials)
         dres = dz if has_res else None
         # dz is a private buffer only when dy is separate: then it can become the
         # accumulator of the consumer linear's dgrad GEMM

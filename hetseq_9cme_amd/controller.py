@@ -342,16 +342,21 @@ class Controller(object):
             used_at = None
             if hasattr(self.optimizer, 'device_used'):
                 self.optimizer.device_used = None   # never a previous update's flags
-            if self.reducer.enabled and self.reducer.find_unused and hasattr(self.optimizer, 'device_used') \
-                    and not capturing:
+            if self.reducer.enabled and self.reducer.find_unused and hasattr(self.optimizer, 'device_used'):
                 used_at = len(fields)
                 fields += [1.0 if u else 0.0 for u in step_used]
             if capturing:
                 # no host->device copy inside a graph (it would keep reading a freed pinned
-                # buffer): the per-shape constants become fill nodes
+                # buffer): the per-shape constants become fill nodes, one per run of equal values
+                # (the used flags of a captured shape are the same on every replay)
                 vec = torch.empty(len(fields), dtype=torch.float64, device=self.device)
-                for k, f in enumerate(fields):
-                    vec[k].fill_(f)
+                k = 0
+                while k < len(fields):
+                    e = k + 1
+                    while e < len(fields) and fields[e] == fields[k]:
+                        e += 1
+                    vec[k:e].fill_(fields[k])
+                    k = e
             else:
                 host = torch.tensor(fields, dtype=torch.float64)
                 vec = host.pin_memory().to(self.device, non_blocking=True) if self.cuda else host

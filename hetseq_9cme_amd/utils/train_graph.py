@@ -20,10 +20,18 @@ synchronisation, see controller.py):
   temporary pinned buffer; host meters are updated after each replay from the graph's
   static output tensors.
 
-Scope: one process (no gradient reducer in the graph), one micro-batch per update, fp32 or
-bf16.  Each distinct input shape is warmed up eagerly ``warmup`` times, then captured into
-a graph that shares one memory pool with the others (``max_graphs`` shapes at most; later
-new shapes, and anything else out of scope, run eagerly).
+* with the gradient reducer on (world > 1, or ``--force-reducer``), the bucket all-reduces
+  the backward hooks launch -- RCCL collectives on the side / comm streams, or the xGMI kernel
+  -- and the stats all-reduce are captured as graph nodes; the per-parameter used flags of
+  ``--find-unused-parameters`` are host-known at capture time and identical on every replay of
+  the shape, so they ride in the stats vector as fill nodes (reference DDP setting of the NER
+  runs: hetseq/controller.py:79-87, run_bert_fine_tuning_ner.sh:36).
+
+Scope: one micro-batch per update, fp32 or bf16; with the reducer, an RCCL (``nccl``) process
+group (gloo collectives are host-driven and cannot be captured).  Each distinct input shape is
+warmed up eagerly ``warmup`` times, then captured into a graph that shares one memory pool with
+the others (``max_graphs`` shapes at most; later new shapes, and anything else out of scope,
+run eagerly).
 """
 import collections
 
@@ -52,6 +60,17 @@ def _clone_structure(sample):
     return sample
 
 
+def _capturable_group(c):
+    """The reducer's collectives (and the stats all-reduce) can be captured: an RCCL group."""
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        return False
+    try:
+        return dist.get_backend(c.reducer.group) == 'nccl'
+    except Exception:
+        return False
+
+
 class _Entry(object):
     __slots__ = ('graph', 'static', 'out', 'meter_args', 'runs_sig')
 
@@ -75,7 +94,9 @@ class GraphedTrainStep(object):
     # ------------------------------------------------------------------ eligibility
     def _eligible(self, samples):
         c = self.ctrl
-        if len(samples) != 1 or samples[0] is None or c.reducer.enabled or c._profile_phases:
+        if len(samples) != 1 or samples[0] is None or c._profile_phases:
+            return False
+        if c.reducer.enabled and not _capturable_group(c):
             return False
         return not getattr(c.args, 'use_bmuf', False)
 

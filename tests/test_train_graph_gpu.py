@@ -95,3 +95,71 @@ def test_graph_step_matches_eager_ner_shapes(dev, tmp_path):
     gs = graph[0]._graph_step
     assert gs.captures >= 2, gs.captures
     _compare(eager, graph, 1e-4)
+
+
+REDUCER_GRAPH_SCRIPT = r'''
+import sys, torch, torch.distributed as dist
+from hetseq_9cme_amd import options, tasks
+from hetseq_9cme_amd.controller import Controller
+from hetseq_9cme_amd.data import iterators
+argv = sys.argv[2:]
+torch.cuda.set_device(0)
+dist.init_process_group('nccl', init_method=sys.argv[1], world_size=1, rank=0)
+res = []
+for extra in ([], ['--graph-train-step']):
+    args = options.parse_training_args(argv + extra)
+    args.device_id, args.distributed_rank = 0, 0
+    torch.manual_seed(args.seed)
+    task = tasks.setup_task(args)
+    ctrl = Controller(args, task, task.build_model(args))
+    assert ctrl.reducer.enabled
+    ep = ctrl.get_train_iterator(epoch=0, load_dataset=True)
+    ctrl.lr_step(ep.epoch)
+    itr = iterators.GroupedIterator(ep.next_epoch_itr(shuffle=False), 1)
+    losses = [float(ctrl.train_step(next(itr))['loss']) for _ in range(24)]
+    torch.cuda.synchronize()
+    st = {k: v.detach().float().cpu().clone() for k, v in ctrl.get_model().state_dict().items()}
+    res.append((ctrl, losses, st))
+gs = res[1][0]._graph_step
+print('captures', gs.captures, 'replays', gs.replays)
+assert gs.captures >= 2 and gs.replays >= 8, (gs.captures, gs.replays)
+for a, b in zip(res[0][1], res[1][1]):
+    assert abs(a - b) <= 1e-4 * max(1.0, abs(a)), (res[0][1], res[1][1])
+for k, v in res[0][2].items():
+    d = (v - res[1][2][k]).abs().max().item()
+    assert d <= 1e-4 * max(1.0, v.abs().max().item()), (k, d)
+dist.destroy_process_group()
+print('GRAPH-REDUCER OK')
+'''
+
+
+def test_graph_step_with_rccl_reducer_ner(dev, tmp_path):
+    """--graph-train-step with the gradient reducer on (a one-rank RCCL group, --force-reducer,
+    --find-unused-parameters: the NER runs' DDP settings, run_bert_fine_tuning_ner.sh:36): the
+    bucket collectives, the stats all-reduce and the used flags are captured into the update
+    graph, and the replayed updates match eager reducer updates on the same batches (to the
+    word-embedding scatter's atomics)."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    from hetseq_9cme_amd.data.synthetic import (BERT_TINY, WORDS, write_bert_config, write_synthetic_conll,
+                                                write_vocab)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    vocab = write_vocab(str(tmp_path / 'vocab.txt'), 1024, extra_words=WORDS)
+    cfg = write_bert_config(str(tmp_path / 'c.json'), **BERT_TINY)
+    tr = write_synthetic_conll(str(tmp_path / 'train.txt'), 40 * 8, seed=0, min_len=4, max_len=40)
+    argv = ['--task', 'BertForTokenClassification', '--optimizer', 'adam', '--fast-stat-sync', '--lr', '1e-4',
+            '--dict', vocab, '--config_file', cfg, '--train_file', tr, '--extension_file', 'conll',
+            '--max-sentences', '8', '--num-workers', '1', '--find-unused-parameters', '--disable-validation',
+            '--no-save', '--pad-to-multiple-of', '16', '--force-reducer', '--distributed-world-size', '1',
+            '--distributed-backend', 'nccl', '--bucket-cap-mb', '1']
+    script = tmp_path / 'graph_reducer.py'
+    script.write_text(REDUCER_GRAPH_SCRIPT)
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    r = subprocess.run([sys.executable, str(script), 'tcp://127.0.0.1:{}'.format(port)] + argv,
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                       env=dict(os.environ, PYTHONPATH=root), timeout=300)
+    assert r.returncode == 0 and 'GRAPH-REDUCER OK' in r.stdout, r.stdout[-4000:]

@@ -41,6 +41,11 @@ def main():
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'])
     ap.add_argument('--same-device', action='store_true', help='rehearsal: every rank on GPU 0')
     ap.add_argument('--model', default='base', choices=['base', 'tiny'])
+    ap.add_argument('--fp32-gemm', default=None, choices=['native', 'bf16x3', 'bf16x6', 'fp16x3'],
+                    help='fp32 GEMM mode (default: the framework default)')
+    ap.add_argument('--force-reducer', action='store_true',
+                    help='one GPU: run the gradient reducer on a one-rank RCCL group (buckets, used flags in the '
+                         'stats all-reduce) -- with --graph-train-step, captured into the update graph')
     a = ap.parse_args()
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -76,12 +81,24 @@ def main():
         argv.append('--graph-train-step')
     if a.no_overlap_wgrad:
         argv.append('--no-overlap-wgrad')
+    if a.fp32_gemm:
+        argv += ['--fp32-gemm', a.fp32_gemm]
+    if a.force_reducer:
+        argv.append('--force-reducer')
     args = options.parse_training_args(argv + ['--distributed-world-size', str(world)])
     args.device_id = dev
     args.distributed_backend = a.backend
     if world > 1:
         args.distributed_init_method = 'env://'
         args.distributed_rank = rank
+        dist_utils.distributed_init(args)
+    elif a.force_reducer:
+        import socket
+        with socket.socket() as sk:
+            sk.bind(('127.0.0.1', 0))
+            port = sk.getsockname()[1]
+        args.distributed_init_method = 'tcp://127.0.0.1:{}'.format(port)
+        args.distributed_rank = 0
         dist_utils.distributed_init(args)
     else:
         args.distributed_rank = 0
@@ -139,11 +156,13 @@ def main():
                           'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
                           'reference_1gpu': 0.214, 'speedup_vs_reference': round(0.214 / dt, 1),
                           'batch': a.batch, 'global_batch': a.batch * world, 'dtype': a.precision,
-                          'graph_train_step': a.graph_train_step,
+                          'graph_train_step': a.graph_train_step, 'force_reducer': a.force_reducer,
+                          'fp32_gemm': args.fp32_gemm if a.precision == 'fp32' else None,
+                          'graph_replays': gs.replays if gs is not None else 0,
                           'parallelism': 'dp{}'.format(world) + (' (find-unused-parameters)' if world > 1 else ''),
                           'data': 'synthetic CoNLL-format sentences (8-40 words), random-init BERT-{}'.format(
                               a.model)}), flush=True)
-    if world > 1:
+    if world > 1 or a.force_reducer:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
 

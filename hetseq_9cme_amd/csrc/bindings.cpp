@@ -900,7 +900,7 @@ static HxGemmF16 f16_args(const Tensor& a, const Tensor& aa, const Tensor& b, co
   check_amax(ba, a, what);
   TORCH_CHECK(b.device() == a.device() && b.size(0) < (1LL << 31), what, ": operands on one device");
   HxGemmF16 p{};
-  p.A = a.data_ptr<float>();
+  p.A = a.data_ptr();
   p.lda = a.stride(0);
   p.a_amax = aa.data_ptr<float>();
   p.na = (int)aa.numel();
@@ -1042,6 +1042,74 @@ Tensor wgrad_f16(Tensor dy, Tensor dy_amax, Tensor x, Tensor x_amax, Tensor out)
                            cfg, nsplit, (int)out.size(0), cur_stream(dy)) == 0,
               "wgrad_f16: launch failed");
   dbg_finite(out, "wgrad_f16");
+  return out;
+}
+
+// --precision bf16 on the same kernel: out (+)= a . b^T (+ bias), a bf16 [M, K], b bf16 [N, K]
+// (contiguous); the output is bf16 (out_bf16) or fp32
+Tensor gemm_bf16(Tensor a, Tensor b, OptT out_, bool beta, OptT bias, bool out_bf16) {
+  TORCH_CHECK(a.is_cuda() && a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16 &&
+                  a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && a.stride(0) % 8 == 0 &&
+                  aligned16(a.data_ptr()) && b.is_contiguous() && aligned16(b.data_ptr()) && a.size(1) == b.size(1) &&
+                  a.size(1) % 32 == 0 && a.device() == b.device(),
+              "gemm_bf16: a [M, K] / b [N, K] bf16 with 16-B rows, K % 32 == 0");
+  HxGemmF16 p{};
+  p.A = a.data_ptr();
+  p.lda = a.stride(0);
+  p.B = reinterpret_cast<const uint16_t*>(b.data_ptr());
+  p.ldb = b.size(1);
+  p.M = (int)a.size(0);
+  p.N = (int)b.size(0);
+  p.K = (int)a.size(1);
+  p.ks = 1;
+  p.abf16 = 1;
+  p.obf16 = out_bf16 ? 1 : 0;
+  check_vec(bias, p.N, "gemm_bf16 bias");
+  const int cfg = hx_gemm_f16_plan(p.M, p.N, p.K);
+  TORCH_CHECK(cfg >= 0, "gemm_bf16: no tile for N = ", p.N);
+  TORCH_CHECK(!beta || has(out_), "gemm_bf16: beta needs an output to accumulate into");
+  Tensor out = has(out_) ? *out_ : torch::empty({p.M, p.N}, a.options().dtype(out_bf16 ? torch::kBFloat16
+                                                                                       : torch::kFloat32));
+  TORCH_CHECK(out.scalar_type() == (out_bf16 ? torch::kBFloat16 : torch::kFloat32) && out.dim() == 2 &&
+                  out.size(0) == p.M && out.size(1) == p.N && out.stride(1) == 1 && out.stride(0) % 8 == 0 &&
+                  aligned16(out.data_ptr()),
+              "gemm_bf16: out [M, N] of the output dtype with 16-B rows");
+  p.C = reinterpret_cast<float*>(out.data_ptr());
+  p.ldc = out.stride(0);
+  p.beta = beta ? 1 : 0;
+  p.bias = ptr_or_null<float>(bias);
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  TORCH_CHECK(hx_gemm_f16(p, cfg, cur_stream(a)) == 0, "gemm_bf16: launch failed");
+  dbg_finite(out, "gemm_bf16");
+  return out;
+}
+
+// W^T in bf16 ([K, N]) of every fp32 weight W [N, K] in the list, one launch
+std::vector<Tensor> weight_bf16_t(std::vector<Tensor> Ws) {
+  TORCH_CHECK(!Ws.empty() && Ws.size() <= HX_WBATCH, "weight_bf16_t: 1..64 weights");
+  HxWeightBatch d{};
+  d.n = (int)Ws.size();
+  std::vector<Tensor> out;
+  int tiles = 0;
+  for (int i = 0; i < d.n; ++i) {
+    const Tensor& W = Ws[i];
+    check_f32(W, "weight_bf16_t input");
+    TORCH_CHECK(W.dim() == 2 && W.is_contiguous() && W.size(0) % 64 == 0 && W.size(1) % 64 == 0 &&
+                    aligned16(W.data_ptr()) && W.device() == Ws[0].device(),
+                "weight_bf16_t: every W contiguous [N, K], N and K multiples of 64, one device");
+    Tensor wt = torch::empty({W.size(1), W.size(0)}, W.options().dtype(torch::kBFloat16));
+    d.W[i] = W.data_ptr<float>();
+    d.wt[i] = reinterpret_cast<uint16_t*>(wt.data_ptr());
+    d.wf[i] = nullptr;
+    d.N[i] = (int)W.size(0);
+    d.K[i] = (int)W.size(1);
+    d.start[i] = tiles;
+    tiles += (int)((W.size(0) / 64) * (W.size(1) / 64));
+    out.push_back(wt);
+  }
+  d.start[d.n] = tiles;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(Ws[0].device());
+  hx_weight_bf16_t(d, cur_stream(Ws[0]));
   return out;
 }
 
@@ -1256,6 +1324,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_f16_dgelu", &gemm_f16_dgelu, py::arg("a"), py::arg("a_amax"), py::arg("b"), py::arg("b_amax"),
         py::arg("u"), py::arg("bias") = py::none(), py::arg("dbias_out") = py::none(), py::arg("dmode") = 1);
   m.def("wgrad_f16", &wgrad_f16);
+  m.def("gemm_bf16", &gemm_bf16, py::arg("a"), py::arg("b"), py::arg("out") = py::none(), py::arg("beta") = false,
+        py::arg("bias") = py::none(), py::arg("out_bf16") = true);
+  m.def("weight_bf16_t", &weight_bf16_t);
+
   m.def("gemm_f16_plan", &hx_gemm_f16_plan);
   m.def("gemm_f16_ks", &hx_gemm_f16_ks);
   m.def("gemm_f16_tiles", &hx_gemm_f16_tiles);

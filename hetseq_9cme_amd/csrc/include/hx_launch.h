@@ -172,7 +172,7 @@ void hx_fold_cols(const float* partial, int rows, int N, float* out, int accumul
 // kind 2: t = s acc * (dmode ? aux : gelu'(aux + bias)) -> P fp32, amax_out, colpart
 //         [hx_gemm_f16_colpart_rows][N] per-wave column sums of t
 struct HxGemmF16 {
-  const float* A;
+  const void* A;     // fp32, or bf16 when abf16 (then B is bf16 [N][K] and there is no scaling)
   int64_t lda;
   const float* a_amax;
   int na;
@@ -192,7 +192,10 @@ struct HxGemmF16 {
   float* amax_out;
   int dmode, ks;
   int64_t c_zs;
+  int abf16, obf16;   // --precision bf16: bf16 operands (one pass), bf16 output C (kind 0)
 };
+// --precision bf16: W^T [K][N] bf16 of every weight of a batch (wt used, wf / mask ignored)
+void hx_weight_bf16_t(const HxWeightBatch& d, hipStream_t s);
 int hx_gemm_f16_plan(int M, int N, int K);
 int hx_gemm_f16_tiles(int M, int N, int cfg);
 int hx_gemm_f16_colpart_rows(int M, int cfg);

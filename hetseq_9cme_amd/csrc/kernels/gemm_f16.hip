@@ -42,6 +42,8 @@ namespace {
 
 using namespace hx::g;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 
@@ -50,7 +52,7 @@ __device__ __forceinline__ f32x16 mfma16(const f16x8& a, const f16x8& b, const f
 }
 
 struct F16Args {
-  const float* A;
+  const void* A;   // fp32 (AT 0) or bf16 (AT 1)
   int64_t lda;
   const float* a_amax;
   int na;
@@ -73,8 +75,15 @@ struct F16Args {
   int64_t c_zs;
 };
 
-template <int BM, int BN, int WM, int WN, int EPI, int OCC>
+// AT 0: fp32 A split into two scaled fp16 pieces, B = fp16 P2 pieces, three passes (fp16x3);
+// AT 1: --precision bf16: A and B bf16 [rows][K] (32-deep k steps: again 64 B per row), one pass;
+//       OB: the output C in bf16 (EPI 0 / 3 only)
+template <int BM, int BN, int WM, int WN, int EPI, int OCC, int AT = 0, int OB = 0>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F16Args g) {
+  static_assert(AT == 0 || EPI == 0 || EPI == 3, "bf16 operands: plain / beta epilogues");
+  static_assert(OB == 0 || AT == 1, "bf16 output with bf16 operands");
+  constexpr int KD = AT ? 32 : 16;       // k elements per stage
+  constexpr int AE = AT ? 2 : 4;         // A element bytes
   constexpr int NWM = BM / WM, NW = NWM * (BN / WN), NT = NW * 64;
   constexpr int MB = WM / 32, NB = WN / 32;
   constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64, STAGE = A_BYTES + B_BYTES;
@@ -92,14 +101,14 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
   const int z = work0 / total, work = work0 - z * total;
   const int nt = work % TN, mt = work / TN;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int nit = g.K / 16 / g.ks, it0 = z * nit;
+  const int nit = g.K / KD / g.ks, it0 = z * nit;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w % NWM, wn = w / NWM, h = lane >> 5, l32 = lane & 31;
   const int wv = __builtin_amdgcn_readfirstlane(w);
 
   const int mrows = min(BM, g.M - m0);
-  const u32x4 ra = rsrc_of(g.A + (int64_t)m0 * g.lda, (uint32_t)((int64_t)mrows * g.lda * 4));
+  const u32x4 ra = rsrc_of((const char*)g.A + (int64_t)m0 * g.lda * AE, (uint32_t)((int64_t)mrows * g.lda * AE));
   const u32x4 rb = rsrc_of(g.B + (int64_t)n0 * g.ldb, (uint32_t)((int64_t)BN * g.ldb * 2));
 
   // this wave's DMA pieces q = wv + NW j of a stage: [A pieces (16 rows of fp32) | B pieces]
@@ -112,7 +121,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
   for (int j = 0; j < JHI; ++j) {
     const int q = wv + NW * j;
     isa[j] = q < KA;
-    if (q < KA) voff[j] = (uint32_t)(((int64_t)(q * 16 + rl) * g.lda + 4 * ch) * 4);
+    if (q < KA) voff[j] = (uint32_t)(((int64_t)(q * 16 + rl) * g.lda + (16 / AE) * ch) * AE);
     else voff[j] = (uint32_t)(((int64_t)((q - KA) * 16 + rl) * g.ldb + 8 * ch) * 2);
     dsto[j] = 1024 * q;
   }
@@ -153,8 +162,8 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
   dma(0, 0);
   if (nit > 1) dma(1, 1);
   // operand scales (their loads over-wait the DMAs above: harmless)
-  const int Ea = f16_scale_exp(block_amax(g.a_amax, g.na, red));
-  const int Eb = f16_scale_exp(block_amax(g.b_amax, g.nb, red));
+  const int Ea = AT ? 0 : f16_scale_exp(block_amax(g.a_amax, g.na, red));
+  const int Eb = AT ? 0 : f16_scale_exp(block_amax(g.b_amax, g.nb, red));
   const float sa = ldexpf(1.f, Ea), ia = ldexpf(1.f, -Ea), ib = ldexpf(1.f, -Eb);
   if (nit > 1) wait_stage();
   else dma_wait<0>();
@@ -170,6 +179,35 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
   for (int it = 0; it < nit; ++it) {
     const int nxt2 = cur == 0 ? 2 : cur - 1;
     const char* st = lds + cur * STAGE;
+    const int dit = it + 2 < nit ? it + 2 : -1;
+    if constexpr (AT == 1) {
+      // two 16-deep bf16 k steps per stage, one MFMA pass each; the next-next stage's DMA pieces
+      // between them
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8v fa[MB], fb[NB];
+#pragma unroll
+        for (int a = 0; a < MB; ++a)
+          fa[a] = *reinterpret_cast<const bf16x8v*>(st + img_off(wm * WM + 32 * a + l32, 2 * ks + h));
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          fb[b] = *reinterpret_cast<const bf16x8v*>(st + A_BYTES + img_off(wn * WN + 32 * b + l32, 2 * ks + h));
+#pragma unroll
+        for (int a = 0; a < MB; ++a)
+#pragma unroll
+          for (int b = 0; b < NB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
+        if (dit >= 0) {
+#pragma unroll
+          for (int j = ks; j < JHI; j += 2) {
+            if (j < JLO || j < cnt) {
+              __builtin_amdgcn_sched_barrier(0);
+              dma_one(dit, nxt2, j);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          }
+        }
+      }
+    } else {
     f16x8 a0[MB], a1[MB], b0[NB], b1[NB];
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -183,7 +221,6 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
       const f32x8 y = f32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]} * sa;
       split2(y, a0[a], a1[a]);
     }
-    const int dit = it + 2 < nit ? it + 2 : -1;
     // pass q, then this wave's DMA pieces j = q, q + 3, ... of stage it + 2
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -202,6 +239,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
           }
         }
       }
+    }
     }
     if (it + 2 < nit) wait_stage();
     else dma_wait<0>();
@@ -228,7 +266,33 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
     if (g.bias) t = *reinterpret_cast<const float4*>(g.bias + n0 + ncol + 32 * b);
     bias[b][0] = t.x; bias[b][1] = t.y; bias[b][2] = t.z; bias[b][3] = t.w;
   }
-  if constexpr (EPI == 0 || EPI == 3) {
+  if constexpr (OB == 1) {
+    // bf16 output [M][ldc]: 4 consecutive columns of a row per lane -> one 8-B store
+    const hx::Buf obuf(reinterpret_cast<uint16_t*>(g.C) + (int64_t)m0 * g.ldc + n0, (uint32_t)((int64_t)mrows * g.ldc * 2));
+#pragma unroll
+    for (int a = 0; a < MB; ++a) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) {
+          float v[4];
+          tr(a, b, gq, v);
+          const uint32_t off = (uint32_t)((mrow + 32 * a + 8 * gq) * g.ldc + ncol + 32 * b) * 2;
+          float o[4] = {v[0] + bias[b][0], v[1] + bias[b][1], v[2] + bias[b][2], v[3] + bias[b][3]};
+          if constexpr (EPI == 3) {
+            const u32x2 c = __builtin_amdgcn_raw_buffer_load_b64(obuf.r, off, 0, 0);
+            o[0] += hx::bf2f((uint16_t)(c[0] & 0xffff));
+            o[1] += hx::bf2f((uint16_t)(c[0] >> 16));
+            o[2] += hx::bf2f((uint16_t)(c[1] & 0xffff));
+            o[3] += hx::bf2f((uint16_t)(c[1] >> 16));
+          }
+          const uint2 pk = make_uint2(hx::f2bf(o[0]) | ((uint32_t)hx::f2bf(o[1]) << 16),
+                                      hx::f2bf(o[2]) | ((uint32_t)hx::f2bf(o[3]) << 16));
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, pk), obuf.r, off, 0, 0);
+        }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  } else if constexpr (EPI == 0 || EPI == 3) {
 #pragma unroll
     for (int a = 0; a < MB; ++a) {
 #pragma unroll
@@ -352,7 +416,7 @@ int cfg_bm(int c) { return c <= 1 ? 256 : c == 2 ? 128 : 64; }
 int cfg_bn(int c) { return c <= 1 ? 192 : c == 2 ? 96 : 64; }
 int cfg_nwm(int c) { return c == 0 ? 8 : c == 1 ? 4 : c == 2 ? 4 : 2; }
 
-template <int BM, int BN, int WM, int WN, int EPI>
+template <int BM, int BN, int WM, int WN, int EPI, int AT = 0, int OB = 0>
 void launch_one(const F16Args& a, hipStream_t s) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int total = ((a.M + BM - 1) / BM) * (a.N / BN) * a.ks;
@@ -360,19 +424,19 @@ void launch_one(const F16Args& a, hipStream_t s) {
   const size_t smem = (size_t)3 * (BM + BN) * 64;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_f16_k<BM, BN, WM, WN, EPI, 1>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_f16_k<BM, BN, WM, WN, EPI, 1, AT, OB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
-  gemm_f16_k<BM, BN, WM, WN, EPI, 1><<<8 * per, NT, smem, s>>>(a);
+  gemm_f16_k<BM, BN, WM, WN, EPI, 1, AT, OB><<<8 * per, NT, smem, s>>>(a);
 }
 
-template <int EPI>
+template <int EPI, int AT = 0, int OB = 0>
 void launch_cfg(int cfg, const F16Args& a, hipStream_t s) {
-  if (cfg == 0) launch_one<256, 192, 32, 192, EPI>(a, s);
-  else if (cfg == 1) launch_one<256, 192, 64, 96, EPI>(a, s);
-  else if (cfg == 2) launch_one<128, 96, 32, 96, EPI>(a, s);
-  else launch_one<64, 64, 32, 32, EPI>(a, s);
+  if (cfg == 0) launch_one<256, 192, 32, 192, EPI, AT, OB>(a, s);
+  else if (cfg == 1) launch_one<256, 192, 64, 96, EPI, AT, OB>(a, s);
+  else if (cfg == 2) launch_one<128, 96, 32, 96, EPI, AT, OB>(a, s);
+  else launch_one<64, 64, 32, 32, EPI, AT, OB>(a, s);
 }
 
 // ---------------------------------------------------------------- weight gradient (tokens = reduction)
@@ -675,7 +739,45 @@ __global__ __launch_bounds__(256) void split_weight_f16_k(HxWeightBatch d, const
   }
 }
 
+// --precision bf16: W [N][K] fp32 -> W^T [K][N] bf16 (RNE, as the bf16 shadow), every weight of a
+// batch in one launch, 64 x 64 tiles transposed through LDS
+__global__ __launch_bounds__(256) void weight_bf16_t_k(HxWeightBatch d) {
+  __shared__ uint16_t tile[64][66];
+  const int blk = blockIdx.x;
+  int i = 0;
+  while (i + 1 < d.n && blk >= d.start[i + 1]) ++i;   // uniform per workgroup
+  const int N = d.N[i], K = d.K[i];
+  const int tk = K / 64, loc = blk - d.start[i];
+  const int k0 = (loc % tk) * 64, n0 = (loc / tk) * 64;
+  const float* W = d.W[i];
+  const int t = threadIdx.x, c4 = (t & 15) * 4;
+#pragma unroll
+  for (int r4 = 0; r4 < 4; ++r4) {
+    const int r = (t >> 4) + 16 * r4;
+    const float4 v = *reinterpret_cast<const float4*>(W + (int64_t)(n0 + r) * K + k0 + c4);
+    tile[r][c4] = hx::f2bf(v.x);
+    tile[r][c4 + 1] = hx::f2bf(v.y);
+    tile[r][c4 + 2] = hx::f2bf(v.z);
+    tile[r][c4 + 3] = hx::f2bf(v.w);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r4 = 0; r4 < 4; ++r4) {
+    const int kk = (t >> 4) + 16 * r4;
+    uint16_t q[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) q[j] = tile[c4 + j][kk];
+    *reinterpret_cast<uint2*>(d.wt[i] + (int64_t)(k0 + kk) * N + n0 + c4) =
+        make_uint2(q[0] | ((uint32_t)q[1] << 16), q[2] | ((uint32_t)q[3] << 16));
+  }
+}
+
 }  // namespace
+
+void hx_weight_bf16_t(const HxWeightBatch& d, hipStream_t s) {
+  if (d.n < 1) return;
+  weight_bf16_t_k<<<d.start[d.n], 256, 0, s>>>(d);
+}
 
 // ---------------------------------------------------------------- host API (hx_launch.h)
 int hx_gemm_f16_plan(int M, int N, int K) {
@@ -711,11 +813,14 @@ int hx_gemm_f16_ks(int M, int N, int K, int cfg) {
 }
 
 int hx_gemm_f16(const HxGemmF16& p, int cfg, hipStream_t s) {
-  if (cfg < 0 || cfg >= kCfgs || p.M < 1 || p.N % cfg_bn(cfg) || p.K % 16 || p.lda % 4 || p.ldb != 2 * (int64_t)p.K)
+  const int kd = p.abf16 ? 32 : 16;
+  if (cfg < 0 || cfg >= kCfgs || p.M < 1 || p.N % cfg_bn(cfg) || p.K % kd || p.lda % (p.abf16 ? 8 : 4) ||
+      p.ldb != (p.abf16 ? 1 : 2) * (int64_t)p.K)
     return -1;
   const int ks = p.ks < 1 ? 1 : p.ks;
-  if (p.K % (16 * ks) || (ks > 1 && (p.beta || p.kind || p.bias || p.c_zs < (int64_t)(p.M - 1) * p.ldc + p.N)))
+  if (p.K % (kd * ks) || (ks > 1 && (p.beta || p.kind || p.bias || p.obf16 || p.c_zs < (int64_t)(p.M - 1) * p.ldc + p.N)))
     return -1;
+  if ((p.abf16 && p.kind) || (p.obf16 && (!p.abf16 || p.ldc % 4))) return -1;
   if (p.kind < 0 || p.kind > 2 || (p.kind && (!p.P || p.beta || p.ldp % 4)) || (p.kind == 2 && !p.aux)) return -1;
   F16Args a;
   a.A = p.A;
@@ -742,6 +847,13 @@ int hx_gemm_f16(const HxGemmF16& p, int cfg, hipStream_t s) {
   a.dmode = p.dmode;
   a.ks = ks;
   a.c_zs = p.c_zs;
+  if (p.abf16) {
+    if (p.obf16 && p.beta) launch_cfg<3, 1, 1>(cfg, a, s);
+    else if (p.obf16) launch_cfg<0, 1, 1>(cfg, a, s);
+    else if (p.beta) launch_cfg<3, 1, 0>(cfg, a, s);
+    else launch_cfg<0, 1, 0>(cfg, a, s);
+    return 0;
+  }
   if (p.kind == 0 && !p.beta) launch_cfg<0>(cfg, a, s);
   else if (p.kind == 0) launch_cfg<3>(cfg, a, s);
   else if (p.kind == 1) launch_cfg<1>(cfg, a, s);

@@ -149,6 +149,20 @@ def _dgrad(dy2, W, xshape, mbox):
     return dx if other is None else dx + other.view(xshape).to(dx.dtype)
 
 
+def _dgrad_bf16(dy2, W, xshape, mbox):
+    """``_dgrad`` for --precision bf16 on the hand-written kernel: dy . (W^T)^T with the bf16 W^T
+    of the running forward, beta = 1 into the deposited residual gradient if any."""
+    wt = gemm16.bf16_wt(W)
+    dy2 = gemm16.rows2(dy2)
+    if mbox is not None:
+        g, other = mbox.take(dy2.dtype)
+        if g is not None:
+            return gemm16.mm_bf16(dy2, wt, out=g.view(-1, W.shape[1]), beta=True).view(xshape)
+        dx = gemm16.mm_bf16(dy2, wt).view(xshape)
+        return dx if other is None else dx + other.view(xshape).to(dx.dtype)
+    return gemm16.mm_bf16(dy2, wt).view(xshape)
+
+
 def _dgrad_pieces(dys, wt, xshape, mbox):
     """``_dgrad`` from dy's pieces and W^T's pieces (hand-written piece GEMM, beta = 1 into
     the deposited residual gradient)."""
@@ -519,7 +533,11 @@ class _LinearFn(torch.autograd.Function):
                 y.add_(b)
         else:
             Wc = cast_w(W, x.dtype)
-            y = torch.mm(x2, Wc.t()) if b is None else torch.addmm(cast_w(b, x.dtype), x2, Wc.t())
+            ctx.b16 = gemm16.bf16_ok(x2, W.shape[0], W.shape[1]) and Wc.is_contiguous()
+            if ctx.b16:   # --precision bf16 on the hand-written kernel (bias in the epilogue)
+                y = gemm16.mm_bf16(gemm16.rows2(x), Wc, bias=b)
+            else:
+                y = torch.mm(x2, Wc.t()) if b is None else torch.addmm(cast_w(b, x.dtype), x2, Wc.t())
         ctx.save_for_backward(x2, Wsave)
         ctx.W = W
         ctx.b = b
@@ -546,6 +564,8 @@ class _LinearFn(torch.autograd.Function):
             dx = _dgrad_pieces(dys, Wsaved, ctx.xshape, ctx.mbox)
         elif ctx.split:
             dx = _dgrad_split(dys, W, ctx.xshape, ctx.mbox)
+        elif getattr(ctx, 'b16', False):
+            dx = _dgrad_bf16(dy2, W, ctx.xshape, ctx.mbox)
         else:
             dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox)
         if ctx.defer is not None:   # dW is computed (grouped) by the joining linear's backward
@@ -817,6 +837,8 @@ def weight_pieces_scope(Ws, x):
     activations ``x`` [.., H] (``split_gemm.producer_pieces``), else a no-op context.
     ``HX_WSPLIT_BATCH=0`` turns the batch split off."""
     import contextlib
+    if torch.is_tensor(x) and x.dtype == torch.bfloat16 and use_kernels(x):
+        return gemm16.bf16_scope(Ws)   # --precision bf16: W^T copies for the data gradients
     if os.environ.get('HX_WSPLIT_BATCH', '1') == '0' or not torch.is_tensor(x) or x.dtype != torch.float32:
         return contextlib.nullcontext()
     if gemm16.enabled():
@@ -881,7 +903,11 @@ class _Linear3Fn(torch.autograd.Function):
                 y.add_(b)
         else:
             # without biases (applied inside the fused attention instead) this is a plain GEMM
-            y = torch.addmm(bc, x2, Wc.t()) if has_b else torch.mm(x2, Wc.t())
+            ctx.b16 = gemm16.bf16_ok(x2, W.shape[0], W.shape[1]) and Wc.is_contiguous()
+            if ctx.b16:
+                y = gemm16.mm_bf16(gemm16.rows2(x), Wc, bias=b if has_b else None)
+            else:
+                y = torch.addmm(bc, x2, Wc.t()) if has_b else torch.mm(x2, Wc.t())
         ctx.save_for_backward(x2, Wc)
         ctx.params = (wq, wk, wv, bq, bk, bv)
         ctx.has_b = has_b
@@ -921,6 +947,11 @@ class _Linear3Fn(torch.autograd.Function):
             if ctx.split:
                 dys = dep if dep is not None else split_gemm.grad_planes(dy2.float())
                 dx = _dgrad_split(dys, W, ctx.xshape, ctx.mbox, prefix=pf)
+            elif getattr(ctx, 'b16', False):
+                dys = None
+                wq_, wk_, wv_ = ctx.params[:3]
+                Wf = _adjacent_view([wq_, wk_, wv_])
+                dx = _dgrad_bf16(dy2, Wf if Wf is not None else torch.cat([wq_, wk_, wv_], 0), ctx.xshape, ctx.mbox)
             else:
                 dys = None
                 dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox)

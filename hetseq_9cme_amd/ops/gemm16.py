@@ -164,3 +164,53 @@ def gemm_dgelu(dy2, dparts, wt2, parts2, d, dbias_out):
     """FFN-down data gradient with the GELU backward: (t = (dy W2) * gelu'(u), max |t| partials,
     d b1)."""
     return C().gemm_f16_dgelu(dy2, dparts, wt2, parts2, d, None, dbias_out, 1)
+
+
+# ---------------------------------------------------------------- --precision bf16 (same kernel, one pass)
+class _B16(object):
+    scope = None        # {(data_ptr, shape): W^T in bf16} for the running forward
+
+
+def bf16_ok(x2, n_out, n_in):
+    """--precision bf16 products on gemm_f16.hip's bf16 variant: bf16 GPU activations, 32-deep k
+    steps, tile-able widths (the tiny heads stay on the library GEMM)."""
+    return (x2.dtype == torch.bfloat16 and use_kernels(x2) and n_in % 64 == 0 and n_out % 64 == 0 and
+            x2.numel() > 0)
+
+
+class bf16_scope(object):
+    """W^T in bf16 for every weight in ``Ws`` (the data-gradient operands of the NT kernel), one
+    launch per forward; ``bf16_wt`` returns them until exit."""
+
+    def __init__(self, Ws):
+        self.Ws = [W for W in Ws if W is not None and W.dim() == 2 and W.shape[0] % 64 == 0 and
+                   W.shape[1] % 64 == 0 and W.is_contiguous() and W.dtype == torch.float32 and W.is_cuda]
+
+    def __enter__(self):
+        self.prev = _B16.scope
+        if self.Ws:
+            d = {}
+            for i in range(0, len(self.Ws), 64):
+                chunk = self.Ws[i:i + 64]
+                for W, wt in zip(chunk, C().weight_bf16_t(chunk)):
+                    d[(W.data_ptr(), tuple(W.shape))] = wt
+            _B16.scope = d
+        return self
+
+    def __exit__(self, *exc):
+        _B16.scope = self.prev
+        return False
+
+
+def bf16_wt(W):
+    """W^T [K, N] in bf16 (the running forward's, or converted now)."""
+    if _B16.scope is not None:
+        e = _B16.scope.get((W.data_ptr(), tuple(W.shape)))
+        if e is not None:
+            return e
+    return C().weight_bf16_t([W.detach().contiguous()])[0]
+
+
+def mm_bf16(a2, b, out=None, beta=False, bias=None, out_bf16=True):
+    """a2 [M, K] bf16 . b^T (b bf16 [N, K]) (+ out) (+ bias) on the hand-written kernel."""
+    return C().gemm_bf16(a2, b, out=out, beta=beta, bias=bias, out_bf16=out_bf16)

@@ -147,3 +147,31 @@ def test_f16_scale_extremes(dev):
         assert _rel_err(out, ref, a, W) < 4e-6, s
     z = torch.zeros(4096, 768, device=dev)
     assert C().gemm_f16(z, C().amax_rows(z), wf, parts).abs().max().item() == 0.0
+
+
+@pytest.mark.parametrize('M,N,K', [(16384, 768, 768), (16384, 3072, 768), (4096, 768, 3072), (300, 2304, 768)])
+def test_gemm_bf16_mode(dev, M, N, K):
+    """--precision bf16 on the same kernel (one bf16 pass, bf16 or fp32 output, bias / beta): against
+    the fp64 product of the same bf16 operands (only fp32 accumulation and the output rounding)."""
+    g = torch.Generator(device=dev).manual_seed(M + K)
+    a = torch.randn(M, K, device=dev, generator=g).bfloat16()
+    W = torch.randn(N, K, device=dev, generator=g) * 0.02
+    Wb = W.bfloat16()
+    bias = torch.randn(N, device=dev, generator=g)
+    ref = a.double() @ Wb.double().t() + bias.double()
+    den = a.double().abs() @ Wb.double().abs().t() + bias.double().abs()
+    out32 = C().gemm_bf16(a, Wb, bias=bias, out_bf16=False)
+    assert ((out32.double() - ref).abs() / den).max().item() < 1e-5
+    out16 = C().gemm_bf16(a, Wb, bias=bias)
+    assert out16.dtype == torch.bfloat16
+    assert ((out16.double() - ref).abs() / den).max().item() < 8e-3
+    # data gradient through W^T (bf16 copy) with beta into a bf16 accumulator
+    wt = C().weight_bf16_t([W.contiguous()])[0]
+    assert torch.equal(wt, Wb.t().contiguous())
+    dy = torch.randn(M, N, device=dev, generator=g).bfloat16()
+    acc = torch.randn(M, K, device=dev, generator=g).bfloat16()
+    ref2 = acc.double() + dy.double() @ Wb.double()
+    den2 = acc.double().abs() + dy.double().abs() @ Wb.double().abs()
+    out = acc.clone()
+    C().gemm_bf16(dy, wt, out=out, beta=True)
+    assert ((out.double() - ref2).abs() / den2).max().item() < 8e-3

@@ -1078,6 +1078,14 @@ class _DecoderXentFn(torch.autograd.Function):
             else:
                 full, _ = split_gemm.forward(h, W, rpad=Vp)
             logits = full[:, :V]
+        elif gemm16.bf16_ok(h, 64, W.shape[1]) and h.is_contiguous():
+            # --precision bf16 on the hand-written kernel: vocabulary padded to a multiple of 768
+            # (zero rows), bf16 logits as before
+            V = W.shape[0]
+            Vp = (V + 767) // 768 * 768
+            ctx.b16 = True
+            full = gemm16.mm_bf16(h, _padded_rows(cast_w(W, torch.bfloat16), Vp))
+            logits = full[:, :V]
         else:
             full = logits = torch.mm(h, cast_w(W, h.dtype).t())
         loss_rows = C().softmax_xent_(logits, bias, labels, -1)   # logits <- softmax - onehot
@@ -1137,10 +1145,20 @@ class _DecoderXentFn(torch.autograd.Function):
             else:
                 dW = torch.mm(a.t(), b, out_dtype=torch.float32)
             return dh, dW, dbias, None
-        dh = torch.mm(dl, cast_w(Wp, dl.dtype)).mul_(scale.to(dl.dtype))
+        if getattr(ctx, 'b16', False):
+            # dl over the padded vocabulary (padding columns 0) against the padded W^T in bf16
+            wt = C().weight_bf16_t([_padded_rows(Wp, dl_full.shape[1])])[0]
+            dh = gemm16.mm_bf16(dl_full, wt).mul_(scale.to(dl.dtype))
+        else:
+            dh = torch.mm(dl, cast_w(Wp, dl.dtype)).mul_(scale.to(dl.dtype))
         side = side_begin(dl.device) if slot is not None else None
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            dW = _wgrad(dl, hs, slot)
+            if getattr(ctx, 'b16', False) and C().wgrad_bf16_ok(dl_full, hs):
+                # over the padded vocabulary (whole 128-row tiles); rows past V are not stored
+                out = slot if slot is not None else torch.empty(Wp.shape[0], hs.shape[1], device=dl.device)
+                dW = C().wgrad_bf16(dl_full, hs, out)
+            else:
+                dW = _wgrad(dl, hs, slot)
         if side is not None:
             dl.record_stream(side)
             hs.record_stream(side)
@@ -1151,11 +1169,12 @@ _PAD = {}
 
 
 def _padded_rows(W, rows):
-    """W [V, H] copied into a cached zero-padded [rows, H] buffer (the padding rows stay 0)."""
-    key = (W.device, rows, W.shape[1])
+    """W [V, H] copied into a cached zero-padded [rows, H] buffer of W's dtype (the padding rows
+    stay 0)."""
+    key = (W.device, rows, W.shape[1], W.dtype)
     buf = _PAD.get(key)
-    if buf is None or buf.shape[0] != rows:
-        buf = _PAD[key] = torch.zeros(rows, W.shape[1], device=W.device, dtype=torch.float32)
+    if buf is None:
+        buf = _PAD[key] = torch.zeros(rows, W.shape[1], device=W.device, dtype=W.dtype)
     buf[:W.shape[0]].copy_(W.detach())
     return buf
 

@@ -375,7 +375,7 @@ Tensor softmax_xent_(Tensor logits, OptT bias, Tensor labels, int64_t ignore_ind
 
 // ------------------------------------------------------------------ attention
 std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed, int64_t stream,
-                             OptT bias, bool split = false, int64_t npieces = 0) {
+                             OptT bias, bool split = false, int64_t npieces = 0, OptT amax_out = OptT()) {
   check_cuda(qkv, "qkv");
   const int bf = act_bf16(qkv);
   check_f32(mask_bias, "mask_bias");
@@ -404,7 +404,8 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
     hx_attn_fwd_x6(qkv.data_ptr<float>(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(),
                    out.data_ptr<float>(), lse.data_ptr<float>(), dm, (int)B, (int)S, (int)nh, (float)keep,
                    seed_ptr(seed), (uint64_t)stream, cur_stream(qkv),
-                   npieces ? reinterpret_cast<uint16_t*>(pcs.data_ptr()) : nullptr, (int)npieces);
+                   npieces ? reinterpret_cast<uint16_t*>(pcs.data_ptr()) : nullptr, (int)npieces,
+                   amax_ptr(amax_out, ((S + 127) / 128) * nh * B * 4, "attn_fwd_x6 amax"));
   } else {
     hx_attn_fwd(bf, qkv.data_ptr(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(), out.data_ptr(),
                 lse.data_ptr<float>(), dm, (int)B, (int)S, (int)nh, (float)keep, seed_ptr(seed), (uint64_t)stream,
@@ -417,8 +418,8 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
 // fp32 attention forward on the bf16 matrix cores (split pieces, attention_x6.hip); returns
 // {out, lse, dmask, pieces of out (npieces > 0) or an undefined tensor}
 std::vector<Tensor> attn_fwd_x6(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed,
-                                int64_t stream, OptT bias, int64_t npieces) {
-  return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, true, npieces);
+                                int64_t stream, OptT bias, int64_t npieces, OptT amax_out) {
+  return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, true, npieces, amax_out);
 }
 
 // returns {dqkv, dbias} (dbias: [3H] fp32 when bias is given -- written into dbq/dbk/dbv
@@ -1281,7 +1282,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", [](Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed, int64_t stream,
                         OptT bias) { return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, false); });
   m.def("attn_fwd_x6", &attn_fwd_x6, py::arg("qkv"), py::arg("mask_bias"), py::arg("nh"), py::arg("keep"),
-        py::arg("seed"), py::arg("stream"), py::arg("bias"), py::arg("npieces") = 0);
+        py::arg("seed"), py::arg("stream"), py::arg("bias"), py::arg("npieces") = 0, py::arg("amax_out") = py::none());
   m.def("attn_bwd", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
                        double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv) {
     return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, false);

@@ -74,7 +74,7 @@ void hx_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, float* out, 
 // opieces != nullptr: out is also written as npc bf16 pieces [B*S][npc][H]
 void hx_attn_fwd_x6(const float* qkv, const float* bias, const float* maskb, float* out, float* lse,
                     uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream,
-                    hipStream_t s, uint16_t* opieces = nullptr, int npc = 0);
+                    hipStream_t s, uint16_t* opieces = nullptr, int npc = 0, float* amax_part = nullptr);
 // planes != nullptr (S <= 128 only): dQKV goes out as npl stacked bf16 planes [B*S][npl * 3H]
 // (plane j = piece (order >> 4j) & 15) instead of fp32 dqkv
 void hx_attn_bwd_x6(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,

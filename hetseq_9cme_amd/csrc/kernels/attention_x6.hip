@@ -109,7 +109,8 @@ template <bool kDrop>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd_x6_k(
     const float* __restrict__ qkv, const float* __restrict__ qkv_bias, const float* __restrict__ maskb,
     float* __restrict__ out, float* __restrict__ lse, uint32_t* __restrict__ dmask, int S, int nh, float keep,
-    const uint64_t* __restrict__ seedp, uint64_t stream, uint16_t* __restrict__ opieces, int npc) {
+    const uint64_t* __restrict__ seedp, uint64_t stream, uint16_t* __restrict__ opieces, int npc,
+    float* __restrict__ amax_part) {
   const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   __shared__ __attribute__((aligned(16))) uint16_t Ks[3][64 * RS];   // [piece][key][dim]
   __shared__ __attribute__((aligned(16))) uint16_t Vt[3][64 * RS];   // [piece][dim][vpos(key)]
@@ -299,6 +300,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if (kDrop && Sp <= kMaxStagedTiles * 64) {
     for (int t = 0; t < nt; ++t)
       dmask[((int64_t)bh * Sp + t * 64 + lane) * (Sp >> 5) + (q0w >> 5)] = Wst[t * 256 + w * 64 + lane];
+  }
+  if (amax_part) {
+    // max |context| of this wave's 32 queries (the fp16x3 attention-output GEMM's operand
+    // scale, ops/gemm16.py): one partial per wave, rows past S count 0
+    const float il = 1.f / l_run;
+    float am = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) am = fmaxf(am, fmaxf(fabsf(o0[i] * il), fabsf(o1[i] * il)));
+    if (q >= S) am = 0.f;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+    if (lane == 0) amax_part[(((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 4 + w] = am;
   }
   if (q >= S) return;
   const float inv_l = 1.f / l_run;
@@ -797,14 +810,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
 void hx_attn_fwd_x6(const float* qkv, const float* bias, const float* maskb, float* out, float* lse,
                     uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream,
-                    hipStream_t s, uint16_t* opieces, int npc) {
+                    hipStream_t s, uint16_t* opieces, int npc, float* amax_part) {
   dim3 grid((S + 127) / 128, nh, B);
   if (keep < 1.f)
     attn_fwd_x6_k<true><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream, opieces,
-                                             npc);
+                                             npc, amax_part);
   else
     attn_fwd_x6_k<false><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream, opieces,
-                                              npc);
+                                              npc, amax_part);
 }
 
 void hx_attn_bwd_x6(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,

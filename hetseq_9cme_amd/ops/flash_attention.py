@@ -19,7 +19,7 @@ import os
 import torch
 import torch.nn.functional as F
 
-from . import split_gemm
+from . import gemm16, split_gemm
 from ._ext import C, use_kernels
 from .rng import get_rng
 
@@ -90,9 +90,13 @@ class _AttnFn(torch.autograd.Function):
             # fp32 products on the bf16 matrix cores (six piece passes, attention_x6.hip)
             B, S = qkv.shape[0], qkv.shape[1]
             npc = split_gemm.producer_pieces(B * S, qkv.shape[2] // 3, qkv)
-            out, lse, dmask, pcs = C().attn_fwd_x6(qkv, mask_bias, num_heads, keep, seed, stream, bias, npc)
-            # the attention-output projection (a piece GEMM) reads the context's pieces directly
+            am = torch.empty(((S + 127) // 128) * num_heads * B * 4, dtype=torch.float32, device=qkv.device) \
+                if gemm16.enabled() else None
+            out, lse, dmask, pcs = C().attn_fwd_x6(qkv, mask_bias, num_heads, keep, seed, stream, bias, npc, am)
+            # the attention-output projection (a piece GEMM) reads the context's pieces directly;
+            # fp16x3: the context's max |x| partials
             split_gemm.attach_pieces(out, pcs)
+            gemm16.attach(out, am)
         else:
             out, lse, dmask = C().attn_fwd(qkv, mask_bias, num_heads, keep, seed, stream, bias)
         ctx.save_for_backward(qkv, mask_bias, out, lse, dmask)

@@ -428,7 +428,7 @@ std::vector<Tensor> attn_fwd_x6(Tensor qkv, Tensor mask_bias, int64_t nh, double
 // ([B*S, len(order) * 3H]) instead of fp32; returns {planes, dbias}
 std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask,
                              int64_t nh, double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, bool split = false,
-                             const std::vector<int64_t>& order = {}) {
+                             const std::vector<int64_t>& order = {}, OptT amax_out = OptT()) {
   check_cuda(dout, "grad_output");
   check_cuda(qkv, "qkv");
   const int bf = act_bf16(qkv);
@@ -485,7 +485,8 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor o
               mask_bias.data_ptr<float>(), dout.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
               keep < 1.0 ? reinterpret_cast<const uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr,
               pl ? nullptr : dqkv.data_ptr(), dq_acc, dq_ld, (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv),
-              pl ? reinterpret_cast<uint16_t*>(planes.data_ptr()) : nullptr, porder, (int)order.size());
+              pl ? reinterpret_cast<uint16_t*>(planes.data_ptr()) : nullptr, porder, (int)order.size(),
+              (split && !pl && !multi) ? amax_ptr(amax_out, B * nh, "attn_bwd_x6 amax") : nullptr);
   if (pl) return {planes, dbias};
   if (multi && bf) dqkv.narrow(-1, 0, H).copy_(dq32);
   dbg_finite(dqkv, "attn_bwd");
@@ -1289,9 +1290,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   // fp32 attention backward on the bf16 matrix cores (split pieces, attention_x6.hip)
   m.def("attn_bwd_x6", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
-                          double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv) {
-    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, true);
-  });
+                          double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, OptT amax_out) {
+    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, true, {}, amax_out);
+  }, py::arg("dout"), py::arg("qkv"), py::arg("mask_bias"), py::arg("out"), py::arg("lse"), py::arg("dmask"),
+     py::arg("nh"), py::arg("keep"), py::arg("bias"), py::arg("dbq"), py::arg("dbk"), py::arg("dbv"),
+     py::arg("amax_out") = py::none());
   // same, dQKV written as the QKV linear's output-gradient planes (S <= 128)
   m.def("attn_bwd_x6_planes", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask,
                                  int64_t nh, double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv,

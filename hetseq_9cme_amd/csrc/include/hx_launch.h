@@ -79,7 +79,9 @@ void hx_attn_fwd_x6(const float* qkv, const float* bias, const float* maskb, flo
 // (plane j = piece (order >> 4j) & 15) instead of fp32 dqkv
 void hx_attn_bwd_x6(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,
                     const float* out, const float* lse, const uint32_t* dmask, float* dqkv, float* dq_acc, int dq_ld,
-                    int B, int S, int nh, float keep, uint16_t* planes, uint32_t order, int npl, hipStream_t s);
+                    int B, int S, int nh, float keep, uint16_t* planes, uint32_t order, int npl, hipStream_t s,
+                    float* amax_part = nullptr);
+// (amax_part, S <= 128 without planes: B * nh max |dQKV| partials, one per workgroup)
 void hx_attn_fwd(int bf16, const void* qkv, const float* bias, const float* maskb, void* out, float* lse,
                  uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream, hipStream_t s);
 // dq_acc: fp32 dQ accumulation target when S > 128 (atomics; row stride dq_ld), else unused.
@@ -88,7 +90,7 @@ void hx_attn_fwd(int bf16, const void* qkv, const float* bias, const float* mask
 void hx_attn_bwd(int kind, const void* qkv, const float* bias, float* dbq, float* dbk, float* dbv, float* dbias_part,
                  const float* maskb, const void* dout, const void* out, const float* lse, const uint32_t* dmask,
                  void* dqkv, float* dq_acc, int dq_ld, int B, int S, int nh, float keep, hipStream_t s,
-                 uint16_t* planes = nullptr, uint32_t order = 0, int npl = 0);
+                 uint16_t* planes = nullptr, uint32_t order = 0, int npl = 0, float* amax_part = nullptr);
 
 // wgrad_split.hip -- dW[M][N] (fp32) = sum over piece pairs of dY_a^T X_b (bf16 pieces of fp32
 // operands, --fp32-gemm bf16x3 / bf16x6); piece pointers share the row strides ldy / ldx.

@@ -429,8 +429,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     const float* __restrict__ qkv, const float* __restrict__ qkv_bias, float* __restrict__ dbias_part,
     const float* __restrict__ maskb, const float* __restrict__ dout, const float* __restrict__ outp,
     const float* __restrict__ lse, const uint32_t* __restrict__ dmask, float* __restrict__ dqkv,
-    float* __restrict__ dq_acc, int dq_ld, int S, int nh, float keep, PlaneOut pout) {
+    float* __restrict__ dq_acc, int dq_ld, int S, int nh, float keep, PlaneOut pout, float* __restrict__ amax_part) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  float am = 0.f;   // max |dQKV| of this block's stores (one key block per head only: fp16x3 operand scale)
   uint16_t* Kt = reinterpret_cast<uint16_t*>(smem);                       // [3][64][KTS]
   uint16_t* dSs = reinterpret_cast<uint16_t*>(smem + 3 * KT_B);           // [3][32][KTS]
   uint16_t* Qs = reinterpret_cast<uint16_t*>(smem + 3 * (KT_B + DS_B));   // [3][32][RS]
@@ -713,6 +714,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         if (q0 + r >= S) continue;
         dq[r * H3] = qa0[r] * scale;
         dq[r * H3 + 16] = qa1[r] * scale;
+        am = fmaxf(am, fmaxf(fabsf(qa0[r] * scale), fabsf(qa1[r] * scale)));
       }
     } else {
       float* dq = dqa_b + (int64_t)q0 * dq_ld + dcol;
@@ -799,6 +801,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       dk[(int64_t)key * H3 + 32 + l32] = dk1[r];
       dvp[(int64_t)key * H3 + l32] = dv0[r];
       dvp[(int64_t)key * H3 + 32 + l32] = dv1[r];
+      am = fmaxf(am, fmaxf(fmaxf(fabsf(dk0[r]), fabsf(dk1[r])), fmaxf(fabsf(dv0[r]), fabsf(dv1[r]))));
+    }
+    if (amax_part && single) {
+      __shared__ float red_am[4];
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+      if (lane == 0) red_am[w] = am;
+      __syncthreads();
+      if (tid == 0)
+        amax_part[(int64_t)blockIdx.z * gridDim.y + blockIdx.y] =
+            fmaxf(fmaxf(red_am[0], red_am[1]), fmaxf(red_am[2], red_am[3]));
     }
   }
 }
@@ -822,7 +835,8 @@ void hx_attn_fwd_x6(const float* qkv, const float* bias, const float* maskb, flo
 
 void hx_attn_bwd_x6(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,
                     const float* out, const float* lse, const uint32_t* dmask, float* dqkv, float* dq_acc, int dq_ld,
-                    int B, int S, int nh, float keep, uint16_t* planes, uint32_t order, int npl, hipStream_t s) {
+                    int B, int S, int nh, float keep, uint16_t* planes, uint32_t order, int npl, hipStream_t s,
+                    float* amax_part) {
   dim3 grid((S + 127) / 128, nh, B);
   static bool attr = false;
   if (!attr) {   // > 64 KiB of dynamic LDS needs an explicit opt-in (gfx950: 160 KiB per CU)
@@ -836,7 +850,7 @@ void hx_attn_bwd_x6(const float* qkv, const float* bias, float* dbias_part, cons
   const PlaneOut po{planes, order, npl};
 #define HX_BWD_X6(D_, P_)                                                                                        \
   attn_bwd_x6_k<D_, P_><<<grid, 256, BWD_SMEM, s>>>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv, dq_acc, \
-                                                    dq_ld, S, nh, keep, po)
+                                                    dq_ld, S, nh, keep, po, amax_part)
   if (planes) {   // S <= 128 (one key block: every dQ row complete in one workgroup), checked by the caller
     if (keep < 1.f) HX_BWD_X6(true, true);
     else HX_BWD_X6(false, true);

@@ -126,9 +126,17 @@ class _AttnFn(torch.autograd.Function):
                                                       keep, ctx.bias, *slots, list(order))
             from .fused import _zero_scalar
             dqkv = _zero_scalar(qkv.device, qkv.dtype).expand(qkv.shape)
+        elif ctx.split and _X6_BWD:
+            # fp16x3 with one key block (S <= 128): the kernel writes max |dQKV| partials for the QKV
+            # projection's data / weight gradient GEMMs
+            am = torch.empty(qkv.shape[0] * num_heads, dtype=torch.float32, device=qkv.device) \
+                if gemm16.enabled() and qkv.shape[1] <= 128 else None
+            dqkv, dbias = C().attn_bwd_x6(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep,
+                                          ctx.bias, *slots, am)
+            gemm16.attach(dqkv, am)
         else:
-            bwd = C().attn_bwd_x6 if ctx.split and _X6_BWD else C().attn_bwd
-            dqkv, dbias = bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep, ctx.bias, *slots)
+            dqkv, dbias = C().attn_bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep, ctx.bias,
+                                       *slots)
         if ctx.bias is None:
             return dqkv, None, None, None, None, None, None, None
         if slots[0] is not None:

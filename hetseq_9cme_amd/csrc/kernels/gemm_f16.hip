@@ -781,12 +781,13 @@ void hx_weight_bf16_t(const HxWeightBatch& d, hipStream_t s) {
 
 // ---------------------------------------------------------------- host API (hx_launch.h)
 int hx_gemm_f16_plan(int M, int N, int K) {
-  (void)K;
   if (const char* e = getenv("HX_GEMM_F16_CFG")) {
     const int c = atoi(e);
     if (c >= 0 && c < kCfgs && N % cfg_bn(c) == 0) return c;
   }
-  if (M >= 8192 && N % 192 == 0) return 0;
+  // deep reductions (the MLM decoder's data gradient, K = 30720) on the large tile whatever M: split-K
+  // slabs fill the CUs, and the big tile halves the operand re-reads of the 128 x 96 one
+  if ((M >= 8192 || K >= 8192) && N % 192 == 0) return 0;
   if (M >= 1024 && N % 96 == 0) return 2;
   if (N % 64 == 0) return 3;
   return -1;

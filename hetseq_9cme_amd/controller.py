@@ -73,8 +73,7 @@ class Controller(object):
             ops.set_fused(False)      # A/B mode: plain torch ops on the GPU
         ops.set_fp32_gemm(getattr(args, 'fp32_gemm', 'native'))
         ow = getattr(args, 'overlap_wgrad', 'auto')
-        ops.set_side_stream('on' if os.environ.get('HETSEQ_SIDE_STREAM') == '1' else
-                            {True: 'on', False: 'off', None: 'auto'}.get(ow, ow))
+        ops.set_side_stream({True: 'on', False: 'off', None: 'auto'}.get(ow, ow))
         if getattr(args, 'debug_kernels', False) and self.cuda:
             ops.C().set_debug(True)   # validation inside the bindings (see csrc/bindings.cpp)
         if self.cuda:

@@ -16,11 +16,8 @@ namespace hx {
 
 // Streaming (nontemporal) stores for write-once outputs that the NEXT kernel reads from
 // HBM / MALL anyway (the bf16 split planes of the fp32-on-bf16 GEMM path): no L2
-// allocation.  Host switch read once per process; HX_NT_STORES=0 turns them off (A/B).
-inline bool nt_stores() {
-  static const bool on = !(getenv("HX_NT_STORES") && getenv("HX_NT_STORES")[0] == '0');
-  return on;
-}
+// allocation (forward 180 -> 130 us at T=16384, N=3072, bf16x6: tools/probe/nt_store_probe.py).
+inline bool nt_stores() { return true; }
 typedef unsigned int nt_u32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int nt_u32x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void st_nt16(void* p, uint4 v) {

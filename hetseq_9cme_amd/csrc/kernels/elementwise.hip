@@ -387,7 +387,7 @@ void hx_bias_act_planes(int act, const float* y, const float* b, const float* do
   float* part = (dout && dbias) ? partial : nullptr;
   // planes are written once and read by the next GEMM from HBM / MALL: nontemporal 16-B
   // stores (no L2 allocation) -- forward 180 -> 130 us at T=16384, N=3072, bf16x6
-  // (tools/probe/nt_store_probe.py); HX_NT_STORES=0 restores plain stores for A/B runs
+  // (tools/probe/nt_store_probe.py)
   static const bool nt = hx::nt_stores();
 #define HX_BAP(A, P)                                                                                 \
   do {                                                                                               \

@@ -940,10 +940,8 @@ int hx_gemm_split_plan(int M, int N, int K, int passes, int lay) {
 // bf16x6 on the 256 x 192 / 256 x 256 tiles: 3-9 % faster (tools/probe/gemm_layout_probe.py),
 // the QKV forward (N = 2304) included: 256 x 192 over B16 weights 282 us against 306 us for the
 // 256 x 128 tile over natural ones (tools/probe/qkv_plan_probe.py, profiles/r3_qkv_plan_probe.log).
-// HX_W_B16=0 turns it off.
 int hx_gemm_split_weight_b16(int N, int passes) {
-  static const bool on = !(getenv("HX_W_B16") && getenv("HX_W_B16")[0] == '0');
-  if (!on || passes != 6) return 0;
+  if (passes != 6) return 0;
   const int c = hx_gemm_split_plan(1 << 14, N, 768, passes, 2);
   return (c == 0 || c == 1 || c == 7) ? 1 : 0;
 }

@@ -61,10 +61,10 @@ def _bias3(bq, bk, bv):
     return v if v is not None else torch.cat([bq, bk, bv], 0)
 
 
-# HX_ATTN_X6_BWD=0 keeps the fp32-MFMA backward under --fp32-gemm bf16x6 (A/B switch)
-_X6_BWD = os.environ.get('HX_ATTN_X6_BWD', '1') != '0'
-# HX_ATTN_PLANES=0 keeps the fp32 dQKV + split pass instead of the gradient-plane hand-off
-_X6_PLANES = os.environ.get('HX_ATTN_PLANES', '1') != '0'
+# the split-piece backward (attention_x6.hip) whenever the forward ran split; with bf16x6 and one key
+# block it hands the QKV projection its gradient planes directly
+_X6_BWD = True
+_X6_PLANES = True
 
 
 class _AttnFn(torch.autograd.Function):

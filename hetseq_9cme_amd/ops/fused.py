@@ -194,7 +194,7 @@ class _Side(object):
     # (profiles/r3_overlap_wgrad_ab.md); the library paths (small batches, NER: 11.9 -> 15.5 ms per
     # update, host-bound; round 1: 69.5 -> 71.7 ms/step) stay on the compute stream.
     # 'on': every path; 'off': none.
-    mode = 'on' if os.environ.get('HETSEQ_SIDE_STREAM', '') == '1' else 'auto'
+    mode = 'auto'
     streams = {}          # device index -> torch.cuda.Stream
     active = set()        # device indices with side work queued in the current backward
 
@@ -218,8 +218,9 @@ def side_begin(device, pieces=False):
     idx = device.index if device.index is not None else torch.cuda.current_device()
     st = _Side.streams.get(idx)
     if st is None:
-        # HX_SIDE_PRIO: HIP stream priority of the side stream (-1 = high, 0 = normal; A/B knob)
-        st = _Side.streams[idx] = torch.cuda.Stream(device=idx, priority=int(os.environ.get('HX_SIDE_PRIO', '0')))
+        # normal priority: high priority measured no different (50.87 / 50.90 vs 50.76 / 51.01 ms/step,
+        # round 3)
+        st = _Side.streams[idx] = torch.cuda.Stream(device=idx)
     st.wait_stream(torch.cuda.current_stream(idx))
     if not _Side.active:
         torch.autograd.Variable._execution_engine.queue_callback(side_join)
@@ -641,7 +642,7 @@ def linear(x, W, b=None, res_grad=None, grad_planes=None, wgrad_defer=None):
 # ----------------------------------------------------------------- FFN block on split planes
 # FFN W1 / W2 weight gradients as one grouped launch: measured 732 -> 756 us (3 token splits over
 # 72 tiles lose to 7 over 36 each; profiles/r3_wgrad_group_probe.log) -- off by default
-_GROUP_FFN = os.environ.get('HX_WGRAD_GROUP_FFN', '0') == '1'
+_GROUP_FFN = False
 
 
 class _FFNSplitFn(torch.autograd.Function):
@@ -832,14 +833,18 @@ def qkv_weight_view(wq, wk, wv):
     return _adjacent_view([wq, wk, wv])
 
 
+_WSPLIT_BATCH = True      # every encoder weight split in one launch per forward
+_DECODER_PIECES = True    # MLM decoder on the piece GEMMs (bf16x6)
+
+
 def weight_pieces_scope(Ws, x):
     """``split_gemm.weight_pieces_scope`` over ``Ws`` when the piece GEMMs will run for the
     activations ``x`` [.., H] (``split_gemm.producer_pieces``), else a no-op context.
-    ``HX_WSPLIT_BATCH=0`` turns the batch split off."""
+    (``_WSPLIT_BATCH = False`` turns the batch split off.)"""
     import contextlib
     if torch.is_tensor(x) and x.dtype == torch.bfloat16 and use_kernels(x):
         return gemm16.bf16_scope(Ws)   # --precision bf16: W^T copies for the data gradients
-    if os.environ.get('HX_WSPLIT_BATCH', '1') == '0' or not torch.is_tensor(x) or x.dtype != torch.float32:
+    if not _WSPLIT_BATCH or not torch.is_tensor(x) or x.dtype != torch.float32:
         return contextlib.nullcontext()
     if gemm16.enabled():
         return gemm16.weight_scope(Ws) if use_kernels(x) else contextlib.nullcontext()
@@ -887,10 +892,9 @@ class _Linear3Fn(torch.autograd.Function):
         if ctx.gp is not None:
             ctx.gp.want = True
             ctx.gp.pieces = ctx.pieces
-            # deep data gradient (3H -> H): the producer's planes in the prefix form are opt-in
-            # (HX_PREFIX_QKV=1): measured neutral to 0.1 ms/step slower at BERT-base phase 1,
-            # unlike the 4H -> H products (split_gemm.prefix_ok)
-            ctx.gp.prefix = os.environ.get('HX_PREFIX_QKV', '0') == '1' and split_gemm.prefix_ok(W.shape[0], W.shape[1])
+            # deep data gradient (3H -> H): natural pass order (the prefix form measured neutral to
+            # 0.1 ms/step slower here, unlike the 4H -> H products: split_gemm.prefix_ok)
+            ctx.gp.prefix = False
         if ctx.pieces:    # fp32 on bf16 matrix cores, hand-written piece GEMMs
             x2 = split_gemm.input_pieces(x, x2)
             wf, Wc = split_gemm.weight_pieces(W)
@@ -1201,7 +1205,7 @@ def _decoder_pieces_ok(h, W, Vp):
     split_gemm.nt_ok): forward [M, Vp] over K = H, data gradient [M, H] over K = Vp in split-K
     slabs, weight gradient on wgrad_split.hip."""
     H = W.shape[1]
-    if not split_gemm.nt_ok(H, Vp) or os.environ.get('HX_DECODER_PIECES', '1') == '0':
+    if not split_gemm.nt_ok(H, Vp) or not _DECODER_PIECES:
         return False
     npc = split_gemm.npieces()
     return Vp * npc * H * 2 < (1 << 31) and Vp % 256 == 0 and H % 192 == 0

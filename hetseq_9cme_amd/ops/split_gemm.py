@@ -64,8 +64,13 @@ ORDER_W_PREFIX = {3: (0, 0, 1), 6: (0, 0, 0, 1, 1, 2)}
 # weight-gradient kernel; it was 22.6 vs 21.2 before them); NER fine-tuning batches (~1000
 # tokens) still run faster native (10.8 vs 12.9 ms/update).  Both are fp32-exact class, so
 # small GEMMs (MLM head on the masked rows, pooler, small batches) simply stay native.
-MIN_ROWS = {3: int(os.environ.get('HETSEQ_SPLIT_MIN_ROWS_X3', '2048')),
+MIN_ROWS = {3: 2048,
             6: int(os.environ.get('HETSEQ_SPLIT_MIN_ROWS_X6', '4096'))}
+
+
+_SPLITK = True        # split-K slabs for deep, narrow library products (the MLM decoder's dgrad)
+_WGRAD_GROUP = True   # two weight gradients over the same tokens in one launch
+_PREFIX_GEMM = True   # prefix form for the deep 4H -> H library products
 
 
 class _State(object):
@@ -174,7 +179,7 @@ def _splitk(m, n, k):
     """Reduction slabs for a product with few 256 x 256 output tiles and a deep reduction
     (1 = none): enough slabs for ~512 tiles, each slab >= 8192 deep and a multiple of 64."""
     tiles = ((m + 255) // 256) * ((n + 255) // 256)
-    if tiles >= 64 or k < 65536 or os.environ.get('HX_SPLITK', '1') == '0':
+    if tiles >= 64 or k < 65536 or not _SPLITK:
         return 1
     for s in (16, 12, 8, 4, 2):
         if tiles * s <= 768 and k % (64 * s) == 0 and k // s >= 8192:
@@ -368,8 +373,8 @@ def wgrad_pieces_group(items):
     """Two weight gradients over the same tokens as ONE launch (wgrad_split.hip's grouped form):
     ``items`` = [(dys, xs, n_out, n_in, slot)] x 2, as for ``wgrad_pieces``.  Returns the two
     dW tensors, or None when the pair does not qualify (then run them one by one).
-    ``HX_WGRAD_GROUP=0`` turns grouping off."""
-    if _State.passes != 6 or os.environ.get('HX_WGRAD_GROUP', '1') == '0':
+    (``_WGRAD_GROUP = False`` turns grouping off.)"""
+    if _State.passes != 6 or not _WGRAD_GROUP:
         return None
     args, outs = [], []
     for dys, xs, n_out, n_in, slot in items:
@@ -416,8 +421,7 @@ def wgrad(dys, xs, n_out, n_in, slot, dy_order=None, x_order=None):
 
 # ---------------------------------------------------------------- prefix form
 def _prefix_on():
-    import os
-    return os.environ.get('HX_PREFIX_GEMM', '1') != '0'
+    return _PREFIX_GEMM
 
 
 def prefix_ok(k, n_out):

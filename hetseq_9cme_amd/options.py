@@ -226,7 +226,8 @@ def add_distributed_training_args(parser):
     group.add_argument('--find-unused-parameters', default=False, action='store_true')
     group.add_argument('--fast-stat-sync', default=False, action='store_true')
     group.add_argument('--check-params-every', default=0, type=int,
-                       help='debug: all-gather a parameter checksum every N updates and assert equality')
+                       help='debug / race check, NOT a fast path: every N updates a host-synchronising '
+                            'parameter checksum (.item()) is all-gathered (pickled) and compared across ranks')
     return group
 
 

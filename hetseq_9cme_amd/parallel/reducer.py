@@ -180,6 +180,10 @@ class GradReducer(object):
     def global_used(self, step_used):
         """Per-parameter 'received a gradient this step' flags, OR-ed over ranks.
 
+        Slow path (host-synchronising: a MAX all-reduce + ``.tolist()``), taken only with
+        ``--find-unused-parameters`` WITHOUT ``--fast-stat-sync``; the fast path carries the flags
+        in the stats all-reduce and the optimizer consumes them on device (controller.py).
+
         Without ``--find-unused-parameters`` every parameter takes part in every
         reduction (DDP's contract), so all are treated as used and no collective
         is needed.  With it, one small MAX all-reduce of the flags runs (the

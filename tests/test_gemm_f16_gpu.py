@@ -175,3 +175,57 @@ def test_gemm_bf16_mode(dev, M, N, K):
     out = acc.clone()
     C().gemm_bf16(dy, wt, out=out, beta=True)
     assert ((out.double() - ref2).abs() / den2).max().item() < 8e-3
+
+
+@pytest.mark.parametrize('cfg', ['0', '1', '2', '3'])
+def test_gemm_f16_every_tile(dev, monkeypatch, cfg):
+    """Every tile configuration of gemm_f16_k (HX_GEMM_F16_CFG forces it): forward with bias and the
+    beta = 1 data gradient, rows not a multiple of the tile."""
+    monkeypatch.setenv('HX_GEMM_F16_CFG', cfg)
+    g = torch.Generator(device=dev).manual_seed(int(cfg))
+    M, N, K = 4096 + 37, 768, 768
+    a = torch.randn(M, K, device=dev, generator=g)
+    W = torch.randn(N, K, device=dev, generator=g) * 0.02
+    bias = torch.randn(N, device=dev, generator=g)
+    wf, wt, parts = _pieces(W)
+    out = C().gemm_f16(a, C().amax_rows(a), wf, parts, bias=bias)
+    ref = a.double() @ W.double().t() + bias.double()
+    den = a.abs().double() @ W.abs().double().t() + bias.abs().double()
+    assert ((out.double() - ref).abs() / den).max().item() < 4e-6
+    acc = torch.randn(M, K, device=dev, generator=g)
+    dy = torch.randn(M, N, device=dev, generator=g)
+    o2 = acc.clone()
+    C().gemm_f16(dy, C().amax_rows(dy), wt, parts, out=o2, beta=True)
+    ref2 = acc.double() + dy.double() @ W.double()
+    den2 = acc.abs().double() + dy.abs().double() @ W.abs().double()
+    assert ((o2.double() - ref2).abs() / den2).max().item() < 4e-6
+
+
+@pytest.mark.parametrize('plan', ['0:1', '0:5', '1:1', '1:3'])
+def test_wgrad_f16_every_plan(dev, monkeypatch, plan):
+    """Both tiles and split counts of wgrad_f16_k (HX_WGRAD_F16="cfg:nsplit" forces them)."""
+    monkeypatch.setenv('HX_WGRAD_F16', plan)
+    g = torch.Generator(device=dev).manual_seed(len(plan))
+    T, M, N = 3000, 768, 512
+    dy = torch.randn(T, M, device=dev, generator=g) * 1e-3
+    x = torch.randn(T, N, device=dev, generator=g)
+    out = torch.empty(M, N, device=dev)
+    C().wgrad_f16(dy, C().amax_rows(dy), x, C().amax_rows(x), out)
+    ref = dy.double().t() @ x.double()
+    den = dy.abs().double().t() @ x.abs().double()
+    assert ((out.double() - ref).abs() / den).max().item() < 4e-6
+
+
+@pytest.mark.parametrize('plan', ['0:1', '1:3', '2:2', '3:4'])
+def test_wgrad_bf16_every_plan(dev, monkeypatch, plan):
+    """The bf16 weight-gradient kernel's tiles / split counts (HX_WGRAD_CFG="cfg:nsplit")."""
+    monkeypatch.setenv('HX_WGRAD_CFG', plan)
+    g = torch.Generator(device=dev).manual_seed(7)
+    T, M, N = 4096, 768, 512
+    dy = torch.randn(T, M, device=dev, generator=g).bfloat16()
+    x = torch.randn(T, N, device=dev, generator=g).bfloat16()
+    out = torch.empty(M, N, device=dev)
+    C().wgrad_bf16(dy, x, out)
+    ref = dy.double().t() @ x.double()
+    den = dy.double().abs().t() @ x.double().abs()
+    assert ((out.double() - ref).abs() / den).max().item() < 1e-5

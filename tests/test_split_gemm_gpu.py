@@ -190,8 +190,8 @@ def test_training_split_modes_track_native(dev, tmp_path):
                '--disable-validation', '--num-workers', '1', '--lr', '1e-3', '--weight-decay', '0.01',
                '--clip-norm', '0.5', '--save-dir', save, '--distributed-world-size', '1', '--fp32-gemm', mode]
         r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
-                           env=dict(os.environ, PYTHONPATH=root, HETSEQ_SPLIT_MIN_ROWS_X3='0',
-                                    HETSEQ_SPLIT_MIN_ROWS_X6='0', HX_PIECE_MIN_ROWS='0'), timeout=300)
+                           env=dict(os.environ, PYTHONPATH=root, HETSEQ_SPLIT_MIN_ROWS_X6='0', HX_PIECE_MIN_ROWS='0'),
+                           timeout=300)
         assert r.returncode == 0, r.stdout[-3000:]
         with torch.serialization.safe_globals([argparse.Namespace]):
             outs[mode] = torch.load(os.path.join(save, 'checkpoint_last.pt'), map_location='cpu', weights_only=True)
@@ -238,8 +238,9 @@ def test_ffn_split_block(dev, mode, tol, prefix, monkeypatch):
     """FFN block as one node (GELU epilogue writes the FFN-down planes, GELU backward the
     FFN-up gradient planes + dbias) against an fp64 autograd reference; with and without the
     prefix form of the deep products (split_gemm.prefix_mm: distinct pieces only)."""
-    monkeypatch.setenv('HX_PREFIX_GEMM', prefix)
     from hetseq_9cme_amd import ops
+    from hetseq_9cme_amd.ops import split_gemm as _sg
+    monkeypatch.setattr(_sg, '_PREFIX_GEMM', prefix != '0')
     g = torch.Generator(device='cpu').manual_seed(13)
     T, H, I = 384, 256, 1024
     x = torch.randn(T, H, generator=g).to(dev).requires_grad_(True)
@@ -738,7 +739,7 @@ def test_bert_grouped_wgrads_match_ungrouped(dev, monkeypatch):
                      max_position_embeddings=128, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
     grads = []
     for grouped in (True, False):
-        monkeypatch.setenv('HX_WGRAD_GROUP', '1' if grouped else '0')
+        monkeypatch.setattr(split_gemm, '_WGRAD_GROUP', grouped)
         monkeypatch.setattr(fused, '_GROUP_FFN', grouped)
         torch.manual_seed(0)
         model = BertForPreTraining(cfg).to(dev)
@@ -792,7 +793,7 @@ def test_piece_gemm_split_k(dev, ks):
 def test_decoder_pieces_path_matches_fp64(dev, monkeypatch):
     """The MLM decoder + softmax-xent on the piece GEMMs (forward over the padded vocabulary,
     split-K data gradient, split-piece weight gradient) against fp64 autograd, and against the
-    pass-planes path it replaces (HX_DECODER_PIECES=0)."""
+    pass-planes path it replaces (fused._DECODER_PIECES = False)."""
     from hetseq_9cme_amd import ops
     g = torch.Generator(device='cpu').manual_seed(91)
     M, H, V = 512, 768, 9000
@@ -813,7 +814,8 @@ def test_decoder_pieces_path_matches_fp64(dev, monkeypatch):
     try:
         ops.set_fp32_gemm('bf16x6')
         got = run()
-        monkeypatch.setenv('HX_DECODER_PIECES', '0')
+        from hetseq_9cme_amd.ops import fused as _fused
+        monkeypatch.setattr(_fused, '_DECODER_PIECES', False)
         old = run()
     finally:
         ops.set_fp32_gemm('native')
@@ -857,7 +859,8 @@ def test_bert_batch_weight_split_matches_per_call(dev, monkeypatch):
                      max_position_embeddings=128, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
     res = []
     for batch in ('1', '0'):
-        monkeypatch.setenv('HX_WSPLIT_BATCH', batch)
+        from hetseq_9cme_amd.ops import fused as _fused
+        monkeypatch.setattr(_fused, '_WSPLIT_BATCH', batch == '1')
         torch.manual_seed(0)
         model = BertForPreTraining(cfg).to(dev)
         model.max_predictions_per_seq = 4

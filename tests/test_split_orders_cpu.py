@@ -85,8 +85,6 @@ def test_dispatch_plans(monkeypatch):
     """Which product form each BERT-base GEMM takes (pure host logic of ops/split_gemm.py):
     split path from 4096 tokens per GEMM under bf16x6 (the 32 x 128-token batch), split-K
     only for the MLM decoder's data gradient, prefix form only for the deep narrow products."""
-    monkeypatch.delenv('HX_SPLITK', raising=False)
-    monkeypatch.delenv('HX_PREFIX_GEMM', raising=False)
     if 'HETSEQ_SPLIT_MIN_ROWS_X6' not in os.environ:
         assert sg.MIN_ROWS[6] == 4096
     # decoder dgrad: 2560 masked rows x 768 from K' = 6 x 30720 -> 16 reduction slabs
@@ -99,9 +97,9 @@ def test_dispatch_plans(monkeypatch):
         assert sg.prefix_ok(3072, 768)          # FFN-down forward / FFN-up data gradient
         assert not sg.prefix_ok(768, 2304)      # QKV forward: k < 2 n
         assert not sg.prefix_ok(768, 768)
-        monkeypatch.setenv('HX_PREFIX_GEMM', '0')
+        monkeypatch.setattr(sg, '_PREFIX_GEMM', False)
         assert not sg.prefix_ok(3072, 768)
-        monkeypatch.delenv('HX_PREFIX_GEMM')
+        monkeypatch.setattr(sg, '_PREFIX_GEMM', True)
     finally:
         sg.set_fp32_gemm('native')
     assert not sg.prefix_ok(3072, 768)          # native mode: no split products at all

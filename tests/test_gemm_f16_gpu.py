@@ -100,7 +100,10 @@ def test_gemm_f16_gelu_epilogues(dev):
     t64 = dh64 * d.double()
     den = (dy.abs().double() @ W2.abs().double()) * d.abs().double()
     assert ((t.double() - t64).abs() / den.clamp_min(1e-300)).max().item() < 1e-5
-    torch.testing.assert_close(db.double(), t64.sum(0), rtol=1e-4, atol=1e-9)
+    # d b1 = column sums of t over 16448 rows: relative to the sum of |t| (cancellation), and exactly
+    # the kernel's own t summed (the per-wave partials + fold are the only extra rounding)
+    assert ((db.double() - t64.sum(0)).abs() / t64.abs().sum(0)).max().item() < 1e-6
+    assert ((db.double() - t.double().sum(0)).abs() / t.double().abs().sum(0)).max().item() < 1e-6
     assert tmax.max().item() == t.abs().max().item()
 
 

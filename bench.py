@@ -4,15 +4,16 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 
 is launched by ``torch.distributed.run`` (one rank per GPU, RCCL).  Runs the real
 framework path -- synthetic NVIDIA-schema HDF5 shards -> native reader -> pinned
 staging on the HIP copy stream -> Controller.train_step (fused HIP kernels,
-hand-written piece GEMMs for every BERT linear and the MLM decoder, flat-buffer
+hand-written fp16x3 GEMMs for every BERT linear and the MLM decoder, flat-buffer
 RCCL / xGMI reducer, fused norm/clip/Adam) -- with
 random-init BERT-base weights (no network: no corpus, no checkpoint).
 
 Config = BASELINE.json's: BERT-base (L12 H768 A12 V30522), seq 128, 20 masked
 positions per sequence, per-GPU batch 128 (weak scaling: global batch 128*N),
 Adam lr 1e-4 + warmup 10000 + wd 0.01, clip 25, fast stat sync, fp32-class compute
-(the reference's precision; ``--fp32-gemm bf16x6`` = fp32 GEMMs as six bf16 piece
-products, parity vs native fp32 over 300 updates in profiles/r3_parity_bert_base_300.md).  W untimed warm-up steps, then exactly K timed steps
+(the reference's precision; ``--fp32-gemm fp16x3`` = fp32 GEMMs as three fp16 piece
+products of power-of-two-scaled operands, ops/gemm16.py; parity vs native fp32 over 300
+updates in profiles/).  W untimed warm-up steps, then exactly K timed steps
 bracketed by barrier + device synchronize; the max over ranks is reported.
 """
 import argparse
@@ -42,9 +43,9 @@ def parse():
     ap.add_argument('--seq', type=int, default=128)
     ap.add_argument('--max-pred', type=int, default=20)
     ap.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'])
-    ap.add_argument('--fp32-gemm', default='bf16x6', choices=['native', 'bf16x3', 'bf16x6', 'fp16x3'],
-                    help='fp32 linear GEMMs: bf16x6 (default, fp32-exact class), bf16x3 (near-fp32) or '
-                         'native f32 MFMA (ops/split_gemm.py)')
+    ap.add_argument('--fp32-gemm', default='fp16x3', choices=['native', 'bf16x3', 'bf16x6', 'fp16x3'],
+                    help='fp32 linear GEMMs: fp16x3 (default, fp32 class: ops/gemm16.py), bf16x6 '
+                         '(fp32-exact class), bf16x3 (near-fp32) or native f32 MFMA (ops/split_gemm.py)')
     ap.add_argument('--model', default='base', choices=['base', 'large', 'tiny'])
     ap.add_argument('--no-fused', action='store_true', help='torch-op baseline (A/B only)')
     ap.add_argument('--data-dir', default=None)

@@ -99,7 +99,7 @@ void adam(Tensor p, Tensor g, Tensor m, Tensor v, OptT shadow, Tensor gscale, in
 }
 
 void adam_masked(Tensor p, Tensor g, Tensor m, Tensor v, OptT shadow, Tensor gscale, Tensor table, Tensor used,
-                 Tensor steps, Tensor hp, double lr, double b1, double b2, double eps, double wd) {
+                 Tensor steps, Tensor hp, double lr, double b1, double b2, double eps, double wd, OptT lr_dev) {
   check_f32(p, "param");
   check_f32(g, "grad");
   check_f32(m, "exp_avg");
@@ -117,10 +117,13 @@ void adam_masked(Tensor p, Tensor g, Tensor m, Tensor v, OptT shadow, Tensor gsc
     TORCH_CHECK(shadow->scalar_type() == torch::kBFloat16 && shadow->numel() == p.numel(), "bad bf16 shadow");
     sh = reinterpret_cast<uint16_t*>(shadow->data_ptr());
   }
+  if (has(lr_dev))
+    TORCH_CHECK(lr_dev->is_cuda() && lr_dev->scalar_type() == torch::kFloat64 && lr_dev->numel() == 1, "lr_dev: f64 [1]");
   c10::hip::HIPGuardMasqueradingAsCUDA guard(p.device());
   hx_adam_masked(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), sh,
                  gscale.data_ptr<float>(), table.data_ptr<int64_t>(), (int)table.size(0), used.data_ptr<double>(),
-                 steps.data_ptr<int>(), hp.data_ptr<float>(), (int)nparam, lr, b1, b2, (float)eps, wd, cur_stream(p));
+                 steps.data_ptr<int>(), hp.data_ptr<float>(), (int)nparam, lr, b1, b2, (float)eps, wd,
+                 has(lr_dev) ? lr_dev->data_ptr<double>() : nullptr, cur_stream(p));
 }
 
 void adadelta(Tensor p, Tensor g, Tensor sq, Tensor acc, Tensor gscale, int64_t start, int64_t end, double lr,
@@ -1258,7 +1261,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "hetseq_9cme_amd gfx950 (MI355X) kernels";
   m.def("grad_norm_clip", &grad_norm_clip);
   m.def("adam", &adam);
-  m.def("adam_masked", &adam_masked);
+  m.def("adam_masked", &adam_masked, py::arg("p"), py::arg("g"), py::arg("m"), py::arg("v"), py::arg("shadow"),
+        py::arg("gscale"), py::arg("table"), py::arg("used"), py::arg("steps"), py::arg("hp"), py::arg("lr"),
+        py::arg("b1"), py::arg("b2"), py::arg("eps"), py::arg("wd"), py::arg("lr_dev") = py::none());
   m.def("adam_mask_chunk", &hx_adam_mask_chunk);
   m.def("adadelta", &adadelta);
   m.def("ln_fwd", &ln_fwd, py::arg("y"), py::arg("bias"), py::arg("res"), py::arg("gamma"), py::arg("beta"),

@@ -14,7 +14,7 @@ void hx_grad_norm_clip(const float* g, int64_t n, double* partial_ws, float* gsc
 int hx_adam_mask_chunk();
 void hx_adam_masked(float* p, const float* g, float* m, float* v, uint16_t* shadow, const float* gscale,
                     const int64_t* table, int nblocks, const double* used, int* steps, float* hp, int nparam,
-                    double lr, double b1, double b2, float eps, double wd, hipStream_t s);
+                    double lr, double b1, double b2, float eps, double wd, const double* lr_dev, hipStream_t s);
 void hx_adam(float* p, const float* g, float* m, float* v, uint16_t* shadow, const float* gscale, int64_t n, float b1,
              float b2, float eps, float step_size, float wd_lr, const float* hp,
              hipStream_t s);

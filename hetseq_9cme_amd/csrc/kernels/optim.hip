@@ -182,7 +182,8 @@ constexpr int kMaskChunk = NT * 4 * 4;   // 4096 floats per block
 
 __global__ __launch_bounds__(NT) void adam_steps_k(int nparam, const double* __restrict__ used,
                                                  int* __restrict__ steps, float* __restrict__ hp, double lr,
-                                                 double b1, double b2, double wd) {
+                                                 double b1, double b2, double wd, const double* __restrict__ lr_dev) {
+  if (lr_dev) lr = lr_dev[0];   // graph-captured updates: this update's lr, written before the replay
   for (int i = threadIdx.x; i < nparam; i += NT) {
     const bool u = used[i] > 0.0;
     const int t = steps[i] + (u ? 1 : 0);
@@ -258,8 +259,8 @@ int hx_adam_mask_chunk() { return kMaskChunk; }
 
 void hx_adam_masked(float* p, const float* g, float* m, float* v, uint16_t* shadow, const float* gscale,
                     const int64_t* table, int nblocks, const double* used, int* steps, float* hp, int nparam,
-                    double lr, double b1, double b2, float eps, double wd, hipStream_t s) {
-  adam_steps_k<<<1, NT, 0, s>>>(nparam, used, steps, hp, lr, b1, b2, wd);
+                    double lr, double b1, double b2, float eps, double wd, const double* lr_dev, hipStream_t s) {
+  adam_steps_k<<<1, NT, 0, s>>>(nparam, used, steps, hp, lr, b1, b2, wd, lr_dev);
   if (nblocks <= 0) return;
   if (shadow)
     adam_masked_k<true><<<nblocks, NT, 0, s>>>(p, g, m, v, shadow, gscale, table, used, hp, (float)b1, (float)b2,

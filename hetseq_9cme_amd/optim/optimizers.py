@@ -228,6 +228,13 @@ class _Adam(_Optimizer):
     device_used = None
     _steps_dev = None
     _mask_table = None
+    _masked = False     # the latest update took the masked path
+    _lr_dev = None      # f64 [1]: the masked update's lr (a replayed graph reads the current one)
+
+    def _write_hparams(self):
+        super()._write_hparams()
+        if self._masked and self._lr_dev is not None and not torch.cuda.is_current_stream_capturing():
+            self._lr_dev.fill_(self._lr)
 
     def _device_steps(self):
         if self._steps_dev is None:
@@ -260,13 +267,17 @@ class _Adam(_Optimizer):
         beta1, beta2 = g['betas']
         eps, wd, lr = g['eps'], g['weight_decay'], self._lr
         self._fold_host_scale()
+        self._masked = False
         if self.device_used is not None:
             used, self.device_used = self.device_used, None
             if self.use_kernels:
+                self._masked = True
+                self._host_step()
                 ops.C().adam_masked(self.flat.param_flat, self.flat.grad_flat, self.exp_avg, self.exp_avg_sq,
                                     self.bf16_shadow, self._gscale, self._masked_table(),
                                     used.reshape(-1).to(torch.float64).contiguous(), self._device_steps(),
-                                    self._mask_hp, float(lr), float(beta1), float(beta2), float(eps), float(wd))
+                                    self._mask_hp, float(lr), float(beta1), float(beta2), float(eps), float(wd),
+                                    lr_dev=self._lr_dev)
                 return
             self.used_mask = [bool(u > 0) for u in used.reshape(-1).tolist()]   # CPU reference path
         runs = self._host_step()
@@ -296,7 +307,16 @@ class _Adam(_Optimizer):
     def _host_step(self):
         """Host half of an update: advance the step counters, compute this update's
         hyper-parameters and (graph mode) write them to the device buffer.  A replayed
-        graph calls only this; ``step`` calls it and then launches the kernels."""
+        graph calls only this; ``step`` calls it and then launches the kernels.  The masked
+        (``device_used``) update advances its counters on the device: its host half is only
+        the learning rate, which a graph-captured update reads from ``_lr_dev``."""
+        if self._masked:
+            if self._lr_dev is None:   # allocated by the first (eager) masked update, never in a capture
+                self._lr_dev = torch.zeros(1, dtype=torch.float64, device=self.device)
+            self._hp_vals = []
+            self._runs_sig = ('masked',)
+            self._write_hparams()
+            return []
         self._pull_steps()
         g = self.param_groups[0]
         beta1, beta2 = g['betas']

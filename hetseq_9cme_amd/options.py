@@ -51,19 +51,18 @@ def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialD
     # --- MI355X-native execution knobs (not in the reference) ---
     parser.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'],
                         help='compute precision: fp32 (the reference\'s precision: fp32 tensors end to end; '
-                             'the GEMMs and attention products run as --fp32-gemm says -- by default bf16x6, '
-                             'fp32-exact class on the bf16 matrix cores; --fp32-gemm native gives plain f32 MFMA, '
+                             'the GEMMs and attention products run as --fp32-gemm says -- by default fp16x3, '
+                             'fp32 class on the fp16 matrix cores; --fp32-gemm native gives plain f32 MFMA, '
                              'bitwise the reference\'s fp32 FMA chain) or bf16 (bf16 MFMA, fp32 master weights '
                              'and optimizer state)')
-    parser.add_argument('--fp32-gemm', default='bf16x6', choices=['native', 'bf16x3', 'bf16x6', 'fp16x3'],
-                        help='how fp32 (--precision fp32) linear-layer GEMMs run on the GPU: bf16x6 (default: '
-                             'operands split into three bf16 pieces, six passes on the 16x faster bf16 MFMA, '
-                             'fp32-exact class -- measured GEMM error within 1.2x of native), bf16x3 (two '
-                             'pieces, three passes, ~2^-17 per product: near-fp32), fp16x3 (operands scaled by '
-                             'a power of two from their max |x| and split into two fp16 pieces inside the GEMM '
-                             'kernels: 22 bits each, three passes, fp32 class at half the matrix work of bf16x6: '
-                             'ops/gemm16.py) or native f32 '
-                             'MFMA (157 TF/s peak); see ops/split_gemm.py')
+    parser.add_argument('--fp32-gemm', default='fp16x3', choices=['native', 'bf16x3', 'bf16x6', 'fp16x3'],
+                        help='how fp32 (--precision fp32) linear-layer GEMMs run on the GPU: fp16x3 (default: '
+                             'operands scaled by a power of two from their max |x| and split into two fp16 '
+                             'pieces inside the GEMM kernels -- 22 bits each, three passes; measured GEMM error '
+                             '0.6-0.7x native fp32\'s: ops/gemm16.py), bf16x6 (three bf16 pieces, six passes, '
+                             'fp32-exact class at twice the matrix work), bf16x3 (two bf16 pieces, three passes, '
+                             '~2^-17 per product: near-fp32) or native f32 MFMA (157 TF/s peak); see '
+                             'ops/split_gemm.py')
     parser.add_argument('--graph-train-step', action='store_true',
                         help='single GPU, one micro-batch per update: capture each input shape\'s whole '
                              'update (forward, backward, clip, optimizer) in a HIP graph after two eager '

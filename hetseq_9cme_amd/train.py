@@ -176,6 +176,16 @@ def distributed_main(i, args, start_rank=0):
     if args.distributed_rank is None:
         args.distributed_rank = start_rank + i
     main(args, init_distributed=True)
+    _teardown()
+
+
+def _teardown():
+    """An orderly process-group teardown: a group left to the interpreter's exit can abort a rank
+    ("terminate called without an active exception") while its gloo / RCCL threads still run."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def _from_torchrun(args):
@@ -198,6 +208,7 @@ def cli_main(argv=None):
         os.environ['HIP_LAUNCH_BLOCKING'] = '1'
     if _from_torchrun(args):
         main(args, init_distributed=True)
+        _teardown()
     elif args.distributed_init_method is not None:
         if not args.cpu and args.distributed_backend == 'nccl':
             assert args.distributed_gpus <= max(1, torch.cuda.device_count())

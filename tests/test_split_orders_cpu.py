@@ -75,10 +75,10 @@ def test_mode_switch_and_cpu_inactive():
         sg.set_fp32_gemm('native')
 
 
-def test_option_default_is_bf16x6():
+def test_option_default_is_fp16x3():
     from hetseq_9cme_amd import options
     args = options.parse_training_args(['--task', 'mnist', '--data', '/tmp'])
-    assert args.fp32_gemm == 'bf16x6'
+    assert args.fp32_gemm == 'fp16x3'
 
 
 def test_dispatch_plans(monkeypatch):

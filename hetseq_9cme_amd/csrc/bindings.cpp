@@ -519,7 +519,8 @@ Tensor wgrad_bf16(Tensor dy, Tensor x, Tensor out) {
   Tensor ws;
   if (nsplit > 1) ws = torch::empty({nsplit * M * N}, out.options());
   hx_wgrad_bf16(dy.data_ptr(), (int)dy.stride(0), x.data_ptr(), (int)x.stride(0), out.data_ptr<float>(),
-                nsplit > 1 ? ws.data_ptr<float>() : nullptr, (int)M, (int)N, (int)T, cfg, nsplit, cur_stream(dy));
+                nsplit > 1 ? ws.data_ptr<float>() : nullptr, (int)M, (int)N, (int)T, cfg, nsplit, (int)out.size(0),
+                cur_stream(dy));
   dbg_finite(out, "wgrad_bf16");
   return out;
 }

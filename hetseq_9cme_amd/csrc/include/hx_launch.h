@@ -69,7 +69,7 @@ void hx_attn_bwd_bf16(const void* qkv, const float* bias, float* dbias_part, con
 // bf16 weight gradient dW[M][N] (fp32) = dY[T][M]^T . X[T][N] (wgrad_bf16.hip); ws: nsplit * M * N floats
 void hx_wgrad_bf16_plan(int M, int N, int T, int* cfg, int* nsplit);
 void hx_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, float* out, float* ws, int M, int N, int T,
-                   int cfg, int nsplit, hipStream_t s);
+                   int cfg, int nsplit, int mvalid, hipStream_t s);
 // attention_x6.hip -- fp32 attention forward on bf16 MFMA with split pieces (bf16x6 class)
 // opieces != nullptr: out is also written as npc bf16 pieces [B*S][npc][H]
 void hx_attn_fwd_x6(const float* qkv, const float* bias, const float* maskb, float* out, float* lse,

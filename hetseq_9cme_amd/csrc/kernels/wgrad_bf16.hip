@@ -85,7 +85,7 @@ __device__ __forceinline__ bf16x8 frag(const char* tile, const int (&lo)[2], con
 template <int BM, int BN, int WM, int WN, int BK>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_bf16_k(
     const uint16_t* __restrict__ A, int lda, const uint16_t* __restrict__ B, int ldb, float* __restrict__ out,
-    int M, int N, int T, int kchunk, int nsplit) {
+    int M, int N, int T, int kchunk, int nsplit, int mvalid) {
   constexpr int NWM = BM / WM, NW = NWM * (BN / WN), NT = NW * 64;
   constexpr int MB = WM / 32, NB = WN / 32;
   constexpr int CA = BK * BM / 8 / NT, CB = BK * BN / 8 / NT;   // 16-B chunks per thread
@@ -192,7 +192,8 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_bf16_k(
     __syncthreads();
   }
 
-  // ---- epilogue: rows m (accumulator rows), columns n (lanes): 128-B coalesced fp32 stores
+  // ---- epilogue: rows m (accumulator rows), columns n (lanes): 128-B coalesced fp32 stores;
+  // rows from mvalid on (the tile padding of M) are not stored
   float* o = out + (nsplit > 1 ? (int64_t)sp * M * N : 0);
 #pragma unroll
   for (int a = 0; a < MB; ++a)
@@ -202,18 +203,18 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_bf16_k(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * WM + 32 * a + crow(r, h);
-        o[(int64_t)m * N + n] = acc[a][b][r];
+        if (m < mvalid) o[(int64_t)m * N + n] = acc[a][b][r];
       }
     }
 }
 
-// out[i] = sum_s ws[s][i]  (float4)
+// out[i] = sum_s ws[s][i]  (float4) over the first n4 of each slab of slab4
 __global__ __launch_bounds__(256) void split_sum_k(const float4* __restrict__ ws, float4* __restrict__ out, int64_t n4,
-                                                  int nsplit) {
+                                                  int64_t slab4, int nsplit) {
   for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
     float4 s = ws[i];
     for (int k = 1; k < nsplit; ++k) {
-      const float4 v = ws[(int64_t)k * n4 + i];
+      const float4 v = ws[(int64_t)k * slab4 + i];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
     out[i] = s;
@@ -222,7 +223,7 @@ __global__ __launch_bounds__(256) void split_sum_k(const float4* __restrict__ ws
 
 template <int BM, int BN, int WM, int WN, int BK>
 void launch(const uint16_t* A, int lda, const uint16_t* B, int ldb, float* out, float* ws, int M, int N, int T,
-            int nsplit, hipStream_t s) {
+            int nsplit, int mvalid, hipStream_t s) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int kchunk = ((T + nsplit - 1) / nsplit + BK - 1) / BK * BK;
   nsplit = (T + kchunk - 1) / kchunk;   // no empty splits
@@ -236,12 +237,12 @@ void launch(const uint16_t* A, int lda, const uint16_t* B, int ldb, float* out, 
     attr = true;
   }
   wgrad_bf16_k<BM, BN, WM, WN, BK><<<8 * per, NT, smem, s>>>(A, lda, B, ldb, nsplit > 1 ? ws : out, M, N, T, kchunk,
-                                                      nsplit);
+                                                      nsplit, nsplit > 1 ? M : mvalid);
   if (nsplit > 1) {
-    const int64_t n4 = (int64_t)M * N / 4;
+    const int64_t n4 = (int64_t)mvalid * N / 4, slab4 = (int64_t)M * N / 4;
     const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
     split_sum_k<<<blocks, 256, 0, s>>>(reinterpret_cast<const float4*>(ws), reinterpret_cast<float4*>(out), n4,
-                                       nsplit);
+                                       slab4, nsplit);
   }
 }
 
@@ -283,12 +284,12 @@ void hx_wgrad_bf16_plan(int M, int N, int T, int* cfg, int* nsplit) {
 }
 
 void hx_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, float* out, float* ws, int M, int N, int T,
-                   int cfg, int nsplit, hipStream_t s) {
+                   int cfg, int nsplit, int mvalid, hipStream_t s) {
   const uint16_t *a = (const uint16_t*)dy, *b = (const uint16_t*)x;
   switch (cfg) {
-    case 1: launch<256, 128, 64, 64, 32>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
-    case 2: launch<256, 128, 64, 64, 64>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
-    case 3: launch<128, 128, 64, 64, 64>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
-    default: launch<128, 128, 64, 64, 32>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, s); break;
+    case 1: launch<256, 128, 64, 64, 32>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, mvalid, s); break;
+    case 2: launch<256, 128, 64, 64, 64>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, mvalid, s); break;
+    case 3: launch<128, 128, 64, 64, 64>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, mvalid, s); break;
+    default: launch<128, 128, 64, 64, 32>(a, ldy, b, ldx, out, ws, M, N, T, nsplit, mvalid, s); break;
   }
 }

@@ -232,3 +232,23 @@ def test_wgrad_bf16_every_plan(dev, monkeypatch, plan):
     ref = dy.double().t() @ x.double()
     den = dy.double().abs().t() @ x.double().abs()
     assert ((out.double() - ref).abs() / den).max().item() < 1e-5
+
+
+@pytest.mark.parametrize('plan', ['0:1', '2:3'])
+def test_wgrad_bf16_row_limit(dev, monkeypatch, plan):
+    """dW over a tile-padded M (the MLM decoder's padded vocabulary) into an output of fewer rows:
+    the rows past it are not stored (a canary row right after the output stays untouched), with
+    and without the split-K slab sum."""
+    monkeypatch.setenv('HX_WGRAD_CFG', plan)
+    g = torch.Generator(device=dev).manual_seed(3)
+    T, M, N, V = 2048, 1536, 128, 1000
+    dy = torch.randn(T, M, device=dev, generator=g).bfloat16()
+    dy[:, V:] = 0
+    x = torch.randn(T, N, device=dev, generator=g).bfloat16()
+    buf = torch.full((V + 8, N), 7.0, device=dev)
+    out = buf[:V]
+    C().wgrad_bf16(dy, x, out)
+    ref = dy[:, :V].double().t() @ x.double()
+    den = dy[:, :V].double().abs().t() @ x.double().abs()
+    assert ((out.double() - ref).abs() / den).max().item() < 1e-5
+    assert (buf[V:] == 7.0).all()

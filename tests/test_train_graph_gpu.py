@@ -122,7 +122,7 @@ for extra in ([], ['--graph-train-step']):
     res.append((ctrl, losses, st))
 gs = res[1][0]._graph_step
 print('captures', gs.captures, 'replays', gs.replays)
-assert gs.captures >= 2 and gs.replays >= 8, (gs.captures, gs.replays)
+assert gs.captures >= 1 and gs.replays >= 8, (gs.captures, gs.replays)
 for a, b in zip(res[0][1], res[1][1]):
     assert abs(a - b) <= 1e-4 * max(1.0, abs(a)), (res[0][1], res[1][1])
 for k, v in res[0][2].items():

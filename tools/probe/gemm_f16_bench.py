@@ -1,0 +1,80 @@
+"""Standalone speed of the fp16x3 and bf16 GEMM kernels (csrc/kernels/gemm_f16.hip) at the
+BERT-base phase-1 shapes (T = 16384 token rows), against hipBLASLt bf16 (torch.mm) on the same
+shapes: median of 20 event-timed calls each.  ``eff`` = fp16 MFMA rate achieved counting all three
+passes (the dense f16 peak is ~2.5 PF/s); ``fp32eq`` = the fp32 product rate it delivers."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+
+def timed(fn, n=20):
+    for _ in range(3):
+        fn()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n)]
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    ts = sorted(a.elapsed_time(b) for a, b in ev)
+    return ts[n // 2] * 1e3
+
+
+def main():
+    from hetseq_9cme_amd.ops._ext import C
+    dev = torch.device('cuda', 0)
+    T = int(os.environ.get('T', '16384'))
+    g = torch.Generator(device=dev).manual_seed(0)
+
+    def rnd(*s):
+        return torch.randn(*s, device=dev, generator=g)
+    rows = []
+    for (name, N, K) in [('qkv', 2304, 768), ('attn_out', 768, 768), ('ffn_up', 3072, 768), ('ffn_down', 768, 3072)]:
+        x = rnd(T, K)
+        W = rnd(N, K) * 0.03
+        b = rnd(N)
+        xp = C().amax_rows(x)
+        wf, wt, wp = C().split_weight_f16([W])[0]
+        fl = 2.0 * T * N * K
+        if name == 'ffn_up':
+            us = timed(lambda: C().gemm_f16_gelu(x, xp, wf, wp, b, 1))
+        else:
+            us = timed(lambda: C().gemm_f16(x, xp, wf, wp, bias=b))
+        rows.append(('fwd ' + name, T, N, K, us, fl))
+        dy = rnd(T, N)
+        dp = C().amax_rows(dy)
+        acc = rnd(T, K)
+        if name == 'ffn_down':
+            d = rnd(T, K)
+            db = torch.zeros(K, device=dev)
+            us = timed(lambda: C().gemm_f16_dgelu(dy, dp, wt, wp, d, None, db, 1))
+        else:
+            us = timed(lambda: C().gemm_f16(dy, dp, wt, wp, out=acc, beta=True))
+        rows.append(('dgrad ' + name, T, K, N, us, fl))
+        out = torch.empty(N, K, device=dev)
+        us = timed(lambda: C().wgrad_f16(dy, dp, x, xp, out))
+        rows.append(('wgrad ' + name, N, K, T, us, fl))
+        xb, Wb, dyb = x.bfloat16(), W.bfloat16(), dy.bfloat16()
+        us = timed(lambda: C().gemm_bf16(xb, Wb, bias=b))
+        rows.append(('bf16 fwd ' + name, T, N, K, us, fl / 3))
+        us = timed(lambda: torch.mm(xb, Wb.t()))
+        rows.append(('blas bf16 fwd ' + name, T, N, K, us, fl / 3))
+        us = timed(lambda: torch.mm(dyb.t(), xb))
+        rows.append(('blas bf16 wgrad ' + name, N, K, T, us, fl / 3))
+    tot = 0.0
+    for (name, M, N, K, us, f16flops) in rows:
+        # f16flops: three passes' worth for the fp16x3 kernels (fl), one pass for bf16 ones (fl / 3)
+        passes = 3 if f16flops == 2.0 * M * N * K else 1
+        eff = passes * 2.0 * M * N * K / (us * 1e-6) / 1e15
+        print('{:24s} M{:6d} N{:5d} K{:6d} {:8.1f} us  eff {:5.2f} PF/s  fp32eq {:5.2f} PF/s'.format(
+            name, M, N, K, us, eff, 2.0 * M * N * K / (us * 1e-6) / 1e15), flush=True)
+        if not name.startswith(('bf16', 'blas')):
+            tot += us
+    print('fp16x3 total per layer (fwd + dgrad + wgrad): {:.1f} us'.format(tot))
+
+
+if __name__ == '__main__':
+    main()

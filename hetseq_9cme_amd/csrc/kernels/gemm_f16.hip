@@ -411,10 +411,12 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
 // cfg 1: 256 x 192, 8 waves (4 x 2) of 64 x 96 (A fragments split by two waves, fewer B reads)
 // cfg 2: 128 x 96, 4 waves of 32 x 96                                            -- M < 8192
 // cfg 3: 64 x 64, 4 waves (2 x 2) of 32 x 32                                     -- tiny M
-constexpr int kCfgs = 4;
-int cfg_bm(int c) { return c <= 1 ? 256 : c == 2 ? 128 : 64; }
-int cfg_bn(int c) { return c <= 1 ? 192 : c == 2 ? 96 : 64; }
-int cfg_nwm(int c) { return c == 0 ? 8 : c == 1 ? 4 : c == 2 ? 4 : 2; }
+// cfg 4: 128 x 192, 4 waves of 32 x 192: two workgroups per CU (60 KB of LDS each), so one
+//        tile's prologue / epilogue store burst overlaps the other's main loop
+constexpr int kCfgs = 5;
+int cfg_bm(int c) { return c <= 1 ? 256 : c == 2 || c == 4 ? 128 : 64; }
+int cfg_bn(int c) { return c <= 1 || c == 4 ? 192 : c == 2 ? 96 : 64; }
+int cfg_nwm(int c) { return c == 0 ? 8 : c == 1 ? 4 : c == 2 || c == 4 ? 4 : 2; }
 
 template <int BM, int BN, int WM, int WN, int EPI, int AT = 0, int OB = 0>
 void launch_one(const F16Args& a, hipStream_t s) {
@@ -436,6 +438,7 @@ void launch_cfg(int cfg, const F16Args& a, hipStream_t s) {
   if (cfg == 0) launch_one<256, 192, 32, 192, EPI, AT, OB>(a, s);
   else if (cfg == 1) launch_one<256, 192, 64, 96, EPI, AT, OB>(a, s);
   else if (cfg == 2) launch_one<128, 96, 32, 96, EPI, AT, OB>(a, s);
+  else if (cfg == 4) launch_one<128, 192, 32, 192, EPI, AT, OB>(a, s);
   else launch_one<64, 64, 32, 32, EPI, AT, OB>(a, s);
 }
 

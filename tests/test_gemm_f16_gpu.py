@@ -71,10 +71,14 @@ def test_gemm_f16_dgrad_beta_bias(dev, M, N, K):
     assert ((out2.double() - ref2).abs() / den2).max().item() < 4e-6
 
 
-def test_gemm_f16_gelu_epilogues(dev):
+@pytest.mark.parametrize('cfg', ['plan', '4'])
+def test_gemm_f16_gelu_epilogues(dev, monkeypatch, cfg):
     """FFN up (bias + GELU: C = gelu'(u), P = gelu(u), per-tile max |P|) and the FFN-down data
-    gradient with the GELU backward (t = acc * gelu'(u), column sums = d bias, max |t|)."""
+    gradient with the GELU backward (t = acc * gelu'(u), column sums = d bias, max |t|), on the
+    planned tile and on the two-per-CU 128 x 192 one."""
     from hetseq_9cme_amd.ops.fused import gelu_ref
+    if cfg != 'plan':
+        monkeypatch.setenv('HX_GEMM_F16_CFG', cfg)
     g = torch.Generator(device=dev).manual_seed(11)
     M, H, I = 16384 + 64, 768, 3072
     x = torch.randn(M, H, device=dev, generator=g)
@@ -180,7 +184,7 @@ def test_gemm_bf16_mode(dev, M, N, K):
     assert ((out.double() - ref2).abs() / den2).max().item() < 8e-3
 
 
-@pytest.mark.parametrize('cfg', ['0', '1', '2', '3'])
+@pytest.mark.parametrize('cfg', ['0', '1', '2', '3', '4'])
 def test_gemm_f16_every_tile(dev, monkeypatch, cfg):
     """Every tile configuration of gemm_f16_k (HX_GEMM_F16_CFG forces it): forward with bias and the
     beta = 1 data gradient, rows not a multiple of the tile."""

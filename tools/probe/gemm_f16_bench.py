@@ -23,9 +23,51 @@ def timed(fn, n=20):
     return ts[n // 2] * 1e3
 
 
+def sweep(C, dev, cfgs):
+    """fwd / dgrad (fp16x3 and bf16) of every shape under each forced tile configuration."""
+    T = int(os.environ.get('T', '16384'))
+    g = torch.Generator(device=dev).manual_seed(0)
+    for (name, N, K) in [('qkv', 2304, 768), ('attn_out', 768, 768), ('ffn_up', 3072, 768), ('ffn_down', 768, 3072)]:
+        x = torch.randn(T, K, device=dev, generator=g)
+        W = torch.randn(N, K, device=dev, generator=g) * 0.03
+        b = torch.randn(N, device=dev, generator=g)
+        xp = C().amax_rows(x)
+        wf, wt, wp = C().split_weight_f16([W])[0]
+        dy = torch.randn(T, N, device=dev, generator=g)
+        dp = C().amax_rows(dy)
+        acc = torch.randn(T, K, device=dev, generator=g)
+        d = torch.randn(T, K, device=dev, generator=g)
+        db = torch.zeros(K, device=dev)
+        xb, Wb = x.bfloat16(), W.bfloat16()
+        fl = 2.0 * T * N * K
+        for c in cfgs:
+            if c == 'plan':
+                os.environ.pop('HX_GEMM_F16_CFG', None)
+            else:
+                os.environ['HX_GEMM_F16_CFG'] = c
+            try:
+                if name == 'ffn_up':
+                    f = timed(lambda: C().gemm_f16_gelu(x, xp, wf, wp, b, 1))
+                else:
+                    f = timed(lambda: C().gemm_f16(x, xp, wf, wp, bias=b))
+                if name == 'ffn_down':
+                    dg = timed(lambda: C().gemm_f16_dgelu(dy, dp, wt, wp, d, None, db, 1))
+                else:
+                    dg = timed(lambda: C().gemm_f16(dy, dp, wt, wp, out=acc, beta=True))
+                bf = timed(lambda: C().gemm_bf16(xb, Wb, bias=b))
+            except RuntimeError as e:
+                print('{:10s} cfg {}: {}'.format(name, c, str(e).splitlines()[0]), flush=True)
+                continue
+            print('{:10s} cfg {:4s} fwd {:7.1f} us ({:4.2f} PF/s)  dgrad {:7.1f} us ({:4.2f})  bf16 fwd {:6.1f} us '
+                  '({:4.2f})'.format(name, c, f, 3 * fl / f / 1e9, dg, 3 * fl / dg / 1e9, bf, fl / bf / 1e9), flush=True)
+    os.environ.pop('HX_GEMM_F16_CFG', None)
+
+
 def main():
     from hetseq_9cme_amd.ops._ext import C
     dev = torch.device('cuda', 0)
+    if os.environ.get('CFGS'):
+        return sweep(C, dev, os.environ['CFGS'].split(','))
     T = int(os.environ.get('T', '16384'))
     g = torch.Generator(device=dev).manual_seed(0)
 

@@ -43,9 +43,9 @@ def parse():
     ap.add_argument('--seq', type=int, default=128)
     ap.add_argument('--max-pred', type=int, default=20)
     ap.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'])
-    ap.add_argument('--fp32-gemm', default='fp16x3', choices=['native', 'bf16x3', 'bf16x6', 'fp16x3'],
-                    help='fp32 linear GEMMs: fp16x3 (default, fp32 class: ops/gemm16.py), bf16x6 '
-                         '(fp32-exact class), bf16x3 (near-fp32) or native f32 MFMA (ops/split_gemm.py)')
+    ap.add_argument('--fp32-gemm', default='fp16x3', choices=['fp16x3', 'native'],
+                    help='fp32 GEMMs: fp16x3 (default, fp32 class: ops/gemm16.py) or native f32 MFMA '
+                         '(ops/fp32_mode.py)')
     ap.add_argument('--model', default='base', choices=['base', 'large', 'tiny'])
     ap.add_argument('--no-fused', action='store_true', help='torch-op baseline (A/B only)')
     ap.add_argument('--data-dir', default=None)

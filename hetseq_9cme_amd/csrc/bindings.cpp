@@ -145,8 +145,7 @@ inline float* amax_ptr(const OptT& a, int64_t need, const char* what) {
   return a->data_ptr<float>();
 }
 std::vector<Tensor> ln_fwd(Tensor y, OptT bias, OptT res, Tensor gamma, Tensor beta, double eps, double keep_prob,
-                           const Tensor& seed, int64_t stream, bool drop_after, bool save_z, int64_t npieces,
-                           OptT amax_out) {
+                           const Tensor& seed, int64_t stream, bool drop_after, bool save_z, OptT amax_out) {
   check_cuda(y, "input");
   const int H = (int)y.size(-1);
   const int64_t rows = y.numel() / H;
@@ -163,17 +162,13 @@ std::vector<Tensor> ln_fwd(Tensor y, OptT bias, OptT res, Tensor gamma, Tensor b
   Tensor z = save_z ? torch::empty_like(y) : Tensor();
   auto st = y.options().dtype(torch::kFloat32);
   auto mean = torch::empty({rows}, st), rstd = torch::empty({rows}, st);
-  TORCH_CHECK(npieces == 0 || ((npieces == 2 || npieces == 3) && y.scalar_type() == torch::kFloat32),
-              "ln_fwd: pieces (2 or 3) of an fp32 output only");
-  Tensor pcs = npieces ? torch::empty({rows, npieces * H}, y.options().dtype(torch::kBFloat16)) : Tensor();
   hx_ln_fwd(act_bf16(y), y.data_ptr(), ptr_or_null<float>(bias), has(res) ? res->data_ptr() : nullptr,
             gamma.data_ptr<float>(), beta.data_ptr<float>(), out.data_ptr(), save_z ? z.data_ptr() : nullptr,
             mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, H, (float)eps, (float)keep_prob, seed_ptr(seed),
             (uint64_t)stream, drop_after ? 1 : 0, cur_stream(y),
-            npieces ? reinterpret_cast<uint16_t*>(pcs.data_ptr()) : nullptr, (int)npieces,
             act_bf16(y) ? nullptr : amax_ptr(amax_out, hx_ln_fwd_blocks(rows), "ln_fwd amax"));
   dbg_finite(out, "ln_fwd");
-  return {out, z, mean, rstd, pcs};
+  return {out, z, mean, rstd};
 }
 
 std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tensor gamma, double keep_prob,
@@ -198,53 +193,15 @@ std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tens
             gamma.data_ptr<float>(), dz.data_ptr(), want_dy ? dy.data_ptr() : nullptr, partial.data_ptr<float>(), nblk,
             rows, H, (float)keep_prob, seed_ptr(seed), (uint64_t)stream, drop_after ? 1 : 0,
             (want_dy && want_dbias) ? 1 : 0, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
-            want_dbias ? dbias.data_ptr<float>() : nullptr, 0, nullptr, 0, 0, 0, cur_stream(z),
+            want_dbias ? dbias.data_ptr<float>() : nullptr, 0, cur_stream(z),
             act_bf16(z) ? nullptr : amax_ptr(amax_out, nblk, "ln_bwd amax"));
   dbg_finite(dz, "ln_bwd (dz)");
   return {dz, dy, dgamma, dbeta, dbias};
 }
 
-// LN backward whose dy (= dz * dropout mask / keep) leaves as bf16 split planes [rows, npl * H]
-// for the upstream linear's split-GEMM backward (--fp32-gemm bf16x3/x6): {dz, planes, dgamma,
-// dbeta, dbias}
-std::vector<Tensor> ln_bwd_planes(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tensor gamma, double keep_prob,
-                                  const Tensor& seed, int64_t stream, bool want_dbias, std::vector<int64_t> order,
-                                  int64_t npieces, OptT dgamma_out, OptT dbeta_out, OptT dbias_out) {
-  check_f32(dout, "grad_output");
-  check_f32(z, "saved input");
-  TORCH_CHECK(npieces == 2 || npieces == 3, "ln_bwd_planes: 2 or 3 pieces");
-  TORCH_CHECK(!order.empty() && order.size() <= 8, "ln_bwd_planes: 1..8 planes");
-  uint32_t packed = 0;
-  for (size_t k = 0; k < order.size(); ++k) {
-    TORCH_CHECK(order[k] >= 0 && order[k] < npieces, "ln_bwd_planes: piece index out of range");
-    packed |= (uint32_t)order[k] << (4 * k);
-  }
-  const int H = (int)z.size(-1);
-  TORCH_CHECK(H % 4 == 0, "ln_bwd_planes: H must be a multiple of 4");
-  const int64_t rows = z.numel() / H, npl = (int64_t)order.size();
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(z.device());
-  auto dz = torch::empty_like(z);
-  auto planes = torch::empty({rows, npl * H}, z.options().dtype(torch::kBFloat16));
-  auto f32 = z.options();
-  auto dgamma = has(dgamma_out) ? *dgamma_out : torch::empty({H}, f32);
-  auto dbeta = has(dbeta_out) ? *dbeta_out : torch::empty({H}, f32);
-  Tensor dbias = want_dbias ? (has(dbias_out) ? *dbias_out : torch::empty({H}, f32)) : Tensor();
-  TORCH_CHECK(dgamma.numel() == H && dbeta.numel() == H && dgamma.is_contiguous() && dbeta.is_contiguous(),
-              "bad dgamma/dbeta outputs");
-  const int nblk = hx_ln_bwd_blocks(rows);
-  auto partial = torch::empty({(int64_t)nblk * 3 * H}, f32);
-  hx_ln_bwd(0, dout.data_ptr(), z.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(), gamma.data_ptr<float>(),
-            dz.data_ptr(), nullptr, partial.data_ptr<float>(), nblk, rows, H, (float)keep_prob, seed_ptr(seed),
-            (uint64_t)stream, 0, want_dbias ? 1 : 0, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
-            want_dbias ? dbias.data_ptr<float>() : nullptr, 0, reinterpret_cast<uint16_t*>(planes.data_ptr()),
-            packed, (int)npl, (int)npieces, cur_stream(z));
-  dbg_finite(dz, "ln_bwd_planes (dz)");
-  return {dz, planes, dgamma, dbeta, dbias};
-}
-
 std::vector<Tensor> embed_ln_fwd(Tensor ids, OptT tt, Tensor wte, Tensor wpe, Tensor wtt, Tensor gamma, Tensor beta,
                                  double eps, double keep_prob, const Tensor& seed, int64_t stream, bool bf16_out,
-                                 int64_t npieces, OptT amax_out) {
+                                 OptT amax_out) {
   dbg_range(ids, 0, wte.size(0), "token ids");
   if (has(tt)) dbg_range(*tt, 0, wtt.size(0), "token type ids");
   check_cuda(ids, "input_ids");
@@ -262,17 +219,13 @@ std::vector<Tensor> embed_ln_fwd(Tensor ids, OptT tt, Tensor wte, Tensor wpe, Te
   auto out = torch::empty({B, S, H}, opt), z = torch::empty({B, S, H}, opt);
   auto f32 = wte.options();
   auto mean = torch::empty({B * S}, f32), rstd = torch::empty({B * S}, f32);
-  TORCH_CHECK(npieces == 0 || ((npieces == 2 || npieces == 3) && !bf16_out),
-              "embed_ln_fwd: pieces (2 or 3) of an fp32 output only");
-  Tensor pcs = npieces ? torch::empty({B * S, npieces * H}, wte.options().dtype(torch::kBFloat16)) : Tensor();
   hx_embed_ln_fwd(bf16_out ? 1 : 0, ids.data_ptr<int64_t>(), has(tt) ? tt->data_ptr<int64_t>() : nullptr,
                   wte.data_ptr<float>(), wpe.data_ptr<float>(), wtt.data_ptr<float>(), gamma.data_ptr<float>(),
                   beta.data_ptr<float>(), out.data_ptr(), z.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                   B * S, (int)S, H, (float)eps, (float)keep_prob, seed_ptr(seed), (uint64_t)stream, cur_stream(ids),
-                  npieces ? reinterpret_cast<uint16_t*>(pcs.data_ptr()) : nullptr, (int)npieces,
                   bf16_out ? nullptr : amax_ptr(amax_out, hx_ln_fwd_blocks(B * S), "embed_ln_fwd amax"));
   dbg_finite(out, "embed_ln_fwd");
-  return {out, z, mean, rstd, pcs};
+  return {out, z, mean, rstd};
 }
 
 // Scatter-ACCUMULATES the embedding gradients into dwte / dwpe / dwtt (caller zeroes them
@@ -378,7 +331,7 @@ Tensor softmax_xent_(Tensor logits, OptT bias, Tensor labels, int64_t ignore_ind
 
 // ------------------------------------------------------------------ attention
 std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed, int64_t stream,
-                             OptT bias, bool split = false, int64_t npieces = 0, OptT amax_out = OptT()) {
+                             OptT bias, bool split = false, OptT amax_out = OptT()) {
   check_cuda(qkv, "qkv");
   const int bf = act_bf16(qkv);
   check_f32(mask_bias, "mask_bias");
@@ -399,15 +352,11 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
   if (keep < 1.0) dmask = torch::empty({B, nh, Sp, Sp / 32}, qkv.options().dtype(torch::kInt32));
   else dmask = torch::empty({0}, qkv.options().dtype(torch::kInt32));
   uint32_t* dm = keep < 1.0 ? reinterpret_cast<uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr;
-  Tensor pcs;
   if (split) {
     TORCH_CHECK(!bf, "attn_fwd_x6: fp32 activations only");
-    TORCH_CHECK(npieces == 0 || npieces == 2 || npieces == 3, "attn_fwd_x6: 0, 2 or 3 output pieces");
-    if (npieces) pcs = torch::empty({B * S, npieces * H}, qkv.options().dtype(torch::kBFloat16));
     hx_attn_fwd_x6(qkv.data_ptr<float>(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(),
                    out.data_ptr<float>(), lse.data_ptr<float>(), dm, (int)B, (int)S, (int)nh, (float)keep,
                    seed_ptr(seed), (uint64_t)stream, cur_stream(qkv),
-                   npieces ? reinterpret_cast<uint16_t*>(pcs.data_ptr()) : nullptr, (int)npieces,
                    amax_ptr(amax_out, ((S + 127) / 128) * nh * B * 4, "attn_fwd_x6 amax"));
   } else {
     hx_attn_fwd(bf, qkv.data_ptr(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(), out.data_ptr(),
@@ -415,37 +364,23 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
                 cur_stream(qkv));
   }
   dbg_finite(out, "attn_fwd");
-  if (split) return {out, lse, dmask, pcs};
   return {out, lse, dmask};
 }
-// fp32 attention forward on the bf16 matrix cores (split pieces, attention_x6.hip); returns
-// {out, lse, dmask, pieces of out (npieces > 0) or an undefined tensor}
+// fp32 attention forward on the bf16 matrix cores (split pieces, attention_x6.hip): {out, lse, dmask}
 std::vector<Tensor> attn_fwd_x6(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed,
-                                int64_t stream, OptT bias, int64_t npieces, OptT amax_out) {
-  return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, true, npieces, amax_out);
+                                int64_t stream, OptT bias, OptT amax_out) {
+  return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, true, amax_out);
 }
 
 // returns {dqkv, dbias} (dbias: [3H] fp32 when bias is given -- written into dbq/dbk/dbv
 // when those slots are given -- else an empty tensor)
-// planes form (split only, S <= 128): dQKV as the stacked bf16 planes of order `order`
-// ([B*S, len(order) * 3H]) instead of fp32; returns {planes, dbias}
 std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask,
                              int64_t nh, double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, bool split = false,
-                             const std::vector<int64_t>& order = {}, OptT amax_out = OptT()) {
+                             OptT amax_out = OptT()) {
   check_cuda(dout, "grad_output");
   check_cuda(qkv, "qkv");
   const int bf = act_bf16(qkv);
   TORCH_CHECK(!(split && bf), "attn_bwd_x6: fp32 activations only");
-  const bool pl = !order.empty();
-  uint32_t porder = 0;
-  if (pl) {
-    TORCH_CHECK(split && qkv.size(1) <= 128, "attn_bwd_x6_planes: fp32 split path with S <= 128 only");
-    TORCH_CHECK(order.size() <= 8, "attn_bwd_x6_planes: 1..8 planes");
-    for (size_t k = 0; k < order.size(); ++k) {
-      TORCH_CHECK(order[k] >= 0 && order[k] < 3, "attn_bwd_x6_planes: piece index out of range");
-      porder |= (uint32_t)order[k] << (4 * k);
-    }
-  }
   TORCH_CHECK(dout.scalar_type() == qkv.scalar_type() && out.scalar_type() == qkv.scalar_type(),
               "attention activations must share one dtype");
   const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(2) / 3;
@@ -454,9 +389,7 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor o
   // memset).  Otherwise dQ partials from the S/128 key blocks are added atomically in
   // fp32: into dqkv itself (fp32, zero-filled) or a [B, S, H] fp32 scratch (bf16).
   const bool multi = S > 128;
-  Tensor dqkv, planes;
-  if (pl) planes = torch::empty({B * S, (int64_t)order.size() * 3 * H}, qkv.options().dtype(torch::kBFloat16));
-  else dqkv = (multi && !bf) ? torch::zeros_like(qkv) : torch::empty_like(qkv);
+  Tensor dqkv = (multi && !bf) ? torch::zeros_like(qkv) : torch::empty_like(qkv);
   Tensor dq32;
   float* dq_acc = nullptr;
   int dq_ld = 0;
@@ -487,10 +420,8 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor o
   hx_attn_bwd(split ? 2 : bf, qkv.data_ptr(), ptr_or_null<float>(bias), pq, pk, pv, part.defined() ? part.data_ptr<float>() : nullptr,
               mask_bias.data_ptr<float>(), dout.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
               keep < 1.0 ? reinterpret_cast<const uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr,
-              pl ? nullptr : dqkv.data_ptr(), dq_acc, dq_ld, (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv),
-              pl ? reinterpret_cast<uint16_t*>(planes.data_ptr()) : nullptr, porder, (int)order.size(),
-              (split && !pl && !multi) ? amax_ptr(amax_out, B * nh, "attn_bwd_x6 amax") : nullptr);
-  if (pl) return {planes, dbias};
+              dqkv.data_ptr(), dq_acc, dq_ld, (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv),
+              (split && !multi) ? amax_ptr(amax_out, B * nh, "attn_bwd_x6 amax") : nullptr);
   if (multi && bf) dqkv.narrow(-1, 0, H).copy_(dq32);
   dbg_finite(dqkv, "attn_bwd");
   return {dqkv, dbias};
@@ -523,316 +454,6 @@ Tensor wgrad_bf16(Tensor dy, Tensor x, Tensor out) {
                 cur_stream(dy));
   dbg_finite(out, "wgrad_bf16");
   return out;
-}
-
-// ------------------------------------------------------------------ split-piece weight gradient
-// dys: [T, n * M] bf16 planes of dY, xs: [T, n * N] planes of X (ops/split_gemm.py layouts);
-// dy_off / x_off: column offset (elements) of each distinct piece inside a row.
-bool wgrad_split_ok(const Tensor& dys, const Tensor& xs, int64_t M, int64_t N) {
-  if (!dys.is_cuda() || dys.scalar_type() != torch::kBFloat16 || xs.scalar_type() != torch::kBFloat16) return false;
-  if (dys.dim() != 2 || xs.dim() != 2 || dys.size(0) != xs.size(0) || !dys.is_contiguous() || !xs.is_contiguous())
-    return false;
-  if (!aligned16(dys.data_ptr()) || !aligned16(xs.data_ptr())) return false;
-  return M % 128 == 0 && N % 128 == 0 && dys.size(1) % 8 == 0 && xs.size(1) % 8 == 0 && dys.size(0) < (1LL << 31) &&
-         (int64_t)dys.size(0) * dys.size(1) * 2 < (1LL << 32) && (int64_t)xs.size(0) * xs.size(1) * 2 < (1LL << 32);
-}
-Tensor wgrad_split(Tensor dys, std::vector<int64_t> dy_off, Tensor xs, std::vector<int64_t> x_off, int64_t passes,
-                   int64_t M, int64_t N, Tensor out) {
-  TORCH_CHECK(wgrad_split_ok(dys, xs, M, N), "wgrad_split: unsupported operands");
-  TORCH_CHECK(passes == 3 || passes == 6, "wgrad_split: passes must be 3 or 6");
-  const size_t npc = passes == 6 ? 3 : 2;
-  TORCH_CHECK(dy_off.size() == npc && x_off.size() == npc, "wgrad_split: one offset per piece");
-  for (size_t i = 0; i < npc; ++i) {
-    TORCH_CHECK(dy_off[i] >= 0 && dy_off[i] + M <= dys.size(1) && dy_off[i] % 8 == 0, "wgrad_split: bad dY offset");
-    TORCH_CHECK(x_off[i] >= 0 && x_off[i] + N <= xs.size(1) && x_off[i] % 8 == 0, "wgrad_split: bad X offset");
-  }
-  check_f32(out, "wgrad out");
-  // out may hold fewer rows than the (tile-padded) M: rows past out.size(0) are not stored
-  TORCH_CHECK(out.size(0) <= M && out.size(0) > 0 && out.size(1) == N && out.is_contiguous(),
-              "wgrad out must be [<= M, N]");
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(dys.device());
-  const int64_t T = dys.size(0);
-  int cfg = 0, nsplit = 1;
-  hx_wgrad_split_plan((int)M, (int)N, (int)T, (int)passes, &cfg, &nsplit);
-  Tensor ws;
-  if (nsplit > 1) ws = torch::empty({nsplit * M * N}, out.options());
-  const void* dp[3];
-  const void* xp[3];
-  const char* db = reinterpret_cast<const char*>(dys.data_ptr());
-  const char* xb = reinterpret_cast<const char*>(xs.data_ptr());
-  for (size_t i = 0; i < 3; ++i) {
-    dp[i] = db + 2 * dy_off[i < npc ? i : 0];
-    xp[i] = xb + 2 * x_off[i < npc ? i : 0];
-  }
-  TORCH_CHECK(hx_wgrad_split(dp, (int)dys.size(1), xp, (int)xs.size(1), (int)passes, out.data_ptr<float>(),
-                             nsplit > 1 ? ws.data_ptr<float>() : nullptr, (int)M, (int)N, (int)T, cfg, nsplit,
-                             (int)out.size(0), cur_stream(dys)) == 0,
-              "wgrad_split: launch failed");
-  dbg_finite(out, "wgrad_split");
-  return out;
-}
-
-// two weight gradients over the same tokens in one launch (wgrad_split.hip, bf16x6): each item is
-// (dys, dy_off, xs, x_off, M, N, out) as for wgrad_split; false when the pair does not qualify
-bool wgrad_split_group(std::vector<py::tuple> items) {
-  TORCH_CHECK(items.size() == 2, "wgrad_split_group: two products");
-  struct It {
-    Tensor dys, xs, out;
-    std::vector<int64_t> doff, xoff;
-    int64_t M, N;
-  };
-  It it[2];
-  for (int k = 0; k < 2; ++k) {
-    const py::tuple& t = items[k];
-    TORCH_CHECK(t.size() == 7, "wgrad_split_group: (dys, dy_off, xs, x_off, M, N, out)");
-    it[k].dys = t[0].cast<Tensor>();
-    it[k].doff = t[1].cast<std::vector<int64_t>>();
-    it[k].xs = t[2].cast<Tensor>();
-    it[k].xoff = t[3].cast<std::vector<int64_t>>();
-    it[k].M = t[4].cast<int64_t>();
-    it[k].N = t[5].cast<int64_t>();
-    it[k].out = t[6].cast<Tensor>();
-    TORCH_CHECK(wgrad_split_ok(it[k].dys, it[k].xs, it[k].M, it[k].N), "wgrad_split_group: unsupported operands");
-    TORCH_CHECK(it[k].doff.size() == 3 && it[k].xoff.size() == 3, "wgrad_split_group: three pieces (bf16x6)");
-    for (int i = 0; i < 3; ++i) {
-      TORCH_CHECK(it[k].doff[i] >= 0 && it[k].doff[i] + it[k].M <= it[k].dys.size(1) && it[k].doff[i] % 8 == 0,
-                  "wgrad_split_group: bad dY offset");
-      TORCH_CHECK(it[k].xoff[i] >= 0 && it[k].xoff[i] + it[k].N <= it[k].xs.size(1) && it[k].xoff[i] % 8 == 0,
-                  "wgrad_split_group: bad X offset");
-    }
-    check_f32(it[k].out, "wgrad_split_group out");
-    TORCH_CHECK(it[k].out.size(0) <= it[k].M && it[k].out.size(0) > 0 && it[k].out.size(1) == it[k].N &&
-                    it[k].out.is_contiguous(),
-                "wgrad_split_group: out must be [<= M, N]");
-  }
-  const int64_t T = it[0].dys.size(0);
-  TORCH_CHECK(it[1].dys.size(0) == T && it[0].dys.device() == it[1].dys.device(),
-              "wgrad_split_group: same tokens, same device");
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(it[0].dys.device());
-  const int nsplit = hx_wgrad_split_group_plan((int)it[0].M, (int)it[0].N, (int)it[1].M, (int)it[1].N, (int)T, 6);
-  if (nsplit < 1) return false;
-  Tensor ws[2];
-  const void* dp[2][3];
-  const void* xp[2][3];
-  for (int k = 0; k < 2; ++k) {
-    if (nsplit > 1) ws[k] = torch::empty({nsplit * it[k].M * it[k].N}, it[k].out.options());
-    const char* db = reinterpret_cast<const char*>(it[k].dys.data_ptr());
-    const char* xb = reinterpret_cast<const char*>(it[k].xs.data_ptr());
-    for (int i = 0; i < 3; ++i) {
-      dp[k][i] = db + 2 * it[k].doff[i];
-      xp[k][i] = xb + 2 * it[k].xoff[i];
-    }
-  }
-  TORCH_CHECK(hx_wgrad_split_group(dp[0], (int)it[0].dys.size(1), xp[0], (int)it[0].xs.size(1),
-                                   it[0].out.data_ptr<float>(), nsplit > 1 ? ws[0].data_ptr<float>() : nullptr,
-                                   (int)it[0].M, (int)it[0].N, (int)it[0].out.size(0), dp[1], (int)it[1].dys.size(1),
-                                   xp[1], (int)it[1].xs.size(1), it[1].out.data_ptr<float>(),
-                                   nsplit > 1 ? ws[1].data_ptr<float>() : nullptr, (int)it[1].M, (int)it[1].N,
-                                   (int)it[1].out.size(0), (int)T, nsplit, cur_stream(it[0].dys)) == 0,
-              "wgrad_split_group: launch failed");
-  dbg_finite(it[0].out, "wgrad_split_group");
-  dbg_finite(it[1].out, "wgrad_split_group");
-  return true;
-}
-
-// ------------------------------------------------------------------ bias + activation -> planes
-// forward (dout absent): planes of act(y + b); backward: planes of dout * act'(y + b) and dbias.
-std::vector<Tensor> bias_act_planes(Tensor y, OptT b, OptT dout, int64_t act, std::vector<int64_t> order,
-                                    int64_t npieces, OptT dbias_out) {
-  check_f32(y, "bias_act_planes input");
-  const int N = (int)y.size(-1);
-  const int64_t rows = y.numel() / N;
-  TORCH_CHECK(N % 8 == 0 && aligned16(y.data_ptr()), "bias_act_planes: last dim must be a multiple of 8");
-  TORCH_CHECK(npieces == 2 || npieces == 3, "bias_act_planes: 2 or 3 pieces");
-  TORCH_CHECK(!order.empty() && order.size() <= 8, "bias_act_planes: 1..8 planes");
-  uint32_t packed = 0;
-  for (size_t j = 0; j < order.size(); ++j) {
-    TORCH_CHECK(order[j] >= 0 && order[j] < npieces, "bias_act_planes: piece index out of range");
-    packed |= (uint32_t)order[j] << (4 * j);
-  }
-  if (has(b)) TORCH_CHECK(b->numel() == N && b->scalar_type() == torch::kFloat32, "bias_act_planes: bad bias");
-  if (has(dout)) {
-    check_f32(*dout, "bias_act_planes grad");
-    TORCH_CHECK(dout->numel() == y.numel(), "bias_act_planes: grad shape");
-  }
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(y.device());
-  const int64_t npl = (int64_t)order.size();
-  Tensor planes = torch::empty({rows, npl * N}, y.options().dtype(torch::kBFloat16));
-  Tensor dbias, ws;
-  const bool want_db = has(dout);
-  if (want_db) {
-    auto f32 = y.options().dtype(torch::kFloat32);
-    dbias = has(dbias_out) ? *dbias_out : torch::empty({N}, f32);
-    ws = torch::empty({(int64_t)hx_colsum_ws_floats(rows, N)}, f32);
-  }
-  hx_bias_act_planes((int)act, y.data_ptr<float>(), ptr_or_null<float>(b), has(dout) ? dout->data_ptr<float>() : nullptr,
-                     reinterpret_cast<uint16_t*>(planes.data_ptr()), want_db ? ws.data_ptr<float>() : nullptr,
-                     want_db ? dbias.data_ptr<float>() : nullptr, rows, N, (int)npieces, (int)npl, packed,
-                     cur_stream(y));
-  return {planes, dbias};
-}
-
-// ------------------------------------------------------------------ piece GEMMs
-std::vector<Tensor> split_weight(Tensor W, int64_t npieces, int64_t b16) {
-  check_f32(W, "split_weight input");
-  TORCH_CHECK(W.dim() == 2 && W.size(0) % 64 == 0 && W.size(1) % 64 == 0 && aligned16(W.data_ptr()),
-              "split_weight: W must be [N, K] with N, K multiples of 64");
-  TORCH_CHECK(npieces == 2 || npieces == 3, "split_weight: 2 or 3 pieces");
-  const int64_t N = W.size(0), K = W.size(1);
-  auto bf = W.options().dtype(torch::kBFloat16);
-  Tensor wf = torch::empty({N, npieces * K}, bf), wt = torch::empty({K, npieces * N}, bf);
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(W.device());
-  TORCH_CHECK(!b16 || npieces == 3, "split_weight: the B16 layout is for 3 pieces");
-  TORCH_CHECK(b16 >= 0 && b16 <= 3, "split_weight: b16 is a 2-bit mask");
-  hx_split_weight(W.data_ptr<float>(), (int)N, (int)K, (int)npieces, reinterpret_cast<uint16_t*>(wf.data_ptr()),
-                  reinterpret_cast<uint16_t*>(wt.data_ptr()), cur_stream(W), (int)b16);
-  return {wf, wt};
-}
-
-// split_weight for a list of weights in ONE launch: [(wf, wt)] per weight, masks as split_weight's b16
-std::vector<std::vector<Tensor>> split_weight_many(std::vector<Tensor> Ws, int64_t npieces, std::vector<int64_t> masks) {
-  TORCH_CHECK(!Ws.empty() && Ws.size() <= HX_WBATCH && masks.size() == Ws.size(),
-              "split_weight_many: 1..64 weights, one mask each");
-  TORCH_CHECK(npieces == 2 || npieces == 3, "split_weight_many: 2 or 3 pieces");
-  HxWeightBatch d{};
-  d.n = (int)Ws.size();
-  std::vector<std::vector<Tensor>> out;
-  int tiles = 0;
-  for (int i = 0; i < d.n; ++i) {
-    const Tensor& W = Ws[i];
-    check_f32(W, "split_weight_many input");
-    TORCH_CHECK(W.dim() == 2 && W.is_contiguous() && W.size(0) % 64 == 0 && W.size(1) % 64 == 0 &&
-                    aligned16(W.data_ptr()) && W.device() == Ws[0].device(),
-                "split_weight_many: every W contiguous [N, K], N and K multiples of 64, one device");
-    TORCH_CHECK(masks[i] >= 0 && masks[i] <= 3 && (!masks[i] || npieces == 3), "split_weight_many: mask");
-    const int64_t N = W.size(0), K = W.size(1);
-    auto bf = W.options().dtype(torch::kBFloat16);
-    Tensor wf = torch::empty({N, npieces * K}, bf), wt = torch::empty({K, npieces * N}, bf);
-    d.W[i] = W.data_ptr<float>();
-    d.wf[i] = reinterpret_cast<uint16_t*>(wf.data_ptr());
-    d.wt[i] = reinterpret_cast<uint16_t*>(wt.data_ptr());
-    d.N[i] = (int)N;
-    d.K[i] = (int)K;
-    d.mask[i] = (int)masks[i];
-    d.start[i] = tiles;
-    tiles += (int)((N / 64) * (K / 64));
-    out.push_back({wf, wt});
-  }
-  d.start[d.n] = tiles;
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(Ws[0].device());
-  hx_split_weight_many(d, (int)npieces, cur_stream(Ws[0]));
-  return out;
-}
-
-// a: [M, npc * K] pieces (piece p at column p * K), b: [N, npc * K]; out [M, N] fp32 (+= if beta)
-bool gemm_split_ok(const Tensor& a, const Tensor& b, int64_t npc) {
-  if (!a.is_cuda() || a.scalar_type() != torch::kBFloat16 || b.scalar_type() != torch::kBFloat16) return false;
-  if (a.dim() != 2 || b.dim() != 2 || !a.is_contiguous() || !b.is_contiguous()) return false;
-  if (a.size(1) != b.size(1) || a.size(1) % npc) return false;
-  const int64_t K = a.size(1) / npc;
-  const int cfg = hx_gemm_split_plan((int)a.size(0), (int)b.size(0), (int)K, npc == 3 ? 6 : 3);
-  const int kal = (npc == 3 && cfg != 2) ? 16 : 32;   // k step of the configuration
-  return cfg >= 0 && K % kal == 0 &&
-         aligned16(a.data_ptr()) && aligned16(b.data_ptr()) && a.size(0) < (1LL << 31) &&
-         256 * a.size(1) * 2 < (1LL << 31) && b.size(0) * a.size(1) * 2 < (1LL << 31) &&
-         256 * b.size(0) * 6 < (1LL << 31);
-}
-// lay: bit 0 / bit 1 = A / B operand in the B16 piece layout (gemm_split.hip)
-static int gemm_split_launch(const Tensor& a, const Tensor& b, int64_t passes, float* C, int64_t ldc, bool beta,
-                             const HxGemmEpi* epi, int64_t lay = 0) {
-  const int64_t npc = passes == 6 ? 3 : 2;
-  const int64_t M = a.size(0), N = b.size(0), K = a.size(1) / npc;
-  const int cfg = hx_gemm_split_plan((int)M, (int)N, (int)K, (int)passes, (int)lay);
-  return hx_gemm_split_nt(a.data_ptr(), npc * K, (lay & 1) ? 16 : K, b.data_ptr(), npc * K, (lay & 2) ? 16 : K, C, ldc,
-                          (int)M, (int)N, (int)K, (int)passes, beta ? 1 : 0, epi, cfg, cur_stream(a), (int)lay);
-}
-Tensor gemm_split(Tensor a, Tensor b, int64_t passes, OptT out_, bool beta, int64_t lay) {
-  const int64_t npc = passes == 6 ? 3 : 2;
-  TORCH_CHECK(passes == 3 || passes == 6, "gemm_split: passes must be 3 or 6");
-  TORCH_CHECK(gemm_split_ok(a, b, npc), "gemm_split: unsupported operands");
-  const int64_t M = a.size(0), N = b.size(0);
-  Tensor out = has(out_) ? *out_ : torch::empty({M, N}, a.options().dtype(torch::kFloat32));
-  TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.dim() == 2 && out.size(0) == M && out.size(1) == N &&
-                  out.stride(1) == 1 && out.stride(0) % 4 == 0 && aligned16(out.data_ptr()),
-              "gemm_split: out must be fp32 [M, N] with unit column stride and 16-B rows");
-  TORCH_CHECK(!beta || has(out_), "gemm_split: beta needs an output to accumulate into");
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
-  TORCH_CHECK(gemm_split_launch(a, b, passes, out.data_ptr<float>(), out.stride(0), beta, nullptr, lay) == 0,
-              "gemm_split: launch failed");
-  dbg_finite(out, "gemm_split");
-  return out;
-}
-// a . b^T over a deep reduction with few output tiles: ks split-K slabs (hx_gemm_split_ks when
-// ks = 0) written as partial products, summed here; lay as gemm_split
-Tensor gemm_split_k(Tensor a, Tensor b, int64_t passes, int64_t ks, int64_t lay) {
-  const int64_t npc = passes == 6 ? 3 : 2;
-  TORCH_CHECK(passes == 3 || passes == 6, "gemm_split_k: passes must be 3 or 6");
-  TORCH_CHECK(gemm_split_ok(a, b, npc), "gemm_split_k: unsupported operands");
-  const int64_t M = a.size(0), N = b.size(0), K = a.size(1) / npc;
-  if (ks <= 0) ks = hx_gemm_split_ks((int)M, (int)N, (int)K, (int)passes);
-  if (ks == 1) return gemm_split(a, b, passes, OptT(), false, lay);
-  Tensor part = torch::empty({ks, M, N}, a.options().dtype(torch::kFloat32));
-  const int cfg = hx_gemm_split_plan((int)M, (int)N, (int)K, (int)passes, (int)lay);
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
-  TORCH_CHECK(hx_gemm_split_nt(a.data_ptr(), npc * K, (lay & 1) ? 16 : K, b.data_ptr(), npc * K, (lay & 2) ? 16 : K,
-                               part.data_ptr<float>(), N, (int)M, (int)N, (int)K, (int)passes, 0, nullptr, cfg,
-                               cur_stream(a), (int)lay, (int)ks, M * N) == 0,
-              "gemm_split_k: launch failed (slab count must divide the k steps)");
-  Tensor out = part.sum(0);
-  dbg_finite(out, "gemm_split_k");
-  return out;
-}
-// FFN up: u = a . b^T + bias (fp32, kept for the backward) and the pieces of gelu(u)
-// (dmode 1: C gets gelu'(u) instead of u -- all the backward needs, from the same erf)
-std::vector<Tensor> gemm_split_gelu(Tensor a, Tensor b, int64_t passes, OptT bias, int64_t lay, int64_t dmode) {
-  const int64_t npc = passes == 6 ? 3 : 2;
-  TORCH_CHECK(passes == 3 || passes == 6, "gemm_split_gelu: passes must be 3 or 6");
-  TORCH_CHECK(gemm_split_ok(a, b, npc), "gemm_split_gelu: unsupported operands");
-  const int64_t M = a.size(0), N = b.size(0);
-  if (has(bias)) {
-    check_f32(*bias, "gemm_split_gelu bias");
-    TORCH_CHECK(bias->numel() == N && bias->is_contiguous() && aligned16(bias->data_ptr()), "gemm_split_gelu: bias");
-  }
-  Tensor u = torch::empty({M, N}, a.options().dtype(torch::kFloat32));
-  Tensor p = torch::empty({M, npc * N}, a.options());
-  HxGemmEpi e{1, ptr_or_null<float>(bias), nullptr, 0, reinterpret_cast<uint16_t*>(p.data_ptr()), npc * N, N,
-              nullptr, dmode ? 1 : 0};
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
-  TORCH_CHECK(gemm_split_launch(a, b, passes, u.data_ptr<float>(), N, false, &e, lay) == 0,
-              "gemm_split_gelu: launch failed");
-  dbg_finite(u, "gemm_split_gelu");
-  return {u, p};
-}
-// FFN down data gradient + GELU backward: t = (a . b^T) * gelu'(u (+ bias)); returns the pieces of
-// t and d bias = column sums of t (into dbias_out when given)
-// (dmode 1: u holds gelu'(u) from gemm_split_gelu(dmode=1); bias must be None)
-std::vector<Tensor> gemm_split_dgelu(Tensor a, Tensor b, int64_t passes, Tensor u, OptT bias, OptT dbias_out,
-                                     int64_t lay, int64_t dmode) {
-  TORCH_CHECK(!dmode || !has(bias), "gemm_split_dgelu: dmode 1 takes gelu'(u), which has the bias in it");
-  const int64_t npc = passes == 6 ? 3 : 2;
-  TORCH_CHECK(passes == 3 || passes == 6, "gemm_split_dgelu: passes must be 3 or 6");
-  TORCH_CHECK(gemm_split_ok(a, b, npc), "gemm_split_dgelu: unsupported operands");
-  const int64_t M = a.size(0), N = b.size(0);
-  check_f32(u, "gemm_split_dgelu pre-activation");
-  TORCH_CHECK(u.dim() == 2 && u.size(0) == M && u.size(1) == N && u.is_contiguous() && aligned16(u.data_ptr()),
-              "gemm_split_dgelu: u must be fp32 [M, N]");
-  if (has(bias)) {
-    check_f32(*bias, "gemm_split_dgelu bias");
-    TORCH_CHECK(bias->numel() == N && bias->is_contiguous() && aligned16(bias->data_ptr()), "gemm_split_dgelu: bias");
-  }
-  const int cfg = hx_gemm_split_plan((int)M, (int)N, (int)(a.size(1) / npc), (int)passes, (int)lay);
-  const int prow = hx_gemm_split_colpart_rows((int)M, cfg);
-  auto f32 = a.options().dtype(torch::kFloat32);
-  Tensor p = torch::empty({M, npc * N}, a.options());
-  Tensor part = torch::empty({prow, N}, f32);
-  Tensor db = has(dbias_out) ? *dbias_out : torch::empty({N}, f32);
-  TORCH_CHECK(db.numel() == N && db.scalar_type() == torch::kFloat32 && db.is_contiguous(), "gemm_split_dgelu: dbias");
-  HxGemmEpi e{2, ptr_or_null<float>(bias), u.data_ptr<float>(), N, reinterpret_cast<uint16_t*>(p.data_ptr()),
-              npc * N, N, part.data_ptr<float>(), dmode ? 1 : 0};
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
-  TORCH_CHECK(gemm_split_launch(a, b, passes, nullptr, N, false, &e, lay) == 0, "gemm_split_dgelu: launch failed");
-  hx_fold_cols(part.data_ptr<float>(), prow, (int)N, db.data_ptr<float>(), 0, cur_stream(a));
-  return {p, db};
 }
 
 // ------------------------------------------------------------------ fp16x3 GEMMs (gemm_f16.hip)
@@ -1119,77 +740,6 @@ std::vector<Tensor> weight_bf16_t(std::vector<Tensor> Ws) {
   return out;
 }
 
-// diagnostic: per-wave phase cycle sums of the piece GEMM main loop (cfg 0, bf16x6)
-Tensor gemm_split_stamps(Tensor a, Tensor b, int64_t lay) {
-  TORCH_CHECK(gemm_split_ok(a, b, 3), "gemm_split_stamps: unsupported operands");
-  const int64_t M = a.size(0), N = b.size(0), K = a.size(1) / 3;
-  const int64_t tiles = ((M + 255) / 256) * (N / 192);
-  Tensor st = torch::zeros({8 * ((tiles + 7) / 8) * 8, 5}, a.options().dtype(torch::kInt64));
-  Tensor out = torch::empty({M, N}, a.options().dtype(torch::kFloat32));
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
-  TORCH_CHECK(hx_gemm_split_stamps(a.data_ptr(), b.data_ptr(), out.data_ptr<float>(), (int)M, (int)N, (int)K,
-                                   reinterpret_cast<unsigned long long*>(st.data_ptr()), cur_stream(a),
-                                   (int)lay) > 0,
-              "gemm_split_stamps: launch failed");
-  return st;
-}
-
-void dma_probe(Tensor src, int64_t seg, int64_t ld, int64_t iters, int64_t grid) {
-  TORCH_CHECK(src.is_cuda() && src.nbytes() < (1LL << 32) && src.nbytes() > (1 << 20), "dma_probe: src");
-  TORCH_CHECK(seg == 1024 || seg == 128 || seg == 64 || seg == 32, "dma_probe: seg");
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(src.device());
-  hx_dma_probe(src.data_ptr(), (uint32_t)src.nbytes(), (int)seg, (int)ld, (int)iters, (int)grid, cur_stream(src));
-}
-
-// ------------------------------------------------------------------ split planes
-Tensor split_planes(Tensor x, std::vector<int64_t> order, int64_t npieces, bool stacked, int64_t rpad,
-                    int64_t dpad) {
-  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kFloat32, "split input must be an fp32 GPU tensor");
-  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "split_planes: x must be [R, D] fp32 with unit column stride");
-  TORCH_CHECK(npieces == 2 || npieces == 3, "split_planes: 2 or 3 pieces");
-  TORCH_CHECK(!order.empty() && order.size() <= 8, "split_planes: 1..8 planes");
-  uint32_t packed = 0;
-  for (size_t j = 0; j < order.size(); ++j) {
-    TORCH_CHECK(order[j] >= 0 && order[j] < npieces, "split_planes: piece index out of range");
-    packed |= (uint32_t)order[j] << (4 * j);
-  }
-  const int64_t R = x.size(0), D = x.size(1), npl = (int64_t)order.size();
-  const int64_t Rp = std::max<int64_t>(R, rpad), Dp = std::max<int64_t>(D, dpad);
-  TORCH_CHECK(Rp * Dp < (1LL << 40) && Dp < (1LL << 31), "split_planes: too large");
-  Tensor out = stacked ? torch::empty({npl * Rp, Dp}, x.options().dtype(torch::kBFloat16))
-                       : torch::empty({Rp, npl * Dp}, x.options().dtype(torch::kBFloat16));
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  // interleaved rows past R (row padding, e.g. the vocabulary padded to 256 for aligned GEMM
-  // output rows): the kernel fills the first R rows, the tail is zeroed
-  hx_split_planes(x.data_ptr<float>(), x.stride(0), reinterpret_cast<uint16_t*>(out.data_ptr()), R, (int)D,
-                  stacked ? Rp : R, (int)Dp, (int)npieces, (int)npl, packed, stacked ? 1 : 0, cur_stream(x));
-  if (!stacked && Rp > R) out.narrow(0, R, Rp - R).zero_();
-  return out;
-}
-
-// W [N, K] fp32 -> [K, npl * Np] bf16 transposed planes (the data-gradient operand in NT form)
-Tensor split_planes_t(Tensor W, std::vector<int64_t> order, int64_t npieces, int64_t npad) {
-  TORCH_CHECK(W.is_cuda() && W.scalar_type() == torch::kFloat32, "split_planes_t: W must be an fp32 GPU tensor");
-  TORCH_CHECK(W.dim() == 2 && W.stride(1) == 1 && W.stride(0) % 4 == 0 && aligned16(W.data_ptr()),
-              "split_planes_t: W must be [N, K] with 16-B aligned rows");
-  TORCH_CHECK(npieces == 2 || npieces == 3, "split_planes_t: 2 or 3 pieces");
-  TORCH_CHECK(!order.empty() && order.size() <= 8, "split_planes_t: 1..8 planes");
-  uint32_t packed = 0;
-  for (size_t j = 0; j < order.size(); ++j) {
-    TORCH_CHECK(order[j] >= 0 && order[j] < npieces, "split_planes_t: piece index out of range");
-    packed |= (uint32_t)order[j] << (4 * j);
-  }
-  const int64_t N = W.size(0), K = W.size(1), npl = (int64_t)order.size();
-  const int64_t Np = std::max<int64_t>(N, npad);
-  TORCH_CHECK(K % 64 == 0 && Np % 64 == 0 && K * npl * Np < (1LL << 40) && Np < (1LL << 24) && K < 65536 * 64,
-              "split_planes_t: K and the padded N must be multiples of 64");
-  Tensor out = torch::empty({K, npl * Np}, W.options().dtype(torch::kBFloat16));
-  c10::hip::HIPGuardMasqueradingAsCUDA guard(W.device());
-  hx_split_planes_t(W.data_ptr<float>(), W.stride(0), (int)N, (int)K, reinterpret_cast<uint16_t*>(out.data_ptr()),
-                    (int)Np, (int)npieces, (int)npl, packed, cur_stream(W));
-  return out;
-}
-
 // ------------------------------------------------------------------ xGMI all-reduce
 // Contexts travel to Python as integers (owned by parallel/xgmi.py).
 inline void xar_check(int rc) { TORCH_CHECK(rc == 0, hx_xar_last_error()); }
@@ -1269,17 +819,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adadelta", &adadelta);
   m.def("ln_fwd", &ln_fwd, py::arg("y"), py::arg("bias"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
         py::arg("eps"), py::arg("keep_prob"), py::arg("seed"), py::arg("stream"), py::arg("drop_after"),
-        py::arg("save_z"), py::arg("npieces") = 0, py::arg("amax_out") = py::none());
+        py::arg("save_z"), py::arg("amax_out") = py::none());
   m.def("ln_bwd", &ln_bwd, py::arg("dout"), py::arg("z"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"),
         py::arg("keep_prob"), py::arg("seed"), py::arg("stream"), py::arg("drop_after"), py::arg("want_dy"),
         py::arg("want_dbias"), py::arg("dgamma_out"), py::arg("dbeta_out"), py::arg("dbias_out"),
         py::arg("amax_out") = py::none());
   m.def("ln_fwd_blocks", &hx_ln_fwd_blocks);
   m.def("ln_bwd_blocks", &hx_ln_bwd_blocks);
-  m.def("ln_bwd_planes", &ln_bwd_planes);
   m.def("embed_ln_fwd", &embed_ln_fwd, py::arg("ids"), py::arg("tt"), py::arg("wte"), py::arg("wpe"), py::arg("wtt"),
         py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("keep_prob"), py::arg("seed"), py::arg("stream"),
-        py::arg("bf16_out"), py::arg("npieces") = 0, py::arg("amax_out") = py::none());
+        py::arg("bf16_out"), py::arg("amax_out") = py::none());
   m.def("embed_word_grad", &embed_word_grad);
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);
@@ -1289,7 +838,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", [](Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed, int64_t stream,
                         OptT bias) { return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, false); });
   m.def("attn_fwd_x6", &attn_fwd_x6, py::arg("qkv"), py::arg("mask_bias"), py::arg("nh"), py::arg("keep"),
-        py::arg("seed"), py::arg("stream"), py::arg("bias"), py::arg("npieces") = 0, py::arg("amax_out") = py::none());
+        py::arg("seed"), py::arg("stream"), py::arg("bias"), py::arg("amax_out") = py::none());
   m.def("attn_bwd", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
                        double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv) {
     return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, false);
@@ -1297,34 +846,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   // fp32 attention backward on the bf16 matrix cores (split pieces, attention_x6.hip)
   m.def("attn_bwd_x6", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
                           double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, OptT amax_out) {
-    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, true, {}, amax_out);
+    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, true, amax_out);
   }, py::arg("dout"), py::arg("qkv"), py::arg("mask_bias"), py::arg("out"), py::arg("lse"), py::arg("dmask"),
      py::arg("nh"), py::arg("keep"), py::arg("bias"), py::arg("dbq"), py::arg("dbk"), py::arg("dbv"),
      py::arg("amax_out") = py::none());
-  // same, dQKV written as the QKV linear's output-gradient planes (S <= 128)
-  m.def("attn_bwd_x6_planes", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask,
-                                 int64_t nh, double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv,
-                                 std::vector<int64_t> order) {
-    TORCH_CHECK(!order.empty(), "attn_bwd_x6_planes: empty plane order");
-    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, true, order);
-  });
   m.def("wgrad_bf16", &wgrad_bf16);
   m.def("wgrad_bf16_ok", &wgrad_bf16_ok);
-  m.def("split_planes", &split_planes);
-  m.def("split_planes_t", &split_planes_t);
-  m.def("split_weight", &split_weight, py::arg("W"), py::arg("npieces"), py::arg("b16") = 0);
-  m.def("gemm_split_weight_b16", &hx_gemm_split_weight_b16);
-  m.def("split_weight_many", &split_weight_many);
-  m.def("gemm_split_k", &gemm_split_k, py::arg("a"), py::arg("b"), py::arg("passes"), py::arg("ks") = 0,
-        py::arg("lay") = 0);
-  m.def("gemm_split_ks", &hx_gemm_split_ks);
-  m.def("gemm_split", &gemm_split, py::arg("a"), py::arg("b"), py::arg("passes"), py::arg("out") = py::none(),
-        py::arg("beta") = false, py::arg("lay") = 0);
-  m.def("gemm_split_gelu", &gemm_split_gelu, py::arg("a"), py::arg("b"), py::arg("passes"), py::arg("bias"),
-        py::arg("lay") = 0, py::arg("dmode") = 0);
-  m.def("gemm_split_dgelu", &gemm_split_dgelu, py::arg("a"), py::arg("b"), py::arg("passes"), py::arg("u"),
-        py::arg("bias"), py::arg("dbias_out"), py::arg("lay") = 0, py::arg("dmode") = 0);
-  m.def("gemm_split_stamps", &gemm_split_stamps);
   m.def("amax_rows", &amax_rows);
   m.def("split_weight_f16", &split_weight_f16);
   m.def("gemm_f16", &gemm_f16, py::arg("a"), py::arg("a_amax"), py::arg("b"), py::arg("b_amax"),
@@ -1347,12 +874,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     return std::make_tuple(c, s);
   });
 
-  m.def("dma_probe", &dma_probe);
-  m.def("gemm_split_ok", &gemm_split_ok);
-  m.def("bias_act_planes", &bias_act_planes);
-  m.def("wgrad_split", &wgrad_split);
-  m.def("wgrad_split_ok", &wgrad_split_ok);
-  m.def("wgrad_split_group", &wgrad_split_group);
   m.def("xar_create", &xar_create);
   m.def("xar_register", &xar_register);
   m.def("device_pci_bus_id", &device_pci_bus_id);
@@ -1371,13 +892,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_reserved_cus", &hx_set_reserved_cus);
   m.def("reserved_cus", &hx_reserved_cus);
   m.def("cu_slots", &hx_cu_slots);
-  m.def("gemm_split_plan", &hx_gemm_split_plan, py::arg("M"), py::arg("N"), py::arg("K"), py::arg("passes"),
-        py::arg("lay") = 0);
-  m.def("wgrad_split_plan", [](int64_t M, int64_t N, int64_t T, int64_t passes) {
-    int cfg = 0, nsplit = 1;
-    hx_wgrad_split_plan((int)M, (int)N, (int)T, (int)passes, &cfg, &nsplit);
-    return std::make_pair(cfg, nsplit);
-  });
   m.def("cu_masked_stream", [](int64_t first_cu, int64_t count) {
     hipStream_t st = hx_cu_masked_stream((int)first_cu, (int)count);
     TORCH_CHECK(st != nullptr, "hipExtStreamCreateWithCUMask failed");

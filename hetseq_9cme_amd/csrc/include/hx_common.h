@@ -14,19 +14,6 @@
 
 namespace hx {
 
-// Streaming (nontemporal) stores for write-once outputs that the NEXT kernel reads from
-// HBM / MALL anyway (the bf16 split planes of the fp32-on-bf16 GEMM path): no L2
-// allocation (forward 180 -> 130 us at T=16384, N=3072, bf16x6: tools/probe/nt_store_probe.py).
-inline bool nt_stores() { return true; }
-typedef unsigned int nt_u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int nt_u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void st_nt16(void* p, uint4 v) {
-  __builtin_nontemporal_store(nt_u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<nt_u32x4*>(p));
-}
-__device__ __forceinline__ void st_nt8(void* p, uint2 v) {
-  __builtin_nontemporal_store(nt_u32x2{v.x, v.y}, reinterpret_cast<nt_u32x2*>(p));
-}
-
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

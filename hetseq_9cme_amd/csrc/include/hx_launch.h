@@ -28,20 +28,15 @@ int hx_ln_bwd_blocks(int64_t rows);
 int hx_ln_fwd_blocks(int64_t rows);
 void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, const float* gamma, const float* beta,
                void* out, void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob,
-               const uint64_t* seed, uint64_t stream, int drop_after, hipStream_t s, uint16_t* pieces = nullptr,
-               int npc = 0, float* amax_part = nullptr);
-// (pieces != nullptr, fp32 only: the output is also written as npc bf16 pieces [rows][npc][H])
+               const uint64_t* seed, uint64_t stream, int drop_after, hipStream_t s, float* amax_part = nullptr);
 void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma,
                void* dz, void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
                uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
-               int accumulate, uint16_t* planes, uint32_t order, int npl, int npc, hipStream_t s,
-               float* amax_part = nullptr);
-// (planes != nullptr: dy is written as bf16 split planes [rows][npl][H] instead of to dy)
+               int accumulate, hipStream_t s, float* amax_part = nullptr);
 void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,
                      const float* wtt, const float* gamma, const float* beta, void* out, void* zsave, float* mean,
                      float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, const uint64_t* seed,
-                     uint64_t stream, hipStream_t s, uint16_t* pieces = nullptr, int npc = 0,
-                     float* amax_part = nullptr);
+                     uint64_t stream, hipStream_t s, float* amax_part = nullptr);
 void hx_embed_word_grad_sorted(int bf16, const void* dz, const int64_t* ids, const int64_t* order, float* dwte,
                                int64_t rows, int H, hipStream_t s);
 // elementwise.hip
@@ -70,18 +65,15 @@ void hx_attn_bwd_bf16(const void* qkv, const float* bias, float* dbias_part, con
 void hx_wgrad_bf16_plan(int M, int N, int T, int* cfg, int* nsplit);
 void hx_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, float* out, float* ws, int M, int N, int T,
                    int cfg, int nsplit, int mvalid, hipStream_t s);
-// attention_x6.hip -- fp32 attention forward on bf16 MFMA with split pieces (bf16x6 class)
-// opieces != nullptr: out is also written as npc bf16 pieces [B*S][npc][H]
+// attention_x6.hip -- fp32 attention on bf16 MFMA with split pieces (bf16x6 class); amax_part
+// (optional): max |out| partials (forward, ceil(S/128) * nh * B * 4) / max |dQKV| partials
+// (backward, S <= 128: B * nh) for the fp16x3 GEMMs
 void hx_attn_fwd_x6(const float* qkv, const float* bias, const float* maskb, float* out, float* lse,
                     uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream,
-                    hipStream_t s, uint16_t* opieces = nullptr, int npc = 0, float* amax_part = nullptr);
-// planes != nullptr (S <= 128 only): dQKV goes out as npl stacked bf16 planes [B*S][npl * 3H]
-// (plane j = piece (order >> 4j) & 15) instead of fp32 dqkv
+                    hipStream_t s, float* amax_part = nullptr);
 void hx_attn_bwd_x6(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,
                     const float* out, const float* lse, const uint32_t* dmask, float* dqkv, float* dq_acc, int dq_ld,
-                    int B, int S, int nh, float keep, uint16_t* planes, uint32_t order, int npl, hipStream_t s,
-                    float* amax_part = nullptr);
-// (amax_part, S <= 128 without planes: B * nh max |dQKV| partials, one per workgroup)
+                    int B, int S, int nh, float keep, hipStream_t s, float* amax_part = nullptr);
 void hx_attn_fwd(int bf16, const void* qkv, const float* bias, const float* maskb, void* out, float* lse,
                  uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream, hipStream_t s);
 // dq_acc: fp32 dQ accumulation target when S > 128 (atomics; row stride dq_ld), else unused.
@@ -90,32 +82,10 @@ void hx_attn_fwd(int bf16, const void* qkv, const float* bias, const float* mask
 void hx_attn_bwd(int kind, const void* qkv, const float* bias, float* dbq, float* dbk, float* dbv, float* dbias_part,
                  const float* maskb, const void* dout, const void* out, const float* lse, const uint32_t* dmask,
                  void* dqkv, float* dq_acc, int dq_ld, int B, int S, int nh, float keep, hipStream_t s,
-                 uint16_t* planes = nullptr, uint32_t order = 0, int npl = 0, float* amax_part = nullptr);
+                 float* amax_part = nullptr);
 
-// wgrad_split.hip -- dW[M][N] (fp32) = sum over piece pairs of dY_a^T X_b (bf16 pieces of fp32
-// operands, --fp32-gemm bf16x3 / bf16x6); piece pointers share the row strides ldy / ldx.
-// ws: nsplit * M * N floats.  Returns -1 for an unsupported pass count.
-void hx_wgrad_split_plan(int M, int N, int T, int passes, int* cfg, int* nsplit);
-int hx_wgrad_split_group_plan(int M1, int N1, int M2, int N2, int T, int passes);
-int hx_wgrad_split_group(const void* const* dy1, int ldy1, const void* const* x1, int ldx1, float* out1, float* ws1,
-                         int M1, int N1, int mvalid1, const void* const* dy2, int ldy2, const void* const* x2, int ldx2,
-                         float* out2, float* ws2, int M2, int N2, int mvalid2, int T, int nsplit, hipStream_t s);
-int hx_wgrad_split(const void* const* dy_pieces, int ldy, const void* const* x_pieces, int ldx, int passes,
-                   float* out, float* ws, int M, int N, int T, int cfg, int nsplit, int mvalid,
-                   hipStream_t s);
-
-// elementwise.hip -- bias + activation (dout == nullptr) or its backward (dout != nullptr, with
-// dbias through the [nchunks][N] partial workspace) written as bf16 planes (split-GEMM path);
-// fp32 y / dout [rows][N], N % 8 == 0.
-void hx_bias_act_planes(int act, const float* y, const float* b, const float* dout, uint16_t* planes,
-                        float* partial, float* dbias, int64_t rows, int N, int npieces, int npl, uint32_t order,
-                        hipStream_t s);
-
-// split.hip -- weight pieces in both GEMM layouts: wf [N][npieces][K], wt [K][npieces][N];
-// W fp32 [N][K] contiguous, N and K multiples of 64.
-// b16 bit 0 / bit 1: wf / wt in the B16 layout [rows][C / 16][3][16] (bf16x6 piece GEMM operand B)
-// a batch of weights split in one launch (split.hip split_weight_many_k); start[i] = first 64 x 64
-// tile of weight i, start[n] = total tiles; mask = hx_split_weight's b16 per weight
+// a batch of weights prepared in one launch (gemm_f16.hip: split_weight_f16 / weight_bf16_t);
+// start[i] = first 64 x 64 tile of weight i, start[n] = total tiles
 #define HX_WBATCH 64
 struct HxWeightBatch {
   int n;
@@ -125,43 +95,6 @@ struct HxWeightBatch {
   int N[HX_WBATCH], K[HX_WBATCH], mask[HX_WBATCH];
   int start[HX_WBATCH + 1];
 };
-void hx_split_weight_many(const HxWeightBatch& d, int npieces, hipStream_t s);
-void hx_split_weight(const float* W, int N, int K, int npieces, uint16_t* wf, uint16_t* wt, hipStream_t s,
-                     int b16 = 0);
-
-// gemm_split.hip -- C[M][N] (+)= sum over piece pairs A_a[M][K] . B_b[N][K]^T (bf16 pieces of fp32
-// operands: piece p of row r at X + r * ldx + p * x_ps, npieces * x_ps <= ldx); passes 3 or 6.
-// Epilogue kinds (epi may be null = kind 0):
-//   0  C (+)= acc
-//   1  C = acc + bias (pre-activation) and P = pieces of gelu(C)        (beta must be 0)
-//   2  t = acc * gelu'(aux (+ bias)); P = pieces of t; colpart[(M/BM)*NWM][N] = per-wave
-//      column sums of t (hx_gemm_split_colpart_rows rows; null = none); C unused
-// cfg from hx_gemm_split_plan (-1: shape not covered).  Returns -1 for an unsupported shape.
-struct HxGemmEpi {
-  int kind;
-  const float* bias;
-  const float* aux;
-  int64_t ldaux;
-  uint16_t* P;
-  int64_t ldp, p_ps;
-  float* colpart;
-  // kind 1: 0 = C gets u (the pre-activation), 1 = C gets gelu'(u) (the only thing the backward
-  // needs: its erf is the forward's, so the backward epilogue does no transcendental work);
-  // kind 2: 0 = aux holds u, 1 = aux holds gelu'(u)
-  int dmode = 0;
-};
-int hx_gemm_split_plan(int M, int N, int K, int passes, int lay = 0);
-int hx_gemm_split_colpart_rows(int M, int cfg);
-int hx_gemm_split_weight_b16(int N, int passes);
-int hx_gemm_split_nt(const void* A, int64_t lda, int64_t a_ps, const void* B, int64_t ldb, int64_t b_ps, float* C,
-                     int64_t ldc, int M, int N, int K, int passes, int beta, const HxGemmEpi* epi, int cfg,
-                     hipStream_t s, int lay = 0, int ks = 1, int64_t c_zs = 0);
-// split-K slab count for the piece GEMM of an M x N output over K (1 = none): deep reductions
-// with too few output tiles to fill the CUs (the MLM decoder's data gradient, K = 30720)
-int hx_gemm_split_ks(int M, int N, int K, int passes);
-int hx_gemm_split_stamps(const void* A, const void* B, float* C, int M, int N, int K, unsigned long long* stamps,
-                         hipStream_t s, int lay = 0);
-void hx_dma_probe(const void* src, uint32_t bytes, int seg, int ld, int iters, int grid, hipStream_t s);
 // fold [rows][N] column partials into out[N] (+= if accumulate)
 void hx_fold_cols(const float* partial, int rows, int N, float* out, int accumulate, hipStream_t s);
 

@@ -109,8 +109,7 @@ template <bool kDrop>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd_x6_k(
     const float* __restrict__ qkv, const float* __restrict__ qkv_bias, const float* __restrict__ maskb,
     float* __restrict__ out, float* __restrict__ lse, uint32_t* __restrict__ dmask, int S, int nh, float keep,
-    const uint64_t* __restrict__ seedp, uint64_t stream, uint16_t* __restrict__ opieces, int npc,
-    float* __restrict__ amax_part) {
+    const uint64_t* __restrict__ seedp, uint64_t stream, float* __restrict__ amax_part) {
   const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   __shared__ __attribute__((aligned(16))) uint16_t Ks[3][64 * RS];   // [piece][key][dim]
   __shared__ __attribute__((aligned(16))) uint16_t Vt[3][64 * RS];   // [piece][dim][vpos(key)]
@@ -316,22 +315,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   if (q >= S) return;
   const float inv_l = 1.f / l_run;
   float* op = out + ((int64_t)b * S + q) * H + hd * D;
-  // opieces: the context also goes out as the attention-output projection's input pieces
-  // [rows][npc][H] (natural piece layout), so that GEMM needs no split pass
-  auto put_pieces = [&](int d, float4 v) {
-    float e[4] = {v.x, v.y, v.z, v.w};
-    uint16_t* pp = opieces + ((int64_t)b * S + q) * npc * H + hd * D + d;
-    for (int p = 0; p < npc; ++p) {
-      uint16_t qv[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        qv[i] = hx::f2bf(e[i]);
-        e[i] -= hx::bf2f(qv[i]);
-      }
-      *reinterpret_cast<uint2*>(pp + (int64_t)p * H) =
-          make_uint2(qv[0] | ((uint32_t)qv[1] << 16), qv[2] | ((uint32_t)qv[3] << 16));
-    }
-  };
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
     const int d0 = 8 * g + 4 * h;
@@ -341,10 +324,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         make_float4(o1[4 * g] * inv_l, o1[4 * g + 1] * inv_l, o1[4 * g + 2] * inv_l, o1[4 * g + 3] * inv_l);
     *reinterpret_cast<float4*>(op + d0) = va;
     *reinterpret_cast<float4*>(op + 32 + d0) = vb;
-    if (opieces) {
-      put_pieces(d0, va);
-      put_pieces(32 + d0, vb);
-    }
   }
   if (h == 0) lse[bh * S + q] = m_run + __logf(l_run);
 }
@@ -365,32 +344,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 constexpr int TS = 40;    // transposed 32-query image row stride (bf16)
 constexpr int KTS = 136;  // K^T [dim][128 keys] and dS [query][128 keys] row stride (bf16)
 constexpr int KT_B = 64 * KTS * 2, DS_B = 32 * KTS * 2, QS_B = 32 * RS * 2, QT_B = 64 * TS * 2;
-constexpr int BWD_SMEM_IMG = 3 * (KT_B + DS_B + 2 * QS_B + 2 * QT_B) + 5 * 32 * 4;
-constexpr int DQS = 68;   // dQ staging row stride (floats) of the planes form: rows 4 apart on distinct banks
-constexpr int BWD_SMEM = BWD_SMEM_IMG + 32 * DQS * 4;
-constexpr int EPS = 72;   // dK / dV staging row stride (floats) of the planes form
-
-// Planes form of the output (S <= 128): dQKV goes out as the stacked bf16 planes of the QKV
-// linear's output gradient ([B*S, npl * 3H], plane j = piece order[j], split.hip's layout),
-// which its data- and weight-gradient GEMMs read directly -- no fp32 dQKV written and no
-// split pass reading it back (ops/fused.py GradPlanes).
-struct PlaneOut {
-  uint16_t* p;
-  uint32_t order;   // piece of plane j in bits 4j..4j+3
-  int npl;
-};
-// 8 consecutive fp32 values -> their 16-B chunk in every plane (dst = plane 0's chunk)
-__device__ __forceinline__ void put_planes8(const float (&f)[8], uint16_t* dst, int64_t pstride, const PlaneOut& po) {
-  bf16x8 pc[3];
-  split8(f, pc[0], pc[1], pc[2]);
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    if (j >= po.npl) break;
-    const int k = (po.order >> (4 * j)) & 15;
-    const bf16x8 v = k == 0 ? pc[0] : (k == 1 ? pc[1] : pc[2]);
-    hx::st_nt16(dst + j * pstride, __builtin_bit_cast(uint4, v));
-  }
-}
+constexpr int BWD_SMEM = 3 * (KT_B + DS_B + 2 * QS_B + 2 * QT_B) + 5 * 32 * 4;
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
@@ -424,12 +378,12 @@ __device__ __forceinline__ void ld8(const float* p, const float* bias, float (&f
   }
 }
 
-template <bool kDrop, bool kPl>
+template <bool kDrop>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void attn_bwd_x6_k(
     const float* __restrict__ qkv, const float* __restrict__ qkv_bias, float* __restrict__ dbias_part,
     const float* __restrict__ maskb, const float* __restrict__ dout, const float* __restrict__ outp,
     const float* __restrict__ lse, const uint32_t* __restrict__ dmask, float* __restrict__ dqkv,
-    float* __restrict__ dq_acc, int dq_ld, int S, int nh, float keep, PlaneOut pout, float* __restrict__ amax_part) {
+    float* __restrict__ dq_acc, int dq_ld, int S, int nh, float keep, float* __restrict__ amax_part) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float am = 0.f;   // max |dQKV| of this block's stores (one key block per head only: fp16x3 operand scale)
   uint16_t* Kt = reinterpret_cast<uint16_t*>(smem);                       // [3][64][KTS]
@@ -440,7 +394,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   uint16_t* dOt = Qt + 3 * 64 * TS;                                       // [3][64][TS]
   float* Ls = reinterpret_cast<float*>(dOt + 3 * 64 * TS);                // [32] lse
   float* Ds = Ls + 32;                                                    // [32][4 waves] D partials
-  float* dQs = reinterpret_cast<float*>(smem + BWD_SMEM_IMG);             // [32][DQS] (planes form)
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
   const int b = blockIdx.z, hd = blockIdx.y;
@@ -620,25 +573,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
   };
 
-  // planes form: the staged dQ tile of queries q0t .. q0t + 31 -> planes (8 columns per thread)
-  const int64_t ldp = (int64_t)pout.npl * H3;
-  auto dq_planes = [&](int q0t) {
-    const int row = tid >> 3, c8 = (tid & 7) * 8;
-    if (q0t + row >= S) return;
-    const float4 a = *reinterpret_cast<const float4*>(&dQs[row * DQS + c8]);
-    const float4 c = *reinterpret_cast<const float4*>(&dQs[row * DQS + c8 + 4]);
-    const float f[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-    put_planes8(f, pout.p + ((int64_t)b * S + q0t + row) * ldp + hd * D + c8, H3, pout);
-  };
-
   stage(0);
   uint32_t mnext = pm;
   for (int qt = 0; qt < S; qt += 32) {
     // tile qt is staged; every wave is done with the previous tile's dS
     __syncthreads();
-    if constexpr (kPl) {
-      if (qt > 0) dq_planes(qt - 32);
-    }
     const uint32_t mword = mnext;
     const bool more = qt + 32 < S;
     if (more) ld_tile(qt + 32);   // in flight during this tile's math
@@ -701,13 +640,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       cq1 += (qa1[0] + qa1[1]) + (qa1[2] + qa1[3]);
     }
     const int dcol = 32 * dp2 + r16;
-    if constexpr (kPl) {   // staged; stored as planes after the next barrier
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        dQs[(qh * 16 + 4 * kg + r) * DQS + dcol] = qa0[r] * scale;
-        dQs[(qh * 16 + 4 * kg + r) * DQS + dcol + 16] = qa1[r] * scale;
-      }
-    } else if (single) {
+    if (single) {
       float* dq = dqkv_b + (int64_t)q0 * H3 + dcol;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -764,32 +697,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       dbias_part[((int64_t)b * gridDim.x + blockIdx.x) * H3 + part * H + hd * D + c] = v;
     }
   }
-  if constexpr (kPl) {
-    __syncthreads();   // the last dQ tile is staged; every wave is done with the images
-    dq_planes(((S - 1) >> 5) << 5);
-    __syncthreads();   // dQs read: the dK / dV staging below may reuse any LDS
-    // ---- epilogue, planes form: dK / dV through LDS ([2][128 keys][EPS]) to 8-column chunks
-    float* ep = reinterpret_cast<float*>(smem);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int kl = w * 32 + crow(r, h);
-      ep[kl * EPS + l32] = dk0[r];
-      ep[kl * EPS + 32 + l32] = dk1[r];
-      ep[(128 + kl) * EPS + l32] = dv0[r];
-      ep[(128 + kl) * EPS + 32 + l32] = dv1[r];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int ch = tid + 256 * i, part = ch >> 10, row = (ch & 1023) >> 3, c8 = (ch & 7) * 8;
-      const int key = kbase + row;
-      if (key >= S) continue;
-      const float4 a = *reinterpret_cast<const float4*>(&ep[(part * 128 + row) * EPS + c8]);
-      const float4 c = *reinterpret_cast<const float4*>(&ep[(part * 128 + row) * EPS + c8 + 4]);
-      const float f[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-      put_planes8(f, pout.p + ((int64_t)b * S + key) * ldp + (1 + part) * H + hd * D + c8, H3, pout);
-    }
-  } else {
+  {
     // ---- epilogue: dK (accumulated against pre-scaled Q: already scaled), dV
     float* dk = dqkv + (int64_t)b * S * H3 + H + hd * D;
     float* dvp = dqkv + (int64_t)b * S * H3 + 2 * H + hd * D;
@@ -823,40 +731,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
 void hx_attn_fwd_x6(const float* qkv, const float* bias, const float* maskb, float* out, float* lse,
                     uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream,
-                    hipStream_t s, uint16_t* opieces, int npc, float* amax_part) {
+                    hipStream_t s, float* amax_part) {
   dim3 grid((S + 127) / 128, nh, B);
   if (keep < 1.f)
-    attn_fwd_x6_k<true><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream, opieces,
-                                             npc, amax_part);
+    attn_fwd_x6_k<true><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream, amax_part);
   else
-    attn_fwd_x6_k<false><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream, opieces,
-                                              npc, amax_part);
+    attn_fwd_x6_k<false><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream, amax_part);
 }
 
 void hx_attn_bwd_x6(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,
                     const float* out, const float* lse, const uint32_t* dmask, float* dqkv, float* dq_acc, int dq_ld,
-                    int B, int S, int nh, float keep, uint16_t* planes, uint32_t order, int npl, hipStream_t s,
-                    float* amax_part) {
+                    int B, int S, int nh, float keep, hipStream_t s, float* amax_part) {
   dim3 grid((S + 127) / 128, nh, B);
   static bool attr = false;
   if (!attr) {   // > 64 KiB of dynamic LDS needs an explicit opt-in (gfx950: 160 KiB per CU)
-    const void* k[4] = {reinterpret_cast<const void*>(&attn_bwd_x6_k<true, false>),
-                        reinterpret_cast<const void*>(&attn_bwd_x6_k<false, false>),
-                        reinterpret_cast<const void*>(&attn_bwd_x6_k<true, true>),
-                        reinterpret_cast<const void*>(&attn_bwd_x6_k<false, true>)};
+    const void* k[2] = {reinterpret_cast<const void*>(&attn_bwd_x6_k<true>),
+                        reinterpret_cast<const void*>(&attn_bwd_x6_k<false>)};
     for (const void* f : k) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, BWD_SMEM);
     attr = true;
   }
-  const PlaneOut po{planes, order, npl};
-#define HX_BWD_X6(D_, P_)                                                                                        \
-  attn_bwd_x6_k<D_, P_><<<grid, 256, BWD_SMEM, s>>>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv, dq_acc, \
-                                                    dq_ld, S, nh, keep, po, amax_part)
-  if (planes) {   // S <= 128 (one key block: every dQ row complete in one workgroup), checked by the caller
-    if (keep < 1.f) HX_BWD_X6(true, true);
-    else HX_BWD_X6(false, true);
-  } else {
-    if (keep < 1.f) HX_BWD_X6(true, false);
-    else HX_BWD_X6(false, false);
-  }
-#undef HX_BWD_X6
+  if (keep < 1.f)
+    attn_bwd_x6_k<true><<<grid, 256, BWD_SMEM, s>>>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv, dq_acc,
+                                                    dq_ld, S, nh, keep, amax_part);
+  else
+    attn_bwd_x6_k<false><<<grid, 256, BWD_SMEM, s>>>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv, dq_acc,
+                                                     dq_ld, S, nh, keep, amax_part);
 }

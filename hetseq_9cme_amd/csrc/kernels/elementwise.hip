@@ -166,86 +166,6 @@ __global__ __launch_bounds__(NT) void bias_act_bwd_k(const T* __restrict__ dout,
   }
 }
 
-// bias + activation with the result written as bf16 PLANES for the split-GEMM fp32 path
-// (--fp32-gemm, ops/split_gemm.py) instead of an fp32 tensor that a separate pass would split:
-//   forward  (dout == nullptr): v = act(y + b)
-//   backward (dout != nullptr): v = dout * act'(y + b), plus the column partials of v (dbias)
-// v is split into NPC bf16 pieces (v = v0 + v1 [+ v2]); plane j of row r, columns c..c+7,
-// receives piece (order >> 4j) & 15 at planes[(r * npl + j) * N + c] (16-B stores).
-// Same tiling as bias_act_bwd_k: lane -> 8 adjacent columns, wave w -> rows w, w+4, ...
-template <int ACT, int NPC, bool kNT>
-__global__ __launch_bounds__(NT) void bias_act_planes_k(const float* __restrict__ y, const float* __restrict__ b,
-                                                      const float* __restrict__ dout, uint16_t* __restrict__ planes,
-                                                      float* __restrict__ partial, int64_t rows, int N, int npl,
-                                                      uint32_t order) {
-  constexpr int VEC = 8;
-  __shared__ float red[4][VEC][64];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int j = (blockIdx.x * 64 + lane) * VEC;
-  const int64_t r0 = (int64_t)blockIdx.y * hx::kRowChunk;
-  const int64_t r1 = r0 + hx::kRowChunk < rows ? r0 + hx::kRowChunk : rows;
-  float acc[VEC];
-#pragma unroll
-  for (int k = 0; k < VEC; ++k) acc[k] = 0.f;
-  if (j < N) {
-    float bb[VEC];
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) bb[k] = 0.f;
-    if (b) ldv<float, VEC>(b + j, bb);
-    for (int64_t r = r0 + w; r < r1; r += 4) {
-      const int64_t o = r * N + j;
-      float v[VEC];
-      ldv<float, VEC>(y + o, v);
-      if (dout) {
-        float d[VEC];
-        ldv<float, VEC>(dout + o, d);
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-          const float x = v[k] + bb[k];
-          const float g = ACT == ACT_GELU ? hx::gelu_grad_f(x)
-                        : ACT == ACT_TANH ? 1.f - tanhf(x) * tanhf(x)
-                        : ACT == ACT_RELU ? (x > 0.f ? 1.f : 0.f) : 1.f;
-          v[k] = d[k] * g;
-          acc[k] += v[k];
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) v[k] = act_f<ACT>(v[k] + bb[k]);
-      }
-      uint4 pc[NPC];
-#pragma unroll
-      for (int p = 0; p < NPC; ++p) {
-        uint16_t h[VEC];
-#pragma unroll
-        for (int k = 0; k < VEC; ++k) {
-          h[k] = hx::f2bf(v[k]);
-          v[k] -= hx::bf2f(h[k]);   // exact residual
-        }
-        pc[p] = make_uint4(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16), h[4] | ((uint32_t)h[5] << 16),
-                           h[6] | ((uint32_t)h[7] << 16));
-      }
-      uint16_t* dst = planes + r * (int64_t)npl * N + j;
-      for (int q = 0; q < npl; ++q) {
-        const int k = (order >> (4 * q)) & 15;
-        const uint4 v = pc[k < NPC ? k : NPC - 1];
-        if constexpr (kNT) hx::st_nt16(dst + (int64_t)q * N, v);
-        else *reinterpret_cast<uint4*>(dst + (int64_t)q * N) = v;
-      }
-    }
-  }
-  if (!partial) return;
-#pragma unroll
-  for (int k = 0; k < VEC; ++k) red[w][k][lane] = acc[k];
-  __syncthreads();
-  if (w == 0 && j < N) {
-    float o[VEC];
-#pragma unroll
-    for (int k = 0; k < VEC; ++k) o[k] = (red[0][k][lane] + red[1][k][lane]) + (red[2][k][lane] + red[3][k][lane]);
-    float* dst = partial + (int64_t)blockIdx.y * N + j;
-#pragma unroll
-    for (int k = 0; k < VEC; k += 4) *reinterpret_cast<float4*>(dst + k) = make_float4(o[k], o[k + 1], o[k + 2], o[k + 3]);
-  }
-}
 
 // scalar-column variant (any N); the optional device scalar scales the RESULT
 // (the input is only read: scaling it in place would double the HBM traffic)
@@ -377,38 +297,6 @@ void hx_bias_act_bwd(int bf16, int act, const void* dout, const void* y, const f
                      void* dy, float* partial, float* dbias, int64_t rows, int N, int accumulate, hipStream_t s) {
   if (bf16) bias_act_bwd_t<uint16_t>(act, dout, y, b, saved_out, dy, partial, dbias, rows, N, accumulate, s);
   else bias_act_bwd_t<float>(act, dout, y, b, saved_out, dy, partial, dbias, rows, N, accumulate, s);
-}
-
-void hx_bias_act_planes(int act, const float* y, const float* b, const float* dout, uint16_t* planes,
-                        float* partial, float* dbias, int64_t rows, int N, int npieces, int npl, uint32_t order,
-                        hipStream_t s) {
-  const int nch = nchunks(rows);
-  dim3 g((N + 511) / 512, nch);
-  float* part = (dout && dbias) ? partial : nullptr;
-  // planes are written once and read by the next GEMM from HBM / MALL: nontemporal 16-B
-  // stores (no L2 allocation) -- forward 180 -> 130 us at T=16384, N=3072, bf16x6
-  // (tools/probe/nt_store_probe.py)
-  static const bool nt = hx::nt_stores();
-#define HX_BAP(A, P)                                                                                 \
-  do {                                                                                               \
-    if (nt) bias_act_planes_k<A, P, true><<<g, NT, 0, s>>>(y, b, dout, planes, part, rows, N, npl, order);  \
-    else bias_act_planes_k<A, P, false><<<g, NT, 0, s>>>(y, b, dout, planes, part, rows, N, npl, order);    \
-  } while (0)
-#define HX_BAP_ACT(P)                          \
-  switch (act) {                               \
-    case ACT_GELU: HX_BAP(ACT_GELU, P); break; \
-    case ACT_TANH: HX_BAP(ACT_TANH, P); break; \
-    case ACT_RELU: HX_BAP(ACT_RELU, P); break; \
-    default: HX_BAP(ACT_NONE, P); break;       \
-  }
-  if (npieces == 3) {
-    HX_BAP_ACT(3)
-  } else {
-    HX_BAP_ACT(2)
-  }
-#undef HX_BAP_ACT
-#undef HX_BAP
-  if (part) hx::fold_rows(partial, nch, N, N, N, dbias, nullptr, nullptr, 0, s);
 }
 
 void hx_colsum(int bf16, void* x, const float* scale, float* partial, float* out, int64_t rows, int N,

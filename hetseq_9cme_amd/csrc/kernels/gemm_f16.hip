@@ -37,6 +37,7 @@
 
 #include "hx_gemm.h"
 #include "hx_launch.h"
+#include "hx_reduce.h"
 
 namespace {
 
@@ -783,6 +784,10 @@ void hx_weight_bf16_t(const HxWeightBatch& d, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- host API (hx_launch.h)
+void hx_fold_cols(const float* partial, int rows, int N, float* out, int accumulate, hipStream_t s) {
+  hx::fold_rows(partial, rows, N, N, N, out, nullptr, nullptr, accumulate, s);
+}
+
 int hx_gemm_f16_plan(int M, int N, int K) {
   if (const char* e = getenv("HX_GEMM_F16_CFG")) {
     const int c = atoi(e);

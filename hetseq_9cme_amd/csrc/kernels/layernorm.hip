@@ -48,22 +48,6 @@ __device__ __forceinline__ float amax4(float m, float4 v) {
   return fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
 }
 
-// npc bf16 pieces of the 4 fp32 outputs at columns j..j+3 of row r -> pieces [rows][npc][H]
-// (the natural piece layout the split GEMMs read: ops/split_gemm.py), one 8-B store per piece
-__device__ __forceinline__ void store_pieces4(uint16_t* pieces, int npc, int64_t r, int H, int j, float4 o) {
-  float e[4] = {o.x, o.y, o.z, o.w};
-  for (int p = 0; p < npc; ++p) {
-    uint16_t q[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      q[i] = hx::f2bf(e[i]);
-      e[i] -= hx::bf2f(q[i]);
-    }
-    *reinterpret_cast<uint2*>(pieces + (r * npc + p) * H + j) =
-        make_uint2(q[0] | ((uint32_t)q[1] << 16), q[2] | ((uint32_t)q[3] << 16));
-  }
-}
-
 // ----------------------------------------------------------------------------- fwd
 template <typename T, int CH, bool kDropAfter>
 __global__ __launch_bounds__(NT) void ln_fwd_k(const T* __restrict__ y, const float* __restrict__ bias,
@@ -72,7 +56,7 @@ __global__ __launch_bounds__(NT) void ln_fwd_k(const T* __restrict__ y, const fl
                                              T* __restrict__ zsave, float* __restrict__ mean_out,
                                              float* __restrict__ rstd_out, int64_t rows, int H, float eps,
                                              float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream,
-                                             uint16_t* __restrict__ pieces, int npc, float* __restrict__ amax_part) {
+                                             float* __restrict__ amax_part) {
   const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   const int lane = threadIdx.x & 63;
   const int64_t wave = blockIdx.x * (int64_t)WPB + (threadIdx.x >> 6);
@@ -143,7 +127,6 @@ __global__ __launch_bounds__(NT) void ln_fwd_k(const T* __restrict__ y, const fl
           o.w = (k & 8) ? o.w * inv_keep : 0.f;
         }
         hx::store4(out + r * H + j, o);
-        if (pieces) store_pieces4(pieces, npc, r, H, j, o);
         am = amax4(am, o);
       }
     }
@@ -160,8 +143,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
                                              const float* __restrict__ gamma, T* __restrict__ dz_out,
                                              T* __restrict__ dy_out, float* __restrict__ partial, int64_t rows,
                                              int H, float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream,
-                                             int want_dbias, uint16_t* __restrict__ planes, uint32_t order, int npl,
-                                             int npc, float* __restrict__ amax_part) {
+                                             int want_dbias, float* __restrict__ amax_part) {
   const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   __shared__ float red[WPB][CH * 256];
   const int lane = threadIdx.x & 63;
@@ -239,8 +221,8 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
         float4 dz = make_float4(rstd * (dv.x - m1 - xv.x * m2), rstd * (dv.y - m1 - xv.y * m2),
                                 rstd * (dv.z - m1 - xv.z * m2), rstd * (dv.w - m1 - xv.w * m2));
         hx::store4(dz_out + r * H + j, dz);
-        if (!dy_out && !planes) am = amax4(am, dz);
-        if (dy_out || planes) {
+        if (!dy_out) am = amax4(am, dz);
+        if (dy_out) {
           float4 dy = dz;
           if (drop && !kDropAfter) {
             const uint32_t k = hx::keep4(seed, stream, (uint64_t)(r * H + j) >> 2, keep_prob);
@@ -249,29 +231,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
             dy.z = (k & 4) ? dy.z * inv_keep : 0.f;
             dy.w = (k & 8) ? dy.w * inv_keep : 0.f;
           }
-          if (planes) {
-            // --fp32-gemm bf16x3/x6: dy goes straight out as the consumer linear's bf16
-            // gradient planes [row][npl][H] (piece order[k] in plane k), no fp32 dy pass
-            float e[4] = {dy.x, dy.y, dy.z, dy.w};
-            uint2 pw[3];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-              uint16_t q[4];
-#pragma unroll
-              for (int t = 0; t < 4; ++t) {
-                q[t] = hx::f2bf(e[t]);
-                e[t] -= hx::bf2f(q[t]);
-              }
-              pw[k] = make_uint2(q[0] | ((uint32_t)q[1] << 16), q[2] | ((uint32_t)q[3] << 16));
-            }
-            uint16_t* o = planes + r * npl * H + j;
-            for (int k = 0; k < npl; ++k) {
-              const int pc = (order >> (4 * k)) & 15;
-              hx::st_nt8(o + (int64_t)k * H, pw[pc < npc ? pc : npc - 1]);
-            }
-          } else {
-            hx::store4(dy_out + r * H + j, dy);
-          }
+          hx::store4(dy_out + r * H + j, dy);
           am = amax4(am, dy);
           if (want_dbias) {
             dbias.v[c].x += dy.x; dbias.v[c].y += dy.y; dbias.v[c].z += dy.z; dbias.v[c].w += dy.w;
@@ -312,7 +272,7 @@ __global__ __launch_bounds__(NT) void embed_ln_fwd_k(const int64_t* __restrict__
                                                    T* __restrict__ zsave, float* __restrict__ mean_out,
                                                    float* __restrict__ rstd_out, int64_t rows, int S, int H,
                                                    float eps, float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream,
-                                                   uint16_t* __restrict__ pieces, int npc, float* __restrict__ amax_part) {
+                                                   float* __restrict__ amax_part) {
   const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   const int lane = threadIdx.x & 63;
   const int64_t wave = blockIdx.x * (int64_t)WPB + (threadIdx.x >> 6);
@@ -372,7 +332,6 @@ __global__ __launch_bounds__(NT) void embed_ln_fwd_k(const int64_t* __restrict__
           o.w = (k & 8) ? o.w * inv_keep : 0.f;
         }
         hx::store4(out + r * H + j, o);
-        if (pieces) store_pieces4(pieces, npc, r, H, j, o);
         am = amax4(am, o);
       }
     }
@@ -477,17 +436,15 @@ inline int ln_grid(int64_t rows, int cap) {
 template <typename T>
 void ln_fwd_t(const void* y, const float* bias, const void* res, const float* gamma, const float* beta, void* out,
               void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob, const uint64_t* seed,
-              uint64_t stream, int drop_after, uint16_t* pieces, int npc, hipStream_t s, float* amax_part) {
+              uint64_t stream, int drop_after, hipStream_t s, float* amax_part) {
   const int grid = ln_grid(rows, 4096);
   HX_CH_DISPATCH(H, {
     if (drop_after)
       ln_fwd_k<T, CH, true><<<grid, NT, 0, s>>>((const T*)y, bias, (const T*)res, gamma, beta, (T*)out, (T*)zsave,
-                                                mean, rstd, rows, H, eps, keep_prob, seed, stream, pieces, npc,
-                                                amax_part);
+                                                mean, rstd, rows, H, eps, keep_prob, seed, stream, amax_part);
     else
       ln_fwd_k<T, CH, false><<<grid, NT, 0, s>>>((const T*)y, bias, (const T*)res, gamma, beta, (T*)out, (T*)zsave,
-                                                 mean, rstd, rows, H, eps, keep_prob, seed, stream, pieces, npc,
-                                                 amax_part);
+                                                 mean, rstd, rows, H, eps, keep_prob, seed, stream, amax_part);
   })
 }
 
@@ -495,16 +452,14 @@ template <typename T>
 void ln_bwd_t(const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma, void* dz,
               void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
               uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
-              int accumulate, uint16_t* planes, uint32_t order, int npl, int npc, hipStream_t s, float* amax_part) {
+              int accumulate, hipStream_t s, float* amax_part) {
   HX_CH_DISPATCH(H, {
     if (drop_after)
       ln_bwd_k<T, CH, true><<<nblk, NT, 0, s>>>((const T*)dout, (const T*)z, mean, rstd, gamma, (T*)dz, (T*)dy,
-                                                partial, rows, H, keep_prob, seed, stream, want_dbias, planes, order,
-                                                npl, npc, amax_part);
+                                                partial, rows, H, keep_prob, seed, stream, want_dbias, amax_part);
     else
       ln_bwd_k<T, CH, false><<<nblk, NT, 0, s>>>((const T*)dout, (const T*)z, mean, rstd, gamma, (T*)dz, (T*)dy,
-                                                 partial, rows, H, keep_prob, seed, stream, want_dbias, planes, order,
-                                                 npl, npc, amax_part);
+                                                 partial, rows, H, keep_prob, seed, stream, want_dbias, amax_part);
   })
   // partial is [nblk][3][H]: fold rows of length 3H into dgamma | dbeta | dbias
   hx::fold_rows(partial, nblk, 3 * (int64_t)H, (want_dbias ? 3 : 2) * H, H, dgamma, dbeta,
@@ -518,42 +473,41 @@ int hx_ln_fwd_blocks(int64_t rows) { return ln_grid(rows, 4096); }
 
 void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, const float* gamma, const float* beta,
                void* out, void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob,
-               const uint64_t* seed, uint64_t stream, int drop_after, hipStream_t s, uint16_t* pieces, int npc,
-               float* amax_part) {
+               const uint64_t* seed, uint64_t stream, int drop_after, hipStream_t s, float* amax_part) {
   if (bf16)
     ln_fwd_t<uint16_t>(y, bias, res, gamma, beta, out, zsave, mean, rstd, rows, H, eps, keep_prob, seed, stream,
-                       drop_after, nullptr, 0, s, nullptr);
+                       drop_after, s, nullptr);
   else
     ln_fwd_t<float>(y, bias, res, gamma, beta, out, zsave, mean, rstd, rows, H, eps, keep_prob, seed, stream,
-                    drop_after, pieces, npc, s, amax_part);
+                    drop_after, s, amax_part);
 }
 
 void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma,
                void* dz, void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
                uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
-               int accumulate, uint16_t* planes, uint32_t order, int npl, int npc, hipStream_t s, float* amax_part) {
+               int accumulate, hipStream_t s, float* amax_part) {
   if (bf16)
     ln_bwd_t<uint16_t>(dout, z, mean, rstd, gamma, dz, dy, partial, nblk, rows, H, keep_prob, seed, stream,
-                       drop_after, want_dbias, dgamma, dbeta, dbias, accumulate, planes, order, npl, npc, s, nullptr);
+                       drop_after, want_dbias, dgamma, dbeta, dbias, accumulate, s, nullptr);
   else
     ln_bwd_t<float>(dout, z, mean, rstd, gamma, dz, dy, partial, nblk, rows, H, keep_prob, seed, stream, drop_after,
-                    want_dbias, dgamma, dbeta, dbias, accumulate, planes, order, npl, npc, s, amax_part);
+                    want_dbias, dgamma, dbeta, dbias, accumulate, s, amax_part);
 }
 
 void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,
                      const float* wtt, const float* gamma, const float* beta, void* out, void* zsave, float* mean,
                      float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, const uint64_t* seed,
-                     uint64_t stream, hipStream_t s, uint16_t* pieces, int npc, float* amax_part) {
+                     uint64_t stream, hipStream_t s, float* amax_part) {
   const int grid = ln_grid(rows, 4096);
   HX_CH_DISPATCH(H, {
     if (bf16)
       embed_ln_fwd_k<uint16_t, CH><<<grid, NT, 0, s>>>(ids, tt, wte, wpe, wtt, gamma, beta, (uint16_t*)out,
                                                        (uint16_t*)zsave, mean, rstd, rows, S, H, eps, keep_prob,
-                                                       seed, stream, nullptr, 0, nullptr);
+                                                       seed, stream, nullptr);
     else
       embed_ln_fwd_k<float, CH><<<grid, NT, 0, s>>>(ids, tt, wte, wpe, wtt, gamma, beta, (float*)out,
                                                     (float*)zsave, mean, rstd, rows, S, H, eps, keep_prob, seed,
-                                                    stream, pieces, npc, amax_part);
+                                                    stream, amax_part);
   })
 }
 

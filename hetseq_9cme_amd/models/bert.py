@@ -58,11 +58,6 @@ def swish(x):
 
 ACT2FN = {'gelu': gelu, 'relu': F.relu, 'swish': swish, 'tanh': torch.tanh}
 
-# the attention-output projection's weight gradient runs grouped with the QKV projection's (ops.WgradDefer);
-# running it in its own backward on the side stream measured slower (51.86 / 51.89 -> 52.17 / 52.32 ms, round 3)
-_WGRAD_DEFER = True
-
-
 class BertConfig(object):
     """Configuration of a BERT model (reference bert_modeling.py:180-266)."""
 
@@ -195,14 +190,13 @@ class BertSelfAttention(nn.Module):
         self.value = nn.Linear(config.hidden_size, self.all_head_size)
         self.dropout = nn.Dropout(config.attention_probs_dropout_prob)
 
-    def forward(self, hidden_states, attention_mask_bias, res_grad=None, wgrad_join=None):
+    def forward(self, hidden_states, attention_mask_bias, res_grad=None):
         # bias-less N=3H projection GEMM; the Q/K/V biases are applied (and their
         # gradients produced) inside the fused attention
-        gp = ops.GradPlanes()   # the attention backward hands the projection its gradient planes
         qkv = ops.linear3(hidden_states, self.query.weight, self.key.weight, self.value.weight,
-                          None, None, None, res_grad=res_grad, grad_planes=gp, wgrad_join=wgrad_join)
+                          None, None, None, res_grad=res_grad)
         return ops.attention(qkv, attention_mask_bias, self.num_attention_heads, self.dropout.p, self.training,
-                             bias=(self.query.bias, self.key.bias, self.value.bias), grad_planes=gp)
+                             bias=(self.query.bias, self.key.bias, self.value.bias))
 
 
 class BertSelfOutput(nn.Module):
@@ -212,12 +206,11 @@ class BertSelfOutput(nn.Module):
         self.LayerNorm = BertLayerNorm(config.hidden_size, eps=1e-12)
         self.dropout = nn.Dropout(config.hidden_dropout_prob)
 
-    def forward(self, hidden_states, input_tensor, res_grad=None, wgrad_defer=None):
-        gp = ops.GradPlanes()   # the LN backward hands the dense layer its gradient planes
-        y = ops.linear(hidden_states, self.dense.weight, grad_planes=gp, wgrad_defer=wgrad_defer)
+    def forward(self, hidden_states, input_tensor, res_grad=None):
+        y = ops.linear(hidden_states, self.dense.weight)
         return ops.bias_dropout_residual_ln(y, self.dense.bias, input_tensor, self.LayerNorm.weight,
                                             self.LayerNorm.bias, self.LayerNorm.variance_epsilon,
-                                            self.dropout.p, self.training, res_grad=res_grad, grad_planes=gp)
+                                            self.dropout.p, self.training, res_grad=res_grad)
 
 
 class BertAttention(nn.Module):
@@ -227,13 +220,8 @@ class BertAttention(nn.Module):
         self.output = BertSelfOutput(config)
 
     def forward(self, input_tensor, attention_mask_bias):
-        # the residual gradient of input_tensor is fused into the QKV dgrad GEMM; the output
-        # projection's weight gradient runs grouped with the QKV projection's (ops.WgradDefer)
+        # the residual gradient of input_tensor is fused into the QKV dgrad GEMM
         rg = ops.ResidualGrad()
-        if _WGRAD_DEFER:
-            wd = ops.WgradDefer()
-            ctx = self.self(input_tensor, attention_mask_bias, rg, wgrad_join=(self.output.dense.weight, wd))
-            return self.output(ctx, input_tensor, rg, wgrad_defer=wd)
         ctx = self.self(input_tensor, attention_mask_bias, rg)
         return self.output(ctx, input_tensor, rg)
 
@@ -255,15 +243,13 @@ class BertOutput(nn.Module):
         self.dropout = nn.Dropout(config.hidden_dropout_prob)
 
     def forward(self, hidden_states, input_tensor, res_grad=None):
-        gp = ops.GradPlanes()
-        return self.finish(ops.linear(hidden_states, self.dense.weight, grad_planes=gp), input_tensor, res_grad, gp)
+        return self.finish(ops.linear(hidden_states, self.dense.weight), input_tensor, res_grad)
 
-    def finish(self, y, input_tensor, res_grad=None, grad_planes=None):
+    def finish(self, y, input_tensor, res_grad=None):
         """dense bias -> dropout -> + residual -> LayerNorm on the bias-less projection ``y``."""
         return ops.bias_dropout_residual_ln(y, self.dense.bias, input_tensor, self.LayerNorm.weight,
                                             self.LayerNorm.bias, self.LayerNorm.variance_epsilon,
-                                            self.dropout.p, self.training, res_grad=res_grad,
-                                            grad_planes=grad_planes)
+                                            self.dropout.p, self.training, res_grad=res_grad)
 
 
 class BertLayer(nn.Module):
@@ -278,10 +264,10 @@ class BertLayer(nn.Module):
         rg = ops.ResidualGrad()     # residual grad of attention_output -> FFN-up dgrad GEMM
         up = self.intermediate.dense_act
         if up.act == 'gelu' and ops.ffn_fusable(attention_output, up.weight, up.bias, self.output.dense.weight):
-            # --fp32-gemm bf16x3/x6: the GELU epilogue hands the FFN-down GEMM its bf16 planes
-            gp = ops.GradPlanes()
-            y = ops.ffn(attention_output, up.weight, up.bias, self.output.dense.weight, rg, gp)
-            return self.output.finish(y, attention_output, rg, gp)
+            # fp32 runs: bias + GELU in the FFN-up GEMM's epilogue, the GELU backward in the
+            # FFN-down data gradient's (ops.ffn)
+            y = ops.ffn(attention_output, up.weight, up.bias, self.output.dense.weight, rg)
+            return self.output.finish(y, attention_output, rg)
         return self.output(self.intermediate(attention_output, rg), attention_output, rg)
 
 
@@ -314,9 +300,8 @@ class BertEncoder(nn.Module):
                                  checkpoint_activations)
 
     def _piece_weights(self):
-        """The encoder's linear weights in the order the layers split them (the fused QKV view,
-        attention output, FFN up / down): split in one launch per forward when the piece GEMMs
-        run (ops.weight_pieces_scope)."""
+        """The encoder's linear weights (the fused QKV view, attention output, FFN up / down):
+        prepared for the hand-written GEMMs in one launch per forward (ops.weight_pieces_scope)."""
         ws = []
         for layer in self.layer:
             sa = layer.attention.self

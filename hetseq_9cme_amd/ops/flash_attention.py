@@ -7,19 +7,18 @@ to [B, S, H].  The additive mask is the reference's (1 - m) * -10000 (not -inf).
 GPU path: the fused flash-style HIP kernel (``_C.attn_fwd`` / ``attn_bwd``,
 csrc/kernels/attention.hip) for head_dim 64 at any sequence length (keys past
 S are masked, rows past S are neither computed into nor stored), with fp32 or
-bf16 activations (bf16 activations: bf16 MFMA, attention_bf16.hip; fp32 activations: fp32
-MFMA, or -- under ``--fp32-gemm bf16x3/x6`` -- the forward's products as six bf16 piece passes,
-attention_x6.hip, fp32-exact class);
+bf16 activations (bf16 activations: bf16 MFMA, attention_bf16.hip; fp32 activations: the
+products as six bf16 piece passes, attention_x6.hip, fp32-exact class, from 4096 token rows
+under ``--fp32-gemm fp16x3``; fp32 MFMA below that and under ``--fp32-gemm native``);
 other shapes / dtypes use the composite below (batched GEMMs + softmax), which
 is also the CPU path and the test oracle.
 """
 import math
-import os
 
 import torch
 import torch.nn.functional as F
 
-from . import gemm16, split_gemm
+from . import fp32_mode, gemm16
 from ._ext import C, use_kernels
 from .rng import get_rng
 
@@ -61,12 +60,6 @@ def _bias3(bq, bk, bv):
     return v if v is not None else torch.cat([bq, bk, bv], 0)
 
 
-# the split-piece backward (attention_x6.hip) whenever the forward ran split; with bf16x6 and one key
-# block it hands the QKV projection its gradient planes directly
-_X6_BWD = True
-_X6_PLANES = True
-
-
 class _AttnFn(torch.autograd.Function):
     """Fused attention; with ``bq/bk/bv`` the QKV-projection bias is added to
     Q/K/V inside the kernels as they are loaded (the projection GEMM runs
@@ -75,27 +68,21 @@ class _AttnFn(torch.autograd.Function):
     gradient slots, instead of a separate pass over the [B*S, 3H] gradient."""
 
     @staticmethod
-    def forward(ctx, qkv, mask_bias, bq, bk, bv, num_heads, p, gp):
+    def forward(ctx, qkv, mask_bias, bq, bk, bv, num_heads, p):
         from .fused import grad_slot  # noqa: F401  (import cycle guard)
         keep = 1.0 - p
         seed, stream = get_rng().next(qkv.device) if p > 0 else (get_rng().seed_tensor(qkv.device), 0)
         bias = _bias3(bq, bk, bv).float().contiguous() if bq is not None else None
-        # the split (x6) kernels follow the linears' policy (split_gemm.active: B*S >= MIN_ROWS rows),
-        # so small fine-tuning batches keep the fp32-MFMA attention like their GEMMs (ADVICE r2)
-        ctx.split = qkv.dtype == torch.float32 and split_gemm.attention_split(qkv.reshape(-1, qkv.shape[-1]))
-        # one key block (S <= 128): the backward can write the projection's gradient planes
-        ctx.gp = gp if (ctx.split and split_gemm.passes() > 0 and _X6_BWD and _X6_PLANES and qkv.shape[1] <= 128) \
-            else None
+        # the split (x6) kernels from 4096 token rows (fp32_mode.attention_split); small fine-tuning
+        # batches keep the fp32-MFMA attention (ADVICE r2)
+        ctx.split = qkv.dtype == torch.float32 and fp32_mode.attention_split(qkv.reshape(-1, qkv.shape[-1]))
         if ctx.split:
-            # fp32 products on the bf16 matrix cores (six piece passes, attention_x6.hip)
+            # fp32 products on the bf16 matrix cores (six piece passes, attention_x6.hip); the
+            # context's max |x| partials for the attention-output projection's fp16x3 GEMM
             B, S = qkv.shape[0], qkv.shape[1]
-            npc = split_gemm.producer_pieces(B * S, qkv.shape[2] // 3, qkv)
             am = torch.empty(((S + 127) // 128) * num_heads * B * 4, dtype=torch.float32, device=qkv.device) \
                 if gemm16.enabled() else None
-            out, lse, dmask, pcs = C().attn_fwd_x6(qkv, mask_bias, num_heads, keep, seed, stream, bias, npc, am)
-            # the attention-output projection (a piece GEMM) reads the context's pieces directly;
-            # fp16x3: the context's max |x| partials
-            split_gemm.attach_pieces(out, pcs)
+            out, lse, dmask = C().attn_fwd_x6(qkv, mask_bias, num_heads, keep, seed, stream, bias, am)
             gemm16.attach(out, am)
         else:
             out, lse, dmask = C().attn_fwd(qkv, mask_bias, num_heads, keep, seed, stream, bias)
@@ -116,17 +103,7 @@ class _AttnFn(torch.autograd.Function):
             slots = [grad_slot(t) for t in (bq, bk, bv)]
             if not all(t is not None for t in slots):
                 slots = [None, None, None]
-        gp = ctx.gp
-        if gp is not None and gp.want:
-            # dQKV straight into the QKV projection's output-gradient planes (GradPlanes);
-            # autograd gets a zero-storage placeholder the projection never reads
-            n = split_gemm.passes()
-            order = split_gemm.ORDER_N[n] if (gp.prefix or gp.pieces) else split_gemm.ORDER_Q[n]
-            gp.planes, dbias = C().attn_bwd_x6_planes(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads,
-                                                      keep, ctx.bias, *slots, list(order))
-            from .fused import _zero_scalar
-            dqkv = _zero_scalar(qkv.device, qkv.dtype).expand(qkv.shape)
-        elif ctx.split and _X6_BWD:
+        if ctx.split:
             # fp16x3 with one key block (S <= 128): the kernel writes max |dQKV| partials for the QKV
             # projection's data / weight gradient GEMMs
             am = torch.empty(qkv.shape[0] * num_heads, dtype=torch.float32, device=qkv.device) \
@@ -138,22 +115,20 @@ class _AttnFn(torch.autograd.Function):
             dqkv, dbias = C().attn_bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep, ctx.bias,
                                        *slots)
         if ctx.bias is None:
-            return dqkv, None, None, None, None, None, None, None
+            return dqkv, None, None, None, None, None, None
         if slots[0] is not None:
             db = slots
         else:
             H = dbias.numel() // 3
             db = [dbias[:H].view_as(bq), dbias[H:2 * H].view_as(bk), dbias[2 * H:].view_as(bv)]
-        return dqkv, None, db[0], db[1], db[2], None, None, None
+        return dqkv, None, db[0], db[1], db[2], None, None
 
 
-def attention(qkv, mask_bias, num_heads, p, bias=None, grad_planes=None):
-    """``bias``: optional (bq, bk, bv) of the QKV projection, applied here;
-    ``grad_planes``: the projection's ``GradPlanes`` mailbox (ops/fused.py)."""
+def attention(qkv, mask_bias, num_heads, p, bias=None):
+    """``bias``: optional (bq, bk, bv) of the QKV projection, applied here."""
     if _fused_ok(qkv, num_heads):
         bq, bk, bv = bias if bias is not None else (None, None, None)
-        return _AttnFn.apply(qkv.contiguous(), mask_bias.float().contiguous(), bq, bk, bv, int(num_heads), float(p),
-                             grad_planes)
+        return _AttnFn.apply(qkv.contiguous(), mask_bias.float().contiguous(), bq, bk, bv, int(num_heads), float(p))
     if bias is not None:
         qkv = qkv + torch.cat(list(bias), 0).to(qkv.dtype)
     return attention_ref(qkv, mask_bias, num_heads, p)

@@ -5,12 +5,10 @@ hand-written HIP kernels (``_C``), CPU tensors run the plain-torch reference of
 the same math (used by the CPU test-suite and as the numerics oracle for the GPU
 kernel tests).  Semantics follow the reference model (hetseq/bert_modeling.py).
 """
-import os
-
 import torch
 import torch.nn.functional as F
 
-from . import gemm16, split_gemm
+from . import gemm16
 from ._ext import C, use_kernels
 from .rng import get_rng
 
@@ -89,54 +87,6 @@ class ResidualGrad(object):
         return g, None
 
 
-class WgradDefer(object):
-    """Per-forward mailbox that moves one linear's weight gradient into a LATER backward, where
-    it runs grouped with that backward's own weight gradient in one launch (wgrad_split.hip):
-    the attention-output projection (768 x 768: 9 output tiles, alone a 14-way token split at
-    ~0.9 PF/s) joins the QKV projection's (27 tiles).  The joining linear (``linear3``) takes the
-    deferring weight as an extra input so autograd routes that weight's gradient through its
-    backward; its forward arms the box, the deferring linear's backward fills it."""
-    __slots__ = ('armed', 'item')
-
-    def __init__(self):
-        self.armed = False
-        self.item = None
-
-
-class GradPlanes(object):
-    """Per-forward mailbox that hands a linear its OUTPUT gradient already split.
-
-    Under ``--fp32-gemm bf16x3/x6`` the backward of a linear whose output feeds a fused
-    bias + dropout + residual + LayerNorm (BertSelfOutput / BertOutput) starts by
-    splitting the fp32 output gradient dy into bf16 planes.  Instead the LayerNorm
-    backward (which runs first) writes those planes directly (``ln_bwd_planes``: no fp32
-    dy written and read back, one launch less) and deposits them here; the LayerNorm
-    returns a zero-storage placeholder as dy, which the linear never reads.  The linear's
-    forward sets ``want`` only when its backward will take the split-plane path, and
-    ``prefix`` when it wants the prefix form (each distinct piece once, natural order:
-    split_gemm.prefix_mm) instead of the pass-stacked order Q, ``pieces`` when it runs the
-    hand-written piece GEMMs (natural order too: [rows][npieces][N]).
-    """
-    __slots__ = ('want', 'planes', 'prefix', 'pieces')
-
-    def __init__(self):
-        self.want = False
-        self.planes = None
-        self.prefix = False
-        self.pieces = False
-
-    def take(self):
-        p, self.planes = self.planes, None
-        return p
-
-
-def _dy_planes(gp, dy2):
-    """Output-gradient planes of a split-path linear: the LayerNorm's deposit if there is
-    one, else split here."""
-    p = gp.take() if gp is not None else None
-    return p if p is not None else split_gemm.grad_planes(dy2.float())
-
-
 def _dgrad(dy2, W, xshape, mbox):
     """dx = dy2 @ W, accumulated into the deposited residual gradient if any."""
     Wc = cast_w(W, dy2.dtype)
@@ -163,36 +113,11 @@ def _dgrad_bf16(dy2, W, xshape, mbox):
     return gemm16.mm_bf16(dy2, wt).view(xshape)
 
 
-def _dgrad_pieces(dys, wt, xshape, mbox):
-    """``_dgrad`` from dy's pieces and W^T's pieces (hand-written piece GEMM, beta = 1 into
-    the deposited residual gradient)."""
-    if mbox is not None:
-        g, other = mbox.take(torch.float32)
-        if g is not None:
-            return split_gemm.dgrad_pieces(dys, wt, acc=g.view(-1, wt.shape[0])).view(xshape)
-        dx = split_gemm.dgrad_pieces(dys, wt).view(xshape)
-        return dx if other is None else dx + other.view(xshape).to(dx.dtype)
-    return split_gemm.dgrad_pieces(dys, wt).view(xshape)
-
-
-def _dgrad_split(dys, W, xshape, mbox, prefix=False):
-    """``_dgrad`` on the bf16 split planes of dy (``--fp32-gemm bf16x3/x6``); ``prefix``: dy
-    is in the prefix form's natural piece order (split_gemm.prefix_mm)."""
-    dg = split_gemm.dgrad_prefix if prefix else split_gemm.dgrad
-    if mbox is not None:
-        g, other = mbox.take(torch.float32)
-        if g is not None:
-            return dg(dys, W, acc=g.view(-1, W.shape[1])).view(xshape)
-        dx = dg(dys, W).view(xshape)
-        return dx if other is None else dx + other.view(xshape).to(dx.dtype)
-    return dg(dys, W).view(xshape)
-
-
 # ----------------------------------------------------------------- weight-grad side stream
 class _Side(object):
-    # 'auto' (default): the piece-GEMM backward paths only -- BERT-base phase 1 53.9 -> 52.9 ms/step
-    # (profiles/r3_overlap_wgrad_ab.md); the library paths (small batches, NER: 11.9 -> 15.5 ms per
-    # update, host-bound; round 1: 69.5 -> 71.7 ms/step) stay on the compute stream.
+    # 'auto' (default): the hand-written fp16x3 GEMM backward paths only (round 3 on the same
+    # structure: BERT-base phase 1 53.9 -> 52.9 ms/step, profiles/r3_overlap_wgrad_ab.md); the
+    # library paths (native fp32, bf16: round 1 69.5 -> 71.7 ms/step) stay on the compute stream.
     # 'on': every path; 'off': none.
     mode = 'auto'
     streams = {}          # device index -> torch.cuda.Stream
@@ -201,19 +126,19 @@ class _Side(object):
 
 def set_side_stream(flag):
     """Weight-gradient work on a side stream: True / 'on', False / 'off', or 'auto'
-    (the piece-GEMM paths only)."""
+    (the hand-written GEMM paths only)."""
     _Side.mode = {True: 'on', False: 'off'}.get(flag, flag) if isinstance(flag, bool) else str(flag)
     assert _Side.mode in ('on', 'off', 'auto'), flag
 
 
-def side_begin(device, pieces=False):
+def side_begin(device, hand=False):
     """Side stream for off-critical-path weight-gradient work (dW GEMMs, bias
     column sums) of the running backward, ordered after everything already
     queued on the compute stream.  While the compute stream continues with the
     dgrad chain (attention / LayerNorm / GELU backward: mostly memory-bound),
     the side stream's GEMMs fill the matrix cores.  Joined back into the compute
     stream by an end-of-backward callback (``side_join``)."""
-    if _Side.mode == 'off' or (_Side.mode == 'auto' and not pieces) or device.type != 'cuda':
+    if _Side.mode == 'off' or (_Side.mode == 'auto' and not hand) or device.type != 'cuda':
         return None
     idx = device.index if device.index is not None else torch.cuda.current_device()
     st = _Side.streams.get(idx)
@@ -276,12 +201,10 @@ class _EmbedLNFn(torch.autograd.Function):
     def forward(ctx, ids, tt, wte, wpe, wtt, gamma, beta, eps, p, out_bf16):
         keep = 1.0 - p
         seed, stream = get_rng().next(ids.device) if p > 0 else (get_rng().seed_tensor(ids.device), 0)
-        npc = 0 if out_bf16 else split_gemm.producer_pieces(ids.numel(), wte.shape[1], wte)
         am = _amax_buf(ids.numel(), wte, out_bf16)
-        out, z, mean, rstd, pcs = C().embed_ln_fwd(ids, tt, wte, wpe, wtt, gamma, beta, eps, keep, seed, stream,
-                                                   out_bf16, npc, am)
-        split_gemm.attach_pieces(out, pcs)   # the first layer's QKV GEMM reads them
-        gemm16.attach(out, am)               # (fp16x3: its max |x| partials)
+        out, z, mean, rstd = C().embed_ln_fwd(ids, tt, wte, wpe, wtt, gamma, beta, eps, keep, seed, stream,
+                                              out_bf16, am)
+        gemm16.attach(out, am)   # fp16x3: its max |x| partials for the first layer's QKV GEMM
         ctx.save_for_backward(ids, tt if tt is not None else torch.Tensor(), z, mean, rstd, gamma)
         ctx.params = (wte, wpe, wtt, beta)
         ctx.has_tt = tt is not None
@@ -359,76 +282,46 @@ def _amax_buf(rows, ref, bf16, bwd=False):
 
 
 # ----------------------------------------------------------------- bias + dropout + residual + LN
-_ZERO_SCALARS = {}
-
-
-def _zero_scalar(device, dtype):
-    """A cached 0-dim zero (one fill per device / dtype instead of one per backward call):
-    the storage behind the expanded placeholder gradients, never written."""
-    key = (device, dtype)
-    z = _ZERO_SCALARS.get(key)
-    if z is None:
-        z = _ZERO_SCALARS[key] = torch.zeros((), dtype=dtype, device=device)
-    return z
-
-
 class _BiasDropResLNFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, y, bias, res, gamma, beta, eps, p, mbox, gp):
+    def forward(ctx, y, bias, res, gamma, beta, eps, p, mbox):
         keep = 1.0 - p
         seed, stream = get_rng().next(y.device) if p > 0 else (get_rng().seed_tensor(y.device), 0)
-        npc = split_gemm.producer_pieces(y.numel() // y.shape[-1], y.shape[-1], y) if y.dtype == torch.float32 else 0
         am = _amax_buf(y.numel() // y.shape[-1], y, y.dtype != torch.float32)
-        out, z, mean, rstd, pcs = C().ln_fwd(y, bias, res, gamma, beta, eps, keep, seed, stream, False, True, npc, am)
-        split_gemm.attach_pieces(out, pcs)   # the next QKV / FFN-up piece GEMM reads them
-        gemm16.attach(out, am)               # (fp16x3: its max |x| partials)
+        out, z, mean, rstd = C().ln_fwd(y, bias, res, gamma, beta, eps, keep, seed, stream, False, True, am)
+        gemm16.attach(out, am)   # fp16x3: its max |x| partials for the next QKV / FFN-up GEMM
         ctx.save_for_backward(z, mean, rstd, gamma)
         ctx.params = (bias, beta)
         ctx.mbox = mbox
-        ctx.gp = gp
-        ctx.yshape = y.shape
-        ctx.meta = (keep, seed, stream, bias is not None, res is not None, y.numel() != z.numel())
+        ctx.meta = (keep, seed, stream, bias is not None, res is not None)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         z, mean, rstd, gamma = ctx.saved_tensors
-        keep, seed, stream, has_bias, has_res, _ = ctx.meta
+        keep, seed, stream, has_bias, has_res = ctx.meta
         bias, beta = ctx.params
         need_dy = has_bias or keep < 1.0
-        gp = ctx.gp
-        if gp is not None and gp.want and need_dy and z.dtype == torch.float32:
-            # the upstream split-path linear gets dy as bf16 planes; autograd gets a
-            # zero-storage placeholder of dy's shape that nothing reads
-            n = split_gemm.passes()
-            order = split_gemm.ORDER_N[n] if gp.pieces else split_gemm.ORDER_Q[n]
-            dz, planes, dgamma, dbeta, dbias = C().ln_bwd_planes(
-                dout.contiguous(), z, mean, rstd, gamma, keep, seed, stream, has_bias, list(order),
-                split_gemm.PIECES[n], grad_slot(gamma), grad_slot(beta), grad_slot(bias) if has_bias else None)
-            gp.planes = planes
-            dy_ret = _zero_scalar(z.device, z.dtype).expand(ctx.yshape)
-        else:
-            am = _amax_buf(z.numel() // z.shape[-1], z, z.dtype != torch.float32, bwd=True)
-            dz, dy, dgamma, dbeta, dbias = C().ln_bwd(dout.contiguous(), z, mean, rstd, gamma, keep, seed, stream,
-                                                      False, need_dy, has_bias, grad_slot(gamma), grad_slot(beta),
-                                                      grad_slot(bias) if has_bias else None, am)
-            dy_ret = gemm16.attach(dy if need_dy else dz, am)   # (fp16x3: max |dy| partials)
+        am = _amax_buf(z.numel() // z.shape[-1], z, z.dtype != torch.float32, bwd=True)
+        dz, dy, dgamma, dbeta, dbias = C().ln_bwd(dout.contiguous(), z, mean, rstd, gamma, keep, seed, stream,
+                                                  False, need_dy, has_bias, grad_slot(gamma), grad_slot(beta),
+                                                  grad_slot(bias) if has_bias else None, am)
+        dy_ret = gemm16.attach(dy if need_dy else dz, am)   # fp16x3: max |dy| partials
         dres = dz if has_res else None
         # dz is a private buffer only when dy is separate: then it can become the
         # accumulator of the consumer linear's dgrad GEMM
         if dres is not None and need_dy and ctx.mbox is not None and ctx.mbox.deposit(dz):
             dres = None
-        return dy_ret, (dbias if has_bias else None), dres, dgamma, dbeta, None, None, None, None
+        return dy_ret, (dbias if has_bias else None), dres, dgamma, dbeta, None, None, None
 
 
-def bias_dropout_residual_ln(y, bias, res, gamma, beta, eps, p, training, res_grad=None, grad_planes=None):
+def bias_dropout_residual_ln(y, bias, res, gamma, beta, eps, p, training, res_grad=None):
     """LN(dropout(y + bias) + res)  (BertSelfOutput / BertOutput, bert_modeling.py:387-391).
-    ``res_grad``: a ``ResidualGrad`` shared with the linear that also consumed ``res``;
-    ``grad_planes``: a ``GradPlanes`` shared with the linear that produced ``y``."""
+    ``res_grad``: a ``ResidualGrad`` shared with the linear that also consumed ``res``."""
     p = p if training else 0.0
     if use_kernels(y):
         return _BiasDropResLNFn.apply(y.contiguous(), bias, None if res is None else res.contiguous(), gamma, beta,
-                                      float(eps), float(p), res_grad, grad_planes)
+                                      float(eps), float(p), res_grad)
     x = y if bias is None else y + bias
     x = F.dropout(x, p, training)
     if res is not None:
@@ -500,88 +393,47 @@ def dropout(x, p, training):
 # ----------------------------------------------------------------- linear (direct grad write)
 class _LinearFn(torch.autograd.Function):
     """y = x W^T (+ b).  Backward writes dW (one GEMM) and db (one column-sum
-    kernel) straight into the parameters' flat gradient slots."""
+    kernel) straight into the parameters' flat gradient slots.  fp32 runs: the fp16x3 GEMMs
+    (ops/gemm16.py); --precision bf16: the same kernel's bf16 variant; --fp32-gemm native and
+    shapes without a tile (heads narrower than 64 outputs): the library fp32 / bf16 GEMM."""
 
     @staticmethod
-    def forward(ctx, x, W, b, mbox, gp, defer=None):
+    def forward(ctx, x, W, b, mbox):
         x2 = x.reshape(-1, x.shape[-1])
         ctx.f16 = gemm16.ok(x2, W.shape[0])
-        if ctx.f16:   # --fp32-gemm fp16x3: fp32 operands split inside the GEMM kernels
+        ctx.W, ctx.b, ctx.mbox, ctx.xshape = W, b, mbox, x.shape
+        if ctx.f16:   # fp32 operands split inside the GEMM kernels
             x2 = gemm16.rows2(x)
             ctx.xparts = gemm16.amax(x, x2)
             y, wt, ctx.wparts = gemm16.linear(x2, ctx.xparts, W, b)
             ctx.save_for_backward(x2, wt)
-            ctx.W, ctx.b, ctx.mbox, ctx.xshape = W, b, mbox, x.shape
             return y.view(*x.shape[:-1], y.shape[-1])
-        ctx.split = split_gemm.active(x2)
-        ctx.pieces = ctx.split and split_gemm.nt_ok(W.shape[1], W.shape[0], x2.shape[0])
-        ctx.gp = gp if (ctx.split and b is None) else None
-        # weight gradient deferred to the joining linear's backward (WgradDefer)
-        ctx.defer = defer if (defer is not None and defer.armed and ctx.pieces and b is None) else None
-        if ctx.gp is not None:
-            ctx.gp.want = True
-            ctx.gp.pieces = ctx.pieces
-        Wsave = W
-        if ctx.pieces:    # fp32 on bf16 matrix cores, hand-written piece GEMMs
-            x2 = split_gemm.input_pieces(x, x2)
-            wf, Wsave = split_gemm.weight_pieces(W)
-            y = split_gemm.gemm(x2, wf)
-            if b is not None:
-                y.add_(b)
-        elif ctx.split:   # library GEMMs on pass-stacked planes
-            y, x2 = split_gemm.forward(x2, W)
-            if b is not None:
-                y.add_(b)
+        Wc = cast_w(W, x.dtype)
+        ctx.b16 = gemm16.bf16_ok(x2, W.shape[0], W.shape[1]) and Wc.is_contiguous()
+        if ctx.b16:   # --precision bf16 on the hand-written kernel (bias in the epilogue)
+            y = gemm16.mm_bf16(gemm16.rows2(x), Wc, bias=b)
         else:
-            Wc = cast_w(W, x.dtype)
-            ctx.b16 = gemm16.bf16_ok(x2, W.shape[0], W.shape[1]) and Wc.is_contiguous()
-            if ctx.b16:   # --precision bf16 on the hand-written kernel (bias in the epilogue)
-                y = gemm16.mm_bf16(gemm16.rows2(x), Wc, bias=b)
-            else:
-                y = torch.mm(x2, Wc.t()) if b is None else torch.addmm(cast_w(b, x.dtype), x2, Wc.t())
-        ctx.save_for_backward(x2, Wsave)
-        ctx.W = W
-        ctx.b = b
-        ctx.mbox = mbox
-        ctx.xshape = x.shape
+            y = torch.mm(x2, Wc.t()) if b is None else torch.addmm(cast_w(b, x.dtype), x2, Wc.t())
+        ctx.save_for_backward(x2, Wc)
         return y.view(*x.shape[:-1], y.shape[-1])
 
     @staticmethod
     def backward(ctx, dy):
         if ctx.f16:
-            return _LinearFn._backward_f16(ctx, dy)
-        x2, Wsaved = ctx.saved_tensors
-        W = ctx.W
-        b = ctx.b
+            return _linear_backward_f16(ctx, dy)
+        x2, _ = ctx.saved_tensors
+        W, b = ctx.W, ctx.b
         dy2 = dy.reshape(-1, dy.shape[-1])
-        if ctx.pieces:
-            dys = ctx.gp.take() if ctx.gp is not None else None
-            dys = dys if dys is not None else split_gemm.pieces(dy2.float())
-        else:
-            dys = _dy_planes(ctx.gp, dy2) if ctx.split else None
         if not ctx.needs_input_grad[0]:
             dx = None
-        elif ctx.pieces:
-            dx = _dgrad_pieces(dys, Wsaved, ctx.xshape, ctx.mbox)
-        elif ctx.split:
-            dx = _dgrad_split(dys, W, ctx.xshape, ctx.mbox)
-        elif getattr(ctx, 'b16', False):
+        elif ctx.b16:
             dx = _dgrad_bf16(dy2, W, ctx.xshape, ctx.mbox)
         else:
             dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox)
-        if ctx.defer is not None:   # dW is computed (grouped) by the joining linear's backward
-            ctx.defer.item = (dys, x2, W.shape[0], W.shape[1])
-            return dx, None, None, None, None, None
         slot = grad_slot(W)
-        direct = slot is not None
-        side = side_begin(dy2.device, ctx.pieces) if direct else None
+        side = side_begin(dy2.device) if slot is not None else None
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            if ctx.pieces:
-                dW = split_gemm.wgrad_pieces(dys, x2, W.shape[0], W.shape[1], slot)
-            elif ctx.split:
-                dW = split_gemm.wgrad(dys, x2, W.shape[0], W.shape[1], slot)
-            else:
-                dW = _wgrad(dy2, x2, slot)
+            dW = _wgrad(dy2, x2, slot)
             db = None
             if b is not None:
                 if dy2.shape[-1] % 4 == 0:
@@ -591,9 +443,7 @@ class _LinearFn(torch.autograd.Function):
         if side is not None:
             dy2.record_stream(side)
             x2.record_stream(side)
-            if dys is not None:
-                dys.record_stream(side)
-        return dx, dW, db, None, None, None
+        return dx, dW, db, None
 
 
 def _f16_dgrad(dy2, dparts, wt, wparts, xshape, mbox):
@@ -624,148 +474,39 @@ def _linear_backward_f16(ctx, dy):
     if side is not None:
         for t in (dy2, x2, dparts, ctx.xparts):
             t.record_stream(side)
-    return dx, dW, db, None, None, None
+    return dx, dW, db, None
 
 
-_LinearFn._backward_f16 = staticmethod(_linear_backward_f16)
-
-
-def linear(x, W, b=None, res_grad=None, grad_planes=None, wgrad_defer=None):
+def linear(x, W, b=None, res_grad=None):
     """F.linear with direct-to-slot weight/bias gradients on the GPU;
-    ``res_grad``: see ``ResidualGrad``; ``grad_planes``: see ``GradPlanes``;
-    ``wgrad_defer``: see ``WgradDefer`` (the weight must also be passed to the joining linear)."""
+    ``res_grad``: see ``ResidualGrad``."""
     if use_kernels(x):
-        return _LinearFn.apply(x, W, b, res_grad, grad_planes, wgrad_defer)
+        return _LinearFn.apply(x, W, b, res_grad)
     return F.linear(x, cast_w(W, x.dtype), cast_w(b, x.dtype))
 
 
-# ----------------------------------------------------------------- FFN block on split planes
-# FFN W1 / W2 weight gradients as one grouped launch: measured 732 -> 756 us (3 token splits over
-# 72 tiles lose to 7 over 36 each; profiles/r3_wgrad_group_probe.log) -- off by default
-_GROUP_FFN = False
-
-
-class _FFNSplitFn(torch.autograd.Function):
-    """y2 = gelu(x W1^T + b1) W2^T for ``--fp32-gemm bf16x3/x6`` as one autograd node, so
-    the GELU epilogue writes the FFN-down GEMM's bf16 input planes directly and the GELU
-    backward writes the FFN-up gradient's planes (+ dbias) directly: no fp32 [T, 4H]
-    activation / gradient and no separate split pass over either (2 x ~200 MB of HBM
-    traffic per layer at BERT-base phase-1 sizes)."""
+# ----------------------------------------------------------------- FFN block (fp16x3)
+class _FFNFn(torch.autograd.Function):
+    """y2 = gelu(x W1^T + b1) W2^T for fp32 runs as one autograd node: the FFN-up GEMM's
+    epilogue applies bias + GELU (hetseq/bert_modeling.py:166-168, :409) and writes gelu(u) with
+    its max |.| partials -- the FFN-down GEMM's operand -- and gelu'(u) for the backward, whose
+    FFN-down data-gradient epilogue applies the GELU backward and the FFN-up bias gradient (:419):
+    no separate bias / activation pass in either direction."""
 
     @staticmethod
-    def forward(ctx, x, W1, b1, W2, mbox, gp):
-        x2 = x.reshape(-1, x.shape[-1])
-        ctx.f16 = gemm16.ok(x2, W1.shape[0]) and W2.shape[0] % 64 == 0
-        if ctx.f16:
-            # fp16x3: the FFN-up epilogue writes gelu'(u) (backward) and gelu(u) in fp32 with its
-            # max |.| partials -- the FFN-down GEMM's operand, split in that GEMM's registers
-            x2 = gemm16.rows2(x)
-            xparts = gemm16.amax(x, x2)
-            d, h, hparts, w1t, p1 = gemm16.gemm_gelu(x2, xparts, W1, b1)
-            y2, w2t, p2 = gemm16.linear(h, hparts, W2)
-            ctx.save_for_backward(x2, d, h, w1t, w2t)
-            ctx.parts = (xparts, hparts, p1, p2)
-            ctx.W, ctx.b1, ctx.mbox, ctx.xshape = (W1, W2), b1, mbox, x.shape
-            return y2.view(*x.shape[:-1], y2.shape[-1])
-        rows = x.numel() // x.shape[-1]
-        ctx.pieces = split_gemm.nt_ok(W1.shape[1], W1.shape[0], rows) and split_gemm.nt_ok(W2.shape[1], W2.shape[0], rows)
-        ctx.gp = gp
-        if ctx.gp is not None:
-            ctx.gp.want = True
-            ctx.gp.pieces = ctx.pieces
-        if ctx.pieces:
-            # bias + GELU in the FFN-up GEMM's epilogue (gelu(u) written as the FFN-down GEMM's
-            # pieces; gelu'(u) kept in fp32 for the backward, from the same erf):
-            # bert_modeling.py:166-168
-            xs = split_gemm.input_pieces(x, x2)
-            w1f, w1t = split_gemm.weight_pieces(W1)
-            u, hs = split_gemm.gemm_gelu(xs, w1f, b1, deriv=True)
-            w2f, w2t = split_gemm.weight_pieces(W2)
-            y2 = split_gemm.gemm(hs, w2f)
-            ctx.save_for_backward(xs, u, hs, w1t, b1, w2t)
-        else:
-            y1, xs = split_gemm.forward(x2, W1)
-            n = split_gemm.passes()
-            # prefix form for the deep products (FFN-down forward, FFN-up data gradient): the
-            # GELU epilogue / backward write each distinct piece once
-            ctx.pf_down = split_gemm.prefix_ok(W2.shape[1], W2.shape[0])
-            ctx.pf_up = split_gemm.prefix_ok(W1.shape[0], W1.shape[1])
-            if ctx.pf_down:
-                hs = split_gemm.act_planes(y1, b1, 'gelu', order=split_gemm.ORDER_N[n])
-                y2 = split_gemm.forward_prefix(hs, W2)
-            else:
-                hs = split_gemm.act_planes(y1, b1, 'gelu')
-                y2 = split_gemm.forward_planes(hs, W2)
-            ctx.save_for_backward(xs, y1, hs, W1, b1, W2)
-        ctx.W = (W1, W2)
-        ctx.mbox = mbox
-        ctx.xshape = x.shape
+    def forward(ctx, x, W1, b1, W2, mbox):
+        x2 = gemm16.rows2(x)
+        xparts = gemm16.amax(x, x2)
+        d, h, hparts, w1t, p1 = gemm16.gemm_gelu(x2, xparts, W1, b1)
+        y2, w2t, p2 = gemm16.linear(h, hparts, W2)
+        ctx.save_for_backward(x2, d, h, w1t, w2t)
+        ctx.parts = (xparts, hparts, p1, p2)
+        ctx.W, ctx.b1, ctx.mbox, ctx.xshape = (W1, W2), b1, mbox, x.shape
         return y2.view(*x.shape[:-1], y2.shape[-1])
 
     @staticmethod
     def backward(ctx, dy):
-        if ctx.f16:
-            return _ffn_backward_f16(ctx, dy)
-        xs, y1, hs, w1, b1, w2 = ctx.saved_tensors
-        W1, W2 = ctx.W
-        dy2 = dy.reshape(-1, dy.shape[-1])
-        if ctx.pieces:
-            dys = ctx.gp.take() if ctx.gp is not None else None
-            dys = dys if dys is not None else split_gemm.pieces(dy2.float())
-            # GELU backward in the FFN-down data-gradient epilogue: the pieces of
-            # dh * gelu'(u) and the FFN-up bias gradient (y1 = gelu'(u), saved by the forward)
-            slot2, slot1 = grad_slot(W2), grad_slot(W1)
-            # --overlap-wgrad: each weight gradient on the side stream, concurrent with the next
-            # data-gradient GEMM of the compute stream, so one kernel's epilogue store bursts
-            # (all CUs at once, nothing else to run) meet the other's MFMA work
-            side = side_begin(dy2.device, True) if slot2 is not None and slot1 is not None else None
-            if side is not None:
-                with torch.cuda.stream(side):
-                    dW2 = split_gemm.wgrad_pieces(dys, hs, W2.shape[0], W2.shape[1], slot2)
-                dys.record_stream(side)
-                hs.record_stream(side)
-            dy1s, db1 = split_gemm.gemm_dgelu(dys, w2, y1, None, grad_slot(b1), deriv=True)
-            if side is not None:
-                side = side_begin(dy2.device, True)   # after the dGELU pieces
-                with torch.cuda.stream(side):
-                    dW1 = split_gemm.wgrad_pieces(dy1s, xs, W1.shape[0], W1.shape[1], slot1)
-                dy1s.record_stream(side)
-                xs.record_stream(side)
-                dx = _dgrad_pieces(dy1s, w1, ctx.xshape, ctx.mbox)
-                return dx, dW1, db1, dW2, None, None
-            # both weight gradients in one launch when they qualify (wgrad_split_group)
-            grp = split_gemm.wgrad_pieces_group([(dys, hs, W2.shape[0], W2.shape[1], slot2),
-                                                 (dy1s, xs, W1.shape[0], W1.shape[1], slot1)]) \
-                if _GROUP_FFN else None
-            if grp is not None:
-                dW2, dW1 = grp
-            else:
-                dW2 = split_gemm.wgrad_pieces(dys, hs, W2.shape[0], W2.shape[1], slot2)
-            dx = _dgrad_pieces(dy1s, w1, ctx.xshape, ctx.mbox)
-            if grp is None:
-                dW1 = split_gemm.wgrad_pieces(dy1s, xs, W1.shape[0], W1.shape[1], slot1)
-            return dx, dW1, db1, dW2, None, None
-        dys = _dy_planes(ctx.gp, dy2)
-        dh = split_gemm.dgrad(dys, W2)
-        slot2, slot1 = grad_slot(W2), grad_slot(W1)
-        # --overlap-wgrad: the two weight-gradient GEMMs run on the side stream, beside the
-        # memory-bound GELU backward / plane writes of the dgrad chain
-        side = side_begin(dy2.device) if slot2 is not None else None
-        nat = split_gemm.ORDER_N[split_gemm.passes()]
-        with torch.cuda.stream(side) if side is not None else _nullctx():
-            dW2 = split_gemm.wgrad(dys, hs, W2.shape[0], W2.shape[1], slot2, x_order=nat if ctx.pf_down else None)
-        if side is not None:
-            dys.record_stream(side)
-            hs.record_stream(side)
-        dy1s, db1 = split_gemm.act_grad_planes(dh, y1, b1, 'gelu', grad_slot(b1), order=nat if ctx.pf_up else None)
-        dx = _dgrad_split(dy1s, W1, ctx.xshape, ctx.mbox, prefix=ctx.pf_up)
-        side = side_begin(dy2.device) if slot1 is not None else None
-        with torch.cuda.stream(side) if side is not None else _nullctx():
-            dW1 = split_gemm.wgrad(dy1s, xs, W1.shape[0], W1.shape[1], slot1, dy_order=nat if ctx.pf_up else None)
-        if side is not None:
-            dy1s.record_stream(side)
-            xs.record_stream(side)
-        return dx, dW1, db1, dW2, None, None
+        return _ffn_backward_f16(ctx, dy)
 
 
 def _ffn_backward_f16(ctx, dy):
@@ -792,19 +533,17 @@ def _ffn_backward_f16(ctx, dy):
         for q in (t, tparts, x2, xparts):
             q.record_stream(side)
     dx = _f16_dgrad(t, tparts, w1t, p1, ctx.xshape, ctx.mbox)
-    return dx, dW1, db1, dW2, None, None
+    return dx, dW1, db1, dW2, None
 
 
 def ffn_fusable(x, W1, b1, W2):
-    """The fused FFN path applies (fp32 GPU activations, --fp32-gemm bf16x3/x6/fp16x3)."""
-    if b1 is not None and gemm16.ok(x.reshape(-1, x.shape[-1]), W1.shape[0]) and W2.shape[0] % 64 == 0:
-        return True
-    return split_gemm.active(x) and b1 is not None and W1.shape[0] % 8 == 0 and x.shape[-1] % 8 == 0
+    """The fused FFN path applies (fp32 GPU activations on the fp16x3 GEMMs)."""
+    return b1 is not None and gemm16.ok(x.reshape(-1, x.shape[-1]), W1.shape[0]) and W2.shape[0] % 64 == 0
 
 
-def ffn(x, W1, b1, W2, res_grad=None, grad_planes=None):
+def ffn(x, W1, b1, W2, res_grad=None):
     """gelu(x W1^T + b1) W2^T (the output bias / dropout / residual / LayerNorm follow)."""
-    return _FFNSplitFn.apply(x, W1, b1, W2, res_grad, grad_planes)
+    return _FFNFn.apply(x, W1, b1, W2, res_grad)
 
 
 # ----------------------------------------------------------------- fused Q/K/V projection
@@ -833,32 +572,26 @@ def qkv_weight_view(wq, wk, wv):
     return _adjacent_view([wq, wk, wv])
 
 
-_WSPLIT_BATCH = True      # every encoder weight split in one launch per forward
-_DECODER_PIECES = True    # MLM decoder on the piece GEMMs (bf16x6)
-
-
 def weight_pieces_scope(Ws, x):
-    """``split_gemm.weight_pieces_scope`` over ``Ws`` when the piece GEMMs will run for the
-    activations ``x`` [.., H] (``split_gemm.producer_pieces``), else a no-op context.
-    (``_WSPLIT_BATCH = False`` turns the batch split off.)"""
+    """Per-forward weight operands of the hand-written GEMMs for activations ``x`` [.., H]: every
+    weight in ``Ws`` split into its fp16x3 pieces (fp32 runs, ``gemm16.weight_scope``) or
+    transposed to bf16 (``--precision bf16``, ``gemm16.bf16_scope``) in one launch pair; a no-op
+    context otherwise."""
     import contextlib
-    if torch.is_tensor(x) and x.dtype == torch.bfloat16 and use_kernels(x):
-        return gemm16.bf16_scope(Ws)   # --precision bf16: W^T copies for the data gradients
-    if not _WSPLIT_BATCH or not torch.is_tensor(x) or x.dtype != torch.float32:
+    if not torch.is_tensor(x) or not use_kernels(x):
         return contextlib.nullcontext()
-    if gemm16.enabled():
-        return gemm16.weight_scope(Ws) if use_kernels(x) else contextlib.nullcontext()
-    rows = x.numel() // max(1, x.shape[-1])
-    if not split_gemm.producer_pieces(rows, x.shape[-1], x):
-        return contextlib.nullcontext()
-    return split_gemm.weight_pieces_scope(Ws)
+    if x.dtype == torch.bfloat16:
+        return gemm16.bf16_scope(Ws)   # W^T copies for the data gradients
+    if x.dtype == torch.float32 and gemm16.enabled():
+        return gemm16.weight_scope(Ws)
+    return contextlib.nullcontext()
 
 
 class _Linear3Fn(torch.autograd.Function):
     """y = x @ [Wq;Wk;Wv]^T + [bq;bk;bv] as ONE GEMM (N = 3H)."""
 
     @staticmethod
-    def forward(ctx, x, wq, wk, wv, bq, bk, bv, mbox, gp, wjoin=None, join=None):
+    def forward(ctx, x, wq, wk, wv, bq, bk, bv, mbox):
         has_b = bq is not None
         W = _adjacent_view([wq, wk, wv])
         if W is None:
@@ -868,100 +601,53 @@ class _Linear3Fn(torch.autograd.Function):
             b = _adjacent_view([bq, bk, bv])
             if b is None:
                 b = torch.cat([bq, bk, bv], 0)
+        x2 = x.reshape(-1, x.shape[-1])
+        ctx.params = (wq, wk, wv, bq, bk, bv)
+        ctx.has_b, ctx.mbox, ctx.xshape = has_b, mbox, x.shape
+        ctx.n = [wq.shape[0], wk.shape[0], wv.shape[0]]
+        ctx.f16 = gemm16.ok(x2, W.shape[0])
+        if ctx.f16:   # fp32 runs: the fp16x3 GEMM
+            x2 = gemm16.rows2(x)
+            ctx.xparts = gemm16.amax(x, x2)
+            y, wt, ctx.wparts = gemm16.linear(x2, ctx.xparts, W, b)
+            ctx.save_for_backward(x2, wt)
+            return y.view(*x.shape[:-1], y.shape[-1])
         Wc, bc = W, b
         if x.dtype != W.dtype:
             sh = [getattr(t, '_hx_bf16', None) for t in (wq, wk, wv)]
             Wc = _adjacent_view(sh) if all(t is not None for t in sh) else None
             Wc = Wc if Wc is not None else W.to(x.dtype)
             bc = cast_w(b, x.dtype) if has_b else None
-        x2 = x.reshape(-1, x.shape[-1])
-        ctx.f16 = gemm16.ok(x2, W.shape[0])
-        if ctx.f16:   # --fp32-gemm fp16x3
-            ctx.split = ctx.pieces = False
-            x2 = gemm16.rows2(x)
-            ctx.xparts = gemm16.amax(x, x2)
-            y, wt, ctx.wparts = gemm16.linear(x2, ctx.xparts, W, b)
-            ctx.save_for_backward(x2, wt)
-            ctx.params = (wq, wk, wv, bq, bk, bv)
-            ctx.has_b, ctx.join, ctx.wjoin, ctx.mbox, ctx.xshape = has_b, None, None, mbox, x.shape
-            ctx.n = [wq.shape[0], wk.shape[0], wv.shape[0]]
-            return y.view(*x.shape[:-1], y.shape[-1])
-        ctx.split = split_gemm.active(x2)
-        ctx.pieces = ctx.split and split_gemm.nt_ok(W.shape[1], W.shape[0], x2.shape[0])
-        ctx.gp = gp if (ctx.split and not has_b) else None
-        if ctx.gp is not None:
-            ctx.gp.want = True
-            ctx.gp.pieces = ctx.pieces
-            # deep data gradient (3H -> H): natural pass order (the prefix form measured neutral to
-            # 0.1 ms/step slower here, unlike the 4H -> H products: split_gemm.prefix_ok)
-            ctx.gp.prefix = False
-        if ctx.pieces:    # fp32 on bf16 matrix cores, hand-written piece GEMMs
-            x2 = split_gemm.input_pieces(x, x2)
-            wf, Wc = split_gemm.weight_pieces(W)
-            y = split_gemm.gemm(x2, wf)
-            if has_b:
-                y.add_(b)
-        elif ctx.split:   # library GEMMs on pass-stacked planes
-            y, x2 = split_gemm.forward(x2, W)
-            if has_b:
-                y.add_(b)
+        ctx.b16 = gemm16.bf16_ok(x2, W.shape[0], W.shape[1]) and Wc.is_contiguous()
+        if ctx.b16:
+            y = gemm16.mm_bf16(gemm16.rows2(x), Wc, bias=b if has_b else None)
         else:
-            # without biases (applied inside the fused attention instead) this is a plain GEMM
-            ctx.b16 = gemm16.bf16_ok(x2, W.shape[0], W.shape[1]) and Wc.is_contiguous()
-            if ctx.b16:
-                y = gemm16.mm_bf16(gemm16.rows2(x), Wc, bias=b if has_b else None)
-            else:
-                y = torch.addmm(bc, x2, Wc.t()) if has_b else torch.mm(x2, Wc.t())
+            y = torch.addmm(bc, x2, Wc.t()) if has_b else torch.mm(x2, Wc.t())
         ctx.save_for_backward(x2, Wc)
-        ctx.params = (wq, wk, wv, bq, bk, bv)
-        ctx.has_b = has_b
-        # WgradDefer: this backward also produces ``wjoin``'s gradient (grouped launch)
-        ctx.join = join if (join is not None and wjoin is not None and ctx.pieces and not has_b) else None
-        ctx.wjoin = wjoin if ctx.join is not None else None
-        if ctx.join is not None:
-            ctx.join.armed = True
-        ctx.mbox = mbox
-        ctx.xshape = x.shape
-        ctx.n = [wq.shape[0], wk.shape[0], wv.shape[0]]
         return y.view(*x.shape[:-1], y.shape[-1])
 
     @staticmethod
     def backward(ctx, dy):
         x2, W = ctx.saved_tensors
         wq, wk, wv, bq, bk, bv = ctx.params
-        dy2 = dy.reshape(-1, dy.shape[-1])
+        n_out, n_in = sum(ctx.n), x2.shape[1]
         if ctx.f16:
             # W holds W^T's fp16 pieces here; dx after the side-stream weight gradient is queued
-            n_out = sum(ctx.n)
             dy2 = gemm16.rows2(dy)
             dys = gemm16.amax(dy, dy2)
             dx = None
-            n_in = x2.shape[1]
             wg = lambda slot: gemm16.wgrad(dy2, dys, x2, ctx.xparts, n_out, n_in, slot)
-        elif ctx.pieces:
-            n_out = sum(ctx.n)
-            dys = ctx.gp.take() if ctx.gp is not None else None   # the attention backward's pieces
-            dys = dys if dys is not None else split_gemm.pieces(dy2.float())
-            dx = None   # after the side-stream weight gradients are queued (they overlap it)
-            n_in = W.shape[0]
-            wg = lambda slot: split_gemm.wgrad_pieces(dys, x2, n_out, n_in, slot)
         else:
-            dep = ctx.gp.take() if ctx.gp is not None else None
-            pf = dep is not None and ctx.gp.prefix   # the producer wrote the prefix form
-            if ctx.split:
-                dys = dep if dep is not None else split_gemm.grad_planes(dy2.float())
-                dx = _dgrad_split(dys, W, ctx.xshape, ctx.mbox, prefix=pf)
-            elif getattr(ctx, 'b16', False):
-                dys = None
-                wq_, wk_, wv_ = ctx.params[:3]
-                Wf = _adjacent_view([wq_, wk_, wv_])
-                dx = _dgrad_bf16(dy2, Wf if Wf is not None else torch.cat([wq_, wk_, wv_], 0), ctx.xshape, ctx.mbox)
+            dy2 = dy.reshape(-1, dy.shape[-1])
+            dys = None
+            if not ctx.needs_input_grad[0]:
+                dx = None
+            elif ctx.b16:
+                Wf = _adjacent_view([wq, wk, wv])
+                dx = _dgrad_bf16(dy2, Wf if Wf is not None else torch.cat([wq, wk, wv], 0), ctx.xshape, ctx.mbox)
             else:
-                dys = None
                 dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox)
-            dy_order = split_gemm.ORDER_N[split_gemm.passes()] if pf else None
-            wg = ((lambda slot: split_gemm.wgrad(dys, x2, W.shape[0], W.shape[1], slot, dy_order=dy_order))
-                  if ctx.split else (lambda slot: _wgrad(dy2, x2, slot)))
+            wg = lambda slot: _wgrad(dy2, x2, slot)
         a, b_, _ = ctx.n
         # weight grads: ONE GEMM straight into the three adjacent flat slots when possible
         ws = [grad_slot(w) for w in (wq, wk, wv)]
@@ -970,28 +656,9 @@ class _Linear3Fn(torch.autograd.Function):
         bs = [grad_slot(t) for t in (bq, bk, bv)] if has_b else [None, None, None]
         fb = _adjacent_view(bs) if all(t is not None for t in bs) else None
         direct = fused is not None and (fb is not None or not has_b)
-        side = side_begin(dy2.device, ctx.pieces or ctx.f16) if direct else None
-        item = ctx.join.item if ctx.join is not None else None
-        gjoin = None
+        side = side_begin(dy2.device, ctx.f16) if direct else None
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            if item is not None:
-                # the deferred linear's weight gradient, grouped with this one in one launch
-                jdys, jx2, jn_out, jn_in = item
-                ctx.join.item = None
-                jslot = grad_slot(ctx.wjoin)
-                grp = split_gemm.wgrad_pieces_group([(dys, x2, n_out, n_in, fused),
-                                                     (jdys, jx2, jn_out, jn_in, jslot)]) \
-                    if fused is not None else None
-                if grp is not None:
-                    gjoin = grp[1]
-                else:
-                    gjoin = split_gemm.wgrad_pieces(jdys, jx2, jn_out, jn_in, jslot)
-                if side is not None:
-                    jdys.record_stream(side)
-                    jx2.record_stream(side)
-            if item is not None and grp is not None:
-                gW = ws
-            elif fused is not None:
+            if fused is not None:
                 wg(fused)
                 gW = ws
             else:
@@ -1016,86 +683,52 @@ class _Linear3Fn(torch.autograd.Function):
                 ctx.xparts.record_stream(side)
         if ctx.f16 and ctx.needs_input_grad[0]:
             dx = _f16_dgrad(dy2, dys, W, ctx.wparts, ctx.xshape, ctx.mbox)
-        elif ctx.pieces:
-            dx = _dgrad_pieces(dys, W, ctx.xshape, ctx.mbox)     # W holds the W^T pieces here
         if not has_b:
-            return (dx, gW[0], gW[1], gW[2], None, None, None, None, None, gjoin, None)
+            return (dx, gW[0], gW[1], gW[2], None, None, None, None)
         gb = bs if fb is not None else [db[:a], db[a:a + b_], db[a + b_:]]
-        return (dx, gW[0], gW[1], gW[2], gb[0], gb[1], gb[2], None, None, gjoin, None)
+        return (dx, gW[0], gW[1], gW[2], gb[0], gb[1], gb[2], None)
 
 
-def linear3(x, wq, wk, wv, bq, bk, bv, res_grad=None, grad_planes=None, wgrad_join=None):
-    """``grad_planes``: see ``GradPlanes`` (the fused attention backward deposits the
-    projection's output-gradient planes); ``wgrad_join`` = (weight, ``WgradDefer``): this
-    backward also produces that weight's gradient, deferred from a later linear."""
-    wj, box = wgrad_join if wgrad_join is not None else (None, None)
-    return _Linear3Fn.apply(x, wq, wk, wv, bq, bk, bv, res_grad, grad_planes, wj, box)
+def linear3(x, wq, wk, wv, bq, bk, bv, res_grad=None):
+    """The fused Q/K/V projection (``res_grad``: see ``ResidualGrad``)."""
+    return _Linear3Fn.apply(x, wq, wk, wv, bq, bk, bv, res_grad)
 
 
 # ----------------------------------------------------------------- attention core
-def attention(qkv, mask_bias, num_heads, p, training, bias=None, grad_planes=None):
+def attention(qkv, mask_bias, num_heads, p, training, bias=None):
     """softmax(Q K^T / sqrt(d) + mask) -> dropout -> @ V  on the packed [B, S, 3H]
     projection; returns [B, S, H] (reference BertSelfAttention, :351-377).
     ``mask_bias`` is the additive [B, S] key mask ((1 - m) * -10000); ``bias`` the
-    optional (bq, bk, bv) of a bias-less QKV projection, added inside the kernel;
-    ``grad_planes``: the projection's ``GradPlanes`` mailbox."""
+    optional (bq, bk, bv) of a bias-less QKV projection, added inside the kernel."""
     from .flash_attention import attention as _attention
-    return _attention(qkv, mask_bias, num_heads, p if training else 0.0, bias, grad_planes)
+    return _attention(qkv, mask_bias, num_heads, p if training else 0.0, bias)
 
 
 # ----------------------------------------------------------------- MLM decoder + softmax-xent
 class _DecoderXentFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, W, bias, labels):
-        ctx.f16 = gemm16.ok(h, 64) and h.is_contiguous() and W.shape[1] % 64 == 0
-        if ctx.f16:
-            # --fp32-gemm fp16x3: the vocabulary padded to a multiple of 768 with zero weight rows
-            # (whole 192 / 256 tiles; the padding logits are exactly 0 and never read as logits)
-            V, H = W.shape
-            Vp = (V + 767) // 768 * 768
-            Wp = _padded_rows(W, Vp)
-            wf, wt, wparts = C().split_weight_f16([Wp])[0]
-            hparts = gemm16.amax(h, h)
-            full = gemm16.mm(h, hparts, wf, wparts)
-            logits = full[:, :V]
-            loss_rows = C().softmax_xent_(logits, bias, labels, -1)   # logits <- softmax - onehot
-            count = (labels != -1).sum().to(torch.float32)
-            loss = loss_rows.sum() / count
-            ctx.save_for_backward(h, W, full, count, wt, wparts)
-            ctx.params = (W, bias)
-            return loss
-        ctx.split = split_gemm.active(h, W.shape[0])
-        ctx.pieces = False
-        if ctx.split:    # fp32 on bf16 matrix cores (--fp32-gemm)
-            # vocabulary padded to a multiple of 256 (zero weight rows): 16-B aligned logits
-            # rows for the GEMM epilogue (694 -> 598 us at BERT-base phase 1) and the backward's
-            # planes; the padding columns stay exactly 0 and are never read as logits
-            V = W.shape[0]
-            Vp = (V + 255) // 256 * 256
-            if _decoder_pieces_ok(h, W, Vp):
-                # hand-written piece GEMM (gemm_split.hip): each distinct piece of h and of the
-                # padded W staged once, all passes from registers
-                npc = split_gemm.npieces()
-                ctx.pieces = True
-                wf = split_gemm.planes(W, tuple(range(npc)), rpad=Vp)
-                full = C().gemm_split(split_gemm.pieces(h), wf, split_gemm.passes(), None, False, 0)
-            else:
-                full, _ = split_gemm.forward(h, W, rpad=Vp)
-            logits = full[:, :V]
-        elif gemm16.bf16_ok(h, 64, W.shape[1]) and h.is_contiguous():
-            # --precision bf16 on the hand-written kernel: vocabulary padded to a multiple of 768
-            # (zero rows), bf16 logits as before
-            V = W.shape[0]
-            Vp = (V + 767) // 768 * 768
+        V, H = W.shape
+        # the vocabulary padded to a multiple of 768 with zero weight rows (whole 192 / 256 tiles
+        # of the hand-written GEMMs; the padding logits are exactly 0 and never read as logits)
+        Vp = (V + 767) // 768 * 768
+        ctx.f16 = gemm16.ok(h, 64) and h.is_contiguous() and H % 64 == 0
+        ctx.b16 = False
+        if ctx.f16:   # fp32 runs: the fp16x3 GEMM
+            wf, wt, wparts = C().split_weight_f16([_padded_rows(W, Vp)])[0]
+            full = gemm16.mm(h, gemm16.amax(h, h), wf, wparts)
+            ctx.wpieces = (wt, wparts)
+        elif gemm16.bf16_ok(h, 64, H) and h.is_contiguous():
+            # --precision bf16 on the hand-written kernel (bf16 logits)
             ctx.b16 = True
             full = gemm16.mm_bf16(h, _padded_rows(cast_w(W, torch.bfloat16), Vp))
-            logits = full[:, :V]
         else:
-            full = logits = torch.mm(h, cast_w(W, h.dtype).t())
+            full = torch.mm(h, cast_w(W, h.dtype).t())
+        logits = full[:, :V]
         loss_rows = C().softmax_xent_(logits, bias, labels, -1)   # logits <- softmax - onehot
         count = (labels != -1).sum().to(torch.float32)
         loss = loss_rows.sum() / count
-        ctx.save_for_backward(h, W, full, count)
+        ctx.save_for_backward(h, full, count)
         ctx.params = (W, bias)
         return loss
 
@@ -1103,8 +736,8 @@ class _DecoderXentFn(torch.autograd.Function):
     def backward(ctx, g):
         if ctx.f16:
             return _decoder_backward_f16(ctx, g)
-        h, W, dl_full, count = ctx.saved_tensors
-        Wp, bias = ctx.params
+        h, dl_full, count = ctx.saved_tensors
+        W, bias = ctx.params
         dl = dl_full[:, :W.shape[0]]
         # d loss / d logits = (softmax - onehot) * g / count.  The scale stays a
         # device scalar (no host sync) and is applied to the small operands -- the
@@ -1113,53 +746,18 @@ class _DecoderXentFn(torch.autograd.Function):
         scale = (g.float() / count).reshape(1)
         dbias = C().colsum(dl, scale, grad_slot(bias) if bias is not None else None)
         hs = h * scale.to(h.dtype)
-        slot = grad_slot(Wp)
-        if ctx.split and ctx.pieces:
-            # pieces form: dh = dl . W on the piece GEMM with the reduction over the padded
-            # vocabulary cut into split-K slabs (40 output tiles alone would leave 216 CUs idle),
-            # W^T's pieces zero for the padding rows; dW on the split-piece wgrad kernel
-            V, H = dl.shape[1], hs.shape[1]
-            Vp = dl_full.shape[1]
-            npc = split_gemm.npieces()
-            dls = split_gemm.pieces(dl_full)
-            wt = split_gemm.weight_planes_t(Wp, rpad=Vp, order=tuple(range(npc)))
-            dh = C().gemm_split_k(dls, wt, split_gemm.passes(), 0, 0).mul_(scale)
-            out = slot if slot is not None else torch.empty(V, H, device=dl.device)
-            dW = split_gemm.wgrad_pieces(dls, split_gemm.pieces(hs), Vp, H, out)
-            return dh, dW, dbias, None
-        if ctx.split:
-            # logits-gradient planes zero-padded to a multiple of 256 columns: 16-B rows for
-            # the data-gradient GEMM and whole 256-row tiles for the weight-gradient kernel
-            V, H = dl.shape[1], hs.shape[1]
-            Vp = dl_full.shape[1]
-            dls = split_gemm.grad_planes(dl_full)   # zero padding columns: planes [M, n * Vp]
-            dh = split_gemm.dgrad(dls, Wp, rpad=Vp).mul_(scale)
-            n = split_gemm.passes()
-            hsp = split_gemm.planes(hs, split_gemm.ORDER_P[n])
-            if C().wgrad_split_ok(dls, hsp, Vp, H):
-                # the split-piece weight-gradient kernel over the masked rows (1.2 PF/s vs 0.8
-                # for the library product over the stacked plane rows, tools/probe/decoder_probe.py)
-                out = slot if slot is not None else torch.empty(V, H, device=dl.device)
-                dW = split_gemm.wgrad(dls, hsp, Vp, H, out)   # rows past V (padding) are not stored
-                return dh, dW, dbias, None
-            a = dls.view(-1, Vp)[:, :V]
-            b = hsp.view(-1, H)
-            if slot is not None:
-                dW = torch.mm(a.t(), b, out_dtype=torch.float32, out=slot)
-            else:
-                dW = torch.mm(a.t(), b, out_dtype=torch.float32)
-            return dh, dW, dbias, None
-        if getattr(ctx, 'b16', False):
+        slot = grad_slot(W)
+        if ctx.b16:
             # dl over the padded vocabulary (padding columns 0) against the padded W^T in bf16
-            wt = C().weight_bf16_t([_padded_rows(Wp, dl_full.shape[1])])[0]
+            wt = C().weight_bf16_t([_padded_rows(W, dl_full.shape[1])])[0]
             dh = gemm16.mm_bf16(dl_full, wt).mul_(scale.to(dl.dtype))
         else:
-            dh = torch.mm(dl, cast_w(Wp, dl.dtype)).mul_(scale.to(dl.dtype))
+            dh = torch.mm(dl, cast_w(W, dl.dtype)).mul_(scale.to(dl.dtype))
         side = side_begin(dl.device) if slot is not None else None
         with torch.cuda.stream(side) if side is not None else _nullctx():
-            if getattr(ctx, 'b16', False) and C().wgrad_bf16_ok(dl_full, hs):
+            if ctx.b16 and C().wgrad_bf16_ok(dl_full, hs):
                 # over the padded vocabulary (whole 128-row tiles); rows past V are not stored
-                out = slot if slot is not None else torch.empty(Wp.shape[0], hs.shape[1], device=dl.device)
+                out = slot if slot is not None else torch.empty(W.shape[0], hs.shape[1], device=dl.device)
                 dW = C().wgrad_bf16(dl_full, hs, out)
             else:
                 dW = _wgrad(dl, hs, slot)
@@ -1184,9 +782,10 @@ def _padded_rows(W, rows):
 
 
 def _decoder_backward_f16(ctx, g):
-    h, W, dl_full, count, wt, wparts = ctx.saved_tensors
+    h, dl_full, count = ctx.saved_tensors
     Wt, bias = ctx.params
-    V = W.shape[0]
+    wt, wparts = ctx.wpieces
+    V = Wt.shape[0]
     dl = dl_full[:, :V]
     scale = (g.float() / count).reshape(1)
     dbias = C().colsum(dl, scale, grad_slot(bias) if bias is not None else None)
@@ -1198,17 +797,6 @@ def _decoder_backward_f16(ctx, g):
     slot = grad_slot(Wt)
     dW = gemm16.wgrad(dl_full, one, hs, gemm16.amax(hs, hs), V, h.shape[1], slot)
     return dh, dW, dbias, None
-
-
-def _decoder_pieces_ok(h, W, Vp):
-    """The MLM decoder on the hand-written piece GEMMs (bf16x6 default, as the linears:
-    split_gemm.nt_ok): forward [M, Vp] over K = H, data gradient [M, H] over K = Vp in split-K
-    slabs, weight gradient on wgrad_split.hip."""
-    H = W.shape[1]
-    if not split_gemm.nt_ok(H, Vp) or not _DECODER_PIECES:
-        return False
-    npc = split_gemm.npieces()
-    return Vp * npc * H * 2 < (1 << 31) and Vp % 256 == 0 and H % 192 == 0
 
 
 def decoder_xent(h, W, bias, labels):

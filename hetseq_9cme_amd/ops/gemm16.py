@@ -3,7 +3,7 @@
 Every fp32 operand x is used as 2^-E (h0 + h1) with h0 = fp16(2^E x), h1 = fp16(2^E x - h0):
 22 significant bits per element; the product a.b is a0 b0 + a0 b1 + a1 b0 (the dropped a1 b1
 is 2^-22 relative) -- three fp16 MFMA passes where the bf16 emulation needs six
-(``--fp32-gemm bf16x6``, ops/split_gemm.py).  E comes from the operand's max |x|, so every
+(the round-3 ``bf16x6`` mode).  E comes from the operand's max |x|, so every
 tensor handed to these GEMMs travels with **max |x| partials**: a small fp32 vector whose max is
 max |x| (its producer writes it -- this module's GELU epilogues, LayerNorm, attention -- or
 ``amax`` computes it in one read pass).  The GEMMs read activations and gradients AS fp32 and

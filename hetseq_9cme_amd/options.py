@@ -55,14 +55,13 @@ def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialD
                              'fp32 class on the fp16 matrix cores; --fp32-gemm native gives plain f32 MFMA, '
                              'bitwise the reference\'s fp32 FMA chain) or bf16 (bf16 MFMA, fp32 master weights '
                              'and optimizer state)')
-    parser.add_argument('--fp32-gemm', default='fp16x3', choices=['native', 'bf16x3', 'bf16x6', 'fp16x3'],
-                        help='how fp32 (--precision fp32) linear-layer GEMMs run on the GPU: fp16x3 (default: '
-                             'operands scaled by a power of two from their max |x| and split into two fp16 '
-                             'pieces inside the GEMM kernels -- 22 bits each, three passes; measured GEMM error '
-                             '0.6-0.7x native fp32\'s: ops/gemm16.py), bf16x6 (three bf16 pieces, six passes, '
-                             'fp32-exact class at twice the matrix work), bf16x3 (two bf16 pieces, three passes, '
-                             '~2^-17 per product: near-fp32) or native f32 MFMA (157 TF/s peak); see '
-                             'ops/split_gemm.py')
+    parser.add_argument('--fp32-gemm', default='fp16x3', choices=['fp16x3', 'native'],
+                        help='how fp32 (--precision fp32) runs use the matrix cores: fp16x3 (default: every '
+                             'linear-layer GEMM on the hand-written kernels with operands scaled by a power of two '
+                             'from their max |x| and split into two fp16 pieces -- 22 bits each, three exact piece '
+                             'products; measured GEMM error 0.6-0.7x native fp32\'s; attention products as six '
+                             'bf16 piece passes from 4096 token rows) or native (f32 MFMA, 157 TF/s peak, '
+                             'through the libraries: the numerics oracle); see ops/fp32_mode.py')
     parser.add_argument('--graph-train-step', action='store_true',
                         help='single GPU, one micro-batch per update: capture each input shape\'s whole '
                              'update (forward, backward, clip, optimizer) in a HIP graph after two eager '
@@ -83,9 +82,9 @@ def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialD
                         help='where --gemm-tuning online writes its table (device ordinal appended)')
     parser.add_argument('--overlap-wgrad', dest='overlap_wgrad', action='store_const', const='on', default='auto',
                         help='run weight-gradient GEMMs / bias column sums on a side HIP stream, concurrent '
-                             'with the data-gradient GEMMs, on every backward path (default: the piece-GEMM '
-                             'paths only -- BERT-base phase 1 53.9 -> 52.9 ms/step, while the host-bound '
-                             'library paths lose; profiles/r3_overlap_wgrad_ab.md)')
+                             'with the data-gradient GEMMs, on every backward path (default: the hand-written '
+                             'fp16x3 GEMM paths only -- the library paths (native fp32, bf16) lose: '
+                             'profiles/r3_overlap_wgrad_ab.md)')
     parser.add_argument('--no-overlap-wgrad', dest='overlap_wgrad', action='store_const', const='off',
                         help='weight gradients on the compute stream on every path')
     parser.add_argument('--debug-kernels', action='store_true',

@@ -36,16 +36,13 @@ def test_two_rank_gpu_equivalence(dev, tmp_path):
             # (both ranks on this box's one GPU; kernel waits bounded by the 60 s timeout)
             'twox': ['--distributed-world-size', '2', '--distributed-backend', 'gloo', '--allreduce-impl', 'xgmi',
                      '--distributed-timeout', '60'],
-            # the default fp32 path (bf16x6 split GEMMs) forced onto these small GEMMs
-            'one6': ['--update-freq', '2', '--distributed-world-size', '1', '--fp32-gemm', 'bf16x6'],
-            'two6': ['--distributed-world-size', '2', '--distributed-backend', 'gloo', '--fp32-gemm', 'bf16x6']}
+            # the other fp32 mode (f32 MFMA through the libraries; the runs above take the default fp16x3)
+            'oneN': ['--update-freq', '2', '--distributed-world-size', '1', '--fp32-gemm', 'native'],
+            'twoN': ['--distributed-world-size', '2', '--distributed-backend', 'gloo', '--fp32-gemm', 'native']}
     ck = {}
     for name, extra in runs.items():
         save = str(tmp_path / name)
         env = dict(os.environ, PYTHONPATH=ROOT)
-        if name.endswith('6'):
-            env['HETSEQ_SPLIT_MIN_ROWS_X6'] = '0'
-            env['HX_PIECE_MIN_ROWS'] = '0'
         r = subprocess.run([sys.executable, '-m', 'hetseq_9cme_amd.train'] + common + extra + ['--save-dir', save],
                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, timeout=400)
         assert r.returncode == 0, r.stdout[-3000:]
@@ -57,8 +54,8 @@ def test_two_rank_gpu_equivalence(dev, tmp_path):
         torch.testing.assert_close(ck['twox']['model'][k], v, rtol=1e-4, atol=1e-6, msg=k)
     for k, v in ck['one4']['model'].items():
         torch.testing.assert_close(ck['two2']['model'][k], v, rtol=1e-4, atol=1e-6, msg=k)
-    for k, v in ck['one6']['model'].items():
-        torch.testing.assert_close(ck['two6']['model'][k], v, rtol=1e-4, atol=1e-6, msg=k)
+    for k, v in ck['oneN']['model'].items():
+        torch.testing.assert_close(ck['twoN']['model'][k], v, rtol=1e-4, atol=1e-6, msg=k)
     assert ck['two2']['optimizer_history'][-1]['num_updates'] == 2
 
 
@@ -169,7 +166,7 @@ def test_rccl_one_rank_reducer_matches_local(dev, tmp_path):
     ck = {}
     for name, extra in runs.items():
         save = str(tmp_path / name)
-        env = dict(os.environ, PYTHONPATH=ROOT, HETSEQ_SPLIT_MIN_ROWS_X6='0', HX_PIECE_MIN_ROWS='0')
+        env = dict(os.environ, PYTHONPATH=ROOT)
         r = subprocess.run([sys.executable, '-m', 'hetseq_9cme_amd.train'] + common + extra + ['--save-dir', save],
                            stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, timeout=400)
         assert r.returncode == 0, r.stdout[-3000:]

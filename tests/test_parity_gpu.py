@@ -1,9 +1,9 @@
-"""Training-level fp32 parity of the bf16 piece-emulation GEMM modes.
+"""Training-level fp32 parity of the default fp32 GEMM mode.
 
-BERT-tiny, 60 Adam updates, dropout on, learnable synthetic corpus: ``bf16x6`` (the
-default fp32 path) and ``bf16x3`` must track ``--fp32-gemm native`` (fp32 MFMA)
-per update and in the final weights.  The long BERT-base horizon (300 updates) is
-``tools/parity_run.py`` -> ``profiles/r3_parity_bert_base_300.md``.
+BERT-tiny, 60 Adam updates, dropout on, learnable synthetic corpus: ``fp16x3`` (the default fp32
+path: scaled fp16 pieces, ops/gemm16.py) must track ``--fp32-gemm native`` (fp32 MFMA) per update
+and in the final weights.  The long BERT-base horizon (300 updates) is ``tools/parity_run.py`` ->
+``profiles/r4_parity_bert_base_300.md``.
 """
 import json
 import os
@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.mark.gpu
-def test_split_modes_track_native_60_updates(tmp_path):
+def test_fp16x3_tracks_native_60_updates(tmp_path):
     out = tmp_path / 'parity'
     r = subprocess.run([sys.executable, '-u', os.path.join(ROOT, 'tools', 'parity_run.py'), '--model', 'tiny',
                         '--updates', '60', '--batch', '32', '--lr', '5e-4', '--warmup-updates', '10',
@@ -27,7 +27,7 @@ def test_split_modes_track_native_60_updates(tmp_path):
     curve = res['loss_curve']['native']
     assert curve[-1] < curve[0] - 0.5 * abs(curve[0] - curve[-1]) or curve[-1] < 0.9 * curve[0], \
         'corpus should be learnable: {} -> {}'.format(curve[0], curve[-1])
-    for mode, tol in (('bf16x6', 1e-4), ('bf16x3', 1e-3)):
+    for mode, tol in (('fp16x3', 1e-4),):
         s = res['modes'][mode]
         assert s['finite']
         assert s['loss_reldiff_max'] < tol, (mode, s)

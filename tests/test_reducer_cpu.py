@@ -333,25 +333,23 @@ def test_xgmi_eligibility_by_bus_id():
 
 def test_plans_leave_reserved_cus_to_comm():
     """--comm-cus (csrc/kernels/cu_reserve.hip): with R CUs held by a concurrent all-reduce the
-    one-round plans are sized for the remaining CUs -- the weight-gradient split counts fill
-    n_cu - R slots, and the N = 768 piece GEMM (256 x 192 tiles: exactly one round of 256) moves to
-    the 256 x 256 tile (192 tiles: still one round).  Host-side plan functions only (no GPU:
-    the CU count falls back to the MI355X's 256)."""
+    one-round plans are sized for the remaining CUs -- the fp16x3 weight-gradient token splits
+    fill n_cu - R slots.  Host-side plan functions only (no GPU: the CU count falls back to the
+    MI355X's 256)."""
     from hetseq_9cme_amd.ops._ext import C
     c = C()
     n = c.num_cus()
+    shapes = ((2304, 768, 16384), (3072, 768, 16384), (768, 3072, 16384), (768, 768, 16384))
     try:
         c.set_reserved_cus(0)
         assert c.cu_slots() == n
-        base = {s: c.wgrad_split_plan(*s, 6) for s in ((2304, 768, 16384), (3072, 768, 16384), (768, 3072, 16384))}
-        assert c.gemm_split_plan(16384, 768, 3072, 6, 2) == 0
-        c.set_reserved_cus(16)
-        assert c.cu_slots() == n - 16
-        for (M, N, T), (cfg, ns) in base.items():
-            cfg2, ns2 = c.wgrad_split_plan(M, N, T, 6)
-            tiles = (M // 256) * (N // (256 if cfg2 == 2 else 128))
-            assert tiles * ns2 <= n - 16 < tiles * (ns2 + 1), (M, N, cfg2, ns2)
-        assert c.gemm_split_plan(16384, 768, 3072, 6, 2) == 1
-        assert c.gemm_split_plan(16384, 3072, 768, 6, 2) == 1   # wide outputs: unchanged
+        for r in (0, 16):
+            c.set_reserved_cus(r)
+            assert c.cu_slots() == n - r
+            for (M, N, T) in shapes:
+                cfg, ns = c.wgrad_f16_plan(M, N, T)
+                tiles = (M // 256) * (N // 256) if cfg == 1 else (M // 128) * (N // 128)
+                slots = (1 if cfg == 1 else 2) * (n - r)
+                assert tiles * ns <= max(slots, tiles) and (ns == 1 or slots < tiles * (ns + 1)), (M, N, r, cfg, ns)
     finally:
         c.set_reserved_cus(0)

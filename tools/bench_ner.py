@@ -41,7 +41,7 @@ def main():
     ap.add_argument('--backend', default='nccl', choices=['nccl', 'gloo'])
     ap.add_argument('--same-device', action='store_true', help='rehearsal: every rank on GPU 0')
     ap.add_argument('--model', default='base', choices=['base', 'tiny'])
-    ap.add_argument('--fp32-gemm', default=None, choices=['native', 'bf16x3', 'bf16x6', 'fp16x3'],
+    ap.add_argument('--fp32-gemm', default=None, choices=['fp16x3', 'native'],
                     help='fp32 GEMM mode (default: the framework default)')
     ap.add_argument('--force-reducer', action='store_true',
                     help='one GPU: run the gradient reducer on a one-rank RCCL group (buckets, used flags in the '

@@ -33,16 +33,9 @@ def timeit(fn, iters=30, warmup=5):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--tokens', type=int, default=16384)
-    ap.add_argument('--split', type=int, default=0, help='time the split-piece kernel (3 or 6 passes) vs stacked')
-    ap.add_argument('--variants', action='store_true',
-                    help='with --split: time the pipeline variants (HX_WGRAD_SPLIT_VAR) at the planned split')
     ap.add_argument('--sweep', action='store_true',
                     help='time every (tile config, token split) of the hand-written kernel via HX_WGRAD_CFG')
     a = ap.parse_args()
-    if a.split and a.variants:
-        return split_variants(a.tokens, a.split)
-    if a.split:
-        return split_bench(a.tokens, a.split)
     if a.sweep:
         return sweep(a.tokens)
     T = a.tokens
@@ -112,69 +105,6 @@ def sweep(T):
             n_out, n_in, T, base, best[1], best[0], fl / best[0] / 1e6), flush=True)
 
 
-def split_bench(T, passes):
-    """--fp32-gemm bf16x3/x6 weight gradients: split-piece kernel (all token splits) vs the
-    stacked-rows kernel, checked against an fp64 product of the fp32 operands."""
-    from hetseq_9cme_amd import ops
-    from hetseq_9cme_amd.ops import split_gemm as sg
-    from hetseq_9cme_amd.ops._ext import C
-    ops.set_fp32_gemm('bf16x{}'.format(passes))
-    for (n_out, n_in) in [(3072, 768), (768, 3072), (2304, 768), (768, 768)]:
-        dy = torch.randn(T, n_out, device='cuda')
-        x = torch.randn(T, n_in, device='cuda')
-        dys, xs = sg.grad_planes(dy), sg.planes(x, sg.ORDER_P[passes])
-        slot = torch.empty(n_out, n_in, device='cuda')
-        ref = dy.double().t() @ x.double()
-        scale = dy.double().abs().t() @ x.double().abs()
-        fl = 2.0 * T * n_out * n_in * passes
-        stacked = timeit(lambda: C().wgrad_bf16(dys.view(-1, n_out), xs.view(-1, n_in), slot))
-        print('[{}x{} T={} x{}] stacked {:8.1f} us {:7.1f} TF/s'.format(n_out, n_in, T, passes, stacked,
-                                                                       fl / stacked / 1e6), flush=True)
-        po, px = sg._piece_offsets(sg.ORDER_Q[passes], n_out), sg._piece_offsets(sg.ORDER_P[passes], n_in)
-        cfgs = [int(c) for c in os.environ.get('HX_SWEEP_CFGS', '0,1,2').split(',')]
-        runs = [(None, 0)] + [(cfg, ns) for cfg in cfgs for ns in (1, 2, 3, 4, 6, 7, 8, 9, 12, 14, 16)
-                              if not (n_out % (256 if cfg else 128) or (cfg >= 2 and passes != 6)
-                                      or (cfg == 2 and n_in % 256))]
-        for cfg, ns in runs:
-            if ns:
-                os.environ['HX_WGRAD_SPLIT_CFG'] = '{}:{}'.format(cfg, ns)
-            else:
-                os.environ.pop('HX_WGRAD_SPLIT_CFG', None)
-            us = timeit(lambda: C().wgrad_split(dys, po, xs, px, passes, n_out, n_in, slot))
-            err = ((slot.double() - ref).abs() / scale).max().item()
-            print('[{}x{} T={} x{}] split cfg {} nsplit {} {:8.1f} us {:7.1f} TF/s err {:.2e}'.format(
-                n_out, n_in, T, passes, 'plan' if cfg is None else cfg, ns or 'plan', us, fl / us / 1e6, err),
-                flush=True)
-        os.environ.pop('HX_WGRAD_SPLIT_CFG', None)
-
-
-def split_variants(T, passes, rounds=3):
-    """Pipeline variants of the split-piece kernel (register stages ahead x work order),
-    interleaved over several rounds in one process (median per round, min over rounds)."""
-    from hetseq_9cme_amd import ops
-    from hetseq_9cme_amd.ops import split_gemm as sg
-    from hetseq_9cme_amd.ops._ext import C
-    ops.set_fp32_gemm('bf16x{}'.format(passes))
-    variants = ['2,0', '2,1', '1,0', '1,1', '0,0', '0,1']
-    for (n_out, n_in) in [(3072, 768), (768, 3072), (2304, 768), (768, 768)]:
-        dy = torch.randn(T, n_out, device='cuda')
-        x = torch.randn(T, n_in, device='cuda')
-        dys, xs = sg.grad_planes(dy), sg.planes(x, sg.ORDER_P[passes])
-        slot = torch.empty(n_out, n_in, device='cuda')
-        ref = dy.double().t() @ x.double()
-        scale = dy.double().abs().t() @ x.double().abs()
-        fl = 2.0 * T * n_out * n_in * passes
-        po, px = sg._piece_offsets(sg.ORDER_Q[passes], n_out), sg._piece_offsets(sg.ORDER_P[passes], n_in)
-        best = {v: float('inf') for v in variants}
-        for _ in range(rounds):
-            for v in variants:
-                os.environ['HX_WGRAD_SPLIT_VAR'] = v
-                best[v] = min(best[v], timeit(lambda: C().wgrad_split(dys, po, xs, px, passes, n_out, n_in, slot)))
-                err = ((slot.double() - ref).abs() / scale).max().item()
-                assert err < 1e-5, (v, err)
-        os.environ.pop('HX_WGRAD_SPLIT_VAR', None)
-        print('[{}x{} T={} x{}] '.format(n_out, n_in, T, passes) + '  '.join(
-            'var {} {:7.1f} us {:6.0f} TF/s'.format(v, best[v], fl / best[v] / 1e6) for v in variants), flush=True)
 
 
 if __name__ == '__main__':

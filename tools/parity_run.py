@@ -3,8 +3,8 @@
 Trains BERT (default: base, phase-1 shape, dropout on) for ``--updates`` Adam updates
 from the SAME seed on the SAME synthetic shards (a learnable bigram corpus, so the
 loss actually falls) once per ``--modes`` entry, each in
-its own child process (``--fp32-gemm native`` = fp32 MFMA, ``bf16x6`` / ``bf16x3`` =
-bf16 piece emulation), records the per-update loss and grad norm, and compares every
+its own child process (``--fp32-gemm native`` = fp32 MFMA, ``fp16x3`` = fp16-piece
+emulation), records the per-update loss and grad norm, and compares every
 mode against ``native``:
 
 * per-update |loss difference| (max / mean, absolute and relative),
@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--updates', type=int, default=300)
-    ap.add_argument('--modes', default='native,native#2,bf16x6,bf16x3',
+    ap.add_argument('--modes', default='native,native#2,fp16x3',
                     help='"native#2" = a second native run (the run-to-run noise floor)')
     ap.add_argument('--model', default='base', choices=['base', 'tiny'])
     ap.add_argument('--batch', type=int, default=128)

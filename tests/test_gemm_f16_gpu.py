@@ -156,10 +156,12 @@ def test_f16_scale_extremes(dev):
     assert C().gemm_f16(z, C().amax_rows(z), wf, parts).abs().max().item() == 0.0
 
 
+@pytest.mark.parametrize('pf', ['0', '1'])
 @pytest.mark.parametrize('M,N,K', [(16384, 768, 768), (16384, 3072, 768), (4096, 768, 3072), (300, 2304, 768)])
-def test_gemm_bf16_mode(dev, M, N, K):
+def test_gemm_bf16_mode(dev, monkeypatch, M, N, K, pf):
     """--precision bf16 on the same kernel (one bf16 pass, bf16 or fp32 output, bias / beta): against
     the fp64 product of the same bf16 operands (only fp32 accumulation and the output rounding)."""
+    monkeypatch.setenv('HX_GEMM_F16_PF', pf)
     g = torch.Generator(device=dev).manual_seed(M + K)
     a = torch.randn(M, K, device=dev, generator=g).bfloat16()
     W = torch.randn(N, K, device=dev, generator=g) * 0.02
@@ -184,11 +186,14 @@ def test_gemm_bf16_mode(dev, M, N, K):
     assert ((out.double() - ref2).abs() / den2).max().item() < 8e-3
 
 
+@pytest.mark.parametrize('pf', ['0', '1'])
 @pytest.mark.parametrize('cfg', ['0', '1', '2', '3', '4'])
-def test_gemm_f16_every_tile(dev, monkeypatch, cfg):
-    """Every tile configuration of gemm_f16_k (HX_GEMM_F16_CFG forces it): forward with bias and the
-    beta = 1 data gradient, rows not a multiple of the tile."""
+def test_gemm_f16_every_tile(dev, monkeypatch, cfg, pf):
+    """Every tile configuration of gemm_f16_k (HX_GEMM_F16_CFG forces it) in both main-loop forms
+    (HX_GEMM_F16_PF): forward with bias and the beta = 1 data gradient, rows not a multiple of the
+    tile."""
     monkeypatch.setenv('HX_GEMM_F16_CFG', cfg)
+    monkeypatch.setenv('HX_GEMM_F16_PF', pf)
     g = torch.Generator(device=dev).manual_seed(int(cfg))
     M, N, K = 4096 + 37, 768, 768
     a = torch.randn(M, K, device=dev, generator=g)

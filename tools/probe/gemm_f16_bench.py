@@ -41,10 +41,13 @@ def sweep(C, dev, cfgs):
         xb, Wb = x.bfloat16(), W.bfloat16()
         fl = 2.0 * T * N * K
         for c in cfgs:
-            if c == 'plan':
+            # 'cfg' or 'cfg/pf' (pf: HX_GEMM_F16_PF main-loop form)
+            cfg, _, pf = c.partition('/')
+            os.environ['HX_GEMM_F16_PF'] = pf or '0'
+            if cfg == 'plan':
                 os.environ.pop('HX_GEMM_F16_CFG', None)
             else:
-                os.environ['HX_GEMM_F16_CFG'] = c
+                os.environ['HX_GEMM_F16_CFG'] = cfg
             try:
                 if name == 'ffn_up':
                     f = timed(lambda: C().gemm_f16_gelu(x, xp, wf, wp, b, 1))
@@ -61,6 +64,7 @@ def sweep(C, dev, cfgs):
             print('{:10s} cfg {:4s} fwd {:7.1f} us ({:4.2f} PF/s)  dgrad {:7.1f} us ({:4.2f})  bf16 fwd {:6.1f} us '
                   '({:4.2f})'.format(name, c, f, 3 * fl / f / 1e9, dg, 3 * fl / dg / 1e9, bf, fl / bf / 1e9), flush=True)
     os.environ.pop('HX_GEMM_F16_CFG', None)
+    os.environ.pop('HX_GEMM_F16_PF', None)
 
 
 def main():

@@ -547,34 +547,33 @@ inline void check_vec(const OptT& v, int64_t n, const char* what) {
   TORCH_CHECK(v->numel() == n && v->is_contiguous() && aligned16(v->data_ptr()), what, ": fp32 [N], 16-B aligned");
 }
 
-// C (+)= a . b^T (+ bias); ks split-K slabs (0 = plan: deep reductions with few tiles), summed here
+// C (+)= a . b^T (+ bias); ks split-K slabs (0 = plan: deep reductions with few output tiles),
+// combined (with the beta / bias epilogue) by one pass over the slabs
 Tensor gemm_f16(Tensor a, Tensor a_amax, Tensor b, Tensor b_amax, OptT out_, bool beta, OptT bias, int64_t ks) {
   HxGemmF16 p = f16_args(a, a_amax, b, b_amax, "gemm_f16");
   check_vec(bias, p.N, "gemm_f16 bias");
   const int cfg = hx_gemm_f16_plan(p.M, p.N, p.K);
   TORCH_CHECK(cfg >= 0, "gemm_f16: no tile for N = ", p.N);
   TORCH_CHECK(!beta || has(out_), "gemm_f16: beta needs an output to accumulate into");
-  if (ks <= 0) ks = (beta || has(bias)) ? 1 : hx_gemm_f16_ks(p.M, p.N, p.K, cfg);
+  if (ks <= 0) ks = hx_gemm_f16_ks(p.M, p.N, p.K, cfg);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
   auto f32 = a.options();
+  Tensor out = has(out_) ? *out_ : torch::empty({p.M, p.N}, f32);
+  TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.dim() == 2 && out.size(0) == p.M && out.size(1) == p.N &&
+                  out.stride(1) == 1 && out.stride(0) % 4 == 0 && aligned16(out.data_ptr()),
+              "gemm_f16: out must be fp32 [M, N] with unit column stride and 16-B rows");
   if (ks > 1) {
-    TORCH_CHECK(!beta && !has(bias), "gemm_f16: split-K without beta / bias");
     Tensor part = torch::empty({ks, p.M, p.N}, f32);
     p.C = part.data_ptr<float>();
     p.ldc = p.N;
     p.ks = (int)ks;
     p.c_zs = (int64_t)p.M * p.N;
     TORCH_CHECK(hx_gemm_f16(p, cfg, cur_stream(a)) == 0, "gemm_f16: split-K launch failed (ks must divide K / 16)");
-    if (has(out_)) {
-      at::sum_out(*out_, part, {0});
-      return *out_;
-    }
-    return part.sum(0);
+    hx_gemm_f16_slab_combine(part.data_ptr<float>(), out.data_ptr<float>(), out.stride(0), p.M, p.N, (int)ks,
+                             beta ? 1 : 0, ptr_or_null<float>(bias), cur_stream(a));
+    dbg_finite(out, "gemm_f16");
+    return out;
   }
-  Tensor out = has(out_) ? *out_ : torch::empty({p.M, p.N}, f32);
-  TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.dim() == 2 && out.size(0) == p.M && out.size(1) == p.N &&
-                  out.stride(1) == 1 && out.stride(0) % 4 == 0 && aligned16(out.data_ptr()),
-              "gemm_f16: out must be fp32 [M, N] with unit column stride and 16-B rows");
   p.C = out.data_ptr<float>();
   p.ldc = out.stride(0);
   p.beta = beta ? 1 : 0;
@@ -855,7 +854,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("amax_rows", &amax_rows);
   m.def("split_weight_f16", &split_weight_f16);
   m.def("gemm_f16", &gemm_f16, py::arg("a"), py::arg("a_amax"), py::arg("b"), py::arg("b_amax"),
-        py::arg("out") = py::none(), py::arg("beta") = false, py::arg("bias") = py::none(), py::arg("ks") = 1);
+        py::arg("out") = py::none(), py::arg("beta") = false, py::arg("bias") = py::none(), py::arg("ks") = 0);
   m.def("gemm_f16_gelu", &gemm_f16_gelu, py::arg("a"), py::arg("a_amax"), py::arg("b"), py::arg("b_amax"),
         py::arg("bias"), py::arg("dmode") = 1);
   m.def("gemm_f16_dgelu", &gemm_f16_dgelu, py::arg("a"), py::arg("a_amax"), py::arg("b"), py::arg("b_amax"),

@@ -135,6 +135,9 @@ int hx_gemm_f16_plan(int M, int N, int K);
 int hx_gemm_f16_tiles(int M, int N, int cfg);
 int hx_gemm_f16_colpart_rows(int M, int cfg);
 int hx_gemm_f16_ks(int M, int N, int K, int cfg);
+// split-K combine: C[M][ldc] (+= if beta) = sum of ks [M][N] slabs at ws (+ bias [N]); N % 4 == 0
+void hx_gemm_f16_slab_combine(const float* ws, float* C, int64_t ldc, int M, int N, int ks, int beta,
+                              const float* bias, hipStream_t s);
 int hx_gemm_f16(const HxGemmF16& p, int cfg, hipStream_t s);
 // dW[M][N] = dY[T][M]^T X[T][N] (fp32 operands, row strides ldy / ldx); rows >= mvalid not stored;
 // ws: nsplit * M * N floats when nsplit > 1

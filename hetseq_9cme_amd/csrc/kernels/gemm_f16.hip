@@ -79,7 +79,7 @@ struct F16Args {
 // AT 0: fp32 A split into two scaled fp16 pieces, B = fp16 P2 pieces, three passes (fp16x3);
 // AT 1: --precision bf16: A and B bf16 [rows][K] (32-deep k steps: again 64 B per row), one pass;
 //       OB: the output C in bf16 (EPI 0 / 3 only)
-template <int BM, int BN, int WM, int WN, int EPI, int OCC, int AT = 0, int OB = 0, int PF = 0>
+template <int BM, int BN, int WM, int WN, int EPI, int OCC, int AT = 0, int OB = 0>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F16Args g) {
   static_assert(AT == 0 || EPI == 0 || EPI == 3, "bf16 operands: plain / beta epilogues");
   static_assert(OB == 0 || AT == 1, "bf16 output with bf16 operands");
@@ -176,66 +176,30 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[a][b] = f32x16{0};
 
-  if constexpr (PF == 0) {
-    // one stage per iteration: fragment reads at the top, the next-next stage's DMA pieces between
-    // the MFMA passes, then the wait for the next stage and the barrier
-    int cur = 0;
-    for (int it = 0; it < nit; ++it) {
-      const int nxt2 = cur == 0 ? 2 : cur - 1;
-      const char* st = lds + cur * STAGE;
-      const int dit = it + 2 < nit ? it + 2 : -1;
-      if constexpr (AT == 1) {
-        // two 16-deep bf16 k steps per stage, one MFMA pass each; the next-next stage's DMA pieces
-        // between them
-  #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          bf16x8v fa[MB], fb[NB];
-  #pragma unroll
-          for (int a = 0; a < MB; ++a)
-            fa[a] = *reinterpret_cast<const bf16x8v*>(st + img_off(wm * WM + 32 * a + l32, 2 * ks + h));
-  #pragma unroll
-          for (int b = 0; b < NB; ++b)
-            fb[b] = *reinterpret_cast<const bf16x8v*>(st + A_BYTES + img_off(wn * WN + 32 * b + l32, 2 * ks + h));
-  #pragma unroll
-          for (int a = 0; a < MB; ++a)
-  #pragma unroll
-            for (int b = 0; b < NB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
-          if (dit >= 0) {
-  #pragma unroll
-            for (int j = ks; j < JHI; j += 2) {
-              if (j < JLO || j < cnt) {
-                __builtin_amdgcn_sched_barrier(0);
-                dma_one(dit, nxt2, j);
-                __builtin_amdgcn_sched_barrier(0);
-              }
-            }
-          }
-        }
-      } else {
-      f16x8 a0[MB], a1[MB], b0[NB], b1[NB];
-  #pragma unroll
-      for (int b = 0; b < NB; ++b) {
-        b0[b] = *reinterpret_cast<const f16x8*>(st + offb[b][0]);
-        b1[b] = *reinterpret_cast<const f16x8*>(st + offb[b][1]);
-      }
-  #pragma unroll
-      for (int a = 0; a < MB; ++a) {
-        const f32x4 lo = *reinterpret_cast<const f32x4*>(st + offa[a][0]);
-        const f32x4 hi = *reinterpret_cast<const f32x4*>(st + offa[a][1]);
-        const f32x8 y = f32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]} * sa;
-        split2(y, a0[a], a1[a]);
-      }
-      // pass q, then this wave's DMA pieces j = q, q + 3, ... of stage it + 2
-  #pragma unroll
-      for (int q = 0; q < 3; ++q) {
-  #pragma unroll
+  int cur = 0;
+  for (int it = 0; it < nit; ++it) {
+    const int nxt2 = cur == 0 ? 2 : cur - 1;
+    const char* st = lds + cur * STAGE;
+    const int dit = it + 2 < nit ? it + 2 : -1;
+    if constexpr (AT == 1) {
+      // two 16-deep bf16 k steps per stage, one MFMA pass each; the next-next stage's DMA pieces
+      // between them
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8v fa[MB], fb[NB];
+#pragma unroll
         for (int a = 0; a < MB; ++a)
-  #pragma unroll
-          for (int b = 0; b < NB; ++b)
-            acc[a][b] = mfma16(q == 2 ? a1[a] : a0[a], q == 1 ? b1[b] : b0[b], acc[a][b]);
+          fa[a] = *reinterpret_cast<const bf16x8v*>(st + img_off(wm * WM + 32 * a + l32, 2 * ks + h));
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          fb[b] = *reinterpret_cast<const bf16x8v*>(st + A_BYTES + img_off(wn * WN + 32 * b + l32, 2 * ks + h));
+#pragma unroll
+        for (int a = 0; a < MB; ++a)
+#pragma unroll
+          for (int b = 0; b < NB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
         if (dit >= 0) {
-  #pragma unroll
-          for (int j = q; j < JHI; j += 3) {
+#pragma unroll
+          for (int j = ks; j < JHI; j += 2) {
             if (j < JLO || j < cnt) {
               __builtin_amdgcn_sched_barrier(0);
               dma_one(dit, nxt2, j);
@@ -244,137 +208,44 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
           }
         }
       }
-      }
-      if (it + 2 < nit) wait_stage();
-      else dma_wait<0>();
-      __syncthreads();
-      cur = cur == 2 ? 0 : cur + 1;
-    }
-  } else {
-    // Main loop, one stage per step, its fragments already in registers (read during the previous
-    // step): pass 0 with the next-next stage's DMA pieces between its MFMAs -> wait for the next
-    // stage + barrier (pass 0's MFMAs cover it) -> the next stage's fragment reads, in flight
-    // under the remaining passes.  Two register sets alternate (steps unrolled by two: no copies).
-    //   RAW: stage it + 1 is read after this wave's vmcnt wait for it and the barrier every
-    //        issuing wave passed after its own wait.
-    //   WAR: stage it + 2's DMA overwrites stage it - 1's buffer, whose fragments every wave
-    //        consumed (waited) in pass 0 of step it - 1, before that step's barrier.
-    auto dma_piece = [&](int dit, int buf, int j) {
-      if (dit >= 0 && j < JHI && (j < JLO || j < cnt)) {
-        __builtin_amdgcn_sched_barrier(0);
-        dma_one(dit, buf, j);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    };
-    auto next_stage_ready = [&](int it) {   // after stage it + 2's DMA issue
-      if (it + 2 < nit) wait_stage();
-      else dma_wait<0>();
-      __syncthreads();
-    };
-    if constexpr (AT == 1) {
-      // bf16 operands: two 16-deep k steps per 32-deep stage
-      struct Frag {
-        bf16x8v a[2][MB], b[2][NB];
-      };
-      auto read = [&](Frag& f, const char* st) {
-  #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-  #pragma unroll
-          for (int a = 0; a < MB; ++a)
-            f.a[ks][a] = *reinterpret_cast<const bf16x8v*>(st + img_off(wm * WM + 32 * a + l32, 2 * ks + h));
-  #pragma unroll
-          for (int b = 0; b < NB; ++b)
-            f.b[ks][b] = *reinterpret_cast<const bf16x8v*>(st + A_BYTES + img_off(wn * WN + 32 * b + l32, 2 * ks + h));
-        }
-      };
-      auto step = [&](int it, int cur, const Frag& c, Frag& n) {
-        const int nxt = cur == 2 ? 0 : cur + 1, nxt2 = nxt == 2 ? 0 : nxt + 1;
-        const int dit = it + 2 < nit ? it + 2 : -1;
-  #pragma unroll
-        for (int b = 0; b < NB; ++b) {
-  #pragma unroll
-          for (int a = 0; a < MB; ++a)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c.a[0][a], c.b[0][b], acc[a][b], 0, 0, 0);
-          dma_piece(dit, nxt2, b);
-        }
-  #pragma unroll
-        for (int j = NB; j < JHI; ++j) dma_piece(dit, nxt2, j);
-        if (it + 1 < nit) {
-          next_stage_ready(it);
-          read(n, lds + nxt * STAGE);
-        }
-  #pragma unroll
-        for (int a = 0; a < MB; ++a)
-  #pragma unroll
-          for (int b = 0; b < NB; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(c.a[1][a], c.b[1][b], acc[a][b], 0, 0, 0);
-        return nxt;
-      };
-      Frag f0, f1;
-      read(f0, lds);
-      int cur = 0;
-      for (int it = 0; it < nit; it += 2) {
-        cur = step(it, cur, f0, f1);
-        if (it + 1 < nit) cur = step(it + 1, cur, f1, f0);
-      }
     } else {
-      // fp32 A (split here into two scaled fp16 pieces), fp16 B pieces; passes (a0 b0), (a0 b1), (a1 b0)
-      struct Frag {
-        f32x4 lo[MB], hi[MB];
-        f16x8 b0[NB], b1[NB];
-      };
-      auto read = [&](Frag& f, const char* st) {
-  #pragma unroll
-        for (int b = 0; b < NB; ++b) {
-          f.b0[b] = *reinterpret_cast<const f16x8*>(st + offb[b][0]);
-          f.b1[b] = *reinterpret_cast<const f16x8*>(st + offb[b][1]);
+    f16x8 a0[MB], a1[MB], b0[NB], b1[NB];
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      b0[b] = *reinterpret_cast<const f16x8*>(st + offb[b][0]);
+      b1[b] = *reinterpret_cast<const f16x8*>(st + offb[b][1]);
+    }
+#pragma unroll
+    for (int a = 0; a < MB; ++a) {
+      const f32x4 lo = *reinterpret_cast<const f32x4*>(st + offa[a][0]);
+      const f32x4 hi = *reinterpret_cast<const f32x4*>(st + offa[a][1]);
+      const f32x8 y = f32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]} * sa;
+      split2(y, a0[a], a1[a]);
+    }
+    // pass q, then this wave's DMA pieces j = q, q + 3, ... of stage it + 2
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          acc[a][b] = mfma16(q == 2 ? a1[a] : a0[a], q == 1 ? b1[b] : b0[b], acc[a][b]);
+      if (dit >= 0) {
+#pragma unroll
+        for (int j = q; j < JHI; j += 3) {
+          if (j < JLO || j < cnt) {
+            __builtin_amdgcn_sched_barrier(0);
+            dma_one(dit, nxt2, j);
+            __builtin_amdgcn_sched_barrier(0);
+          }
         }
-  #pragma unroll
-        for (int a = 0; a < MB; ++a) {
-          f.lo[a] = *reinterpret_cast<const f32x4*>(st + offa[a][0]);
-          f.hi[a] = *reinterpret_cast<const f32x4*>(st + offa[a][1]);
-        }
-      };
-      auto step = [&](int it, int cur, const Frag& c, Frag& n) {
-        const int nxt = cur == 2 ? 0 : cur + 1, nxt2 = nxt == 2 ? 0 : nxt + 1;
-        const int dit = it + 2 < nit ? it + 2 : -1;
-        f16x8 a0[MB], a1[MB];
-  #pragma unroll
-        for (int a = 0; a < MB; ++a) {
-          const f32x8 y = f32x8{c.lo[a][0], c.lo[a][1], c.lo[a][2], c.lo[a][3],
-                                c.hi[a][0], c.hi[a][1], c.hi[a][2], c.hi[a][3]} * sa;
-          split2(y, a0[a], a1[a]);
-        }
-  #pragma unroll
-        for (int b = 0; b < NB; ++b) {
-  #pragma unroll
-          for (int a = 0; a < MB; ++a) acc[a][b] = mfma16(a0[a], c.b0[b], acc[a][b]);
-          dma_piece(dit, nxt2, b);
-        }
-  #pragma unroll
-        for (int j = NB; j < JHI; ++j) dma_piece(dit, nxt2, j);
-        if (it + 1 < nit) {
-          next_stage_ready(it);
-          read(n, lds + nxt * STAGE);
-        }
-  #pragma unroll
-        for (int a = 0; a < MB; ++a)
-  #pragma unroll
-          for (int b = 0; b < NB; ++b) acc[a][b] = mfma16(a0[a], c.b1[b], acc[a][b]);
-  #pragma unroll
-        for (int a = 0; a < MB; ++a)
-  #pragma unroll
-          for (int b = 0; b < NB; ++b) acc[a][b] = mfma16(a1[a], c.b0[b], acc[a][b]);
-        return nxt;
-      };
-      Frag f0, f1;
-      read(f0, lds);
-      int cur = 0;
-      for (int it = 0; it < nit; it += 2) {
-        cur = step(it, cur, f0, f1);
-        if (it + 1 < nit) cur = step(it + 1, cur, f1, f0);
       }
     }
+    }
+    if (it + 2 < nit) wait_stage();
+    else dma_wait<0>();
+    __syncthreads();
+    cur = cur == 2 ? 0 : cur + 1;
   }
 
   // ---- epilogue: quad transpose, then lane (l32 & 3) owns row 8 gq + 4 h + (l32 & 3) of each
@@ -548,32 +419,19 @@ int cfg_bm(int c) { return c <= 1 ? 256 : c == 2 || c == 4 ? 128 : 64; }
 int cfg_bn(int c) { return c <= 1 || c == 4 ? 192 : c == 2 ? 96 : 64; }
 int cfg_nwm(int c) { return c == 0 ? 8 : c == 1 ? 4 : c == 2 || c == 4 ? 4 : 2; }
 
-// main-loop form (PF template parameter): 0 = fragment reads after the barrier, 1 = reads of the
-// next stage under the current stage's later passes (HX_GEMM_F16_PF, A/B only)
-inline int pipe_form() {
-  const char* e = getenv("HX_GEMM_F16_PF");
-  return e ? atoi(e) : 0;
-}
-
-template <int BM, int BN, int WM, int WN, int EPI, int AT, int OB, int PF>
-void launch_pf(const F16Args& a, hipStream_t s) {
+template <int BM, int BN, int WM, int WN, int EPI, int AT = 0, int OB = 0>
+void launch_one(const F16Args& a, hipStream_t s) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int total = ((a.M + BM - 1) / BM) * (a.N / BN) * a.ks;
   const int per = (total + 7) / 8;
   const size_t smem = (size_t)3 * (BM + BN) * 64;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_f16_k<BM, BN, WM, WN, EPI, 1, AT, OB, PF>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_f16_k<BM, BN, WM, WN, EPI, 1, AT, OB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
-  gemm_f16_k<BM, BN, WM, WN, EPI, 1, AT, OB, PF><<<8 * per, NT, smem, s>>>(a);
-}
-
-template <int BM, int BN, int WM, int WN, int EPI, int AT = 0, int OB = 0>
-void launch_one(const F16Args& a, hipStream_t s) {
-  if (pipe_form() == 1) launch_pf<BM, BN, WM, WN, EPI, AT, OB, 1>(a, s);
-  else launch_pf<BM, BN, WM, WN, EPI, AT, OB, 0>(a, s);
+  gemm_f16_k<BM, BN, WM, WN, EPI, 1, AT, OB><<<8 * per, NT, smem, s>>>(a);
 }
 
 template <int EPI, int AT = 0, int OB = 0>
@@ -954,13 +812,50 @@ int hx_gemm_f16_colpart_rows(int M, int cfg) {
 }
 
 int hx_gemm_f16_ks(int M, int N, int K, int cfg) {
+  // split-K slabs when the output tiles fill less than half the CUs and the reduction is deep:
+  // the MLM decoder's data gradient (K = 30720) and the fine-tuning-sized data gradients
+  // (~1-2k token rows, K = 2304 / 3072); each slab keeps >= 512 of the reduction
   if (cfg < 0) return 1;
   const int tiles = hx_gemm_f16_tiles(M, N, cfg), slots = hx_cu_slots();
-  if (tiles * 2 > slots || K < 8192) return 1;
+  if (tiles * 2 > slots || K < 1024) return 1;
   int best = 1;
   for (int ks = 2; ks <= 16; ++ks)
-    if (tiles * ks <= slots && K % (16 * ks) == 0 && K / ks >= 2048) best = ks;
+    if (tiles * ks <= slots && K % (16 * ks) == 0 && K / ks >= 512) best = ks;
   return best;
+}
+
+// C (+)= sum of the ks slabs (+ bias): the split-K combine with the epilogue the slabs could not apply
+__global__ __launch_bounds__(256) void slab_combine_k(const float4* __restrict__ ws, float* __restrict__ C, int64_t ldc,
+                                                      int64_t M, int n4, int ks, int beta,
+                                                      const float4* __restrict__ bias) {
+  const int64_t total = M * n4, slab = M * n4;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / n4;
+    const int c = (int)(i - r * n4);
+    float4 s = ws[i];
+    for (int k = 1; k < ks; ++k) {
+      const float4 v = ws[(int64_t)k * slab + i];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    if (bias) {
+      const float4 b = bias[c];
+      s.x += b.x; s.y += b.y; s.z += b.z; s.w += b.w;
+    }
+    float4* o = reinterpret_cast<float4*>(C + r * ldc) + c;
+    if (beta) {
+      const float4 v = *o;
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    *o = s;
+  }
+}
+
+void hx_gemm_f16_slab_combine(const float* ws, float* C, int64_t ldc, int M, int N, int ks, int beta,
+                              const float* bias, hipStream_t s) {
+  const int64_t n = (int64_t)M * (N / 4);
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 4096);
+  slab_combine_k<<<blocks, 256, 0, s>>>(reinterpret_cast<const float4*>(ws), C, ldc, M, N / 4, ks, beta,
+                                        reinterpret_cast<const float4*>(bias));
 }
 
 int hx_gemm_f16(const HxGemmF16& p, int cfg, hipStream_t s) {

@@ -125,8 +125,9 @@ def weight_pieces(W):
 
 
 # ---------------------------------------------------------------- products
-def mm(a2, a_parts, b, b_parts, out=None, beta=False, bias=None, ks=1):
-    """a2 [M, K] (fp32) . b^T (b = P2 pieces [N, 2K]) (+ out if beta) (+ bias) -> fp32 [M, N]."""
+def mm(a2, a_parts, b, b_parts, out=None, beta=False, bias=None, ks=0):
+    """a2 [M, K] (fp32) . b^T (b = P2 pieces [N, 2K]) (+ out if beta) (+ bias) -> fp32 [M, N];
+    ``ks``: split-K slabs (0 = the kernel's plan: deep reductions with few output tiles)."""
     return C().gemm_f16(a2, a_parts, b, b_parts, out=out, beta=beta, bias=bias, ks=ks)
 
 

@@ -125,6 +125,30 @@ def test_gemm_f16_split_k(dev):
     assert _rel_err(out, ref, a, W) < 4e-6
 
 
+@pytest.mark.parametrize('ks', [2, 3, 6])
+def test_gemm_f16_split_k_beta_bias(dev, ks):
+    """Fine-tuning-sized data gradient (1000 token rows, K = 3072): split-K slabs combined with the
+    beta = 1 accumulation and the bias in one pass (slab_combine_k), forced and planned."""
+    g = torch.Generator(device=dev).manual_seed(ks)
+    M, N, K = 1000, 768, 3072
+    a = torch.randn(M, K, device=dev, generator=g)
+    W = torch.randn(N, K, device=dev, generator=g) * 0.02
+    bias = torch.randn(N, device=dev, generator=g)
+    acc = torch.randn(M, N, device=dev, generator=g)
+    wf, wt, parts = _pieces(W)
+    ap = C().amax_rows(a)
+    out = acc.clone()
+    C().gemm_f16(a, ap, wf, parts, out=out, beta=True, bias=bias, ks=ks)
+    ref = acc.double() + a.double() @ W.double().t() + bias.double()
+    den = acc.double().abs() + a.double().abs() @ W.double().abs().t() + bias.double().abs()
+    assert ((out.double() - ref).abs() / den).max().item() < 4e-6
+    assert C().gemm_f16_ks(M, N, K, C().gemm_f16_plan(M, N, K)) > 1      # the plan splits this shape
+    out2 = acc.clone()
+    C().gemm_f16(a, ap, wf, parts, out=out2, beta=True)
+    ref2 = acc.double() + a.double() @ W.double().t()
+    assert ((out2.double() - ref2).abs() / den).max().item() < 4e-6
+
+
 @pytest.mark.parametrize('T,M,N,mvalid', [(16384, 2304, 768, 2304), (16384, 768, 3072, 768), (16384, 3072, 768, 3072),
                                           (4096, 768, 768, 768), (2560, 30720, 768, 30522), (1000, 256, 384, 256)])
 def test_wgrad_f16(dev, T, M, N, mvalid):
@@ -156,12 +180,10 @@ def test_f16_scale_extremes(dev):
     assert C().gemm_f16(z, C().amax_rows(z), wf, parts).abs().max().item() == 0.0
 
 
-@pytest.mark.parametrize('pf', ['0', '1'])
 @pytest.mark.parametrize('M,N,K', [(16384, 768, 768), (16384, 3072, 768), (4096, 768, 3072), (300, 2304, 768)])
-def test_gemm_bf16_mode(dev, monkeypatch, M, N, K, pf):
+def test_gemm_bf16_mode(dev, M, N, K):
     """--precision bf16 on the same kernel (one bf16 pass, bf16 or fp32 output, bias / beta): against
     the fp64 product of the same bf16 operands (only fp32 accumulation and the output rounding)."""
-    monkeypatch.setenv('HX_GEMM_F16_PF', pf)
     g = torch.Generator(device=dev).manual_seed(M + K)
     a = torch.randn(M, K, device=dev, generator=g).bfloat16()
     W = torch.randn(N, K, device=dev, generator=g) * 0.02
@@ -186,14 +208,11 @@ def test_gemm_bf16_mode(dev, monkeypatch, M, N, K, pf):
     assert ((out.double() - ref2).abs() / den2).max().item() < 8e-3
 
 
-@pytest.mark.parametrize('pf', ['0', '1'])
 @pytest.mark.parametrize('cfg', ['0', '1', '2', '3', '4'])
-def test_gemm_f16_every_tile(dev, monkeypatch, cfg, pf):
-    """Every tile configuration of gemm_f16_k (HX_GEMM_F16_CFG forces it) in both main-loop forms
-    (HX_GEMM_F16_PF): forward with bias and the beta = 1 data gradient, rows not a multiple of the
-    tile."""
+def test_gemm_f16_every_tile(dev, monkeypatch, cfg):
+    """Every tile configuration of gemm_f16_k (HX_GEMM_F16_CFG forces it): forward with bias and the
+    beta = 1 data gradient, rows not a multiple of the tile."""
     monkeypatch.setenv('HX_GEMM_F16_CFG', cfg)
-    monkeypatch.setenv('HX_GEMM_F16_PF', pf)
     g = torch.Generator(device=dev).manual_seed(int(cfg))
     M, N, K = 4096 + 37, 768, 768
     a = torch.randn(M, K, device=dev, generator=g)

@@ -41,9 +41,9 @@ def sweep(C, dev, cfgs):
         xb, Wb = x.bfloat16(), W.bfloat16()
         fl = 2.0 * T * N * K
         for c in cfgs:
-            # 'cfg' or 'cfg/pf' (pf: HX_GEMM_F16_PF main-loop form)
-            cfg, _, pf = c.partition('/')
-            os.environ['HX_GEMM_F16_PF'] = pf or '0'
+            # 'cfg' or 'cfg:ks' (ks: split-K slabs of the plain / beta GEMMs; default = the plan)
+            cfg, _, ks = c.partition(':')
+            ks = int(ks) if ks else 0
             if cfg == 'plan':
                 os.environ.pop('HX_GEMM_F16_CFG', None)
             else:
@@ -52,11 +52,11 @@ def sweep(C, dev, cfgs):
                 if name == 'ffn_up':
                     f = timed(lambda: C().gemm_f16_gelu(x, xp, wf, wp, b, 1))
                 else:
-                    f = timed(lambda: C().gemm_f16(x, xp, wf, wp, bias=b))
+                    f = timed(lambda: C().gemm_f16(x, xp, wf, wp, bias=b, ks=ks))
                 if name == 'ffn_down':
                     dg = timed(lambda: C().gemm_f16_dgelu(dy, dp, wt, wp, d, None, db, 1))
                 else:
-                    dg = timed(lambda: C().gemm_f16(dy, dp, wt, wp, out=acc, beta=True))
+                    dg = timed(lambda: C().gemm_f16(dy, dp, wt, wp, out=acc, beta=True, ks=ks))
                 bf = timed(lambda: C().gemm_bf16(xb, Wb, bias=b))
             except RuntimeError as e:
                 print('{:10s} cfg {}: {}'.format(name, c, str(e).splitlines()[0]), flush=True)
@@ -64,7 +64,6 @@ def sweep(C, dev, cfgs):
             print('{:10s} cfg {:4s} fwd {:7.1f} us ({:4.2f} PF/s)  dgrad {:7.1f} us ({:4.2f})  bf16 fwd {:6.1f} us '
                   '({:4.2f})'.format(name, c, f, 3 * fl / f / 1e9, dg, 3 * fl / dg / 1e9, bf, fl / bf / 1e9), flush=True)
     os.environ.pop('HX_GEMM_F16_CFG', None)
-    os.environ.pop('HX_GEMM_F16_PF', None)
 
 
 def main():

@@ -528,26 +528,31 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
   tr_base<BM>(lane, alo, ahi);
   tr_base<BN>(lane, blo, bhi);
 
-  f32x4 rA[CA][2], rB[CB][2];
-  auto load = [&](int it) {
+  // two register stages: the fp32 tiles of step it + 2 are loaded while step it runs on the
+  // matrix cores, so a load has a whole step of MFMA work (plus the split / LDS write of step
+  // it + 1) to land before it is split and written to LDS
+  struct Regs {
+    f32x4 a[CA][2], b[CB][2];
+  };
+  auto load = [&](int it, Regs& r) {
     const uint32_t soa = (uint32_t)it * BKT * lda * 4, sob = (uint32_t)it * BKT * ldb * 4;
 #pragma unroll
     for (int i = 0; i < CA; ++i)
 #pragma unroll
       for (int k = 0; k < 2; ++k)
-        rA[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(abuf.r, va[i] + 16 * k, soa, 0));
+        r.a[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(abuf.r, va[i] + 16 * k, soa, 0));
 #pragma unroll
     for (int i = 0; i < CB; ++i)
 #pragma unroll
       for (int k = 0; k < 2; ++k)
-        rB[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(bbuf.r, vb[i] + 16 * k, sob, 0));
+        r.b[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(bbuf.r, vb[i] + 16 * k, sob, 0));
   };
-  auto store = [&](int buf) {
+  auto store = [&](int buf, const Regs& r) {
     char* st = lds + buf * STAGE;
 #pragma unroll
     for (int i = 0; i < CA; ++i) {
-      const f32x8 y = f32x8{rA[i][0][0], rA[i][0][1], rA[i][0][2], rA[i][0][3],
-                            rA[i][1][0], rA[i][1][1], rA[i][1][2], rA[i][1][3]} * sa;
+      const f32x8 y = f32x8{r.a[i][0][0], r.a[i][0][1], r.a[i][0][2], r.a[i][0][3],
+                            r.a[i][1][0], r.a[i][1][1], r.a[i][1][2], r.a[i][1][3]} * sa;
       f16x8 h0, h1;
       split2(y, h0, h1);
       *reinterpret_cast<f16x8*>(st + sa_[i]) = h0;
@@ -555,8 +560,8 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
     }
 #pragma unroll
     for (int i = 0; i < CB; ++i) {
-      const f32x8 y = f32x8{rB[i][0][0], rB[i][0][1], rB[i][0][2], rB[i][0][3],
-                            rB[i][1][0], rB[i][1][1], rB[i][1][2], rB[i][1][3]} * sb;
+      const f32x8 y = f32x8{r.b[i][0][0], r.b[i][0][1], r.b[i][0][2], r.b[i][0][3],
+                            r.b[i][1][0], r.b[i][1][1], r.b[i][1][2], r.b[i][1][3]} * sb;
       f16x8 h0, h1;
       split2(y, h0, h1);
       *reinterpret_cast<f16x8*>(st + 2 * A_T + sb_[i]) = h0;
@@ -591,17 +596,23 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
         for (int b = 0; b < NB; ++b) acc[a][b] = mfma16(q == 2 ? a1[a] : a0[a], q == 1 ? b1[b] : b0[b], acc[a][b]);
   };
 
-  // one register stage: step it + 1 is loaded while step it runs on the matrix cores, then split
-  // and written to the other LDS buffer (last read before the previous barrier)
-  load(0);
-  store(0);
+  // step it: load step it + 2 into the register set step it used, multiply LDS buffer it & 1,
+  // split and write step it + 1 (loaded a step ago) into the other buffer (last read before the
+  // previous barrier); the two register sets alternate (steps unrolled by two: no copies)
+  Regs r0, r1;
+  load(0, r0);
+  if (nit > 1) load(1, r1);
+  store(0, r0);
   __syncthreads();
-  for (int it = 0; it < nit; ++it) {
-    const int cur = it & 1;
-    if (it + 1 < nit) load(it + 1);
-    mma(cur);
-    if (it + 1 < nit) store(cur ^ 1);
+  auto step = [&](int it, Regs& mine, const Regs& next) {
+    if (it + 2 < nit) load(it + 2, mine);
+    mma(it & 1);
+    if (it + 1 < nit) store((it & 1) ^ 1, next);
     __syncthreads();
+  };
+  for (int it = 0; it < nit; it += 2) {
+    step(it, r0, r1);
+    if (it + 1 < nit) step(it + 1, r1, r0);
   }
 
   float* o = out + (nsplit > 1 ? (int64_t)sp * M * N : 0);

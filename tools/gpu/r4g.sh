@@ -1,11 +1,13 @@
 # round 4 (g): split-K for few-tile GEMMs (fine-tuning sizes) + slab combine with beta / bias;
-# NER-size tile sweep; NER probe; GPU suite
+# NER-size tile sweep; two-register-stage weight gradient; bench; NER probe
 set -o pipefail
 mkdir -p gpurun_out
 . tools/gpu/run_step.sh
 run_step 200 gpurun_out/r4g_gemmtests.log python -u -m pytest -x -v --timeout 100 --timeout-method thread tests/test_gemm_f16_gpu.py
 T=2048 CFGS=2:1,2:2,2:4,3:1,3:2,plan run_step 240 gpurun_out/r4g_sweep2048.log python -u tools/probe/gemm_f16_bench.py
 T=4096 CFGS=2:1,3:1,plan run_step 240 gpurun_out/r4g_sweep4096.log python -u tools/probe/gemm_f16_bench.py
+run_step 180 gpurun_out/r4g_gemm_bench.log python -u tools/probe/gemm_f16_bench.py
+run_step 300 gpurun_out/r4g_bench.log python -u bench.py
 run_step 240 gpurun_out/r4g_ner_probe.log python -u tools/probe/ner_graph_probe.py --no-overlap-wgrad
 run_step 240 gpurun_out/r4g_ner.log python -u tools/bench_ner.py --steps 40
 run_step 300 gpurun_out/r4g_bench_b32.log python -u bench.py --batch 32

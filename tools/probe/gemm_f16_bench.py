@@ -77,7 +77,10 @@ def main():
     def rnd(*s):
         return torch.randn(*s, device=dev, generator=g)
     rows = []
+    only = os.environ.get('ONLY')   # one shape name (PMC passes)
     for (name, N, K) in [('qkv', 2304, 768), ('attn_out', 768, 768), ('ffn_up', 3072, 768), ('ffn_down', 768, 3072)]:
+        if only and name != only:
+            continue
         x = rnd(T, K)
         W = rnd(N, K) * 0.03
         b = rnd(N)

@@ -64,6 +64,9 @@ def parse():
                     help='weight-gradient GEMMs on a side HIP stream on every backward path (default: the '
                          'piece-GEMM paths only)')
     ap.add_argument('--no-overlap-wgrad', dest='overlap_wgrad', action='store_const', const='off')
+    ap.add_argument('--graph-train-step', action='store_true',
+                    help='capture each whole update (forward, backward, all-reduce, optimizer) in a HIP graph '
+                         'and replay it (utils/train_graph.py)')
     ap.add_argument('--profile-phases', action='store_true',
                     help='extra untimed steps reporting host time per step phase (stderr)')
     ap.add_argument('--sync-debug', action='store_true',
@@ -180,6 +183,8 @@ def run(a, rank, world, dev_index, init_method):
             '--comm-cus', str(a.comm_cus)]
     if a.profile_phases:
         argv += ['--profile-phases']
+    if a.graph_train_step:
+        argv += ['--graph-train-step']
     if a.overlap_wgrad != 'auto':
         argv += ['--overlap-wgrad' if a.overlap_wgrad == 'on' else '--no-overlap-wgrad']
     if a.gemm_tuning_file:

@@ -9,10 +9,10 @@ T=4096 CFGS=2:1,3:1,plan run_step 240 gpurun_out/r4g_sweep4096.log python -u too
 run_step 180 gpurun_out/r4g_gemm_bench.log python -u tools/probe/gemm_f16_bench.py
 run_step 300 gpurun_out/r4g_bench.log python -u bench.py
 run_step 300 gpurun_out/r4g_bench_nooverlap.log python -u bench.py --no-overlap-wgrad
+run_step 300 gpurun_out/r4g_bench_graph.log python -u bench.py --graph-train-step
 run_step 240 gpurun_out/r4g_ner_probe.log python -u tools/probe/ner_graph_probe.py --no-overlap-wgrad
 run_step 240 gpurun_out/r4g_ner.log python -u tools/bench_ner.py --steps 40
 run_step 300 gpurun_out/r4g_bench_b32.log python -u bench.py --batch 32
-export TMPDIR=/tmp
 export TMPDIR=/tmp
 run_step 60 gpurun_out/r4h_counters.txt rocprofv3 -L
 ONLY=qkv run_step 90 gpurun_out/r4h_pmc1.log rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS --output-format csv -d gpurun_out/pmc_r4h1 -o run -- python3 tools/probe/gemm_f16_bench.py

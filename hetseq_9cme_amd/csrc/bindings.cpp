@@ -375,8 +375,9 @@ std::vector<Tensor> attn_fwd_x6(Tensor qkv, Tensor mask_bias, int64_t nh, double
 // returns {dqkv, dbias} (dbias: [3H] fp32 when bias is given -- written into dbq/dbk/dbv
 // when those slots are given -- else an empty tensor)
 std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask,
-                             int64_t nh, double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, bool split = false,
+                             int64_t nh, double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, int split = 0,
                              OptT amax_out = OptT()) {
+  // split: 0 none, 1 bf16 x6 pieces (attention_x6.hip), 2 fp16x3 (attention_f16.hip)
   check_cuda(dout, "grad_output");
   check_cuda(qkv, "qkv");
   const int bf = act_bf16(qkv);
@@ -417,7 +418,7 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor o
     }
     part = torch::empty({B * ((S + 127) / 128), 3 * H}, qkv.options().dtype(torch::kFloat32));
   }
-  hx_attn_bwd(split ? 2 : bf, qkv.data_ptr(), ptr_or_null<float>(bias), pq, pk, pv, part.defined() ? part.data_ptr<float>() : nullptr,
+  hx_attn_bwd(split == 2 ? 3 : (split ? 2 : bf), qkv.data_ptr(), ptr_or_null<float>(bias), pq, pk, pv, part.defined() ? part.data_ptr<float>() : nullptr,
               mask_bias.data_ptr<float>(), dout.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
               keep < 1.0 ? reinterpret_cast<const uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr,
               dqkv.data_ptr(), dq_acc, dq_ld, (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv),
@@ -840,12 +841,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("seed"), py::arg("stream"), py::arg("bias"), py::arg("amax_out") = py::none());
   m.def("attn_bwd", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
                        double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv) {
-    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, false);
+    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, 0);
   });
   // fp32 attention backward on the bf16 matrix cores (split pieces, attention_x6.hip)
   m.def("attn_bwd_x6", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
                           double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, OptT amax_out) {
-    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, true, amax_out);
+    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, 1, amax_out);
+  }, py::arg("dout"), py::arg("qkv"), py::arg("mask_bias"), py::arg("out"), py::arg("lse"), py::arg("dmask"),
+     py::arg("nh"), py::arg("keep"), py::arg("bias"), py::arg("dbq"), py::arg("dbk"), py::arg("dbv"),
+     py::arg("amax_out") = py::none());
+  // fp32 attention backward on the fp16 matrix cores (fp16x3, attention_f16.hip)
+  m.def("attn_bwd_f16", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
+                           double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, OptT amax_out) {
+    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, 2, amax_out);
   }, py::arg("dout"), py::arg("qkv"), py::arg("mask_bias"), py::arg("out"), py::arg("lse"), py::arg("dmask"),
      py::arg("nh"), py::arg("keep"), py::arg("bias"), py::arg("dbq"), py::arg("dbk"), py::arg("dbv"),
      py::arg("amax_out") = py::none());

@@ -74,11 +74,17 @@ void hx_attn_fwd_x6(const float* qkv, const float* bias, const float* maskb, flo
 void hx_attn_bwd_x6(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,
                     const float* out, const float* lse, const uint32_t* dmask, float* dqkv, float* dq_acc, int dq_ld,
                     int B, int S, int nh, float keep, hipStream_t s, float* amax_part = nullptr);
+// the same backward on the fp16 matrix cores (three passes over scaled two-piece operands,
+// attention_f16.hip: --fp32-gemm fp16x3)
+void hx_attn_bwd_f16(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,
+                     const float* out, const float* lse, const uint32_t* dmask, float* dqkv, float* dq_acc, int dq_ld,
+                     int B, int S, int nh, float keep, hipStream_t s, float* amax_part = nullptr);
 void hx_attn_fwd(int bf16, const void* qkv, const float* bias, const float* maskb, void* out, float* lse,
                  uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream, hipStream_t s);
 // dq_acc: fp32 dQ accumulation target when S > 128 (atomics; row stride dq_ld), else unused.
 // With bias: its gradient (column sums of dQ / dK / dV) goes to dbq / dbk / dbv through the
-// dbias_part workspace ([B * ceil(S/128)][3H] fp32).  kind: 0 fp32 MFMA, 1 bf16, 2 fp32 split (x6).
+// dbias_part workspace ([B * ceil(S/128)][3H] fp32).  kind: 0 fp32 MFMA, 1 bf16, 2 fp32 split (x6),
+// 3 fp32 as fp16x3.
 void hx_attn_bwd(int kind, const void* qkv, const float* bias, float* dbq, float* dbk, float* dbv, float* dbias_part,
                  const float* maskb, const void* dout, const void* out, const float* lse, const uint32_t* dmask,
                  void* dqkv, float* dq_acc, int dq_ld, int B, int S, int nh, float keep, hipStream_t s,

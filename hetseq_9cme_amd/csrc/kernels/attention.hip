@@ -538,6 +538,9 @@ void hx_attn_bwd(int kind, const void* qkv, const float* bias, float* dbq, float
   else if (kind == 2)   // fp32 on bf16 MFMA, split pieces (attention_x6.hip)
     hx_attn_bwd_x6((const float*)qkv, bias, dbias_part, maskb, (const float*)dout, (const float*)out, lse, dmask,
                    (float*)dqkv, dq_acc, dq_ld, B, S, nh, keep, s, amax_part);
+  else if (kind == 3)   // fp32 on fp16 MFMA, scaled two-piece operands (attention_f16.hip)
+    hx_attn_bwd_f16((const float*)qkv, bias, dbias_part, maskb, (const float*)dout, (const float*)out, lse, dmask,
+                    (float*)dqkv, dq_acc, dq_ld, B, S, nh, keep, s, amax_part);
   else
     attn_bwd_t<float>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv, dq_acc, dq_ld, B, S, nh, keep, s);
   if (dbias_part) {

@@ -1,0 +1,578 @@
+// fp32 attention backward on the fp16 matrix cores (--fp32-gemm fp16x3).
+//
+// Same math and I/O as the other attention backward kernels (reference
+// hetseq/bert_modeling.py:351-377 differentiated): packed fp32 [B, S, 3H] QKV (+ the
+// projection bias), fp32 context gradient, context, per-query logsumexp and the transposed dropout
+// bitmask in; fp32 dQKV (+ QKV-bias gradient partials, + max |dQKV| partials) out.
+//
+// Every product runs as three fp16 MFMA passes over scaled two-piece operands (the GEMMs' fp16x3
+// class, hx_gemm.h): x = 2^-E (h0 + h1), h0 = fp16(2^E x), h1 = fp16(2^E x - h0), the product
+// a.b = a0 b0 + a0 b1 + a1 b0 -- half the MFMA passes of the bf16 x6 kernel (attention_x6.hip),
+// two LDS images per operand instead of three.  The scale exponents are powers of two chosen so
+// the largest magnitude of an operand lands below 2^15:
+//   K, V      one exponent per workgroup (its 128 keys), fixed for the kernel;
+//   Q, dO     one running exponent per workgroup: each 32-query tile's max |x| is reduced over the
+//             workgroup before the tile is split, and the exponent only ever decreases -- the dK
+//             and dV accumulators (which sum over query tiles) are rescaled by the exact power of
+//             two when it does;
+//   Pd        fixed: P <= 1, so Pd <= 1 / keep;
+//   dS (dK)   one running exponent per wave (its 32 keys), from the wave's max |dS| of each tile,
+//             again with an exact rescale of the wave's dK accumulator when it decreases;
+//   dS (dQ)   one exponent per tile over the workgroup's 128 keys: dS goes through LDS as fp32 and
+//             is split after the barrier that publishes every wave's max.
+// Unscaling is exact (ldexp) and happens on the fp32 results: S and dP per tile, dQ per tile, dK
+// and dV once in the epilogue.
+//
+// Structure (the x6 kernel's): grid (ceil(S/128), nh, B), block 256 = 4 waves; wave w owns keys
+// kbase + 32w .. +31 ON THE LANES (K / V piece fragments in registers) and the workgroup sweeps
+// 32-query tiles:
+//   S = Qs . K^T, dP = dO . V^T            (32x32x16: A = piece rows of the tile, B = key pieces)
+//   P = exp(S + mask - lse), Pd = P drop/keep, dS = P (dP drop/keep - D)     (fp32, in place)
+//   dV += Pd^T . dO, dK += dS^T . Qs        (A = pieces of the P / dS accumulators, B = pieces
+//                                            of transposed, query-permuted images of dO / Q)
+//   dQ  = dS . K over the block's 128 keys  (16x16x32: dS from LDS split per tile, K^T pieces)
+// D = rowsum(dO * O) in fp32 while staging.
+#include "hx_launch.h"
+#include "hx_vec.h"
+#include "hx_attn.h"
+#include "hx_gemm.h"
+
+namespace {
+
+using hx::attn::crow;
+using hx::attn::f32x16;
+using hx::g::f16_scale_exp;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int D = 64;
+constexpr int RS = 72;    // [query][dim] image row stride (halves): conflict-free 16-B fragment reads
+constexpr int TS = 40;    // transposed 32-query image row stride (halves)
+constexpr int KTS = 136;  // K^T [dim][128 keys] row stride (halves)
+constexpr int DSF = 132;  // fp32 dS [query][128 keys] row stride (floats): conflict-free dQ fragment reads
+constexpr int KT_B = 64 * KTS * 2, DS_B = 32 * DSF * 4, QS_B = 32 * RS * 2, QT_B = 64 * TS * 2;
+constexpr int NSC = 16;   // per-tile scalars: max |Q|, max |dO|, max |dS| per wave (+ spare)
+constexpr int BWD_SMEM = 2 * KT_B + DS_B + 2 * (2 * QS_B) + 2 * (2 * QT_B) + (32 + 128 + NSC) * 4;
+constexpr int kNoScale = 120;   // exponent of an operand seen only as zeros so far (no constraint)
+
+__device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+// (a0, b0), (a0, b1), (a1, b0)
+#define HX_X3(ACC, A, B)          \
+  do {                            \
+    ACC = mfma(A[0], B[0], ACC);  \
+    ACC = mfma(A[0], B[1], ACC);  \
+    ACC = mfma(A[1], B[0], ACC);  \
+  } while (0)
+#define HX_X3_16(ACC, A, B)         \
+  do {                              \
+    ACC = mfma16(A[0], B[0], ACC);  \
+    ACC = mfma16(A[0], B[1], ACC);  \
+    ACC = mfma16(A[1], B[0], ACC);  \
+  } while (0)
+
+// exponent for an operand whose max |x| so far is m (zeros: no constraint)
+__device__ __forceinline__ int run_exp(float m) { return m > 0.f ? f16_scale_exp(m) : kNoScale; }
+
+// 8 fp32 values * s -> two fp16 pieces
+__device__ __forceinline__ void sp8(const f32x8 x, float s, f16x8 (&p)[2]) {
+  const f32x8 y = x * s;
+  p[0] = __builtin_convertvector(y, f16x8);
+  p[1] = __builtin_convertvector(y - __builtin_convertvector(p[0], f32x8), f16x8);
+}
+// 4 fp32 values * s -> two pieces of 4 halves (two words each)
+__device__ __forceinline__ void sp4(const float (&x)[4], float s, uint2 (&p)[2]) {
+  const f32x4 y = f32x4{x[0], x[1], x[2], x[3]} * s;
+  const f16x4 h0 = __builtin_convertvector(y, f16x4);
+  const f16x4 h1 = __builtin_convertvector(y - __builtin_convertvector(h0, f32x4), f16x4);
+  p[0] = __builtin_bit_cast(uint2, h0);
+  p[1] = __builtin_bit_cast(uint2, h1);
+}
+template <int O>
+__device__ __forceinline__ f32x8 acc8(const f32x16& s) {
+  return f32x8{s[O], s[O + 1], s[O + 2], s[O + 3], s[O + 4], s[O + 5], s[O + 6], s[O + 7]};
+}
+
+// key k (0..63 of a 64-position group) -> its column in a transposed, permuted image
+// (attention_bf16.hip): the accumulator's row order, so P / dS pieces feed the MFMA A operand
+__device__ __forceinline__ int vpos(int k) {
+  const int kk = k & 15;
+  return (k & ~15) + 8 * ((kk >> 2) & 1) + (kk & 3) + 4 * (kk >> 3);
+}
+// rows r0, r1 (consecutive image positions) x 4 dims -> 4 words of a transposed image
+__device__ __forceinline__ void put_t4(uint16_t* img, int stride, int dim0, int pos, uint2 r0, uint2 r1) {
+  uint32_t* p = reinterpret_cast<uint32_t*>(img + dim0 * stride + pos);
+  const int sw = stride / 2;
+  p[0] = (r0.x & 0xffffu) | (r1.x << 16);
+  p[sw] = (r0.x >> 16) | (r1.x & 0xffff0000u);
+  p[2 * sw] = (r0.y & 0xffffu) | (r1.y << 16);
+  p[3 * sw] = (r0.y >> 16) | (r1.y & 0xffff0000u);
+}
+__device__ __forceinline__ f32x8 ld8(const float* p, const float* bias) {
+  const float4 a = *reinterpret_cast<const float4*>(p), c = *reinterpret_cast<const float4*>(p + 4);
+  f32x8 f = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+  if (bias) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] += bias[j];
+  }
+  return f;
+}
+__device__ __forceinline__ float amax8(const f32x8 f) {
+  float m = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(f[j]));
+  return m;
+}
+__device__ __forceinline__ float wave_max(float m) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  return m;
+}
+// v *= 2^e, every element (exact unless the result leaves the normal range)
+__device__ __forceinline__ void rescale(f32x16& v, int e) {
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = ldexpf(v[r], e);
+}
+
+template <bool kDrop>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void attn_bwd_f16_k(
+    const float* __restrict__ qkv, const float* __restrict__ qkv_bias, float* __restrict__ dbias_part,
+    const float* __restrict__ maskb, const float* __restrict__ dout, const float* __restrict__ outp,
+    const float* __restrict__ lse, const uint32_t* __restrict__ dmask, float* __restrict__ dqkv,
+    float* __restrict__ dq_acc, int dq_ld, int S, int nh, float keep, float* __restrict__ amax_part) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* Kt = reinterpret_cast<uint16_t*>(smem);                      // [2][64][KTS]
+  float* dSf = reinterpret_cast<float*>(smem + 2 * KT_B);                // [32][DSF] fp32
+  uint16_t* Qs = reinterpret_cast<uint16_t*>(smem + 2 * KT_B + DS_B);    // [2][32][RS]
+  uint16_t* dOs = Qs + 2 * 32 * RS;                                      // [2][32][RS]
+  uint16_t* Qt = dOs + 2 * 32 * RS;                                      // [2][64][TS]
+  uint16_t* dOt = Qt + 2 * 64 * TS;                                      // [2][64][TS]
+  float* Ls = reinterpret_cast<float*>(dOt + 2 * 64 * TS);               // [32] lse
+  float* Ds = Ls + 32;                                                   // [32][4 waves] D partials
+  float* Sc = Ds + 128;                                                  // per-tile scalars
+  float* ScQ = Sc, *ScD = Sc + 4, *ScS = Sc + 8;                         // [4 waves] each
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const int b = blockIdx.z, hd = blockIdx.y;
+  const int H = nh * D, H3 = 3 * H;
+  const int kbase = blockIdx.x * 128;
+  const bool single = gridDim.x == 1;
+  const int64_t bh = (int64_t)b * nh + hd;
+  const float scale = 0.125f, inv_keep = 1.f / keep;
+  const int Sp = (S + 127) & ~127;
+  const int nwords = Sp >> 5;
+  const float* base = qkv + (int64_t)b * S * H3 + hd * D;
+  const float* qbias = qkv_bias ? qkv_bias + hd * D : nullptr;
+  const float* kbias = qkv_bias ? qkv_bias + H + hd * D : nullptr;
+  const float* vbias = qkv_bias ? qkv_bias + 2 * H + hd * D : nullptr;
+  float am = 0.f;   // max |dQKV| of this block's stores (one key block per head only)
+
+  // ---- this lane's key: fp32 K and V fragments (dims 16ks + 8h .. +7), the block's max |K|, |V|
+  const int mykey = kbase + w * 32 + l32;
+  const int mykc = mykey < S ? mykey : S - 1;
+  f32x8 kx[4], vx[4];
+  float mkx = 0.f, mvx = 0.f;
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int c = 16 * ks + 8 * h;
+    kx[ks] = ld8(base + (int64_t)mykc * H3 + H + c, kbias ? kbias + c : nullptr);
+    vx[ks] = ld8(base + (int64_t)mykc * H3 + 2 * H + c, vbias ? vbias + c : nullptr);
+    mkx = fmaxf(mkx, amax8(kx[ks]));
+    mvx = fmaxf(mvx, amax8(vx[ks]));
+  }
+  mkx = wave_max(mkx);
+  mvx = wave_max(mvx);
+  if (lane == 0) {
+    ScQ[w] = mkx;
+    ScD[w] = mvx;
+  }
+  const float mk = mykey < S ? maskb[(int64_t)b * S + mykey] : -INFINITY;
+
+  const float* dout_b = dout + (int64_t)b * S * H + hd * D;
+  const float* out_b = outp + (int64_t)b * S * H + hd * D;
+  float* dqkv_b = dqkv + (int64_t)b * S * H3 + hd * D;
+  float* dqa_b = dq_acc ? dq_acc + (int64_t)b * S * dq_ld + hd * D : nullptr;
+  const float* lse_bh = lse + bh * S;
+  const uint32_t* dmask_bh = kDrop ? dmask + bh * Sp * nwords : nullptr;
+  const int moff = mykey * nwords;
+
+  // staging unit of this thread: query pair (2sqp, 2sqp+1) x dims 4sdq .. 4sdq+3; lanes run
+  // over the query pairs so the transposed-image stores (put_t4) hit 64 distinct banks
+  const int sqp = tid & 15, sdq = tid >> 4;
+  float4 pq[2], pd[2], po[2];
+  float pl = 0.f;
+  uint32_t pm = 0;
+  auto ld_tile = [&](int qt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int qr = qt + 2 * sqp + i;
+      const int r = qr < S ? qr : S - 1;
+      pq[i] = *reinterpret_cast<const float4*>(base + (int64_t)r * H3 + 4 * sdq);
+      pd[i] = *reinterpret_cast<const float4*>(dout_b + (int64_t)r * H + 4 * sdq);
+      po[i] = *reinterpret_cast<const float4*>(out_b + (int64_t)r * H + 4 * sdq);
+    }
+    const int lq = qt + (tid & 31);
+    pl = lse_bh[lq < S ? lq : S - 1];
+    if (kDrop) pm = dmask_bh[moff + (qt >> 5)];
+  };
+  // (q + bias) / 8 of the prefetched tile
+  auto qvals = [&](float (&q0)[4], float (&q1)[4]) {
+    const float a[8] = {pq[0].x, pq[0].y, pq[0].z, pq[0].w, pq[1].x, pq[1].y, pq[1].z, pq[1].w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float bj = qbias ? qbias[4 * sdq + j] : 0.f;
+      q0[j] = (a[j] + bj) * scale;
+      q1[j] = (a[4 + j] + bj) * scale;
+    }
+  };
+  // the prefetched tile's max |Q|, |dO| -> this wave's slots
+  auto tile_max = [&]() {
+    float q0[4], q1[4];
+    qvals(q0, q1);
+    float mq = 0.f, md = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) mq = fmaxf(mq, fmaxf(fabsf(q0[j]), fabsf(q1[j])));
+    md = fmaxf(fmaxf(fmaxf(fabsf(pd[0].x), fabsf(pd[0].y)), fmaxf(fabsf(pd[0].z), fabsf(pd[0].w))),
+               fmaxf(fmaxf(fabsf(pd[1].x), fabsf(pd[1].y)), fmaxf(fabsf(pd[1].z), fabsf(pd[1].w))));
+    mq = wave_max(mq);
+    md = wave_max(md);
+    if (lane == 0) {
+      ScQ[w] = mq;
+      ScD[w] = md;
+    }
+  };
+  auto max4 = [&](const float* p) { return fmaxf(fmaxf(p[0], p[1]), fmaxf(p[2], p[3])); };
+
+  ld_tile(0);
+  __syncthreads();   // block max |K|, |V| published
+  const int ek = f16_scale_exp(max4(ScQ)), ev = f16_scale_exp(max4(ScD));
+  const float sk = ldexpf(1.f, ek), sv = ldexpf(1.f, ev);
+  f16x8 kf[4][2], vf[4][2];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    sp8(kx[ks], sk, kf[ks]);
+    sp8(vx[ks], sv, vf[ks]);
+  }
+  // ---- K^T pieces of the 128 keys (natural key order) for dQ: 64 key pairs x 16 dim quads
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int u = tid + 256 * i, kp = u & 63, dq = u >> 6;   // lanes over key pairs: conflict-free put_t4
+    const int k0 = kbase + 2 * kp < S ? kbase + 2 * kp : S - 1;
+    const int k1 = kbase + 2 * kp + 1 < S ? kbase + 2 * kp + 1 : S - 1;
+    const float4 a = *reinterpret_cast<const float4*>(base + (int64_t)k0 * H3 + H + 4 * dq);
+    const float4 c = *reinterpret_cast<const float4*>(base + (int64_t)k1 * H3 + H + 4 * dq);
+    float fa[4] = {a.x, a.y, a.z, a.w}, fc[4] = {c.x, c.y, c.z, c.w};
+    if (kbias) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        fa[j] += kbias[4 * dq + j];
+        fc[j] += kbias[4 * dq + j];
+      }
+    }
+    uint2 pa[2], pc[2];
+    sp4(fa, sk, pa);
+    sp4(fc, sk, pc);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) put_t4(Kt + p * 64 * KTS, KTS, 4 * dq, 2 * kp, pa[p], pc[p]);
+  }
+  __syncthreads();   // every wave has read the K / V maxima
+  tile_max();
+  __syncthreads();
+  int eq = run_exp(max4(ScQ)), ed = run_exp(max4(ScD));   // running exponents of the Q / dO images
+
+  // dQ tiles of this wave (16x16x32 layout): queries 16qh .., dims 32dp2 .. and 32dp2 + 16 ..
+  const int qh = w & 1, dp2 = w >> 1;
+  const int r16 = lane & 15, kg = lane >> 4;
+
+  // accumulators and the exponents they are held at: dv = dV 2^(ep + dv_e), dk = dK 2^(dk_e)
+  f32x16 dv0 = {0}, dv1 = {0}, dk0 = {0}, dk1 = {0};
+  const int ep = f16_scale_exp(inv_keep);   // Pd <= 1 / keep
+  const float keep_s = ldexpf(inv_keep, ep), one_s = ldexpf(1.f, ep);
+  int dv_e = ed, es = kNoScale, dk_e = eq + kNoScale;
+  float cq0 = 0.f, cq1 = 0.f;
+
+  // split the prefetched tile into the piece images (+ bias, 1/8 on Q) at the running exponents,
+  // D = rowsum(dO * O), lse
+  auto stage = [&](int qt) {
+    float q0[4], q1[4];
+    qvals(q0, q1);
+    const float d0[4] = {pd[0].x, pd[0].y, pd[0].z, pd[0].w}, d1[4] = {pd[1].x, pd[1].y, pd[1].z, pd[1].w};
+    const float sq = ldexpf(1.f, eq), sd = ldexpf(1.f, ed);
+    uint2 q0p[2], q1p[2], d0p[2], d1p[2];
+    sp4(q0, sq, q0p);
+    sp4(q1, sq, q1p);
+    sp4(d0, sd, d0p);
+    sp4(d1, sd, d1p);
+    const int pos = vpos(2 * sqp);
+    // Q / dO image rows q with q2 ^ q3 ^ q4 = 1 hold their 16-B chunks pair-swapped (chunk ^ 1):
+    // 2-way instead of 4-way staging-store conflicts, conflict-free 16-B fragment reads
+    const int qcol = 8 * ((sdq >> 1) ^ (((sqp >> 1) ^ (sqp >> 2) ^ (sqp >> 3)) & 1)) + 4 * (sdq & 1);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      *reinterpret_cast<uint2*>(&Qs[p * 32 * RS + (2 * sqp) * RS + qcol]) = q0p[p];
+      *reinterpret_cast<uint2*>(&Qs[p * 32 * RS + (2 * sqp + 1) * RS + qcol]) = q1p[p];
+      *reinterpret_cast<uint2*>(&dOs[p * 32 * RS + (2 * sqp) * RS + qcol]) = d0p[p];
+      *reinterpret_cast<uint2*>(&dOs[p * 32 * RS + (2 * sqp + 1) * RS + qcol]) = d1p[p];
+      put_t4(Qt + p * 64 * TS, TS, 4 * sdq, pos, q0p[p], q1p[p]);
+      put_t4(dOt + p * 64 * TS, TS, 4 * sdq, pos, d0p[p], d1p[p]);
+    }
+    float e0 = pd[0].x * po[0].x + pd[0].y * po[0].y + pd[0].z * po[0].z + pd[0].w * po[0].w;
+    float e1 = pd[1].x * po[1].x + pd[1].y * po[1].y + pd[1].z * po[1].z + pd[1].w * po[1].w;
+    // this wave's 16 dims (lanes 16 apart), then one partial per wave: Ds[query][wave]
+    e0 += __shfl_xor(e0, 16, 64);
+    e1 += __shfl_xor(e1, 16, 64);
+    e0 += __shfl_xor(e0, 32, 64);
+    e1 += __shfl_xor(e1, 32, 64);
+    if (lane < 16) {
+      Ds[(2 * sqp) * 4 + w] = e0;
+      Ds[(2 * sqp + 1) * 4 + w] = e1;
+    }
+    if (tid < 32) Ls[tid] = qt + tid < S ? pl : INFINITY;   // rows past S: P = 0
+  };
+  auto load_img = [&](const uint16_t* img, int half, f16x8 (&t0)[2], f16x8 (&t1)[2]) {
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      t0[p] = *reinterpret_cast<const f16x8*>(&img[p * 64 * TS + l32 * TS + 8 * h + 16 * half]);
+      t1[p] = *reinterpret_cast<const f16x8*>(&img[p * 64 * TS + (32 + l32) * TS + 8 * h + 16 * half]);
+    }
+  };
+
+  stage(0);
+  uint32_t mnext = pm;
+  for (int qt = 0; qt < S; qt += 32) {
+    // tile qt is staged at exponents (eq, ed); every wave is done with the previous tile's dS
+    __syncthreads();
+    const uint32_t mword = mnext;
+    const bool more = qt + 32 < S;
+    if (more) ld_tile(qt + 32);   // in flight during this tile's math
+
+    // ---- S = Qs . K^T, dP = dO . V^T (queries on accumulator rows, keys on lanes)
+    f32x16 sa = {0}, dpa = {0};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      f16x8 qa[2], da[2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const int qc = 8 * ((2 * ks + h) ^ (((l32 >> 2) ^ (l32 >> 3) ^ (l32 >> 4)) & 1));   // stores' swizzle
+        qa[p] = *reinterpret_cast<const f16x8*>(&Qs[p * 32 * RS + l32 * RS + qc]);
+        da[p] = *reinterpret_cast<const f16x8*>(&dOs[p * 32 * RS + l32 * RS + qc]);
+      }
+      HX_X3(sa, qa, kf[ks]);
+      HX_X3(dpa, da, vf[ks]);
+    }
+    if (ed != dv_e) {   // the dO images' exponent dropped: bring dV along
+      rescale(dv0, ed - dv_e);
+      rescale(dv1, ed - dv_e);
+      dv_e = ed;
+    }
+    // ---- P, Pd (at 2^ep), dS in place; the wave's max |dS|
+    const float fs = ldexpf(1.f, -(eq + ek)), fd = ldexpf(1.f, -(ed + ev));
+    float smax = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qr = crow(r, h);
+      const float p = __expf(fmaf(sa[r], fs, mk) - Ls[qr]);
+      float keepf = 1.f, keeps = one_s;
+      if (kDrop) {
+        const bool kb = (mword >> qr) & 1;
+        keepf = kb ? inv_keep : 0.f;
+        keeps = kb ? keep_s : 0.f;
+      }
+      sa[r] = p * keeps;
+      const float4 dq4 = *reinterpret_cast<const float4*>(&Ds[4 * qr]);
+      const float ds = p * (dpa[r] * fd * keepf - ((dq4.x + dq4.y) + (dq4.z + dq4.w)));
+      dpa[r] = ds;
+      smax = fmaxf(smax, fabsf(ds));
+      dSf[qr * DSF + w * 32 + l32] = ds;
+    }
+    smax = wave_max(smax);
+    if (lane == 0) ScS[w] = smax;
+    {   // the wave's dS exponent (running, decreasing) and the dK accumulator's
+      const int es_new = min(es, run_exp(smax));
+      if (eq + es_new != dk_e) {
+        rescale(dk0, eq + es_new - dk_e);
+        rescale(dk1, eq + es_new - dk_e);
+        dk_e = eq + es_new;
+      }
+      es = es_new;
+    }
+    const float ss = ldexpf(1.f, es);
+    // ---- dV += Pd^T . dO, dK += dS^T . Qs over the two accumulator halves (k-slots = query rows)
+    {
+      f16x8 a[2], c[2], t0[2], t1[2];
+      sp8(acc8<0>(sa), 1.f, a);
+      sp8(acc8<0>(dpa), ss, c);
+      load_img(dOt, 0, t0, t1);
+      HX_X3(dv0, a, t0);
+      HX_X3(dv1, a, t1);
+      load_img(Qt, 0, t0, t1);
+      HX_X3(dk0, c, t0);
+      HX_X3(dk1, c, t1);
+    }
+    {
+      f16x8 a[2], c[2], t0[2], t1[2];
+      sp8(acc8<8>(sa), 1.f, a);
+      sp8(acc8<8>(dpa), ss, c);
+      load_img(dOt, 1, t0, t1);
+      HX_X3(dv0, a, t0);
+      HX_X3(dv1, a, t1);
+      load_img(Qt, 1, t0, t1);
+      HX_X3(dk0, c, t0);
+      HX_X3(dk1, c, t1);
+    }
+    if (more) tile_max();   // the next tile's max |Q|, |dO| (its loads have landed by now)
+    // every wave's dS and maxima are in LDS; the piece images of tile qt are free
+    __syncthreads();
+    const int et = run_exp(max4(ScS));   // this tile's dS exponent over the 128 keys
+    const float st = ldexpf(1.f, et);
+    if (more) {
+      eq = min(eq, run_exp(max4(ScQ)));
+      ed = min(ed, run_exp(max4(ScD)));
+    }
+    // ---- dQ = dS . K over the block's 128 keys (16x16x32 tiles)
+    f32x4 qa0 = {0.f, 0.f, 0.f, 0.f}, qa1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const float* src = &dSf[(qh * 16 + r16) * DSF + 32 * ks + 8 * kg];
+      const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
+      f16x8 a[2], b0[2], b1[2];
+      sp8(f32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w}, st, a);
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        b0[p] = *reinterpret_cast<const f16x8*>(&Kt[p * 64 * KTS + (32 * dp2 + r16) * KTS + 32 * ks + 8 * kg]);
+        b1[p] = *reinterpret_cast<const f16x8*>(&Kt[p * 64 * KTS + (32 * dp2 + 16 + r16) * KTS + 32 * ks + 8 * kg]);
+      }
+      HX_X3_16(qa0, a, b0);
+      HX_X3_16(qa1, a, b1);
+    }
+    if (more) {   // next tile's staging in the dQ MFMAs' shadow
+      stage(qt + 32);
+      mnext = pm;
+    }
+    const int eqo = -(et + ek);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      qa0[r] = ldexpf(qa0[r], eqo) * scale;
+      qa1[r] = ldexpf(qa1[r], eqo) * scale;
+    }
+    const int q0 = qt + qh * 16 + 4 * kg;
+    if (dbias_part) {   // rows past S hold exact zeros (their P, hence dS, is 0)
+      cq0 += (qa0[0] + qa0[1]) + (qa0[2] + qa0[3]);
+      cq1 += (qa1[0] + qa1[1]) + (qa1[2] + qa1[3]);
+    }
+    const int dcol = 32 * dp2 + r16;
+    if (single) {
+      float* dq = dqkv_b + (int64_t)q0 * H3 + dcol;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (q0 + r >= S) continue;
+        dq[r * H3] = qa0[r];
+        dq[r * H3 + 16] = qa1[r];
+        am = fmaxf(am, fmaxf(fabsf(qa0[r]), fabsf(qa1[r])));
+      }
+    } else {
+      float* dq = dqa_b + (int64_t)q0 * dq_ld + dcol;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (q0 + r >= S) continue;
+        atomicAdd(dq + r * dq_ld, qa0[r]);
+        atomicAdd(dq + r * dq_ld + 16, qa1[r]);
+      }
+    }
+  }
+  // ---- undo the accumulators' scales: dK (against pre-scaled Q: already scaled by 1/8), dV
+  rescale(dk0, -dk_e);
+  rescale(dk1, -dk_e);
+  rescale(dv0, -(ep + dv_e));
+  rescale(dv1, -(ep + dv_e));
+  if (dbias_part) {
+    // QKV-bias gradient = column sums of dQ, dK, dV: one row of 3H partials per
+    // (batch, key block), folded into the bias-grad slots afterwards (attention.hip)
+    float sk0 = 0.f, sk1 = 0.f, sv0 = 0.f, sv1 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sk0 += dk0[r]; sk1 += dk1[r]; sv0 += dv0[r]; sv1 += dv1[r];
+    }
+    sk0 += __shfl_xor(sk0, 32, 64); sk1 += __shfl_xor(sk1, 32, 64);
+    sv0 += __shfl_xor(sv0, 32, 64); sv1 += __shfl_xor(sv1, 32, 64);
+    cq0 += __shfl_xor(cq0, 16, 64); cq0 += __shfl_xor(cq0, 32, 64);
+    cq1 += __shfl_xor(cq1, 16, 64); cq1 += __shfl_xor(cq1, 32, 64);
+    __syncthreads();   // every wave is done with dSf
+    float* red = dSf;   // [4 waves][3][64] floats
+    if (lane < 32) {
+      red[(w * 3 + 1) * 64 + l32] = sk0; red[(w * 3 + 1) * 64 + 32 + l32] = sk1;
+      red[(w * 3 + 2) * 64 + l32] = sv0; red[(w * 3 + 2) * 64 + 32 + l32] = sv1;
+    }
+    if (lane < 16) {   // dQ columns 32dp2 + lane and 32dp2 + 16 + lane of this wave's query half
+      red[(w * 3) * 64 + 32 * dp2 + lane] = cq0;
+      red[(w * 3) * 64 + 32 * dp2 + 16 + lane] = cq1;
+    }
+    __syncthreads();
+    if (tid < 192) {
+      const int part = tid >> 6, c = tid & 63;
+      float v;
+      if (part == 0) {   // waves (0,1) own dQ columns 0..31, waves (2,3) own 32..63
+        const int wa = c < 32 ? 0 : 2;
+        v = red[(wa * 3) * 64 + c] + red[((wa + 1) * 3) * 64 + c];
+      } else {
+        v = (red[(0 * 3 + part) * 64 + c] + red[(1 * 3 + part) * 64 + c]) +
+            (red[(2 * 3 + part) * 64 + c] + red[(3 * 3 + part) * 64 + c]);
+      }
+      dbias_part[((int64_t)b * gridDim.x + blockIdx.x) * H3 + part * H + hd * D + c] = v;
+    }
+  }
+  {
+    // ---- epilogue: dK, dV
+    float* dk = dqkv + (int64_t)b * S * H3 + H + hd * D;
+    float* dvp = dqkv + (int64_t)b * S * H3 + 2 * H + hd * D;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kbase + w * 32 + crow(r, h);
+      if (key >= S) continue;
+      dk[(int64_t)key * H3 + l32] = dk0[r];
+      dk[(int64_t)key * H3 + 32 + l32] = dk1[r];
+      dvp[(int64_t)key * H3 + l32] = dv0[r];
+      dvp[(int64_t)key * H3 + 32 + l32] = dv1[r];
+      am = fmaxf(am, fmaxf(fmaxf(fabsf(dk0[r]), fabsf(dk1[r])), fmaxf(fabsf(dv0[r]), fabsf(dv1[r]))));
+    }
+    if (amax_part && single) {
+      __shared__ float red_am[4];
+      am = wave_max(am);
+      if (lane == 0) red_am[w] = am;
+      __syncthreads();
+      if (tid == 0)
+        amax_part[(int64_t)blockIdx.z * gridDim.y + blockIdx.y] =
+            fmaxf(fmaxf(red_am[0], red_am[1]), fmaxf(red_am[2], red_am[3]));
+    }
+  }
+}
+
+#undef HX_X3_16
+#undef HX_X3
+
+}  // namespace
+
+void hx_attn_bwd_f16(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,
+                     const float* out, const float* lse, const uint32_t* dmask, float* dqkv, float* dq_acc, int dq_ld,
+                     int B, int S, int nh, float keep, hipStream_t s, float* amax_part) {
+  dim3 grid((S + 127) / 128, nh, B);
+  static bool attr = false;
+  if (!attr) {   // > 64 KiB of dynamic LDS needs an explicit opt-in (gfx950: 160 KiB per CU)
+    const void* k[2] = {reinterpret_cast<const void*>(&attn_bwd_f16_k<true>),
+                        reinterpret_cast<const void*>(&attn_bwd_f16_k<false>)};
+    for (const void* f : k) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, BWD_SMEM);
+    attr = true;
+  }
+  if (keep < 1.f)
+    attn_bwd_f16_k<true><<<grid, 256, BWD_SMEM, s>>>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv, dq_acc,
+                                                     dq_ld, S, nh, keep, amax_part);
+  else
+    attn_bwd_f16_k<false><<<grid, 256, BWD_SMEM, s>>>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv,
+                                                      dq_acc, dq_ld, S, nh, keep, amax_part);
+}

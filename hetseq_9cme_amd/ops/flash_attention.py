@@ -7,9 +7,10 @@ to [B, S, H].  The additive mask is the reference's (1 - m) * -10000 (not -inf).
 GPU path: the fused flash-style HIP kernel (``_C.attn_fwd`` / ``attn_bwd``,
 csrc/kernels/attention.hip) for head_dim 64 at any sequence length (keys past
 S are masked, rows past S are neither computed into nor stored), with fp32 or
-bf16 activations (bf16 activations: bf16 MFMA, attention_bf16.hip; fp32 activations: the
-products as six bf16 piece passes, attention_x6.hip, fp32-exact class, from 4096 token rows
-under ``--fp32-gemm fp16x3``; fp32 MFMA below that and under ``--fp32-gemm native``);
+bf16 activations (bf16 activations: bf16 MFMA, attention_bf16.hip; fp32 activations under
+``--fp32-gemm fp16x3`` from 4096 token rows: the forward's products as six bf16 piece passes,
+attention_x6.hip, the backward's as three fp16 passes over scaled two-piece operands,
+attention_f16.hip; fp32 MFMA below that and under ``--fp32-gemm native``);
 other shapes / dtypes use the composite below (batched GEMMs + softmax), which
 is also the CPU path and the test oracle.
 """
@@ -108,8 +109,9 @@ class _AttnFn(torch.autograd.Function):
             # projection's data / weight gradient GEMMs
             am = torch.empty(qkv.shape[0] * num_heads, dtype=torch.float32, device=qkv.device) \
                 if gemm16.enabled() and qkv.shape[1] <= 128 else None
-            dqkv, dbias = C().attn_bwd_x6(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep,
-                                          ctx.bias, *slots, am)
+            # products as three fp16 passes over scaled two-piece operands (attention_f16.hip)
+            dqkv, dbias = C().attn_bwd_f16(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep,
+                                           ctx.bias, *slots, am)
             gemm16.attach(dqkv, am)
         else:
             dqkv, dbias = C().attn_bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep, ctx.bias,

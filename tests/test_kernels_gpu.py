@@ -621,3 +621,63 @@ def test_attention_x6_backward_fp32_exact_class(dev, S, with_bias, keep):
         e_db = ((g6[1].double() - db_ref).abs().max() / db_ref.abs().max()).item()
         e_db32 = ((g32[1].double() - db_ref).abs().max() / db_ref.abs().max()).item()
         assert e_db < 8 * max(e_db32, 1e-7) and e_db < 2e-5, (e_db, e_db32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('S,with_bias,keep,case', [(128, False, 0.9, 'plain'), (77, True, 0.9, 'plain'),
+                                                   (200, False, 1.0, 'plain'), (512, True, 0.9, 'plain'),
+                                                   (640, True, 1.0, 'plain'), (128, True, 0.9, 'tiny'),
+                                                   (384, True, 0.9, 'ramp'), (256, False, 1.0, 'ramp')])
+def test_attention_f16_backward_fp32_class(dev, S, with_bias, keep, case):
+    """fp32 attention backward on fp16 MFMA (attention_f16.hip: three passes over scaled two-piece
+    operands): dQ / dK / dV and the QKV-bias gradient against an fp64 autograd reference on the
+    same dropout bits, row by row, next to the fp32-MFMA kernel's error.  'tiny': a 1e-8 gradient
+    (the scales follow it); 'ramp': Q and dO rows spanning 2^-16 .. 2^4 over the sequence (the
+    running exponents drop tile after tile and the dK / dV accumulators are rescaled)."""
+    from hetseq_9cme_amd.ops._ext import C
+    torch.manual_seed(2)
+    B, nh, d = 2, 4, 64
+    H = nh * d
+    qkv = 2 * torch.randn(B, S, 3 * H, device=dev)
+    dout = torch.randn(B, S, H, device=dev)
+    if case == 'tiny':
+        dout = dout * 1e-8
+    elif case == 'ramp':
+        r = torch.pow(2.0, torch.linspace(-16, 4, S, device=dev))
+        dout = dout * r[None, :, None]
+        qkv[:, :, :H] *= torch.pow(2.0, torch.linspace(-6, 3, S, device=dev))[None, :, None]
+    bias = (0.5 * torch.randn(3 * H, device=dev)) if with_bias else None
+    mask = torch.ones(B, S, device=dev)
+    mask[1, S - 29:] = 0
+    mb = ((1 - mask) * -10000.0).contiguous()
+    out, lse, dm = C().attn_fwd(qkv, mb, nh, keep, _seed(dev, 99), 3, bias)
+    g16 = C().attn_bwd_f16(dout, qkv, mb, out, lse, dm, nh, keep, bias, None, None, None)
+    g32 = C().attn_bwd(dout, qkv, mb, out, lse, dm, nh, keep, bias, None, None, None)
+
+    x = (qkv.double() + (bias.double() if bias is not None else 0)).requires_grad_(True)
+    q = x.view(B, S, 3, nh, d).permute(2, 0, 3, 1, 4)
+    p = torch.softmax(q[0] @ q[1].transpose(-1, -2) / 8.0 + mb.double()[:, None, None, :], -1)
+    if keep < 1.0:
+        bits = dm.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+        Sp = dm.shape[2]
+        km = ((bits.unsqueeze(-1) >> torch.arange(32, device=dev)) & 1).reshape(B, nh, Sp, Sp)
+        p = p * km[:, :, :S, :S].transpose(-1, -2).double() / keep
+    ref = (p @ q[2]).permute(0, 2, 1, 3).reshape(B, S, H)
+    ref.backward(dout.double())
+    gref = x.grad.view(B, S, 3, nh, d)
+
+    def err(g):   # worst row (token, head) of each of dQ / dK / dV, relative to that row's max
+        g = g.double().view(B, S, 3, nh, d)
+        e = (g - gref).abs().amax(-1)
+        m = gref.abs().amax(-1)
+        live = m > 0
+        return [(e[:, :, i][live[:, :, i]] / m[:, :, i][live[:, :, i]]).max().item() for i in range(3)]
+
+    e16, e32 = err(g16[0]), err(g32[0])
+    for a, c in zip(e16, e32):
+        assert a < 16 * max(c, 1e-7) and a < 1e-4, (e16, e32)
+    if with_bias:
+        db_ref = gref.sum((0, 1)).reshape(-1)
+        e_db = ((g16[1].double() - db_ref).abs().max() / db_ref.abs().max()).item()
+        e_db32 = ((g32[1].double() - db_ref).abs().max() / db_ref.abs().max()).item()
+        assert e_db < 16 * max(e_db32, 1e-7) and e_db < 1e-4, (e_db, e_db32)

@@ -331,7 +331,8 @@ Tensor softmax_xent_(Tensor logits, OptT bias, Tensor labels, int64_t ignore_ind
 
 // ------------------------------------------------------------------ attention
 std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed, int64_t stream,
-                             OptT bias, bool split = false, OptT amax_out = OptT()) {
+                             OptT bias, int split = 0, OptT amax_out = OptT()) {
+  // split: 0 none, 1 bf16 x6 pieces (attention_x6.hip), 2 fp16x3 (attention_f16.hip)
   check_cuda(qkv, "qkv");
   const int bf = act_bf16(qkv);
   check_f32(mask_bias, "mask_bias");
@@ -353,11 +354,16 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
   else dmask = torch::empty({0}, qkv.options().dtype(torch::kInt32));
   uint32_t* dm = keep < 1.0 ? reinterpret_cast<uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr;
   if (split) {
-    TORCH_CHECK(!bf, "attn_fwd_x6: fp32 activations only");
-    hx_attn_fwd_x6(qkv.data_ptr<float>(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(),
-                   out.data_ptr<float>(), lse.data_ptr<float>(), dm, (int)B, (int)S, (int)nh, (float)keep,
-                   seed_ptr(seed), (uint64_t)stream, cur_stream(qkv),
-                   amax_ptr(amax_out, ((S + 127) / 128) * nh * B * 4, "attn_fwd_x6 amax"));
+    TORCH_CHECK(!bf, "attn_fwd_x6 / attn_fwd_f16: fp32 activations only");
+    float* am = amax_ptr(amax_out, ((S + 127) / 128) * nh * B * 4, "attn_fwd amax");
+    if (split == 2)
+      hx_attn_fwd_f16(qkv.data_ptr<float>(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(),
+                      out.data_ptr<float>(), lse.data_ptr<float>(), dm, (int)B, (int)S, (int)nh, (float)keep,
+                      seed_ptr(seed), (uint64_t)stream, cur_stream(qkv), am);
+    else
+      hx_attn_fwd_x6(qkv.data_ptr<float>(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(),
+                     out.data_ptr<float>(), lse.data_ptr<float>(), dm, (int)B, (int)S, (int)nh, (float)keep,
+                     seed_ptr(seed), (uint64_t)stream, cur_stream(qkv), am);
   } else {
     hx_attn_fwd(bf, qkv.data_ptr(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(), out.data_ptr(),
                 lse.data_ptr<float>(), dm, (int)B, (int)S, (int)nh, (float)keep, seed_ptr(seed), (uint64_t)stream,
@@ -369,7 +375,12 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
 // fp32 attention forward on the bf16 matrix cores (split pieces, attention_x6.hip): {out, lse, dmask}
 std::vector<Tensor> attn_fwd_x6(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed,
                                 int64_t stream, OptT bias, OptT amax_out) {
-  return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, true, amax_out);
+  return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, 1, amax_out);
+}
+// the same on the fp16 matrix cores (fp16x3, attention_f16.hip)
+std::vector<Tensor> attn_fwd_f16(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed,
+                                 int64_t stream, OptT bias, OptT amax_out) {
+  return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, 2, amax_out);
 }
 
 // returns {dqkv, dbias} (dbias: [3H] fp32 when bias is given -- written into dbq/dbk/dbv
@@ -838,6 +849,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_fwd", [](Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed, int64_t stream,
                         OptT bias) { return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, false); });
   m.def("attn_fwd_x6", &attn_fwd_x6, py::arg("qkv"), py::arg("mask_bias"), py::arg("nh"), py::arg("keep"),
+        py::arg("seed"), py::arg("stream"), py::arg("bias"), py::arg("amax_out") = py::none());
+  m.def("attn_fwd_f16", &attn_fwd_f16, py::arg("qkv"), py::arg("mask_bias"), py::arg("nh"), py::arg("keep"),
         py::arg("seed"), py::arg("stream"), py::arg("bias"), py::arg("amax_out") = py::none());
   m.def("attn_bwd", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
                        double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv) {

@@ -76,6 +76,9 @@ void hx_attn_bwd_x6(const float* qkv, const float* bias, float* dbias_part, cons
                     int B, int S, int nh, float keep, hipStream_t s, float* amax_part = nullptr);
 // the same backward on the fp16 matrix cores (three passes over scaled two-piece operands,
 // attention_f16.hip: --fp32-gemm fp16x3)
+void hx_attn_fwd_f16(const float* qkv, const float* bias, const float* maskb, float* out, float* lse,
+                     uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream,
+                     hipStream_t s, float* amax_part = nullptr);
 void hx_attn_bwd_f16(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,
                      const float* out, const float* lse, const uint32_t* dmask, float* dqkv, float* dq_acc, int dq_ld,
                      int B, int S, int nh, float keep, hipStream_t s, float* amax_part = nullptr);

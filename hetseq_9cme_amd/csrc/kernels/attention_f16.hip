@@ -1,4 +1,4 @@
-// fp32 attention backward on the fp16 matrix cores (--fp32-gemm fp16x3).
+// fp32 attention on the fp16 matrix cores (--fp32-gemm fp16x3): backward and forward.
 //
 // Same math and I/O as the other attention backward kernels (reference
 // hetseq/bert_modeling.py:351-377 differentiated): packed fp32 [B, S, 3H] QKV (+ the
@@ -553,10 +553,299 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   }
 }
 
+// ============================================================================ forward
+// The x6 forward's structure (attention_x6.hip) with two fp16 pieces and three passes per product:
+// one workgroup = 4 waves x 32 queries ON THE LANES, 64-key tiles, keys on the accumulator rows
+// (S^T = K . Q^T with Q's piece fragments in VGPRs), K staged as piece images [key][dim], V as
+// transposed piece images [dim][vpos(key)] so O^T += V^T . P^T takes P's pieces straight from the
+// accumulator.  Exponents: Q one per wave (fixed); K and V one per 64-key tile, from the tile's
+// max |x| reduced over the workgroup before it is split (S is unscaled per tile; the tile-to-tile
+// change of V's exponent rides in the online-softmax rescale of the O accumulator); P <= 1 / keep
+// fixed.  Single-buffered images (37 KiB: two workgroups per CU), the next tile's fp32 loads in
+// flight in registers during the current tile's math.
+template <bool kDrop>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd_f16_k(
+    const float* __restrict__ qkv, const float* __restrict__ qkv_bias, const float* __restrict__ maskb,
+    float* __restrict__ out, float* __restrict__ lse, uint32_t* __restrict__ dmask, int S, int nh, float keep,
+    const uint64_t* __restrict__ seedp, uint64_t stream, float* __restrict__ amax_part) {
+  const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[2][64 * RS];   // [piece][key][dim]
+  __shared__ __attribute__((aligned(16))) uint16_t Vt[2][64 * RS];   // [piece][dim][vpos(key)]
+  __shared__ float Ms[64];
+  __shared__ float Mx[8];                                             // per-wave max |K|, |V|
+  constexpr int kMaxStagedTiles = 8;   // S <= 512: mask words staged, stored after the loop
+  __shared__ uint32_t Wst[kDrop ? kMaxStagedTiles * 256 : 1];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
+  const int b = blockIdx.z, hd = blockIdx.y;
+  const int H = nh * D, H3 = 3 * H;
+  const int q = blockIdx.x * 128 + w * 32 + l32;
+  const int qc = q < S ? q : S - 1;            // rows past S: clamped loads, no stores
+  const int Sp = (S + 127) & ~127;
+  const int q0w = blockIdx.x * 128 + w * 32;
+  const uint32_t t16 = (uint32_t)(keep * 65536.f + 0.5f);
+  const float inv_keep = 1.f / keep;
+  const float* base = qkv + (int64_t)b * S * H3 + hd * D;
+  const int64_t bh = (int64_t)b * nh + hd;
+  const float* kbias = qkv_bias ? qkv_bias + H + hd * D : nullptr;
+  const float* vbias = qkv_bias ? qkv_bias + 2 * H + hd * D : nullptr;
+
+  // Q pieces: lane (query, half h), fragment ks = dims 16ks + 8h .. +7, scaled by 1/8 (exact) and
+  // by the wave's exponent
+  f16x8 qf[4][2];
+  int eq;
+  {
+    const float* qp = base + (int64_t)qc * H3 + 8 * h;
+    f32x8 x[4];
+    float m = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      x[ks] = ld8(qp + 16 * ks, qkv_bias ? qkv_bias + hd * D + 16 * ks + 8 * h : nullptr) * 0.125f;
+      m = fmaxf(m, amax8(x[ks]));
+    }
+    eq = f16_scale_exp(wave_max(m));
+    const float sq = ldexpf(1.f, eq);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) sp8(x[ks], sq, qf[ks]);
+  }
+
+  // ---- tile staging: K rows (2 x 8 dims per thread), V key pairs x 4 dims (2 x 2 x 4)
+  float4 kr[2][2], vr[2][2];
+  float mr = 0.f;
+  auto stage_load = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 256 * i, row = e >> 3, c8 = (e & 7) * 8;
+      const int key = kt + row < S ? kt + row : S - 1;
+      const float* kp = base + (int64_t)key * H3 + H + c8;
+      kr[i][0] = *reinterpret_cast<const float4*>(kp);
+      kr[i][1] = *reinterpret_cast<const float4*>(kp + 4);
+      const int kp2 = e & 31, dq = e >> 5;   // lanes over key pairs: the Vt stores spread over the banks
+      const int k0 = kt + 2 * kp2 < S ? kt + 2 * kp2 : S - 1, k1 = kt + 2 * kp2 + 1 < S ? kt + 2 * kp2 + 1 : S - 1;
+      vr[i][0] = *reinterpret_cast<const float4*>(base + (int64_t)k0 * H3 + 2 * H + 4 * dq);
+      vr[i][1] = *reinterpret_cast<const float4*>(base + (int64_t)k1 * H3 + 2 * H + 4 * dq);
+    }
+    if (tid < 64) mr = kt + tid < S ? maskb[(int64_t)b * S + kt + tid] : -INFINITY;
+  };
+  // (+ bias) values of the loaded tile
+  auto kvals = [&](int i, f32x8& f) {
+    const int c8 = ((tid + 256 * i) & 7) * 8;
+    f = f32x8{kr[i][0].x, kr[i][0].y, kr[i][0].z, kr[i][0].w, kr[i][1].x, kr[i][1].y, kr[i][1].z, kr[i][1].w};
+    if (kbias) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] += kbias[c8 + j];
+    }
+  };
+  auto vvals = [&](int i, float (&v0)[4], float (&v1)[4]) {
+    const int dq = (tid + 256 * i) >> 5;
+    const float a[8] = {vr[i][0].x, vr[i][0].y, vr[i][0].z, vr[i][0].w, vr[i][1].x, vr[i][1].y, vr[i][1].z, vr[i][1].w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float bj = vbias ? vbias[4 * dq + j] : 0.f;
+      v0[j] = a[j] + bj;
+      v1[j] = a[4 + j] + bj;
+    }
+  };
+  // the loaded tile's max |K|, |V| -> this wave's slots (read after the next barrier)
+  auto tile_max = [&]() {
+    float mk = 0.f, mv = 0.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      f32x8 f;
+      kvals(i, f);
+      mk = fmaxf(mk, amax8(f));
+      float v0[4], v1[4];
+      vvals(i, v0, v1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mv = fmaxf(mv, fmaxf(fabsf(v0[j]), fabsf(v1[j])));
+    }
+    mk = wave_max(mk);
+    mv = wave_max(mv);
+    if (lane == 0) {
+      Mx[w] = mk;
+      Mx[4 + w] = mv;
+    }
+  };
+  auto stage_store = [&](float sk, float sv) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int e = tid + 256 * i, row = e >> 3, c8 = (e & 7) * 8;
+      f32x8 f;
+      kvals(i, f);
+      f16x8 p[2];
+      sp8(f, sk, p);
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) *reinterpret_cast<f16x8*>(&Ks[pc][row * RS + c8]) = p[pc];
+      const int kp2 = e & 31, dq = e >> 5;
+      float v0[4], v1[4];
+      vvals(i, v0, v1);
+      uint2 a0[2], a1[2];
+      sp4(v0, sv, a0);   // key 2kp2, dims 4dq .. +3
+      sp4(v1, sv, a1);   // key 2kp2 + 1
+      constexpr int RW = RS / 2;   // row stride in 32-bit words
+      const int pos = vpos(2 * kp2) >> 1;
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) {
+        uint32_t* vt = reinterpret_cast<uint32_t*>(Vt[pc]);
+        vt[(4 * dq + 0) * RW + pos] = (a0[pc].x & 0xffffu) | (a1[pc].x << 16);
+        vt[(4 * dq + 1) * RW + pos] = (a0[pc].x >> 16) | (a1[pc].x & 0xffff0000u);
+        vt[(4 * dq + 2) * RW + pos] = (a0[pc].y & 0xffffu) | (a1[pc].y << 16);
+        vt[(4 * dq + 3) * RW + pos] = (a0[pc].y >> 16) | (a1[pc].y & 0xffff0000u);
+      }
+    }
+    if (tid < 64) Ms[tid] = mr;
+  };
+  auto max4 = [&](const float* p) { return fmaxf(fmaxf(p[0], p[1]), fmaxf(p[2], p[3])); };
+
+  f32x16 o0 = {0}, o1 = {0};
+  float m_run = -INFINITY, l_run = 0.f;
+  const int ep = f16_scale_exp(inv_keep);   // P' <= 1 / keep
+  const float ps = ldexpf(1.f, ep);
+  int ek, ev, ev_o = 0;                     // the tile's K / V exponents; o holds O 2^(ep + ev_o)
+  const int nt = (S + 63) >> 6;
+  stage_load(0);
+  tile_max();
+  __syncthreads();
+  ek = f16_scale_exp(max4(Mx));
+  ev = f16_scale_exp(max4(Mx + 4));
+  ev_o = ev;
+  stage_store(ldexpf(1.f, ek), ldexpf(1.f, ev));
+  __syncthreads();
+
+  for (int t = 0; t < nt; ++t) {
+    const int kt = t * 64;
+    if (t + 1 < nt) stage_load(kt + 64);   // in flight during this tile's math
+
+    uint32_t keepbits[4] = {0u, 0u, 0u, 0u};
+    if (kDrop) {
+      // Philox chain first: it has no input from the tile's math and fills the MFMA shadow
+      const uint64_t cbase = hx::attn::drop_counter(bh, S, q, Sp, kt, h);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) keepbits[j] = hx::keep8(seed, stream, cbase + j, t16);
+    }
+    // ---- S^T = K . Q^T, two 32-key blocks, three piece passes each
+    f32x16 s0 = {0}, s1 = {0};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      f16x8 ka[2], kb[2];
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) {
+        ka[pc] = *reinterpret_cast<const f16x8*>(&Ks[pc][l32 * RS + 16 * ks + 8 * h]);
+        kb[pc] = *reinterpret_cast<const f16x8*>(&Ks[pc][(32 + l32) * RS + 16 * ks + 8 * h]);
+      }
+      HX_X3(s0, ka, qf[ks]);
+      HX_X3(s1, kb, qf[ks]);
+    }
+    // unscale, + mask, running max, exp, row sum (the fp32 kernel's formulation)
+    const float fs = ldexpf(1.f, -(ek + eq));
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s0[r] = fmaf(s0[r], fs, Ms[crow(r, h)]);
+      s1[r] = fmaf(s1[r], fs, Ms[32 + crow(r, h)]);
+      mx = fmaxf(mx, fmaxf(s0[r], s1[r]));
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = __expf(m_run - m_new);
+    float rs = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s0[r] = __expf(s0[r] - m_new);
+      s1[r] = __expf(s1[r] - m_new);
+      rs += s0[r] + s1[r];
+    }
+    rs += __shfl_xor(rs, 32, 64);
+    l_run = l_run * alpha + rs;
+    m_run = m_new;
+    // the online-softmax rescale of O, with the move to this tile's V exponent folded in
+    const float oa = ldexpf(alpha, ev - ev_o);
+    ev_o = ev;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      o0[r] *= oa;
+      o1[r] *= oa;
+    }
+    if (kDrop) {
+      uint32_t myword = 0;
+      hx::attn::drop_step<0>(s0, s1, keepbits, inv_keep, myword);
+      if (Sp <= kMaxStagedTiles * 64)
+        Wst[t * 256 + w * 64 + lane] = myword;
+      else
+        dmask[((int64_t)bh * Sp + kt + lane) * (Sp >> 5) + (q0w >> 5)] = myword;
+    }
+    // ---- O^T += V^T . P^T : P's pieces from the accumulator, V^T rows from the piece images
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      f16x8 pp[2];
+      if (g == 0) sp8(acc8<0>(s0), ps, pp);
+      else if (g == 1) sp8(acc8<8>(s0), ps, pp);
+      else if (g == 2) sp8(acc8<0>(s1), ps, pp);
+      else sp8(acc8<8>(s1), ps, pp);
+      f16x8 va[2], vb[2];
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) {
+        va[pc] = *reinterpret_cast<const f16x8*>(&Vt[pc][l32 * RS + 16 * g + 8 * h]);
+        vb[pc] = *reinterpret_cast<const f16x8*>(&Vt[pc][(32 + l32) * RS + 16 * g + 8 * h]);
+      }
+      HX_X3(o0, va, pp);
+      HX_X3(o1, vb, pp);
+    }
+    if (t + 1 < nt) {
+      tile_max();                // the next tile's max |K|, |V| (its loads have landed)
+      __syncthreads();           // every wave is done with this tile's images; maxima published
+      ek = f16_scale_exp(max4(Mx));
+      ev = f16_scale_exp(max4(Mx + 4));
+      stage_store(ldexpf(1.f, ek), ldexpf(1.f, ev));
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue
+  if (kDrop && Sp <= kMaxStagedTiles * 64) {
+    for (int t = 0; t < nt; ++t)
+      dmask[((int64_t)bh * Sp + t * 64 + lane) * (Sp >> 5) + (q0w >> 5)] = Wst[t * 256 + w * 64 + lane];
+  }
+  const float inv_l = ldexpf(1.f / l_run, -(ep + ev_o));
+  if (amax_part) {
+    // max |context| of this wave's 32 queries (the fp16x3 attention-output GEMM's operand
+    // scale, ops/gemm16.py): one partial per wave, rows past S count 0
+    float am = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) am = fmaxf(am, fmaxf(fabsf(o0[i] * inv_l), fabsf(o1[i] * inv_l)));
+    if (q >= S) am = 0.f;
+    am = wave_max(am);
+    if (lane == 0) amax_part[(((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 4 + w] = am;
+  }
+  if (q >= S) return;
+  float* op = out + ((int64_t)b * S + q) * H + hd * D;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int d0 = 8 * g + 4 * h;
+    const float4 va =
+        make_float4(o0[4 * g] * inv_l, o0[4 * g + 1] * inv_l, o0[4 * g + 2] * inv_l, o0[4 * g + 3] * inv_l);
+    const float4 vb =
+        make_float4(o1[4 * g] * inv_l, o1[4 * g + 1] * inv_l, o1[4 * g + 2] * inv_l, o1[4 * g + 3] * inv_l);
+    *reinterpret_cast<float4*>(op + d0) = va;
+    *reinterpret_cast<float4*>(op + 32 + d0) = vb;
+  }
+  if (h == 0) lse[bh * S + q] = m_run + __logf(l_run);
+}
+
 #undef HX_X3_16
 #undef HX_X3
 
 }  // namespace
+
+void hx_attn_fwd_f16(const float* qkv, const float* bias, const float* maskb, float* out, float* lse,
+                     uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream,
+                     hipStream_t s, float* amax_part) {
+  dim3 grid((S + 127) / 128, nh, B);
+  if (keep < 1.f)
+    attn_fwd_f16_k<true><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream, amax_part);
+  else
+    attn_fwd_f16_k<false><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream, amax_part);
+}
 
 void hx_attn_bwd_f16(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,
                      const float* out, const float* lse, const uint32_t* dmask, float* dqkv, float* dq_acc, int dq_ld,

@@ -1,4 +1,4 @@
-"""Attention backward kernels side by side at the BERT-base shapes: the bf16 x6 kernel
+"""Attention kernels (backward, and forward timings) side by side at the BERT-base shapes: the bf16 x6 kernel
 (attention_x6.hip), the fp16x3 kernel (attention_f16.hip) and the fp32-MFMA kernel -- time per
 call (HIP events over back-to-back launches) and the worst-row error of dQ / dK / dV against an
 fp64 reference on a small slice.  ``python tools/probe/attn_bwd_probe.py``."""
@@ -41,6 +41,11 @@ def main():
         res = {}
         for name, f in (('x6', C().attn_bwd_x6), ('f16', C().attn_bwd_f16), ('fp32', C().attn_bwd)):
             res[name] = timed(lambda: f(dout, qkv, mb, out, lse, dm, nh, keep, bias, *slots))
+        fw = {}
+        for name, f in (('x6', C().attn_fwd_x6), ('f16', C().attn_fwd_f16), ('fp32', C().attn_fwd)):
+            fw[name] = timed(lambda: f(qkv, mb, nh, keep, seed, 3, bias))
+        print('B={} S={} forward: '.format(B, S) + ', '.join('{} {:.1f} us'.format(k, v) for k, v in fw.items()),
+              flush=True)
         flops = 5 * 2 * B * nh * S * S * d
         print('B={} S={}: '.format(B, S) + ', '.join(
             '{} {:.1f} us ({:.0f} TF/s fp32-equiv)'.format(k, v, flops / v * 1e-6) for k, v in res.items()),

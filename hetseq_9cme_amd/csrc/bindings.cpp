@@ -399,9 +399,10 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor o
   c10::hip::HIPGuardMasqueradingAsCUDA guard(qkv.device());
   // one key block per head (S <= 128): every dQKV element is written exactly once (no
   // memset).  Otherwise dQ partials from the S/128 key blocks are added atomically in
-  // fp32: into dqkv itself (fp32, zero-filled) or a [B, S, H] fp32 scratch (bf16).
+  // fp32: into dqkv itself (fp32, its dQ third zero-filled) or a [B, S, H] fp32 scratch (bf16).
   const bool multi = S > 128;
-  Tensor dqkv = (multi && !bf) ? torch::zeros_like(qkv) : torch::empty_like(qkv);
+  Tensor dqkv = torch::empty_like(qkv);
+  if (multi && !bf) dqkv.narrow(-1, 0, H).zero_();   // only the dQ third is accumulated into
   Tensor dq32;
   float* dq_acc = nullptr;
   int dq_ld = 0;

@@ -140,6 +140,25 @@ __device__ __forceinline__ void rescale(f32x16& v, int e) {
   for (int r = 0; r < 16; ++r) v[r] = ldexpf(v[r], e);
 }
 
+// (block, head, batch) of this workgroup, XCD-aware: the hardware deals consecutive workgroups
+// round-robin over the 8 XCDs, so the grid is walked so that the key (query) blocks of one head --
+// which read the same query (key) rows, and add into the same dQ rows -- run on the same XCD and
+// share its L2
+struct Blk {
+  int x, hd, b;
+};
+__device__ __forceinline__ Blk xcd_block() {
+  const int n = gridDim.x * gridDim.y * gridDim.z;
+  int id = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+  if ((n & 7) == 0) id = (id & 7) * (n >> 3) + (id >> 3);
+  Blk k;
+  k.x = id % gridDim.x;
+  id /= gridDim.x;
+  k.hd = id % gridDim.y;
+  k.b = id / gridDim.y;
+  return k;
+}
+
 template <bool kDrop>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void attn_bwd_f16_k(
     const float* __restrict__ qkv, const float* __restrict__ qkv_bias, float* __restrict__ dbias_part,
@@ -159,9 +178,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   float* ScQ = Sc, *ScD = Sc + 4, *ScS = Sc + 8;                         // [4 waves] each
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
-  const int b = blockIdx.z, hd = blockIdx.y;
+  const Blk blk = xcd_block();
+  const int b = blk.b, hd = blk.hd;
   const int H = nh * D, H3 = 3 * H;
-  const int kbase = blockIdx.x * 128;
+  const int kbase = blk.x * 128;
   const bool single = gridDim.x == 1;
   const int64_t bh = (int64_t)b * nh + hd;
   const float scale = 0.125f, inv_keep = 1.f / keep;
@@ -524,7 +544,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         v = (red[(0 * 3 + part) * 64 + c] + red[(1 * 3 + part) * 64 + c]) +
             (red[(2 * 3 + part) * 64 + c] + red[(3 * 3 + part) * 64 + c]);
       }
-      dbias_part[((int64_t)b * gridDim.x + blockIdx.x) * H3 + part * H + hd * D + c] = v;
+      dbias_part[((int64_t)b * gridDim.x + blk.x) * H3 + part * H + hd * D + c] = v;
     }
   }
   {
@@ -547,7 +567,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       if (lane == 0) red_am[w] = am;
       __syncthreads();
       if (tid == 0)
-        amax_part[(int64_t)blockIdx.z * gridDim.y + blockIdx.y] =
+        amax_part[(int64_t)b * gridDim.y + hd] =
             fmaxf(fmaxf(red_am[0], red_am[1]), fmaxf(red_am[2], red_am[3]));
     }
   }
@@ -577,12 +597,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   __shared__ uint32_t Wst[kDrop ? kMaxStagedTiles * 256 : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, h = lane >> 5, l32 = lane & 31;
-  const int b = blockIdx.z, hd = blockIdx.y;
+  const Blk blk = xcd_block();
+  const int b = blk.b, hd = blk.hd;
   const int H = nh * D, H3 = 3 * H;
-  const int q = blockIdx.x * 128 + w * 32 + l32;
+  const int q = blk.x * 128 + w * 32 + l32;
   const int qc = q < S ? q : S - 1;            // rows past S: clamped loads, no stores
   const int Sp = (S + 127) & ~127;
-  const int q0w = blockIdx.x * 128 + w * 32;
+  const int q0w = blk.x * 128 + w * 32;
   const uint32_t t16 = (uint32_t)(keep * 65536.f + 0.5f);
   const float inv_keep = 1.f / keep;
   const float* base = qkv + (int64_t)b * S * H3 + hd * D;
@@ -815,7 +836,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int i = 0; i < 16; ++i) am = fmaxf(am, fmaxf(fabsf(o0[i] * inv_l), fabsf(o1[i] * inv_l)));
     if (q >= S) am = 0.f;
     am = wave_max(am);
-    if (lane == 0) amax_part[(((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x) * 4 + w] = am;
+    if (lane == 0) amax_part[(((int64_t)b * gridDim.y + hd) * gridDim.x + blk.x) * 4 + w] = am;
   }
   if (q >= S) return;
   float* op = out + ((int64_t)b * S + q) * H + hd * D;

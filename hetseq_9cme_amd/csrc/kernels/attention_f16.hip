@@ -54,7 +54,8 @@ constexpr int KTS = 136;  // K^T [dim][128 keys] row stride (halves)
 constexpr int DSF = 132;  // fp32 dS [query][128 keys] row stride (floats): conflict-free dQ fragment reads
 constexpr int KT_B = 64 * KTS * 2, DS_B = 32 * DSF * 4, QS_B = 32 * RS * 2, QT_B = 64 * TS * 2;
 constexpr int NSC = 16;   // per-tile scalars: max |Q|, max |dO|, max |dS| per wave (+ spare)
-constexpr int BWD_SMEM = 2 * KT_B + DS_B + 2 * (2 * QS_B) + 2 * (2 * QT_B) + (32 + 128 + NSC) * 4;
+constexpr int VF_B = 4 * 4 * 2 * 64 * 16;   // each wave's V piece fragments (B operands of dP), 32 KiB
+constexpr int BWD_SMEM = 2 * KT_B + DS_B + 2 * (2 * QS_B) + 2 * (2 * QT_B) + VF_B + (32 + 128 + NSC) * 4;
 constexpr int kNoScale = 120;   // exponent of an operand seen only as zeros so far (no constraint)
 
 __device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
@@ -129,15 +130,37 @@ __device__ __forceinline__ float amax8(const f32x8 f) {
   for (int j = 0; j < 8; ++j) m = fmaxf(m, fabsf(f[j]));
   return m;
 }
+// max over the wave, in every lane: DPP within each row of 16 lanes (quad xor 1, xor 2, half-row
+// mirror, row mirror), then the four row maxima through readlane -- no LDS round trip
+template <int CTRL>
+__device__ __forceinline__ float dmax(float v) {
+  return fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false)));
+}
 __device__ __forceinline__ float wave_max(float m) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  return m;
+  m = dmax<0xB1>(m);    // quad_perm [1, 0, 3, 2]
+  m = dmax<0x4E>(m);    // quad_perm [2, 3, 0, 1]
+  m = dmax<0x141>(m);   // row_half_mirror
+  m = dmax<0x140>(m);   // row_mirror
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(m), 48));
+  return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
 }
 // v *= 2^e, every element (exact unless the result leaves the normal range)
 __device__ __forceinline__ void rescale(f32x16& v, int e) {
 #pragma unroll
   for (int r = 0; r < 16; ++r) v[r] = ldexpf(v[r], e);
+}
+// the same behind a wave-uniform branch that stays a branch (taken on the few tiles whose
+// exponent moves): the empty asm keeps the compiler from if-converting it into unconditional
+// ldexps and accumulator copies on every tile
+__device__ __forceinline__ void rescale2_if(bool c, f32x16& a, f32x16& b, int e) {
+  if (c) {
+    asm volatile("" ::: "memory");
+    rescale(a, e);
+    rescale(b, e);
+  }
 }
 
 // (block, head, batch) of this workgroup, XCD-aware: the hardware deals consecutive workgroups
@@ -172,7 +195,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   uint16_t* dOs = Qs + 2 * 32 * RS;                                      // [2][32][RS]
   uint16_t* Qt = dOs + 2 * 32 * RS;                                      // [2][64][TS]
   uint16_t* dOt = Qt + 2 * 64 * TS;                                      // [2][64][TS]
-  float* Ls = reinterpret_cast<float*>(dOt + 2 * 64 * TS);               // [32] lse
+  f16x8* Vf = reinterpret_cast<f16x8*>(dOt + 2 * 64 * TS);              // [4 waves][4 ks][2][64 lanes]
+  float* Ls = reinterpret_cast<float*>(smem + 2 * KT_B + DS_B + 4 * QS_B + 4 * QT_B + VF_B);   // [32] lse
   float* Ds = Ls + 32;                                                   // [32][4 waves] D partials
   float* Sc = Ds + 128;                                                  // per-tile scalars
   float* ScQ = Sc, *ScD = Sc + 4, *ScS = Sc + 8;                         // [4 waves] each
@@ -273,11 +297,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   __syncthreads();   // block max |K|, |V| published
   const int ek = f16_scale_exp(max4(ScQ)), ev = f16_scale_exp(max4(ScD));
   const float sk = ldexpf(1.f, ek), sv = ldexpf(1.f, ev);
-  f16x8 kf[4][2], vf[4][2];
+  // K's fragments stay in registers (B operands of S); V's go to this wave's LDS slots (read once
+  // per tile by dP): 32 fewer live VGPRs across the loop
+  f16x8 kf[4][2];
+  f16x8* vfw = Vf + w * 512 + lane;
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     sp8(kx[ks], sk, kf[ks]);
-    sp8(vx[ks], sv, vf[ks]);
+    f16x8 v2[2];
+    sp8(vx[ks], sv, v2);
+    vfw[(2 * ks) * 64] = v2[0];
+    vfw[(2 * ks + 1) * 64] = v2[1];
   }
   // ---- K^T pieces of the 128 keys (natural key order) for dQ: 64 key pairs x 16 dim quads
 #pragma unroll
@@ -383,14 +413,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
         qa[p] = *reinterpret_cast<const f16x8*>(&Qs[p * 32 * RS + l32 * RS + qc]);
         da[p] = *reinterpret_cast<const f16x8*>(&dOs[p * 32 * RS + l32 * RS + qc]);
       }
+      const f16x8 vfr[2] = {vfw[(2 * ks) * 64], vfw[(2 * ks + 1) * 64]};
       HX_X3(sa, qa, kf[ks]);
-      HX_X3(dpa, da, vf[ks]);
+      HX_X3(dpa, da, vfr);
     }
-    if (ed != dv_e) {   // the dO images' exponent dropped: bring dV along
-      rescale(dv0, ed - dv_e);
-      rescale(dv1, ed - dv_e);
-      dv_e = ed;
-    }
+    rescale2_if(ed != dv_e, dv0, dv1, ed - dv_e);   // the dO images' exponent dropped: bring dV along
+    dv_e = ed;
     // ---- P, Pd (at 2^ep), dS in place; the wave's max |dS|
     const float fs = ldexpf(1.f, -(eq + ek)), fd = ldexpf(1.f, -(ed + ev));
     float smax = 0.f;
@@ -415,11 +443,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     if (lane == 0) ScS[w] = smax;
     {   // the wave's dS exponent (running, decreasing) and the dK accumulator's
       const int es_new = min(es, run_exp(smax));
-      if (eq + es_new != dk_e) {
-        rescale(dk0, eq + es_new - dk_e);
-        rescale(dk1, eq + es_new - dk_e);
-        dk_e = eq + es_new;
-      }
+      rescale2_if(eq + es_new != dk_e, dk0, dk1, eq + es_new - dk_e);
+      dk_e = eq + es_new;
       es = es_new;
     }
     const float ss = ldexpf(1.f, es);

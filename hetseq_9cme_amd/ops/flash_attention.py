@@ -8,9 +8,9 @@ GPU path: the fused flash-style HIP kernel (``_C.attn_fwd`` / ``attn_bwd``,
 csrc/kernels/attention.hip) for head_dim 64 at any sequence length (keys past
 S are masked, rows past S are neither computed into nor stored), with fp32 or
 bf16 activations (bf16 activations: bf16 MFMA, attention_bf16.hip; fp32 activations under
-``--fp32-gemm fp16x3`` from 4096 token rows: the forward's products as six bf16 piece passes,
-attention_x6.hip, the backward's as three fp16 passes over scaled two-piece operands,
-attention_f16.hip; fp32 MFMA below that and under ``--fp32-gemm native``);
+``--fp32-gemm fp16x3`` from 4096 token rows: the products as six bf16 piece passes,
+attention_x6.hip, or with ``--fp32-attention fp16x3`` as three fp16 passes over scaled two-piece
+operands, attention_f16.hip; fp32 MFMA below that and under ``--fp32-gemm native``);
 other shapes / dtypes use the composite below (batched GEMMs + softmax), which
 is also the CPU path and the test oracle.
 """
@@ -83,7 +83,8 @@ class _AttnFn(torch.autograd.Function):
             B, S = qkv.shape[0], qkv.shape[1]
             am = torch.empty(((S + 127) // 128) * num_heads * B * 4, dtype=torch.float32, device=qkv.device) \
                 if gemm16.enabled() else None
-            out, lse, dmask = C().attn_fwd_x6(qkv, mask_bias, num_heads, keep, seed, stream, bias, am)
+            fwd = C().attn_fwd_f16 if fp32_mode.fp32_attention_mode() == 'fp16x3' else C().attn_fwd_x6
+            out, lse, dmask = fwd(qkv, mask_bias, num_heads, keep, seed, stream, bias, am)
             gemm16.attach(out, am)
         else:
             out, lse, dmask = C().attn_fwd(qkv, mask_bias, num_heads, keep, seed, stream, bias)
@@ -109,9 +110,9 @@ class _AttnFn(torch.autograd.Function):
             # projection's data / weight gradient GEMMs
             am = torch.empty(qkv.shape[0] * num_heads, dtype=torch.float32, device=qkv.device) \
                 if gemm16.enabled() and qkv.shape[1] <= 128 else None
-            # products as three fp16 passes over scaled two-piece operands (attention_f16.hip)
-            dqkv, dbias = C().attn_bwd_f16(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep,
-                                           ctx.bias, *slots, am)
+            bwd = C().attn_bwd_f16 if fp32_mode.fp32_attention_mode() == 'fp16x3' else C().attn_bwd_x6
+            dqkv, dbias = bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep, ctx.bias,
+                              *slots, am)
             gemm16.attach(dqkv, am)
         else:
             dqkv, dbias = C().attn_bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep, ctx.bias,

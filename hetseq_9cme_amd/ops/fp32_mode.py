@@ -9,8 +9,9 @@ fp16/bf16 MFMA rate.  Two modes:
   csrc/kernels/gemm_f16.hip): operands scaled by a power of two from their max |x| and split
   into two fp16 pieces (22 significant bits), three exact piece products per GEMM.  Measured
   GEMM error vs fp64 0.6-0.7x that of native f32 MFMA (tests/test_gemm_f16_gpu.py).  The
-  attention products run as six bf16 piece passes (attention_x6.hip, fp32-exact class) from
-  ``ATTN_X6_MIN_ROWS`` token rows, f32 MFMA below.
+  attention products run as six bf16 piece passes (attention_x6.hip, fp32-exact class; or, with
+  ``--fp32-attention fp16x3``, three fp16 passes, attention_f16.hip) from ``ATTN_X6_MIN_ROWS``
+  token rows, f32 MFMA below.
 * ``native``: f32 MFMA everywhere (library GEMMs, attention.hip) -- bitwise the reference's fp32
   FMA chain class; the numerics oracle of the parity runs (tools/parity_run.py).
 """
@@ -19,6 +20,7 @@ import torch
 from ._ext import use_kernels
 
 MODES = ('native', 'fp16x3')
+ATTN_MODES = ('x6', 'fp16x3')
 
 # Token rows from which the fp32 attention runs its products as bf16 pieces (attention_x6.hip):
 # at 4096 rows (BERT-base 32 x 128) and above the split kernels win; NER fine-tuning batches
@@ -32,6 +34,27 @@ def set_fp32_gemm(mode):
     if mode not in MODES:
         raise ValueError('--fp32-gemm must be one of {}'.format(list(MODES)))
     gemm16.set_enabled(mode == 'fp16x3')
+
+
+class _Attn(object):
+    kernel = 'x6'
+
+
+def set_fp32_attention(mode):
+    """``--fp32-attention``: the kernels of the fp32 attention products under fp16x3 GEMMs, from
+    ``ATTN_X6_MIN_ROWS`` rows: ``'x6'`` (default; six bf16 piece passes, attention_x6.hip: bf16's
+    exponent range, so every row keeps fp32-class accuracy whatever its magnitude) or ``'fp16x3'``
+    (three fp16 passes over scaled two-piece operands, attention_f16.hip: per-tile / per-wave
+    power-of-two scales, so a dQ / dK row more than 2^40 below its tile's largest dS is flushed --
+    the fp16x3 GEMMs' per-tensor floor).  Measured at the same speed on BERT-base
+    (profiles/r4_attention_bwd_pmc.md): both are latency-bound at one wave per SIMD."""
+    if mode not in ATTN_MODES:
+        raise ValueError('--fp32-attention must be one of {}'.format(list(ATTN_MODES)))
+    _Attn.kernel = mode
+
+
+def fp32_attention_mode():
+    return _Attn.kernel
 
 
 def fp32_gemm_mode():

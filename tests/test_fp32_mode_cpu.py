@@ -72,6 +72,27 @@ def test_mode_switch_and_option():
         fp32_mode.set_fp32_gemm(prev)
 
 
+def test_attention_mode_option():
+    """--fp32-attention: x6 by default, fp16x3 selectable, anything else refused; the controller
+    applies it."""
+    from hetseq_9cme_amd import options
+    args = options.parse_training_args(['--task', 'mnist', '--data', '/tmp'])
+    assert args.fp32_attention == 'x6'
+    args = options.parse_training_args(['--task', 'mnist', '--data', '/tmp', '--fp32-attention', 'fp16x3'])
+    assert args.fp32_attention == 'fp16x3'
+    with pytest.raises(SystemExit):
+        options.parse_training_args(['--task', 'mnist', '--data', '/tmp', '--fp32-attention', 'bf16'])
+    with pytest.raises(ValueError):
+        fp32_mode.set_fp32_attention('fp32')
+    prev = fp32_mode.fp32_attention_mode()
+    try:
+        fp32_mode.set_fp32_attention('fp16x3')
+        assert fp32_mode.fp32_attention_mode() == 'fp16x3'
+    finally:
+        fp32_mode.set_fp32_attention(prev)
+    assert fp32_mode.fp32_attention_mode() == 'x6'
+
+
 # (tokens, [(n_out, n_in)]) of every BERT-base GEMM the BASELINE configs run
 _SHAPES = [(n_out, n_in) for (n_out, n_in) in [(2304, 768), (768, 768), (3072, 768), (768, 3072)]]
 _ROWS = {'phase1_b128': 16384, 'phase1_b32': 4096, 'phase2_b32': 16384, 'ner_b32': 32 * 40, 'tiny': 100}

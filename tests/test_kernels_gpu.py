@@ -693,8 +693,9 @@ def test_attention_f16_backward_fp32_class(dev, S, with_bias, keep, case):
         assert a < 8 * max(c, 1e-7) and a < 2e-4, (e16, e32)
     if with_bias:
         db_ref = gref.sum((0, 1)).reshape(-1)
-        e_db = ((g16[1].double() - db_ref).abs().max() / db_ref.abs().max()).item()
-        e_db32 = ((g32[1].double() - db_ref).abs().max() / db_ref.abs().max()).item()
+        den = sc.sum((0, 1)).reshape(-1)      # the column sums' natural scale
+        e_db = ((g16[1].double() - db_ref).abs() / den).max().item()
+        e_db32 = ((g32[1].double() - db_ref).abs() / den).max().item()
         assert e_db < 8 * max(e_db32, 1e-7) and e_db < 2e-4, (e_db, e_db32)
 
 

@@ -46,8 +46,8 @@ def parse():
     ap.add_argument('--fp32-gemm', default='fp16x3', choices=['fp16x3', 'native'],
                     help='fp32 GEMMs: fp16x3 (default, fp32 class: ops/gemm16.py) or native f32 MFMA '
                          '(ops/fp32_mode.py)')
-    ap.add_argument('--fp32-attention', default='x6', choices=['x6', 'fp16x3'],
-                    help='fp32 attention products: x6 (default) or fp16x3 (ops/fp32_mode.py)')
+    ap.add_argument('--fp32-attention', default='fp16x3', choices=['fp16x3', 'x6'],
+                    help='fp32 attention products: fp16x3 (default) or x6 (ops/fp32_mode.py)')
     ap.add_argument('--model', default='base', choices=['base', 'large', 'tiny'])
     ap.add_argument('--no-fused', action='store_true', help='torch-op baseline (A/B only)')
     ap.add_argument('--data-dir', default=None)

@@ -49,13 +49,13 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int D = 64;
 constexpr int RS = 72;    // [query][dim] image row stride (halves): conflict-free 16-B fragment reads
-constexpr int TS = 40;    // transposed 32-query image row stride (halves)
-constexpr int KTS = 136;  // K^T [dim][128 keys] row stride (halves)
 constexpr int DSF = 132;  // fp32 dS [query][128 keys] row stride (floats): conflict-free dQ fragment reads
-constexpr int KT_B = 64 * KTS * 2, DS_B = 32 * DSF * 4, QS_B = 32 * RS * 2, QT_B = 64 * TS * 2;
+constexpr int DS_B = 32 * DSF * 4, QS_B = 32 * RS * 2;
 constexpr int NSC = 16;   // per-tile scalars: max |Q|, max |dO|, max |dS| per wave (+ spare)
-constexpr int VF_B = 4 * 4 * 2 * 64 * 16;   // each wave's V piece fragments (B operands of dP), 32 KiB
-constexpr int BWD_SMEM = 2 * KT_B + DS_B + 2 * (2 * QS_B) + 2 * (2 * QT_B) + VF_B + (32 + 128 + NSC) * 4;
+constexpr int KRS = 72;   // K image [128 keys][64 dims] row stride (halves)
+constexpr int KI_B = 128 * KRS * 2;
+// 71 KiB: two workgroups (two waves per SIMD) per CU
+constexpr int BWD_SMEM = 2 * KI_B + DS_B + 2 * (2 * QS_B) + (32 + 128 + NSC) * 4;
 constexpr int kNoScale = 120;   // exponent of an operand seen only as zeros so far (no constraint)
 
 __device__ __forceinline__ f32x16 mfma(f16x8 a, f16x8 b, f32x16 c) {
@@ -105,15 +105,6 @@ __device__ __forceinline__ f32x8 acc8(const f32x16& s) {
 __device__ __forceinline__ int vpos(int k) {
   const int kk = k & 15;
   return (k & ~15) + 8 * ((kk >> 2) & 1) + (kk & 3) + 4 * (kk >> 3);
-}
-// rows r0, r1 (consecutive image positions) x 4 dims -> 4 words of a transposed image
-__device__ __forceinline__ void put_t4(uint16_t* img, int stride, int dim0, int pos, uint2 r0, uint2 r1) {
-  uint32_t* p = reinterpret_cast<uint32_t*>(img + dim0 * stride + pos);
-  const int sw = stride / 2;
-  p[0] = (r0.x & 0xffffu) | (r1.x << 16);
-  p[sw] = (r0.x >> 16) | (r1.x & 0xffff0000u);
-  p[2 * sw] = (r0.y & 0xffffu) | (r1.y << 16);
-  p[3 * sw] = (r0.y >> 16) | (r1.y & 0xffff0000u);
 }
 __device__ __forceinline__ f32x8 ld8(const float* p, const float* bias) {
   const float4 a = *reinterpret_cast<const float4*>(p), c = *reinterpret_cast<const float4*>(p + 4);
@@ -182,21 +173,34 @@ __device__ __forceinline__ Blk xcd_block() {
   return k;
 }
 
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+// B operand (8 consecutive k = image rows r0 .. r0 + 7, one column per lane) of a row-major fp16
+// image through two ds_read_b64_tr_b16: per 16-lane group, lane 4q + p addresses row q (+4),
+// columns c0 + 4p .. +3, and lane i receives column c0 + i of the four rows (T10)
+__device__ __forceinline__ f16x8 tr8(const uint16_t* img, int stride, int r0, int c0, int i) {
+  const uint16_t* a = img + (r0 + (i >> 2)) * stride + c0 + 4 * (i & 3);
+  const v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a));
+  const v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a + 4 * stride));
+  const v4i16 v[2] = {lo, hi};
+  return *reinterpret_cast<const f16x8*>(v);
+}
+
 template <bool kDrop>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void attn_bwd_f16_k(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_bwd_f16_k(
     const float* __restrict__ qkv, const float* __restrict__ qkv_bias, float* __restrict__ dbias_part,
     const float* __restrict__ maskb, const float* __restrict__ dout, const float* __restrict__ outp,
     const float* __restrict__ lse, const uint32_t* __restrict__ dmask, float* __restrict__ dqkv,
     float* __restrict__ dq_acc, int dq_ld, int S, int nh, float keep, float* __restrict__ amax_part) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint16_t* Kt = reinterpret_cast<uint16_t*>(smem);                      // [2][64][KTS]
-  float* dSf = reinterpret_cast<float*>(smem + 2 * KT_B);                // [32][DSF] fp32
-  uint16_t* Qs = reinterpret_cast<uint16_t*>(smem + 2 * KT_B + DS_B);    // [2][32][RS]
+  // one row-major image per operand, read both ways: K [key][dim] as the B operand of S (rows) and
+  // of dQ (transposed reads); Q / dO [vpos(query)][dim] as the A operand of S / dP (rows) and the
+  // B operand of dK / dV (transposed reads of 8 consecutive rows = the accumulator's k order)
+  uint16_t* Ki = reinterpret_cast<uint16_t*>(smem);                      // [2][128][KRS]
+  float* dSf = reinterpret_cast<float*>(smem + 2 * KI_B);                // [32][DSF] fp32
+  uint16_t* Qs = reinterpret_cast<uint16_t*>(smem + 2 * KI_B + DS_B);    // [2][32][RS]
   uint16_t* dOs = Qs + 2 * 32 * RS;                                      // [2][32][RS]
-  uint16_t* Qt = dOs + 2 * 32 * RS;                                      // [2][64][TS]
-  uint16_t* dOt = Qt + 2 * 64 * TS;                                      // [2][64][TS]
-  f16x8* Vf = reinterpret_cast<f16x8*>(dOt + 2 * 64 * TS);              // [4 waves][4 ks][2][64 lanes]
-  float* Ls = reinterpret_cast<float*>(smem + 2 * KT_B + DS_B + 4 * QS_B + 4 * QT_B + VF_B);   // [32] lse
+  float* Ls = reinterpret_cast<float*>(smem + 2 * KI_B + DS_B + 4 * QS_B);   // [32] lse
   float* Ds = Ls + 32;                                                   // [32][4 waves] D partials
   float* Sc = Ds + 128;                                                  // per-tile scalars
   float* ScQ = Sc, *ScD = Sc + 4, *ScS = Sc + 8;                         // [4 waves] each
@@ -217,17 +221,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const float* vbias = qkv_bias ? qkv_bias + 2 * H + hd * D : nullptr;
   float am = 0.f;   // max |dQKV| of this block's stores (one key block per head only)
 
-  // ---- this lane's key: fp32 K and V fragments (dims 16ks + 8h .. +7), the block's max |K|, |V|
+  // ---- the block's K rows (4 x 8 dims per thread, for the K image) and this lane's V fragments
+  // (dims 16ks + 8h .. +7), the block's max |K|, |V|
   const int mykey = kbase + w * 32 + l32;
   const int mykc = mykey < S ? mykey : S - 1;
   f32x8 kx[4], vx[4];
   float mkx = 0.f, mvx = 0.f;
 #pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int u = tid + 256 * i, key = kbase + (u >> 3), c8 = (u & 7) * 8;
+    kx[i] = ld8(base + (int64_t)(key < S ? key : S - 1) * H3 + H + c8, kbias ? kbias + c8 : nullptr);
+    mkx = fmaxf(mkx, amax8(kx[i]));
+  }
+#pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     const int c = 16 * ks + 8 * h;
-    kx[ks] = ld8(base + (int64_t)mykc * H3 + H + c, kbias ? kbias + c : nullptr);
     vx[ks] = ld8(base + (int64_t)mykc * H3 + 2 * H + c, vbias ? vbias + c : nullptr);
-    mkx = fmaxf(mkx, amax8(kx[ks]));
     mvx = fmaxf(mvx, amax8(vx[ks]));
   }
   mkx = wave_max(mkx);
@@ -246,8 +255,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   const uint32_t* dmask_bh = kDrop ? dmask + bh * Sp * nwords : nullptr;
   const int moff = mykey * nwords;
 
-  // staging unit of this thread: query pair (2sqp, 2sqp+1) x dims 4sdq .. 4sdq+3; lanes run
-  // over the query pairs so the transposed-image stores (put_t4) hit 64 distinct banks
+  // staging unit of this thread: query pair (2sqp, 2sqp+1) x dims 4sdq .. 4sdq+3
   const int sqp = tid & 15, sdq = tid >> 4;
   float4 pq[2], pd[2], po[2];
   float pl = 0.f;
@@ -297,39 +305,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
   __syncthreads();   // block max |K|, |V| published
   const int ek = f16_scale_exp(max4(ScQ)), ev = f16_scale_exp(max4(ScD));
   const float sk = ldexpf(1.f, ek), sv = ldexpf(1.f, ev);
-  // K's fragments stay in registers (B operands of S); V's go to this wave's LDS slots (read once
-  // per tile by dP): 32 fewer live VGPRs across the loop
-  f16x8 kf[4][2];
-  f16x8* vfw = Vf + w * 512 + lane;
+  // V's piece fragments in registers (B operands of dP); K's pieces into the image
+  f16x8 vf[4][2];
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    sp8(kx[ks], sk, kf[ks]);
-    f16x8 v2[2];
-    sp8(vx[ks], sv, v2);
-    vfw[(2 * ks) * 64] = v2[0];
-    vfw[(2 * ks + 1) * 64] = v2[1];
-  }
-  // ---- K^T pieces of the 128 keys (natural key order) for dQ: 64 key pairs x 16 dim quads
+  for (int ks = 0; ks < 4; ++ks) sp8(vx[ks], sv, vf[ks]);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int u = tid + 256 * i, kp = u & 63, dq = u >> 6;   // lanes over key pairs: conflict-free put_t4
-    const int k0 = kbase + 2 * kp < S ? kbase + 2 * kp : S - 1;
-    const int k1 = kbase + 2 * kp + 1 < S ? kbase + 2 * kp + 1 : S - 1;
-    const float4 a = *reinterpret_cast<const float4*>(base + (int64_t)k0 * H3 + H + 4 * dq);
-    const float4 c = *reinterpret_cast<const float4*>(base + (int64_t)k1 * H3 + H + 4 * dq);
-    float fa[4] = {a.x, a.y, a.z, a.w}, fc[4] = {c.x, c.y, c.z, c.w};
-    if (kbias) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        fa[j] += kbias[4 * dq + j];
-        fc[j] += kbias[4 * dq + j];
-      }
-    }
-    uint2 pa[2], pc[2];
-    sp4(fa, sk, pa);
-    sp4(fc, sk, pc);
-#pragma unroll
-    for (int p = 0; p < 2; ++p) put_t4(Kt + p * 64 * KTS, KTS, 4 * dq, 2 * kp, pa[p], pc[p]);
+    const int u = tid + 256 * i, row = u >> 3, c8 = (u & 7) * 8;
+    f16x8 p2[2];
+    sp8(kx[i], sk, p2);
+    *reinterpret_cast<f16x8*>(&Ki[row * KRS + c8]) = p2[0];
+    *reinterpret_cast<f16x8*>(&Ki[128 * KRS + row * KRS + c8]) = p2[1];
   }
   __syncthreads();   // every wave has read the K / V maxima
   tile_max();
@@ -338,6 +324,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 
   // dQ tiles of this wave (16x16x32 layout): queries 16qh .., dims 32dp2 .. and 32dp2 + 16 ..
   const int qh = w & 1, dp2 = w >> 1;
+  const int vq = vpos(l32);   // image row of query l32 (A operand row of S / dP)
   const int r16 = lane & 15, kg = lane >> 4;
 
   // accumulators and the exponents they are held at: dv = dV 2^(ep + dv_e), dk = dK 2^(dk_e)
@@ -359,18 +346,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     sp4(q1, sq, q1p);
     sp4(d0, sd, d0p);
     sp4(d1, sd, d1p);
-    const int pos = vpos(2 * sqp);
-    // Q / dO image rows q with q2 ^ q3 ^ q4 = 1 hold their 16-B chunks pair-swapped (chunk ^ 1):
-    // 2-way instead of 4-way staging-store conflicts, conflict-free 16-B fragment reads
-    const int qcol = 8 * ((sdq >> 1) ^ (((sqp >> 1) ^ (sqp >> 2) ^ (sqp >> 3)) & 1)) + 4 * (sdq & 1);
+    // rows in the accumulator's k order (vpos): 8 consecutive rows = one k slice of dK / dV
+    const int r0 = vpos(2 * sqp), col = 4 * sdq;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
-      *reinterpret_cast<uint2*>(&Qs[p * 32 * RS + (2 * sqp) * RS + qcol]) = q0p[p];
-      *reinterpret_cast<uint2*>(&Qs[p * 32 * RS + (2 * sqp + 1) * RS + qcol]) = q1p[p];
-      *reinterpret_cast<uint2*>(&dOs[p * 32 * RS + (2 * sqp) * RS + qcol]) = d0p[p];
-      *reinterpret_cast<uint2*>(&dOs[p * 32 * RS + (2 * sqp + 1) * RS + qcol]) = d1p[p];
-      put_t4(Qt + p * 64 * TS, TS, 4 * sdq, pos, q0p[p], q1p[p]);
-      put_t4(dOt + p * 64 * TS, TS, 4 * sdq, pos, d0p[p], d1p[p]);
+      *reinterpret_cast<uint2*>(&Qs[p * 32 * RS + r0 * RS + col]) = q0p[p];
+      *reinterpret_cast<uint2*>(&Qs[p * 32 * RS + (r0 + 1) * RS + col]) = q1p[p];
+      *reinterpret_cast<uint2*>(&dOs[p * 32 * RS + r0 * RS + col]) = d0p[p];
+      *reinterpret_cast<uint2*>(&dOs[p * 32 * RS + (r0 + 1) * RS + col]) = d1p[p];
     }
     float e0 = pd[0].x * po[0].x + pd[0].y * po[0].y + pd[0].z * po[0].z + pd[0].w * po[0].w;
     float e1 = pd[1].x * po[1].x + pd[1].y * po[1].y + pd[1].z * po[1].z + pd[1].w * po[1].w;
@@ -385,11 +368,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     }
     if (tid < 32) Ls[tid] = qt + tid < S ? pl : INFINITY;   // rows past S: P = 0
   };
+  // dims l32 (t0) and 32 + l32 (t1) of image rows 16 half + 8h .. +7, transposed
+  const int gcol = 16 * ((lane >> 4) & 1), li = lane & 15;
   auto load_img = [&](const uint16_t* img, int half, f16x8 (&t0)[2], f16x8 (&t1)[2]) {
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
-      t0[p] = *reinterpret_cast<const f16x8*>(&img[p * 64 * TS + l32 * TS + 8 * h + 16 * half]);
-      t1[p] = *reinterpret_cast<const f16x8*>(&img[p * 64 * TS + (32 + l32) * TS + 8 * h + 16 * half]);
+      t0[p] = tr8(img + p * 32 * RS, RS, 16 * half + 8 * h, gcol, li);
+      t1[p] = tr8(img + p * 32 * RS, RS, 16 * half + 8 * h, 32 + gcol, li);
     }
   };
 
@@ -406,16 +391,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
     f32x16 sa = {0}, dpa = {0};
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      f16x8 qa[2], da[2];
+      f16x8 qa[2], da[2], kf[2];
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
-        const int qc = 8 * ((2 * ks + h) ^ (((l32 >> 2) ^ (l32 >> 3) ^ (l32 >> 4)) & 1));   // stores' swizzle
-        qa[p] = *reinterpret_cast<const f16x8*>(&Qs[p * 32 * RS + l32 * RS + qc]);
-        da[p] = *reinterpret_cast<const f16x8*>(&dOs[p * 32 * RS + l32 * RS + qc]);
+        const int off = p * 32 * RS + vq * RS + 16 * ks + 8 * h;
+        qa[p] = *reinterpret_cast<const f16x8*>(&Qs[off]);
+        da[p] = *reinterpret_cast<const f16x8*>(&dOs[off]);
+        kf[p] = *reinterpret_cast<const f16x8*>(&Ki[p * 128 * KRS + (w * 32 + l32) * KRS + 16 * ks + 8 * h]);
       }
-      const f16x8 vfr[2] = {vfw[(2 * ks) * 64], vfw[(2 * ks + 1) * 64]};
-      HX_X3(sa, qa, kf[ks]);
-      HX_X3(dpa, da, vfr);
+      HX_X3(sa, qa, kf);
+      HX_X3(dpa, da, vf[ks]);
     }
     rescale2_if(ed != dv_e, dv0, dv1, ed - dv_e);   // the dO images' exponent dropped: bring dV along
     dv_e = ed;
@@ -453,10 +438,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       f16x8 a[2], c[2], t0[2], t1[2];
       sp8(acc8<0>(sa), 1.f, a);
       sp8(acc8<0>(dpa), ss, c);
-      load_img(dOt, 0, t0, t1);
+      load_img(dOs, 0, t0, t1);
       HX_X3(dv0, a, t0);
       HX_X3(dv1, a, t1);
-      load_img(Qt, 0, t0, t1);
+      load_img(Qs, 0, t0, t1);
       HX_X3(dk0, c, t0);
       HX_X3(dk1, c, t1);
     }
@@ -464,10 +449,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       f16x8 a[2], c[2], t0[2], t1[2];
       sp8(acc8<8>(sa), 1.f, a);
       sp8(acc8<8>(dpa), ss, c);
-      load_img(dOt, 1, t0, t1);
+      load_img(dOs, 1, t0, t1);
       HX_X3(dv0, a, t0);
       HX_X3(dv1, a, t1);
-      load_img(Qt, 1, t0, t1);
+      load_img(Qs, 1, t0, t1);
       HX_X3(dk0, c, t0);
       HX_X3(dk1, c, t1);
     }
@@ -489,9 +474,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
       f16x8 a[2], b0[2], b1[2];
       sp8(f32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w}, st, a);
 #pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        b0[p] = *reinterpret_cast<const f16x8*>(&Kt[p * 64 * KTS + (32 * dp2 + r16) * KTS + 32 * ks + 8 * kg]);
-        b1[p] = *reinterpret_cast<const f16x8*>(&Kt[p * 64 * KTS + (32 * dp2 + 16 + r16) * KTS + 32 * ks + 8 * kg]);
+      for (int p = 0; p < 2; ++p) {   // K^T fragments: dims 32dp2 + r16 (+ 16), keys 32ks + 8kg .. +7
+        b0[p] = tr8(Ki + p * 128 * KRS, KRS, 32 * ks + 8 * kg, 32 * dp2, r16);
+        b1[p] = tr8(Ki + p * 128 * KRS, KRS, 32 * ks + 8 * kg, 32 * dp2 + 16, r16);
       }
       HX_X3_16(qa0, a, b0);
       HX_X3_16(qa1, a, b1);

@@ -9,9 +9,9 @@ fp16/bf16 MFMA rate.  Two modes:
   csrc/kernels/gemm_f16.hip): operands scaled by a power of two from their max |x| and split
   into two fp16 pieces (22 significant bits), three exact piece products per GEMM.  Measured
   GEMM error vs fp64 0.6-0.7x that of native f32 MFMA (tests/test_gemm_f16_gpu.py).  The
-  attention products run as six bf16 piece passes (attention_x6.hip, fp32-exact class; or, with
-  ``--fp32-attention fp16x3``, three fp16 passes, attention_f16.hip) from ``ATTN_X6_MIN_ROWS``
-  token rows, f32 MFMA below.
+  attention products run as three fp16 passes (attention_f16.hip; or, with ``--fp32-attention
+  x6``, six bf16 piece passes, attention_x6.hip) from ``ATTN_X6_MIN_ROWS`` token rows, f32 MFMA
+  below.
 * ``native``: f32 MFMA everywhere (library GEMMs, attention.hip) -- bitwise the reference's fp32
   FMA chain class; the numerics oracle of the parity runs (tools/parity_run.py).
 """
@@ -37,17 +37,17 @@ def set_fp32_gemm(mode):
 
 
 class _Attn(object):
-    kernel = 'x6'
+    kernel = 'fp16x3'
 
 
 def set_fp32_attention(mode):
     """``--fp32-attention``: the kernels of the fp32 attention products under fp16x3 GEMMs, from
-    ``ATTN_X6_MIN_ROWS`` rows: ``'x6'`` (default; six bf16 piece passes, attention_x6.hip: bf16's
-    exponent range, so every row keeps fp32-class accuracy whatever its magnitude) or ``'fp16x3'``
-    (three fp16 passes over scaled two-piece operands, attention_f16.hip: per-tile / per-wave
-    power-of-two scales, so a dQ / dK row more than 2^40 below its tile's largest dS is flushed --
-    the fp16x3 GEMMs' per-tensor floor).  Measured at the same speed on BERT-base
-    (profiles/r4_attention_bwd_pmc.md): both are latency-bound at one wave per SIMD."""
+    ``ATTN_X6_MIN_ROWS`` rows: ``'fp16x3'`` (default; three fp16 passes over scaled two-piece
+    operands, attention_f16.hip -- the backward 21-25 % faster than x6 at two waves per SIMD,
+    profiles/r4_attention_bwd_pmc.md; per-tile / per-wave power-of-two scales, so a dQ / dK row more
+    than 2^40 below its tile's largest dS is flushed, the fp16x3 GEMMs' per-tensor floor) or
+    ``'x6'`` (six bf16 piece passes, attention_x6.hip: bf16's exponent range, every row fp32
+    class whatever its magnitude)."""
     if mode not in ATTN_MODES:
         raise ValueError('--fp32-attention must be one of {}'.format(list(ATTN_MODES)))
     _Attn.kernel = mode

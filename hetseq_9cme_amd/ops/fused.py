@@ -115,18 +115,18 @@ def _dgrad_bf16(dy2, W, xshape, mbox):
 
 # ----------------------------------------------------------------- weight-grad side stream
 class _Side(object):
-    # 'auto' (default): the hand-written fp16x3 GEMM backward paths only (round 3 on the same
-    # structure: BERT-base phase 1 53.9 -> 52.9 ms/step, profiles/r3_overlap_wgrad_ab.md); the
-    # library paths (native fp32, bf16: round 1 69.5 -> 71.7 ms/step) stay on the compute stream.
-    # 'on': every path; 'off': none.
+    # 'auto' (default) = 'off' since the two-waves-per-SIMD fp16x3 attention backward: with the
+    # weight gradients on the compute stream BERT-base phase 1 runs 36.42 vs 36.80 ms/step, phase 2
+    # 42.04 vs 43.15 (profiles/r4p_overlap_ab.md; round 3 measured the side stream 1 ms ahead on
+    # the x6 attention).  'on' (--overlap-wgrad): the side stream on every path.
     mode = 'auto'
     streams = {}          # device index -> torch.cuda.Stream
     active = set()        # device indices with side work queued in the current backward
 
 
 def set_side_stream(flag):
-    """Weight-gradient work on a side stream: True / 'on', False / 'off', or 'auto'
-    (the hand-written GEMM paths only)."""
+    """Weight-gradient work on a side stream: True / 'on', False / 'off', or 'auto' (= off, the
+    measured default)."""
     _Side.mode = {True: 'on', False: 'off'}.get(flag, flag) if isinstance(flag, bool) else str(flag)
     assert _Side.mode in ('on', 'off', 'auto'), flag
 
@@ -138,7 +138,7 @@ def side_begin(device, hand=False):
     dgrad chain (attention / LayerNorm / GELU backward: mostly memory-bound),
     the side stream's GEMMs fill the matrix cores.  Joined back into the compute
     stream by an end-of-backward callback (``side_join``)."""
-    if _Side.mode == 'off' or (_Side.mode == 'auto' and not hand) or device.type != 'cuda':
+    if _Side.mode != 'on' or device.type != 'cuda':
         return None
     idx = device.index if device.index is not None else torch.cuda.current_device()
     st = _Side.streams.get(idx)

@@ -87,11 +87,11 @@ def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialD
                         help='where --gemm-tuning online writes its table (device ordinal appended)')
     parser.add_argument('--overlap-wgrad', dest='overlap_wgrad', action='store_const', const='on', default='auto',
                         help='run weight-gradient GEMMs / bias column sums on a side HIP stream, concurrent '
-                             'with the data-gradient GEMMs, on every backward path (default: the hand-written '
-                             'fp16x3 GEMM paths only -- the library paths (native fp32, bf16) lose: '
-                             'profiles/r3_overlap_wgrad_ab.md)')
+                             'with the data-gradient chain (default: on the compute stream -- measured faster '
+                             'since the fp16x3 attention backward runs two waves per SIMD: '
+                             'profiles/r4p_overlap_ab.md)')
     parser.add_argument('--no-overlap-wgrad', dest='overlap_wgrad', action='store_const', const='off',
-                        help='weight gradients on the compute stream on every path')
+                        help='weight gradients on the compute stream (the default)')
     parser.add_argument('--debug-kernels', action='store_true',
                         help='debug mode: serialised kernel launches (AMD_SERIALIZE_KERNEL=3, '
                              'HIP_LAUNCH_BLOCKING=1), range checks on token/type ids and labels and finite '

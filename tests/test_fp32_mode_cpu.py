@@ -125,9 +125,8 @@ def test_dispatch_single_backend(monkeypatch, config):
 
 
 def test_overlap_wgrad_modes():
-    """--overlap-wgrad is tri-state: default 'auto' (side stream on the hand-written GEMM backward
-    paths only), '--overlap-wgrad' = every path, '--no-overlap-wgrad' = none; CPU tensors never
-    get a side stream."""
+    """--overlap-wgrad is tri-state: default 'auto' (= off, the measured default),
+    '--overlap-wgrad' = on, '--no-overlap-wgrad' = off; CPU tensors never get a side stream."""
     from hetseq_9cme_amd import options
     from hetseq_9cme_amd.ops import fused
     base = ['--task', 'mnist', '--data', '/tmp']

@@ -434,27 +434,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     const float ss = ldexpf(1.f, es);
     // ---- dV += Pd^T . dO, dK += dS^T . Qs over the two accumulator halves (k-slots = query rows)
-    {
-      f16x8 a[2], c[2], t0[2], t1[2];
-      sp8(acc8<0>(sa), 1.f, a);
-      sp8(acc8<0>(dpa), ss, c);
-      load_img(dOs, 0, t0, t1);
-      HX_X3(dv0, a, t0);
-      HX_X3(dv1, a, t1);
-      load_img(Qs, 0, t0, t1);
-      HX_X3(dk0, c, t0);
-      HX_X3(dk1, c, t1);
+    // one operand pair live at a time (fewer VGPRs at the loop's peak: no spills in the loop)
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      f16x8 a[2], t[2];
+      sp8(half ? acc8<8>(sa) : acc8<0>(sa), 1.f, a);
+#pragma unroll
+      for (int p = 0; p < 2; ++p) t[p] = tr8(dOs + p * 32 * RS, RS, 16 * half + 8 * h, gcol, li);
+      HX_X3(dv0, a, t);
+#pragma unroll
+      for (int p = 0; p < 2; ++p) t[p] = tr8(dOs + p * 32 * RS, RS, 16 * half + 8 * h, 32 + gcol, li);
+      HX_X3(dv1, a, t);
     }
-    {
-      f16x8 a[2], c[2], t0[2], t1[2];
-      sp8(acc8<8>(sa), 1.f, a);
-      sp8(acc8<8>(dpa), ss, c);
-      load_img(dOs, 1, t0, t1);
-      HX_X3(dv0, a, t0);
-      HX_X3(dv1, a, t1);
-      load_img(Qs, 1, t0, t1);
-      HX_X3(dk0, c, t0);
-      HX_X3(dk1, c, t1);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      f16x8 c[2], t[2];
+      sp8(half ? acc8<8>(dpa) : acc8<0>(dpa), ss, c);
+#pragma unroll
+      for (int p = 0; p < 2; ++p) t[p] = tr8(Qs + p * 32 * RS, RS, 16 * half + 8 * h, gcol, li);
+      HX_X3(dk0, c, t);
+#pragma unroll
+      for (int p = 0; p < 2; ++p) t[p] = tr8(Qs + p * 32 * RS, RS, 16 * half + 8 * h, 32 + gcol, li);
+      HX_X3(dk1, c, t);
     }
     if (more) tile_max();   // the next tile's max |Q|, |dO| (its loads have landed by now)
     // every wave's dS and maxima are in LDS; the piece images of tile qt are free

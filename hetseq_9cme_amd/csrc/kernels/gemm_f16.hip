@@ -52,6 +52,9 @@ __device__ __forceinline__ f32x16 mfma16(const f16x8& a, const f16x8& b, const f
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
+// DMA ring depth of gemm_f16_k (LDS: depth x (BM + BN) x 64 B)
+constexpr int kGemmStages = 3;   // 4 measured 3 % slower (r4s GEMM bench: 2516 vs 2445 us per layer)
+
 struct F16Args {
   const void* A;   // fp32 (AT 0) or bf16 (AT 1)
   int64_t lda;
@@ -88,6 +91,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
   constexpr int NWM = BM / WM, NW = NWM * (BN / WN), NT = NW * 64;
   constexpr int MB = WM / 32, NB = WN / 32;
   constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64, STAGE = A_BYTES + B_BYTES;
+  constexpr int NS = kGemmStages;   // DMA ring depth: stage it + NS - 1 in flight during step it
   constexpr int KA = BM / 16, KB = BN / 16, PTOT = KA + KB;   // 1-KiB DMA pieces per stage
   constexpr int JHI = (PTOT + NW - 1) / NW, JLO = PTOT / NW;
   static_assert(JLO >= 1, "fewer DMA pieces than waves");
@@ -138,12 +142,18 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
     for (int j = 0; j < JHI; ++j)
       if (j < JLO || j < cnt) dma_one(it, buf, j);
   };
-  auto wait_stage = [&]() {   // all but this wave's youngest stage of DMAs landed
-    if constexpr (JHI == JLO) {
-      dma_wait<JLO>();
-    } else {
-      if (cnt == JHI) dma_wait<JHI>();
+  // all but this wave's youngest `young` stages of DMAs landed (young = 0 .. NS - 2)
+  auto wait_young = [&](int young) {
+    if (young <= 0) {
+      dma_wait<0>();
+    } else if (young == 1) {
+      if constexpr (JHI == JLO) dma_wait<JLO>();
+      else if (cnt == JHI) dma_wait<JHI>();
       else dma_wait<JLO>();
+    } else {
+      if constexpr (JHI == JLO) dma_wait<2 * JLO>();
+      else if (cnt == JHI) dma_wait<2 * JHI>();
+      else dma_wait<2 * JLO>();
     }
   };
 
@@ -160,14 +170,15 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
     offb[b][1] = A_BYTES + img_off(wn * WN + 32 * b + l32, 2 + h);   // piece 1
   }
 
-  dma(0, 0);
-  if (nit > 1) dma(1, 1);
+  static_assert(NS == 3 || NS == 4, "ring depth");
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < nit) dma(i, i);
   // operand scales (their loads over-wait the DMAs above: harmless)
   const int Ea = AT ? 0 : f16_scale_exp(block_amax(g.a_amax, g.na, red));
   const int Eb = AT ? 0 : f16_scale_exp(block_amax(g.b_amax, g.nb, red));
   const float sa = ldexpf(1.f, Ea), ia = ldexpf(1.f, -Ea), ib = ldexpf(1.f, -Eb);
-  if (nit > 1) wait_stage();
-  else dma_wait<0>();
+  wait_young(min(nit, NS - 1) - 1);   // stage 0 landed
   __syncthreads();
 
   f32x16 acc[MB][NB];
@@ -178,9 +189,9 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
 
   int cur = 0;
   for (int it = 0; it < nit; ++it) {
-    const int nxt2 = cur == 0 ? 2 : cur - 1;
+    const int nxt2 = cur == 0 ? NS - 1 : cur - 1;   // the buffer of stage it + NS - 1
     const char* st = lds + cur * STAGE;
-    const int dit = it + 2 < nit ? it + 2 : -1;
+    const int dit = it + NS - 1 < nit ? it + NS - 1 : -1;
     if constexpr (AT == 1) {
       // two 16-deep bf16 k steps per stage, one MFMA pass each; the next-next stage's DMA pieces
       // between them
@@ -242,10 +253,10 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
       }
     }
     }
-    if (it + 2 < nit) wait_stage();
-    else dma_wait<0>();
+    // stage it + 1 landed; stages it + 2 .. it + NS - 1 (those that exist) may still be in flight
+    wait_young(min(nit - 1 - it, NS - 1) - 1);
     __syncthreads();
-    cur = cur == 2 ? 0 : cur + 1;
+    cur = cur == NS - 1 ? 0 : cur + 1;
   }
 
   // ---- epilogue: quad transpose, then lane (l32 & 3) owns row 8 gq + 4 h + (l32 & 3) of each
@@ -424,7 +435,7 @@ void launch_one(const F16Args& a, hipStream_t s) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int total = ((a.M + BM - 1) / BM) * (a.N / BN) * a.ks;
   const int per = (total + 7) / 8;
-  const size_t smem = (size_t)3 * (BM + BN) * 64;
+  const size_t smem = (size_t)kGemmStages * (BM + BN) * 64;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_f16_k<BM, BN, WM, WN, EPI, 1, AT, OB>),

@@ -59,8 +59,10 @@ def child(a):
             '--max-sentences', str(a.batch), '--fast-stat-sync', '--lr', str(a.lr),
             '--warmup-updates', str(a.warmup_updates), '--weight-decay', '0.01',
             '--total-num-update', str(max(10 * a.updates, 1000)), '--clip-norm', '25', '--num-workers', '2',
-            '--log-format', 'none', '--disable-validation', '--no-save', '--fp32-gemm', a.child.split('#')[0],
-            '--distributed-world-size', '1']
+            '--log-format', 'none', '--disable-validation', '--no-save', '--distributed-world-size', '1']
+    # mode = GEMM mode [':' attention mode] ['#' repeat], e.g. 'fp16x3:x6'
+    gemm_mode, _, attn_mode = a.child.split('#')[0].partition(':')
+    argv += ['--fp32-gemm', gemm_mode] + (['--fp32-attention', attn_mode] if attn_mode else [])
     args = options.parse_training_args(argv)
     args.device_id = 0
     args.distributed_rank = 0
@@ -85,7 +87,7 @@ def child(a):
     torch.cuda.synchronize()
     torch.save({'loss': torch.stack(losses).cpu(), 'gnorm': torch.stack(gnorms).cpu(),
                 'p0': p0.cpu(), 'p': ctrl.flat.param_flat.detach().cpu()},
-               os.path.join(a.work, 'run_{}.pt'.format(a.child.replace('#', '_'))))
+               os.path.join(a.work, 'run_{}.pt'.format(a.child.replace('#', '_').replace(':', '-'))))
 
 
 def main():
@@ -112,7 +114,7 @@ def main():
         r = subprocess.run(base + ['--child', m])
         if r.returncode:
             sys.exit(r.returncode)
-    runs = {m: torch.load(os.path.join(a.work, 'run_{}.pt'.format(m.replace('#', '_'))), weights_only=True)
+    runs = {m: torch.load(os.path.join(a.work, 'run_{}.pt'.format(m.replace('#', '_').replace(':', '-'))), weights_only=True)
             for m in modes}
     ref = runs['native']
     moved = (ref['p'].double() - ref['p0'].double()).norm().item()

@@ -8,9 +8,9 @@ GPU path: the fused flash-style HIP kernel (``_C.attn_fwd`` / ``attn_bwd``,
 csrc/kernels/attention.hip) for head_dim 64 at any sequence length (keys past
 S are masked, rows past S are neither computed into nor stored), with fp32 or
 bf16 activations (bf16 activations: bf16 MFMA, attention_bf16.hip; fp32 activations under
-``--fp32-gemm fp16x3`` from 4096 token rows: the products as six bf16 piece passes,
-attention_x6.hip, or with ``--fp32-attention fp16x3`` as three fp16 passes over scaled two-piece
-operands, attention_f16.hip; fp32 MFMA below that and under ``--fp32-gemm native``);
+``--fp32-gemm fp16x3``: the products as three fp16 passes over scaled two-piece operands,
+attention_f16.hip, or with ``--fp32-attention x6`` from 4096 token rows as six bf16 piece passes,
+attention_x6.hip; fp32 MFMA otherwise and under ``--fp32-gemm native``);
 other shapes / dtypes use the composite below (batched GEMMs + softmax), which
 is also the CPU path and the test oracle.
 """
@@ -74,8 +74,8 @@ class _AttnFn(torch.autograd.Function):
         keep = 1.0 - p
         seed, stream = get_rng().next(qkv.device) if p > 0 else (get_rng().seed_tensor(qkv.device), 0)
         bias = _bias3(bq, bk, bv).float().contiguous() if bq is not None else None
-        # the split (x6) kernels from 4096 token rows (fp32_mode.attention_split); small fine-tuning
-        # batches keep the fp32-MFMA attention
+        # the piece kernels (fp32_mode.attention_split: fp16x3 at every size, x6 from 4096 token rows --
+        # smaller batches keep the fp32-MFMA attention under x6)
         ctx.split = qkv.dtype == torch.float32 and fp32_mode.attention_split(qkv.reshape(-1, qkv.shape[-1]))
         if ctx.split:
             # fp32 products on the bf16 matrix cores (six piece passes, attention_x6.hip); the

@@ -22,9 +22,9 @@ from ._ext import use_kernels
 MODES = ('native', 'fp16x3')
 ATTN_MODES = ('x6', 'fp16x3')
 
-# Token rows from which the fp32 attention runs its products as bf16 pieces (attention_x6.hip):
-# at 4096 rows (BERT-base 32 x 128) and above the split kernels win; NER fine-tuning batches
-# (~1000 rows) keep the f32-MFMA kernel (rounds 2-3 measurements).
+# Token rows from which the x6 attention (attention_x6.hip) runs the fp32 attention: at 4096 rows
+# (BERT-base 32 x 128) and above it wins; NER fine-tuning batches (~1000 rows) keep the f32-MFMA
+# kernel under x6 (rounds 2-3 measurements).  The fp16x3 kernels run at every size.
 ATTN_X6_MIN_ROWS = 4096
 
 
@@ -63,8 +63,10 @@ def fp32_gemm_mode():
 
 
 def attention_split(x2):
-    """Does the fp32 attention over the [rows, 3H] projection ``x2`` run its products on the bf16
-    matrix cores (attention_x6.hip)?"""
+    """Does the fp32 attention over the [rows, 3H] projection ``x2`` run its products on the piece
+    kernels (attention_f16.hip at any size -- faster than the f32-MFMA kernel from fine-tuning
+    batches up, tools/probe/attn_bwd_probe.py; attention_x6.hip from ``ATTN_X6_MIN_ROWS`` rows)?"""
     from . import gemm16
     rows = x2.numel() // max(1, x2.shape[-1])
-    return gemm16.enabled() and x2.dtype == torch.float32 and use_kernels(x2) and rows >= ATTN_X6_MIN_ROWS
+    min_rows = ATTN_X6_MIN_ROWS if _Attn.kernel == 'x6' else 1
+    return gemm16.enabled() and x2.dtype == torch.float32 and use_kernels(x2) and rows >= min_rows

@@ -63,10 +63,10 @@ def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialD
                              'bf16 piece passes from 4096 token rows) or native (f32 MFMA, 157 TF/s peak, '
                              'through the libraries: the numerics oracle); see ops/fp32_mode.py')
     parser.add_argument('--fp32-attention', default='fp16x3', choices=['fp16x3', 'x6'],
-                        help='with --fp32-gemm fp16x3, the attention products from 4096 token rows: fp16x3 '
-                             '(default: three fp16 passes over scaled two-piece operands, backward at two waves per '
+                        help='with --fp32-gemm fp16x3, the attention products: fp16x3 (default, every batch '
+                             'size: three fp16 passes over scaled two-piece operands, backward at two waves per '
                              'SIMD; rows 2^40 below their tile\'s largest value flushed) or x6 (six bf16 piece '
-                             'passes, every row fp32 class); see ops/fp32_mode.py')
+                             'passes from 4096 token rows, every row fp32 class); see ops/fp32_mode.py')
     parser.add_argument('--graph-train-step', action='store_true',
                         help='single GPU, one micro-batch per update: capture each input shape\'s whole '
                              'update (forward, backward, clip, optimizer) in a HIP graph after two eager '

@@ -704,7 +704,7 @@ Tensor gemm_bf16(Tensor a, Tensor b, OptT out_, bool beta, OptT bias, bool out_b
   p.abf16 = 1;
   p.obf16 = out_bf16 ? 1 : 0;
   check_vec(bias, p.N, "gemm_bf16 bias");
-  const int cfg = hx_gemm_f16_plan(p.M, p.N, p.K);
+  const int cfg = hx_gemm_bf16_plan(p.M, p.N, p.K);
   TORCH_CHECK(cfg >= 0, "gemm_bf16: no tile for N = ", p.N);
   TORCH_CHECK(!beta || has(out_), "gemm_bf16: beta needs an output to accumulate into");
   Tensor out = has(out_) ? *out_ : torch::empty({p.M, p.N}, a.options().dtype(out_bf16 ? torch::kBFloat16

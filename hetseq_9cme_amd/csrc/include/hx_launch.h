@@ -141,6 +141,7 @@ struct HxGemmF16 {
 // --precision bf16: W^T [K][N] bf16 of every weight of a batch (wt used, wf / mask ignored)
 void hx_weight_bf16_t(const HxWeightBatch& d, hipStream_t s);
 int hx_gemm_f16_plan(int M, int N, int K);
+int hx_gemm_bf16_plan(int M, int N, int K);
 int hx_gemm_f16_tiles(int M, int N, int cfg);
 int hx_gemm_f16_colpart_rows(int M, int cfg);
 int hx_gemm_f16_ks(int M, int N, int K, int cfg);

@@ -423,12 +423,13 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
 // cfg 1: 256 x 192, 8 waves (4 x 2) of 64 x 96 (A fragments split by two waves, fewer B reads)
 // cfg 2: 128 x 96, 4 waves of 32 x 96                                            -- M < 8192
 // cfg 3: 64 x 64, 4 waves (2 x 2) of 32 x 32                                     -- tiny M
+// cfg 5: 256 x 256, 8 waves (4 x 2) of 64 x 128                                  -- explicit only
 // cfg 4: 128 x 192, 4 waves of 32 x 192: two workgroups per CU (60 KB of LDS each), so one
 //        tile's prologue / epilogue store burst overlaps the other's main loop
-constexpr int kCfgs = 5;
-int cfg_bm(int c) { return c <= 1 ? 256 : c == 2 || c == 4 ? 128 : 64; }
-int cfg_bn(int c) { return c <= 1 || c == 4 ? 192 : c == 2 ? 96 : 64; }
-int cfg_nwm(int c) { return c == 0 ? 8 : c == 1 ? 4 : c == 2 || c == 4 ? 4 : 2; }
+constexpr int kCfgs = 6;
+int cfg_bm(int c) { return c <= 1 || c == 5 ? 256 : c == 2 || c == 4 ? 128 : 64; }
+int cfg_bn(int c) { return c == 5 ? 256 : c <= 1 || c == 4 ? 192 : c == 2 ? 96 : 64; }
+int cfg_nwm(int c) { return c == 0 ? 8 : c == 1 || c == 5 ? 4 : c == 2 || c == 4 ? 4 : 2; }
 
 template <int BM, int BN, int WM, int WN, int EPI, int AT = 0, int OB = 0>
 void launch_one(const F16Args& a, hipStream_t s) {
@@ -451,6 +452,7 @@ void launch_cfg(int cfg, const F16Args& a, hipStream_t s) {
   else if (cfg == 1) launch_one<256, 192, 64, 96, EPI, AT, OB>(a, s);
   else if (cfg == 2) launch_one<128, 96, 32, 96, EPI, AT, OB>(a, s);
   else if (cfg == 4) launch_one<128, 192, 32, 192, EPI, AT, OB>(a, s);
+  else if (cfg == 5) launch_one<256, 256, 64, 128, EPI, AT, OB>(a, s);
   else launch_one<64, 64, 32, 32, EPI, AT, OB>(a, s);
 }
 
@@ -822,6 +824,11 @@ int hx_gemm_f16_plan(int M, int N, int K) {
   if (N % 64 == 0) return 3;
   return -1;
 }
+
+// --precision bf16: the same plan.  The 256 x 256 tile (cfg 5) measured no better on either mode
+// in the step (r4y: 36.61 vs 36.65 ms/step forced to 256 x 192; bf16 19.48 with it on every
+// N % 256 product vs 18.8 without), so it stays an explicit choice (HX_GEMM_F16_CFG=5)
+int hx_gemm_bf16_plan(int M, int N, int K) { return hx_gemm_f16_plan(M, N, K); }
 
 int hx_gemm_f16_tiles(int M, int N, int cfg) {
   if (cfg < 0 || cfg >= kCfgs) return 0;

@@ -208,7 +208,7 @@ def test_gemm_bf16_mode(dev, M, N, K):
     assert ((out.double() - ref2).abs() / den2).max().item() < 8e-3
 
 
-@pytest.mark.parametrize('cfg', ['0', '1', '2', '3', '4'])
+@pytest.mark.parametrize('cfg', ['0', '1', '2', '3', '4', '5'])
 def test_gemm_f16_every_tile(dev, monkeypatch, cfg):
     """Every tile configuration of gemm_f16_k (HX_GEMM_F16_CFG forces it): forward with bias and the
     beta = 1 data gradient, rows not a multiple of the tile."""

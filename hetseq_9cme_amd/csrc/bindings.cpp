@@ -723,6 +723,80 @@ Tensor gemm_bf16(Tensor a, Tensor b, OptT out_, bool beta, OptT bias, bool out_b
   return out;
 }
 
+static HxGemmF16 bf16_args(const Tensor& a, const Tensor& b, const char* what) {
+  TORCH_CHECK(a.is_cuda() && a.scalar_type() == torch::kBFloat16 && b.scalar_type() == torch::kBFloat16 &&
+                  a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && a.stride(0) % 8 == 0 &&
+                  aligned16(a.data_ptr()) && b.is_contiguous() && aligned16(b.data_ptr()) && a.size(1) == b.size(1) &&
+                  a.size(1) % 32 == 0 && a.device() == b.device(),
+              what, ": a [M, K] / b [N, K] bf16 with 16-B rows, K % 32 == 0");
+  HxGemmF16 p{};
+  p.A = a.data_ptr();
+  p.lda = a.stride(0);
+  p.B = reinterpret_cast<const uint16_t*>(b.data_ptr());
+  p.ldb = b.size(1);
+  p.M = (int)a.size(0);
+  p.N = (int)b.size(0);
+  p.K = (int)a.size(1);
+  p.ks = 1;
+  p.abf16 = 1;
+  p.obf16 = 1;
+  return p;
+}
+
+// --precision bf16 FFN up: u = a . b^T + bias -> (gelu'(u), gelu(u)), both bf16 [M, N]
+std::vector<Tensor> gemm_bf16_gelu(Tensor a, Tensor b, Tensor bias) {
+  HxGemmF16 p = bf16_args(a, b, "gemm_bf16_gelu");
+  check_vec(bias, p.N, "gemm_bf16_gelu bias");
+  const int cfg = hx_gemm_bf16_plan(p.M, p.N, p.K);
+  TORCH_CHECK(cfg >= 0, "gemm_bf16_gelu: no tile for N = ", p.N);
+  Tensor d = torch::empty({p.M, p.N}, a.options()), h = torch::empty({p.M, p.N}, a.options());
+  p.kind = 1;
+  p.C = reinterpret_cast<float*>(d.data_ptr());
+  p.ldc = p.N;
+  p.bias = bias.data_ptr<float>();
+  p.P = reinterpret_cast<float*>(h.data_ptr());
+  p.ldp = p.N;
+  p.dmode = 1;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  TORCH_CHECK(hx_gemm_f16(p, cfg, cur_stream(a)) == 0, "gemm_bf16_gelu: launch failed");
+  dbg_finite(h, "gemm_bf16_gelu");
+  return {d, h};
+}
+
+// --precision bf16 FFN-down data gradient + GELU backward: t = (a . b^T) * (dmode ? d : gelu'(d + bias))
+// (d: bf16 gelu'(u) from gemm_bf16_gelu, or the pre-bias u) -> (t bf16, dbias = column sums of t
+// into dbias_out when given)
+std::vector<Tensor> gemm_bf16_dgelu(Tensor a, Tensor b, Tensor d, OptT dbias_out, OptT bias, int64_t dmode) {
+  TORCH_CHECK(!dmode || !has(bias), "gemm_bf16_dgelu: dmode 1 takes gelu'(u), which has the bias in it");
+  HxGemmF16 p = bf16_args(a, b, "gemm_bf16_dgelu");
+  check_vec(bias, p.N, "gemm_bf16_dgelu bias");
+  TORCH_CHECK(d.scalar_type() == torch::kBFloat16 && d.dim() == 2 && d.size(0) == p.M && d.size(1) == p.N &&
+                  d.is_contiguous() && aligned16(d.data_ptr()) && d.device() == a.device(),
+              "gemm_bf16_dgelu: d must be bf16 [M, N]");
+  const int cfg = hx_gemm_bf16_plan(p.M, p.N, p.K);
+  TORCH_CHECK(cfg >= 0, "gemm_bf16_dgelu: no tile for N = ", p.N);
+  const int prow = hx_gemm_f16_colpart_rows(p.M, cfg);
+  auto f32 = a.options().dtype(torch::kFloat32);
+  Tensor t = torch::empty({p.M, p.N}, a.options());
+  Tensor part = torch::empty({prow, p.N}, f32);
+  Tensor db = has(dbias_out) ? *dbias_out : torch::empty({p.N}, f32);
+  TORCH_CHECK(db.numel() == p.N && db.scalar_type() == torch::kFloat32 && db.is_contiguous() && db.device() == a.device(),
+              "gemm_bf16_dgelu: dbias");
+  p.kind = 2;
+  p.bias = ptr_or_null<float>(bias);
+  p.aux = reinterpret_cast<const float*>(d.data_ptr());
+  p.ldaux = p.N;
+  p.P = reinterpret_cast<float*>(t.data_ptr());
+  p.ldp = p.N;
+  p.colpart = part.data_ptr<float>();
+  p.dmode = dmode ? 1 : 0;
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
+  TORCH_CHECK(hx_gemm_f16(p, cfg, cur_stream(a)) == 0, "gemm_bf16_dgelu: launch failed");
+  hx_fold_cols(part.data_ptr<float>(), prow, p.N, db.data_ptr<float>(), 0, cur_stream(a));
+  dbg_finite(t, "gemm_bf16_dgelu");
+  return {t, db};
+}
+
 // W^T in bf16 ([K, N]) of every fp32 weight W [N, K] in the list, one launch
 std::vector<Tensor> weight_bf16_t(std::vector<Tensor> Ws) {
   TORCH_CHECK(!Ws.empty() && Ws.size() <= HX_WBATCH, "weight_bf16_t: 1..64 weights");
@@ -882,6 +956,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_f16_dgelu", &gemm_f16_dgelu, py::arg("a"), py::arg("a_amax"), py::arg("b"), py::arg("b_amax"),
         py::arg("u"), py::arg("bias") = py::none(), py::arg("dbias_out") = py::none(), py::arg("dmode") = 1);
   m.def("wgrad_f16", &wgrad_f16);
+  m.def("gemm_bf16_gelu", &gemm_bf16_gelu, py::arg("a"), py::arg("b"), py::arg("bias"));
+  m.def("gemm_bf16_dgelu", &gemm_bf16_dgelu, py::arg("a"), py::arg("b"), py::arg("d"),
+        py::arg("dbias_out") = py::none(), py::arg("bias") = py::none(), py::arg("dmode") = 1);
   m.def("gemm_bf16", &gemm_bf16, py::arg("a"), py::arg("b"), py::arg("out") = py::none(), py::arg("beta") = false,
         py::arg("bias") = py::none(), py::arg("out_bf16") = true);
   m.def("weight_bf16_t", &weight_bf16_t);

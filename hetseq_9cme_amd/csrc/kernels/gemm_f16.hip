@@ -84,7 +84,7 @@ struct F16Args {
 //       OB: the output C in bf16 (EPI 0 / 3 only)
 template <int BM, int BN, int WM, int WN, int EPI, int OCC, int AT = 0, int OB = 0>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F16Args g) {
-  static_assert(AT == 0 || EPI == 0 || EPI == 3, "bf16 operands: plain / beta epilogues");
+  static_assert(AT == 0 || EPI == 0 || EPI == 3 || OB == 1, "bf16 operands: GELU epilogues in bf16");
   static_assert(OB == 0 || AT == 1, "bf16 output with bf16 operands");
   constexpr int KD = AT ? 32 : 16;       // k elements per stage
   constexpr int AE = AT ? 2 : 4;         // A element bytes
@@ -278,7 +278,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
     if (g.bias) t = *reinterpret_cast<const float4*>(g.bias + n0 + ncol + 32 * b);
     bias[b][0] = t.x; bias[b][1] = t.y; bias[b][2] = t.z; bias[b][3] = t.w;
   }
-  if constexpr (OB == 1) {
+  if constexpr (OB == 1 && (EPI == 0 || EPI == 3)) {
     // bf16 output [M][ldc]: 4 consecutive columns of a row per lane -> one 8-B store
     const hx::Buf obuf(reinterpret_cast<uint16_t*>(g.C) + (int64_t)m0 * g.ldc + n0, (uint32_t)((int64_t)mrows * g.ldc * 2));
 #pragma unroll
@@ -321,9 +321,22 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
       __builtin_amdgcn_sched_barrier(0);
     }
   } else {
-    const hx::Buf pbuf(g.P + (int64_t)m0 * g.ldp + n0, (uint32_t)((int64_t)mrows * g.ldp * 4));
-    const hx::Buf xbuf(EPI == 2 ? g.aux + (int64_t)m0 * g.ldaux + n0 : g.C, (uint32_t)((int64_t)mrows * g.ldaux * 4));
-    auto poff = [&](int a, int b, int gq) { return (uint32_t)((mrow + 32 * a + 8 * gq) * g.ldp + ncol + 32 * b) * 4; };
+    // GELU epilogues; OB: C / P / aux in bf16 (--precision bf16: 8-B accesses of 4 columns)
+    constexpr int OE = OB ? 2 : 4;
+    const hx::Buf pbuf((const char*)g.P + ((int64_t)m0 * g.ldp + n0) * OE, (uint32_t)((int64_t)mrows * g.ldp * OE));
+    const hx::Buf xbuf(EPI == 2 ? (const char*)g.aux + ((int64_t)m0 * g.ldaux + n0) * OE : (const char*)g.C,
+                       (uint32_t)((int64_t)mrows * g.ldaux * OE));
+    const hx::Buf obuf((const char*)g.C + ((int64_t)m0 * g.ldc + n0) * OE, (uint32_t)((int64_t)mrows * g.ldc * OE));
+    auto poff = [&](int a, int b, int gq) { return (uint32_t)((mrow + 32 * a + 8 * gq) * g.ldp + ncol + 32 * b) * OE; };
+    auto st4 = [&](const hx::Buf& bf, uint32_t off, f32x4 v) {
+      if constexpr (OB == 1) {
+        const uint2 pk = make_uint2(hx::f2bf(v[0]) | ((uint32_t)hx::f2bf(v[1]) << 16),
+                                    hx::f2bf(v[2]) | ((uint32_t)hx::f2bf(v[3]) << 16));
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, pk), bf.r, off, 0, 0);
+      } else {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), bf.r, off, 0, 0);
+      }
+    };
     float csum[NB][4];
 #pragma unroll
     for (int b = 0; b < NB; ++b)
@@ -337,10 +350,16 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
         f32x4 u[4];
         if constexpr (EPI == 2) {
 #pragma unroll
-          for (int gq = 0; gq < 4; ++gq)
-            u[gq] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                  xbuf.r, (uint32_t)((mrow + 32 * a + 8 * gq) * g.ldaux + ncol + 32 * b) * 4,
-                                                  0, 0));
+          for (int gq = 0; gq < 4; ++gq) {
+            const uint32_t off = (uint32_t)((mrow + 32 * a + 8 * gq) * g.ldaux + ncol + 32 * b) * OE;
+            if constexpr (OB == 1) {
+              const u32x2 c = __builtin_amdgcn_raw_buffer_load_b64(xbuf.r, off, 0, 0);
+              u[gq] = f32x4{hx::bf2f((uint16_t)(c[0] & 0xffff)), hx::bf2f((uint16_t)(c[0] >> 16)),
+                            hx::bf2f((uint16_t)(c[1] & 0xffff)), hx::bf2f((uint16_t)(c[1] >> 16))};
+            } else {
+              u[gq] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xbuf.r, off, 0, 0));
+            }
+          }
         }
 #pragma unroll
         for (int gq = 0; gq < 4; ++gq) {
@@ -367,7 +386,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
                 o[i] = hx::gelu_f(v[i]);
               }
             }
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, c), cbuf.r, coff(a, b, gq), 0, 0);
+            st4(obuf, coff(a, b, gq) / 4 * OE, c);
           } else {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
@@ -376,7 +395,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
             }
           }
           if (in) amx = fmaxf(amx, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), pbuf.r, poff(a, b, gq), 0, 0);
+          st4(pbuf, poff(a, b, gq), o);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -825,10 +844,16 @@ int hx_gemm_f16_plan(int M, int N, int K) {
   return -1;
 }
 
-// --precision bf16: the same plan.  The 256 x 256 tile (cfg 5) measured no better on either mode
-// in the step (r4y: 36.61 vs 36.65 ms/step forced to 256 x 192; bf16 19.48 with it on every
-// N % 256 product vs 18.8 without), so it stays an explicit choice (HX_GEMM_F16_CFG=5)
-int hx_gemm_bf16_plan(int M, int N, int K) { return hx_gemm_f16_plan(M, N, K); }
+// --precision bf16: the same plan, except that the large tile's bf16 products run on 64 x 96
+// waves (cfg 1): with one pass per 32-deep stage the A fragments shared by two waves read less LDS
+// per MFMA (r4af: FFN up 109 vs 116-121 us, with the GELU epilogue 158 vs 183 us; step 18.88 vs
+// 19.02 ms).  The 256 x 256 tile (cfg 5) measured no better on either mode in the step (r4y:
+// 36.61 vs 36.65 ms/step forced to 256 x 192; bf16 19.48 with it on every N % 256 product vs 18.8
+// without), so it stays an explicit choice (HX_GEMM_F16_CFG=5)
+int hx_gemm_bf16_plan(int M, int N, int K) {
+  const int c = hx_gemm_f16_plan(M, N, K);
+  return c == 0 && !getenv("HX_GEMM_F16_CFG") ? 1 : c;
+}
 
 int hx_gemm_f16_tiles(int M, int N, int cfg) {
   if (cfg < 0 || cfg >= kCfgs) return 0;
@@ -895,7 +920,7 @@ int hx_gemm_f16(const HxGemmF16& p, int cfg, hipStream_t s) {
   const int ks = p.ks < 1 ? 1 : p.ks;
   if (p.K % (kd * ks) || (ks > 1 && (p.beta || p.kind || p.bias || p.obf16 || p.c_zs < (int64_t)(p.M - 1) * p.ldc + p.N)))
     return -1;
-  if ((p.abf16 && p.kind) || (p.obf16 && (!p.abf16 || p.ldc % 4))) return -1;
+  if ((p.abf16 && p.kind && !p.obf16) || (p.obf16 && (!p.abf16 || p.ldc % 4))) return -1;
   if (p.kind < 0 || p.kind > 2 || (p.kind && (!p.P || p.beta || p.ldp % 4)) || (p.kind == 2 && !p.aux)) return -1;
   F16Args a;
   a.A = p.A;
@@ -923,7 +948,9 @@ int hx_gemm_f16(const HxGemmF16& p, int cfg, hipStream_t s) {
   a.ks = ks;
   a.c_zs = p.c_zs;
   if (p.abf16) {
-    if (p.obf16 && p.beta) launch_cfg<3, 1, 1>(cfg, a, s);
+    if (p.kind == 1) launch_cfg<1, 1, 1>(cfg, a, s);        // bf16 FFN up: gelu'(u), gelu(u) in bf16
+    else if (p.kind == 2) launch_cfg<2, 1, 1>(cfg, a, s);   // bf16 FFN-down dgrad * gelu'(u)
+    else if (p.obf16 && p.beta) launch_cfg<3, 1, 1>(cfg, a, s);
     else if (p.obf16) launch_cfg<0, 1, 1>(cfg, a, s);
     else if (p.beta) launch_cfg<3, 1, 0>(cfg, a, s);
     else launch_cfg<0, 1, 0>(cfg, a, s);

@@ -99,15 +99,16 @@ def _dgrad(dy2, W, xshape, mbox):
     return dx if other is None else dx + other.view(xshape).to(dx.dtype)
 
 
-def _dgrad_bf16(dy2, W, xshape, mbox):
+def _dgrad_bf16(dy2, W, xshape, mbox, wt=None):
     """``_dgrad`` for --precision bf16 on the hand-written kernel: dy . (W^T)^T with the bf16 W^T
-    of the running forward, beta = 1 into the deposited residual gradient if any."""
-    wt = gemm16.bf16_wt(W)
+    (``wt``: kept by the forward from its one-launch batch, so the backward converts nothing),
+    beta = 1 into the deposited residual gradient if any."""
+    wt = wt if wt is not None else gemm16.bf16_wt(W)
     dy2 = gemm16.rows2(dy2)
     if mbox is not None:
         g, other = mbox.take(dy2.dtype)
         if g is not None:
-            return gemm16.mm_bf16(dy2, wt, out=g.view(-1, W.shape[1]), beta=True).view(xshape)
+            return gemm16.mm_bf16(dy2, wt, out=g.view(-1, xshape[-1]), beta=True).view(xshape)
         dx = gemm16.mm_bf16(dy2, wt).view(xshape)
         return dx if other is None else dx + other.view(xshape).to(dx.dtype)
     return gemm16.mm_bf16(dy2, wt).view(xshape)
@@ -410,8 +411,11 @@ class _LinearFn(torch.autograd.Function):
             return y.view(*x.shape[:-1], y.shape[-1])
         Wc = cast_w(W, x.dtype)
         ctx.b16 = gemm16.bf16_ok(x2, W.shape[0], W.shape[1]) and Wc.is_contiguous()
+        ctx.wt_b16 = None
         if ctx.b16:   # --precision bf16 on the hand-written kernel (bias in the epilogue)
             y = gemm16.mm_bf16(gemm16.rows2(x), Wc, bias=b)
+            if ctx.needs_input_grad[0]:
+                ctx.wt_b16 = gemm16.bf16_wt(W)   # the forward's batched W^T, for the data gradient
         else:
             y = torch.mm(x2, Wc.t()) if b is None else torch.addmm(cast_w(b, x.dtype), x2, Wc.t())
         ctx.save_for_backward(x2, Wc)
@@ -427,7 +431,7 @@ class _LinearFn(torch.autograd.Function):
         if not ctx.needs_input_grad[0]:
             dx = None
         elif ctx.b16:
-            dx = _dgrad_bf16(dy2, W, ctx.xshape, ctx.mbox)
+            dx = _dgrad_bf16(dy2, W, ctx.xshape, ctx.mbox, ctx.wt_b16)
         else:
             dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox)
         slot = grad_slot(W)
@@ -536,13 +540,52 @@ def _ffn_backward_f16(ctx, dy):
     return dx, dW1, db1, dW2, None
 
 
+class _FFNBf16Fn(torch.autograd.Function):
+    """``_FFNFn`` for --precision bf16 on the same kernel's bf16 variant: the FFN-up epilogue adds
+    the bias and writes gelu(u) and gelu'(u) in bf16; the FFN-down data gradient's epilogue
+    multiplies by gelu'(u) and sums the FFN-up bias gradient (no bias_act pass either way)."""
+
+    @staticmethod
+    def forward(ctx, x, W1, b1, W2, mbox):
+        x2 = gemm16.rows2(x)
+        d, h = C().gemm_bf16_gelu(x2, cast_w(W1, torch.bfloat16), b1)
+        y2 = gemm16.mm_bf16(h, cast_w(W2, torch.bfloat16))
+        # the forward's batched W^T copies (one launch per forward) for the data gradients
+        ctx.save_for_backward(x2, d, h, gemm16.bf16_wt(W1), gemm16.bf16_wt(W2))
+        ctx.W, ctx.b1, ctx.mbox, ctx.xshape = (W1, W2), b1, mbox, x.shape
+        return y2.view(*x.shape[:-1], y2.shape[-1])
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, d, h, w1t, w2t = ctx.saved_tensors
+        W1, W2 = ctx.W
+        dy2 = gemm16.rows2(dy)
+        dW2 = _wgrad(dy2, h, grad_slot(W2))
+        t, db1 = C().gemm_bf16_dgelu(dy2, w2t, d, grad_slot(ctx.b1))
+        dW1 = _wgrad(t, x2, grad_slot(W1))
+        dx = _dgrad_bf16(t, None, ctx.xshape, ctx.mbox, w1t)
+        return dx, dW1, db1, dW2, None
+
+
+def _ffn_bf16_ok(x, W1, b1, W2):
+    x2 = x.reshape(-1, x.shape[-1])
+    return (b1 is not None and b1.dtype == torch.float32 and b1.is_contiguous() and
+            gemm16.bf16_ok(x2, W1.shape[0], W1.shape[1]) and W2.shape[0] % 64 == 0 and
+            cast_w(W1, torch.bfloat16).is_contiguous() and cast_w(W2, torch.bfloat16).is_contiguous())
+
+
 def ffn_fusable(x, W1, b1, W2):
-    """The fused FFN path applies (fp32 GPU activations on the fp16x3 GEMMs)."""
+    """The fused FFN path applies: fp32 GPU activations on the fp16x3 GEMMs, or bf16 GPU
+    activations (--precision bf16) on the bf16 variant."""
+    if x.dtype == torch.bfloat16:
+        return _ffn_bf16_ok(x, W1, b1, W2)
     return b1 is not None and gemm16.ok(x.reshape(-1, x.shape[-1]), W1.shape[0]) and W2.shape[0] % 64 == 0
 
 
 def ffn(x, W1, b1, W2, res_grad=None):
     """gelu(x W1^T + b1) W2^T (the output bias / dropout / residual / LayerNorm follow)."""
+    if x.dtype == torch.bfloat16:
+        return _FFNBf16Fn.apply(x, W1, b1, W2, res_grad)
     return _FFNFn.apply(x, W1, b1, W2, res_grad)
 
 
@@ -619,8 +662,11 @@ class _Linear3Fn(torch.autograd.Function):
             Wc = Wc if Wc is not None else W.to(x.dtype)
             bc = cast_w(b, x.dtype) if has_b else None
         ctx.b16 = gemm16.bf16_ok(x2, W.shape[0], W.shape[1]) and Wc.is_contiguous()
+        ctx.wt_b16 = None
         if ctx.b16:
             y = gemm16.mm_bf16(gemm16.rows2(x), Wc, bias=b if has_b else None)
+            if ctx.needs_input_grad[0]:
+                ctx.wt_b16 = gemm16.bf16_wt(W)   # the forward's batched W^T, for the data gradient
         else:
             y = torch.addmm(bc, x2, Wc.t()) if has_b else torch.mm(x2, Wc.t())
         ctx.save_for_backward(x2, Wc)
@@ -643,8 +689,7 @@ class _Linear3Fn(torch.autograd.Function):
             if not ctx.needs_input_grad[0]:
                 dx = None
             elif ctx.b16:
-                Wf = _adjacent_view([wq, wk, wv])
-                dx = _dgrad_bf16(dy2, Wf if Wf is not None else torch.cat([wq, wk, wv], 0), ctx.xshape, ctx.mbox)
+                dx = _dgrad_bf16(dy2, None, ctx.xshape, ctx.mbox, ctx.wt_b16)
             else:
                 dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox)
             wg = lambda slot: _wgrad(dy2, x2, slot)

@@ -208,6 +208,69 @@ def test_gemm_bf16_mode(dev, M, N, K):
     assert ((out.double() - ref2).abs() / den2).max().item() < 8e-3
 
 
+@pytest.mark.parametrize('cfg', ['plan', '2', '4'])
+def test_gemm_bf16_gelu_epilogues(dev, monkeypatch, cfg):
+    """--precision bf16 FFN epilogues on the bf16 variant: up (bias + GELU -> gelu'(u), gelu(u) in
+    bf16) and the FFN-down data gradient times gelu'(u) with the bias-gradient column sums, against
+    fp64 of the same bf16 operands (bf16 output rounding only); rows not a multiple of the tile."""
+    from hetseq_9cme_amd.ops.fused import gelu_ref
+    if cfg != 'plan':
+        monkeypatch.setenv('HX_GEMM_F16_CFG', cfg)
+    g = torch.Generator(device=dev).manual_seed(13)
+    M, H, I = 4096 + 37, 768, 3072
+    x = torch.randn(M, H, device=dev, generator=g).bfloat16()
+    W1 = (torch.randn(I, H, device=dev, generator=g) * 0.02).bfloat16()
+    b1 = torch.randn(I, device=dev, generator=g) * 0.1
+    d, h = C().gemm_bf16_gelu(x, W1, b1)
+    assert d.dtype == h.dtype == torch.bfloat16
+    u64 = x.double() @ W1.double().t() + b1.double()
+    den = x.abs().double() @ W1.abs().double().t() + b1.abs().double()
+    assert ((h.double() - gelu_ref(u64)).abs() / den).max().item() < 8e-3
+    ug = u64.float().requires_grad_(True)
+    gelu_ref(ug).sum().backward()
+    torch.testing.assert_close(d.float(), ug.grad, rtol=8e-3, atol=8e-3)
+    W2 = (torch.randn(H, I, device=dev, generator=g) * 0.02).bfloat16()
+    w2t = W2.t().contiguous()
+    dy = (torch.randn(M, H, device=dev, generator=g) * 1e-3).bfloat16()
+    t, db = C().gemm_bf16_dgelu(dy, w2t, d)
+    assert t.dtype == torch.bfloat16 and db.dtype == torch.float32
+    t64 = (dy.double() @ W2.double()) * d.double()
+    den = (dy.abs().double() @ W2.abs().double()) * d.abs().double()
+    assert ((t.double() - t64).abs() / den.clamp_min(1e-300)).max().item() < 8e-3
+    # d b1: fp32 sums of the fp32 products (before their bf16 rounding)
+    assert ((db.double() - t64.sum(0)).abs() / t64.abs().sum(0)).max().item() < 1e-5
+    slot = torch.zeros(I, device=dev)
+    C().gemm_bf16_dgelu(dy, w2t, d, slot)
+    assert torch.equal(slot, db)
+
+
+def test_ffn_bf16_autograd(dev):
+    """ops.ffn on bf16 activations (the --precision bf16 BERT FFN): output and every gradient
+    against the fp32 reference of the same op on the same bf16-rounded operands."""
+    from hetseq_9cme_amd.ops import fused
+    from hetseq_9cme_amd.ops.fused import gelu_ref
+    g = torch.Generator(device=dev).manual_seed(17)
+    T, H, I = 2048, 768, 3072
+    x = torch.randn(4, T // 4, H, device=dev, generator=g).bfloat16().requires_grad_(True)
+    W1 = (torch.randn(I, H, device=dev, generator=g) * 0.02).requires_grad_(True)
+    b1 = (torch.randn(I, device=dev, generator=g) * 0.1).requires_grad_(True)
+    W2 = (torch.randn(H, I, device=dev, generator=g) * 0.02).requires_grad_(True)
+    assert fused.ffn_fusable(x, W1, b1, W2)
+    y = fused.ffn(x, W1, b1, W2)
+    assert y.dtype == torch.bfloat16
+    dy = torch.randn(y.shape, device=dev, generator=g).bfloat16()
+    y.backward(dy)
+    xr = x.detach().float().requires_grad_(True)
+    W1r, b1r, W2r = [t.detach().clone().requires_grad_(True) for t in (W1, b1, W2)]
+    h = gelu_ref(xr @ W1r.bfloat16().float().t() + b1r)
+    yr = h @ W2r.bfloat16().float().t()
+    yr.backward(dy.float())
+    rel = lambda a, b: ((a.float() - b).norm() / b.norm()).item()
+    assert rel(y, yr) < 1e-2
+    assert rel(x.grad, xr.grad) < 1e-2
+    assert rel(W1.grad, W1r.grad) < 1e-2 and rel(W2.grad, W2r.grad) < 1e-2 and rel(b1.grad, b1r.grad) < 1e-2
+
+
 @pytest.mark.parametrize('cfg', ['0', '1', '2', '3', '4', '5'])
 def test_gemm_f16_every_tile(dev, monkeypatch, cfg):
     """Every tile configuration of gemm_f16_k (HX_GEMM_F16_CFG forces it): forward with bias and the

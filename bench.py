@@ -88,8 +88,9 @@ def parse():
                          'beside one) spins for US microseconds beside the step on its own stream, its workgroups '
                          'dealt over the XCDs like an RCCL kernel\'s ("mask": confined to CUs 0..CUS-1 by a CU-masked '
                          'stream instead) (tools/probe/comm_contention_probe.sh)')
-    ap.add_argument('--comm-cus', default='auto',
-                    help='CUs left to the overlapped gradient all-reduce for N > 1 (train.py --comm-cus)')
+    ap.add_argument('--comm-cus', default='0',
+                    help='CUs left to the overlapped gradient all-reduce for N > 1 (train.py --comm-cus; '
+                         'default 0 = no reservation and no RCCL channel cap)')
     ap.add_argument('--comm-probe-steps', type=int, default=5,
                     help='N > 1: untimed steps AFTER the timed region with the gradient collectives off, for '
                          'exposed_comm_ms (0 = skip)')
@@ -99,6 +100,39 @@ def parse():
     ap.add_argument('--init-method', default=None, help=argparse.SUPPRESS)
     ap.add_argument('--nodes-meta', default=None, help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+def _bus_id(dev):
+    try:
+        return int(torch.cuda.get_device_properties(dev).pci_bus_id)
+    except Exception:
+        return -1
+
+
+def allreduce_busbw(ctrl, world, reps=3):
+    """Bus bandwidth (GB/s) of the gradient all-reduce alone: every reducer bucket (slices of
+    the flat gradient buffer, the reducer's sizes and order) all-reduced ``reps`` times on the
+    compute stream, timed between barriers; None without a reducer.  Runs after the timed
+    region and leaves the gradients summed over ranks (the next step overwrites them)."""
+    red = getattr(ctrl, 'reducer', None)
+    if red is None or not red.enabled or world < 2:
+        return None
+    g = ctrl.flat.grad_flat
+    sizes = [(s, e) for (s, e, _) in red.buckets]
+    nbytes = sum(e - s for s, e in sizes) * g.element_size()
+    for s, e in sizes:   # warm-up
+        torch.distributed.all_reduce(g[s:e], group=red.group)
+    torch.cuda.synchronize()
+    torch.distributed.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        for s, e in sizes:
+            torch.distributed.all_reduce(g[s:e], group=red.group)
+    torch.cuda.synchronize()
+    dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device='cuda')
+    torch.distributed.all_reduce(dt, op=torch.distributed.ReduceOp.MAX)
+    t = float(dt.item()) / reps
+    return round(2.0 * (world - 1) / world * nbytes / t / 1e9, 1)
 
 
 def launch_nodes(a):
@@ -279,6 +313,14 @@ def run(a, rank, world, dev_index, init_method):
         torch.distributed.all_reduce(nc, op=torch.distributed.ReduceOp.MAX)
         ctrl.reducer.enabled = True
         exposed = ms - float(nc.item()) / a.comm_probe_steps * 1000.0
+    busbw, dev_map = None, None
+    if world > 1:
+        busbw = allreduce_busbw(ctrl, world)
+        # rank -> (node-local device index, PCI bus id): which GPUs the ranks really drove
+        me = torch.tensor([rank, dev_index, _bus_id(dev_index)], dtype=torch.int64, device='cuda')
+        allm = [torch.zeros_like(me) for _ in range(world)]
+        torch.distributed.all_gather(allm, me)
+        dev_map = {int(t[0]): [int(t[1]), '{:02x}'.format(int(t[2]))] for t in allm}
     global_batch = a.batch * a.update_freq * world
     value = global_batch * a.steps / elapsed
     ref = REF_SAMPLES_PER_SEC.get(world)
@@ -315,6 +357,12 @@ def run(a, rank, world, dev_index, init_method):
             'transport': ('xgmi' if getattr(ctrl.reducer, 'xgmi', None) is not None else a.backend)
                          if world > 1 else None,
             'comm_cus': getattr(ctrl, 'comm_cus', 0),
+            # N > 1: the gradient buckets' all-reduce measured alone after the timed region
+            # (bus bandwidth = 2 (W - 1) / W x bytes / time, the RCCL-tests convention), the RCCL
+            # channel cap in effect, and the rank -> [device index, PCI bus] map
+            'allreduce_busbw_gbs': busbw,
+            'rccl_max_nchannels': os.environ.get('NCCL_MAX_NCHANNELS') if world > 1 else None,
+            'rank_devices': dev_map,
         }
         print(json.dumps(rec), flush=True)
     if a.profile_phases or a.sync_debug:

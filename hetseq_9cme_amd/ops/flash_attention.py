@@ -83,7 +83,9 @@ class _AttnFn(torch.autograd.Function):
             B, S = qkv.shape[0], qkv.shape[1]
             am = torch.empty(((S + 127) // 128) * num_heads * B * 4, dtype=torch.float32, device=qkv.device) \
                 if gemm16.enabled() else None
-            fwd = C().attn_fwd_f16 if fp32_mode.fp32_attention_mode() == 'fp16x3' else C().attn_fwd_x6
+            # the backward pairs with the kernel family THIS forward ran, whatever the mode is later
+            ctx.f16 = fp32_mode.fp32_attention_mode() == 'fp16x3'
+            fwd = C().attn_fwd_f16 if ctx.f16 else C().attn_fwd_x6
             out, lse, dmask = fwd(qkv, mask_bias, num_heads, keep, seed, stream, bias, am)
             gemm16.attach(out, am)
         else:
@@ -110,7 +112,7 @@ class _AttnFn(torch.autograd.Function):
             # projection's data / weight gradient GEMMs
             am = torch.empty(qkv.shape[0] * num_heads, dtype=torch.float32, device=qkv.device) \
                 if gemm16.enabled() and qkv.shape[1] <= 128 else None
-            bwd = C().attn_bwd_f16 if fp32_mode.fp32_attention_mode() == 'fp16x3' else C().attn_bwd_x6
+            bwd = C().attn_bwd_f16 if ctx.f16 else C().attn_bwd_x6
             dqkv, dbias = bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep, ctx.bias,
                               *slots, am)
             gemm16.attach(dqkv, am)

@@ -213,14 +213,15 @@ def add_distributed_training_args(parser):
                             'bucket all-reduces are scheduled ahead of queued backward kernels)')
     group.add_argument('--xgmi-blocks', default=64, type=int, metavar='N',
                        help='workgroups per xGMI all-reduce launch (CUs taken from backward while it runs)')
-    group.add_argument('--comm-cus', default='auto', type=_comm_cus_arg, metavar='N',
+    group.add_argument('--comm-cus', default=0, type=_comm_cus_arg, metavar='N',
                        help='MI355X: CUs left to the gradient all-reduce while it overlaps the backward (world > 1): '
                             'from the first bucket collective to the end of backward the one-round GEMM / '
                             'weight-gradient plans are sized for the other CUs, RCCL is capped at N channels '
                             '(NCCL_MAX_NCHANNELS, one workgroup each) and the xGMI kernel runs on N CUs -- see '
                             'csrc/kernels/cu_reserve.hip and profiles/r3_comm_contention.md (a 16-CU comm load: '
-                            '+15 %% step time unplanned, +6 %% with the plans sized around it).  0 = off; '
-                            'auto (default) = 16 on GPU runs with world > 1, else off')
+                            '+15 %% step time unplanned, +6 %% with the plans sized around it).  0 (default) = off '
+                            'until a multi-GPU measurement justifies a reservation; auto = 16 on GPU runs with '
+                            'world > 1, else off')
     group.add_argument('--force-reducer', action='store_true',
                        help='MI355X: run the bucketed gradient reducer even in a one-rank process group, so a '
                             'one-GPU run exercises the RCCL stream path (buckets, side-stream ordering, '

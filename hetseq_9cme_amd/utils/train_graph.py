@@ -98,6 +98,15 @@ class GraphedTrainStep(object):
             return False
         if c.reducer.enabled and not _capturable_group(c):
             return False
+        # the xGMI all-reduce numbers its rounds from a host counter passed as a kernel argument
+        # (xgmi_allreduce.hip): a captured launch would replay the capture-time round, its peer
+        # waits would pass at once and ranks could read half-reduced buckets -- RCCL only
+        if c.reducer.enabled and getattr(c.reducer, 'xgmi', None) is not None:
+            return False
+        # the slow stats path (all_gather_list + .item(), the used-flag .tolist()) synchronises
+        # with the host and cannot be captured: with synced stats the update must use the fast path
+        if c.reducer.enabled and c._sync_stats() and not c.fast_stat_sync:
+            return False
         return not getattr(c.args, 'use_bmuf', False)
 
     def _key(self, sample):

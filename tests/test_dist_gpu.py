@@ -88,7 +88,13 @@ def test_bench_two_ranks_contract(tmp_path):
     assert rec['ranks_seen'] == rec['n_gpus'] == 2
     assert rec['per_rank_ms']['min'] <= rec['per_rank_ms']['max'] == rec['ms_per_step']
     assert rec['exposed_comm_ms'] is not None and rec['transport'] == 'gloo'
-    assert rec['comm_cus'] == 0          # auto: no reservation for a gloo rehearsal
+    assert rec['comm_cus'] == 0          # default: no reservation
+    # comm self-description of an N > 1 run: bucket all-reduce bus bandwidth, channel cap, and
+    # the rank -> device map (both ranks on this box's one GPU here)
+    assert rec['allreduce_busbw_gbs'] is not None and rec['allreduce_busbw_gbs'] > 0
+    assert 'rccl_max_nchannels' in rec and rec['rccl_max_nchannels'] is None
+    assert sorted(rec['rank_devices']) == ['0', '1']
+    assert all(v[0] == 0 for v in rec['rank_devices'].values())
 
 
 def test_bench_heterogeneous_nodes_contract(tmp_path):

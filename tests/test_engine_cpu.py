@@ -192,3 +192,41 @@ def test_four_rank_gradient_equivalence_small_buckets(tmp_path, bert_data):
     c4 = load(os.path.join(four, 'checkpoint_last.pt'))
     for k in c1['model']:
         torch.testing.assert_close(c1['model'][k], c4['model'][k], rtol=1e-5, atol=1e-6, msg=k)
+
+
+@pytest.mark.slow
+def test_heterogeneous_5p3_replicas_match_update_freq(tmp_path):
+    """The BASELINE 5+3 heterogeneous launch in miniature on the CPU: tools/launch_hetero.py
+    starts two "nodes" (5 and 3 ranks, one tcp:// rendezvous, gloo), BERT-tiny, 3 updates.
+    --check-params-every 1 asserts bit-identical replicas after every update on every rank, and
+    the result equals ONE rank with --update-freq 8 (the 8 micro-batches of an update, summed
+    locally instead of all-reduced: same math, different summation order)."""
+    d = tmp_path / 'data'
+    d.mkdir()
+    write_synthetic_bert_shards(str(d), n_files=2, samples_per_file=64, seq_len=32, max_pred=5, vocab_size=1024,
+                                split='train', seed=3)
+    write_synthetic_bert_shards(str(d), n_files=1, samples_per_file=16, seq_len=32, max_pred=5, vocab_size=1024,
+                                split='test', seed=4)
+    cfg0 = write_bert_config(str(tmp_path / 'nodrop.json'),
+                             **dict(BERT_TINY, hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0))
+    vocab = write_vocab(str(tmp_path / 'vocab.txt'), 1024)
+    het, one = str(tmp_path / 'het'), str(tmp_path / 'one')
+    common = ['--task', 'bert', '--data', str(d), '--dict', vocab, '--config_file', cfg0, '--max-sentences', '4',
+              '--fast-stat-sync', '--valid-subset', 'test', '--num-workers', '0', '--lr', '1e-3',
+              '--warmup-updates', '2', '--weight-decay', '0.01', '--log-interval', '1', '--max-update', '3',
+              '--disable-validation']
+    e = dict(os.environ)
+    e['PYTHONPATH'] = ROOT + os.pathsep + e.get('PYTHONPATH', '')
+    e['OMP_NUM_THREADS'] = '1'
+    r = subprocess.run([sys.executable, os.path.join(ROOT, 'tools', 'launch_hetero.py'), '--cpu', '--nodes', '5,3',
+                        '--'] + common + ['--save-dir', het, '--check-params-every', '1',
+                                          '--distributed-backend', 'gloo'],
+                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=e, timeout=900)
+    assert r.returncode == 0, r.stdout[-4000:]
+    run_cli(common + ['--save-dir', one, '--cpu', '--update-freq', '8'])
+    ch = load(os.path.join(het, 'checkpoint_last.pt'))
+    c1 = load(os.path.join(one, 'checkpoint_last.pt'))
+    assert ch['args'].distributed_world_size == 8
+    assert ch['optimizer_history'][-1]['num_updates'] == c1['optimizer_history'][-1]['num_updates'] == 3
+    for k in c1['model']:
+        torch.testing.assert_close(ch['model'][k], c1['model'][k], rtol=1e-5, atol=1e-6, msg=k)

@@ -94,13 +94,17 @@ def test_epoch_step_lr_list():
 
 
 def test_comm_cus_auto_plan():
-    """--comm-cus defaults to 'auto': the RCCL channel cap + plan reservation (16 CUs) on GPU runs
-    with world > 1 (profiles/r3_comm_contention.md: a 16-CU comm load costs +15 % unplanned, +6 %
-    planned), off for one rank, CPU / gloo rehearsals, and whatever the user sets explicitly."""
+    """--comm-cus defaults to 0 (no CU reservation, no RCCL channel cap) until a multi-GPU run
+    measures the trade-off; 'auto' is opt-in: the channel cap + plan reservation (16 CUs) on GPU
+    runs with world > 1 (profiles/r3_comm_contention.md: a one-GPU 16-CU comm load costs +15 %
+    unplanned, +6 % planned), off for one rank, CPU / gloo rehearsals."""
     from hetseq_9cme_amd import options
     base = ['--task', 'mnist', '--data', '/tmp/x']
     a = options.parse_training_args(base)
-    assert a.comm_cus == 'auto'
+    assert a.comm_cus == 0
+    a.distributed_world_size = 8
+    assert options.comm_cus(a) == 0
+    a = options.parse_training_args(base + ['--comm-cus', 'auto'])
     a.distributed_world_size = 8
     assert options.comm_cus(a) == options.AUTO_COMM_CUS == 16
     a.distributed_world_size = 1

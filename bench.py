@@ -46,8 +46,6 @@ def parse():
     ap.add_argument('--fp32-gemm', default='fp16x3', choices=['fp16x3', 'native'],
                     help='fp32 GEMMs: fp16x3 (default, fp32 class: ops/gemm16.py) or native f32 MFMA '
                          '(ops/fp32_mode.py)')
-    ap.add_argument('--fp32-attention', default='fp16x3', choices=['fp16x3', 'x6'],
-                    help='fp32 attention products: fp16x3 (default) or x6 (ops/fp32_mode.py)')
     ap.add_argument('--model', default='base', choices=['base', 'large', 'tiny'])
     ap.add_argument('--no-fused', action='store_true', help='torch-op baseline (A/B only)')
     ap.add_argument('--data-dir', default=None)
@@ -213,7 +211,6 @@ def run(a, rank, world, dev_index, init_method):
             '--fast-stat-sync', '--lr', '1e-4', '--warmup-updates', '10000', '--weight-decay', '0.01',
             '--total-num-update', '1000000', '--clip-norm', '25', '--num-workers', str(a.num_workers), '--log-format', 'none',
             '--disable-validation', '--no-save', '--precision', a.precision, '--fp32-gemm', a.fp32_gemm,
-            '--fp32-attention', a.fp32_attention,
             '--distributed-world-size', str(world),
             '--update-freq', str(a.update_freq), '--gemm-tuning', a.gemm_tuning,
             '--allreduce-impl', a.allreduce_impl, '--bucket-cap-mb', str(a.bucket_cap_mb),
@@ -347,7 +344,7 @@ def run(a, rank, world, dev_index, init_method):
                        'nodes': [int(x) for x in a.nodes_meta.split(',')] if a.nodes_meta else None,
                        'fused_kernels': not a.no_fused, 'gemm_tuning': a.gemm_tuning,
                        'fp32_gemm': a.fp32_gemm if a.precision == 'fp32' else None,
-                       'fp32_attention': a.fp32_attention if a.precision == 'fp32' else None,
+                       'fp32_attention': 'fp16x3' if a.precision == 'fp32' and a.fp32_gemm == 'fp16x3' else None,
                        'allreduce': a.allreduce_impl if world > 1 else None},
             'final_logged_loss': round(loss, 5),
             'ranks_seen': ranks_seen,

@@ -72,7 +72,6 @@ class Controller(object):
         if not getattr(args, 'fused_kernels', True):
             ops.set_fused(False)      # A/B mode: plain torch ops on the GPU
         ops.set_fp32_gemm(getattr(args, 'fp32_gemm', 'native'))
-        ops.set_fp32_attention(getattr(args, 'fp32_attention', 'fp16x3'))
         ow = getattr(args, 'overlap_wgrad', 'auto')
         ops.set_side_stream({True: 'on', False: 'off', None: 'auto'}.get(ow, ow))
         if getattr(args, 'debug_kernels', False) and self.cuda:

@@ -137,7 +137,8 @@ void adadelta(Tensor p, Tensor g, Tensor sq, Tensor acc, Tensor gscale, int64_t 
 }
 
 // ------------------------------------------------------------------ layernorm
-// amax_out (fp32 runs only): receives hx_ln_fwd_blocks(rows) max |out| partials (ops/gemm16.py)
+// amax_out (fp32 runs only): receives max |out| of every row, [rows] (the fp16x3 GEMMs' per-row
+// operand scale, ops/gemm16.py)
 inline float* amax_ptr(const OptT& a, int64_t need, const char* what) {
   if (!has(a)) return nullptr;
   check_f32(*a, what);
@@ -166,14 +167,14 @@ std::vector<Tensor> ln_fwd(Tensor y, OptT bias, OptT res, Tensor gamma, Tensor b
             gamma.data_ptr<float>(), beta.data_ptr<float>(), out.data_ptr(), save_z ? z.data_ptr() : nullptr,
             mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, H, (float)eps, (float)keep_prob, seed_ptr(seed),
             (uint64_t)stream, drop_after ? 1 : 0, cur_stream(y),
-            act_bf16(y) ? nullptr : amax_ptr(amax_out, hx_ln_fwd_blocks(rows), "ln_fwd amax"));
+            act_bf16(y) ? nullptr : amax_ptr(amax_out, rows, "ln_fwd amax"));
   dbg_finite(out, "ln_fwd");
   return {out, z, mean, rstd};
 }
 
 std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tensor gamma, double keep_prob,
                            const Tensor& seed, int64_t stream, bool drop_after, bool want_dy, bool want_dbias,
-                           OptT dgamma_out, OptT dbeta_out, OptT dbias_out, OptT amax_out) {
+                           OptT dgamma_out, OptT dbeta_out, OptT dbias_out, OptT amax_out, OptT colmax_out) {
   check_cuda(dout, "grad_output");
   check_cuda(z, "saved input");
   const int H = (int)z.size(-1);
@@ -188,13 +189,14 @@ std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tens
   TORCH_CHECK(dgamma.numel() == H && dbeta.numel() == H && dgamma.is_contiguous() && dbeta.is_contiguous(),
               "bad dgamma/dbeta outputs");
   const int nblk = hx_ln_bwd_blocks(rows);
-  auto partial = torch::empty({(int64_t)nblk * 3 * H}, f32);
+  auto partial = torch::empty({(int64_t)nblk * 4 * H}, f32);
   hx_ln_bwd(act_bf16(z), dout.data_ptr(), z.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
             gamma.data_ptr<float>(), dz.data_ptr(), want_dy ? dy.data_ptr() : nullptr, partial.data_ptr<float>(), nblk,
             rows, H, (float)keep_prob, seed_ptr(seed), (uint64_t)stream, drop_after ? 1 : 0,
             (want_dy && want_dbias) ? 1 : 0, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
             want_dbias ? dbias.data_ptr<float>() : nullptr, 0, cur_stream(z),
-            act_bf16(z) ? nullptr : amax_ptr(amax_out, nblk, "ln_bwd amax"));
+            act_bf16(z) ? nullptr : amax_ptr(amax_out, rows, "ln_bwd amax"),
+            act_bf16(z) ? nullptr : amax_ptr(colmax_out, H, "ln_bwd colmax"));
   dbg_finite(dz, "ln_bwd (dz)");
   return {dz, dy, dgamma, dbeta, dbias};
 }
@@ -223,7 +225,7 @@ std::vector<Tensor> embed_ln_fwd(Tensor ids, OptT tt, Tensor wte, Tensor wpe, Te
                   wte.data_ptr<float>(), wpe.data_ptr<float>(), wtt.data_ptr<float>(), gamma.data_ptr<float>(),
                   beta.data_ptr<float>(), out.data_ptr(), z.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                   B * S, (int)S, H, (float)eps, (float)keep_prob, seed_ptr(seed), (uint64_t)stream, cur_stream(ids),
-                  bf16_out ? nullptr : amax_ptr(amax_out, hx_ln_fwd_blocks(B * S), "embed_ln_fwd amax"));
+                  bf16_out ? nullptr : amax_ptr(amax_out, B * S, "embed_ln_fwd amax"));
   dbg_finite(out, "embed_ln_fwd");
   return {out, z, mean, rstd};
 }
@@ -331,8 +333,8 @@ Tensor softmax_xent_(Tensor logits, OptT bias, Tensor labels, int64_t ignore_ind
 
 // ------------------------------------------------------------------ attention
 std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed, int64_t stream,
-                             OptT bias, int split = 0, OptT amax_out = OptT()) {
-  // split: 0 none, 1 bf16 x6 pieces (attention_x6.hip), 2 fp16x3 (attention_f16.hip)
+                             OptT bias, int split = 0, OptT amax_out = OptT(), OptT colmax_out = OptT()) {
+  // split: 0 none (fp32 / bf16 MFMA), 2 fp16x3 (attention_f16.hip)
   check_cuda(qkv, "qkv");
   const int bf = act_bf16(qkv);
   check_f32(mask_bias, "mask_bias");
@@ -354,16 +356,12 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
   else dmask = torch::empty({0}, qkv.options().dtype(torch::kInt32));
   uint32_t* dm = keep < 1.0 ? reinterpret_cast<uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr;
   if (split) {
-    TORCH_CHECK(!bf, "attn_fwd_x6 / attn_fwd_f16: fp32 activations only");
-    float* am = amax_ptr(amax_out, ((S + 127) / 128) * nh * B * 4, "attn_fwd amax");
-    if (split == 2)
-      hx_attn_fwd_f16(qkv.data_ptr<float>(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(),
-                      out.data_ptr<float>(), lse.data_ptr<float>(), dm, (int)B, (int)S, (int)nh, (float)keep,
-                      seed_ptr(seed), (uint64_t)stream, cur_stream(qkv), am);
-    else
-      hx_attn_fwd_x6(qkv.data_ptr<float>(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(),
-                     out.data_ptr<float>(), lse.data_ptr<float>(), dm, (int)B, (int)S, (int)nh, (float)keep,
-                     seed_ptr(seed), (uint64_t)stream, cur_stream(qkv), am);
+    TORCH_CHECK(!bf, "attn_fwd_f16: fp32 activations only");
+    float* am = amax_ptr(amax_out, B * S * nh, "attn_fwd amax");   // [B * S rows][nh heads]
+    float* cm = amax_ptr(colmax_out, B * ((S + 127) / 128) * H, "attn_fwd colmax");   // [B * qblocks][H]
+    hx_attn_fwd_f16(qkv.data_ptr<float>(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(),
+                    out.data_ptr<float>(), lse.data_ptr<float>(), dm, (int)B, (int)S, (int)nh, (float)keep,
+                    seed_ptr(seed), (uint64_t)stream, cur_stream(qkv), am, cm);
   } else {
     hx_attn_fwd(bf, qkv.data_ptr(), ptr_or_null<float>(bias), mask_bias.data_ptr<float>(), out.data_ptr(),
                 lse.data_ptr<float>(), dm, (int)B, (int)S, (int)nh, (float)keep, seed_ptr(seed), (uint64_t)stream,
@@ -372,27 +370,22 @@ std::vector<Tensor> attn_fwd(Tensor qkv, Tensor mask_bias, int64_t nh, double ke
   dbg_finite(out, "attn_fwd");
   return {out, lse, dmask};
 }
-// fp32 attention forward on the bf16 matrix cores (split pieces, attention_x6.hip): {out, lse, dmask}
-std::vector<Tensor> attn_fwd_x6(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed,
-                                int64_t stream, OptT bias, OptT amax_out) {
-  return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, 1, amax_out);
-}
-// the same on the fp16 matrix cores (fp16x3, attention_f16.hip)
+// fp32 attention forward on the fp16 matrix cores (fp16x3, attention_f16.hip): {out, lse, dmask}
 std::vector<Tensor> attn_fwd_f16(Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed,
-                                 int64_t stream, OptT bias, OptT amax_out) {
-  return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, 2, amax_out);
+                                 int64_t stream, OptT bias, OptT amax_out, OptT colmax_out) {
+  return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, 2, amax_out, colmax_out);
 }
 
 // returns {dqkv, dbias} (dbias: [3H] fp32 when bias is given -- written into dbq/dbk/dbv
 // when those slots are given -- else an empty tensor)
 std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask,
                              int64_t nh, double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, int split = 0,
-                             OptT amax_out = OptT()) {
-  // split: 0 none, 1 bf16 x6 pieces (attention_x6.hip), 2 fp16x3 (attention_f16.hip)
+                             OptT amax_out = OptT(), OptT colmax_out = OptT()) {
+  // split: 0 none (fp32 / bf16 MFMA), 2 fp16x3 (attention_f16.hip)
   check_cuda(dout, "grad_output");
   check_cuda(qkv, "qkv");
   const int bf = act_bf16(qkv);
-  TORCH_CHECK(!(split && bf), "attn_bwd_x6: fp32 activations only");
+  TORCH_CHECK(!(split && bf), "attn_bwd_f16: fp32 activations only");
   TORCH_CHECK(dout.scalar_type() == qkv.scalar_type() && out.scalar_type() == qkv.scalar_type(),
               "attention activations must share one dtype");
   const int64_t B = qkv.size(0), S = qkv.size(1), H = qkv.size(2) / 3;
@@ -430,11 +423,12 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor o
     }
     part = torch::empty({B * ((S + 127) / 128), 3 * H}, qkv.options().dtype(torch::kFloat32));
   }
-  hx_attn_bwd(split == 2 ? 3 : (split ? 2 : bf), qkv.data_ptr(), ptr_or_null<float>(bias), pq, pk, pv, part.defined() ? part.data_ptr<float>() : nullptr,
+  hx_attn_bwd(split ? 3 : bf, qkv.data_ptr(), ptr_or_null<float>(bias), pq, pk, pv, part.defined() ? part.data_ptr<float>() : nullptr,
               mask_bias.data_ptr<float>(), dout.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
               keep < 1.0 ? reinterpret_cast<const uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr,
               dqkv.data_ptr(), dq_acc, dq_ld, (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv),
-              (split && !multi) ? amax_ptr(amax_out, B * nh, "attn_bwd_x6 amax") : nullptr);
+              (split && !multi) ? amax_ptr(amax_out, B * S * nh, "attn_bwd amax") : nullptr,   // [B * S][nh]
+              (split && !multi) ? amax_ptr(colmax_out, B * 3 * H, "attn_bwd colmax") : nullptr);   // [B][3H]
   if (multi && bf) dqkv.narrow(-1, 0, H).copy_(dq32);
   dbg_finite(dqkv, "attn_bwd");
   return {dqkv, dbias};
@@ -478,36 +472,55 @@ inline void check_af32(const Tensor& a, const char* what) {
                   a.size(1) % 16 == 0 && a.size(0) < (1LL << 31),
               what, ": fp32 [rows, K] with unit column stride, 16-B aligned rows and K % 16 == 0");
 }
+// max |x| partials of an fp32 operand: 1-D = partials of the whole tensor (any number; their max
+// is a per-tensor bound), 2-D [rows, P] = P partials per operand row (the row's own scale)
+struct ScaleSrc {
+  const float* p;
+  int np, rs;
+};
+inline ScaleSrc scale_src(const Tensor& t, const Tensor& ref, int64_t rows, const char* what) {
+  check_f32(t, what);
+  TORCH_CHECK(t.is_contiguous() && t.numel() >= 1 && t.numel() < (1LL << 31) && t.device() == ref.device(), what,
+              ": max |x| partials on the operand's device");
+  if (t.dim() == 1) return {t.data_ptr<float>(), (int)t.numel(), 0};
+  TORCH_CHECK(t.dim() == 2 && t.size(0) == rows && t.size(1) >= 1 && t.size(1) <= 64, what,
+              ": per-row max |x| partials must be [rows, P <= 64] (rows = ", rows, ")");
+  return {t.data_ptr<float>(), (int)t.size(1), (int)t.size(1)};
+}
 inline void check_amax(const Tensor& t, const Tensor& ref, const char* what) {
   check_f32(t, what);
-  TORCH_CHECK(t.dim() == 1 && t.is_contiguous() && t.numel() >= 1 && t.numel() < (1 << 24) &&
-                  t.device() == ref.device(), what, ": 1-D fp32 max |x| partials on the operand's device");
+  TORCH_CHECK(t.is_contiguous() && t.numel() >= 1 && t.numel() < (1LL << 31) && t.device() == ref.device(), what,
+              ": max |x| partials on the operand's device");
 }
 inline void check_p2(const Tensor& b, int64_t K, const char* what) {
   TORCH_CHECK(b.is_cuda() && b.scalar_type() == torch::kHalf && b.dim() == 2 && b.is_contiguous() &&
                   b.size(1) == 2 * K && aligned16(b.data_ptr()), what, ": fp16 P2 pieces [N, 2K]");
 }
 
+// max |x| of every row: [rows, 1]
 Tensor amax_rows(Tensor x) {
   check_f32(x, "amax_rows");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 4 == 0 && x.size(1) % 4 == 0 &&
                   aligned16(x.data_ptr()), "amax_rows: fp32 [rows, cols] with 16-B rows, cols % 4 == 0");
-  const int np = hx_amax_rows_parts(x.size(0), (int)x.size(1));
-  Tensor part = torch::empty({np}, x.options());
+  Tensor out = torch::empty({x.size(0), 1}, x.options());
   c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
-  hx_amax_rows(x.data_ptr<float>(), x.size(0), (int)x.size(1), x.stride(0), part.data_ptr<float>(), np, cur_stream(x));
-  return part;
+  hx_amax_rows(x.data_ptr<float>(), x.size(0), (int)x.size(1), x.stride(0), out.data_ptr<float>(), cur_stream(x));
+  return out;
 }
 
-// [(wf, wt, parts)] per weight: P2 fp16 pieces of W and of W^T, and W's max |x| partials
+// [(wf, wt, rmax, cmax)] per weight W [N, K]: P2 fp16 pieces of W (rows scaled by their own
+// maxima) and of W^T (rows = columns of W, scaled by the column maxima); rmax [N, 1] / cmax [K, 1]
+// are the per-row scale sources of the forward / data-gradient products
 std::vector<std::vector<Tensor>> split_weight_f16(std::vector<Tensor> Ws) {
   TORCH_CHECK(!Ws.empty() && Ws.size() <= HX_WBATCH, "split_weight_f16: 1..64 weights");
   HxWeightBatch d{};
   d.n = (int)Ws.size();
-  const int P = hx_weight_f16_parts();
-  Tensor part = torch::empty({d.n * P}, Ws[0].options());
+  int64_t rc_floats = 0;
+  for (const Tensor& W : Ws) rc_floats += W.size(0) + W.size(1);
+  Tensor rc = torch::empty({rc_floats}, Ws[0].options());
   std::vector<std::vector<Tensor>> out;
   int tiles = 0;
+  int64_t off = 0;
   for (int i = 0; i < d.n; ++i) {
     const Tensor& W = Ws[i];
     check_f32(W, "split_weight_f16 input");
@@ -524,30 +537,33 @@ std::vector<std::vector<Tensor>> split_weight_f16(std::vector<Tensor> Ws) {
     d.K[i] = (int)K;
     d.mask[i] = 0;
     d.start[i] = tiles;
+    d.roff[i] = off;
     tiles += (int)((N / 64) * (K / 64));
-    out.push_back({wf, wt, part.narrow(0, (int64_t)i * P, P)});
+    out.push_back({wf, wt, rc.narrow(0, off, N).view({N, 1}), rc.narrow(0, off + N, K).view({K, 1})});
+    off += N + K;
   }
   d.start[d.n] = tiles;
   c10::hip::HIPGuardMasqueradingAsCUDA guard(Ws[0].device());
-  hx_split_weight_f16(d, part.data_ptr<float>(), cur_stream(Ws[0]));
+  hx_split_weight_f16(d, rc.data_ptr<float>(), rc_floats, cur_stream(Ws[0]));
   return out;
 }
 
 static HxGemmF16 f16_args(const Tensor& a, const Tensor& aa, const Tensor& b, const Tensor& ba, const char* what) {
   check_af32(a, what);
-  check_amax(aa, a, what);
   check_p2(b, a.size(1), what);
-  check_amax(ba, a, what);
   TORCH_CHECK(b.device() == a.device() && b.size(0) < (1LL << 31), what, ": operands on one device");
+  const ScaleSrc sa = scale_src(aa, a, a.size(0), what), sb = scale_src(ba, a, b.size(0), what);
   HxGemmF16 p{};
   p.A = a.data_ptr();
   p.lda = a.stride(0);
-  p.a_amax = aa.data_ptr<float>();
-  p.na = (int)aa.numel();
+  p.a_amax = sa.p;
+  p.na = sa.np;
+  p.a_rs = sa.rs;
   p.B = reinterpret_cast<const uint16_t*>(b.data_ptr());
   p.ldb = b.size(1);
-  p.b_amax = ba.data_ptr<float>();
-  p.nb = (int)ba.numel();
+  p.b_amax = sb.p;
+  p.nb = sb.np;
+  p.b_rs = sb.rs;
   p.M = (int)a.size(0);
   p.N = (int)b.size(0);
   p.K = (int)a.size(1);
@@ -596,7 +612,9 @@ Tensor gemm_f16(Tensor a, Tensor a_amax, Tensor b, Tensor b_amax, OptT out_, boo
   return out;
 }
 
-// FFN up: u = a . b^T + bias -> (gelu'(u) if dmode else u, gelu(u) fp32, max |gelu(u)| partials)
+// FFN up: u = a . b^T + bias -> (gelu'(u) if dmode else u, h = gelu(u) fp32, max |h| per (row, N
+// tile) [M, TN] -- h's per-row scale source for the FFN-down GEMM --, max |h| per (M tile, column)
+// [TM, N] -- h's column maxima for the FFN-down weight gradient)
 std::vector<Tensor> gemm_f16_gelu(Tensor a, Tensor a_amax, Tensor b, Tensor b_amax, OptT bias, int64_t dmode) {
   HxGemmF16 p = f16_args(a, a_amax, b, b_amax, "gemm_f16_gelu");
   check_vec(bias, p.N, "gemm_f16_gelu bias");
@@ -604,23 +622,25 @@ std::vector<Tensor> gemm_f16_gelu(Tensor a, Tensor a_amax, Tensor b, Tensor b_am
   TORCH_CHECK(cfg >= 0, "gemm_f16_gelu: no tile for N = ", p.N);
   auto f32 = a.options();
   Tensor c = torch::empty({p.M, p.N}, f32), h = torch::empty({p.M, p.N}, f32);
-  Tensor am = torch::empty({hx_gemm_f16_tiles(p.M, p.N, cfg)}, f32);
+  Tensor rm = torch::empty({p.M, hx_gemm_f16_tn(p.N, cfg)}, f32), cm = torch::empty({hx_gemm_f16_tm(p.M, cfg), p.N}, f32);
   p.kind = 1;
   p.C = c.data_ptr<float>();
   p.ldc = p.N;
   p.bias = ptr_or_null<float>(bias);
   p.P = h.data_ptr<float>();
   p.ldp = p.N;
-  p.amax_out = am.data_ptr<float>();
+  p.rowmax = rm.data_ptr<float>();
+  p.colmax = cm.data_ptr<float>();
   p.dmode = dmode ? 1 : 0;
   c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
   TORCH_CHECK(hx_gemm_f16(p, cfg, cur_stream(a)) == 0, "gemm_f16_gelu: launch failed");
   dbg_finite(h, "gemm_f16_gelu");
-  return {c, h, am};
+  return {c, h, rm, cm};
 }
 
 // FFN down data gradient + GELU backward: t = (a . b^T) * (dmode ? u : gelu'(u + bias)) ->
-// (t fp32, max |t| partials, dbias = column sums of t (into dbias_out when given))
+// (t fp32, max |t| per (row, N tile) [M, TN], max |t| per (M tile, column) [TM, N], dbias =
+// column sums of t (into dbias_out when given))
 std::vector<Tensor> gemm_f16_dgelu(Tensor a, Tensor a_amax, Tensor b, Tensor b_amax, Tensor u, OptT bias,
                                    OptT dbias_out, int64_t dmode) {
   TORCH_CHECK(!dmode || !has(bias), "gemm_f16_dgelu: dmode 1 takes gelu'(u), which has the bias in it");
@@ -634,7 +654,7 @@ std::vector<Tensor> gemm_f16_dgelu(Tensor a, Tensor a_amax, Tensor b, Tensor b_a
   const int prow = hx_gemm_f16_colpart_rows(p.M, cfg);
   auto f32 = a.options();
   Tensor t = torch::empty({p.M, p.N}, f32);
-  Tensor am = torch::empty({hx_gemm_f16_tiles(p.M, p.N, cfg)}, f32);
+  Tensor rm = torch::empty({p.M, hx_gemm_f16_tn(p.N, cfg)}, f32), cm = torch::empty({hx_gemm_f16_tm(p.M, cfg), p.N}, f32);
   Tensor part = torch::empty({prow, p.N}, f32);
   Tensor db = has(dbias_out) ? *dbias_out : torch::empty({p.N}, f32);
   TORCH_CHECK(db.numel() == p.N && db.scalar_type() == torch::kFloat32 && db.is_contiguous(), "gemm_f16_dgelu: dbias");
@@ -645,28 +665,75 @@ std::vector<Tensor> gemm_f16_dgelu(Tensor a, Tensor a_amax, Tensor b, Tensor b_a
   p.P = t.data_ptr<float>();
   p.ldp = p.N;
   p.colpart = part.data_ptr<float>();
-  p.amax_out = am.data_ptr<float>();
+  p.rowmax = rm.data_ptr<float>();
+  p.colmax = cm.data_ptr<float>();
   p.dmode = dmode ? 1 : 0;
   c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
   TORCH_CHECK(hx_gemm_f16(p, cfg, cur_stream(a)) == 0, "gemm_f16_dgelu: launch failed");
   hx_fold_cols(part.data_ptr<float>(), prow, p.N, db.data_ptr<float>(), 0, cur_stream(a));
   dbg_finite(t, "gemm_f16_dgelu");
-  return {t, am, db};
+  return {t, rm, cm, db};
+}
+
+// the per-column scale source of a weight-gradient operand: 1-D = partials of the whole tensor (a
+// per-tensor bound), 2-D [P, cols] = P partials per column; with aff = (gamma, beta) the
+// LayerNorm-output bound (|gamma| z + |beta|) mul instead (t unused)
+inline HxColScale col_scale_src(const Tensor& t, const Tensor& ref, int64_t cols, const char* what, const OptT& g,
+                                const OptT& b, double z, double mul) {
+  HxColScale c{};
+  if (has(g)) {
+    TORCH_CHECK(has(b), what, ": the affine bound needs gamma and beta");
+    check_f32(*g, what);
+    check_f32(*b, what);
+    TORCH_CHECK(g->numel() == cols && b->numel() == cols && g->is_contiguous() && b->is_contiguous() &&
+                    g->device() == ref.device() && b->device() == ref.device(), what, ": gamma / beta [cols]");
+    c.g = g->data_ptr<float>();
+    c.b = b->data_ptr<float>();
+    c.z = (float)z;
+    c.mul = (float)mul;
+    return c;
+  }
+  check_f32(t, what);
+  TORCH_CHECK(t.is_contiguous() && t.numel() >= 1 && t.numel() < (1LL << 31) && t.device() == ref.device(), what,
+              ": max |x| partials on the operand's device");
+  c.p = t.data_ptr<float>();
+  if (t.dim() == 1) {
+    c.np = (int)t.numel();
+    return c;
+  }
+  TORCH_CHECK(t.dim() == 2 && t.size(1) == cols && t.size(0) >= 1 && t.size(0) <= 256, what,
+              ": per-column max |x| partials must be [P <= 256, cols] (cols = ", cols, ")");
+  c.np = (int)t.size(0);
+  c.cs = (int)cols;
+  return c;
+}
+
+// max |x| of every column: [1, cols]
+Tensor amax_cols(Tensor x) {
+  check_f32(x, "amax_cols");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 4 == 0 && x.size(1) % 4 == 0 &&
+                  aligned16(x.data_ptr()), "amax_cols: fp32 [rows, cols] with 16-B rows, cols % 4 == 0");
+  Tensor out = torch::empty({1, x.size(1)}, x.options());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  hx_amax_cols(x.data_ptr<float>(), x.size(0), (int)x.size(1), x.stride(0), out.data_ptr<float>(), cur_stream(x));
+  return out;
 }
 
 // dW = dy^T x over the token rows: dy [T, M], x [T, N] fp32 (M, N multiples of 128); out [<= M, N]
-// (rows of dy's padding columns past out.size(0) are not stored)
-Tensor wgrad_f16(Tensor dy, Tensor dy_amax, Tensor x, Tensor x_amax, Tensor out) {
+// (rows of dy's padding columns past out.size(0) are not stored); dy_amax / x_amax: per-column
+// max |x| partials of each operand ([P, M] / [P, N]) or per-tensor partials (1-D)
+Tensor wgrad_f16(Tensor dy, Tensor dy_amax, Tensor x, Tensor x_amax, Tensor out, OptT x_gamma, OptT x_beta, double x_z,
+                 double x_mul) {
   check_f32(dy, "wgrad_f16 dy");
   check_f32(x, "wgrad_f16 x");
-  check_amax(dy_amax, dy, "wgrad_f16");
-  check_amax(x_amax, dy, "wgrad_f16");
   TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0) && dy.stride(1) == 1 && x.stride(1) == 1 &&
                   dy.stride(0) % 4 == 0 && x.stride(0) % 4 == 0 && aligned16(dy.data_ptr()) &&
                   aligned16(x.data_ptr()) && dy.size(1) % 128 == 0 && x.size(1) % 128 == 0 &&
                   dy.size(0) < (1 << 30) && x.device() == dy.device(),
               "wgrad_f16: dy [T, M], x [T, N] fp32 with 16-B rows, M and N multiples of 128");
   const int64_t T = dy.size(0), M = dy.size(1), N = x.size(1);
+  const HxColScale sa = col_scale_src(dy_amax, dy, M, "wgrad_f16 dy partials", OptT(), OptT(), 0, 0);
+  const HxColScale sb = col_scale_src(x_amax, dy, N, "wgrad_f16 x partials", x_gamma, x_beta, x_z, x_mul);
   check_f32(out, "wgrad_f16 out");
   TORCH_CHECK(out.dim() == 2 && out.size(0) <= M && out.size(1) == N && out.is_contiguous(),
               "wgrad_f16: out must be contiguous fp32 [<= M, N]");
@@ -675,8 +742,7 @@ Tensor wgrad_f16(Tensor dy, Tensor dy_amax, Tensor x, Tensor x_amax, Tensor out)
   Tensor ws;
   if (nsplit > 1) ws = torch::empty({nsplit, M, N}, dy.options());
   c10::hip::HIPGuardMasqueradingAsCUDA guard(dy.device());
-  TORCH_CHECK(hx_wgrad_f16(dy.data_ptr<float>(), (int)dy.stride(0), dy_amax.data_ptr<float>(), (int)dy_amax.numel(),
-                           x.data_ptr<float>(), (int)x.stride(0), x_amax.data_ptr<float>(), (int)x_amax.numel(),
+  TORCH_CHECK(hx_wgrad_f16(dy.data_ptr<float>(), (int)dy.stride(0), sa, x.data_ptr<float>(), (int)x.stride(0), sb,
                            out.data_ptr<float>(), nsplit > 1 ? ws.data_ptr<float>() : nullptr, (int)M, (int)N, (int)T,
                            cfg, nsplit, (int)out.size(0), cur_stream(dy)) == 0,
               "wgrad_f16: launch failed");
@@ -909,7 +975,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ln_bwd", &ln_bwd, py::arg("dout"), py::arg("z"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"),
         py::arg("keep_prob"), py::arg("seed"), py::arg("stream"), py::arg("drop_after"), py::arg("want_dy"),
         py::arg("want_dbias"), py::arg("dgamma_out"), py::arg("dbeta_out"), py::arg("dbias_out"),
-        py::arg("amax_out") = py::none());
+        py::arg("amax_out") = py::none(), py::arg("colmax_out") = py::none());
   m.def("ln_fwd_blocks", &hx_ln_fwd_blocks);
   m.def("ln_bwd_blocks", &hx_ln_bwd_blocks);
   m.def("embed_ln_fwd", &embed_ln_fwd, py::arg("ids"), py::arg("tt"), py::arg("wte"), py::arg("wpe"), py::arg("wtt"),
@@ -923,31 +989,24 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_xent_", &softmax_xent_);
   m.def("attn_fwd", [](Tensor qkv, Tensor mask_bias, int64_t nh, double keep, const Tensor& seed, int64_t stream,
                         OptT bias) { return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, false); });
-  m.def("attn_fwd_x6", &attn_fwd_x6, py::arg("qkv"), py::arg("mask_bias"), py::arg("nh"), py::arg("keep"),
-        py::arg("seed"), py::arg("stream"), py::arg("bias"), py::arg("amax_out") = py::none());
   m.def("attn_fwd_f16", &attn_fwd_f16, py::arg("qkv"), py::arg("mask_bias"), py::arg("nh"), py::arg("keep"),
-        py::arg("seed"), py::arg("stream"), py::arg("bias"), py::arg("amax_out") = py::none());
+        py::arg("seed"), py::arg("stream"), py::arg("bias"), py::arg("amax_out") = py::none(),
+        py::arg("colmax_out") = py::none());
   m.def("attn_bwd", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
                        double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv) {
     return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, 0);
   });
-  // fp32 attention backward on the bf16 matrix cores (split pieces, attention_x6.hip)
-  m.def("attn_bwd_x6", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
-                          double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, OptT amax_out) {
-    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, 1, amax_out);
-  }, py::arg("dout"), py::arg("qkv"), py::arg("mask_bias"), py::arg("out"), py::arg("lse"), py::arg("dmask"),
-     py::arg("nh"), py::arg("keep"), py::arg("bias"), py::arg("dbq"), py::arg("dbk"), py::arg("dbv"),
-     py::arg("amax_out") = py::none());
   // fp32 attention backward on the fp16 matrix cores (fp16x3, attention_f16.hip)
   m.def("attn_bwd_f16", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
-                           double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, OptT amax_out) {
-    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, 2, amax_out);
+                           double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, OptT amax_out, OptT colmax_out) {
+    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, 2, amax_out, colmax_out);
   }, py::arg("dout"), py::arg("qkv"), py::arg("mask_bias"), py::arg("out"), py::arg("lse"), py::arg("dmask"),
      py::arg("nh"), py::arg("keep"), py::arg("bias"), py::arg("dbq"), py::arg("dbk"), py::arg("dbv"),
-     py::arg("amax_out") = py::none());
+     py::arg("amax_out") = py::none(), py::arg("colmax_out") = py::none());
   m.def("wgrad_bf16", &wgrad_bf16);
   m.def("wgrad_bf16_ok", &wgrad_bf16_ok);
   m.def("amax_rows", &amax_rows);
+  m.def("amax_cols", &amax_cols);
   m.def("split_weight_f16", &split_weight_f16);
   m.def("gemm_f16", &gemm_f16, py::arg("a"), py::arg("a_amax"), py::arg("b"), py::arg("b_amax"),
         py::arg("out") = py::none(), py::arg("beta") = false, py::arg("bias") = py::none(), py::arg("ks") = 0);
@@ -955,7 +1014,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bias"), py::arg("dmode") = 1);
   m.def("gemm_f16_dgelu", &gemm_f16_dgelu, py::arg("a"), py::arg("a_amax"), py::arg("b"), py::arg("b_amax"),
         py::arg("u"), py::arg("bias") = py::none(), py::arg("dbias_out") = py::none(), py::arg("dmode") = 1);
-  m.def("wgrad_f16", &wgrad_f16);
+  m.def("wgrad_f16", &wgrad_f16, py::arg("dy"), py::arg("dy_amax"), py::arg("x"), py::arg("x_amax"), py::arg("out"),
+        py::arg("x_gamma") = py::none(), py::arg("x_beta") = py::none(), py::arg("x_z") = 0.0,
+        py::arg("x_mul") = 1.0);
   m.def("gemm_bf16_gelu", &gemm_bf16_gelu, py::arg("a"), py::arg("b"), py::arg("bias"));
   m.def("gemm_bf16_dgelu", &gemm_bf16_dgelu, py::arg("a"), py::arg("b"), py::arg("d"),
         py::arg("dbias_out") = py::none(), py::arg("bias") = py::none(), py::arg("dmode") = 1);

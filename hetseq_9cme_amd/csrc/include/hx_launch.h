@@ -22,8 +22,10 @@ void hx_adadelta(float* p, const float* g, float* sq, float* acc, const float* g
                  float eps, float wd, const float* hp, hipStream_t s);
 
 // layernorm.hip
-// amax_part (fp32 only, may be null): one max |output| per block -- hx_ln_fwd_blocks(rows) of them for
-// the forward / embedding, hx_ln_bwd_blocks(rows) for the backward (max |dy|, or |dz| without dy)
+// amax_part (fp32 only, may be null): max |output| of every row, [rows] (the backward: max |dy|, or
+// |dz| without dy) -- the fp16x3 GEMMs' per-row operand scale; colmax (backward, may be null): max
+// |dy| (|dz|) of every column, [H] -- the weight gradient's per-column scale.  The backward's
+// partial workspace is [nblk][4][H].
 int hx_ln_bwd_blocks(int64_t rows);
 int hx_ln_fwd_blocks(int64_t rows);
 void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, const float* gamma, const float* beta,
@@ -32,7 +34,7 @@ void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, cons
 void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma,
                void* dz, void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
                uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
-               int accumulate, hipStream_t s, float* amax_part = nullptr);
+               int accumulate, hipStream_t s, float* amax_part = nullptr, float* colmax = nullptr);
 void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,
                      const float* wtt, const float* gamma, const float* beta, void* out, void* zsave, float* mean,
                      float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, const uint64_t* seed,
@@ -65,33 +67,28 @@ void hx_attn_bwd_bf16(const void* qkv, const float* bias, float* dbias_part, con
 void hx_wgrad_bf16_plan(int M, int N, int T, int* cfg, int* nsplit);
 void hx_wgrad_bf16(const void* dy, int ldy, const void* x, int ldx, float* out, float* ws, int M, int N, int T,
                    int cfg, int nsplit, int mvalid, hipStream_t s);
-// attention_x6.hip -- fp32 attention on bf16 MFMA with split pieces (bf16x6 class); amax_part
-// (optional): max |out| partials (forward, ceil(S/128) * nh * B * 4) / max |dQKV| partials
-// (backward, S <= 128: B * nh) for the fp16x3 GEMMs
-void hx_attn_fwd_x6(const float* qkv, const float* bias, const float* maskb, float* out, float* lse,
-                    uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream,
-                    hipStream_t s, float* amax_part = nullptr);
-void hx_attn_bwd_x6(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,
-                    const float* out, const float* lse, const uint32_t* dmask, float* dqkv, float* dq_acc, int dq_ld,
-                    int B, int S, int nh, float keep, hipStream_t s, float* amax_part = nullptr);
-// the same backward on the fp16 matrix cores (three passes over scaled two-piece operands,
-// attention_f16.hip: --fp32-gemm fp16x3)
+// attention_f16.hip -- fp32 attention on the fp16 matrix cores (three passes over scaled two-piece
+// operands: --fp32-gemm fp16x3); amax_part (optional): max |out| (forward) / max |dQKV| (backward,
+// S <= 128) per (row, head), [B * S][nh] -- the fp16x3 GEMMs' per-row operand scales; colmax_part
+// (optional): max |out| of each column per (batch, 128-query block), [B * ceil(S / 128)][H]
+// (forward) / max |dQKV| of each column per batch, [B][3H] (backward, S <= 128) -- the weight
+// gradients' per-column scales
 void hx_attn_fwd_f16(const float* qkv, const float* bias, const float* maskb, float* out, float* lse,
                      uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream,
-                     hipStream_t s, float* amax_part = nullptr);
+                     hipStream_t s, float* amax_part = nullptr, float* colmax_part = nullptr);
 void hx_attn_bwd_f16(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,
                      const float* out, const float* lse, const uint32_t* dmask, float* dqkv, float* dq_acc, int dq_ld,
-                     int B, int S, int nh, float keep, hipStream_t s, float* amax_part = nullptr);
+                     int B, int S, int nh, float keep, hipStream_t s, float* amax_part = nullptr,
+                     float* colmax_part = nullptr);
 void hx_attn_fwd(int bf16, const void* qkv, const float* bias, const float* maskb, void* out, float* lse,
                  uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream, hipStream_t s);
 // dq_acc: fp32 dQ accumulation target when S > 128 (atomics; row stride dq_ld), else unused.
 // With bias: its gradient (column sums of dQ / dK / dV) goes to dbq / dbk / dbv through the
-// dbias_part workspace ([B * ceil(S/128)][3H] fp32).  kind: 0 fp32 MFMA, 1 bf16, 2 fp32 split (x6),
-// 3 fp32 as fp16x3.
+// dbias_part workspace ([B * ceil(S/128)][3H] fp32).  kind: 0 fp32 MFMA, 1 bf16, 3 fp32 as fp16x3.
 void hx_attn_bwd(int kind, const void* qkv, const float* bias, float* dbq, float* dbk, float* dbv, float* dbias_part,
                  const float* maskb, const void* dout, const void* out, const float* lse, const uint32_t* dmask,
                  void* dqkv, float* dq_acc, int dq_ld, int B, int S, int nh, float keep, hipStream_t s,
-                 float* amax_part = nullptr);
+                 float* amax_part = nullptr, float* colmax_part = nullptr);
 
 // a batch of weights prepared in one launch (gemm_f16.hip: split_weight_f16 / weight_bf16_t);
 // start[i] = first 64 x 64 tile of weight i, start[n] = total tiles
@@ -103,27 +100,32 @@ struct HxWeightBatch {
   uint16_t* wt[HX_WBATCH];
   int N[HX_WBATCH], K[HX_WBATCH], mask[HX_WBATCH];
   int start[HX_WBATCH + 1];
+  int64_t roff[HX_WBATCH];   // split_weight_f16: weight i's row maxima [N] then column maxima [K] at rc + roff[i]
 };
 // fold [rows][N] column partials into out[N] (+= if accumulate)
 void hx_fold_cols(const float* partial, int rows, int N, float* out, int accumulate, hipStream_t s);
 
 // gemm_f16.hip -- --fp32-gemm fp16x3: fp32 operands as two scaled fp16 pieces, three MFMA passes.
-// A: fp32 [M][K] (row stride lda, split in the kernel), B: fp16 pieces in the P2 layout [N][2K];
-// a_amax / b_amax: max |x| partials of each operand (na / nb of them) giving its power-of-two scale.
-// kind 0: C (+)= s acc (+ bias)  [ks > 1: split-K slabs C + z c_zs, no bias / beta]
-// kind 1: u = s acc + bias -> C = gelu'(u) (dmode 1) or u (dmode 0); P = gelu(u) fp32; amax_out
-//         [hx_gemm_f16_tiles] = per-tile max |P|
-// kind 2: t = s acc * (dmode ? aux : gelu'(aux + bias)) -> P fp32, amax_out, colpart
+// A: fp32 [M][K] (row stride lda, split in the kernel), B: fp16 pieces in the P2 layout [N][2K].
+// Operand scales are per ROW of A and per row of B (= output column): row r's max |x| is the max
+// of a_amax[r * a_rs + j], j < na (a_rs = 0: the same na partials for every row, a per-tensor
+// bound); likewise b_amax / nb / b_rs.
+// kind 0: C (+)= acc (+ bias)  [ks > 1: split-K slabs C + z c_zs, no bias / beta]
+// kind 1: u = acc + bias -> C = gelu'(u) (dmode 1) or u (dmode 0); P = gelu(u) fp32
+// kind 2: t = acc * (dmode ? aux : gelu'(aux + bias)) -> P fp32, colpart
 //         [hx_gemm_f16_colpart_rows][N] per-wave column sums of t
+// kinds 1 / 2 (optional): rowmax [M][hx_gemm_f16_tn] = max |P| per (row, N tile) -- the next
+//         GEMM's row scale; colmax [hx_gemm_f16_tm][N] = max |P| per (M tile, column) -- the weight
+//         gradient's column scale
 struct HxGemmF16 {
   const void* A;     // fp32, or bf16 when abf16 (then B is bf16 [N][K] and there is no scaling)
   int64_t lda;
   const float* a_amax;
-  int na;
+  int na, a_rs;
   const uint16_t* B;
   int64_t ldb;
   const float* b_amax;
-  int nb;
+  int nb, b_rs;
   float* C;
   int64_t ldc;
   int M, N, K, beta, kind;
@@ -133,7 +135,8 @@ struct HxGemmF16 {
   float* P;
   int64_t ldp;
   float* colpart;
-  float* amax_out;
+  float* rowmax;
+  float* colmax;
   int dmode, ks;
   int64_t c_zs;
   int abf16, obf16;   // --precision bf16: bf16 operands (one pass), bf16 output C (kind 0)
@@ -143,6 +146,8 @@ void hx_weight_bf16_t(const HxWeightBatch& d, hipStream_t s);
 int hx_gemm_f16_plan(int M, int N, int K);
 int hx_gemm_bf16_plan(int M, int N, int K);
 int hx_gemm_f16_tiles(int M, int N, int cfg);
+int hx_gemm_f16_tm(int M, int cfg);   // M tiles
+int hx_gemm_f16_tn(int N, int cfg);   // N tiles
 int hx_gemm_f16_colpart_rows(int M, int cfg);
 int hx_gemm_f16_ks(int M, int N, int K, int cfg);
 // split-K combine: C[M][ldc] (+= if beta) = sum of ks [M][N] slabs at ws (+ bias [N]); N % 4 == 0
@@ -150,17 +155,29 @@ void hx_gemm_f16_slab_combine(const float* ws, float* C, int64_t ldc, int M, int
                               const float* bias, hipStream_t s);
 int hx_gemm_f16(const HxGemmF16& p, int cfg, hipStream_t s);
 // dW[M][N] = dY[T][M]^T X[T][N] (fp32 operands, row strides ldy / ldx); rows >= mvalid not stored;
-// ws: nsplit * M * N floats when nsplit > 1
+// ws: nsplit * M * N floats when nsplit > 1.  Operand scales per COLUMN (the non-reduction
+// dimension), each operand's from an HxColScale: column c's max |x| is
+//   g != null:  (|g[c]| z + |b[c]|) mul  (a bound: a LayerNorm output gamma zhat + beta, |zhat| <= z)
+//   cs > 0:     max over j < np of p[j cs + c]  ([np][C] column partials)
+//   cs == 0:    max over the np partials at p   (one per-tensor bound)
+struct HxColScale {
+  const float* p;
+  int np, cs;
+  const float* g;
+  const float* b;
+  float z, mul;
+};
 void hx_wgrad_f16_plan(int M, int N, int T, int* cfg, int* nsplit);
-int hx_wgrad_f16(const float* dy, int ldy, const float* dy_amax, int na, const float* x, int ldx, const float* x_amax,
-                 int nb, float* out, float* ws, int M, int N, int T, int cfg, int nsplit, int mvalid, hipStream_t s);
-// max |x| partials of a [rows][cols] fp32 matrix (cols % 4 == 0, 16-B rows)
-int hx_amax_rows_parts(int64_t rows, int cols);
-void hx_amax_rows(const float* x, int64_t rows, int cols, int64_t ld, float* part, int nparts, hipStream_t s);
-// every weight of a batch -> P2 fp16 pieces wf [N][2K], wt [K][2N] (mask ignored); part: n *
-// hx_weight_f16_parts() max |W| partials, weight i's at part + i * hx_weight_f16_parts()
-int hx_weight_f16_parts();
-void hx_split_weight_f16(const HxWeightBatch& d, float* part, hipStream_t s);
+int hx_wgrad_f16(const float* dy, int ldy, const HxColScale& ca, const float* x, int ldx, const HxColScale& cb,
+                 float* out, float* ws, int M, int N, int T, int cfg, int nsplit, int mvalid, hipStream_t s);
+// max |x| of each column of a [rows][cols] fp32 matrix (cols % 4 == 0, 16-B rows) -> out[cols]
+void hx_amax_cols(const float* x, int64_t rows, int cols, int64_t ld, float* out, hipStream_t s);
+// max |x| of each row of a [rows][cols] fp32 matrix (cols % 4 == 0, 16-B rows) -> out[rows]
+void hx_amax_rows(const float* x, int64_t rows, int cols, int64_t ld, float* out, hipStream_t s);
+// every weight of a batch -> P2 fp16 pieces wf [N][2K] (row n scaled by its own 2^E), wt [K][2N]
+// (row k = column k of W, scaled by that column's 2^E); rc: per weight its row maxima [N] then
+// column maxima [K] at rc + roff[i] (rc_floats in all, zeroed here)
+void hx_split_weight_f16(const HxWeightBatch& d, float* rc, int64_t rc_floats, hipStream_t s);
 
 // split.hip -- fp32 -> bf16 planes (piece order[j] = (order >> 4j) & 15) for bf16-MFMA
 // emulation of fp32 GEMMs; interleaved [R][npl][D] or stacked [npl][R][D].

@@ -532,15 +532,12 @@ void hx_attn_fwd(int bf16, const void* qkv, const float* bias, const float* mask
 void hx_attn_bwd(int kind, const void* qkv, const float* bias, float* dbq, float* dbk, float* dbv, float* dbias_part,
                  const float* maskb, const void* dout, const void* out, const float* lse, const uint32_t* dmask,
                  void* dqkv, float* dq_acc, int dq_ld, int B, int S, int nh, float keep, hipStream_t s,
-                 float* amax_part) {
+                 float* amax_part, float* colmax_part) {
   if (kind == 1)   // bf16 MFMA (attention_bf16.hip)
     hx_attn_bwd_bf16(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv, dq_acc, dq_ld, B, S, nh, keep, s);
-  else if (kind == 2)   // fp32 on bf16 MFMA, split pieces (attention_x6.hip)
-    hx_attn_bwd_x6((const float*)qkv, bias, dbias_part, maskb, (const float*)dout, (const float*)out, lse, dmask,
-                   (float*)dqkv, dq_acc, dq_ld, B, S, nh, keep, s, amax_part);
   else if (kind == 3)   // fp32 on fp16 MFMA, scaled two-piece operands (attention_f16.hip)
     hx_attn_bwd_f16((const float*)qkv, bias, dbias_part, maskb, (const float*)dout, (const float*)out, lse, dmask,
-                    (float*)dqkv, dq_acc, dq_ld, B, S, nh, keep, s, amax_part);
+                    (float*)dqkv, dq_acc, dq_ld, B, S, nh, keep, s, amax_part, colmax_part);
   else
     attn_bwd_t<float>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv, dq_acc, dq_ld, B, S, nh, keep, s);
   if (dbias_part) {

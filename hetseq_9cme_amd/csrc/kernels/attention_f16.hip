@@ -191,7 +191,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const float* __restrict__ qkv, const float* __restrict__ qkv_bias, float* __restrict__ dbias_part,
     const float* __restrict__ maskb, const float* __restrict__ dout, const float* __restrict__ outp,
     const float* __restrict__ lse, const uint32_t* __restrict__ dmask, float* __restrict__ dqkv,
-    float* __restrict__ dq_acc, int dq_ld, int S, int nh, float keep, float* __restrict__ amax_part) {
+    float* __restrict__ dq_acc, int dq_ld, int S, int nh, float keep, float* __restrict__ amax_part,
+    float* __restrict__ colmax_part) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // one row-major image per operand, read both ways: K [key][dim] as the B operand of S (rows) and
   // of dQ (transposed reads); Q / dO [vpos(query)][dim] as the A operand of S / dP (rows) and the
@@ -219,7 +220,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float* qbias = qkv_bias ? qkv_bias + hd * D : nullptr;
   const float* kbias = qkv_bias ? qkv_bias + H + hd * D : nullptr;
   const float* vbias = qkv_bias ? qkv_bias + 2 * H + hd * D : nullptr;
-  float am = 0.f;   // max |dQKV| of this block's stores (one key block per head only)
+  // one key block (S <= 128): max |dQ|, |dK|, |dV| of each of the head's rows, for the QKV GEMMs'
+  // per-row operand scale (amax_part[row][head]; ops/gemm16.py takes the max over the heads)
+  __shared__ unsigned rmx_s[128];
+  const bool want_am = amax_part != nullptr && single;
+  if (want_am && tid < 128) rmx_s[tid] = 0u;
+  // ... and max |dQ| / |dK| / |dV| of each of its columns -> colmax_part[b][3H] (the QKV weight
+  // gradient's per-column scale)
+  const bool want_cm = colmax_part != nullptr && single;
+  float cqm0 = 0.f, cqm1 = 0.f;   // running column maxima of this lane's two dQ columns
 
   // ---- the block's K rows (4 x 8 dims per thread, for the K image) and this lane's V fragments
   // (dims 16ks + 8h .. +7), the block's max |K|, |V|
@@ -505,7 +514,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         if (q0 + r >= S) continue;
         dq[r * H3] = qa0[r];
         dq[r * H3 + 16] = qa1[r];
-        am = fmaxf(am, fmaxf(fabsf(qa0[r]), fabsf(qa1[r])));
+      }
+      if (want_cm) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (q0 + r < S) {
+            cqm0 = fmaxf(cqm0, fabsf(qa0[r]));
+            cqm1 = fmaxf(cqm1, fabsf(qa1[r]));
+          }
+      }
+      if (want_am) {   // row q0 + r: its 32 columns of this wave over the 16 lanes of the group
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float m = fmaxf(fabsf(qa0[r]), fabsf(qa1[r]));
+#pragma unroll
+          for (int o = 1; o < 16; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+          if (r16 == 0 && q0 + r < S) atomicMax(&rmx_s[q0 + r], __float_as_uint(m));
+        }
       }
     } else {
       float* dq = dqa_b + (int64_t)q0 * dq_ld + dcol;
@@ -570,16 +595,57 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       dk[(int64_t)key * H3 + 32 + l32] = dk1[r];
       dvp[(int64_t)key * H3 + l32] = dv0[r];
       dvp[(int64_t)key * H3 + 32 + l32] = dv1[r];
-      am = fmaxf(am, fmaxf(fmaxf(fabsf(dk0[r]), fabsf(dk1[r])), fmaxf(fabsf(dv0[r]), fabsf(dv1[r]))));
     }
-    if (amax_part && single) {
-      __shared__ float red_am[4];
-      am = wave_max(am);
-      if (lane == 0) red_am[w] = am;
+    if (want_am) {
+      // key rows: the 64 dK and 64 dV columns of a row sit on the 32 lanes of a half-wave
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        float m = fmaxf(fmaxf(fabsf(dk0[r]), fabsf(dk1[r])), fmaxf(fabsf(dv0[r]), fabsf(dv1[r])));
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        const int key = kbase + w * 32 + crow(r, h);
+        if (l32 == 0 && key < S) atomicMax(&rmx_s[key], __float_as_uint(m));
+      }
       __syncthreads();
-      if (tid == 0)
-        amax_part[(int64_t)b * gridDim.y + hd] =
-            fmaxf(fmaxf(red_am[0], red_am[1]), fmaxf(red_am[2], red_am[3]));
+      if (tid < S) amax_part[((int64_t)b * S + tid) * nh + hd] = __uint_as_float(rmx_s[tid]);
+    }
+    if (want_cm) {
+      __shared__ float cmx_s[4][3][64];
+      // dQ: lane (r16, kg) of wave (qh, dp2) holds columns 32 dp2 + r16 (+ 16) over rows 4 kg + r
+      cqm0 = fmaxf(cqm0, __shfl_xor(cqm0, 16, 64));
+      cqm0 = fmaxf(cqm0, __shfl_xor(cqm0, 32, 64));
+      cqm1 = fmaxf(cqm1, __shfl_xor(cqm1, 16, 64));
+      cqm1 = fmaxf(cqm1, __shfl_xor(cqm1, 32, 64));
+      // dK / dV: lane (l32, h) holds columns l32 and 32 + l32 of the wave's key rows crow(r, h)
+      float mk0 = 0.f, mk1 = 0.f, mv0 = 0.f, mv1 = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if (kbase + w * 32 + crow(r, h) >= S) continue;
+        mk0 = fmaxf(mk0, fabsf(dk0[r])); mk1 = fmaxf(mk1, fabsf(dk1[r]));
+        mv0 = fmaxf(mv0, fabsf(dv0[r])); mv1 = fmaxf(mv1, fabsf(dv1[r]));
+      }
+      mk0 = fmaxf(mk0, __shfl_xor(mk0, 32, 64)); mk1 = fmaxf(mk1, __shfl_xor(mk1, 32, 64));
+      mv0 = fmaxf(mv0, __shfl_xor(mv0, 32, 64)); mv1 = fmaxf(mv1, __shfl_xor(mv1, 32, 64));
+      if (lane < 16) {   // this wave's dQ columns; the other query half's wave fills the same slots
+        cmx_s[w][0][32 * dp2 + lane] = cqm0;
+        cmx_s[w][0][32 * dp2 + 16 + lane] = cqm1;
+      }
+      if (lane < 32) {
+        cmx_s[w][1][l32] = mk0; cmx_s[w][1][32 + l32] = mk1;
+        cmx_s[w][2][l32] = mv0; cmx_s[w][2][32 + l32] = mv1;
+      }
+      __syncthreads();
+      if (tid < 192) {
+        const int sec = tid >> 6, c = tid & 63;
+        float m;
+        if (sec == 0) {   // waves (0,1) own dQ columns 0..31 (dp2 = 0), waves (2,3) 32..63
+          const int wa = c < 32 ? 0 : 2;
+          m = fmaxf(cmx_s[wa][0][c], cmx_s[wa + 1][0][c]);
+        } else {
+          m = fmaxf(fmaxf(cmx_s[0][sec][c], cmx_s[1][sec][c]), fmaxf(cmx_s[2][sec][c], cmx_s[3][sec][c]));
+        }
+        colmax_part[(int64_t)b * 3 * H + sec * H + hd * D + c] = m;
+      }
     }
   }
 }
@@ -598,7 +664,8 @@ template <bool kDrop>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void attn_fwd_f16_k(
     const float* __restrict__ qkv, const float* __restrict__ qkv_bias, const float* __restrict__ maskb,
     float* __restrict__ out, float* __restrict__ lse, uint32_t* __restrict__ dmask, int S, int nh, float keep,
-    const uint64_t* __restrict__ seedp, uint64_t stream, float* __restrict__ amax_part) {
+    const uint64_t* __restrict__ seedp, uint64_t stream, float* __restrict__ amax_part,
+    float* __restrict__ colmax_part) {
   const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   __shared__ __attribute__((aligned(16))) uint16_t Ks[2][64 * RS];   // [piece][key][dim]
   __shared__ __attribute__((aligned(16))) uint16_t Vt[2][64 * RS];   // [piece][dim][vpos(key)]
@@ -840,14 +907,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   }
   const float inv_l = ldexpf(1.f / l_run, -(ep + ev_o));
   if (amax_part) {
-    // max |context| of this wave's 32 queries (the fp16x3 attention-output GEMM's operand
-    // scale, ops/gemm16.py): one partial per wave, rows past S count 0
+    // max |context| of each query row over this head's 64 columns (lanes l and l + 32 hold its two
+    // halves) -> amax_part[row][head]: the attention-output GEMM's per-row operand scale
+    // (ops/gemm16.py takes the max over the nh heads of a row)
     float am = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) am = fmaxf(am, fmaxf(fabsf(o0[i] * inv_l), fabsf(o1[i] * inv_l)));
-    if (q >= S) am = 0.f;
-    am = wave_max(am);
-    if (lane == 0) amax_part[(((int64_t)b * gridDim.y + hd) * gridDim.x + blk.x) * 4 + w] = am;
+    am = fmaxf(am, __shfl_xor(am, 32, 64));
+    if (q < S && h == 0) amax_part[((int64_t)b * S + q) * nh + hd] = am;
+  }
+  if (colmax_part) {
+    // max |context| of each of the head's 64 columns over this block's 128 queries ->
+    // colmax_part[b * query blocks + block][column]: the attention-output weight gradient's
+    // per-column scale.  A column's 32 queries of a wave are the 32 lanes of a half.
+    __shared__ float cmx_s[4][64];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      float m0 = q < S ? fabsf(o0[i] * inv_l) : 0.f, m1 = q < S ? fabsf(o1[i] * inv_l) : 0.f;
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) {
+        m0 = fmaxf(m0, __shfl_xor(m0, o, 64));
+        m1 = fmaxf(m1, __shfl_xor(m1, o, 64));
+      }
+      if (l32 == 0) {
+        const int d = 8 * (i >> 2) + 4 * h + (i & 3);
+        cmx_s[w][d] = m0;
+        cmx_s[w][32 + d] = m1;
+      }
+    }
+    __syncthreads();
+    if (tid < 64)
+      colmax_part[((int64_t)b * gridDim.x + blk.x) * H + hd * D + tid] =
+          fmaxf(fmaxf(cmx_s[0][tid], cmx_s[1][tid]), fmaxf(cmx_s[2][tid], cmx_s[3][tid]));
   }
   if (q >= S) return;
   float* op = out + ((int64_t)b * S + q) * H + hd * D;
@@ -871,17 +962,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 
 void hx_attn_fwd_f16(const float* qkv, const float* bias, const float* maskb, float* out, float* lse,
                      uint32_t* dmask, int B, int S, int nh, float keep, const uint64_t* seed, uint64_t stream,
-                     hipStream_t s, float* amax_part) {
+                     hipStream_t s, float* amax_part, float* colmax_part) {
   dim3 grid((S + 127) / 128, nh, B);
   if (keep < 1.f)
-    attn_fwd_f16_k<true><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream, amax_part);
+    attn_fwd_f16_k<true><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream, amax_part,
+                                              colmax_part);
   else
-    attn_fwd_f16_k<false><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream, amax_part);
+    attn_fwd_f16_k<false><<<grid, 256, 0, s>>>(qkv, bias, maskb, out, lse, dmask, S, nh, keep, seed, stream,
+                                               amax_part, colmax_part);
 }
 
 void hx_attn_bwd_f16(const float* qkv, const float* bias, float* dbias_part, const float* maskb, const float* dout,
                      const float* out, const float* lse, const uint32_t* dmask, float* dqkv, float* dq_acc, int dq_ld,
-                     int B, int S, int nh, float keep, hipStream_t s, float* amax_part) {
+                     int B, int S, int nh, float keep, hipStream_t s, float* amax_part, float* colmax_part) {
   dim3 grid((S + 127) / 128, nh, B);
   static bool attr = false;
   if (!attr) {   // > 64 KiB of dynamic LDS needs an explicit opt-in (gfx950: 160 KiB per CU)
@@ -892,8 +985,8 @@ void hx_attn_bwd_f16(const float* qkv, const float* bias, float* dbias_part, con
   }
   if (keep < 1.f)
     attn_bwd_f16_k<true><<<grid, 256, BWD_SMEM, s>>>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv, dq_acc,
-                                                     dq_ld, S, nh, keep, amax_part);
+                                                     dq_ld, S, nh, keep, amax_part, colmax_part);
   else
     attn_bwd_f16_k<false><<<grid, 256, BWD_SMEM, s>>>(qkv, bias, dbias_part, maskb, dout, out, lse, dmask, dqkv,
-                                                      dq_acc, dq_ld, S, nh, keep, amax_part);
+                                                      dq_acc, dq_ld, S, nh, keep, amax_part, colmax_part);
 }

@@ -34,6 +34,7 @@
 //    XOR-swizzled LDS image read with the transposing ds_read_b64_tr_b16; token-range split-K
 //    over the CUs, partial slabs summed by one vectorised pass.
 #include <algorithm>
+#include <type_traits>
 
 #include "hx_gemm.h"
 #include "hx_launch.h"
@@ -52,18 +53,19 @@ __device__ __forceinline__ f32x16 mfma16(const f16x8& a, const f16x8& b, const f
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
-// DMA ring depth of gemm_f16_k (LDS: depth x (BM + BN) x 64 B)
-constexpr int kGemmStages = 3;   // 4 measured 3 % slower (r4s GEMM bench: 2516 vs 2445 us per layer)
+// raw workgroup barrier: no vmcnt / lgkmcnt drain (LDS-DMA and fragment reads stay in flight
+// across it; the k loop retires what it needs with counted waits), and a compiler memory fence
+__device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
 struct F16Args {
   const void* A;   // fp32 (AT 0) or bf16 (AT 1)
   int64_t lda;
-  const float* a_amax;
-  int na;
+  const float* a_amax;   // A row r's max |x| partials: a_amax[r a_rs + j], j < na (a_rs 0: one set, per tensor)
+  int na, a_rs;
   const uint16_t* B;
   int64_t ldb;
-  const float* b_amax;
-  int nb;
+  const float* b_amax;   // B row n's (= output column n's) partials, the same way
+  int nb, b_rs;
   float* C;
   int64_t ldc;
   int M, N, K, beta;
@@ -72,37 +74,73 @@ struct F16Args {
   int64_t ldaux;
   float* P;
   int64_t ldp;
-  float* colpart;
-  float* amax_out;   // EPI 1 / 2: one max |P| per output tile
-  int dmode;         // EPI 1: C gets gelu'(u) (1) or u (0); EPI 2: aux holds gelu'(u) (1) or u (0)
-  int ks;            // split-K slabs (EPI 0 only): slab z reduces k steps [z, z + 1) K / ks into C + z c_zs
+  float* colpart;   // EPI 2: per-wave column sums of t, [TM NWM][N]
+  float* rowmax;    // EPI 1 / 2: max |P| per (row, N tile), [M][N / BN] (the consumer GEMM's row scale)
+  float* colmax;    // EPI 1 / 2: max |P| per (M tile, column), [TM][N] (the weight gradient's column scale)
+  int dmode;        // EPI 1: C gets gelu'(u) (1) or u (0); EPI 2: aux holds gelu'(u) (1) or u (0)
+  int ks;           // split-K slabs (EPI 0 only): slab z reduces k steps [z, z + 1) K / ks into C + z c_zs
   int64_t c_zs;
 };
 
-// AT 0: fp32 A split into two scaled fp16 pieces, B = fp16 P2 pieces, three passes (fp16x3);
-// AT 1: --precision bf16: A and B bf16 [rows][K] (32-deep k steps: again 64 B per row), one pass;
-//       OB: the output C in bf16 (EPI 0 / 3 only)
-template <int BM, int BN, int WM, int WN, int EPI, int OCC, int AT = 0, int OB = 0>
-__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F16Args g) {
+// max |x| of `rows` operand rows starting at r0 from their partials -> scale tables (2^E, 2^-E);
+// rs == 0: one per-tensor bound for every row.  Rows past `valid` get 1.
+__device__ __forceinline__ void row_scales(const float* __restrict__ p, int np, int rs, int r0, int rows, int valid,
+                                           float* s, float* is, float* red) {
+  if (rs == 0) {
+    const int E = f16_scale_exp(block_amax(p, np, red));
+    for (int t = threadIdx.x; t < rows; t += blockDim.x) {
+      if (s) s[t] = ldexpf(1.f, E);
+      is[t] = ldexpf(1.f, -E);
+    }
+    return;
+  }
+  for (int t = threadIdx.x; t < rows; t += blockDim.x) {
+    float m = 0.f;
+    if (t < valid) {
+      const float* q = p + (int64_t)(r0 + t) * rs;
+      for (int j = 0; j < np; ++j) m = fmaxf(m, q[j]);
+    }
+    const int E = f16_scale_exp(m);
+    if (s) s[t] = ldexpf(1.f, E);
+    is[t] = ldexpf(1.f, -E);
+  }
+}
+
+// ---------------------------------------------------------------- the GEMM
+// C[M][N] (+)= A[M][K] . B[N][K]^T on a BM x BN tile per workgroup, NW = (BM / WM)(BN / WN) waves.
+// k loop, step it (16-deep fp16x3 stage, or 32-deep bf16):
+//   * the MFMA passes of stage it run on fragments already in registers (read during step it - 1),
+//   * under them: the fragment reads (and, fp16x3, the fp32 -> two-piece split of A) of stage
+//     it + 1, and this wave's LDS-DMA pieces of stage it + NS - 1 into the ring slot stage it - 1
+//     used (its fragments were consumed in step it - 1, before the previous barrier),
+//   * a counted vmcnt that leaves only stage it + NS - 1's pieces in flight (so stage it + 2 has
+//     landed: NS = 4 gives every DMA two steps), then ONE raw barrier.
+// The barrier opens step it + 1 straight into MFMAs: no wave waits on a fragment read after it.
+template <int BM, int BN, int WM, int WN, int EPI, int WGS, int NS, int AT = 0, int OB = 0>
+__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) * WGS / 4) void gemm_f16_k(F16Args g) {
   static_assert(AT == 0 || EPI == 0 || EPI == 3 || OB == 1, "bf16 operands: GELU epilogues in bf16");
   static_assert(OB == 0 || AT == 1, "bf16 output with bf16 operands");
+  static_assert(NS == 3 || NS == 4, "ring depth");
   constexpr int KD = AT ? 32 : 16;       // k elements per stage
   constexpr int AE = AT ? 2 : 4;         // A element bytes
-  constexpr int NWM = BM / WM, NW = NWM * (BN / WN), NT = NW * 64;
+  constexpr int NWM = BM / WM, NWN = BN / WN, NW = NWM * NWN, NT = NW * 64;
   constexpr int MB = WM / 32, NB = WN / 32;
   constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64, STAGE = A_BYTES + B_BYTES;
-  constexpr int NS = kGemmStages;   // DMA ring depth: stage it + NS - 1 in flight during step it
   constexpr int KA = BM / 16, KB = BN / 16, PTOT = KA + KB;   // 1-KiB DMA pieces per stage
   constexpr int JHI = (PTOT + NW - 1) / NW, JLO = PTOT / NW;
   static_assert(JLO >= 1, "fewer DMA pieces than waves");
   static_assert(BM % 16 == 0 && BN % 16 == 0 && WM % 32 == 0 && WN % 32 == 0, "tile shape");
+  static_assert(NT >= BM && NT >= BN, "one thread per table row");
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  __shared__ float red[NW];
+  float* tsa = reinterpret_cast<float*>(lds + NS * STAGE);   // [BM] 2^Ea of each A row
+  float* tia = tsa + BM;                                      // [BM] 2^-Ea
+  float* tib = tia + BM;                                      // [BN] 2^-Eb of each B row
+  float* red = tib + BN;                                      // [NW] block reductions
 
   const int TM = (g.M + BM - 1) / BM, TN = g.N / BN, total = TM * TN;
   const int per = (total * g.ks + 7) / 8;
-  const int work0 = (blockIdx.x % 8) * per + blockIdx.x / 8;
-  if (work0 >= total * g.ks) return;   // uniform per workgroup
+  const int work0 = (blockIdx.x % 8) * per + blockIdx.x / 8;   // tiles dealt XCD by XCD
+  if (work0 >= total * g.ks) return;                          // uniform per workgroup
   const int z = work0 / total, work = work0 - z * total;
   const int nt = work % TN, mt = work / TN;
   const int m0 = mt * BM, n0 = nt * BN;
@@ -116,69 +154,51 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
   const u32x4 ra = rsrc_of((const char*)g.A + (int64_t)m0 * g.lda * AE, (uint32_t)((int64_t)mrows * g.lda * AE));
   const u32x4 rb = rsrc_of(g.B + (int64_t)n0 * g.ldb, (uint32_t)((int64_t)BN * g.ldb * 2));
 
-  // this wave's DMA pieces q = wv + NW j of a stage: [A pieces (16 rows of fp32) | B pieces]
-  uint32_t voff[JHI];
-  int dsto[JHI];
-  bool isa[JHI];
-  int rl, ch;
-  img_lane_src(lane, rl, ch);
+  // this wave's DMA pieces q = wv + NW j of a stage: [A pieces (16 rows) | B pieces].  Every wave
+  // issues JHI pieces (no wave-dependent branch in the k loop): a wave with JLO real pieces aims
+  // the last one past every buffer (no memory traffic) into a junk KiB after the tables.
+  constexpr int JUNK = NS * STAGE + (2 * BM + BN + NW) * 4;
+  uint32_t voff[JHI], dbase[JHI], dslot[JHI];
+  {
+    int rl, ch;
+    img_lane_src(lane, rl, ch);
 #pragma unroll
-  for (int j = 0; j < JHI; ++j) {
-    const int q = wv + NW * j;
-    isa[j] = q < KA;
-    if (q < KA) voff[j] = (uint32_t)(((int64_t)(q * 16 + rl) * g.lda + (16 / AE) * ch) * AE);
-    else voff[j] = (uint32_t)(((int64_t)((q - KA) * 16 + rl) * g.ldb + 8 * ch) * 2);
-    dsto[j] = 1024 * q;
+    for (int j = 0; j < JHI; ++j) {
+      const int q = wv + NW * j;
+      if (q < KA) voff[j] = (uint32_t)(((int64_t)(q * 16 + rl) * g.lda + (16 / AE) * ch) * AE);
+      else voff[j] = (uint32_t)(((int64_t)((q - KA) * 16 + rl) * g.ldb + 8 * ch) * 2);
+      dbase[j] = q < PTOT ? 1024u * q : (uint32_t)JUNK;
+      dslot[j] = q < PTOT ? 1u : 0u;
+      if (q >= PTOT) voff[j] = 0x40000000u;   // + any k offset stays past the buffer, never wraps
+    }
   }
-  const int cnt = (PTOT - wv + NW - 1) / NW;   // JHI or JLO
   const uint32_t lds0 = (uint32_t)(size_t)(lds_void*)lds;
-  auto dma_one = [&](int it, int buf, int j) {
-    const uint32_t st = lds0 + buf * STAGE;
-    const uint32_t ko = (uint32_t)(it0 + it) * (isa[j] ? 64u : 64u);   // 16 fp32 / 32 fp16 per row and k step
-    dma16(isa[j] ? ra : rb, st + dsto[j], voff[j] + ko);
-  };
-  auto dma = [&](int it, int buf) {
+  auto dma = [&](int it) {   // every piece of stage it into its ring slot (64 B of each row per stage)
+    const uint32_t st = (uint32_t)(it % NS) * STAGE;
+    // stages past this slab's end: an offset past every buffer (the load returns zeros, reads nothing)
+    const uint32_t ko = it < nit ? (uint32_t)(it0 + it) * 64u : 0x80000000u;
 #pragma unroll
-    for (int j = 0; j < JHI; ++j)
-      if (j < JLO || j < cnt) dma_one(it, buf, j);
-  };
-  // all but this wave's youngest `young` stages of DMAs landed (young = 0 .. NS - 2)
-  auto wait_young = [&](int young) {
-    if (young <= 0) {
-      dma_wait<0>();
-    } else if (young == 1) {
-      if constexpr (JHI == JLO) dma_wait<JLO>();
-      else if (cnt == JHI) dma_wait<JHI>();
-      else dma_wait<JLO>();
-    } else {
-      if constexpr (JHI == JLO) dma_wait<2 * JLO>();
-      else if (cnt == JHI) dma_wait<2 * JHI>();
-      else dma_wait<2 * JLO>();
+    for (int j = 0; j < JHI; ++j) {
+      const int q = wv + NW * j;   // A or B piece: uniform per wave, a select of the descriptor
+      dma16(q < KA ? ra : rb, lds0 + dbase[j] + dslot[j] * st, voff[j] + ko);
     }
   };
+  // all but this wave's youngest stage of DMA pieces landed (young = 1), or all (young = 0)
+  auto wait_young = [&](int young) {
+    if (young <= 0) dma_wait<0>();
+    else dma_wait<JHI>();
+  };
 
-  // fragment byte offsets in a stage (fixed for the k loop)
-  int offa[MB][2], offb[NB][2];
 #pragma unroll
-  for (int a = 0; a < MB; ++a) {
-    offa[a][0] = img_off(wm * WM + 32 * a + l32, 2 * h);
-    offa[a][1] = img_off(wm * WM + 32 * a + l32, 2 * h + 1);
+  for (int i = 0; i < NS - 1; ++i) dma(i);
+  if constexpr (AT == 0) {
+    // operand scales: per row (partials per row) or per tensor (one set of partials)
+    row_scales(g.a_amax, g.na, g.a_rs, m0, BM, mrows, tsa, tia, red);
+    row_scales(g.b_amax, g.nb, g.b_rs, n0, BN, BN, nullptr, tib, red);
   }
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    offb[b][0] = A_BYTES + img_off(wn * WN + 32 * b + l32, h);       // piece 0
-    offb[b][1] = A_BYTES + img_off(wn * WN + 32 * b + l32, 2 + h);   // piece 1
-  }
-
-  static_assert(NS == 3 || NS == 4, "ring depth");
-#pragma unroll
-  for (int i = 0; i < NS - 1; ++i)
-    if (i < nit) dma(i, i);
-  // operand scales (their loads over-wait the DMAs above: harmless)
-  const int Ea = AT ? 0 : f16_scale_exp(block_amax(g.a_amax, g.na, red));
-  const int Eb = AT ? 0 : f16_scale_exp(block_amax(g.b_amax, g.nb, red));
-  const float sa = ldexpf(1.f, Ea), ia = ldexpf(1.f, -Ea), ib = ldexpf(1.f, -Eb);
-  wait_young(min(nit, NS - 1) - 1);   // stage 0 landed
+  // stages 0 and 1 landed (NS = 4: stage 2 may still be in flight)
+  if constexpr (NS == 4) wait_young(1);
+  else dma_wait<0>();
   __syncthreads();
 
   f32x16 acc[MB][NB];
@@ -187,89 +207,167 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[a][b] = f32x16{0};
 
-  int cur = 0;
-  for (int it = 0; it < nit; ++it) {
-    const int nxt2 = cur == 0 ? NS - 1 : cur - 1;   // the buffer of stage it + NS - 1
-    const char* st = lds + cur * STAGE;
-    const int dit = it + NS - 1 < nit ? it + NS - 1 : -1;
-    if constexpr (AT == 1) {
-      // two 16-deep bf16 k steps per stage, one MFMA pass each; the next-next stage's DMA pieces
-      // between them
+  // fragment byte offsets in a stage (fixed for the k loop)
+  int offa[MB], offb[NB];
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8v fa[MB], fb[NB];
+  for (int a = 0; a < MB; ++a) offa[a] = (wm * WM + 32 * a + l32) * 64;
 #pragma unroll
-        for (int a = 0; a < MB; ++a)
-          fa[a] = *reinterpret_cast<const bf16x8v*>(st + img_off(wm * WM + 32 * a + l32, 2 * ks + h));
+  for (int b = 0; b < NB; ++b) offb[b] = A_BYTES + (wn * WN + 32 * b + l32) * 64;
+  const int sw = 16 * ((l32 >> 2) & 3);   // chunk swizzle of the lane's rows (img_off)
+  auto chunk = [&](int row_off, int ch) { return row_off + ((16 * ch) ^ sw); };
+
+  if constexpr (AT == 0) {
+    float sa[MB];
 #pragma unroll
-        for (int b = 0; b < NB; ++b)
-          fb[b] = *reinterpret_cast<const bf16x8v*>(st + A_BYTES + img_off(wn * WN + 32 * b + l32, 2 * ks + h));
+    for (int a = 0; a < MB; ++a) sa[a] = tsa[wm * WM + 32 * a + l32];
+    struct Fr {
+      f16x8 a0[MB], a1[MB], b0[NB], b1[NB];
+    };
+    auto read_a = [&](const char* st, f32x4 (&raw)[MB][2]) {
 #pragma unroll
-        for (int a = 0; a < MB; ++a)
-#pragma unroll
-          for (int b = 0; b < NB; ++b) acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[a], fb[b], acc[a][b], 0, 0, 0);
-        if (dit >= 0) {
-#pragma unroll
-          for (int j = ks; j < JHI; j += 2) {
-            if (j < JLO || j < cnt) {
-              __builtin_amdgcn_sched_barrier(0);
-              dma_one(dit, nxt2, j);
-              __builtin_amdgcn_sched_barrier(0);
-            }
-          }
-        }
+      for (int a = 0; a < MB; ++a) {
+        raw[a][0] = *reinterpret_cast<const f32x4*>(st + chunk(offa[a], 2 * h));
+        raw[a][1] = *reinterpret_cast<const f32x4*>(st + chunk(offa[a], 2 * h + 1));
       }
-    } else {
-    f16x8 a0[MB], a1[MB], b0[NB], b1[NB];
+    };
+    auto read_b = [&](const char* st, Fr& F) {
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      b0[b] = *reinterpret_cast<const f16x8*>(st + offb[b][0]);
-      b1[b] = *reinterpret_cast<const f16x8*>(st + offb[b][1]);
-    }
+      for (int b = 0; b < NB; ++b) {
+        F.b0[b] = *reinterpret_cast<const f16x8*>(st + chunk(offb[b], h));       // piece 0
+        F.b1[b] = *reinterpret_cast<const f16x8*>(st + chunk(offb[b], 2 + h));   // piece 1
+      }
+    };
+    auto split_a = [&](const f32x4 (&raw)[MB][2], Fr& F) {
 #pragma unroll
-    for (int a = 0; a < MB; ++a) {
-      const f32x4 lo = *reinterpret_cast<const f32x4*>(st + offa[a][0]);
-      const f32x4 hi = *reinterpret_cast<const f32x4*>(st + offa[a][1]);
-      const f32x8 y = f32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]} * sa;
-      split2(y, a0[a], a1[a]);
-    }
-    // pass q, then this wave's DMA pieces j = q, q + 3, ... of stage it + 2
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
+      for (int a = 0; a < MB; ++a) {
+        const f32x8 y = f32x8{raw[a][0][0], raw[a][0][1], raw[a][0][2], raw[a][0][3],
+                              raw[a][1][0], raw[a][1][1], raw[a][1][2], raw[a][1][3]} * sa[a];
+        split2(y, F.a0[a], F.a1[a]);
+        // pin the split here: the pieces are used one step later, past the barrier, and LLVM
+        // would otherwise sink the VALU into the next step's head (a VALU burst before its MFMAs)
+        asm volatile("" ::"v"(F.a0[a]), "v"(F.a1[a]));
+      }
+    };
+    auto pass = [&](const Fr& F, int q) {
 #pragma unroll
       for (int a = 0; a < MB; ++a)
 #pragma unroll
         for (int b = 0; b < NB; ++b)
-          acc[a][b] = mfma16(q == 2 ? a1[a] : a0[a], q == 1 ? b1[b] : b0[b], acc[a][b]);
-      if (dit >= 0) {
+          acc[a][b] = mfma16(q == 2 ? F.a1[a] : F.a0[a], q == 1 ? F.b1[b] : F.b0[b], acc[a][b]);
+    };
+    // one k step on Fc (stage it) while stage it + 1 is read into Fn -- branch-free: past the
+    // end the reads fetch a stale slot (never used) and the DMA is aimed past the buffer (no
+    // memory traffic, still counted by vmcnt), so every step has the same waits.  The fragment
+    // reads are spread over pass 0 and the split's VALU over passes 1 and 2: each wave keeps
+    // issuing MFMAs between its own reads / VALU (both waves of a SIMD leave a barrier together,
+    // so a VALU burst of one is not covered by its partner).
+    auto step = [&](int it, const Fr& Fc, Fr& Fn) {
+      const char* nx = lds + ((it + 1) % NS) * STAGE;
+      f32x4 raw[MB][2];
+      read_a(nx, raw);
+      read_b(nx, Fn);
+      pass(Fc, 0);
 #pragma unroll
-        for (int j = q; j < JHI; j += 3) {
-          if (j < JLO || j < cnt) {
-            __builtin_amdgcn_sched_barrier(0);
-            dma_one(dit, nxt2, j);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-        }
+      for (int i = 0; i < MB * NB; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, (2 * MB + 2 * NB + MB * NB - 1) / (MB * NB), 0);
       }
+      __builtin_amdgcn_sched_barrier(0);
+      dma(it + NS - 1);
+      __builtin_amdgcn_sched_barrier(0);
+      pass(Fc, 1);
+      split_a(raw, Fn);
+      pass(Fc, 2);
+#pragma unroll
+      for (int i = 0; i < 2 * MB * NB; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
+        __builtin_amdgcn_sched_group_barrier(0x002, (24 * MB + 2 * MB * NB - 1) / (2 * MB * NB), 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      // stage it + 2 landed on this wave's side (stage it + NS - 1 stays in flight), then the
+      // barrier publishes it to every wave and frees stage it's slot for the DMA of step it + 1
+      if constexpr (NS == 4) wait_young(1);
+      else dma_wait<0>();
+      raw_barrier();
+    };
+    Fr F0, F1;
+    {
+      f32x4 raw[MB][2];
+      read_a(lds, raw);
+      read_b(lds, F0);
+      split_a(raw, F0);
     }
+    for (int it = 0; it < nit; it += 2) {
+      step(it, F0, F1);
+      if (it + 1 < nit) step(it + 1, F1, F0);
     }
-    // stage it + 1 landed; stages it + 2 .. it + NS - 1 (those that exist) may still be in flight
-    wait_young(min(nit - 1 - it, NS - 1) - 1);
-    __syncthreads();
-    cur = cur == NS - 1 ? 0 : cur + 1;
+  } else {
+    // --precision bf16: two 16-deep k halves per 32-deep stage, one MFMA pass each
+    struct Fr {
+      bf16x8v a[2][MB], b[2][NB];
+    };
+    auto read = [&](const char* st, Fr& F) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int a = 0; a < MB; ++a) F.a[ks][a] = *reinterpret_cast<const bf16x8v*>(st + chunk(offa[a], 2 * ks + h));
+#pragma unroll
+        for (int b = 0; b < NB; ++b) F.b[ks][b] = *reinterpret_cast<const bf16x8v*>(st + chunk(offb[b], 2 * ks + h));
+      }
+    };
+    auto pass = [&](const Fr& F, int ks) {
+#pragma unroll
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b)
+          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.a[ks][a], F.b[ks][b], acc[a][b], 0, 0, 0);
+    };
+    auto step = [&](int it, const Fr& Fc, Fr& Fn) {   // branch-free, as the fp16x3 step
+      read(lds + ((it + 1) % NS) * STAGE, Fn);
+      pass(Fc, 0);
+#pragma unroll
+      for (int i = 0; i < MB * NB; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, (4 * MB + 4 * NB + MB * NB - 1) / (MB * NB), 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      dma(it + NS - 1);
+      __builtin_amdgcn_sched_barrier(0);
+      pass(Fc, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (NS == 4) wait_young(1);
+      else dma_wait<0>();
+      raw_barrier();
+    };
+    Fr F0, F1;
+    read(lds, F0);
+    for (int it = 0; it < nit; it += 2) {
+      step(it, F0, F1);
+      if (it + 1 < nit) step(it + 1, F1, F0);
+    }
   }
+  // every wave is past its last fragment read before the ring is reused below
+  __syncthreads();
 
   // ---- epilogue: quad transpose, then lane (l32 & 3) owns row 8 gq + 4 h + (l32 & 3) of each
   // 32 x 32 block and its columns (l32 & ~3) .. + 3; stores past M dropped by the descriptor
   const int mrow = wm * WM + 4 * h + (l32 & 3), ncol = wn * WN + (l32 & ~3);
   const hx::Buf cbuf(g.C + z * g.c_zs + (int64_t)m0 * g.ldc + n0, (uint32_t)((int64_t)mrows * g.ldc * 4));
   auto coff = [&](int a, int b, int gq) { return (uint32_t)((mrow + 32 * a + 8 * gq) * g.ldc + ncol + 32 * b) * 4; };
+  float ibc[NB][4];
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) ibc[b][i] = AT ? 1.f : tib[ncol + 32 * b + i];
   auto tr = [&](int a, int b, int gq, float (&v)[4]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = acc[a][b][4 * gq + i];
     transpose4(v, lane);
+    if constexpr (AT == 0) {
+      const float ir = tia[mrow + 32 * a + 8 * gq];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = v[i] * ia * ib;
+      for (int i = 0; i < 4; ++i) v[i] = v[i] * ir * ibc[b][i];
+    }
   };
   float bias[NB][4];
 #pragma unroll
@@ -337,12 +435,15 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
         __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), bf.r, off, 0, 0);
       }
     };
-    float csum[NB][4];
+    float csum[NB][4], cmx[NB][4], rmx[MB][4];
 #pragma unroll
     for (int b = 0; b < NB; ++b)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) csum[b][i] = 0.f;
-    float amx = 0.f;
+      for (int i = 0; i < 4; ++i) csum[b][i] = cmx[b][i] = 0.f;
+#pragma unroll
+    for (int a = 0; a < MB; ++a)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) rmx[a][gq] = 0.f;
 #pragma unroll
     for (int a = 0; a < MB; ++a) {
 #pragma unroll
@@ -394,85 +495,120 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, OCC) void gemm_f16_k(F1
               csum[b][i] += in ? o[i] : 0.f;
             }
           }
-          if (in) amx = fmaxf(amx, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+          if (in) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float m = fabsf(o[i]);
+              rmx[a][gq] = fmaxf(rmx[a][gq], m);
+              cmx[b][i] = fmaxf(cmx[b][i], m);
+            }
+          }
           st4(pbuf, poff(a, b, gq), o);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+    // column sums (EPI 2) and column maxima: over the 4 rows of a quad and the two 32-lane
+    // halves; lanes (l32 & 3) == 0, h == 0 then hold this wave's 4-column values
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        float m = cmx[b][i];
+        m = fmaxf(m, qx1(m));
+        m = fmaxf(m, qx2(m));
+        cmx[b][i] = fmaxf(m, __shfl_xor(m, 32, 64));
+        if constexpr (EPI == 2) {
+          float t = csum[b][i];
+          t += qx1(t);
+          t += qx2(t);
+          csum[b][i] = t + __shfl_xor(t, 32, 64);
+        }
+      }
+    // row maxima: over the 8 lanes of a row's 4-column groups
+#pragma unroll
+    for (int a = 0; a < MB; ++a)
+#pragma unroll
+      for (int gq = 0; gq < 4; ++gq) {
+        float m = rmx[a][gq];
+        m = fmaxf(m, __shfl_xor(m, 4, 64));
+        m = fmaxf(m, __shfl_xor(m, 8, 64));
+        rmx[a][gq] = fmaxf(m, __shfl_xor(m, 16, 64));
+      }
     if constexpr (EPI == 2) {
-      if (g.colpart) {
-        // sum over the 4 rows of a quad and the two 32-lane halves; lanes (l32 & 3) == 0, h == 0
-        // then hold this wave's 4-column sums -> partial row (mt * NWM + wm)
+      if (g.colpart && (l32 & 3) == 0 && h == 0) {
         float* row = g.colpart + (int64_t)(mt * NWM + wm) * g.N + n0 + wn * WN;
 #pragma unroll
         for (int b = 0; b < NB; ++b)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            float t = csum[b][i];
-            t += qx1(t);
-            t += qx2(t);
-            t += __shfl_xor(t, 32, 64);
-            csum[b][i] = t;
-          }
-        if ((l32 & 3) == 0 && h == 0) {
-#pragma unroll
-          for (int b = 0; b < NB; ++b)
-            *reinterpret_cast<float4*>(row + 32 * b + l32) = make_float4(csum[b][0], csum[b][1], csum[b][2], csum[b][3]);
-        }
+          *reinterpret_cast<float4*>(row + 32 * b + l32) = make_float4(csum[b][0], csum[b][1], csum[b][2], csum[b][3]);
       }
     }
-    if (g.amax_out) {
+    // across the waves sharing rows (NWN) / columns (NWM), through the (free) ring
+    float* rx = reinterpret_cast<float*>(lds);   // [NWN][BM]
+    float* cx = rx + NWN * BM;                    // [NWM][BN]
+    if (l32 < 4) {
 #pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) amx = fmaxf(amx, __shfl_xor(amx, o, 64));
-      __syncthreads();
-      if (lane == 0) red[w] = amx;
-      __syncthreads();
-      if (tid == 0) {
-        float m = red[0];
-        for (int i = 1; i < NW; ++i) m = fmaxf(m, red[i]);
-        g.amax_out[work] = m;
-      }
+      for (int a = 0; a < MB; ++a)
+#pragma unroll
+        for (int gq = 0; gq < 4; ++gq) rx[wn * BM + mrow + 32 * a + 8 * gq] = rmx[a][gq];
+    }
+    if ((l32 & 3) == 0 && h == 0) {
+#pragma unroll
+      for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cx[wm * BN + ncol + 32 * b + i] = cmx[b][i];
+    }
+    __syncthreads();
+    if (g.rowmax && tid < mrows) {
+      float m = rx[tid];
+#pragma unroll
+      for (int j = 1; j < NWN; ++j) m = fmaxf(m, rx[j * BM + tid]);
+      g.rowmax[(int64_t)(m0 + tid) * TN + nt] = m;
+    }
+    if (g.colmax && tid < BN) {
+      float m = cx[tid];
+#pragma unroll
+      for (int j = 1; j < NWM; ++j) m = fmaxf(m, cx[j * BN + tid]);
+      g.colmax[(int64_t)mt * g.N + n0 + tid] = m;
     }
   }
 }
 
 // ---------------------------------------------------------------- configurations
-// cfg 0: 256 x 192, 8 waves of 32 x 192 (each A fragment split by ONE wave)      -- M >= 8192
-// cfg 1: 256 x 192, 8 waves (4 x 2) of 64 x 96 (A fragments split by two waves, fewer B reads)
-// cfg 2: 128 x 96, 4 waves of 32 x 96                                            -- M < 8192
-// cfg 3: 64 x 64, 4 waves (2 x 2) of 32 x 32                                     -- tiny M
-// cfg 5: 256 x 256, 8 waves (4 x 2) of 64 x 128                                  -- explicit only
-// cfg 4: 128 x 192, 4 waves of 32 x 192: two workgroups per CU (60 KB of LDS each), so one
-//        tile's prologue / epilogue store burst overlaps the other's main loop
+// cfg 0: 256 x 192, 8 waves of 32 x 192, one workgroup per CU, 4-stage ring       -- M >= 8192
+// cfg 1: 256 x 192, 8 waves (4 x 2) of 64 x 96, one workgroup per CU, 4-stage ring
+// cfg 2: 128 x 96, 4 waves of 32 x 96, two workgroups per CU, 4-stage ring        -- M < 8192
+// cfg 3: 64 x 64, 4 waves (2 x 2) of 32 x 32, 4-stage ring                          -- tiny M
+// cfg 4: 128 x 192, 4 waves (2 x 2) of 64 x 96, two workgroups per CU, 3-stage ring
+// cfg 5: 256 x 256, 8 waves (4 x 2) of 64 x 128, one workgroup per CU, 4-stage ring
 constexpr int kCfgs = 6;
 int cfg_bm(int c) { return c <= 1 || c == 5 ? 256 : c == 2 || c == 4 ? 128 : 64; }
 int cfg_bn(int c) { return c == 5 ? 256 : c <= 1 || c == 4 ? 192 : c == 2 ? 96 : 64; }
-int cfg_nwm(int c) { return c == 0 ? 8 : c == 1 || c == 5 ? 4 : c == 2 || c == 4 ? 4 : 2; }
+int cfg_nwm(int c) { return c == 0 ? 8 : c == 1 || c == 5 ? 4 : c == 2 ? 4 : 2; }
 
-template <int BM, int BN, int WM, int WN, int EPI, int AT = 0, int OB = 0>
+template <int BM, int BN, int WM, int WN, int EPI, int WGS, int NS, int AT = 0, int OB = 0>
 void launch_one(const F16Args& a, hipStream_t s) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int total = ((a.M + BM - 1) / BM) * (a.N / BN) * a.ks;
   const int per = (total + 7) / 8;
-  const size_t smem = (size_t)kGemmStages * (BM + BN) * 64;
+  const size_t smem = (size_t)NS * (BM + BN) * 64 + (2 * BM + BN + NT / 64) * 4 + 1024;   // + junk DMA KiB
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_f16_k<BM, BN, WM, WN, EPI, 1, AT, OB>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_f16_k<BM, BN, WM, WN, EPI, WGS, NS, AT, OB>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
-  gemm_f16_k<BM, BN, WM, WN, EPI, 1, AT, OB><<<8 * per, NT, smem, s>>>(a);
+  gemm_f16_k<BM, BN, WM, WN, EPI, WGS, NS, AT, OB><<<8 * per, NT, smem, s>>>(a);
 }
 
 template <int EPI, int AT = 0, int OB = 0>
 void launch_cfg(int cfg, const F16Args& a, hipStream_t s) {
-  if (cfg == 0) launch_one<256, 192, 32, 192, EPI, AT, OB>(a, s);
-  else if (cfg == 1) launch_one<256, 192, 64, 96, EPI, AT, OB>(a, s);
-  else if (cfg == 2) launch_one<128, 96, 32, 96, EPI, AT, OB>(a, s);
-  else if (cfg == 4) launch_one<128, 192, 32, 192, EPI, AT, OB>(a, s);
-  else if (cfg == 5) launch_one<256, 256, 64, 128, EPI, AT, OB>(a, s);
-  else launch_one<64, 64, 32, 32, EPI, AT, OB>(a, s);
+  if (cfg == 0) launch_one<256, 192, 32, 192, EPI, 1, 4, AT, OB>(a, s);
+  else if (cfg == 1) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB>(a, s);
+  else if (cfg == 2) launch_one<128, 96, 32, 96, EPI, 2, 4, AT, OB>(a, s);
+  else if (cfg == 4) launch_one<128, 192, 64, 96, EPI, 2, 3, AT, OB>(a, s);
+  else if (cfg == 5) launch_one<256, 256, 64, 128, EPI, 1, 4, AT, OB>(a, s);
+  else launch_one<64, 64, 32, 32, EPI, 2, 4, AT, OB>(a, s);
 }
 
 // ---------------------------------------------------------------- weight gradient (tokens = reduction)
@@ -503,11 +639,34 @@ __device__ __forceinline__ f16x8 tfrag(const char* tile, const int (&lo)[2], con
   return *reinterpret_cast<const f16x8*>(v);
 }
 
+// column scale tables of a weight-gradient operand (ColScale, hx_launch.h)
+__device__ __forceinline__ void col_scales(const HxColScale& c, int c0, int cols, float* s, float* is, float* red) {
+  if (c.g == nullptr && c.cs == 0) {
+    const int E = f16_scale_exp(block_amax(c.p, c.np, red));
+    for (int t = threadIdx.x; t < cols; t += blockDim.x) {
+      s[t] = ldexpf(1.f, E);
+      is[t] = ldexpf(1.f, -E);
+    }
+    return;
+  }
+  for (int t = threadIdx.x; t < cols; t += blockDim.x) {
+    float m = 0.f;
+    if (c.g) {
+      m = (fabsf(c.g[c0 + t]) * c.z + fabsf(c.b[c0 + t])) * c.mul;
+    } else {
+      for (int j = 0; j < c.np; ++j) m = fmaxf(m, c.p[(int64_t)j * c.cs + c0 + t]);
+    }
+    const int E = f16_scale_exp(m);
+    s[t] = ldexpf(1.f, E);
+    is[t] = ldexpf(1.f, -E);
+  }
+}
+
 template <int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const float* __restrict__ A, int lda,
-                                                                         const float* __restrict__ a_amax, int na,
+                                                                         const HxColScale ca,
                                                                          const float* __restrict__ B, int ldb,
-                                                                         const float* __restrict__ b_amax, int nb,
+                                                                         const HxColScale cb,
                                                                          float* __restrict__ out, int M, int N, int T,
                                                                          int kchunk, int nsplit, int mvalid) {
   constexpr int NWM = BM / WM, NW = NWM * (BN / WN), NT = NW * 64;
@@ -519,7 +678,12 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
   constexpr int A_T = BKT * BM * 2, B_T = BKT * BN * 2;   // one fp16 piece tile
   constexpr int STAGE = 2 * (A_T + B_T);
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  __shared__ float red[NW];
+  // per-column scales of the two operands (dY's columns = dW's rows, X's columns = dW's columns)
+  float* tsa = reinterpret_cast<float*>(lds + 2 * STAGE);
+  float* tia = tsa + BM;
+  float* tsb = tia + BM;
+  float* tib = tsb + BN;
+  float* red = tib + BN;
 
   const int total = (M / BM) * (N / BN) * nsplit;
   const int per = (total + 7) / 8;
@@ -537,24 +701,30 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w % NWM, wn = w / NWM;
 
-  const int Ea = f16_scale_exp(block_amax(a_amax, na, red)), Eb = f16_scale_exp(block_amax(b_amax, nb, red));
-  const float sa = ldexpf(1.f, Ea), sb = ldexpf(1.f, Eb), ia = ldexpf(1.f, -Ea), ib = ldexpf(1.f, -Eb);
+  col_scales(ca, m0, BM, tsa, tia, red);
+  col_scales(cb, n0, BN, tsb, tib, red);
+  __syncthreads();
 
   const hx::Buf abuf(A + (int64_t)t0 * lda, (uint32_t)((int64_t)(t1 - t0) * lda * 4));
   const hx::Buf bbuf(B + (int64_t)t0 * ldb, (uint32_t)((int64_t)(t1 - t0) * ldb * 4));
   uint32_t va[CA], vb[CB];
   int sa_[CA], sb_[CB];
+  f32x8 csa[CA], csb[CB];   // the chunks' 8 column scales
 #pragma unroll
   for (int i = 0; i < CA; ++i) {
     const int e = tid + i * NT, row = e / (BM / 8), c = e % (BM / 8);
     va[i] = (uint32_t)(row * lda + m0 + 8 * c) * 4;
     sa_[i] = toff<BM>(row, c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) csa[i][j] = tsa[8 * c + j];
   }
 #pragma unroll
   for (int i = 0; i < CB; ++i) {
     const int e = tid + i * NT, row = e / (BN / 8), c = e % (BN / 8);
     vb[i] = (uint32_t)(row * ldb + n0 + 8 * c) * 4;
     sb_[i] = toff<BN>(row, c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) csb[i][j] = tsb[8 * c + j];
   }
   int alo[2], ahi[2], blo[2], bhi[2];
   tr_base<BM>(lane, alo, ahi);
@@ -584,7 +754,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
 #pragma unroll
     for (int i = 0; i < CA; ++i) {
       const f32x8 y = f32x8{r.a[i][0][0], r.a[i][0][1], r.a[i][0][2], r.a[i][0][3],
-                            r.a[i][1][0], r.a[i][1][1], r.a[i][1][2], r.a[i][1][3]} * sa;
+                            r.a[i][1][0], r.a[i][1][1], r.a[i][1][2], r.a[i][1][3]} * csa[i];
       f16x8 h0, h1;
       split2(y, h0, h1);
       *reinterpret_cast<f16x8*>(st + sa_[i]) = h0;
@@ -593,7 +763,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
 #pragma unroll
     for (int i = 0; i < CB; ++i) {
       const f32x8 y = f32x8{r.b[i][0][0], r.b[i][0][1], r.b[i][0][2], r.b[i][0][3],
-                            r.b[i][1][0], r.b[i][1][1], r.b[i][1][2], r.b[i][1][3]} * sb;
+                            r.b[i][1][0], r.b[i][1][1], r.b[i][1][2], r.b[i][1][3]} * csb[i];
       f16x8 h0, h1;
       split2(y, h0, h1);
       *reinterpret_cast<f16x8*>(st + 2 * A_T + sb_[i]) = h0;
@@ -656,7 +826,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int m = m0 + wm * WM + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (m < mvalid) o[(int64_t)m * N + n] = acc[a][b][r] * ia * ib;   // rows past mvalid: padding
+        if (m < mvalid) o[(int64_t)m * N + n] = acc[a][b][r] * tia[m - m0] * tib[n - n0];   // rows past mvalid: padding
       }
     }
 }
@@ -674,16 +844,22 @@ __global__ __launch_bounds__(256) void slab_sum_k(const float4* __restrict__ ws,
 }
 
 template <int BM, int BN, int WM, int WN>
-void wgrad_launch(const float* A, int lda, const float* aam, int na, const float* B, int ldb, const float* bam, int nb,
+void wgrad_launch(const float* A, int lda, const HxColScale& ca, const float* B, int ldb, const HxColScale& cb,
                   float* out, float* ws, int M, int N, int T, int nsplit, int mvalid, hipStream_t s) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int kchunk = ((T + nsplit - 1) / nsplit + 15) / 16 * 16;
   nsplit = (T + kchunk - 1) / kchunk;
   const int total = (M / BM) * (N / BN) * nsplit;
   const int per = (total + 7) / 8;
-  const size_t smem = (size_t)2 * 2 * 16 * (BM + BN) * 2;
-  wgrad_f16_k<BM, BN, WM, WN><<<8 * per, NT, smem, s>>>(A, lda, aam, na, B, ldb, bam, nb, nsplit > 1 ? ws : out, M, N,
-                                                        T, kchunk, nsplit, nsplit > 1 ? M : mvalid);
+  const size_t smem = (size_t)2 * 2 * 16 * (BM + BN) * 2 + (2 * BM + 2 * BN + NT / 64) * 4;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_f16_k<BM, BN, WM, WN>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    attr = true;
+  }
+  wgrad_f16_k<BM, BN, WM, WN><<<8 * per, NT, smem, s>>>(A, lda, ca, B, ldb, cb, nsplit > 1 ? ws : out, M, N, T,
+                                                        kchunk, nsplit, nsplit > 1 ? M : mvalid);
   if (nsplit > 1) {
     const int64_t n4 = (int64_t)mvalid * N / 4, slab4 = (int64_t)M * N / 4;
     const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
@@ -692,44 +868,68 @@ void wgrad_launch(const float* A, int lda, const float* aam, int na, const float
   }
 }
 
-// ---------------------------------------------------------------- max |x| partials, weight pieces
-// max |x| over a [rows][cols] fp32 matrix (row stride ld, cols % 4 == 0): one partial per block
+// ---------------------------------------------------------------- max |x| per row, weight pieces
+// max |x| of every row of a [rows][cols] fp32 matrix (row stride ld, cols % 4 == 0): one wave per
+// row (the per-row operand scale of the fp16x3 GEMMs, when no producer wrote it)
 __global__ __launch_bounds__(256) void amax_rows_k(const float* __restrict__ x, int64_t rows, int cols, int64_t ld,
-                                                   float* __restrict__ part) {
-  __shared__ float red[4];
-  const int c4 = cols / 4;
-  const int64_t n4 = rows * c4;
+                                                   float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const float4* p = reinterpret_cast<const float4*>(x + r * ld);
   float m = 0.f;
-  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
-    const int64_t r = i / c4;
-    const int c = (int)(i - r * c4);
-    const float4 v = *reinterpret_cast<const float4*>(x + r * ld + 4 * c);
+  for (int c = lane; c < cols / 4; c += 64) {
+    const float4 v = p[c];
     m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  if (lane == 0) out[r] = m;
 }
 
-// HX_WAMAX_PARTS partials per weight of a batch: block b -> weight b / P, slice b % P
-constexpr int kWParts = 32;
-__global__ __launch_bounds__(256) void amax_weights_k(HxWeightBatch d, float* __restrict__ part) {
-  __shared__ float red[4];
-  const int i = blockIdx.x / kWParts, j = blockIdx.x % kWParts;
-  const int64_t n4 = (int64_t)d.N[i] * d.K[i] / 4;
-  const float4* x = reinterpret_cast<const float4*>(d.W[i]);
-  float m = 0.f;
-  for (int64_t k = (int64_t)j * 256 + threadIdx.x; k < n4; k += (int64_t)kWParts * 256) {
-    const float4 v = x[k];
-    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-  }
+// row and column maxima of every weight of a batch, one 64 x 64 tile per workgroup: atomic max
+// (non-negative floats order as their bit patterns) into rmax[n] / cmax[k], zeroed beforehand
+__global__ __launch_bounds__(256) void amax_weights_k(HxWeightBatch d, float* __restrict__ rc) {
+  __shared__ float cm[4][64];
+  const int blk = blockIdx.x;
+  int i = 0;
+  while (i + 1 < d.n && blk >= d.start[i + 1]) ++i;   // uniform per workgroup
+  const int N = d.N[i], K = d.K[i];
+  const int tk = K / 64, loc = blk - d.start[i];
+  const int k0 = (loc % tk) * 64, n0 = (loc / tk) * 64;
+  const float* W = d.W[i];
+  float* rmax = rc + d.roff[i];
+  float* cmax = rmax + N;
+  const int t = threadIdx.x, c4 = (t & 15) * 4;
+  float col[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  for (int r4 = 0; r4 < 4; ++r4) {
+    const int r = (t >> 4) + 16 * r4;
+    const float4 v = *reinterpret_cast<const float4*>(W + (int64_t)(n0 + r) * K + k0 + c4);
+    const float a[4] = {fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w)};
+    float m = fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) col[j] = fmaxf(col[j], a[j]);
+    // the 16 lanes of a row (t & 15) are consecutive lanes of one wave
+#pragma unroll
+    for (int o = 8; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if ((t & 15) == 0) atomicMax(reinterpret_cast<unsigned*>(rmax + n0 + r), __float_as_uint(m));
+  }
+  // columns: over the 4 row groups of a wave (lanes t, t + 16, t + 32, t + 48), then the 4 waves
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    col[j] = fmaxf(col[j], __shfl_xor(col[j], 16, 64));
+    col[j] = fmaxf(col[j], __shfl_xor(col[j], 32, 64));
+  }
+  if ((t & 63) < 16) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) cm[t >> 6][c4 + j] = col[j];
+  }
   __syncthreads();
-  if (threadIdx.x == 0) part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  if (t < 64) {
+    const float m = fmaxf(fmaxf(cm[0][t], cm[1][t]), fmaxf(cm[2][t], cm[3][t]));
+    atomicMax(reinterpret_cast<unsigned*>(cmax + k0 + t), __float_as_uint(m));
+  }
 }
 
 // element offset of (row, piece p, column c) in the P2 layout [rows][C / 16][2][16]
@@ -738,33 +938,39 @@ __device__ __forceinline__ int64_t p2_off(int64_t row, int p, int c, int C) {
 }
 
 // both P2 piece layouts of every weight of a batch, one 64 x 64 tile per workgroup:
-//   wf[n] = pieces of W[n][:] (forward B operand), wt[k] = pieces of W[:][k] (data gradient)
-__global__ __launch_bounds__(256) void split_weight_f16_k(HxWeightBatch d, const float* __restrict__ part) {
+//   wf[n] = pieces of W[n][:] scaled by row n's 2^E (forward B operand, rows = output columns),
+//   wt[k] = pieces of W[:][k] scaled by column k's 2^E (data gradient B operand)
+__global__ __launch_bounds__(256) void split_weight_f16_k(HxWeightBatch d, const float* __restrict__ rc) {
   __shared__ uint16_t tile[2][64][66];
-  __shared__ float red[4];
   const int blk = blockIdx.x;
   int i = 0;
   while (i + 1 < d.n && blk >= d.start[i + 1]) ++i;   // uniform per workgroup
-  const float s = ldexpf(1.f, f16_scale_exp(block_amax(part + i * kWParts, kWParts, red)));
   const int N = d.N[i], K = d.K[i];
   const int tk = K / 64, loc = blk - d.start[i];
   const int k0 = (loc % tk) * 64, n0 = (loc / tk) * 64;
   const float* W = d.W[i];
+  const float* rmax = rc + d.roff[i];
+  const float* cmax = rmax + N;
   const int t = threadIdx.x, c4 = (t & 15) * 4;
+  float cs[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) cs[j] = ldexpf(1.f, f16_scale_exp(cmax[k0 + c4 + j]));
 #pragma unroll
   for (int r4 = 0; r4 < 4; ++r4) {
     const int r = (t >> 4) + 16 * r4;
+    const float rs = ldexpf(1.f, f16_scale_exp(rmax[n0 + r]));
     const float4 v = *reinterpret_cast<const float4*>(W + (int64_t)(n0 + r) * K + k0 + c4);
-    const float e[4] = {v.x * s, v.y * s, v.z * s, v.w * s};
+    const float x[4] = {v.x, v.y, v.z, v.w};
     uint16_t q0[4], q1[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const _Float16 h0 = (_Float16)e[j];
-      const _Float16 h1 = (_Float16)(e[j] - (float)h0);
+      const float e = x[j] * rs, f = x[j] * cs[j];
+      const _Float16 h0 = (_Float16)e, h1 = (_Float16)(e - (float)h0);
+      const _Float16 g0 = (_Float16)f, g1 = (_Float16)(f - (float)g0);
       q0[j] = __builtin_bit_cast(uint16_t, h0);
       q1[j] = __builtin_bit_cast(uint16_t, h1);
-      tile[0][r][c4 + j] = q0[j];
-      tile[1][r][c4 + j] = q1[j];
+      tile[0][r][c4 + j] = __builtin_bit_cast(uint16_t, g0);
+      tile[1][r][c4 + j] = __builtin_bit_cast(uint16_t, g1);
     }
     *reinterpret_cast<uint2*>(d.wf[i] + p2_off(n0 + r, 0, k0 + c4, K)) =
         make_uint2(q0[0] | ((uint32_t)q0[1] << 16), q0[2] | ((uint32_t)q0[3] << 16));
@@ -859,6 +1065,8 @@ int hx_gemm_f16_tiles(int M, int N, int cfg) {
   if (cfg < 0 || cfg >= kCfgs) return 0;
   return (M + cfg_bm(cfg) - 1) / cfg_bm(cfg) * (N / cfg_bn(cfg));
 }
+int hx_gemm_f16_tm(int M, int cfg) { return cfg < 0 || cfg >= kCfgs ? 0 : (M + cfg_bm(cfg) - 1) / cfg_bm(cfg); }
+int hx_gemm_f16_tn(int N, int cfg) { return cfg < 0 || cfg >= kCfgs ? 0 : N / cfg_bn(cfg); }
 
 int hx_gemm_f16_colpart_rows(int M, int cfg) {
   if (cfg < 0 || cfg >= kCfgs) return 0;
@@ -927,10 +1135,12 @@ int hx_gemm_f16(const HxGemmF16& p, int cfg, hipStream_t s) {
   a.lda = p.lda;
   a.a_amax = p.a_amax;
   a.na = p.na;
+  a.a_rs = p.a_rs;
   a.B = p.B;
   a.ldb = p.ldb;
   a.b_amax = p.b_amax;
   a.nb = p.nb;
+  a.b_rs = p.b_rs;
   a.C = p.C;
   a.ldc = p.ldc;
   a.M = p.M;
@@ -943,7 +1153,8 @@ int hx_gemm_f16(const HxGemmF16& p, int cfg, hipStream_t s) {
   a.P = p.P;
   a.ldp = p.ldp;
   a.colpart = p.colpart;
-  a.amax_out = p.amax_out;
+  a.rowmax = p.rowmax;
+  a.colmax = p.colmax;
   a.dmode = p.dmode;
   a.ks = ks;
   a.c_zs = p.c_zs;
@@ -984,31 +1195,69 @@ void hx_wgrad_f16_plan(int M, int N, int T, int* cfg, int* nsplit) {
   *nsplit = sp;
 }
 
-int hx_wgrad_f16(const float* dy, int ldy, const float* dy_amax, int na, const float* x, int ldx, const float* x_amax,
-                 int nb, float* out, float* ws, int M, int N, int T, int cfg, int nsplit, int mvalid, hipStream_t s) {
+int hx_wgrad_f16(const float* dy, int ldy, const HxColScale& ca, const float* x, int ldx, const HxColScale& cb,
+                 float* out, float* ws, int M, int N, int T, int cfg, int nsplit, int mvalid, hipStream_t s) {
   if (ldy % 4 || ldx % 4 || M % 128 || N % 128 || T < 1) return -1;
   if (cfg == 1) {
     if (M % 256 || N % 256) return -1;
-    wgrad_launch<256, 256, 128, 64>(dy, ldy, dy_amax, na, x, ldx, x_amax, nb, out, ws, M, N, T, nsplit, mvalid, s);
+    wgrad_launch<256, 256, 128, 64>(dy, ldy, ca, x, ldx, cb, out, ws, M, N, T, nsplit, mvalid, s);
   } else {
-    wgrad_launch<128, 128, 64, 64>(dy, ldy, dy_amax, na, x, ldx, x_amax, nb, out, ws, M, N, T, nsplit, mvalid, s);
+    wgrad_launch<128, 128, 64, 64>(dy, ldy, ca, x, ldx, cb, out, ws, M, N, T, nsplit, mvalid, s);
   }
   return 0;
 }
 
-int hx_amax_rows_parts(int64_t rows, int cols) {
-  const int64_t n4 = rows * (cols / 4);
-  return (int)std::max<int64_t>(1, std::min<int64_t>(512, (n4 + 4095) / 4096));
+// column maxima of a [rows][cols] fp32 matrix: each block a 64-row x 256-column slab (float4 per
+// thread), atomic max (non-negative floats order as their bits) into out[cols], zeroed beforehand
+__global__ __launch_bounds__(256) void amax_cols_k(const float* __restrict__ x, int64_t rows, int cols, int64_t ld,
+                                                   int rows_per_block, float* __restrict__ out) {
+  __shared__ float4 red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = (blockIdx.x * 64 + lane) * 4;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per_block;
+  const int64_t r1 = min(rows, r0 + rows_per_block);
+  float4 m = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < cols) {
+    for (int64_t r = r0 + w; r < r1; r += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(x + r * ld + c);
+      m.x = fmaxf(m.x, fabsf(v.x)); m.y = fmaxf(m.y, fabsf(v.y));
+      m.z = fmaxf(m.z, fabsf(v.z)); m.w = fmaxf(m.w, fabsf(v.w));
+    }
+  }
+  red[w][lane] = m;
+  __syncthreads();
+  if (w == 0 && c < cols) {
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+      const float4 v = red[j][lane];
+      m.x = fmaxf(m.x, v.x); m.y = fmaxf(m.y, v.y); m.z = fmaxf(m.z, v.z); m.w = fmaxf(m.w, v.w);
+    }
+    atomicMax(reinterpret_cast<unsigned*>(out + c), __float_as_uint(m.x));
+    atomicMax(reinterpret_cast<unsigned*>(out + c + 1), __float_as_uint(m.y));
+    atomicMax(reinterpret_cast<unsigned*>(out + c + 2), __float_as_uint(m.z));
+    atomicMax(reinterpret_cast<unsigned*>(out + c + 3), __float_as_uint(m.w));
+  }
 }
 
-void hx_amax_rows(const float* x, int64_t rows, int cols, int64_t ld, float* part, int nparts, hipStream_t s) {
-  amax_rows_k<<<nparts, 256, 0, s>>>(x, rows, cols, ld, part);
+void hx_amax_cols(const float* x, int64_t rows, int cols, int64_t ld, float* out, hipStream_t s) {
+  (void)hipMemsetAsync(out, 0, (size_t)cols * 4, s);
+  if (rows < 1) return;
+  const int cb = (cols / 4 + 63) / 64;
+  // ~4 workgroups per CU over the row slabs
+  int64_t slabs = std::max<int64_t>(1, std::min<int64_t>((rows + 63) / 64, (1024 + cb - 1) / cb));
+  const int rpb = (int)((rows + slabs - 1) / slabs);
+  slabs = (rows + rpb - 1) / rpb;
+  amax_cols_k<<<dim3(cb, (unsigned)slabs), 256, 0, s>>>(x, rows, cols, ld, rpb, out);
 }
 
-int hx_weight_f16_parts() { return kWParts; }
+void hx_amax_rows(const float* x, int64_t rows, int cols, int64_t ld, float* out, hipStream_t s) {
+  if (rows < 1) return;
+  amax_rows_k<<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(x, rows, cols, ld, out);
+}
 
-void hx_split_weight_f16(const HxWeightBatch& d, float* part, hipStream_t s) {
+void hx_split_weight_f16(const HxWeightBatch& d, float* rc, int64_t rc_floats, hipStream_t s) {
   if (d.n < 1) return;
-  amax_weights_k<<<d.n * kWParts, 256, 0, s>>>(d, part);
-  split_weight_f16_k<<<d.start[d.n], 256, 0, s>>>(d, part);
+  (void)hipMemsetAsync(rc, 0, (size_t)rc_floats * 4, s);
+  amax_weights_k<<<d.start[d.n], 256, 0, s>>>(d, rc);
+  split_weight_f16_k<<<d.start[d.n], 256, 0, s>>>(d, rc);
 }

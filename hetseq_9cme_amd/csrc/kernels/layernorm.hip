@@ -29,20 +29,11 @@ struct Row {
   float4 v[CH];
 };
 
-// max |x| over the block -> part[blockIdx.x] (the fp16x3 GEMMs' operand scale, ops/gemm16.py);
-// every thread of the block must call it
-__device__ __forceinline__ void block_amax_out(float m, float* __restrict__ part) {
-  __shared__ float red_am[WPB];
+// max |x| of the wave's row -> amax_row[r] (the fp16x3 GEMMs' per-row operand scale, ops/gemm16.py)
+__device__ __forceinline__ void row_amax_out(float m, float* __restrict__ amax_row, int64_t r) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  if ((threadIdx.x & 63) == 0) red_am[threadIdx.x >> 6] = m;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float r = red_am[0];
-#pragma unroll
-    for (int i = 1; i < WPB; ++i) r = fmaxf(r, red_am[i]);
-    part[blockIdx.x] = r;
-  }
+  if ((threadIdx.x & 63) == 0) amax_row[r] = m;
 }
 __device__ __forceinline__ float amax4(float m, float4 v) {
   return fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
@@ -63,8 +54,8 @@ __global__ __launch_bounds__(NT) void ln_fwd_k(const T* __restrict__ y, const fl
   const int64_t nw = (int64_t)gridDim.x * WPB;
   const float inv_keep = keep_prob > 0.f ? 1.f / keep_prob : 0.f;
   const bool drop = keep_prob < 1.f;
-  float am = 0.f;
   for (int64_t r = wave; r < rows; r += nw) {
+    float am = 0.f;
     Row<CH> x;
     float s = 0.f;
 #pragma unroll
@@ -130,8 +121,8 @@ __global__ __launch_bounds__(NT) void ln_fwd_k(const T* __restrict__ y, const fl
         am = amax4(am, o);
       }
     }
+    if (amax_part) row_amax_out(am, amax_part, r);
   }
-  if (amax_part) block_amax_out(am, amax_part);
 }
 
 // ----------------------------------------------------------------------------- bwd
@@ -143,7 +134,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
                                              const float* __restrict__ gamma, T* __restrict__ dz_out,
                                              T* __restrict__ dy_out, float* __restrict__ partial, int64_t rows,
                                              int H, float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream,
-                                             int want_dbias, float* __restrict__ amax_part) {
+                                             int want_dbias, float* __restrict__ amax_part, int want_cmax) {
   const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   __shared__ float red[WPB][CH * 256];
   const int lane = threadIdx.x & 63;
@@ -152,10 +143,9 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
   const int64_t nw = (int64_t)gridDim.x * WPB;
   const float inv_keep = keep_prob > 0.f ? 1.f / keep_prob : 0.f;
   const bool drop = keep_prob < 1.f;
-  Row<CH> dg, db, dbias;
+  Row<CH> dg, db, dbias, cmx;   // cmx: column max |dy| (|dz| without dy), the weight gradient's scale
 #pragma unroll
-  for (int c = 0; c < CH; ++c) dg.v[c] = db.v[c] = dbias.v[c] = hx::f4(0.f);
-  float am = 0.f;   // max |dy| (max |dz| without a separate dy): the upstream GEMMs' operand
+  for (int c = 0; c < CH; ++c) dg.v[c] = db.v[c] = dbias.v[c] = cmx.v[c] = hx::f4(0.f);
   float4 gam[CH];
 #pragma unroll
   for (int c = 0; c < CH; ++c) {
@@ -183,6 +173,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
   for (int64_t r = wave; r < rows; r += nw) {
     const Row<CH> zc = zn, dc = dn;
     const float mean = mn, rstd = rn;
+    float am = 0.f;   // max |dy| (max |dz| without a separate dy): the upstream GEMMs' row scale
     if (r + nw < rows) load_row(r + nw);
     Row<CH> xh, dxh;
     float s1 = 0.f, s2 = 0.f;
@@ -221,7 +212,10 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
         float4 dz = make_float4(rstd * (dv.x - m1 - xv.x * m2), rstd * (dv.y - m1 - xv.y * m2),
                                 rstd * (dv.z - m1 - xv.z * m2), rstd * (dv.w - m1 - xv.w * m2));
         hx::store4(dz_out + r * H + j, dz);
-        if (!dy_out) am = amax4(am, dz);
+        if (!dy_out) {
+          am = amax4(am, dz);
+          if (want_cmax) cmx.v[c] = hx::max4(cmx.v[c], hx::abs4(dz));
+        }
         if (dy_out) {
           float4 dy = dz;
           if (drop && !kDropAfter) {
@@ -233,12 +227,14 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
           }
           hx::store4(dy_out + r * H + j, dy);
           am = amax4(am, dy);
+          if (want_cmax) cmx.v[c] = hx::max4(cmx.v[c], hx::abs4(dy));
           if (want_dbias) {
             dbias.v[c].x += dy.x; dbias.v[c].y += dy.y; dbias.v[c].z += dy.z; dbias.v[c].w += dy.w;
           }
         }
       }
     }
+    if (amax_part) row_amax_out(am, amax_part, r);
   }
   // fold the 4 waves' column partials through LDS (each accumulator selected at
   // compile time: a runtime-selected reference would demote them to scratch)
@@ -252,15 +248,15 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
     for (int j = threadIdx.x; j < H; j += NT) {
       float a = 0.f;
 #pragma unroll
-      for (int ww = 0; ww < WPB; ++ww) a += red[ww][j];
-      partial[((int64_t)blockIdx.x * 3 + q) * H + j] = a;
+      for (int ww = 0; ww < WPB; ++ww) a = q == 3 ? fmaxf(a, red[ww][j]) : a + red[ww][j];
+      partial[((int64_t)blockIdx.x * 4 + q) * H + j] = a;
     }
     __syncthreads();
   };
   fold(dg, 0);
   fold(db, 1);
   if (want_dbias) fold(dbias, 2);
-  if (amax_part) block_amax_out(am, amax_part);
+  if (want_cmax) fold(cmx, 3);
 }
 
 // ------------------------------------------------------------------------ embedding
@@ -278,8 +274,8 @@ __global__ __launch_bounds__(NT) void embed_ln_fwd_k(const int64_t* __restrict__
   const int64_t wave = blockIdx.x * (int64_t)WPB + (threadIdx.x >> 6);
   const int64_t nw = (int64_t)gridDim.x * WPB;
   const float inv_keep = keep_prob > 0.f ? 1.f / keep_prob : 0.f;
-  float am = 0.f;
   for (int64_t r = wave; r < rows; r += nw) {
+    float am = 0.f;
     const int64_t id = ids[r];
     const int64_t ty = tt ? tt[r] : 0;
     const int64_t pos = r % S;
@@ -335,8 +331,8 @@ __global__ __launch_bounds__(NT) void embed_ln_fwd_k(const int64_t* __restrict__
         am = amax4(am, o);
       }
     }
+    if (amax_part) row_amax_out(am, amax_part, r);
   }
-  if (amax_part) block_amax_out(am, amax_part);
 }
 
 // word-embedding gradient: scatter-add rows of dz into dW[ids] (fp32 atomics,
@@ -452,18 +448,20 @@ template <typename T>
 void ln_bwd_t(const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma, void* dz,
               void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
               uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
-              int accumulate, hipStream_t s, float* amax_part) {
+              int accumulate, hipStream_t s, float* amax_part, float* colmax) {
+  const int wc = colmax != nullptr;
   HX_CH_DISPATCH(H, {
     if (drop_after)
       ln_bwd_k<T, CH, true><<<nblk, NT, 0, s>>>((const T*)dout, (const T*)z, mean, rstd, gamma, (T*)dz, (T*)dy,
-                                                partial, rows, H, keep_prob, seed, stream, want_dbias, amax_part);
+                                                partial, rows, H, keep_prob, seed, stream, want_dbias, amax_part, wc);
     else
       ln_bwd_k<T, CH, false><<<nblk, NT, 0, s>>>((const T*)dout, (const T*)z, mean, rstd, gamma, (T*)dz, (T*)dy,
-                                                 partial, rows, H, keep_prob, seed, stream, want_dbias, amax_part);
+                                                 partial, rows, H, keep_prob, seed, stream, want_dbias, amax_part, wc);
   })
-  // partial is [nblk][3][H]: fold rows of length 3H into dgamma | dbeta | dbias
-  hx::fold_rows(partial, nblk, 3 * (int64_t)H, (want_dbias ? 3 : 2) * H, H, dgamma, dbeta,
-                want_dbias ? dbias : nullptr, accumulate, s);
+  // partial is [nblk][4][H]: fold rows of length 4H into dgamma | dbeta | dbias (sums) and the
+  // column maxima (max)
+  hx::fold_rows(partial, nblk, 4 * (int64_t)H, wc ? 4 * H : (want_dbias ? 3 : 2) * H, H, dgamma, dbeta,
+                want_dbias ? dbias : nullptr, accumulate, s, 3 * H, colmax);
 }
 
 }  // namespace
@@ -485,13 +483,13 @@ void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, cons
 void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma,
                void* dz, void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
                uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
-               int accumulate, hipStream_t s, float* amax_part) {
+               int accumulate, hipStream_t s, float* amax_part, float* colmax) {
   if (bf16)
     ln_bwd_t<uint16_t>(dout, z, mean, rstd, gamma, dz, dy, partial, nblk, rows, H, keep_prob, seed, stream,
-                       drop_after, want_dbias, dgamma, dbeta, dbias, accumulate, s, nullptr);
+                       drop_after, want_dbias, dgamma, dbeta, dbias, accumulate, s, nullptr, nullptr);
   else
     ln_bwd_t<float>(dout, z, mean, rstd, gamma, dz, dy, partial, nblk, rows, H, keep_prob, seed, stream, drop_after,
-                    want_dbias, dgamma, dbeta, dbias, accumulate, s, amax_part);
+                    want_dbias, dgamma, dbeta, dbias, accumulate, s, amax_part, colmax);
 }
 
 void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,

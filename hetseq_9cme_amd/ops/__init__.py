@@ -5,7 +5,7 @@ hand-written HIP kernel for GPU tensors and a torch reference for CPU tensors.
 """
 from ._ext import C, use_kernels, set_fused, fused_enabled  # noqa: F401
 from .rng import get_rng, set_step_seed  # noqa: F401
-from .fp32_mode import set_fp32_gemm, fp32_gemm_mode, set_fp32_attention, fp32_attention_mode  # noqa: F401
+from .fp32_mode import set_fp32_gemm, fp32_gemm_mode  # noqa: F401
 from .fused import (  # noqa: F401
     embed_ln, bias_dropout_residual_ln, layer_norm, bias_act, dropout, linear3, attention,
     decoder_xent, masked_rows, gelu_ref, layer_norm_ref, linear, grad_slot, ResidualGrad,

@@ -9,8 +9,7 @@ csrc/kernels/attention.hip) for head_dim 64 at any sequence length (keys past
 S are masked, rows past S are neither computed into nor stored), with fp32 or
 bf16 activations (bf16 activations: bf16 MFMA, attention_bf16.hip; fp32 activations under
 ``--fp32-gemm fp16x3``: the products as three fp16 passes over scaled two-piece operands,
-attention_f16.hip, or with ``--fp32-attention x6`` from 4096 token rows as six bf16 piece passes,
-attention_x6.hip; fp32 MFMA otherwise and under ``--fp32-gemm native``);
+attention_f16.hip; fp32 MFMA under ``--fp32-gemm native``, attention.hip);
 other shapes / dtypes use the composite below (batched GEMMs + softmax), which
 is also the CPU path and the test oracle.
 """
@@ -74,19 +73,13 @@ class _AttnFn(torch.autograd.Function):
         keep = 1.0 - p
         seed, stream = get_rng().next(qkv.device) if p > 0 else (get_rng().seed_tensor(qkv.device), 0)
         bias = _bias3(bq, bk, bv).float().contiguous() if bq is not None else None
-        # the piece kernels (fp32_mode.attention_split: fp16x3 at every size, x6 from 4096 token rows --
-        # smaller batches keep the fp32-MFMA attention under x6)
+        # fp32 under fp16x3: the fp16x3 piece kernels (fp32_mode.attention_split), which also write
+        # the context's max |x| per (row, head) -- the attention-output GEMM's per-row scale
         ctx.split = qkv.dtype == torch.float32 and fp32_mode.attention_split(qkv.reshape(-1, qkv.shape[-1]))
         if ctx.split:
-            # fp32 products on the bf16 matrix cores (six piece passes, attention_x6.hip); the
-            # context's max |x| partials for the attention-output projection's fp16x3 GEMM
             B, S = qkv.shape[0], qkv.shape[1]
-            am = torch.empty(((S + 127) // 128) * num_heads * B * 4, dtype=torch.float32, device=qkv.device) \
-                if gemm16.enabled() else None
-            # the backward pairs with the kernel family THIS forward ran, whatever the mode is later
-            ctx.f16 = fp32_mode.fp32_attention_mode() == 'fp16x3'
-            fwd = C().attn_fwd_f16 if ctx.f16 else C().attn_fwd_x6
-            out, lse, dmask = fwd(qkv, mask_bias, num_heads, keep, seed, stream, bias, am)
+            am = torch.empty(B * S, num_heads, dtype=torch.float32, device=qkv.device)
+            out, lse, dmask = C().attn_fwd_f16(qkv, mask_bias, num_heads, keep, seed, stream, bias, am)
             gemm16.attach(out, am)
         else:
             out, lse, dmask = C().attn_fwd(qkv, mask_bias, num_heads, keep, seed, stream, bias)
@@ -108,13 +101,12 @@ class _AttnFn(torch.autograd.Function):
             if not all(t is not None for t in slots):
                 slots = [None, None, None]
         if ctx.split:
-            # fp16x3 with one key block (S <= 128): the kernel writes max |dQKV| partials for the QKV
-            # projection's data / weight gradient GEMMs
-            am = torch.empty(qkv.shape[0] * num_heads, dtype=torch.float32, device=qkv.device) \
-                if gemm16.enabled() and qkv.shape[1] <= 128 else None
-            bwd = C().attn_bwd_f16 if ctx.f16 else C().attn_bwd_x6
-            dqkv, dbias = bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep, ctx.bias,
-                              *slots, am)
+            # one key block (S <= 128): the kernel writes max |dQKV| per (row, head) -- the QKV
+            # projection's per-row operand scale
+            am = torch.empty(qkv.shape[0] * qkv.shape[1], num_heads, dtype=torch.float32, device=qkv.device) \
+                if qkv.shape[1] <= 128 else None
+            dqkv, dbias = C().attn_bwd_f16(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep,
+                                           ctx.bias, *slots, am)
             gemm16.attach(dqkv, am)
         else:
             dqkv, dbias = C().attn_bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep, ctx.bias,

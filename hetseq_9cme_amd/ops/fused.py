@@ -274,12 +274,11 @@ def embed_ln(ids, tt, wte, wpe, wtt, gamma, beta, eps, p, training, out_dtype=to
 
 
 def _amax_buf(rows, ref, bf16, bwd=False):
-    """Buffer for a LayerNorm kernel's max |out| partials when the fp16x3 GEMMs consume its output
-    (ops/gemm16.py), else None."""
+    """[rows, 1] buffer for a LayerNorm kernel's max |out| of every row (the per-row operand scale
+    of the fp16x3 GEMMs that consume its output, ops/gemm16.py), or None when no such GEMM runs."""
     if bf16 or not gemm16.enabled() or not ref.is_cuda:
         return None
-    n = C().ln_bwd_blocks(rows) if bwd else C().ln_fwd_blocks(rows)
-    return torch.empty(n, dtype=torch.float32, device=ref.device)
+    return torch.empty(rows, 1, dtype=torch.float32, device=ref.device)
 
 
 # ----------------------------------------------------------------- bias + dropout + residual + LN
@@ -501,10 +500,11 @@ class _FFNFn(torch.autograd.Function):
     def forward(ctx, x, W1, b1, W2, mbox):
         x2 = gemm16.rows2(x)
         xparts = gemm16.amax(x, x2)
-        d, h, hparts, w1t, p1 = gemm16.gemm_gelu(x2, xparts, W1, b1)
+        d, h, hparts, hcols, w1t, p1 = gemm16.gemm_gelu(x2, xparts, W1, b1)
         y2, w2t, p2 = gemm16.linear(h, hparts, W2)
         ctx.save_for_backward(x2, d, h, w1t, w2t)
         ctx.parts = (xparts, hparts, p1, p2)
+        ctx.hcols = hcols
         ctx.W, ctx.b1, ctx.mbox, ctx.xshape = (W1, W2), b1, mbox, x.shape
         return y2.view(*x.shape[:-1], y2.shape[-1])
 
@@ -528,7 +528,7 @@ def _ffn_backward_f16(ctx, dy):
         for t in (dy2, dparts, h, hparts):
             t.record_stream(side)
     # GELU backward in the FFN-down data-gradient epilogue: t = (dy W2) * gelu'(u), d b1
-    t, tparts, db1 = gemm16.gemm_dgelu(dy2, dparts, w2t, p2, d, grad_slot(ctx.b1))
+    t, tparts, tcols, db1 = gemm16.gemm_dgelu(dy2, dparts, w2t, p2, d, grad_slot(ctx.b1))
     if side is not None:
         side = side_begin(dy2.device, True)   # after t
     with torch.cuda.stream(side) if side is not None else _nullctx():
@@ -760,9 +760,9 @@ class _DecoderXentFn(torch.autograd.Function):
         ctx.f16 = gemm16.ok(h, 64) and h.is_contiguous() and H % 64 == 0
         ctx.b16 = False
         if ctx.f16:   # fp32 runs: the fp16x3 GEMM
-            wf, wt, wparts = C().split_weight_f16([_padded_rows(W, Vp)])[0]
-            full = gemm16.mm(h, gemm16.amax(h, h), wf, wparts)
-            ctx.wpieces = (wt, wparts)
+            wf, wt, wrow, wcol = C().split_weight_f16([_padded_rows(W, Vp)])[0]
+            full = gemm16.mm(h, gemm16.amax(h, h), wf, wrow)
+            ctx.wpieces = (wt, wcol)
         elif gemm16.bf16_ok(h, 64, H) and h.is_contiguous():
             # --precision bf16 on the hand-written kernel (bf16 logits)
             ctx.b16 = True

@@ -1,14 +1,18 @@
 """fp32 GEMMs as three fp16 piece products (``--fp32-gemm fp16x3``; csrc/kernels/gemm_f16.hip).
 
-Every fp32 operand x is used as 2^-E (h0 + h1) with h0 = fp16(2^E x), h1 = fp16(2^E x - h0):
+Every fp32 operand row x is used as 2^-E (h0 + h1) with h0 = fp16(2^E x), h1 = fp16(2^E x - h0):
 22 significant bits per element; the product a.b is a0 b0 + a0 b1 + a1 b0 (the dropped a1 b1
 is 2^-22 relative) -- three fp16 MFMA passes where the bf16 emulation needs six
-(the round-3 ``bf16x6`` mode).  E comes from the operand's max |x|, so every
-tensor handed to these GEMMs travels with **max |x| partials**: a small fp32 vector whose max is
-max |x| (its producer writes it -- this module's GELU epilogues, LayerNorm, attention -- or
-``amax`` computes it in one read pass).  The GEMMs read activations and gradients AS fp32 and
-split them in registers; only weights are split ahead of time (one launch per forward for the
-whole encoder, ``weight_scope``).
+(the round-3 ``bf16x6`` mode).  E is chosen PER ROW of each operand (per row of A and per row
+of B = output column; the epilogue multiplies by 2^-(Ea[r] + Eb[c])), so a row keeps 22 bits
+however far below the tensor's largest row it lies.  Every tensor handed to these GEMMs
+travels with **max |x| partials per row**: a [rows, P] fp32 tensor whose row-wise max is that
+row's max |x| (its producer writes it -- LayerNorm [rows, 1], attention [rows, heads], this
+module's GELU epilogues [rows, N tiles] -- or ``amax`` computes it in one read pass).  A 1-D
+tensor instead is a per-tensor bound (e.g. ``bound``).  The GEMMs read activations and gradients
+AS fp32 and split them in registers; only weights are split ahead of time (one launch per forward
+for the whole encoder, ``weight_scope``), W's rows scaled by their own maxima and W^T's rows
+(= W's columns) by the column maxima.
 
 Reference sites: hetseq/bert_modeling.py:334-336 (Q/K/V), :383 (attention output), :409 +
 :166-168 (FFN up, bias_gelu), :419 (FFN down), :509 (pooler), :522 (MLM transform), :538-547
@@ -65,7 +69,8 @@ def attach(t, parts):
 
 
 def amax(t, t2=None):
-    """max |t| partials: the producer's (if ``t`` has not changed since), else one read pass."""
+    """max |t| partials per row ([rows, P]): the producer's (if ``t`` has not changed since), else
+    one read pass ([rows, 1])."""
     p = getattr(t, '_hx_amax', None)
     if p is not None and getattr(t, '_hx_amax_ver', -1) == t._version:
         return p
@@ -116,7 +121,8 @@ class weight_scope(object):
 
 
 def weight_pieces(W):
-    """(wf [N, 2K], wt [K, 2N], parts) of W [N, K] (N, K multiples of 64)."""
+    """(wf [N, 2K], wt [K, 2N], rmax [N, 1], cmax [K, 1]) of W [N, K] (N, K multiples of 64): the
+    pieces of W and of W^T, and the per-row scale sources of each (W's row / column maxima)."""
     if _State.scope is not None:
         e = _State.scope.get((W.data_ptr(), tuple(W.shape)))
         if e is not None:
@@ -127,21 +133,28 @@ def weight_pieces(W):
 # ---------------------------------------------------------------- products
 def mm(a2, a_parts, b, b_parts, out=None, beta=False, bias=None, ks=0):
     """a2 [M, K] (fp32) . b^T (b = P2 pieces [N, 2K]) (+ out if beta) (+ bias) -> fp32 [M, N];
+    ``a_parts`` / ``b_parts``: per-row max |x| partials of a2 and of b's rows;
     ``ks``: split-K slabs (0 = the kernel's plan: deep reductions with few output tiles)."""
     return C().gemm_f16(a2, a_parts, b, b_parts, out=out, beta=beta, bias=bias, ks=ks)
 
 
 def linear(x2, xparts, W, bias=None):
-    """y = x2 W^T (+ bias); also returns W^T's pieces and W's partials for the backward."""
-    wf, wt, parts = weight_pieces(W)
-    return mm(x2, xparts, wf, parts, bias=bias), wt, parts
+    """y = x2 W^T (+ bias); also returns W^T's pieces and their row scale source (W's column
+    maxima) for the backward."""
+    wf, wt, rmax, cmax = weight_pieces(W)
+    return mm(x2, xparts, wf, rmax, bias=bias), wt, cmax
 
 
-def dgrad(dy2, dparts, wt, parts, acc=None):
+def dgrad(dy2, dparts, wt, wt_parts, acc=None):
     """dx = dy2 W from W^T's pieces, accumulated into ``acc`` (beta = 1) when given."""
     if acc is not None:
-        return mm(dy2, dparts, wt, parts, out=acc, beta=True)
-    return mm(dy2, dparts, wt, parts)
+        return mm(dy2, dparts, wt, wt_parts, out=acc, beta=True)
+    return mm(dy2, dparts, wt, wt_parts)
+
+
+def _tensor_bound(p):
+    """A per-tensor max |x| bound from any partials (the weight gradient's operand scale)."""
+    return p if p.dim() == 1 and p.numel() <= 4096 else p.amax().reshape(1)
 
 
 def wgrad(dy2, dparts, x2, xparts, n_out, n_in, slot=None):
@@ -149,22 +162,22 @@ def wgrad(dy2, dparts, x2, xparts, n_out, n_in, slot=None):
     (shapes without a tile: the library fp32 product)."""
     out = slot if slot is not None else torch.empty(n_out, n_in, device=dy2.device)
     if wgrad_ok(dy2.shape[1], n_in) and dy2.shape[1] >= n_out and _aligned(dy2) and _aligned(x2):
-        return C().wgrad_f16(dy2, dparts, x2, xparts, out)
+        return C().wgrad_f16(dy2, _tensor_bound(dparts), x2, _tensor_bound(xparts), out)
     return torch.mm(dy2[:, :n_out].t(), x2, out=out)
 
 
 def gemm_gelu(x2, xparts, W1, b1):
-    """FFN up with its bias + GELU epilogue: (gelu'(u), h = gelu(u), max |h| partials, W1^T's
-    pieces, W1's partials)."""
-    wf, wt, parts = weight_pieces(W1)
-    d, h, hmax = C().gemm_f16_gelu(x2, xparts, wf, parts, b1, 1)
-    return d, h, hmax, wt, parts
+    """FFN up with its bias + GELU epilogue: (gelu'(u), h = gelu(u), h's per-row max |.| partials
+    [M, N tiles], h's column maxima per M tile [M tiles, N], W1^T's pieces, W1's column maxima)."""
+    wf, wt, rmax, cmax = weight_pieces(W1)
+    d, h, hrow, hcol = C().gemm_f16_gelu(x2, xparts, wf, rmax, b1, 1)
+    return d, h, hrow, hcol, wt, cmax
 
 
-def gemm_dgelu(dy2, dparts, wt2, parts2, d, dbias_out):
-    """FFN-down data gradient with the GELU backward: (t = (dy W2) * gelu'(u), max |t| partials,
-    d b1)."""
-    return C().gemm_f16_dgelu(dy2, dparts, wt2, parts2, d, None, dbias_out, 1)
+def gemm_dgelu(dy2, dparts, wt2, wt2_parts, d, dbias_out):
+    """FFN-down data gradient with the GELU backward: (t = (dy W2) * gelu'(u), t's per-row max |.|
+    partials, t's column maxima per M tile, d b1)."""
+    return C().gemm_f16_dgelu(dy2, dparts, wt2, wt2_parts, d, None, dbias_out, 1)
 
 
 # ---------------------------------------------------------------- --precision bf16 (same kernel, one pass)

@@ -59,14 +59,9 @@ def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialD
                         help='how fp32 (--precision fp32) runs use the matrix cores: fp16x3 (default: every '
                              'linear-layer GEMM on the hand-written kernels with operands scaled by a power of two '
                              'from their max |x| and split into two fp16 pieces -- 22 bits each, three exact piece '
-                             'products; measured GEMM error 0.6-0.7x native fp32\'s; attention products as six '
-                             'bf16 piece passes from 4096 token rows) or native (f32 MFMA, 157 TF/s peak, '
+                             'products; measured GEMM error 0.6-0.7x native fp32\'s; the attention products as three '
+                             'fp16 passes as well) or native (f32 MFMA, 157 TF/s peak, '
                              'through the libraries: the numerics oracle); see ops/fp32_mode.py')
-    parser.add_argument('--fp32-attention', default='fp16x3', choices=['fp16x3', 'x6'],
-                        help='with --fp32-gemm fp16x3, the attention products: fp16x3 (default, every batch '
-                             'size: three fp16 passes over scaled two-piece operands, backward at two waves per '
-                             'SIMD; rows 2^40 below their tile\'s largest value flushed) or x6 (six bf16 piece '
-                             'passes from 4096 token rows, every row fp32 class); see ops/fp32_mode.py')
     parser.add_argument('--graph-train-step', action='store_true',
                         help='single GPU, one micro-batch per update: capture each input shape\'s whole '
                              'update (forward, backward, clip, optimizer) in a HIP graph after two eager '

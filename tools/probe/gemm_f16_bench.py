@@ -32,7 +32,7 @@ def sweep(C, dev, cfgs):
         W = torch.randn(N, K, device=dev, generator=g) * 0.03
         b = torch.randn(N, device=dev, generator=g)
         xp = C().amax_rows(x)
-        wf, wt, wp = C().split_weight_f16([W])[0]
+        wf, wt, wp, wc = C().split_weight_f16([W])[0]
         dy = torch.randn(T, N, device=dev, generator=g)
         dp = C().amax_rows(dy)
         acc = torch.randn(T, K, device=dev, generator=g)
@@ -54,9 +54,9 @@ def sweep(C, dev, cfgs):
                 else:
                     f = timed(lambda: C().gemm_f16(x, xp, wf, wp, bias=b, ks=ks))
                 if name == 'ffn_down':
-                    dg = timed(lambda: C().gemm_f16_dgelu(dy, dp, wt, wp, d, None, db, 1))
+                    dg = timed(lambda: C().gemm_f16_dgelu(dy, dp, wt, wc, d, None, db, 1))
                 else:
-                    dg = timed(lambda: C().gemm_f16(dy, dp, wt, wp, out=acc, beta=True, ks=ks))
+                    dg = timed(lambda: C().gemm_f16(dy, dp, wt, wc, out=acc, beta=True, ks=ks))
                 bf = timed(lambda: C().gemm_bf16(xb, Wb, bias=b))
             except RuntimeError as e:
                 print('{:10s} cfg {}: {}'.format(name, c, str(e).splitlines()[0]), flush=True)
@@ -85,7 +85,7 @@ def main():
         W = rnd(N, K) * 0.03
         b = rnd(N)
         xp = C().amax_rows(x)
-        wf, wt, wp = C().split_weight_f16([W])[0]
+        wf, wt, wp, wc = C().split_weight_f16([W])[0]
         fl = 2.0 * T * N * K
         if name == 'ffn_up':
             us = timed(lambda: C().gemm_f16_gelu(x, xp, wf, wp, b, 1))
@@ -98,12 +98,13 @@ def main():
         if name == 'ffn_down':
             d = rnd(T, K)
             db = torch.zeros(K, device=dev)
-            us = timed(lambda: C().gemm_f16_dgelu(dy, dp, wt, wp, d, None, db, 1))
+            us = timed(lambda: C().gemm_f16_dgelu(dy, dp, wt, wc, d, None, db, 1))
         else:
-            us = timed(lambda: C().gemm_f16(dy, dp, wt, wp, out=acc, beta=True))
+            us = timed(lambda: C().gemm_f16(dy, dp, wt, wc, out=acc, beta=True))
         rows.append(('dgrad ' + name, T, K, N, us, fl))
         out = torch.empty(N, K, device=dev)
-        us = timed(lambda: C().wgrad_f16(dy, dp, x, xp, out))
+        dc, xc = C().amax_cols(dy), C().amax_cols(x)
+        us = timed(lambda: C().wgrad_f16(dy, dc, x, xc, out))
         rows.append(('wgrad ' + name, N, K, T, us, fl))
         xb, Wb, dyb = x.bfloat16(), W.bfloat16(), dy.bfloat16()
         us = timed(lambda: C().gemm_bf16(xb, Wb, bias=b))

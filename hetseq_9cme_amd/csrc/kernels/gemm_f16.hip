@@ -57,6 +57,19 @@ __device__ __forceinline__ f32x16 mfma16(const f16x8& a, const f16x8& b, const f
 // across it; the k loop retires what it needs with counted waits), and a compiler memory fence
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
 
+// the two-piece split of two fp32 values (x0, x1) at scale s: h0 = fp16(s x), h1 = fp16(s x - h0),
+// both round-to-nearest-even, as two packed halves -- four v_fma_mix instructions (the fma is exact
+// before its one rounding), against 12 for cvt / pk_fma / cvt (hx_gemm.h split2)
+__device__ __forceinline__ void split_pair_mix(float x0, float x1, float s, uint32_t& h0, uint32_t& h1) {
+  asm volatile(
+      "v_fma_mixlo_f16 %0, %2, %4, 0 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %3, %4, 0 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %3, %4, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(h0), "=&v"(h1)
+      : "v"(x0), "v"(x1), "v"(s));
+}
+
 struct F16Args {
   const void* A;   // fp32 (AT 0) or bf16 (AT 1)
   int64_t lda;
@@ -116,11 +129,11 @@ __device__ __forceinline__ void row_scales(const float* __restrict__ p, int np, 
 //   * a counted vmcnt that leaves only stage it + NS - 1's pieces in flight (so stage it + 2 has
 //     landed: NS = 4 gives every DMA two steps), then ONE raw barrier.
 // The barrier opens step it + 1 straight into MFMAs: no wave waits on a fragment read after it.
-template <int BM, int BN, int WM, int WN, int EPI, int WGS, int NS, int AT = 0, int OB = 0>
+template <int BM, int BN, int WM, int WN, int EPI, int WGS, int NS, int AT = 0, int OB = 0, int DIL = 1>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) * WGS / 4) void gemm_f16_k(F16Args g) {
   static_assert(AT == 0 || EPI == 0 || EPI == 3 || OB == 1, "bf16 operands: GELU epilogues in bf16");
   static_assert(OB == 0 || AT == 1, "bf16 output with bf16 operands");
-  static_assert(NS == 3 || NS == 4, "ring depth");
+  static_assert(NS >= 3 && NS <= 5, "ring depth");
   constexpr int KD = AT ? 32 : 16;       // k elements per stage
   constexpr int AE = AT ? 2 : 4;         // A element bytes
   constexpr int NWM = BM / WM, NWN = BN / WN, NW = NWM * NWN, NT = NW * 64;
@@ -167,27 +180,34 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
       const int q = wv + NW * j;
       if (q < KA) voff[j] = (uint32_t)(((int64_t)(q * 16 + rl) * g.lda + (16 / AE) * ch) * AE);
       else voff[j] = (uint32_t)(((int64_t)((q - KA) * 16 + rl) * g.ldb + 8 * ch) * 2);
+      if constexpr (DIL == 9) {   // DIAGNOSTIC (timing only, wrong image): 8 rows x 128 B per piece
+        const int r8 = lane >> 3, c8 = lane & 7;
+        if (q < KA) voff[j] = (uint32_t)(((int64_t)(q * 8 + r8) * g.lda) * AE + 16 * c8);
+        else voff[j] = (uint32_t)(((int64_t)((q - KA) * 8 + r8) * g.ldb) * 2 + 16 * c8);
+      }
       dbase[j] = q < PTOT ? 1024u * q : (uint32_t)JUNK;
       dslot[j] = q < PTOT ? 1u : 0u;
       if (q >= PTOT) voff[j] = 0x40000000u;   // + any k offset stays past the buffer, never wraps
     }
   }
   const uint32_t lds0 = (uint32_t)(size_t)(lds_void*)lds;
-  auto dma = [&](int it) {   // every piece of stage it into its ring slot (64 B of each row per stage)
+  auto dma_one = [&](int it, int j) {   // piece j of this wave for stage it (64 B of each row per stage)
     const uint32_t st = (uint32_t)(it % NS) * STAGE;
     // stages past this slab's end: an offset past every buffer (the load returns zeros, reads nothing)
     const uint32_t ko = it < nit ? (uint32_t)(it0 + it) * 64u : 0x80000000u;
-#pragma unroll
-    for (int j = 0; j < JHI; ++j) {
-      const int q = wv + NW * j;   // A or B piece: uniform per wave, a select of the descriptor
-      dma16(q < KA ? ra : rb, lds0 + dbase[j] + dslot[j] * st, voff[j] + ko);
+    const int q = wv + NW * j;   // A or B piece: uniform per wave, a select of the descriptor
+    dma16(q < KA ? ra : rb, lds0 + dbase[j] + dslot[j] * st, voff[j] + ko);
+  };
+  auto dma = [&](int it) {   // every piece of stage it into its ring slot
+    if constexpr (DIL == 8 || DIL >= 11) {   // DIAGNOSTIC (timing only, stale data): no DMA after the prologue
+      if (it >= NS - 1) return;
     }
+#pragma unroll
+    for (int j = 0; j < JHI; ++j) dma_one(it, j);
   };
-  // all but this wave's youngest stage of DMA pieces landed (young = 1), or all (young = 0)
-  auto wait_young = [&](int young) {
-    if (young <= 0) dma_wait<0>();
-    else dma_wait<JHI>();
-  };
+  // stage it + 2 landed on this wave's side: the youngest NS - 3 stages (it + 3 .. it + NS - 1) may
+  // stay in flight
+  auto wait_ring = [&]() { dma_wait<(NS - 3) * JHI>(); };
 
 #pragma unroll
   for (int i = 0; i < NS - 1; ++i) dma(i);
@@ -197,8 +217,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
     row_scales(g.b_amax, g.nb, g.b_rs, n0, BN, BN, nullptr, tib, red);
   }
   // stages 0 and 1 landed (NS = 4: stage 2 may still be in flight)
-  if constexpr (NS == 4) wait_young(1);
-  else dma_wait<0>();
+  wait_ring();   // stages 0 and 1 landed
   __syncthreads();
 
   f32x16 acc[MB][NB];
@@ -238,6 +257,14 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
       }
     };
     auto split_a = [&](const f32x4 (&raw)[MB][2], Fr& F) {
+      if constexpr (DIL >= 10) {   // DIAGNOSTIC (timing only): no split VALU
+#pragma unroll
+        for (int a = 0; a < MB; ++a) {
+          F.a0[a] = __builtin_bit_cast(f16x8, raw[a][0]);
+          F.a1[a] = __builtin_bit_cast(f16x8, raw[a][1]);
+        }
+        return;
+      }
 #pragma unroll
       for (int a = 0; a < MB; ++a) {
         const f32x8 y = f32x8{raw[a][0][0], raw[a][0][1], raw[a][0][2], raw[a][0][3],
@@ -248,19 +275,21 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
         asm volatile("" ::"v"(F.a0[a]), "v"(F.a1[a]));
       }
     };
+    auto mma = [&](const Fr& F, int q, int i) {   // MFMA i (= a NB + b) of pass q
+      const int a = i / NB, b = i % NB;
+      acc[a][b] = mfma16(q == 2 ? F.a1[a] : F.a0[a], q == 1 ? F.b1[b] : F.b0[b], acc[a][b]);
+    };
     auto pass = [&](const Fr& F, int q) {
 #pragma unroll
-      for (int a = 0; a < MB; ++a)
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-          acc[a][b] = mfma16(q == 2 ? F.a1[a] : F.a0[a], q == 1 ? F.b1[b] : F.b0[b], acc[a][b]);
+      for (int i = 0; i < MB * NB; ++i) mma(F, q, i);
     };
     // one k step on Fc (stage it) while stage it + 1 is read into Fn -- branch-free: past the
     // end the reads fetch a stale slot (never used) and the DMA is aimed past the buffer (no
     // memory traffic, still counted by vmcnt), so every step has the same waits.  The fragment
-    // reads are spread over pass 0 and the split's VALU over passes 1 and 2: each wave keeps
-    // issuing MFMAs between its own reads / VALU (both waves of a SIMD leave a barrier together,
-    // so a VALU burst of one is not covered by its partner).
+    // reads are spread over pass 0; the DMA pieces go as one burst (r5d: interleaving them with
+    // MFMAs measured 2-5 % slower); the split of the next A fragments runs as v_fma_mix pairs, one
+    // pair after each of the first pass-1 / pass-2 MFMAs (r5g: the packed cvt / pk_fma split cost
+    // 17 % of the kernel).
     auto step = [&](int it, const Fr& Fc, Fr& Fn) {
       const char* nx = lds + ((it + 1) % NS) * STAGE;
       f32x4 raw[MB][2];
@@ -275,20 +304,34 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
       __builtin_amdgcn_sched_barrier(0);
       dma(it + NS - 1);
       __builtin_amdgcn_sched_barrier(0);
-      pass(Fc, 1);
-      split_a(raw, Fn);
-      pass(Fc, 2);
+      if constexpr (DIL >= 10 || 4 * MB > 2 * MB * NB) {   // small wave tiles / DIL diag: compiler split
+        pass(Fc, 1);
+        split_a(raw, Fn);
+        pass(Fc, 2);
+      } else {
+        uint32_t h0w[MB][4], h1w[MB][4];
+        constexpr int P0 = DIL == 2 ? 2 * MB * NB - 4 * MB : 0;   // MFMA of the first pair
 #pragma unroll
-      for (int i = 0; i < 2 * MB * NB; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 1);
-        __builtin_amdgcn_sched_group_barrier(0x002, (24 * MB + 2 * MB * NB - 1) / (2 * MB * NB), 1);
+        for (int i = 0; i < 2 * MB * NB; ++i) {
+          mma(Fc, 1 + i / (MB * NB), i % (MB * NB));
+          if (i >= P0 && i < P0 + 4 * MB) {
+            const int a = (i - P0) / 4, w = (i - P0) % 4;
+            const f32x4& r = raw[a][w >> 1];
+            split_pair_mix(r[2 * (w & 1)], r[2 * (w & 1) + 1], sa[a], h0w[a][w], h1w[a][w]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int a = 0; a < MB; ++a) {
+          Fn.a0[a] = __builtin_bit_cast(f16x8, u32x4{h0w[a][0], h0w[a][1], h0w[a][2], h0w[a][3]});
+          Fn.a1[a] = __builtin_bit_cast(f16x8, u32x4{h1w[a][0], h1w[a][1], h1w[a][2], h1w[a][3]});
+        }
       }
       __builtin_amdgcn_sched_barrier(0);
       // stage it + 2 landed on this wave's side (stage it + NS - 1 stays in flight), then the
       // barrier publishes it to every wave and frees stage it's slot for the DMA of step it + 1
-      if constexpr (NS == 4) wait_young(1);
-      else dma_wait<0>();
-      raw_barrier();
+      wait_ring();
+      if constexpr (DIL != 12) raw_barrier();   // (12: the no-barrier timing diagnostic)
     };
     Fr F0, F1;
     {
@@ -315,12 +358,13 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
         for (int b = 0; b < NB; ++b) F.b[ks][b] = *reinterpret_cast<const bf16x8v*>(st + chunk(offb[b], 2 * ks + h));
       }
     };
+    auto mma = [&](const Fr& F, int ks, int i) {
+      const int a = i / NB, b = i % NB;
+      acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.a[ks][a], F.b[ks][b], acc[a][b], 0, 0, 0);
+    };
     auto pass = [&](const Fr& F, int ks) {
 #pragma unroll
-      for (int a = 0; a < MB; ++a)
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-          acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(F.a[ks][a], F.b[ks][b], acc[a][b], 0, 0, 0);
+      for (int i = 0; i < MB * NB; ++i) mma(F, ks, i);
     };
     auto step = [&](int it, const Fr& Fc, Fr& Fn) {   // branch-free, as the fp16x3 step
       read(lds + ((it + 1) % NS) * STAGE, Fn);
@@ -331,12 +375,22 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
         __builtin_amdgcn_sched_group_barrier(0x100, (4 * MB + 4 * NB + MB * NB - 1) / (MB * NB), 0);
       }
       __builtin_amdgcn_sched_barrier(0);
-      dma(it + NS - 1);
+      constexpr int NI = DIL == 1 ? (JHI < MB * NB ? JHI : MB * NB) : 0;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {   // one DMA piece after each of the first MFMAs (fp16x3 step)
+        mma(Fc, 1, j);
+        dma_one(it + NS - 1, j);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if constexpr (DIL != 8) {   // (8: the no-DMA timing diagnostic)
+#pragma unroll
+        for (int j = NI; j < JHI; ++j) dma_one(it + NS - 1, j);
+      }
       __builtin_amdgcn_sched_barrier(0);
-      pass(Fc, 1);
+#pragma unroll
+      for (int i = NI; i < MB * NB; ++i) mma(Fc, 1, i);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (NS == 4) wait_young(1);
-      else dma_wait<0>();
+      wait_ring();
       raw_barrier();
     };
     Fr F0, F1;
@@ -575,18 +629,20 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
 }
 
 // ---------------------------------------------------------------- configurations
-// cfg 0: 256 x 192, 8 waves of 32 x 192, one workgroup per CU, 4-stage ring       -- M >= 8192
-// cfg 1: 256 x 192, 8 waves (4 x 2) of 64 x 96, one workgroup per CU, 4-stage ring
+// cfg 0: 256 x 192, 8 waves of 32 x 192, one workgroup per CU, 4-stage ring
+// cfg 1: 256 x 192, 8 waves (4 x 2) of 64 x 96, one workgroup per CU, 4-stage ring -- M >= 8192
 // cfg 2: 128 x 96, 4 waves of 32 x 96, two workgroups per CU, 4-stage ring        -- M < 8192
 // cfg 3: 64 x 64, 4 waves (2 x 2) of 32 x 32, 4-stage ring                          -- tiny M
 // cfg 4: 128 x 192, 4 waves (2 x 2) of 64 x 96, two workgroups per CU, 3-stage ring
 // cfg 5: 256 x 256, 8 waves (4 x 2) of 64 x 128, one workgroup per CU, 4-stage ring
-constexpr int kCfgs = 6;
-int cfg_bm(int c) { return c <= 1 || c == 5 ? 256 : c == 2 || c == 4 ? 128 : 64; }
-int cfg_bn(int c) { return c == 5 ? 256 : c <= 1 || c == 4 ? 192 : c == 2 ? 96 : 64; }
-int cfg_nwm(int c) { return c == 0 ? 8 : c == 1 || c == 5 ? 4 : c == 2 ? 4 : 2; }
+// cfg 6: cfg 1 with the DMA pieces issued as one burst (A/B of the interleave)
+// cfg 7: cfg 1 on a 5-stage ring (A/B of the ring depth: r5c, no gain)
+constexpr int kCfgs = 13;   // 8 .. 12: timing diagnostics (wrong results), never planned
+int cfg_bm(int c) { return c <= 1 || c >= 5 ? 256 : c == 2 || c == 4 ? 128 : 64; }
+int cfg_bn(int c) { return c == 5 ? 256 : c <= 1 || c == 4 || c >= 6 ? 192 : c == 2 ? 96 : 64; }
+int cfg_nwm(int c) { return c == 0 || c == 9 ? 8 : c == 1 || c >= 5 ? 4 : c == 2 ? 4 : 2; }
 
-template <int BM, int BN, int WM, int WN, int EPI, int WGS, int NS, int AT = 0, int OB = 0>
+template <int BM, int BN, int WM, int WN, int EPI, int WGS, int NS, int AT = 0, int OB = 0, int DIL = 1>
 void launch_one(const F16Args& a, hipStream_t s) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int total = ((a.M + BM - 1) / BM) * (a.N / BN) * a.ks;
@@ -594,17 +650,24 @@ void launch_one(const F16Args& a, hipStream_t s) {
   const size_t smem = (size_t)NS * (BM + BN) * 64 + (2 * BM + BN + NT / 64) * 4 + 1024;   // + junk DMA KiB
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_f16_k<BM, BN, WM, WN, EPI, WGS, NS, AT, OB>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_f16_k<BM, BN, WM, WN, EPI, WGS, NS, AT, OB, DIL>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
-  gemm_f16_k<BM, BN, WM, WN, EPI, WGS, NS, AT, OB><<<8 * per, NT, smem, s>>>(a);
+  gemm_f16_k<BM, BN, WM, WN, EPI, WGS, NS, AT, OB, DIL><<<8 * per, NT, smem, s>>>(a);
 }
 
 template <int EPI, int AT = 0, int OB = 0>
 void launch_cfg(int cfg, const F16Args& a, hipStream_t s) {
   if (cfg == 0) launch_one<256, 192, 32, 192, EPI, 1, 4, AT, OB>(a, s);
   else if (cfg == 1) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB>(a, s);
+  else if (cfg == 6) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 0>(a, s);
+  else if (cfg == 7) launch_one<256, 192, 64, 96, EPI, 1, 5, AT, OB>(a, s);
+  else if (cfg == 8) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 2>(a, s);   // cfg 1, late split pairs
+  else if (cfg == 9) launch_one<256, 192, 32, 192, EPI, 1, 4, AT, OB, 2>(a, s);  // cfg 0, late split pairs
+  else if (cfg == 10) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 10>(a, s);  // DIAGNOSTIC: no split
+  else if (cfg == 11) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 11>(a, s);  // DIAGNOSTIC: no split / DMA
+  else if (cfg == 12) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 12>(a, s);  // DIAGNOSTIC: + no barrier
   else if (cfg == 2) launch_one<128, 96, 32, 96, EPI, 2, 4, AT, OB>(a, s);
   else if (cfg == 4) launch_one<128, 192, 64, 96, EPI, 2, 3, AT, OB>(a, s);
   else if (cfg == 5) launch_one<256, 256, 64, 128, EPI, 1, 4, AT, OB>(a, s);
@@ -1044,7 +1107,7 @@ int hx_gemm_f16_plan(int M, int N, int K) {
   }
   // deep reductions (the MLM decoder's data gradient, K = 30720) on the large tile whatever M: split-K
   // slabs fill the CUs, and the big tile halves the operand re-reads of the 128 x 96 one
-  if ((M >= 8192 || K >= 8192) && N % 192 == 0) return 0;
+  if ((M >= 8192 || K >= 8192) && N % 192 == 0) return 1;
   if (M >= 1024 && N % 96 == 0) return 2;
   if (N % 64 == 0) return 3;
   return -1;
@@ -1057,8 +1120,7 @@ int hx_gemm_f16_plan(int M, int N, int K) {
 // 36.61 vs 36.65 ms/step forced to 256 x 192; bf16 19.48 with it on every N % 256 product vs 18.8
 // without), so it stays an explicit choice (HX_GEMM_F16_CFG=5)
 int hx_gemm_bf16_plan(int M, int N, int K) {
-  const int c = hx_gemm_f16_plan(M, N, K);
-  return c == 0 && !getenv("HX_GEMM_F16_CFG") ? 1 : c;
+  return hx_gemm_f16_plan(M, N, K);
 }
 
 int hx_gemm_f16_tiles(int M, int N, int cfg) {

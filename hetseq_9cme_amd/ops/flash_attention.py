@@ -77,10 +77,12 @@ class _AttnFn(torch.autograd.Function):
         # the context's max |x| per (row, head) -- the attention-output GEMM's per-row scale
         ctx.split = qkv.dtype == torch.float32 and fp32_mode.attention_split(qkv.reshape(-1, qkv.shape[-1]))
         if ctx.split:
-            B, S = qkv.shape[0], qkv.shape[1]
+            B, S, H = qkv.shape[0], qkv.shape[1], qkv.shape[2] // 3
             am = torch.empty(B * S, num_heads, dtype=torch.float32, device=qkv.device)
-            out, lse, dmask = C().attn_fwd_f16(qkv, mask_bias, num_heads, keep, seed, stream, bias, am)
-            gemm16.attach(out, am)
+            cm = torch.empty(B * ((S + 127) // 128), H, dtype=torch.float32, device=qkv.device)
+            out, lse, dmask = C().attn_fwd_f16(qkv, mask_bias, num_heads, keep, seed, stream, bias, am, cm)
+            # per-row (output projection) and per-column (its weight gradient) max |context|
+            gemm16.attach_cols(gemm16.attach(out, am), cm if cm.shape[0] <= 256 else None)
         else:
             out, lse, dmask = C().attn_fwd(qkv, mask_bias, num_heads, keep, seed, stream, bias)
         ctx.save_for_backward(qkv, mask_bias, out, lse, dmask)
@@ -103,11 +105,15 @@ class _AttnFn(torch.autograd.Function):
         if ctx.split:
             # one key block (S <= 128): the kernel writes max |dQKV| per (row, head) -- the QKV
             # projection's per-row operand scale
+            one = qkv.shape[1] <= 128
             am = torch.empty(qkv.shape[0] * qkv.shape[1], num_heads, dtype=torch.float32, device=qkv.device) \
-                if qkv.shape[1] <= 128 else None
+                if one else None
+            cm = torch.empty(qkv.shape[0], qkv.shape[2], dtype=torch.float32, device=qkv.device) \
+                if one and qkv.shape[0] <= 256 else None
             dqkv, dbias = C().attn_bwd_f16(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep,
-                                           ctx.bias, *slots, am)
-            gemm16.attach(dqkv, am)
+                                           ctx.bias, *slots, am, cm)
+            # per-row (QKV data gradient) and per-column (QKV weight gradient) max |dQKV|
+            gemm16.attach_cols(gemm16.attach(dqkv, am), cm)
         else:
             dqkv, dbias = C().attn_bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep, ctx.bias,
                                        *slots)

@@ -206,6 +206,8 @@ class _EmbedLNFn(torch.autograd.Function):
         out, z, mean, rstd = C().embed_ln_fwd(ids, tt, wte, wpe, wtt, gamma, beta, eps, keep, seed, stream,
                                               out_bf16, am)
         gemm16.attach(out, am)   # fp16x3: its max |x| partials for the first layer's QKV GEMM
+        if am is not None:       # and the column bound of LN (+ dropout) for its weight gradient
+            gemm16.attach_cols(out, gemm16.ln_affine(gamma, beta, keep))
         ctx.save_for_backward(ids, tt if tt is not None else torch.Tensor(), z, mean, rstd, gamma)
         ctx.params = (wte, wpe, wtt, beta)
         ctx.has_tt = tt is not None
@@ -290,6 +292,8 @@ class _BiasDropResLNFn(torch.autograd.Function):
         am = _amax_buf(y.numel() // y.shape[-1], y, y.dtype != torch.float32)
         out, z, mean, rstd = C().ln_fwd(y, bias, res, gamma, beta, eps, keep, seed, stream, False, True, am)
         gemm16.attach(out, am)   # fp16x3: its max |x| partials for the next QKV / FFN-up GEMM
+        if am is not None:       # and its column bound for their weight gradients
+            gemm16.attach_cols(out, gemm16.ln_affine(gamma, beta))
         ctx.save_for_backward(z, mean, rstd, gamma)
         ctx.params = (bias, beta)
         ctx.mbox = mbox
@@ -303,10 +307,12 @@ class _BiasDropResLNFn(torch.autograd.Function):
         bias, beta = ctx.params
         need_dy = has_bias or keep < 1.0
         am = _amax_buf(z.numel() // z.shape[-1], z, z.dtype != torch.float32, bwd=True)
+        cm = torch.empty(1, z.shape[-1], dtype=torch.float32, device=z.device) if am is not None else None
         dz, dy, dgamma, dbeta, dbias = C().ln_bwd(dout.contiguous(), z, mean, rstd, gamma, keep, seed, stream,
                                                   False, need_dy, has_bias, grad_slot(gamma), grad_slot(beta),
-                                                  grad_slot(bias) if has_bias else None, am)
-        dy_ret = gemm16.attach(dy if need_dy else dz, am)   # fp16x3: max |dy| partials
+                                                  grad_slot(bias) if has_bias else None, am, cm)
+        # fp16x3: max |dy| per row (data gradient) and per column (weight gradient)
+        dy_ret = gemm16.attach_cols(gemm16.attach(dy if need_dy else dz, am), cm)
         dres = dz if has_res else None
         # dz is a private buffer only when dy is separate: then it can become the
         # accumulator of the consumer linear's dgrad GEMM
@@ -405,6 +411,7 @@ class _LinearFn(torch.autograd.Function):
         if ctx.f16:   # fp32 operands split inside the GEMM kernels
             x2 = gemm16.rows2(x)
             ctx.xparts = gemm16.amax(x, x2)
+            ctx.xcols = gemm16.cols_peek(x)
             y, wt, ctx.wparts = gemm16.linear(x2, ctx.xparts, W, b)
             ctx.save_for_backward(x2, wt)
             return y.view(*x.shape[:-1], y.shape[-1])
@@ -466,11 +473,13 @@ def _linear_backward_f16(ctx, dy):
     W, b = ctx.W, ctx.b
     dy2 = gemm16.rows2(dy)
     dparts = gemm16.amax(dy, dy2)
+    dcols = gemm16.cols(dy, dy2)
+    xcols = ctx.xcols if ctx.xcols is not None else gemm16.cols(x2, x2)
     dx = _f16_dgrad(dy2, dparts, wt, ctx.wparts, ctx.xshape, ctx.mbox) if ctx.needs_input_grad[0] else None
     slot = grad_slot(W)
     side = side_begin(dy2.device, True) if slot is not None else None
     with torch.cuda.stream(side) if side is not None else _nullctx():
-        dW = gemm16.wgrad(dy2, dparts, x2, ctx.xparts, W.shape[0], W.shape[1], slot)
+        dW = gemm16.wgrad(dy2, dcols, x2, xcols, W.shape[0], W.shape[1], slot)
         db = None
         if b is not None:
             db = C().colsum(dy2, None, grad_slot(b)) if dy2.shape[-1] % 4 == 0 else dy2.sum(0)
@@ -500,6 +509,7 @@ class _FFNFn(torch.autograd.Function):
     def forward(ctx, x, W1, b1, W2, mbox):
         x2 = gemm16.rows2(x)
         xparts = gemm16.amax(x, x2)
+        ctx.xcols = gemm16.cols_peek(x)
         d, h, hparts, hcols, w1t, p1 = gemm16.gemm_gelu(x2, xparts, W1, b1)
         y2, w2t, p2 = gemm16.linear(h, hparts, W2)
         ctx.save_for_backward(x2, d, h, w1t, w2t)
@@ -519,22 +529,24 @@ def _ffn_backward_f16(ctx, dy):
     W1, W2 = ctx.W
     dy2 = gemm16.rows2(dy)
     dparts = gemm16.amax(dy, dy2)
+    dcols = gemm16.cols(dy, dy2)
     slot2, slot1 = grad_slot(W2), grad_slot(W1)
     # each weight gradient on the side stream, beside the next data-gradient GEMM
     side = side_begin(dy2.device, True) if slot2 is not None and slot1 is not None else None
     with torch.cuda.stream(side) if side is not None else _nullctx():
-        dW2 = gemm16.wgrad(dy2, dparts, h, hparts, W2.shape[0], W2.shape[1], slot2)
+        dW2 = gemm16.wgrad(dy2, dcols, h, ctx.hcols, W2.shape[0], W2.shape[1], slot2)
     if side is not None:
-        for t in (dy2, dparts, h, hparts):
+        for t in (dy2, dparts, h, hparts, ctx.hcols):
             t.record_stream(side)
     # GELU backward in the FFN-down data-gradient epilogue: t = (dy W2) * gelu'(u), d b1
     t, tparts, tcols, db1 = gemm16.gemm_dgelu(dy2, dparts, w2t, p2, d, grad_slot(ctx.b1))
     if side is not None:
         side = side_begin(dy2.device, True)   # after t
+    xcols = ctx.xcols if ctx.xcols is not None else gemm16.cols(x2, x2)
     with torch.cuda.stream(side) if side is not None else _nullctx():
-        dW1 = gemm16.wgrad(t, tparts, x2, xparts, W1.shape[0], W1.shape[1], slot1)
+        dW1 = gemm16.wgrad(t, tcols, x2, xcols, W1.shape[0], W1.shape[1], slot1)
     if side is not None:
-        for q in (t, tparts, x2, xparts):
+        for q in (t, tparts, tcols, x2, xparts):
             q.record_stream(side)
     dx = _f16_dgrad(t, tparts, w1t, p1, ctx.xshape, ctx.mbox)
     return dx, dW1, db1, dW2, None
@@ -652,6 +664,7 @@ class _Linear3Fn(torch.autograd.Function):
         if ctx.f16:   # fp32 runs: the fp16x3 GEMM
             x2 = gemm16.rows2(x)
             ctx.xparts = gemm16.amax(x, x2)
+            ctx.xcols = gemm16.cols_peek(x)
             y, wt, ctx.wparts = gemm16.linear(x2, ctx.xparts, W, b)
             ctx.save_for_backward(x2, wt)
             return y.view(*x.shape[:-1], y.shape[-1])
@@ -681,8 +694,10 @@ class _Linear3Fn(torch.autograd.Function):
             # W holds W^T's fp16 pieces here; dx after the side-stream weight gradient is queued
             dy2 = gemm16.rows2(dy)
             dys = gemm16.amax(dy, dy2)
+            dcols = gemm16.cols(dy, dy2)
+            xcols = ctx.xcols if ctx.xcols is not None else gemm16.cols(x2, x2)
             dx = None
-            wg = lambda slot: gemm16.wgrad(dy2, dys, x2, ctx.xparts, n_out, n_in, slot)
+            wg = lambda slot: gemm16.wgrad(dy2, dcols, x2, xcols, n_out, n_in, slot)
         else:
             dy2 = dy.reshape(-1, dy.shape[-1])
             dys = None
@@ -840,7 +855,9 @@ def _decoder_backward_f16(ctx, g):
     dh = gemm16.mm(dl_full, one, wt, wparts, ks=0).mul_(scale)
     hs = h * scale.to(h.dtype)
     slot = grad_slot(Wt)
-    dW = gemm16.wgrad(dl_full, one, hs, gemm16.amax(hs, hs), V, h.shape[1], slot)
+    # per-column scales: dl's columns are the vocabulary (rare words' probabilities sit far below
+    # the tensor's max), hs's the hidden features -- one column-max pass each
+    dW = gemm16.wgrad(dl_full, gemm16.cols(dl_full, dl_full), hs, gemm16.cols(hs, hs), V, h.shape[1], slot)
     return dh, dW, dbias, None
 
 

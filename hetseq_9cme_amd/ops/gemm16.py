@@ -80,6 +80,41 @@ def amax(t, t2=None):
     return attach(t, C().amax_rows(x2))._hx_amax
 
 
+def attach_cols(t, src):
+    """Hand the weight gradients that consume ``t`` its per-COLUMN scale source: a [P, C] tensor of
+    column-max partials (producer-written), or ``('affine', gamma, beta, z, mul)`` for a LayerNorm
+    output gamma zhat + beta (|column c| <= (|gamma_c| z + |beta_c|) mul, z = sqrt(H - 1) bounds
+    |zhat| of any normalised row)."""
+    if src is not None:
+        t._hx_cmax = src
+        t._hx_cmax_ver = t._version
+    return t
+
+
+def cols(t, t2=None):
+    """``t``'s per-column scale source: the producer's (if ``t`` has not changed since), else one
+    column-max read pass ([1, C])."""
+    c = getattr(t, '_hx_cmax', None)
+    if c is not None and getattr(t, '_hx_cmax_ver', -1) == t._version:
+        return c
+    x2 = t2 if t2 is not None else rows2(t)
+    if not (x2.shape[-1] % 4 == 0 and _aligned(x2)):
+        x2 = x2.contiguous()
+    return attach_cols(t, C().amax_cols(x2))._hx_cmax
+
+
+def cols_peek(t):
+    """The producer-attached column scale source of ``t`` (None if there is none / it is stale)."""
+    c = getattr(t, '_hx_cmax', None)
+    return c if c is not None and getattr(t, '_hx_cmax_ver', -1) == t._version else None
+
+
+def ln_affine(gamma, beta, keep=1.0):
+    """The column scale source of a LayerNorm output (``attach_cols``)."""
+    H = gamma.numel()
+    return ('affine', gamma.detach(), beta.detach(), float(max(H - 1, 1)) ** 0.5, 1.0 / keep)
+
+
 _ONES = {}
 
 
@@ -152,17 +187,16 @@ def dgrad(dy2, dparts, wt, wt_parts, acc=None):
     return mm(dy2, dparts, wt, wt_parts)
 
 
-def _tensor_bound(p):
-    """A per-tensor max |x| bound from any partials (the weight gradient's operand scale)."""
-    return p if p.dim() == 1 and p.numel() <= 4096 else p.amax().reshape(1)
-
-
-def wgrad(dy2, dparts, x2, xparts, n_out, n_in, slot=None):
+def wgrad(dy2, dcols, x2, xcols, n_out, n_in, slot=None):
     """dW [n_out, n_in] = dy2^T x2 over the token rows, straight into ``slot`` when given
-    (shapes without a tile: the library fp32 product)."""
+    (shapes without a tile: the library fp32 product).  ``dcols`` / ``xcols``: the operands' column
+    scale sources (``cols``): dW's rows are scaled by dy2's column maxima, its columns by x2's."""
     out = slot if slot is not None else torch.empty(n_out, n_in, device=dy2.device)
     if wgrad_ok(dy2.shape[1], n_in) and dy2.shape[1] >= n_out and _aligned(dy2) and _aligned(x2):
-        return C().wgrad_f16(dy2, _tensor_bound(dparts), x2, _tensor_bound(xparts), out)
+        if isinstance(xcols, tuple):   # ('affine', gamma, beta, z, mul)
+            _, g, b, z, mul = xcols
+            return C().wgrad_f16(dy2, dcols, x2, bound(x2.device), out, x_gamma=g, x_beta=b, x_z=z, x_mul=mul)
+        return C().wgrad_f16(dy2, dcols, x2, xcols, out)
     return torch.mm(dy2[:, :n_out].t(), x2, out=out)
 
 

@@ -72,24 +72,13 @@ def test_mode_switch_and_option():
         fp32_mode.set_fp32_gemm(prev)
 
 
-def test_attention_mode_option():
-    """--fp32-attention: fp16x3 by default, x6 selectable, anything else refused."""
+def test_attention_switch_removed():
+    """--fp32-attention is gone (round 5: the x6 attention was deleted; fp32 attention runs on the
+    fp16x3 kernels under --fp32-gemm fp16x3, on f32 MFMA under native)."""
     from hetseq_9cme_amd import options
-    args = options.parse_training_args(['--task', 'mnist', '--data', '/tmp'])
-    assert args.fp32_attention == 'fp16x3'
-    args = options.parse_training_args(['--task', 'mnist', '--data', '/tmp', '--fp32-attention', 'x6'])
-    assert args.fp32_attention == 'x6'
     with pytest.raises(SystemExit):
-        options.parse_training_args(['--task', 'mnist', '--data', '/tmp', '--fp32-attention', 'bf16'])
-    with pytest.raises(ValueError):
-        fp32_mode.set_fp32_attention('fp32')
-    prev = fp32_mode.fp32_attention_mode()
-    try:
-        fp32_mode.set_fp32_attention('x6')
-        assert fp32_mode.fp32_attention_mode() == 'x6'
-    finally:
-        fp32_mode.set_fp32_attention(prev)
-    assert fp32_mode.fp32_attention_mode() == 'fp16x3'
+        options.parse_training_args(['--task', 'mnist', '--data', '/tmp', '--fp32-attention', 'x6'])
+    assert not hasattr(fp32_mode, 'set_fp32_attention')
 
 
 # (tokens, [(n_out, n_in)]) of every BERT-base GEMM the BASELINE configs run

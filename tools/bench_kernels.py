@@ -62,10 +62,10 @@ def bench_attn(B, S, nh=12, keep=0.9, dtype=torch.float32):
     out1, lse1, dm1 = C().attn_fwd(qkv, mb, nh, 1.0, SEED, 0, None)
     report('attn_bwd (no dropout)', timeit(lambda: C().attn_bwd(dout, qkv, mb, out1, lse1, dm1, nh, 1.0, None, None, None, None)[0]),
            flops=2.5 * f_fwd)
-    if dtype == torch.float32:   # fp32 on the bf16 matrix cores (split pieces, attention_x6.hip)
-        report('attn_fwd_x6', timeit(lambda: C().attn_fwd_x6(qkv, mb, nh, keep, SEED, 0, None)), flops=f_fwd)
-        report('attn_bwd_x6', timeit(lambda: C().attn_bwd_x6(dout, qkv, mb, out, lse, dm, nh, keep, None, None, None,
-                                                              None)[0]), flops=2.5 * f_fwd)
+    if dtype == torch.float32:   # fp32 on the fp16 matrix cores (fp16x3 pieces, attention_f16.hip)
+        report('attn_fwd_f16', timeit(lambda: C().attn_fwd_f16(qkv, mb, nh, keep, SEED, 0, None)), flops=f_fwd)
+        report('attn_bwd_f16', timeit(lambda: C().attn_bwd_f16(dout, qkv, mb, out, lse, dm, nh, keep, None, None, None,
+                                                                None)[0]), flops=2.5 * f_fwd)
 
 
 def bench_ln(B, S, H=768):

@@ -60,9 +60,9 @@ def child(a):
             '--warmup-updates', str(a.warmup_updates), '--weight-decay', '0.01',
             '--total-num-update', str(max(10 * a.updates, 1000)), '--clip-norm', '25', '--num-workers', '2',
             '--log-format', 'none', '--disable-validation', '--no-save', '--distributed-world-size', '1']
-    # mode = GEMM mode [':' attention mode] ['#' repeat], e.g. 'fp16x3:x6'
-    gemm_mode, _, attn_mode = a.child.split('#')[0].partition(':')
-    argv += ['--fp32-gemm', gemm_mode] + (['--fp32-attention', attn_mode] if attn_mode else [])
+    # mode = GEMM mode ['#' repeat], e.g. 'fp16x3#2'
+    gemm_mode = a.child.split('#')[0]
+    argv += ['--fp32-gemm', gemm_mode]
     args = options.parse_training_args(argv)
     args.device_id = 0
     args.distributed_rank = 0

@@ -1,5 +1,5 @@
-"""Attention kernels (backward, and forward timings) side by side at the BERT-base shapes: the bf16 x6 kernel
-(attention_x6.hip), the fp16x3 kernel (attention_f16.hip) and the fp32-MFMA kernel -- time per
+"""Attention kernels (backward, and forward timings) side by side at the BERT-base shapes: the fp16x3
+kernel (attention_f16.hip) and the fp32-MFMA kernel (attention.hip) -- time per
 call (HIP events over back-to-back launches) and the worst-row error of dQ / dK / dV against an
 fp64 reference on a small slice.  ``python tools/probe/attn_bwd_probe.py``."""
 import os
@@ -39,10 +39,10 @@ def main():
         dout = torch.randn(B, S, H, device=dev)
         slots = [torch.empty(H, device=dev) for _ in range(3)]
         res = {}
-        for name, f in (('x6', C().attn_bwd_x6), ('f16', C().attn_bwd_f16), ('fp32', C().attn_bwd)):
+        for name, f in (('f16', C().attn_bwd_f16), ('fp32', C().attn_bwd)):
             res[name] = timed(lambda: f(dout, qkv, mb, out, lse, dm, nh, keep, bias, *slots))
         fw = {}
-        for name, f in (('x6', C().attn_fwd_x6), ('f16', C().attn_fwd_f16), ('fp32', C().attn_fwd)):
+        for name, f in (('f16', C().attn_fwd_f16), ('fp32', C().attn_fwd)):
             fw[name] = timed(lambda: f(qkv, mb, nh, keep, seed, 3, bias))
         print('B={} S={} forward: '.format(B, S) + ', '.join('{} {:.1f} us'.format(k, v) for k, v in fw.items()),
               flush=True)
@@ -61,7 +61,7 @@ def main():
     p = torch.softmax(q[0] @ q[1].transpose(-1, -2) / 8.0, -1)
     (p @ q[2]).permute(0, 2, 1, 3).reshape(B, S, H).backward(dout.double())
     gref = x.grad.view(B, S, 3, nh, d)
-    for name, f in (('x6', C().attn_bwd_x6), ('f16', C().attn_bwd_f16), ('fp32', C().attn_bwd)):
+    for name, f in (('f16', C().attn_bwd_f16), ('fp32', C().attn_bwd)):
         g = f(dout, qkv, mb, out, lse, dm, nh, 1.0, None, None, None, None)[0].double().view(B, S, 3, nh, d)
         e = ((g - gref).abs().amax(-1) / gref.abs().amax(-1)).amax((0, 1, 3))
         print('{:5s} worst-row rel err dQ {:.2e} dK {:.2e} dV {:.2e}'.format(name, *e.tolist()), flush=True)

@@ -7,8 +7,8 @@
 //
 // Every product runs as three fp16 MFMA passes over scaled two-piece operands (the GEMMs' fp16x3
 // class, hx_gemm.h): x = 2^-E (h0 + h1), h0 = fp16(2^E x), h1 = fp16(2^E x - h0), the product
-// a.b = a0 b0 + a0 b1 + a1 b0 -- half the MFMA passes of the bf16 x6 kernel (attention_x6.hip),
-// two LDS images per operand instead of three.  The scale exponents are powers of two chosen so
+// a.b = a0 b0 + a0 b1 + a1 b0 -- half the MFMA passes of a three-piece bf16 split (the round-4
+// x6 kernels, deleted in round 5), two LDS images per operand instead of three.  The scale exponents are powers of two chosen so
 // the largest magnitude of an operand lands below 2^15:
 //   K, V      one exponent per workgroup (its 128 keys), fixed for the kernel;
 //   Q, dO     one running exponent per workgroup: each 32-query tile's max |x| is reduced over the
@@ -651,7 +651,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
 }
 
 // ============================================================================ forward
-// The x6 forward's structure (attention_x6.hip) with two fp16 pieces and three passes per product:
+// Two fp16 pieces and three passes per product:
 // one workgroup = 4 waves x 32 queries ON THE LANES, 64-key tiles, keys on the accumulator rows
 // (S^T = K . Q^T with Q's piece fragments in VGPRs), K staged as piece images [key][dim], V as
 // transposed piece images [dim][vpos(key)] so O^T += V^T . P^T takes P's pieces straight from the

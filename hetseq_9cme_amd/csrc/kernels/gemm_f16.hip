@@ -70,6 +70,17 @@ __device__ __forceinline__ void split_pair_mix(float x0, float x1, float s, uint
       : "v"(x0), "v"(x1), "v"(s));
 }
 
+// the same with one scale per value (the weight gradient's per-column scales)
+__device__ __forceinline__ void split_pair_mix2(float x0, float x1, float s0, float s1, uint32_t& h0, uint32_t& h1) {
+  asm volatile(
+      "v_fma_mixlo_f16 %0, %2, %4, 0 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %3, %5, 0 op_sel_hi:[0,0,0]\n\t"
+      "v_fma_mixlo_f16 %1, %2, %4, -%0 op_sel_hi:[0,0,1]\n\t"
+      "v_fma_mixhi_f16 %1, %3, %5, -%0 op_sel:[0,0,1] op_sel_hi:[0,0,1]"
+      : "=&v"(h0), "=&v"(h1)
+      : "v"(x0), "v"(x1), "v"(s0), "v"(s1));
+}
+
 struct F16Args {
   const void* A;   // fp32 (AT 0) or bf16 (AT 1)
   int64_t lda;
@@ -93,6 +104,7 @@ struct F16Args {
   int dmode;        // EPI 1: C gets gelu'(u) (1) or u (0); EPI 2: aux holds gelu'(u) (1) or u (0)
   int ks;           // split-K slabs (EPI 0 only): slab z reduces k steps [z, z + 1) K / ks into C + z c_zs
   int64_t c_zs;
+  int diag;         // timing diagnostics (HX_GEMM_DIAG, wrong results): 1 no epilogue, 2 no k loop
 };
 
 // max |x| of `rows` operand rows starting at r0 from their partials -> scale tables (2^E, 2^-E);
@@ -157,7 +169,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
   const int z = work0 / total, work = work0 - z * total;
   const int nt = work % TN, mt = work / TN;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int nit = g.K / KD / g.ks, it0 = z * nit;
+  const int nit = (g.diag & 2) ? 0 : g.K / KD / g.ks, it0 = z * (g.K / KD / g.ks);
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w % NWM, wn = w / NWM, h = lane >> 5, l32 = lane & 31;
@@ -180,11 +192,6 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
       const int q = wv + NW * j;
       if (q < KA) voff[j] = (uint32_t)(((int64_t)(q * 16 + rl) * g.lda + (16 / AE) * ch) * AE);
       else voff[j] = (uint32_t)(((int64_t)((q - KA) * 16 + rl) * g.ldb + 8 * ch) * 2);
-      if constexpr (DIL == 9) {   // DIAGNOSTIC (timing only, wrong image): 8 rows x 128 B per piece
-        const int r8 = lane >> 3, c8 = lane & 7;
-        if (q < KA) voff[j] = (uint32_t)(((int64_t)(q * 8 + r8) * g.lda) * AE + 16 * c8);
-        else voff[j] = (uint32_t)(((int64_t)((q - KA) * 8 + r8) * g.ldb) * 2 + 16 * c8);
-      }
       dbase[j] = q < PTOT ? 1024u * q : (uint32_t)JUNK;
       dslot[j] = q < PTOT ? 1u : 0u;
       if (q >= PTOT) voff[j] = 0x40000000u;   // + any k offset stays past the buffer, never wraps
@@ -199,9 +206,6 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
     dma16(q < KA ? ra : rb, lds0 + dbase[j] + dslot[j] * st, voff[j] + ko);
   };
   auto dma = [&](int it) {   // every piece of stage it into its ring slot
-    if constexpr (DIL == 8 || DIL >= 11) {   // DIAGNOSTIC (timing only, stale data): no DMA after the prologue
-      if (it >= NS - 1) return;
-    }
 #pragma unroll
     for (int j = 0; j < JHI; ++j) dma_one(it, j);
   };
@@ -257,7 +261,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
       }
     };
     auto split_a = [&](const f32x4 (&raw)[MB][2], Fr& F) {
-      if constexpr (DIL >= 10) {   // DIAGNOSTIC (timing only): no split VALU
+      if constexpr (DIL == 10) {   // DIAGNOSTIC (timing only): no split VALU
 #pragma unroll
         for (int a = 0; a < MB; ++a) {
           F.a0[a] = __builtin_bit_cast(f16x8, raw[a][0]);
@@ -304,7 +308,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
       __builtin_amdgcn_sched_barrier(0);
       dma(it + NS - 1);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (DIL >= 10 || 4 * MB > 2 * MB * NB) {   // small wave tiles / DIL diag: compiler split
+      if constexpr (DIL == 10 || 4 * MB > 2 * MB * NB) {   // small wave tiles / DIL diag: compiler split
         pass(Fc, 1);
         split_a(raw, Fn);
         pass(Fc, 2);
@@ -331,7 +335,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
       // stage it + 2 landed on this wave's side (stage it + NS - 1 stays in flight), then the
       // barrier publishes it to every wave and frees stage it's slot for the DMA of step it + 1
       wait_ring();
-      if constexpr (DIL != 12) raw_barrier();   // (12: the no-barrier timing diagnostic)
+      raw_barrier();
     };
     Fr F0, F1;
     {
@@ -382,10 +386,8 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
         dma_one(it + NS - 1, j);
         __builtin_amdgcn_sched_barrier(0);
       }
-      if constexpr (DIL != 8) {   // (8: the no-DMA timing diagnostic)
 #pragma unroll
-        for (int j = NI; j < JHI; ++j) dma_one(it + NS - 1, j);
-      }
+      for (int j = NI; j < JHI; ++j) dma_one(it + NS - 1, j);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = NI; i < MB * NB; ++i) mma(Fc, 1, i);
@@ -402,7 +404,13 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
   }
   // every wave is past its last fragment read before the ring is reused below
   __syncthreads();
+  if (g.diag & 1) return;
 
+  // output store cache policy: the GELU epilogues' two outputs (2 x 201 MB at the FFN shapes) go
+  // non-temporal -- r5m: FFN up 326 -> 305 us, FFN-down dgrad 294 -> 285 us; the plain / beta
+  // epilogues' outputs are read by the next kernel at once and stay cached (A/B: cfg 11 all
+  // non-temporal, cfg 12 sc0 sc1)
+  constexpr int SP = DIL == 21 ? 2 : DIL == 22 ? 17 : (EPI == 1 || EPI == 2) ? 2 : 0;
   // ---- epilogue: quad transpose, then lane (l32 & 3) owns row 8 gq + 4 h + (l32 & 3) of each
   // 32 x 32 block and its columns (l32 & ~3) .. + 3; stores past M dropped by the descriptor
   const int mrow = wm * WM + 4 * h + (l32 & 3), ncol = wn * WN + (l32 & ~3);
@@ -452,7 +460,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
           }
           const uint2 pk = make_uint2(hx::f2bf(o[0]) | ((uint32_t)hx::f2bf(o[1]) << 16),
                                       hx::f2bf(o[2]) | ((uint32_t)hx::f2bf(o[3]) << 16));
-          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, pk), obuf.r, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, pk), obuf.r, off, 0, SP);
         }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -468,7 +476,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
           f32x4 o = {v[0] + bias[b][0], v[1] + bias[b][1], v[2] + bias[b][2], v[3] + bias[b][3]};
           if constexpr (EPI == 3)
             o += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(cbuf.r, coff(a, b, gq), 0, 0));
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), cbuf.r, coff(a, b, gq), 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), cbuf.r, coff(a, b, gq), 0, SP);
         }
       __builtin_amdgcn_sched_barrier(0);
     }
@@ -484,9 +492,9 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
       if constexpr (OB == 1) {
         const uint2 pk = make_uint2(hx::f2bf(v[0]) | ((uint32_t)hx::f2bf(v[1]) << 16),
                                     hx::f2bf(v[2]) | ((uint32_t)hx::f2bf(v[3]) << 16));
-        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, pk), bf.r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, pk), bf.r, off, 0, SP);
       } else {
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), bf.r, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), bf.r, off, 0, SP);
       }
     };
     float csum[NB][4], cmx[NB][4], rmx[MB][4];
@@ -666,8 +674,8 @@ void launch_cfg(int cfg, const F16Args& a, hipStream_t s) {
   else if (cfg == 8) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 2>(a, s);   // cfg 1, late split pairs
   else if (cfg == 9) launch_one<256, 192, 32, 192, EPI, 1, 4, AT, OB, 2>(a, s);  // cfg 0, late split pairs
   else if (cfg == 10) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 10>(a, s);  // DIAGNOSTIC: no split
-  else if (cfg == 11) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 11>(a, s);  // DIAGNOSTIC: no split / DMA
-  else if (cfg == 12) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 12>(a, s);  // DIAGNOSTIC: + no barrier
+  else if (cfg == 11) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 21>(a, s);  // cfg 6, non-temporal stores
+  else if (cfg == 12) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 22>(a, s);  // cfg 6, sc0 sc1 stores
   else if (cfg == 2) launch_one<128, 96, 32, 96, EPI, 2, 4, AT, OB>(a, s);
   else if (cfg == 4) launch_one<128, 192, 64, 96, EPI, 2, 3, AT, OB>(a, s);
   else if (cfg == 5) launch_one<256, 256, 64, 128, EPI, 1, 4, AT, OB>(a, s);
@@ -795,12 +803,15 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
 
   // two register stages: the fp32 tiles of step it + 2 are loaded while step it runs on the
   // matrix cores, so a load has a whole step of MFMA work (plus the split / LDS write of step
-  // it + 1) to land before it is split and written to LDS
+  // it + 1) to land before it is split and written to LDS.  Past the slab's end the loads are
+  // aimed past the buffer (zeros, no memory traffic): every step has the same shape, no branch.
   struct Regs {
     f32x4 a[CA][2], b[CB][2];
   };
   auto load = [&](int it, Regs& r) {
-    const uint32_t soa = (uint32_t)it * BKT * lda * 4, sob = (uint32_t)it * BKT * ldb * 4;
+    const bool in = it < nit;
+    const uint32_t soa = in ? (uint32_t)it * BKT * lda * 4 : 0x80000000u;
+    const uint32_t sob = in ? (uint32_t)it * BKT * ldb * 4 : 0x80000000u;
 #pragma unroll
     for (int i = 0; i < CA; ++i)
 #pragma unroll
@@ -812,25 +823,33 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
       for (int k = 0; k < 2; ++k)
         r.b[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(bbuf.r, vb[i] + 16 * k, sob, 0));
   };
-  auto store = [&](int buf, const Regs& r) {
+  // the split of one 8-column chunk (c < CA: of dY, else of X) as four v_fma_mix pairs, and its
+  // two LDS piece writes
+  constexpr int NCH = CA + CB;
+  auto split_pair = [&](const Regs& r, int c, int p, uint32_t (&h0)[4], uint32_t (&h1)[4]) {
+    const f32x4& v = c < CA ? r.a[c][p >> 1] : r.b[c - CA][p >> 1];
+    const f32x8& sc = c < CA ? csa[c] : csb[c - CA];
+    const int e = 2 * (p & 1);
+    split_pair_mix2(v[e], v[e + 1], sc[4 * (p >> 1) + e], sc[4 * (p >> 1) + e + 1], h0[p], h1[p]);
+  };
+  auto write_chunk = [&](int buf, int c, const uint32_t (&h0)[4], const uint32_t (&h1)[4]) {
     char* st = lds + buf * STAGE;
-#pragma unroll
-    for (int i = 0; i < CA; ++i) {
-      const f32x8 y = f32x8{r.a[i][0][0], r.a[i][0][1], r.a[i][0][2], r.a[i][0][3],
-                            r.a[i][1][0], r.a[i][1][1], r.a[i][1][2], r.a[i][1][3]} * csa[i];
-      f16x8 h0, h1;
-      split2(y, h0, h1);
-      *reinterpret_cast<f16x8*>(st + sa_[i]) = h0;
-      *reinterpret_cast<f16x8*>(st + A_T + sa_[i]) = h1;
+    const u32x4 v0 = {h0[0], h0[1], h0[2], h0[3]}, v1 = {h1[0], h1[1], h1[2], h1[3]};
+    if (c < CA) {
+      *reinterpret_cast<u32x4*>(st + sa_[c]) = v0;
+      *reinterpret_cast<u32x4*>(st + A_T + sa_[c]) = v1;
+    } else {
+      *reinterpret_cast<u32x4*>(st + 2 * A_T + sb_[c - CA]) = v0;
+      *reinterpret_cast<u32x4*>(st + 2 * A_T + B_T + sb_[c - CA]) = v1;
     }
+  };
+  auto store_all = [&](int buf, const Regs& r) {   // (the prologue's stage 0)
 #pragma unroll
-    for (int i = 0; i < CB; ++i) {
-      const f32x8 y = f32x8{r.b[i][0][0], r.b[i][0][1], r.b[i][0][2], r.b[i][0][3],
-                            r.b[i][1][0], r.b[i][1][1], r.b[i][1][2], r.b[i][1][3]} * csb[i];
-      f16x8 h0, h1;
-      split2(y, h0, h1);
-      *reinterpret_cast<f16x8*>(st + 2 * A_T + sb_[i]) = h0;
-      *reinterpret_cast<f16x8*>(st + 2 * A_T + B_T + sb_[i]) = h1;
+    for (int c = 0; c < NCH; ++c) {
+      uint32_t h0[4], h1[4];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) split_pair(r, c, p, h0, h1);
+      write_chunk(buf, c, h0, h1);
     }
   };
 
@@ -840,39 +859,55 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
 #pragma unroll
     for (int b = 0; b < NB; ++b) acc[a][b] = f32x16{0};
 
-  auto mma = [&](int buf) {
+  struct Fr {
+    f16x8 a0[MB], b0[NB], b1[NB];   // a0[a] holds piece 1 of A rows a during pass 2
+  };
+  // fragments of a stage; the second A pieces (a1, pass 2 only) are read one by one after the
+  // last pass-1 MFMA on the first piece of the same rows, into its registers (16 VGPRs fewer)
+  auto read = [&](int buf, Fr& F) {
     const char* st = lds + buf * STAGE;
-    f16x8 a0[MB], a1[MB], b0[NB], b1[NB];
-#pragma unroll
-    for (int a = 0; a < MB; ++a) {
-      a0[a] = tfrag<BM>(st, alo, ahi, wm * WM + 32 * a, a & 1);
-      a1[a] = tfrag<BM>(st + A_T, alo, ahi, wm * WM + 32 * a, a & 1);
-    }
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      b0[b] = tfrag<BN>(st + 2 * A_T, blo, bhi, wn * WN + 32 * b, b & 1);
-      b1[b] = tfrag<BN>(st + 2 * A_T + B_T, blo, bhi, wn * WN + 32 * b, b & 1);
+      F.b0[b] = tfrag<BN>(st + 2 * A_T, blo, bhi, wn * WN + 32 * b, b & 1);
+      F.b1[b] = tfrag<BN>(st + 2 * A_T + B_T, blo, bhi, wn * WN + 32 * b, b & 1);
     }
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
-#pragma unroll
-      for (int a = 0; a < MB; ++a)
-#pragma unroll
-        for (int b = 0; b < NB; ++b) acc[a][b] = mfma16(q == 2 ? a1[a] : a0[a], q == 1 ? b1[b] : b0[b], acc[a][b]);
+    for (int a = 0; a < MB; ++a) F.a0[a] = tfrag<BM>(st, alo, ahi, wm * WM + 32 * a, a & 1);
+  };
+  auto read_a1 = [&](int buf, Fr& F, int a) {
+    F.a0[a] = tfrag<BM>(lds + buf * STAGE + A_T, alo, ahi, wm * WM + 32 * a, a & 1);
+  };
+  constexpr int NMF = 3 * MB * NB;   // MFMAs per step
+  static_assert(4 * NCH <= NMF, "one split pair per MFMA");
+  auto mma = [&](const Fr& F, int i) {   // MFMA i: pass q = i / (MB NB)
+    const int q = i / (MB * NB), a = (i % (MB * NB)) / NB, b = i % NB;
+    acc[a][b] = mfma16(F.a0[a], q == 1 ? F.b1[b] : F.b0[b], acc[a][b]);
   };
 
-  // step it: load step it + 2 into the register set step it used, multiply LDS buffer it & 1,
-  // split and write step it + 1 (loaded a step ago) into the other buffer (last read before the
-  // previous barrier); the two register sets alternate (steps unrolled by two: no copies)
+  // step it: issue the loads of step it + 2 into the register set step it's data used, read
+  // stage it's fragments, then its MFMAs with the split of step it + 1 (loaded a step ago) placed
+  // pair by pair between them and its LDS pieces written into the other buffer (last read before
+  // the previous barrier); one barrier.  The two register sets alternate (steps unrolled by two).
   Regs r0, r1;
   load(0, r0);
-  if (nit > 1) load(1, r1);
-  store(0, r0);
+  load(1, r1);
+  store_all(0, r0);
   __syncthreads();
   auto step = [&](int it, Regs& mine, const Regs& next) {
-    if (it + 2 < nit) load(it + 2, mine);
-    mma(it & 1);
-    if (it + 1 < nit) store((it & 1) ^ 1, next);
+    load(it + 2, mine);
+    Fr F;
+    read(it & 1, F);
+    uint32_t h0[4], h1[4];
+#pragma unroll
+    for (int i = 0; i < NMF; ++i) {
+      mma(F, i);
+      if (i / (MB * NB) == 1 && i % NB == NB - 1) read_a1(it & 1, F, (i % (MB * NB)) / NB);
+      if (i < 4 * NCH) {
+        split_pair(next, i / 4, i % 4, h0, h1);
+        if (i % 4 == 3) write_chunk((it & 1) ^ 1, i / 4, h0, h1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
     __syncthreads();
   };
   for (int it = 0; it < nit; it += 2) {
@@ -1220,6 +1255,8 @@ int hx_gemm_f16(const HxGemmF16& p, int cfg, hipStream_t s) {
   a.dmode = p.dmode;
   a.ks = ks;
   a.c_zs = p.c_zs;
+  static const int diag = getenv("HX_GEMM_DIAG") ? atoi(getenv("HX_GEMM_DIAG")) : 0;
+  a.diag = diag;
   if (p.abf16) {
     if (p.kind == 1) launch_cfg<1, 1, 1>(cfg, a, s);        // bf16 FFN up: gelu'(u), gelu(u) in bf16
     else if (p.kind == 2) launch_cfg<2, 1, 1>(cfg, a, s);   // bf16 FFN-down dgrad * gelu'(u)

@@ -117,8 +117,14 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    t_data = t_step = 0.0
     for _ in range(a.steps):
-        ctrl.train_step(next(itr))
+        ta = time.perf_counter()
+        batch = next(itr)
+        tb = time.perf_counter()
+        ctrl.train_step(batch)
+        t_data += tb - ta
+        t_step += time.perf_counter() - tb
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -159,6 +165,8 @@ def main():
                           'graph_train_step': a.graph_train_step, 'force_reducer': a.force_reducer,
                           'fp32_gemm': args.fp32_gemm if a.precision == 'fp32' else None,
                           'graph_replays': gs.replays if gs is not None else 0,
+                          'host_ms': {'next_batch': round(t_data * 1e3 / a.steps, 3),
+                                      'train_step_call': round(t_step * 1e3 / a.steps, 3)},
                           'parallelism': 'dp{}'.format(world) + (' (find-unused-parameters)' if world > 1 else ''),
                           'data': 'synthetic CoNLL-format sentences (8-40 words), random-init BERT-{}'.format(
                               a.model)}), flush=True)

@@ -51,76 +51,58 @@ __global__ __launch_bounds__(kFoldNT) void fold_rows_k(const float* __restrict__
   }
 }
 
-// the same fold, 4 columns per lane: a block = 16 waves over 256 columns (float4 loads, four
-// independent accumulators per lane), so the few column blocks of a bias / LayerNorm gradient
-// each keep 16 x 4 loads in flight per row pass instead of one (the fold is latency-bound: ~12
-// blocks on 256 CUs).  Needs stride, ncols, seg and nsum multiples of 4 and a 16-B aligned base.
-constexpr int kFold4NT = 1024;
+// the same fold with more, narrower blocks: the fold is bound by how much one block can pull
+// (r5n: 12 blocks of 256 columns x 512 partial rows each reading 512 KB -> 12 us), so a block
+// takes 32 columns (8 lanes x float4) over 32 row slots (4 waves x 8), four loads in flight per
+// lane, and a [32][32] LDS combine.  Needs stride, ncols, seg and nsum multiples of 4 and a 16-B
+// aligned base.
+constexpr int kFold4NT = 256;
 __global__ __launch_bounds__(kFold4NT) void fold_rows4_k(const float* __restrict__ partial, int nrows, int64_t stride,
                                                        int ncols, int seg, float* __restrict__ out0,
                                                        float* __restrict__ out1, float* __restrict__ out2,
                                                        int accumulate, int nsum, float* __restrict__ outm) {
-  __shared__ float4 red[16][64];
+  __shared__ float4 red[32][8];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int c = (blockIdx.x * 64 + lane) * 4;
+  const int q = lane & 7, slot = w * 8 + (lane >> 3);   // column quad, row slot (0 .. 31)
+  const int c = blockIdx.x * 32 + 4 * q;
   const bool mx = c >= nsum;
+  auto acc = [&](float4& a, const float4& x) {
+    if (mx) {
+      a.x = fmaxf(a.x, x.x); a.y = fmaxf(a.y, x.y); a.z = fmaxf(a.z, x.z); a.w = fmaxf(a.w, x.w);
+    } else {
+      a.x += x.x; a.y += x.y; a.z += x.z; a.w += x.w;
+    }
+  };
   float4 a[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) a[j] = make_float4(0.f, 0.f, 0.f, 0.f);
   if (c < ncols) {
     const float* p = partial + c;
-    int r = w;
-    for (; r + 48 < nrows; r += 64) {
+    int r = slot;
+    for (; r + 96 < nrows; r += 128) {
+      float4 x[4];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float4 x = *reinterpret_cast<const float4*>(p + (int64_t)(r + 16 * j) * stride);
-        if (mx) {
-          a[j].x = fmaxf(a[j].x, x.x); a[j].y = fmaxf(a[j].y, x.y); a[j].z = fmaxf(a[j].z, x.z); a[j].w = fmaxf(a[j].w, x.w);
-        } else {
-          a[j].x += x.x; a[j].y += x.y; a[j].z += x.z; a[j].w += x.w;
-        }
-      }
+      for (int j = 0; j < 4; ++j) x[j] = *reinterpret_cast<const float4*>(p + (int64_t)(r + 32 * j) * stride);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc(a[j], x[j]);
     }
-    for (; r < nrows; r += 16) {
-      const float4 x = *reinterpret_cast<const float4*>(p + (int64_t)r * stride);
-      if (mx) {
-        a[0].x = fmaxf(a[0].x, x.x); a[0].y = fmaxf(a[0].y, x.y); a[0].z = fmaxf(a[0].z, x.z); a[0].w = fmaxf(a[0].w, x.w);
-      } else {
-        a[0].x += x.x; a[0].y += x.y; a[0].z += x.z; a[0].w += x.w;
-      }
-    }
+    for (; r < nrows; r += 32) acc(a[0], *reinterpret_cast<const float4*>(p + (int64_t)r * stride));
   }
-  float4 t;
-  if (mx) {
-    t.x = fmaxf(fmaxf(a[0].x, a[1].x), fmaxf(a[2].x, a[3].x));
-    t.y = fmaxf(fmaxf(a[0].y, a[1].y), fmaxf(a[2].y, a[3].y));
-    t.z = fmaxf(fmaxf(a[0].z, a[1].z), fmaxf(a[2].z, a[3].z));
-    t.w = fmaxf(fmaxf(a[0].w, a[1].w), fmaxf(a[2].w, a[3].w));
-  } else {
-    t.x = (a[0].x + a[1].x) + (a[2].x + a[3].x);
-    t.y = (a[0].y + a[1].y) + (a[2].y + a[3].y);
-    t.z = (a[0].z + a[1].z) + (a[2].z + a[3].z);
-    t.w = (a[0].w + a[1].w) + (a[2].w + a[3].w);
-  }
-  red[w][lane] = t;
+  acc(a[0], a[1]);
+  acc(a[2], a[3]);
+  acc(a[0], a[2]);
+  red[slot][q] = a[0];
   __syncthreads();
-  if (w == 0 && c < ncols) {
-    float4 v = red[0][lane];
+  if (threadIdx.x < 8 && c < ncols) {   // threads 0 .. 7: q == threadIdx.x, slot 0
+    float4 v = red[0][q];
 #pragma unroll
-    for (int k = 1; k < 16; ++k) {
-      const float4 x = red[k][lane];
-      if (mx) {
-        v.x = fmaxf(v.x, x.x); v.y = fmaxf(v.y, x.y); v.z = fmaxf(v.z, x.z); v.w = fmaxf(v.w, x.w);
-      } else {
-        v.x += x.x; v.y += x.y; v.z += x.z; v.w += x.w;
-      }
-    }
+    for (int k = 1; k < 32; ++k) acc(v, red[k][q]);
     if (mx) {
       *reinterpret_cast<float4*>(outm + (c - nsum)) = v;
       return;
     }
-    const int q = c / seg, j = c - q * seg;
-    float* o = q == 0 ? out0 : (q == 1 ? out1 : out2);
+    const int qq = c / seg, j = c - qq * seg;
+    float* o = qq == 0 ? out0 : (qq == 1 ? out1 : out2);
     if (o) {
       float4* op = reinterpret_cast<float4*>(o + j);
       if (accumulate) {
@@ -138,7 +120,7 @@ inline void fold_rows(const float* partial, int nrows, int64_t stride, int ncols
   const auto a16 = [](const void* p) { return p == nullptr || reinterpret_cast<uintptr_t>(p) % 16 == 0; };
   if (stride % 4 == 0 && ncols % 4 == 0 && seg % 4 == 0 && nsum % 4 == 0 && a16(partial) && a16(o0) && a16(o1) &&
       a16(o2) && a16(outm)) {
-    fold_rows4_k<<<(ncols + 255) / 256, kFold4NT, 0, s>>>(partial, nrows, stride, ncols, seg, o0, o1, o2, accumulate,
+    fold_rows4_k<<<(ncols + 31) / 32, kFold4NT, 0, s>>>(partial, nrows, stride, ncols, seg, o0, o1, o2, accumulate,
                                                          nsum, outm);
     return;
   }

@@ -135,8 +135,20 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
     gs = ctrl._graph_step
+    replay_ms = None
     if gs is not None:
         print('graph-train-step: {} captures, {} replays'.format(gs.captures, gs.replays), file=sys.stderr)
+        if gs.graphs:
+            # device time of one captured update alone: its graph replayed back to back (same inputs)
+            ent = max(gs.graphs.values(), key=lambda e: id(e))
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(10):
+                ent.graph.replay()
+            e1.record()
+            e1.synchronize()
+            replay_ms = round(e0.elapsed_time(e1) / 10, 3)
     if a.cprofile:
         import cProfile
         import io
@@ -165,6 +177,7 @@ def main():
                           'graph_train_step': a.graph_train_step, 'force_reducer': a.force_reducer,
                           'fp32_gemm': args.fp32_gemm if a.precision == 'fp32' else None,
                           'graph_replays': gs.replays if gs is not None else 0,
+                          'graph_replay_device_ms': replay_ms,
                           'host_ms': {'next_batch': round(t_data * 1e3 / a.steps, 3),
                                       'train_step_call': round(t_step * 1e3 / a.steps, 3)},
                           'parallelism': 'dp{}'.format(world) + (' (find-unused-parameters)' if world > 1 else ''),

@@ -2,6 +2,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 . tools/gpu/run_step.sh
+run_step 60 gpurun_out/r5p_mfma_shape.log ./tools/probe/mfma_shape_probe &&
 run_step 120 gpurun_out/r5p_g_default.log python -u tools/probe/graph_replay_probe.py &&
 DEBUG_CLR_GRAPH_PACKET_CAPTURE=1 run_step 120 gpurun_out/r5p_g_pc1.log python -u tools/probe/graph_replay_probe.py &&
 DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 run_step 120 gpurun_out/r5p_g_pc0.log python -u tools/probe/graph_replay_probe.py &&

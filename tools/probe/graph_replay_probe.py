@@ -16,8 +16,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--nodes', type=int, default=220)
     ap.add_argument('--reps', type=int, default=50)
+    ap.add_argument('--numel', type=int, default=1024, help='floats per kernel (dirty bytes per node)')
     a = ap.parse_args()
-    x = torch.zeros(1024, device='cuda')
+    x = torch.zeros(a.numel, device='cuda')
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
@@ -51,7 +52,7 @@ def main():
     t_eager = e0.elapsed_time(e1) / a.reps
     host_eager = (time.perf_counter() - t0) * 1e3 / a.reps
     env = {k: v for k, v in os.environ.items() if k.startswith(('DEBUG_CLR', 'DEBUG_HIP'))}
-    print(json.dumps({'nodes': a.nodes, 'env': env, 'graph_ms': round(t_graph, 3),
+    print(json.dumps({'nodes': a.nodes, 'numel': a.numel, 'env': env, 'graph_ms': round(t_graph, 3),
                       'graph_us_per_node': round(t_graph * 1e3 / a.nodes, 2), 'graph_host_ms': round(host_graph, 3),
                       'eager_ms': round(t_eager, 3), 'eager_us_per_kernel': round(t_eager * 1e3 / a.nodes, 2),
                       'eager_host_ms': round(host_eager, 3)}), flush=True)

@@ -708,6 +708,20 @@ inline HxColScale col_scale_src(const Tensor& t, const Tensor& ref, int64_t cols
   return c;
 }
 
+// max |x| of every row and every column in one read: ([rows, 1], [1, cols]); cols <= 4096
+std::vector<Tensor> amax_rows_cols(Tensor x) {
+  check_f32(x, "amax_rows_cols");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 4 == 0 && x.size(1) % 4 == 0 &&
+                  x.size(1) <= 4096 && aligned16(x.data_ptr()),
+              "amax_rows_cols: fp32 [rows, cols <= 4096] with 16-B rows, cols % 4 == 0");
+  Tensor r = torch::empty({x.size(0), 1}, x.options());
+  Tensor c = torch::empty({1, x.size(1)}, x.options());
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  TORCH_CHECK(hx_amax_rows_cols(x.data_ptr<float>(), x.size(0), (int)x.size(1), x.stride(0), r.data_ptr<float>(),
+                                c.data_ptr<float>(), cur_stream(x)) == 0, "amax_rows_cols: launch");
+  return {r, c};
+}
+
 // max |x| of every column: [1, cols]
 Tensor amax_cols(Tensor x) {
   check_f32(x, "amax_cols");
@@ -1007,6 +1021,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_bf16_ok", &wgrad_bf16_ok);
   m.def("amax_rows", &amax_rows);
   m.def("amax_cols", &amax_cols);
+  m.def("amax_rows_cols", &amax_rows_cols);
   m.def("split_weight_f16", &split_weight_f16);
   m.def("gemm_f16", &gemm_f16, py::arg("a"), py::arg("a_amax"), py::arg("b"), py::arg("b_amax"),
         py::arg("out") = py::none(), py::arg("beta") = false, py::arg("bias") = py::none(), py::arg("ks") = 0);

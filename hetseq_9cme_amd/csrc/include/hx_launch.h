@@ -174,6 +174,8 @@ int hx_wgrad_f16(const float* dy, int ldy, const HxColScale& ca, const float* x,
 void hx_amax_cols(const float* x, int64_t rows, int cols, int64_t ld, float* out, hipStream_t s);
 // max |x| of each row of a [rows][cols] fp32 matrix (cols % 4 == 0, 16-B rows) -> out[rows]
 void hx_amax_rows(const float* x, int64_t rows, int cols, int64_t ld, float* out, hipStream_t s);
+int hx_amax_rows_cols(const float* x, int64_t rows, int cols, int64_t ld, float* rowmax, float* colmax,
+                      hipStream_t s);
 // every weight of a batch -> P2 fp16 pieces wf [N][2K] (row n scaled by its own 2^E), wt [K][2N]
 // (row k = column k of W, scaled by that column's 2^E); rc: per weight its row maxima [N] then
 // column maxima [K] at rc + roff[i] (rc_floats in all, zeroed here)

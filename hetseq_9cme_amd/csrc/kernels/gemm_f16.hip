@@ -1356,6 +1356,74 @@ void hx_amax_cols(const float* x, int64_t rows, int cols, int64_t ld, float* out
   amax_cols_k<<<dim3(cb, (unsigned)slabs), 256, 0, s>>>(x, rows, cols, ld, rpb, out);
 }
 
+// max |x| of every row AND every column of a [rows][cols] fp32 matrix in one read: a block = 4
+// waves over 64 rows, lane l owns column quads l, l + 64, .. (cols <= 4096: 16 quads); row maxima
+// by wave shuffles, column maxima over the block's rows through LDS, then one atomic max per
+// column (non-negative floats order as their bits) into colmax, zeroed beforehand.  The operand
+// scales of a tensor both a data-gradient GEMM (rows) and a weight gradient (columns) consume
+// (the attention backward's dQKV at S > 128, whose key blocks cannot know the final dQ).
+constexpr int kRcRows = 64, kRcMaxQ = 16;
+__global__ __launch_bounds__(256) void amax_rows_cols_k(const float* __restrict__ x, int64_t rows, int cols,
+                                                        int64_t ld, float* __restrict__ rowmax,
+                                                        float* __restrict__ colmax) {
+  extern __shared__ float4 cred[];   // [4 waves][cols / 4]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int nq = cols >> 2;
+  const int64_t r0 = (int64_t)blockIdx.x * kRcRows;
+  float4 cm[kRcMaxQ];
+#pragma unroll
+  for (int i = 0; i < kRcMaxQ; ++i) cm[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int rr = w; rr < kRcRows; rr += 4) {
+    const int64_t r = r0 + rr;
+    if (r >= rows) break;
+    const float4* xr = reinterpret_cast<const float4*>(x + r * ld);
+    float m = 0.f;
+#pragma unroll
+    for (int i = 0; i < kRcMaxQ; ++i) {
+      const int j = lane + 64 * i;
+      if (j < nq) {
+        const float4 v = xr[j];
+        const float ax = fabsf(v.x), ay = fabsf(v.y), az = fabsf(v.z), aw = fabsf(v.w);
+        cm[i].x = fmaxf(cm[i].x, ax); cm[i].y = fmaxf(cm[i].y, ay);
+        cm[i].z = fmaxf(cm[i].z, az); cm[i].w = fmaxf(cm[i].w, aw);
+        m = fmaxf(m, fmaxf(fmaxf(ax, ay), fmaxf(az, aw)));
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+    if (lane == 0) rowmax[r] = m;
+  }
+#pragma unroll
+  for (int i = 0; i < kRcMaxQ; ++i) {
+    const int j = lane + 64 * i;
+    if (j < nq) cred[w * nq + j] = cm[i];
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < nq; j += 256) {
+    float4 v = cred[j];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const float4 u = cred[k * nq + j];
+      v.x = fmaxf(v.x, u.x); v.y = fmaxf(v.y, u.y); v.z = fmaxf(v.z, u.z); v.w = fmaxf(v.w, u.w);
+    }
+    unsigned* o = reinterpret_cast<unsigned*>(colmax + 4 * j);
+    atomicMax(o, __float_as_uint(v.x));
+    atomicMax(o + 1, __float_as_uint(v.y));
+    atomicMax(o + 2, __float_as_uint(v.z));
+    atomicMax(o + 3, __float_as_uint(v.w));
+  }
+}
+
+int hx_amax_rows_cols(const float* x, int64_t rows, int cols, int64_t ld, float* rowmax, float* colmax,
+                      hipStream_t s) {
+  if (cols % 4 || cols > 4 * 64 * kRcMaxQ) return -1;
+  (void)hipMemsetAsync(colmax, 0, (size_t)cols * 4, s);
+  if (rows < 1) return 0;
+  amax_rows_cols_k<<<(unsigned)((rows + kRcRows - 1) / kRcRows), 256, (size_t)cols * 16, s>>>(x, rows, cols, ld,
+                                                                                              rowmax, colmax);
+  return 0;
+}
+
 void hx_amax_rows(const float* x, int64_t rows, int cols, int64_t ld, float* out, hipStream_t s) {
   if (rows < 1) return;
   amax_rows_k<<<(unsigned)((rows + 3) / 4), 256, 0, s>>>(x, rows, cols, ld, out);

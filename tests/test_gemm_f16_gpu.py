@@ -412,3 +412,17 @@ def test_wgrad_f16_column_ramp(dev):
     e32 = ((torch.mm(dy.t(), x).double() - ref).abs() / den.clamp_min(1e-300))
     print('wgrad column ramp: max err fp16x3 {:.3g} native {:.3g}'.format(e16.max().item(), e32.max().item()))
     assert (e16.amax(1) <= 4 * e32.amax(1) + 2e-7).all()
+
+
+@pytest.mark.parametrize('rows,cols', [(16384, 2304), (1000, 768), (77, 4096), (5, 4)])
+def test_amax_rows_cols_one_pass(rows, cols):
+    """The fused row + column max |x| pass (the scale sources of a tensor no producer described)
+    equals the row-wise and column-wise maxima exactly, rows ramped over 2^-20 .. 2^20."""
+    from hetseq_9cme_amd.ops._ext import C
+    dev = torch.device('cuda')
+    g = torch.Generator(device=dev).manual_seed(3)
+    x = torch.randn(rows, cols, device=dev, generator=g) * torch.pow(
+        2.0, torch.linspace(-20, 20, rows, device=dev))[:, None]
+    r, c = C().amax_rows_cols(x)
+    assert torch.equal(r, x.abs().amax(1, keepdim=True))
+    assert torch.equal(c, x.abs().amax(0, keepdim=True))

@@ -66,9 +66,32 @@ def sweep(C, dev, cfgs):
     os.environ.pop('HX_GEMM_F16_CFG', None)
 
 
+def wgrad_sweep(C, dev, plans):
+    """weight gradients of every shape under forced (tile config : token splits) plans
+    (HX_WGRAD_F16, 'plan' = the kernel's own)."""
+    T = int(os.environ.get('T', '16384'))
+    g = torch.Generator(device=dev).manual_seed(0)
+    for (name, N, K) in [('qkv', 2304, 768), ('attn_out', 768, 768), ('ffn_up', 3072, 768), ('ffn_down', 768, 3072)]:
+        x = torch.randn(T, K, device=dev, generator=g)
+        dy = torch.randn(T, N, device=dev, generator=g)
+        out = torch.empty(N, K, device=dev)
+        dc, xc = C().amax_cols(dy), C().amax_cols(x)
+        fl = 2.0 * T * N * K
+        for c in plans:
+            if c == 'plan':
+                os.environ.pop('HX_WGRAD_F16', None)
+            else:
+                os.environ['HX_WGRAD_F16'] = c
+            us = timed(lambda: C().wgrad_f16(dy, dc, x, xc, out))
+            print('{:10s} wgrad {:6s} {:7.1f} us ({:4.2f} PF/s)'.format(name, c, us, 3 * fl / us / 1e9), flush=True)
+    os.environ.pop('HX_WGRAD_F16', None)
+
+
 def main():
     from hetseq_9cme_amd.ops._ext import C
     dev = torch.device('cuda', 0)
+    if os.environ.get('WGRAD_PLANS'):
+        return wgrad_sweep(C, dev, os.environ['WGRAD_PLANS'].split(','))
     if os.environ.get('CFGS'):
         return sweep(C, dev, os.environ['CFGS'].split(','))
     T = int(os.environ.get('T', '16384'))

@@ -1285,6 +1285,9 @@ void hx_wgrad_f16_plan(int M, int N, int T, int* cfg, int* nsplit) {
   const int c = (t256 >= 24 && t256 <= 512) ? 1 : 0;
   const int tiles = c ? t256 : (M / 128) * (N / 128);
   const int slots = (c ? 1 : 2) * hx_cu_slots();
+  // splits fill the CUs: more is faster up to one workgroup per CU (r5y, repeated A/B on one box:
+  // QKV 27 tiles x 6 / 7 / 8 / 9 splits 222 / 194 / 178 / 179 us, FFN 36 x 6 / 7 255 / 233 us, x 8
+  // (two rounds) 338 us; a single-pass sweep is biased by the warm-up of its first entries)
   int sp = std::max(1, slots / std::max(1, tiles));
   sp = std::min(sp, std::max(1, T / 256));
   if (const char* e = getenv("HX_WGRAD_F16")) {

@@ -104,7 +104,6 @@ struct F16Args {
   int dmode;        // EPI 1: C gets gelu'(u) (1) or u (0); EPI 2: aux holds gelu'(u) (1) or u (0)
   int ks;           // split-K slabs (EPI 0 only): slab z reduces k steps [z, z + 1) K / ks into C + z c_zs
   int64_t c_zs;
-  int diag;         // timing diagnostics (HX_GEMM_DIAG, wrong results): 1 no epilogue, 2 no k loop
 };
 
 // max |x| of `rows` operand rows starting at r0 from their partials -> scale tables (2^E, 2^-E);
@@ -169,7 +168,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
   const int z = work0 / total, work = work0 - z * total;
   const int nt = work % TN, mt = work / TN;
   const int m0 = mt * BM, n0 = nt * BN;
-  const int nit = (g.diag & 2) ? 0 : g.K / KD / g.ks, it0 = z * (g.K / KD / g.ks);
+  const int nit = g.K / KD / g.ks, it0 = z * nit;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w % NWM, wn = w / NWM, h = lane >> 5, l32 = lane & 31;
@@ -261,14 +260,6 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
       }
     };
     auto split_a = [&](const f32x4 (&raw)[MB][2], Fr& F) {
-      if constexpr (DIL == 10) {   // DIAGNOSTIC (timing only): no split VALU
-#pragma unroll
-        for (int a = 0; a < MB; ++a) {
-          F.a0[a] = __builtin_bit_cast(f16x8, raw[a][0]);
-          F.a1[a] = __builtin_bit_cast(f16x8, raw[a][1]);
-        }
-        return;
-      }
 #pragma unroll
       for (int a = 0; a < MB; ++a) {
         const f32x8 y = f32x8{raw[a][0][0], raw[a][0][1], raw[a][0][2], raw[a][0][3],
@@ -308,18 +299,17 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
       __builtin_amdgcn_sched_barrier(0);
       dma(it + NS - 1);
       __builtin_amdgcn_sched_barrier(0);
-      if constexpr (DIL == 10 || 4 * MB > 2 * MB * NB) {   // small wave tiles / DIL diag: compiler split
+      if constexpr (4 * MB > 2 * MB * NB) {   // small wave tiles (NB = 1): the compiler's split
         pass(Fc, 1);
         split_a(raw, Fn);
         pass(Fc, 2);
       } else {
         uint32_t h0w[MB][4], h1w[MB][4];
-        constexpr int P0 = DIL == 2 ? 2 * MB * NB - 4 * MB : 0;   // MFMA of the first pair
 #pragma unroll
         for (int i = 0; i < 2 * MB * NB; ++i) {
           mma(Fc, 1 + i / (MB * NB), i % (MB * NB));
-          if (i >= P0 && i < P0 + 4 * MB) {
-            const int a = (i - P0) / 4, w = (i - P0) % 4;
+          if (i < 4 * MB) {   // (r5i: placing the pairs after the last MFMAs instead measured the same)
+            const int a = i / 4, w = i % 4;
             const f32x4& r = raw[a][w >> 1];
             split_pair_mix(r[2 * (w & 1)], r[2 * (w & 1) + 1], sa[a], h0w[a][w], h1w[a][w]);
           }
@@ -404,13 +394,12 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
   }
   // every wave is past its last fragment read before the ring is reused below
   __syncthreads();
-  if (g.diag & 1) return;
 
   // output store cache policy: the GELU epilogues' two outputs (2 x 201 MB at the FFN shapes) go
   // non-temporal -- r5m: FFN up 326 -> 305 us, FFN-down dgrad 294 -> 285 us; the plain / beta
-  // epilogues' outputs are read by the next kernel at once and stay cached (A/B: cfg 11 all
-  // non-temporal, cfg 12 sc0 sc1)
-  constexpr int SP = DIL == 21 ? 2 : DIL == 22 ? 17 : (EPI == 1 || EPI == 2) ? 2 : 0;
+  // epilogues' outputs are read by the next kernel at once and stay cached (r5z: non-temporal
+  // there too measured the same, sc0 sc1 no better)
+  constexpr int SP = (EPI == 1 || EPI == 2) ? 2 : 0;
   // ---- epilogue: quad transpose, then lane (l32 & 3) owns row 8 gq + 4 h + (l32 & 3) of each
   // 32 x 32 block and its columns (l32 & ~3) .. + 3; stores past M dropped by the descriptor
   const int mrow = wm * WM + 4 * h + (l32 & 3), ncol = wn * WN + (l32 & ~3);
@@ -643,12 +632,12 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
 // cfg 3: 64 x 64, 4 waves (2 x 2) of 32 x 32, 4-stage ring                          -- tiny M
 // cfg 4: 128 x 192, 4 waves (2 x 2) of 64 x 96, two workgroups per CU, 3-stage ring
 // cfg 5: 256 x 256, 8 waves (4 x 2) of 64 x 128, one workgroup per CU, 4-stage ring
-// cfg 6: cfg 1 with the DMA pieces issued as one burst (A/B of the interleave)
-// cfg 7: cfg 1 on a 5-stage ring (A/B of the ring depth: r5c, no gain)
-constexpr int kCfgs = 13;   // 8 .. 12: timing diagnostics (wrong results), never planned
+// cfg 6: cfg 1 with the bf16 variant's DMA pieces issued as one burst (the fp16x3 step always
+//        bursts them: interleaving measured 2-5 % slower, r5d); a 5-stage ring measured no gain (r5c)
+constexpr int kCfgs = 7;
 int cfg_bm(int c) { return c <= 1 || c >= 5 ? 256 : c == 2 || c == 4 ? 128 : 64; }
 int cfg_bn(int c) { return c == 5 ? 256 : c <= 1 || c == 4 || c >= 6 ? 192 : c == 2 ? 96 : 64; }
-int cfg_nwm(int c) { return c == 0 || c == 9 ? 8 : c == 1 || c >= 5 ? 4 : c == 2 ? 4 : 2; }
+int cfg_nwm(int c) { return c == 0 ? 8 : c == 1 || c >= 5 ? 4 : c == 2 ? 4 : 2; }
 
 template <int BM, int BN, int WM, int WN, int EPI, int WGS, int NS, int AT = 0, int OB = 0, int DIL = 1>
 void launch_one(const F16Args& a, hipStream_t s) {
@@ -670,12 +659,6 @@ void launch_cfg(int cfg, const F16Args& a, hipStream_t s) {
   if (cfg == 0) launch_one<256, 192, 32, 192, EPI, 1, 4, AT, OB>(a, s);
   else if (cfg == 1) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB>(a, s);
   else if (cfg == 6) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 0>(a, s);
-  else if (cfg == 7) launch_one<256, 192, 64, 96, EPI, 1, 5, AT, OB>(a, s);
-  else if (cfg == 8) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 2>(a, s);   // cfg 1, late split pairs
-  else if (cfg == 9) launch_one<256, 192, 32, 192, EPI, 1, 4, AT, OB, 2>(a, s);  // cfg 0, late split pairs
-  else if (cfg == 10) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 10>(a, s);  // DIAGNOSTIC: no split
-  else if (cfg == 11) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 21>(a, s);  // cfg 6, non-temporal stores
-  else if (cfg == 12) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 22>(a, s);  // cfg 6, sc0 sc1 stores
   else if (cfg == 2) launch_one<128, 96, 32, 96, EPI, 2, 4, AT, OB>(a, s);
   else if (cfg == 4) launch_one<128, 192, 64, 96, EPI, 2, 3, AT, OB>(a, s);
   else if (cfg == 5) launch_one<256, 256, 64, 128, EPI, 1, 4, AT, OB>(a, s);
@@ -1262,8 +1245,6 @@ int hx_gemm_f16(const HxGemmF16& p, int cfg, hipStream_t s) {
   a.dmode = p.dmode;
   a.ks = ks;
   a.c_zs = p.c_zs;
-  static const int diag = getenv("HX_GEMM_DIAG") ? atoi(getenv("HX_GEMM_DIAG")) : 0;
-  a.diag = diag;
   if (p.abf16) {
     if (p.kind == 1) launch_cfg<1, 1, 1>(cfg, a, s);        // bf16 FFN up: gelu'(u), gelu(u) in bf16
     else if (p.kind == 2) launch_cfg<2, 1, 1>(cfg, a, s);   // bf16 FFN-down dgrad * gelu'(u)

@@ -273,7 +273,7 @@ def test_ffn_bf16_autograd(dev):
     assert rel(W1.grad, W1r.grad) < 1e-2 and rel(W2.grad, W2r.grad) < 1e-2 and rel(b1.grad, b1r.grad) < 1e-2
 
 
-@pytest.mark.parametrize('cfg', ['0', '1', '2', '3', '4', '5', '6', '7'])
+@pytest.mark.parametrize('cfg', ['0', '1', '2', '3', '4', '5', '6'])
 def test_gemm_f16_every_tile(dev, monkeypatch, cfg):
     """Every tile configuration of gemm_f16_k (HX_GEMM_F16_CFG forces it): forward with bias and the
     beta = 1 data gradient, rows not a multiple of the tile."""

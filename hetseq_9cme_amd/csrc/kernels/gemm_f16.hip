@@ -30,7 +30,7 @@
 //    per-wave column partials of t = the FFN-up bias gradient).  Split-K slabs for deep
 //    reductions with few tiles (the MLM decoder's data gradient).
 //  * wgrad_f16_k  dW[M][N] = dY[T][M]^T . X[T][N] (tokens = reduction): both operands fp32,
-//    16 tokens per stage loaded into registers, split, and written as fp16 piece tiles into an
+//    32 tokens per stage loaded into registers, split, and written as fp16 piece tiles into an
 //    XOR-swizzled LDS image read with the transposing ds_read_b64_tr_b16; token-range split-K
 //    over the CUs, partial slabs summed by one vectorised pass.
 #include <algorithm>
@@ -716,7 +716,7 @@ __device__ __forceinline__ void col_scales(const HxColScale& c, int c0, int cols
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int BKT = 32>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const float* __restrict__ A, int lda,
                                                                          const HxColScale ca,
                                                                          const float* __restrict__ B, int ldb,
@@ -725,11 +725,15 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
                                                                          int kchunk, int nsplit, int mvalid) {
   constexpr int NWM = BM / WM, NW = NWM * (BN / WN), NT = NW * 64;
   constexpr int MB = WM / 32, NB = WN / 32;
-  constexpr int BKT = 16;
+  // BKT tokens per stage: BKT / 16 MFMA substeps per barrier.  32 (r5): half the barriers and
+  // post-barrier fragment reads per MFMA of 16, measured the same (r5ag, repeated A/B: QKV 185 /
+  // 185, FFN 234 / 233 us) -- neither bounds this kernel; the vector-memory path and the clock do
+  constexpr int NSUB = BKT / 16;
   constexpr int CA = BKT * BM / 8 / NT, CB = BKT * BN / 8 / NT;   // 8-column chunks per thread
   static_assert(CA >= 1 && CB >= 1 && BKT * BM / 8 % NT == 0 && BKT * BN / 8 % NT == 0, "tile / thread mismatch");
   static_assert(WM % 64 == 0 && WN % 64 == 0, "subtile parity of fragment a is a & 1");
-  constexpr int A_T = BKT * BM * 2, B_T = BKT * BN * 2;   // one fp16 piece tile
+  constexpr int A_T = BKT * BM * 2, B_T = BKT * BN * 2;   // one fp16 piece tile [32 tokens][cols]
+  constexpr int A_S = 16 * BM * 2, B_S = 16 * BN * 2;    // a 16-token substep's offset (toff rows 16..31)
   constexpr int STAGE = 2 * (A_T + B_T);
   extern __shared__ __attribute__((aligned(16))) char lds[];
   // per-column scales of the two operands (dY's columns = dW's rows, X's columns = dW's columns)
@@ -763,33 +767,30 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
   const hx::Buf bbuf(B + (int64_t)t0 * ldb, (uint32_t)((int64_t)(t1 - t0) * ldb * 4));
   uint32_t va[CA], vb[CB];
   int sa_[CA], sb_[CB];
-  f32x8 csa[CA], csb[CB];   // the chunks' 8 column scales
+  const float* cs[CA + CB];   // the chunks' 8 column scales (LDS tables; read at split time)
 #pragma unroll
   for (int i = 0; i < CA; ++i) {
     const int e = tid + i * NT, row = e / (BM / 8), c = e % (BM / 8);
     va[i] = (uint32_t)(row * lda + m0 + 8 * c) * 4;
     sa_[i] = toff<BM>(row, c);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) csa[i][j] = tsa[8 * c + j];
+    cs[i] = tsa + 8 * c;
   }
 #pragma unroll
   for (int i = 0; i < CB; ++i) {
     const int e = tid + i * NT, row = e / (BN / 8), c = e % (BN / 8);
     vb[i] = (uint32_t)(row * ldb + n0 + 8 * c) * 4;
     sb_[i] = toff<BN>(row, c);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) csb[i][j] = tsb[8 * c + j];
+    cs[CA + i] = tsb + 8 * c;
   }
   int alo[2], ahi[2], blo[2], bhi[2];
   tr_base<BM>(lane, alo, ahi);
   tr_base<BN>(lane, blo, bhi);
 
-  // two register stages: the fp32 tiles of step it + 2 are loaded while step it runs on the
-  // matrix cores, so a load has a whole step of MFMA work (plus the split / LDS write of step
-  // it + 1) to land before it is split and written to LDS.  Past the slab's end the loads are
-  // aimed past the buffer (zeros, no memory traffic): every step has the same shape, no branch.
+  // ONE register stage: the fp32 tiles of stage it + 2 are loaded right after stage it + 1's
+  // split (in step it's second substep), so a load has a full step of MFMA work to land; past the
+  // slab's end the loads are aimed past the buffer (zeros, no memory traffic)
   struct Regs {
-    f32x4 a[CA][2], b[CB][2];
+    f32x4 v[CA + CB][2];   // chunks: CA of dY, then CB of X
   };
   auto load = [&](int it, Regs& r) {
     const bool in = it < nit;
@@ -799,21 +800,24 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
     for (int i = 0; i < CA; ++i)
 #pragma unroll
       for (int k = 0; k < 2; ++k)
-        r.a[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(abuf.r, va[i] + 16 * k, soa, 0));
+        r.v[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(abuf.r, va[i] + 16 * k, soa, 0));
 #pragma unroll
     for (int i = 0; i < CB; ++i)
 #pragma unroll
       for (int k = 0; k < 2; ++k)
-        r.b[i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(bbuf.r, vb[i] + 16 * k, sob, 0));
+        r.v[CA + i][k] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(bbuf.r, vb[i] + 16 * k, sob, 0));
   };
   // the split of one 8-column chunk (c < CA: of dY, else of X) as four v_fma_mix pairs, and its
   // two LDS piece writes
   constexpr int NCH = CA + CB;
-  auto split_pair = [&](const Regs& r, int c, int p, uint32_t (&h0)[4], uint32_t (&h1)[4]) {
-    const f32x4& v = c < CA ? r.a[c][p >> 1] : r.b[c - CA][p >> 1];
-    const f32x8& sc = c < CA ? csa[c] : csb[c - CA];
+  auto scales = [&](int c, f32x4 (&sc)[2]) {
+    sc[0] = *reinterpret_cast<const f32x4*>(cs[c]);
+    sc[1] = *reinterpret_cast<const f32x4*>(cs[c] + 4);
+  };
+  auto split_pair = [&](const Regs& r, int c, int p, const f32x4 (&sc)[2], uint32_t (&h0)[4], uint32_t (&h1)[4]) {
+    const f32x4& v = r.v[c][p >> 1];
     const int e = 2 * (p & 1);
-    split_pair_mix2(v[e], v[e + 1], sc[4 * (p >> 1) + e], sc[4 * (p >> 1) + e + 1], h0[p], h1[p]);
+    split_pair_mix2(v[e], v[e + 1], sc[p >> 1][e], sc[p >> 1][e + 1], h0[p], h1[p]);
   };
   auto write_chunk = [&](int buf, int c, const uint32_t (&h0)[4], const uint32_t (&h1)[4]) {
     char* st = lds + buf * STAGE;
@@ -829,9 +833,11 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
   auto store_all = [&](int buf, const Regs& r) {   // (the prologue's stage 0)
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
+      f32x4 sc[2];
+      scales(c, sc);
       uint32_t h0[4], h1[4];
 #pragma unroll
-      for (int p = 0; p < 4; ++p) split_pair(r, c, p, h0, h1);
+      for (int p = 0; p < 4; ++p) split_pair(r, c, p, sc, h0, h1);
       write_chunk(buf, c, h0, h1);
     }
   };
@@ -845,57 +851,62 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64) void wgrad_f16_k(const 
   struct Fr {
     f16x8 a0[MB], b0[NB], b1[NB];   // a0[a] holds piece 1 of A rows a during pass 2
   };
-  // fragments of a stage; the second A pieces (a1, pass 2 only) are read one by one after the
-  // last pass-1 MFMA on the first piece of the same rows, into its registers (16 VGPRs fewer)
-  auto read = [&](int buf, Fr& F) {
+  // fragments of substep s of a stage; the second A pieces (a1, pass 2 only) are read one by one
+  // after the last pass-1 MFMA on the first piece of the same rows, into its registers
+  auto read = [&](int buf, Fr& F, int s) {
     const char* st = lds + buf * STAGE;
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      F.b0[b] = tfrag<BN>(st + 2 * A_T, blo, bhi, wn * WN + 32 * b, b & 1);
-      F.b1[b] = tfrag<BN>(st + 2 * A_T + B_T, blo, bhi, wn * WN + 32 * b, b & 1);
+      F.b0[b] = tfrag<BN>(st + 2 * A_T + s * B_S, blo, bhi, wn * WN + 32 * b, b & 1);
+      F.b1[b] = tfrag<BN>(st + 2 * A_T + B_T + s * B_S, blo, bhi, wn * WN + 32 * b, b & 1);
     }
 #pragma unroll
-    for (int a = 0; a < MB; ++a) F.a0[a] = tfrag<BM>(st, alo, ahi, wm * WM + 32 * a, a & 1);
+    for (int a = 0; a < MB; ++a) F.a0[a] = tfrag<BM>(st + s * A_S, alo, ahi, wm * WM + 32 * a, a & 1);
   };
-  auto read_a1 = [&](int buf, Fr& F, int a) {
-    F.a0[a] = tfrag<BM>(lds + buf * STAGE + A_T, alo, ahi, wm * WM + 32 * a, a & 1);
+  auto read_a1 = [&](int buf, Fr& F, int a, int s) {
+    F.a0[a] = tfrag<BM>(lds + buf * STAGE + A_T + s * A_S, alo, ahi, wm * WM + 32 * a, a & 1);
   };
-  constexpr int NMF = 3 * MB * NB;   // MFMAs per step
-  static_assert(4 * NCH <= NMF, "one split pair per MFMA");
+  constexpr int NMF = 3 * MB * NB;   // MFMAs per substep
+  constexpr int G0 = NSUB * NMF - 4 * NCH;   // the step's MFMA after which the first split pair goes
+  static_assert(G0 >= 0, "one split pair per MFMA");
   auto mma = [&](const Fr& F, int i) {   // MFMA i: pass q = i / (MB NB)
     const int q = i / (MB * NB), a = (i % (MB * NB)) / NB, b = i % NB;
     acc[a][b] = mfma16(F.a0[a], q == 1 ? F.b1[b] : F.b0[b], acc[a][b]);
   };
 
-  // step it: issue the loads of step it + 2 into the register set step it's data used, read
-  // stage it's fragments, then its MFMAs with the split of step it + 1 (loaded a step ago) placed
-  // pair by pair between them and its LDS pieces written into the other buffer (last read before
-  // the previous barrier); one barrier.  The two register sets alternate (steps unrolled by two).
-  Regs r0, r1;
-  load(0, r0);
-  load(1, r1);
-  store_all(0, r0);
+  // step it (32 tokens, two 16-token substeps): each substep's fragments, then its MFMAs; the
+  // split of stage it + 1 (loaded a step ago) rides pair by pair behind the step's last MFMAs and
+  // goes into the other buffer (last read before the previous barrier), then stage it + 2's loads
+  // are issued into the freed registers (a full step to land); one barrier per step
+  Regs rr;
+  load(0, rr);
+  store_all(0, rr);
+  load(1, rr);
   __syncthreads();
-  auto step = [&](int it, Regs& mine, const Regs& next) {
-    load(it + 2, mine);
-    Fr F;
-    read(it & 1, F);
+  for (int it = 0; it < nit; ++it) {
+    const int cur = it & 1;
+    f32x4 sc[2];
     uint32_t h0[4], h1[4];
 #pragma unroll
-    for (int i = 0; i < NMF; ++i) {
-      mma(F, i);
-      if (i / (MB * NB) == 1 && i % NB == NB - 1) read_a1(it & 1, F, (i % (MB * NB)) / NB);
-      if (i < 4 * NCH) {
-        split_pair(next, i / 4, i % 4, h0, h1);
-        if (i % 4 == 3) write_chunk((it & 1) ^ 1, i / 4, h0, h1);
+    for (int s = 0; s < NSUB; ++s) {
+      Fr F;
+      read(cur, F, s);
+#pragma unroll
+      for (int i = 0; i < NMF; ++i) {
+        mma(F, i);
+        if (i / (MB * NB) == 1 && i % NB == NB - 1) read_a1(cur, F, (i % (MB * NB)) / NB, s);
+        const int g = s * NMF + i;
+        if (g >= G0) {
+          const int k = g - G0;
+          if (k % 4 == 0) scales(k / 4, sc);
+          split_pair(rr, k / 4, k % 4, sc, h0, h1);
+          if (k % 4 == 3) write_chunk(cur ^ 1, k / 4, h0, h1);
+        }
+        if (g == NSUB * NMF - 1) load(it + 2, rr);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
     }
     __syncthreads();
-  };
-  for (int it = 0; it < nit; it += 2) {
-    step(it, r0, r1);
-    if (it + 1 < nit) step(it + 1, r1, r0);
   }
 
   float* o = out + (nsplit > 1 ? (int64_t)sp * M * N : 0);
@@ -924,22 +935,22 @@ __global__ __launch_bounds__(256) void slab_sum_k(const float4* __restrict__ ws,
   }
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int BKT = 32>
 void wgrad_launch(const float* A, int lda, const HxColScale& ca, const float* B, int ldb, const HxColScale& cb,
                   float* out, float* ws, int M, int N, int T, int nsplit, int mvalid, hipStream_t s) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
-  const int kchunk = ((T + nsplit - 1) / nsplit + 15) / 16 * 16;
+  const int kchunk = ((T + nsplit - 1) / nsplit + BKT - 1) / BKT * BKT;
   nsplit = (T + kchunk - 1) / kchunk;
   const int total = (M / BM) * (N / BN) * nsplit;
   const int per = (total + 7) / 8;
-  const size_t smem = (size_t)2 * 2 * 16 * (BM + BN) * 2 + (2 * BM + 2 * BN + NT / 64) * 4;
+  const size_t smem = (size_t)2 * 2 * BKT * (BM + BN) * 2 + (2 * BM + 2 * BN + NT / 64) * 4;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_f16_k<BM, BN, WM, WN>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_f16_k<BM, BN, WM, WN, BKT>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
-  wgrad_f16_k<BM, BN, WM, WN><<<8 * per, NT, smem, s>>>(A, lda, ca, B, ldb, cb, nsplit > 1 ? ws : out, M, N, T,
+  wgrad_f16_k<BM, BN, WM, WN, BKT><<<8 * per, NT, smem, s>>>(A, lda, ca, B, ldb, cb, nsplit > 1 ? ws : out, M, N, T,
                                                         kchunk, nsplit, nsplit > 1 ? M : mvalid);
   if (nsplit > 1) {
     const int64_t n4 = (int64_t)mvalid * N / 4, slab4 = (int64_t)M * N / 4;
@@ -1273,8 +1284,11 @@ void hx_wgrad_f16_plan(int M, int N, int T, int* cfg, int* nsplit) {
   sp = std::min(sp, std::max(1, T / 256));
   if (const char* e = getenv("HX_WGRAD_F16")) {
     int ec = -1, es = -1;
-    if (sscanf(e, "%d:%d", &ec, &es) == 2 && (ec == 0 || ec == 1) && es >= 1) {
+    // "cfg:splits" (splits 0: the plan's for that tile)
+    if (sscanf(e, "%d:%d", &ec, &es) == 2 && (ec == 0 || ec == 1) && es >= 0) {
       if (ec == 0 || t256) {
+        const int ft = ec ? t256 : (M / 128) * (N / 128), fs = (ec ? 1 : 2) * hx_cu_slots();
+        if (es == 0) es = std::min(std::max(1, fs / std::max(1, ft)), std::max(1, T / 256));
         *cfg = ec;
         *nsplit = std::min(es, std::max(1, T / 16));
         return;

@@ -64,6 +64,8 @@ def bench_attn(B, S, nh=12, keep=0.9, dtype=torch.float32):
            flops=2.5 * f_fwd)
     if dtype == torch.float32:   # fp32 on the fp16 matrix cores (fp16x3 pieces, attention_f16.hip)
         report('attn_fwd_f16', timeit(lambda: C().attn_fwd_f16(qkv, mb, nh, keep, SEED, 0, None)), flops=f_fwd)
+        report('attn_fwd_f16 (no dropout)', timeit(lambda: C().attn_fwd_f16(qkv, mb, nh, 1.0, SEED, 0, None)),
+               flops=f_fwd)
         report('attn_bwd_f16', timeit(lambda: C().attn_bwd_f16(dout, qkv, mb, out, lse, dm, nh, keep, None, None, None,
                                                                 None)[0]), flops=2.5 * f_fwd)
 

@@ -282,14 +282,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     pl = lse_bh[lq < S ? lq : S - 1];
     if (kDrop) pm = dmask_bh[moff + (qt >> 5)];
   };
-  // (q + bias) / 8 of the prefetched tile
+  // (q + bias) / 8 of the prefetched tile (the head's Q bias from LDS, staged once)
+  __shared__ __attribute__((aligned(16))) float Qb[64];
+  if (tid < 64) Qb[tid] = qbias ? qbias[tid] : 0.f;   // published by the barrier after ld_tile(0)
   auto qvals = [&](float (&q0)[4], float (&q1)[4]) {
     const float a[8] = {pq[0].x, pq[0].y, pq[0].z, pq[0].w, pq[1].x, pq[1].y, pq[1].z, pq[1].w};
+    const float4 bq = *reinterpret_cast<const float4*>(&Qb[4 * sdq]);
+    const float bb[4] = {bq.x, bq.y, bq.z, bq.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float bj = qbias ? qbias[4 * sdq + j] : 0.f;
-      q0[j] = (a[j] + bj) * scale;
-      q1[j] = (a[4 + j] + bj) * scale;
+      q0[j] = (a[j] + bb[j]) * scale;
+      q1[j] = (a[4 + j] + bb[j]) * scale;
     }
   };
   // the prefetched tile's max |Q|, |dO| -> this wave's slots
@@ -597,14 +600,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       dvp[(int64_t)key * H3 + 32 + l32] = dv1[r];
     }
     if (want_am) {
-      // key rows: the 64 dK and 64 dV columns of a row sit on the 32 lanes of a half-wave
+      // key rows: the 64 dK and 64 dV columns of a row sit on the 32 lanes of a half-wave.
+      // Transposing max-reduction: at lane masks 16 .. 2 a lane keeps the half of its row values
+      // its lane bit selects and takes the partner's other half, then one more exchange (mask 1):
+      // 16 shuffles instead of 16 x 5; lanes 2k, 2k + 1 end with row value k
+      float v[16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        float m = fmaxf(fmaxf(fabsf(dk0[r]), fabsf(dk1[r])), fmaxf(fabsf(dv0[r]), fabsf(dv1[r])));
+      for (int r = 0; r < 16; ++r) v[r] = fmaxf(fmaxf(fabsf(dk0[r]), fabsf(dk1[r])), fmaxf(fabsf(dv0[r]), fabsf(dv1[r])));
 #pragma unroll
-        for (int o = 1; o < 32; o <<= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-        const int key = kbase + w * 32 + crow(r, h);
-        if (l32 == 0 && key < S) atomicMax(&rmx_s[key], __float_as_uint(m));
+      for (int m = 16, n = 16; m >= 2; m >>= 1, n >>= 1) {
+        const bool up = (l32 & m) != 0;
+#pragma unroll
+        for (int j = 0; j < n / 2; ++j) {
+          const float keepv = up ? v[j + n / 2] : v[j], sendv = up ? v[j] : v[j + n / 2];
+          v[j] = fmaxf(keepv, __shfl_xor(sendv, m, 64));
+        }
+      }
+      v[0] = fmaxf(v[0], __shfl_xor(v[0], 1, 64));
+      {
+        const int key = kbase + w * 32 + crow(l32 >> 1, h);
+        if ((l32 & 1) == 0 && key < S) atomicMax(&rmx_s[key], __float_as_uint(v[0]));
       }
       __syncthreads();
       if (tid < S) amax_part[((int64_t)b * S + tid) * nh + hd] = __uint_as_float(rmx_s[tid]);
@@ -671,6 +686,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   __shared__ __attribute__((aligned(16))) uint16_t Vt[2][64 * RS];   // [piece][dim][vpos(key)]
   __shared__ float Ms[64];
   __shared__ float Mx[8];                                             // per-wave max |K|, |V|
+  __shared__ __attribute__((aligned(16))) float Bkv[128];             // the K | V bias of this head
   constexpr int kMaxStagedTiles = 8;   // S <= 512: mask words staged, stored after the loop
   __shared__ uint32_t Wst[kDrop ? kMaxStagedTiles * 256 : 1];
 
@@ -708,6 +724,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     for (int ks = 0; ks < 4; ++ks) sp8(x[ks], sq, qf[ks]);
   }
 
+  // the head's K and V bias, once per workgroup (the staging adds them at every tile: from LDS,
+  // not 12 dependent global loads per tile and thread)
+  if (tid < 128) Bkv[tid] = qkv_bias ? (tid < 64 ? kbias[tid] : vbias[tid - 64]) : 0.f;
+  __syncthreads();
+
   // ---- tile staging: K rows (2 x 8 dims per thread), V key pairs x 4 dims (2 x 2 x 4)
   float4 kr[2][2], vr[2][2];
   float mr = 0.f;
@@ -729,20 +750,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // (+ bias) values of the loaded tile
   auto kvals = [&](int i, f32x8& f) {
     const int c8 = ((tid + 256 * i) & 7) * 8;
-    f = f32x8{kr[i][0].x, kr[i][0].y, kr[i][0].z, kr[i][0].w, kr[i][1].x, kr[i][1].y, kr[i][1].z, kr[i][1].w};
-    if (kbias) {
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] += kbias[c8 + j];
-    }
+    const float4 b0 = *reinterpret_cast<const float4*>(&Bkv[c8]), b1 = *reinterpret_cast<const float4*>(&Bkv[c8 + 4]);
+    f = f32x8{kr[i][0].x + b0.x, kr[i][0].y + b0.y, kr[i][0].z + b0.z, kr[i][0].w + b0.w,
+              kr[i][1].x + b1.x, kr[i][1].y + b1.y, kr[i][1].z + b1.z, kr[i][1].w + b1.w};
   };
   auto vvals = [&](int i, float (&v0)[4], float (&v1)[4]) {
     const int dq = (tid + 256 * i) >> 5;
     const float a[8] = {vr[i][0].x, vr[i][0].y, vr[i][0].z, vr[i][0].w, vr[i][1].x, vr[i][1].y, vr[i][1].z, vr[i][1].w};
+    const float4 bv = *reinterpret_cast<const float4*>(&Bkv[64 + 4 * dq]);
+    const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float bj = vbias ? vbias[4 * dq + j] : 0.f;
-      v0[j] = a[j] + bj;
-      v1[j] = a[4 + j] + bj;
+      v0[j] = a[j] + bb[j];
+      v1[j] = a[4 + j] + bb[j];
     }
   };
   // the loaded tile's max |K|, |V| -> this wave's slots (read after the next barrier)
@@ -921,19 +941,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     // colmax_part[b * query blocks + block][column]: the attention-output weight gradient's
     // per-column scale.  A column's 32 queries of a wave are the 32 lanes of a half.
     __shared__ float cmx_s[4][64];
+    // transposing max-reduction over the 32 queries of a half-wave: at each level (lane masks 16 ..
+    // 1) a lane keeps the half of its values its lane bit selects and takes the partner's other
+    // half; after 31 shuffles (not 32 x 5) lane l32 holds the max of value l32 over the half
+    float v[32];
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      float m0 = q < S ? fabsf(o0[i] * inv_l) : 0.f, m1 = q < S ? fabsf(o1[i] * inv_l) : 0.f;
+      v[i] = q < S ? fabsf(o0[i] * inv_l) : 0.f;
+      v[16 + i] = q < S ? fabsf(o1[i] * inv_l) : 0.f;
+    }
 #pragma unroll
-      for (int o = 1; o < 32; o <<= 1) {
-        m0 = fmaxf(m0, __shfl_xor(m0, o, 64));
-        m1 = fmaxf(m1, __shfl_xor(m1, o, 64));
+    for (int m = 16, n = 32; m >= 1; m >>= 1, n >>= 1) {
+      const bool up = (l32 & m) != 0;
+#pragma unroll
+      for (int j = 0; j < n / 2; ++j) {
+        const float keepv = up ? v[j + n / 2] : v[j], sendv = up ? v[j] : v[j + n / 2];
+        v[j] = fmaxf(keepv, __shfl_xor(sendv, m, 64));
       }
-      if (l32 == 0) {
-        const int d = 8 * (i >> 2) + 4 * h + (i & 3);
-        cmx_s[w][d] = m0;
-        cmx_s[w][32 + d] = m1;
-      }
+    }
+    {
+      const int k = l32 & 15;   // value l32: o0 (l32 < 16) or o1 (l32 >= 16) register k
+      const int d = 8 * (k >> 2) + 4 * h + (k & 3);
+      cmx_s[w][(l32 < 16 ? 0 : 32) + d] = v[0];
     }
     __syncthreads();
     if (tid < 64)

@@ -693,3 +693,27 @@ def test_attention_op_fp32_split(dev):
     _close(out, ref, rtol=2e-4, atol=2e-5)
     for a, r in zip(leaves, rl):
         _close(a.grad, r.grad, rtol=1e-3, atol=2e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('S,with_bias', [(128, True), (77, False)])
+def test_attention_f16_backward_scale_producers(dev, S, with_bias):
+    """The fp16x3 attention backward (one key block, S <= 128) writes the GEMM scale sources of
+    dQKV exactly: max |dQ|, |dK|, |dV| of each (token row, head) over the head's 192 columns, and
+    of each (sequence, column) over the rows."""
+    from hetseq_9cme_amd.ops._ext import C
+    torch.manual_seed(7)
+    B, nh, d = 2, 4, 64
+    H = nh * d
+    qkv = torch.randn(B, S, 3 * H, device=dev)
+    bias = (0.5 * torch.randn(3 * H, device=dev)) if with_bias else None
+    mb = torch.zeros(B, S, device=dev)
+    mb[1, S - 9:] = -10000.0
+    out, lse, dm = C().attn_fwd(qkv, mb, nh, 0.9, _seed(dev, 5), 3, bias)
+    dout = torch.randn(B, S, H, device=dev) * torch.pow(2.0, torch.linspace(-8, 8, S, device=dev))[None, :, None]
+    am = torch.full((B * S, nh), -1.0, device=dev)
+    cm = torch.full((B, 3 * H), -1.0, device=dev)
+    dqkv = C().attn_bwd_f16(dout, qkv, mb, out, lse, dm, nh, 0.9, bias, None, None, None, am, cm)[0]
+    g = dqkv.abs().view(B * S, 3, nh, d)
+    assert torch.equal(am, g.amax(-1).amax(1))
+    assert torch.equal(cm, dqkv.abs().amax(1))

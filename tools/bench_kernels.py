@@ -66,6 +66,15 @@ def bench_attn(B, S, nh=12, keep=0.9, dtype=torch.float32):
         report('attn_fwd_f16', timeit(lambda: C().attn_fwd_f16(qkv, mb, nh, keep, SEED, 0, None)), flops=f_fwd)
         report('attn_fwd_f16 (no dropout)', timeit(lambda: C().attn_fwd_f16(qkv, mb, nh, 1.0, SEED, 0, None)),
                flops=f_fwd)
+        # with the GEMM scale producers on (row max per (row, head), column max per query block)
+        H = qkv.shape[-1] // 3
+        am = torch.empty(B * S, nh, device=qkv.device)
+        cm = torch.empty(B * ((S + 127) // 128), H, device=qkv.device)
+        report('attn_fwd_f16 (+ row / col max)', timeit(lambda: C().attn_fwd_f16(qkv, mb, nh, keep, SEED, 0, None,
+                                                                                   am, cm)), flops=f_fwd)
+        bias = 0.1 * torch.randn(3 * H, device=qkv.device)
+        report('attn_fwd_f16 (+ max, + QKV bias: the step)', timeit(lambda: C().attn_fwd_f16(
+            qkv, mb, nh, keep, SEED, 0, bias, am, cm)), flops=f_fwd)
         report('attn_bwd_f16', timeit(lambda: C().attn_bwd_f16(dout, qkv, mb, out, lse, dm, nh, keep, None, None, None,
                                                                 None)[0]), flops=2.5 * f_fwd)
 

@@ -18,6 +18,8 @@ Reference sites: hetseq/bert_modeling.py:334-336 (Q/K/V), :383 (attention output
 :166-168 (FFN up, bias_gelu), :419 (FFN down), :509 (pooler), :522 (MLM transform), :538-547
 (MLM decoder), :1221 (NER classifier) and their backward products.
 """
+import os
+
 import torch
 
 from ._ext import C, use_kernels
@@ -266,6 +268,23 @@ def bf16_wt(W):
     return C().weight_bf16_t([W.detach().contiguous()])[0]
 
 
+_BF16_LIB = os.environ.get('HX_BF16_LIB', '1') != '0'
+
+
+def bf16_lib():
+    """--precision bf16 runs its plain products on hipBLASLt (HX_BF16_LIB=0: all on gemm_f16.hip)."""
+    return _BF16_LIB
+
+
 def mm_bf16(a2, b, out=None, beta=False, bias=None, out_bf16=True):
-    """a2 [M, K] bf16 . b^T (b bf16 [N, K]) (+ out) (+ bias) on the hand-written kernel."""
+    """a2 [M, K] bf16 . b^T (b bf16 [N, K]) (+ out) (+ bias).  Plain and beta products with a bf16
+    output go to hipBLASLt (the library's bf16 kernels are 20-35 % faster than the hand-written
+    bf16 variant on these shapes, r5m); the products with fused epilogues (bias + GELU, GELU
+    backward) stay on gemm_f16.hip."""
+    if _BF16_LIB and out_bf16 and a2.dtype == torch.bfloat16 and b.dtype == torch.bfloat16:
+        if beta:
+            return out.view(a2.shape[0], b.shape[0]).addmm_(a2, b.t())
+        if bias is not None:
+            return torch.addmm(bias.to(torch.bfloat16), a2, b.t())
+        return torch.mm(a2, b.t())
     return C().gemm_bf16(a2, b, out=out, beta=beta, bias=bias, out_bf16=out_bf16)

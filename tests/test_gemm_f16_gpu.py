@@ -246,11 +246,15 @@ def test_gemm_bf16_gelu_epilogues(dev, monkeypatch, cfg):
     assert torch.equal(slot, db)
 
 
-def test_ffn_bf16_autograd(dev):
+@pytest.mark.parametrize('lib', [True, False])
+def test_ffn_bf16_autograd(dev, monkeypatch, lib):
     """ops.ffn on bf16 activations (the --precision bf16 BERT FFN): output and every gradient
-    against the fp32 reference of the same op on the same bf16-rounded operands."""
-    from hetseq_9cme_amd.ops import fused
+    against the fp32 reference of the same op on the same bf16-rounded operands -- both routes:
+    hipBLASLt products with the bias-GELU passes (default) and the hand-written kernel's fused
+    GELU epilogues (HX_BF16_LIB=0)."""
+    from hetseq_9cme_amd.ops import fused, gemm16
     from hetseq_9cme_amd.ops.fused import gelu_ref
+    monkeypatch.setattr(gemm16, '_BF16_LIB', lib)
     g = torch.Generator(device=dev).manual_seed(17)
     T, H, I = 2048, 768, 3072
     x = torch.randn(4, T // 4, H, device=dev, generator=g).bfloat16().requires_grad_(True)

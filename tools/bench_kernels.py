@@ -75,6 +75,14 @@ def bench_attn(B, S, nh=12, keep=0.9, dtype=torch.float32):
         bias = 0.1 * torch.randn(3 * H, device=qkv.device)
         report('attn_fwd_f16 (+ max, + QKV bias: the step)', timeit(lambda: C().attn_fwd_f16(
             qkv, mb, nh, keep, SEED, 0, bias, am, cm)), flops=f_fwd)
+        slots = [torch.empty(H, device=qkv.device) for _ in range(3)]
+        report('attn_bwd_f16 (+ QKV bias grad)', timeit(lambda: C().attn_bwd_f16(
+            dout, qkv, mb, out, lse, dm, nh, keep, bias, *slots)[0]), flops=2.5 * f_fwd)
+        if S <= 128:
+            bam = torch.empty(B * S, nh, device=qkv.device)
+            bcm = torch.empty(B, 3 * H, device=qkv.device)
+            report('attn_bwd_f16 (+ bias grad, + max: the step)', timeit(lambda: C().attn_bwd_f16(
+                dout, qkv, mb, out, lse, dm, nh, keep, bias, *slots, bam, bcm)[0]), flops=2.5 * f_fwd)
         report('attn_bwd_f16', timeit(lambda: C().attn_bwd_f16(dout, qkv, mb, out, lse, dm, nh, keep, None, None, None,
                                                                 None)[0]), flops=2.5 * f_fwd)
 

@@ -747,22 +747,33 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     if (tid < 64) mr = kt + tid < S ? maskb[(int64_t)b * S + kt + tid] : -INFINITY;
   };
-  // (+ bias) values of the loaded tile
+  // the thread's K bias (its 8 columns are the same for both rows it stages) and V bias (4 dims of
+  // each of its two key pairs), in registers for the whole kernel
+  float4 kb[2], vb[2];
+  kb[0] = *reinterpret_cast<const float4*>(&Bkv[(tid & 7) * 8]);
+  kb[1] = *reinterpret_cast<const float4*>(&Bkv[(tid & 7) * 8 + 4]);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) vb[i] = *reinterpret_cast<const float4*>(&Bkv[64 + 4 * ((tid + 256 * i) >> 5)]);
+  auto add4 = [](float4& a, const float4& b) { a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w; };
+  // the loaded tile + bias, in place (once per tile, before its max and its split)
+  auto add_bias = [&]() {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      add4(kr[i][0], kb[0]);
+      add4(kr[i][1], kb[1]);
+      add4(vr[i][0], vb[i]);
+      add4(vr[i][1], vb[i]);
+    }
+  };
   auto kvals = [&](int i, f32x8& f) {
-    const int c8 = ((tid + 256 * i) & 7) * 8;
-    const float4 b0 = *reinterpret_cast<const float4*>(&Bkv[c8]), b1 = *reinterpret_cast<const float4*>(&Bkv[c8 + 4]);
-    f = f32x8{kr[i][0].x + b0.x, kr[i][0].y + b0.y, kr[i][0].z + b0.z, kr[i][0].w + b0.w,
-              kr[i][1].x + b1.x, kr[i][1].y + b1.y, kr[i][1].z + b1.z, kr[i][1].w + b1.w};
+    f = f32x8{kr[i][0].x, kr[i][0].y, kr[i][0].z, kr[i][0].w, kr[i][1].x, kr[i][1].y, kr[i][1].z, kr[i][1].w};
   };
   auto vvals = [&](int i, float (&v0)[4], float (&v1)[4]) {
-    const int dq = (tid + 256 * i) >> 5;
     const float a[8] = {vr[i][0].x, vr[i][0].y, vr[i][0].z, vr[i][0].w, vr[i][1].x, vr[i][1].y, vr[i][1].z, vr[i][1].w};
-    const float4 bv = *reinterpret_cast<const float4*>(&Bkv[64 + 4 * dq]);
-    const float bb[4] = {bv.x, bv.y, bv.z, bv.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      v0[j] = a[j] + bb[j];
-      v1[j] = a[4 + j] + bb[j];
+      v0[j] = a[j];
+      v1[j] = a[4 + j];
     }
   };
   // the loaded tile's max |K|, |V| -> this wave's slots (read after the next barrier)
@@ -823,6 +834,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   int ek, ev, ev_o = 0;                     // the tile's K / V exponents; o holds O 2^(ep + ev_o)
   const int nt = (S + 63) >> 6;
   stage_load(0);
+  add_bias();
   tile_max();
   __syncthreads();
   ek = f16_scale_exp(max4(Mx));
@@ -911,6 +923,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       HX_X3(o1, vb, pp);
     }
     if (t + 1 < nt) {
+      add_bias();
       tile_max();                // the next tile's max |K|, |V| (its loads have landed)
       __syncthreads();           // every wave is done with this tile's images; maxima published
       ek = f16_scale_exp(max4(Mx));

@@ -145,8 +145,18 @@ inline float* amax_ptr(const OptT& a, int64_t need, const char* what) {
   TORCH_CHECK(a->is_contiguous() && a->numel() >= need, what, ": needs ", need, " fp32 partials");
   return a->data_ptr<float>();
 }
+// pieces_out (fp32 runs, with amax_out): fp16 P2 pieces [rows, 2H] of the output at its row scales,
+// the consumer GEMM's A operand already split (gemm_f16 with fp16 A)
+inline uint16_t* pieces_ptr(const OptT& p, int64_t rows, int H, const OptT& amax, const char* what) {
+  if (!has(p)) return nullptr;
+  TORCH_CHECK(has(amax), what, ": pieces need the row maxima output too");
+  TORCH_CHECK(p->is_cuda() && p->scalar_type() == torch::kHalf && p->is_contiguous() && p->numel() == rows * 2 * H &&
+                  H % 16 == 0 && aligned16(p->data_ptr()), what, ": fp16 [rows, 2H] (H % 16 == 0)");
+  return reinterpret_cast<uint16_t*>(p->data_ptr());
+}
 std::vector<Tensor> ln_fwd(Tensor y, OptT bias, OptT res, Tensor gamma, Tensor beta, double eps, double keep_prob,
-                           const Tensor& seed, int64_t stream, bool drop_after, bool save_z, OptT amax_out) {
+                           const Tensor& seed, int64_t stream, bool drop_after, bool save_z, OptT amax_out,
+                           OptT pieces_out) {
   check_cuda(y, "input");
   const int H = (int)y.size(-1);
   const int64_t rows = y.numel() / H;
@@ -167,14 +177,16 @@ std::vector<Tensor> ln_fwd(Tensor y, OptT bias, OptT res, Tensor gamma, Tensor b
             gamma.data_ptr<float>(), beta.data_ptr<float>(), out.data_ptr(), save_z ? z.data_ptr() : nullptr,
             mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, H, (float)eps, (float)keep_prob, seed_ptr(seed),
             (uint64_t)stream, drop_after ? 1 : 0, cur_stream(y),
-            act_bf16(y) ? nullptr : amax_ptr(amax_out, rows, "ln_fwd amax"));
+            act_bf16(y) ? nullptr : amax_ptr(amax_out, rows, "ln_fwd amax"),
+            act_bf16(y) ? nullptr : pieces_ptr(pieces_out, rows, H, amax_out, "ln_fwd pieces"));
   dbg_finite(out, "ln_fwd");
   return {out, z, mean, rstd};
 }
 
 std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tensor gamma, double keep_prob,
                            const Tensor& seed, int64_t stream, bool drop_after, bool want_dy, bool want_dbias,
-                           OptT dgamma_out, OptT dbeta_out, OptT dbias_out, OptT amax_out, OptT colmax_out) {
+                           OptT dgamma_out, OptT dbeta_out, OptT dbias_out, OptT amax_out, OptT colmax_out,
+                           OptT pieces_out) {
   check_cuda(dout, "grad_output");
   check_cuda(z, "saved input");
   const int H = (int)z.size(-1);
@@ -196,7 +208,8 @@ std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tens
             (want_dy && want_dbias) ? 1 : 0, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(),
             want_dbias ? dbias.data_ptr<float>() : nullptr, 0, cur_stream(z),
             act_bf16(z) ? nullptr : amax_ptr(amax_out, rows, "ln_bwd amax"),
-            act_bf16(z) ? nullptr : amax_ptr(colmax_out, H, "ln_bwd colmax"));
+            act_bf16(z) ? nullptr : amax_ptr(colmax_out, H, "ln_bwd colmax"),
+            act_bf16(z) ? nullptr : pieces_ptr(pieces_out, rows, H, amax_out, "ln_bwd pieces"));
   dbg_finite(dz, "ln_bwd (dz)");
   return {dz, dy, dgamma, dbeta, dbias};
 }
@@ -508,6 +521,19 @@ Tensor amax_rows(Tensor x) {
   return out;
 }
 
+// fp32 rows [rows, K] -> fp16 P2 pieces [rows, 2K] at each row's scale (the max of its partials
+// amax [rows, P]): the pre-split A operand of gemm_f16*
+Tensor split_rows_f16(Tensor x, Tensor amax) {
+  check_af32(x, "split_rows_f16");
+  const ScaleSrc sa = scale_src(amax, x, x.size(0), "split_rows_f16");
+  TORCH_CHECK(sa.rs == sa.np, "split_rows_f16: per-row partials [rows, P]");
+  Tensor out = torch::empty({x.size(0), 2 * x.size(1)}, x.options().dtype(torch::kHalf));
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(x.device());
+  hx_split_rows_f16(x.data_ptr<float>(), x.stride(0), sa.p, sa.np, x.size(0), (int)x.size(1),
+                    reinterpret_cast<uint16_t*>(out.data_ptr()), cur_stream(x));
+  return out;
+}
+
 // [(wf, wt, rmax, cmax)] per weight W [N, K]: P2 fp16 pieces of W (rows scaled by their own
 // maxima) and of W^T (rows = columns of W, scaled by the column maxima); rmax [N, 1] / cmax [K, 1]
 // are the per-row scale sources of the forward / data-gradient products
@@ -548,14 +574,25 @@ std::vector<std::vector<Tensor>> split_weight_f16(std::vector<Tensor> Ws) {
   return out;
 }
 
+// A is fp32 [M, K], or its fp16 P2 pieces [M, 2K] split at the row scales of aa (split_rows_f16,
+// or a fused producer): then the kernel reads them as they are (no split in the k loop)
 static HxGemmF16 f16_args(const Tensor& a, const Tensor& aa, const Tensor& b, const Tensor& ba, const char* what) {
-  check_af32(a, what);
-  check_p2(b, a.size(1), what);
+  const bool pieces = a.scalar_type() == torch::kHalf;
+  if (pieces) {
+    TORCH_CHECK(a.is_cuda() && a.dim() == 2 && a.stride(1) == 1 && a.size(1) % 32 == 0 && a.stride(0) % 8 == 0 &&
+                    aligned16(a.data_ptr()) && a.size(0) < (1LL << 31) && aa.dim() == 2,
+                what, ": fp16 A pieces [M, 2K] (K % 16 == 0, 16-B rows) with per-row max |x| partials");
+  } else {
+    check_af32(a, what);
+  }
+  const int64_t K = pieces ? a.size(1) / 2 : a.size(1);
+  check_p2(b, K, what);
   TORCH_CHECK(b.device() == a.device() && b.size(0) < (1LL << 31), what, ": operands on one device");
-  const ScaleSrc sa = scale_src(aa, a, a.size(0), what), sb = scale_src(ba, a, b.size(0), what);
+  const ScaleSrc sa = scale_src(aa, b, a.size(0), what), sb = scale_src(ba, b, b.size(0), what);
   HxGemmF16 p{};
   p.A = a.data_ptr();
-  p.lda = a.stride(0);
+  p.lda = pieces ? a.stride(0) / 2 : a.stride(0);
+  p.apieces = pieces ? 1 : 0;
   p.a_amax = sa.p;
   p.na = sa.np;
   p.a_rs = sa.rs;
@@ -566,7 +603,7 @@ static HxGemmF16 f16_args(const Tensor& a, const Tensor& aa, const Tensor& b, co
   p.b_rs = sb.rs;
   p.M = (int)a.size(0);
   p.N = (int)b.size(0);
-  p.K = (int)a.size(1);
+  p.K = (int)K;
   p.ks = 1;
   return p;
 }
@@ -586,7 +623,7 @@ Tensor gemm_f16(Tensor a, Tensor a_amax, Tensor b, Tensor b_amax, OptT out_, boo
   TORCH_CHECK(!beta || has(out_), "gemm_f16: beta needs an output to accumulate into");
   if (ks <= 0) ks = hx_gemm_f16_ks(p.M, p.N, p.K, cfg);
   c10::hip::HIPGuardMasqueradingAsCUDA guard(a.device());
-  auto f32 = a.options();
+  auto f32 = a.options().dtype(torch::kFloat32);
   Tensor out = has(out_) ? *out_ : torch::empty({p.M, p.N}, f32);
   TORCH_CHECK(out.scalar_type() == torch::kFloat32 && out.dim() == 2 && out.size(0) == p.M && out.size(1) == p.N &&
                   out.stride(1) == 1 && out.stride(0) % 4 == 0 && aligned16(out.data_ptr()),
@@ -620,7 +657,7 @@ std::vector<Tensor> gemm_f16_gelu(Tensor a, Tensor a_amax, Tensor b, Tensor b_am
   check_vec(bias, p.N, "gemm_f16_gelu bias");
   const int cfg = hx_gemm_f16_plan(p.M, p.N, p.K);
   TORCH_CHECK(cfg >= 0, "gemm_f16_gelu: no tile for N = ", p.N);
-  auto f32 = a.options();
+  auto f32 = a.options().dtype(torch::kFloat32);
   Tensor c = torch::empty({p.M, p.N}, f32), h = torch::empty({p.M, p.N}, f32);
   Tensor rm = torch::empty({p.M, hx_gemm_f16_tn(p.N, cfg)}, f32), cm = torch::empty({hx_gemm_f16_tm(p.M, cfg), p.N}, f32);
   p.kind = 1;
@@ -652,7 +689,7 @@ std::vector<Tensor> gemm_f16_dgelu(Tensor a, Tensor a_amax, Tensor b, Tensor b_a
   const int cfg = hx_gemm_f16_plan(p.M, p.N, p.K);
   TORCH_CHECK(cfg >= 0, "gemm_f16_dgelu: no tile for N = ", p.N);
   const int prow = hx_gemm_f16_colpart_rows(p.M, cfg);
-  auto f32 = a.options();
+  auto f32 = a.options().dtype(torch::kFloat32);
   Tensor t = torch::empty({p.M, p.N}, f32);
   Tensor rm = torch::empty({p.M, hx_gemm_f16_tn(p.N, cfg)}, f32), cm = torch::empty({hx_gemm_f16_tm(p.M, cfg), p.N}, f32);
   Tensor part = torch::empty({prow, p.N}, f32);
@@ -985,11 +1022,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adadelta", &adadelta);
   m.def("ln_fwd", &ln_fwd, py::arg("y"), py::arg("bias"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
         py::arg("eps"), py::arg("keep_prob"), py::arg("seed"), py::arg("stream"), py::arg("drop_after"),
-        py::arg("save_z"), py::arg("amax_out") = py::none());
+        py::arg("save_z"), py::arg("amax_out") = py::none(), py::arg("pieces_out") = py::none());
   m.def("ln_bwd", &ln_bwd, py::arg("dout"), py::arg("z"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"),
         py::arg("keep_prob"), py::arg("seed"), py::arg("stream"), py::arg("drop_after"), py::arg("want_dy"),
         py::arg("want_dbias"), py::arg("dgamma_out"), py::arg("dbeta_out"), py::arg("dbias_out"),
-        py::arg("amax_out") = py::none(), py::arg("colmax_out") = py::none());
+        py::arg("amax_out") = py::none(), py::arg("colmax_out") = py::none(), py::arg("pieces_out") = py::none());
   m.def("ln_fwd_blocks", &hx_ln_fwd_blocks);
   m.def("ln_bwd_blocks", &hx_ln_bwd_blocks);
   m.def("embed_ln_fwd", &embed_ln_fwd, py::arg("ids"), py::arg("tt"), py::arg("wte"), py::arg("wpe"), py::arg("wtt"),
@@ -1020,6 +1057,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wgrad_bf16", &wgrad_bf16);
   m.def("wgrad_bf16_ok", &wgrad_bf16_ok);
   m.def("amax_rows", &amax_rows);
+  m.def("split_rows_f16", &split_rows_f16);
   m.def("amax_cols", &amax_cols);
   m.def("amax_rows_cols", &amax_rows_cols);
   m.def("split_weight_f16", &split_weight_f16);

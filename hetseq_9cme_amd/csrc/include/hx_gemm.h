@@ -111,5 +111,23 @@ __device__ __forceinline__ void split2(const f32x8 y, f16x8& h0, f16x8& h1) {
   h1 = __builtin_convertvector(y - __builtin_convertvector(h0, f32x8), f16x8);
 }
 
+// 4 consecutive fp32 values of a row (columns c .. c + 3, c % 4 == 0) -> their two pieces at scale
+// s, into the row's P2 image (piece p of column c at (c / 16) 32 + p 16 + c % 16): two 8-B stores.
+// Bit-identical to the GEMM's in-register split (s x is exact; the residual is exact in fp32).
+__device__ __forceinline__ void store_p2x4(uint16_t* __restrict__ row, int c, float4 v, float s) {
+  const float x[4] = {v.x * s, v.y * s, v.z * s, v.w * s};
+  uint32_t q0[2], q1[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const _Float16 a0 = (_Float16)x[2 * j], b0 = (_Float16)x[2 * j + 1];
+    const _Float16 a1 = (_Float16)(x[2 * j] - (float)a0), b1 = (_Float16)(x[2 * j + 1] - (float)b0);
+    q0[j] = __builtin_bit_cast(uint16_t, a0) | ((uint32_t)__builtin_bit_cast(uint16_t, b0) << 16);
+    q1[j] = __builtin_bit_cast(uint16_t, a1) | ((uint32_t)__builtin_bit_cast(uint16_t, b1) << 16);
+  }
+  uint16_t* p = row + (c >> 4) * 32 + (c & 15);
+  *reinterpret_cast<uint2*>(p) = make_uint2(q0[0], q0[1]);
+  *reinterpret_cast<uint2*>(p + 16) = make_uint2(q1[0], q1[1]);
+}
+
 }  // namespace g
 }  // namespace hx

@@ -30,11 +30,13 @@ int hx_ln_bwd_blocks(int64_t rows);
 int hx_ln_fwd_blocks(int64_t rows);
 void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, const float* gamma, const float* beta,
                void* out, void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob,
-               const uint64_t* seed, uint64_t stream, int drop_after, hipStream_t s, float* amax_part = nullptr);
+               const uint64_t* seed, uint64_t stream, int drop_after, hipStream_t s, float* amax_part = nullptr,
+               uint16_t* pieces = nullptr);   // pieces: fp16 P2 [rows][2H] of out at its row scales
 void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma,
                void* dz, void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
                uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
-               int accumulate, hipStream_t s, float* amax_part = nullptr, float* colmax = nullptr);
+               int accumulate, hipStream_t s, float* amax_part = nullptr, float* colmax = nullptr,
+               uint16_t* pieces = nullptr);   // pieces: of dy (dz without dy), as hx_ln_fwd
 void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,
                      const float* wtt, const float* gamma, const float* beta, void* out, void* zsave, float* mean,
                      float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, const uint64_t* seed,
@@ -140,9 +142,14 @@ struct HxGemmF16 {
   int dmode, ks;
   int64_t c_zs;
   int abf16, obf16;   // --precision bf16: bf16 operands (one pass), bf16 output C (kind 0)
+  int apieces;        // A is fp16 P2 pieces [M][2K] split at its row scale (lda counts 4-B k slots)
 };
 // --precision bf16: W^T [K][N] bf16 of every weight of a batch (wt used, wf / mask ignored)
 void hx_weight_bf16_t(const HxWeightBatch& d, hipStream_t s);
+// fp32 rows [rows][K] (row stride ldx) -> fp16 P2 pieces [rows][2K] at each row's scale (max of np
+// partials per row, amax[r np + j])
+void hx_split_rows_f16(const float* x, int64_t ldx, const float* amax, int np, int64_t rows, int K, uint16_t* out,
+                       hipStream_t s);
 int hx_gemm_f16_plan(int M, int N, int K);
 int hx_gemm_bf16_plan(int M, int N, int K);
 int hx_gemm_f16_tiles(int M, int N, int cfg);

@@ -82,7 +82,7 @@ __device__ __forceinline__ void split_pair_mix2(float x0, float x1, float s0, fl
 }
 
 struct F16Args {
-  const void* A;   // fp32 (AT 0) or bf16 (AT 1)
+  const void* A;   // fp32 (AT 0), bf16 (AT 1) or fp16 P2 pieces already split at the row scale (AT 2)
   int64_t lda;
   const float* a_amax;   // A row r's max |x| partials: a_amax[r a_rs + j], j < na (a_rs 0: one set, per tensor)
   int na, a_rs;
@@ -142,11 +142,13 @@ __device__ __forceinline__ void row_scales(const float* __restrict__ p, int np, 
 // The barrier opens step it + 1 straight into MFMAs: no wave waits on a fragment read after it.
 template <int BM, int BN, int WM, int WN, int EPI, int WGS, int NS, int AT = 0, int OB = 0, int DIL = 1>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) * WGS / 4) void gemm_f16_k(F16Args g) {
-  static_assert(AT == 0 || EPI == 0 || EPI == 3 || OB == 1, "bf16 operands: GELU epilogues in bf16");
+  static_assert(AT != 1 || EPI == 0 || EPI == 3 || OB == 1, "bf16 operands: GELU epilogues in bf16");
+  static_assert(AT >= 0 && AT <= 2, "operand kind");
+  constexpr bool BF = AT == 1;           // --precision bf16 (one pass, no scales)
   static_assert(OB == 0 || AT == 1, "bf16 output with bf16 operands");
   static_assert(NS >= 3 && NS <= 5, "ring depth");
-  constexpr int KD = AT ? 32 : 16;       // k elements per stage
-  constexpr int AE = AT ? 2 : 4;         // A element bytes
+  constexpr int KD = BF ? 32 : 16;       // k elements per stage
+  constexpr int AE = BF ? 2 : 4;         // A element bytes (AT 2: a row's two pieces take 4 B per k)
   constexpr int NWM = BM / WM, NWN = BN / WN, NW = NWM * NWN, NT = NW * 64;
   constexpr int MB = WM / 32, NB = WN / 32;
   constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64, STAGE = A_BYTES + B_BYTES;
@@ -214,9 +216,9 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
 
 #pragma unroll
   for (int i = 0; i < NS - 1; ++i) dma(i);
-  if constexpr (AT == 0) {
+  if constexpr (!BF) {
     // operand scales: per row (partials per row) or per tensor (one set of partials)
-    row_scales(g.a_amax, g.na, g.a_rs, m0, BM, mrows, tsa, tia, red);
+    row_scales(g.a_amax, g.na, g.a_rs, m0, BM, mrows, AT == 0 ? tsa : nullptr, tia, red);
     row_scales(g.b_amax, g.nb, g.b_rs, n0, BN, BN, nullptr, tib, red);
   }
   // stages 0 and 1 landed (NS = 4: stage 2 may still be in flight)
@@ -238,7 +240,55 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
   const int sw = 16 * ((l32 >> 2) & 3);   // chunk swizzle of the lane's rows (img_off)
   auto chunk = [&](int row_off, int ch) { return row_off + ((16 * ch) ^ sw); };
 
-  if constexpr (AT == 0) {
+  if constexpr (AT == 2) {
+    // A pieces written by their producer at the row scale (LayerNorm forward / backward): the
+    // fragments are read like B's and the k step is three MFMA passes and nothing else
+    struct Fr {
+      f16x8 a0[MB], a1[MB], b0[NB], b1[NB];
+    };
+    auto read = [&](const char* st, Fr& F) {
+#pragma unroll
+      for (int a = 0; a < MB; ++a) {
+        F.a0[a] = *reinterpret_cast<const f16x8*>(st + chunk(offa[a], h));
+        F.a1[a] = *reinterpret_cast<const f16x8*>(st + chunk(offa[a], 2 + h));
+      }
+#pragma unroll
+      for (int b = 0; b < NB; ++b) {
+        F.b0[b] = *reinterpret_cast<const f16x8*>(st + chunk(offb[b], h));
+        F.b1[b] = *reinterpret_cast<const f16x8*>(st + chunk(offb[b], 2 + h));
+      }
+    };
+    auto pass = [&](const Fr& F, int q) {
+#pragma unroll
+      for (int i = 0; i < MB * NB; ++i) {
+        const int a = i / NB, b = i % NB;
+        acc[a][b] = mfma16(q == 2 ? F.a1[a] : F.a0[a], q == 1 ? F.b1[b] : F.b0[b], acc[a][b]);
+      }
+    };
+    auto step = [&](int it, const Fr& Fc, Fr& Fn) {   // branch-free, as the AT 0 step
+      read(lds + ((it + 1) % NS) * STAGE, Fn);
+      pass(Fc, 0);
+#pragma unroll
+      for (int i = 0; i < MB * NB; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, (2 * MB + 2 * NB + MB * NB - 1) / (MB * NB), 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      dma(it + NS - 1);
+      __builtin_amdgcn_sched_barrier(0);
+      pass(Fc, 1);
+      pass(Fc, 2);
+      __builtin_amdgcn_sched_barrier(0);
+      wait_ring();
+      raw_barrier();
+    };
+    Fr F0, F1;
+    read(lds, F0);
+    for (int it = 0; it < nit; it += 2) {
+      step(it, F0, F1);
+      if (it + 1 < nit) step(it + 1, F1, F0);
+    }
+  } else if constexpr (AT == 0) {
     float sa[MB];
 #pragma unroll
     for (int a = 0; a < MB; ++a) sa[a] = tsa[wm * WM + 32 * a + l32];
@@ -409,12 +459,12 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
 #pragma unroll
   for (int b = 0; b < NB; ++b)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) ibc[b][i] = AT ? 1.f : tib[ncol + 32 * b + i];
+    for (int i = 0; i < 4; ++i) ibc[b][i] = BF ? 1.f : tib[ncol + 32 * b + i];
   auto tr = [&](int a, int b, int gq, float (&v)[4]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) v[i] = acc[a][b][4 * gq + i];
     transpose4(v, lane);
-    if constexpr (AT == 0) {
+    if constexpr (!BF) {
       const float ir = tia[mrow + 32 * a + 8 * gq];
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = v[i] * ir * ibc[b][i];
@@ -1084,6 +1134,23 @@ __global__ __launch_bounds__(256) void split_weight_f16_k(HxWeightBatch d, const
   }
 }
 
+// fp32 rows -> their P2 pieces at each row's own scale (the max of its partials): the A operand of
+// an AT 2 product when no fused producer wrote it (tests, and producers without a row-max pass)
+__global__ __launch_bounds__(256) void split_rows_f16_k(const float* __restrict__ x, int64_t ldx,
+                                                        const float* __restrict__ amax, int np, int64_t rows, int K,
+                                                        uint16_t* __restrict__ out) {
+  const int k4 = K / 4;
+  const int64_t n = rows * k4;
+  for (int64_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / k4;
+    const int c = (int)(i - r * k4) * 4;
+    float m = 0.f;
+    for (int j = 0; j < np; ++j) m = fmaxf(m, amax[r * np + j]);
+    const float4 v = *reinterpret_cast<const float4*>(x + r * ldx + c);
+    store_p2x4(out + r * 2 * K, c, v, ldexpf(1.f, f16_scale_exp(m)));
+  }
+}
+
 // --precision bf16: W [N][K] fp32 -> W^T [K][N] bf16 (RNE, as the bf16 shadow), every weight of a
 // batch in one launch, 64 x 64 tiles transposed through LDS
 __global__ __launch_bounds__(256) void weight_bf16_t_k(HxWeightBatch d) {
@@ -1125,6 +1192,13 @@ void hx_weight_bf16_t(const HxWeightBatch& d, hipStream_t s) {
 }
 
 // ---------------------------------------------------------------- host API (hx_launch.h)
+void hx_split_rows_f16(const float* x, int64_t ldx, const float* amax, int np, int64_t rows, int K, uint16_t* out,
+                       hipStream_t s) {
+  const int64_t n = rows * (K / 4);
+  if (n < 1) return;
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 8192);
+  split_rows_f16_k<<<blocks, 256, 0, s>>>(x, ldx, amax, np, rows, K, out);
+}
 void hx_fold_cols(const float* partial, int rows, int N, float* out, int accumulate, hipStream_t s) {
   hx::fold_rows(partial, rows, N, N, N, out, nullptr, nullptr, accumulate, s);
 }
@@ -1226,7 +1300,7 @@ int hx_gemm_f16(const HxGemmF16& p, int cfg, hipStream_t s) {
   const int ks = p.ks < 1 ? 1 : p.ks;
   if (p.K % (kd * ks) || (ks > 1 && (p.beta || p.kind || p.bias || p.obf16 || p.c_zs < (int64_t)(p.M - 1) * p.ldc + p.N)))
     return -1;
-  if ((p.abf16 && p.kind && !p.obf16) || (p.obf16 && (!p.abf16 || p.ldc % 4))) return -1;
+  if ((p.abf16 && p.kind && !p.obf16) || (p.obf16 && (!p.abf16 || p.ldc % 4)) || (p.apieces && p.abf16)) return -1;
   if (p.kind < 0 || p.kind > 2 || (p.kind && (!p.P || p.beta || p.ldp % 4)) || (p.kind == 2 && !p.aux)) return -1;
   F16Args a;
   a.A = p.A;
@@ -1263,6 +1337,13 @@ int hx_gemm_f16(const HxGemmF16& p, int cfg, hipStream_t s) {
     else if (p.obf16) launch_cfg<0, 1, 1>(cfg, a, s);
     else if (p.beta) launch_cfg<3, 1, 0>(cfg, a, s);
     else launch_cfg<0, 1, 0>(cfg, a, s);
+    return 0;
+  }
+  if (p.apieces) {   // A already split into P2 pieces by its producer
+    if (p.kind == 0 && !p.beta) launch_cfg<0, 2>(cfg, a, s);
+    else if (p.kind == 0) launch_cfg<3, 2>(cfg, a, s);
+    else if (p.kind == 1) launch_cfg<1, 2>(cfg, a, s);
+    else launch_cfg<2, 2>(cfg, a, s);
     return 0;
   }
   if (p.kind == 0 && !p.beta) launch_cfg<0>(cfg, a, s);

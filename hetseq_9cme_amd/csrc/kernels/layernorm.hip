@@ -15,6 +15,7 @@
 //     column partials of dgamma / dbeta / dbias that a second kernel folds; rows are
 //     grid-strided over a bounded number of workgroups so the partial slab stays small.
 // Activations may be fp32 or bf16 (T); statistics and affine params are fp32.
+#include "hx_gemm.h"
 #include "hx_launch.h"
 #include "hx_vec.h"
 #include "hx_reduce.h"
@@ -30,10 +31,24 @@ struct Row {
 };
 
 // max |x| of the wave's row -> amax_row[r] (the fp16x3 GEMMs' per-row operand scale, ops/gemm16.py)
-__device__ __forceinline__ void row_amax_out(float m, float* __restrict__ amax_row, int64_t r) {
+__device__ __forceinline__ float row_amax_out(float m, float* __restrict__ amax_row, int64_t r) {
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-  if ((threadIdx.x & 63) == 0) amax_row[r] = m;
+  if (amax_row && (threadIdx.x & 63) == 0) amax_row[r] = m;
+  return m;
+}
+// the row's fp16 P2 pieces at its own scale (row max m): the A operand of the consumer GEMM,
+// already split (gemm_f16.hip AT 2), [rows][2H]
+template <int CH>
+__device__ __forceinline__ void row_pieces_out(const Row<CH>& v, float m, uint16_t* __restrict__ pieces, int64_t r,
+                                               int H) {
+  const float sc = ldexpf(1.f, hx::g::f16_scale_exp(m));
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int j = (c * 64 + lane) * 4;
+    if (j < H) hx::g::store_p2x4(pieces + r * 2 * H, j, v.v[c], sc);
+  }
 }
 __device__ __forceinline__ float amax4(float m, float4 v) {
   return fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
@@ -47,7 +62,7 @@ __global__ __launch_bounds__(NT) void ln_fwd_k(const T* __restrict__ y, const fl
                                              T* __restrict__ zsave, float* __restrict__ mean_out,
                                              float* __restrict__ rstd_out, int64_t rows, int H, float eps,
                                              float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream,
-                                             float* __restrict__ amax_part) {
+                                             float* __restrict__ amax_part, uint16_t* __restrict__ pieces) {
   const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   const int lane = threadIdx.x & 63;
   const int64_t wave = blockIdx.x * (int64_t)WPB + (threadIdx.x >> 6);
@@ -119,9 +134,11 @@ __global__ __launch_bounds__(NT) void ln_fwd_k(const T* __restrict__ y, const fl
         }
         hx::store4(out + r * H + j, o);
         am = amax4(am, o);
+        x.v[c] = o;
       }
     }
-    if (amax_part) row_amax_out(am, amax_part, r);
+    if (pieces) row_pieces_out(x, row_amax_out(am, amax_part, r), pieces, r, H);
+    else if (amax_part) row_amax_out(am, amax_part, r);
   }
 }
 
@@ -134,7 +151,8 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
                                              const float* __restrict__ gamma, T* __restrict__ dz_out,
                                              T* __restrict__ dy_out, float* __restrict__ partial, int64_t rows,
                                              int H, float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream,
-                                             int want_dbias, float* __restrict__ amax_part, int want_cmax) {
+                                             int want_dbias, float* __restrict__ amax_part, int want_cmax,
+                                             uint16_t* __restrict__ pieces) {
   const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   __shared__ float red[WPB][CH * 256];
   const int lane = threadIdx.x & 63;
@@ -212,6 +230,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
         float4 dz = make_float4(rstd * (dv.x - m1 - xv.x * m2), rstd * (dv.y - m1 - xv.y * m2),
                                 rstd * (dv.z - m1 - xv.z * m2), rstd * (dv.w - m1 - xv.w * m2));
         hx::store4(dz_out + r * H + j, dz);
+        xh.v[c] = dz;   // the consumer GEMM's operand (dy below when separate): its pieces
         if (!dy_out) {
           am = amax4(am, dz);
           if (want_cmax) cmx.v[c] = hx::max4(cmx.v[c], hx::abs4(dz));
@@ -226,6 +245,7 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
             dy.w = (k & 8) ? dy.w * inv_keep : 0.f;
           }
           hx::store4(dy_out + r * H + j, dy);
+          xh.v[c] = dy;
           am = amax4(am, dy);
           if (want_cmax) cmx.v[c] = hx::max4(cmx.v[c], hx::abs4(dy));
           if (want_dbias) {
@@ -234,7 +254,8 @@ __global__ __launch_bounds__(NT) void ln_bwd_k(const T* __restrict__ dout, const
         }
       }
     }
-    if (amax_part) row_amax_out(am, amax_part, r);
+    if (pieces) row_pieces_out(xh, row_amax_out(am, amax_part, r), pieces, r, H);
+    else if (amax_part) row_amax_out(am, amax_part, r);
   }
   // fold the 4 waves' column partials through LDS (each accumulator selected at
   // compile time: a runtime-selected reference would demote them to scratch)
@@ -432,15 +453,15 @@ inline int ln_grid(int64_t rows, int cap) {
 template <typename T>
 void ln_fwd_t(const void* y, const float* bias, const void* res, const float* gamma, const float* beta, void* out,
               void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob, const uint64_t* seed,
-              uint64_t stream, int drop_after, hipStream_t s, float* amax_part) {
+              uint64_t stream, int drop_after, hipStream_t s, float* amax_part, uint16_t* pieces) {
   const int grid = ln_grid(rows, 4096);
   HX_CH_DISPATCH(H, {
     if (drop_after)
       ln_fwd_k<T, CH, true><<<grid, NT, 0, s>>>((const T*)y, bias, (const T*)res, gamma, beta, (T*)out, (T*)zsave,
-                                                mean, rstd, rows, H, eps, keep_prob, seed, stream, amax_part);
+                                                mean, rstd, rows, H, eps, keep_prob, seed, stream, amax_part, pieces);
     else
       ln_fwd_k<T, CH, false><<<grid, NT, 0, s>>>((const T*)y, bias, (const T*)res, gamma, beta, (T*)out, (T*)zsave,
-                                                 mean, rstd, rows, H, eps, keep_prob, seed, stream, amax_part);
+                                                 mean, rstd, rows, H, eps, keep_prob, seed, stream, amax_part, pieces);
   })
 }
 
@@ -448,15 +469,17 @@ template <typename T>
 void ln_bwd_t(const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma, void* dz,
               void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
               uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
-              int accumulate, hipStream_t s, float* amax_part, float* colmax) {
+              int accumulate, hipStream_t s, float* amax_part, float* colmax, uint16_t* pieces) {
   const int wc = colmax != nullptr;
   HX_CH_DISPATCH(H, {
     if (drop_after)
       ln_bwd_k<T, CH, true><<<nblk, NT, 0, s>>>((const T*)dout, (const T*)z, mean, rstd, gamma, (T*)dz, (T*)dy,
-                                                partial, rows, H, keep_prob, seed, stream, want_dbias, amax_part, wc);
+                                                partial, rows, H, keep_prob, seed, stream, want_dbias, amax_part, wc,
+                                                pieces);
     else
       ln_bwd_k<T, CH, false><<<nblk, NT, 0, s>>>((const T*)dout, (const T*)z, mean, rstd, gamma, (T*)dz, (T*)dy,
-                                                 partial, rows, H, keep_prob, seed, stream, want_dbias, amax_part, wc);
+                                                 partial, rows, H, keep_prob, seed, stream, want_dbias, amax_part, wc,
+                                                 pieces);
   })
   // partial is [nblk][4][H]: fold rows of length 4H into dgamma | dbeta | dbias (sums) and the
   // column maxima (max)
@@ -471,25 +494,26 @@ int hx_ln_fwd_blocks(int64_t rows) { return ln_grid(rows, 4096); }
 
 void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, const float* gamma, const float* beta,
                void* out, void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob,
-               const uint64_t* seed, uint64_t stream, int drop_after, hipStream_t s, float* amax_part) {
+               const uint64_t* seed, uint64_t stream, int drop_after, hipStream_t s, float* amax_part,
+               uint16_t* pieces) {
   if (bf16)
     ln_fwd_t<uint16_t>(y, bias, res, gamma, beta, out, zsave, mean, rstd, rows, H, eps, keep_prob, seed, stream,
-                       drop_after, s, nullptr);
+                       drop_after, s, nullptr, nullptr);
   else
     ln_fwd_t<float>(y, bias, res, gamma, beta, out, zsave, mean, rstd, rows, H, eps, keep_prob, seed, stream,
-                    drop_after, s, amax_part);
+                    drop_after, s, amax_part, pieces);
 }
 
 void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, const float* rstd, const float* gamma,
                void* dz, void* dy, float* partial, int nblk, int64_t rows, int H, float keep_prob, const uint64_t* seed,
                uint64_t stream, int drop_after, int want_dbias, float* dgamma, float* dbeta, float* dbias,
-               int accumulate, hipStream_t s, float* amax_part, float* colmax) {
+               int accumulate, hipStream_t s, float* amax_part, float* colmax, uint16_t* pieces) {
   if (bf16)
     ln_bwd_t<uint16_t>(dout, z, mean, rstd, gamma, dz, dy, partial, nblk, rows, H, keep_prob, seed, stream,
-                       drop_after, want_dbias, dgamma, dbeta, dbias, accumulate, s, nullptr, nullptr);
+                       drop_after, want_dbias, dgamma, dbeta, dbias, accumulate, s, nullptr, nullptr, nullptr);
   else
     ln_bwd_t<float>(dout, z, mean, rstd, gamma, dz, dy, partial, nblk, rows, H, keep_prob, seed, stream, drop_after,
-                    want_dbias, dgamma, dbeta, dbias, accumulate, s, amax_part, colmax);
+                    want_dbias, dgamma, dbeta, dbias, accumulate, s, amax_part, colmax, pieces);
 }
 
 void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,

@@ -283,15 +283,25 @@ def _amax_buf(rows, ref, bf16, bwd=False):
     return torch.empty(rows, 1, dtype=torch.float32, device=ref.device)
 
 
+def _pieces_buf(rows, H, ref, bwd=False):
+    """[rows, 2H] fp16 buffer for a LayerNorm kernel's output pieces (gemm16.attach_pieces), or None."""
+    if not gemm16.presplit(H, bwd):
+        return None
+    return torch.empty(rows, 2 * H, dtype=torch.float16, device=ref.device)
+
+
 # ----------------------------------------------------------------- bias + dropout + residual + LN
 class _BiasDropResLNFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, bias, res, gamma, beta, eps, p, mbox):
         keep = 1.0 - p
         seed, stream = get_rng().next(y.device) if p > 0 else (get_rng().seed_tensor(y.device), 0)
-        am = _amax_buf(y.numel() // y.shape[-1], y, y.dtype != torch.float32)
-        out, z, mean, rstd = C().ln_fwd(y, bias, res, gamma, beta, eps, keep, seed, stream, False, True, am)
+        rows, H = y.numel() // y.shape[-1], y.shape[-1]
+        am = _amax_buf(rows, y, y.dtype != torch.float32)
+        pc = _pieces_buf(rows, H, y) if am is not None else None
+        out, z, mean, rstd = C().ln_fwd(y, bias, res, gamma, beta, eps, keep, seed, stream, False, True, am, pc)
         gemm16.attach(out, am)   # fp16x3: its max |x| partials for the next QKV / FFN-up GEMM
+        gemm16.attach_pieces(out, pc)   # and its pieces, split at those row scales
         if am is not None:       # and its column bound for their weight gradients
             gemm16.attach_cols(out, gemm16.ln_affine(gamma, beta))
         ctx.save_for_backward(z, mean, rstd, gamma)
@@ -306,13 +316,15 @@ class _BiasDropResLNFn(torch.autograd.Function):
         keep, seed, stream, has_bias, has_res = ctx.meta
         bias, beta = ctx.params
         need_dy = has_bias or keep < 1.0
-        am = _amax_buf(z.numel() // z.shape[-1], z, z.dtype != torch.float32, bwd=True)
-        cm = torch.empty(1, z.shape[-1], dtype=torch.float32, device=z.device) if am is not None else None
+        rows, H = z.numel() // z.shape[-1], z.shape[-1]
+        am = _amax_buf(rows, z, z.dtype != torch.float32, bwd=True)
+        cm = torch.empty(1, H, dtype=torch.float32, device=z.device) if am is not None else None
+        pc = _pieces_buf(rows, H, z, True) if am is not None else None
         dz, dy, dgamma, dbeta, dbias = C().ln_bwd(dout.contiguous(), z, mean, rstd, gamma, keep, seed, stream,
                                                   False, need_dy, has_bias, grad_slot(gamma), grad_slot(beta),
-                                                  grad_slot(bias) if has_bias else None, am, cm)
-        # fp16x3: max |dy| per row (data gradient) and per column (weight gradient)
-        dy_ret = gemm16.attach_cols(gemm16.attach(dy if need_dy else dz, am), cm)
+                                                  grad_slot(bias) if has_bias else None, am, cm, pc)
+        # fp16x3: max |dy| per row (data gradient) and per column (weight gradient), and dy's pieces
+        dy_ret = gemm16.attach_pieces(gemm16.attach_cols(gemm16.attach(dy if need_dy else dz, am), cm), pc)
         dres = dz if has_res else None
         # dz is a private buffer only when dy is separate: then it can become the
         # accumulator of the consumer linear's dgrad GEMM
@@ -412,7 +424,8 @@ class _LinearFn(torch.autograd.Function):
             x2 = gemm16.rows2(x)
             ctx.xparts = gemm16.amax(x, x2)
             ctx.xcols = gemm16.cols_peek(x)
-            y, wt, ctx.wparts = gemm16.linear(x2, ctx.xparts, W, b)
+            xp = gemm16.take_pieces(x)   # the LayerNorm's pre-split copy of x, if it wrote one
+            y, wt, ctx.wparts = gemm16.linear(x2 if xp is None else xp, ctx.xparts, W, b)
             ctx.save_for_backward(x2, wt)
             return y.view(*x.shape[:-1], y.shape[-1])
         Wc = cast_w(W, x.dtype)
@@ -474,8 +487,10 @@ def _linear_backward_f16(ctx, dy):
     dy2 = gemm16.rows2(dy)
     dparts = gemm16.amax(dy, dy2)
     dcols = gemm16.cols(dy, dy2)
+    dp = gemm16.take_pieces(dy)
     xcols = ctx.xcols if ctx.xcols is not None else gemm16.cols(x2, x2)
-    dx = _f16_dgrad(dy2, dparts, wt, ctx.wparts, ctx.xshape, ctx.mbox) if ctx.needs_input_grad[0] else None
+    dx = (_f16_dgrad(dy2 if dp is None else dp, dparts, wt, ctx.wparts, ctx.xshape, ctx.mbox)
+          if ctx.needs_input_grad[0] else None)
     slot = grad_slot(W)
     side = side_begin(dy2.device, True) if slot is not None else None
     with torch.cuda.stream(side) if side is not None else _nullctx():
@@ -510,7 +525,8 @@ class _FFNFn(torch.autograd.Function):
         x2 = gemm16.rows2(x)
         xparts = gemm16.amax(x, x2)
         ctx.xcols = gemm16.cols_peek(x)
-        d, h, hparts, hcols, w1t, p1 = gemm16.gemm_gelu(x2, xparts, W1, b1)
+        xp = gemm16.take_pieces(x)
+        d, h, hparts, hcols, w1t, p1 = gemm16.gemm_gelu(x2 if xp is None else xp, xparts, W1, b1)
         y2, w2t, p2 = gemm16.linear(h, hparts, W2)
         ctx.save_for_backward(x2, d, h, w1t, w2t)
         ctx.parts = (xparts, hparts, p1, p2)
@@ -530,6 +546,7 @@ def _ffn_backward_f16(ctx, dy):
     dy2 = gemm16.rows2(dy)
     dparts = gemm16.amax(dy, dy2)
     dcols = gemm16.cols(dy, dy2)
+    dp = gemm16.take_pieces(dy)
     slot2, slot1 = grad_slot(W2), grad_slot(W1)
     # each weight gradient on the side stream, beside the next data-gradient GEMM
     side = side_begin(dy2.device, True) if slot2 is not None and slot1 is not None else None
@@ -539,7 +556,7 @@ def _ffn_backward_f16(ctx, dy):
         for t in (dy2, dparts, h, hparts, ctx.hcols):
             t.record_stream(side)
     # GELU backward in the FFN-down data-gradient epilogue: t = (dy W2) * gelu'(u), d b1
-    t, tparts, tcols, db1 = gemm16.gemm_dgelu(dy2, dparts, w2t, p2, d, grad_slot(ctx.b1))
+    t, tparts, tcols, db1 = gemm16.gemm_dgelu(dy2 if dp is None else dp, dparts, w2t, p2, d, grad_slot(ctx.b1))
     if side is not None:
         side = side_begin(dy2.device, True)   # after t
     xcols = ctx.xcols if ctx.xcols is not None else gemm16.cols(x2, x2)
@@ -694,7 +711,8 @@ class _Linear3Fn(torch.autograd.Function):
             x2 = gemm16.rows2(x)
             ctx.xparts = gemm16.amax(x, x2)
             ctx.xcols = gemm16.cols_peek(x)
-            y, wt, ctx.wparts = gemm16.linear(x2, ctx.xparts, W, b)
+            xp = gemm16.take_pieces(x)   # the LayerNorm's pre-split copy of x, if it wrote one
+            y, wt, ctx.wparts = gemm16.linear(x2 if xp is None else xp, ctx.xparts, W, b)
             ctx.save_for_backward(x2, wt)
             return y.view(*x.shape[:-1], y.shape[-1])
         Wc, bc = W, b

@@ -89,6 +89,41 @@ def amax(t, t2=None):
     return attach(t, C().amax_rows(x2))._hx_amax
 
 
+# LayerNorm outputs (forward) and gradients (backward) also travel with their fp16 P2 pieces, split
+# at the same row scales by the LayerNorm kernel (the values are in its registers anyway): the
+# consumer GEMM (QKV / FFN up forward, attention-output / FFN-down data gradient) then reads the
+# pieces instead of splitting fp32 in its k loop -- bit-identical results, 5-7 % faster products
+# (profiles/r5as_presplit_gemm_ab.log) for one extra 4 B / element write by the LayerNorm (+8 us per
+# call at BERT-base phase 1).  That pays in the forward (QKV -14 us, FFN up -15 us in the step) but
+# not in the backward (attention-output dgrad -4 us, FFN-down dgrad with its GELU epilogue -4 us):
+# the default splits in the forward LayerNorms only (profiles/r5av_presplit_step_ab.txt: 36.60 /
+# 36.67 / 36.77 ms for forward / off / both, medians of three on one box).
+_PRESPLIT = int(os.environ.get('HX_PRESPLIT', '1'))   # 0 off, 1 forward LayerNorms, 2 and backward
+
+
+def presplit(H, bwd=False):
+    """Should a LayerNorm of width H write its output's (bwd: its gradient's) pieces?"""
+    return _PRESPLIT >= (2 if bwd else 1) and _State.on and H % 16 == 0
+
+
+def attach_pieces(t, pieces):
+    if pieces is not None:
+        t._hx_p2 = pieces
+        t._hx_p2_ver = t._version
+    return t
+
+
+def take_pieces(t):
+    """The producer-written pieces of ``t`` (None if none / stale), handed over once: the attribute
+    is dropped so the pieces die with their one consumer GEMM."""
+    p = getattr(t, '_hx_p2', None)
+    if p is None:
+        return None
+    ok = getattr(t, '_hx_p2_ver', -1) == t._version
+    del t._hx_p2
+    return p if ok else None
+
+
 def attach_cols(t, src):
     """Hand the weight gradients that consume ``t`` its per-COLUMN scale source: a [P, C] tensor of
     column-max partials (producer-written), or ``('affine', gamma, beta, z, mul)`` for a LayerNorm
@@ -176,7 +211,7 @@ def weight_pieces(W):
 
 # ---------------------------------------------------------------- products
 def mm(a2, a_parts, b, b_parts, out=None, beta=False, bias=None, ks=0):
-    """a2 [M, K] (fp32) . b^T (b = P2 pieces [N, 2K]) (+ out if beta) (+ bias) -> fp32 [M, N];
+    """a2 [M, K] (fp32, or its fp16 P2 pieces [M, 2K] at the row scales of a_parts) . b^T (b = P2 pieces [N, 2K]) (+ out if beta) (+ bias) -> fp32 [M, N];
     ``a_parts`` / ``b_parts``: per-row max |x| partials of a2 and of b's rows;
     ``ks``: split-K slabs (0 = the kernel's plan: deep reductions with few output tiles)."""
     return C().gemm_f16(a2, a_parts, b, b_parts, out=out, beta=beta, bias=bias, ks=ks)

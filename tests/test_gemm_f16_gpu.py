@@ -430,3 +430,72 @@ def test_amax_rows_cols_one_pass(rows, cols):
     r, c = C().amax_rows_cols(x)
     assert torch.equal(r, x.abs().amax(1, keepdim=True))
     assert torch.equal(c, x.abs().amax(0, keepdim=True))
+
+
+@pytest.mark.parametrize('cfg', ['plan', '0', '2', '3', '4', '5', '6'])
+def test_gemm_f16_presplit_a_bitwise(dev, monkeypatch, cfg):
+    """A handed over already split into fp16 P2 pieces at its row scales (split_rows_f16, or a
+    LayerNorm's pieces_out) is read as it is (AT 2: no split in the k loop) and gives results
+    bit-identical to the fp32 A split in registers -- every epilogue, ragged M, rows ramped over
+    2^-20 .. 2^20."""
+    if cfg != 'plan':
+        monkeypatch.setenv('HX_GEMM_F16_CFG', cfg)
+    g = torch.Generator(device=dev).manual_seed(31)
+    M, N, K = 4096 + 37, 768, 768
+    a = torch.randn(M, K, device=dev, generator=g) * torch.pow(2.0, torch.linspace(-20, 20, M, device=dev))[:, None]
+    am = C().amax_rows(a)
+    ap = C().split_rows_f16(a, am)
+    assert ap.dtype == torch.float16 and ap.shape == (M, 2 * K)
+    W = torch.randn(N, K, device=dev, generator=g) * 0.02
+    wf, wt, rmax, cmax = _pieces(W)
+    b = torch.randn(N, device=dev, generator=g)
+    assert torch.equal(C().gemm_f16(a, am, wf, rmax, bias=b), C().gemm_f16(ap, am, wf, rmax, bias=b))
+    acc = torch.randn(M, N, device=dev, generator=g)
+    o0, o1 = acc.clone(), acc.clone()
+    C().gemm_f16(a, am, wf, rmax, out=o0, beta=True)
+    C().gemm_f16(ap, am, wf, rmax, out=o1, beta=True)
+    assert torch.equal(o0, o1)
+    for p, q in zip(C().gemm_f16_gelu(a, am, wf, rmax, b, 1), C().gemm_f16_gelu(ap, am, wf, rmax, b, 1)):
+        assert torch.equal(p, q)
+    u = torch.randn(M, N, device=dev, generator=g)
+    for p, q in zip(C().gemm_f16_dgelu(a, am, wf, rmax, u, None, None, 1),
+                    C().gemm_f16_dgelu(ap, am, wf, rmax, u, None, None, 1)):
+        assert torch.equal(p, q)
+
+
+def test_gemm_f16_presplit_a_split_k(dev):
+    """Pre-split A through the split-K slabs (deep K): bit-identical to the fp32 operand."""
+    g = torch.Generator(device=dev).manual_seed(37)
+    M, N, K = 512, 768, 3072
+    a = torch.randn(M, K, device=dev, generator=g)
+    am = C().amax_rows(a)
+    W = torch.randn(N, K, device=dev, generator=g) * 0.02
+    wf, wt, rmax, cmax = _pieces(W)
+    assert torch.equal(C().gemm_f16(a, am, wf, rmax, ks=3), C().gemm_f16(C().split_rows_f16(a, am), am, wf, rmax, ks=3))
+
+
+def test_layernorm_pieces_out(dev):
+    """LayerNorm forward / backward write their output's P2 pieces at the row scales they compute
+    (the consumer GEMM's A operand, pre-split): equal to split_rows_f16 of the fp32 output."""
+    g = torch.Generator(device=dev).manual_seed(41)
+    rows, H = 4096 + 3, 768
+    seed = torch.full((1,), 1234, dtype=torch.int64, device=dev)
+    y = torch.randn(rows, H, device=dev, generator=g)
+    res = torch.randn(rows, H, device=dev, generator=g)
+    bias = torch.randn(H, device=dev, generator=g)
+    gamma = torch.randn(H, device=dev, generator=g)
+    beta = torch.randn(H, device=dev, generator=g)
+    am = torch.empty(rows, 1, device=dev)
+    pc = torch.empty(rows, 2 * H, dtype=torch.float16, device=dev)
+    out, z, mean, rstd = C().ln_fwd(y, bias, res, gamma, beta, 1e-12, 0.9, seed, 3, False, True, am, pc)
+    assert torch.equal(am, out.abs().amax(1, keepdim=True))
+    assert torch.equal(pc, C().split_rows_f16(out, am))
+    dout = torch.randn(rows, H, device=dev, generator=g) * 1e-3
+    for want_dy in (True, False):
+        bm = torch.empty(rows, 1, device=dev)
+        bp = torch.empty(rows, 2 * H, dtype=torch.float16, device=dev)
+        dz, dy, _, _, _ = C().ln_bwd(dout, z, mean, rstd, gamma, 0.9, seed, 3, False, want_dy, want_dy, None, None,
+                                     None, bm, None, bp)
+        src = dy if want_dy else dz
+        assert torch.equal(bm, src.abs().amax(1, keepdim=True))
+        assert torch.equal(bp, C().split_rows_f16(src, bm))

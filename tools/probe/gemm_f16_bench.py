@@ -87,9 +87,59 @@ def wgrad_sweep(C, dev, plans):
     os.environ.pop('HX_WGRAD_F16', None)
 
 
+def pieces_ab(C, dev, reps):
+    """A read as fp32 and split in the k loop vs A pre-split into P2 pieces (split_rows_f16), on the
+    four products whose A operand a LayerNorm produces; alternated `reps` times on one box, and the
+    outputs compared bit for bit (the split is the same rounding either way)."""
+    T = int(os.environ.get('T', '16384'))
+    g = torch.Generator(device=dev).manual_seed(0)
+    for (name, N, K) in [('qkv fwd', 2304, 768), ('ffn_up fwd', 3072, 768), ('ffn_down dgrad', 3072, 768),
+                         ('attn_out dgrad', 768, 768)]:
+        x = torch.randn(T, K, device=dev, generator=g)
+        W = torch.randn(N, K, device=dev, generator=g) * 0.03
+        b = torch.randn(N, device=dev, generator=g)
+        xp = C().amax_rows(x)
+        xs = C().split_rows_f16(x, xp)
+        wf, wt, wp, wc = C().split_weight_f16([W])[0]
+        if name == 'ffn_up fwd':
+            def run(a):
+                return C().gemm_f16_gelu(a, xp, wf, wp, b, 1)
+        elif name == 'ffn_down dgrad':
+            u = torch.randn(T, N, device=dev, generator=g)
+            db = torch.zeros(N, device=dev)
+
+            def run(a):
+                return C().gemm_f16_dgelu(a, xp, wf, wp, u, None, db, 1)
+        elif name == 'attn_out dgrad':
+            acc = torch.randn(T, N, device=dev, generator=g)
+
+            def run(a):
+                return [C().gemm_f16(a, xp, wf, wp, out=acc.clone(), beta=True)]
+        else:
+            def run(a):
+                return [C().gemm_f16(a, xp, wf, wp, bias=b)]
+        r0, r1 = run(x), run(xs)
+        same = all(torch.equal(p, q) for p, q in zip(r0, r1) if p.dtype == torch.float32)
+        t0, t1 = [], []
+        for _ in range(reps):
+            t0.append(timed(lambda: run(x)))
+            t1.append(timed(lambda: run(xs)))
+        t0.sort()
+        t1.sort()
+        print('{:16s} fp32 A {:7.1f} us  pieces A {:7.1f} us  ({:+.1f} %)  bitwise equal: {}  [{}] [{}]'.format(
+            name, t0[reps // 2], t1[reps // 2], 100 * (t1[reps // 2] / t0[reps // 2] - 1), same,
+            ' '.join('%.0f' % v for v in t0), ' '.join('%.0f' % v for v in t1)), flush=True)
+        x16 = C().split_rows_f16(x, xp)
+        us = timed(lambda: C().split_rows_f16(x, xp))
+        print('{:16s} split_rows_f16 (standalone) {:6.1f} us'.format(name, us), flush=True)
+        del x16
+
+
 def main():
     from hetseq_9cme_amd.ops._ext import C
     dev = torch.device('cuda', 0)
+    if os.environ.get('PIECES_AB'):
+        return pieces_ab(C, dev, int(os.environ['PIECES_AB']))
     if os.environ.get('WGRAD_PLANS'):
         return wgrad_sweep(C, dev, os.environ['WGRAD_PLANS'].split(','))
     if os.environ.get('CFGS'):

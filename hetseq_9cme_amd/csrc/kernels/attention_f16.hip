@@ -49,12 +49,17 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int D = 64;
 constexpr int RS = 72;    // [query][dim] image row stride (halves): conflict-free 16-B fragment reads
-constexpr int DSF = 132;  // fp32 dS [query][128 keys] row stride (floats): conflict-free dQ fragment reads
+// fp32 dS [query][128 keys]: 144-float rows, the two 4-float halves of each 8-float unit swapped
+// on rows with bit 2 set -- conflict-free dQ fragment reads and dS stores (tools/probe/
+// lds_conflicts.py models them with the lane groups of MI355X_MICROARCH.md §LDS; the previous
+// unswizzled 132-float rows cost 4 extra cycles per ds_read_b128).  Row bit 2 is a lane constant at
+// every access (h at the stores, r16 at the reads), so the addresses keep additive constants.
+constexpr int DSF = 144;
 constexpr int DS_B = 32 * DSF * 4, QS_B = 32 * RS * 2;
 constexpr int NSC = 16;   // per-tile scalars: max |Q|, max |dO|, max |dS| per wave (+ spare)
 constexpr int KRS = 72;   // K image [128 keys][64 dims] row stride (halves)
 constexpr int KI_B = 128 * KRS * 2;
-// 71 KiB: two workgroups (two waves per SIMD) per CU
+// 73 KiB: two workgroups (two waves per SIMD) per CU
 constexpr int BWD_SMEM = 2 * KI_B + DS_B + 2 * (2 * QS_B) + (32 + 128 + NSC) * 4;
 constexpr int kNoScale = 120;   // exponent of an operand seen only as zeros so far (no constraint)
 
@@ -175,6 +180,7 @@ __device__ __forceinline__ Blk xcd_block() {
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
 // B operand (8 consecutive k = image rows r0 .. r0 + 7, one column per lane) of a row-major fp16
 // image through two ds_read_b64_tr_b16: per 16-lane group, lane 4q + p addresses row q (+4),
 // columns c0 + 4p .. +3, and lane i receives column c0 + i of the four rows (T10)
@@ -202,7 +208,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   uint16_t* Qs = reinterpret_cast<uint16_t*>(smem + 2 * KI_B + DS_B);    // [2][32][RS]
   uint16_t* dOs = Qs + 2 * 32 * RS;                                      // [2][32][RS]
   float* Ls = reinterpret_cast<float*>(smem + 2 * KI_B + DS_B + 4 * QS_B);   // [32] lse
-  float* Ds = Ls + 32;                                                   // [32][4 waves] D partials
+  float* Ds = Ls + 32;                                                   // [32] D = rowsum(dO * O)
   float* Sc = Ds + 128;                                                  // per-tile scalars
   float* ScQ = Sc, *ScD = Sc + 4, *ScS = Sc + 8;                         // [4 waves] each
 
@@ -264,8 +270,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const uint32_t* dmask_bh = kDrop ? dmask + bh * Sp * nwords : nullptr;
   const int moff = mykey * nwords;
 
-  // staging unit of this thread: query pair (2sqp, 2sqp+1) x dims 4sdq .. 4sdq+3
-  const int sqp = tid & 15, sdq = tid >> 4;
+  // staging unit of this thread: query pair (2sqp, 2sqp+1) x dims 4sdq .. 4sdq+3 -- the 16 lanes of
+  // a group share the query pair, so each image store of the group fills one row (conflict-free:
+  // with the lanes on 16 rows a ds_write_b64 took 4x its cycles) and D = rowsum(dO * O) completes
+  // inside the group
+  const int sqp = tid >> 4, sdq = tid & 15;
   float4 pq[2], pd[2], po[2];
   float pl = 0.f;
   uint32_t pm = 0;
@@ -369,26 +378,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     }
     float e0 = pd[0].x * po[0].x + pd[0].y * po[0].y + pd[0].z * po[0].z + pd[0].w * po[0].w;
     float e1 = pd[1].x * po[1].x + pd[1].y * po[1].y + pd[1].z * po[1].z + pd[1].w * po[1].w;
-    // this wave's 16 dims (lanes 16 apart), then one partial per wave: Ds[query][wave]
-    e0 += __shfl_xor(e0, 16, 64);
-    e1 += __shfl_xor(e1, 16, 64);
-    e0 += __shfl_xor(e0, 32, 64);
-    e1 += __shfl_xor(e1, 32, 64);
-    if (lane < 16) {
-      Ds[(2 * sqp) * 4 + w] = e0;
-      Ds[(2 * sqp + 1) * 4 + w] = e1;
+    // the 64 dims of the query pair sit on the 16 lanes of the group
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      e0 += __shfl_xor(e0, o, 64);
+      e1 += __shfl_xor(e1, o, 64);
+    }
+    if (sdq == 0) {
+      Ds[2 * sqp] = e0;
+      Ds[2 * sqp + 1] = e1;
     }
     if (tid < 32) Ls[tid] = qt + tid < S ? pl : INFINITY;   // rows past S: P = 0
   };
   // dims l32 (t0) and 32 + l32 (t1) of image rows 16 half + 8h .. +7, transposed
   const int gcol = 16 * ((lane >> 4) & 1), li = lane & 15;
-  auto load_img = [&](const uint16_t* img, int half, f16x8 (&t0)[2], f16x8 (&t1)[2]) {
-#pragma unroll
-    for (int p = 0; p < 2; ++p) {
-      t0[p] = tr8(img + p * 32 * RS, RS, 16 * half + 8 * h, gcol, li);
-      t1[p] = tr8(img + p * 32 * RS, RS, 16 * half + 8 * h, 32 + gcol, li);
-    }
-  };
 
   stage(0);
   uint32_t mnext = pm;
@@ -430,11 +433,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         keeps = kb ? keep_s : 0.f;
       }
       sa[r] = p * keeps;
-      const float4 dq4 = *reinterpret_cast<const float4*>(&Ds[4 * qr]);
-      const float ds = p * (dpa[r] * fd * keepf - ((dq4.x + dq4.y) + (dq4.z + dq4.w)));
+      const float ds = p * (dpa[r] * fd * keepf - Ds[qr]);
       dpa[r] = ds;
       smax = fmaxf(smax, fabsf(ds));
-      dSf[qr * DSF + w * 32 + l32] = ds;
+      dSf[qr * DSF + w * 32 + (l32 ^ (4 * h))] = ds;   // row bit 2 of crow(r, h) is h
     }
     smax = wave_max(smax);
     if (lane == 0) ScS[w] = smax;
@@ -478,12 +480,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       eq = min(eq, run_exp(max4(ScQ)));
       ed = min(ed, run_exp(max4(ScD)));
     }
-    // ---- dQ = dS . K over the block's 128 keys (16x16x32 tiles)
+    // ---- dQ = dS . K over the block's 128 keys (16x16x32 tiles); dq_sw: this lane row's half swap
+    const int dq_sw = 4 * ((r16 >> 2) & 1);
     f32x4 qa0 = {0.f, 0.f, 0.f, 0.f}, qa1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const float* src = &dSf[(qh * 16 + r16) * DSF + 32 * ks + 8 * kg];
-      const float4 x0 = *reinterpret_cast<const float4*>(src), x1 = *reinterpret_cast<const float4*>(src + 4);
+      const float4 x0 = *reinterpret_cast<const float4*>(src + dq_sw),
+                   x1 = *reinterpret_cast<const float4*>(src + 4 - dq_sw);
       f16x8 a[2], b0[2], b1[2];
       sp8(f32x8{x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w}, st, a);
 #pragma unroll

@@ -299,6 +299,9 @@ def test_gemm_f16_every_tile(dev, monkeypatch, cfg):
     ref2 = acc.double() + dy.double() @ W.double()
     den2 = acc.abs().double() + dy.abs().double() @ W.abs().double()
     assert ((o2.double() - ref2).abs() / den2).max().item() < 4e-6
+    # an odd number of k steps per slab (16 slabs of 3 steps): the loop's last step is unpaired
+    o3 = C().gemm_f16(a, C().amax_rows(a), wf, rmax, bias=bias, ks=16)
+    assert ((o3.double() - ref).abs() / den).max().item() < 4e-6
 
 
 @pytest.mark.parametrize('plan', ['0:1', '0:5', '1:1', '1:3'])

@@ -10,10 +10,12 @@
 // the fp32 accumulator, and the scales are undone exactly in the epilogue.  Half the matrix-core
 // work of bf16x6 at fp32-class accuracy (tests/test_gemm_f16_gpu.py: fp64-referenced errors).
 //
-// Operands: activations and gradients are read AS fp32 and split in registers here -- no piece
-// tensors are written or read in HBM (fp32 = 4 B per element; three bf16 pieces were 6) -- and
-// their scale comes from the max |x| partials written by their producer (LayerNorm, attention,
-// this kernel's own epilogues) or by hx_amax_rows.  Weights are split once per forward
+// Operands: activations and gradients are read AS fp32 and split in registers here (fp32 = 4 B per
+// element; three bf16 pieces were 6), and their scale comes from the max |x| partials written by
+// their producer (LayerNorm, attention, this kernel's own epilogues) or by hx_amax_rows.  A
+// producer that knows a whole row when it writes it (the forward LayerNorms, ops/gemm16.py
+// presplit) may instead hand over the row's two pieces, split at that same scale (AT 2: the same
+// 4 B per element, read like B, no split in the k loop; bit-identical).  Weights are split once per forward
 // (split_weight_f16_many_k) into the "P2" piece layout: element (r, p, k) at r 2K + (k / 16) 32 +
 // p 16 + k % 16, so one 16-deep k step of a row is 64 contiguous bytes holding both pieces.
 //

@@ -10,9 +10,10 @@ travels with **max |x| partials per row**: a [rows, P] fp32 tensor whose row-wis
 row's max |x| (its producer writes it -- LayerNorm [rows, 1], attention [rows, heads], this
 module's GELU epilogues [rows, N tiles] -- or ``amax`` computes it in one read pass).  A 1-D
 tensor instead is a per-tensor bound (e.g. ``bound``).  The GEMMs read activations and gradients
-AS fp32 and split them in registers; only weights are split ahead of time (one launch per forward
-for the whole encoder, ``weight_scope``), W's rows scaled by their own maxima and W^T's rows
-(= W's columns) by the column maxima.
+AS fp32 and split them in registers -- except the forward LayerNorms' outputs, which travel with
+their pieces already split (``attach_pieces``, ``HX_PRESPLIT``); weights are split ahead of time
+(one launch per forward for the whole encoder, ``weight_scope``), W's rows scaled by their own
+maxima and W^T's rows (= W's columns) by the column maxima.
 
 Reference sites: hetseq/bert_modeling.py:334-336 (Q/K/V), :383 (attention output), :409 +
 :166-168 (FFN up, bias_gelu), :419 (FFN down), :509 (pooler), :522 (MLM transform), :538-547

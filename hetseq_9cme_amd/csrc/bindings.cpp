@@ -389,11 +389,11 @@ std::vector<Tensor> attn_fwd_f16(Tensor qkv, Tensor mask_bias, int64_t nh, doubl
   return attn_fwd(qkv, mask_bias, nh, keep, seed, stream, bias, 2, amax_out, colmax_out);
 }
 
-// returns {dqkv, dbias} (dbias: [3H] fp32 when bias is given -- written into dbq/dbk/dbv
-// when those slots are given -- else an empty tensor)
+// returns {dqkv, dbias} (dbias: [3H] fp32 when bias is given or want_dbias -- written into
+// dbq/dbk/dbv when those slots are given -- else an empty tensor)
 std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask,
                              int64_t nh, double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, int split = 0,
-                             OptT amax_out = OptT(), OptT colmax_out = OptT()) {
+                             OptT amax_out = OptT(), OptT colmax_out = OptT(), bool want_dbias = false) {
   // split: 0 none (fp32 / bf16 MFMA), 2 fp16x3 (attention_f16.hip)
   check_cuda(dout, "grad_output");
   check_cuda(qkv, "qkv");
@@ -422,7 +422,9 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor o
   }
   Tensor dbias, part;
   float *pq = nullptr, *pk = nullptr, *pv = nullptr;
-  if (has(bias)) {
+  // the QKV-bias gradient: when the bias is added here, or (want_dbias) when the projection
+  // already added it and only its gradient -- the column sums of dQKV -- is wanted
+  if (has(bias) || want_dbias) {
     const bool slots = has(dbq) && has(dbk) && has(dbv);
     if (slots) {
       for (const auto* t : {&dbq, &dbk, &dbv}) {
@@ -1044,16 +1046,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("seed"), py::arg("stream"), py::arg("bias"), py::arg("amax_out") = py::none(),
         py::arg("colmax_out") = py::none());
   m.def("attn_bwd", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
-                       double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv) {
-    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, 0);
-  });
-  // fp32 attention backward on the fp16 matrix cores (fp16x3, attention_f16.hip)
-  m.def("attn_bwd_f16", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
-                           double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, OptT amax_out, OptT colmax_out) {
-    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, 2, amax_out, colmax_out);
+                       double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, bool want_dbias) {
+    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, 0, OptT(), OptT(), want_dbias);
   }, py::arg("dout"), py::arg("qkv"), py::arg("mask_bias"), py::arg("out"), py::arg("lse"), py::arg("dmask"),
      py::arg("nh"), py::arg("keep"), py::arg("bias"), py::arg("dbq"), py::arg("dbk"), py::arg("dbv"),
-     py::arg("amax_out") = py::none(), py::arg("colmax_out") = py::none());
+     py::arg("want_dbias") = false);
+  // fp32 attention backward on the fp16 matrix cores (fp16x3, attention_f16.hip)
+  m.def("attn_bwd_f16", [](Tensor dout, Tensor qkv, Tensor mask_bias, Tensor out, Tensor lse, Tensor dmask, int64_t nh,
+                           double keep, OptT bias, OptT dbq, OptT dbk, OptT dbv, OptT amax_out, OptT colmax_out,
+                           bool want_dbias) {
+    return attn_bwd(dout, qkv, mask_bias, out, lse, dmask, nh, keep, bias, dbq, dbk, dbv, 2, amax_out, colmax_out,
+                    want_dbias);
+  }, py::arg("dout"), py::arg("qkv"), py::arg("mask_bias"), py::arg("out"), py::arg("lse"), py::arg("dmask"),
+     py::arg("nh"), py::arg("keep"), py::arg("bias"), py::arg("dbq"), py::arg("dbk"), py::arg("dbv"),
+     py::arg("amax_out") = py::none(), py::arg("colmax_out") = py::none(), py::arg("want_dbias") = false);
   m.def("wgrad_bf16", &wgrad_bf16);
   m.def("wgrad_bf16_ok", &wgrad_bf16_ok);
   m.def("amax_rows", &amax_rows);

@@ -176,6 +176,12 @@ class BertEmbeddings(nn.Module):
                             self.dropout.p, self.training, self.compute_dtype)
 
 
+# where the Q/K/V biases are added: the projection GEMM's epilogue (default; the attention kernels
+# then skip the adds and only produce the bias gradient) or the attention kernels
+# (HX_QKV_BIAS_EPILOGUE=0, the round-2..5 layout)
+_QKV_BIAS_EPILOGUE = os.environ.get('HX_QKV_BIAS_EPILOGUE', '1') != '0'
+
+
 class BertSelfAttention(nn.Module):
     def __init__(self, config):
         super().__init__()
@@ -191,12 +197,19 @@ class BertSelfAttention(nn.Module):
         self.dropout = nn.Dropout(config.attention_probs_dropout_prob)
 
     def forward(self, hidden_states, attention_mask_bias, res_grad=None):
-        # bias-less N=3H projection GEMM; the Q/K/V biases are applied (and their
-        # gradients produced) inside the fused attention
+        bias = (self.query.bias, self.key.bias, self.value.bias)
+        if _QKV_BIAS_EPILOGUE:
+            # one N=3H projection GEMM with the Q/K/V biases in its epilogue; their gradients (the
+            # column sums of dQKV) come out of the fused attention backward's registers
+            qkv = ops.linear3(hidden_states, self.query.weight, self.key.weight, self.value.weight, *bias,
+                              res_grad=res_grad, bias_grad=False)
+            return ops.attention(qkv, attention_mask_bias, self.num_attention_heads, self.dropout.p, self.training,
+                                 bias_grad=bias)
+        # bias-less projection; the biases are added (and their gradients produced) in the attention
         qkv = ops.linear3(hidden_states, self.query.weight, self.key.weight, self.value.weight,
                           None, None, None, res_grad=res_grad)
         return ops.attention(qkv, attention_mask_bias, self.num_attention_heads, self.dropout.p, self.training,
-                             bias=(self.query.bias, self.key.bias, self.value.bias))
+                             bias=bias)
 
 
 class BertSelfOutput(nn.Module):

@@ -61,18 +61,21 @@ def _bias3(bq, bk, bv):
 
 
 class _AttnFn(torch.autograd.Function):
-    """Fused attention; with ``bq/bk/bv`` the QKV-projection bias is added to
-    Q/K/V inside the kernels as they are loaded (the projection GEMM runs
-    without a bias epilogue) and its gradient -- the column sums of dQ/dK/dV --
-    comes out of the backward kernel's registers, straight into the flat
-    gradient slots, instead of a separate pass over the [B*S, 3H] gradient."""
+    """Fused attention; with ``bq/bk/bv`` the QKV-projection bias's gradient -- the column
+    sums of dQ/dK/dV -- comes out of the backward kernel's registers, straight into the flat
+    gradient slots, instead of a separate pass over the [B*S, 3H] gradient.  ``add``: the
+    kernels also add the bias to Q/K/V as they load them (a bias-less projection); else it is
+    already in qkv (the projection GEMM's epilogue, the default)."""
 
     @staticmethod
-    def forward(ctx, qkv, mask_bias, bq, bk, bv, num_heads, p):
+    def forward(ctx, qkv, mask_bias, bq, bk, bv, num_heads, p, add=True):
         from .fused import grad_slot  # noqa: F401  (import cycle guard)
         keep = 1.0 - p
         seed, stream = get_rng().next(qkv.device) if p > 0 else (get_rng().seed_tensor(qkv.device), 0)
-        bias = _bias3(bq, bk, bv).float().contiguous() if bq is not None else None
+        # add: the bias is added here; else it is already in qkv (the projection's epilogue) and
+        # only its gradient comes out of the backward
+        bias = _bias3(bq, bk, bv).float().contiguous() if bq is not None and add else None
+        ctx.want_db = bq is not None
         # fp32 under fp16x3: the fp16x3 piece kernels (fp32_mode.attention_split), which also write
         # the context's max |x| per (row, head) -- the attention-output GEMM's per-row scale
         ctx.split = qkv.dtype == torch.float32 and fp32_mode.attention_split(qkv.reshape(-1, qkv.shape[-1]))
@@ -98,7 +101,7 @@ class _AttnFn(torch.autograd.Function):
         num_heads, keep = ctx.meta
         bq, bk, bv = ctx.bparams
         slots = [None, None, None]
-        if ctx.bias is not None:
+        if ctx.want_db:
             slots = [grad_slot(t) for t in (bq, bk, bv)]
             if not all(t is not None for t in slots):
                 slots = [None, None, None]
@@ -111,27 +114,52 @@ class _AttnFn(torch.autograd.Function):
             cm = torch.empty(qkv.shape[0], qkv.shape[2], dtype=torch.float32, device=qkv.device) \
                 if one and qkv.shape[0] <= 256 else None
             dqkv, dbias = C().attn_bwd_f16(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep,
-                                           ctx.bias, *slots, am, cm)
+                                           ctx.bias, *slots, am, cm, want_dbias=ctx.want_db)
             # per-row (QKV data gradient) and per-column (QKV weight gradient) max |dQKV|
             gemm16.attach_cols(gemm16.attach(dqkv, am), cm)
         else:
             dqkv, dbias = C().attn_bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep, ctx.bias,
-                                       *slots)
-        if ctx.bias is None:
-            return dqkv, None, None, None, None, None, None
+                                       *slots, want_dbias=ctx.want_db)
+        if not ctx.want_db:
+            return dqkv, None, None, None, None, None, None, None
         if slots[0] is not None:
             db = slots
         else:
             H = dbias.numel() // 3
             db = [dbias[:H].view_as(bq), dbias[H:2 * H].view_as(bk), dbias[2 * H:].view_as(bv)]
-        return dqkv, None, db[0], db[1], db[2], None, None
+        return dqkv, None, db[0], db[1], db[2], None, None, None
 
 
-def attention(qkv, mask_bias, num_heads, p, bias=None):
-    """``bias``: optional (bq, bk, bv) of the QKV projection, applied here."""
+class _BiasGradTap(torch.autograd.Function):
+    """Identity on qkv whose backward also returns the column sums of dqkv as the gradients of the
+    (bq, bk, bv) already added into it (the composite path of ``attention(bias_grad=...)``)."""
+
+    @staticmethod
+    def forward(ctx, qkv, bq, bk, bv):
+        ctx.n = (bq.numel(), bk.numel())
+        return qkv.view_as(qkv)
+
+    @staticmethod
+    def backward(ctx, dqkv):
+        a, b = ctx.n
+        low = dqkv.dtype in (torch.float16, torch.bfloat16)
+        db = dqkv.reshape(-1, dqkv.shape[-1]).sum(0, dtype=torch.float32 if low else dqkv.dtype)
+        return dqkv, db[:a], db[a:a + b], db[a + b:]
+
+
+def attention(qkv, mask_bias, num_heads, p, bias=None, bias_grad=None):
+    """``bias``: optional (bq, bk, bv) of the QKV projection, applied here; ``bias_grad``: the
+    (bq, bk, bv) already added into qkv by the projection GEMM's epilogue -- only their gradient
+    (the column sums of dQKV) is produced here, by the backward kernel."""
     if _fused_ok(qkv, num_heads):
+        if bias_grad is not None:
+            bq, bk, bv = bias_grad
+            return _AttnFn.apply(qkv.contiguous(), mask_bias.float().contiguous(), bq, bk, bv, int(num_heads),
+                                 float(p), False)
         bq, bk, bv = bias if bias is not None else (None, None, None)
         return _AttnFn.apply(qkv.contiguous(), mask_bias.float().contiguous(), bq, bk, bv, int(num_heads), float(p))
+    if bias_grad is not None:
+        qkv = _BiasGradTap.apply(qkv, *bias_grad)
     if bias is not None:
         qkv = qkv + torch.cat(list(bias), 0).to(qkv.dtype)
     return attention_ref(qkv, mask_bias, num_heads, p)

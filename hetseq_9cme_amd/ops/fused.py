@@ -692,8 +692,9 @@ class _Linear3Fn(torch.autograd.Function):
     """y = x @ [Wq;Wk;Wv]^T + [bq;bk;bv] as ONE GEMM (N = 3H)."""
 
     @staticmethod
-    def forward(ctx, x, wq, wk, wv, bq, bk, bv, mbox):
+    def forward(ctx, x, wq, wk, wv, bq, bk, bv, mbox, bgrad=True):
         has_b = bq is not None
+        ctx.bgrad = bgrad   # False: the bias gradient comes from the consumer (the fused attention)
         W = _adjacent_view([wq, wk, wv])
         if W is None:
             W = torch.cat([wq, wk, wv], 0)
@@ -759,7 +760,7 @@ class _Linear3Fn(torch.autograd.Function):
         # weight grads: ONE GEMM straight into the three adjacent flat slots when possible
         ws = [grad_slot(w) for w in (wq, wk, wv)]
         fused = _adjacent_view(ws) if all(t is not None for t in ws) else None
-        has_b = ctx.has_b
+        has_b = ctx.has_b and ctx.bgrad
         bs = [grad_slot(t) for t in (bq, bk, bv)] if has_b else [None, None, None]
         fb = _adjacent_view(bs) if all(t is not None for t in bs) else None
         direct = fused is not None and (fb is not None or not has_b)
@@ -791,24 +792,30 @@ class _Linear3Fn(torch.autograd.Function):
         if ctx.f16 and ctx.needs_input_grad[0]:
             dx = _f16_dgrad(dy2, dys, W, ctx.wparts, ctx.xshape, ctx.mbox)
         if not has_b:
-            return (dx, gW[0], gW[1], gW[2], None, None, None, None)
+            return (dx, gW[0], gW[1], gW[2], None, None, None, None, None)
         gb = bs if fb is not None else [db[:a], db[a:a + b_], db[a + b_:]]
-        return (dx, gW[0], gW[1], gW[2], gb[0], gb[1], gb[2], None)
+        return (dx, gW[0], gW[1], gW[2], gb[0], gb[1], gb[2], None, None)
 
 
-def linear3(x, wq, wk, wv, bq, bk, bv, res_grad=None):
-    """The fused Q/K/V projection (``res_grad``: see ``ResidualGrad``)."""
-    return _Linear3Fn.apply(x, wq, wk, wv, bq, bk, bv, res_grad)
+def linear3(x, wq, wk, wv, bq, bk, bv, res_grad=None, bias_grad=True):
+    """The fused Q/K/V projection (``res_grad``: see ``ResidualGrad``).  ``bias_grad=False``: the
+    bias is added in the GEMM epilogue but its gradient is produced by the consumer (``attention``
+    with ``bias_grad=(bq, bk, bv)``: the column sums of dQKV from the attention backward's
+    registers) -- this function then returns none for it."""
+    return _Linear3Fn.apply(x, wq, wk, wv, bq, bk, bv, res_grad, bool(bias_grad))
 
 
 # ----------------------------------------------------------------- attention core
-def attention(qkv, mask_bias, num_heads, p, training, bias=None):
+def attention(qkv, mask_bias, num_heads, p, training, bias=None, bias_grad=None):
     """softmax(Q K^T / sqrt(d) + mask) -> dropout -> @ V  on the packed [B, S, 3H]
     projection; returns [B, S, H] (reference BertSelfAttention, :351-377).
     ``mask_bias`` is the additive [B, S] key mask ((1 - m) * -10000); ``bias`` the
-    optional (bq, bk, bv) of a bias-less QKV projection, added inside the kernel."""
+    optional (bq, bk, bv) of a bias-less QKV projection, added inside the kernel
+    (``HX_QKV_BIAS_EPILOGUE=0``);
+    ``bias_grad`` the (bq, bk, bv) already in ``qkv`` (``linear3(..., bias_grad=False)``):
+    only their gradient is produced here."""
     from .flash_attention import attention as _attention
-    return _attention(qkv, mask_bias, num_heads, p if training else 0.0, bias)
+    return _attention(qkv, mask_bias, num_heads, p if training else 0.0, bias, bias_grad)
 
 
 # ----------------------------------------------------------------- MLM decoder + softmax-xent

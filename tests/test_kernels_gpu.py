@@ -696,6 +696,51 @@ def test_attention_op_fp32_split(dev):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('mode', ['fp16x3', 'bf16'])
+def test_attention_op_bias_grad_only(dev, mode):
+    """QKV bias already in qkv (the projection GEMM's epilogue, ``linear3(bias_grad=False)``):
+    ``ops.attention(bias_grad=...)`` adds nothing and returns the bias gradients (the column sums
+    of dQKV) from the backward kernel -- equal to the attention-added path's."""
+    from hetseq_9cme_amd.ops import fp32_mode
+    torch.manual_seed(6)
+    B, S, nh, d = 32, 128, 2, 64
+    H = nh * d
+    dt = torch.bfloat16 if mode == 'bf16' else torch.float32
+    base = torch.randn(B, S, 3 * H, device=dev).to(dt)
+    bias = [(0.5 * torch.randn(H, device=dev)) for _ in range(3)]
+    mb = torch.zeros(B, S, device=dev)
+    mb[3, S - 20:] = -10000.0
+    d_ = torch.randn(B, S, H, device=dev).to(dt)
+    pg = fp32_mode.fp32_gemm_mode()
+    outs = []
+    try:
+        fp32_mode.set_fp32_gemm('fp16x3')
+        for pre in (False, True):
+            qkv = (base.float() + torch.cat(bias).to(dev)).to(dt) if pre else base.clone()
+            qkv.requires_grad_()
+            bs = [b.clone().requires_grad_() for b in bias]
+            if pre:
+                out = ops.attention(qkv, mb, nh, 0.0, True, bias_grad=bs)
+            else:
+                out = ops.attention(qkv, mb, nh, 0.0, True, bias=bs)
+            out.backward(d_)
+            outs.append((out.detach().float(), qkv.grad.float(), [b.grad for b in bs]))
+    finally:
+        fp32_mode.set_fp32_gemm(pg)
+    (o0, g0, b0), (o1, g1, b1) = outs
+    tol = dict(rtol=2e-2, atol=2e-2) if mode == 'bf16' else dict(rtol=1e-4, atol=1e-5)
+    _close(o1, o0, **tol)
+    _close(g1, g0, **tol)
+    for a, b in zip(b1, b0):
+        _close(a, b, **tol)
+    H3 = torch.cat(b1)   # the gradient is the column sum of the kernel's own dQKV
+    if mode == 'bf16':   # the kernel sums dQKV before its bf16 rounding
+        _close(H3, g1.reshape(-1, 3 * H).sum(0), rtol=2e-2, atol=5e-2)
+    else:
+        _close(H3, g1.reshape(-1, 3 * H).sum(0), rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('S,with_bias', [(128, True), (77, False)])
 def test_attention_f16_backward_scale_producers(dev, S, with_bias):
     """The fp16x3 attention backward (one key block, S <= 128) writes the GEMM scale sources of

@@ -648,9 +648,28 @@ def ffn(x, W1, b1, W2, res_grad=None):
 
 
 # ----------------------------------------------------------------- fused Q/K/V projection
+_ADJ = {}   # (data_ptr, shape, dtype) of each tensor -> the view (host cost: built once per layout)
+
+
 def _adjacent_view(ts):
     """If tensors ``ts`` are laid out back to back in one storage (FlatParamSpace
-    guarantees it for Q/K/V), return a single [sum(rows), cols] view without copying."""
+    guarantees it for Q/K/V), return a single [sum(rows), cols] view without copying.
+    Views are cached by the tensors' addresses and shapes: the cached view holds its storage,
+    so an address in the key cannot be reused by another allocation while the entry lives."""
+    key = tuple((t.data_ptr(), tuple(t.shape), t.dtype) for t in ts if t is not None) if ts[0] is not None else None
+    if key is not None and len(key) == len(ts):
+        v = _ADJ.get(key)
+        if v is not None:
+            return v
+    v = _adjacent_view_build(ts)
+    if v is not None and key is not None and len(key) == len(ts):
+        if len(_ADJ) > 4096:
+            _ADJ.clear()
+        _ADJ[key] = v
+    return v
+
+
+def _adjacent_view_build(ts):
     t0 = ts[0]
     es = t0.element_size()
     base = t0.data_ptr()

@@ -663,7 +663,7 @@ def _adjacent_view(ts):
             return v
     v = _adjacent_view_build(ts)
     if v is not None and key is not None and len(key) == len(ts):
-        if len(_ADJ) > 4096:
+        if len(_ADJ) >= 256:   # a model uses a few per layer; the bound caps what stale entries pin
             _ADJ.clear()
         _ADJ[key] = v
     return v

@@ -1357,7 +1357,15 @@ int hx_gemm_f16(const HxGemmF16& p, int cfg, hipStream_t s) {
 
 void hx_wgrad_f16_plan(int M, int N, int T, int* cfg, int* nsplit) {
   const int t256 = (M % 256 == 0 && N % 256 == 0) ? (M / 256) * (N / 256) : 0;
-  const int c = (t256 >= 24 && t256 <= 512) ? 1 : 0;
+  // the large tile also for few-tile shapes whose token splits (one workgroup per CU) keep >= 512
+  // tokens each: the attention-output gradient (768 x 768, 9 tiles x 28 splits over 16384 tokens)
+  // 78 vs 85-89 us on the 128 tile (r5bm, repeated); at 4096 tokens the splits would be too short
+  static const bool few = [] {
+    const char* e = getenv("HX_WGRAD_FEW256");
+    return !(e && atoi(e) == 0);
+  }();
+  const int sp_few = t256 ? hx_cu_slots() / t256 : 0;
+  const int c = ((t256 >= 24 && t256 <= 512) || (few && t256 >= 8 && t256 < 24 && T / sp_few >= 512)) ? 1 : 0;
   const int tiles = c ? t256 : (M / 128) * (N / 128);
   const int slots = (c ? 1 : 2) * hx_cu_slots();
   // splits fill the CUs: more is faster up to one workgroup per CU (r5y, repeated A/B on one box:

@@ -71,7 +71,10 @@ def wgrad_sweep(C, dev, plans):
     (HX_WGRAD_F16, 'plan' = the kernel's own)."""
     T = int(os.environ.get('T', '16384'))
     g = torch.Generator(device=dev).manual_seed(0)
+    only = os.environ.get('ONLY')   # one shape name
     for (name, N, K) in [('qkv', 2304, 768), ('attn_out', 768, 768), ('ffn_up', 3072, 768), ('ffn_down', 768, 3072)]:
+        if only and name != only:
+            continue
         x = torch.randn(T, K, device=dev, generator=g)
         dy = torch.randn(T, N, device=dev, generator=g)
         out = torch.empty(N, K, device=dev)

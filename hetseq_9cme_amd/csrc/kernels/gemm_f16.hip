@@ -1212,15 +1212,18 @@ int hx_gemm_f16_plan(int M, int N, int K) {
   }
   // deep reductions (the MLM decoder's data gradient, K = 30720) on the large tile whatever M: split-K
   // slabs fill the CUs, and the big tile halves the operand re-reads of the 128 x 96 one
-  if ((M >= 8192 || K >= 8192) && N % 192 == 0) return 1;
+  if ((M >= 8192 || (K >= 8192 && M >= 2048)) && N % 192 == 0) return 1;
   // batch 32 (M = 4096, r5r): the large tile also wins when its tiles fill >= 70 % of the CUs (QKV
   // 55 vs 61 us, FFN up 80 vs 97, FFN-down dgrad 75 vs 88) or the reduction is deep (K >= 2048:
   // data gradients 64-76 vs 65-83); the 128 x 96 tile keeps the shallow narrow ones (attention
-  // output 24 vs 42 us)
-  if (M >= 2048 && N % 192 == 0 &&
-      (10 * ((M + 255) / 256) * (N / 192) >= 7 * hx_cu_slots() || K >= 2048))
+  // output 24 vs 42 us).  Down to M = 512 when the N tiles alone fill the CUs: the MLM decoder
+  // forward at batch 32 (640 masked rows x 30528) 122 vs 181-213 us on the 64 x 64 tile (r5bq)
+  if (M >= 512 && N % 192 == 0 &&
+      (10 * ((M + 255) / 256) * (N / 192) >= 7 * hx_cu_slots() || (K >= 2048 && M >= 2048)))
     return 1;
-  if (M >= 1024 && N % 96 == 0) return 2;
+  // 128 x 96 from 1024 rows, or from 512 with a split-K-deep reduction (the decoder's data
+  // gradient at batch 32: 117 vs 137-152 us on the large tile, r5bq)
+  if ((M >= 1024 || (M >= 512 && K >= 8192)) && N % 96 == 0) return 2;
   if (N % 64 == 0) return 3;
   return -1;
 }

@@ -262,6 +262,23 @@ void embed_word_grad(Tensor dz, Tensor ids, Tensor order, Tensor dwte) {
                             dwte.data_ptr<float>(), rows, H, cur_stream(dz));
 }
 
+// token-type embedding gradient (ntypes <= 3) into dwtt [ntypes, H] (overwritten)
+void embed_type_grad(Tensor dz, Tensor tt, Tensor dwtt) {
+  check_cuda(dz, "grad");
+  check_f32(dwtt, "dwtt");
+  TORCH_CHECK(tt.scalar_type() == torch::kLong && tt.is_contiguous() && tt.device() == dz.device(), "tt: int64");
+  const int H = (int)dz.size(-1);
+  const int64_t rows = dz.numel() / H;
+  const int ntypes = (int)dwtt.size(0);
+  TORCH_CHECK(dz.is_contiguous() && tt.numel() == rows && dwtt.dim() == 2 && dwtt.size(1) == H &&
+                  dwtt.is_contiguous() && ntypes >= 1 && ntypes <= 3 && H % 4 == 0 && H <= 2048,
+              "embed_type_grad: contiguous dz [rows, H], tt [rows], dwtt [ntypes <= 3, H]");
+  dbg_range(tt, 0, ntypes, "token type ids");
+  c10::hip::HIPGuardMasqueradingAsCUDA guard(dz.device());
+  Tensor part = torch::empty({(int64_t)hx_type_grad_blocks(rows) * ntypes * H}, dz.options().dtype(torch::kFloat32));
+  hx_type_grad(act_bf16(dz), dz.data_ptr(), tt.data_ptr<int64_t>(), part.data_ptr<float>(), dwtt.data_ptr<float>(),
+               rows, H, ntypes, cur_stream(dz));
+}
 
 // ------------------------------------------------------------------ elementwise
 Tensor bias_act_fwd(Tensor y, OptT b, int64_t act) {
@@ -1035,6 +1052,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("keep_prob"), py::arg("seed"), py::arg("stream"),
         py::arg("bf16_out"), py::arg("amax_out") = py::none());
   m.def("embed_word_grad", &embed_word_grad);
+  m.def("embed_type_grad", &embed_type_grad);
   m.def("bias_act_fwd", &bias_act_fwd);
   m.def("bias_act_bwd", &bias_act_bwd);
   m.def("colsum", &colsum);

@@ -41,6 +41,11 @@ void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const floa
                      const float* wtt, const float* gamma, const float* beta, void* out, void* zsave, float* mean,
                      float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, const uint64_t* seed,
                      uint64_t stream, hipStream_t s, float* amax_part = nullptr);
+// token-type embedding gradient for ntypes <= 3: dwtt[t] = sum of dz rows with tt == t (part: a
+// [hx_type_grad_blocks(rows)][ntypes][H] fp32 workspace; deterministic block partials + fold)
+int hx_type_grad_blocks(int64_t rows);
+void hx_type_grad(int bf16, const void* dz, const int64_t* tt, float* part, float* dwtt, int64_t rows, int H, int ntypes,
+                  hipStream_t s);
 void hx_embed_word_grad_sorted(int bf16, const void* dz, const int64_t* ids, const int64_t* order, float* dwte,
                                int64_t rows, int H, hipStream_t s);
 // elementwise.hip

@@ -426,6 +426,46 @@ __global__ __launch_bounds__(NT) void embed_word_grad_sorted_k(const T* __restri
   flush(cur, true);   // the last run may continue in the next chunk
 }
 
+// token-type embedding gradient (few types): part[block][t][H] = sum of the block's rows r with
+// tt[r] == t, a wave per row as the LayerNorm kernels (the row read once), the 4 waves' sums folded
+// through LDS; fold_rows sums the blocks.  Replaces one_hot(tt)^T . dz (a one-hot tensor and a
+// [NT x rows] x [rows x H] library GEMM: 32 us fp32, 73 us bf16 at 16384 x 768).
+template <typename T, int CH, int NTY>
+__global__ __launch_bounds__(NT) void type_grad_k(const T* __restrict__ dz, const int64_t* __restrict__ tt,
+                                                  float* __restrict__ part, int64_t rows, int H) {
+  __shared__ float red[WPB][CH * 256];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t nw = (int64_t)gridDim.x * WPB;
+  Row<CH> acc[NTY];
+#pragma unroll
+  for (int t = 0; t < NTY; ++t)
+#pragma unroll
+    for (int c = 0; c < CH; ++c) acc[t].v[c] = hx::f4(0.f);
+  for (int64_t r = blockIdx.x * (int64_t)WPB + w; r < rows; r += nw) {
+    const int ty = (int)tt[r];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int j = (c * 64 + lane) * 4;
+      if (j < H) {
+        const float4 v = hx::load4(dz + r * H + j);
+#pragma unroll
+        for (int t = 0; t < NTY; ++t)
+          if (ty == t) {
+            acc[t].v[c].x += v.x; acc[t].v[c].y += v.y; acc[t].v[c].z += v.z; acc[t].v[c].w += v.w;
+          }
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < NTY; ++t) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) *reinterpret_cast<float4*>(&red[w][(c * 64 + lane) * 4]) = acc[t].v[c];
+    __syncthreads();
+    for (int j = threadIdx.x; j < H; j += NT)
+      part[((int64_t)blockIdx.x * NTY + t) * H + j] = (red[0][j] + red[1][j]) + (red[2][j] + red[3][j]);
+    __syncthreads();
+  }
+}
 
 int pick_ch(int H) {
   const int c = (H + 255) / 256;
@@ -531,6 +571,32 @@ void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const floa
                                                     (float*)zsave, mean, rstd, rows, S, H, eps, keep_prob, seed,
                                                     stream, amax_part);
   })
+}
+
+int hx_type_grad_blocks(int64_t rows) { return ln_grid(rows, 256); }
+
+void hx_type_grad(int bf16, const void* dz, const int64_t* tt, float* part, float* dwtt, int64_t rows, int H, int ntypes,
+                  hipStream_t s) {
+  const int grid = hx_type_grad_blocks(rows);
+  HX_CH_DISPATCH(H, {
+    switch (ntypes) {
+      case 1:
+        if (bf16) type_grad_k<uint16_t, CH, 1><<<grid, NT, 0, s>>>((const uint16_t*)dz, tt, part, rows, H);
+        else type_grad_k<float, CH, 1><<<grid, NT, 0, s>>>((const float*)dz, tt, part, rows, H);
+        break;
+      case 2:
+        if (bf16) type_grad_k<uint16_t, CH, 2><<<grid, NT, 0, s>>>((const uint16_t*)dz, tt, part, rows, H);
+        else type_grad_k<float, CH, 2><<<grid, NT, 0, s>>>((const float*)dz, tt, part, rows, H);
+        break;
+      default:
+        if (bf16) type_grad_k<uint16_t, CH, 3><<<grid, NT, 0, s>>>((const uint16_t*)dz, tt, part, rows, H);
+        else type_grad_k<float, CH, 3><<<grid, NT, 0, s>>>((const float*)dz, tt, part, rows, H);
+        break;
+    }
+  })
+  // [grid][ntypes][H] -> dwtt[t] (rows of ntypes H, one output segment per type)
+  hx::fold_rows(part, grid, (int64_t)ntypes * H, ntypes * H, H, dwtt, ntypes > 1 ? dwtt + H : nullptr,
+                ntypes > 2 ? dwtt + 2 * H : nullptr, 0, s);
 }
 
 void hx_embed_word_grad_sorted(int bf16, const void* dz, const int64_t* ids, const int64_t* order, float* dwte,

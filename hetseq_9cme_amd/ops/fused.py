@@ -247,8 +247,11 @@ class _EmbedLNFn(torch.autograd.Function):
         C().embed_word_grad(dz2, ids_f, torch.argsort(ids_f), dwte)
         # positions: a column sum over the batch of the [B, S*H] view
         C().colsum(dz.reshape(B, S * H), None, dwpe[:S].reshape(-1))
-        # token types: one_hot(tt)^T . dz  (one small GEMM, any number of types)
-        if ctx.has_tt:
+        # token types: per-type column sums (one pass over dz) for the usual 2 types; one_hot(tt)^T . dz
+        # (one small GEMM) for more
+        if ctx.has_tt and NT <= 3 and dwtt.is_contiguous():
+            C().embed_type_grad(dz2, tt.reshape(-1), dwtt)
+        elif ctx.has_tt:
             oh = F.one_hot(tt.reshape(-1), NT).to(dz2.dtype)
             if dz2.dtype == torch.float32:
                 torch.mm(oh.t(), dz2, out=dwtt)

@@ -573,7 +573,7 @@ void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const floa
   })
 }
 
-int hx_type_grad_blocks(int64_t rows) { return ln_grid(rows, 256); }
+int hx_type_grad_blocks(int64_t rows) { return ln_grid(rows, 1024); }
 
 void hx_type_grad(int bf16, const void* dz, const int64_t* tt, float* part, float* dwtt, int64_t rows, int H, int ntypes,
                   hipStream_t s) {

@@ -556,12 +556,15 @@ Tensor split_rows_f16(Tensor x, Tensor amax) {
 // [(wf, wt, rmax, cmax)] per weight W [N, K]: P2 fp16 pieces of W (rows scaled by their own
 // maxima) and of W^T (rows = columns of W, scaled by the column maxima); rmax [N, 1] / cmax [K, 1]
 // are the per-row scale sources of the forward / data-gradient products
-std::vector<std::vector<Tensor>> split_weight_f16(std::vector<Tensor> Ws) {
+// rows: optional padded row count per weight (>= its rows, a multiple of 64): the pieces cover the
+// padded rows, read as zero past W's own (the MLM decoder's vocabulary, without a padded copy)
+std::vector<std::vector<Tensor>> split_weight_f16(std::vector<Tensor> Ws, std::vector<int64_t> rows) {
   TORCH_CHECK(!Ws.empty() && Ws.size() <= HX_WBATCH, "split_weight_f16: 1..64 weights");
+  TORCH_CHECK(rows.empty() || rows.size() == Ws.size(), "split_weight_f16: one padded row count per weight");
   HxWeightBatch d{};
   d.n = (int)Ws.size();
   int64_t rc_floats = 0;
-  for (const Tensor& W : Ws) rc_floats += W.size(0) + W.size(1);
+  for (size_t i = 0; i < Ws.size(); ++i) rc_floats += (rows.empty() ? Ws[i].size(0) : rows[i]) + Ws[i].size(1);
   Tensor rc = torch::empty({rc_floats}, Ws[0].options());
   std::vector<std::vector<Tensor>> out;
   int tiles = 0;
@@ -569,10 +572,11 @@ std::vector<std::vector<Tensor>> split_weight_f16(std::vector<Tensor> Ws) {
   for (int i = 0; i < d.n; ++i) {
     const Tensor& W = Ws[i];
     check_f32(W, "split_weight_f16 input");
-    TORCH_CHECK(W.dim() == 2 && W.is_contiguous() && W.size(0) % 64 == 0 && W.size(1) % 64 == 0 &&
-                    aligned16(W.data_ptr()) && W.device() == Ws[0].device(),
-                "split_weight_f16: every W contiguous [N, K], N and K multiples of 64, one device");
-    const int64_t N = W.size(0), K = W.size(1);
+    const int64_t N = rows.empty() ? W.size(0) : rows[i], K = W.size(1);
+    TORCH_CHECK(W.dim() == 2 && W.is_contiguous() && N % 64 == 0 && N >= W.size(0) && W.size(0) >= 1 &&
+                    K % 64 == 0 && aligned16(W.data_ptr()) && W.device() == Ws[0].device(),
+                "split_weight_f16: every W contiguous [N, K] (N padded to a multiple of 64 >= its rows), K a "
+                "multiple of 64, one device");
     auto hf = W.options().dtype(torch::kHalf);
     Tensor wf = torch::empty({N, 2 * K}, hf), wt = torch::empty({K, 2 * N}, hf);
     d.W[i] = W.data_ptr<float>();
@@ -580,7 +584,7 @@ std::vector<std::vector<Tensor>> split_weight_f16(std::vector<Tensor> Ws) {
     d.wt[i] = reinterpret_cast<uint16_t*>(wt.data_ptr());
     d.N[i] = (int)N;
     d.K[i] = (int)K;
-    d.mask[i] = 0;
+    d.nv[i] = N > W.size(0) ? (int)W.size(0) : 0;
     d.start[i] = tiles;
     d.roff[i] = off;
     tiles += (int)((N / 64) * (K / 64));
@@ -1084,7 +1088,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("split_rows_f16", &split_rows_f16);
   m.def("amax_cols", &amax_cols);
   m.def("amax_rows_cols", &amax_rows_cols);
-  m.def("split_weight_f16", &split_weight_f16);
+  m.def("split_weight_f16", &split_weight_f16, py::arg("Ws"), py::arg("rows") = std::vector<int64_t>());
   m.def("gemm_f16", &gemm_f16, py::arg("a"), py::arg("a_amax"), py::arg("b"), py::arg("b_amax"),
         py::arg("out") = py::none(), py::arg("beta") = false, py::arg("bias") = py::none(), py::arg("ks") = 0);
   m.def("gemm_f16_gelu", &gemm_f16_gelu, py::arg("a"), py::arg("a_amax"), py::arg("b"), py::arg("b_amax"),

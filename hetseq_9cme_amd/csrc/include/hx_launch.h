@@ -105,7 +105,8 @@ struct HxWeightBatch {
   const float* W[HX_WBATCH];
   uint16_t* wf[HX_WBATCH];
   uint16_t* wt[HX_WBATCH];
-  int N[HX_WBATCH], K[HX_WBATCH], mask[HX_WBATCH];
+  int N[HX_WBATCH], K[HX_WBATCH];
+  int nv[HX_WBATCH];   // split_weight_f16: rows at or past nv read as zero (0: all N rows) -- padded vocabularies
   int start[HX_WBATCH + 1];
   int64_t roff[HX_WBATCH];   // split_weight_f16: weight i's row maxima [N] then column maxima [K] at rc + roff[i]
 };

@@ -1042,6 +1042,7 @@ __global__ __launch_bounds__(256) void amax_weights_k(HxWeightBatch d, float* __
   const int tk = K / 64, loc = blk - d.start[i];
   const int k0 = (loc % tk) * 64, n0 = (loc / tk) * 64;
   const float* W = d.W[i];
+  const int nv = d.nv[i] ? d.nv[i] : N;
   float* rmax = rc + d.roff[i];
   float* cmax = rmax + N;
   const int t = threadIdx.x, c4 = (t & 15) * 4;
@@ -1049,7 +1050,8 @@ __global__ __launch_bounds__(256) void amax_weights_k(HxWeightBatch d, float* __
 #pragma unroll
   for (int r4 = 0; r4 < 4; ++r4) {
     const int r = (t >> 4) + 16 * r4;
-    const float4 v = *reinterpret_cast<const float4*>(W + (int64_t)(n0 + r) * K + k0 + c4);
+    const float4 v = n0 + r < nv ? *reinterpret_cast<const float4*>(W + (int64_t)(n0 + r) * K + k0 + c4)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
     const float a[4] = {fabsf(v.x), fabsf(v.y), fabsf(v.z), fabsf(v.w)};
     float m = fmaxf(fmaxf(a[0], a[1]), fmaxf(a[2], a[3]));
 #pragma unroll
@@ -1093,6 +1095,7 @@ __global__ __launch_bounds__(256) void split_weight_f16_k(HxWeightBatch d, const
   const int tk = K / 64, loc = blk - d.start[i];
   const int k0 = (loc % tk) * 64, n0 = (loc / tk) * 64;
   const float* W = d.W[i];
+  const int nv = d.nv[i] ? d.nv[i] : N;
   const float* rmax = rc + d.roff[i];
   const float* cmax = rmax + N;
   const int t = threadIdx.x, c4 = (t & 15) * 4;
@@ -1103,7 +1106,8 @@ __global__ __launch_bounds__(256) void split_weight_f16_k(HxWeightBatch d, const
   for (int r4 = 0; r4 < 4; ++r4) {
     const int r = (t >> 4) + 16 * r4;
     const float rs = ldexpf(1.f, f16_scale_exp(rmax[n0 + r]));
-    const float4 v = *reinterpret_cast<const float4*>(W + (int64_t)(n0 + r) * K + k0 + c4);
+    const float4 v = n0 + r < nv ? *reinterpret_cast<const float4*>(W + (int64_t)(n0 + r) * K + k0 + c4)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
     const float x[4] = {v.x, v.y, v.z, v.w};
     uint16_t q0[4], q1[4];
 #pragma unroll

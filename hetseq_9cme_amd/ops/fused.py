@@ -851,7 +851,11 @@ class _DecoderXentFn(torch.autograd.Function):
         ctx.f16 = gemm16.ok(h, 64) and h.is_contiguous() and H % 64 == 0
         ctx.b16 = False
         if ctx.f16:   # fp32 runs: the fp16x3 GEMM
-            wf, wt, wrow, wcol = C().split_weight_f16([_padded_rows(W, Vp)])[0]
+            Wd = W.detach()
+            if Wd.is_contiguous() and Wd.data_ptr() % 16 == 0:   # padding rows read as zero, no copy
+                wf, wt, wrow, wcol = C().split_weight_f16([Wd], [Vp])[0]
+            else:
+                wf, wt, wrow, wcol = C().split_weight_f16([_padded_rows(W, Vp)])[0]
             full = gemm16.mm(h, gemm16.amax(h, h), wf, wrow)
             ctx.wpieces = (wt, wcol)
         elif gemm16.bf16_ok(h, 64, H) and h.is_contiguous():

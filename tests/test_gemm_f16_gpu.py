@@ -502,3 +502,17 @@ def test_layernorm_pieces_out(dev):
         src = dy if want_dy else dz
         assert torch.equal(bm, src.abs().amax(1, keepdim=True))
         assert torch.equal(bp, C().split_rows_f16(src, bm))
+
+
+def test_split_weight_virtual_padding(dev):
+    """split_weight_f16 with a padded row count reads the rows past W's own as zero: bit-identical
+    to splitting a zero-padded copy (the MLM decoder's vocabulary, 30522 -> 30720 rows)."""
+    g = torch.Generator(device=dev).manual_seed(43)
+    V, H, Vp = 30522, 768, 30720
+    W = torch.randn(V, H, device=dev, generator=g) * 0.05
+    Wp = torch.zeros(Vp, H, device=dev)
+    Wp[:V] = W
+    a = C().split_weight_f16([W], [Vp])[0]
+    b = C().split_weight_f16([Wp])[0]
+    for p, q in zip(a, b):
+        assert p.shape == q.shape and torch.equal(p, q)

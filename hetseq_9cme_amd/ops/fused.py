@@ -651,7 +651,7 @@ def ffn(x, W1, b1, W2, res_grad=None):
 
 
 # ----------------------------------------------------------------- fused Q/K/V projection
-_ADJ = {}   # (data_ptr, shape, dtype) of each tensor -> the view (host cost: built once per layout)
+_ADJ = {}   # (data_ptr, shape, stride, dtype) of each tensor -> the view (built once per layout)
 
 
 def _adjacent_view(ts):
@@ -659,7 +659,8 @@ def _adjacent_view(ts):
     guarantees it for Q/K/V), return a single [sum(rows), cols] view without copying.
     Views are cached by the tensors' addresses and shapes: the cached view holds its storage,
     so an address in the key cannot be reused by another allocation while the entry lives."""
-    key = tuple((t.data_ptr(), tuple(t.shape), t.dtype) for t in ts if t is not None) if ts[0] is not None else None
+    key = (tuple((t.data_ptr(), tuple(t.shape), t.stride(), t.dtype) for t in ts if t is not None)
+           if ts[0] is not None else None)
     if key is not None and len(key) == len(ts):
         v = _ADJ.get(key)
         if v is not None:

@@ -459,8 +459,8 @@ std::vector<Tensor> attn_bwd(Tensor dout, Tensor qkv, Tensor mask_bias, Tensor o
               mask_bias.data_ptr<float>(), dout.data_ptr(), out.data_ptr(), lse.data_ptr<float>(),
               keep < 1.0 ? reinterpret_cast<const uint32_t*>(dmask.data_ptr<int32_t>()) : nullptr,
               dqkv.data_ptr(), dq_acc, dq_ld, (int)B, (int)S, (int)nh, (float)keep, cur_stream(qkv),
-              (split && !multi) ? amax_ptr(amax_out, B * S * nh, "attn_bwd amax") : nullptr,   // [B * S][nh]
-              (split && !multi) ? amax_ptr(colmax_out, B * 3 * H, "attn_bwd colmax") : nullptr);   // [B][3H]
+              split ? amax_ptr(amax_out, B * S * nh, "attn_bwd amax") : nullptr,   // [B * S][nh]
+              split ? amax_ptr(colmax_out, B * ((S + 127) / 128) * 3 * H, "attn_bwd colmax") : nullptr);   // [B * kb][3H]
   if (multi && bf) dqkv.narrow(-1, 0, H).copy_(dq32);
   dbg_finite(dqkv, "attn_bwd");
   return {dqkv, dbias};
@@ -770,7 +770,8 @@ inline HxColScale col_scale_src(const Tensor& t, const Tensor& ref, int64_t cols
 
 // max |x| of every row and every column in one read: ([rows, 1], [1, cols]); cols <= 4096
 std::vector<Tensor> amax_rows_cols(Tensor x) {
-  check_f32(x, "amax_rows_cols");
+  // rows may be strided (the dQ third of a [rows, 3H] gradient)
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == torch::kFloat32, "amax_rows_cols: fp32 GPU tensor");
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && x.stride(0) % 4 == 0 && x.size(1) % 4 == 0 &&
                   x.size(1) <= 4096 && aligned16(x.data_ptr()),
               "amax_rows_cols: fp32 [rows, cols <= 4096] with 16-B rows, cols % 4 == 0");

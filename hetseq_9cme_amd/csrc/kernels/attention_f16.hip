@@ -226,14 +226,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float* qbias = qkv_bias ? qkv_bias + hd * D : nullptr;
   const float* kbias = qkv_bias ? qkv_bias + H + hd * D : nullptr;
   const float* vbias = qkv_bias ? qkv_bias + 2 * H + hd * D : nullptr;
-  // one key block (S <= 128): max |dQ|, |dK|, |dV| of each of the head's rows, for the QKV GEMMs'
-  // per-row operand scale (amax_part[row][head]; ops/gemm16.py takes the max over the heads)
+  // max |dQ|, |dK|, |dV| of each of the head's rows, for the QKV GEMMs' per-row operand scale
+  // (amax_part[row][head]; ops/gemm16.py takes the max over the heads).  Several key blocks
+  // (S > 128): this block's key rows' dK / dV only -- dQ is summed over the blocks by atomics, its
+  // maxima come from one pass over the dQ third (ops/flash_attention.py)
   __shared__ unsigned rmx_s[128];
-  const bool want_am = amax_part != nullptr && single;
+  const bool want_am = amax_part != nullptr;
   if (want_am && tid < 128) rmx_s[tid] = 0u;
-  // ... and max |dQ| / |dK| / |dV| of each of its columns -> colmax_part[b][3H] (the QKV weight
-  // gradient's per-column scale)
-  const bool want_cm = colmax_part != nullptr && single;
+  // ... and max |dQ| / |dK| / |dV| of each of its columns -> colmax_part[b][key block][3H] (the QKV
+  // weight gradient's per-column scale; several key blocks: the dQ section stays 0)
+  const bool want_cm = colmax_part != nullptr;
   float cqm0 = 0.f, cqm1 = 0.f;   // running column maxima of this lane's two dQ columns
 
   // ---- the block's K rows (4 x 8 dims per thread, for the K image) and this lane's V fragments
@@ -623,10 +625,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
       v[0] = fmaxf(v[0], __shfl_xor(v[0], 1, 64));
       {
         const int key = kbase + w * 32 + crow(l32 >> 1, h);
-        if ((l32 & 1) == 0 && key < S) atomicMax(&rmx_s[key], __float_as_uint(v[0]));
+        if ((l32 & 1) == 0 && key < S) atomicMax(&rmx_s[key - kbase], __float_as_uint(v[0]));
       }
       __syncthreads();
-      if (tid < S) amax_part[((int64_t)b * S + tid) * nh + hd] = __uint_as_float(rmx_s[tid]);
+      if (tid < 128 && kbase + tid < S)
+        amax_part[((int64_t)b * S + kbase + tid) * nh + hd] = __uint_as_float(rmx_s[tid]);
     }
     if (want_cm) {
       __shared__ float cmx_s[4][3][64];
@@ -663,7 +666,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
         } else {
           m = fmaxf(fmaxf(cmx_s[0][sec][c], cmx_s[1][sec][c]), fmaxf(cmx_s[2][sec][c], cmx_s[3][sec][c]));
         }
-        colmax_part[(int64_t)b * 3 * H + sec * H + hd * D + c] = m;
+        colmax_part[((int64_t)b * gridDim.x + blk.x) * 3 * H + sec * H + hd * D + c] = m;
       }
     }
   }

@@ -106,15 +106,24 @@ class _AttnFn(torch.autograd.Function):
             if not all(t is not None for t in slots):
                 slots = [None, None, None]
         if ctx.split:
-            # one key block (S <= 128): the kernel writes max |dQKV| per (row, head) -- the QKV
-            # projection's per-row operand scale
-            one = qkv.shape[1] <= 128
-            am = torch.empty(qkv.shape[0] * qkv.shape[1], num_heads, dtype=torch.float32, device=qkv.device) \
-                if one else None
-            cm = torch.empty(qkv.shape[0], qkv.shape[2], dtype=torch.float32, device=qkv.device) \
-                if one and qkv.shape[0] <= 256 else None
+            # the kernel writes max |dQKV| per (row, head) -- the QKV projection's per-row operand
+            # scale -- and per (batch, key block, column) -- its weight gradient's column scale.
+            # Several key blocks (S > 128): dK / dV only; dQ (summed by atomics over the blocks)
+            # gets its row and column maxima from one pass over the dQ third
+            B, S, H3 = qkv.shape
+            kb = (S + 127) // 128
+            am = torch.empty(B * S, num_heads, dtype=torch.float32, device=qkv.device)
+            cm = (torch.empty(B * kb, H3, dtype=torch.float32, device=qkv.device)
+                  if B * kb + (kb > 1) <= 256 else None)   # <= 256 column partials (+ the dQ row)
             dqkv, dbias = C().attn_bwd_f16(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep,
                                            ctx.bias, *slots, am, cm, want_dbias=ctx.want_db)
+            if kb > 1:
+                rq, cq = C().amax_rows_cols(dqkv.view(B * S, H3)[:, :H3 // 3])
+                am = torch.cat([am, rq], 1)
+                if cm is not None:
+                    q = torch.zeros(1, H3, dtype=torch.float32, device=qkv.device)
+                    q[:, :H3 // 3] = cq
+                    cm = torch.cat([q, cm], 0)
             # per-row (QKV data gradient) and per-column (QKV weight gradient) max |dQKV|
             gemm16.attach_cols(gemm16.attach(dqkv, am), cm)
         else:

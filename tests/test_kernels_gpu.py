@@ -765,6 +765,60 @@ def test_attention_f16_backward_scale_producers(dev, S, with_bias):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('S', [300, 512])
+def test_attention_f16_backward_scale_producers_multi_block(dev, S):
+    """Several key blocks (S > 128): the kernel writes the dK / dV row maxima per (row, head) and
+    the dK / dV column maxima per (sequence, key block) with the dQ section 0; ops.attention adds
+    the dQ maxima from one pass over the dQ third -- the attached scale sources equal the exact
+    row / column maxima of dQKV."""
+    from hetseq_9cme_amd.ops import fp32_mode, gemm16
+    from hetseq_9cme_amd.ops._ext import C
+    torch.manual_seed(8)
+    B, nh, d = 2, 4, 64
+    H = nh * d
+    kb = (S + 127) // 128
+    qkv = torch.randn(B, S, 3 * H, device=dev)
+    mb = torch.zeros(B, S, device=dev)
+    mb[1, S - 9:] = -10000.0
+    out, lse, dm = C().attn_fwd(qkv, mb, nh, 0.9, _seed(dev, 5), 3, None)
+    dout = torch.randn(B, S, H, device=dev) * torch.pow(2.0, torch.linspace(-8, 8, S, device=dev))[None, :, None]
+    am = torch.full((B * S, nh), -1.0, device=dev)
+    cm = torch.full((B * kb, 3 * H), -1.0, device=dev)
+    dqkv = C().attn_bwd_f16(dout, qkv, mb, out, lse, dm, nh, 0.9, None, None, None, None, am, cm)[0]
+    g = dqkv.abs().view(B * S, 3, nh, d)
+    assert torch.equal(am, g[:, 1:].amax(-1).amax(1))   # dK / dV of the head
+    pad = torch.zeros(B, kb * 128, 3 * H, device=dev)
+    pad[:, :S] = dqkv.abs()
+    ref_cm = pad.view(B, kb, 128, 3 * H).amax(2).reshape(B * kb, 3 * H)
+    ref_cm[:, :H] = 0.0
+    assert torch.equal(cm, ref_cm)
+    # through ops.attention: the scale sources attached to dQKV give its exact maxima
+    pg = fp32_mode.fp32_gemm_mode()
+    seen = {}
+    attach, attach_cols = gemm16.attach, gemm16.attach_cols
+
+    def rec_attach(t, parts):
+        seen['t'], seen['rows'] = t, parts
+        return attach(t, parts)
+
+    def rec_cols(t, src):
+        seen['cols'] = src
+        return attach_cols(t, src)
+    try:
+        fp32_mode.set_fp32_gemm('fp16x3')
+        gemm16.attach, gemm16.attach_cols = rec_attach, rec_cols
+        q = qkv.clone().requires_grad_()
+        o = ops.attention(q, mb, nh, 0.0, True)
+        o.backward(dout)
+    finally:
+        gemm16.attach, gemm16.attach_cols = attach, attach_cols
+        fp32_mode.set_fp32_gemm(pg)
+    dq = seen['t'].abs().view(B * S, 3 * H)
+    assert seen['rows'].shape == (B * S, nh + 1) and torch.equal(seen['rows'].amax(1), dq.amax(1))
+    assert seen['cols'].shape == (B * kb + 1, 3 * H) and torch.equal(seen['cols'].amax(0), dq.amax(0))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('dt', [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize('ntypes,H', [(2, 768), (1, 1024), (3, 320)])
 def test_embed_type_grad(dev, dt, ntypes, H):

@@ -1,7 +1,11 @@
 """Headline benchmark: BERT-base phase-1 (seq 128) pre-training throughput.
 
-Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 it
-is launched by ``torch.distributed.run`` (one rank per GPU, RCCL).  Runs the real
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``.  For N > 1 it runs one
+rank per GPU over RCCL either under ``torch.distributed.run`` (RANK / WORLD_SIZE in the env)
+or, launched plainly, by spawning its N rank processes itself on a 127.0.0.1 rendezvous
+before anything touches the GPU (``launch_ranks``; the reference's single-node self-spawn,
+hetseq/train.py:233-243).  A world that is not N, or a communicator that did not reduce over
+N ranks, exits non-zero.  Runs the real
 framework path -- synthetic NVIDIA-schema HDF5 shards -> native reader -> pinned
 staging on the HIP copy stream -> Controller.train_step (fused HIP kernels,
 hand-written fp16x3 GEMMs for every BERT linear and the MLM decoder, flat-buffer
@@ -158,10 +162,44 @@ def launch_nodes(a):
     return rc
 
 
+def launch_ranks(a):
+    """Parent of a plain ``bench.py --gpus N`` (N > 1, no RANK in the env): N rank processes with
+    the env a ``torch.distributed.run`` launch would give them (RANK = LOCAL_RANK = device index,
+    WORLD_SIZE = N, MASTER_ADDR 127.0.0.1 and a free port).  This process never touches the GPU.
+    When one rank fails the others (stuck in a collective) are terminated; returns the exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(a.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.gpus), LOCAL_WORLD_SIZE=str(a.gpus),
+                   GROUP_RANK='0', MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        time.sleep(0.2)
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                print('bench: a rank exited with {}; stopping the others'.format(code), file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+    return rc
+
+
 def node_worker(i, a):
     """One rank of a --nodes launch: rank = node base + i, device = node offset + i."""
     os.environ.update(RANK=str(a.node_rank + i), LOCAL_RANK=str(i), WORLD_SIZE=str(a.world))
-    run(a, a.node_rank + i, a.world, 0 if a.same_device else a.device_offset + i, a.init_method)
+    rc = run(a, a.node_rank + i, a.world, 0 if a.same_device else a.device_offset + i, a.init_method)
+    if rc:
+        sys.exit(rc)
 
 
 def main():
@@ -172,12 +210,17 @@ def main():
         import torch.multiprocessing as mp
         mp.spawn(node_worker, args=(a,), nprocs=a.node_gpus, join=True)
         return
+    if a.gpus > 1 and 'RANK' not in os.environ:
+        sys.exit(launch_ranks(a))
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
-    if world != a.gpus and world > 1:
-        print('warning: --gpus {} but WORLD_SIZE {}'.format(a.gpus, world), file=sys.stderr)
-    run(a, rank, world, 0 if a.same_device else local_rank, 'env://')
+    if world != a.gpus:
+        # e.g. torch.distributed.run with a different --nproc-per-node: never report an N-GPU
+        # number from another world size
+        print('bench: --gpus {} but the launch gives WORLD_SIZE {}'.format(a.gpus, world), file=sys.stderr)
+        sys.exit(2)
+    sys.exit(run(a, rank, world, 0 if a.same_device else local_rank, 'env://'))
 
 
 def run(a, rank, world, dev_index, init_method):
@@ -191,6 +234,11 @@ def run(a, rank, world, dev_index, init_method):
     from hetseq_9cme_amd.parallel import distributed as dist_utils
     from hetseq_9cme_amd import tasks
 
+    print('bench: rank {}/{} on device {} ({})'.format(rank, world, dev_index, init_method), file=sys.stderr,
+          flush=True)
+    if not torch.cuda.is_available():
+        print('bench: rank {} sees no GPU'.format(rank), file=sys.stderr, flush=True)
+        return 4
     torch.cuda.set_device(dev_index)
 
     cfg = {'base': BERT_BASE, 'large': BERT_LARGE, 'tiny': BERT_TINY}[a.model]
@@ -361,6 +409,8 @@ def run(a, rank, world, dev_index, init_method):
             'rccl_max_nchannels': os.environ.get('NCCL_MAX_NCHANNELS') if world > 1 else None,
             'rank_devices': dev_map,
         }
+        if ranks_seen != world:
+            rec['error'] = 'communicator reduced over {} ranks, world is {}'.format(ranks_seen, world)
         print(json.dumps(rec), flush=True)
     if a.profile_phases or a.sync_debug:
         # diagnostics run AFTER the timed region so they cannot perturb it
@@ -401,6 +451,10 @@ def run(a, rank, world, dev_index, init_method):
     if world > 1:
         torch.distributed.barrier()
         torch.distributed.destroy_process_group()
+    if ranks_seen != world:
+        print('bench: ranks_seen {} != world {}'.format(ranks_seen, world), file=sys.stderr)
+        return 3
+    return 0
 
 
 if __name__ == '__main__':

@@ -97,6 +97,25 @@ def test_bench_two_ranks_contract(tmp_path):
     assert all(v[0] == 0 for v in rec['rank_devices'].values())
 
 
+def test_bench_self_launch_two_ranks(tmp_path):
+    """A plain ``bench.py --gpus 2`` (no torch.distributed.run): bench.py spawns both ranks itself
+    on a 127.0.0.1 rendezvous, so the driver's N-GPU line can never come from one rank."""
+    import json
+    env = dict(os.environ, PYTHONPATH=ROOT, TMPDIR=str(tmp_path))
+    for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT'):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, 'bench.py'), '--gpus', '2', '--steps', '3', '--warmup', '1',
+           '--model', 'tiny', '--batch', '8', '--backend', 'gloo', '--same-device', '--num-workers', '1']
+    r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, timeout=300,
+                       cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith('{"metric"')]
+    assert len(lines) == 1, r.stdout[-3000:]
+    rec = json.loads(lines[0])
+    assert rec['n_gpus'] == 2 and rec['ranks_seen'] == 2 and rec['config']['global_batch'] == 16
+    assert rec['config']['parallelism'] == 'dp2' and 'error' not in rec
+
+
 def test_bench_heterogeneous_nodes_contract(tmp_path):
     """bench.py --nodes 2,1 (the BASELINE config-3 5+3 launch in miniature): one launcher per
     "node" spawns its ranks like train.py mode (a), all meet over one tcp:// rendezvous; rank 0

@@ -85,7 +85,7 @@ class _AttnFn(torch.autograd.Function):
             cm = torch.empty(B * ((S + 127) // 128), H, dtype=torch.float32, device=qkv.device)
             out, lse, dmask = C().attn_fwd_f16(qkv, mask_bias, num_heads, keep, seed, stream, bias, am, cm)
             # per-row (output projection) and per-column (its weight gradient) max |context|
-            gemm16.attach_cols(gemm16.attach(out, am), cm if cm.shape[0] <= 256 else None)
+            gemm16.attach_cols(gemm16.attach(out, am), gemm16.fit_cols(cm))
         else:
             out, lse, dmask = C().attn_fwd(qkv, mask_bias, num_heads, keep, seed, stream, bias)
         ctx.save_for_backward(qkv, mask_bias, out, lse, dmask)
@@ -113,19 +113,18 @@ class _AttnFn(torch.autograd.Function):
             B, S, H3 = qkv.shape
             kb = (S + 127) // 128
             am = torch.empty(B * S, num_heads, dtype=torch.float32, device=qkv.device)
-            cm = (torch.empty(B * kb, H3, dtype=torch.float32, device=qkv.device)
-                  if B * kb + (kb > 1) <= 256 else None)   # <= 256 column partials (+ the dQ row)
+            cm = torch.empty(B * kb, H3, dtype=torch.float32, device=qkv.device)
             dqkv, dbias = C().attn_bwd_f16(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep,
                                            ctx.bias, *slots, am, cm, want_dbias=ctx.want_db)
             if kb > 1:
                 rq, cq = C().amax_rows_cols(dqkv.view(B * S, H3)[:, :H3 // 3])
                 am = torch.cat([am, rq], 1)
-                if cm is not None:
-                    q = torch.zeros(1, H3, dtype=torch.float32, device=qkv.device)
-                    q[:, :H3 // 3] = cq
-                    cm = torch.cat([q, cm], 0)
-            # per-row (QKV data gradient) and per-column (QKV weight gradient) max |dQKV|
-            gemm16.attach_cols(gemm16.attach(dqkv, am), cm)
+                q = torch.zeros(1, H3, dtype=torch.float32, device=qkv.device)
+                q[:, :H3 // 3] = cq
+                cm = torch.cat([q, cm], 0)
+            # per-row (QKV data gradient) and per-column (QKV weight gradient) max |dQKV|; more
+            # than 256 column partials (B * key blocks) are folded to one row (same maxima)
+            gemm16.attach_cols(gemm16.attach(dqkv, am), gemm16.fit_cols(cm))
         else:
             dqkv, dbias = C().attn_bwd(dout.contiguous(), qkv, mask_bias, out, lse, dmask, num_heads, keep, ctx.bias,
                                        *slots, want_dbias=ctx.want_db)

@@ -472,6 +472,23 @@ class _LinearFn(torch.autograd.Function):
         return dx, dW, db, None
 
 
+def _record(side, *ts):
+    """``record_stream(side)`` on every tensor a side-stream weight gradient reads -- operands and
+    their scale sources (per-row / per-column max partials, which may be fresh allocations held
+    only by an attribute): without it the caching allocator could hand their memory to the
+    compute stream while the side-stream kernel still reads it.  Non-tensors (None, the LayerNorm's
+    ('affine', ...) column bound) are skipped."""
+    if side is None:
+        return
+    for t in ts:
+        if torch.is_tensor(t):
+            t.record_stream(side)
+        elif isinstance(t, (tuple, list)):
+            for u in t:
+                if torch.is_tensor(u):
+                    u.record_stream(side)
+
+
 def _f16_dgrad(dy2, dparts, wt, wparts, xshape, mbox):
     """``_dgrad`` on the fp16x3 GEMM: beta = 1 into the deposited residual gradient if any."""
     K = xshape[-1]
@@ -501,9 +518,7 @@ def _linear_backward_f16(ctx, dy):
         db = None
         if b is not None:
             db = C().colsum(dy2, None, grad_slot(b)) if dy2.shape[-1] % 4 == 0 else dy2.sum(0)
-    if side is not None:
-        for t in (dy2, x2, dparts, ctx.xparts):
-            t.record_stream(side)
+    _record(side, dy2, x2, dparts, ctx.xparts, dcols, xcols)
     return dx, dW, db, None
 
 
@@ -555,9 +570,7 @@ def _ffn_backward_f16(ctx, dy):
     side = side_begin(dy2.device, True) if slot2 is not None and slot1 is not None else None
     with torch.cuda.stream(side) if side is not None else _nullctx():
         dW2 = gemm16.wgrad(dy2, dcols, h, ctx.hcols, W2.shape[0], W2.shape[1], slot2)
-    if side is not None:
-        for t in (dy2, dparts, h, hparts, ctx.hcols):
-            t.record_stream(side)
+    _record(side, dy2, dparts, h, hparts, ctx.hcols, dcols)
     # GELU backward in the FFN-down data-gradient epilogue: t = (dy W2) * gelu'(u), d b1
     t, tparts, tcols, db1 = gemm16.gemm_dgelu(dy2 if dp is None else dp, dparts, w2t, p2, d, grad_slot(ctx.b1))
     if side is not None:
@@ -565,9 +578,7 @@ def _ffn_backward_f16(ctx, dy):
     xcols = ctx.xcols if ctx.xcols is not None else gemm16.cols(x2, x2)
     with torch.cuda.stream(side) if side is not None else _nullctx():
         dW1 = gemm16.wgrad(t, tcols, x2, xcols, W1.shape[0], W1.shape[1], slot1)
-    if side is not None:
-        for q in (t, tparts, tcols, x2, xparts):
-            q.record_stream(side)
+    _record(side, t, tparts, tcols, x2, xparts, xcols)
     dx = _f16_dgrad(t, tparts, w1t, p1, ctx.xshape, ctx.mbox)
     return dx, dW1, db1, dW2, None
 
@@ -805,13 +816,10 @@ class _Linear3Fn(torch.autograd.Function):
                     db = C().colsum(dy2.contiguous(), None, fb)
                 else:
                     db = dy2.float().sum(0)
-        if side is not None:
-            dy2.record_stream(side)
-            x2.record_stream(side)
-            if dys is not None:
-                dys.record_stream(side)
-            if ctx.f16:
-                ctx.xparts.record_stream(side)
+        if ctx.f16:
+            _record(side, dy2, x2, dys, ctx.xparts, dcols, xcols)
+        else:
+            _record(side, dy2, x2)
         if ctx.f16 and ctx.needs_input_grad[0]:
             dx = _f16_dgrad(dy2, dys, W, ctx.wparts, ctx.xshape, ctx.mbox)
         if not has_b:

@@ -250,13 +250,32 @@ def gemm_gelu(x2, xparts, W1, b1):
     [M, N tiles], h's column maxima per M tile [M tiles, N], W1^T's pieces, W1's column maxima)."""
     wf, wt, rmax, cmax = weight_pieces(W1)
     d, h, hrow, hcol = C().gemm_f16_gelu(x2, xparts, wf, rmax, b1, 1)
-    return d, h, hrow, hcol, wt, cmax
+    return d, h, fit_rows(hrow), fit_cols(hcol), wt, cmax
 
 
 def gemm_dgelu(dy2, dparts, wt2, wt2_parts, d, dbias_out):
     """FFN-down data gradient with the GELU backward: (t = (dy W2) * gelu'(u), t's per-row max |.|
     partials, t's column maxima per M tile, d b1)."""
-    return C().gemm_f16_dgelu(dy2, dparts, wt2, wt2_parts, d, None, dbias_out, 1)
+    t, trow, tcol, db = C().gemm_f16_dgelu(dy2, dparts, wt2, wt2_parts, d, None, dbias_out, 1)
+    return t, fit_rows(trow), fit_cols(tcol), db
+
+
+# the consumers' limits on producer-written partials (csrc/bindings.cpp: a GEMM's row scale source
+# has at most 64 partials per row, a weight gradient's column source at most 256 per column)
+MAX_ROW_PARTS = 64
+MAX_COL_PARTS = 256
+
+
+def fit_rows(p):
+    """Row partials [M, P] with P over the GEMMs' limit (an epilogue tile narrower than N / 64,
+    e.g. the 64-wide tile of an intermediate size > 4096) folded to [M, 1]: same maxima."""
+    return p.amax(1, keepdim=True) if p is not None and p.dim() == 2 and p.shape[1] > MAX_ROW_PARTS else p
+
+
+def fit_cols(p):
+    """Column partials [P, N] with P over the weight gradient's limit (more than 256 M tiles, e.g.
+    BERT-large's 64-row FFN tile above 16384 token rows) folded to [1, N]: same maxima."""
+    return p.amax(0, keepdim=True) if p is not None and p.dim() == 2 and p.shape[0] > MAX_COL_PARTS else p
 
 
 # ---------------------------------------------------------------- --precision bf16 (same kernel, one pass)

@@ -27,6 +27,8 @@ ROCM = os.environ.get('ROCM_PATH', '/opt/rocm')
 HIPCC = os.path.join(ROCM, 'bin', 'hipcc')
 ARCH = os.environ.get('PYTORCH_ROCM_ARCH', 'gfx950')
 HDF5_ROOT = os.environ.get('HDF5_ROOT', '/opt/conda')
+# what the last build_* call did per output: {basename: {'mode': 'compiled' | 'reused', 'objects': n}}
+LAST = {}
 
 
 def _torch_paths():
@@ -94,10 +96,13 @@ def build_kernels(force=False, jobs=8, verbose=False):
         for out in ex.map(_run, jobs_list):
             if verbose and out.strip():
                 print(out)
-    if force or jobs_list or _newer(out_so, objs):
+    linked = bool(force or jobs_list or _newer(out_so, objs))
+    if linked:
         _run([HIPCC, '-shared', '-fPIC', '--offload-arch=' + ARCH] + objs + ['-o', out_so, '-L' + tlib,
              '-lc10', '-lc10_hip', '-ltorch', '-ltorch_cpu', '-ltorch_hip', '-ltorch_python',
              '-Wl,-rpath,' + tlib])
+    LAST[os.path.basename(out_so)] = {'mode': 'compiled' if linked else 'reused', 'objects': len(jobs_list),
+                                      'arch': ARCH}
     return out_so
 
 
@@ -105,7 +110,9 @@ def build_data_native(force=False):
     os.makedirs(BUILD, exist_ok=True)
     src = os.path.join(CSRC, 'native', 'data_native.cpp')
     out_so = os.path.join(HERE, '_data_native' + EXT)
-    if force or _newer(out_so, [src]):
+    built = bool(force or _newer(out_so, [src]))
+    LAST[os.path.basename(out_so)] = {'mode': 'compiled' if built else 'reused', 'objects': int(built)}
+    if built:
         py_inc = sysconfig.get_paths()['include']
         # the compiler's own libstdc++ directory goes first in the rpath: the HDF5 prefix
         # (/opt/conda/lib) ships an older libstdc++ that lacks symbols g++ 11 emits, and
@@ -133,5 +140,5 @@ if __name__ == '__main__':
     ap.add_argument('-v', action='store_true')
     a = ap.parse_args()
     for so in build_all(a.force, a.j, a.v):
-        print('built', so)
+        print(LAST[os.path.basename(so)]['mode'], so)
     sys.exit(0)

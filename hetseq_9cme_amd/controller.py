@@ -198,9 +198,9 @@ class Controller(object):
             state = checkpoint_utils.load_checkpoint_to_cpu(filename)
             try:
                 self.get_model().load_state_dict(state['model'], strict=True)
-            except Exception:
+            except Exception as e:
                 raise Exception('Cannot load model parameters from checkpoint {}; '
-                                'please ensure that the architectures match.'.format(filename))
+                                'please ensure that the architectures match.'.format(filename)) from e
             extra_state = state['extra_state']
             self._optim_history = state['optimizer_history']
             last_optim_state = state.get('last_optimizer_state', None)

@@ -12,7 +12,7 @@ step.  PyTorch-ROCm's TunableOp layer lets us pin a solution per
 * ``table`` (default): loads the solution table shipped in
   ``hetseq_9cme_amd/tuning/gemm_gfx950.csv`` (tuned on an MI355X with
   ``tools/tune_gemm.sh``; fp32 keys for BERT-base phase 1/2 and BERT-large
-  phase 1 at their per-GPU batches, and -- round 5, ``tools/gpu/r5bv.sh`` -- the bf16 keys of
+  phase 1 at their per-GPU batches, and -- round 5 (its one-off GPU script is in git history) -- the bf16 keys of
   the ``--precision bf16`` BERT-base phase-1 products: 15.49-15.59 vs 15.74-15.90 ms/step,
   ``profiles/r5bw_bf16_tuned_table_ab.txt``), with tuning disabled -- shapes not in the table keep the
   library default, nothing is benchmarked at run time;

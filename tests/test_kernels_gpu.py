@@ -381,13 +381,19 @@ def test_training_gpu_matches_cpu(dev, tmp_path):
                                                                attention_probs_dropout_prob=0.0))
     vocab = write_vocab(str(tmp_path / 'v.txt'), 1024)
     outs = {}
-    for name, extra in (('gpu', ['--no-overlap-wgrad']), ('gpu_side', ['--overlap-wgrad']), ('cpu', ['--cpu'])):
+    runs = (('gpu', ['--no-overlap-wgrad', '--fp32-gemm', 'native']),
+            ('gpu_side', ['--overlap-wgrad', '--fp32-gemm', 'native']),
+            # the fp16x3 GEMMs with the weight gradients on the side stream: their operands' scale
+            # sources (column maxima) must stay alive for the side stream (record_stream)
+            ('f16', ['--no-overlap-wgrad', '--fp32-gemm', 'fp16x3']),
+            ('f16_side', ['--overlap-wgrad', '--fp32-gemm', 'fp16x3']),
+            ('cpu', ['--cpu']))
+    for name, extra in runs:
         save = str(tmp_path / name)
         cmd = [sys.executable, '-m', 'hetseq_9cme_amd.train', '--task', 'bert', '--data', str(d), '--dict', vocab,
                '--config_file', cfg, '--max-sentences', '8', '--fast-stat-sync', '--max-update', '3',
                '--disable-validation', '--num-workers', '1', '--lr', '1e-3', '--weight-decay', '0.01',
-               '--clip-norm', '0.5', '--save-dir', save, '--distributed-world-size', '1',
-               '--fp32-gemm', 'native'] + extra
+               '--clip-norm', '0.5', '--save-dir', save, '--distributed-world-size', '1'] + extra
         env = dict(os.environ, PYTHONPATH=root)
         r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env, timeout=300)
         assert r.returncode == 0, r.stdout[-3000:]
@@ -397,6 +403,9 @@ def test_training_gpu_matches_cpu(dev, tmp_path):
         _close(outs['gpu']['model'][k], v, rtol=1e-3, atol=2e-5)
         # (only the word-embedding scatter uses float atomics: order-dependent rounding)
         dmax = (outs['gpu_side']['model'][k] - outs['gpu']['model'][k]).abs().max().item()
+        assert dmax <= 1e-6, (k, dmax)
+        _close(outs['f16']['model'][k], v, rtol=1e-3, atol=2e-5)
+        dmax = (outs['f16_side']['model'][k] - outs['f16']['model'][k]).abs().max().item()
         assert dmax <= 1e-6, (k, dmax)
     sg, sc = outs['gpu']['last_optimizer_state']['state'], outs['cpu']['last_optimizer_state']['state']
     assert sorted(sg.keys()) == sorted(sc.keys())
@@ -696,14 +705,17 @@ def test_attention_op_fp32_split(dev):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('mode', ['fp16x3', 'bf16'])
-def test_attention_op_bias_grad_only(dev, mode):
+@pytest.mark.parametrize('mode', ['fp16x3', 'bf16', 'native'])
+@pytest.mark.parametrize('S', [128, 300, 512])
+def test_attention_op_bias_grad_only(dev, mode, S):
     """QKV bias already in qkv (the projection GEMM's epilogue, ``linear3(bias_grad=False)``):
     ``ops.attention(bias_grad=...)`` adds nothing and returns the bias gradients (the column sums
-    of dQKV) from the backward kernel -- equal to the attention-added path's."""
+    of dQKV) from the backward kernel -- equal to the attention-added path's.  S > 128: several key
+    blocks per head (dQ summed by atomics, dbias partials from every block); 'native': the fp32
+    MFMA kernel (attention.hip)."""
     from hetseq_9cme_amd.ops import fp32_mode
     torch.manual_seed(6)
-    B, S, nh, d = 32, 128, 2, 64
+    B, nh, d = 32 if S == 128 else 8, 2, 64
     H = nh * d
     dt = torch.bfloat16 if mode == 'bf16' else torch.float32
     base = torch.randn(B, S, 3 * H, device=dev).to(dt)
@@ -714,7 +726,7 @@ def test_attention_op_bias_grad_only(dev, mode):
     pg = fp32_mode.fp32_gemm_mode()
     outs = []
     try:
-        fp32_mode.set_fp32_gemm('fp16x3')
+        fp32_mode.set_fp32_gemm('native' if mode == 'native' else 'fp16x3')
         for pre in (False, True):
             qkv = (base.float() + torch.cat(bias).to(dev)).to(dt) if pre else base.clone()
             qkv.requires_grad_()

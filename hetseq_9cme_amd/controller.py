@@ -34,7 +34,7 @@ import torch
 
 from . import checkpoint_utils, ops
 from .ops import gemm_tuning
-from .options import comm_cus
+from .options import comm_cus, graph_train_step_enabled
 from .data.prefetch import unwrap
 from .optim import build_lr_scheduler, build_optimizer
 from .parallel import distributed as dist_utils
@@ -115,7 +115,7 @@ class Controller(object):
         self._save_thread = None
         self._transport_monitor = TransportErrorMonitor(lag=2)
         self._graph_step = None
-        if getattr(args, 'graph_train_step', False) and self.cuda:
+        if graph_train_step_enabled(args) and self.cuda:
             from .utils.train_graph import GraphedTrainStep
             self._graph_step = GraphedTrainStep(self)
         self._profile_phases = bool(getattr(args, 'profile_phases', False))

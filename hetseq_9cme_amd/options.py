@@ -62,14 +62,18 @@ def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialD
                              'products; measured GEMM error 0.6-0.7x native fp32\'s; the attention products as three '
                              'fp16 passes as well) or native (f32 MFMA, 157 TF/s peak, '
                              'through the libraries: the numerics oracle); see ops/fp32_mode.py')
-    parser.add_argument('--graph-train-step', action='store_true',
-                        help='single GPU, one micro-batch per update: capture each input shape\'s whole '
-                             'update (forward, backward, clip, optimizer) in a HIP graph after two eager '
-                             'warm-up steps and replay it -- removes the host launch overhead of '
-                             'small-batch fine-tuning (see utils/train_graph.py)')
+    parser.add_argument('--graph-train-step', dest='graph_train_step', action='store_const', const='on',
+                        default='auto',
+                        help='one micro-batch per update: capture each input shape\'s whole update (forward, '
+                             'backward, clip, optimizer; with an RCCL group the bucket all-reduces too) in a HIP '
+                             'graph after two eager warm-up steps and replay it -- removes the host launch '
+                             'overhead of small-batch fine-tuning (see utils/train_graph.py).  Default (auto): on '
+                             'for GPU token-classification fine-tuning (BertForTokenClassification), off otherwise; '
+                             'updates the graph cannot hold run eagerly either way')
+    parser.add_argument('--no-graph-train-step', dest='graph_train_step', action='store_const', const='off')
     parser.add_argument('--pad-to-multiple-of', type=int, default=None, metavar='N',
                         help='token-classification batches: pad sequence length to a multiple of N '
-                             '(default 16 under --graph-train-step, else the batch maximum)')
+                             '(default 16 when graph-captured updates are on, else the batch maximum)')
     parser.add_argument('--fused-kernels', default=True, type=eval_bool_arg,
                         help='use the hand-written HIP kernels on GPU (True) or plain torch ops')
     parser.add_argument('--user-module', default=None, metavar='PATH',
@@ -390,3 +394,18 @@ def parse_training_args(argv=None):
     args = parse_args_and_arch(parser, rest)
     args.lr_scheduler = pre.lr_scheduler
     return args
+
+
+# tasks whose GPU updates default to HIP-graph replay (--graph-train-step auto): small-batch
+# fine-tuning, host-bound when eager (docs/performance.md, NER)
+GRAPH_STEP_TASKS = ('BertForTokenClassification',)
+
+
+def graph_train_step_enabled(args):
+    """--graph-train-step on / off / auto (auto: on for GPU runs of GRAPH_STEP_TASKS)."""
+    v = getattr(args, 'graph_train_step', 'auto')
+    if v in (True, 'on'):
+        return True
+    if v in (False, None, 'off'):
+        return False
+    return getattr(args, 'task', None) in GRAPH_STEP_TASKS and not getattr(args, 'cpu', False)

@@ -57,7 +57,8 @@ class BertForTokenClassificationTask(Task):
         tokenizer = build_tokenizer(args.dict)
         # --graph-train-step captures one graph per batch shape: pad lengths to a multiple of 16
         # so a handful of shapes cover the corpus (attention masks make padding exact)
-        mult = getattr(args, 'pad_to_multiple_of', None) or (16 if getattr(args, 'graph_train_step', False) else None)
+        from .. import options
+        mult = getattr(args, 'pad_to_multiple_of', None) or (16 if options.graph_train_step_enabled(args) else None)
         collator = cls.collator_cls(tokenizer, max_length=args.max_pred_length, padding=True,
                                     pad_to_multiple_of=mult)
         files = {'train': args.train_file, 'validation': args.validation_file, 'test': args.test_file}

@@ -132,3 +132,20 @@ def test_overlap_wgrad_modes():
             fused.set_side_stream('sometimes')
     finally:
         fused._Side.mode = prev
+
+
+def test_graph_train_step_modes():
+    """--graph-train-step is tri-state: default 'auto' = on for GPU token-classification
+    fine-tuning only; explicit on / off win; --cpu never captures."""
+    from types import SimpleNamespace as NS
+    from hetseq_9cme_amd import options
+    on = options.graph_train_step_enabled
+    assert on(NS(graph_train_step='auto', task='BertForTokenClassification', cpu=False))
+    assert not on(NS(graph_train_step='auto', task='BertForTokenClassification', cpu=True))
+    assert not on(NS(graph_train_step='auto', task='bert', cpu=False))
+    assert on(NS(graph_train_step='on', task='bert', cpu=False))
+    assert not on(NS(graph_train_step='off', task='BertForTokenClassification', cpu=False))
+    base = ['--task', 'mnist', '--data', '/tmp']
+    assert options.parse_training_args(base).graph_train_step == 'auto'
+    assert options.parse_training_args(base + ['--graph-train-step']).graph_train_step == 'on'
+    assert options.parse_training_args(base + ['--no-graph-train-step']).graph_train_step == 'off'

@@ -90,8 +90,9 @@ def test_graph_step_matches_eager_ner_shapes(dev, tmp_path):
             '--max-sentences', '8', '--num-workers', '1', '--find-unused-parameters', '--disable-validation',
             '--no-save', '--pad-to-multiple-of', '4']
     n = 30
-    eager = _run(argv, n)
-    graph = _run(argv + ['--graph-train-step'], n)
+    eager = _run(argv + ['--no-graph-train-step'], n)
+    assert eager[0]._graph_step is None
+    graph = _run(argv, n)   # the default for token classification on a GPU: graph-captured updates
     gs = graph[0]._graph_step
     assert gs.captures >= 2, gs.captures
     _compare(eager, graph, 1e-4)

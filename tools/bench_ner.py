@@ -33,7 +33,14 @@ def main():
     ap.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'])
     ap.add_argument('--profile-phases', action='store_true', help='host/device time per step phase (stderr)')
     ap.add_argument('--gemm-tuning', default='table', choices=['off', 'table'])
-    ap.add_argument('--graph-train-step', action='store_true', help='replay captured HIP graphs of the update')
+    ap.add_argument('--graph-train-step', dest='graph_train_step', action='store_const', const='on', default='auto',
+                    help='replay captured HIP graphs of the update (default auto = the framework default: on for '
+                         'this task on a GPU)')
+    ap.add_argument('--no-graph-train-step', dest='graph_train_step', action='store_const', const='off',
+                    help='eager updates')
+    ap.add_argument('--repeats', type=int, default=5,
+                    help='timed blocks of --steps updates each; min / median / max of their s/update reported '
+                         '(value = the median)')
     ap.add_argument('--no-overlap-wgrad', action='store_true', help='weight gradients on the compute stream')
     ap.add_argument('--cprofile', default=None, metavar='OUT',
                     help='after the timed steps, cProfile 20 more steps and write the top host functions to OUT')
@@ -77,8 +84,8 @@ def main():
             '--gemm-tuning', a.gemm_tuning]
     if a.profile_phases:
         argv.append('--profile-phases')
-    if a.graph_train_step:
-        argv.append('--graph-train-step')
+    if a.graph_train_step != 'auto':
+        argv.append('--graph-train-step' if a.graph_train_step == 'on' else '--no-graph-train-step')
     if a.no_overlap_wgrad:
         argv.append('--no-overlap-wgrad')
     if a.fp32_gemm:
@@ -116,24 +123,32 @@ def main():
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
     t_data = t_step = 0.0
-    for _ in range(a.steps):
-        ta = time.perf_counter()
-        batch = next(itr)
-        tb = time.perf_counter()
-        ctrl.train_step(batch)
-        t_data += tb - ta
-        t_step += time.perf_counter() - tb
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / a.steps
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device='cuda')
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-        dt = float(t.item())
+    blocks = []
+    for _ in range(max(1, a.repeats)):
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            ta = time.perf_counter()
+            batch = next(itr)
+            tb = time.perf_counter()
+            ctrl.train_step(batch)
+            t_data += tb - ta
+            t_step += time.perf_counter() - tb
+        torch.cuda.synchronize()
+        if world > 1:
+            torch.distributed.barrier()
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / a.steps
+        if world > 1:
+            t = torch.tensor([dt], dtype=torch.float64, device='cuda')
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+            dt = float(t.item())
+        blocks.append(dt)
+    nb = len(blocks)
+    spread = sorted(blocks)
+    dt = spread[nb // 2]
+    t_data /= nb
+    t_step /= nb
     gs = ctrl._graph_step
     replay_ms = None
     if gs is not None:
@@ -174,7 +189,10 @@ def main():
                           'n_gpus': world, 'steps': a.steps, 'warmup': a.warmup,
                           'reference_1gpu': 0.214, 'speedup_vs_reference': round(0.214 / dt, 1),
                           'batch': a.batch, 'global_batch': a.batch * world, 'dtype': a.precision,
-                          'graph_train_step': a.graph_train_step, 'force_reducer': a.force_reducer,
+                          'graph_train_step': gs is not None, 'force_reducer': a.force_reducer,
+                          'repeats': nb, 's_per_update_min_median_max': [round(spread[0], 5), round(dt, 5),
+                                                                         round(spread[-1], 5)],
+                          'first_block_s': round(blocks[0], 5),
                           'fp32_gemm': args.fp32_gemm if a.precision == 'fp32' else None,
                           'graph_replays': gs.replays if gs is not None else 0,
                           'graph_replay_device_ms': replay_ms,

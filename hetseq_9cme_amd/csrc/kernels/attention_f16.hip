@@ -12,12 +12,12 @@
 // the largest magnitude of an operand lands below 2^15:
 //   K, V      one exponent per workgroup (its 128 keys), fixed for the kernel;
 //   Q, dO     one running exponent per workgroup: each 32-query tile's max |x| is reduced over the
-//             workgroup before the tile is split, and the exponent only ever decreases -- the dK
-//             and dV accumulators (which sum over query tiles) are rescaled by the exact power of
-//             two when it does;
+//             workgroup before the tile is split; the exponent follows the tiles down at once and up
+//             when a tile lies more than 2^12 below it (next_exp) -- the dK and dV accumulators
+//             (which sum over query tiles) are rescaled by the exact power of two when it moves;
 //   Pd        fixed: P <= 1, so Pd <= 1 / keep;
 //   dS (dK)   one running exponent per wave (its 32 keys), from the wave's max |dS| of each tile,
-//             again with an exact rescale of the wave's dK accumulator when it decreases;
+//             again with an exact rescale of the wave's dK accumulator when it moves;
 //   dS (dQ)   one exponent per tile over the workgroup's 128 keys: dS goes through LDS as fp32 and
 //             is split after the barrier that publishes every wave's max.
 // Unscaling is exact (ldexp) and happens on the fp32 results: S and dP per tile, dQ per tile, dK
@@ -85,6 +85,22 @@ __device__ __forceinline__ f32x4 mfma16(f16x8 a, f16x8 b, f32x4 c) {
 
 // exponent for an operand whose max |x| so far is m (zeros: no constraint)
 __device__ __forceinline__ int run_exp(float m) { return m > 0.f ? f16_scale_exp(m) : kNoScale; }
+
+// Running exponent of a tiled operand whose accumulators are rescaled exactly when it moves: the
+// next tile (max |x| = m) lowers it at once, but raises it only when the tile lies more than
+// 2^kRaise below it -- a value down to 2^-17 of the scaled range keeps both pieces normal (22 bits),
+// so tiles within 2^kRaise need no rescale -- and never above lo + kSpan, lo the smallest exponent
+// seen (accumulators built at lo hold <= 2^43 at S <= 8192: 2^(43 + 2 kSpan) stays finite for the dK
+// accumulator, whose exponent is the sum of two).  Zero tiles leave it alone.  Rows far below
+// earlier, larger rows (a decreasing ramp) thus keep the 22 bits of their own exponent.
+constexpr int kRaise = 12, kSpan = 36;
+__device__ __forceinline__ int next_exp(int cur, float m, int& lo) {
+  if (!(m > 0.f)) return cur;
+  const int t = f16_scale_exp(m);
+  const int e = t < cur ? t : t > cur + kRaise ? min(t, lo + kSpan) : cur;
+  lo = min(lo, e);
+  return e;
+}
 
 // 8 fp32 values * s -> two fp16 pieces
 __device__ __forceinline__ void sp8(const f32x8 x, float s, f16x8 (&p)[2]) {
@@ -355,6 +371,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const int ep = f16_scale_exp(inv_keep);   // Pd <= 1 / keep
   const float keep_s = ldexpf(inv_keep, ep), one_s = ldexpf(1.f, ep);
   int dv_e = ed, es = kNoScale, dk_e = eq + kNoScale;
+  int eq_lo = eq, ed_lo = ed, es_lo = kNoScale;   // the smallest exponents seen (next_exp)
   float cq0 = 0.f, cq1 = 0.f;
 
   // split the prefetched tile into the piece images (+ bias, 1/8 on Q) at the running exponents,
@@ -443,7 +460,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     smax = wave_max(smax);
     if (lane == 0) ScS[w] = smax;
     {   // the wave's dS exponent (running, decreasing) and the dK accumulator's
-      const int es_new = min(es, run_exp(smax));
+      const int es_new = next_exp(es, smax, es_lo);
       rescale2_if(eq + es_new != dk_e, dk0, dk1, eq + es_new - dk_e);
       dk_e = eq + es_new;
       es = es_new;
@@ -479,8 +496,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const int et = run_exp(max4(ScS));   // this tile's dS exponent over the 128 keys
     const float st = ldexpf(1.f, et);
     if (more) {
-      eq = min(eq, run_exp(max4(ScQ)));
-      ed = min(ed, run_exp(max4(ScD)));
+      eq = next_exp(eq, max4(ScQ), eq_lo);
+      ed = next_exp(ed, max4(ScD), ed_lo);
     }
     // ---- dQ = dS . K over the block's 128 keys (16x16x32 tiles); dq_sw: this lane row's half swap
     const int dq_sw = 4 * ((r16 >> 2) & 1);

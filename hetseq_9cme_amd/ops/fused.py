@@ -116,30 +116,33 @@ def _dgrad_bf16(dy2, W, xshape, mbox, wt=None):
 
 # ----------------------------------------------------------------- weight-grad side stream
 class _Side(object):
-    # 'auto' (default) = 'off' since the two-waves-per-SIMD fp16x3 attention backward: with the
-    # weight gradients on the compute stream BERT-base phase 1 runs 36.42 vs 36.80 ms/step, phase 2
-    # 42.04 vs 43.15 (profiles/r4p_overlap_ab.md; round 3 measured the side stream 1 ms ahead on
-    # the x6 attention).  'on' (--overlap-wgrad): the side stream on every path.
+    # 'auto' (default): the side stream for products of >= AUTO_ROWS token rows (BERT-base phase 1
+    # at 128 sequences per GPU, phase 2), the compute stream below (batch 32, fine-tuning).  Round 6,
+    # same box, alternated: batch 128 35.38 / 35.43 vs 36.56 / 35.48 ms/step with / without
+    # (profiles/r6e_overlap_ab.txt); batch 32 13.52 vs 13.32.  (Round 4, before the attention and
+    # GEMM changes since, had measured the compute stream ahead: profiles/r4p_overlap_ab.md.)
+    # 'on' (--overlap-wgrad) / 'off' (--no-overlap-wgrad): every product / none.
     mode = 'auto'
+    AUTO_ROWS = 8192
     streams = {}          # device index -> torch.cuda.Stream
     active = set()        # device indices with side work queued in the current backward
 
 
 def set_side_stream(flag):
-    """Weight-gradient work on a side stream: True / 'on', False / 'off', or 'auto' (= off, the
-    measured default)."""
+    """Weight-gradient work on a side stream: True / 'on', False / 'off', or 'auto' (on for products
+    of >= _Side.AUTO_ROWS token rows, the measured default)."""
     _Side.mode = {True: 'on', False: 'off'}.get(flag, flag) if isinstance(flag, bool) else str(flag)
     assert _Side.mode in ('on', 'off', 'auto'), flag
 
 
-def side_begin(device, hand=False):
+def side_begin(device, rows=0):
     """Side stream for off-critical-path weight-gradient work (dW GEMMs, bias
     column sums) of the running backward, ordered after everything already
     queued on the compute stream.  While the compute stream continues with the
     dgrad chain (attention / LayerNorm / GELU backward: mostly memory-bound),
     the side stream's GEMMs fill the matrix cores.  Joined back into the compute
     stream by an end-of-backward callback (``side_join``)."""
-    if _Side.mode != 'on' or device.type != 'cuda':
+    if device.type != 'cuda' or _Side.mode == 'off' or (_Side.mode == 'auto' and rows < _Side.AUTO_ROWS):
         return None
     idx = device.index if device.index is not None else torch.cuda.current_device()
     st = _Side.streams.get(idx)
@@ -457,7 +460,7 @@ class _LinearFn(torch.autograd.Function):
         else:
             dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox)
         slot = grad_slot(W)
-        side = side_begin(dy2.device) if slot is not None else None
+        side = side_begin(dy2.device, dy2.shape[0]) if slot is not None else None
         with torch.cuda.stream(side) if side is not None else _nullctx():
             dW = _wgrad(dy2, x2, slot)
             db = None
@@ -512,7 +515,7 @@ def _linear_backward_f16(ctx, dy):
     dx = (_f16_dgrad(dy2 if dp is None else dp, dparts, wt, ctx.wparts, ctx.xshape, ctx.mbox)
           if ctx.needs_input_grad[0] else None)
     slot = grad_slot(W)
-    side = side_begin(dy2.device, True) if slot is not None else None
+    side = side_begin(dy2.device, dy2.shape[0]) if slot is not None else None
     with torch.cuda.stream(side) if side is not None else _nullctx():
         dW = gemm16.wgrad(dy2, dcols, x2, xcols, W.shape[0], W.shape[1], slot)
         db = None
@@ -567,14 +570,14 @@ def _ffn_backward_f16(ctx, dy):
     dp = gemm16.take_pieces(dy)
     slot2, slot1 = grad_slot(W2), grad_slot(W1)
     # each weight gradient on the side stream, beside the next data-gradient GEMM
-    side = side_begin(dy2.device, True) if slot2 is not None and slot1 is not None else None
+    side = side_begin(dy2.device, dy2.shape[0]) if slot2 is not None and slot1 is not None else None
     with torch.cuda.stream(side) if side is not None else _nullctx():
         dW2 = gemm16.wgrad(dy2, dcols, h, ctx.hcols, W2.shape[0], W2.shape[1], slot2)
     _record(side, dy2, dparts, h, hparts, ctx.hcols, dcols)
     # GELU backward in the FFN-down data-gradient epilogue: t = (dy W2) * gelu'(u), d b1
     t, tparts, tcols, db1 = gemm16.gemm_dgelu(dy2 if dp is None else dp, dparts, w2t, p2, d, grad_slot(ctx.b1))
     if side is not None:
-        side = side_begin(dy2.device, True)   # after t
+        side = side_begin(dy2.device, dy2.shape[0])   # after t
     xcols = ctx.xcols if ctx.xcols is not None else gemm16.cols(x2, x2)
     with torch.cuda.stream(side) if side is not None else _nullctx():
         dW1 = gemm16.wgrad(t, tcols, x2, xcols, W1.shape[0], W1.shape[1], slot1)
@@ -798,7 +801,7 @@ class _Linear3Fn(torch.autograd.Function):
         bs = [grad_slot(t) for t in (bq, bk, bv)] if has_b else [None, None, None]
         fb = _adjacent_view(bs) if all(t is not None for t in bs) else None
         direct = fused is not None and (fb is not None or not has_b)
-        side = side_begin(dy2.device, ctx.f16) if direct else None
+        side = side_begin(dy2.device, dy2.shape[0]) if direct else None
         with torch.cuda.stream(side) if side is not None else _nullctx():
             if fused is not None:
                 wg(fused)
@@ -902,7 +905,7 @@ class _DecoderXentFn(torch.autograd.Function):
             dh = gemm16.mm_bf16(dl_full, wt).mul_(scale.to(dl.dtype))
         else:
             dh = torch.mm(dl, cast_w(W, dl.dtype)).mul_(scale.to(dl.dtype))
-        side = side_begin(dl.device) if slot is not None else None
+        side = side_begin(dl.device, dl.shape[0]) if slot is not None else None
         with torch.cuda.stream(side) if side is not None else _nullctx():
             if ctx.b16 and C().wgrad_bf16_ok(dl_full, hs):
                 # over the padded vocabulary (whole 128-row tiles); rows past V are not stored

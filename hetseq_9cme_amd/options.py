@@ -85,12 +85,12 @@ def get_training_parser(task='bert', optimizer='adam', lr_scheduler='PolynomialD
     parser.add_argument('--gemm-tuning-file', default=None, metavar='PATH',
                         help='where --gemm-tuning online writes its table (device ordinal appended)')
     parser.add_argument('--overlap-wgrad', dest='overlap_wgrad', action='store_const', const='on', default='auto',
-                        help='run weight-gradient GEMMs / bias column sums on a side HIP stream, concurrent '
-                             'with the data-gradient chain (default: on the compute stream -- measured faster '
-                             'since the fp16x3 attention backward runs two waves per SIMD: '
-                             'profiles/r4p_overlap_ab.md)')
+                        help='run every weight-gradient GEMM / bias column sum on a side HIP stream, '
+                             'concurrent with the data-gradient chain (default, auto: the side stream for '
+                             'products of >= 8192 token rows -- BERT-base phase 1 at 128 sequences per GPU, phase '
+                             '2 -- the compute stream for smaller ones; measured, profiles/r6e_overlap_ab.txt)')
     parser.add_argument('--no-overlap-wgrad', dest='overlap_wgrad', action='store_const', const='off',
-                        help='weight gradients on the compute stream (the default)')
+                        help='weight gradients on the compute stream always')
     parser.add_argument('--debug-kernels', action='store_true',
                         help='debug mode: serialised kernel launches (AMD_SERIALIZE_KERNEL=3, '
                              'HIP_LAUNCH_BLOCKING=1), range checks on token/type ids and labels and finite '

@@ -114,7 +114,7 @@ def test_dispatch_single_backend(monkeypatch, config):
 
 
 def test_overlap_wgrad_modes():
-    """--overlap-wgrad is tri-state: default 'auto' (= off, the measured default),
+    """--overlap-wgrad is tri-state: default 'auto' (the side stream from 8192 token rows),
     '--overlap-wgrad' = on, '--no-overlap-wgrad' = off; CPU tensors never get a side stream."""
     from hetseq_9cme_amd import options
     from hetseq_9cme_amd.ops import fused
@@ -127,7 +127,7 @@ def test_overlap_wgrad_modes():
         for flag, mode in ((True, 'on'), (False, 'off'), ('auto', 'auto'), ('on', 'on')):
             fused.set_side_stream(flag)
             assert fused._Side.mode == mode
-            assert fused.side_begin(torch.device('cpu'), True) is None
+            assert fused.side_begin(torch.device('cpu'), 16384) is None
         with pytest.raises(AssertionError):
             fused.set_side_stream('sometimes')
     finally:

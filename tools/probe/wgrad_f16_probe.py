@@ -1,0 +1,70 @@
+"""Timing-only probe of the fp16x3 weight gradient (wgrad_f16_k, 256 x 256 tile): what the k loop's
+parts cost.  HX_WGRAD_PROBE (a measurement build's switch; results are WRONG for 1-7): 0 normal,
+1 every stage re-reads the first 32 tokens (cache-resident loads), 2 no split (raw bits as pieces),
+6 no split and no piece stores (stale LDS), 7 all three.  ``python tools/probe/wgrad_f16_probe.py``"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+
+
+def timed(fn, n=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) * 1e3 / n
+
+
+def main():
+    from hetseq_9cme_amd.ops._ext import C
+    T = 16384
+    g = torch.Generator(device='cuda').manual_seed(0)
+    for (M, N) in [(2304, 768), (3072, 768), (768, 3072), (768, 768)]:
+        dy = torch.randn(T, M, device='cuda', generator=g)
+        x = torch.randn(T, N, device='cuda', generator=g)
+        dc, xc = C().amax_cols(dy), C().amax_cols(x)
+        out = torch.empty(M, N, device='cuda')
+        row = []
+        for p in ('0', '1', '2', '6', '7'):
+            os.environ['HX_WGRAD_PROBE'] = p
+            us = timed(lambda: C().wgrad_f16(dy, dc, x, xc, out))
+            row.append('{}: {:.1f} us ({:.0f} TF/s pieces)'.format(p, us, 3 * 2.0 * T * M * N / us / 1e6))
+        os.environ.pop('HX_WGRAD_PROBE')
+        print('wgrad {}x{} T{}: '.format(M, N, T) + ', '.join(row), flush=True)
+
+
+if __name__ == '__main__' and len(sys.argv) == 1:
+    main()
+
+
+def gemm_main():
+    """The same for the forward / data-gradient GEMM (gemm_f16_k 256 x 192, plain epilogue, fp32 A):
+    HX_GEMM_PROBE 0 normal, 2 cache-resident DMA (every k step re-reads stage 0), 3 no split of A,
+    4 both."""
+    from hetseq_9cme_amd.ops._ext import C
+    T = 16384
+    g = torch.Generator(device='cuda').manual_seed(0)
+    for (N, K) in [(2304, 768), (768, 768), (768, 3072)]:
+        x = torch.randn(T, K, device='cuda', generator=g)
+        W = torch.randn(N, K, device='cuda', generator=g) * 0.03
+        xp = C().amax_rows(x)
+        wf, wt, wp, wc = C().split_weight_f16([W])[0]
+        row = []
+        for p in ('0', '2', '3', '4'):
+            os.environ['HX_GEMM_PROBE'] = p
+            us = timed(lambda: C().gemm_f16(x, xp, wf, wp))
+            row.append('{}: {:.1f} us ({:.0f} TF/s pieces)'.format(p, us, 3 * 2.0 * T * N * K / us / 1e6))
+        os.environ.pop('HX_GEMM_PROBE')
+        print('gemm N{} K{} T{}: '.format(N, K, T) + ', '.join(row), flush=True)
+
+
+if __name__ == '__main__' and len(sys.argv) > 1 and sys.argv[1] == 'gemm':
+    gemm_main()

@@ -28,7 +28,8 @@ while [ $# -gt 0 ]; do
     ner)     run_step 400 $out.log python -u tools/bench_ner.py $a || exit 1 ;;
     profile) run_step 400 $out.log rocprofv3 --kernel-trace --stats -d /tmp/prof$n -o run -- \
                python3 bench.py --steps 5 --warmup 3 $a || exit 1
-             python tools/prof_summary.py /tmp/prof$n/run_results.db --steps 6 --marker adam_k --top 45 > $out.md ;;
+             python tools/prof_summary.py /tmp/prof$n/run_results.db --steps 6 --marker adam_k --top 45 > $out.md
+             python tools/step_sequence.py /tmp/prof$n/run_results.db > ${out}_sequence.md || true ;;
     pmc)     run_step 120 $out.log timeout -s KILL 100 rocprofv3 --pmc $a --output-format csv -d /tmp/pmc$n -o run -- \
                python3 tools/probe/gemm_f16_bench.py || exit 1
              python tools/pmc_summary.py /tmp/pmc$n/run_counter_collection.csv > $out.md 2>&1 || true ;;

@@ -1,5 +1,7 @@
 """Timing-only probe of the fp16x3 weight gradient (wgrad_f16_k, 256 x 256 tile): what the k loop's
-parts cost.  HX_WGRAD_PROBE (a measurement build's switch; results are WRONG for 1-7): 0 normal,
+parts cost (profiles/r6g_gemm_wgrad_split_probe.md).  The switches lived in a measurement build of
+gemm_f16.hip (a PRB template parameter read from the env at launch) that was removed after
+measuring; the production kernels ignore these variables.  HX_WGRAD_PROBE (results WRONG for 1-7): 0 normal,
 1 every stage re-reads the first 32 tokens (cache-resident loads), 2 no split (raw bits as pieces),
 6 no split and no piece stores (stale LDS), 7 all three.  ``python tools/probe/wgrad_f16_probe.py``"""
 import os

@@ -30,12 +30,14 @@ def main():
     T = 16384
     g = torch.Generator(device='cuda').manual_seed(0)
     for (M, N) in [(2304, 768), (3072, 768), (768, 3072), (768, 768)]:
+        os.environ.pop('HX_WGRAD_PROBE', None)
         dy = torch.randn(T, M, device='cuda', generator=g)
         x = torch.randn(T, N, device='cuda', generator=g)
         dc, xc = C().amax_cols(dy), C().amax_cols(x)
         out = torch.empty(M, N, device='cuda')
+        timed(lambda: C().wgrad_f16(dy, dc, x, xc, out), n=100)   # warm the clock / caches first
         row = []
-        for p in ('0', '1', '2', '6', '7'):
+        for p in os.environ.get('PROBES', '0,1,2,6,7').split(','):
             os.environ['HX_WGRAD_PROBE'] = p
             us = timed(lambda: C().wgrad_f16(dy, dc, x, xc, out))
             row.append('{}: {:.1f} us ({:.0f} TF/s pieces)'.format(p, us, 3 * 2.0 * T * M * N / us / 1e6))

@@ -1222,8 +1222,10 @@ int hx_gemm_f16_plan(int M, int N, int K) {
   // data gradients 64-76 vs 65-83); the 128 x 96 tile keeps the shallow narrow ones (attention
   // output 24 vs 42 us).  Down to M = 512 when the N tiles alone fill the CUs: the MLM decoder
   // forward at batch 32 (640 masked rows x 30528) 122 vs 181-213 us on the 64 x 64 tile (r5bq)
+  // (deep reductions from M = 4096: at M = 2048 -- NER fine-tuning batches -- the QKV data
+  // gradient runs 38 us on 128 x 96 against 46-50 us on the large tile with split-K, r6j)
   if (M >= 512 && N % 192 == 0 &&
-      (10 * ((M + 255) / 256) * (N / 192) >= 7 * hx_cu_slots() || (K >= 2048 && M >= 2048)))
+      (10 * ((M + 255) / 256) * (N / 192) >= 7 * hx_cu_slots() || (K >= 2048 && M >= 4096)))
     return 1;
   // 128 x 96 from 1024 rows, or from 512 with a split-K-deep reduction (the decoder's data
   // gradient at batch 32: 117 vs 137-152 us on the large tile, r5bq)

@@ -340,6 +340,13 @@ def mm_bf16(a2, b, out=None, beta=False, bias=None, out_bf16=True):
         if beta:
             return out.view(a2.shape[0], b.shape[0]).addmm_(a2, b.t())
         if bias is not None:
+            # the library epilogue takes the bias in the operands' dtype: it is rounded to bf16 before
+            # the add (the hand-written kernel adds it in fp32) -- one extra bf16 rounding of the bias
+            # on an output that is rounded to bf16 anyway
+            if out is not None:
+                return torch.addmm(bias.to(torch.bfloat16), a2, b.t(), out=out.view(a2.shape[0], b.shape[0]))
             return torch.addmm(bias.to(torch.bfloat16), a2, b.t())
+        if out is not None:
+            return torch.mm(a2, b.t(), out=out.view(a2.shape[0], b.shape[0]))
         return torch.mm(a2, b.t())
     return C().gemm_bf16(a2, b, out=out, beta=beta, bias=bias, out_bf16=out_bf16)

@@ -1012,6 +1012,225 @@ void wgrad_launch(const float* A, int lda, const HxColScale& ca, const float* B,
   }
 }
 
+// ---------------------------------------------------------------- weight gradient, add-tid staging
+// The same product as wgrad_f16_k on the 256 x 256 tile, with the piece tiles written to LDS by
+// ds_write_addtid_b32 (lane l -> dword l of a 256-B block: 128 B/clk/CU) instead of ds_write_b128
+// (~79 B/clk/CU, MI355X_MICROARCH.md §LDS): the piece stores were the largest non-MFMA cost of the
+// k loop (profiles/r6g_gemm_wgrad_split_probe.md: -14..-19 % without them).
+// Per 16-token stage, each of the 8 waves loads 8 (token row, 128-column block) units of ONE
+// operand: lane l takes the two columns 2 ((l + 16 r) & 63) of the block (a b64 load; 512 B per
+// wave-load, permuted inside the row), splits the pair at its column scales and stores one dword
+// per piece at slot l.  Image per (stage, piece, operand): [16 rows][2 blocks][64 slots x 4 B],
+// slot l of row r holding column pair (l + 16 r) & 63: the rotation by 16 pairs per row puts the
+// four rows of a transposed 16-lane read (ds_read_b64_tr_b16: lane 4q + p reads row q, columns
+// 4p .. 4p + 3) on four disjoint 16-bank ranges -- conflict-free reads, and every store is one
+// contiguous 256-B block.  Layout: stage 32 KiB, piece 16 KiB, operand 8 KiB, row 512 B, block
+// 256 B (64 KiB double-buffered: every store address is M0 (< 16 KiB) + a 16-bit immediate).
+// Loads run two stages ahead in a two-set register ring.
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+template <int C0>
+__device__ __forceinline__ void st_tid2(uint32_t m0, uint32_t h0, uint32_t h1) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+               "ds_write_addtid_b32 %1 offset:%4\n\tds_write_addtid_b32 %2 offset:%5\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(h0), "v"(h1), "s"(m0), "i"(C0), "i"(C0 + 16384)
+               : "memory");
+}
+
+__global__ __launch_bounds__(512) void wgrad_f16_tid_k(const float* __restrict__ A, int lda, const HxColScale ca,
+                                                        const float* __restrict__ B, int ldb, const HxColScale cb,
+                                                        float* __restrict__ out, int M, int N, int T, int kchunk,
+                                                        int nsplit, int mvalid) {
+  constexpr int BM = 256, BN = 256, WM = 128, WN = 64, NWM = 2, MB = 4, NB = 2, BKT = 16;
+  constexpr int STG = 32768, PCE = 16384, OPB = 8192;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  float* tsa = reinterpret_cast<float*>(lds + 2 * STG);
+  float* tia = tsa + BM;
+  float* tsb = tia + BM;
+  float* tib = tsb + BN;
+  float* red = tib + BN;
+
+  const int total = (M / BM) * (N / BN) * nsplit;
+  const int per = (total + 7) / 8;
+  const int work = (blockIdx.x % 8) * per + blockIdx.x / 8;
+  if (work >= total) return;   // uniform per workgroup
+  const int TM = M / BM, TN = N / BN;
+  const bool mord = M < N;
+  const int nt = mord ? (work / TM) % TN : work % TN;
+  const int mt = mord ? work % TM : (work / TN) % TM;
+  const int sp = work / (TN * TM);
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int t0 = sp * kchunk, t1 = min(T, t0 + kchunk);
+  const int nit = (t1 - t0 + BKT - 1) / BKT;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w % NWM, wn = w / NWM;
+  const int wv = __builtin_amdgcn_readfirstlane(w);
+
+  col_scales(ca, m0, BM, tsa, tia, red);
+  col_scales(cb, n0, BN, tsb, tib, red);
+  __syncthreads();
+
+  // ---- this wave's staging units: operand op, column block blk, token rows par + 2 i (i < 8)
+  const int op = wv & 1, blk = (wv >> 1) & 1, par = wv >> 2;
+  const float* src = op ? B : A;
+  const int ld = op ? ldb : lda;
+  const hx::Buf buf(src + (int64_t)t0 * ld, (uint32_t)((int64_t)(t1 - t0) * ld * 4));
+  const float* tsc = op ? tsb : tsa;
+  const int pe = (lane + 16 * par) & 63, po = (lane + 16 * (par + 2)) & 63;   // column pairs (even / odd i)
+  const int ce = 128 * blk + 2 * pe, co = 128 * blk + 2 * po;
+  const uint32_t ve = (uint32_t)((op ? n0 : m0) + ce) * 4, vo = (uint32_t)((op ? n0 : m0) + co) * 4;
+  const float se0 = tsc[ce], se1 = tsc[ce + 1], so0 = tsc[co], so1 = tsc[co + 1];
+  const uint32_t lds0 = (uint32_t)(size_t)(lds_void*)lds;
+  const uint32_t mu = __builtin_amdgcn_readfirstlane(lds0 + op * OPB + par * 512 + blk * 256);
+  const uint32_t row_b = (uint32_t)ld * 4u;
+
+  typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+  struct Regs {
+    u32x2v v[8];
+  };
+  auto load_one = [&](int it, Regs& r, int i) {
+    const bool in = it < nit;
+    const uint32_t so = in ? (uint32_t)(it * BKT + par + 2 * i) * row_b : 0x80000000u;
+    r.v[i] = __builtin_amdgcn_raw_buffer_load_b64(buf.r, (i & 1) ? vo : ve, so, 0);
+  };
+  auto load = [&](int it, Regs& r) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) load_one(it, r, i);
+  };
+  // unit i of the register set -> its two piece dwords into stage buffer S (compile-time)
+  auto store_one = [&](const Regs& r, auto S, auto I) {
+    constexpr int s = decltype(S)::value, i = decltype(I)::value;
+    uint32_t h0, h1;
+    const float x0 = __uint_as_float(r.v[i].x), x1 = __uint_as_float(r.v[i].y);
+    if constexpr ((i & 1) != 0) split_pair_mix2(x0, x1, so0, so1, h0, h1);
+    else split_pair_mix2(x0, x1, se0, se1, h0, h1);
+    st_tid2<s * STG + i * 1024>(mu, h0, h1);
+  };
+
+  // transposed fragment offsets (bytes within an operand image): lane (gq, q, p) reads row
+  // 8 (gq >> 1) + q (+ 4: the hi read), column pairs (c0 & 127) / 2 + 8 (gq & 1) + 2 p
+  const int gq = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const int lrow = 8 * (gq >> 1) + q;
+  int offa[MB], offb[NB];
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+    offa[a] = lrow * 512 + wm * 256 + 4 * ((16 * a + 8 * (gq & 1) + 2 * p - 16 * q) & 63);
+#pragma unroll
+  for (int b = 0; b < NB; ++b)
+    offb[b] = lrow * 512 + (wn >> 1) * 256 + 4 * ((32 * (wn & 1) + 16 * b + 8 * (gq & 1) + 2 * p - 16 * q) & 63);
+  auto frag = [&](int off) {
+    const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(lds + off));
+    const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(lds + off + 2048));
+    const v4i16 v[2] = {a, b};
+    return *reinterpret_cast<const f16x8*>(v);
+  };
+
+  f32x16 acc[MB][NB];
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) acc[a][b] = f32x16{0};
+
+  struct Fr {
+    f16x8 a0[MB], b0[NB], b1[NB];   // a0[a] holds piece 1 of A rows a during pass 2
+  };
+  constexpr int NMF = 3 * MB * NB;
+  auto mma = [&](const Fr& F, int i) {
+    const int qq = i / (MB * NB), a = (i % (MB * NB)) / NB, b = i % NB;
+    acc[a][b] = mfma16(F.a0[a], qq == 1 ? F.b1[b] : F.b0[b], acc[a][b]);
+  };
+  // one 16-token step on stage buffer S: fragments, 24 MFMAs; under them the split + stores of the
+  // next stage (register set S ^ 1) into buffer S ^ 1, each unit's register refilled with the stage
+  // after next right after its split; one barrier
+  Regs R[2];
+  auto step = [&](int it, auto S) {
+    constexpr int s = decltype(S)::value;
+    const int base = s * STG;
+    Fr F;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      F.b0[b] = frag(base + OPB + offb[b]);
+      F.b1[b] = frag(base + PCE + OPB + offb[b]);
+    }
+#pragma unroll
+    for (int a = 0; a < MB; ++a) F.a0[a] = frag(base + offa[a]);
+    static_for<0, NMF>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      mma(F, i);
+      if constexpr (i / (MB * NB) == 1 && i % NB == NB - 1) {
+        constexpr int a = (i % (MB * NB)) / NB;
+        F.a0[a] = frag(base + PCE + offa[a]);
+      }
+      if constexpr (i % 3 == 2) {   // units 0 .. 7 after MFMAs 2, 5, .., 23
+        store_one(R[s ^ 1], std::integral_constant<int, s ^ 1>{}, std::integral_constant<int, i / 3>{});
+        load_one(it + 3, R[s ^ 1], i / 3);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    // the add-tid stores come from asm: the compiler does not count them, so retire them here,
+    // before the barrier that publishes the stage
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+
+  load(0, R[0]);
+  load(1, R[1]);
+  static_for<0, 8>([&](auto I) {
+    store_one(R[0], std::integral_constant<int, 0>{}, I);
+    load_one(2, R[0], decltype(I)::value);
+  });
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int it = 0; it < nit; it += 2) {
+    step(it, std::integral_constant<int, 0>{});
+    if (it + 1 < nit) step(it + 1, std::integral_constant<int, 1>{});
+  }
+
+  float* o = out + (nsplit > 1 ? (int64_t)sp * M * N : 0);
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      const int n = n0 + wn * WN + 32 * b + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm * WM + 32 * a + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        if (m < mvalid) o[(int64_t)m * N + n] = acc[a][b][r] * tia[m - m0] * tib[n - n0];
+      }
+    }
+}
+
+void wgrad_tid_launch(const float* A, int lda, const HxColScale& ca, const float* B, int ldb, const HxColScale& cb,
+                      float* out, float* ws, int M, int N, int T, int nsplit, int mvalid, hipStream_t s) {
+  const int kchunk = ((T + nsplit - 1) / nsplit + 15) / 16 * 16;
+  nsplit = (T + kchunk - 1) / kchunk;
+  const int total = (M / 256) * (N / 256) * nsplit;
+  const int per = (total + 7) / 8;
+  const size_t smem = (size_t)2 * 32768 + (4 * 256 + 8) * 4;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_f16_tid_k),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    attr = true;
+  }
+  wgrad_f16_tid_k<<<8 * per, 512, smem, s>>>(A, lda, ca, B, ldb, cb, nsplit > 1 ? ws : out, M, N, T, kchunk, nsplit,
+                                             nsplit > 1 ? M : mvalid);
+  if (nsplit > 1) {
+    const int64_t n4 = (int64_t)mvalid * N / 4, slab4 = (int64_t)M * N / 4;
+    const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+    slab_sum_k<<<blocks, 256, 0, s>>>(reinterpret_cast<const float4*>(ws), reinterpret_cast<float4*>(out), n4, slab4,
+                                      nsplit);
+  }
+}
+
 // ---------------------------------------------------------------- max |x| per row, weight pieces
 // max |x| of every row of a [rows][cols] fp32 matrix (row stride ld, cols % 4 == 0): one wave per
 // row (the per-row operand scale of the fp16x3 GEMMs, when no producer wrote it)
@@ -1404,6 +1623,11 @@ int hx_wgrad_f16(const float* dy, int ldy, const HxColScale& ca, const float* x,
   if (ldy % 4 || ldx % 4 || M % 128 || N % 128 || T < 1) return -1;
   if (cfg == 1) {
     if (M % 256 || N % 256) return -1;
+    const char* e = getenv("HX_WGRAD_TID");   // read per call: same-process A/B
+    if (e && atoi(e) == 1) {
+      wgrad_tid_launch(dy, ldy, ca, x, ldx, cb, out, ws, M, N, T, nsplit, mvalid, s);
+      return 0;
+    }
     wgrad_launch<256, 256, 128, 64>(dy, ldy, ca, x, ldx, cb, out, ws, M, N, T, nsplit, mvalid, s);
   } else {
     wgrad_launch<128, 128, 64, 64>(dy, ldy, ca, x, ldx, cb, out, ws, M, N, T, nsplit, mvalid, s);

@@ -551,3 +551,28 @@ def test_ffn_large_partials_fit(dev):
         assert ((dW1.double() - ref).abs() / den).max().item() < 4e-6
     finally:
         gemm16.set_enabled(was)
+
+
+@pytest.mark.parametrize('T,M,N,mvalid', [(16384, 2304, 768, 2304), (16384, 768, 3072, 768), (4096, 768, 768, 768),
+                                          (2560, 30720, 768, 30522), (1000, 3072, 768, 3072), (333, 768, 768, 768)])
+def test_wgrad_f16_addtid_staging_bitwise(dev, monkeypatch, T, M, N, mvalid):
+    """The 256 x 256 weight gradient with add-tid piece staging (HX_WGRAD_TID=1: b64 column-pair
+    loads, ds_write_addtid_b32 stores into a row-rotated image) against the ds_write_b128 kernel:
+    the same pieces in the same MFMA order, so bit for bit -- token counts off the 16-token stage,
+    split-K slabs and the MLM decoder's padded rows included."""
+    g = torch.Generator(device=dev).manual_seed(T + M + N)
+    dy = torch.randn(T, M, device=dev, generator=g) * 1e-3
+    x = torch.randn(T, N, device=dev, generator=g)
+    dc, xc = C().amax_cols(dy), C().amax_cols(x)
+    ref = torch.full((mvalid, N), float('nan'), device=dev)
+    monkeypatch.setenv('HX_WGRAD_TID', '0')
+    C().wgrad_f16(dy, dc, x, xc, ref)
+    out = torch.full((mvalid, N), float('nan'), device=dev)
+    monkeypatch.setenv('HX_WGRAD_TID', '1')
+    C().wgrad_f16(dy, dc, x, xc, out)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out).all()
+    assert torch.equal(out, ref), (out - ref).abs().max().item()
+    r64 = dy.double().t()[:mvalid] @ x.double()
+    den = dy.abs().double().t()[:mvalid] @ x.abs().double()
+    assert ((out.double() - r64).abs() / den).max().item() < 4e-6

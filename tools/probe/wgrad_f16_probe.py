@@ -70,5 +70,30 @@ def gemm_main():
         print('gemm N{} K{} T{}: '.format(N, K, T) + ', '.join(row), flush=True)
 
 
+def tid_main():
+    """The add-tid staged weight gradient (HX_WGRAD_TID=1) against the ds_write_b128 one, same
+    process, warmed up, alternated three times per shape."""
+    from hetseq_9cme_amd.ops._ext import C
+    T = int(os.environ.get('T', '16384'))
+    g = torch.Generator(device='cuda').manual_seed(0)
+    for (M, N) in [(2304, 768), (3072, 768), (768, 3072), (768, 768)]:
+        dy = torch.randn(T, M, device='cuda', generator=g)
+        x = torch.randn(T, N, device='cuda', generator=g)
+        dc, xc = C().amax_cols(dy), C().amax_cols(x)
+        out = torch.empty(M, N, device='cuda')
+        os.environ['HX_WGRAD_TID'] = '0'
+        timed(lambda: C().wgrad_f16(dy, dc, x, xc, out), n=100)
+        res = {'0': [], '1': []}
+        for _ in range(3):
+            for v in ('0', '1'):
+                os.environ['HX_WGRAD_TID'] = v
+                res[v].append(timed(lambda: C().wgrad_f16(dy, dc, x, xc, out)))
+        os.environ.pop('HX_WGRAD_TID')
+        print('wgrad {}x{} T{}: b128 stores {} us | add-tid {} us'.format(
+            M, N, T, ' '.join('%.1f' % v for v in res['0']), ' '.join('%.1f' % v for v in res['1'])), flush=True)
+
+
 if __name__ == '__main__' and len(sys.argv) > 1 and sys.argv[1] == 'gemm':
     gemm_main()
+if __name__ == '__main__' and len(sys.argv) > 1 and sys.argv[1] == 'tid':
+    tid_main()

@@ -1210,7 +1210,8 @@ __global__ __launch_bounds__(512) void wgrad_f16_tid_k(const float* __restrict__
 
 void wgrad_tid_launch(const float* A, int lda, const HxColScale& ca, const float* B, int ldb, const HxColScale& cb,
                       float* out, float* ws, int M, int N, int T, int nsplit, int mvalid, hipStream_t s) {
-  const int kchunk = ((T + nsplit - 1) / nsplit + 15) / 16 * 16;
+  // the token splits of wgrad_launch<.., 32> (32-token granularity): the same slabs, the same sums
+  const int kchunk = ((T + nsplit - 1) / nsplit + 31) / 32 * 32;
   nsplit = (T + kchunk - 1) / kchunk;
   const int total = (M / 256) * (N / 256) * nsplit;
   const int per = (total + 7) / 8;

@@ -1624,8 +1624,11 @@ int hx_wgrad_f16(const float* dy, int ldy, const HxColScale& ca, const float* x,
   if (ldy % 4 || ldx % 4 || M % 128 || N % 128 || T < 1) return -1;
   if (cfg == 1) {
     if (M % 256 || N % 256) return -1;
-    const char* e = getenv("HX_WGRAD_TID");   // read per call: same-process A/B
-    if (e && atoi(e) == 1) {
+    // the add-tid staged kernel (bitwise the same result) unless HX_WGRAD_TID=0: 2-3 % faster
+    // standalone (profiles/r6l_wgrad_addtid_ab.log), 0.5 ms/step in the step (36.66 / 36.72 ->
+    // 36.18 / 36.15 ms, profiles/r6m_wgrad_addtid_step_ab.txt); read per call (same-process A/B)
+    const char* e = getenv("HX_WGRAD_TID");
+    if (!(e && atoi(e) == 0)) {
       wgrad_tid_launch(dy, ldy, ca, x, ldx, cb, out, ws, M, N, T, nsplit, mvalid, s);
       return 0;
     }

@@ -556,8 +556,9 @@ def test_ffn_large_partials_fit(dev):
 @pytest.mark.parametrize('T,M,N,mvalid', [(16384, 2304, 768, 2304), (16384, 768, 3072, 768), (4096, 768, 768, 768),
                                           (2560, 30720, 768, 30522), (1000, 3072, 768, 3072), (333, 768, 768, 768)])
 def test_wgrad_f16_addtid_staging_bitwise(dev, monkeypatch, T, M, N, mvalid):
-    """The 256 x 256 weight gradient with add-tid piece staging (HX_WGRAD_TID=1: b64 column-pair
-    loads, ds_write_addtid_b32 stores into a row-rotated image) against the ds_write_b128 kernel:
+    """The 256 x 256 weight gradient with add-tid piece staging (the default; HX_WGRAD_TID=0 selects
+    the ds_write_b128 kernel): b64 column-pair loads, ds_write_addtid_b32 stores into a row-rotated
+    image, against the ds_write_b128 kernel:
     the same pieces in the same MFMA order, so bit for bit -- token counts off the 16-token stage,
     split-K slabs and the MLM decoder's padded rows included."""
     g = torch.Generator(device=dev).manual_seed(T + M + N)

@@ -1034,22 +1034,30 @@ __device__ __forceinline__ void static_for(F&& f) {
     static_for<B + 1, E>(f);
   }
 }
-template <int C0>
-__device__ __forceinline__ void st_tid2(uint32_t m0, uint32_t h0, uint32_t h1) {
+// one ds_write_addtid_b32 of dword h to LDS byte address U + C (U wave-uniform, at most UMAX; C a
+// compile-time constant): M0[15:0] + a 16-bit immediate, split so that both fit
+template <int C, int UMAX>
+__device__ __forceinline__ void st_tid(uint32_t u, uint32_t h) {
+  constexpr int IMM = C > 65535 ? C - 65535 : 0;   // into M0; the immediate is C - IMM
+  static_assert(C - IMM <= 65535 && IMM + UMAX <= 65535, "add-tid address range");
   uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
-               "ds_write_addtid_b32 %1 offset:%4\n\tds_write_addtid_b32 %2 offset:%5\n\ts_mov_b32 m0, %0"
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tds_write_addtid_b32 %1 offset:%3\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
-               : "v"(h0), "v"(h1), "s"(m0), "i"(C0), "i"(C0 + 16384)
+               : "v"(h), "s"(u + (uint32_t)IMM), "i"(C - IMM)
                : "memory");
 }
 
+template <int BKT>
 __global__ __launch_bounds__(512) void wgrad_f16_tid_k(const float* __restrict__ A, int lda, const HxColScale ca,
                                                         const float* __restrict__ B, int ldb, const HxColScale cb,
                                                         float* __restrict__ out, int M, int N, int T, int kchunk,
                                                         int nsplit, int mvalid) {
-  constexpr int BM = 256, BN = 256, WM = 128, WN = 64, NWM = 2, MB = 4, NB = 2, BKT = 16;
-  constexpr int STG = 32768, PCE = 16384, OPB = 8192;
+  static_assert(BKT == 16 || BKT == 32, "16- or 32-token stages");
+  constexpr int BM = 256, BN = 256, WM = 128, WN = 64, NWM = 2, MB = 4, NB = 2;
+  constexpr int NU = BKT / 2, NSUB = BKT / 16;      // staging units per wave, 16-token substeps
+  constexpr int NSET = BKT == 16 ? 2 : 1;           // register sets: loads run NSET stages ahead
+  constexpr int OPB = BKT * 512, PCE = 2 * OPB, STG = 2 * PCE;   // image strides (bytes)
+  constexpr int UMAX = OPB + 512 + 256;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   float* tsa = reinterpret_cast<float*>(lds + 2 * STG);
   float* tia = tsa + BM;
@@ -1078,7 +1086,7 @@ __global__ __launch_bounds__(512) void wgrad_f16_tid_k(const float* __restrict__
   col_scales(cb, n0, BN, tsb, tib, red);
   __syncthreads();
 
-  // ---- this wave's staging units: operand op, column block blk, token rows par + 2 i (i < 8)
+  // ---- this wave's staging units: operand op, column block blk, token rows par + 2 i (i < NU)
   const int op = wv & 1, blk = (wv >> 1) & 1, par = wv >> 2;
   const float* src = op ? B : A;
   const int ld = op ? ldb : lda;
@@ -1094,7 +1102,7 @@ __global__ __launch_bounds__(512) void wgrad_f16_tid_k(const float* __restrict__
 
   typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
   struct Regs {
-    u32x2v v[8];
+    u32x2v v[NU];
   };
   auto load_one = [&](int it, Regs& r, int i) {
     const bool in = it < nit;
@@ -1103,16 +1111,17 @@ __global__ __launch_bounds__(512) void wgrad_f16_tid_k(const float* __restrict__
   };
   auto load = [&](int it, Regs& r) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) load_one(it, r, i);
+    for (int i = 0; i < NU; ++i) load_one(it, r, i);
   };
-  // unit i of the register set -> its two piece dwords into stage buffer S (compile-time)
+  // unit i of a register set -> its two piece dwords into stage buffer S (compile-time)
   auto store_one = [&](const Regs& r, auto S, auto I) {
     constexpr int s = decltype(S)::value, i = decltype(I)::value;
     uint32_t h0, h1;
     const float x0 = __uint_as_float(r.v[i].x), x1 = __uint_as_float(r.v[i].y);
     if constexpr ((i & 1) != 0) split_pair_mix2(x0, x1, so0, so1, h0, h1);
     else split_pair_mix2(x0, x1, se0, se1, h0, h1);
-    st_tid2<s * STG + i * 1024>(mu, h0, h1);
+    st_tid<s * STG + i * 1024, UMAX>(mu, h0);
+    st_tid<s * STG + PCE + i * 1024, UMAX>(mu, h1);
   };
 
   // transposed fragment offsets (bytes within an operand image): lane (gq, q, p) reads row
@@ -1147,33 +1156,38 @@ __global__ __launch_bounds__(512) void wgrad_f16_tid_k(const float* __restrict__
     const int qq = i / (MB * NB), a = (i % (MB * NB)) / NB, b = i % NB;
     acc[a][b] = mfma16(F.a0[a], qq == 1 ? F.b1[b] : F.b0[b], acc[a][b]);
   };
-  // one 16-token step on stage buffer S: fragments, 24 MFMAs; under them the split + stores of the
-  // next stage (register set S ^ 1) into buffer S ^ 1, each unit's register refilled with the stage
-  // after next right after its split; one barrier
-  Regs R[2];
+  // one BKT-token step on stage buffer S: per 16-token substep, fragments and 24 MFMAs; under them
+  // the split + stores of the next stage (register set (S ^ 1) % NSET) into buffer S ^ 1, eight units
+  // per substep, each unit's register refilled NSET stages ahead right after its split; one barrier
+  Regs R[NSET];
   auto step = [&](int it, auto S) {
-    constexpr int s = decltype(S)::value;
+    constexpr int s = decltype(S)::value, rs = (s ^ 1) % NSET;
     const int base = s * STG;
-    Fr F;
+    static_for<0, NSUB>([&](auto SS) {
+      constexpr int ss = decltype(SS)::value;
+      const int sb = base + ss * 8192;
+      Fr F;
 #pragma unroll
-    for (int b = 0; b < NB; ++b) {
-      F.b0[b] = frag(base + OPB + offb[b]);
-      F.b1[b] = frag(base + PCE + OPB + offb[b]);
-    }
+      for (int b = 0; b < NB; ++b) {
+        F.b0[b] = frag(sb + OPB + offb[b]);
+        F.b1[b] = frag(sb + PCE + OPB + offb[b]);
+      }
 #pragma unroll
-    for (int a = 0; a < MB; ++a) F.a0[a] = frag(base + offa[a]);
-    static_for<0, NMF>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      mma(F, i);
-      if constexpr (i / (MB * NB) == 1 && i % NB == NB - 1) {
-        constexpr int a = (i % (MB * NB)) / NB;
-        F.a0[a] = frag(base + PCE + offa[a]);
-      }
-      if constexpr (i % 3 == 2) {   // units 0 .. 7 after MFMAs 2, 5, .., 23
-        store_one(R[s ^ 1], std::integral_constant<int, s ^ 1>{}, std::integral_constant<int, i / 3>{});
-        load_one(it + 3, R[s ^ 1], i / 3);
-      }
-      __builtin_amdgcn_sched_barrier(0);
+      for (int a = 0; a < MB; ++a) F.a0[a] = frag(sb + offa[a]);
+      static_for<0, NMF>([&](auto I) {
+        constexpr int i = decltype(I)::value;
+        mma(F, i);
+        if constexpr (i / (MB * NB) == 1 && i % NB == NB - 1) {
+          constexpr int a = (i % (MB * NB)) / NB;
+          F.a0[a] = frag(sb + PCE + offa[a]);
+        }
+        if constexpr (i % 3 == 2) {   // units 8 ss + 0 .. 7 after MFMAs 2, 5, .., 23
+          constexpr int u = 8 * ss + i / 3;
+          store_one(R[rs], std::integral_constant<int, s ^ 1>{}, std::integral_constant<int, u>{});
+          load_one(it + 1 + NSET, R[rs], u);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      });
     });
     // the add-tid stores come from asm: the compiler does not count them, so retire them here,
     // before the barrier that publishes the stage
@@ -1182,10 +1196,10 @@ __global__ __launch_bounds__(512) void wgrad_f16_tid_k(const float* __restrict__
   };
 
   load(0, R[0]);
-  load(1, R[1]);
-  static_for<0, 8>([&](auto I) {
+  if constexpr (NSET == 2) load(1, R[1]);
+  static_for<0, NU>([&](auto I) {
     store_one(R[0], std::integral_constant<int, 0>{}, I);
-    load_one(2, R[0], decltype(I)::value);
+    load_one(NSET, R[0], decltype(I)::value);
   });
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1208,6 +1222,7 @@ __global__ __launch_bounds__(512) void wgrad_f16_tid_k(const float* __restrict__
     }
 }
 
+template <int BKT>
 void wgrad_tid_launch(const float* A, int lda, const HxColScale& ca, const float* B, int ldb, const HxColScale& cb,
                       float* out, float* ws, int M, int N, int T, int nsplit, int mvalid, hipStream_t s) {
   // the token splits of wgrad_launch<.., 32> (32-token granularity): the same slabs, the same sums
@@ -1215,15 +1230,15 @@ void wgrad_tid_launch(const float* A, int lda, const HxColScale& ca, const float
   nsplit = (T + kchunk - 1) / kchunk;
   const int total = (M / 256) * (N / 256) * nsplit;
   const int per = (total + 7) / 8;
-  const size_t smem = (size_t)2 * 32768 + (4 * 256 + 8) * 4;
+  const size_t smem = (size_t)2 * 4 * BKT * 512 + (4 * 256 + 8) * 4;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_f16_tid_k),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad_f16_tid_k<BKT>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
-  wgrad_f16_tid_k<<<8 * per, 512, smem, s>>>(A, lda, ca, B, ldb, cb, nsplit > 1 ? ws : out, M, N, T, kchunk, nsplit,
-                                             nsplit > 1 ? M : mvalid);
+  wgrad_f16_tid_k<BKT><<<8 * per, 512, smem, s>>>(A, lda, ca, B, ldb, cb, nsplit > 1 ? ws : out, M, N, T, kchunk,
+                                                  nsplit, nsplit > 1 ? M : mvalid);
   if (nsplit > 1) {
     const int64_t n4 = (int64_t)mvalid * N / 4, slab4 = (int64_t)M * N / 4;
     const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
@@ -1627,9 +1642,14 @@ int hx_wgrad_f16(const float* dy, int ldy, const HxColScale& ca, const float* x,
     // the add-tid staged kernel (bitwise the same result) unless HX_WGRAD_TID=0: 2-3 % faster
     // standalone (profiles/r6l_wgrad_addtid_ab.log), 0.5 ms/step in the step (36.66 / 36.72 ->
     // 36.18 / 36.15 ms, profiles/r6m_wgrad_addtid_step_ab.txt); read per call (same-process A/B)
-    const char* e = getenv("HX_WGRAD_TID");
-    if (!(e && atoi(e) == 0)) {
-      wgrad_tid_launch(dy, ldy, ca, x, ldx, cb, out, ws, M, N, T, nsplit, mvalid, s);
+    const char* e = getenv("HX_WGRAD_TID");   // 0: ds_write_b128 kernel; 1 (default): 16-token stages; 2: 32
+    const int tv = e ? atoi(e) : 1;
+    if (tv == 1) {
+      wgrad_tid_launch<16>(dy, ldy, ca, x, ldx, cb, out, ws, M, N, T, nsplit, mvalid, s);
+      return 0;
+    }
+    if (tv == 2) {
+      wgrad_tid_launch<32>(dy, ldy, ca, x, ldx, cb, out, ws, M, N, T, nsplit, mvalid, s);
       return 0;
     }
     wgrad_launch<256, 256, 128, 64>(dy, ldy, ca, x, ldx, cb, out, ws, M, N, T, nsplit, mvalid, s);

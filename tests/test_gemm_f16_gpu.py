@@ -568,12 +568,13 @@ def test_wgrad_f16_addtid_staging_bitwise(dev, monkeypatch, T, M, N, mvalid):
     ref = torch.full((mvalid, N), float('nan'), device=dev)
     monkeypatch.setenv('HX_WGRAD_TID', '0')
     C().wgrad_f16(dy, dc, x, xc, ref)
-    out = torch.full((mvalid, N), float('nan'), device=dev)
-    monkeypatch.setenv('HX_WGRAD_TID', '1')
-    C().wgrad_f16(dy, dc, x, xc, out)
-    torch.cuda.synchronize()
-    assert torch.isfinite(out).all()
-    assert torch.equal(out, ref), (out - ref).abs().max().item()
+    for variant in ('1', '2'):   # 16- and 32-token stages
+        out = torch.full((mvalid, N), float('nan'), device=dev)
+        monkeypatch.setenv('HX_WGRAD_TID', variant)
+        C().wgrad_f16(dy, dc, x, xc, out)
+        torch.cuda.synchronize()
+        assert torch.isfinite(out).all()
+        assert torch.equal(out, ref), (variant, (out - ref).abs().max().item())
     r64 = dy.double().t()[:mvalid] @ x.double()
     den = dy.abs().double().t()[:mvalid] @ x.abs().double()
     assert ((out.double() - r64).abs() / den).max().item() < 4e-6

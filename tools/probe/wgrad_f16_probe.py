@@ -83,14 +83,15 @@ def tid_main():
         out = torch.empty(M, N, device='cuda')
         os.environ['HX_WGRAD_TID'] = '0'
         timed(lambda: C().wgrad_f16(dy, dc, x, xc, out), n=100)
-        res = {'0': [], '1': []}
+        res = {'0': [], '1': [], '2': []}
         for _ in range(3):
-            for v in ('0', '1'):
+            for v in ('0', '1', '2'):
                 os.environ['HX_WGRAD_TID'] = v
                 res[v].append(timed(lambda: C().wgrad_f16(dy, dc, x, xc, out)))
         os.environ.pop('HX_WGRAD_TID')
-        print('wgrad {}x{} T{}: b128 stores {} us | add-tid {} us'.format(
-            M, N, T, ' '.join('%.1f' % v for v in res['0']), ' '.join('%.1f' % v for v in res['1'])), flush=True)
+        print('wgrad {}x{} T{}: b128 stores {} us | add-tid 16-token stages {} us | add-tid 32 {} us'.format(
+            M, N, T, ' '.join('%.1f' % v for v in res['0']), ' '.join('%.1f' % v for v in res['1']),
+            ' '.join('%.1f' % v for v in res['2'])), flush=True)
 
 
 if __name__ == '__main__' and len(sys.argv) > 1 and sys.argv[1] == 'gemm':

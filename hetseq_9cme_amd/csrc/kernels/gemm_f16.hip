@@ -711,11 +711,7 @@ void launch_cfg(int cfg, const F16Args& a, hipStream_t s) {
   if (cfg == 0) launch_one<256, 192, 32, 192, EPI, 1, 4, AT, OB>(a, s);
   else if (cfg == 1) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB>(a, s);
   else if (cfg == 6) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 0>(a, s);
-  else if (cfg == 2) {
-    const char* e = getenv("HX_GEMM_NS5");   // (probe) a five-stage ring on the 128 x 96 tile
-    if (e && atoi(e) == 1) launch_one<128, 96, 32, 96, EPI, 2, 5, AT, OB>(a, s);
-    else launch_one<128, 96, 32, 96, EPI, 2, 4, AT, OB>(a, s);
-  }
+  else if (cfg == 2) launch_one<128, 96, 32, 96, EPI, 2, 4, AT, OB>(a, s);
   else if (cfg == 4) launch_one<128, 192, 64, 96, EPI, 2, 3, AT, OB>(a, s);
   else if (cfg == 5) launch_one<256, 256, 64, 128, EPI, 1, 4, AT, OB>(a, s);
   else launch_one<64, 64, 32, 32, EPI, 2, 4, AT, OB>(a, s);

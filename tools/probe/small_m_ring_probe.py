@@ -1,6 +1,7 @@
 """The 128 x 96 GEMM tile (cfg 2, two workgroups per CU) with a four- vs five-stage DMA ring at
-fine-tuning-sized M (HX_GEMM_NS5, read per call), forward and beta data gradient of the BERT-base
-products, warmed up and alternated.  ``T=2048 python tools/probe/small_m_ring_probe.py``"""
+fine-tuning-sized M (HX_GEMM_NS5, read per call), forward of the BERT-base products, warmed up and
+alternated.  ``T=2048 python tools/probe/small_m_ring_probe.py``.  The switch lived in a measurement
+build (removed: the five-stage ring was 3-20 % slower, profiles/r6o_small_m_ring_probe.log)."""
 import os
 import sys
 

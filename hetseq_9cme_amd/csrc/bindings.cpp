@@ -216,7 +216,7 @@ std::vector<Tensor> ln_bwd(Tensor dout, Tensor z, Tensor mean, Tensor rstd, Tens
 
 std::vector<Tensor> embed_ln_fwd(Tensor ids, OptT tt, Tensor wte, Tensor wpe, Tensor wtt, Tensor gamma, Tensor beta,
                                  double eps, double keep_prob, const Tensor& seed, int64_t stream, bool bf16_out,
-                                 OptT amax_out) {
+                                 OptT amax_out, OptT pieces_out) {
   dbg_range(ids, 0, wte.size(0), "token ids");
   if (has(tt)) dbg_range(*tt, 0, wtt.size(0), "token type ids");
   check_cuda(ids, "input_ids");
@@ -238,7 +238,8 @@ std::vector<Tensor> embed_ln_fwd(Tensor ids, OptT tt, Tensor wte, Tensor wpe, Te
                   wte.data_ptr<float>(), wpe.data_ptr<float>(), wtt.data_ptr<float>(), gamma.data_ptr<float>(),
                   beta.data_ptr<float>(), out.data_ptr(), z.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
                   B * S, (int)S, H, (float)eps, (float)keep_prob, seed_ptr(seed), (uint64_t)stream, cur_stream(ids),
-                  bf16_out ? nullptr : amax_ptr(amax_out, B * S, "embed_ln_fwd amax"));
+                  bf16_out ? nullptr : amax_ptr(amax_out, B * S, "embed_ln_fwd amax"),
+                  bf16_out ? nullptr : pieces_ptr(pieces_out, B * S, H, amax_out, "embed_ln_fwd pieces"));
   dbg_finite(out, "embed_ln_fwd");
   return {out, z, mean, rstd};
 }
@@ -1055,7 +1056,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ln_bwd_blocks", &hx_ln_bwd_blocks);
   m.def("embed_ln_fwd", &embed_ln_fwd, py::arg("ids"), py::arg("tt"), py::arg("wte"), py::arg("wpe"), py::arg("wtt"),
         py::arg("gamma"), py::arg("beta"), py::arg("eps"), py::arg("keep_prob"), py::arg("seed"), py::arg("stream"),
-        py::arg("bf16_out"), py::arg("amax_out") = py::none());
+        py::arg("bf16_out"), py::arg("amax_out") = py::none(), py::arg("pieces_out") = py::none());
   m.def("embed_word_grad", &embed_word_grad);
   m.def("embed_type_grad", &embed_type_grad);
   m.def("bias_act_fwd", &bias_act_fwd);

@@ -40,7 +40,7 @@ void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, con
 void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,
                      const float* wtt, const float* gamma, const float* beta, void* out, void* zsave, float* mean,
                      float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, const uint64_t* seed,
-                     uint64_t stream, hipStream_t s, float* amax_part = nullptr);
+                     uint64_t stream, hipStream_t s, float* amax_part = nullptr, uint16_t* pieces = nullptr);
 // token-type embedding gradient for ntypes <= 3: dwtt[t] = sum of dz rows with tt == t (part: a
 // [hx_type_grad_blocks(rows)][ntypes][H] fp32 workspace; deterministic block partials + fold)
 int hx_type_grad_blocks(int64_t rows);

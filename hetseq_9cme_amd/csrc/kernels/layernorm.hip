@@ -289,7 +289,7 @@ __global__ __launch_bounds__(NT) void embed_ln_fwd_k(const int64_t* __restrict__
                                                    T* __restrict__ zsave, float* __restrict__ mean_out,
                                                    float* __restrict__ rstd_out, int64_t rows, int S, int H,
                                                    float eps, float keep_prob, const uint64_t* __restrict__ seedp, uint64_t stream,
-                                                   float* __restrict__ amax_part) {
+                                                   float* __restrict__ amax_part, uint16_t* __restrict__ pieces) {
   const uint64_t seed = *seedp;   // per-update Philox key, device-resident (graph-safe)
   const int lane = threadIdx.x & 63;
   const int64_t wave = blockIdx.x * (int64_t)WPB + (threadIdx.x >> 6);
@@ -350,9 +350,12 @@ __global__ __launch_bounds__(NT) void embed_ln_fwd_k(const int64_t* __restrict__
         }
         hx::store4(out + r * H + j, o);
         am = amax4(am, o);
+        x.v[c] = o;
       }
     }
-    if (amax_part) row_amax_out(am, amax_part, r);
+    // (fp32 runs) the first layer's QKV GEMM operand, pre-split at the row scale (ln_fwd_k's pieces)
+    if (pieces) row_pieces_out(x, row_amax_out(am, amax_part, r), pieces, r, H);
+    else if (amax_part) row_amax_out(am, amax_part, r);
   }
 }
 
@@ -559,17 +562,17 @@ void hx_ln_bwd(int bf16, const void* dout, const void* z, const float* mean, con
 void hx_embed_ln_fwd(int bf16, const int64_t* ids, const int64_t* tt, const float* wte, const float* wpe,
                      const float* wtt, const float* gamma, const float* beta, void* out, void* zsave, float* mean,
                      float* rstd, int64_t rows, int S, int H, float eps, float keep_prob, const uint64_t* seed,
-                     uint64_t stream, hipStream_t s, float* amax_part) {
+                     uint64_t stream, hipStream_t s, float* amax_part, uint16_t* pieces) {
   const int grid = ln_grid(rows, 4096);
   HX_CH_DISPATCH(H, {
     if (bf16)
       embed_ln_fwd_k<uint16_t, CH><<<grid, NT, 0, s>>>(ids, tt, wte, wpe, wtt, gamma, beta, (uint16_t*)out,
                                                        (uint16_t*)zsave, mean, rstd, rows, S, H, eps, keep_prob,
-                                                       seed, stream, nullptr);
+                                                       seed, stream, nullptr, nullptr);
     else
       embed_ln_fwd_k<float, CH><<<grid, NT, 0, s>>>(ids, tt, wte, wpe, wtt, gamma, beta, (float*)out,
                                                     (float*)zsave, mean, rstd, rows, S, H, eps, keep_prob, seed,
-                                                    stream, amax_part);
+                                                    stream, amax_part, pieces);
   })
 }
 

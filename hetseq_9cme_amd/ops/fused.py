@@ -206,9 +206,11 @@ class _EmbedLNFn(torch.autograd.Function):
         keep = 1.0 - p
         seed, stream = get_rng().next(ids.device) if p > 0 else (get_rng().seed_tensor(ids.device), 0)
         am = _amax_buf(ids.numel(), wte, out_bf16)
+        pc = _pieces_buf(ids.numel(), wte.shape[1], wte) if am is not None else None
         out, z, mean, rstd = C().embed_ln_fwd(ids, tt, wte, wpe, wtt, gamma, beta, eps, keep, seed, stream,
-                                              out_bf16, am)
+                                              out_bf16, am, pc)
         gemm16.attach(out, am)   # fp16x3: its max |x| partials for the first layer's QKV GEMM
+        gemm16.attach_pieces(out, pc)   # and its pieces at those row scales
         if am is not None:       # and the column bound of LN (+ dropout) for its weight gradient
             gemm16.attach_cols(out, gemm16.ln_affine(gamma, beta, keep))
         ctx.save_for_backward(ids, tt if tt is not None else torch.Tensor(), z, mean, rstd, gamma)

@@ -504,6 +504,29 @@ def test_layernorm_pieces_out(dev):
         assert torch.equal(bp, C().split_rows_f16(src, bm))
 
 
+def test_embed_layernorm_pieces_out(dev):
+    """The embedding LayerNorm (gather + sum + LN + dropout) writes its output's P2 pieces at the
+    row scales it computes, like ln_fwd: the first layer's QKV GEMM reads them pre-split (AT 2)."""
+    g = torch.Generator(device=dev).manual_seed(43)
+    B, S, H, V = 8, 128, 768, 1000
+    ids = torch.randint(0, V, (B, S), device=dev, generator=g)
+    tt = torch.randint(0, 2, (B, S), device=dev, generator=g)
+    wte = torch.randn(V, H, device=dev, generator=g) * 0.05
+    wpe = torch.randn(512, H, device=dev, generator=g) * 0.05
+    wtt = torch.randn(2, H, device=dev, generator=g) * 0.05
+    gamma = torch.randn(H, device=dev, generator=g)
+    beta = torch.randn(H, device=dev, generator=g)
+    seed = torch.full((1,), 99, dtype=torch.int64, device=dev)
+    am = torch.empty(B * S, 1, device=dev)
+    pc = torch.empty(B * S, 2 * H, dtype=torch.float16, device=dev)
+    out, z, mean, rstd = C().embed_ln_fwd(ids, tt, wte, wpe, wtt, gamma, beta, 1e-12, 0.9, seed, 5, False, am, pc)
+    o2 = out.view(B * S, H)
+    assert torch.equal(am, o2.abs().amax(1, keepdim=True))
+    assert torch.equal(pc, C().split_rows_f16(o2, am))
+    out_ref = C().embed_ln_fwd(ids, tt, wte, wpe, wtt, gamma, beta, 1e-12, 0.9, seed, 5, False, am)[0]
+    assert torch.equal(out, out_ref)   # the pieces output changes nothing else
+
+
 def test_split_weight_virtual_padding(dev):
     """split_weight_f16 with a padded row count reads the rows past W's own as zero: bit-identical
     to splitting a zero-padded copy (the MLM decoder's vocabulary, 30522 -> 30720 rows)."""

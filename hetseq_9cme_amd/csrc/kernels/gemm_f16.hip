@@ -677,408 +677,6 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
   }
 }
 
-// ---------------------------------------------------------------- the GEMM on 16x16x32 MFMAs
-// gemm_f16q_k: the product, operands, DMA ring and epilogues of gemm_f16_k (fp16x3 operands, AT 0
-// or 2), with the three passes on v_mfma_f32_16x16x32_f16.  One MFMA's 32-deep K spans TWO 16-deep
-// ring stages: lane group g = lane >> 4 holds k 8 (g & 1) .. + 7 of stage 2s + (g >> 1), so the
-// fragment [piece p of stage 2s | piece p of stage 2s + 1] of 16 rows is ONE ds_read_b128 per lane
-// (a lane-constant stage offset into the same P2 / fp32 images), and a0 b0, a0 b1, a1 b0 cover both
-// stages: the MFMA cycles and LDS bytes per FLOP of the 32x32x16 loop, half the barriers, and the
-// smaller MFMA, which holds a higher clock under load (MI355X_MICROARCH.md, DVFS item 7: 1.12-1.14x
-// the FLOP/s of an LDS-fed 32x32x16 loop).
-// Super-step s (stages 2s, 2s + 1; the stage count per slab is even, host-checked):
-//   * MB x NB triples (a0 b0, a0 b1, a1 b0) of one 16 x 16 block, column block by column block; a
-//     column block's two B pieces are re-read for super-step s + 1 (stages 2s + 2, 2s + 3, published
-//     by the previous barrier) right after its last triple -- B fragments rotate, A fragments are
-//     double-buffered (AT 0: read as fp32, split by v_fma_mix pairs between the triples),
-//   * the DMA of stages 2s + 4, 2s + 5 into the slots of stages 2s, 2s + 1 (read in s - 1),
-//   * vmcnt(0) lgkmcnt(0) -- the DMA of s + 1 overwrites the slots read here -- and ONE barrier.
-// PR: timing-only probe switches (results WRONG; tools/probe/gemm_f16_bench.py QPROBE): 1 no k-loop
-// DMA, 2 no k-loop fragment reads, 4 no k-loop waits / barrier, 8 no MFMAs; 16: (not a probe) the
-// DMA issued at the head of the super-step instead of after its first triple; 32 (probe) the wait
-// leaves the super-step's own DMA in flight (what a two-super-step DMA lead would give)
-template <int BM, int BN, int WM, int WN, int EPI, int WGS, int AT, int PR = 0>
-__global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) * WGS / 4) void gemm_f16q_k(F16Args g) {
-  static_assert(AT == 0 || AT == 2, "fp16x3 operands");
-  constexpr int NS = 4, KD = 16;
-  constexpr int NWM = BM / WM, NWN = BN / WN, NW = NWM * NWN, NT = NW * 64;
-  constexpr int MB = WM / 16, NB = WN / 16;
-  constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64, STAGE = A_BYTES + B_BYTES;
-  constexpr int KA = BM / 16, KB = BN / 16, PTOT = KA + KB;
-  constexpr int JHI = (PTOT + NW - 1) / NW, JLO = PTOT / NW;
-  static_assert(JLO >= 1, "fewer DMA pieces than waves");
-  static_assert(BM % 16 == 0 && BN % 16 == 0 && WM % 16 == 0 && WN % 16 == 0, "tile shape");
-  static_assert(NT >= BM && NT >= BN, "one thread per table row");
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  float* tsa = reinterpret_cast<float*>(lds + NS * STAGE);
-  float* tia = tsa + BM;
-  float* tib = tia + BM;
-  float* red = tib + BN;
-
-  const int TM = (g.M + BM - 1) / BM, TN = g.N / BN, total = TM * TN;
-  const int per = (total * g.ks + 7) / 8;
-  const int work0 = (blockIdx.x % 8) * per + blockIdx.x / 8;   // tiles dealt XCD by XCD
-  if (work0 >= total * g.ks) return;
-  const int z = work0 / total, work = work0 - z * total;
-  const int nt = work % TN, mt = work / TN;
-  const int m0 = mt * BM, n0 = nt * BN;
-  const int nit = g.K / KD / g.ks, it0 = z * nit;
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w % NWM, wn = w / NWM, r16 = lane & 15, g4 = lane >> 4;
-  const int wv = __builtin_amdgcn_readfirstlane(w);
-
-  const int mrows = min(BM, g.M - m0);
-  const u32x4 ra = rsrc_of((const char*)g.A + (int64_t)m0 * g.lda * 4, (uint32_t)((int64_t)mrows * g.lda * 4));
-  const u32x4 rb = rsrc_of(g.B + (int64_t)n0 * g.ldb, (uint32_t)((int64_t)BN * g.ldb * 2));
-  constexpr int JUNK = NS * STAGE + (2 * BM + BN + NW) * 4;
-  uint32_t voff[JHI], dbase[JHI], dslot[JHI];
-  {
-    // the q image: chunk ch of row r at r 64 + 16 (ch ^ 3 ((r >> 3) & 1)) -- the ds_read_b128 lane
-    // groups of a 16x16x32 fragment ({0-3, 12-15, 20-27}, ...: row quads 0 and 3 at one chunk, 1 and
-    // 2 at its neighbour) then hit four distinct 16-B slots per row quad (img_off's (r >> 2) & 3
-    // swizzle leaves them 2-way conflicted); lane L of a 1-KiB piece fetches row L >> 2 and the
-    // chunk that lands at its slot L & 3
-    const int rl = lane >> 2, ch = (lane & 3) ^ (3 * (lane >> 5));
-#pragma unroll
-    for (int j = 0; j < JHI; ++j) {
-      const int q = wv + NW * j;
-      if (q < KA) voff[j] = (uint32_t)(((int64_t)(q * 16 + rl) * g.lda + 4 * ch) * 4);
-      else voff[j] = (uint32_t)(((int64_t)((q - KA) * 16 + rl) * g.ldb + 8 * ch) * 2);
-      dbase[j] = q < PTOT ? 1024u * q : (uint32_t)JUNK;
-      dslot[j] = q < PTOT ? 1u : 0u;
-      if (q >= PTOT) voff[j] = 0x40000000u;
-    }
-  }
-  const uint32_t lds0 = (uint32_t)(size_t)(lds_void*)lds;
-  auto dma = [&](int it) {
-    const uint32_t st = (uint32_t)(it % NS) * STAGE;
-    const uint32_t ko = it < nit ? (uint32_t)(it0 + it) * 64u : 0x80000000u;
-#pragma unroll
-    for (int j = 0; j < JHI; ++j) {
-      const int q = wv + NW * j;
-      dma16(q < KA ? ra : rb, lds0 + dbase[j] + dslot[j] * st, voff[j] + ko);
-    }
-  };
-
-#pragma unroll
-  for (int i = 0; i < NS; ++i) dma(i);
-  row_scales(g.a_amax, g.na, g.a_rs, m0, BM, mrows, AT == 0 ? tsa : nullptr, tia, red);
-  row_scales(g.b_amax, g.nb, g.b_rs, n0, BN, BN, nullptr, tib, red);
-  dma_wait<0>();   // stages 0 .. 3 landed
-  __syncthreads();
-
-  f32x4 acc[MB][NB];
-#pragma unroll
-  for (int a = 0; a < MB; ++a)
-#pragma unroll
-    for (int b = 0; b < NB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  int offa[MB], offb[NB];
-#pragma unroll
-  for (int a = 0; a < MB; ++a) offa[a] = (wm * WM + 16 * a + r16) * 64;
-#pragma unroll
-  for (int b = 0; b < NB; ++b) offb[b] = A_BYTES + (wn * WN + 16 * b + r16) * 64;
-  const int sw = 16 * 3 * ((r16 >> 3) & 1);   // the q image's chunk swizzle: a lane constant
-  const int gch = g4 & 1;
-  auto chunk = [&](int row_off, int ch) { return row_off + ((16 * ch) ^ sw); };
-  // this lane group's stage of super-step s: slot (2s) % 4 + (g4 >> 1)
-  const int gst = (g4 >> 1) * STAGE;
-  auto sbase = [&](int s) { return lds + ((2 * s) & 3) * STAGE + gst; };
-  float sa[MB];
-  if constexpr (AT == 0) {
-#pragma unroll
-    for (int a = 0; a < MB; ++a) sa[a] = tsa[wm * WM + 16 * a + r16];
-  }
-
-  struct FA {
-    f16x8 a0[MB], a1[MB];
-  };
-  f16x8 B0[NB], B1[NB];
-  auto read_b = [&](const char* st, int b) {
-    B0[b] = *reinterpret_cast<const f16x8*>(st + chunk(offb[b], gch));
-    B1[b] = *reinterpret_cast<const f16x8*>(st + chunk(offb[b], 2 + gch));
-  };
-  auto read_a2 = [&](const char* st, FA& F) {   // AT 2: producer-written pieces
-#pragma unroll
-    for (int a = 0; a < MB; ++a) {
-      F.a0[a] = *reinterpret_cast<const f16x8*>(st + chunk(offa[a], gch));
-      F.a1[a] = *reinterpret_cast<const f16x8*>(st + chunk(offa[a], 2 + gch));
-    }
-  };
-  auto read_raw = [&](const char* st, f32x4 (&raw)[MB][2]) {   // AT 0: k 8 gch .. + 7 as fp32
-#pragma unroll
-    for (int a = 0; a < MB; ++a) {
-      raw[a][0] = *reinterpret_cast<const f32x4*>(st + chunk(offa[a], 2 * gch));
-      raw[a][1] = *reinterpret_cast<const f32x4*>(st + chunk(offa[a], 2 * gch + 1));
-    }
-  };
-  auto mma = [&](const FA& F, int a, int b) {
-    if constexpr ((PR & 8) != 0) {
-      asm volatile("" ::"v"(F.a0[a]), "v"(F.a1[a]), "v"(B0[b]), "v"(B1[b]));
-      return;
-    }
-    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(F.a0[a], B0[b], acc[a][b], 0, 0, 0);
-    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(F.a0[a], B1[b], acc[a][b], 0, 0, 0);
-    acc[a][b] = __builtin_amdgcn_mfma_f32_16x16x32_f16(F.a1[a], B0[b], acc[a][b], 0, 0, 0);
-  };
-
-  // the last column block's pieces for s + 1 are read at the head of super-step s into a second
-  // buffer (the other blocks' are re-read right after their last triple): the super-step then ends
-  // on MFMAs, not on a fragment read the closing lgkmcnt(0) would wait for
-  f16x8 L0, L1;
-  auto step = [&](int s, const FA& Fc, FA& Fn) {
-    const char* nx = sbase(s + 1);
-    f32x4 raw[MB][2];
-    uint32_t h0w[MB][4], h1w[MB][4];
-    if constexpr ((PR & 16) != 0 && (PR & 1) == 0) {   // DMA first
-      dma(2 * s + 4);
-      dma(2 * s + 5);
-    }
-    if constexpr ((PR & 2) == 0) {
-      L0 = *reinterpret_cast<const f16x8*>(nx + chunk(offb[NB - 1], gch));
-      L1 = *reinterpret_cast<const f16x8*>(nx + chunk(offb[NB - 1], 2 + gch));
-    }
-    if constexpr (AT == 2) {
-      if constexpr ((PR & 2) == 0) read_a2(nx, Fn);
-    } else {
-      read_raw(nx, raw);
-    }
-#pragma unroll
-    for (int i = 0; i < MB * NB; ++i) {
-      const int b = i / MB, a = i % MB;
-      mma(Fc, a, b);
-      if (a == MB - 1 && b < NB - 1 && (PR & 2) == 0) read_b(nx, b);   // block b's last triple: its pieces for s + 1
-      if constexpr (AT == 0) {
-        if (i < 4 * MB) {
-          const int pa = i / 4, pw = i % 4;
-          const f32x4& r = raw[pa][pw >> 1];
-          split_pair_mix(r[2 * (pw & 1)], r[2 * (pw & 1) + 1], sa[pa], h0w[pa][pw], h1w[pa][pw]);
-        }
-      }
-      if (i == 0 && (PR & 1) == 0 && (PR & 16) == 0) {
-        dma(2 * s + 4);
-        dma(2 * s + 5);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if constexpr ((PR & 2) == 0) {
-      B0[NB - 1] = L0;
-      B1[NB - 1] = L1;
-    }
-    if constexpr (AT == 0) {
-#pragma unroll
-      for (int a = 0; a < MB; ++a) {
-        Fn.a0[a] = __builtin_bit_cast(f16x8, u32x4{h0w[a][0], h0w[a][1], h0w[a][2], h0w[a][3]});
-        Fn.a1[a] = __builtin_bit_cast(f16x8, u32x4{h1w[a][0], h1w[a][1], h1w[a][2], h1w[a][3]});
-      }
-    }
-    if constexpr ((PR & 32) != 0) {   // probe: this super-step's DMA stays in flight (a 2-super-step lead)
-      dma_wait<2 * JHI>();
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      raw_barrier();
-    } else if constexpr ((PR & 4) == 0) {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      raw_barrier();
-    } else {
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-  };
-  FA F0, F1;
-  {
-    const char* st = sbase(0);
-    if constexpr (AT == 2) {
-      read_a2(st, F0);
-    } else {
-      f32x4 raw[MB][2];
-      read_raw(st, raw);
-#pragma unroll
-      for (int a = 0; a < MB; ++a) {
-        const f32x8 y = f32x8{raw[a][0][0], raw[a][0][1], raw[a][0][2], raw[a][0][3],
-                              raw[a][1][0], raw[a][1][1], raw[a][1][2], raw[a][1][3]} * sa[a];
-        split2(y, F0.a0[a], F0.a1[a]);
-      }
-    }
-#pragma unroll
-    for (int b = 0; b < NB; ++b) read_b(st, b);
-    // super-step 0's DMA refills the slots of stages 0 and 1 that every wave reads just above
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    raw_barrier();
-  }
-  const int nss = nit / 2;
-  for (int s = 0; s < nss; s += 2) {
-    step(s, F0, F1);
-    if (s + 1 < nss) step(s + 1, F1, F0);
-  }
-  __syncthreads();
-
-  // ---- epilogue (gemm_f16_k's, on the 16 x 16 layout): after the quad transpose lane (lane & 3)
-  // owns row 16 a + 4 g4 + (lane & 3) of block (a, b) and its columns 16 b + (lane & 12) .. + 3
-  constexpr int SP = (EPI == 1 || EPI == 2) ? 2 : 0;
-  const int mrow = wm * WM + 4 * g4 + (lane & 3), ncol = wn * WN + (lane & 12);
-  const hx::Buf cbuf(g.C + z * g.c_zs + (int64_t)m0 * g.ldc + n0, (uint32_t)((int64_t)mrows * g.ldc * 4));
-  auto coff = [&](int a, int b) { return (uint32_t)((mrow + 16 * a) * g.ldc + ncol + 16 * b) * 4; };
-  float ibc[NB][4];
-#pragma unroll
-  for (int b = 0; b < NB; ++b)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) ibc[b][i] = tib[ncol + 16 * b + i];
-  auto tr = [&](int a, int b, float (&v)[4]) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = acc[a][b][i];
-    transpose4(v, lane);
-    const float ir = tia[mrow + 16 * a];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = v[i] * ir * ibc[b][i];
-  };
-  float bias[NB][4];
-#pragma unroll
-  for (int b = 0; b < NB; ++b) {
-    float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (g.bias) t = *reinterpret_cast<const float4*>(g.bias + n0 + ncol + 16 * b);
-    bias[b][0] = t.x; bias[b][1] = t.y; bias[b][2] = t.z; bias[b][3] = t.w;
-  }
-  if constexpr (EPI == 0 || EPI == 3) {
-#pragma unroll
-    for (int a = 0; a < MB; ++a) {
-#pragma unroll
-      for (int b = 0; b < NB; ++b) {
-        float v[4];
-        tr(a, b, v);
-        f32x4 o = {v[0] + bias[b][0], v[1] + bias[b][1], v[2] + bias[b][2], v[3] + bias[b][3]};
-        if constexpr (EPI == 3)
-          o += __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(cbuf.r, coff(a, b), 0, 0));
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), cbuf.r, coff(a, b), 0, SP);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  } else {
-    const hx::Buf pbuf((const char*)g.P + ((int64_t)m0 * g.ldp + n0) * 4, (uint32_t)((int64_t)mrows * g.ldp * 4));
-    const hx::Buf xbuf(EPI == 2 ? (const char*)g.aux + ((int64_t)m0 * g.ldaux + n0) * 4 : (const char*)g.C,
-                       (uint32_t)((int64_t)mrows * g.ldaux * 4));
-    auto poff = [&](int a, int b) { return (uint32_t)((mrow + 16 * a) * g.ldp + ncol + 16 * b) * 4; };
-    float csum[NB][4], cmx[NB][4], rmx[MB];
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) csum[b][i] = cmx[b][i] = 0.f;
-#pragma unroll
-    for (int a = 0; a < MB; ++a) rmx[a] = 0.f;
-#pragma unroll
-    for (int a = 0; a < MB; ++a) {
-      const bool in = mrow + 16 * a < mrows;
-#pragma unroll
-      for (int b = 0; b < NB; ++b) {
-        f32x4 u;
-        if constexpr (EPI == 2) {
-          const uint32_t off = (uint32_t)((mrow + 16 * a) * g.ldaux + ncol + 16 * b) * 4;
-          u = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xbuf.r, off, 0, 0));
-        }
-        float v[4];
-        tr(a, b, v);
-        f32x4 o;
-        if constexpr (EPI == 1) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] += bias[b][i];
-          f32x4 c;
-          if (g.dmode) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const float e = erff(v[i] * (1.0f / 1.41421f));
-              c[i] = 0.5f * (1.0f + e) + hx::gelu_pdf_f(v[i]);
-              o[i] = v[i] * 0.5f * (1.0f + e);
-            }
-          } else {
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              c[i] = v[i];
-              o[i] = hx::gelu_f(v[i]);
-            }
-          }
-          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, c), cbuf.r, coff(a, b), 0, SP);
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            o[i] = g.dmode ? v[i] * u[i] : v[i] * hx::gelu_grad_f(u[i] + bias[b][i]);
-            csum[b][i] += in ? o[i] : 0.f;
-          }
-        }
-        if (in) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float m = fabsf(o[i]);
-            rmx[a] = fmaxf(rmx[a], m);
-            cmx[b][i] = fmaxf(cmx[b][i], m);
-          }
-        }
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, o), pbuf.r, poff(a, b), 0, SP);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    // column values: over the 4 rows of a quad and the four lane groups; lanes (lane & 3) == 0,
-    // g4 == 0 then hold this wave's 4-column values
-#pragma unroll
-    for (int b = 0; b < NB; ++b)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        float m = cmx[b][i];
-        m = fmaxf(m, qx1(m));
-        m = fmaxf(m, qx2(m));
-        m = fmaxf(m, __shfl_xor(m, 16, 64));
-        cmx[b][i] = fmaxf(m, __shfl_xor(m, 32, 64));
-        if constexpr (EPI == 2) {
-          float t = csum[b][i];
-          t += qx1(t);
-          t += qx2(t);
-          t += __shfl_xor(t, 16, 64);
-          csum[b][i] = t + __shfl_xor(t, 32, 64);
-        }
-      }
-    // row maxima: over the 4 lanes of a row's 4-column groups
-#pragma unroll
-    for (int a = 0; a < MB; ++a) {
-      float m = rmx[a];
-      m = fmaxf(m, __shfl_xor(m, 4, 64));
-      rmx[a] = fmaxf(m, __shfl_xor(m, 8, 64));
-    }
-    const bool colLane = (lane & 3) == 0 && g4 == 0;
-    if constexpr (EPI == 2) {
-      if (g.colpart && colLane) {
-        float* row = g.colpart + (int64_t)(mt * NWM + wm) * g.N + n0 + wn * WN;
-#pragma unroll
-        for (int b = 0; b < NB; ++b)
-          *reinterpret_cast<float4*>(row + 16 * b + (lane & 12)) =
-              make_float4(csum[b][0], csum[b][1], csum[b][2], csum[b][3]);
-      }
-    }
-    float* rx = reinterpret_cast<float*>(lds);   // [NWN][BM]
-    float* cx = rx + NWN * BM;                    // [NWM][BN]
-    if (((lane >> 2) & 3) == 0) {
-#pragma unroll
-      for (int a = 0; a < MB; ++a) rx[wn * BM + mrow + 16 * a] = rmx[a];
-    }
-    if (colLane) {
-#pragma unroll
-      for (int b = 0; b < NB; ++b)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) cx[wm * BN + ncol + 16 * b + i] = cmx[b][i];
-    }
-    __syncthreads();
-    if (g.rowmax && tid < mrows) {
-      float m = rx[tid];
-#pragma unroll
-      for (int j = 1; j < NWN; ++j) m = fmaxf(m, rx[j * BM + tid]);
-      g.rowmax[(int64_t)(m0 + tid) * TN + nt] = m;
-    }
-    if (g.colmax && tid < BN) {
-      float m = cx[tid];
-#pragma unroll
-      for (int j = 1; j < NWM; ++j) m = fmaxf(m, cx[j * BN + tid]);
-      g.colmax[(int64_t)mt * g.N + n0 + tid] = m;
-    }
-  }
-}
-
 // ---------------------------------------------------------------- configurations
 // cfg 0: 256 x 192, 8 waves of 32 x 192, one workgroup per CU, 4-stage ring
 // cfg 1: 256 x 192, 8 waves (4 x 2) of 64 x 96, one workgroup per CU, 4-stage ring -- M >= 8192
@@ -1088,9 +686,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
 // cfg 5: 256 x 256, 8 waves (4 x 2) of 64 x 128, one workgroup per CU, 4-stage ring
 // cfg 6: cfg 1 with the bf16 variant's DMA pieces issued as one burst (the fp16x3 step always
 //        bursts them: interleaving measured 2-5 % slower, r5d); a 5-stage ring measured no gain (r5c)
-// cfg 7: cfg 1 on 16x16x32 MFMAs (gemm_f16q_k), fp16x3 only (bf16 operands run cfg 1), and only
-//        when a slab's stage count is even (otherwise cfg 1)
-constexpr int kCfgs = 8;
+constexpr int kCfgs = 7;
 int cfg_bm(int c) { return c <= 1 || c >= 5 ? 256 : c == 2 || c == 4 ? 128 : 64; }
 int cfg_bn(int c) { return c == 5 ? 256 : c <= 1 || c == 4 || c >= 6 ? 192 : c == 2 ? 96 : 64; }
 int cfg_nwm(int c) { return c == 0 ? 8 : c == 1 || c >= 5 ? 4 : c == 2 ? 4 : 2; }
@@ -1110,62 +706,8 @@ void launch_one(const F16Args& a, hipStream_t s) {
   gemm_f16_k<BM, BN, WM, WN, EPI, WGS, NS, AT, OB, DIL><<<8 * per, NT, smem, s>>>(a);
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, int WGS, int AT, int PR = 0>
-void launch_q(const F16Args& a, hipStream_t s) {
-  constexpr int NT = (BM / WM) * (BN / WN) * 64;
-  const int total = ((a.M + BM - 1) / BM) * (a.N / BN) * a.ks;
-  const int per = (total + 7) / 8;
-  const size_t smem = (size_t)4 * (BM + BN) * 64 + (2 * BM + BN + NT / 64) * 4 + 1024;   // + junk DMA KiB
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_f16q_k<BM, BN, WM, WN, EPI, WGS, AT, PR>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    attr = true;
-  }
-  gemm_f16q_k<BM, BN, WM, WN, EPI, WGS, AT, PR><<<8 * per, NT, smem, s>>>(a);
-}
-int q_probe() {   // HX_GEMM_Q_PROBE (read per call): the timing-only switches of gemm_f16q_k
-  const char* e = getenv("HX_GEMM_Q_PROBE");
-  return e ? atoi(e) : 0;
-}
-
-// HX_GEMM_F16_Q=1: the large tile (cfg 1) on 16x16x32 MFMAs (cfg 7) wherever it applies
-bool q_default() {
-  static const bool on = [] {
-    const char* e = getenv("HX_GEMM_F16_Q");
-    return e && atoi(e) == 1;
-  }();
-  return on;
-}
-
 template <int EPI, int AT = 0, int OB = 0>
 void launch_cfg(int cfg, const F16Args& a, hipStream_t s) {
-  if (cfg == 1 && q_default()) cfg = 7;
-  if (cfg == 7) {
-    if constexpr (AT != 1 && OB == 0) {
-      if ((a.K / 16 / a.ks) % 2 == 0) {
-        if constexpr (EPI == 0 && AT == 2) {
-          switch (q_probe()) {
-            case 1: launch_q<256, 192, 64, 96, EPI, 1, AT, 1>(a, s); return;
-            case 2: launch_q<256, 192, 64, 96, EPI, 1, AT, 2>(a, s); return;
-            case 3: launch_q<256, 192, 64, 96, EPI, 1, AT, 3>(a, s); return;
-            case 4: launch_q<256, 192, 64, 96, EPI, 1, AT, 4>(a, s); return;
-            case 7: launch_q<256, 192, 64, 96, EPI, 1, AT, 7>(a, s); return;
-            case 8: launch_q<256, 192, 64, 96, EPI, 1, AT, 8>(a, s); return;
-            case 15: launch_q<256, 192, 64, 96, EPI, 1, AT, 15>(a, s); return;
-            case 16: launch_q<256, 192, 64, 96, EPI, 1, AT, 16>(a, s); return;
-            case 32: launch_q<256, 192, 64, 96, EPI, 1, AT, 32>(a, s); return;
-            case 40: launch_q<256, 192, 64, 96, EPI, 1, AT, 40>(a, s); return;
-            case 48: launch_q<256, 192, 64, 96, EPI, 1, AT, 48>(a, s); return;
-            default: break;
-          }
-        }
-        launch_q<256, 192, 64, 96, EPI, 1, AT>(a, s);
-        return;
-      }
-    }
-    cfg = 1;
-  }
   if (cfg == 0) launch_one<256, 192, 32, 192, EPI, 1, 4, AT, OB>(a, s);
   else if (cfg == 1) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB>(a, s);
   else if (cfg == 6) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 0>(a, s);

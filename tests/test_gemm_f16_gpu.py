@@ -73,7 +73,7 @@ def test_gemm_f16_dgrad_beta_bias(dev, M, N, K):
     assert ((out2.double() - ref2).abs() / den2).max().item() < 4e-6
 
 
-@pytest.mark.parametrize('cfg', ['plan', '4', '7'])
+@pytest.mark.parametrize('cfg', ['plan', '4'])
 def test_gemm_f16_gelu_epilogues(dev, monkeypatch, cfg):
     """FFN up (bias + GELU: C = gelu'(u), P = gelu(u), max |P| per (row, N tile) and per (M tile,
     column)) and the FFN-down data gradient with the GELU backward (t = acc * gelu'(u), column sums
@@ -277,7 +277,7 @@ def test_ffn_bf16_autograd(dev, monkeypatch, lib):
     assert rel(W1.grad, W1r.grad) < 1e-2 and rel(W2.grad, W2r.grad) < 1e-2 and rel(b1.grad, b1r.grad) < 1e-2
 
 
-@pytest.mark.parametrize('cfg', ['0', '1', '2', '3', '4', '5', '6', '7'])
+@pytest.mark.parametrize('cfg', ['0', '1', '2', '3', '4', '5', '6'])
 def test_gemm_f16_every_tile(dev, monkeypatch, cfg):
     """Every tile configuration of gemm_f16_k (HX_GEMM_F16_CFG forces it): forward with bias and the
     beta = 1 data gradient, rows not a multiple of the tile."""
@@ -360,9 +360,8 @@ def _row_err(out, ref64, den):
     return ((out.double() - ref64).abs() / den.clamp_min(1e-300)).amax(1)
 
 
-@pytest.mark.parametrize('cfg', ['plan', '7'])
 @pytest.mark.parametrize('side', ['a', 'b'])
-def test_gemm_f16_row_ramp(dev, monkeypatch, side, cfg):
+def test_gemm_f16_row_ramp(dev, side):
     """The fp16x3 precision envelope across rows (VERDICT r4 Next #2): A's rows (side a) or W's rows
     = output columns (side b) ramped over 2^0 .. 2^-30 of the tensor's largest.  Per-row operand
     scales keep every row at fp32 class: the row-wise error (each row against its own sum of
@@ -436,7 +435,7 @@ def test_amax_rows_cols_one_pass(rows, cols):
     assert torch.equal(c, x.abs().amax(0, keepdim=True))
 
 
-@pytest.mark.parametrize('cfg', ['plan', '0', '2', '3', '4', '5', '6', '7'])
+@pytest.mark.parametrize('cfg', ['plan', '0', '2', '3', '4', '5', '6'])
 def test_gemm_f16_presplit_a_bitwise(dev, monkeypatch, cfg):
     """A handed over already split into fp16 P2 pieces at its row scales (split_rows_f16, or a
     LayerNorm's pieces_out) is read as it is (AT 2: no split in the k loop) and gives results

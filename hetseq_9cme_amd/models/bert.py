@@ -40,8 +40,8 @@ logger = logging.getLogger(__name__)
 
 CONFIG_NAME = 'bert_config.json'
 WEIGHTS_NAME = 'pytorch_model.bin'
-# short names -> the archive URLs the reference downloads (bert_modeling.py:30-38); here they
-# resolve only through a pre-populated offline cache (utils.file_utils.cached_path)
+# short names -> the archive URLs the reference downloads (bert_modeling.py:30-38), fetched into
+# the ETag-keyed download cache by utils.file_utils.cached_path (a cached copy is used offline)
 _S3 = 'https://s3.amazonaws.com/models.huggingface.co/bert/{}.tar.gz'
 PRETRAINED_MODEL_ARCHIVE_MAP = {n: _S3.format(n) for n in (
     'bert-base-uncased', 'bert-large-uncased', 'bert-base-cased', 'bert-large-cased',
@@ -598,8 +598,8 @@ class BertPreTrainedModel(nn.Module):
         ``pretrained_model_name_or_path`` is a local directory holding
         ``bert_config.json`` + ``pytorch_model.bin`` (or ``model.safetensors``), a
         ``.tar.gz`` archive of such a directory (extracted to a temp dir with the
-        reference's path-traversal guard), or anything ``utils.file_utils.cached_path``
-        resolves offline (a pre-populated cache entry).  ``from_tf=True`` reads
+        reference's path-traversal guard), or a URL / short name that ``utils.file_utils.cached_path``
+        downloads into its cache (or finds there when offline).  ``from_tf=True`` reads
         ``model.ckpt`` (TF V2 bundle) from the directory through the native-format
         reader -- no tensorflow needed.  Weights load with ``weights_only=True``."""
         import shutil
@@ -610,8 +610,8 @@ class BertPreTrainedModel(nn.Module):
         try:
             resolved = cached_path(archive, cache_dir=cache_dir)
         except EnvironmentError:
-            raise EnvironmentError('pretrained model not found (offline: local paths and cache only): {}'
-                                   .format(pretrained_model_name_or_path))
+            raise EnvironmentError('pretrained model not found (neither a local path, a reachable URL nor a '
+                                   'cached download): {}'.format(pretrained_model_name_or_path))
         tempdir = None
         if os.path.isdir(resolved) or from_tf:
             serialization_dir = resolved

@@ -42,6 +42,7 @@ def main():
                     help='timed blocks of --steps updates each; min / median / max of their s/update reported '
                          '(value = the median)')
     ap.add_argument('--no-overlap-wgrad', action='store_true', help='weight gradients on the compute stream')
+    ap.add_argument('--overlap-wgrad', action='store_true', help='weight gradients on the side stream at every size')
     ap.add_argument('--cprofile', default=None, metavar='OUT',
                     help='after the timed steps, cProfile 20 more steps and write the top host functions to OUT')
     ap.add_argument('--gpus', type=int, default=1, help='ranks (launched by torch.distributed.run when > 1)')
@@ -88,6 +89,8 @@ def main():
         argv.append('--graph-train-step' if a.graph_train_step == 'on' else '--no-graph-train-step')
     if a.no_overlap_wgrad:
         argv.append('--no-overlap-wgrad')
+    if a.overlap_wgrad:
+        argv.append('--overlap-wgrad')
     if a.fp32_gemm:
         argv += ['--fp32-gemm', a.fp32_gemm]
     if a.force_reducer:

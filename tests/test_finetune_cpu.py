@@ -90,6 +90,18 @@ def test_ner_scores_match_seqeval_semantics():
     assert get_entities(['I-PER', 'I-PER', 'B-PER']) == [('PER', 0, 1), ('PER', 2, 2)]
     r = ner_scores([['B-PER', 'I-PER', 'O', 'B-LOC']], [['B-PER', 'I-PER', 'O', 'B-ORG']])
     assert r['precision'] == 0.5 and r['recall'] == 0.5 and abs(r['accuracy'] - 0.75) < 1e-9
+    # seqeval's README example (its documented output: accuracy 0.80, precision / recall / f1 0.50,
+    # per type MISC 0 / 0 / 0 support 1, PER 1 / 1 / 1 support 1)
+    y_true = [['O', 'O', 'O', 'B-MISC', 'I-MISC', 'I-MISC', 'O'], ['B-PER', 'I-PER', 'O']]
+    y_pred = [['O', 'O', 'B-MISC', 'I-MISC', 'I-MISC', 'I-MISC', 'O'], ['B-PER', 'I-PER', 'O']]
+    r = ner_scores(y_true, y_pred, per_type=True)
+    assert abs(r['accuracy'] - 0.8) < 1e-12 and r['precision'] == r['recall'] == r['f1'] == 0.5
+    assert r['per_type'] == {'MISC': {'precision': 0.0, 'recall': 0.0, 'f1': 0.0, 'support': 1},
+                             'PER': {'precision': 1.0, 'recall': 1.0, 'f1': 1.0, 'support': 1}}
+    # IOBES / IOE tags (conlleval rules): S- is a one-token chunk, E- closes one
+    assert get_entities(['S-PER', 'B-LOC', 'E-LOC', 'O', 'I-ORG', 'E-ORG']) == [
+        ('PER', 0, 0), ('LOC', 1, 2), ('ORG', 4, 5)]
+    assert get_entities(['B-PER', 'S-PER', 'I-LOC']) == [('PER', 0, 0), ('PER', 1, 1), ('LOC', 2, 2)]
 
 
 def test_ner_eval_cli_and_transformers_task(tmp_path):

@@ -142,7 +142,10 @@ __device__ __forceinline__ void row_scales(const float* __restrict__ p, int np, 
 //   * a counted vmcnt that leaves only stage it + NS - 1's pieces in flight (so stage it + 2 has
 //     landed: NS = 4 gives every DMA two steps), then ONE raw barrier.
 // The barrier opens step it + 1 straight into MFMAs: no wave waits on a fragment read after it.
-template <int BM, int BN, int WM, int WN, int EPI, int WGS, int NS, int AT = 0, int OB = 0, int DIL = 1>
+// DW = 4: only waves 0 .. 3 (one per SIMD: waves w and w + 4 share a SIMD) issue the LDS-DMA pieces,
+// the others only read fragments and run MFMAs -- a DMA burst then stalls one wave of a SIMD pair,
+// not both (DW = 12: waves 4 .. 7 instead, measured slower)
+template <int BM, int BN, int WM, int WN, int EPI, int WGS, int NS, int AT = 0, int OB = 0, int DIL = 1, int DW = 0>
 __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) * WGS / 4) void gemm_f16_k(F16Args g) {
   static_assert(AT != 1 || EPI == 0 || EPI == 3 || OB == 1, "bf16 operands: GELU epilogues in bf16");
   static_assert(AT >= 0 && AT <= 2, "operand kind");
@@ -155,7 +158,10 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
   constexpr int MB = WM / 32, NB = WN / 32;
   constexpr int A_BYTES = BM * 64, B_BYTES = BN * 64, STAGE = A_BYTES + B_BYTES;
   constexpr int KA = BM / 16, KB = BN / 16, PTOT = KA + KB;   // 1-KiB DMA pieces per stage
-  constexpr int JHI = (PTOT + NW - 1) / NW, JLO = PTOT / NW;
+  constexpr int NDW = DW > 0 ? (DW & 7) : NW;                   // waves that issue DMA
+  constexpr int DW0 = DW >= 8 ? NW - NDW : 0;                   // the first of them
+  static_assert(NDW <= NW && NDW > 0, "DMA waves");
+  constexpr int JHI = (PTOT + NDW - 1) / NDW, JLO = PTOT / NDW;
   static_assert(JLO >= 1, "fewer DMA pieces than waves");
   static_assert(BM % 16 == 0 && BN % 16 == 0 && WM % 32 == 0 && WN % 32 == 0, "tile shape");
   static_assert(NT >= BM && NT >= BN, "one thread per table row");
@@ -192,7 +198,7 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
     img_lane_src(lane, rl, ch);
 #pragma unroll
     for (int j = 0; j < JHI; ++j) {
-      const int q = wv + NW * j;
+      const int q = wv - DW0 + NDW * j;
       if (q < KA) voff[j] = (uint32_t)(((int64_t)(q * 16 + rl) * g.lda + (16 / AE) * ch) * AE);
       else voff[j] = (uint32_t)(((int64_t)((q - KA) * 16 + rl) * g.ldb + 8 * ch) * 2);
       dbase[j] = q < PTOT ? 1024u * q : (uint32_t)JUNK;
@@ -202,10 +208,11 @@ __global__ __launch_bounds__((BM / WM) * (BN / WN) * 64, (BM / WM) * (BN / WN) *
   }
   const uint32_t lds0 = (uint32_t)(size_t)(lds_void*)lds;
   auto dma_one = [&](int it, int j) {   // piece j of this wave for stage it (64 B of each row per stage)
+    if (DW > 0 && (wv < DW0 || wv >= DW0 + NDW)) return;   // wave-uniform: a non-DMA wave
     const uint32_t st = (uint32_t)(it % NS) * STAGE;
     // stages past this slab's end: an offset past every buffer (the load returns zeros, reads nothing)
     const uint32_t ko = it < nit ? (uint32_t)(it0 + it) * 64u : 0x80000000u;
-    const int q = wv + NW * j;   // A or B piece: uniform per wave, a select of the descriptor
+    const int q = wv - DW0 + NDW * j;   // A or B piece: uniform per wave, a select of the descriptor
     dma16(q < KA ? ra : rb, lds0 + dbase[j] + dslot[j] * st, voff[j] + ko);
   };
   auto dma = [&](int it) {   // every piece of stage it into its ring slot
@@ -691,7 +698,7 @@ int cfg_bm(int c) { return c <= 1 || c >= 5 ? 256 : c == 2 || c == 4 ? 128 : 64;
 int cfg_bn(int c) { return c == 5 ? 256 : c <= 1 || c == 4 || c >= 6 ? 192 : c == 2 ? 96 : 64; }
 int cfg_nwm(int c) { return c == 0 ? 8 : c == 1 || c >= 5 ? 4 : c == 2 ? 4 : 2; }
 
-template <int BM, int BN, int WM, int WN, int EPI, int WGS, int NS, int AT = 0, int OB = 0, int DIL = 1>
+template <int BM, int BN, int WM, int WN, int EPI, int WGS, int NS, int AT = 0, int OB = 0, int DIL = 1, int DW = 0>
 void launch_one(const F16Args& a, hipStream_t s) {
   constexpr int NT = (BM / WM) * (BN / WN) * 64;
   const int total = ((a.M + BM - 1) / BM) * (a.N / BN) * a.ks;
@@ -699,15 +706,30 @@ void launch_one(const F16Args& a, hipStream_t s) {
   const size_t smem = (size_t)NS * (BM + BN) * 64 + (2 * BM + BN + NT / 64) * 4 + 1024;   // + junk DMA KiB
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_f16_k<BM, BN, WM, WN, EPI, WGS, NS, AT, OB, DIL>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&gemm_f16_k<BM, BN, WM, WN, EPI, WGS, NS, AT, OB, DIL, DW>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
-  gemm_f16_k<BM, BN, WM, WN, EPI, WGS, NS, AT, OB, DIL><<<8 * per, NT, smem, s>>>(a);
+  gemm_f16_k<BM, BN, WM, WN, EPI, WGS, NS, AT, OB, DIL, DW><<<8 * per, NT, smem, s>>>(a);
+}
+
+// which waves of the large fp16x3 tile issue its LDS-DMA: 4 (default) waves 0 .. 3, one per SIMD --
+// the headline step 35.54-35.66 vs 35.77-35.81 ms with every wave issuing, 9 alternated pairs on two
+// boxes, 8 of them faster (profiles/r6u_gemm_dma_waves_ab.txt; the kernels alone measure equal);
+// waves 4 .. 7 instead measured 35.94-36.02.  HX_GEMM_DMA_WAVES=0: every wave (read per call)
+int dma_waves() {
+  const char* e = getenv("HX_GEMM_DMA_WAVES");
+  return e ? atoi(e) : 4;
 }
 
 template <int EPI, int AT = 0, int OB = 0>
 void launch_cfg(int cfg, const F16Args& a, hipStream_t s) {
+  if constexpr (AT != 1) {
+    if (cfg == 1 && dma_waves() == 4) {
+      launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 1, 4>(a, s);
+      return;
+    }
+  }
   if (cfg == 0) launch_one<256, 192, 32, 192, EPI, 1, 4, AT, OB>(a, s);
   else if (cfg == 1) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB>(a, s);
   else if (cfg == 6) launch_one<256, 192, 64, 96, EPI, 1, 4, AT, OB, 0>(a, s);

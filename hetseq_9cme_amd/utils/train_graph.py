@@ -153,7 +153,11 @@ class GraphedTrainStep(object):
         g = torch.cuda.CUDAGraph()
         rng.external = True
         try:
-            with torch.cuda.graph(g, pool=self.pool):
+            # thread-local capture: the RCCL process group's watchdog thread keeps querying its
+            # events during the capture; under the default global mode those queries fail
+            # ('operation not permitted when stream is capturing') and the watchdog aborts the
+            # process (seen once in test_graph_step_with_rccl_reducer_ner)
+            with torch.cuda.graph(g, pool=self.pool, capture_error_mode='thread_local'):
                 ent.out = c._train_step([ent.static])
         except Exception:
             # a failed capture must not leave the optimizer pointed at the graph's buffer:

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for dw in ${DWS:-4 12}; do
+for dw in ${TDWS:-}; do
   HX_GEMM_DMA_WAVES=$dw timeout -k 10 300 python -u -m pytest tests/test_gemm_f16_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/dw_tests_$dw.log 2>&1 || { tail -30 gpurun_out/dw_tests_$dw.log; exit 1; }
   echo "tests dma_waves=$dw: $(tail -1 gpurun_out/dw_tests_$dw.log)"
 done

@@ -69,16 +69,32 @@ __global__ __launch_bounds__(NT) void ln_fwd_k(const T* __restrict__ y, const fl
   const int64_t nw = (int64_t)gridDim.x * WPB;
   const float inv_keep = keep_prob > 0.f ? 1.f / keep_prob : 0.f;
   const bool drop = keep_prob < 1.f;
+  // one row of look-ahead (grid-strided launches): the next row's y / res loads are in flight
+  // while this row reduces and stores
+  Row<CH> yn, qn;
+  auto load_row = [&](int64_t r) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int j = (c * 64 + lane) * 4;
+      if (j < H) {
+        yn.v[c] = hx::load4(y + r * H + j);
+        if (res) qn.v[c] = hx::load4(res + r * H + j);
+      }
+    }
+  };
+  if (wave < rows) load_row(wave);
   for (int64_t r = wave; r < rows; r += nw) {
     float am = 0.f;
     Row<CH> x;
+    const Row<CH> yc = yn, qc = qn;
+    if (r + nw < rows) load_row(r + nw);
     float s = 0.f;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int j = (c * 64 + lane) * 4;
       float4 v = hx::f4(0.f);
       if (j < H) {
-        v = hx::load4(y + r * H + j);
+        v = yc.v[c];
         if (bias) {
           const float4 b = *reinterpret_cast<const float4*>(bias + j);
           v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
@@ -91,7 +107,7 @@ __global__ __launch_bounds__(NT) void ln_fwd_k(const T* __restrict__ y, const fl
           v.w = (k & 8) ? v.w * inv_keep : 0.f;
         }
         if (res) {
-          const float4 q = hx::load4(res + r * H + j);
+          const float4 q = qc.v[c];
           v.x += q.x; v.y += q.y; v.z += q.z; v.w += q.w;
         }
         if (zsave) hx::store4(zsave + r * H + j, v);
@@ -497,7 +513,7 @@ template <typename T>
 void ln_fwd_t(const void* y, const float* bias, const void* res, const float* gamma, const float* beta, void* out,
               void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob, const uint64_t* seed,
               uint64_t stream, int drop_after, hipStream_t s, float* amax_part, uint16_t* pieces) {
-  const int grid = ln_grid(rows, 4096);
+  const int grid = hx_ln_fwd_blocks(rows);
   HX_CH_DISPATCH(H, {
     if (drop_after)
       ln_fwd_k<T, CH, true><<<grid, NT, 0, s>>>((const T*)y, bias, (const T*)res, gamma, beta, (T*)out, (T*)zsave,
@@ -532,8 +548,16 @@ void ln_bwd_t(const void* dout, const void* z, const float* mean, const float* r
 
 }  // namespace
 
-int hx_ln_bwd_blocks(int64_t rows) { return ln_grid(rows, 512); }
-int hx_ln_fwd_blocks(int64_t rows) { return ln_grid(rows, 4096); }
+namespace {
+int env_cap(const char* name, int dflt) {
+  const char* e = getenv(name);
+  const int v = e ? atoi(e) : 0;
+  return v > 0 ? v : dflt;
+}
+}  // namespace
+
+int hx_ln_bwd_blocks(int64_t rows) { return ln_grid(rows, env_cap("HX_LN_BWD_CAP", 512)); }
+int hx_ln_fwd_blocks(int64_t rows) { return ln_grid(rows, env_cap("HX_LN_FWD_CAP", 4096)); }
 
 void hx_ln_fwd(int bf16, const void* y, const float* bias, const void* res, const float* gamma, const float* beta,
                void* out, void* zsave, float* mean, float* rstd, int64_t rows, int H, float eps, float keep_prob,

@@ -33,7 +33,8 @@ def main():
     g = torch.Generator(device=dev).manual_seed(0)
     tag = os.path.basename(os.environ.get('HX_EXT_SO', 'in-tree'))
     keep = float(os.environ.get('KEEP', '0.9'))
-    tag += ' keep %g' % keep
+    tag += ' keep %g fwd cap %s bwd cap %s' % (keep, os.environ.get('HX_LN_FWD_CAP', '-'),
+                                              os.environ.get('HX_LN_BWD_CAP', '-'))
     for dt in (torch.float32, torch.bfloat16):
         y = torch.randn(n, H, device=dev, generator=g).to(dt)
         res = torch.randn(n, H, device=dev, generator=g).to(dt)
@@ -42,8 +43,9 @@ def main():
         beta = torch.randn(H, device=dev, generator=g)
         f32 = dt == torch.float32
         am = torch.empty(n, 1, device=dev) if f32 else None
-        out, z, mean, rstd = C().ln_fwd(y, bias, res, gamma, beta, 1e-12, keep, seed, 1, False, True, am)
-        tf = timed(lambda: C().ln_fwd(y, bias, res, gamma, beta, 1e-12, keep, seed, 1, False, True, am))
+        pc = torch.empty(n, 2 * H, dtype=torch.float16, device=dev) if f32 else None   # training's pieces
+        out, z, mean, rstd = C().ln_fwd(y, bias, res, gamma, beta, 1e-12, keep, seed, 1, False, True, am, pc)
+        tf = timed(lambda: C().ln_fwd(y, bias, res, gamma, beta, 1e-12, keep, seed, 1, False, True, am, pc))
         dout = torch.randn(n, H, device=dev, generator=g).to(dt)
         dg, db, dbb = (torch.zeros(H, device=dev) for _ in range(3))
         bm = torch.empty(n, 1, device=dev) if f32 else None

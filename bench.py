@@ -323,11 +323,13 @@ def run(a, rank, world, dev_index, init_method):
     t0 = time.perf_counter()
     for _ in range(a.steps):
         out = step()
+    t_enq = time.perf_counter()   # the host's last launch: close to the end => the host bounds the step
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    host_ms = (t_enq - t0) / a.steps * 1000.0
     loss = float(out['loss']) if out is not None else float('nan')
     # every rank's time and a count of the ranks the communicator really reduced over
     per_rank = [elapsed]
@@ -379,6 +381,8 @@ def run(a, rank, world, dev_index, init_method):
             'warmup': a.warmup,
             'ms_per_step': round(ms, 3),
             'sec_per_step': round(ms / 1000.0, 5),
+            # host time to enqueue the timed steps (rank 0): near ms_per_step when the host bounds it
+            'host_enqueue_ms_per_step': round(host_ms, 3),
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': round(value / ref, 2) if ref else None,

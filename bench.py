@@ -307,11 +307,22 @@ def run(a, rank, world, dev_index, init_method):
         from hetseq_9cme_amd import ops as _ops
         _ops.set_reserved_cus(a.reserve_cus)
 
+    prio = None
+    if os.environ.get('HX_COMPUTE_PRIO') == '1':
+        # experiment: the step on a high-priority stream (the weight-gradient side stream stays at
+        # normal priority), so the dispatcher serves the critical path first when CUs free up
+        torch.cuda.synchronize()
+        prio = torch.cuda.Stream(priority=torch.cuda.Stream.priority_range()[1])
+        print('bench: compute stream priority {}'.format(prio.priority), file=sys.stderr, flush=True)
+
     def step():
         samples = next(itr)
         if load is not None:
             c, st, n, us, lds, sink = load
             c.spin(n, us, lds, sink, st)
+        if prio is not None:
+            with torch.cuda.stream(prio):
+                return ctrl.train_step(samples)
         return ctrl.train_step(samples)
 
     for _ in range(a.warmup):

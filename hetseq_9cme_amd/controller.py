@@ -73,7 +73,13 @@ class Controller(object):
             ops.set_fused(False)      # A/B mode: plain torch ops on the GPU
         ops.set_fp32_gemm(getattr(args, 'fp32_gemm', 'native'))
         ow = getattr(args, 'overlap_wgrad', 'auto')
-        ops.set_side_stream({True: 'on', False: 'off', None: 'auto'}.get(ow, ow))
+        # 'auto' threshold: products of >= 8192 token rows; >= 4096 for hidden sizes >= 1024, whose
+        # wider products pay for the overlap already there (BERT-large seq 128 b32 44.34-44.40 vs
+        # 45.38-45.55 ms/step, seq 512 b8 48.80-49.03 vs 49.35-49.36; BERT-base at 4096 rows is
+        # bimodal, 12.6 or 13.9 vs 13.1: profiles/r6ae_side_stream_low_priority_ab.txt)
+        hidden = getattr(getattr(model, 'config', None), 'hidden_size', 0) or 0
+        ops.set_side_stream({True: 'on', False: 'off', None: 'auto'}.get(ow, ow),
+                            auto_rows=4096 if hidden >= 1024 else None)
         if getattr(args, 'debug_kernels', False) and self.cuda:
             ops.C().set_debug(True)   # validation inside the bindings (see csrc/bindings.cpp)
         if self.cuda:

@@ -1139,6 +1139,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     TORCH_CHECK(st != nullptr, "hipExtStreamCreateWithCUMask failed");
     return (int64_t)(uintptr_t)st;
   });
+  m.def("priority_stream", [](int64_t prio) {
+    hipStream_t st = hx_priority_stream((int)prio);
+    TORCH_CHECK(st != nullptr, "hipStreamCreateWithPriority failed");
+    return (int64_t)(uintptr_t)st;
+  });
+  m.def("stream_priority_range", []() {
+    int least = 0, greatest = 0;
+    hx_stream_priority_range(&least, &greatest);
+    return std::vector<int64_t>{least, greatest};
+  });
   m.def("destroy_stream", [](int64_t h) { hx_destroy_stream(reinterpret_cast<hipStream_t>((uintptr_t)h)); });
   m.def("spin", [](int64_t blocks, double us, int64_t lds_bytes, Tensor sink, int64_t stream) {
     TORCH_CHECK(sink.is_cuda() && sink.scalar_type() == torch::kInt32 && sink.numel() >= 256, "spin: int32 sink[256]");

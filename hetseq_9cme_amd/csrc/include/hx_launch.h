@@ -229,5 +229,7 @@ void hx_set_reserved_cus(int r);
 int hx_reserved_cus();
 int hx_cu_slots();   // workgroup slots of one round: n_cu - reserved
 hipStream_t hx_cu_masked_stream(int first_cu, int count);
+hipStream_t hx_priority_stream(int prio);
+void hx_stream_priority_range(int* least, int* greatest);
 void hx_destroy_stream(hipStream_t s);
 void hx_spin(int blocks, double us, int lds_bytes, uint32_t* sink, hipStream_t s);

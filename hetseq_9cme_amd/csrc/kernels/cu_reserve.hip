@@ -67,6 +67,22 @@ hipStream_t hx_cu_masked_stream(int first_cu, int count) {
   return s;
 }
 
+// A non-blocking stream at HIP priority `prio` (clamped to the device range: least = the lowest,
+// e.g. 1 below the default 0; greatest = the highest, -1); returns 0 on failure.  The caller owns it.
+hipStream_t hx_priority_stream(int prio) {
+  int least = 0, greatest = 0;
+  if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return nullptr;
+  const int p = prio > least ? least : (prio < greatest ? greatest : prio);
+  hipStream_t s = nullptr;
+  if (hipStreamCreateWithPriority(&s, hipStreamNonBlocking, p) != hipSuccess) return nullptr;
+  return s;
+}
+
+void hx_stream_priority_range(int* least, int* greatest) {
+  *least = *greatest = 0;
+  (void)hipDeviceGetStreamPriorityRange(least, greatest);
+}
+
 void hx_destroy_stream(hipStream_t s) {
   if (s) (void)hipStreamDestroy(s);
 }

@@ -5,6 +5,7 @@ hand-written HIP kernels (``_C``), CPU tensors run the plain-torch reference of
 the same math (used by the CPU test-suite and as the numerics oracle for the GPU
 kernel tests).  Semantics follow the reference model (hetseq/bert_modeling.py).
 """
+import os
 import torch
 import torch.nn.functional as F
 
@@ -124,15 +125,18 @@ class _Side(object):
     # 'on' (--overlap-wgrad) / 'off' (--no-overlap-wgrad): every product / none.
     mode = 'auto'
     AUTO_ROWS = 8192
-    streams = {}          # device index -> torch.cuda.Stream
-    active = set()        # device indices with side work queued in the current backward
+    auto_rows = AUTO_ROWS   # set_side_stream(..., auto_rows=): 4096 for hidden sizes >= 1024
+    priority = os.environ.get('HX_SIDE_PRIO', 'low')   # 'low' (default) or 'normal' HIP priority
+    streams = {}          # (device index, low priority) -> stream
+    active = {}           # device index -> the side stream this backward queued work on
 
 
-def set_side_stream(flag):
+def set_side_stream(flag, auto_rows=None):
     """Weight-gradient work on a side stream: True / 'on', False / 'off', or 'auto' (on for products
-    of >= _Side.AUTO_ROWS token rows, the measured default)."""
+    of >= ``auto_rows`` token rows, default _Side.AUTO_ROWS, the measured default)."""
     _Side.mode = {True: 'on', False: 'off'}.get(flag, flag) if isinstance(flag, bool) else str(flag)
     assert _Side.mode in ('on', 'off', 'auto'), flag
+    _Side.auto_rows = int(auto_rows) if auto_rows else _Side.AUTO_ROWS
 
 
 def side_begin(device, rows=0):
@@ -142,20 +146,42 @@ def side_begin(device, rows=0):
     dgrad chain (attention / LayerNorm / GELU backward: mostly memory-bound),
     the side stream's GEMMs fill the matrix cores.  Joined back into the compute
     stream by an end-of-backward callback (``side_join``)."""
-    if device.type != 'cuda' or _Side.mode == 'off' or (_Side.mode == 'auto' and rows < _Side.AUTO_ROWS):
+    if device.type != 'cuda' or _Side.mode == 'off' or (_Side.mode == 'auto' and rows < _Side.auto_rows):
+        return None
+    if torch.cuda.is_current_stream_capturing():
+        # a captured update (utils/train_graph.py) stays on one stream: replays of updates captured
+        # with the side-stream branch ran at twice the device time (NER 17.6-19.2 vs 8.3 ms/update,
+        # profiles/r6ae_side_stream_low_priority_ab.txt)
         return None
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    st = _Side.streams.get(idx)
+    st = _Side.active.get(idx)
     if st is None:
-        # normal priority: high priority measured no different (50.87 / 50.90 vs 50.76 / 51.01 ms/step,
-        # round 3)
-        st = _Side.streams[idx] = torch.cuda.Stream(device=idx)
-    st.wait_stream(torch.cuda.current_stream(idx))
-    if not _Side.active:
-        torch.autograd.Variable._execution_engine.queue_callback(side_join)
-    if idx not in _Side.active:
+        st = _side_stream(idx)
+        if not _Side.active:
+            torch.autograd.Variable._execution_engine.queue_callback(side_join)
         C().reducer_set_side_stream(st.cuda_stream)   # bucket collectives order after it
-    _Side.active.add(idx)
+        _Side.active[idx] = st
+    st.wait_stream(torch.cuda.current_stream(idx))
+    return st
+
+
+def _side_stream(idx):
+    low = _Side.priority == 'low'
+    key = (idx, low)
+    st = _Side.streams.get(key)
+    if st is None:
+        if low:
+            # HIP's LOWEST stream priority (1; the compute stream is at 0, RCCL's streams at -1): when
+            # CUs free up, the dispatcher serves the critical path (attention, LayerNorm, data
+            # gradients) before these weight gradients.  Same box, alternated 3x: phase 2 41.19-41.38
+            # -> 40.14-40.15 ms/step, batch 128 35.14-35.22 -> 34.95-35.02
+            # (profiles/r6ad_stream_priority_ab.txt).  (A high-priority side stream measured no
+            # different in round 3.)
+            with torch.cuda.device(idx):
+                st = torch.cuda.ExternalStream(C().priority_stream(1), device=torch.device('cuda', idx))
+        else:
+            st = torch.cuda.Stream(device=idx)
+        _Side.streams[key] = st
     return st
 
 
@@ -164,15 +190,15 @@ def active_side_stream(device):
     if device.type != 'cuda':
         return None
     idx = device.index if device.index is not None else torch.cuda.current_device()
-    return _Side.streams.get(idx) if idx in _Side.active else None
+    return _Side.active.get(idx)
 
 
 def side_join():
     """Make the compute stream wait for all queued side-stream work."""
     if not _Side.active:
         return
-    for idx in list(_Side.active):
-        torch.cuda.current_stream(idx).wait_stream(_Side.streams[idx])
+    for idx, st in list(_Side.active.items()):
+        torch.cuda.current_stream(idx).wait_stream(st)
     _Side.active.clear()
     C().reducer_set_side_stream(0)
 

@@ -876,3 +876,33 @@ def test_embed_type_grad(dev, dt, ntypes, H):
     out2 = torch.empty_like(out)
     ops.C().embed_type_grad(dz, tt, out2)
     assert torch.equal(out, out2)   # run-to-run identical
+
+
+@pytest.mark.gpu
+def test_side_stream_priority_and_capture(dev):
+    """The weight-gradient side stream is created at HIP's LOWEST priority (the compute stream is at
+    the default, RCCL's streams at the highest), and a captured update gets no side stream (its
+    replays would run the branch at twice the device time, profiles/r6ae)."""
+    from hetseq_9cme_amd.ops._ext import C
+    least, greatest = C().stream_priority_range()
+    assert least > greatest
+    old = fused._Side.mode
+    try:
+        fused.set_side_stream('on')
+        st = fused._side_stream(dev.index or 0)
+        assert st.priority == least
+        x = torch.randn(64, 64, device=dev)
+        g = torch.cuda.CUDAGraph()
+        cap = torch.cuda.Stream(device=dev)
+        cap.wait_stream(torch.cuda.current_stream(dev))
+        seen = []
+        with torch.cuda.stream(cap):
+            with torch.cuda.graph(g, stream=cap):
+                seen.append(fused.side_begin(dev, 1 << 20))
+                y = x * 2
+        assert seen == [None]
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(y, x * 2)
+    finally:
+        fused.set_side_stream(old)

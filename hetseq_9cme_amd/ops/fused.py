@@ -127,6 +127,10 @@ class _Side(object):
     AUTO_ROWS = 8192
     auto_rows = AUTO_ROWS   # set_side_stream(..., auto_rows=): 4096 for hidden sizes >= 1024
     priority = os.environ.get('HX_SIDE_PRIO', 'low')   # 'low' (default) or 'normal' HIP priority
+    # CUs the side-stream plans leave free (-1: a quarter of the device's, 64 on MI355X).  Alternated
+    # on one box (profiles/r6ah_side_reserve_ab.txt): batch 128 35.34 / 35.35 -> 35.04 / 35.05 ms/step,
+    # phase 2 40.36 / 40.47 -> 39.24 / 39.28 at 64; 48 and 80 in between / worse
+    reserve = int(os.environ.get('HX_SIDE_RESERVE', '-1'))
     streams = {}          # (device index, low priority) -> stream
     active = {}           # device index -> the side stream this backward queued work on
 
@@ -183,6 +187,38 @@ def _side_stream(idx):
             st = torch.cuda.Stream(device=idx)
         _Side.streams[key] = st
     return st
+
+
+class _SideCtx(object):
+    """Launches on the side stream, planned for ``_Side.reserve`` fewer workgroup slots than CUs:
+    the one-workgroup-per-CU weight gradients then leave those CUs to the compute stream's
+    LayerNorm / attention backward instead of holding every CU for a whole kernel (the CU
+    reservation of cu_reserve.hip, set only while side-stream work is launched)."""
+    __slots__ = ('st', 'sc', 'prev')
+
+    def __init__(self, st):
+        self.st = st
+
+    def __enter__(self):
+        self.sc = torch.cuda.stream(self.st)
+        self.sc.__enter__()
+        self.prev = None
+        if _Side.reserve < 0:
+            _Side.reserve = C().num_cus() // 4
+        if _Side.reserve > 0:
+            self.prev = C().reserved_cus()
+            C().set_reserved_cus(max(self.prev, _Side.reserve))
+        return self
+
+    def __exit__(self, *exc):
+        if self.prev is not None:
+            C().set_reserved_cus(self.prev)
+        return self.sc.__exit__(*exc)
+
+
+def side_ctx(side):
+    """``with side_ctx(side_begin(...))``: the side stream (+ its CU reservation), or nothing."""
+    return _SideCtx(side) if side is not None else _nullctx()
 
 
 def active_side_stream(device):
@@ -489,7 +525,7 @@ class _LinearFn(torch.autograd.Function):
             dx = _dgrad(dy2, W, ctx.xshape, ctx.mbox)
         slot = grad_slot(W)
         side = side_begin(dy2.device, dy2.shape[0]) if slot is not None else None
-        with torch.cuda.stream(side) if side is not None else _nullctx():
+        with side_ctx(side):
             dW = _wgrad(dy2, x2, slot)
             db = None
             if b is not None:
@@ -544,7 +580,7 @@ def _linear_backward_f16(ctx, dy):
           if ctx.needs_input_grad[0] else None)
     slot = grad_slot(W)
     side = side_begin(dy2.device, dy2.shape[0]) if slot is not None else None
-    with torch.cuda.stream(side) if side is not None else _nullctx():
+    with side_ctx(side):
         dW = gemm16.wgrad(dy2, dcols, x2, xcols, W.shape[0], W.shape[1], slot)
         db = None
         if b is not None:
@@ -599,7 +635,7 @@ def _ffn_backward_f16(ctx, dy):
     slot2, slot1 = grad_slot(W2), grad_slot(W1)
     # each weight gradient on the side stream, beside the next data-gradient GEMM
     side = side_begin(dy2.device, dy2.shape[0]) if slot2 is not None and slot1 is not None else None
-    with torch.cuda.stream(side) if side is not None else _nullctx():
+    with side_ctx(side):
         dW2 = gemm16.wgrad(dy2, dcols, h, ctx.hcols, W2.shape[0], W2.shape[1], slot2)
     _record(side, dy2, dparts, h, hparts, ctx.hcols, dcols)
     # GELU backward in the FFN-down data-gradient epilogue: t = (dy W2) * gelu'(u), d b1
@@ -607,7 +643,7 @@ def _ffn_backward_f16(ctx, dy):
     if side is not None:
         side = side_begin(dy2.device, dy2.shape[0])   # after t
     xcols = ctx.xcols if ctx.xcols is not None else gemm16.cols(x2, x2)
-    with torch.cuda.stream(side) if side is not None else _nullctx():
+    with side_ctx(side):
         dW1 = gemm16.wgrad(t, tcols, x2, xcols, W1.shape[0], W1.shape[1], slot1)
     _record(side, t, tparts, tcols, x2, xparts, xcols)
     dx = _f16_dgrad(t, tparts, w1t, p1, ctx.xshape, ctx.mbox)
@@ -830,7 +866,7 @@ class _Linear3Fn(torch.autograd.Function):
         fb = _adjacent_view(bs) if all(t is not None for t in bs) else None
         direct = fused is not None and (fb is not None or not has_b)
         side = side_begin(dy2.device, dy2.shape[0]) if direct else None
-        with torch.cuda.stream(side) if side is not None else _nullctx():
+        with side_ctx(side):
             if fused is not None:
                 wg(fused)
                 gW = ws
@@ -934,7 +970,7 @@ class _DecoderXentFn(torch.autograd.Function):
         else:
             dh = torch.mm(dl, cast_w(W, dl.dtype)).mul_(scale.to(dl.dtype))
         side = side_begin(dl.device, dl.shape[0]) if slot is not None else None
-        with torch.cuda.stream(side) if side is not None else _nullctx():
+        with side_ctx(side):
             if ctx.b16 and C().wgrad_bf16_ok(dl_full, hs):
                 # over the padded vocabulary (whole 128-row tiles); rows past V are not stored
                 out = slot if slot is not None else torch.empty(W.shape[0], hs.shape[1], device=dl.device)

@@ -1,5 +1,6 @@
 """Numerics of every gfx950 kernel against a plain PyTorch fp32 reference of the
 same op (run on the MI355X: ``pytest -m gpu``)."""
+import os
 import math
 
 import pytest
@@ -891,6 +892,15 @@ def test_side_stream_priority_and_capture(dev):
         fused.set_side_stream('on')
         st = fused._side_stream(dev.index or 0)
         assert st.priority == least
+        # launches on it are planned for a quarter fewer workgroup slots (HX_SIDE_RESERVE), restored after
+        prev = C().reserved_cus()
+        with fused.side_ctx(st):
+            assert torch.cuda.current_stream(dev).cuda_stream == st.cuda_stream
+            assert fused._Side.reserve >= 0
+            assert C().reserved_cus() == max(prev, fused._Side.reserve)
+            if 'HX_SIDE_RESERVE' not in os.environ:
+                assert fused._Side.reserve == C().num_cus() // 4
+        assert C().reserved_cus() == prev
         x = torch.randn(64, 64, device=dev)
         g = torch.cuda.CUDAGraph()
         cap = torch.cuda.Stream(device=dev)
